@@ -1,0 +1,352 @@
+// oracle/ref/harness.cpp -- TEST INFRASTRUCTURE ONLY (never part of the product).
+//
+// A thin extern "C" wrapper, written for this repo, around the REFERENCE's own
+// C++ classes (sfiligoi/bowtie2-server, compiled from /root/reference by
+// oracle/ref/Makefile into oracle/_ref/libbt2ref.so).  It lets the Python tests
+// and bench.py's cpu_baseline leg call the reference's exact code paths:
+//
+//   * Ebwt load            bt2_search.cpp:5080-5097, 4870-4892 (same ctor/load args)
+//   * SeedAligner::exactSweep     aligner_seed.cpp:854
+//   * SeedAligner::oneMmSearch    aligner_seed.cpp:973
+//   * SeedAligner::instantiateSeeds/searchAllSeeds  aligner_seed.cpp:498,597
+//   * SwAligner::initRead/initRef/align (+ btncand_)  aligner_sw.cpp:34,73,500
+//   * Ebwt::getOffset             bt2_idx.cpp:150
+//
+// No reference source is copied here; everything is reached through the
+// reference headers at build time.
+#include <stdint.h>
+#include <string.h>
+#include <vector>
+#include <string>
+#include <algorithm>
+#include "bt2_idx.h"
+#include "reference.h"
+#include "read.h"
+#include "aligner_seed.h"
+#include "aligner_cache.h"
+#include "aligner_sw.h"
+#include "scoring.h"
+#include "simple_func.h"
+#include "search_globals.h"
+#include "random_source.h"
+
+// Globals normally defined by bt2_search.cpp (search_globals.h, aligner_seed_policy.h).
+bool gReportOverhangs = false;
+bool gNoMaqRound = false;
+bool gStrandFix = true;
+bool gRangeMode = false;
+int gVerbose = 0;
+int gQuiet = 1;
+bool gNofw = false;
+bool gNorc = false;
+bool gMate1fw = true;
+bool gMate2fw = false;
+int gMinInsert = 0;
+int gMaxInsert = 500;
+int gGapBarrier = 4;
+int gAllowRedundant = 0;
+int gDefaultSeedLen = 22;
+bool gFlippedMatesOK = false;
+bool gDovetailMatesOK = false;
+bool gContainMatesOK = true;
+bool gOlapMatesOK = true;
+bool gExpandToFrag = true;
+bool gReportDiscordant = true;
+bool gReportMixed = true;
+
+namespace {
+
+struct RefHandle {
+	Ebwt* fw = nullptr;
+	Ebwt* bw = nullptr;
+	BitPairReference* refs = nullptr;
+};
+
+// Scoring exactly as bt2_search.cpp:5134-5148 builds it, parameterised.
+struct ScoreParams {
+	int32_t match;       // bonusMatch (0 e2e, 2 local)
+	int32_t mmp_max;     // --mp MX (6)
+	int32_t mmp_min;     // --mp MN (2)
+	int32_t npen;        // --np (1)
+	int32_t rdg_const;   // --rdg 5,3
+	int32_t rdg_lin;
+	int32_t rfg_const;   // --rfg 5,3
+	int32_t rfg_lin;
+	int32_t gapbar;      // --gbar (4)
+	int32_t local;       // 1 = local mode
+	double  ncl_const;   // --n-ceil L,0,0.15
+	double  ncl_lin;
+};
+
+Scoring makeScoring(const ScoreParams& p) {
+	SimpleFunc scoreMin;
+	if(p.local) scoreMin.init(SIMPLE_FUNC_LOG, 20.0, 8.0);
+	else        scoreMin.init(SIMPLE_FUNC_LINEAR, -0.6, -0.6);
+	SimpleFunc nCeil;
+	nCeil.init(SIMPLE_FUNC_LINEAR, 0.0, std::numeric_limits<double>::max(), p.ncl_const, p.ncl_lin);
+	return Scoring(
+		p.match, COST_MODEL_QUAL, p.mmp_max, p.mmp_min, scoreMin, nCeil,
+		COST_MODEL_CONSTANT, p.npen, false,
+		p.rdg_const, p.rfg_const, p.rdg_lin, p.rfg_lin, p.gapbar);
+}
+
+// Gives the harness read access to SwAligner's protected results.
+struct SwAlignerX : public SwAligner {
+	SwAlignerX() : SwAligner(NULL) {}
+	const EList<DpBtCandidate>& cands() const { return btncand_; }
+	size_t colstop() const { return colstop_; }
+	size_t lastsolcol() const { return lastsolcol_; }
+	bool u8succ() const { return sse8succ_; }
+	bool i16succ() const { return sse16succ_; }
+	const SSEMatrix& mat(bool u8, bool fw) const {
+		if(u8) return fw ? sseU8fw_.mat_ : sseU8rc_.mat_;
+		return fw ? sseI16fw_.mat_ : sseI16rc_.mat_;
+	}
+};
+
+} // namespace
+
+extern "C" {
+
+void* bt2ref_open(const char* base) {
+	RefHandle* h = new RefHandle();
+	std::string b(base);
+	h->fw = new Ebwt(b, 0, -1, true, -1, 0, false, false, false, false, true, true, true,
+	                 false, false, false, false);
+	h->fw->loadIntoMemory(0, -1, true, true, true, false, false);
+	h->bw = new Ebwt(b + ".rev", 0, 1, false, -1, 0, false, false, false, false, false, true, false,
+	                 false, false, false, false);
+	h->bw->loadIntoMemory(0, 1, false, true, false, false, false);
+	h->refs = new BitPairReference(b, false, false, NULL, NULL, false, false, false, false, false, false);
+	return h;
+}
+
+void bt2ref_close(void* vh) {
+	RefHandle* h = (RefHandle*)vh;
+	delete h->fw; delete h->bw; delete h->refs; delete h;
+}
+
+// out: [len, zOff_fw, zOff_bw, fchr0..4, ftabChars, offRate, numSides, nPat, nFrag]
+void bt2ref_info(void* vh, uint64_t* out) {
+	RefHandle* h = (RefHandle*)vh;
+	const EbwtParams& e = h->fw->eh();
+	out[0] = e.len(); out[1] = h->fw->zOff(); out[2] = h->bw->zOff();
+	for(int i = 0; i < 5; i++) out[3 + i] = h->fw->fchr()[i];
+	out[8] = e.ftabChars(); out[9] = e.offRate(); out[10] = e.numSides();
+	out[11] = h->fw->nPat(); out[12] = h->fw->nFrag();
+}
+
+// Ebwt::contains on fw and (reversed string) on the mirror -> SA ranges.
+// seq: ASCII ACGT.  Returns 1 iff found in fw.
+int bt2ref_contains(void* vh, const char* seq, uint32_t* out4) {
+	RefHandle* h = (RefHandle*)vh;
+	BTDnaString s(seq, true);
+	TIndexOffU tf = 0, bf = 0, tb = 0, bb = 0;
+	bool ok = h->fw->contains(s, &tf, &bf);
+	s.reverse();
+	h->bw->contains(s, &tb, &bb);
+	out4[0] = tf; out4[1] = bf; out4[2] = tb; out4[3] = bb;
+	return ok ? 1 : 0;
+}
+
+// One bidirectional LF step on index `which` (0 fw, 1 mirror) from range [top,bot)
+// with mirror range starting at topp: INIT_LOCS + mapBiLFEx (aligner_seed.h:1847,
+// bt2_idx.h:2372) or, for a 1-row range, mapLF1 (bt2_idx.h:2451).
+void bt2ref_bilf(void* vh, int which, uint32_t top, uint32_t bot, uint32_t topp,
+                 uint32_t* t4, uint32_t* b4, uint32_t* tp4, uint32_t* bp4) {
+	RefHandle* h = (RefHandle*)vh;
+	const Ebwt* e = which ? h->bw : h->fw;
+	TIndexOffU t[4] = {0,0,0,0}, b[4] = {0,0,0,0};
+	TIndexOffU tp[4] = {topp,topp,topp,topp}, bp[4] = {topp + (bot - top), topp + (bot - top), topp + (bot - top), topp + (bot - top)};
+	SideLocus tloc, bloc;
+	INIT_LOCS(top, bot, tloc, bloc, *e);
+	if(bloc.valid()) {
+		e->mapBiLFEx(tloc, bloc, t, b, tp, bp);
+	} else {
+		TIndexOffU row = top;
+		int c = e->mapLF1(row, tloc);
+		if(c >= 0) { t[c] = row; b[c] = row + 1; }
+		for(int i = 0; i < 4; i++) { tp[i] = topp; bp[i] = topp + ((int)i == c ? 1 : 0); }
+	}
+	for(int i = 0; i < 4; i++) { t4[i] = t[i]; b4[i] = b[i]; tp4[i] = tp[i]; bp4[i] = bp[i]; }
+}
+
+uint32_t bt2ref_ftab_lohi(void* vh, int which, uint32_t i, uint32_t* bot) {
+	RefHandle* h = (RefHandle*)vh;
+	const Ebwt* e = which ? h->bw : h->fw;
+	TIndexOffU t = 0, b = 0;
+	e->ftabLoHi(i, t, b);
+	*bot = b;
+	return t;
+}
+
+uint32_t bt2ref_get_offset(void* vh, uint32_t row) {
+	RefHandle* h = (RefHandle*)vh;
+	return h->fw->getOffset(row);
+}
+
+// Fetch 2-bit reference bases [off, off+len) of reference `refidx` (values 0..4).
+int bt2ref_get_stretch(void* vh, uint32_t refidx, uint64_t off, uint64_t len, uint8_t* dst) {
+	RefHandle* h = (RefHandle*)vh;
+	for(uint64_t i = 0; i < len; i++) dst[i] = (uint8_t)h->refs->getBase(refidx, off + i);
+	return 0;
+}
+
+// SeedAligner::exactSweep over n reads (ASCII seq/qual, NUL-terminated).
+// out per read: mineFw, mineRc, nelt, exact fw [top,bot), exact rc [top,bot), bwops
+void bt2ref_exact_sweep(void* vh, int n, const char** seqs, const char** quals,
+                        int mineMax, uint64_t* out /* 8 per read */) {
+	RefHandle* h = (RefHandle*)vh;
+	SeedAligner al;
+	SeedResults sr;
+	SeedSearchMetrics met;
+	ScoreParams sp = {0, 6, 2, 1, 5, 3, 5, 3, 4, 0, 0.0, 0.15};
+	Scoring sc = makeScoring(sp);
+	for(int i = 0; i < n; i++) {
+		Read rd("r", seqs[i], quals[i]);
+		sr.clear();
+		sr.nextRead(rd);
+		size_t mineFw = 0, mineRc = 0;
+		met.reset();
+		size_t nelt = al.exactSweep(*h->fw, rd, sc, false, false, (size_t)mineMax,
+		                            mineFw, mineRc, true, sr, met);
+		uint64_t* o = out + 8 * (size_t)i;
+		o[0] = mineFw; o[1] = mineRc; o[2] = nelt;
+		EEHit f = sr.exactFwEEHit(), r = sr.exactRcEEHit();
+		o[3] = f.top; o[4] = f.bot; o[5] = r.top; o[6] = r.bot;
+		o[7] = met.bwops;
+	}
+}
+
+// SeedAligner::oneMmSearch (rep1mm, no repex, as bt2_search.cpp:3654-3667).
+// Writes hits in discovery order: 6 words each (top, bot, fw, score, edit pos, edit chr|readc<<8).
+// counts[i] = number of hits for read i (capped at cap per read).  out stride = cap*6.
+void bt2ref_one_mm(void* vh, int n, const char** seqs, const char** quals,
+                   const int64_t* minsc, int local, int nofw, int norc,
+                   int cap, int64_t* out, int32_t* counts, uint64_t* bwops) {
+	RefHandle* h = (RefHandle*)vh;
+	SeedAligner al;
+	SeedResults sr;
+	SeedSearchMetrics met;
+	ScoreParams sp = {local ? 2 : 0, 6, 2, 1, 5, 3, 5, 3, 4, local, 0.0, 0.15};
+	Scoring sc = makeScoring(sp);
+	for(int i = 0; i < n; i++) {
+		Read rd("r", seqs[i], quals[i]);
+		sr.clear();
+		sr.nextRead(rd);
+		met.reset();
+		al.oneMmSearch(h->fw, h->bw, rd, sc, minsc[i], nofw != 0, norc != 0, local != 0,
+		               false, true, sr, met);
+		const EList<EEHit>& hits = sr.mm1EEHits();
+		int k = 0;
+		for(size_t j = 0; j < hits.size() && k < cap; j++, k++) {
+			int64_t* o = out + ((size_t)i * cap + k) * 6;
+			o[0] = hits[j].top; o[1] = hits[j].bot; o[2] = hits[j].fw ? 1 : 0;
+			o[3] = hits[j].score;
+			o[4] = hits[j].e1.pos; o[5] = (int64_t)hits[j].e1.chr | ((int64_t)hits[j].e1.qchr << 8);
+		}
+		counts[i] = (int32_t)hits.size();
+		bwops[i] = met.bwops;
+	}
+}
+
+// Exact-seed search exactly as one seed round of bt2_search.cpp:3853-3906:
+// Seed::mmSeeds(0, seedlen) -> instantiateSeeds(offset, interval) -> searchAllSeeds.
+// out per read, per strand (fw then rc), per seed offset index (up to maxseeds):
+//   topf, botf, topb, botb  (all 0 when the seed had no hit / was filtered)
+// nseeds[i] = number of seed offsets instantiated for read i; bwops[i] = FM ops.
+void bt2ref_seed_search(void* vh, int n, const char** seqs, const char** quals,
+                        int seedlen, int interval, int offset, int maxseeds,
+                        uint32_t* out, int32_t* nseeds, uint64_t* bwops) {
+	RefHandle* h = (RefHandle*)vh;
+	SeedAligner al;
+	SeedResults sr;
+	SeedSearchMetrics met;
+	PerReadMetrics prm;
+	ScoreParams sp = {0, 6, 2, 1, 5, 3, 5, 3, 4, 0, 0.0, 0.15};
+	Scoring sc = makeScoring(sp);
+	AlignmentCache scCurrent(16 * 1024 * 1024, false);
+	AlignmentCacheIface ca(&scCurrent, NULL, NULL);
+	EList<Seed> seeds;
+	Constraint gc = Constraint::penaltyFuncBased(sc.scoreMin);
+	EList<SATuple> satups;
+	for(int i = 0; i < n; i++) {
+		Read rd("r", seqs[i], quals[i]);
+		sr.clear();
+		sr.nextRead(rd);
+		ca.nextRead();
+		met.reset(); prm.reset();
+		seeds.clear();
+		Seed::mmSeeds(0, seedlen, seeds, gc);
+		std::pair<int, int> instFw, instRc;
+		al.instantiateSeeds(seeds, (size_t)offset, interval, rd, sc, false, false, ca, sr, met,
+		                    instFw, instRc);
+		al.searchAllSeeds(seeds, h->fw, h->bw, rd, sc, ca, sr, met, prm);
+		int ns = (int)sr.numOffs();
+		nseeds[i] = ns;
+		bwops[i] = met.bwops;
+		uint32_t* o = out + (size_t)i * 2 * maxseeds * 4;
+		memset(o, 0, sizeof(uint32_t) * 2 * maxseeds * 4);
+		for(int fwi = 0; fwi < 2; fwi++) {
+			bool fw = fwi == 0;
+			for(int s = 0; s < ns && s < maxseeds; s++) {
+				const QVal& qv = sr.hitsAtOffIdx(fw, s);
+				if(!qv.valid() || qv.empty()) continue;
+				satups.clear();
+				size_t nrange = 0, nelt = 0;
+				ca.queryQval(qv, satups, nrange, nelt);
+				if(satups.size() == 0) continue;
+				uint32_t* q = o + ((size_t)fwi * maxseeds + s) * 4;
+				q[0] = satups[0].topf; q[1] = satups[0].topf + (uint32_t)satups[0].offs.size();
+				q[2] = satups[0].topb; q[3] = satups[0].topb + (uint32_t)satups[0].offs.size();
+			}
+		}
+	}
+}
+
+// SwAligner fill + gather for one DP problem, exactly as bt2_dp.cpp:720-744 drives it.
+// rfmask: ncol+1 reference masks (1,2,4,8 or 16=N); the extra one is the column
+// right of the rectangle (aligner_sw.cpp:174-176).
+// out: [0]=aligned(0/1) [1]=best [2]=u8succ [3]=i16succ [4]=colstop [5]=lastsolcol [6]=ncand
+// cands: up to cap triples (row, col, score), in the reference's sorted order.
+// mat (optional, nrow*ncol*3 int32: H,E,F of the successful matrix, or NULL).
+int bt2ref_sw(const char* seq, const char* qual, int fw, const uint8_t* rfmask, int ncol,
+              int64_t minsc, const ScoreParams* sp, int enable8, int cap,
+              int64_t* out, int64_t* cands, int32_t* mat) {
+	Scoring sc = makeScoring(*sp);
+	BTDnaString rdfw(seq, true), rdrc;
+	BTString qufw(qual), qurc;
+	rdrc = rdfw; rdrc.reverseComp();
+	qurc = qufw; qurc.reverse();
+	SwAlignerX sw;
+	sw.initRead(rdfw, rdrc, qufw, qurc, 0, rdfw.length(), sc);
+	std::vector<char> rf(ncol + 16, 0);
+	for(int i = 0; i <= ncol; i++) rf[i] = (char)rfmask[i];
+	DPRect rect;
+	rect.refl = 0; rect.refr = ncol - 1; rect.refl_pretrim = 0; rect.refr_pretrim = ncol - 1;
+	rect.triml = rect.trimr = 0; rect.corel = 0; rect.corer = 0; rect.maxgap = 0;
+	sw.initRef(fw != 0, 0, rect, rf.data(), 0, (size_t)ncol, (TRefOff)ncol + 1000, sc, minsc,
+	           enable8 != 0, 2000, 4, false, true);
+	TAlScore best = std::numeric_limits<TAlScore>::min();
+	bool aligned = sw.align(best);
+	out[0] = aligned ? 1 : 0; out[1] = best;
+	out[2] = sw.u8succ(); out[3] = sw.i16succ();
+	out[4] = (int64_t)sw.colstop(); out[5] = (int64_t)sw.lastsolcol();
+	const EList<DpBtCandidate>& c = sw.cands();
+	out[6] = (int64_t)c.size();
+	for(size_t i = 0; i < c.size() && (int)i < cap; i++) {
+		cands[3 * i] = c[i].row; cands[3 * i + 1] = c[i].col; cands[3 * i + 2] = c[i].score;
+	}
+	if(mat != NULL && (sw.u8succ() || sw.i16succ())) {
+		const SSEMatrix& m = sw.mat(sw.u8succ(), fw != 0);
+		size_t nrow = rdfw.length();
+		for(size_t r = 0; r < nrow; r++)
+			for(int cc = 0; cc < ncol; cc++) {
+				int32_t* p = mat + 3 * (r * ncol + cc);
+				p[0] = m.helt(r, cc); p[1] = m.eelt(r, cc); p[2] = m.felt(r, cc);
+			}
+	}
+	return 0;
+}
+
+} // extern "C"
