@@ -1,0 +1,240 @@
+"""Python binding of the C ABI in include/bt2g.h (libbt2g.so, built in-tree).
+
+Thin ctypes layer used by the tests, bench.py and __graft_entry__; the product
+is the C ABI itself (a C++ host such as bt2_search.cpp would call it
+directly).  Raises if the HIP library is missing: there is
+no CPU fallback anywhere on this path.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+import subprocess
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(HERE, "libbt2g.so")
+
+BT2G_OK = 0
+BT2G_ERR_OVERFLOW = -6
+K_EXACT_SWEEP, K_SEED_SEARCH, K_ONE_MM, K_GET_OFFSET, K_SW_ALIGN = range(5)
+
+
+class Scoring(C.Structure):
+    _fields_ = [(n, C.c_int32) for n in ("match", "mmp_max", "mmp_min", "npen", "rdg_const", "rdg_lin",
+                                          "rfg_const", "rfg_lin", "gapbar", "local")] + \
+               [("ncl_const", C.c_double), ("ncl_lin", C.c_double)]
+
+
+def scoring(local=False):
+    """bowtie2 defaults (scoring.h:28-83, bt2_search.cpp:452)."""
+    return Scoring(match=2 if local else 0, mmp_max=6, mmp_min=2, npen=1, rdg_const=5, rdg_lin=3,
+                   rfg_const=5, rfg_lin=3, gapbar=4, local=1 if local else 0, ncl_const=0.0, ncl_lin=0.15)
+
+
+MM1_DTYPE = np.dtype([("top", "<u4"), ("bot", "<u4"), ("fw", "<i4"), ("score", "<i4"), ("pos", "<i4"),
+                      ("chr", "<i4"), ("qchr", "<i4"), ("pad", "<i4")])
+SWPROB_DTYPE = np.dtype([("read", "<u4"), ("fw", "<i4"), ("refl", "<i8"), ("win_off", "<i8"), ("refidx", "<u4"),
+                         ("ncol", "<u4"), ("minsc", "<i4"), ("pad", "<u4")])
+SWRES_DTYPE = np.dtype([("aligned", "<i4"), ("best", "<i4"), ("u8succ", "<i4"), ("i16succ", "<i4"),
+                        ("colstop", "<i4"), ("lastsolcol", "<i4"), ("ncand", "<i4"), ("flag", "<i4")])
+SWCAND_DTYPE = np.dtype([("row", "<i4"), ("col", "<i4"), ("score", "<i4")])
+
+
+class EbwtMem(C.Structure):
+    _fields_ = [("len", C.c_uint32), ("zoff", C.c_uint32), ("ftab_chars", C.c_uint32), ("off_rate", C.c_uint32),
+                ("line_rate", C.c_uint32), ("fchr", C.c_void_p), ("sides", C.c_void_p), ("sides_bytes", C.c_uint64),
+                ("ftab", C.c_void_p), ("eftab", C.c_void_p), ("offs", C.c_void_p), ("offs_len", C.c_uint64),
+                ("rstarts", C.c_void_p), ("nfrag", C.c_uint32)]
+
+
+class IndexMem(C.Structure):
+    _fields_ = [("fw", EbwtMem), ("bw", EbwtMem), ("ref_codes", C.c_void_p), ("ref_starts", C.c_void_p),
+                ("nref", C.c_uint32)]
+
+
+def build(force=False):
+    """Compile libbt2g.so for gfx950 (make -C bowtie2-server_amd)."""
+    if force or not os.path.exists(LIB_PATH):
+        subprocess.check_call(["make", "-C", HERE, "-j8"], stdout=subprocess.DEVNULL)
+    return LIB_PATH
+
+
+_lib = None
+
+
+def lib():
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            raise RuntimeError(f"{LIB_PATH} is missing: build it with `make -C bowtie2-server_amd` "
+                               "(there is no CPU fallback)")
+        L = C.CDLL(LIB_PATH)
+        vp, u32, i32, u64 = C.c_void_p, C.c_uint32, C.c_int32, C.c_uint64
+        L.bt2g_last_error.restype = C.c_char_p
+        L.bt2g_open.argtypes = [C.c_char_p, C.c_int, C.POINTER(vp)]
+        L.bt2g_open_mem.argtypes = [C.POINTER(IndexMem), C.c_int, C.POINTER(vp)]
+        L.bt2g_close.argtypes = [vp]
+        L.bt2g_info.argtypes = [vp, vp, C.c_int]
+        L.bt2g_exact_sweep.argtypes = [vp, vp, u32, vp, u32, u32, C.c_int, C.c_int, vp]
+        L.bt2g_exact_sweep_dev.argtypes = [vp, vp, u32, vp, u32, u32, C.c_int, C.c_int, vp, vp]
+        L.bt2g_seed_search.argtypes = [vp, vp, u32, vp, u32, u32, u32, u32, u32, vp, vp, vp, vp]
+        L.bt2g_seed_search_dev.argtypes = [vp, vp, u32, vp, u32, u32, u32, u32, u32, vp, vp, vp, vp, vp]
+        L.bt2g_one_mm.argtypes = [vp, vp, vp, u32, vp, u32, vp, C.POINTER(Scoring), C.c_int, C.c_int, u32, vp, vp,
+                                  vp, vp]
+        L.bt2g_one_mm_dev.argtypes = [vp, vp, vp, u32, vp, u32, vp, C.POINTER(Scoring), C.c_int, C.c_int, u32, vp,
+                                      vp, vp, vp, vp]
+        L.bt2g_get_offset.argtypes = [vp, vp, u32, vp, vp]
+        L.bt2g_get_offset_dev.argtypes = [vp, vp, u32, vp, vp, vp]
+        L.bt2g_sw_align.argtypes = [vp, vp, vp, u32, vp, vp, u32, vp, u64, C.POINTER(Scoring), C.c_int, u32, vp, vp,
+                                    vp, vp]
+        L.bt2g_sw_align_dev.argtypes = [vp, vp, vp, u32, vp, vp, u32, vp, C.POINTER(Scoring), C.c_int, u32, vp, vp,
+                                        vp, vp, vp]
+        L.bt2g_set_profiling.argtypes = [vp, C.c_int]
+        L.bt2g_kernel_stats.argtypes = [vp, C.c_int, C.POINTER(u64), C.POINTER(C.c_double)]
+        L.bt2g_reset_stats.argtypes = [vp]
+        _lib = L
+    return _lib
+
+
+class Bt2gError(RuntimeError):
+    def __init__(self, rc, msg):
+        super().__init__(f"bt2g error {rc}: {msg}")
+        self.rc = rc
+
+
+def _chk(rc, allow=()):
+    if rc != BT2G_OK and rc not in allow:
+        raise Bt2gError(rc, lib().bt2g_last_error().decode(errors="replace"))
+    return rc
+
+
+def _ptr(a):
+    return None if a is None else C.c_void_p(a.ctypes.data)
+
+
+def _c(a, dt):
+    return np.ascontiguousarray(a, dtype=dt)
+
+
+class Engine:
+    """An index resident in HBM of one GPU (bt2g_open / bt2g_open_mem)."""
+
+    def __init__(self, index_base=None, device=0, index=None):
+        self.h = C.c_void_p()
+        if index is not None:
+            self._keep = []
+            m = IndexMem()
+            for dst, e, fw in ((m.fw, index.fw, True), (m.bw, index.bw, False)):
+                arrs = dict(fchr=_c(e.fchr, np.uint32), sides=_c(e.ebwt, np.uint8), ftab=_c(e.ftab, np.uint32),
+                            eftab=_c(e.eftab, np.uint32), rstarts=_c(e.rstarts, np.uint32))
+                if fw and e.offs is not None:
+                    arrs["offs"] = _c(e.offs, np.uint32)
+                self._keep.append(arrs)
+                dst.len, dst.zoff, dst.ftab_chars = e.length, e.zoff, e.ftab_chars
+                dst.off_rate, dst.line_rate = e.off_rate, e.line_rate
+                dst.fchr, dst.sides = arrs["fchr"].ctypes.data, arrs["sides"].ctypes.data
+                dst.sides_bytes = arrs["sides"].nbytes
+                dst.ftab, dst.eftab = arrs["ftab"].ctypes.data, arrs["eftab"].ctypes.data
+                if "offs" in arrs:
+                    dst.offs, dst.offs_len = arrs["offs"].ctypes.data, len(arrs["offs"])
+                dst.rstarts, dst.nfrag = arrs["rstarts"].ctypes.data, len(arrs["rstarts"]) // 3
+            codes = np.concatenate(index.ref_codes).astype(np.uint8)
+            starts = np.zeros(len(index.ref_codes) + 1, np.uint64)
+            starts[1:] = np.cumsum([len(c) for c in index.ref_codes])
+            self._keep.append((codes, starts))
+            m.ref_codes, m.ref_starts, m.nref = codes.ctypes.data, starts.ctypes.data, len(index.ref_codes)
+            _chk(lib().bt2g_open_mem(C.byref(m), device, C.byref(self.h)))
+            self._keep = None
+        else:
+            _chk(lib().bt2g_open(index_base.encode(), device, C.byref(self.h)))
+
+    def close(self):
+        if self.h:
+            lib().bt2g_close(self.h)
+            self.h = C.c_void_p()
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *a):
+        self.close()
+
+    def info(self):
+        o = np.zeros(13, np.uint64)
+        _chk(lib().bt2g_info(self.h, _ptr(o), 13))
+        return o
+
+    # ---- FM ----------------------------------------------------------------
+    def exact_sweep(self, reads, lens, mine_max=2, nofw=False, norc=False):
+        reads, lens = _c(reads, np.uint8), _c(lens, np.uint32)
+        out = np.zeros((len(lens), 8), np.uint32)
+        _chk(lib().bt2g_exact_sweep(self.h, _ptr(reads), reads.shape[1], _ptr(lens), len(lens), mine_max,
+                                    int(nofw), int(norc), _ptr(out)))
+        return out
+
+    def seed_search(self, reads, lens, seedlen, interval, offset, maxseeds=64):
+        reads, lens = _c(reads, np.uint8), _c(lens, np.uint32)
+        n = len(lens)
+        out = np.zeros((n, 2, maxseeds, 4), np.uint32)
+        ns = np.zeros(n, np.int32)
+        ops = np.zeros(n, np.uint32)
+        loads = np.zeros(n, np.uint32)
+        _chk(lib().bt2g_seed_search(self.h, _ptr(reads), reads.shape[1], _ptr(lens), n, seedlen, interval, offset,
+                                    maxseeds, _ptr(out), _ptr(ns), _ptr(ops), _ptr(loads)))
+        return out, ns, ops, loads
+
+    def one_mm(self, reads, quals, lens, minsc, local, nofw=False, norc=False, cap=64):
+        reads, quals, lens = _c(reads, np.uint8), _c(quals, np.uint8), _c(lens, np.uint32)
+        ms = _c(minsc, np.int32)
+        n = len(lens)
+        hits = np.zeros((n, cap), MM1_DTYPE)
+        cnt = np.zeros(n, np.int32)
+        ops = np.zeros(n, np.uint32)
+        loads = np.zeros(n, np.uint32)
+        sc = scoring(local)
+        rc = lib().bt2g_one_mm(self.h, _ptr(reads), _ptr(quals), reads.shape[1], _ptr(lens), n, _ptr(ms),
+                               C.byref(sc), int(nofw), int(norc), cap, _ptr(hits), _ptr(cnt), _ptr(ops), _ptr(loads))
+        _chk(rc)
+        return hits, cnt, ops, loads
+
+    def get_offset(self, rows):
+        rows = _c(rows, np.uint32)
+        offs = np.zeros(len(rows), np.uint32)
+        loads = np.zeros(len(rows), np.uint32)
+        _chk(lib().bt2g_get_offset(self.h, _ptr(rows), len(rows), _ptr(offs), _ptr(loads)))
+        return offs, loads
+
+    # ---- SW ----------------------------------------------------------------
+    def sw_align(self, reads, quals, lens, probs, windows=None, local=False, enable8=True, cap=4096,
+                 want_mat=False):
+        reads, quals, lens = _c(reads, np.uint8), _c(quals, np.uint8), _c(lens, np.uint32)
+        probs = _c(probs, SWPROB_DTYPE)
+        n = len(probs)
+        res = np.zeros(n, SWRES_DTYPE)
+        cands = np.zeros((n, cap), SWCAND_DTYPE)
+        win = _c(windows, np.uint8) if windows is not None else None
+        mat = mat_off = None
+        if want_mat:
+            sizes = lens[probs["read"]].astype(np.uint64) * probs["ncol"].astype(np.uint64) * 3
+            mat_off = np.zeros(n, np.uint64)
+            mat_off[1:] = np.cumsum(sizes)[:-1]
+            mat = np.zeros(int(sizes.sum()), np.int16)
+        sc = scoring(local)
+        _chk(lib().bt2g_sw_align(self.h, _ptr(reads), _ptr(quals), reads.shape[1], _ptr(lens), _ptr(probs), n,
+                                 _ptr(win), 0 if win is None else win.nbytes, C.byref(sc), int(enable8), cap,
+                                 _ptr(res), _ptr(cands), _ptr(mat), _ptr(mat_off)))
+        return res, cands, (mat, mat_off)
+
+    # ---- measurement -------------------------------------------------------
+    def set_profiling(self, on=True):
+        _chk(lib().bt2g_set_profiling(self.h, int(on)))
+
+    def kernel_stats(self, k):
+        n, ms = C.c_uint64(0), C.c_double(0)
+        _chk(lib().bt2g_kernel_stats(self.h, k, C.byref(n), C.byref(ms)))
+        return n.value, ms.value
+
+    def reset_stats(self):
+        _chk(lib().bt2g_reset_stats(self.h))

@@ -1,0 +1,652 @@
+// bt2g_api.cpp -- host side of the C ABI (include/bt2g.h).
+//
+// Owns the HBM-resident index (one replica per GPU), turns the
+// batch calls into kernel launches on a HIP stream, and provides the
+// host-pointer convenience wrappers.  No exception crosses the ABI; errors are
+// status codes plus a thread-local message (bt2g_last_error).
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+#include <stdio.h>
+#include <string.h>
+
+#include <cstdarg>
+#include <fstream>
+#include <string>
+#include <vector>
+
+#include "bt2g_kernels.h"
+
+namespace {
+
+thread_local std::string g_err;
+
+int fail(int code, const char* fmt, ...) {
+	char buf[512];
+	va_list ap;
+	va_start(ap, fmt);
+	vsnprintf(buf, sizeof(buf), fmt, ap);
+	va_end(ap);
+	g_err = buf;
+	return code;
+}
+
+#define HIPCHK(x)                                                                          \
+	do {                                                                                   \
+		hipError_t e_ = (x);                                                               \
+		if(e_ != hipSuccess) return fail(BT2G_ERR_HIP, "%s: %s", #x, hipGetErrorString(e_)); \
+	} while(0)
+
+struct DevBuf {
+	void* p = nullptr;
+	size_t n = 0;
+};
+
+}  // namespace
+
+struct bt2g_ctx {
+	int device = 0;
+	hipStream_t stream = nullptr;
+	DevEbwt fw{}, bw{};
+	std::vector<void*> owned;           // device allocations of the index
+	uint8_t* ref_codes = nullptr;
+	uint64_t* ref_starts = nullptr;
+	uint32_t nref = 0;
+	uint64_t num_sides = 0;
+	uint64_t hbm_bytes = 0;
+	// profiling
+	bool prof = false;
+	struct Pending { int kid; hipEvent_t a, b; };
+	std::vector<Pending> pending;
+	std::vector<hipEvent_t> evpool;
+	uint64_t launches[8] = {0};
+	double total_ms[8] = {0};
+};
+
+namespace {
+
+int dalloc(bt2g_ctx* c, void** p, size_t n) {
+	if(n == 0) n = 16;
+	hipError_t e = hipMalloc(p, n);
+	if(e != hipSuccess) return fail(BT2G_ERR_NOMEM, "hipMalloc(%zu): %s", n, hipGetErrorString(e));
+	c->owned.push_back(*p);
+	c->hbm_bytes += n;
+	return BT2G_OK;
+}
+
+template <typename T>
+int upload(bt2g_ctx* c, T** dst, const T* src, size_t count) {
+	int rc = dalloc(c, (void**)dst, count * sizeof(T));
+	if(rc) return rc;
+	if(count) HIPCHK(hipMemcpy(*dst, src, count * sizeof(T), hipMemcpyHostToDevice));
+	return BT2G_OK;
+}
+
+hipEvent_t get_event(bt2g_ctx* c) {
+	if(!c->evpool.empty()) {
+		hipEvent_t e = c->evpool.back();
+		c->evpool.pop_back();
+		return e;
+	}
+	hipEvent_t e;
+	if(hipEventCreate(&e) != hipSuccess) return nullptr;
+	return e;
+}
+
+struct ProfScope {
+	bt2g_ctx* c;
+	int kid;
+	hipStream_t st;
+	hipEvent_t a = nullptr;
+	ProfScope(bt2g_ctx* c_, int kid_, hipStream_t st_) : c(c_), kid(kid_), st(st_) {
+		if(c->prof) {
+			a = get_event(c);
+			if(a) (void)hipEventRecord(a, st);
+		}
+	}
+	~ProfScope() {
+		if(c->prof && a) {
+			hipEvent_t b = get_event(c);
+			if(b) {
+				(void)hipEventRecord(b, st);
+				c->pending.push_back({kid, a, b});
+			}
+		}
+	}
+};
+
+void drain_prof(bt2g_ctx* c) {
+	for(auto& p : c->pending) {
+		float ms = 0.f;
+		(void)hipEventSynchronize(p.b);
+		if(hipEventElapsedTime(&ms, p.a, p.b) == hipSuccess) {
+			c->launches[p.kid]++;
+			c->total_ms[p.kid] += ms;
+		}
+		c->evpool.push_back(p.a);
+		c->evpool.push_back(p.b);
+	}
+	c->pending.clear();
+}
+
+hipStream_t pick(bt2g_ctx* c, void* s) { return s ? (hipStream_t)s : c->stream; }
+
+// --- .bt2 reading (bt2_io.cpp:39-616; reference.cpp:100-235) ---------------
+bool read_file(const std::string& path, std::vector<uint8_t>& out) {
+	std::ifstream f(path, std::ios::binary);
+	if(!f) return false;
+	f.seekg(0, std::ios::end);
+	size_t n = (size_t)f.tellg();
+	f.seekg(0, std::ios::beg);
+	out.resize(n);
+	if(n) f.read((char*)out.data(), (std::streamsize)n);
+	return (bool)f;
+}
+
+struct HostEbwt {
+	uint32_t len = 0, zoff = 0, line_rate = 0, off_rate = 0, ftab_chars = 0;
+	std::vector<uint32_t> fchr, ftab, eftab, offs, rstarts;
+	std::vector<uint8_t> sides;
+};
+
+int parse_ebwt(const std::string& p1, const std::string& p2, HostEbwt& e) {
+	std::vector<uint8_t> d;
+	if(!read_file(p1, d)) return fail(BT2G_ERR_IO, "cannot read %s", p1.c_str());
+	size_t p = 0;
+	auto u32 = [&](uint32_t& v) -> bool {
+		if(p + 4 > d.size()) return false;
+		memcpy(&v, d.data() + p, 4);
+		p += 4;
+		return true;
+	};
+	uint32_t one, lps, flags, npat, nfrag;
+	if(!u32(one) || one != 1) return fail(BT2G_ERR_FORMAT, "%s: bad endianness word", p1.c_str());
+	if(!u32(e.len) || !u32(e.line_rate) || !u32(lps) || !u32(e.off_rate) || !u32(e.ftab_chars) || !u32(flags))
+		return fail(BT2G_ERR_FORMAT, "%s: short header", p1.c_str());
+	if(e.line_rate != 6) return fail(BT2G_ERR_FORMAT, "%s: lineRate %u unsupported (64-B sides)", p1.c_str(), e.line_rate);
+	if(!u32(npat)) return fail(BT2G_ERR_FORMAT, "%s: short", p1.c_str());
+	p += 4ull * npat;
+	if(!u32(nfrag)) return fail(BT2G_ERR_FORMAT, "%s: short", p1.c_str());
+	e.rstarts.resize(3ull * nfrag);
+	if(p + 12ull * nfrag > d.size()) return fail(BT2G_ERR_FORMAT, "%s: short rstarts", p1.c_str());
+	memcpy(e.rstarts.data(), d.data() + p, 12ull * nfrag);
+	p += 12ull * nfrag;
+	uint64_t bwt_sz = e.len / 4 + 1, side_bwt_sz = 48;
+	uint64_t nsides = (bwt_sz + side_bwt_sz - 1) / side_bwt_sz;
+	if(p + nsides * 64 > d.size()) return fail(BT2G_ERR_FORMAT, "%s: short ebwt", p1.c_str());
+	e.sides.assign(d.begin() + p, d.begin() + p + nsides * 64);
+	p += nsides * 64;
+	if(!u32(e.zoff)) return fail(BT2G_ERR_FORMAT, "%s: short", p1.c_str());
+	e.fchr.resize(5);
+	for(int i = 0; i < 5; i++) if(!u32(e.fchr[i])) return fail(BT2G_ERR_FORMAT, "%s: short fchr", p1.c_str());
+	uint64_t flen = (1ull << (2 * e.ftab_chars)) + 1;
+	e.ftab.resize(flen);
+	e.eftab.resize(2ull * e.ftab_chars);
+	if(p + 4 * (flen + e.eftab.size()) > d.size()) return fail(BT2G_ERR_FORMAT, "%s: short ftab", p1.c_str());
+	memcpy(e.ftab.data(), d.data() + p, 4 * flen);
+	p += 4 * flen;
+	memcpy(e.eftab.data(), d.data() + p, 4 * e.eftab.size());
+	if(!p2.empty()) {
+		std::vector<uint8_t> d2;
+		if(!read_file(p2, d2)) return fail(BT2G_ERR_IO, "cannot read %s", p2.c_str());
+		if(d2.size() < 4) return fail(BT2G_ERR_FORMAT, "%s: short", p2.c_str());
+		e.offs.resize((d2.size() - 4) / 4);
+		memcpy(e.offs.data(), d2.data() + 4, e.offs.size() * 4);
+	}
+	return BT2G_OK;
+}
+
+int parse_ref(const std::string& base, std::vector<uint8_t>& codes, std::vector<uint64_t>& starts) {
+	std::vector<uint8_t> d3, d4;
+	if(!read_file(base + ".3.bt2", d3)) return fail(BT2G_ERR_IO, "cannot read %s.3.bt2", base.c_str());
+	if(!read_file(base + ".4.bt2", d4)) return fail(BT2G_ERR_IO, "cannot read %s.4.bt2", base.c_str());
+	if(d3.size() < 8) return fail(BT2G_ERR_FORMAT, ".3.bt2 short");
+	uint32_t one, nrec;
+	memcpy(&one, d3.data(), 4);
+	memcpy(&nrec, d3.data() + 4, 4);
+	if(one != 1) return fail(BT2G_ERR_FORMAT, ".3.bt2 endianness");
+	uint64_t jo = 0;
+	for(uint32_t i = 0; i < nrec; i++) {
+		size_t q = 8 + 9ull * i;
+		if(q + 9 > d3.size()) return fail(BT2G_ERR_FORMAT, ".3.bt2 short");
+		uint32_t off, len;
+		memcpy(&off, d3.data() + q, 4);
+		memcpy(&len, d3.data() + q + 4, 4);
+		bool first = d3[q + 8] != 0;
+		if(first) starts.push_back(codes.size());
+		codes.insert(codes.end(), off, (uint8_t)4);
+		for(uint32_t k = 0; k < len; k++, jo++) {
+			if((jo >> 2) >= d4.size()) return fail(BT2G_ERR_FORMAT, ".4.bt2 short");
+			codes.push_back((d4[jo >> 2] >> ((jo & 3) * 2)) & 3);
+		}
+	}
+	starts.push_back(codes.size());
+	return BT2G_OK;
+}
+
+int make_dev_ebwt(bt2g_ctx* c, const bt2g_ebwt_mem& m, bool fw, DevEbwt& d) {
+	int rc;
+	uint8_t* sides;
+	uint32_t *ftab, *eftab, *offs = nullptr;
+	if((rc = upload(c, &sides, m.sides, m.sides_bytes))) return rc;
+	if((rc = upload(c, &ftab, m.ftab, (size_t)(1ull << (2 * m.ftab_chars)) + 1))) return rc;
+	if((rc = upload(c, &eftab, m.eftab, (size_t)2 * m.ftab_chars))) return rc;
+	if(m.offs && m.offs_len) {
+		if((rc = upload(c, &offs, m.offs, (size_t)m.offs_len))) return rc;
+	}
+	d.sides = sides; d.ftab = ftab; d.eftab = eftab; d.offs = offs;
+	d.len = m.len; d.zoff = m.zoff; d.ftab_chars = m.ftab_chars; d.off_rate = m.off_rate; d.fw = fw ? 1 : 0;
+	uint32_t side = m.zoff / 192u, co = m.zoff % 192u;
+	d.zbyte = side * 64u + (co >> 2);
+	d.zbp = (int32_t)(co & 3);
+	for(int i = 0; i < 5; i++) d.fchr[i] = m.fchr[i];
+	if(fw) c->num_sides = m.sides_bytes / 64;
+	return BT2G_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+const char* bt2g_last_error(void) { return g_err.c_str(); }
+
+int bt2g_open_mem(const bt2g_index_mem* m, int device, bt2g_ctx** out) {
+	if(!m || !out) return fail(BT2G_ERR_ARG, "null argument");
+	if(m->fw.line_rate != 6 || m->bw.line_rate != 6) return fail(BT2G_ERR_FORMAT, "lineRate must be 6");
+	int ndev = 0;
+	HIPCHK(hipGetDeviceCount(&ndev));
+	if(device < 0 || device >= ndev) return fail(BT2G_ERR_ARG, "device %d of %d", device, ndev);
+	HIPCHK(hipSetDevice(device));
+	bt2g_ctx* c = new bt2g_ctx();
+	c->device = device;
+	int rc;
+	if(hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess) {
+		delete c;
+		return fail(BT2G_ERR_HIP, "hipStreamCreate failed");
+	}
+	if((rc = make_dev_ebwt(c, m->fw, true, c->fw)) || (rc = make_dev_ebwt(c, m->bw, false, c->bw)) ||
+	   (rc = upload(c, &c->ref_codes, m->ref_codes, (size_t)m->ref_starts[m->nref])) ||
+	   (rc = upload(c, &c->ref_starts, m->ref_starts, (size_t)m->nref + 1))) {
+		bt2g_close(c);
+		return rc;
+	}
+	c->nref = m->nref;
+	*out = c;
+	return BT2G_OK;
+}
+
+int bt2g_open(const char* index_base, int device, bt2g_ctx** out) {
+	if(!index_base || !out) return fail(BT2G_ERR_ARG, "null argument");
+	std::string b(index_base);
+	HostEbwt F, B;
+	int rc;
+	if((rc = parse_ebwt(b + ".1.bt2", b + ".2.bt2", F))) return rc;
+	if((rc = parse_ebwt(b + ".rev.1.bt2", "", B))) return rc;
+	std::vector<uint8_t> codes;
+	std::vector<uint64_t> starts;
+	if((rc = parse_ref(b, codes, starts))) return rc;
+	auto mem = [](HostEbwt& e) {
+		bt2g_ebwt_mem m{};
+		m.len = e.len; m.zoff = e.zoff; m.ftab_chars = e.ftab_chars; m.off_rate = e.off_rate;
+		m.line_rate = e.line_rate; m.fchr = e.fchr.data(); m.sides = e.sides.data();
+		m.sides_bytes = e.sides.size(); m.ftab = e.ftab.data(); m.eftab = e.eftab.data();
+		m.offs = e.offs.empty() ? nullptr : e.offs.data(); m.offs_len = e.offs.size();
+		m.rstarts = e.rstarts.data(); m.nfrag = (uint32_t)(e.rstarts.size() / 3);
+		return m;
+	};
+	bt2g_index_mem m{};
+	m.fw = mem(F);
+	m.bw = mem(B);
+	m.ref_codes = codes.data();
+	m.ref_starts = starts.data();
+	m.nref = (uint32_t)(starts.size() - 1);
+	return bt2g_open_mem(&m, device, out);
+}
+
+int bt2g_close(bt2g_ctx* c) {
+	if(!c) return BT2G_OK;
+	(void)hipSetDevice(c->device);
+	if(c->stream) (void)hipStreamSynchronize(c->stream);
+	drain_prof(c);
+	for(hipEvent_t e : c->evpool) (void)hipEventDestroy(e);
+	for(void* p : c->owned) (void)hipFree(p);
+	if(c->stream) (void)hipStreamDestroy(c->stream);
+	delete c;
+	return BT2G_OK;
+}
+
+int bt2g_info(bt2g_ctx* c, uint64_t* out, int n) {
+	if(!c || !out) return fail(BT2G_ERR_ARG, "null argument");
+	uint64_t v[13] = {c->fw.len, c->fw.zoff, c->bw.zoff, c->fw.fchr[0], c->fw.fchr[1], c->fw.fchr[2],
+	                  c->fw.fchr[3], c->fw.fchr[4], c->fw.ftab_chars, c->fw.off_rate, c->num_sides, c->nref,
+	                  c->hbm_bytes};
+	for(int i = 0; i < n && i < 13; i++) out[i] = v[i];
+	return BT2G_OK;
+}
+
+int bt2g_set_profiling(bt2g_ctx* c, int on) {
+	if(!c) return fail(BT2G_ERR_ARG, "null ctx");
+	c->prof = on != 0;
+	return BT2G_OK;
+}
+
+int bt2g_kernel_stats(bt2g_ctx* c, int k, uint64_t* launches, double* total_ms) {
+	if(!c || k < 0 || k >= 8) return fail(BT2G_ERR_ARG, "bad kernel id");
+	drain_prof(c);
+	if(launches) *launches = c->launches[k];
+	if(total_ms) *total_ms = c->total_ms[k];
+	return BT2G_OK;
+}
+
+int bt2g_reset_stats(bt2g_ctx* c) {
+	if(!c) return fail(BT2G_ERR_ARG, "null ctx");
+	drain_prof(c);
+	memset(c->launches, 0, sizeof(c->launches));
+	memset(c->total_ms, 0, sizeof(c->total_ms));
+	return BT2G_OK;
+}
+
+// ---------------------------------------------------------------- FM engine
+static int check_reads(uint32_t stride, uint32_t n) {
+	if(stride == 0 || stride > BT2G_MAX_READ_LEN) return fail(BT2G_ERR_ARG, "stride %u out of range", stride);
+	(void)n;
+	return BT2G_OK;
+}
+
+int bt2g_exact_sweep_dev(bt2g_ctx* c, const uint8_t* reads, uint32_t stride, const uint32_t* lens, uint32_t n,
+                         uint32_t mine_max, int nofw, int norc, uint32_t* out, void* stream) {
+	if(!c) return fail(BT2G_ERR_ARG, "null ctx");
+	if(int rc = check_reads(stride, n)) return rc;
+	if(n == 0) return BT2G_OK;
+	hipStream_t st = pick(c, stream);
+	{
+		ProfScope ps(c, 0, st);
+		launch_exact_sweep(c->fw, reads, stride, lens, n, mine_max, nofw, norc, out, st);
+	}
+	HIPCHK(hipGetLastError());
+	return BT2G_OK;
+}
+
+int bt2g_seed_search_dev(bt2g_ctx* c, const uint8_t* reads, uint32_t stride, const uint32_t* lens, uint32_t n,
+                         uint32_t seedlen, uint32_t interval, uint32_t offset, uint32_t maxseeds, uint32_t* out,
+                         int32_t* nseeds, uint32_t* bwops, uint32_t* loads, void* stream) {
+	if(!c) return fail(BT2G_ERR_ARG, "null ctx");
+	if(int rc = check_reads(stride, n)) return rc;
+	if(seedlen == 0 || interval == 0 || maxseeds == 0) return fail(BT2G_ERR_ARG, "bad seed policy");
+	if(n == 0) return BT2G_OK;
+	hipStream_t st = pick(c, stream);
+	HIPCHK(hipMemsetAsync(bwops, 0, sizeof(uint32_t) * n, st));
+	if(loads) HIPCHK(hipMemsetAsync(loads, 0, sizeof(uint32_t) * n, st));
+	{
+		ProfScope ps(c, 1, st);
+		launch_seed_search(c->fw, c->bw, reads, stride, lens, n, seedlen, interval, offset, maxseeds, out, nseeds,
+		                   bwops, loads, st);
+	}
+	HIPCHK(hipGetLastError());
+	return BT2G_OK;
+}
+
+namespace {
+struct OneMmScratch {
+	bt2g_mm1* slots = nullptr;
+	int32_t* slot_counts = nullptr;
+	int32_t* ovf = nullptr;
+};
+}  // namespace
+
+int bt2g_one_mm_dev(bt2g_ctx* c, const uint8_t* reads, const uint8_t* quals, uint32_t stride, const uint32_t* lens,
+                    uint32_t n, const int32_t* minsc, const bt2g_scoring* sc, int nofw, int norc, uint32_t cap,
+                    bt2g_mm1* hits, int32_t* counts, uint32_t* bwops, uint32_t* loads, void* stream) {
+	if(!c || !sc) return fail(BT2G_ERR_ARG, "null argument");
+	if(int rc = check_reads(stride, n)) return rc;
+	if(cap == 0) return fail(BT2G_ERR_ARG, "cap must be > 0");
+	if(n == 0) return BT2G_OK;
+	hipStream_t st = pick(c, stream);
+	OneMmScratch s;
+	HIPCHK(hipMallocAsync((void**)&s.slots, sizeof(bt2g_mm1) * (size_t)n * 4 * cap, st));
+	HIPCHK(hipMallocAsync((void**)&s.slot_counts, sizeof(int32_t) * (size_t)n * 4, st));
+	HIPCHK(hipMallocAsync((void**)&s.ovf, sizeof(int32_t), st));
+	HIPCHK(hipMemsetAsync(s.ovf, 0, sizeof(int32_t), st));
+	HIPCHK(hipMemsetAsync(bwops, 0, sizeof(uint32_t) * n, st));
+	if(loads) HIPCHK(hipMemsetAsync(loads, 0, sizeof(uint32_t) * n, st));
+	{
+		ProfScope ps(c, 2, st);
+		launch_one_mm(c->fw, c->bw, reads, quals, stride, lens, n, minsc, *sc, nofw, norc, cap, s.slots,
+		              s.slot_counts, hits, counts, bwops, loads, s.ovf, st);
+	}
+	HIPCHK(hipGetLastError());
+	int32_t ovf = 0;
+	HIPCHK(hipMemcpyAsync(&ovf, s.ovf, sizeof(int32_t), hipMemcpyDeviceToHost, st));
+	HIPCHK(hipFreeAsync(s.slots, st));
+	HIPCHK(hipFreeAsync(s.slot_counts, st));
+	HIPCHK(hipFreeAsync(s.ovf, st));
+	HIPCHK(hipStreamSynchronize(st));
+	if(ovf) return fail(BT2G_ERR_OVERFLOW, "one-mismatch hits exceed cap %u", cap);
+	return BT2G_OK;
+}
+
+int bt2g_get_offset_dev(bt2g_ctx* c, const uint32_t* rows, uint32_t n, uint32_t* offs, uint32_t* loads,
+                        void* stream) {
+	if(!c) return fail(BT2G_ERR_ARG, "null ctx");
+	if(!c->fw.offs) return fail(BT2G_ERR_ARG, "SA sample not loaded");
+	if(n == 0) return BT2G_OK;
+	hipStream_t st = pick(c, stream);
+	{
+		ProfScope ps(c, 3, st);
+		launch_get_offset(c->fw, rows, n, offs, loads, st);
+	}
+	HIPCHK(hipGetLastError());
+	return BT2G_OK;
+}
+
+// ---------------------------------------------------------------- SW engine
+int bt2g_sw_align_dev(bt2g_ctx* c, const uint8_t* reads, const uint8_t* quals, uint32_t stride,
+                      const uint32_t* lens, const bt2g_sw_problem* probs, uint32_t nprob, const uint8_t* windows,
+                      const bt2g_scoring* sc, int enable8, uint32_t cap, bt2g_sw_result* res, bt2g_sw_cand* cands,
+                      int16_t* mat, const uint64_t* mat_off, void* stream) {
+	if(!c || !sc) return fail(BT2G_ERR_ARG, "null argument");
+	if(int rc = check_reads(stride, nprob)) return rc;
+	if(cap == 0 || cap > 65536) return fail(BT2G_ERR_ARG, "cap out of range");
+	if(sc->local && sc->match <= 0) return fail(BT2G_ERR_ARG, "local mode needs a match bonus");
+	if(nprob == 0) return BT2G_OK;
+	hipStream_t st = pick(c, stream);
+	SwConst C;
+	sw_fill_consts(*sc, C);
+	// problem lists per fill variant + boundary scratch
+	uint32_t *lists, *counts, *bnd;
+	size_t nblk = (nprob + 63) / 64;
+	// widest problem decides the boundary buffer width
+	std::vector<bt2g_sw_problem> hp;  // only the ncol field is needed; read it back once
+	uint32_t maxcol = 0;
+	{
+		// the problems live on the device; fetch ncol by a strided copy
+		hp.resize(nprob);
+		HIPCHK(hipMemcpyAsync(hp.data(), probs, sizeof(bt2g_sw_problem) * nprob, hipMemcpyDeviceToHost, st));
+		HIPCHK(hipStreamSynchronize(st));
+		for(auto& p : hp) maxcol = p.ncol > maxcol ? p.ncol : maxcol;
+	}
+	HIPCHK(hipMallocAsync((void**)&lists, sizeof(uint32_t) * (size_t)nprob * 3, st));
+	HIPCHK(hipMallocAsync((void**)&counts, sizeof(uint32_t) * 4, st));
+	HIPCHK(hipMallocAsync((void**)&bnd, sizeof(uint32_t) * nblk * (size_t)maxcol * 64 * 2, st));
+	HIPCHK(hipMemsetAsync(counts, 0, sizeof(uint32_t) * 4, st));
+	uint32_t* list8 = lists;
+	uint32_t* list16 = lists + nprob;
+	uint32_t* satl = lists + 2 * (size_t)nprob;
+	{
+		ProfScope ps(c, 4, st);
+		launch_sw_partition(probs, nprob, sc->local, enable8, list8, counts + 0, list16, counts + 1, st);
+		int v8 = sc->local ? 2 : 0, v16 = sc->local ? 3 : 1;
+		launch_sw_fill(v8, probs, nprob, list8, counts + 0, reads, quals, stride, lens, windows, c->ref_codes,
+		               c->ref_starts, C, cap, bnd, maxcol, res, cands, mat, mat_off, satl, counts + 2, st);
+		launch_sw_fill(v16, probs, nprob, list16, counts + 1, reads, quals, stride, lens, windows, c->ref_codes,
+		               c->ref_starts, C, cap, bnd, maxcol, res, cands, mat, mat_off, satl, counts + 3, st);
+		if(sc->local) {
+			// local u8 saturated -> i16 (aligner_sw.cpp:587-605)
+			launch_sw_fill(3, probs, nprob, satl, counts + 2, reads, quals, stride, lens, windows, c->ref_codes,
+			               c->ref_starts, C, cap, bnd, maxcol, res, cands, mat, mat_off, satl, counts + 3, st);
+		}
+		launch_sort_cands(res, cands, nprob, cap, st);
+	}
+	HIPCHK(hipGetLastError());
+	HIPCHK(hipFreeAsync(lists, st));
+	HIPCHK(hipFreeAsync(counts, st));
+	HIPCHK(hipFreeAsync(bnd, st));
+	return BT2G_OK;
+}
+
+}  // extern "C"
+
+// ------------------------------------------------------ host-pointer wrappers
+namespace {
+struct Tmp {
+	std::vector<void*> ps;
+	~Tmp() {
+		for(void* p : ps) (void)hipFree(p);
+	}
+	template <typename T>
+	int up(T** d, const T* h, size_t count) {
+		if(hipMalloc((void**)d, count * sizeof(T) + 16) != hipSuccess) return fail(BT2G_ERR_NOMEM, "hipMalloc");
+		ps.push_back(*d);
+		if(h && count) {
+			if(hipMemcpy(*d, h, count * sizeof(T), hipMemcpyHostToDevice) != hipSuccess)
+				return fail(BT2G_ERR_HIP, "hipMemcpy H2D");
+		}
+		return BT2G_OK;
+	}
+};
+
+template <typename T>
+int down(T* h, const T* d, size_t count) {
+	if(count == 0) return BT2G_OK;
+	HIPCHK(hipMemcpy(h, d, count * sizeof(T), hipMemcpyDeviceToHost));
+	return BT2G_OK;
+}
+}  // namespace
+
+extern "C" {
+
+int bt2g_exact_sweep(bt2g_ctx* c, const uint8_t* reads, uint32_t stride, const uint32_t* lens, uint32_t n,
+                     uint32_t mine_max, int nofw, int norc, uint32_t* out) {
+	if(!c) return fail(BT2G_ERR_ARG, "null ctx");
+	HIPCHK(hipSetDevice(c->device));
+	Tmp t;
+	uint8_t* dr;
+	uint32_t *dl, *dout;
+	int rc;
+	if((rc = t.up(&dr, reads, (size_t)n * stride)) || (rc = t.up(&dl, lens, n)) ||
+	   (rc = t.up(&dout, (const uint32_t*)nullptr, (size_t)n * 8)))
+		return rc;
+	if((rc = bt2g_exact_sweep_dev(c, dr, stride, dl, n, mine_max, nofw, norc, dout, nullptr))) return rc;
+	HIPCHK(hipStreamSynchronize(c->stream));
+	return down(out, dout, (size_t)n * 8);
+}
+
+int bt2g_seed_search(bt2g_ctx* c, const uint8_t* reads, uint32_t stride, const uint32_t* lens, uint32_t n,
+                     uint32_t seedlen, uint32_t interval, uint32_t offset, uint32_t maxseeds, uint32_t* out,
+                     int32_t* nseeds, uint32_t* bwops, uint32_t* loads) {
+	if(!c) return fail(BT2G_ERR_ARG, "null ctx");
+	HIPCHK(hipSetDevice(c->device));
+	Tmp t;
+	uint8_t* dr;
+	uint32_t *dl, *dout, *dops, *dld = nullptr;
+	int32_t* dns;
+	int rc;
+	size_t no = (size_t)n * 2 * maxseeds * 4;
+	if((rc = t.up(&dr, reads, (size_t)n * stride)) || (rc = t.up(&dl, lens, n)) ||
+	   (rc = t.up(&dout, (const uint32_t*)nullptr, no)) || (rc = t.up(&dns, (const int32_t*)nullptr, n)) ||
+	   (rc = t.up(&dops, (const uint32_t*)nullptr, n)))
+		return rc;
+	if(loads && (rc = t.up(&dld, (const uint32_t*)nullptr, n))) return rc;
+	if((rc = bt2g_seed_search_dev(c, dr, stride, dl, n, seedlen, interval, offset, maxseeds, dout, dns, dops, dld,
+	                              nullptr)))
+		return rc;
+	HIPCHK(hipStreamSynchronize(c->stream));
+	if((rc = down(out, dout, no)) || (rc = down(nseeds, dns, n)) || (rc = down(bwops, dops, n))) return rc;
+	if(loads && (rc = down(loads, dld, n))) return rc;
+	return BT2G_OK;
+}
+
+int bt2g_one_mm(bt2g_ctx* c, const uint8_t* reads, const uint8_t* quals, uint32_t stride, const uint32_t* lens,
+                uint32_t n, const int32_t* minsc, const bt2g_scoring* sc, int nofw, int norc, uint32_t cap,
+                bt2g_mm1* hits, int32_t* counts, uint32_t* bwops, uint32_t* loads) {
+	if(!c) return fail(BT2G_ERR_ARG, "null ctx");
+	HIPCHK(hipSetDevice(c->device));
+	Tmp t;
+	uint8_t *dr, *dq;
+	uint32_t *dl, *dops, *dld = nullptr;
+	int32_t *dms, *dcnt;
+	bt2g_mm1* dh;
+	int rc;
+	if((rc = t.up(&dr, reads, (size_t)n * stride)) || (rc = t.up(&dq, quals, (size_t)n * stride)) ||
+	   (rc = t.up(&dl, lens, n)) || (rc = t.up(&dms, minsc, n)) ||
+	   (rc = t.up(&dh, (const bt2g_mm1*)nullptr, (size_t)n * cap)) ||
+	   (rc = t.up(&dcnt, (const int32_t*)nullptr, n)) || (rc = t.up(&dops, (const uint32_t*)nullptr, n)))
+		return rc;
+	if(loads && (rc = t.up(&dld, (const uint32_t*)nullptr, n))) return rc;
+	int rc2 = bt2g_one_mm_dev(c, dr, dq, stride, dl, n, dms, sc, nofw, norc, cap, dh, dcnt, dops, dld, nullptr);
+	if(rc2 && rc2 != BT2G_ERR_OVERFLOW) return rc2;
+	HIPCHK(hipStreamSynchronize(c->stream));
+	if((rc = down(hits, dh, (size_t)n * cap)) || (rc = down(counts, dcnt, n)) || (rc = down(bwops, dops, n)))
+		return rc;
+	if(loads && (rc = down(loads, dld, n))) return rc;
+	return rc2;
+}
+
+int bt2g_get_offset(bt2g_ctx* c, const uint32_t* rows, uint32_t n, uint32_t* offs, uint32_t* loads) {
+	if(!c) return fail(BT2G_ERR_ARG, "null ctx");
+	HIPCHK(hipSetDevice(c->device));
+	Tmp t;
+	uint32_t *drow, *doff, *dld = nullptr;
+	int rc;
+	if((rc = t.up(&drow, rows, n)) || (rc = t.up(&doff, (const uint32_t*)nullptr, n))) return rc;
+	if(loads && (rc = t.up(&dld, (const uint32_t*)nullptr, n))) return rc;
+	if((rc = bt2g_get_offset_dev(c, drow, n, doff, dld, nullptr))) return rc;
+	HIPCHK(hipStreamSynchronize(c->stream));
+	if((rc = down(offs, doff, n))) return rc;
+	if(loads && (rc = down(loads, dld, n))) return rc;
+	return BT2G_OK;
+}
+
+int bt2g_sw_align(bt2g_ctx* c, const uint8_t* reads, const uint8_t* quals, uint32_t stride, const uint32_t* lens,
+                  const bt2g_sw_problem* probs, uint32_t nprob, const uint8_t* windows, uint64_t windows_len,
+                  const bt2g_scoring* sc, int enable8, uint32_t cap, bt2g_sw_result* res, bt2g_sw_cand* cands,
+                  int16_t* mat, const uint64_t* mat_off) {
+	if(!c) return fail(BT2G_ERR_ARG, "null ctx");
+	HIPCHK(hipSetDevice(c->device));
+	if(nprob == 0) return BT2G_OK;
+	uint32_t nreads = 0;
+	for(uint32_t i = 0; i < nprob; i++) nreads = probs[i].read + 1 > nreads ? probs[i].read + 1 : nreads;
+	Tmp t;
+	uint8_t *dr, *dq, *dw = nullptr;
+	uint32_t* dl;
+	bt2g_sw_problem* dp;
+	bt2g_sw_result* dres;
+	bt2g_sw_cand* dc;
+	int16_t* dm = nullptr;
+	uint64_t* dmo = nullptr;
+	int rc;
+	if((rc = t.up(&dr, reads, (size_t)nreads * stride)) || (rc = t.up(&dq, quals, (size_t)nreads * stride)) ||
+	   (rc = t.up(&dl, lens, nreads)) || (rc = t.up(&dp, probs, nprob)) ||
+	   (rc = t.up(&dres, (const bt2g_sw_result*)nullptr, nprob)) ||
+	   (rc = t.up(&dc, (const bt2g_sw_cand*)nullptr, (size_t)nprob * cap)))
+		return rc;
+	if(windows && windows_len && (rc = t.up(&dw, windows, windows_len))) return rc;
+	size_t matn = 0;
+	if(mat) {
+		for(uint32_t i = 0; i < nprob; i++) {
+			size_t e = mat_off[i] + (size_t)lens[probs[i].read] * probs[i].ncol * 3;
+			matn = e > matn ? e : matn;
+		}
+		if((rc = t.up(&dm, (const int16_t*)nullptr, matn)) || (rc = t.up(&dmo, mat_off, nprob))) return rc;
+	}
+	if((rc = bt2g_sw_align_dev(c, dr, dq, stride, dl, dp, nprob, dw, sc, enable8, cap, dres, dc, dm, dmo, nullptr)))
+		return rc;
+	HIPCHK(hipStreamSynchronize(c->stream));
+	if((rc = down(res, dres, nprob)) || (rc = down(cands, dc, (size_t)nprob * cap))) return rc;
+	if(mat && (rc = down(mat, dm, matn))) return rc;
+	for(uint32_t i = 0; i < nprob; i++)
+		if(res[i].ncand > (int32_t)cap) return fail(BT2G_ERR_OVERFLOW, "problem %u: %d candidates > cap %u", i,
+		                                             res[i].ncand, cap);
+	return BT2G_OK;
+}
+
+}  // extern "C"

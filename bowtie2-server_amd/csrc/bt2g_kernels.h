@@ -1,0 +1,38 @@
+// bt2g_kernels.h -- launchers shared by the kernel files and the host API.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+#include "../../include/bt2g.h"
+#include "fm_device.h"
+
+// Scoring constants of the SW fills (Scoring, scoring.h:103-131, 417-440).
+struct SwConst {
+	int32_t match, npen, gapbar;
+	int32_t rdgo, rdge, rfgo, rfge;
+	int32_t mmpen[41];          // Scoring::mmpens for Phred 0..40 (capped at 40)
+};
+
+void sw_fill_consts(const bt2g_scoring& sc, SwConst& h);
+
+void launch_exact_sweep(const DevEbwt& e, const uint8_t* reads, uint32_t stride, const uint32_t* lens, uint32_t n,
+                        uint32_t mine_max, int nofw, int norc, uint32_t* out, hipStream_t st);
+void launch_seed_search(const DevEbwt& F, const DevEbwt& B, const uint8_t* reads, uint32_t stride,
+                        const uint32_t* lens, uint32_t n, uint32_t seedlen, uint32_t interval, uint32_t offset,
+                        uint32_t maxseeds, uint32_t* out, int32_t* nseeds, uint32_t* bwops, uint32_t* loads,
+                        hipStream_t st);
+void launch_one_mm(const DevEbwt& F, const DevEbwt& B, const uint8_t* reads, const uint8_t* quals, uint32_t stride,
+                   const uint32_t* lens, uint32_t n, const int32_t* minsc, const bt2g_scoring& sc, int nofw,
+                   int norc, uint32_t cap, bt2g_mm1* slots, int32_t* slot_counts, bt2g_mm1* hits, int32_t* counts,
+                   uint32_t* ops, uint32_t* loads, int32_t* overflow, hipStream_t st);
+void launch_get_offset(const DevEbwt& e, const uint32_t* rows, uint32_t n, uint32_t* offs, uint32_t* loads,
+                       hipStream_t st);
+void launch_sw_partition(const bt2g_sw_problem* probs, uint32_t nprob, int local, int enable8, uint32_t* list8,
+                         uint32_t* n8, uint32_t* list16, uint32_t* n16, hipStream_t st);
+void launch_sw_fill(int variant, const bt2g_sw_problem* probs, uint32_t nprob, const uint32_t* list,
+                    const uint32_t* list_n, const uint8_t* reads, const uint8_t* quals, uint32_t stride,
+                    const uint32_t* lens, const uint8_t* windows, const uint8_t* ref_codes,
+                    const uint64_t* ref_starts, const SwConst& c, uint32_t cap, uint32_t* bnd,
+                    uint32_t bnd_cols, bt2g_sw_result* res, bt2g_sw_cand* cands, int16_t* mat,
+                    const uint64_t* mat_off, uint32_t* sat_list, uint32_t* sat_n, hipStream_t st);
+void launch_sort_cands(const bt2g_sw_result* res, bt2g_sw_cand* cands, uint32_t nprob, uint32_t cap,
+                       hipStream_t st);

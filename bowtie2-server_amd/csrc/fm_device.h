@@ -1,0 +1,167 @@
+// fm_device.h -- device-side FM-index primitives for gfx950.
+//
+// HBM layout (one copy per GPU, written once by index_load.cpp):
+//   sides  : the .bt2 "ebwt" array unchanged -- 64-B sides, 48 B of 2-bit BWT
+//            (192 rows, row k at bits 2*(k%4) of byte k/4) followed by 4 u32
+//            occurrence counts of A,C,G,T before the side (bt2_idx.h:1753-1757,
+//            2929-3081).  A side is exactly one 64-B HBM request: an LF step is
+//            one (or two, when top/bot rows sit in different sides) 64-B gathers.
+//   ftab/eftab/fchr/offs : the .bt2 arrays unchanged.
+//
+// Counting follows bt2_idx.h:1758-2080 (countBt2Side[Ex], countUpTo[Ex],
+// '$'-as-'A' correction at 1766-1774/1891-1899), but per side it is done with
+// 32-bit bit-plane masks and popcounts instead of the byte LUT.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#define BT2G_OFF_MASK 0xffffffffu
+
+struct DevEbwt {
+	const uint8_t*  sides;
+	const uint32_t* ftab;
+	const uint32_t* eftab;
+	const uint32_t* offs;
+	uint32_t len;
+	uint32_t zoff;
+	uint32_t zbyte;      // _zEbwtByteOff (bt2_idx.h:1631-1641)
+	int32_t  zbp;        // _zEbwtBpOff
+	uint32_t ftab_chars;
+	uint32_t off_rate;
+	int32_t  fw;         // Ebwt::fw()
+	uint32_t fchr[5];
+};
+
+// One loaded side: 12 BWT words (16 rows each) + 4 occ counts.
+struct SideData {
+	uint32_t w[12];
+	uint32_t occ[4];
+};
+
+__device__ __forceinline__ void load_side(const DevEbwt& e, uint32_t side, SideData& s) {
+	typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+	const u32x4* p = reinterpret_cast<const u32x4*>(e.sides + (size_t)side * 64u);
+	u32x4 a = p[0], b = p[1], c = p[2], d = p[3];
+	s.w[0] = a.x; s.w[1] = a.y; s.w[2] = a.z; s.w[3] = a.w;
+	s.w[4] = b.x; s.w[5] = b.y; s.w[6] = b.z; s.w[7] = b.w;
+	s.w[8] = c.x; s.w[9] = c.y; s.w[10] = c.z; s.w[11] = c.w;
+	s.occ[0] = d.x; s.occ[1] = d.y; s.occ[2] = d.z; s.occ[3] = d.w;
+}
+
+// Raw counts of A, C, G, T among the first `charOff` rows of the side (the '$'
+// is still counted as an 'A' here).
+__device__ __forceinline__ void side_counts(const SideData& s, uint32_t charOff, uint32_t cnt[4]) {
+	uint32_t a = 0, c = 0, g = 0;
+#pragma unroll
+	for(int k = 0; k < 12; k++) {
+		int nk = (int)charOff - 16 * k;
+		nk = nk < 0 ? 0 : (nk > 16 ? 16 : nk);
+		uint32_t m = nk >= 16 ? 0x55555555u : ((1u << (2 * nk)) - 1u) & 0x55555555u;
+		uint32_t lo = s.w[k] & 0x55555555u;
+		uint32_t hi = (s.w[k] >> 1) & 0x55555555u;
+		a += __builtin_popcount(~(lo | hi) & m);
+		c += __builtin_popcount(lo & ~hi & m);
+		g += __builtin_popcount(hi & ~lo & m);
+	}
+	cnt[0] = a; cnt[1] = c; cnt[2] = g; cnt[3] = charOff - a - c - g;
+}
+
+__device__ __forceinline__ uint32_t side_count1(const SideData& s, uint32_t charOff, int ch) {
+	uint32_t n = 0;
+	const uint32_t x = (uint32_t)(3 - ch) * 0x55555555u;   // c_table[ch] restricted to 32 bits
+#pragma unroll
+	for(int k = 0; k < 12; k++) {
+		int nk = (int)charOff - 16 * k;
+		nk = nk < 0 ? 0 : (nk > 16 ? 16 : nk);
+		uint32_t m = nk >= 16 ? 0x55555555u : ((1u << (2 * nk)) - 1u) & 0x55555555u;
+		uint32_t y = s.w[k] ^ x;
+		n += __builtin_popcount(y & (y >> 1) & m);
+	}
+	return n;
+}
+
+__device__ __forceinline__ int side_rowL(const SideData& s, uint32_t charOff) {
+	return (int)((s.w[charOff >> 4] >> (2 * (charOff & 15))) & 3u);
+}
+
+// '$' correction of countBt2Side/Ex: true iff the '$' (stored as 'A') lies in
+// this side strictly before <by,bp>.
+__device__ __forceinline__ bool dollar_before(const DevEbwt& e, uint32_t side, uint32_t charOff) {
+	uint32_t sbo = side * 64u, by = charOff >> 2, bp = charOff & 3u;
+	if(sbo <= e.zbyte && sbo + by >= e.zbyte) {
+		if(sbo + by > e.zbyte || (sbo + by == e.zbyte && (int)bp > e.zbp)) return true;
+	}
+	return false;
+}
+
+// countBt2SideEx for a row whose side is loaded in s.
+__device__ __forceinline__ void occ4(const DevEbwt& e, const SideData& s, uint32_t row, uint32_t out[4]) {
+	uint32_t side = row / 192u, co = row % 192u;
+	uint32_t c[4];
+	side_counts(s, co, c);
+	if(dollar_before(e, side, co)) c[0]--;
+#pragma unroll
+	for(int i = 0; i < 4; i++) out[i] = c[i] + s.occ[i] + e.fchr[i];
+}
+
+// countBt2Side for one character.
+__device__ __forceinline__ uint32_t occ1(const DevEbwt& e, const SideData& s, uint32_t row, int ch) {
+	uint32_t side = row / 192u, co = row % 192u;
+	uint32_t n = side_count1(s, co, ch);
+	if(ch == 0 && dollar_before(e, side, co)) n--;
+	return n + s.occ[ch] + e.fchr[ch];
+}
+
+__device__ __forceinline__ uint32_t ftab_hi(const DevEbwt& e, uint32_t i) {
+	uint32_t v = e.ftab[i];
+	return v <= e.len ? v : e.eftab[(v ^ BT2G_OFF_MASK) * 2 + 1];
+}
+__device__ __forceinline__ uint32_t ftab_lo(const DevEbwt& e, uint32_t i) {
+	uint32_t v = e.ftab[i];
+	return v <= e.len ? v : e.eftab[(v ^ BT2G_OFF_MASK) * 2];
+}
+
+// Bidirectional range state after one step.
+struct BiRange {
+	uint32_t t[4], b[4], tp[4], bp[4];
+};
+
+// INIT_LOCS + mapBiLFEx / mapLF1 as one step from [top,bot) (mirror start topp).
+// Loads one side when both rows share it (initFromTopBot, bt2_idx.h:325-352).
+// Returns the number of 64-B sides loaded.
+__device__ __forceinline__ int bi_step(const DevEbwt& e, uint32_t top, uint32_t bot, uint32_t topp,
+                                       uint32_t t[4], uint32_t b[4], uint32_t tp[4], uint32_t bp[4]) {
+	uint32_t st = top / 192u, sb = bot / 192u;
+	SideData s1;
+	load_side(e, st, s1);
+	occ4(e, s1, top, t);
+	int loads = 1;
+	if(sb == st) {
+		occ4(e, s1, bot, b);
+	} else {
+		SideData s2;
+		load_side(e, sb, s2);
+		occ4(e, s2, bot, b);
+		loads = 2;
+	}
+	bp[0] = tp[0] + (b[0] - t[0]);
+	tp[1] = bp[0];
+	bp[1] = tp[1] + (b[1] - t[1]);
+	tp[2] = bp[1];
+	bp[2] = tp[2] + (b[2] - t[2]);
+	tp[3] = bp[2];
+	bp[3] = tp[3] + (b[3] - t[3]);
+	return loads;
+}
+
+// A read (or its reverse complement / reversal) as the reference's BTDnaString
+// views: patFw (rev=0,cmp=0), patRc (1,1), patFwRev (1,0), patRcRev (0,1).
+struct SeqView {
+	const uint8_t* p;
+	uint32_t len;
+	bool rev, cmp;
+	__device__ __forceinline__ int operator[](uint32_t i) const {
+		int c = p[rev ? len - 1 - i : i];
+		return cmp ? (c > 3 ? 4 : 3 - c) : c;
+	}
+};

@@ -247,22 +247,20 @@ def build_ebwt(text, sa, recs, flags, rstarts, plen, off_rate=4, ftab_chars=10, 
         tgt = np.where(nxt < len(long_rows), sufint_by_row[long_rows[np.minimum(nxt, len(long_rows) - 1)]],
                        ftab_len - 1)
         np.add.at(absorb, tgt, 1)
+    # Ebwt::buildToDisk prefix pass (bt2_idx.h:3145-3159), vectorised:
+    # lo[i] = ftab[i] + ftabHi(i-1), ftabHi(i) = lo[i] + absorb[i]
+    cnt = ftab.copy()
+    cnt[0] = 0
+    ab = absorb.copy()
+    ab[0] = 0
+    lo = np.cumsum(cnt) + np.concatenate([[0], np.cumsum(ab)[:-1]])
+    out = lo.copy()
     eftab = np.zeros(eftab_len, dtype=np.int64)
-    out = np.zeros(ftab_len, dtype=np.int64)
-    ecur = 0
-    hi_prev = 0  # ftabHi(i-1)
-    for i in range(1, ftab_len):
-        lo = ftab[i] + hi_prev
-        if absorb[i] > 0:
-            hi = lo + absorb[i]
-            eftab[ecur * 2] = lo
-            eftab[ecur * 2 + 1] = hi
-            out[i] = ecur ^ OFF_MASK
-            ecur += 1
-            hi_prev = hi
-        else:
-            out[i] = lo
-            hi_prev = lo
+    for ecur, i in enumerate(np.nonzero(ab > 0)[0]):
+        eftab[ecur * 2] = lo[i]
+        eftab[ecur * 2 + 1] = lo[i] + ab[i]
+        out[i] = ecur ^ OFF_MASK
+    out[0] = 0
     offs = sa[:: 1 << off_rate].astype(np.uint32)
     return Ebwt(length=n, line_rate=line_rate, off_rate=off_rate, ftab_chars=ftab_chars, flags=flags,
                 plen=np.asarray(plen, np.uint32), rstarts=np.asarray(rstarts, np.uint32),

@@ -1,0 +1,222 @@
+/*
+ * bt2g.h -- C ABI of the MI355X (gfx950) engines for bowtie2's seed-and-extend
+ * hot path.  Drop-in boundary for the reference's per-thread C++ seams
+ * (SURVEY.md section 8b); every entry point names the reference interface it
+ * replaces.  Plain pointers and sizes only; no C++ or torch types cross it; no
+ * exceptions escape it; every call returns a status (BT2G_OK == 0).
+ *
+ * Batching model: the reference calls its seams one read (one DP problem) at a
+ * time from each worker thread; here the caller hands over a whole batch.  The
+ * per-read results are exactly those of the reference call on that read.
+ *
+ *   reads   : n rows of `stride` bytes, codes 0..3 = A,C,G,T, 4 = N (Read::patFw)
+ *   quals   : n rows of `stride` bytes, Phred+33 ASCII (Read::qual)
+ *   lens    : n read lengths (<= stride, <= BT2G_MAX_READ_LEN)
+ *
+ * Two flavours of every batch call:
+ *   <name>_dev(...)     all array arguments are device pointers (HBM-resident),
+ *                      enqueued on `stream` (a hipStream_t, NULL = context stream),
+ *                      asynchronous.
+ *   <name>(...)         same arguments as host pointers; copies in, runs, copies
+ *                      out, synchronises.  For callers that keep data on the host.
+ */
+#ifndef BT2G_H_
+#define BT2G_H_
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define BT2G_OK            0
+#define BT2G_ERR_IO       -1
+#define BT2G_ERR_FORMAT   -2
+#define BT2G_ERR_HIP      -3
+#define BT2G_ERR_ARG      -4
+#define BT2G_ERR_NOMEM    -5
+#define BT2G_ERR_OVERFLOW -6
+
+#define BT2G_MAX_READ_LEN 1024
+
+typedef struct bt2g_ctx bt2g_ctx;
+
+/* Scoring scheme, same parameters as Scoring::Scoring (scoring.h:136-173) with
+ * COST_MODEL_QUAL mismatches and COST_MODEL_CONSTANT N penalty (bowtie2
+ * defaults: end-to-end {0,6,2,1,5,3,5,3,4,0}, --local {2,6,2,1,5,3,5,3,4,1}). */
+typedef struct {
+	int32_t match;      /* --ma, bonus for a match (0 in end-to-end mode) */
+	int32_t mmp_max;    /* --mp MX */
+	int32_t mmp_min;    /* --mp MN */
+	int32_t npen;       /* --np */
+	int32_t rdg_const;  /* --rdg open part */
+	int32_t rdg_lin;    /* --rdg extend */
+	int32_t rfg_const;  /* --rfg open part */
+	int32_t rfg_lin;    /* --rfg extend */
+	int32_t gapbar;     /* --gbar */
+	int32_t local;      /* 1 = --local */
+	double  ncl_const;  /* --n-ceil constant (L,0,0.15 default) */
+	double  ncl_lin;    /* --n-ceil linear coefficient */
+} bt2g_scoring;
+
+/* Index arrays already in host memory (the arrays of Ebwt::readIntoMemory,
+ * bt2_io.cpp:39-616, for the forward index and the mirror ".rev" index, plus
+ * the unpacked reference of BitPairReference, reference.cpp:100-235). */
+typedef struct {
+	uint32_t len, zoff, ftab_chars, off_rate, line_rate;
+	const uint32_t* fchr;      /* 5 */
+	const uint8_t*  sides;     /* numSides * 64 */
+	uint64_t        sides_bytes;
+	const uint32_t* ftab;      /* 4^ftab_chars + 1 */
+	const uint32_t* eftab;     /* 2 * ftab_chars */
+	const uint32_t* offs;      /* SA sample, forward index only (NULL for mirror) */
+	uint64_t        offs_len;
+	const uint32_t* rstarts;   /* 3 * nfrag (forward index) */
+	uint32_t        nfrag;
+} bt2g_ebwt_mem;
+
+typedef struct {
+	bt2g_ebwt_mem fw, bw;
+	const uint8_t*  ref_codes;   /* all references concatenated, codes 0..4 */
+	const uint64_t* ref_starts;  /* nref + 1 offsets into ref_codes */
+	uint32_t        nref;
+} bt2g_index_mem;
+
+/* ---- lifetime ---------------------------------------------------------- */
+
+/* Load <base>.{1,2,rev.1,3,4}.bt2 and make the FM index (fw + mirror sides,
+ * ftab/eftab, fchr, SA sample) and the reference resident in HBM of `device`.
+ * Replaces Ebwt ctor + loadIntoMemory (bt2_search.cpp:5080-5097, 4870-4892) and
+ * BitPairReference (bt2_search.cpp:4816-4832). */
+int bt2g_open(const char* index_base, int device, bt2g_ctx** out);
+/* Same from arrays already in host memory. */
+int bt2g_open_mem(const bt2g_index_mem* m, int device, bt2g_ctx** out);
+int bt2g_close(bt2g_ctx* ctx);
+/* out: [len, zoff_fw, zoff_bw, fchr0..4, ftab_chars, off_rate, num_sides,
+ *       nref, hbm_bytes]  (n <= 13 words written) */
+int bt2g_info(bt2g_ctx* ctx, uint64_t* out, int n);
+/* Last error message of this thread. */
+const char* bt2g_last_error(void);
+
+/* ---- FM engine ----------------------------------------------------------- */
+
+/* SeedAligner::exactSweep (aligner_seed.h:1715-1726, aligner_seed.cpp:854-968)
+ * for every read, both strands.  out: n x 8 u32 =
+ *   {mineFw, mineRc, fw_top, fw_bot, rc_top, rc_bot, bwops, side_loads}
+ * (top/bot = the exact end-to-end SA range when min edits == 0, else 0,0;
+ * mineFw/mineRc are left 0 for a skipped strand). */
+int bt2g_exact_sweep(bt2g_ctx* ctx, const uint8_t* reads, uint32_t stride, const uint32_t* lens, uint32_t n,
+                     uint32_t mine_max, int nofw, int norc, uint32_t* out);
+int bt2g_exact_sweep_dev(bt2g_ctx* ctx, const uint8_t* reads, uint32_t stride, const uint32_t* lens, uint32_t n,
+                         uint32_t mine_max, int nofw, int norc, uint32_t* out, void* stream);
+
+/* One exact-seed round: Seed::mmSeeds(0, seedlen) + instantiateSeeds(offset,
+ * interval) + searchAllSeeds (aligner_seed.h:1667-1694, aligner_seed.cpp:498-718,
+ * 1633-2033; bt2_search.cpp:3853-3906).  For read i, strand f (0 = fw, 1 = rc)
+ * and seed s: out[((i*2+f)*maxseeds+s)*4 + {0..3}] = {topf, botf, topb, botb}
+ * (all 0 when the seed has no hit or was filtered for an N).  nseeds[i] =
+ * number of seed offsets (0 when the round is skipped, bt2_search.cpp:3866).
+ * bwops[i] = FM ops of the read (== SeedSearchMetrics::bwops); loads[i] (optional,
+ * may be NULL) = 64-B sides gathered for the read (roofline bytes). */
+int bt2g_seed_search(bt2g_ctx* ctx, const uint8_t* reads, uint32_t stride, const uint32_t* lens, uint32_t n,
+                     uint32_t seedlen, uint32_t interval, uint32_t offset, uint32_t maxseeds,
+                     uint32_t* out, int32_t* nseeds, uint32_t* bwops, uint32_t* loads);
+int bt2g_seed_search_dev(bt2g_ctx* ctx, const uint8_t* reads, uint32_t stride, const uint32_t* lens, uint32_t n,
+                         uint32_t seedlen, uint32_t interval, uint32_t offset, uint32_t maxseeds,
+                         uint32_t* out, int32_t* nseeds, uint32_t* bwops, uint32_t* loads, void* stream);
+
+/* One 1-mismatch end-to-end hit (SeedResults::add1mmEe, aligner_seed.h:1248). */
+typedef struct {
+	uint32_t top, bot;   /* SA range in the forward BWT */
+	int32_t  fw;         /* read orientation */
+	int32_t  score;
+	int32_t  pos;        /* Edit::pos, offset from the 5' end */
+	int32_t  chr;        /* reference base 0..3 */
+	int32_t  qchr;       /* read base 0..4 */
+	int32_t  pad;
+} bt2g_mm1;
+
+/* SeedAligner::oneMmSearch with rep1mm=true, repex=false exactly as
+ * bt2_search.cpp:3654-3667 calls it (aligner_seed.h:1731-1743,
+ * aligner_seed.cpp:973-1323).  Hits are returned per read in the reference's
+ * discovery order: hits[i*cap .. i*cap+counts[i]), counts[i] may exceed cap
+ * (then BT2G_ERR_OVERFLOW is returned and only cap hits are stored).  bwops and
+ * loads (optional) as for bt2g_seed_search. */
+int bt2g_one_mm(bt2g_ctx* ctx, const uint8_t* reads, const uint8_t* quals, uint32_t stride, const uint32_t* lens,
+                uint32_t n, const int32_t* minsc, const bt2g_scoring* sc, int nofw, int norc, uint32_t cap,
+                bt2g_mm1* hits, int32_t* counts, uint32_t* bwops, uint32_t* loads);
+int bt2g_one_mm_dev(bt2g_ctx* ctx, const uint8_t* reads, const uint8_t* quals, uint32_t stride,
+                    const uint32_t* lens, uint32_t n, const int32_t* minsc, const bt2g_scoring* sc, int nofw,
+                    int norc, uint32_t cap, bt2g_mm1* hits, int32_t* counts, uint32_t* bwops, uint32_t* loads,
+                    void* stream);
+
+/* Ebwt::getOffset (bt2_idx.cpp:150-171): joined-text offset of each SA row.
+ * loads (optional): 64-B sides gathered per row. */
+int bt2g_get_offset(bt2g_ctx* ctx, const uint32_t* rows, uint32_t n, uint32_t* offs, uint32_t* loads);
+int bt2g_get_offset_dev(bt2g_ctx* ctx, const uint32_t* rows, uint32_t n, uint32_t* offs, uint32_t* loads,
+                        void* stream);
+
+/* ---- SW engine ----------------------------------------------------------- */
+
+/* One dynamic-programming problem (SwAligner::initRead + initRef,
+ * aligner_sw.cpp:34-271).  The reference window is either taken from the
+ * resident reference (win_off < 0: columns refl .. refl+ncol-1 of reference
+ * `refidx`, N outside it, plus the extra right column, aligner_sw.cpp:171-253)
+ * or given explicitly as ncol+1 masks (1,2,4,8,16) at windows[win_off]. */
+typedef struct {
+	uint32_t read;       /* row in reads/quals/lens */
+	int32_t  fw;         /* 1: align the read, 0: its reverse complement */
+	int64_t  refl;       /* leftmost reference offset (may be < 0) */
+	int64_t  win_off;    /* >= 0: offset of ncol+1 masks in `windows` */
+	uint32_t refidx;
+	uint32_t ncol;
+	int32_t  minsc;
+	uint32_t pad;
+} bt2g_sw_problem;
+
+/* Result of SwAligner::align (aligner_sw.cpp:500-729). */
+typedef struct {
+	int32_t  aligned;    /* return value of align() */
+	int32_t  best;       /* `best` (MIN_I32 for MIN_I64) */
+	int32_t  u8succ;     /* sse8succ_ */
+	int32_t  i16succ;    /* sse16succ_ */
+	int32_t  colstop;    /* colstop_ */
+	int32_t  lastsolcol; /* lastsolcol_ */
+	int32_t  ncand;      /* btncand_.size() (may exceed cap -> BT2G_ERR_OVERFLOW) */
+	int32_t  flag;
+} bt2g_sw_result;
+
+/* DpBtCandidate (aligner_sw_nuc.h), sorted by the reference's total order. */
+typedef struct {
+	int32_t row, col, score;
+} bt2g_sw_cand;
+
+/* Fill + candidate gather for every problem: the u8/i16 end-to-end or local
+ * fill chosen exactly as SwAligner::align does (u8 first when enable8; local
+ * u8 saturation falls back to i16).  cands[p*cap ..] receives the sorted
+ * candidate cells.  mat (optional, NULL to skip): per problem
+ * nrow*ncol*3 int16 H,E,F values in the fill's native domain, at mat_off[p]. */
+int bt2g_sw_align(bt2g_ctx* ctx, const uint8_t* reads, const uint8_t* quals, uint32_t stride, const uint32_t* lens,
+                  const bt2g_sw_problem* probs, uint32_t nprob, const uint8_t* windows, uint64_t windows_len,
+                  const bt2g_scoring* sc, int enable8, uint32_t cap, bt2g_sw_result* res, bt2g_sw_cand* cands,
+                  int16_t* mat, const uint64_t* mat_off);
+int bt2g_sw_align_dev(bt2g_ctx* ctx, const uint8_t* reads, const uint8_t* quals, uint32_t stride,
+                      const uint32_t* lens, const bt2g_sw_problem* probs, uint32_t nprob, const uint8_t* windows,
+                      const bt2g_scoring* sc, int enable8, uint32_t cap, bt2g_sw_result* res, bt2g_sw_cand* cands,
+                      int16_t* mat, const uint64_t* mat_off, void* stream);
+
+/* ---- multi-GPU ----------------------------------------------------------- */
+/* The only collective of the path: the caller sums these
+ * counters over ranks (RCCL all-reduce in bench.py / the server). */
+
+/* ---- measurement --------------------------------------------------------- */
+/* Kernel timing with HIP events on the launch stream (off by default). */
+int bt2g_set_profiling(bt2g_ctx* ctx, int on);
+/* kernel ids: 0 exact_sweep, 1 seed_search, 2 one_mm, 3 get_offset, 4 sw_align */
+int bt2g_kernel_stats(bt2g_ctx* ctx, int kernel, uint64_t* launches, double* total_ms);
+int bt2g_reset_stats(bt2g_ctx* ctx);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* BT2G_H_ */

@@ -104,6 +104,11 @@ struct SwAlignerX : public SwAligner {
 	}
 };
 
+// Gives the harness read access to SeedAligner's FM-op counter (bwops_).
+struct SeedAlignerX : public SeedAligner {
+	uint64_t ops() const { return bwops_; }
+};
+
 } // namespace
 
 extern "C" {
@@ -197,7 +202,7 @@ int bt2ref_get_stretch(void* vh, uint32_t refidx, uint64_t off, uint64_t len, ui
 void bt2ref_exact_sweep(void* vh, int n, const char** seqs, const char** quals,
                         int mineMax, uint64_t* out /* 8 per read */) {
 	RefHandle* h = (RefHandle*)vh;
-	SeedAligner al;
+	SeedAlignerX al;
 	SeedResults sr;
 	SeedSearchMetrics met;
 	ScoreParams sp = {0, 6, 2, 1, 5, 3, 5, 3, 4, 0, 0.0, 0.15};
@@ -208,13 +213,14 @@ void bt2ref_exact_sweep(void* vh, int n, const char** seqs, const char** quals,
 		sr.nextRead(rd);
 		size_t mineFw = 0, mineRc = 0;
 		met.reset();
+		uint64_t ops0 = al.ops();
 		size_t nelt = al.exactSweep(*h->fw, rd, sc, false, false, (size_t)mineMax,
 		                            mineFw, mineRc, true, sr, met);
 		uint64_t* o = out + 8 * (size_t)i;
 		o[0] = mineFw; o[1] = mineRc; o[2] = nelt;
 		EEHit f = sr.exactFwEEHit(), r = sr.exactRcEEHit();
 		o[3] = f.top; o[4] = f.bot; o[5] = r.top; o[6] = r.bot;
-		o[7] = met.bwops;
+		o[7] = al.ops() - ops0;  // exactSweep adds to bwops_ only (aligner_seed.cpp:808-818)
 	}
 }
 
@@ -225,7 +231,7 @@ void bt2ref_one_mm(void* vh, int n, const char** seqs, const char** quals,
                    const int64_t* minsc, int local, int nofw, int norc,
                    int cap, int64_t* out, int32_t* counts, uint64_t* bwops) {
 	RefHandle* h = (RefHandle*)vh;
-	SeedAligner al;
+	SeedAlignerX al;
 	SeedResults sr;
 	SeedSearchMetrics met;
 	ScoreParams sp = {local ? 2 : 0, 6, 2, 1, 5, 3, 5, 3, 4, local, 0.0, 0.15};
@@ -235,6 +241,7 @@ void bt2ref_one_mm(void* vh, int n, const char** seqs, const char** quals,
 		sr.clear();
 		sr.nextRead(rd);
 		met.reset();
+		uint64_t ops0 = al.ops();
 		al.oneMmSearch(h->fw, h->bw, rd, sc, minsc[i], nofw != 0, norc != 0, local != 0,
 		               false, true, sr, met);
 		const EList<EEHit>& hits = sr.mm1EEHits();
@@ -246,7 +253,7 @@ void bt2ref_one_mm(void* vh, int n, const char** seqs, const char** quals,
 			o[4] = hits[j].e1.pos; o[5] = (int64_t)hits[j].e1.chr | ((int64_t)hits[j].e1.qchr << 8);
 		}
 		counts[i] = (int32_t)hits.size();
-		bwops[i] = met.bwops;
+		bwops[i] = al.ops() - ops0;
 	}
 }
 
@@ -272,6 +279,12 @@ void bt2ref_seed_search(void* vh, int n, const char** seqs, const char** quals,
 	EList<SATuple> satups;
 	for(int i = 0; i < n; i++) {
 		Read rd("r", seqs[i], quals[i]);
+		uint32_t* o = out + (size_t)i * 2 * maxseeds * 4;
+		memset(o, 0, sizeof(uint32_t) * 2 * maxseeds * 4);
+		nseeds[i] = 0; bwops[i] = 0;
+		// bt2_search.cpp:3866-3869: the round is skipped when the offset drives
+		// the first seed off the end of the read.
+		if(offset > 0 && (size_t)(seedlen + offset) > rd.length()) continue;
 		sr.clear();
 		sr.nextRead(rd);
 		ca.nextRead();
@@ -285,8 +298,6 @@ void bt2ref_seed_search(void* vh, int n, const char** seqs, const char** quals,
 		int ns = (int)sr.numOffs();
 		nseeds[i] = ns;
 		bwops[i] = met.bwops;
-		uint32_t* o = out + (size_t)i * 2 * maxseeds * 4;
-		memset(o, 0, sizeof(uint32_t) * 2 * maxseeds * 4);
 		for(int fwi = 0; fwi < 2; fwi++) {
 			bool fw = fwi == 0;
 			for(int s = 0; s < ns && s < maxseeds; s++) {

@@ -1,0 +1,124 @@
+"""FM engine on the GPU (libbt2g.so) vs the reference's golden vectors and the
+CPU oracle.  Bit-exact: SA ranges, edit bounds, hit lists, FM-op counts."""
+import numpy as np
+import pytest
+
+from conftest import get_index, load_golden
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def engines():
+    import bt2g
+    es = {name: bt2g.Engine(index=get_index(name)) for name in ("lambda", "synth")}
+    yield es
+    for e in es.values():
+        e.close()
+
+
+@pytest.fixture(scope="module")
+def orc():
+    from oracle.oracle import Oracle
+    return Oracle()
+
+
+def _gold_exact_to_gpu_layout(ex):
+    # golden: mineFw, mineRc, nelt, fwtop, fwbot, rctop, rcbot, bwops
+    return np.stack([ex[:, 0], ex[:, 1], ex[:, 3], ex[:, 4], ex[:, 5], ex[:, 6], ex[:, 7]], 1).astype(np.uint32)
+
+
+@pytest.mark.parametrize("name", ["lambda", "synth"])
+def test_exact_sweep_golden(engines, name):
+    g = load_golden("fm_" + name)
+    out = engines[name].exact_sweep(g["reads"], g["lens"])
+    assert np.array_equal(out[:, :7], _gold_exact_to_gpu_layout(g["exact"]))
+    assert (out[:, 7] <= out[:, 6]).all()          # one side load per FM op at most
+
+
+@pytest.mark.parametrize("name", ["lambda", "synth"])
+@pytest.mark.parametrize("pol", ["s22", "s20", "s10"])
+def test_seed_search_golden(engines, name, pol):
+    g = load_golden("fm_" + name)
+    L, iv, off = (int(x) for x in g["seedpol_" + pol])
+    out, ns, ops, loads = engines[name].seed_search(g["reads"], g["lens"], L, iv, off, 64)
+    assert np.array_equal(ns, g["seedn_" + pol])
+    assert np.array_equal(out, g["seed_" + pol])
+    assert np.array_equal(ops, g["seedops_" + pol].astype(np.uint32))
+
+
+@pytest.mark.parametrize("name", ["lambda", "synth"])
+@pytest.mark.parametrize("mode", ["ee", "loc"])
+def test_one_mm_golden(engines, name, mode):
+    g = load_golden("fm_" + name)
+    hits, cnt, ops, _ = engines[name].one_mm(g["reads"], g["quals"], g["lens"], g["mmminsc_" + mode],
+                                             mode == "loc")
+    ref, refn = g["mm_" + mode], g["mmn_" + mode]
+    assert np.array_equal(cnt, refn)
+    assert np.array_equal(ops, g["mmops_" + mode].astype(np.uint32))
+    for i in range(len(refn)):
+        for k in range(refn[i]):
+            x, h = ref[i, k], hits[i, k]
+            assert (h["top"], h["bot"], h["fw"], h["score"], h["pos"]) == tuple(int(v) for v in x[:5]), (i, k)
+            assert (x[5] & 0xff) == ord("ACGTN"[h["chr"]]) and (x[5] >> 8) == ord("ACGTN"[h["qchr"]])
+
+
+@pytest.mark.parametrize("name", ["lambda", "synth"])
+def test_get_offset_golden(engines, name):
+    g = load_golden("fm_" + name)
+    offs, loads = engines[name].get_offset(g["off_rows"])
+    assert np.array_equal(offs, g["off_vals"])
+    assert loads.max() < 64
+
+
+def test_large_batch_vs_oracle(engines, orc):
+    """20k synthetic reads with errors, N's and ragged lengths; GPU == oracle."""
+    import synth
+    idx = get_index("synth")
+    gen = np.concatenate(idx.ref_codes)
+    n = 20000
+    codes, quals, _, _ = synth.reads(4242, gen, n, 150, sub=0.01, nrate=0.002)
+    lens = np.full(n, 150, np.uint32)
+    rng = np.random.default_rng(1)
+    short = rng.random(n) < 0.1
+    lens[short] = rng.integers(1, 150, short.sum())
+    for i in np.nonzero(short)[0]:
+        codes[i, lens[i]:] = 4
+    codes[5, :] = 4                                     # all-N read
+    fe, be = orc.ebwt(idx.fw, True), orc.ebwt(idx.bw, False)
+    e = engines["synth"]
+    o_gpu = e.exact_sweep(codes, lens)
+    o_cpu = orc.exact_sweep(fe, codes, lens)
+    assert np.array_equal(o_gpu[:, :7], _gold_exact_to_gpu_layout(o_cpu))
+    s_gpu, ns_gpu, ops_gpu, _ = e.seed_search(codes, lens, 22, 15, 0, 16)
+    s_cpu, ns_cpu, ops_cpu = orc.seed_search(fe, be, codes, lens, 22, 15, 0, 16)
+    assert np.array_equal(ns_gpu, ns_cpu) and np.array_equal(s_gpu, s_cpu)
+    assert np.array_equal(ops_gpu, ops_cpu.astype(np.uint32))
+    ms = np.array([int(-0.6 - 0.6 * L) for L in lens], np.int64)
+    h_gpu, c_gpu, op_gpu, _ = e.one_mm(codes[:4000], quals[:4000], lens[:4000], ms[:4000], False)
+    h_cpu, c_cpu, op_cpu = orc.one_mm(fe, be, codes[:4000], quals[:4000], lens[:4000], ms[:4000], False)
+    assert np.array_equal(c_gpu, c_cpu) and np.array_equal(op_gpu, op_cpu.astype(np.uint32))
+    for i in np.nonzero(c_cpu)[0]:
+        for k in range(c_cpu[i]):
+            h = h_gpu[i, k]
+            assert (h["top"], h["bot"], h["fw"], h["score"], h["pos"], h["chr"], h["qchr"]) == \
+                tuple(int(v) for v in h_cpu[i, k])
+
+
+def test_open_from_files_and_edge_cases(tmp_path):
+    import bt2g
+    import bt2_index as bi
+    idx = get_index("lambda")
+    base = str(tmp_path / "lam")
+    bi.write_index(base, idx)
+    with bt2g.Engine(index_base=base) as e:
+        info = e.info()
+        assert info[0] == idx.fw.length and info[1] == idx.fw.zoff and info[2] == idx.bw.zoff
+        empty = e.exact_sweep(np.zeros((0, 150), np.uint8), np.zeros(0, np.uint32))
+        assert empty.shape == (0, 8)
+        # nofw / norc leave the skipped strand empty
+        g = load_golden("fm_lambda")
+        a = e.exact_sweep(g["reads"], g["lens"], nofw=True)
+        assert (a[:, 0] == 0).all() and (a[:, 2] == 0).all()
+        b = e.exact_sweep(g["reads"], g["lens"])
+        assert np.array_equal(a[:, [1, 4, 5]], b[:, [1, 4, 5]])

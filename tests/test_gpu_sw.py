@@ -1,0 +1,108 @@
+"""SW engine on the GPU vs SwAligner::align's own outputs (golden fixtures from
+the reference server's DP log and random problems) and vs the CPU oracle's full
+H/E/F matrices.  Bit-exact for all four fills (u8/i16 x end-to-end/local)."""
+import numpy as np
+import pytest
+
+from conftest import get_index, load_golden
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def eng():
+    import bt2g
+    e = bt2g.Engine(index=get_index("lambda"))
+    yield e
+    e.close()
+
+
+def golden_batch(g):
+    import bt2g
+    n = len(g["rd_index"])
+    probs = np.zeros(n, bt2g.SWPROB_DTYPE)
+    probs["read"] = g["rd_index"]
+    probs["fw"] = g["fw"]
+    probs["win_off"] = g["rf_off"][:-1]
+    probs["ncol"] = np.diff(g["rf_off"]) - 1
+    probs["minsc"] = g["minsc"]
+    return probs
+
+
+@pytest.mark.parametrize("fx", ["sw_log_ee", "sw_log_loc", "sw_rand_ee", "sw_rand_loc"])
+def test_sw_golden(eng, fx):
+    g = load_golden(fx)
+    local = bool(g["local"])
+    probs = golden_batch(g)
+    res, cands, _ = eng.sw_align(g["reads"], g["quals"], g["lens"], probs, windows=g["rf"], local=local,
+                                 cap=4096)
+    out = g["out"]
+    assert np.array_equal(res["aligned"], out[:, 0])
+    al = out[:, 0] == 1
+    assert np.array_equal(res["best"][al], out[al, 1])
+    assert np.array_equal(res["u8succ"], out[:, 2]) and np.array_equal(res["i16succ"], out[:, 3])
+    assert np.array_equal(res["colstop"], out[:, 4]) and np.array_equal(res["lastsolcol"], out[:, 5])
+    assert np.array_equal(res["ncand"], out[:, 6])
+    for p in range(len(probs)):
+        ref = g["cands"][g["cand_off"][p]:g["cand_off"][p + 1]]
+        got = cands[p, :len(ref)]
+        assert np.array_equal(np.stack([got["row"], got["col"], got["score"]], 1), ref), (fx, p)
+
+
+@pytest.mark.parametrize("local", [False, True])
+def test_sw_matrices_vs_oracle(eng, local):
+    """Full H/E/F of every cell (native value domain) against the oracle."""
+    from oracle.oracle import Oracle
+    orc = Oracle()
+    g = load_golden("sw_rand_loc" if local else "sw_rand_ee")
+    probs = golden_batch(g)[:120]
+    res, cands, (mat, off) = eng.sw_align(g["reads"], g["quals"], g["lens"], probs, windows=g["rf"],
+                                          local=local, want_mat=True)
+    for p in range(len(probs)):
+        ri = g["rd_index"][p]
+        L = int(g["lens"][ri])
+        rd, q = g["reads"][ri, :L], g["quals"][ri, :L]
+        if not g["fw"][p]:
+            rd, q = np.where(rd > 3, 4, 3 - rd)[::-1], q[::-1]
+        rf = g["rf"][g["rf_off"][p]:g["rf_off"][p + 1]]
+        o, c, m = orc.sw(rd, q, rf, int(probs["minsc"][p]), local, want_mat=True)
+        if not (o[2] or o[3]):
+            continue
+        ncol = int(probs["ncol"][p])
+        got = mat[off[p]:off[p] + L * ncol * 3].reshape(L, ncol, 3).astype(np.int32)
+        cs = int(o[4]) if local else ncol
+        assert np.array_equal(got[:, :cs], m[:, :cs]), p
+
+
+def test_sw_resident_reference(eng):
+    """Problems that point into the HBM-resident reference (incl. off-end N
+    padding and the extra right column) == the same windows given explicitly."""
+    import bt2g
+    import synth
+    idx = get_index("lambda")
+    gen = idx.ref_codes[0]
+    codes, quals, pos, fw = synth.reads(99, gen, 256, 150, sub=0.01)
+    rng = np.random.default_rng(2)
+    n = len(codes)
+    probs = np.zeros(n, bt2g.SWPROB_DTYPE)
+    probs["read"] = np.arange(n)
+    probs["fw"] = fw.astype(np.int32)
+    refl = pos.astype(np.int64) - 30 + rng.integers(-10, 10, n)
+    refl[:8] = [-40, -5, len(gen) - 100, len(gen) - 150, len(gen) - 200, 0, -150, len(gen) - 60]
+    probs["refl"] = refl
+    probs["win_off"] = -1
+    probs["ncol"] = 210
+    probs["minsc"] = -90
+    lens = np.full(n, 150, np.uint32)
+    res1, c1, _ = eng.sw_align(codes, quals, lens, probs)
+    wins = []
+    for i in range(n):
+        idxs = np.arange(refl[i], refl[i] + 211)
+        cc = np.where((idxs >= 0) & (idxs < len(gen)), gen[np.clip(idxs, 0, len(gen) - 1)], 4)
+        wins.append((1 << cc.astype(np.int32)).astype(np.uint8))
+    p2 = probs.copy()
+    p2["win_off"] = np.arange(n) * 211
+    res2, c2, _ = eng.sw_align(codes, quals, lens, p2, windows=np.concatenate(wins))
+    assert np.array_equal(res1, res2)
+    assert np.array_equal(c1, c2)
+    assert res1["aligned"].sum() > n // 2

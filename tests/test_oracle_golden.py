@@ -1,0 +1,98 @@
+"""Pins the CPU oracle (oracle/oracle.c) to the reference's own outputs
+(tests/golden/*.npz, generated from oracle/_ref by make_golden.py)."""
+import numpy as np
+import pytest
+
+from conftest import get_index, load_golden
+
+
+@pytest.fixture(scope="module")
+def orc():
+    from oracle.oracle import Oracle
+    return Oracle()
+
+
+def _ebwts(orc, name):
+    idx = get_index(name)
+    return orc.ebwt(idx.fw, True), orc.ebwt(idx.bw, False)
+
+
+@pytest.mark.parametrize("name", ["lambda", "synth"])
+def test_exact_sweep(orc, name):
+    g = load_golden("fm_" + name)
+    fe, _ = _ebwts(orc, name)
+    out = orc.exact_sweep(fe, g["reads"], g["lens"])
+    assert np.array_equal(out, g["exact"].astype(np.uint64))
+
+
+@pytest.mark.parametrize("name", ["lambda", "synth"])
+@pytest.mark.parametrize("pol", ["s22", "s20", "s10"])
+def test_seed_search(orc, name, pol):
+    g = load_golden("fm_" + name)
+    fe, be = _ebwts(orc, name)
+    L, iv, off = g["seedpol_" + pol]
+    out, ns, ops = orc.seed_search(fe, be, g["reads"], g["lens"], int(L), int(iv), int(off), 64)
+    assert np.array_equal(ns, g["seedn_" + pol])
+    assert np.array_equal(out, g["seed_" + pol])
+    assert np.array_equal(ops, g["seedops_" + pol])
+
+
+def _mm_eq(ref, refn, out, cnt):
+    assert np.array_equal(cnt, refn)
+    for i in range(len(refn)):
+        for k in range(refn[i]):
+            x, y = ref[i, k], out[i, k]
+            assert tuple(x[:5]) == tuple(y[:5]), (i, k)
+            assert (x[5] & 0xff) == ord("ACGTN"[y[5]]) and (x[5] >> 8) == ord("ACGTN"[y[6]]), (i, k)
+
+
+@pytest.mark.parametrize("name", ["lambda", "synth"])
+@pytest.mark.parametrize("mode", ["ee", "loc"])
+def test_one_mm(orc, name, mode):
+    g = load_golden("fm_" + name)
+    fe, be = _ebwts(orc, name)
+    out, cnt, ops = orc.one_mm(fe, be, g["reads"], g["quals"], g["lens"], g["mmminsc_" + mode], mode == "loc")
+    _mm_eq(g["mm_" + mode], g["mmn_" + mode], out, cnt)
+    assert np.array_equal(ops, g["mmops_" + mode])
+
+
+@pytest.mark.parametrize("name", ["lambda", "synth"])
+def test_get_offset_and_bilf(orc, name):
+    g = load_golden("fm_" + name)
+    idx = get_index(name)
+    fe, be = _ebwts(orc, name)
+    got = [orc.get_offset(fe, int(r)) for r in g["off_rows"]]
+    assert np.array_equal(np.array(got, np.uint32), g["off_vals"])
+    for row in g["bilf"]:
+        which, a, b, tp0 = (int(x) for x in row[:4])
+        arrs = orc.bilf(be if which else fe, a, b, tp0)
+        assert np.array_equal(np.concatenate(arrs), row[4:].astype(np.uint32)), row[:4]
+    assert idx.fw.length > 0
+
+
+def sw_problems(g):
+    """Yield (read codes as aligned, quals as aligned, rfmask, minsc, fw, expected out, expected cands)."""
+    for p in range(len(g["rd_index"])):
+        ri = g["rd_index"][p]
+        L = int(g["lens"][ri])
+        rd, q = g["reads"][ri, :L], g["quals"][ri, :L]
+        fw = bool(g["fw"][p])
+        if not fw:
+            rd = np.where(rd > 3, 4, 3 - rd)[::-1]
+            q = q[::-1]
+        rf = g["rf"][g["rf_off"][p]:g["rf_off"][p + 1]]
+        c = g["cands"][g["cand_off"][p]:g["cand_off"][p + 1]]
+        yield p, rd, q, rf, int(g["minsc"][p]), fw, g["out"][p], c
+
+
+@pytest.mark.parametrize("fx", ["sw_log_ee", "sw_log_loc", "sw_rand_ee", "sw_rand_loc"])
+def test_sw(orc, fx):
+    g = load_golden(fx)
+    local = bool(g["local"])
+    n = 0
+    for p, rd, q, rf, minsc, fw, out, cands in sw_problems(g):
+        o, c, _ = orc.sw(rd, q, rf, minsc, local)
+        assert np.array_equal(o[:7], out), (fx, p, o[:7], out)
+        assert np.array_equal(c, cands), (fx, p)
+        n += 1
+    assert n > 300
