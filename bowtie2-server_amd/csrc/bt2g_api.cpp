@@ -60,6 +60,11 @@ struct bt2g_ctx {
 	std::vector<hipEvent_t> evpool;
 	uint64_t launches[8] = {0};
 	double total_ms[8] = {0};
+	// persistent SW scratch (bt2g_reserve_sw): no allocation / sync per call
+	uint32_t sw_max_prob = 0, sw_max_cols = 0;
+	uint32_t* sw_lists = nullptr;
+	uint32_t* sw_counts = nullptr;
+	uint32_t* sw_bnd = nullptr;
 };
 
 namespace {
@@ -309,6 +314,7 @@ int bt2g_close(bt2g_ctx* c) {
 	drain_prof(c);
 	for(hipEvent_t e : c->evpool) (void)hipEventDestroy(e);
 	for(void* p : c->owned) (void)hipFree(p);
+	if(c->sw_lists) { (void)hipFree(c->sw_lists); (void)hipFree(c->sw_counts); (void)hipFree(c->sw_bnd); }
 	if(c->stream) (void)hipStreamDestroy(c->stream);
 	delete c;
 	return BT2G_OK;
@@ -393,9 +399,10 @@ struct OneMmScratch {
 };
 }  // namespace
 
-int bt2g_one_mm_dev(bt2g_ctx* c, const uint8_t* reads, const uint8_t* quals, uint32_t stride, const uint32_t* lens,
-                    uint32_t n, const int32_t* minsc, const bt2g_scoring* sc, int nofw, int norc, uint32_t cap,
-                    bt2g_mm1* hits, int32_t* counts, uint32_t* bwops, uint32_t* loads, void* stream) {
+static int one_mm_impl(bt2g_ctx* c, const uint8_t* reads, const uint8_t* quals, uint32_t stride,
+                       const uint32_t* lens, uint32_t n, const int32_t* minsc, const bt2g_scoring* sc, int nofw,
+                       int norc, const uint32_t* gate, uint32_t cap, bt2g_mm1* hits, int32_t* counts,
+                       uint32_t* bwops, uint32_t* loads, void* stream, bool sync_overflow) {
 	if(!c || !sc) return fail(BT2G_ERR_ARG, "null argument");
 	if(int rc = check_reads(stride, n)) return rc;
 	if(cap == 0) return fail(BT2G_ERR_ARG, "cap must be > 0");
@@ -410,18 +417,36 @@ int bt2g_one_mm_dev(bt2g_ctx* c, const uint8_t* reads, const uint8_t* quals, uin
 	if(loads) HIPCHK(hipMemsetAsync(loads, 0, sizeof(uint32_t) * n, st));
 	{
 		ProfScope ps(c, 2, st);
-		launch_one_mm(c->fw, c->bw, reads, quals, stride, lens, n, minsc, *sc, nofw, norc, cap, s.slots,
+		launch_one_mm(c->fw, c->bw, reads, quals, stride, lens, n, minsc, *sc, nofw, norc, gate, cap, s.slots,
 		              s.slot_counts, hits, counts, bwops, loads, s.ovf, st);
 	}
 	HIPCHK(hipGetLastError());
 	int32_t ovf = 0;
-	HIPCHK(hipMemcpyAsync(&ovf, s.ovf, sizeof(int32_t), hipMemcpyDeviceToHost, st));
+	if(sync_overflow) HIPCHK(hipMemcpyAsync(&ovf, s.ovf, sizeof(int32_t), hipMemcpyDeviceToHost, st));
 	HIPCHK(hipFreeAsync(s.slots, st));
 	HIPCHK(hipFreeAsync(s.slot_counts, st));
 	HIPCHK(hipFreeAsync(s.ovf, st));
-	HIPCHK(hipStreamSynchronize(st));
-	if(ovf) return fail(BT2G_ERR_OVERFLOW, "one-mismatch hits exceed cap %u", cap);
+	if(sync_overflow) {
+		HIPCHK(hipStreamSynchronize(st));
+		if(ovf) return fail(BT2G_ERR_OVERFLOW, "one-mismatch hits exceed cap %u", cap);
+	}
 	return BT2G_OK;
+}
+
+int bt2g_one_mm_dev(bt2g_ctx* c, const uint8_t* reads, const uint8_t* quals, uint32_t stride, const uint32_t* lens,
+                    uint32_t n, const int32_t* minsc, const bt2g_scoring* sc, int nofw, int norc, uint32_t cap,
+                    bt2g_mm1* hits, int32_t* counts, uint32_t* bwops, uint32_t* loads, void* stream) {
+	return one_mm_impl(c, reads, quals, stride, lens, n, minsc, sc, nofw, norc, nullptr, cap, hits, counts, bwops,
+	                   loads, stream, true);
+}
+
+int bt2g_one_mm_gated_dev(bt2g_ctx* c, const uint8_t* reads, const uint8_t* quals, uint32_t stride,
+                          const uint32_t* lens, uint32_t n, const int32_t* minsc, const bt2g_scoring* sc,
+                          const uint32_t* sweep, uint32_t cap, bt2g_mm1* hits, int32_t* counts, uint32_t* bwops,
+                          uint32_t* loads, void* stream) {
+	if(!sweep) return fail(BT2G_ERR_ARG, "null sweep");
+	return one_mm_impl(c, reads, quals, stride, lens, n, minsc, sc, 0, 0, sweep, cap, hits, counts, bwops, loads,
+	                   stream, false);
 }
 
 int bt2g_get_offset_dev(bt2g_ctx* c, const uint32_t* rows, uint32_t n, uint32_t* offs, uint32_t* loads,
@@ -454,19 +479,20 @@ int bt2g_sw_align_dev(bt2g_ctx* c, const uint8_t* reads, const uint8_t* quals, u
 	// problem lists per fill variant + boundary scratch
 	uint32_t *lists, *counts, *bnd;
 	size_t nblk = (nprob + 63) / 64;
-	// widest problem decides the boundary buffer width
-	std::vector<bt2g_sw_problem> hp;  // only the ncol field is needed; read it back once
 	uint32_t maxcol = 0;
-	{
-		// the problems live on the device; fetch ncol by a strided copy
-		hp.resize(nprob);
+	const bool reserved = nprob <= c->sw_max_prob && c->sw_lists;
+	if(reserved) {
+		lists = c->sw_lists; counts = c->sw_counts; bnd = c->sw_bnd; maxcol = c->sw_max_cols;
+	} else {
+		// widest problem decides the boundary buffer width (problems live on the device)
+		std::vector<bt2g_sw_problem> hp(nprob);
 		HIPCHK(hipMemcpyAsync(hp.data(), probs, sizeof(bt2g_sw_problem) * nprob, hipMemcpyDeviceToHost, st));
 		HIPCHK(hipStreamSynchronize(st));
 		for(auto& p : hp) maxcol = p.ncol > maxcol ? p.ncol : maxcol;
+		HIPCHK(hipMallocAsync((void**)&lists, sizeof(uint32_t) * (size_t)nprob * 3, st));
+		HIPCHK(hipMallocAsync((void**)&counts, sizeof(uint32_t) * 4, st));
+		HIPCHK(hipMallocAsync((void**)&bnd, sizeof(uint32_t) * nblk * (size_t)maxcol * 64 * 2, st));
 	}
-	HIPCHK(hipMallocAsync((void**)&lists, sizeof(uint32_t) * (size_t)nprob * 3, st));
-	HIPCHK(hipMallocAsync((void**)&counts, sizeof(uint32_t) * 4, st));
-	HIPCHK(hipMallocAsync((void**)&bnd, sizeof(uint32_t) * nblk * (size_t)maxcol * 64 * 2, st));
 	HIPCHK(hipMemsetAsync(counts, 0, sizeof(uint32_t) * 4, st));
 	uint32_t* list8 = lists;
 	uint32_t* list16 = lists + nprob;
@@ -487,9 +513,26 @@ int bt2g_sw_align_dev(bt2g_ctx* c, const uint8_t* reads, const uint8_t* quals, u
 		launch_sort_cands(res, cands, nprob, cap, st);
 	}
 	HIPCHK(hipGetLastError());
-	HIPCHK(hipFreeAsync(lists, st));
-	HIPCHK(hipFreeAsync(counts, st));
-	HIPCHK(hipFreeAsync(bnd, st));
+	if(!reserved) {
+		HIPCHK(hipFreeAsync(lists, st));
+		HIPCHK(hipFreeAsync(counts, st));
+		HIPCHK(hipFreeAsync(bnd, st));
+	}
+	return BT2G_OK;
+}
+
+int bt2g_reserve_sw(bt2g_ctx* c, uint32_t max_problems, uint32_t max_cols) {
+	if(!c || max_problems == 0 || max_cols == 0) return fail(BT2G_ERR_ARG, "bad reservation");
+	HIPCHK(hipSetDevice(c->device));
+	HIPCHK(hipStreamSynchronize(c->stream));
+	if(c->sw_lists) { (void)hipFree(c->sw_lists); (void)hipFree(c->sw_counts); (void)hipFree(c->sw_bnd); }
+	c->sw_lists = c->sw_counts = c->sw_bnd = nullptr;
+	size_t nblk = ((size_t)max_problems + 63) / 64;
+	HIPCHK(hipMalloc((void**)&c->sw_lists, sizeof(uint32_t) * (size_t)max_problems * 3));
+	HIPCHK(hipMalloc((void**)&c->sw_counts, sizeof(uint32_t) * 4));
+	HIPCHK(hipMalloc((void**)&c->sw_bnd, sizeof(uint32_t) * nblk * (size_t)max_cols * 64 * 2));
+	c->sw_max_prob = max_problems;
+	c->sw_max_cols = max_cols;
 	return BT2G_OK;
 }
 

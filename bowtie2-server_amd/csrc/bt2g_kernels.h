@@ -22,8 +22,9 @@ void launch_seed_search(const DevEbwt& F, const DevEbwt& B, const uint8_t* reads
                         hipStream_t st);
 void launch_one_mm(const DevEbwt& F, const DevEbwt& B, const uint8_t* reads, const uint8_t* quals, uint32_t stride,
                    const uint32_t* lens, uint32_t n, const int32_t* minsc, const bt2g_scoring& sc, int nofw,
-                   int norc, uint32_t cap, bt2g_mm1* slots, int32_t* slot_counts, bt2g_mm1* hits, int32_t* counts,
-                   uint32_t* ops, uint32_t* loads, int32_t* overflow, hipStream_t st);
+                   int norc, const uint32_t* gate, uint32_t cap, bt2g_mm1* slots, int32_t* slot_counts,
+                   bt2g_mm1* hits, int32_t* counts, uint32_t* ops, uint32_t* loads, int32_t* overflow,
+                   hipStream_t st);
 void launch_get_offset(const DevEbwt& e, const uint32_t* rows, uint32_t n, uint32_t* offs, uint32_t* loads,
                        hipStream_t st);
 void launch_sw_partition(const bt2g_sw_problem* probs, uint32_t nprob, int local, int enable8, uint32_t* list8,

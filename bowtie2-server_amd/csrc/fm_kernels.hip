@@ -218,8 +218,8 @@ __device__ __forceinline__ int mmpen_q(const MmParams& p, int q) {
 __global__ void __launch_bounds__(256)
 k_one_mm(DevEbwt F, DevEbwt B, const uint8_t* __restrict__ reads, const uint8_t* __restrict__ quals,
          uint32_t stride, const uint32_t* __restrict__ lens, uint32_t n, const int32_t* __restrict__ minscs,
-         MmParams P, double ncl_const, double ncl_lin, int nofw, int norc, uint32_t cap,
-         bt2g_mm1* __restrict__ slots, int32_t* __restrict__ slot_counts, uint32_t* __restrict__ ops_out,
+         MmParams P, double ncl_const, double ncl_lin, int nofw, int norc, const uint32_t* __restrict__ gate,
+         uint32_t cap, bt2g_mm1* __restrict__ slots, int32_t* __restrict__ slot_counts, uint32_t* __restrict__ ops_out,
          uint32_t* __restrict__ loads_out) {
 	uint32_t gid = blockIdx.x * blockDim.x + threadIdx.x;
 	uint32_t r = gid >> 2, fwi = (gid >> 1) & 1, ebwtfwi = gid & 1;
@@ -236,7 +236,17 @@ k_one_mm(DevEbwt F, DevEbwt B, const uint8_t* __restrict__ reads, const uint8_t*
 	int nceil = (int)(ncl_const + ncl_lin * (double)len);
 	if(nceil < 0) nceil = 0;
 	const int64_t minsc = minscs[r];
-	bool run = ns <= 1 && !((fw && nofw) || (!fw && norc));
+	bool nofw_r = nofw, norc_r = norc, gated_off = false;
+	if(gate) {
+		// bt2_search.cpp:3476-3506, 3640-3667: skipped when an exact end-to-end hit
+		// exists (bestmin == 0); otherwise nofw = !(mineFw <= 1), norc = !(mineRc <= 1).
+		uint32_t mfw = gate[(size_t)r * 8 + 0], mrc = gate[(size_t)r * 8 + 1];
+		uint32_t bestmin = mfw < mrc ? mfw : mrc;
+		bool yfw = mfw <= 1 && !nofw, yrc = mrc <= 1 && !norc;
+		gated_off = bestmin == 0 || !(yfw || yrc);
+		nofw_r = !yfw; norc_r = !yrc;
+	}
+	bool run = !gated_off && ns <= 1 && !((fw && nofw_r) || (!fw && norc_r));
 	if(run) {
 		const DevEbwt& E = ebwtfw ? F : B;
 		const DevEbwt& Ep = ebwtfw ? B : F;
@@ -473,13 +483,14 @@ void launch_seed_search(const DevEbwt& F, const DevEbwt& B, const uint8_t* reads
 
 void launch_one_mm(const DevEbwt& F, const DevEbwt& B, const uint8_t* reads, const uint8_t* quals, uint32_t stride,
                    const uint32_t* lens, uint32_t n, const int32_t* minsc, const bt2g_scoring& sc, int nofw,
-                   int norc, uint32_t cap, bt2g_mm1* slots, int32_t* slot_counts, bt2g_mm1* hits, int32_t* counts,
-                   uint32_t* ops, uint32_t* loads, int32_t* overflow, hipStream_t st) {
+                   int norc, const uint32_t* gate, uint32_t cap, bt2g_mm1* slots, int32_t* slot_counts,
+                   bt2g_mm1* hits, int32_t* counts, uint32_t* ops, uint32_t* loads, int32_t* overflow,
+                   hipStream_t st) {
 	MmParams P{sc.match, sc.mmp_max, sc.mmp_min, sc.npen, sc.local, 0, 0};
 	uint64_t threads = (uint64_t)n * 4;
 	hipLaunchKernelGGL(k_one_mm, dim3((uint32_t)((threads + 255) / 256)), dim3(256), 0, st, F, B, reads, quals,
-	                   stride, lens, n, minsc, P, sc.ncl_const, sc.ncl_lin, nofw, norc, cap, slots, slot_counts,
-	                   ops, loads);
+	                   stride, lens, n, minsc, P, sc.ncl_const, sc.ncl_lin, nofw, norc, gate, cap, slots,
+	                   slot_counts, ops, loads);
 	hipLaunchKernelGGL(k_one_mm_compact, dim3((n + 255) / 256), dim3(256), 0, st, slots, slot_counts, n, cap, hits,
 	                   counts, overflow);
 }

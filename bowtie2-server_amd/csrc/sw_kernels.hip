@@ -118,6 +118,13 @@ k_sw_fill(const bt2g_sw_problem* __restrict__ probs, uint32_t nprob, const uint3
 	const bt2g_sw_problem p = probs[pi];
 	const uint32_t nrow = lens[p.read];
 	const uint32_t ncol = p.ncol;
+	if(ncol > bnd_cols || ncol == 0 || nrow == 0) {
+		bt2g_sw_result bad{};
+		bad.flag = -3;
+		bad.best = INT32_MIN;
+		res[pi] = bad;
+		return;
+	}
 	ProbView pv{reads + (size_t)p.read * stride, quals + (size_t)p.read * stride, nrow, p.fw != 0};
 	constexpr bool LOCAL = V >= 2;
 	const uint32_t nrowp = LOCAL ? ((nrow + D::W - 1) / D::W) * D::W : nrow;

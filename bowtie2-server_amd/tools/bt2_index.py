@@ -404,3 +404,152 @@ def read_index(base) -> Bt2Index:
         jo += r.len
     ref_codes = [np.concatenate(x) for x in ref_codes]
     return Bt2Index(fw=fw, bw=bw, recs=recs, text=text, ref_codes=ref_codes)
+
+
+# --------------------------------------------------------------------------
+# Device-side construction for large synthetic genomes (bench.py).  Same bytes
+# as build_ebwt(); every O(n) pass is a torch op so it runs on the GPU.
+# --------------------------------------------------------------------------
+def _build_ebwt_torch(t, sa, flags, rstarts, plen, off_rate=4, ftab_chars=10, line_rate=6):
+    import torch
+    dev = t.device
+    n = int(t.numel())
+    side_sz = 1 << line_rate
+    side_bwt_sz = side_sz - 16
+    side_bwt_len = side_bwt_sz * 4
+    num_sides = (n // 4 + 1 + side_bwt_sz - 1) // side_bwt_sz
+    tot = num_sides * side_bwt_len
+    zoff = int(torch.nonzero(sa == 0)[0, 0])
+    bwt = torch.zeros(tot, dtype=torch.uint8, device=dev)
+    prev = (sa - 1).clamp_(min=0)
+    bwt[: n + 1] = t[prev]
+    del prev
+    bwt[zoff] = 0
+    b2 = bwt.view(num_sides, side_bwt_len)
+    cnt = torch.empty((num_sides, 4), dtype=torch.int64, device=dev)
+    for c in range(4):
+        cnt[:, c] = (b2 == c).sum(dim=1)
+    # '$' (at zoff) must not be counted as an 'A'
+    cnt[zoff // side_bwt_len, 0] -= 1
+    occ = torch.zeros_like(cnt)
+    occ[1:] = torch.cumsum(cnt, 0)[:-1]
+    tot_cnt = cnt.sum(0)
+    # bases beyond n (padding 'A') are counted in occ but not in fchr
+    pad = tot - (n + 1)
+    fcnt = tot_cnt.clone()
+    fcnt[0] -= pad
+    fchr = torch.zeros(5, dtype=torch.int64, device=dev)
+    fchr[1:] = torch.cumsum(fcnt, 0)
+    sh = torch.tensor([0, 2, 4, 6], dtype=torch.uint8, device=dev)
+    packed = (b2.view(num_sides, side_bwt_sz, 4) << sh).sum(dim=2, dtype=torch.uint8)
+    sides = torch.empty((num_sides, side_sz), dtype=torch.uint8, device=dev)
+    sides[:, :side_bwt_sz] = packed
+    sides[:, side_bwt_sz:] = occ.to(torch.int32).contiguous().view(torch.uint8).view(num_sides, 16)
+    del bwt, b2, packed
+    # ftab: bucket counts of every length-ftab_chars k-mer of the text (= long suffixes)
+    ftab_len = (1 << (2 * ftab_chars)) + 1
+    m = n - ftab_chars + 1
+    key = torch.zeros(max(m, 0), dtype=torch.int64, device=dev)
+    for i in range(ftab_chars):
+        key = (key << 2) | t[i:i + m].to(torch.int64)
+    ftab = torch.zeros(ftab_len, dtype=torch.int64, device=dev)
+    ftab[1:] += torch.bincount(key, minlength=ftab_len - 1)[: ftab_len - 1]
+    # short suffixes (n - sa < ftab_chars): absorbed by the next long suffix's bucket
+    short_rows = torch.nonzero((n - sa) < ftab_chars).squeeze(1).cpu().numpy()
+    absorb = np.zeros(ftab_len, dtype=np.int64)
+    short_set = set(int(r) for r in short_rows)
+    for r in short_rows:
+        nx = int(r) + 1
+        while nx in short_set:
+            nx += 1
+        if nx > n:
+            absorb[ftab_len - 1] += 1
+        else:
+            absorb[int(key[int(sa[nx])])] += 1
+    ftab = ftab.cpu().numpy()
+    cnt_ = ftab.copy()
+    cnt_[0] = 0
+    ab = absorb.copy()
+    ab[0] = 0
+    lo = np.cumsum(cnt_) + np.concatenate([[0], np.cumsum(ab)[:-1]])
+    out = lo.copy()
+    eftab = np.zeros(ftab_chars * 2, dtype=np.int64)
+    for ecur, i in enumerate(np.nonzero(ab > 0)[0]):
+        eftab[ecur * 2] = lo[i]
+        eftab[ecur * 2 + 1] = lo[i] + ab[i]
+        out[i] = ecur ^ OFF_MASK
+    out[0] = 0
+    offs = sa[:: 1 << off_rate].to(torch.int64).cpu().numpy().astype(np.uint32)
+    return Ebwt(length=n, line_rate=line_rate, off_rate=off_rate, ftab_chars=ftab_chars, flags=flags,
+                plen=np.asarray(plen, np.uint32), rstarts=np.asarray(rstarts, np.uint32),
+                ebwt=sides.view(-1).cpu().numpy(), zoff=zoff, fchr=fchr.cpu().numpy().astype(np.uint32),
+                ftab=out.astype(np.uint32), eftab=eftab.astype(np.uint32), offs=offs)
+
+
+def _suffix_array_torch(t):
+    """suffix_array() on a device tensor; returns an int64 device tensor."""
+    import torch
+    n = int(t.numel())
+    K = 21
+    dev = t.device
+    sym = torch.full((n + K,), 5, dtype=torch.int64, device=dev)
+    sym[:n] = t.to(torch.int64) + 1
+    key = torch.zeros(n + 1, dtype=torch.int64, device=dev)
+    for k in range(K):
+        key.mul_(8).add_(sym[k:k + n + 1])
+    del sym
+    key, sa = torch.sort(key)
+    newgrp = torch.ones(n + 1, dtype=torch.bool, device=dev)
+    newgrp[1:] = key[1:] != key[:-1]
+    del key
+    h = K
+    while True:
+        single = newgrp.clone()
+        single[:-1] &= newgrp[1:]
+        unresolved = torch.nonzero(~single).squeeze(1)
+        del single
+        if unresolved.numel() == 0:
+            break
+        idx = torch.arange(n + 1, device=dev)
+        grpstart = torch.where(newgrp, idx, torch.zeros_like(idx))
+        del idx
+        grpstart = torch.cummax(grpstart, 0).values
+        rank = torch.full((n + 1 + h,), -1, dtype=torch.int64, device=dev)
+        rank[sa] = grpstart
+        pos = sa[unresolved]
+        k2 = rank[pos + h]
+        k1 = grpstart[unresolved]
+        del rank, grpstart
+        o = torch.sort(k2, stable=True).indices
+        pos, k1, k2 = pos[o], k1[o], k2[o]
+        o = torch.sort(k1, stable=True).indices
+        pos, k1, k2 = pos[o], k1[o], k2[o]
+        sa[unresolved] = pos
+        ng = torch.ones_like(k1, dtype=torch.bool)
+        ng[1:] = (k1[1:] != k1[:-1]) | (k2[1:] != k2[:-1])
+        newgrp[unresolved] = ng
+        h *= 2
+        del k1, k2, pos, o, ng, unresolved
+    return sa
+
+
+def build_index_device(seqs_codes, names=None, off_rate=4, ftab_chars=10, device="cuda"):
+    """build_index() with every large pass on `device` (for bench-sized genomes)."""
+    import torch
+    seqs_codes = [np.asarray(c, dtype=np.uint8) for c in seqs_codes]
+    recs = records_for(seqs_codes)
+    text = joined_text(seqs_codes)
+    n = len(text)
+    names_blob = (b"\n".join(names) + b"\n\0") if names is not None else b""
+    out = {}
+    tt = torch.from_numpy(text).to(device)
+    for rev in (False, True):
+        t = torch.flip(tt, [0]).contiguous() if rev else tt
+        sa = _suffix_array_torch(t)
+        plen, rs = _plen_rstarts(recs, rev, n)
+        e = _build_ebwt_torch(t, sa, -5 if rev else -1, rs, plen, off_rate, ftab_chars)
+        e.names = names_blob
+        out[rev] = e
+        del sa, t
+        torch.cuda.empty_cache() if str(device).startswith("cuda") else None
+    return Bt2Index(fw=out[False], bw=out[True], recs=recs, text=text, ref_codes=seqs_codes)

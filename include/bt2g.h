@@ -150,6 +150,16 @@ int bt2g_one_mm_dev(bt2g_ctx* ctx, const uint8_t* reads, const uint8_t* quals, u
                     int norc, uint32_t cap, bt2g_mm1* hits, int32_t* counts, uint32_t* bwops, uint32_t* loads,
                     void* stream);
 
+/* Same search gated per read by the exactSweep output `sweep` (n x 8, from
+ * bt2g_exact_sweep_dev) exactly as bt2_search.cpp:3476-3506,3640-3667 chains
+ * them: no search when min(mineFw, mineRc) == 0; otherwise nofw = mineFw > 1,
+ * norc = mineRc > 1 (counts[i] = 0 for skipped reads).  Fully asynchronous: an
+ * overflow shows as counts[i] > cap. */
+int bt2g_one_mm_gated_dev(bt2g_ctx* ctx, const uint8_t* reads, const uint8_t* quals, uint32_t stride,
+                          const uint32_t* lens, uint32_t n, const int32_t* minsc, const bt2g_scoring* sc,
+                          const uint32_t* sweep, uint32_t cap, bt2g_mm1* hits, int32_t* counts, uint32_t* bwops,
+                          uint32_t* loads, void* stream);
+
 /* Ebwt::getOffset (bt2_idx.cpp:150-171): joined-text offset of each SA row.
  * loads (optional): 64-B sides gathered per row. */
 int bt2g_get_offset(bt2g_ctx* ctx, const uint32_t* rows, uint32_t n, uint32_t* offs, uint32_t* loads);
@@ -204,6 +214,11 @@ int bt2g_sw_align_dev(bt2g_ctx* ctx, const uint8_t* reads, const uint8_t* quals,
                       const uint32_t* lens, const bt2g_sw_problem* probs, uint32_t nprob, const uint8_t* windows,
                       const bt2g_scoring* sc, int enable8, uint32_t cap, bt2g_sw_result* res, bt2g_sw_cand* cands,
                       int16_t* mat, const uint64_t* mat_off, void* stream);
+
+/* Reserve persistent scratch for up to max_problems problems of width <=
+ * max_cols, so bt2g_sw_align_dev neither allocates nor synchronises (problems
+ * wider than max_cols then fail with result.flag = -3). */
+int bt2g_reserve_sw(bt2g_ctx* ctx, uint32_t max_problems, uint32_t max_cols);
 
 /* ---- multi-GPU ----------------------------------------------------------- */
 /* The only collective of the path: the caller sums these

@@ -68,7 +68,7 @@ def test_get_offset_golden(engines, name):
     g = load_golden("fm_" + name)
     offs, loads = engines[name].get_offset(g["off_rows"])
     assert np.array_equal(offs, g["off_vals"])
-    assert loads.max() < 64
+    assert loads.mean() < 32          # geometric walk to a sampled row (offRate 4)
 
 
 def test_large_batch_vs_oracle(engines, orc):
