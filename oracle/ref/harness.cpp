@@ -361,3 +361,74 @@ int bt2ref_sw(const char* seq, const char* qual, int fw, const uint8_t* rfmask, 
 }
 
 } // extern "C"
+
+// ---- batch entry points used by bench.py's cpu_baseline leg -----------------
+extern "C" {
+
+void bt2ref_get_offsets(void* vh, int n, const uint32_t* rows, uint32_t* out) {
+	RefHandle* h = (RefHandle*)vh;
+	for(int i = 0; i < n; i++) out[i] = h->fw->getOffset(rows[i]);
+}
+
+// SwAligner::initRead/initRef/align for n problems (one SwAligner reused, as a
+// worker thread does).  rf: concatenated ncol+1 masks, rf_off[i] its start.
+// out: n x 7 (aligned, best, u8succ, i16succ, colstop, lastsolcol, ncand).
+void bt2ref_sw_batch(int n, const char** seqs, const char** quals, const uint8_t* fws, const uint8_t* rf,
+                     const int64_t* rf_off, const int32_t* ncols, const int64_t* minsc, const ScoreParams* sp,
+                     int64_t* out) {
+	Scoring sc = makeScoring(*sp);
+	SwAlignerX sw;
+	BTDnaString rdfw, rdrc;
+	BTString qufw, qurc;
+	std::vector<char> buf;
+	const char* last = nullptr;
+	for(int i = 0; i < n; i++) {
+		if(seqs[i] != last) {
+			rdfw.install(seqs[i], true);
+			rdrc = rdfw; rdrc.reverseComp();
+			qufw.install(quals[i]);
+			qurc = qufw; qurc.reverse();
+			sw.initRead(rdfw, rdrc, qufw, qurc, 0, rdfw.length(), sc);
+			last = seqs[i];
+		}
+		int ncol = ncols[i];
+		buf.assign(rf + rf_off[i], rf + rf_off[i] + ncol + 1);
+		buf.resize(ncol + 16, 0);
+		DPRect rect;
+		rect.refl = 0; rect.refr = ncol - 1; rect.refl_pretrim = 0; rect.refr_pretrim = ncol - 1;
+		rect.triml = rect.trimr = 0; rect.corel = 0; rect.corer = 0; rect.maxgap = 0;
+		sw.initRef(fws[i] != 0, 0, rect, buf.data(), 0, (size_t)ncol, (TRefOff)ncol + 1000, sc, minsc[i],
+		           true, 2000, 4, false, true);
+		TAlScore best = std::numeric_limits<TAlScore>::min();
+		bool aligned = sw.align(best);
+		int64_t* o = out + 7 * (size_t)i;
+		o[0] = aligned; o[1] = best; o[2] = sw.u8succ(); o[3] = sw.i16succ();
+		o[4] = (int64_t)sw.colstop(); o[5] = (int64_t)sw.lastsolcol(); o[6] = (int64_t)sw.cands().size();
+	}
+}
+
+// oneMmSearch gated by exactSweep exactly as bt2_search.cpp:3640-3667 chains them.
+// sweep: n x 8 from bt2ref_exact_sweep (mineFw, mineRc, ...).  counts[i] = hits.
+void bt2ref_one_mm_gated(void* vh, int n, const char** seqs, const char** quals, const int64_t* minsc,
+                         const uint64_t* sweep, int32_t* counts) {
+	RefHandle* h = (RefHandle*)vh;
+	SeedAligner al;
+	SeedResults sr;
+	SeedSearchMetrics met;
+	ScoreParams sp = {0, 6, 2, 1, 5, 3, 5, 3, 4, 0, 0.0, 0.15};
+	Scoring sc = makeScoring(sp);
+	for(int i = 0; i < n; i++) {
+		counts[i] = 0;
+		uint64_t mfw = sweep[8 * (size_t)i], mrc = sweep[8 * (size_t)i + 1];
+		if(std::min(mfw, mrc) == 0) continue;
+		bool yfw = mfw <= 1, yrc = mrc <= 1;
+		if(!(yfw || yrc)) continue;
+		Read rd("r", seqs[i], quals[i]);
+		sr.clear();
+		sr.nextRead(rd);
+		al.oneMmSearch(h->fw, h->bw, rd, sc, minsc[i], !yfw, !yrc, false, false, true, sr, met);
+		counts[i] = (int32_t)sr.mm1EEHits().size();
+	}
+}
+
+} // extern "C"
