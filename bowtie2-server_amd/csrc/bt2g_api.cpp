@@ -133,7 +133,9 @@ void drain_prof(bt2g_ctx* c) {
 	c->pending.clear();
 }
 
-hipStream_t pick(bt2g_ctx* c, void* s) { return s ? (hipStream_t)s : c->stream; }
+// NULL is the null (legacy default) stream, as everywhere in HIP; the host
+// wrappers below pass the context stream explicitly.
+hipStream_t pick(bt2g_ctx*, void* s) { return (hipStream_t)s; }
 
 // --- .bt2 reading (bt2_io.cpp:39-616; reference.cpp:100-235) ---------------
 bool read_file(const std::string& path, std::vector<uint8_t>& out) {
@@ -524,7 +526,7 @@ int bt2g_sw_align_dev(bt2g_ctx* c, const uint8_t* reads, const uint8_t* quals, u
 int bt2g_reserve_sw(bt2g_ctx* c, uint32_t max_problems, uint32_t max_cols) {
 	if(!c || max_problems == 0 || max_cols == 0) return fail(BT2G_ERR_ARG, "bad reservation");
 	HIPCHK(hipSetDevice(c->device));
-	HIPCHK(hipStreamSynchronize(c->stream));
+	HIPCHK(hipDeviceSynchronize());   // the old scratch may be in use on any stream
 	if(c->sw_lists) { (void)hipFree(c->sw_lists); (void)hipFree(c->sw_counts); (void)hipFree(c->sw_bnd); }
 	c->sw_lists = c->sw_counts = c->sw_bnd = nullptr;
 	size_t nblk = ((size_t)max_problems + 63) / 64;
@@ -578,7 +580,7 @@ int bt2g_exact_sweep(bt2g_ctx* c, const uint8_t* reads, uint32_t stride, const u
 	if((rc = t.up(&dr, reads, (size_t)n * stride)) || (rc = t.up(&dl, lens, n)) ||
 	   (rc = t.up(&dout, (const uint32_t*)nullptr, (size_t)n * 8)))
 		return rc;
-	if((rc = bt2g_exact_sweep_dev(c, dr, stride, dl, n, mine_max, nofw, norc, dout, nullptr))) return rc;
+	if((rc = bt2g_exact_sweep_dev(c, dr, stride, dl, n, mine_max, nofw, norc, dout, c->stream))) return rc;
 	HIPCHK(hipStreamSynchronize(c->stream));
 	return down(out, dout, (size_t)n * 8);
 }
@@ -600,7 +602,7 @@ int bt2g_seed_search(bt2g_ctx* c, const uint8_t* reads, uint32_t stride, const u
 		return rc;
 	if(loads && (rc = t.up(&dld, (const uint32_t*)nullptr, n))) return rc;
 	if((rc = bt2g_seed_search_dev(c, dr, stride, dl, n, seedlen, interval, offset, maxseeds, dout, dns, dops, dld,
-	                              nullptr)))
+	                              c->stream)))
 		return rc;
 	HIPCHK(hipStreamSynchronize(c->stream));
 	if((rc = down(out, dout, no)) || (rc = down(nseeds, dns, n)) || (rc = down(bwops, dops, n))) return rc;
@@ -625,7 +627,7 @@ int bt2g_one_mm(bt2g_ctx* c, const uint8_t* reads, const uint8_t* quals, uint32_
 	   (rc = t.up(&dcnt, (const int32_t*)nullptr, n)) || (rc = t.up(&dops, (const uint32_t*)nullptr, n)))
 		return rc;
 	if(loads && (rc = t.up(&dld, (const uint32_t*)nullptr, n))) return rc;
-	int rc2 = bt2g_one_mm_dev(c, dr, dq, stride, dl, n, dms, sc, nofw, norc, cap, dh, dcnt, dops, dld, nullptr);
+	int rc2 = bt2g_one_mm_dev(c, dr, dq, stride, dl, n, dms, sc, nofw, norc, cap, dh, dcnt, dops, dld, c->stream);
 	if(rc2 && rc2 != BT2G_ERR_OVERFLOW) return rc2;
 	HIPCHK(hipStreamSynchronize(c->stream));
 	if((rc = down(hits, dh, (size_t)n * cap)) || (rc = down(counts, dcnt, n)) || (rc = down(bwops, dops, n)))
@@ -642,7 +644,7 @@ int bt2g_get_offset(bt2g_ctx* c, const uint32_t* rows, uint32_t n, uint32_t* off
 	int rc;
 	if((rc = t.up(&drow, rows, n)) || (rc = t.up(&doff, (const uint32_t*)nullptr, n))) return rc;
 	if(loads && (rc = t.up(&dld, (const uint32_t*)nullptr, n))) return rc;
-	if((rc = bt2g_get_offset_dev(c, drow, n, doff, dld, nullptr))) return rc;
+	if((rc = bt2g_get_offset_dev(c, drow, n, doff, dld, c->stream))) return rc;
 	HIPCHK(hipStreamSynchronize(c->stream));
 	if((rc = down(offs, doff, n))) return rc;
 	if(loads && (rc = down(loads, dld, n))) return rc;
@@ -681,7 +683,7 @@ int bt2g_sw_align(bt2g_ctx* c, const uint8_t* reads, const uint8_t* quals, uint3
 		}
 		if((rc = t.up(&dm, (const int16_t*)nullptr, matn)) || (rc = t.up(&dmo, mat_off, nprob))) return rc;
 	}
-	if((rc = bt2g_sw_align_dev(c, dr, dq, stride, dl, dp, nprob, dw, sc, enable8, cap, dres, dc, dm, dmo, nullptr)))
+	if((rc = bt2g_sw_align_dev(c, dr, dq, stride, dl, dp, nprob, dw, sc, enable8, cap, dres, dc, dm, dmo, c->stream)))
 		return rc;
 	HIPCHK(hipStreamSynchronize(c->stream));
 	if((rc = down(res, dres, nprob)) || (rc = down(cands, dc, (size_t)nprob * cap))) return rc;

@@ -15,7 +15,7 @@
  *
  * Two flavours of every batch call:
  *   <name>_dev(...)     all array arguments are device pointers (HBM-resident),
- *                      enqueued on `stream` (a hipStream_t, NULL = context stream),
+ *                      enqueued on `stream` (a hipStream_t; NULL = the null stream),
  *                      asynchronous.
  *   <name>(...)         same arguments as host pointers; copies in, runs, copies
  *                      out, synchronises.  For callers that keep data on the host.
