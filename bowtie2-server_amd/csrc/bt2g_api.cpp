@@ -466,6 +466,16 @@ int bt2g_get_offset_dev(bt2g_ctx* c, const uint32_t* rows, uint32_t n, uint32_t*
 }
 
 // ---------------------------------------------------------------- SW engine
+// The packed two-problems-per-lane end-to-end fill covers the default
+// end-to-end scoring (no match bonus, byte-sized penalties) without matrix
+// dumps; anything else runs the one-problem-per-lane fills.
+static bool sw_packed_ok(const bt2g_scoring& sc, const SwConst& C, const int16_t* mat) {
+	if(sc.local || mat || sc.match != 0 || C.npen < 0 || C.npen > 255) return false;
+	for(int q = 0; q <= 40; q++)
+		if(C.mmpen[q] < 0 || C.mmpen[q] > 255) return false;
+	return C.rdgo >= 0 && C.rdge >= 0 && C.rfgo >= 0 && C.rfge >= 0;
+}
+
 int bt2g_sw_align_dev(bt2g_ctx* c, const uint8_t* reads, const uint8_t* quals, uint32_t stride,
                       const uint32_t* lens, const bt2g_sw_problem* probs, uint32_t nprob, const uint8_t* windows,
                       const bt2g_scoring* sc, int enable8, uint32_t cap, bt2g_sw_result* res, bt2g_sw_cand* cands,
@@ -503,6 +513,12 @@ int bt2g_sw_align_dev(bt2g_ctx* c, const uint8_t* reads, const uint8_t* quals, u
 		ProfScope ps(c, 4, st);
 		launch_sw_partition(probs, nprob, sc->local, enable8, list8, counts + 0, list16, counts + 1, st);
 		int v8 = sc->local ? 2 : 0, v16 = sc->local ? 3 : 1;
+		if(sw_packed_ok(*sc, C, mat)) {
+			launch_sw_ee_packed(0, probs, nprob, list8, counts + 0, reads, quals, stride, lens, windows, c->ref_codes,
+			                    c->ref_starts, C, cap, bnd, maxcol, res, cands, st);
+			launch_sw_ee_packed(1, probs, nprob, list16, counts + 1, reads, quals, stride, lens, windows,
+			                    c->ref_codes, c->ref_starts, C, cap, bnd, maxcol, res, cands, st);
+		} else {
 		launch_sw_fill(v8, probs, nprob, list8, counts + 0, reads, quals, stride, lens, windows, c->ref_codes,
 		               c->ref_starts, C, cap, bnd, maxcol, res, cands, mat, mat_off, satl, counts + 2, st);
 		launch_sw_fill(v16, probs, nprob, list16, counts + 1, reads, quals, stride, lens, windows, c->ref_codes,
@@ -511,6 +527,7 @@ int bt2g_sw_align_dev(bt2g_ctx* c, const uint8_t* reads, const uint8_t* quals, u
 			// local u8 saturated -> i16 (aligner_sw.cpp:587-605)
 			launch_sw_fill(3, probs, nprob, satl, counts + 2, reads, quals, stride, lens, windows, c->ref_codes,
 			               c->ref_starts, C, cap, bnd, maxcol, res, cands, mat, mat_off, satl, counts + 3, st);
+		}
 		}
 		launch_sort_cands(res, cands, nprob, cap, st);
 	}

@@ -106,3 +106,48 @@ def test_sw_resident_reference(eng):
     assert np.array_equal(res1, res2)
     assert np.array_equal(c1, c2)
     assert res1["aligned"].sum() > n // 2
+
+
+def test_sw_packed_vs_per_lane(eng):
+    """The packed two-problems-per-lane end-to-end fill (default path) against
+    the one-problem-per-lane fill (taken when matrices are requested) on
+    ragged problems: read lengths 1..400, widths 1..500, u8 and i16 minsc,
+    Ns in reads and reference, windows off both reference ends."""
+    import bt2g
+    import synth
+    idx = get_index("lambda")
+    gen = idx.ref_codes[0]
+    rng = np.random.default_rng(5)
+    n = 700
+    lens = rng.integers(1, 401, n).astype(np.uint32)
+    lens[:5] = [1, 2, 4, 8, 400]
+    stride = 400
+    codes = np.full((n, stride), 4, np.uint8)
+    quals = np.full((n, stride), 73, np.uint8)
+    pos = rng.integers(-50, len(gen) + 50, n)
+    fw = rng.random(n) < 0.5
+    for i in range(n):
+        L = int(lens[i])
+        o = np.arange(pos[i], pos[i] + L)
+        c = np.where((o >= 0) & (o < len(gen)), gen[np.clip(o, 0, len(gen) - 1)], 4)
+        m = rng.random(L) < 0.03
+        c[m] = rng.integers(0, 5, m.sum())
+        if not fw[i]:
+            c = np.where(c > 3, 4, 3 - c)[::-1]
+        codes[i, :L] = c
+        quals[i, :L] = rng.integers(33, 75, L)
+    probs = np.zeros(n, bt2g.SWPROB_DTYPE)
+    probs["read"] = np.arange(n)
+    probs["fw"] = fw
+    probs["ncol"] = np.clip(lens.astype(np.int64) + rng.integers(-20, 100, n), 1, 500)
+    probs["refl"] = pos - rng.integers(0, 40, n)
+    probs["win_off"] = -1
+    probs["minsc"] = np.where(rng.random(n) < 0.3, -(0.6 + 2.5 * lens).astype(np.int64),
+                              -(0.6 + 0.6 * lens).astype(np.int64))
+    probs["minsc"][:3] = [0, -254, -255]
+    res_p, c_p, _ = eng.sw_align(codes, quals, lens, probs, cap=512)
+    res_g, c_g, _ = eng.sw_align(codes, quals, lens, probs, cap=512, want_mat=True)
+    assert np.array_equal(res_p, res_g)
+    assert np.array_equal(c_p, c_g)
+    assert 0 < res_p["aligned"].sum() < n
+    assert (res_p["i16succ"] == 1).sum() > 0 and (res_p["u8succ"] == 1).sum() > 0
