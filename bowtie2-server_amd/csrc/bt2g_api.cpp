@@ -482,7 +482,7 @@ int bt2g_sw_align_dev(bt2g_ctx* c, const uint8_t* reads, const uint8_t* quals, u
                       int16_t* mat, const uint64_t* mat_off, void* stream) {
 	if(!c || !sc) return fail(BT2G_ERR_ARG, "null argument");
 	if(int rc = check_reads(stride, nprob)) return rc;
-	if(cap == 0 || cap > 65536) return fail(BT2G_ERR_ARG, "cap out of range");
+	if(cap == 0 || cap > 8192) return fail(BT2G_ERR_ARG, "cap out of range (1..8192)");
 	if(sc->local && sc->match <= 0) return fail(BT2G_ERR_ARG, "local mode needs a match bonus");
 	if(nprob == 0) return BT2G_OK;
 	hipStream_t st = pick(c, stream);
@@ -502,10 +502,10 @@ int bt2g_sw_align_dev(bt2g_ctx* c, const uint8_t* reads, const uint8_t* quals, u
 		HIPCHK(hipStreamSynchronize(st));
 		for(auto& p : hp) maxcol = p.ncol > maxcol ? p.ncol : maxcol;
 		HIPCHK(hipMallocAsync((void**)&lists, sizeof(uint32_t) * (size_t)nprob * 3, st));
-		HIPCHK(hipMallocAsync((void**)&counts, sizeof(uint32_t) * 4, st));
+		HIPCHK(hipMallocAsync((void**)&counts, sizeof(uint32_t) * 8, st));
 		HIPCHK(hipMallocAsync((void**)&bnd, sizeof(uint32_t) * nblk * (size_t)maxcol * 64 * 2, st));
 	}
-	HIPCHK(hipMemsetAsync(counts, 0, sizeof(uint32_t) * 4, st));
+	HIPCHK(hipMemsetAsync(counts, 0, sizeof(uint32_t) * 8, st));
 	uint32_t* list8 = lists;
 	uint32_t* list16 = lists + nprob;
 	uint32_t* satl = lists + 2 * (size_t)nprob;
@@ -529,7 +529,7 @@ int bt2g_sw_align_dev(bt2g_ctx* c, const uint8_t* reads, const uint8_t* quals, u
 			               c->ref_starts, C, cap, bnd, maxcol, res, cands, mat, mat_off, satl, counts + 3, st);
 		}
 		}
-		launch_sort_cands(res, cands, nprob, cap, st);
+		launch_sort_cands(res, cands, nprob, cap, list8, counts + 4, st);   // list8 is free again
 	}
 	HIPCHK(hipGetLastError());
 	if(!reserved) {
@@ -548,7 +548,7 @@ int bt2g_reserve_sw(bt2g_ctx* c, uint32_t max_problems, uint32_t max_cols) {
 	c->sw_lists = c->sw_counts = c->sw_bnd = nullptr;
 	size_t nblk = ((size_t)max_problems + 63) / 64;
 	HIPCHK(hipMalloc((void**)&c->sw_lists, sizeof(uint32_t) * (size_t)max_problems * 3));
-	HIPCHK(hipMalloc((void**)&c->sw_counts, sizeof(uint32_t) * 4));
+	HIPCHK(hipMalloc((void**)&c->sw_counts, sizeof(uint32_t) * 8));
 	HIPCHK(hipMalloc((void**)&c->sw_bnd, sizeof(uint32_t) * nblk * (size_t)max_cols * 64 * 2));
 	c->sw_max_prob = max_problems;
 	c->sw_max_cols = max_cols;

@@ -41,4 +41,4 @@ void launch_sw_ee_packed(int variant, const bt2g_sw_problem* probs, uint32_t npr
                          const uint64_t* ref_starts, const SwConst& C, uint32_t cap, uint32_t* bnd,
                          uint32_t bnd_cols, bt2g_sw_result* res, bt2g_sw_cand* cands, hipStream_t st);
 void launch_sort_cands(const bt2g_sw_result* res, bt2g_sw_cand* cands, uint32_t nprob, uint32_t cap,
-                       hipStream_t st);
+                       uint32_t* big, uint32_t* nbig, hipStream_t st);

@@ -317,14 +317,27 @@ k_sw_fill(const bt2g_sw_problem* __restrict__ probs, uint32_t nprob, const uint3
 
 // Split problems by the fill SwAligner::align picks first (aligner_sw.cpp:516-586):
 // end-to-end u8 iff enable8 && minsc >= -254, else i16; local u8 iff enable8.
-__global__ void k_sw_partition(const bt2g_sw_problem* __restrict__ probs, uint32_t nprob, int local, int enable8,
-                               uint32_t* __restrict__ list8, uint32_t* __restrict__ n8,
-                               uint32_t* __restrict__ list16, uint32_t* __restrict__ n16) {
-	uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
-	if(i >= nprob) return;
-	bool u8 = enable8 && (local || probs[i].minsc >= -254);
-	if(u8) list8[atomicAdd(n8, 1u)] = i;
-	else list16[atomicAdd(n16, 1u)] = i;
+// One atomic per wave and list (ballot + prefix popcount), not per problem.
+__global__ void __launch_bounds__(256)
+k_sw_partition(const bt2g_sw_problem* __restrict__ probs, uint32_t nprob, int local, int enable8,
+               uint32_t* __restrict__ list8, uint32_t* __restrict__ n8, uint32_t* __restrict__ list16,
+               uint32_t* __restrict__ n16) {
+	const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+	const uint32_t lane = threadIdx.x & 63u;
+	const bool valid = i < nprob;
+	const bool u8 = valid && enable8 && (local || probs[i].minsc >= -254);
+	const bool w16 = valid && !u8;
+	const uint64_t m8 = __ballot(u8), m16 = __ballot(w16);
+	uint32_t b8 = 0, b16 = 0;
+	if(lane == 0) {
+		if(m8) b8 = atomicAdd(n8, (uint32_t)__popcll(m8));
+		if(m16) b16 = atomicAdd(n16, (uint32_t)__popcll(m16));
+	}
+	b8 = __shfl(b8, 0);
+	b16 = __shfl(b16, 0);
+	const uint64_t below = (1ull << lane) - 1ull;
+	if(u8) list8[b8 + (uint32_t)__popcll(m8 & below)] = i;
+	if(w16) list16[b16 + (uint32_t)__popcll(m16 & below)] = i;
 }
 
 void launch_sw_partition(const bt2g_sw_problem* probs, uint32_t nprob, int local, int enable8, uint32_t* list8,
@@ -335,49 +348,81 @@ void launch_sw_partition(const bt2g_sw_problem* probs, uint32_t nprob, int local
 }
 
 // Sort each problem's candidates by the DpBtCandidate total order
-// (score desc, row desc, col desc; aligner_sw_nuc.h:149-157).  One workgroup
-// per problem, bitonic sort of packed 64-bit keys in LDS.
+// (score desc, row desc, col desc; aligner_sw_nuc.h:149-157) on packed 64-bit
+// keys: key = ~((score ^ sign) << 32 | row << 16 | col), ascending.
+__device__ __forceinline__ unsigned long long cand_key(const bt2g_sw_cand& c) {
+	return ~(((unsigned long long)(uint32_t)(c.score ^ 0x80000000) << 32) |
+	         ((unsigned long long)(uint32_t)c.row << 16) | (uint32_t)c.col);
+}
+__device__ __forceinline__ bt2g_sw_cand cand_of(unsigned long long key) {
+	const unsigned long long k = ~key;
+	bt2g_sw_cand o;
+	o.score = (int32_t)((uint32_t)(k >> 32) ^ 0x80000000u);
+	o.row = (int32_t)((k >> 16) & 0xffff);
+	o.col = (int32_t)(k & 0xffff);
+	return o;
+}
+
+// One wave per problem: up to 64 candidates sorted in registers by a bitonic
+// network over lanes (shuffles); larger lists are queued for k_sort_big.
 __global__ void __launch_bounds__(256)
-k_sort_cands(const bt2g_sw_result* __restrict__ res, bt2g_sw_cand* __restrict__ cands, uint32_t cap) {
-	extern __shared__ __attribute__((aligned(16))) unsigned long long keys[];
-	const uint32_t pi = blockIdx.x;
+k_sort_small(const bt2g_sw_result* __restrict__ res, bt2g_sw_cand* __restrict__ cands, uint32_t nprob,
+             uint32_t cap, uint32_t* __restrict__ big, uint32_t* __restrict__ nbig) {
+	const uint32_t pi = blockIdx.x * 4u + (threadIdx.x >> 6);
+	const uint32_t lane = threadIdx.x & 63u;
+	if(pi >= nprob) return;
 	const int n0 = res[pi].ncand;
 	const uint32_t n = (uint32_t)(n0 < 0 ? 0 : (n0 > (int)cap ? cap : n0));
 	if(n <= 1) return;
-	uint32_t P2 = 1;
-	while(P2 < n) P2 <<= 1;
+	if(n > 64) {
+		if(lane == 0) big[atomicAdd(nbig, 1u)] = pi;
+		return;
+	}
 	bt2g_sw_cand* c = cands + (size_t)pi * cap;
-	for(uint32_t i = threadIdx.x; i < P2; i += blockDim.x) {
-		if(i < n) {
-			// descending order of (score, row, col) == ascending order of the complement
-			unsigned long long k = ((unsigned long long)(uint32_t)(c[i].score ^ 0x80000000) << 32) |
-			                       ((unsigned long long)(uint32_t)c[i].row << 16) | (uint32_t)c[i].col;
-			keys[i] = ~k;
-		} else {
-			keys[i] = ~0ull;
-		}
-	}
-	__syncthreads();
-	for(uint32_t size = 2; size <= P2; size <<= 1) {
+	unsigned long long key = lane < n ? cand_key(c[lane]) : ~0ull;
+	for(uint32_t size = 2; size <= 64; size <<= 1) {
 		for(uint32_t stride = size >> 1; stride > 0; stride >>= 1) {
-			for(uint32_t i = threadIdx.x; i < P2; i += blockDim.x) {
-				uint32_t jx = i ^ stride;
-				if(jx > i) {
-					bool up = (i & size) == 0;
-					unsigned long long a = keys[i], b = keys[jx];
-					if((a > b) == up) { keys[i] = b; keys[jx] = a; }
-				}
-			}
-			__syncthreads();
+			const unsigned long long other = __shfl_xor(key, (int)stride);
+			const bool up = (lane & size) == 0 || size == 64;
+			const bool lower = (lane & stride) == 0;
+			const unsigned long long lo = key < other ? key : other, hi = key < other ? other : key;
+			key = (lower == up) ? lo : hi;
 		}
 	}
-	for(uint32_t i = threadIdx.x; i < n; i += blockDim.x) {
-		unsigned long long k = ~keys[i];
-		bt2g_sw_cand o;
-		o.score = (int32_t)((uint32_t)(k >> 32) ^ 0x80000000u);
-		o.row = (int32_t)((k >> 16) & 0xffff);
-		o.col = (int32_t)(k & 0xffff);
-		c[i] = o;
+	if(lane < n) c[lane] = cand_of(key);
+}
+
+// Lists longer than 64: one workgroup per queued problem, bitonic sort in LDS
+// (grid-stride over the queue, whose length is only known on the device).
+__global__ void __launch_bounds__(256)
+k_sort_big(const bt2g_sw_result* __restrict__ res, bt2g_sw_cand* __restrict__ cands, uint32_t cap,
+           const uint32_t* __restrict__ big, const uint32_t* __restrict__ nbig) {
+	extern __shared__ __attribute__((aligned(16))) unsigned long long keys[];
+	const uint32_t nq = *nbig;
+	for(uint32_t qi = blockIdx.x; qi < nq; qi += gridDim.x) {
+		const uint32_t pi = big[qi];
+		const int n0 = res[pi].ncand;
+		const uint32_t n = (uint32_t)(n0 > (int)cap ? cap : n0);
+		uint32_t P2 = 1;
+		while(P2 < n) P2 <<= 1;
+		bt2g_sw_cand* c = cands + (size_t)pi * cap;
+		for(uint32_t i = threadIdx.x; i < P2; i += blockDim.x) keys[i] = i < n ? cand_key(c[i]) : ~0ull;
+		__syncthreads();
+		for(uint32_t size = 2; size <= P2; size <<= 1) {
+			for(uint32_t stride = size >> 1; stride > 0; stride >>= 1) {
+				for(uint32_t i = threadIdx.x; i < P2; i += blockDim.x) {
+					const uint32_t jx = i ^ stride;
+					if(jx > i) {
+						const bool up = (i & size) == 0;
+						const unsigned long long a = keys[i], b = keys[jx];
+						if((a > b) == up) { keys[i] = b; keys[jx] = a; }
+					}
+				}
+				__syncthreads();
+			}
+		}
+		for(uint32_t i = threadIdx.x; i < n; i += blockDim.x) c[i] = cand_of(keys[i]);
+		__syncthreads();
 	}
 }
 
@@ -417,9 +462,12 @@ void launch_sw_fill(int variant, const bt2g_sw_problem* probs, uint32_t nprob, c
 }
 
 void launch_sort_cands(const bt2g_sw_result* res, bt2g_sw_cand* cands, uint32_t nprob, uint32_t cap,
-                       hipStream_t st) {
+                       uint32_t* big, uint32_t* nbig, hipStream_t st) {
 	if(nprob == 0) return;
+	hipLaunchKernelGGL(k_sort_small, dim3((nprob + 3) / 4), dim3(256), 0, st, res, cands, nprob, cap, big, nbig);
+	if(cap <= 64) return;
 	uint32_t P2 = 1;
 	while(P2 < cap) P2 <<= 1;
-	hipLaunchKernelGGL(k_sort_cands, dim3(nprob), dim3(256), P2 * sizeof(unsigned long long), st, res, cands, cap);
+	hipLaunchKernelGGL(k_sort_big, dim3(1024), dim3(256), P2 * sizeof(unsigned long long), st, res, cands, cap, big,
+	                   nbig);
 }

@@ -204,7 +204,7 @@ typedef struct {
 /* Fill + candidate gather for every problem: the u8/i16 end-to-end or local
  * fill chosen exactly as SwAligner::align does (u8 first when enable8; local
  * u8 saturation falls back to i16).  cands[p*cap ..] receives the sorted
- * candidate cells.  mat (optional, NULL to skip): per problem
+ * candidate cells (cap: 1..8192 per problem).  mat (optional, NULL to skip): per problem
  * nrow*ncol*3 int16 H,E,F values in the fill's native domain, at mat_off[p]. */
 int bt2g_sw_align(bt2g_ctx* ctx, const uint8_t* reads, const uint8_t* quals, uint32_t stride, const uint32_t* lens,
                   const bt2g_sw_problem* probs, uint32_t nprob, const uint8_t* windows, uint64_t windows_len,
