@@ -467,12 +467,13 @@ int bt2g_get_offset_dev(bt2g_ctx* c, const uint32_t* rows, uint32_t n, uint32_t*
 
 // ---------------------------------------------------------------- SW engine
 // The packed two-problems-per-lane end-to-end fill covers the default
-// end-to-end scoring (no match bonus, byte-sized penalties) without matrix
+// end-to-end scoring (no match bonus, penalties 1..255) without matrix
 // dumps; anything else runs the one-problem-per-lane fills.
 static bool sw_packed_ok(const bt2g_scoring& sc, const SwConst& C, const int16_t* mat) {
-	if(sc.local || mat || sc.match != 0 || C.npen < 0 || C.npen > 255) return false;
+	if(sc.local || mat || sc.match != 0 || sc.gapbar < 1 || C.npen < 0 || C.npen > 255) return false;
 	for(int q = 0; q <= 40; q++)
-		if(C.mmpen[q] < 0 || C.mmpen[q] > 255) return false;
+		if(C.mmpen[q] < 1 || C.mmpen[q] > 255) return false;   // non-zero profile marks a real row
+	if(C.npen < 1) return false;
 	return C.rdgo >= 0 && C.rdge >= 0 && C.rfgo >= 0 && C.rfge >= 0;
 }
 
@@ -511,14 +512,13 @@ int bt2g_sw_align_dev(bt2g_ctx* c, const uint8_t* reads, const uint8_t* quals, u
 	uint32_t* satl = lists + 2 * (size_t)nprob;
 	{
 		ProfScope ps(c, 4, st);
+		const uint32_t S = (stride + 15u) / 16u, lds = 2u * (64u / S) * ((maxcol + 3u) & ~3u);
+		if(sw_packed_ok(*sc, C, mat) && lds <= 65536u) {
+			launch_sw_ee_packed(probs, nprob, reads, quals, stride, lens, windows, c->ref_codes, c->ref_starts, C,
+			                    enable8, cap, maxcol, res, cands, st);
+		} else {
 		launch_sw_partition(probs, nprob, sc->local, enable8, list8, counts + 0, list16, counts + 1, st);
 		int v8 = sc->local ? 2 : 0, v16 = sc->local ? 3 : 1;
-		if(sw_packed_ok(*sc, C, mat)) {
-			launch_sw_ee_packed(0, probs, nprob, list8, counts + 0, reads, quals, stride, lens, windows, c->ref_codes,
-			                    c->ref_starts, C, cap, bnd, maxcol, res, cands, st);
-			launch_sw_ee_packed(1, probs, nprob, list16, counts + 1, reads, quals, stride, lens, windows,
-			                    c->ref_codes, c->ref_starts, C, cap, bnd, maxcol, res, cands, st);
-		} else {
 		launch_sw_fill(v8, probs, nprob, list8, counts + 0, reads, quals, stride, lens, windows, c->ref_codes,
 		               c->ref_starts, C, cap, bnd, maxcol, res, cands, mat, mat_off, satl, counts + 2, st);
 		launch_sw_fill(v16, probs, nprob, list16, counts + 1, reads, quals, stride, lens, windows, c->ref_codes,

@@ -35,10 +35,9 @@ void launch_sw_fill(int variant, const bt2g_sw_problem* probs, uint32_t nprob, c
                     const uint64_t* ref_starts, const SwConst& c, uint32_t cap, uint32_t* bnd,
                     uint32_t bnd_cols, bt2g_sw_result* res, bt2g_sw_cand* cands, int16_t* mat,
                     const uint64_t* mat_off, uint32_t* sat_list, uint32_t* sat_n, hipStream_t st);
-void launch_sw_ee_packed(int variant, const bt2g_sw_problem* probs, uint32_t nprob, const uint32_t* list,
-                         const uint32_t* list_n, const uint8_t* reads, const uint8_t* quals, uint32_t stride,
-                         const uint32_t* lens, const uint8_t* windows, const uint8_t* ref_codes,
-                         const uint64_t* ref_starts, const SwConst& C, uint32_t cap, uint32_t* bnd,
-                         uint32_t bnd_cols, bt2g_sw_result* res, bt2g_sw_cand* cands, hipStream_t st);
+void launch_sw_ee_packed(const bt2g_sw_problem* probs, uint32_t nprob, const uint8_t* reads, const uint8_t* quals,
+                         uint32_t stride, const uint32_t* lens, const uint8_t* windows, const uint8_t* ref_codes,
+                         const uint64_t* ref_starts, const SwConst& C, int enable8, uint32_t cap, uint32_t max_cols,
+                         bt2g_sw_result* res, bt2g_sw_cand* cands, hipStream_t st);
 void launch_sort_cands(const bt2g_sw_result* res, bt2g_sw_cand* cands, uint32_t nprob, uint32_t cap,
                        uint32_t* big, uint32_t* nbig, hipStream_t st);
