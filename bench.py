@@ -228,6 +228,25 @@ class Pipeline:
         return aligned
 
 
+def combine_ranks(elapsed, n_aligned, dev):
+    """Max of the per-rank times, sum of the aligned-read counters: the path's
+    only collective (RCCL on the GPUs, gloo in the CPU tests)."""
+    import torch
+    import torch.distributed as dist
+    if not (dist.is_available() and dist.is_initialized()) or dist.get_world_size() == 1:
+        return elapsed, n_aligned
+    el = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+    na = torch.tensor([float(n_aligned)], dtype=torch.float64, device=dev)
+    dist.all_reduce(el, op=dist.ReduceOp.MAX)
+    dist.all_reduce(na, op=dist.ReduceOp.SUM)
+    return float(el[0]), int(na[0])
+
+
+def shard_seed(rank):
+    """Weak scaling: every rank aligns its own batch of reads (seed 42 + rank)."""
+    return 42 + rank
+
+
 def cpu_baseline(idx, reads, quals, pipe, sample, threads):
     """Reference code (oracle/_ref/libbt2ref.so = /root/reference built by
     oracle/ref/Makefile) on the same per-read work for `sample` reads, split
@@ -371,7 +390,7 @@ def main():
     eng = bt2g.Engine(index=idx, device=local)
     info = eng.info()
     t2 = time.time()
-    reads_np, quals_np = make_reads(parts, args.reads, args.read_len, seed=42 + rank)
+    reads_np, quals_np = make_reads(parts, args.reads, args.read_len, seed=shard_seed(rank))
     log(f"[rank {rank}] {args.reads} reads in {time.time()-t2:.1f}s; index resident: {info[12]/1e9:.2f} GB")
     reads = torch.from_numpy(reads_np).to(dev)
     quals = torch.from_numpy(quals_np).to(dev)
@@ -396,13 +415,7 @@ def main():
     elapsed = time.perf_counter() - ts
     eng.set_profiling(False)
     stats = {k: eng.kernel_stats(k) for k in range(5)}
-    tt = torch.tensor([elapsed, float(n_aligned)], dtype=torch.float64, device=dev)
-    if world > 1:
-        el = tt[:1].clone()
-        dist.all_reduce(el, op=dist.ReduceOp.MAX)
-        na = tt[1:].clone()
-        dist.all_reduce(na, op=dist.ReduceOp.SUM)      # the path's one collective
-        elapsed, n_aligned = float(el[0]), float(na[0])
+    elapsed, n_aligned = combine_ranks(elapsed, n_aligned, dev)
     total_reads = args.reads * args.steps * world
     value = total_reads / elapsed
 

@@ -14,7 +14,8 @@ import subprocess
 import numpy as np
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(HERE, "libbt2g.so")
+# BT2G_LIB selects an alternative in-tree build (kernel experiments)
+LIB_PATH = os.environ.get("BT2G_LIB", os.path.join(HERE, "libbt2g.so"))
 
 BT2G_OK = 0
 BT2G_ERR_OVERFLOW = -6

@@ -14,8 +14,7 @@
 //             (signed saturation at -0x8000 == unsigned saturation at 0)
 //                                                    -> ROW0 = 0xffff, LO = 0
 // so a lane may pair a u8 problem with an i16 one; the reference's veto of
-// gap opens/extensions in the gap-barrier rows becomes a saturating subtract
-// of 0xffff.
+// gap opens/extensions in the gap-barrier rows becomes an AND with 0 (LO).
 //
 // Layout.  A problem pair (low/high half of every register) is swept by a
 // group of S lanes (S = ceil(stride/16)); lane k of the group owns register
@@ -26,10 +25,14 @@
 // column t-k of its 16 rows and hands its bottom row's H/F and the column's
 // reference selector to lane k+1 by one cross-lane shift -- nothing goes
 // through memory between rows, and the reference windows are staged once in
-// LDS, from which lane 0 feeds the selectors.  The bottom lane holds both problems' last rows and gathers the
-// candidates.  Per cell pair: 12 VALU ops (query-profile byte select by
-// v_perm_b32, diagonal, E, F, vetoes, maxima); an 'N' reference column adds
-// the N penalty in real rows only.
+// LDS as per-column selectors.  The bottom lane holds both problems' last rows and gathers the
+// candidates.  Per cell pair: 10 packed ops + 2 ANDs (query-profile byte
+// select by v_perm_b32, diagonal, E, F, maxima, vetoes); an 'N' reference
+// column adds the N penalty in real rows only.  On gfx950 v_pk_*, v_perm_b32
+// and v_max_u32 issue at half the rate of v_add/v_and/v_max_u16
+// (scripts/micro/valu_rate.hip), so a packed pair costs about what one
+// 32-bit cell would: the packing pays through fewer lanes per problem, not
+// through fewer issue slots.
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 #include <type_traits>
@@ -61,12 +64,6 @@ struct Half {
 	int32_t minsc;
 	uint32_t row0;      // 0xff (u8 fill) or 0xffff (i16 fill)
 	bool fw, live;
-	__device__ __forceinline__ int base(uint32_t r) const {
-		if(fw) return rd[r];
-		int c = rd[nrow - 1 - r];
-		return c > 3 ? 4 : 3 - c;
-	}
-	__device__ __forceinline__ int qual(uint32_t r) const { return fw ? qu[r] : qu[nrow - 1 - r]; }
 	// reference character of column j (aligner_sw.cpp:171-253): 0..3, 4 = N / off the reference
 	__device__ __forceinline__ int refc(uint32_t j, const uint8_t* windows, const uint8_t* ref_codes,
 	                                    const uint64_t* ref_starts) const {
@@ -76,19 +73,14 @@ struct Half {
 		uint64_t s = ref_starts[refidx], e = ref_starts[refidx + 1];
 		return (o < 0 || (uint64_t)o >= e - s) ? 4 : ref_codes[s + (uint64_t)o];
 	}
-	// {pen(A), pen(C), pen(G), pen(T)} of read row r (Scoring::score, scoring.h:237-262, no match bonus)
-	__device__ __forceinline__ uint32_t profile(uint32_t r, const SwConst& C) const {
-		int rdc = base(r);
-		if(rdc > 3) return (uint32_t)C.npen * 0x01010101u;
-		int q = qual(r) - 33;
-		q = q < 0 ? 0 : (q > 40 ? 40 : q);
-		return ((uint32_t)C.mmpen[q] * 0x01010101u) & ~(0xffu << (8 * rdc));
-	}
 };
 
 }  // namespace
 
-__global__ void __launch_bounds__(64)
+#ifndef BT2G_SW_WAVES
+#define BT2G_SW_WAVES 2
+#endif
+__global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(BT2G_SW_WAVES)))
 k_sw_ee_sys(const bt2g_sw_problem* __restrict__ probs, uint32_t nprob, const uint8_t* __restrict__ reads,
             const uint8_t* __restrict__ quals, uint32_t stride, const uint32_t* __restrict__ lens,
             const uint8_t* __restrict__ windows, const uint8_t* __restrict__ ref_codes,
@@ -141,9 +133,30 @@ k_sw_ee_sys(const bt2g_sw_problem* __restrict__ probs, uint32_t nprob, const uin
 	}
 	if(ncolmax == 0) return;
 
-	// this lane's rows: global row 16k+i of the stack; problem row = that - (16S - nrow)
+	// Scoring::mmpens (scoring.h:103-131) staged in LDS for per-lane lookups
+	__shared__ uint8_t mmq[48];
+	if(lane <= 40) mmq[lane] = (uint8_t)C.mmpen[lane];
+	// this lane's rows: global row 16k+i of the stack; problem row = that - (16S - nrow).
+	// All read bytes and qualities are fetched first (independent loads, one
+	// wait), then turned into query-profile words.
+	uint32_t bq[2][R];
+#pragma unroll
+	for(int x = 0; x < 2; x++) {
+		const Half& H = h[x];
+		const int64_t rx0 = (int64_t)(16u * k) - (int64_t)(16u * S - H.nrow);
+#pragma unroll
+		for(int i = 0; i < R; i++) {
+			const int64_t rx = rx0 + i;
+			const bool real = H.live && rx >= 0;
+			const uint32_t o = real ? (H.fw ? (uint32_t)rx : H.nrow - 1 - (uint32_t)rx) : 0u;
+			const uint8_t* rdp = real ? H.rd : reads;
+			const uint8_t* qup = real ? H.qu : quals;
+			bq[x][i] = (uint32_t)rdp[o] | ((uint32_t)qup[o] << 8);
+		}
+	}
+	__syncthreads();
 	const uint32_t row0p = h[0].row0 | (h[1].row0 << 16);
-	uint32_t PA[R], PB[R], V[R], E[R], Hc[R];
+	uint32_t PA[R], PB[R], M[R], E[R], Hc[R];   // M: 0 in gap-barrier rows (veto)
 	const int gb = C.gapbar;
 #pragma unroll
 	for(int i = 0; i < R; i++) {
@@ -157,14 +170,20 @@ k_sw_ee_sys(const bt2g_sw_problem* __restrict__ probs, uint32_t nprob, const uin
 				if(rx < 0) {
 					hinit = H.row0;                  // dead row: H(col -1) = ROW0
 				} else {
-					prof = H.profile((uint32_t)rx, C);
+					// {pen(A), pen(C), pen(G), pen(T)} (Scoring::score, scoring.h:237-262, no match bonus)
+					int c = (int)(bq[x][i] & 0xffu);
+					if(!H.fw) c = c > 3 ? 4 : 3 - c;
+					int q = (int)(bq[x][i] >> 8) - 33;
+					q = q < 0 ? 0 : (q > 40 ? 40 : q);
+					prof = c > 3 ? (uint32_t)C.npen * 0x01010101u
+					             : ((uint32_t)mmq[q] * 0x01010101u) & ~(0xffu << (8 * c));
 					if(rx < gb || rx >= (int64_t)H.nrow - gb) veto = 0xffffu;
 				}
 			}
 			if(x == 0) { pa = prof; v |= veto; hi |= hinit; }
 			else { pb = prof; v |= veto << 16; hi |= hinit << 16; }
 		}
-		PA[i] = pa; PB[i] = pb; V[i] = v; E[i] = 0; Hc[i] = hi;
+		PA[i] = pa; PB[i] = pb; M[i] = ~v; E[i] = 0; Hc[i] = hi;
 	}
 	// H(row above this lane's first row, column -1): ROW0 if that row is dead
 	uint32_t hbprev = 0;
@@ -181,45 +200,80 @@ k_sw_ee_sys(const bt2g_sw_problem* __restrict__ probs, uint32_t nprob, const uin
 	const bool top = k == 0, bottom = k == S - 1 || !in_group;
 	int lrmax[2] = {0, 0};
 	uint32_t ncand[2] = {0, 0};
-	// the pair's reference windows, once, into LDS: [slot = x*G + g][column]
-	// codes 0..4 (aligner_sw.cpp:171-253); lane 0 of the group reads them back
-	extern __shared__ uint8_t win[];
+	// The pair's reference windows, once, as per-column v_perm_b32 selectors in
+	// LDS ([group][column], aligner_sw.cpp:171-253 for the characters): byte 0
+	// picks problem A's profile byte for its reference character, byte 2
+	// problem B's (4 + c); 0x0c (zero) marks an 'N' column.  Columns past a
+	// problem's width (and absent problems) get filler 'A' so that only real
+	// 'N' columns send the wave down the N row loop.
+	extern __shared__ uint32_t selw[];
+	uint32_t* mysel = selw + (size_t)g * ldsw;
 	if(in_group) {
+		const uint8_t* src[2];
+		int64_t lo[2], hi[2];
+		bool masks[2];
 #pragma unroll
 		for(int x = 0; x < 2; x++) {
-			uint8_t* w = win + (size_t)((x ? G : 0u) + g) * ldsw;
-			for(uint32_t c = k; c < h[x].ncol; c += S) w[c] = (uint8_t)h[x].refc(c, windows, ref_codes, ref_starts);
+			const Half& H = h[x];
+			masks[x] = H.win_off >= 0;
+			lo[x] = 0;
+			hi[x] = H.ncol;
+			src[x] = reads;
+			if(!H.live) continue;
+			if(masks[x]) {
+				src[x] = windows + H.win_off;
+			} else {
+				const uint64_t rs = ref_starts[H.refidx], re = ref_starts[H.refidx + 1];
+				src[x] = ref_codes + rs + H.refl;        // only dereferenced inside [lo, hi)
+				lo[x] = H.refl < 0 ? -H.refl : 0;
+				const int64_t end = (int64_t)(re - rs) - H.refl;
+				hi[x] = end < hi[x] ? end : hi[x];
+			}
+		}
+		// eight columns (two characters each) in flight per lane, then the selectors
+		for(uint32_t c0 = k; c0 < ncolmax; c0 += 8u * S) {
+			uint32_t v[2][8];
+#pragma unroll
+			for(int u = 0; u < 8; u++) {
+				const int64_t c = (int64_t)c0 + (int64_t)u * S;
+#pragma unroll
+				for(int x = 0; x < 2; x++)
+					v[x][u] = (c >= lo[x] && c < hi[x]) ? src[x][c] : (c < (int64_t)h[x].ncol ? 0x100u : 0x200u);
+			}
+#pragma unroll
+			for(int u = 0; u < 8; u++) {
+				const uint32_t c = c0 + (uint32_t)u * S;
+				if(c >= ncolmax) break;
+				uint32_t sel = 0x0c000c00u;
+#pragma unroll
+				for(int x = 0; x < 2; x++) {
+					// 0x100: off the reference (N); 0x200: filler
+					int code = v[x][u] == 0x100u ? 4 : v[x][u] == 0x200u ? 0
+					         : (masks[x] ? first5((int)v[x][u]) : (int)v[x][u]);
+					sel |= (code < 4 ? (uint32_t)(4 * x + code) : 0x0cu) << (16 * x);
+				}
+				mysel[c] = sel;
+			}
 		}
 	}
 	__syncthreads();
-	const uint8_t* wa = win + (size_t)g * ldsw;
-	const uint8_t* wb = win + (size_t)(G + g) * ldsw;
-	int ca = 4, cb = 4;
-	if(top && in_group) {
-		ca = h[0].ncol > 0 ? wa[0] : 4;
-		cb = h[1].ncol > 0 ? wb[0] : 4;
-	}
-	uint32_t hout = 0, fout = 0, selout = 0;
+	uint32_t hout = 0, fout = 0;
+	uint32_t nsel = in_group ? mysel[0] : 0u;
 	const uint32_t T = ncolmax + S - 1;
 	for(uint32_t t = 0; t < T; t++) {
 		// the lane above computed this lane's column in the previous step (DPP wave_shr:1)
 		const uint32_t hin = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)hout, 0x138, 0xf, 0xf, false);
 		const uint32_t fin = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)fout, 0x138, 0xf, 0xf, false);
-		const uint32_t selin = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)selout, 0x138, 0xf, 0xf, false);
 		const int j = (int)t - (int)k;
 		if(j < 0 || j >= (int)ncolmax) continue;
-		uint32_t sel, hup, fup, diag;
+		const uint32_t sel = nsel;
+		if(in_group) nsel = mysel[(uint32_t)j + 1 < ncolmax ? j + 1 : j];   // next step's column
+		uint32_t hup, fup, diag;
 		if(top) {
-			sel = (ca < 4 ? (uint32_t)ca : 0x0cu) | 0x0c00u | ((cb < 4 ? 4u + (uint32_t)cb : 0x0cu) << 16) |
-			      0x0c000000u;
-			const uint32_t jn = (uint32_t)j + 1;
-			ca = jn < h[0].ncol ? wa[jn] : 4;
-			cb = jn < h[1].ncol ? wb[jn] : 4;
 			hup = 0;
 			fup = 0;
 			diag = row0p;
 		} else {
-			sel = selin;
 			hup = hin;
 			fup = fin;
 			diag = hbprev;
@@ -246,9 +300,9 @@ k_sw_ee_sys(const bt2g_sw_problem* __restrict__ probs, uint32_t nprob, const uin
 					pen = pmax(pen, nfloor & real);
 				}
 				const uint32_t d = psub(diag, pen);
-				const uint32_t f = psub(pmax(psub(fprev, rfge2), psub(hprev, rfgo2)), V[i]);
+				const uint32_t f = pmax(psub(fprev, rfge2), psub(hprev, rfgo2)) & M[i];
 				const uint32_t hh = pmax(pmax(d, E[i]), f);
-				E[i] = pmax(psub(E[i], rdge2), psub(psub(hh, rdgo2), V[i]));
+				E[i] = pmax(psub(E[i], rdge2), psub(hh, rdgo2) & M[i]);
 				diag = Hc[i];
 				Hc[i] = hh;
 				fprev = f;
@@ -259,26 +313,30 @@ k_sw_ee_sys(const bt2g_sw_problem* __restrict__ probs, uint32_t nprob, const uin
 		else rows(std::false_type{});
 		hout = hprev;
 		fout = fprev;
-		selout = sel;
-		if(bottom) {
-			// both problems' last rows: end-to-end candidates (aligner_swsse_ee_u8.cpp:1190-1201)
+		// the bottom lane is the last reader of column j's selector: the slot now
+		// keeps both problems' last-row H for the gather below
+		if(bottom && in_group) mysel[j] = hprev;
+	}
+	if(!bottom || !in_group) return;
+	// last-row maximum and end-to-end candidates in column order
+	// (aligner_swsse_ee_u8.cpp:1096-1100, 1176-1208)
+	for(uint32_t c = 0; c < ncolmax; c++) {
+		const uint32_t hv = mysel[c];
 #pragma unroll
-			for(int x = 0; x < 2; x++) {
-				if(h[x].live && (uint32_t)j < h[x].ncol) {
-					const int v = (int)((hprev >> (16 * x)) & 0xffffu);
-					lrmax[x] = v > lrmax[x] ? v : lrmax[x];
-					const int64_t sc = (int64_t)v - (int64_t)h[x].row0;
-					if(sc >= h[x].minsc) {
-						if(ncand[x] < cap)
-							cands[(size_t)h[x].pi * cap + ncand[x]] =
-							    bt2g_sw_cand{(int32_t)h[x].nrow - 1, j, (int32_t)sc};
-						ncand[x]++;
-					}
+		for(int x = 0; x < 2; x++) {
+			if(h[x].live && c < h[x].ncol) {
+				const int v = (int)((hv >> (16 * x)) & 0xffffu);
+				lrmax[x] = v > lrmax[x] ? v : lrmax[x];
+				const int64_t sc = (int64_t)v - (int64_t)h[x].row0;
+				if(sc >= h[x].minsc) {
+					if(ncand[x] < cap)
+						cands[(size_t)h[x].pi * cap + ncand[x]] =
+						    bt2g_sw_cand{(int32_t)h[x].nrow - 1, (int32_t)c, (int32_t)sc};
+					ncand[x]++;
 				}
 			}
 		}
 	}
-	if(!bottom || !in_group) return;
 	// SwAligner::align end-to-end outcome (aligner_sw.cpp:500-620), as k_sw_fill
 #pragma unroll
 	for(int x = 0; x < 2; x++) {
@@ -311,8 +369,9 @@ void launch_sw_ee_packed(const bt2g_sw_problem* probs, uint32_t nprob, const uin
 	if(nprob == 0) return;
 	const uint32_t S = (stride + 15u) / 16u;     // <= 64 (stride <= BT2G_MAX_READ_LEN)
 	const uint32_t per_wave = 2u * (64u / S);
-	const uint32_t ldsw = (max_cols + 3u) & ~3u;
-	hipLaunchKernelGGL(k_sw_ee_sys, dim3((nprob + per_wave - 1) / per_wave), dim3(64), per_wave * ldsw, st, probs,
+	const uint32_t ldsw = max_cols | 1u;          // odd word stride: groups hit different banks
+	hipLaunchKernelGGL(k_sw_ee_sys, dim3((nprob + per_wave - 1) / per_wave), dim3(64),
+	                   (per_wave / 2) * ldsw * sizeof(uint32_t), st, probs,
 	                   nprob, reads, quals, stride, lens, windows, ref_codes, ref_starts, C, enable8, cap, max_cols, S,
 	                   ldsw, res, cands);
 }
