@@ -397,7 +397,8 @@ namespace {
 struct OneMmScratch {
 	bt2g_mm1* slots = nullptr;
 	int32_t* slot_counts = nullptr;
-	int32_t* ovf = nullptr;
+	int32_t* ovf = nullptr;        // ovf[0] overflow flag, ovf[1..2] item count / queue head
+	uint32_t* items = nullptr;
 };
 }  // namespace
 
@@ -413,14 +414,15 @@ static int one_mm_impl(bt2g_ctx* c, const uint8_t* reads, const uint8_t* quals, 
 	OneMmScratch s;
 	HIPCHK(hipMallocAsync((void**)&s.slots, sizeof(bt2g_mm1) * (size_t)n * 4 * cap, st));
 	HIPCHK(hipMallocAsync((void**)&s.slot_counts, sizeof(int32_t) * (size_t)n * 4, st));
-	HIPCHK(hipMallocAsync((void**)&s.ovf, sizeof(int32_t), st));
-	HIPCHK(hipMemsetAsync(s.ovf, 0, sizeof(int32_t), st));
+	HIPCHK(hipMallocAsync((void**)&s.ovf, sizeof(int32_t) * 4, st));
+	HIPCHK(hipMallocAsync((void**)&s.items, sizeof(uint32_t) * (size_t)n * 4, st));
+	HIPCHK(hipMemsetAsync(s.ovf, 0, sizeof(int32_t) * 4, st));
 	HIPCHK(hipMemsetAsync(bwops, 0, sizeof(uint32_t) * n, st));
 	if(loads) HIPCHK(hipMemsetAsync(loads, 0, sizeof(uint32_t) * n, st));
 	{
 		ProfScope ps(c, 2, st);
-		launch_one_mm(c->fw, c->bw, reads, quals, stride, lens, n, minsc, *sc, nofw, norc, gate, cap, s.slots,
-		              s.slot_counts, hits, counts, bwops, loads, s.ovf, st);
+		launch_one_mm(c->fw, c->bw, reads, quals, stride, lens, n, minsc, *sc, nofw, norc, gate, cap, s.items,
+		              (uint32_t*)s.ovf + 1, s.slots, s.slot_counts, hits, counts, bwops, loads, s.ovf, st);
 	}
 	HIPCHK(hipGetLastError());
 	int32_t ovf = 0;
@@ -428,6 +430,7 @@ static int one_mm_impl(bt2g_ctx* c, const uint8_t* reads, const uint8_t* quals, 
 	HIPCHK(hipFreeAsync(s.slots, st));
 	HIPCHK(hipFreeAsync(s.slot_counts, st));
 	HIPCHK(hipFreeAsync(s.ovf, st));
+	HIPCHK(hipFreeAsync(s.items, st));
 	if(sync_overflow) {
 		HIPCHK(hipStreamSynchronize(st));
 		if(ovf) return fail(BT2G_ERR_OVERFLOW, "one-mismatch hits exceed cap %u", cap);

@@ -32,6 +32,26 @@ struct DevEbwt {
 	uint32_t fchr[5];
 };
 
+// Field-wise per-lane choice between two indexes (a per-lane reference to one
+// of two kernel arguments would have to live in scratch).
+__device__ __forceinline__ DevEbwt pick_ebwt(bool first, const DevEbwt& a, const DevEbwt& b) {
+	DevEbwt e;
+	e.sides = first ? a.sides : b.sides;
+	e.ftab = first ? a.ftab : b.ftab;
+	e.eftab = first ? a.eftab : b.eftab;
+	e.offs = first ? a.offs : b.offs;
+	e.len = first ? a.len : b.len;
+	e.zoff = first ? a.zoff : b.zoff;
+	e.zbyte = first ? a.zbyte : b.zbyte;
+	e.zbp = first ? a.zbp : b.zbp;
+	e.ftab_chars = first ? a.ftab_chars : b.ftab_chars;
+	e.off_rate = first ? a.off_rate : b.off_rate;
+	e.fw = first ? a.fw : b.fw;
+#pragma unroll
+	for(int i = 0; i < 5; i++) e.fchr[i] = first ? a.fchr[i] : b.fchr[i];
+	return e;
+}
+
 // One loaded side: 12 BWT words (16 rows each) + 4 occ counts.
 struct SideData {
 	uint32_t w[12];
@@ -80,8 +100,26 @@ __device__ __forceinline__ uint32_t side_count1(const SideData& s, uint32_t char
 	return n;
 }
 
+// Character of row charOff of the side.  The word is picked by a select chain
+// over values made opaque to the optimiser: folded back into an indexed load,
+// a data-dependent index would put the whole side in scratch.
 __device__ __forceinline__ int side_rowL(const SideData& s, uint32_t charOff) {
-	return (int)((s.w[charOff >> 4] >> (2 * (charOff & 15))) & 3u);
+	const uint32_t k = charOff >> 4;
+	uint32_t v[12];
+#pragma unroll
+	for(int i = 0; i < 12; i++) v[i] = s.w[i];
+	asm volatile("" : "+v"(v[0]), "+v"(v[1]), "+v"(v[2]), "+v"(v[3]), "+v"(v[4]), "+v"(v[5]), "+v"(v[6]),
+	                  "+v"(v[7]), "+v"(v[8]), "+v"(v[9]), "+v"(v[10]), "+v"(v[11]));
+	uint32_t w = v[0];
+#pragma unroll
+	for(int i = 1; i < 12; i++) w = k == (uint32_t)i ? v[i] : w;
+	return (int)((w >> (2 * (charOff & 15))) & 3u);
+}
+
+
+// fchr[c] without a data-dependent index into the (kernel-argument) array
+__device__ __forceinline__ uint32_t fchr_at(const DevEbwt& e, int c) {
+	return c == 0 ? e.fchr[0] : c == 1 ? e.fchr[1] : c == 2 ? e.fchr[2] : c == 3 ? e.fchr[3] : e.fchr[4];
 }
 
 // '$' correction of countBt2Side/Ex: true iff the '$' (stored as 'A') lies in
@@ -109,7 +147,10 @@ __device__ __forceinline__ uint32_t occ1(const DevEbwt& e, const SideData& s, ui
 	uint32_t side = row / 192u, co = row % 192u;
 	uint32_t n = side_count1(s, co, ch);
 	if(ch == 0 && dollar_before(e, side, co)) n--;
-	return n + s.occ[ch] + e.fchr[ch];
+	uint32_t o0 = s.occ[0], o1 = s.occ[1], o2 = s.occ[2], o3 = s.occ[3];
+	asm volatile("" : "+v"(o0), "+v"(o1), "+v"(o2), "+v"(o3));   // keep the select in registers
+	const uint32_t occ = ch == 0 ? o0 : ch == 1 ? o1 : ch == 2 ? o2 : o3;
+	return n + occ + fchr_at(e, ch);
 }
 
 __device__ __forceinline__ uint32_t ftab_hi(const DevEbwt& e, uint32_t i) {

@@ -46,7 +46,7 @@ k_exact_sweep(DevEbwt e, const uint8_t* __restrict__ reads, uint32_t stride, con
 				dep += flen;
 			} else {
 				int c = seq[len - dep - 1];
-				if(c < 4) { top = e.fchr[c]; bot = e.fchr[c + 1]; }
+				if(c < 4) { top = fchr_at(e, c); bot = fchr_at(e, c + 1); }
 				dep++;
 			}
 			if(bot <= top) {
@@ -165,8 +165,8 @@ k_seed_search(DevEbwt F, DevEbwt B, const uint8_t* __restrict__ reads, uint32_t 
 				step = flen;
 			} else {
 				int c = seq[L - 1];
-				topf = topb = F.fchr[c];
-				botf = botb = F.fchr[c + 1];
+				topf = topb = fchr_at(F, c);
+				botf = botb = fchr_at(F, c + 1);
 				dead = botf == topf;
 				step = 1;
 			}
@@ -199,219 +199,10 @@ k_seed_search(DevEbwt F, DevEbwt B, const uint8_t* __restrict__ reads, uint32_t 
 }
 
 // --------------------------------------------------------------------------
-// oneMmSearch (aligner_seed.cpp:973-1323) with rep1mm=true, repex=false.
-// One lane = one (read, strand, index direction); the 4 lanes of a read write
-// their hits into 4 slots that are concatenated in the reference's loop order
-// (fw/BWT, fw/BWT', rc/BWT, rc/BWT') by k_one_mm_compact.
+// oneMmSearch: the search itself is fm_one_mm.hip (work-queue kernel); its
+// per-(read, strand, index) slots are concatenated here in the reference's
+// loop order (fw/BWT, fw/BWT', rc/BWT, rc/BWT').
 // --------------------------------------------------------------------------
-struct MmParams {
-	int32_t match, mmp_max, mmp_min, npen, local;
-	int32_t nceil_const_x1000, nceil_lin_x1000;
-};
-
-__device__ __forceinline__ int mmpen_q(const MmParams& p, int q) {
-	int ii = q < 40 ? q : 40;
-	float frac = (float)ii / 40.0f;
-	return p.mmp_min + (int)(frac * (float)(p.mmp_max - p.mmp_min));
-}
-
-__global__ void __launch_bounds__(256)
-k_one_mm(DevEbwt F, DevEbwt B, const uint8_t* __restrict__ reads, const uint8_t* __restrict__ quals,
-         uint32_t stride, const uint32_t* __restrict__ lens, uint32_t n, const int32_t* __restrict__ minscs,
-         MmParams P, double ncl_const, double ncl_lin, int nofw, int norc, const uint32_t* __restrict__ gate,
-         uint32_t cap, bt2g_mm1* __restrict__ slots, int32_t* __restrict__ slot_counts, uint32_t* __restrict__ ops_out,
-         uint32_t* __restrict__ loads_out) {
-	uint32_t gid = blockIdx.x * blockDim.x + threadIdx.x;
-	uint32_t r = gid >> 2, fwi = (gid >> 1) & 1, ebwtfwi = gid & 1;
-	if(r >= n) return;
-	int32_t nh = 0;
-	uint32_t ops = 0, loads = 0;
-	bt2g_mm1* myslot = slots + ((size_t)r * 4 + fwi * 2 + ebwtfwi) * cap;
-	const bool fw = fwi == 0, ebwtfw = ebwtfwi == 0;
-	const uint32_t len = lens[r];
-	const uint8_t* rd = reads + (size_t)r * stride;
-	const uint8_t* qd = quals + (size_t)r * stride;
-	uint32_t ns = 0;
-	for(uint32_t i = 0; i < len; i++) ns += rd[i] > 3;
-	int nceil = (int)(ncl_const + ncl_lin * (double)len);
-	if(nceil < 0) nceil = 0;
-	const int64_t minsc = minscs[r];
-	bool nofw_r = nofw, norc_r = norc, gated_off = false;
-	if(gate) {
-		// bt2_search.cpp:3476-3506, 3640-3667: skipped when an exact end-to-end hit
-		// exists (bestmin == 0); otherwise nofw = !(mineFw <= 1), norc = !(mineRc <= 1).
-		uint32_t mfw = gate[(size_t)r * 8 + 0], mrc = gate[(size_t)r * 8 + 1];
-		uint32_t bestmin = mfw < mrc ? mfw : mrc;
-		bool yfw = mfw <= 1 && !nofw, yrc = mrc <= 1 && !norc;
-		gated_off = bestmin == 0 || !(yfw || yrc);
-		nofw_r = !yfw; norc_r = !yrc;
-	}
-	bool run = !gated_off && ns <= 1 && !((fw && nofw_r) || (!fw && norc_r));
-	if(run) {
-		const DevEbwt& E = ebwtfw ? F : B;
-		const DevEbwt& Ep = ebwtfw ? B : F;
-		// seq = fw ? (ebwtfw ? patFw : patFwRev) : (ebwtfw ? patRc : patRcRev)
-		SeqView seq{rd, len, fw ? !ebwtfw : ebwtfw, !fw};
-		// qual = fw ? (ebwtfw ? qual : qualRev) : (ebwtfw ? qualRev : qual)
-		const bool qrev = fw ? !ebwtfw : ebwtfw;
-		const uint32_t halfFw = len >> 1, halfBw = (len >> 1) + (len & 1);
-		const uint32_t nea = ebwtfw ? halfFw : halfBw;
-		const uint32_t flen = E.ftab_chars;
-		const int64_t matchsc = (int64_t)((float)P.match + 0.5f);
-		bool skip = false;
-		for(uint32_t dep = 0; dep < nea; dep++) if(seq[len - dep - 1] > 3) { skip = true; break; }
-		uint32_t t[4] = {0, 0, 0, 0}, b[4] = {0, 0, 0, 0}, tp[4] = {0, 0, 0, 0}, bp[4] = {0, 0, 0, 0};
-		uint32_t top = 0, bot = 0, topp = 0, botp = 0, dep = 0;
-		if(!skip) {
-			if(flen > 1 && flen <= nea) {
-				// ftabSeqToInt(seq, len-flen, rev=!ebwtfw): for E it reads left-to-right,
-				// for Ep right-to-left (bt2_idx.h:1383-1390)
-				uint32_t fi = 0, fip = 0;
-				for(uint32_t i = 0; i < flen; i++) {
-					fi = (fi << 2) | (uint32_t)seq[len - flen + i];
-					fip = (fip << 2) | (uint32_t)seq[len - 1 - i];
-				}
-				top = ftab_hi(E, fi); bot = ftab_lo(E, fi + 1);
-				topp = ftab_hi(Ep, fip); botp = ftab_lo(Ep, fip + 1);
-				if(bot - top == 0) skip = true;
-				else {
-					int c = seq[len - flen];
-					t[c] = top; b[c] = bot; tp[c] = topp; bp[c] = botp;
-					dep = flen;
-				}
-			} else {
-				int c = seq[len - 1];
-				top = topp = tp[c] = E.fchr[c];
-				bot = botp = bp[c] = E.fchr[c + 1];
-				if(bot - top == 0) skip = true;
-				else dep = 1;
-			}
-		}
-		if(!skip) {
-			// near half: exact
-			for(; dep < nea; dep++) {
-				int rdc = seq[len - dep - 1];
-				for(int i = 0; i < 4; i++) { tp[i] = topp; bp[i] = botp; }
-				ops++;
-				if(bot - top > 1) {
-					for(int i = 0; i < 4; i++) t[i] = b[i] = 0;
-					loads += bi_step(E, top, bot, topp, t, b, tp, bp);
-					top = t[rdc]; bot = b[rdc];
-					if(bot <= top) { skip = true; break; }
-					topp = tp[rdc]; botp = bp[rdc];
-				} else {
-					SideData s1;
-					load_side(E, top / 192u, s1);
-					loads++;
-					uint32_t co = top % 192u;
-					if(side_rowL(s1, co) != rdc || top == E.zoff) { skip = true; break; }
-					top = occ1(E, s1, top, rdc);
-					bot = top + 1;
-					t[rdc] = top; b[rdc] = bot; tp[rdc] = topp; bp[rdc] = botp;
-				}
-			}
-		}
-		if(!skip) {
-			// far half: 1 mismatch allowed
-			for(; dep < len; dep++) {
-				int rdc = seq[len - dep - 1];
-				int quc = qd[qrev ? dep : len - dep - 1];
-				if(rdc > 3 && nceil == 0) break;
-				for(int i = 0; i < 4; i++) { tp[i] = topp; bp[i] = botp; }
-				int clo = 0, chi = 3;
-				bool match = true;
-				ops++;
-				if(bot - top > 1) {
-					for(int i = 0; i < 4; i++) t[i] = b[i] = 0;
-					loads += bi_step(E, top, bot, topp, t, b, tp, bp);
-					match = rdc < 4;
-					if(rdc < 4) { top = t[rdc]; bot = b[rdc]; topp = tp[rdc]; botp = bp[rdc]; }
-				} else {
-					if(top == E.zoff) break;       // mapLF1(row&) hit the '$'
-					SideData s1;
-					load_side(E, top / 192u, s1);
-					loads++;
-					uint32_t co = top % 192u;
-					clo = side_rowL(s1, co);
-					top = occ1(E, s1, top, clo);
-					match = clo == rdc;
-					t[clo] = top;
-					b[clo] = bot = top + 1;
-					bp[clo] = botp; tp[clo] = topp;
-					chi = clo;
-				}
-				if(ns == 0 || rdc > 3) {
-					for(int j = clo; j <= chi; j++) {
-						if(j == rdc || b[j] == t[j]) continue;
-						uint32_t depm = dep + 1;
-						uint32_t topm = t[j], botm = b[j], topmp = tp[j], botmp = bp[j];
-						for(; depm < len; depm++) {
-							int rdcm = seq[len - depm - 1];
-							ops++;
-							if(botm - topm > 1) {
-								uint32_t tm[4] = {0, 0, 0, 0}, bm[4] = {0, 0, 0, 0}, tmp[4], bmp[4];
-								tmp[0] = topmp;
-								loads += bi_step(E, topm, botm, topmp, tm, bm, tmp, bmp);
-								topm = tm[rdcm]; botm = bm[rdcm]; topmp = tmp[rdcm]; botmp = bmp[rdcm];
-								if(botm <= topm) break;
-							} else {
-								SideData s1;
-								load_side(E, topm / 192u, s1);
-								loads++;
-								uint32_t co = topm % 192u;
-								if(side_rowL(s1, co) != rdcm || topm == E.zoff) break;
-								topm = occ1(E, s1, topm, rdcm);
-								botm = topm + 1;
-							}
-						}
-						if(depm == len) {
-							uint32_t off5p = dep;
-							if(fw == ebwtfw) off5p = len - off5p - 1;
-							int64_t score = (int64_t)(len - 1) * matchsc;
-							int pen = rdc > 3 ? -P.npen : -mmpen_q(P, quc - 33);
-							score += pen;
-							bool valid = true;
-							if(P.local) {
-								int64_t lf = 0, lb = 0;
-								for(uint32_t i = 0; i < len; i++) {
-									if(i == dep) {
-										if(lf + pen <= 0) { valid = false; break; }
-										lf += pen;
-									} else lf += matchsc;
-									if(len - i - 1 == dep) {
-										if(lb + pen <= 0) { valid = false; break; }
-										lb += pen;
-									} else lb += matchsc;
-								}
-							}
-							if(valid) valid = score >= minsc;
-							if(valid) {
-								if((uint32_t)nh < cap) {
-									bt2g_mm1 h;
-									h.top = ebwtfw ? topm : topmp;
-									h.bot = ebwtfw ? botm : botmp;
-									h.fw = fw ? 1 : 0; h.score = (int32_t)score; h.pos = (int32_t)off5p;
-									h.chr = j; h.qchr = rdc; h.pad = 0;
-									myslot[nh] = h;
-								}
-								nh++;
-							}
-						}
-					}
-				}
-				if(bot > top && match) {
-					if(dep == len - 1) break;
-				} else {
-					break;
-				}
-			}
-		}
-	}
-	slot_counts[(size_t)r * 4 + fwi * 2 + ebwtfwi] = nh;
-	if(ops) atomicAdd(&ops_out[r], ops);
-	if(loads && loads_out) atomicAdd(&loads_out[r], loads);
-}
-
 // Concatenate the 4 per-direction slots of each read in discovery order.
 __global__ void k_one_mm_compact(const bt2g_mm1* __restrict__ slots, const int32_t* __restrict__ slot_counts,
                                  uint32_t n, uint32_t cap, bt2g_mm1* __restrict__ hits, int32_t* __restrict__ counts,
@@ -483,14 +274,11 @@ void launch_seed_search(const DevEbwt& F, const DevEbwt& B, const uint8_t* reads
 
 void launch_one_mm(const DevEbwt& F, const DevEbwt& B, const uint8_t* reads, const uint8_t* quals, uint32_t stride,
                    const uint32_t* lens, uint32_t n, const int32_t* minsc, const bt2g_scoring& sc, int nofw,
-                   int norc, const uint32_t* gate, uint32_t cap, bt2g_mm1* slots, int32_t* slot_counts,
-                   bt2g_mm1* hits, int32_t* counts, uint32_t* ops, uint32_t* loads, int32_t* overflow,
-                   hipStream_t st) {
-	MmParams P{sc.match, sc.mmp_max, sc.mmp_min, sc.npen, sc.local, 0, 0};
-	uint64_t threads = (uint64_t)n * 4;
-	hipLaunchKernelGGL(k_one_mm, dim3((uint32_t)((threads + 255) / 256)), dim3(256), 0, st, F, B, reads, quals,
-	                   stride, lens, n, minsc, P, sc.ncl_const, sc.ncl_lin, nofw, norc, gate, cap, slots,
-	                   slot_counts, ops, loads);
+                   int norc, const uint32_t* gate, uint32_t cap, uint32_t* items, uint32_t* counters,
+                   bt2g_mm1* slots, int32_t* slot_counts, bt2g_mm1* hits, int32_t* counts, uint32_t* ops,
+                   uint32_t* loads, int32_t* overflow, hipStream_t st) {
+	launch_one_mm_q(F, B, reads, quals, stride, lens, n, minsc, sc, nofw, norc, gate, cap, items, counters, slots,
+	                slot_counts, ops, loads, st);
 	hipLaunchKernelGGL(k_one_mm_compact, dim3((n + 255) / 256), dim3(256), 0, st, slots, slot_counts, n, cap, hits,
 	                   counts, overflow);
 }

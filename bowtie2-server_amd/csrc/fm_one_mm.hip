@@ -1,0 +1,344 @@
+// fm_one_mm.hip -- SeedAligner::oneMmSearch (aligner_seed.cpp:973-1323) with
+// rep1mm=true, repex=false, as a persistent work-queue kernel.
+//
+// A work item is one (read, strand, index direction) the reference would run
+// (k_one_mm_items applies the exact-sweep gate of bt2_search.cpp:3640-3667 and
+// the "at most one N" rule).  Each lane runs a small state machine over its
+// item -- near half exact, far half with one mismatch, one branch walk per
+// alternative base -- and performs exactly one LF operation (one or two 64-B
+// side gathers) per loop iteration.  When its item ends the lane takes the next
+// one from a global queue (one atomic per wave), so the wave never idles on
+// finished lanes: the dependent-gather chains stay dense, which is what this
+// latency-bound walk needs.  Hits go to per-item slots in discovery order;
+// k_one_mm_compact concatenates the four slots of a read in the reference's
+// loop order (fw/BWT, fw/BWT', rc/BWT, rc/BWT').
+#include "fm_device.h"
+#include "bt2g_kernels.h"
+
+namespace {
+
+__device__ __forceinline__ int mmpen_q(const MmParams& p, int q) {
+	int ii = q < 40 ? q : 40;
+	float frac = (float)ii / 40.0f;
+	return p.mmp_min + (int)(frac * (float)(p.mmp_max - p.mmp_min));
+}
+
+enum : int { ST_IDLE = 0, ST_NEAR, ST_FAR, ST_ALT, ST_BR, ST_DONE };
+
+// register-array access by a data-dependent index without going through scratch
+__device__ __forceinline__ uint32_t at4(const uint32_t a[4], int i) {
+	return i == 0 ? a[0] : i == 1 ? a[1] : i == 2 ? a[2] : a[3];
+}
+__device__ __forceinline__ void set4(uint32_t a[4], int i, uint32_t v) {
+#pragma unroll
+	for(int k = 0; k < 4; k++) a[k] = i == k ? v : a[k];
+}
+
+}  // namespace
+
+// Work list: item = read << 3 | fwi << 2 | ebwtfwi << 1 | (read has an N).
+__global__ void __launch_bounds__(256)
+k_one_mm_items(const uint8_t* __restrict__ reads, uint32_t stride, const uint32_t* __restrict__ lens, uint32_t n,
+               const uint32_t* __restrict__ gate, int nofw, int norc, uint32_t* __restrict__ items,
+               uint32_t* __restrict__ nitems, int32_t* __restrict__ slot_counts) {
+	const uint32_t r = blockIdx.x * blockDim.x + threadIdx.x;
+	const uint32_t lane = threadIdx.x & 63u;
+	uint32_t runmask = 0, ns = 0;
+	if(r < n) {
+		const uint32_t len = lens[r];
+		const uint8_t* rd = reads + (size_t)r * stride;
+		for(uint32_t i = 0; i < len; i++) ns += rd[i] > 3;
+		bool nofw_r = nofw, norc_r = norc, gated_off = false;
+		if(gate) {
+			// bt2_search.cpp:3476-3506, 3640-3667: skipped when an exact end-to-end hit
+			// exists (bestmin == 0); otherwise nofw = !(mineFw <= 1), norc = !(mineRc <= 1)
+			const uint32_t mfw = gate[(size_t)r * 8 + 0], mrc = gate[(size_t)r * 8 + 1];
+			const uint32_t bestmin = mfw < mrc ? mfw : mrc;
+			const bool yfw = mfw <= 1 && !nofw, yrc = mrc <= 1 && !norc;
+			gated_off = bestmin == 0 || !(yfw || yrc);
+			nofw_r = !yfw;
+			norc_r = !yrc;
+		}
+		for(int d = 0; d < 4; d++) {
+			const bool fw = (d >> 1) == 0;
+			if(!gated_off && ns <= 1 && !((fw && nofw_r) || (!fw && norc_r))) runmask |= 1u << d;
+			slot_counts[(size_t)r * 4 + d] = 0;
+		}
+	}
+	const uint64_t below = (1ull << lane) - 1ull;
+	for(int d = 0; d < 4; d++) {
+		const bool want = (runmask >> d) & 1u;
+		const uint64_t m = __ballot(want);
+		uint32_t base = 0;
+		if(lane == 0 && m) base = atomicAdd(nitems, (uint32_t)__popcll(m));
+		base = __shfl(base, 0);
+		if(want) items[base + (uint32_t)__popcll(m & below)] = (r << 3) | ((uint32_t)d << 1) | (ns ? 1u : 0u);
+	}
+}
+
+__global__ void __launch_bounds__(256)
+k_one_mm_q(DevEbwt F, DevEbwt B, const uint8_t* __restrict__ reads, const uint8_t* __restrict__ quals,
+           uint32_t stride, const uint32_t* __restrict__ lens, const int32_t* __restrict__ minscs, MmParams P,
+           double ncl_const, double ncl_lin, const uint32_t* __restrict__ items,
+           const uint32_t* __restrict__ nitems_p, uint32_t* __restrict__ head, uint32_t cap,
+           bt2g_mm1* __restrict__ slots, int32_t* __restrict__ slot_counts, uint32_t* __restrict__ ops_out,
+           uint32_t* __restrict__ loads_out) {
+	const uint32_t lane = threadIdx.x & 63u;
+	const uint32_t nitems = *nitems_p;
+	const int64_t matchsc = (int64_t)((float)P.match + 0.5f);
+	const uint64_t below = (1ull << lane) - 1ull;
+
+	// per-lane item state
+	int st = ST_IDLE;
+	uint32_t r = 0, len = 0, slot = 0, dep = 0, nea = 0, depm = 0;
+	bool fw = true, ebwtfw = true, hasn = false;
+	int nceil = 0;
+	int64_t minsc = 0;
+	const uint8_t* rd = reads;
+	const uint8_t* qd = quals;
+	SeqView seq{reads, 0, false, false};
+	bool qrev = false;
+	uint32_t top = 0, bot = 0, topp = 0, botp = 0;            // main range (+ mirror)
+	uint32_t t[4], b[4], tp[4], bp[4];                        // far step's four ranges
+	int rdc = 0, quc = 0, clo = 0, chi = 3, j = 0;
+	bool match = true;
+	uint32_t topm = 0, botm = 0, topmp = 0, botmp = 0;        // branch range (+ mirror)
+	int32_t nh = 0;
+	uint32_t ops = 0, loads = 0;
+#pragma unroll
+	for(int i = 0; i < 4; i++) t[i] = b[i] = tp[i] = bp[i] = 0;
+	bool exhausted = false;
+
+	for(;;) {
+		// ---- transitions that need no side gather (bounded per iteration)
+		for(int pass = 0; pass < 8; pass++) {
+			if(st == ST_ALT) {
+				// alternatives clo..chi at depth dep (aligner_seed.cpp:1166-1290)
+				bool started = false;
+				if(!hasn || rdc > 3) {
+					for(; j <= chi; j++) {
+						if(j == rdc || at4(b, j) == at4(t, j)) continue;
+						depm = dep + 1;
+						topm = at4(t, j); botm = at4(b, j); topmp = at4(tp, j); botmp = at4(bp, j);
+						if(depm < len) { started = true; break; }
+						// branch complete at the last base: report (no further LF step)
+						uint32_t off5p = dep;
+						if(fw == ebwtfw) off5p = len - off5p - 1;
+						int64_t score = (int64_t)(len - 1) * matchsc;
+						const int pen = rdc > 3 ? -P.npen : -mmpen_q(P, quc - 33);
+						score += pen;
+						bool valid = true;
+						if(P.local) {
+							int64_t lf = 0, lb = 0;
+							for(uint32_t i = 0; i < len; i++) {
+								if(i == dep) { if(lf + pen <= 0) { valid = false; break; } lf += pen; }
+								else lf += matchsc;
+								if(len - i - 1 == dep) { if(lb + pen <= 0) { valid = false; break; } lb += pen; }
+								else lb += matchsc;
+							}
+						}
+						if(valid && score >= minsc) {
+							if((uint32_t)nh < cap)
+								slots[(size_t)slot * cap + nh] = bt2g_mm1{ebwtfw ? topm : topmp, ebwtfw ? botm : botmp,
+								                                          fw ? 1 : 0, (int32_t)score, (int32_t)off5p,
+								                                          j, rdc, 0};
+							nh++;
+						}
+					}
+				}
+				if(started) {
+					st = ST_BR;
+				} else if(bot > top && match && dep != len - 1) {
+					dep++;
+					st = ST_FAR;
+				} else {
+					st = ST_DONE;
+				}
+			}
+			if(st == ST_DONE) {
+				slot_counts[slot] = nh;
+				if(ops) atomicAdd(&ops_out[r], ops);
+				if(ops && loads_out) atomicAdd(&loads_out[r], loads);
+				st = ST_IDLE;
+			}
+			// refill idle lanes from the queue (one atomic per wave)
+			const bool idle = st == ST_IDLE;
+			const uint64_t m = __ballot(idle && !exhausted);
+			if(m == 0) break;
+			uint32_t base = 0;
+			if(lane == (uint32_t)__ffsll((long long)m) - 1u) base = atomicAdd(head, (uint32_t)__popcll(m));
+			base = __shfl(base, __ffsll((long long)m) - 1);
+			if(base + (uint32_t)__popcll(m) >= nitems) exhausted = true;
+			if(!idle) continue;
+			const uint32_t qi = base + (uint32_t)__popcll(m & below);
+			if(qi >= nitems) continue;
+			// ---- item initialisation (aligner_seed.cpp:1003-1100)
+			const uint32_t item = items[qi];
+			r = item >> 3;
+			const uint32_t fwi = (item >> 2) & 1u, ebi = (item >> 1) & 1u;
+			hasn = item & 1u;
+			fw = fwi == 0;
+			ebwtfw = ebi == 0;
+			slot = r * 4 + fwi * 2 + ebi;
+			len = lens[r];
+			rd = reads + (size_t)r * stride;
+			qd = quals + (size_t)r * stride;
+			minsc = minscs[r];
+			nceil = (int)(ncl_const + ncl_lin * (double)len);
+			if(nceil < 0) nceil = 0;
+			nh = 0;
+			ops = loads = 0;
+			// seq = fw ? (ebwtfw ? patFw : patFwRev) : (ebwtfw ? patRc : patRcRev)
+			seq = SeqView{rd, len, fw ? !ebwtfw : ebwtfw, !fw};
+			qrev = fw ? !ebwtfw : ebwtfw;
+			const uint32_t halfFw = len >> 1, halfBw = (len >> 1) + (len & 1);
+			nea = ebwtfw ? halfFw : halfBw;
+			const DevEbwt E = pick_ebwt(ebwtfw, F, B);
+			const DevEbwt Ep = pick_ebwt(ebwtfw, B, F);
+			const uint32_t flen = E.ftab_chars;
+			bool skip = len == 0;
+			for(uint32_t d = 0; d < nea; d++)
+				if(seq[len - d - 1] > 3) { skip = true; break; }
+			if(!skip) {
+				if(flen > 1 && flen <= nea) {
+					// ftabSeqToInt(seq, len-flen, rev=!ebwtfw) (bt2_idx.h:1383-1390)
+					uint32_t fi = 0, fip = 0;
+					for(uint32_t i = 0; i < flen; i++) {
+						fi = (fi << 2) | (uint32_t)seq[len - flen + i];
+						fip = (fip << 2) | (uint32_t)seq[len - 1 - i];
+					}
+					top = ftab_hi(E, fi); bot = ftab_lo(E, fi + 1);
+					topp = ftab_hi(Ep, fip); botp = ftab_lo(Ep, fip + 1);
+					if(bot - top == 0) skip = true;
+					else dep = flen;
+				} else {
+					const int c = seq[len - 1];
+					top = topp = fchr_at(E, c);
+					bot = botp = fchr_at(E, c + 1);
+					if(bot - top == 0) skip = true;
+					else dep = 1;
+				}
+			}
+			st = skip ? ST_DONE : (dep < nea ? ST_NEAR : ST_FAR);
+		}
+		const uint64_t busy = __ballot(st != ST_IDLE);
+		if(busy == 0 && exhausted) break;
+		if(st == ST_FAR && dep >= len) st = ST_DONE;   // far half empty (len <= flen / 1): no step
+		if(st == ST_FAR) {
+			rdc = seq[len - dep - 1];
+			quc = qd[qrev ? dep : len - dep - 1];
+			if(rdc > 3 && nceil == 0) st = ST_DONE;
+			else if(bot - top <= 1 && top == (ebwtfw ? F.zoff : B.zoff)) st = ST_DONE;   // mapLF1 hit '$'
+		}
+		if(!(st == ST_NEAR || st == ST_FAR || st == ST_BR)) continue;
+
+		// ---- one LF operation (bt2_idx.h mapBiLFEx / mapLF1)
+		const DevEbwt E = pick_ebwt(ebwtfw, F, B);
+		const bool br = st == ST_BR;
+		const uint32_t qT = br ? topm : top, qB = br ? botm : bot, qP = br ? topmp : topp;
+		uint32_t ot[4], ob[4], otp[4], obp[4];
+		ops++;
+		const bool multi = qB - qT > 1;
+		int rowl = 0;
+		uint32_t lf1 = 0;
+		if(multi) {
+#pragma unroll
+			for(int i = 0; i < 4; i++) ot[i] = ob[i] = 0;
+			otp[0] = qP;
+			loads += bi_step(E, qT, qB, qP, ot, ob, otp, obp);
+		} else {
+			SideData s1;
+			load_side(E, qT / 192u, s1);
+			loads++;
+			rowl = side_rowL(s1, qT % 192u);
+			lf1 = occ1(E, s1, qT, rowl);
+		}
+
+		if(st == ST_NEAR) {
+			const int c = seq[len - dep - 1];
+			if(multi) {
+				top = at4(ot, c); bot = at4(ob, c);
+				if(bot <= top) { st = ST_DONE; continue; }
+				topp = at4(otp, c); botp = at4(obp, c);
+			} else {
+				if(rowl != c || qT == E.zoff) { st = ST_DONE; continue; }
+				top = lf1;
+				bot = top + 1;
+			}
+			dep++;
+			if(dep >= nea) st = ST_FAR;
+		} else if(st == ST_FAR) {
+#pragma unroll
+			for(int i = 0; i < 4; i++) { tp[i] = topp; bp[i] = botp; }
+			clo = 0; chi = 3; match = true;
+			if(multi) {
+#pragma unroll
+				for(int i = 0; i < 4; i++) { t[i] = ot[i]; b[i] = ob[i]; tp[i] = otp[i]; bp[i] = obp[i]; }
+				match = rdc < 4;
+				if(rdc < 4) { top = at4(t, rdc); bot = at4(b, rdc); topp = at4(tp, rdc); botp = at4(bp, rdc); }
+			} else {
+				clo = rowl;
+				top = lf1;
+				match = clo == rdc;
+				bot = top + 1;
+				set4(t, clo, top);
+				set4(b, clo, bot);
+				set4(bp, clo, botp);
+				set4(tp, clo, topp);
+				chi = clo;
+			}
+			j = clo;
+			st = ST_ALT;
+		} else {   // ST_BR
+			const int c = seq[len - depm - 1];
+			bool dead;
+			if(multi) {
+				topm = at4(ot, c); botm = at4(ob, c); topmp = at4(otp, c); botmp = at4(obp, c);
+				dead = botm <= topm;
+			} else {
+				dead = rowl != c || qT == E.zoff;
+				if(!dead) { topm = lf1; botm = topm + 1; }
+			}
+			if(dead) { j++; st = ST_ALT; continue; }
+			depm++;
+			if(depm == len) {
+				uint32_t off5p = dep;
+				if(fw == ebwtfw) off5p = len - off5p - 1;
+				int64_t score = (int64_t)(len - 1) * matchsc;
+				const int pen = rdc > 3 ? -P.npen : -mmpen_q(P, quc - 33);
+				score += pen;
+				bool valid = true;
+				if(P.local) {
+					int64_t lf = 0, lb = 0;
+					for(uint32_t i = 0; i < len; i++) {
+						if(i == dep) { if(lf + pen <= 0) { valid = false; break; } lf += pen; }
+						else lf += matchsc;
+						if(len - i - 1 == dep) { if(lb + pen <= 0) { valid = false; break; } lb += pen; }
+						else lb += matchsc;
+					}
+				}
+				if(valid && score >= minsc) {
+					if((uint32_t)nh < cap)
+						slots[(size_t)slot * cap + nh] = bt2g_mm1{ebwtfw ? topm : topmp, ebwtfw ? botm : botmp,
+						                                          fw ? 1 : 0, (int32_t)score, (int32_t)off5p, j, rdc,
+						                                          0};
+					nh++;
+				}
+				j++;
+				st = ST_ALT;
+			}
+		}
+	}
+}
+
+void launch_one_mm_q(const DevEbwt& F, const DevEbwt& B, const uint8_t* reads, const uint8_t* quals, uint32_t stride,
+                     const uint32_t* lens, uint32_t n, const int32_t* minsc, const bt2g_scoring& sc, int nofw,
+                     int norc, const uint32_t* gate, uint32_t cap, uint32_t* items, uint32_t* counters,
+                     bt2g_mm1* slots, int32_t* slot_counts, uint32_t* ops, uint32_t* loads, hipStream_t st) {
+	MmParams P{sc.match, sc.mmp_max, sc.mmp_min, sc.npen, sc.local, 0, 0};
+	// counters[0] = number of items, counters[1] = queue head (zeroed by the caller)
+	hipLaunchKernelGGL(k_one_mm_items, dim3((n + 255) / 256), dim3(256), 0, st, reads, stride, lens, n, gate, nofw,
+	                   norc, items, counters, slot_counts);
+	hipLaunchKernelGGL(k_one_mm_q, dim3(2048), dim3(256), 0, st, F, B, reads, quals, stride, lens, minsc, P,
+	                   sc.ncl_const, sc.ncl_lin, items, counters, counters + 1, cap, slots, slot_counts, ops, loads);
+}
