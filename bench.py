@@ -364,6 +364,7 @@ def main():
     ap.add_argument("--cpu-sample", type=int, default=20000)
     ap.add_argument("--cpu-threads", type=int, default=16)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--index-cache", default="", help="reuse/write the built index at this base path")
     args = ap.parse_args()
 
     import torch
@@ -383,7 +384,13 @@ def main():
     parts, names = make_genome(args.genome_mb)
     log(f"[rank {rank}] genome {sum(len(p) for p in parts)/1e6:.0f} Mbp in {time.time()-t0:.1f}s")
     t1 = time.time()
-    idx = bi.build_index_device(parts, names=names, device=str(dev))
+    cache = args.index_cache
+    if cache and os.path.exists(cache + ".rev.2.bt2"):
+        idx = bi.read_index(cache)                  # same seed -> same genome -> same index
+    else:
+        idx = bi.build_index_device(parts, names=names, device=str(dev))
+        if cache:
+            bi.write_index(cache, idx)
     torch.cuda.synchronize()
     log(f"[rank {rank}] index built on GPU in {time.time()-t1:.1f}s")
     torch.cuda.empty_cache()
@@ -485,6 +492,9 @@ def main():
                          "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS, "traffic": None,
                          "bytes_per_launch": bytes_k[dom], "ms_per_launch": per_launch[dom]},
             "kernels_ms": {names_k[k]: per_launch[k] for k in per_launch},
+            "kernels_gbs": {names_k[k]: bytes_k[k] / (per_launch[k] / 1e3) / 1e9 for k in per_launch
+                            if bytes_k.get(k)},
+            "side_loads_per_step": {names_k[k]: (bytes_k[k] // 64) for k in (0, 1, 2, 3) if bytes_k.get(k)},
             "sw_gcups": sw_gcups,
             "cpu_baseline": cpu,
             "parity_sample": parity,

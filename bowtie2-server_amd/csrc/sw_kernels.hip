@@ -30,20 +30,20 @@ constexpr int R = 16;           // rows per strip held in registers
 
 template <int V> struct Dom;
 template <> struct Dom<0> {   // EE u8
-	static constexpr int LO = 0, ROW0 = 255, HI = 255;
+	static constexpr int LO = 0, ROW0 = 255;
 	static __device__ __forceinline__ int sub(int a, int b) { int r = a - b; return r < 0 ? 0 : r; }
 	static __device__ __forceinline__ int diag(int h, int s, int) { return sub(h, -s); }
 	static constexpr int W = 16;
 };
 template <> struct Dom<1> {   // EE i16
-	static constexpr int LO = -32768, ROW0 = 32767, HI = 32767;
+	static constexpr int LO = -32768, ROW0 = 32767;
 	static __device__ __forceinline__ int sat(int x) { return x < -32768 ? -32768 : (x > 32767 ? 32767 : x); }
 	static __device__ __forceinline__ int sub(int a, int b) { return sat(a - b); }
 	static __device__ __forceinline__ int diag(int h, int s, int) { return sat(h + s); }
 	static constexpr int W = 8;
 };
 template <> struct Dom<2> {   // local u8
-	static constexpr int LO = 0, ROW0 = 0, HI = 255;
+	static constexpr int LO = 0, ROW0 = 0;
 	static __device__ __forceinline__ int sub(int a, int b) { int r = a - b; return r < 0 ? 0 : r; }
 	static __device__ __forceinline__ int diag(int h, int s, int bias) {
 		int t = h + s + bias; t = t > 255 ? 255 : t;
@@ -52,7 +52,7 @@ template <> struct Dom<2> {   // local u8
 	static constexpr int W = 16;
 };
 template <> struct Dom<3> {   // local i16
-	static constexpr int LO = -32768, ROW0 = -32768, HI = 32767;
+	static constexpr int LO = -32768, ROW0 = -32768;
 	static __device__ __forceinline__ int sat(int x) { return x < -32768 ? -32768 : (x > 32767 ? 32767 : x); }
 	static __device__ __forceinline__ int sub(int a, int b) { return sat(a - b); }
 	static __device__ __forceinline__ int diag(int h, int s, int) { return sat(h + s); }
