@@ -397,7 +397,7 @@ namespace {
 struct OneMmScratch {
 	bt2g_mm1* slots = nullptr;
 	int32_t* slot_counts = nullptr;
-	int32_t* ovf = nullptr;        // ovf[0] overflow flag, ovf[1..2] item count / queue head
+	int32_t* ovf = nullptr;        // ovf[0] overflow flag, ovf[1..4] item counts / queue heads
 	uint32_t* items = nullptr;
 };
 }  // namespace
@@ -414,9 +414,9 @@ static int one_mm_impl(bt2g_ctx* c, const uint8_t* reads, const uint8_t* quals, 
 	OneMmScratch s;
 	HIPCHK(hipMallocAsync((void**)&s.slots, sizeof(bt2g_mm1) * (size_t)n * 4 * cap, st));
 	HIPCHK(hipMallocAsync((void**)&s.slot_counts, sizeof(int32_t) * (size_t)n * 4, st));
-	HIPCHK(hipMallocAsync((void**)&s.ovf, sizeof(int32_t) * 4, st));
+	HIPCHK(hipMallocAsync((void**)&s.ovf, sizeof(int32_t) * 8, st));
 	HIPCHK(hipMallocAsync((void**)&s.items, sizeof(uint32_t) * (size_t)n * 4, st));
-	HIPCHK(hipMemsetAsync(s.ovf, 0, sizeof(int32_t) * 4, st));
+	HIPCHK(hipMemsetAsync(s.ovf, 0, sizeof(int32_t) * 8, st));
 	HIPCHK(hipMemsetAsync(bwops, 0, sizeof(uint32_t) * n, st));
 	if(loads) HIPCHK(hipMemsetAsync(loads, 0, sizeof(uint32_t) * n, st));
 	{

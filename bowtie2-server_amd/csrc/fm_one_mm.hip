@@ -1,19 +1,26 @@
 // fm_one_mm.hip -- SeedAligner::oneMmSearch (aligner_seed.cpp:973-1323) with
-// rep1mm=true, repex=false, as a persistent work-queue kernel.
+// rep1mm=true, repex=false.
 //
 // A work item is one (read, strand, index direction) the reference would run
 // (k_one_mm_items applies the exact-sweep gate of bt2_search.cpp:3640-3667 and
-// the "at most one N" rule).  Each lane runs a small state machine over its
-// item -- near half exact, far half with one mismatch, one branch walk per
-// alternative base -- and performs exactly one LF operation (one or two 64-B
-// side gathers) per loop iteration.  When its item ends the lane takes the next
-// one from a global queue (one atomic per wave), so the wave never idles on
-// finished lanes: the dependent-gather chains stay dense, which is what this
-// latency-bound walk needs.  Hits go to per-item slots in discovery order;
+// the "at most one N" rule and splits the items by index direction, so each
+// launch walks one index with wave-uniform parameters).  Each lane runs a
+// small state machine over its item -- near half exact, far half with one
+// mismatch, one branch walk per alternative base -- performing exactly one LF
+// operation (one or two 64-B side gathers) per loop iteration, so lanes in
+// different phases still issue their gathers together.  Hits go to per-item
+// slots in discovery order;
 // k_one_mm_compact concatenates the four slots of a read in the reference's
 // loop order (fw/BWT, fw/BWT', rc/BWT, rc/BWT').
 #include "fm_device.h"
 #include "bt2g_kernels.h"
+
+#ifdef BT2G_MM_DEBUG
+__device__ unsigned long long g_mm_dbg[4];
+extern "C" int bt2g_mm_debug_read(unsigned long long* out) {
+	return (int)hipMemcpyFromSymbol(out, HIP_SYMBOL(g_mm_dbg), sizeof(g_mm_dbg));
+}
+#endif
 
 namespace {
 
@@ -36,7 +43,8 @@ __device__ __forceinline__ void set4(uint32_t a[4], int i, uint32_t v) {
 
 }  // namespace
 
-// Work list: item = read << 3 | fwi << 2 | ebwtfwi << 1 | (read has an N).
+// Work lists: item = read << 3 | fwi << 2 | ebwtfwi << 1 | (read has an N);
+// items[0..2n) for the BWT, items[2n..4n) for BWT'; nitems[0], nitems[2] their lengths.
 __global__ void __launch_bounds__(256)
 k_one_mm_items(const uint8_t* __restrict__ reads, uint32_t stride, const uint32_t* __restrict__ lens, uint32_t n,
                const uint32_t* __restrict__ gate, int nofw, int norc, uint32_t* __restrict__ items,
@@ -66,32 +74,42 @@ k_one_mm_items(const uint8_t* __restrict__ reads, uint32_t stride, const uint32_
 		}
 	}
 	const uint64_t below = (1ull << lane) - 1ull;
+	// two lists by index direction (BWT: d even, BWT': d odd) so that each
+	// search launch reads one index with wave-uniform parameters
 	for(int d = 0; d < 4; d++) {
 		const bool want = (runmask >> d) & 1u;
 		const uint64_t m = __ballot(want);
+		const uint32_t li = d & 1;
 		uint32_t base = 0;
-		if(lane == 0 && m) base = atomicAdd(nitems, (uint32_t)__popcll(m));
+		if(lane == 0 && m) base = atomicAdd(&nitems[2 * li], (uint32_t)__popcll(m));
 		base = __shfl(base, 0);
-		if(want) items[base + (uint32_t)__popcll(m & below)] = (r << 3) | ((uint32_t)d << 1) | (ns ? 1u : 0u);
+		if(want)
+			items[(size_t)li * 2 * n + base + (uint32_t)__popcll(m & below)] =
+			    (r << 3) | ((uint32_t)d << 1) | (ns ? 1u : 0u);
 	}
 }
 
-__global__ void __launch_bounds__(256)
+#ifndef BT2G_MM_WAVES
+#define BT2G_MM_WAVES 3
+#endif
+template <bool EBWTFW>
+__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(BT2G_MM_WAVES)))
 k_one_mm_q(DevEbwt F, DevEbwt B, const uint8_t* __restrict__ reads, const uint8_t* __restrict__ quals,
            uint32_t stride, const uint32_t* __restrict__ lens, const int32_t* __restrict__ minscs, MmParams P,
            double ncl_const, double ncl_lin, const uint32_t* __restrict__ items,
-           const uint32_t* __restrict__ nitems_p, uint32_t* __restrict__ head, uint32_t cap,
+           const uint32_t* __restrict__ nitems_p, uint32_t cap,
            bt2g_mm1* __restrict__ slots, int32_t* __restrict__ slot_counts, uint32_t* __restrict__ ops_out,
            uint32_t* __restrict__ loads_out) {
-	const uint32_t lane = threadIdx.x & 63u;
 	const uint32_t nitems = *nitems_p;
 	const int64_t matchsc = (int64_t)((float)P.match + 0.5f);
-	const uint64_t below = (1ull << lane) - 1ull;
 
 	// per-lane item state
 	int st = ST_IDLE;
 	uint32_t r = 0, len = 0, slot = 0, dep = 0, nea = 0, depm = 0;
-	bool fw = true, ebwtfw = true, hasn = false;
+	constexpr bool ebwtfw = EBWTFW;
+	const DevEbwt& E = EBWTFW ? F : B;          // the index walked (uniform)
+	const DevEbwt& Ep = EBWTFW ? B : F;         // its mirror (ftab only)
+	bool fw = true, hasn = false;
 	int nceil = 0;
 	int64_t minsc = 0;
 	const uint8_t* rd = reads;
@@ -99,14 +117,21 @@ k_one_mm_q(DevEbwt F, DevEbwt B, const uint8_t* __restrict__ reads, const uint8_
 	SeqView seq{reads, 0, false, false};
 	bool qrev = false;
 	uint32_t top = 0, bot = 0, topp = 0, botp = 0;            // main range (+ mirror)
-	uint32_t t[4], b[4], tp[4], bp[4];                        // far step's four ranges
+	// the far step's four ranges (+ mirrors) live in LDS: read only when
+	// alternatives are enumerated, they would otherwise pin 16 registers
+	__shared__ uint32_t alt_s[16][256];
+	const uint32_t tid = threadIdx.x;
+#define T_(i) alt_s[(i)][tid]
+#define B_(i) alt_s[4 + (i)][tid]
+#define TP_(i) alt_s[8 + (i)][tid]
+#define BP_(i) alt_s[12 + (i)][tid]
 	int rdc = 0, quc = 0, clo = 0, chi = 3, j = 0;
 	bool match = true;
 	uint32_t topm = 0, botm = 0, topmp = 0, botmp = 0;        // branch range (+ mirror)
 	int32_t nh = 0;
 	uint32_t ops = 0, loads = 0;
 #pragma unroll
-	for(int i = 0; i < 4; i++) t[i] = b[i] = tp[i] = bp[i] = 0;
+	for(int i = 0; i < 16; i++) alt_s[i][tid] = 0;
 	bool exhausted = false;
 
 	for(;;) {
@@ -117,9 +142,9 @@ k_one_mm_q(DevEbwt F, DevEbwt B, const uint8_t* __restrict__ reads, const uint8_
 				bool started = false;
 				if(!hasn || rdc > 3) {
 					for(; j <= chi; j++) {
-						if(j == rdc || at4(b, j) == at4(t, j)) continue;
+						if(j == rdc || B_(j) == T_(j)) continue;
 						depm = dep + 1;
-						topm = at4(t, j); botm = at4(b, j); topmp = at4(tp, j); botmp = at4(bp, j);
+						topm = T_(j); botm = B_(j); topmp = TP_(j); botmp = BP_(j);
 						if(depm < len) { started = true; break; }
 						// branch complete at the last base: report (no further LF step)
 						uint32_t off5p = dep;
@@ -161,16 +186,11 @@ k_one_mm_q(DevEbwt F, DevEbwt B, const uint8_t* __restrict__ reads, const uint8_
 				if(ops && loads_out) atomicAdd(&loads_out[r], loads);
 				st = ST_IDLE;
 			}
-			// refill idle lanes from the queue (one atomic per wave)
-			const bool idle = st == ST_IDLE;
-			const uint64_t m = __ballot(idle && !exhausted);
-			if(m == 0) break;
-			uint32_t base = 0;
-			if(lane == (uint32_t)__ffsll((long long)m) - 1u) base = atomicAdd(head, (uint32_t)__popcll(m));
-			base = __shfl(base, __ffsll((long long)m) - 1);
-			if(base + (uint32_t)__popcll(m) >= nitems) exhausted = true;
-			if(!idle) continue;
-			const uint32_t qi = base + (uint32_t)__popcll(m & below);
+			// one item per lane (a refilling work queue measured slower: at ~700k
+			// items there is no tail to fill, and the queue costs registers)
+			if(exhausted) break;
+			exhausted = true;
+			const uint32_t qi = blockIdx.x * blockDim.x + threadIdx.x;
 			if(qi >= nitems) continue;
 			// ---- item initialisation (aligner_seed.cpp:1003-1100)
 			const uint32_t item = items[qi];
@@ -178,7 +198,6 @@ k_one_mm_q(DevEbwt F, DevEbwt B, const uint8_t* __restrict__ reads, const uint8_
 			const uint32_t fwi = (item >> 2) & 1u, ebi = (item >> 1) & 1u;
 			hasn = item & 1u;
 			fw = fwi == 0;
-			ebwtfw = ebi == 0;
 			slot = r * 4 + fwi * 2 + ebi;
 			len = lens[r];
 			rd = reads + (size_t)r * stride;
@@ -193,8 +212,6 @@ k_one_mm_q(DevEbwt F, DevEbwt B, const uint8_t* __restrict__ reads, const uint8_
 			qrev = fw ? !ebwtfw : ebwtfw;
 			const uint32_t halfFw = len >> 1, halfBw = (len >> 1) + (len & 1);
 			nea = ebwtfw ? halfFw : halfBw;
-			const DevEbwt E = pick_ebwt(ebwtfw, F, B);
-			const DevEbwt Ep = pick_ebwt(ebwtfw, B, F);
 			const uint32_t flen = E.ftab_chars;
 			bool skip = len == 0;
 			for(uint32_t d = 0; d < nea; d++)
@@ -223,17 +240,27 @@ k_one_mm_q(DevEbwt F, DevEbwt B, const uint8_t* __restrict__ reads, const uint8_
 		}
 		const uint64_t busy = __ballot(st != ST_IDLE);
 		if(busy == 0 && exhausted) break;
+#ifdef BT2G_MM_DEBUG
+		{
+			extern __device__ unsigned long long g_mm_dbg[4];
+			const uint64_t lf = __ballot(st == ST_NEAR || st == ST_FAR || st == ST_BR);
+			if((threadIdx.x & 63u) == 0) {
+				atomicAdd(&g_mm_dbg[0], 1ull);
+				atomicAdd(&g_mm_dbg[1], (unsigned long long)__popcll(lf));
+				atomicAdd(&g_mm_dbg[2], (unsigned long long)__popcll(busy));
+			}
+		}
+#endif
 		if(st == ST_FAR && dep >= len) st = ST_DONE;   // far half empty (len <= flen / 1): no step
 		if(st == ST_FAR) {
 			rdc = seq[len - dep - 1];
 			quc = qd[qrev ? dep : len - dep - 1];
 			if(rdc > 3 && nceil == 0) st = ST_DONE;
-			else if(bot - top <= 1 && top == (ebwtfw ? F.zoff : B.zoff)) st = ST_DONE;   // mapLF1 hit '$'
+			else if(bot - top <= 1 && top == E.zoff) st = ST_DONE;   // mapLF1 hit '$'
 		}
 		if(!(st == ST_NEAR || st == ST_FAR || st == ST_BR)) continue;
 
 		// ---- one LF operation (bt2_idx.h mapBiLFEx / mapLF1)
-		const DevEbwt E = pick_ebwt(ebwtfw, F, B);
 		const bool br = st == ST_BR;
 		const uint32_t qT = br ? topm : top, qB = br ? botm : bot, qP = br ? topmp : topp;
 		uint32_t ot[4], ob[4], otp[4], obp[4];
@@ -268,23 +295,22 @@ k_one_mm_q(DevEbwt F, DevEbwt B, const uint8_t* __restrict__ reads, const uint8_
 			dep++;
 			if(dep >= nea) st = ST_FAR;
 		} else if(st == ST_FAR) {
-#pragma unroll
-			for(int i = 0; i < 4; i++) { tp[i] = topp; bp[i] = botp; }
 			clo = 0; chi = 3; match = true;
 			if(multi) {
 #pragma unroll
-				for(int i = 0; i < 4; i++) { t[i] = ot[i]; b[i] = ob[i]; tp[i] = otp[i]; bp[i] = obp[i]; }
+				for(int i = 0; i < 4; i++) { T_(i) = ot[i]; B_(i) = ob[i]; TP_(i) = otp[i]; BP_(i) = obp[i]; }
 				match = rdc < 4;
-				if(rdc < 4) { top = at4(t, rdc); bot = at4(b, rdc); topp = at4(tp, rdc); botp = at4(bp, rdc); }
+				if(rdc < 4) { top = at4(ot, rdc); bot = at4(ob, rdc); topp = at4(otp, rdc); botp = at4(obp, rdc); }
 			} else {
+				// only alternative clo is visited (clo..chi with chi = clo)
 				clo = rowl;
 				top = lf1;
 				match = clo == rdc;
 				bot = top + 1;
-				set4(t, clo, top);
-				set4(b, clo, bot);
-				set4(bp, clo, botp);
-				set4(tp, clo, topp);
+				T_(clo) = top;
+				B_(clo) = bot;
+				BP_(clo) = botp;
+				TP_(clo) = topp;
 				chi = clo;
 			}
 			j = clo;
@@ -336,9 +362,13 @@ void launch_one_mm_q(const DevEbwt& F, const DevEbwt& B, const uint8_t* reads, c
                      int norc, const uint32_t* gate, uint32_t cap, uint32_t* items, uint32_t* counters,
                      bt2g_mm1* slots, int32_t* slot_counts, uint32_t* ops, uint32_t* loads, hipStream_t st) {
 	MmParams P{sc.match, sc.mmp_max, sc.mmp_min, sc.npen, sc.local, 0, 0};
-	// counters[0] = number of items, counters[1] = queue head (zeroed by the caller)
+	// counters[0]/[2] = item counts of the BWT / BWT' lists (zeroed by the caller)
 	hipLaunchKernelGGL(k_one_mm_items, dim3((n + 255) / 256), dim3(256), 0, st, reads, stride, lens, n, gate, nofw,
 	                   norc, items, counters, slot_counts);
-	hipLaunchKernelGGL(k_one_mm_q, dim3(2048), dim3(256), 0, st, F, B, reads, quals, stride, lens, minsc, P,
-	                   sc.ncl_const, sc.ncl_lin, items, counters, counters + 1, cap, slots, slot_counts, ops, loads);
+	const uint32_t grid = (2 * n + 255) / 256;   // list capacity; lanes past the count exit
+	hipLaunchKernelGGL(k_one_mm_q<true>, dim3(grid), dim3(256), 0, st, F, B, reads, quals, stride, lens, minsc, P,
+	                   sc.ncl_const, sc.ncl_lin, items, counters, cap, slots, slot_counts, ops, loads);
+	hipLaunchKernelGGL(k_one_mm_q<false>, dim3(grid), dim3(256), 0, st, F, B, reads, quals, stride, lens, minsc, P,
+	                   sc.ncl_const, sc.ncl_lin, items + 2 * (size_t)n, counters + 2, cap, slots,
+	                   slot_counts, ops, loads);
 }
