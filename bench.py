@@ -124,8 +124,21 @@ class Pipeline:
         self.fr_toff = torch.tensor(rs[:, 2], device=self.dev)
         fr_end = np.concatenate([rs[1:, 0], [idx.fw.length]])
         self.fr_end = torch.tensor(fr_end, device=self.dev)
+        self.fr = [torch.tensor(a.astype(np.uint32), device=self.dev)
+                   for a in (rs[:, 0], rs[:, 1], rs[:, 2], fr_end)]      # joff, tid, toff, end
+        self.nfrag = int(rs.shape[0])
+        self.inv = torch.empty(n, dtype=torch.int32, device=self.dev)
+        self.row_cap = n * (1 + self.mm_cap + 2 * self.maxseeds)
+        self.rows = torch.empty(self.row_cap, dtype=torch.int32, device=self.dev)
+        self.meta = torch.empty(self.row_cap, dtype=torch.int32, device=self.dev)
+        self.offs = torch.empty(self.row_cap, dtype=torch.int32, device=self.dev)
+        self.loads_off = torch.empty(self.row_cap, dtype=torch.int32, device=self.dev)
+        self.read_base = torch.empty(n, dtype=torch.int32, device=self.dev)
+        self.read_cnt = torch.empty(n, dtype=torch.int32, device=self.dev)
+        self.counters = torch.zeros(2, dtype=torch.int32, device=self.dev)   # rows, problems
         self.ncol = length + 4 * MAXGAP
         self.max_probs = 2 * n
+        self.probs = torch.zeros((self.max_probs, 5), dtype=torch.int64, device=self.dev)
         _chk = bt2g._chk
         _chk(self.L.bt2g_reserve_sw(eng.h, self.max_probs, self.ncol))
         self.sw_cap = 256
@@ -159,72 +172,36 @@ class Pipeline:
         chk(L.bt2g_seed_search_dev(h, self._p(sreads), stride, self._p(self.lens), m, SEEDLEN, INTERVAL, 0,
                                    self.maxseeds, self._p(self.seeds), self._p(self.nseeds), self._p(self.sd_ops),
                                    self._p(self.sd_loads), S))
-        sd = self.seeds[:m].to(torch.int64) & u32                      # [m,2,S,4]
-        hit = sd[..., 1] > sd[..., 0]
-        ri, strand, si = torch.nonzero(hit, as_tuple=True)
-        rows_seed = sd[ri, strand, si, 0]
-        read_seed = sel[ri]
-        depth = si * INTERVAL
-        # exact / 1-mm hits: top rows too (an end-to-end hit spans the whole read)
-        ex_r = torch.nonzero(exact).squeeze(1)
-        ex_fw = sw[ex_r, 3] > sw[ex_r, 2]                                # fw range non-empty
-        ex_row = torch.where(ex_fw, sw[ex_r, 2], sw[ex_r, 4])
-        mmc = self.mm_cnt.clamp(max=self.mm_cap)
-        mr, mk = torch.nonzero(torch.arange(self.mm_cap, device=self.dev)[None, :] < mmc[:, None], as_tuple=True)
-        mm_row = self.mm_hits[mr, mk, 0].to(torch.int64) & u32
-        mm_fw = self.mm_hits[mr, mk, 2] != 0
-        rows = torch.cat([rows_seed, ex_row, mm_row]).to(torch.int32).contiguous()
-        nrows = int(rows.numel())
-        offs = torch.empty(nrows, dtype=torch.int32, device=self.dev)
-        loads_off = torch.empty(nrows, dtype=torch.int32, device=self.dev)
-        # 4. SA rows -> joined-text offsets
-        chk(L.bt2g_get_offset_dev(h, self._p(rows), nrows, self._p(offs), self._p(loads_off), S))
-        off = offs.to(torch.int64) & u32
-        # joinedToTextOff (bt2_idx.cpp:54): fragment -> (ref id, ref offset)
-        frag = torch.searchsorted(self.fr_joff, off, right=True) - 1
-        tidx = self.fr_tid[frag]
-        toff = self.fr_toff[frag] + (off - self.fr_joff[frag])
-        ns = int(rows_seed.numel())
-        ne = int(ex_row.numel())
-        hitlen = torch.cat([torch.full((ns,), SEEDLEN, device=self.dev, dtype=torch.int64),
-                            torch.full((ne + int(mm_row.numel()),), self.len, device=self.dev, dtype=torch.int64)])
-        straddle = off + hitlen > self.fr_end[frag]
-        # read start on the reference (seed at depth d of the read or of its rc)
-        is_fw = torch.cat([strand == 0, ex_fw, mm_fw])
-        rd_of = torch.cat([read_seed, ex_r, mr])
-        dep = torch.cat([depth, torch.zeros(ne + int(mm_row.numel()), dtype=torch.int64, device=self.dev)])
-        start = torch.where(is_fw, toff - dep, toff - (self.len - dep - hitlen))
-        # 5. one DP rectangle per distinct (read, strand, ref, diagonal); <= 2 per read
-        ok = ~straddle
-        rd_of, is_fw, tidx, start = rd_of[ok], is_fw[ok], tidx[ok], start[ok]
-        key = torch.stack([rd_of, is_fw.to(torch.int64), tidx, start], 1)
-        uk = torch.unique(key, dim=0)                                    # sorted lexicographically
-        first = torch.ones(uk.shape[0], dtype=torch.bool, device=self.dev)
-        first[1:] = uk[1:, 0] != uk[:-1, 0]
-        grp = torch.cumsum(first.to(torch.int64), 0) - 1
-        gstart = torch.nonzero(first).squeeze(1)
-        rank = torch.arange(uk.shape[0], device=self.dev) - gstart[grp]
-        uk = uk[rank < 2]
-        npb = min(int(uk.shape[0]), self.max_probs)
-        uk = uk[:npb]
-        probs = torch.zeros((npb, 5), dtype=torch.int64, device=self.dev)   # 40-byte bt2g_sw_problem
-        pw = probs.view(torch.int32)
-        pw[:, 0] = uk[:, 0].to(torch.int32)               # read
-        pw[:, 1] = uk[:, 1].to(torch.int32)               # fw
-        probs[:, 1] = uk[:, 3] - 2 * MAXGAP               # refl (dp_framer.cpp:95-100)
-        probs[:, 2] = -1                                  # win_off: resident reference
-        pw[:, 6] = uk[:, 2].to(torch.int32)               # refidx
-        pw[:, 7] = self.ncol                              # ncol
-        pw[:, 8] = int(-0.6 - 0.6 * self.len)             # minsc
-        chk(L.bt2g_sw_align_dev(h, self._p(self.reads), self._p(self.quals), stride, self._p(self.lens),
-                                self._p(probs), npb, None, C.byref(self.sc), 1, self.sw_cap, self._p(self.res),
-                                self._p(self.cands), None, None, S))
+        # 4. every read's hit rows (exact, 1-mm, seeds) -> one list, contiguous per read
+        self.inv.fill_(-1)
+        self.inv[sel] = torch.arange(m, dtype=torch.int32, device=self.dev)
+        self.counters.zero_()
+        P = self._p
+        chk(L.bt2g_bench_collect_rows_dev(n, P(self.lens), P(self.sweep), P(self.mm_hits), P(self.mm_cnt),
+                                          self.mm_cap, P(self.seeds), P(self.inv), self.maxseeds, SEEDLEN, INTERVAL,
+                                          P(self.rows), P(self.meta), P(self.read_base), P(self.read_cnt),
+                                          P(self.counters), self.row_cap, S))
+        nrows = int(self.counters[0])
+        # 5. SA rows -> joined-text offsets
+        chk(L.bt2g_get_offset_dev(h, P(self.rows), nrows, P(self.offs), P(self.loads_off), S))
+        # 6. joinedToTextOff + straddle filter + rectangles, <= 2 per read (device)
+        chk(L.bt2g_bench_frame_dev(n, P(self.lens), P(self.offs), P(self.meta), P(self.read_base),
+                                   P(self.read_cnt), P(self.fr[0]), P(self.fr[1]), P(self.fr[2]), P(self.fr[3]),
+                                   self.nfrag, MAXGAP, int(-0.6 - 0.6 * self.len), P(self.probs),
+                                   P(self.counters[1:]), self.max_probs, S))
+        npb = min(int(self.counters[1]), self.max_probs)
+        probs = self.probs[:npb]
+        chk(L.bt2g_sw_align_dev(h, P(self.reads), P(self.quals), stride, P(self.lens),
+                                P(probs), npb, None, C.byref(self.sc), 1, self.sw_cap, P(self.res),
+                                P(self.cands), None, None, S))
         aligned = exact.clone()
         al = self.res[:npb, 0] == 1
-        aligned[uk[al, 0]] = True
+        aligned[probs.view(torch.int32)[:, 0][al].to(torch.int64)] = True
+        ns = 0
         if keep:
-            self.last = dict(sel=sel, rows=rows, offs=off, probs=probs, npb=npb, nrows=nrows, m=m, ns=ns,
-                             loads_off=loads_off)
+            self.last = dict(sel=sel, rows=self.rows[:nrows], offs=self.offs[:nrows], probs=probs, npb=npb,
+                             nrows=nrows, m=m, ns=ns, loads_off=self.loads_off[:nrows],
+                             read_base=self.read_base, read_cnt=self.read_cnt)
         return aligned
 
 
@@ -291,12 +268,13 @@ def cpu_baseline(idx, reads, quals, pipe, sample, threads):
         rf_off.append(rf_off[-1] + ncol + 1)
     rf = np.concatenate(rf_all) if rf_all else np.zeros(1, np.uint8)
     rf_off = np.array(rf_off, np.int64)
-    rows_seed = last["rows"].cpu().numpy().astype(np.uint32)
-    # rows of sampled reads only: seed rows are ordered by selected-read index
-    sd = (pipe.seeds[:m].cpu().numpy().astype(np.int64) & 0xFFFFFFFF)
-    nsel = int(np.searchsorted(sel, n))
-    nrow_sample = int((sd[:nsel, :, :, 1] > sd[:nsel, :, :, 0]).sum())
-    rows = rows_seed[:nrow_sample]
+    # the GPU's hit rows of the sampled reads (contiguous per read)
+    rows_all = last["rows"].cpu().numpy().astype(np.uint32)
+    rb = last["read_base"][:n].cpu().numpy().astype(np.int64)
+    rc = last["read_cnt"][:n].cpu().numpy().astype(np.int64)
+    tot = int(rc.sum())
+    within = np.arange(tot) - np.repeat(np.cumsum(rc) - rc, rc)
+    rows = rows_all[np.repeat(rb, rc) + within]
     sp = score_params(False)
     minsc = np.full(n, int(-0.6 - 0.6 * pipe.len), np.int64)
 
