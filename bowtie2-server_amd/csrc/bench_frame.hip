@@ -13,21 +13,9 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 #include "bt2g_kernels.h"
+#include "dev_util.h"
 
 namespace {
-
-// Exclusive prefix of v over the wave and the wave total (shuffles, no LDS).
-__device__ __forceinline__ uint32_t wave_excl_scan(uint32_t v, uint32_t& total) {
-	const uint32_t lane = threadIdx.x & 63u;
-	uint32_t x = v;
-#pragma unroll
-	for(int o = 1; o < 64; o <<= 1) {
-		const uint32_t y = (uint32_t)__shfl_up((int)x, o);
-		if(lane >= (uint32_t)o) x += y;
-	}
-	total = (uint32_t)__shfl((int)x, 63);
-	return x - v;
-}
 
 // meta of a hit row: fw << 31 | depth << 16 | hit length
 __device__ __forceinline__ uint32_t meta_of(bool fw, uint32_t dep, uint32_t hitlen) {
@@ -64,11 +52,7 @@ k_collect_rows(uint32_t n, const uint32_t* __restrict__ lens, const uint32_t* __
 			for(uint32_t k = 0; k < 2 * maxseeds; k++) cnt += sd[k * 4 + 1] > sd[k * 4] ? 1u : 0u;
 		}
 	}
-	uint32_t wtot;
-	const uint32_t pre = wave_excl_scan(cnt, wtot);
-	uint32_t base = 0;
-	if((threadIdx.x & 63u) == 0 && wtot) base = atomicAdd(total, wtot);
-	base = (uint32_t)__shfl((int)base, 0) + pre;
+	uint32_t base = block_alloc<256>(cnt, total);
 	if(!valid) return;
 	if(base + cnt > cap) cnt = base < cap ? cap - base : 0;   // overflow: truncated (caller checks total)
 	read_base[r] = base;
@@ -138,11 +122,7 @@ k_frame(uint32_t n, const uint32_t* __restrict__ lens, const uint32_t* __restric
 		}
 	}
 	const uint32_t np = (k1 != NONE ? 1u : 0u) + (k2 != NONE ? 1u : 0u);
-	uint32_t wtot;
-	const uint32_t pre = wave_excl_scan(np, wtot);
-	uint32_t base = 0;
-	if((threadIdx.x & 63u) == 0 && wtot) base = atomicAdd(nprob, wtot);
-	base = (uint32_t)__shfl((int)base, 0) + pre;
+	const uint32_t base = block_alloc<256>(np, nprob);
 	if(!valid) return;
 	for(uint32_t i = 0; i < np; i++) {
 		if(base + i >= cap) break;

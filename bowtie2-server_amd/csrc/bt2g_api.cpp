@@ -366,6 +366,7 @@ int bt2g_exact_sweep_dev(bt2g_ctx* c, const uint8_t* reads, uint32_t stride, con
 	if(int rc = check_reads(stride, n)) return rc;
 	if(n == 0) return BT2G_OK;
 	hipStream_t st = pick(c, stream);
+	HIPCHK(hipMemsetAsync(out, 0, sizeof(uint32_t) * 8 * (size_t)n, st));   // bwops / loads accumulate
 	{
 		ProfScope ps(c, 0, st);
 		launch_exact_sweep(c->fw, reads, stride, lens, n, mine_max, nofw, norc, out, st);
@@ -399,6 +400,8 @@ struct OneMmScratch {
 	int32_t* slot_counts = nullptr;
 	int32_t* ovf = nullptr;        // ovf[0] overflow flag, ovf[1..4] item counts / queue heads
 	uint32_t* items = nullptr;
+	uint4* near_state = nullptr;
+	uint32_t* near_dep = nullptr;
 };
 }  // namespace
 
@@ -416,13 +419,16 @@ static int one_mm_impl(bt2g_ctx* c, const uint8_t* reads, const uint8_t* quals, 
 	HIPCHK(hipMallocAsync((void**)&s.slot_counts, sizeof(int32_t) * (size_t)n * 4, st));
 	HIPCHK(hipMallocAsync((void**)&s.ovf, sizeof(int32_t) * 8, st));
 	HIPCHK(hipMallocAsync((void**)&s.items, sizeof(uint32_t) * (size_t)n * 4, st));
+	HIPCHK(hipMallocAsync((void**)&s.near_state, sizeof(uint4) * (size_t)n * 4, st));
+	HIPCHK(hipMallocAsync((void**)&s.near_dep, sizeof(uint32_t) * (size_t)n * 4, st));
 	HIPCHK(hipMemsetAsync(s.ovf, 0, sizeof(int32_t) * 8, st));
 	HIPCHK(hipMemsetAsync(bwops, 0, sizeof(uint32_t) * n, st));
 	if(loads) HIPCHK(hipMemsetAsync(loads, 0, sizeof(uint32_t) * n, st));
 	{
 		ProfScope ps(c, 2, st);
 		launch_one_mm(c->fw, c->bw, reads, quals, stride, lens, n, minsc, *sc, nofw, norc, gate, cap, s.items,
-		              (uint32_t*)s.ovf + 1, s.slots, s.slot_counts, hits, counts, bwops, loads, s.ovf, st);
+		              (uint32_t*)s.ovf + 1, s.near_state, s.near_dep, s.slots, s.slot_counts, hits, counts, bwops,
+		              loads, s.ovf, st);
 	}
 	HIPCHK(hipGetLastError());
 	int32_t ovf = 0;
@@ -431,6 +437,8 @@ static int one_mm_impl(bt2g_ctx* c, const uint8_t* reads, const uint8_t* quals, 
 	HIPCHK(hipFreeAsync(s.slot_counts, st));
 	HIPCHK(hipFreeAsync(s.ovf, st));
 	HIPCHK(hipFreeAsync(s.items, st));
+	HIPCHK(hipFreeAsync(s.near_state, st));
+	HIPCHK(hipFreeAsync(s.near_dep, st));
 	if(sync_overflow) {
 		HIPCHK(hipStreamSynchronize(st));
 		if(ovf) return fail(BT2G_ERR_OVERFLOW, "one-mismatch hits exceed cap %u", cap);

@@ -25,16 +25,17 @@ struct MmParams {
 	int32_t match, mmp_max, mmp_min, npen, local;
 	int32_t nceil_const_x1000, nceil_lin_x1000;
 };
-// items: n*4 u32 scratch; counters: 2 u32 zeroed by the caller (item count, queue head)
+// items: n*4 u32 scratch; counters: 4 u32 zeroed by the caller; near_state / near_dep: n*4 each
 void launch_one_mm_q(const DevEbwt& F, const DevEbwt& B, const uint8_t* reads, const uint8_t* quals, uint32_t stride,
                      const uint32_t* lens, uint32_t n, const int32_t* minsc, const bt2g_scoring& sc, int nofw,
                      int norc, const uint32_t* gate, uint32_t cap, uint32_t* items, uint32_t* counters,
-                     bt2g_mm1* slots, int32_t* slot_counts, uint32_t* ops, uint32_t* loads, hipStream_t st);
+                     uint4* near_state, uint32_t* near_dep, bt2g_mm1* slots, int32_t* slot_counts, uint32_t* ops,
+                     uint32_t* loads, hipStream_t st);
 void launch_one_mm(const DevEbwt& F, const DevEbwt& B, const uint8_t* reads, const uint8_t* quals, uint32_t stride,
                    const uint32_t* lens, uint32_t n, const int32_t* minsc, const bt2g_scoring& sc, int nofw,
                    int norc, const uint32_t* gate, uint32_t cap, uint32_t* items, uint32_t* counters,
-                   bt2g_mm1* slots, int32_t* slot_counts, bt2g_mm1* hits, int32_t* counts, uint32_t* ops,
-                   uint32_t* loads, int32_t* overflow, hipStream_t st);
+                   uint4* near_state, uint32_t* near_dep, bt2g_mm1* slots, int32_t* slot_counts, bt2g_mm1* hits,
+                   int32_t* counts, uint32_t* ops, uint32_t* loads, int32_t* overflow, hipStream_t st);
 void launch_get_offset(const DevEbwt& e, const uint32_t* rows, uint32_t n, uint32_t* offs, uint32_t* loads,
                        hipStream_t st);
 void launch_sw_partition(const bt2g_sw_problem* probs, uint32_t nprob, int local, int enable8, uint32_t* list8,

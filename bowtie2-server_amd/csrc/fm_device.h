@@ -180,6 +180,12 @@ __device__ __forceinline__ int bi_step(const DevEbwt& e, uint32_t top, uint32_t 
 	if(sb == st) {
 		occ4(e, s1, bot, b);
 	} else {
+#ifdef BT2G_LEAN_BISTEP
+		// second side only after the first is consumed: one SideData live
+		uint32_t z;
+		asm volatile("v_mov_b32 %0, 0" : "=v"(z) : "v"(t[0]), "v"(t[3]));
+		sb += z;
+#endif
 		SideData s2;
 		load_side(e, sb, s2);
 		occ4(e, s2, bot, b);

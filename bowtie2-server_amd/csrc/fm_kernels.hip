@@ -15,9 +15,10 @@
 __global__ void __launch_bounds__(256)
 k_exact_sweep(DevEbwt e, const uint8_t* __restrict__ reads, uint32_t stride, const uint32_t* __restrict__ lens,
               uint32_t n, uint32_t mine_max, int nofw, int norc, uint32_t* __restrict__ out) {
-	uint32_t gid = blockIdx.x * blockDim.x + threadIdx.x;
-	uint32_t r = gid >> 1, strand = gid & 1;
-	// lanes 2r and 2r+1 always share a wave; no early return before the shuffle
+	// lanes 2r, 2r+1: the two strands of read r (strand-homogeneous waves
+	// measured slower: half the reads of any wave come from either strand)
+	const uint32_t gid = blockIdx.x * blockDim.x + threadIdx.x;
+	const uint32_t r = gid >> 1, strand = gid & 1;
 	const bool valid = r < n;
 	const bool active = valid && !((strand == 0 && nofw) || (strand == 1 && norc));
 	const uint32_t len = active ? lens[r] : 0;
@@ -102,16 +103,13 @@ k_exact_sweep(DevEbwt e, const uint8_t* __restrict__ reads, uint32_t stride, con
 		mine = nedit;
 		if(nedit == 0 && bot > top) { otop = top; obot = bot; }
 	}
-	// bwops / loads of the read = sum of both strands (the pair shares a wave)
-	uint32_t ob = __shfl_xor(bwops, 1), ol = __shfl_xor(loads, 1);
 	if(!valid) return;
 	out[(size_t)r * 8 + strand] = mine;
 	out[(size_t)r * 8 + 2 + 2 * strand] = otop;
 	out[(size_t)r * 8 + 3 + 2 * strand] = obot;
-	if(strand == 0) {
-		out[(size_t)r * 8 + 6] = bwops + ob;
-		out[(size_t)r * 8 + 7] = loads + ol;
-	}
+	// bwops / side loads of the read = sum of both strands (words zeroed by the caller)
+	if(bwops) atomicAdd(&out[(size_t)r * 8 + 6], bwops);
+	if(loads) atomicAdd(&out[(size_t)r * 8 + 7], loads);
 }
 
 // --------------------------------------------------------------------------
@@ -258,7 +256,7 @@ k_get_offset(DevEbwt e, const uint32_t* __restrict__ rows, uint32_t n, uint32_t*
 // --------------------------------------------------------------------------
 void launch_exact_sweep(const DevEbwt& e, const uint8_t* reads, uint32_t stride, const uint32_t* lens, uint32_t n,
                         uint32_t mine_max, int nofw, int norc, uint32_t* out, hipStream_t st) {
-	uint32_t threads = n * 2;
+	const uint32_t threads = n * 2;
 	hipLaunchKernelGGL(k_exact_sweep, dim3((threads + 255) / 256), dim3(256), 0, st, e, reads, stride, lens, n,
 	                   mine_max, nofw, norc, out);
 }
@@ -275,10 +273,10 @@ void launch_seed_search(const DevEbwt& F, const DevEbwt& B, const uint8_t* reads
 void launch_one_mm(const DevEbwt& F, const DevEbwt& B, const uint8_t* reads, const uint8_t* quals, uint32_t stride,
                    const uint32_t* lens, uint32_t n, const int32_t* minsc, const bt2g_scoring& sc, int nofw,
                    int norc, const uint32_t* gate, uint32_t cap, uint32_t* items, uint32_t* counters,
-                   bt2g_mm1* slots, int32_t* slot_counts, bt2g_mm1* hits, int32_t* counts, uint32_t* ops,
-                   uint32_t* loads, int32_t* overflow, hipStream_t st) {
-	launch_one_mm_q(F, B, reads, quals, stride, lens, n, minsc, sc, nofw, norc, gate, cap, items, counters, slots,
-	                slot_counts, ops, loads, st);
+                   uint4* near_state, uint32_t* near_dep, bt2g_mm1* slots, int32_t* slot_counts, bt2g_mm1* hits,
+                   int32_t* counts, uint32_t* ops, uint32_t* loads, int32_t* overflow, hipStream_t st) {
+	launch_one_mm_q(F, B, reads, quals, stride, lens, n, minsc, sc, nofw, norc, gate, cap, items, counters,
+	                near_state, near_dep, slots, slot_counts, ops, loads, st);
 	hipLaunchKernelGGL(k_one_mm_compact, dim3((n + 255) / 256), dim3(256), 0, st, slots, slot_counts, n, cap, hits,
 	                   counts, overflow);
 }

@@ -14,13 +14,8 @@
 // loop order (fw/BWT, fw/BWT', rc/BWT, rc/BWT').
 #include "fm_device.h"
 #include "bt2g_kernels.h"
+#include "dev_util.h"
 
-#ifdef BT2G_MM_DEBUG
-__device__ unsigned long long g_mm_dbg[4];
-extern "C" int bt2g_mm_debug_read(unsigned long long* out) {
-	return (int)hipMemcpyFromSymbol(out, HIP_SYMBOL(g_mm_dbg), sizeof(g_mm_dbg));
-}
-#endif
 
 namespace {
 
@@ -30,7 +25,7 @@ __device__ __forceinline__ int mmpen_q(const MmParams& p, int q) {
 	return p.mmp_min + (int)(frac * (float)(p.mmp_max - p.mmp_min));
 }
 
-enum : int { ST_IDLE = 0, ST_NEAR, ST_FAR, ST_ALT, ST_BR, ST_DONE };
+enum : int { ST_IDLE = 0, ST_FAR, ST_ALT, ST_BR, ST_DONE };
 
 // register-array access by a data-dependent index without going through scratch
 __device__ __forceinline__ uint32_t at4(const uint32_t a[4], int i) {
@@ -49,13 +44,47 @@ __global__ void __launch_bounds__(256)
 k_one_mm_items(const uint8_t* __restrict__ reads, uint32_t stride, const uint32_t* __restrict__ lens, uint32_t n,
                const uint32_t* __restrict__ gate, int nofw, int norc, uint32_t* __restrict__ items,
                uint32_t* __restrict__ nitems, int32_t* __restrict__ slot_counts) {
+	// one wave of 64 reads: their rows are contiguous, so the Ns are counted
+	// from coalesced dword loads (N = code 4: bit 2 of a byte) into per-read
+	// LDS counters
+	__shared__ uint32_t ncount_s[256], lens_s[256];
 	const uint32_t r = blockIdx.x * blockDim.x + threadIdx.x;
 	const uint32_t lane = threadIdx.x & 63u;
+	const uint32_t r0 = blockIdx.x * blockDim.x + (threadIdx.x & ~63u);   // this wave's first read
+	const uint32_t nr = r0 >= n ? 0u : (n - r0 < 64u ? n - r0 : 64u);
+	uint32_t* ncount = ncount_s + (threadIdx.x & ~63u);
+	uint32_t* lenS = lens_s + (threadIdx.x & ~63u);
+	ncount[lane] = 0;
+	lenS[lane] = r < n ? lens[r] : 0u;
+	__syncthreads();
+	{
+		const uint8_t* src = reads + (size_t)r0 * stride;
+		const uint32_t bytes = nr * stride;
+		const uint32_t head = (uint32_t)((4u - ((uintptr_t)src & 3u)) & 3u);   // bytes before a dword boundary
+		// byte o of the wave's rows is an N of read o/stride iff inside its length
+		auto add_byte = [&](uint32_t o, uint32_t code) {
+			const uint32_t rr = o / stride;
+			if(code > 3 && o - rr * stride < lenS[rr]) atomicAdd(&ncount[rr], 1u);
+		};
+		if(lane < head && lane < bytes) add_byte(lane, src[lane]);
+		const uint32_t* src32 = reinterpret_cast<const uint32_t*>(src + head);
+		const uint32_t nw = bytes > head ? (bytes - head) / 4u : 0u;
+		for(uint32_t w = lane; w < nw; w += 64u) {
+			const uint32_t v = src32[w];
+			if(!(v & 0x04040404u)) continue;
+			const uint32_t o = head + 4u * w, rr = o / stride;
+			if(rr == (o + 3) / stride && o + 3 - rr * stride < lenS[rr]) {
+				atomicAdd(&ncount[rr], (uint32_t)__popc(v & 0x04040404u));
+			} else {
+				for(uint32_t k = 0; k < 4; k++) add_byte(o + k, (v >> (8 * k)) & 0xffu);
+			}
+		}
+		for(uint32_t o = head + 4u * nw + lane; o < bytes; o += 64u) add_byte(o, src[o]);
+	}
+	__syncthreads();
 	uint32_t runmask = 0, ns = 0;
 	if(r < n) {
-		const uint32_t len = lens[r];
-		const uint8_t* rd = reads + (size_t)r * stride;
-		for(uint32_t i = 0; i < len; i++) ns += rd[i] > 3;
+		ns = ncount[lane];
 		bool nofw_r = nofw, norc_r = norc, gated_off = false;
 		if(gate) {
 			// bt2_search.cpp:3476-3506, 3640-3667: skipped when an exact end-to-end hit
@@ -73,20 +102,86 @@ k_one_mm_items(const uint8_t* __restrict__ reads, uint32_t stride, const uint32_
 			slot_counts[(size_t)r * 4 + d] = 0;
 		}
 	}
-	const uint64_t below = (1ull << lane) - 1ull;
 	// two lists by index direction (BWT: d even, BWT': d odd) so that each
 	// search launch reads one index with wave-uniform parameters
-	for(int d = 0; d < 4; d++) {
-		const bool want = (runmask >> d) & 1u;
-		const uint64_t m = __ballot(want);
-		const uint32_t li = d & 1;
-		uint32_t base = 0;
-		if(lane == 0 && m) base = atomicAdd(&nitems[2 * li], (uint32_t)__popcll(m));
-		base = __shfl(base, 0);
-		if(want)
-			items[(size_t)li * 2 * n + base + (uint32_t)__popcll(m & below)] =
-			    (r << 3) | ((uint32_t)d << 1) | (ns ? 1u : 0u);
+	for(uint32_t li = 0; li < 2; li++) {
+		const uint32_t want = ((runmask >> li) & 1u) + ((runmask >> (li + 2)) & 1u);
+		uint32_t pos = block_alloc<256>(want, &nitems[2 * li]);
+		for(uint32_t d = li; d < 4; d += 2)
+			if((runmask >> d) & 1u) items[(size_t)li * 2 * n + pos++] = (r << 3) | (d << 1) | (ns ? 1u : 0u);
 	}
+}
+
+// Near half (aligner_seed.cpp:1003-1110): ftab jump and exact bidirectional
+// steps over the half of the read nearest the index's starting end.  One lane
+// per item, lean state (it is most of the LF work and runs at high occupancy);
+// the surviving range (+ mirror) and depth go to the far-half kernel.
+template <bool EBWTFW>
+__global__ void __launch_bounds__(256)
+k_one_mm_near(DevEbwt F, DevEbwt B, const uint8_t* __restrict__ reads, uint32_t stride,
+              const uint32_t* __restrict__ lens, const uint32_t* __restrict__ items,
+              const uint32_t* __restrict__ nitems_p, uint4* __restrict__ st4, uint32_t* __restrict__ sdep,
+              uint32_t* __restrict__ ops_out, uint32_t* __restrict__ loads_out) {
+	const uint32_t qi = blockIdx.x * blockDim.x + threadIdx.x;
+	if(qi >= *nitems_p) return;
+	const DevEbwt& E = EBWTFW ? F : B;
+	const DevEbwt& Ep = EBWTFW ? B : F;
+	const uint32_t item = items[qi];
+	const uint32_t r = item >> 3;
+	const bool fw = ((item >> 2) & 1u) == 0;
+	const uint32_t len = lens[r];
+	// seq = fw ? (ebwtfw ? patFw : patFwRev) : (ebwtfw ? patRc : patRcRev)
+	const SeqView seq{reads + (size_t)r * stride, len, fw ? !EBWTFW : EBWTFW, !fw};
+	const uint32_t nea = EBWTFW ? (len >> 1) : (len >> 1) + (len & 1);
+	const uint32_t flen = E.ftab_chars;
+	uint32_t top = 0, bot = 0, topp = 0, botp = 0, dep = 0, ops = 0, loads = 0;
+	bool alive = len != 0;
+	if(item & 1u)                               // the read has an N: none may be in the near half
+		for(uint32_t d = 0; alive && d < nea; d++)
+			if(seq[len - d - 1] > 3) alive = false;
+	if(alive) {
+		if(flen > 1 && flen <= nea) {
+			// ftabSeqToInt(seq, len-flen, rev=!ebwtfw) (bt2_idx.h:1383-1390)
+			uint32_t fi = 0, fip = 0;
+			for(uint32_t i = 0; i < flen; i++) {
+				fi = (fi << 2) | (uint32_t)seq[len - flen + i];
+				fip = (fip << 2) | (uint32_t)seq[len - 1 - i];
+			}
+			top = ftab_hi(E, fi); bot = ftab_lo(E, fi + 1);
+			topp = ftab_hi(Ep, fip); botp = ftab_lo(Ep, fip + 1);
+			dep = flen;
+		} else {
+			const int c = seq[len - 1];
+			top = topp = fchr_at(E, c);
+			bot = botp = fchr_at(E, c + 1);
+			dep = 1;
+		}
+		alive = bot != top;
+	}
+	while(alive && dep < nea) {
+		const int c = seq[len - dep - 1];
+		ops++;
+		if(bot - top > 1) {
+			uint32_t t[4] = {0, 0, 0, 0}, b[4] = {0, 0, 0, 0}, tp[4], bp[4];
+			tp[0] = topp;
+			loads += bi_step(E, top, bot, topp, t, b, tp, bp);
+			const uint32_t nt = at4(t, c), nb = at4(b, c);
+			if(nb <= nt) { alive = false; break; }
+			top = nt; bot = nb; topp = at4(tp, c); botp = at4(bp, c);
+		} else {
+			SideData s1;
+			load_side(E, top / 192u, s1);
+			loads++;
+			if(side_rowL(s1, top % 192u) != c || top == E.zoff) { alive = false; break; }
+			top = occ1(E, s1, top, c);
+			bot = top + 1;
+		}
+		dep++;
+	}
+	st4[qi] = alive ? make_uint4(top, bot, topp, botp) : make_uint4(0, 0, 0, 0);
+	sdep[qi] = dep | (alive ? 0x80000000u : 0u);
+	if(ops) atomicAdd(&ops_out[r], ops);
+	if(ops && loads_out) atomicAdd(&loads_out[r], loads);
 }
 
 #ifndef BT2G_MM_WAVES
@@ -97,18 +192,17 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(BT2G_M
 k_one_mm_q(DevEbwt F, DevEbwt B, const uint8_t* __restrict__ reads, const uint8_t* __restrict__ quals,
            uint32_t stride, const uint32_t* __restrict__ lens, const int32_t* __restrict__ minscs, MmParams P,
            double ncl_const, double ncl_lin, const uint32_t* __restrict__ items,
-           const uint32_t* __restrict__ nitems_p, uint32_t cap,
-           bt2g_mm1* __restrict__ slots, int32_t* __restrict__ slot_counts, uint32_t* __restrict__ ops_out,
+           const uint32_t* __restrict__ nitems_p, const uint4* __restrict__ st4,
+           const uint32_t* __restrict__ sdep, uint32_t cap, bt2g_mm1* __restrict__ slots, int32_t* __restrict__ slot_counts, uint32_t* __restrict__ ops_out,
            uint32_t* __restrict__ loads_out) {
 	const uint32_t nitems = *nitems_p;
 	const int64_t matchsc = (int64_t)((float)P.match + 0.5f);
 
 	// per-lane item state
 	int st = ST_IDLE;
-	uint32_t r = 0, len = 0, slot = 0, dep = 0, nea = 0, depm = 0;
+	uint32_t r = 0, len = 0, slot = 0, dep = 0, depm = 0;
 	constexpr bool ebwtfw = EBWTFW;
 	const DevEbwt& E = EBWTFW ? F : B;          // the index walked (uniform)
-	const DevEbwt& Ep = EBWTFW ? B : F;         // its mirror (ftab only)
 	bool fw = true, hasn = false;
 	int nceil = 0;
 	int64_t minsc = 0;
@@ -210,55 +304,23 @@ k_one_mm_q(DevEbwt F, DevEbwt B, const uint8_t* __restrict__ reads, const uint8_
 			// seq = fw ? (ebwtfw ? patFw : patFwRev) : (ebwtfw ? patRc : patRcRev)
 			seq = SeqView{rd, len, fw ? !ebwtfw : ebwtfw, !fw};
 			qrev = fw ? !ebwtfw : ebwtfw;
-			const uint32_t halfFw = len >> 1, halfBw = (len >> 1) + (len & 1);
-			nea = ebwtfw ? halfFw : halfBw;
-			const uint32_t flen = E.ftab_chars;
-			bool skip = len == 0;
-			for(uint32_t d = 0; d < nea; d++)
-				if(seq[len - d - 1] > 3) { skip = true; break; }
-			if(!skip) {
-				if(flen > 1 && flen <= nea) {
-					// ftabSeqToInt(seq, len-flen, rev=!ebwtfw) (bt2_idx.h:1383-1390)
-					uint32_t fi = 0, fip = 0;
-					for(uint32_t i = 0; i < flen; i++) {
-						fi = (fi << 2) | (uint32_t)seq[len - flen + i];
-						fip = (fip << 2) | (uint32_t)seq[len - 1 - i];
-					}
-					top = ftab_hi(E, fi); bot = ftab_lo(E, fi + 1);
-					topp = ftab_hi(Ep, fip); botp = ftab_lo(Ep, fip + 1);
-					if(bot - top == 0) skip = true;
-					else dep = flen;
-				} else {
-					const int c = seq[len - 1];
-					top = topp = fchr_at(E, c);
-					bot = botp = fchr_at(E, c + 1);
-					if(bot - top == 0) skip = true;
-					else dep = 1;
-				}
-			}
-			st = skip ? ST_DONE : (dep < nea ? ST_NEAR : ST_FAR);
+			// resume after the near half (k_one_mm_near)
+			const uint32_t sd = sdep[qi];
+			const uint4 q4 = st4[qi];
+			top = q4.x; bot = q4.y; topp = q4.z; botp = q4.w;
+			dep = sd & 0x7fffffffu;
+			st = (sd >> 31) ? ST_FAR : ST_DONE;
 		}
 		const uint64_t busy = __ballot(st != ST_IDLE);
 		if(busy == 0 && exhausted) break;
-#ifdef BT2G_MM_DEBUG
-		{
-			extern __device__ unsigned long long g_mm_dbg[4];
-			const uint64_t lf = __ballot(st == ST_NEAR || st == ST_FAR || st == ST_BR);
-			if((threadIdx.x & 63u) == 0) {
-				atomicAdd(&g_mm_dbg[0], 1ull);
-				atomicAdd(&g_mm_dbg[1], (unsigned long long)__popcll(lf));
-				atomicAdd(&g_mm_dbg[2], (unsigned long long)__popcll(busy));
-			}
-		}
-#endif
-		if(st == ST_FAR && dep >= len) st = ST_DONE;   // far half empty (len <= flen / 1): no step
+		if(st == ST_FAR && dep >= len) st = ST_DONE;   // far half empty: no step
 		if(st == ST_FAR) {
 			rdc = seq[len - dep - 1];
 			quc = qd[qrev ? dep : len - dep - 1];
 			if(rdc > 3 && nceil == 0) st = ST_DONE;
 			else if(bot - top <= 1 && top == E.zoff) st = ST_DONE;   // mapLF1 hit '$'
 		}
-		if(!(st == ST_NEAR || st == ST_FAR || st == ST_BR)) continue;
+		if(!(st == ST_FAR || st == ST_BR)) continue;
 
 		// ---- one LF operation (bt2_idx.h mapBiLFEx / mapLF1)
 		const bool br = st == ST_BR;
@@ -281,20 +343,7 @@ k_one_mm_q(DevEbwt F, DevEbwt B, const uint8_t* __restrict__ reads, const uint8_
 			lf1 = occ1(E, s1, qT, rowl);
 		}
 
-		if(st == ST_NEAR) {
-			const int c = seq[len - dep - 1];
-			if(multi) {
-				top = at4(ot, c); bot = at4(ob, c);
-				if(bot <= top) { st = ST_DONE; continue; }
-				topp = at4(otp, c); botp = at4(obp, c);
-			} else {
-				if(rowl != c || qT == E.zoff) { st = ST_DONE; continue; }
-				top = lf1;
-				bot = top + 1;
-			}
-			dep++;
-			if(dep >= nea) st = ST_FAR;
-		} else if(st == ST_FAR) {
+		if(st == ST_FAR) {
 			clo = 0; chi = 3; match = true;
 			if(multi) {
 #pragma unroll
@@ -360,15 +409,22 @@ k_one_mm_q(DevEbwt F, DevEbwt B, const uint8_t* __restrict__ reads, const uint8_
 void launch_one_mm_q(const DevEbwt& F, const DevEbwt& B, const uint8_t* reads, const uint8_t* quals, uint32_t stride,
                      const uint32_t* lens, uint32_t n, const int32_t* minsc, const bt2g_scoring& sc, int nofw,
                      int norc, const uint32_t* gate, uint32_t cap, uint32_t* items, uint32_t* counters,
-                     bt2g_mm1* slots, int32_t* slot_counts, uint32_t* ops, uint32_t* loads, hipStream_t st) {
+                     uint4* near_state, uint32_t* near_dep, bt2g_mm1* slots, int32_t* slot_counts, uint32_t* ops,
+                     uint32_t* loads, hipStream_t st) {
 	MmParams P{sc.match, sc.mmp_max, sc.mmp_min, sc.npen, sc.local, 0, 0};
 	// counters[0]/[2] = item counts of the BWT / BWT' lists (zeroed by the caller)
 	hipLaunchKernelGGL(k_one_mm_items, dim3((n + 255) / 256), dim3(256), 0, st, reads, stride, lens, n, gate, nofw,
 	                   norc, items, counters, slot_counts);
 	const uint32_t grid = (2 * n + 255) / 256;   // list capacity; lanes past the count exit
+	const size_t half = 2 * (size_t)n;
+	hipLaunchKernelGGL(k_one_mm_near<true>, dim3(grid), dim3(256), 0, st, F, B, reads, stride, lens, items, counters,
+	                   near_state, near_dep, ops, loads);
+	hipLaunchKernelGGL(k_one_mm_near<false>, dim3(grid), dim3(256), 0, st, F, B, reads, stride, lens, items + half,
+	                   counters + 2, near_state + half, near_dep + half, ops, loads);
 	hipLaunchKernelGGL(k_one_mm_q<true>, dim3(grid), dim3(256), 0, st, F, B, reads, quals, stride, lens, minsc, P,
-	                   sc.ncl_const, sc.ncl_lin, items, counters, cap, slots, slot_counts, ops, loads);
+	                   sc.ncl_const, sc.ncl_lin, items, counters, near_state, near_dep, cap, slots, slot_counts, ops,
+	                   loads);
 	hipLaunchKernelGGL(k_one_mm_q<false>, dim3(grid), dim3(256), 0, st, F, B, reads, quals, stride, lens, minsc, P,
-	                   sc.ncl_const, sc.ncl_lin, items + 2 * (size_t)n, counters + 2, cap, slots,
-	                   slot_counts, ops, loads);
+	                   sc.ncl_const, sc.ncl_lin, items + half, counters + 2, near_state + half, near_dep + half, cap,
+	                   slots, slot_counts, ops, loads);
 }
