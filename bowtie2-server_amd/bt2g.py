@@ -216,7 +216,7 @@ class Engine:
 
     # ---- SW ----------------------------------------------------------------
     def sw_align(self, reads, quals, lens, probs, windows=None, local=False, enable8=True, cap=4096,
-                 want_mat=False):
+                 want_mat=False, sc=None):
         reads, quals, lens = _c(reads, np.uint8), _c(quals, np.uint8), _c(lens, np.uint32)
         probs = _c(probs, SWPROB_DTYPE)
         n = len(probs)
@@ -229,7 +229,7 @@ class Engine:
             mat_off = np.zeros(n, np.uint64)
             mat_off[1:] = np.cumsum(sizes)[:-1]
             mat = np.zeros(int(sizes.sum()), np.int16)
-        sc = scoring(local)
+        sc = scoring(local) if sc is None else sc
         _chk(lib().bt2g_sw_align(self.h, _ptr(reads), _ptr(quals), reads.shape[1], _ptr(lens), _ptr(probs), n,
                                  _ptr(win), 0 if win is None else win.nbytes, C.byref(sc), int(enable8), cap,
                                  _ptr(res), _ptr(cands), _ptr(mat), _ptr(mat_off)))

@@ -523,7 +523,7 @@ int bt2g_sw_align_dev(bt2g_ctx* c, const uint8_t* reads, const uint8_t* quals, u
 	uint32_t* satl = lists + 2 * (size_t)nprob;
 	{
 		ProfScope ps(c, 4, st);
-		const uint32_t S = (stride + 15u) / 16u, lds = (64u / S) * (maxcol | 1u) * 4u;
+		const uint32_t S = (stride + 15u) / 16u, lds = (64u / S) * ((maxcol + 1u) | 1u) * 4u;
 		if(sw_packed_ok(*sc, C, mat) && lds <= 65536u) {
 			launch_sw_ee_packed(probs, nprob, reads, quals, stride, lens, windows, c->ref_codes, c->ref_starts, C,
 			                    enable8, cap, maxcol, res, cands, st);

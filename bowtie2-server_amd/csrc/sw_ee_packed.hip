@@ -77,9 +77,13 @@ struct Half {
 
 }  // namespace
 
-#ifndef BT2G_SW_WAVES
-#define BT2G_SW_WAVES 2
+#ifndef BT2G_SW_COLS
+#define BT2G_SW_COLS 1          // columns per systolic step (1, or 2: measured slower, occupancy 2)
 #endif
+#ifndef BT2G_SW_WAVES
+#define BT2G_SW_WAVES 3
+#endif
+template <bool SAMEGO>
 __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(BT2G_SW_WAVES)))
 k_sw_ee_sys(const bt2g_sw_problem* __restrict__ probs, uint32_t nprob, const uint8_t* __restrict__ reads,
             const uint8_t* __restrict__ quals, uint32_t stride, const uint32_t* __restrict__ lens,
@@ -257,6 +261,79 @@ k_sw_ee_sys(const bt2g_sw_problem* __restrict__ probs, uint32_t nprob, const uin
 		}
 	}
 	__syncthreads();
+#if BT2G_SW_COLS == 2
+	// Two columns per step: cell (i, j+1) only waits for (i, j)'s E and
+	// (i-1, j)'s H, so the two F chains of a step interleave (twice the ILP of
+	// the dependent row recurrence) and the lane-to-lane hand-off is halved.
+	uint32_t hout0 = 0, fout0 = 0, hout1 = 0, fout1 = 0;
+	uint32_t nsel0 = in_group ? mysel[0] : 0u, nsel1 = in_group ? mysel[1] : 0u;
+	const uint32_t ncp = (ncolmax + 1) / 2;     // column pairs
+	const uint32_t T = ncp + S - 1;
+	for(uint32_t t = 0; t < T; t++) {
+		const uint32_t hin0 = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)hout0, 0x138, 0xf, 0xf, false);
+		const uint32_t fin0 = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)fout0, 0x138, 0xf, 0xf, false);
+		const uint32_t hin1 = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)hout1, 0x138, 0xf, 0xf, false);
+		const uint32_t fin1 = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)fout1, 0x138, 0xf, 0xf, false);
+		const int jp = (int)t - (int)k;
+		if(jp < 0 || jp >= (int)ncp) continue;
+		const uint32_t j = 2u * (uint32_t)jp;
+		const uint32_t sel0 = nsel0, sel1 = nsel1;
+		if(in_group && jp + 1 < (int)ncp) { nsel0 = mysel[j + 2]; nsel1 = mysel[j + 3]; }
+		uint32_t hup0, fup0, hup1, fup1, diag0;
+		if(top) {
+			hup0 = fup0 = hup1 = fup1 = 0;
+			diag0 = row0p;
+		} else {
+			hup0 = hin0; fup0 = fin0; hup1 = hin1; fup1 = fin1;
+			diag0 = hbprev;
+			hbprev = hup1;
+		}
+		uint32_t diag1 = top ? row0p : hup0;
+		const uint32_t nf0 = ((sel0 & 0xffu) == 0x0cu ? npen : 0u) | (((sel0 >> 16) & 0xffu) == 0x0cu ? npen << 16 : 0u);
+		const uint32_t nf1 = ((sel1 & 0xffu) == 0x0cu ? npen : 0u) | (((sel1 >> 16) & 0xffu) == 0x0cu ? npen << 16 : 0u);
+		uint32_t fprev0 = fup0, hprev0 = hup0, fprev1 = fup1, hprev1 = hup1;
+		auto rows = [&](auto n_tag) {
+			constexpr bool NCOL = decltype(n_tag)::value;
+#pragma unroll
+			for(int i = 0; i < R; i++) {
+				uint32_t pen0 = __builtin_amdgcn_perm(PB[i], PA[i], sel0);
+				uint32_t pen1 = __builtin_amdgcn_perm(PB[i], PA[i], sel1);
+				if(NCOL) {
+					uint32_t pa = PA[i], pb = PB[i];
+					asm volatile("" : "+v"(pa), "+v"(pb));
+					const uint32_t real = (pa ? 0xffffu : 0u) | (pb ? 0xffff0000u : 0u);
+					pen0 = pmax(pen0, nf0 & real);
+					pen1 = pmax(pen1, nf1 & real);
+				}
+				// column j
+				const uint32_t d0 = psub(diag0, pen0);
+				const uint32_t f0 = pmax(psub(fprev0, rfge2), psub(hprev0, rfgo2)) & M[i];
+				const uint32_t h0 = pmax(pmax(d0, E[i]), f0);
+				const uint32_t e0 = pmax(psub(E[i], rdge2), psub(h0, rdgo2) & M[i]);
+				// column j+1
+				const uint32_t d1 = psub(diag1, pen1);
+				const uint32_t f1 = pmax(psub(fprev1, rfge2), psub(hprev1, rfgo2)) & M[i];
+				const uint32_t h1 = pmax(pmax(d1, e0), f1);
+				E[i] = pmax(psub(e0, rdge2), psub(h1, rdgo2) & M[i]);
+				diag0 = Hc[i];      // H(i, j-1): diagonal of (i+1, j)
+				diag1 = h0;         // H(i, j):   diagonal of (i+1, j+1)
+				Hc[i] = h1;
+				fprev0 = f0; hprev0 = h0;
+				fprev1 = f1; hprev1 = h1;
+			}
+		};
+		if(__ballot((nf0 | nf1) != 0)) rows(std::true_type{});
+		else rows(std::false_type{});
+		hout0 = hprev0; fout0 = fprev0;
+		hout1 = hprev1; fout1 = fprev1;
+		// the bottom lane is the last reader of columns j, j+1: their slots now
+		// keep both problems' last-row H for the gather below
+		if(bottom && in_group) {
+			mysel[j] = hprev0;
+			if(j + 1 < ncolmax) mysel[j + 1] = hprev1;
+		}
+	}
+#else
 	uint32_t hout = 0, fout = 0;
 	uint32_t nsel = in_group ? mysel[0] : 0u;
 	const uint32_t T = ncolmax + S - 1;
@@ -285,7 +362,7 @@ k_sw_ee_sys(const bt2g_sw_problem* __restrict__ probs, uint32_t nprob, const uin
 		// its lanes sees one.
 		const uint32_t nfloor = ((sel & 0xffu) == 0x0cu ? npen : 0u) |
 		                        (((sel >> 16) & 0xffu) == 0x0cu ? npen << 16 : 0u);
-		uint32_t fprev = fup, hprev = hup;
+		uint32_t fprev = fup, hprev = SAMEGO ? psub(hup, rfgo2) : hup;
 		auto rows = [&](auto n_tag) {
 			constexpr bool NCOL = decltype(n_tag)::value;
 #pragma unroll
@@ -300,23 +377,37 @@ k_sw_ee_sys(const bt2g_sw_problem* __restrict__ probs, uint32_t nprob, const uin
 					pen = pmax(pen, nfloor & real);
 				}
 				const uint32_t d = psub(diag, pen);
-				const uint32_t f = pmax(psub(fprev, rfge2), psub(hprev, rfgo2)) & M[i];
-				const uint32_t hh = pmax(pmax(d, E[i]), f);
-				E[i] = pmax(psub(E[i], rdge2), psub(hh, rdgo2) & M[i]);
-				diag = Hc[i];
-				Hc[i] = hh;
-				fprev = f;
-				hprev = hh;
+				if(SAMEGO) {
+					// read and reference gap opens equal: H - open serves the F of the
+					// next row and the E of the next column (one subtract less)
+					const uint32_t f = pmax(psub(fprev, rfge2), hprev) & M[i];
+					const uint32_t hh = pmax(pmax(d, E[i]), f);
+					const uint32_t hg = psub(hh, rdgo2);
+					E[i] = pmax(psub(E[i], rdge2), hg & M[i]);
+					diag = Hc[i];
+					Hc[i] = hh;
+					fprev = f;
+					hprev = hg;          // carries H - open
+				} else {
+					const uint32_t f = pmax(psub(fprev, rfge2), psub(hprev, rfgo2)) & M[i];
+					const uint32_t hh = pmax(pmax(d, E[i]), f);
+					E[i] = pmax(psub(E[i], rdge2), psub(hh, rdgo2) & M[i]);
+					diag = Hc[i];
+					Hc[i] = hh;
+					fprev = f;
+					hprev = hh;
+				}
 			}
 		};
 		if(__ballot(nfloor != 0)) rows(std::true_type{});
 		else rows(std::false_type{});
-		hout = hprev;
+		hout = Hc[R - 1];        // the strip's bottom row at column j (== hprev when !SAMEGO)
 		fout = fprev;
 		// the bottom lane is the last reader of column j's selector: the slot now
 		// keeps both problems' last-row H for the gather below
-		if(bottom && in_group) mysel[j] = hprev;
+		if(bottom && in_group) mysel[j] = hout;
 	}
+#endif
 	if(!bottom || !in_group) return;
 	// last-row maximum and end-to-end candidates in column order
 	// (aligner_swsse_ee_u8.cpp:1096-1100, 1176-1208)
@@ -369,9 +460,13 @@ void launch_sw_ee_packed(const bt2g_sw_problem* probs, uint32_t nprob, const uin
 	if(nprob == 0) return;
 	const uint32_t S = (stride + 15u) / 16u;     // <= 64 (stride <= BT2G_MAX_READ_LEN)
 	const uint32_t per_wave = 2u * (64u / S);
-	const uint32_t ldsw = max_cols | 1u;          // odd word stride: groups hit different banks
-	hipLaunchKernelGGL(k_sw_ee_sys, dim3((nprob + per_wave - 1) / per_wave), dim3(64),
-	                   (per_wave / 2) * ldsw * sizeof(uint32_t), st, probs,
-	                   nprob, reads, quals, stride, lens, windows, ref_codes, ref_starts, C, enable8, cap, max_cols, S,
-	                   ldsw, res, cands);
+	const uint32_t ldsw = (max_cols + 1u) | 1u;   // >= ncol+1 (column pairs); odd: groups hit different banks
+	const dim3 grid((nprob + per_wave - 1) / per_wave), block(64);
+	const size_t lds = (per_wave / 2) * ldsw * sizeof(uint32_t);
+	if(C.rdgo == C.rfgo)
+		hipLaunchKernelGGL(k_sw_ee_sys<true>, grid, block, lds, st, probs, nprob, reads, quals, stride, lens, windows,
+		                   ref_codes, ref_starts, C, enable8, cap, max_cols, S, ldsw, res, cands);
+	else
+		hipLaunchKernelGGL(k_sw_ee_sys<false>, grid, block, lds, st, probs, nprob, reads, quals, stride, lens,
+		                   windows, ref_codes, ref_starts, C, enable8, cap, max_cols, S, ldsw, res, cands);
 }

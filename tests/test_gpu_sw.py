@@ -108,7 +108,8 @@ def test_sw_resident_reference(eng):
     assert res1["aligned"].sum() > n // 2
 
 
-def test_sw_packed_vs_per_lane(eng):
+@pytest.mark.parametrize("gaps", ["default", "rdg5,3_rfg4,2"])
+def test_sw_packed_vs_per_lane(eng, gaps):
     """The packed two-problems-per-lane end-to-end fill (default path) against
     the one-problem-per-lane fill (taken when matrices are requested) on
     ragged problems: read lengths 1..400, widths 1..500, u8 and i16 minsc,
@@ -145,8 +146,11 @@ def test_sw_packed_vs_per_lane(eng):
     probs["minsc"] = np.where(rng.random(n) < 0.3, -(0.6 + 2.5 * lens).astype(np.int64),
                               -(0.6 + 0.6 * lens).astype(np.int64))
     probs["minsc"][:3] = [0, -254, -255]
-    res_p, c_p, _ = eng.sw_align(codes, quals, lens, probs, cap=512)
-    res_g, c_g, _ = eng.sw_align(codes, quals, lens, probs, cap=512, want_mat=True)
+    sc = bt2g.scoring(False)
+    if gaps != "default":          # unequal gap opens: the packed fill's general E/F form
+        sc.rfg_const, sc.rfg_lin = 4, 2
+    res_p, c_p, _ = eng.sw_align(codes, quals, lens, probs, cap=512, sc=sc)
+    res_g, c_g, _ = eng.sw_align(codes, quals, lens, probs, cap=512, want_mat=True, sc=sc)
     assert np.array_equal(res_p, res_g)
     assert np.array_equal(c_p, c_g)
     assert 0 < res_p["aligned"].sum() < n
