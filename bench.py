@@ -339,7 +339,7 @@ def main():
     ap.add_argument("--reads", type=int, default=1_000_000, help="reads per GPU per step")
     ap.add_argument("--read-len", type=int, default=150)
     ap.add_argument("--genome-mb", type=float, default=1000.0)
-    ap.add_argument("--cpu-sample", type=int, default=20000)
+    ap.add_argument("--cpu-sample", type=int, default=1_000_000)
     ap.add_argument("--cpu-threads", type=int, default=16)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--index-cache", default="", help="reuse/write the built index at this base path")
