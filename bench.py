@@ -205,6 +205,27 @@ class Pipeline:
         return aligned
 
 
+def pmc_traffic(fetch_csv, write_csv, kernel):
+    """HBM bytes per launch of `kernel` from separate rocprofv3 --pmc FETCH_SIZE /
+    WRITE_SIZE passes of the same command (counter values in KiB per dispatch;
+    FETCH_SIZE is uncalibrated for 64-B gathers on gfx950)."""
+    import csv
+    if not fetch_csv or not write_csv:
+        return None
+    import collections
+    total = 0.0
+    for path in (fetch_csv, write_csv):
+        per = collections.defaultdict(list)          # every kernel of the API call (k_one_mm_near<true>, ...)
+        for r in csv.DictReader(open(path)):
+            name = r["Kernel_Name"].split("(")[0].replace("void ", "").strip()
+            if name == kernel or name.startswith(kernel + "_") or name.startswith(kernel + "<"):
+                per[name].append(float(r["Counter_Value"]))
+        if not per:
+            return None
+        total += sum(sum(v) / len(v) for v in per.values()) * 1024
+    return total
+
+
 def combine_ranks(elapsed, n_aligned, dev):
     """Max of the per-rank times, sum of the aligned-read counters: the path's
     only collective (RCCL on the GPUs, gloo in the CPU tests)."""
@@ -343,6 +364,9 @@ def main():
     ap.add_argument("--cpu-threads", type=int, default=16)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--index-cache", default="", help="reuse/write the built index at this base path")
+    ap.add_argument("--pmc-fetch", default="", help="rocprofv3 --pmc FETCH_SIZE counter_collection.csv of this "
+                                                    "command: fills roofline.traffic")
+    ap.add_argument("--pmc-write", default="", help="same for WRITE_SIZE")
     args = ap.parse_args()
 
     import torch
@@ -467,7 +491,8 @@ def main():
                        "global_batch": args.reads * world, "seq_len": args.read_len, "parallelism": f"dp{world}",
                        "aligned_frac": n_aligned / total_reads},
             "roofline": {"bound": "hbm", "kernel": names_k[dom], "achieved": achieved, "peak": HBM_PEAK_GBS,
-                         "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS, "traffic": None,
+                         "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS,
+                         "traffic": pmc_traffic(args.pmc_fetch, args.pmc_write, "k_" + names_k[dom]),
                          "bytes_per_launch": bytes_k[dom], "ms_per_launch": per_launch[dom]},
             "kernels_ms": {names_k[k]: per_launch[k] for k in per_launch},
             "kernels_gbs": {names_k[k]: bytes_k[k] / (per_launch[k] / 1e3) / 1e9 for k in per_launch
