@@ -20,6 +20,10 @@
  *     loc u8  aligner_swsse_loc_u8.cpp:75-159, 927-1336 (gather 1389-1500)
  *     loc i16 aligner_swsse_loc_i16.cpp:75-145, 938-1367 (gather 1420-1535)
  *     dispatch SwAligner::align aligner_sw.cpp:500-729; Scoring scoring.h:96-440
+ *   backtrace: SwAligner::nextAlignment aligner_sw.cpp:737-1146 with
+ *     backtraceNucleotides{End2End,Local}Sse{U8,I16}
+ *     (aligner_swsse_ee_u8.cpp:1283-1780, aligner_swsse_loc_u8.cpp:1588-2175,
+ *      same walk in the i16 files), SSEMatrix masks aligner_swsse.h:263-494
  *
  * Pinned by tests/test_oracle_golden.py against vectors produced by the
  * reference itself (oracle/_ref/libbt2ref.so, tests/golden/make_golden.py).
@@ -848,4 +852,265 @@ int orc_sw(const uint8_t* rd, const uint8_t* q33, int nrow, const uint8_t* rf, i
 	}
 	free(H); free(E); free(F); free(colmax);
 	return 0;
+}
+
+/* ---------------------------------------------------------------------- */
+/* Backtrace: the SwDriver nextAlignment loop over one filled problem.      */
+/* ---------------------------------------------------------------------- */
+typedef struct { int32_t pos, chr, qchr, type; } orc_edit;
+typedef struct {
+	size_t nedsz, celsz, row, col, gaps, rdg, rfg; int64_t score; int ns; int ct;
+} orc_btframe;
+
+enum { CT_H = 0, CT_E = 1, CT_F = 2 };
+enum { BT_DIAG, BT_REF_OPEN, BT_READ_OPEN, BT_RFGAP_EXT, BT_RDGAP_EXT };
+
+static char mask2dna_c(int m) {
+	switch(m) { case 1: return 'A'; case 2: return 'C'; case 4: return 'G'; case 8: return 'T'; default: return 'N'; }
+}
+
+/* One backtrace from (row, col) (aligner_swsse_ee_u8.cpp:1283-1780 /
+ * aligner_swsse_loc_u8.cpp:1588-2175).  V = H/E/F values in score units
+ * (value + offsetsc); local: neighbour values must be > 0 (floorsc).  marks =
+ * reportedThrough bits (aligner_swsse.h:263-278), persistent across
+ * candidates.  Returns 1 on success with the alignment in *ed / aout. */
+static int orc_bt_one(const int64_t* VH, const int64_t* VE, const int64_t* VF, uint8_t* marks,
+                      const uint8_t* rd, const uint8_t* q33, int nrow, const uint8_t* rf, int ncol,
+                      const orc_scoring* sc, int local, int triml, int corel, int corer, int nceil,
+                      size_t row, size_t col, orc_edit* ed, size_t* ned_o, int64_t* aout,
+                      orc_btframe* stack, size_t* cells) {
+	const int rdgo = sc->rdg_const + sc->rdg_lin, rdge = sc->rdg_lin;
+	const int rfgo = sc->rfg_const + sc->rfg_lin, rfge = sc->rfg_lin;
+	const int64_t match30 = sc->match;
+	size_t nst = 0, ncell = 0, ned = 0;
+	size_t origCol = col, trimEnd = (size_t)nrow - row - 1, trimBeg = 0;
+	size_t gaps = 0, readGaps = 0, refGaps = 0;
+	int64_t score = 0; int ns = 0;
+	int ct = CT_H;
+#define V(M, r, c) (M[(size_t)(r) * ncol + (c)])
+#define OK(x) (!local || (x) > 0)
+	while((long)row >= 0) {
+		int readc = rd[row], refm = rf[col], readq = q33[row];
+		int empty = 0, canMoveThru = 1, branch = 0, cur = -1;
+		if(marks[row * ncol + col]) {
+			canMoveThru = 0;
+		} else if(row > 0) {
+			size_t rowFromEnd = (size_t)nrow - row - 1;
+			int gapsAllowed = !(row < (size_t)sc->gapbar || rowFromEnd < (size_t)sc->gapbar);
+			int origMask = 0;
+			if(ct == CT_E) {
+				int64_t cur_ = V(VE, row, col), hl = V(VH, row, col - 1), el = V(VE, row, col - 1);
+				if(OK(hl) && hl - rdgo == cur_) origMask |= 1;
+				if(OK(el) && el - rdge == cur_) origMask |= 2;
+				/* mask == 3 picks H (the '#if 1' branch, aligner_swsse_ee_u8.cpp:1376-1392) */
+				if(origMask == 3) { cur = BT_READ_OPEN; branch = 1; }
+				else if(origMask == 2) cur = BT_RDGAP_EXT;
+				else if(origMask == 1) cur = BT_READ_OPEN;
+				else { empty = 1; canMoveThru = 1; }
+			} else if(ct == CT_F) {
+				int64_t cur_ = V(VF, row, col), hu = V(VH, row - 1, col), fu = V(VF, row - 1, col);
+				if(OK(hu) && hu - rfgo == cur_) origMask |= 1;
+				if(OK(fu) && fu - rfge == cur_) origMask |= 2;
+				if(origMask == 3) { cur = BT_REF_OPEN; branch = 1; }
+				else if(origMask == 2) cur = BT_RFGAP_EXT;
+				else if(origMask == 1) cur = BT_REF_OPEN;
+				else { empty = 1; canMoveThru = 1; }
+			} else {
+				int64_t cur_ = V(VH, row, col);
+				int64_t fu = V(VF, row - 1, col), hu = V(VH, row - 1, col);
+				int64_t hl = 0, el = 0, hul = 0; int hasl = col > 0;
+				if(hasl) { hl = V(VH, row, col - 1); el = V(VE, row, col - 1); hul = V(VH, row - 1, col - 1); }
+				int64_t sdiag = score_of(sc, readc, refm, readq - 33);
+				if(gapsAllowed) {
+					if(OK(hu) && cur_ == hu - rfgo) origMask |= 1;
+					if(hasl && OK(hl) && cur_ == hl - rdgo) origMask |= 2;
+					if(OK(fu) && cur_ == fu - rfge) origMask |= 4;
+					if(hasl && OK(el) && cur_ == el - rdge) origMask |= 8;
+				}
+				if(hasl && OK(hul) && cur_ == hul + sdiag) origMask |= 16;
+				/* fixed priority of the '#if 1' branch (aligner_swsse_ee_u8.cpp:1509-1520) */
+				int npop = __builtin_popcount((unsigned)origMask);
+				if(npop > 1) branch = 1;
+				if(origMask & 16) cur = BT_DIAG;
+				else if(origMask & 1) cur = BT_REF_OPEN;
+				else if(origMask & 4) cur = BT_RFGAP_EXT;
+				else if(origMask & 2) cur = BT_READ_OPEN;
+				else if(origMask & 8) cur = BT_RDGAP_EXT;
+				else { empty = 1; canMoveThru = 1; }
+			}
+		}
+		marks[row * ncol + col] = 1;
+		if(!canMoveThru) {
+			if(nst > 0) {
+				/* pop the last branch point (aligner_swsse_ee_u8.cpp:1560-1578) */
+				orc_btframe* f = &stack[--nst];
+				ncell = f->celsz; ned = f->nedsz; row = f->row; col = f->col;
+				gaps = f->gaps; readGaps = f->rdg; refGaps = f->rfg; score = f->score; ns = f->ns; ct = f->ct;
+				continue;
+			}
+			return 0;
+		}
+		if(empty || row == 0) {
+			cells[2 * ncell] = row; cells[2 * ncell + 1] = col; ncell++;
+			trimBeg = row;
+			break;
+		}
+		if(branch) {
+			orc_btframe f = { ned, ncell, row, col, gaps, readGaps, refGaps, score, ns, ct };
+			stack[nst++] = f;
+		}
+		cells[2 * ncell] = row; cells[2 * ncell + 1] = col; ncell++;
+		switch(cur) {
+		case BT_DIAG: {
+			int m = (refm >= 16 || readc > 3) ? -1 : (((1 << readc) & refm) ? 1 : 0);
+			ct = CT_H;
+			if(m != 1) {
+				orc_edit e = { (int)row, mask2dna_c(refm), "ACGTN"[readc], 3 };
+				ed[ned++] = e;
+				score -= (readc > 3 || refm > 15) ? sc->npen : mmpen_q(sc, readq - 33);
+			} else score += match30;
+			if(m == -1) ns++;
+			row--; col--;
+			break;
+		}
+		case BT_REF_OPEN: case BT_RFGAP_EXT: {
+			orc_edit e = { (int)row, '-', "ACGTN"[readc], 2 };
+			ed[ned++] = e;
+			score -= cur == BT_REF_OPEN ? rfgo : rfge;
+			ct = cur == BT_REF_OPEN ? CT_H : CT_F;
+			row--; gaps++; refGaps++;
+			break;
+		}
+		default: { /* read gaps */
+			orc_edit e = { (int)row + 1, mask2dna_c(rf[col]), '-', 1 };
+			ed[ned++] = e;
+			score -= cur == BT_READ_OPEN ? rdgo : rdge;
+			ct = cur == BT_READ_OPEN ? CT_H : CT_E;
+			col--; gaps++; readGaps++;
+			break;
+		}
+		}
+	}
+#undef V
+#undef OK
+	/* must overlap a core diagonal (aligner_swsse_ee_u8.cpp:1764-1800) */
+	int core = 0;
+	for(size_t i = 0; i < ncell && !core; i++) {
+		int64_t d = (int64_t)cells[2 * i + 1] - (int64_t)cells[2 * i] + triml;
+		if(d >= 0 && d >= corel && d <= corer) core = 1;
+	}
+	if(!core) return 0;
+	{
+		int readc = rd[row], refm = rf[col];
+		int m = (refm >= 16 || readc > 3) ? -1 : (((1 << readc) & refm) ? 1 : 0);
+		if(m != 1) {
+			orc_edit e = { (int)row, mask2dna_c(refm), "ACGTN"[readc], 3 };
+			ed[ned++] = e;
+			score -= (readc > 3 || refm > 15) ? sc->npen : mmpen_q(sc, q33[row] - 33);
+		} else score += match30;
+		if(m == -1) ns++;
+	}
+	if(ns > nceil) return 0;
+	/* res.reverse(): edits 5'->3' of the DP read */
+	for(size_t i = 0; i < ned / 2; i++) { orc_edit t = ed[i]; ed[i] = ed[ned - 1 - i]; ed[ned - 1 - i] = t; }
+	/* AlnRes::setShape shifts edits by the rows trimmed at the DP top
+	 * (aligner_result.cpp:101-108) */
+	for(size_t i = 0; i < ned; i++) ed[i].pos -= (int32_t)trimBeg;
+	size_t refns = 0;
+	for(size_t i = col; i <= origCol; i++) if(rf[i] > 15) refns++;
+	aout[0] = score; aout[1] = (int64_t)col; aout[2] = ns; aout[3] = (int64_t)gaps; aout[4] = (int64_t)refns;
+	aout[5] = (int64_t)trimBeg; aout[6] = (int64_t)trimEnd;
+	*ned_o = ned;
+	return 1;
+}
+
+/* SwAligner::align + the SwDriver loop of nextAlignment calls
+ * (aligner_sw_driver.cpp:1157-1180, aligner_sw.cpp:737-1146) for one problem.
+ * rd/q33: the read as aligned (reverse-complemented when !fw); fw only decides
+ * 5'/3' orientation of edits and trims (AlnRes::invertEdits,
+ * aligner_result.h:822-828, Edit::invertPoss edit.cpp:50-78).
+ * out[7] as orc_sw.  aln: per alignment 10 words {cand, score, off, refoff,
+ * ns, gaps, refns, nedit, trim5p, trim3p}; edits: (pos, type, chr, qchr) x
+ * maxedit per alignment; fates[i] (aligner_sw_nuc.h:83-88).  Returns the
+ * number of alignments. */
+int orc_sw_bt(const uint8_t* rd, const uint8_t* q33, int nrow, const uint8_t* rf, int ncol, int64_t minsc,
+              const orc_scoring* sc, int enable8, int fw, int triml, int corel, int corer, int maxaln,
+              int maxedit, int64_t* out, int64_t* aln, int32_t* edits, int32_t* fates, int capf) {
+	size_t cells = (size_t)nrow * (size_t)ncol;
+	int32_t* mat = (int32_t*)malloc(sizeof(int32_t) * 3 * cells);
+	int64_t* cands = (int64_t*)malloc(sizeof(int64_t) * 3 * (cells + 1));
+	orc_sw(rd, q33, nrow, rf, ncol, minsc, sc, enable8, (int)cells + 1, out, cands, mat);
+	int na = 0;
+	if(out[0]) {
+		int local = sc->local != 0;
+		int variant = local ? (out[2] ? 2 : 3) : (out[2] ? 0 : 1);
+		int64_t offsc = variant == 0 ? -0xff : variant == 1 ? -0x7fff : variant == 2 ? 0 : 0x8000;
+		int64_t* VH = (int64_t*)malloc(sizeof(int64_t) * cells);
+		int64_t* VE = (int64_t*)malloc(sizeof(int64_t) * cells);
+		int64_t* VF = (int64_t*)malloc(sizeof(int64_t) * cells);
+		for(size_t k = 0; k < cells; k++) {
+			VH[k] = mat[3 * k] + offsc; VE[k] = mat[3 * k + 1] + offsc; VF[k] = mat[3 * k + 2] + offsc;
+		}
+		uint8_t* marks = (uint8_t*)calloc(cells, 1);
+		orc_edit* ed = (orc_edit*)malloc(sizeof(orc_edit) * (size_t)(nrow + ncol + 4));
+		orc_btframe* stack = (orc_btframe*)malloc(sizeof(orc_btframe) * (size_t)(nrow + ncol + 4));
+		size_t* cl = (size_t*)malloc(sizeof(size_t) * 2 * (size_t)(nrow + ncol + 4));
+		int64_t* done = (int64_t*)malloc(sizeof(int64_t) * 2 * (size_t)(out[6] + 1));
+		size_t ndone = 0;
+		int nceil = (int)(sc->ncl_const + sc->ncl_lin * (double)nrow);
+		if(nceil < 0) nceil = 0;
+		size_t SQ = (size_t)nrow >> 4;
+		if(SQ == 0) SQ = 1;
+		for(int64_t c = 0; c < out[6]; c++) {
+			size_t row = (size_t)cands[3 * c], col = (size_t)cands[3 * c + 1];
+			int64_t csc = cands[3 * c + 2];
+			int fate;
+			if(csc < minsc) fate = 5;                          /* FILT_SCORE */
+			else if(marks[row * ncol + col]) fate = 3;         /* FILT_START */
+			else {
+				int dom = 0;
+				if(local) {
+					for(size_t i = 0; i < ndone && !dom; i++) {
+						size_t colhi = col, rowhi = row, rowlo = (size_t)done[2 * i], collo = (size_t)done[2 * i + 1];
+						if(colhi < collo) { size_t t = colhi; colhi = collo; collo = t; }
+						if(rowhi < rowlo) { size_t t = rowhi; rowhi = rowlo; rowlo = t; }
+						if(colhi - collo <= SQ && rowhi - rowlo <= SQ) dom = 1;
+					}
+				}
+				if(dom) fate = 4;                               /* FILT_DOMINATED */
+				else {
+					size_t ned = 0;
+					int64_t a[7];
+					int ok = orc_bt_one(VH, VE, VF, marks, rd, q33, nrow, rf, ncol, sc, local, triml, corel, corer,
+					                    nceil, row, col, ed, &ned, a, stack, cl);
+					if(local) { done[2 * ndone] = (int64_t)row; done[2 * ndone + 1] = (int64_t)col; ndone++; }
+					fate = ok ? 1 : 2;
+					if(ok) {
+						if(!fw) {
+							/* invertEdits: reverse, pos = len - pos - (readgap ? 0 : 1) */
+							for(size_t i = 0; i < ned / 2; i++) { orc_edit t = ed[i]; ed[i] = ed[ned - 1 - i]; ed[ned - 1 - i] = t; }
+							/* rdexrows_ = rows left after trimming (aligner_result.cpp:110-117) */
+							int32_t sz = nrow - (int32_t)a[5] - (int32_t)a[6];
+							for(size_t i = 0; i < ned; i++) ed[i].pos = sz - ed[i].pos - (ed[i].type == 1 ? 0 : 1);
+						}
+						if(na < maxaln) {
+							int64_t* o = aln + 10 * (size_t)na;
+							o[0] = c; o[1] = a[0]; o[2] = a[1]; o[3] = a[1]; o[4] = a[2]; o[5] = a[3]; o[6] = a[4];
+							o[7] = (int64_t)ned;
+							o[8] = fw ? a[5] : a[6]; o[9] = fw ? a[6] : a[5];
+							for(size_t e = 0; e < ned && (int)e < maxedit; e++) {
+								int32_t* q = edits + ((size_t)na * maxedit + e) * 4;
+								q[0] = ed[e].pos; q[1] = ed[e].type; q[2] = ed[e].chr; q[3] = ed[e].qchr;
+							}
+						}
+						na++;
+					}
+				}
+			}
+			if(c < capf) fates[c] = fate;
+		}
+		free(VH); free(VE); free(VF); free(marks); free(ed); free(stack); free(cl); free(done);
+	}
+	free(mat); free(cands);
+	return na;
 }

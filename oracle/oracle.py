@@ -57,6 +57,10 @@ class Oracle:
         L.orc_bilf.argtypes = [C.POINTER(OrcEbwt), C.c_uint32, C.c_uint32, C.c_uint32] + [C.c_void_p] * 4
         L.orc_sw.argtypes = [C.c_void_p, C.c_void_p, C.c_int, C.c_void_p, C.c_int, C.c_int64,
                              C.POINTER(OrcScoring), C.c_int, C.c_int, C.c_void_p, C.c_void_p, C.c_void_p]
+        L.orc_sw_bt.restype = C.c_int
+        L.orc_sw_bt.argtypes = [C.c_void_p, C.c_void_p, C.c_int, C.c_void_p, C.c_int, C.c_int64,
+                                C.POINTER(OrcScoring), C.c_int, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int,
+                                C.c_int, C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_int]
 
     def ebwt(self, e, fw=True):
         """Wrap a bt2_index.Ebwt; keeps references alive on the returned struct."""
@@ -119,3 +123,26 @@ class Oracle:
                         _p(out), _p(cands), _p(mat) if want_mat else None)
         nc = int(out[6])
         return out, cands[: 3 * min(nc, cap)].reshape(-1, 3), (mat.reshape(len(rd), ncol, 3) if want_mat else None)
+
+    def sw_bt(self, rd, q33, rfmask, minsc, local, fw=True, triml=0, corel=0, corer=0, enable8=True,
+              maxaln=64, maxedit=256, sc=None):
+        """SwAligner::align + the nextAlignment loop; rd/q33 already oriented (rc
+        when not fw).  Returns (out[7], alns k x 10, [edits k_i x 4], fates) as
+        oracle.ref_harness.RefLib.sw_bt."""
+        rd = np.ascontiguousarray(rd, np.uint8)
+        q33 = np.ascontiguousarray(q33, np.uint8)
+        rf = np.ascontiguousarray(rfmask, np.uint8)
+        ncol = len(rf) - 1
+        out = np.zeros(8, np.int64)
+        aln = np.zeros(10 * maxaln, np.int64)
+        edits = np.zeros(4 * maxaln * maxedit, np.int32)
+        fates = np.zeros(8192, np.int32)
+        sc = sc if sc is not None else scoring(local)
+        na = self.lib.orc_sw_bt(_p(rd), _p(q33), len(rd), _p(rf), ncol, int(minsc), C.byref(sc),
+                                1 if enable8 else 0, 1 if fw else 0, triml, corel, corer, maxaln, maxedit,
+                                _p(out), _p(aln), _p(edits), _p(fates), len(fates))
+        k = min(na, maxaln)
+        aln = aln[:10 * k].reshape(k, 10)
+        ed = edits.reshape(maxaln, maxedit, 4)
+        eds = [ed[i, :min(int(aln[i, 7]), maxedit)].copy() for i in range(k)]
+        return out[:7], aln, eds, fates[:min(int(out[6]), len(fates))].copy()

@@ -98,6 +98,8 @@ struct SwAlignerX : public SwAligner {
 	size_t lastsolcol() const { return lastsolcol_; }
 	bool u8succ() const { return sse8succ_; }
 	bool i16succ() const { return sse16succ_; }
+	size_t cural() const { return cural_; }
+	EList<DpBtCandidate>& candsMut() { return btncand_; }
 	const SSEMatrix& mat(bool u8, bool fw) const {
 		if(u8) return fw ? sseU8fw_.mat_ : sseU8rc_.mat_;
 		return fw ? sseI16fw_.mat_ : sseI16rc_.mat_;
@@ -429,6 +431,78 @@ void bt2ref_one_mm_gated(void* vh, int n, const char** seqs, const char** quals,
 		al.oneMmSearch(h->fw, h->bw, rd, sc, minsc[i], !yfw, !yrc, false, false, true, sr, met);
 		counts[i] = (int32_t)sr.mm1EEHits().size();
 	}
+}
+
+} // extern "C"
+
+// ---- backtrace (row 8a A21) --------------------------------------------------
+extern "C" {
+
+// SwAligner::align followed by the nextAlignment loop of SwDriver::extendSeeds
+// (aligner_sw_driver.cpp:1157-1180: call until done() or an empty result), on a
+// rectangle with the given trim / core diagonals (dp_framer.cpp:116-125).
+// Alignments in the order returned, up to maxaln, 10 words each:
+//   {cand index, score, off (rectangle column of the leftmost aligned ref
+//    char), refoff, ns, gaps, refns, nedit, trim5p(soft), trim3p(soft)}
+// edits[(k*maxedit + e)*4 + {pos, type, chr, qchr}] (ASCII chr/qchr, 5'->3').
+// fates[i] = btncand_[i].fate after the loop (first capf candidates).
+// Returns the number of alignments.
+int bt2ref_sw_bt(const char* seq, const char* qual, int fw, const uint8_t* rfmask, int ncol, int64_t minsc,
+                 const ScoreParams* sp, int enable8, int triml, int corel, int corer, int maxaln, int maxedit,
+                 int64_t* out, int64_t* aln, int32_t* edits, int32_t* fates, int capf) {
+	Scoring sc = makeScoring(*sp);
+	BTDnaString rdfw(seq, true), rdrc;
+	BTString qufw(qual), qurc;
+	rdrc = rdfw; rdrc.reverseComp();
+	qurc = qufw; qurc.reverse();
+	SwAlignerX sw;
+	sw.initRead(rdfw, rdrc, qufw, qurc, 0, rdfw.length(), sc);
+	std::vector<char> rf(ncol + 16, 0);
+	for(int i = 0; i <= ncol; i++) rf[i] = (char)rfmask[i];
+	DPRect rect;
+	rect.refl = 0; rect.refr = ncol - 1; rect.refl_pretrim = -triml; rect.refr_pretrim = ncol - 1;
+	rect.triml = triml; rect.trimr = 0; rect.corel = corel; rect.corer = corer; rect.maxgap = 0;
+	sw.initRef(fw != 0, 0, rect, rf.data(), 0, (size_t)ncol, (TRefOff)ncol + 1000, sc, minsc,
+	           enable8 != 0, 2000, 4, false, true);
+	TAlScore best = std::numeric_limits<TAlScore>::min();
+	bool aligned = sw.align(best);
+	out[0] = aligned ? 1 : 0; out[1] = best;
+	out[2] = sw.u8succ(); out[3] = sw.i16succ();
+	out[4] = (int64_t)sw.colstop(); out[5] = (int64_t)sw.lastsolcol(); out[6] = (int64_t)sw.cands().size();
+	int na = 0;
+	if(aligned) {
+		RandomSource rnd;
+		rnd.init(0);
+		SwResult res;
+		while(!sw.done()) {
+			res.reset();
+			sw.nextAlignment(res, minsc, rnd);
+			if(res.empty()) break;
+			if(na < maxaln) {
+				const AlnRes& a = res.alres;
+				int64_t* o = aln + 10 * (size_t)na;
+				o[0] = (int64_t)sw.cural() - 1;
+				o[1] = a.score().score();
+				o[2] = a.refoff();
+				o[3] = a.refoff();
+				o[4] = a.score().ns();
+				o[5] = a.score().gaps();
+				o[6] = (int64_t)a.refNs();
+				o[7] = (int64_t)a.ned().size();
+				o[8] = (int64_t)a.trimmed5p(true);
+				o[9] = (int64_t)a.trimmed3p(true);
+				for(size_t e = 0; e < a.ned().size() && (int)e < maxedit; e++) {
+					int32_t* q = edits + ((size_t)na * maxedit + e) * 4;
+					q[0] = (int32_t)a.ned()[e].pos; q[1] = a.ned()[e].type;
+					q[2] = a.ned()[e].chr; q[3] = a.ned()[e].qchr;
+				}
+			}
+			na++;
+		}
+		const EList<DpBtCandidate>& c = sw.cands();
+		for(size_t i = 0; i < c.size() && (int)i < capf; i++) fates[i] = c[i].fate;
+	}
+	return na;
 }
 
 } // extern "C"

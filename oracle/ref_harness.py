@@ -56,6 +56,36 @@ class RefLib:
                                 C.POINTER(ScoreParams), C.c_int, C.c_int, C.POINTER(C.c_int64),
                                 C.POINTER(C.c_int64), C.POINTER(C.c_int32)]
 
+    def sw_bt(self, seq, qual, fw, rfmask, minsc, local, triml=0, corel=0, corer=0, enable8=True,
+              maxaln=64, maxedit=256, sp=None):
+        """SwAligner::align + the SwDriver nextAlignment loop.  Returns (out[7],
+        alns (k x 10: cand, score, off, refoff, ns, gaps, refns, nedit, trim5, trim3),
+        edits (list of k arrays (nedit x 4: pos, type, chr, qchr)), fates)."""
+        L = self.lib
+        if not hasattr(self, "_bt_init"):
+            L.bt2ref_sw_bt.restype = C.c_int
+            L.bt2ref_sw_bt.argtypes = [C.c_char_p, C.c_char_p, C.c_int, C.POINTER(C.c_uint8), C.c_int, C.c_int64,
+                                       C.POINTER(ScoreParams), C.c_int, C.c_int, C.c_int, C.c_int, C.c_int,
+                                       C.c_int, C.POINTER(C.c_int64), C.POINTER(C.c_int64),
+                                       C.POINTER(C.c_int32), C.POINTER(C.c_int32), C.c_int]
+            self._bt_init = True
+        rf = np.ascontiguousarray(rfmask, np.uint8)
+        ncol = len(rf) - 1
+        out = np.zeros(8, np.int64)
+        aln = np.zeros(10 * maxaln, np.int64)
+        edits = np.zeros(4 * maxaln * maxedit, np.int32)
+        fates = np.zeros(8192, np.int32)
+        sp = sp if sp is not None else score_params(local)
+        na = L.bt2ref_sw_bt(seq, qual, 1 if fw else 0, _p(rf, C.c_uint8), ncol, int(minsc), C.byref(sp),
+                            1 if enable8 else 0, triml, corel, corer, maxaln, maxedit, _p(out, C.c_int64),
+                            _p(aln, C.c_int64), _p(edits, C.c_int32), _p(fates, C.c_int32), len(fates))
+        k = min(na, maxaln)
+        aln = aln[:10 * k].reshape(k, 10)
+        ed = edits.reshape(maxaln, maxedit, 4)
+        eds = [ed[i, :min(int(aln[i, 7]), maxedit)].copy() for i in range(k)]
+        nc = int(out[6])
+        return out[:7], aln, eds, fates[:min(nc, len(fates))].copy()
+
     def open(self, base):
         return RefIndex(self, base)
 

@@ -96,3 +96,30 @@ def test_sw(orc, fx):
         assert np.array_equal(c, cands), (fx, p)
         n += 1
     assert n > 300
+
+
+def bt_expected(b, p):
+    """Reference alignments of problem p from a sw_bt_* fixture."""
+    a = b["aln"][b["aln_off"][p]:b["aln_off"][p + 1]]
+    eds = [b["edits"][b["edit_off"][k]:b["edit_off"][k + 1]] for k in range(b["aln_off"][p], b["aln_off"][p + 1])]
+    return a, eds, b["fates"][b["fate_off"][p]:b["fate_off"][p + 1]]
+
+
+@pytest.mark.parametrize("src", ["rand_ee", "rand_loc", "log_ee", "log_loc"])
+def test_sw_backtrace(orc, src):
+    """SwAligner::nextAlignment loop (aligner_sw.cpp:737-1146): every alignment,
+    its candidate, score, offset, N/gap counts, soft trims, edits and every
+    candidate's fate equal the reference's."""
+    g, b = load_golden("sw_" + src), load_golden("sw_bt_" + src)
+    local = bool(g["local"])
+    nal = 0
+    for p, rd, q, rf, minsc, fw, out, _ in sw_problems(g):
+        o, a, eds, fates = orc.sw_bt(rd, q, rf, minsc, local, fw, int(b["triml"][p]), int(b["corel"][p]),
+                                     int(b["corer"][p]), maxaln=4096, maxedit=1024)
+        ea, eeds, efates = bt_expected(b, p)
+        assert np.array_equal(o, b["out"][p]), (src, p)
+        assert np.array_equal(a, ea), (src, p)
+        assert all(np.array_equal(x, y) for x, y in zip(eds, eeds)), (src, p)
+        assert np.array_equal(fates, efates), (src, p)
+        nal += len(a)
+    assert nal > 50
