@@ -13,11 +13,13 @@ seams for an unpaired --end-to-end --sensitive read:
                                                Ebwt::getOffset (GroupWalk's job)
   5. one seed-extension DP rectangle per distinct hit diagonal (<= 2 per read),
      150 x 210, end-to-end u8 fill + candidate gather   SwAligner::align
-  A read counts as aligned when it has an exact end-to-end hit or a DP with a
-  valid candidate.  Glue between the stages is torch on the same stream.
+  6. the driver's nextAlignment loop over every candidate of every aligned DP
+     (backtrace, edits, core-diagonal / N-ceiling checks)  SwAligner::nextAlignment
+  A read counts as aligned when it has an exact end-to-end hit or a DP that
+  yields an alignment.  Glue between the stages is device code on the same stream.
 
 The host decision logic of SwDriver (RNG-ranked seed prioritisation, streak
-limits, backtrace, MAPQ, SAM) is not on the GPU path yet; hg38
+limits, MAPQ, SAM) is not on the GPU path; hg38
 cannot be fetched, so the genome is a synthetic one of --genome-mb Mbp with
 planted near-duplicate repeats and N runs, indexed byte-exactly as
 bowtie2-build would (tools/bt2_index.py).
@@ -44,6 +46,8 @@ for _p in (ROOT, PKG, os.path.join(PKG, "tools"), os.path.join(ROOT, "tests", "g
 
 HBM_PEAK_GBS = 8000.0          # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
 SEEDLEN, INTERVAL = 22, 15     # --sensitive, 150 bp: -L 22, -i S,1,1.15 -> 1+1.15*sqrt(150) = 15
+MAXALN, MAXEDIT = 8, 64        # alignments kept per DP (the loop stops there); edits per alignment
+                               # (150 bp, minsc -90, n-ceil 22: <= 22 N + 34 mismatches = 56)
 MAXGAP = 15                    # min(max(read gaps, ref gaps), maxhalf=15), dp_framer.cpp:95-100
 
 
@@ -140,10 +144,18 @@ class Pipeline:
         self.max_probs = 2 * n
         self.probs = torch.zeros((self.max_probs, 5), dtype=torch.int64, device=self.dev)
         _chk = bt2g._chk
-        _chk(self.L.bt2g_reserve_sw(eng.h, self.max_probs, self.ncol))
+        # fill + backtrace scratch: u8 score plane (end-to-end, minsc >= -254)
+        _chk(self.L.bt2g_reserve_sw_bt(eng.h, self.max_probs, length, self.ncol, 1))
         self.sw_cap = 256
         self.res = torch.empty((self.max_probs, 8), dtype=torch.int32, device=self.dev)
         self.cands = torch.empty((self.max_probs, self.sw_cap, 3), dtype=torch.int32, device=self.dev)
+        # seed-extension rectangles: no trim, core diagonals [maxgap, 3*maxgap] (dp_framer.cpp:116-125)
+        self.rects = torch.zeros((self.max_probs, 4), dtype=torch.int32, device=self.dev)
+        self.rects[:, 1], self.rects[:, 2] = MAXGAP, 3 * MAXGAP
+        self.maxaln, self.maxedit = MAXALN, MAXEDIT
+        self.naln = torch.empty(self.max_probs, dtype=torch.int32, device=self.dev)
+        self.alns = torch.empty((self.max_probs, self.maxaln, 10), dtype=torch.int32, device=self.dev)
+        self.edits = torch.empty((self.max_probs, self.maxaln, self.maxedit, 2), dtype=torch.int32, device=self.dev)
         self.stats = {}
 
     def _p(self, t):
@@ -191,11 +203,13 @@ class Pipeline:
                                    P(self.counters[1:]), self.max_probs, S))
         npb = min(int(self.counters[1]), self.max_probs)
         probs = self.probs[:npb]
-        chk(L.bt2g_sw_align_dev(h, P(self.reads), P(self.quals), stride, P(self.lens),
-                                P(probs), npb, None, C.byref(self.sc), 1, self.sw_cap, P(self.res),
-                                P(self.cands), None, None, S))
+        # 7. fill + candidates + the nextAlignment loop (backtraces)
+        chk(L.bt2g_sw_align_bt_dev(h, P(self.reads), P(self.quals), stride, P(self.lens),
+                                   P(probs), npb, None, P(self.rects), C.byref(self.sc), 1, self.sw_cap,
+                                   P(self.res), P(self.cands), self.maxaln, self.maxedit, P(self.naln),
+                                   P(self.alns), P(self.edits), None, S))
         aligned = exact.clone()
-        al = self.res[:npb, 0] == 1
+        al = self.naln[:npb] > 0
         aligned[probs.view(torch.int32)[:, 0][al].to(torch.int64)] = True
         ns = 0
         if keep:
@@ -256,8 +270,8 @@ def cpu_baseline(idx, reads, quals, pipe, sample, threads):
     lib = RefLib()
     L = lib.lib
     L.bt2ref_get_offsets.argtypes = [C.c_void_p, C.c_int, C.c_void_p, C.c_void_p]
-    L.bt2ref_sw_batch.argtypes = [C.c_int, C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p,
-                                  C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p]
+    L.bt2ref_sw_bt_batch.argtypes = [C.c_int, C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p,
+                                     C.c_void_p, C.c_void_p, C.c_void_p, C.c_int, C.c_int, C.c_void_p]
     L.bt2ref_one_mm_gated.argtypes = [C.c_void_p, C.c_int, C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p,
                                       C.c_void_p]
     tmp = tempfile.mkdtemp(prefix="bt2bench_")
@@ -331,9 +345,9 @@ def cpu_baseline(idx, reads, quals, pipe, sample, threads):
         offs = np.ascontiguousarray(rf_off[lo:hi + 1] - 0)
         nc = np.full(k, ncol, np.int32)
         ms = np.full(k, int(-0.6 - 0.6 * pipe.len), np.int64)
-        out = np.zeros((k, 7), np.int64)
-        L.bt2ref_sw_batch(k, cs, cq, fwv.ctypes.data, rf.ctypes.data, offs.ctypes.data, nc.ctypes.data,
-                          ms.ctypes.data, C.byref(sp), out.ctypes.data)
+        out = np.zeros((k, 8), np.int64)
+        L.bt2ref_sw_bt_batch(k, cs, cq, fwv.ctypes.data, rf.ctypes.data, offs.ctypes.data, nc.ctypes.data,
+                             ms.ctypes.data, C.byref(sp), MAXGAP, 3 * MAXGAP, out.ctypes.data)
         return out
 
     def split(total):
@@ -348,8 +362,35 @@ def cpu_baseline(idx, reads, quals, pipe, sample, threads):
     dt = time.perf_counter() - t0
     R.close()
     ex_all = np.concatenate(exs)
-    sw_all = np.concatenate(sws) if sws else np.zeros((0, 7), np.int64)
+    sw_all = np.concatenate(sws) if sws else np.zeros((0, 8), np.int64)
     return dt, ex_all, sw_all, pr
+
+
+def backtrace_parity(pipe, keep, sw_ref):
+    """GPU nextAlignment results of the sampled DPs vs the reference's
+    (bt2ref_sw_bt_batch): alignment count, first alignment (candidate, score,
+    offset, edit count) and a checksum over every alignment's edits.  Counts
+    DPs that differ; DPs that hit maxaln compare their first maxaln only."""
+    import torch
+    npb = pipe.last["npb"]
+    kp = torch.from_numpy(np.nonzero(keep)[0]).to(pipe.dev)
+    naln = pipe.naln[:npb].index_select(0, kp).to(torch.int64)
+    alns = pipe.alns[:npb].index_select(0, kp).to(torch.int64)
+    ed = pipe.edits[:npb].index_select(0, kp)
+    pos = ed[..., 0].to(torch.int64)
+    w = ed[..., 1].to(torch.int64) & 0xFFFFFFFF
+    typ, chr_, qchr = w & 0xFF, (w >> 8) & 0xFF, (w >> 16) & 0xFF
+    k = torch.arange(pipe.maxaln, device=pipe.dev)[None, :, None]
+    e = torch.arange(pipe.maxedit, device=pipe.dev)[None, None, :]
+    live = (k < naln[:, None, None]) & (e < alns[:, :, 6][:, :, None])
+    term = (k + 1) * (pos * 131 + typ * 31 + chr_ * 7 + qchr)
+    ck = (torch.where(live, term, torch.zeros_like(term)).sum((1, 2)) & 0x7FFFFFFFFFFFFFFF).cpu().numpy()
+    naln = naln.cpu().numpy()
+    first = alns[:, 0][:, [0, 1, 2, 6]].cpu().numpy()
+    bad = np.minimum(sw_ref[:, 2], pipe.maxaln) != naln
+    bad |= (naln > 0) & (first != sw_ref[:, 3:7]).any(1)
+    bad |= (naln < pipe.maxaln) & (ck != sw_ref[:, 7])
+    return int(bad.sum())
 
 
 def main():
@@ -423,14 +464,14 @@ def main():
         dist.barrier()
     elapsed = time.perf_counter() - ts
     eng.set_profiling(False)
-    stats = {k: eng.kernel_stats(k) for k in range(5)}
+    stats = {k: eng.kernel_stats(k) for k in range(6)}
     elapsed, n_aligned = combine_ranks(elapsed, n_aligned, dev)
     total_reads = args.reads * args.steps * world
     value = total_reads / elapsed
 
     # ---- roofline of the dominant kernel (per launch, rank 0's view) --------
     last = pipe.last
-    names_k = ["exact_sweep", "seed_search", "one_mm", "get_offset", "sw_align"]
+    names_k = ["exact_sweep", "seed_search", "one_mm", "get_offset", "sw_align", "sw_backtrace"]
     per_launch = {}
     n = args.reads
     sweep_loads = int((pipe.sweep[:, 7].to(torch.int64) & 0xFFFFFFFF).sum())
@@ -441,18 +482,22 @@ def main():
         2: 64 * int(pipe.mm_loads.to(torch.int64).sum()) + 4 * n * args.read_len,
         3: 64 * int(last["loads_off"].to(torch.int64).sum()) + 12 * last["nrows"],
         4: None,
+        5: None,
     }
-    for k in range(5):
+    for k in range(6):
         launches, ms = stats[k]
         if launches:
             per_launch[k] = ms / launches
-    dom = max((k for k in per_launch if k != 4), key=lambda k: per_launch[k])
+    dom = max((k for k in per_launch if k < 4), key=lambda k: per_launch[k])
     achieved = bytes_k[dom] / (per_launch[dom] / 1e3) / 1e9
     sw_cells = last["npb"] * args.read_len * pipe.ncol
     sw_gcups = sw_cells / (per_launch.get(4, float("nan")) / 1e3) / 1e9
     for k in per_launch:
         log(f"[rank {rank}] {names_k[k]:12s} {per_launch[k]:8.3f} ms/launch")
-    log(f"[rank {rank}] SW: {last['npb']} DPs/step, {sw_gcups:.0f} GCUPS; aligned {n_aligned/(args.steps*world*args.reads):.4f}")
+    naln_np = pipe.naln[:last["npb"]].cpu().numpy()
+    bt_stats = {"alignments": int(naln_np.clip(0).sum()), "dps_with_alignment": int((naln_np > 0).sum()),
+                "dps_at_maxaln": int((naln_np >= pipe.maxaln).sum()), "maxaln": pipe.maxaln}
+    log(f"[rank {rank}] SW: {last['npb']} DPs/step, {sw_gcups:.0f} GCUPS; aligned {n_aligned/(args.steps*world*args.reads):.4f}; backtrace {bt_stats}")
 
     # ---- CPU baseline: the reference on the host cores, rank 0, N=1 ---------
     cpu = None
@@ -464,16 +509,19 @@ def main():
             dt, ex_ref, sw_ref, pr = cpu_baseline(idx, reads_np, quals_np, pipe, sample, threads)
             cpu = {"value": sample / dt, "unit": "reads/s", "cores": threads, "kind": "reference",
                    "sample": f"first {sample} reads of the batch through the reference's exactSweep, "
-                             f"gated oneMmSearch, searchAllSeeds, getOffset and SwAligner::align on the "
-                             f"same rows/DP problems ({len(pr)} DPs), {threads} threads"}
+                             f"gated oneMmSearch, searchAllSeeds, getOffset, SwAligner::align and the "
+                             f"nextAlignment loop on the same rows/DP problems ({len(pr)} DPs), {threads} threads"}
             sw_gpu = pipe.sweep[:sample].cpu().numpy().astype(np.int64) & 0xFFFFFFFF
             mism = int((sw_gpu[:, [0, 1, 2, 3, 4, 5]] != ex_ref[:, [0, 1, 3, 4, 5, 6]].astype(np.int64)).any(1).sum())
-            res = pipe.res[:pipe.last["npb"]].cpu().numpy()
+            npb = pipe.last["npb"]
+            res = pipe.res[:npb].cpu().numpy()
             pr_read = pipe.last["probs"].cpu().numpy().view(np.int32)[:, 0]
-            rr = res[pr_read < sample]
-            sw_mism = int((rr[:, 0] != sw_ref[:, 0]).sum() + (rr[:, 6] != sw_ref[:, 6]).sum())
-            parity = {"exact_sweep_mismatch": mism, "sw_mismatch": sw_mism, "reads": sample,
-                      "dps": int(len(sw_ref))}
+            keep = pr_read < sample
+            rr = res[keep]
+            sw_mism = int((rr[:, 0] != sw_ref[:, 0]).sum() + (rr[:, 6] != sw_ref[:, 1]).sum())
+            bt_mism = backtrace_parity(pipe, keep, sw_ref)
+            parity = {"exact_sweep_mismatch": mism, "sw_mismatch": sw_mism, "backtrace_mismatch": bt_mism,
+                      "reads": sample, "dps": int(len(sw_ref)), "ref_alignments": int(sw_ref[:, 2].sum())}
             log(f"[rank 0] cpu baseline {sample/dt:.0f} reads/s on {threads} threads ({dt:.1f}s); parity {parity}")
         except Exception as e:  # the reference build is optional on the box
             log(f"[rank 0] cpu baseline unavailable: {e!r}")
@@ -499,6 +547,7 @@ def main():
                             if bytes_k.get(k)},
             "side_loads_per_step": {names_k[k]: (bytes_k[k] // 64) for k in (0, 1, 2, 3) if bytes_k.get(k)},
             "sw_gcups": sw_gcups,
+            "backtrace": bt_stats,
             "cpu_baseline": cpu,
             "parity_sample": parity,
         }

@@ -19,7 +19,7 @@ LIB_PATH = os.environ.get("BT2G_LIB", os.path.join(HERE, "libbt2g.so"))
 
 BT2G_OK = 0
 BT2G_ERR_OVERFLOW = -6
-K_EXACT_SWEEP, K_SEED_SEARCH, K_ONE_MM, K_GET_OFFSET, K_SW_ALIGN = range(5)
+K_EXACT_SWEEP, K_SEED_SEARCH, K_ONE_MM, K_GET_OFFSET, K_SW_ALIGN, K_SW_BACKTRACE = range(6)
 
 
 class Scoring(C.Structure):
@@ -41,6 +41,10 @@ SWPROB_DTYPE = np.dtype([("read", "<u4"), ("fw", "<i4"), ("refl", "<i8"), ("win_
 SWRES_DTYPE = np.dtype([("aligned", "<i4"), ("best", "<i4"), ("u8succ", "<i4"), ("i16succ", "<i4"),
                         ("colstop", "<i4"), ("lastsolcol", "<i4"), ("ncand", "<i4"), ("flag", "<i4")])
 SWCAND_DTYPE = np.dtype([("row", "<i4"), ("col", "<i4"), ("score", "<i4")])
+SWRECT_DTYPE = np.dtype([("triml", "<i4"), ("corel", "<i4"), ("corer", "<i4"), ("pad", "<i4")])
+SWALN_DTYPE = np.dtype([(n, "<i4") for n in ("cand", "score", "off", "ns", "gaps", "refns", "nedit", "trim5p",
+                                             "trim3p", "pad")])
+EDIT_DTYPE = np.dtype([("pos", "<u4"), ("type", "u1"), ("chr", "u1"), ("qchr", "u1"), ("pad", "u1")])
 
 
 class EbwtMem(C.Structure):
@@ -99,6 +103,11 @@ def lib():
                                     vp, vp]
         L.bt2g_sw_align_dev.argtypes = [vp, vp, vp, u32, vp, vp, u32, vp, C.POINTER(Scoring), C.c_int, u32, vp, vp,
                                         vp, vp, vp]
+        L.bt2g_sw_align_bt.argtypes = [vp, vp, vp, u32, vp, vp, u32, vp, u64, vp, C.POINTER(Scoring), C.c_int, u32,
+                                       vp, vp, u32, u32, vp, vp, vp, vp]
+        L.bt2g_sw_align_bt_dev.argtypes = [vp, vp, vp, u32, vp, vp, u32, vp, vp, C.POINTER(Scoring), C.c_int, u32,
+                                           vp, vp, u32, u32, vp, vp, vp, vp, vp]
+        L.bt2g_reserve_sw_bt.argtypes = [vp, u32, u32, u32, C.c_int]
         L.bt2g_set_profiling.argtypes = [vp, C.c_int]
         L.bt2g_kernel_stats.argtypes = [vp, C.c_int, C.POINTER(u64), C.POINTER(C.c_double)]
         L.bt2g_reset_stats.argtypes = [vp]
@@ -234,6 +243,29 @@ class Engine:
                                  _ptr(win), 0 if win is None else win.nbytes, C.byref(sc), int(enable8), cap,
                                  _ptr(res), _ptr(cands), _ptr(mat), _ptr(mat_off)))
         return res, cands, (mat, mat_off)
+
+    def sw_align_bt(self, reads, quals, lens, probs, windows=None, rects=None, local=False, enable8=True,
+                    cap=4096, maxaln=64, maxedit=256, sc=None, want_fates=True):
+        """Fill + the nextAlignment loop (bt2g_sw_align_bt).  Returns res, cands,
+        naln (n), alns (n x maxaln SWALN_DTYPE), edits (n x maxaln x maxedit
+        EDIT_DTYPE), fates (n x cap int8 or None)."""
+        reads, quals, lens = _c(reads, np.uint8), _c(quals, np.uint8), _c(lens, np.uint32)
+        probs = _c(probs, SWPROB_DTYPE)
+        n = len(probs)
+        res = np.zeros(n, SWRES_DTYPE)
+        cands = np.zeros((n, cap), SWCAND_DTYPE)
+        naln = np.zeros(n, np.int32)
+        alns = np.zeros((n, maxaln), SWALN_DTYPE)
+        edits = np.zeros((n, maxaln, maxedit), EDIT_DTYPE)
+        fates = np.zeros((n, cap), np.int8) if want_fates else None
+        win = _c(windows, np.uint8) if windows is not None else None
+        rects = _c(rects, SWRECT_DTYPE) if rects is not None else None
+        sc = scoring(local) if sc is None else sc
+        _chk(lib().bt2g_sw_align_bt(self.h, _ptr(reads), _ptr(quals), reads.shape[1], _ptr(lens), _ptr(probs), n,
+                                    _ptr(win), 0 if win is None else win.nbytes, _ptr(rects), C.byref(sc),
+                                    int(enable8), cap, _ptr(res), _ptr(cands), maxaln, maxedit, _ptr(naln),
+                                    _ptr(alns), _ptr(edits), _ptr(fates)))
+        return res, cands, naln, alns, edits, fates
 
     # ---- measurement -------------------------------------------------------
     def set_profiling(self, on=True):

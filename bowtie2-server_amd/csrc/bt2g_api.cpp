@@ -65,6 +65,11 @@ struct bt2g_ctx {
 	uint32_t* sw_lists = nullptr;
 	uint32_t* sw_counts = nullptr;
 	uint32_t* sw_bnd = nullptr;
+	// persistent backtrace scratch (bt2g_reserve_sw_bt)
+	uint32_t bt_max_prob = 0, bt_max_stride = 0, bt_max_cols = 0;
+	int bt_hbytes = 0;
+	uint8_t* bt_plane = nullptr;
+	uint32_t* bt_marks = nullptr;
 };
 
 namespace {
@@ -488,31 +493,31 @@ static bool sw_packed_ok(const bt2g_scoring& sc, const SwConst& C, const int16_t
 	return C.rdgo >= 0 && C.rdge >= 0 && C.rfgo >= 0 && C.rfge >= 0;
 }
 
-int bt2g_sw_align_dev(bt2g_ctx* c, const uint8_t* reads, const uint8_t* quals, uint32_t stride,
-                      const uint32_t* lens, const bt2g_sw_problem* probs, uint32_t nprob, const uint8_t* windows,
-                      const bt2g_scoring* sc, int enable8, uint32_t cap, bt2g_sw_result* res, bt2g_sw_cand* cands,
-                      int16_t* mat, const uint64_t* mat_off, void* stream) {
-	if(!c || !sc) return fail(BT2G_ERR_ARG, "null argument");
-	if(int rc = check_reads(stride, nprob)) return rc;
-	if(cap == 0 || cap > 8192) return fail(BT2G_ERR_ARG, "cap out of range (1..8192)");
-	if(sc->local && sc->match <= 0) return fail(BT2G_ERR_ARG, "local mode needs a match bonus");
-	if(nprob == 0) return BT2G_OK;
-	hipStream_t st = pick(c, stream);
+// Fill + gather + candidate sort.  plane != NULL (systolic path only): also
+// write the score plane for the backtrace.  maxcol_hint: widest problem when
+// the caller already knows it (0: read the problems back).
+static int sw_align_impl(bt2g_ctx* c, const uint8_t* reads, const uint8_t* quals, uint32_t stride,
+                         const uint32_t* lens, const bt2g_sw_problem* probs, uint32_t nprob, const uint8_t* windows,
+                         const bt2g_scoring* sc, int enable8, uint32_t cap, bt2g_sw_result* res, bt2g_sw_cand* cands,
+                         int16_t* mat, const uint64_t* mat_off, uint8_t* plane, uint64_t hslot, int hbytes,
+                         uint32_t maxcol_hint, hipStream_t st) {
 	SwConst C;
 	sw_fill_consts(*sc, C);
 	// problem lists per fill variant + boundary scratch
 	uint32_t *lists, *counts, *bnd;
 	size_t nblk = (nprob + 63) / 64;
-	uint32_t maxcol = 0;
-	const bool reserved = nprob <= c->sw_max_prob && c->sw_lists;
+	uint32_t maxcol = maxcol_hint;
+	const bool reserved = nprob <= c->sw_max_prob && c->sw_lists && (maxcol == 0 || maxcol <= c->sw_max_cols);
 	if(reserved) {
 		lists = c->sw_lists; counts = c->sw_counts; bnd = c->sw_bnd; maxcol = c->sw_max_cols;
 	} else {
-		// widest problem decides the boundary buffer width (problems live on the device)
-		std::vector<bt2g_sw_problem> hp(nprob);
-		HIPCHK(hipMemcpyAsync(hp.data(), probs, sizeof(bt2g_sw_problem) * nprob, hipMemcpyDeviceToHost, st));
-		HIPCHK(hipStreamSynchronize(st));
-		for(auto& p : hp) maxcol = p.ncol > maxcol ? p.ncol : maxcol;
+		if(maxcol == 0) {
+			// widest problem decides the boundary buffer width (problems live on the device)
+			std::vector<bt2g_sw_problem> hp(nprob);
+			HIPCHK(hipMemcpyAsync(hp.data(), probs, sizeof(bt2g_sw_problem) * nprob, hipMemcpyDeviceToHost, st));
+			HIPCHK(hipStreamSynchronize(st));
+			for(auto& p : hp) maxcol = p.ncol > maxcol ? p.ncol : maxcol;
+		}
 		HIPCHK(hipMallocAsync((void**)&lists, sizeof(uint32_t) * (size_t)nprob * 3, st));
 		HIPCHK(hipMallocAsync((void**)&counts, sizeof(uint32_t) * 8, st));
 		HIPCHK(hipMallocAsync((void**)&bnd, sizeof(uint32_t) * nblk * (size_t)maxcol * 64 * 2, st));
@@ -526,7 +531,7 @@ int bt2g_sw_align_dev(bt2g_ctx* c, const uint8_t* reads, const uint8_t* quals, u
 		const uint32_t S = (stride + 15u) / 16u, lds = (64u / S) * ((maxcol + 1u) | 1u) * 4u;
 		if(sw_packed_ok(*sc, C, mat) && lds <= 65536u) {
 			launch_sw_ee_packed(probs, nprob, reads, quals, stride, lens, windows, c->ref_codes, c->ref_starts, C,
-			                    enable8, cap, maxcol, res, cands, st);
+			                    enable8, cap, maxcol, res, cands, plane, hslot, hbytes, st);
 		} else {
 		launch_sw_partition(probs, nprob, sc->local, enable8, list8, counts + 0, list16, counts + 1, st);
 		int v8 = sc->local ? 2 : 0, v16 = sc->local ? 3 : 1;
@@ -548,6 +553,145 @@ int bt2g_sw_align_dev(bt2g_ctx* c, const uint8_t* reads, const uint8_t* quals, u
 		HIPCHK(hipFreeAsync(counts, st));
 		HIPCHK(hipFreeAsync(bnd, st));
 	}
+	return BT2G_OK;
+}
+
+static int sw_args_ok(const bt2g_scoring* sc, uint32_t cap) {
+	if(!sc) return fail(BT2G_ERR_ARG, "null argument");
+	if(cap == 0 || cap > 8192) return fail(BT2G_ERR_ARG, "cap out of range (1..8192)");
+	if(sc->local && sc->match <= 0) return fail(BT2G_ERR_ARG, "local mode needs a match bonus");
+	return BT2G_OK;
+}
+
+int bt2g_sw_align_dev(bt2g_ctx* c, const uint8_t* reads, const uint8_t* quals, uint32_t stride,
+                      const uint32_t* lens, const bt2g_sw_problem* probs, uint32_t nprob, const uint8_t* windows,
+                      const bt2g_scoring* sc, int enable8, uint32_t cap, bt2g_sw_result* res, bt2g_sw_cand* cands,
+                      int16_t* mat, const uint64_t* mat_off, void* stream) {
+	if(!c) return fail(BT2G_ERR_ARG, "null argument");
+	if(int rc = sw_args_ok(sc, cap)) return rc;
+	if(int rc = check_reads(stride, nprob)) return rc;
+	if(nprob == 0) return BT2G_OK;
+	return sw_align_impl(c, reads, quals, stride, lens, probs, nprob, windows, sc, enable8, cap, res, cands, mat,
+	                     mat_off, nullptr, 0, 0, 0, pick(c, stream));
+}
+
+int bt2g_sw_align_bt_dev(bt2g_ctx* c, const uint8_t* reads, const uint8_t* quals, uint32_t stride,
+                         const uint32_t* lens, const bt2g_sw_problem* probs, uint32_t nprob, const uint8_t* windows,
+                         const bt2g_sw_rect* rects, const bt2g_scoring* sc, int enable8, uint32_t cap,
+                         bt2g_sw_result* res, bt2g_sw_cand* cands, uint32_t maxaln, uint32_t maxedit,
+                         int32_t* naln, bt2g_sw_aln* alns, bt2g_edit* edits, int8_t* fates, void* stream) {
+	if(!c) return fail(BT2G_ERR_ARG, "null argument");
+	if(int rc = sw_args_ok(sc, cap)) return rc;
+	if(int rc = check_reads(stride, nprob)) return rc;
+	if(maxaln == 0 || maxedit == 0 || !naln || !alns || !edits) return fail(BT2G_ERR_ARG, "bad backtrace outputs");
+	if(nprob == 0) return BT2G_OK;
+	hipStream_t st = pick(c, stream);
+	SwConst C;
+	sw_fill_consts(*sc, C);
+	const uint32_t S16 = sw_packed_rows(stride);
+	const bool packed = sw_packed_ok(*sc, C, nullptr);
+	BtArgs a{};
+	std::vector<void*> tmp;
+	auto talloc = [&](void** p, size_t n) -> int {
+		HIPCHK(hipMallocAsync(p, n ? n : 16, st));
+		tmp.push_back(*p);
+		return BT2G_OK;
+	};
+	int kind, rc;
+	uint32_t maxcol = 0, maxrow = stride;
+	const bool reserved = packed && c->bt_plane && nprob <= c->bt_max_prob && stride <= c->bt_max_stride &&
+	                      nprob <= c->sw_max_prob && c->sw_lists && c->bt_max_cols <= c->sw_max_cols;
+	if(reserved) {
+		// the fill marks problems wider than the reservation (flag -3, not aligned)
+		maxcol = c->bt_max_cols;
+		kind = c->bt_hbytes == 1 ? 0 : 1;
+		a.plane = c->bt_plane;
+		a.slot = (uint64_t)S16 * maxcol * (uint64_t)c->bt_hbytes;
+		a.marks = c->bt_marks;
+		maxrow = c->bt_max_stride;
+		if((rc = sw_align_impl(c, reads, quals, stride, lens, probs, nprob, windows, sc, enable8, cap, res, cands,
+		                       nullptr, nullptr, c->bt_plane, a.slot, c->bt_hbytes, maxcol, st)))
+			return rc;
+	} else {
+		std::vector<bt2g_sw_problem> hp(nprob);
+		HIPCHK(hipMemcpyAsync(hp.data(), probs, sizeof(bt2g_sw_problem) * nprob, hipMemcpyDeviceToHost, st));
+		uint32_t nreads = 0;
+		HIPCHK(hipStreamSynchronize(st));
+		bool all8 = enable8 != 0;
+		for(auto& p : hp) {
+			maxcol = p.ncol > maxcol ? p.ncol : maxcol;
+			nreads = p.read + 1 > nreads ? p.read + 1 : nreads;
+			all8 = all8 && p.minsc >= -254;
+		}
+		std::vector<uint32_t> hl(nreads);
+		HIPCHK(hipMemcpyAsync(hl.data(), lens, sizeof(uint32_t) * nreads, hipMemcpyDeviceToHost, st));
+		HIPCHK(hipStreamSynchronize(st));
+		if(packed) {
+			const int hb = all8 ? 1 : 2;
+			kind = hb == 1 ? 0 : 1;
+			a.slot = (uint64_t)S16 * maxcol * (uint64_t)hb;
+			uint8_t* plane;
+			if((rc = talloc((void**)&plane, (size_t)a.slot * nprob))) return rc;
+			a.plane = plane;
+			if((rc = sw_align_impl(c, reads, quals, stride, lens, probs, nprob, windows, sc, enable8, cap, res,
+			                       cands, nullptr, nullptr, plane, a.slot, hb, maxcol, st)))
+				return rc;
+		} else {
+			// generic fills: H,E,F int16 matrices per problem
+			kind = 2;
+			std::vector<uint64_t> off(nprob);
+			uint64_t tot = 0;
+			for(uint32_t i = 0; i < nprob; i++) {
+				off[i] = tot;
+				tot += (uint64_t)hl[hp[i].read] * hp[i].ncol * 3;
+			}
+			int16_t* mat;
+			uint64_t* moff;
+			if((rc = talloc((void**)&mat, (size_t)tot * 2)) || (rc = talloc((void**)&moff, sizeof(uint64_t) * nprob)))
+				return rc;
+			HIPCHK(hipMemcpyAsync(moff, off.data(), sizeof(uint64_t) * nprob, hipMemcpyHostToDevice, st));
+			a.mat = mat;
+			a.mat_off = moff;
+			if((rc = sw_align_impl(c, reads, quals, stride, lens, probs, nprob, windows, sc, enable8, cap, res,
+			                       cands, mat, moff, nullptr, 0, 0, maxcol, st)))
+				return rc;
+			HIPCHK(hipStreamSynchronize(st));   // keep `off` alive until the copy is done
+		}
+		maxrow = 0;
+		for(uint32_t i = 0; i < nreads; i++) maxrow = hl[i] > maxrow ? hl[i] : maxrow;
+	}
+	a.mwords = sw_bt_mwords(maxcol);
+	a.mrows = maxrow;
+	a.mslot = sw_bt_mslot(maxrow, maxcol);
+	if(!a.marks && (rc = talloc((void**)&a.marks, sizeof(uint32_t) * a.mslot * nprob))) return rc;
+	if(sc->local && (rc = talloc((void**)&a.done, sizeof(int2) * (size_t)cap * nprob))) return rc;
+	a.probs = probs; a.nprob = nprob; a.reads = reads; a.quals = quals; a.stride = stride; a.lens = lens;
+	a.windows = windows; a.ref_codes = c->ref_codes; a.ref_starts = c->ref_starts; a.rects = rects;
+	a.res = res; a.cands = cands; a.cap = cap; a.cstride = S16;
+	a.C = C; a.local = sc->local; a.ncl_const = sc->ncl_const; a.ncl_lin = sc->ncl_lin;
+	a.maxaln = maxaln; a.maxedit = maxedit; a.naln = naln; a.alns = alns; a.edits = edits; a.fates = fates;
+	{
+		ProfScope ps(c, 5, st);
+		launch_sw_bt(kind, a, st);
+	}
+	HIPCHK(hipGetLastError());
+	for(void* p : tmp) HIPCHK(hipFreeAsync(p, st));
+	return BT2G_OK;
+}
+
+int bt2g_reserve_sw_bt(bt2g_ctx* c, uint32_t max_problems, uint32_t max_stride, uint32_t max_cols, int hbytes) {
+	if(!c || max_problems == 0 || max_cols == 0 || max_stride == 0 || (hbytes != 1 && hbytes != 2))
+		return fail(BT2G_ERR_ARG, "bad reservation");
+	if(int rc = bt2g_reserve_sw(c, max_problems, max_cols)) return rc;
+	if(c->bt_plane) { (void)hipFree(c->bt_plane); (void)hipFree(c->bt_marks); }
+	c->bt_plane = nullptr; c->bt_marks = nullptr;
+	const uint64_t slot = (uint64_t)sw_packed_rows(max_stride) * max_cols * (uint64_t)hbytes;
+	HIPCHK(hipMalloc((void**)&c->bt_plane, slot * max_problems));
+	HIPCHK(hipMalloc((void**)&c->bt_marks, sizeof(uint32_t) * sw_bt_mslot(max_stride, max_cols) * max_problems));
+	c->bt_max_prob = max_problems;
+	c->bt_max_stride = max_stride;
+	c->bt_max_cols = max_cols;
+	c->bt_hbytes = hbytes;
 	return BT2G_OK;
 }
 
@@ -716,6 +860,57 @@ int bt2g_sw_align(bt2g_ctx* c, const uint8_t* reads, const uint8_t* quals, uint3
 	HIPCHK(hipStreamSynchronize(c->stream));
 	if((rc = down(res, dres, nprob)) || (rc = down(cands, dc, (size_t)nprob * cap))) return rc;
 	if(mat && (rc = down(mat, dm, matn))) return rc;
+	for(uint32_t i = 0; i < nprob; i++)
+		if(res[i].ncand > (int32_t)cap) return fail(BT2G_ERR_OVERFLOW, "problem %u: %d candidates > cap %u", i,
+		                                             res[i].ncand, cap);
+	return BT2G_OK;
+}
+
+}  // extern "C"
+
+extern "C" {
+
+int bt2g_sw_align_bt(bt2g_ctx* c, const uint8_t* reads, const uint8_t* quals, uint32_t stride,
+                     const uint32_t* lens, const bt2g_sw_problem* probs, uint32_t nprob, const uint8_t* windows,
+                     uint64_t windows_len, const bt2g_sw_rect* rects, const bt2g_scoring* sc, int enable8,
+                     uint32_t cap, bt2g_sw_result* res, bt2g_sw_cand* cands, uint32_t maxaln, uint32_t maxedit,
+                     int32_t* naln, bt2g_sw_aln* alns, bt2g_edit* edits, int8_t* fates) {
+	if(!c) return fail(BT2G_ERR_ARG, "null ctx");
+	HIPCHK(hipSetDevice(c->device));
+	if(nprob == 0) return BT2G_OK;
+	uint32_t nreads = 0;
+	for(uint32_t i = 0; i < nprob; i++) nreads = probs[i].read + 1 > nreads ? probs[i].read + 1 : nreads;
+	Tmp t;
+	uint8_t *dr, *dq, *dw = nullptr;
+	uint32_t* dl;
+	bt2g_sw_problem* dp;
+	bt2g_sw_rect* drc = nullptr;
+	bt2g_sw_result* dres;
+	bt2g_sw_cand* dc;
+	int32_t* dna;
+	bt2g_sw_aln* dal;
+	bt2g_edit* ded;
+	int8_t* dft = nullptr;
+	int rc;
+	const size_t na = (size_t)nprob * maxaln;
+	if((rc = t.up(&dr, reads, (size_t)nreads * stride)) || (rc = t.up(&dq, quals, (size_t)nreads * stride)) ||
+	   (rc = t.up(&dl, lens, nreads)) || (rc = t.up(&dp, probs, nprob)) ||
+	   (rc = t.up(&dres, (const bt2g_sw_result*)nullptr, nprob)) ||
+	   (rc = t.up(&dc, (const bt2g_sw_cand*)nullptr, (size_t)nprob * cap)) ||
+	   (rc = t.up(&dna, (const int32_t*)nullptr, nprob)) || (rc = t.up(&dal, (const bt2g_sw_aln*)nullptr, na)) ||
+	   (rc = t.up(&ded, (const bt2g_edit*)nullptr, na * maxedit)))
+		return rc;
+	if(windows && windows_len && (rc = t.up(&dw, windows, windows_len))) return rc;
+	if(rects && (rc = t.up(&drc, rects, nprob))) return rc;
+	if(fates && (rc = t.up(&dft, (const int8_t*)nullptr, (size_t)nprob * cap))) return rc;
+	if((rc = bt2g_sw_align_bt_dev(c, dr, dq, stride, dl, dp, nprob, dw, drc, sc, enable8, cap, dres, dc, maxaln,
+	                              maxedit, dna, dal, ded, dft, c->stream)))
+		return rc;
+	HIPCHK(hipStreamSynchronize(c->stream));
+	if((rc = down(res, dres, nprob)) || (rc = down(cands, dc, (size_t)nprob * cap)) || (rc = down(naln, dna, nprob)) ||
+	   (rc = down(alns, dal, na)) || (rc = down(edits, ded, na * maxedit)))
+		return rc;
+	if(fates && (rc = down(fates, dft, (size_t)nprob * cap))) return rc;
 	for(uint32_t i = 0; i < nprob; i++)
 		if(res[i].ncand > (int32_t)cap) return fail(BT2G_ERR_OVERFLOW, "problem %u: %d candidates > cap %u", i,
 		                                             res[i].ncand, cap);

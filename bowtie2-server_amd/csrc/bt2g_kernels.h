@@ -49,6 +49,50 @@ void launch_sw_fill(int variant, const bt2g_sw_problem* probs, uint32_t nprob, c
 void launch_sw_ee_packed(const bt2g_sw_problem* probs, uint32_t nprob, const uint8_t* reads, const uint8_t* quals,
                          uint32_t stride, const uint32_t* lens, const uint8_t* windows, const uint8_t* ref_codes,
                          const uint64_t* ref_starts, const SwConst& C, int enable8, uint32_t cap, uint32_t max_cols,
-                         bt2g_sw_result* res, bt2g_sw_cand* cands, hipStream_t st);
+                         bt2g_sw_result* res, bt2g_sw_cand* cands, uint8_t* plane, uint64_t hslot, int hbytes,
+                         hipStream_t st);
+// Rows per strip stack of the systolic fill (its score-plane column stride).
+inline uint32_t sw_packed_rows(uint32_t stride) { return 16u * ((stride + 15u) / 16u); }
+
+// Backtrace (sw_backtrace.hip): one lane per problem.
+struct BtArgs {
+	const bt2g_sw_problem* probs;
+	uint32_t nprob;
+	const uint8_t* reads;
+	const uint8_t* quals;
+	uint32_t stride;
+	const uint32_t* lens;
+	const uint8_t* windows;
+	const uint8_t* ref_codes;
+	const uint64_t* ref_starts;
+	const bt2g_sw_rect* rects;        // may be null
+	const bt2g_sw_result* res;
+	const bt2g_sw_cand* cands;
+	uint32_t cap;
+	const uint8_t* plane;             // kinds 0/1: systolic score plane
+	uint64_t slot;                    //   bytes per problem
+	uint32_t cstride;                 //   rows per column
+	const int16_t* mat;               // kind 2: H,E,F triples
+	const uint64_t* mat_off;
+	uint32_t* marks;                  // per problem (mslot words): reportedThrough bitmap of
+	uint64_t mslot;                   //   mrows x mwords words, then mrows first-walk intervals
+	uint32_t mwords, mrows;
+	int2* done;                       // local mode: cap (row, col) per problem
+	SwConst C;
+	int local;
+	double ncl_const, ncl_lin;
+	uint32_t maxaln, maxedit;
+	int32_t* naln;
+	bt2g_sw_aln* alns;
+	bt2g_edit* edits;
+	int8_t* fates;                    // may be null
+};
+// kind: 0 u8 score plane, 1 u16 score plane, 2 generic H,E,F matrices
+void launch_sw_bt(int kind, const BtArgs& a, hipStream_t st);
+// words of backtrace mark scratch per problem of <= rows x cols
+inline uint32_t sw_bt_mwords(uint32_t cols) { return (((cols + 31u) / 32u) + 3u) & ~3u; }
+inline uint64_t sw_bt_mslot(uint32_t rows, uint32_t cols) {
+	return (((uint64_t)rows * sw_bt_mwords(cols) + rows) + 3u) & ~(uint64_t)3u;
+}
 void launch_sort_cands(const bt2g_sw_result* res, bt2g_sw_cand* cands, uint32_t nprob, uint32_t cap,
                        uint32_t* big, uint32_t* nbig, hipStream_t st);

@@ -83,13 +83,17 @@ struct Half {
 #ifndef BT2G_SW_WAVES
 #define BT2G_SW_WAVES 3
 #endif
-template <bool SAMEGO>
+// STORE: also write every cell's H to the score plane for the backtrace
+// (sw_backtrace.hip): problem pi's column j, stack rows 16k..16k+15 at
+// plane + pi*hslot + (j*16S + 16k)*hbytes; hbytes 1 keeps u8 fills only.
+template <bool SAMEGO, bool STORE>
 __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(BT2G_SW_WAVES)))
 k_sw_ee_sys(const bt2g_sw_problem* __restrict__ probs, uint32_t nprob, const uint8_t* __restrict__ reads,
             const uint8_t* __restrict__ quals, uint32_t stride, const uint32_t* __restrict__ lens,
             const uint8_t* __restrict__ windows, const uint8_t* __restrict__ ref_codes,
             const uint64_t* __restrict__ ref_starts, SwConst C, int enable8, uint32_t cap, uint32_t max_cols,
-            uint32_t S, uint32_t ldsw, bt2g_sw_result* __restrict__ res, bt2g_sw_cand* __restrict__ cands) {
+            uint32_t S, uint32_t ldsw, bt2g_sw_result* __restrict__ res, bt2g_sw_cand* __restrict__ cands,
+            uint8_t* __restrict__ plane, uint64_t hslot, int hbytes) {
 	const uint32_t lane = threadIdx.x;
 	const uint32_t G = 64u / S;                  // problem pairs per wave
 	const uint32_t g = lane / S, k = lane % S;
@@ -401,6 +405,42 @@ k_sw_ee_sys(const bt2g_sw_problem* __restrict__ probs, uint32_t nprob, const uin
 		};
 		if(__ballot(nfloor != 0)) rows(std::true_type{});
 		else rows(std::false_type{});
+		if(STORE && in_group) {
+			const bool s0 = h[0].live && (uint32_t)j < h[0].ncol, s1 = h[1].live && (uint32_t)j < h[1].ncol;
+			const size_t cell = (size_t)j * (16u * S) + 16u * k;
+			if(hbytes == 1) {
+				// bytes of 16 rows per problem: low halves -> a, high halves -> b
+				uint32_t a[4], b[4];
+#pragma unroll
+				for(int qd = 0; qd < 4; qd++) {
+					const uint32_t y0 = __builtin_amdgcn_perm(Hc[4 * qd + 1], Hc[4 * qd], 0x06020400u);
+					const uint32_t y1 = __builtin_amdgcn_perm(Hc[4 * qd + 3], Hc[4 * qd + 2], 0x06020400u);
+					a[qd] = __builtin_amdgcn_perm(y1, y0, 0x05040100u);
+					b[qd] = __builtin_amdgcn_perm(y1, y0, 0x07060302u);
+				}
+				if(s0 && h[0].row0 == 0xffu)
+					*(uint4*)(plane + (size_t)h[0].pi * hslot + cell) = make_uint4(a[0], a[1], a[2], a[3]);
+				if(s1 && h[1].row0 == 0xffu)
+					*(uint4*)(plane + (size_t)h[1].pi * hslot + cell) = make_uint4(b[0], b[1], b[2], b[3]);
+			} else {
+				uint32_t a[8], b[8];
+#pragma unroll
+				for(int i = 0; i < 8; i++) {
+					a[i] = __builtin_amdgcn_perm(Hc[2 * i + 1], Hc[2 * i], 0x05040100u);
+					b[i] = __builtin_amdgcn_perm(Hc[2 * i + 1], Hc[2 * i], 0x07060302u);
+				}
+				if(s0) {
+					uint4* d = (uint4*)(plane + (size_t)h[0].pi * hslot + cell * 2u);
+					d[0] = make_uint4(a[0], a[1], a[2], a[3]);
+					d[1] = make_uint4(a[4], a[5], a[6], a[7]);
+				}
+				if(s1) {
+					uint4* d = (uint4*)(plane + (size_t)h[1].pi * hslot + cell * 2u);
+					d[0] = make_uint4(b[0], b[1], b[2], b[3]);
+					d[1] = make_uint4(b[4], b[5], b[6], b[7]);
+				}
+			}
+		}
 		hout = Hc[R - 1];        // the strip's bottom row at column j (== hprev when !SAMEGO)
 		fout = fprev;
 		// the bottom lane is the last reader of column j's selector: the slot now
@@ -456,17 +496,23 @@ k_sw_ee_sys(const bt2g_sw_problem* __restrict__ probs, uint32_t nprob, const uin
 void launch_sw_ee_packed(const bt2g_sw_problem* probs, uint32_t nprob, const uint8_t* reads, const uint8_t* quals,
                          uint32_t stride, const uint32_t* lens, const uint8_t* windows, const uint8_t* ref_codes,
                          const uint64_t* ref_starts, const SwConst& C, int enable8, uint32_t cap, uint32_t max_cols,
-                         bt2g_sw_result* res, bt2g_sw_cand* cands, hipStream_t st) {
+                         bt2g_sw_result* res, bt2g_sw_cand* cands, uint8_t* plane, uint64_t hslot, int hbytes,
+                         hipStream_t st) {
 	if(nprob == 0) return;
 	const uint32_t S = (stride + 15u) / 16u;     // <= 64 (stride <= BT2G_MAX_READ_LEN)
 	const uint32_t per_wave = 2u * (64u / S);
 	const uint32_t ldsw = (max_cols + 1u) | 1u;   // >= ncol+1 (column pairs); odd: groups hit different banks
 	const dim3 grid((nprob + per_wave - 1) / per_wave), block(64);
 	const size_t lds = (per_wave / 2) * ldsw * sizeof(uint32_t);
-	if(C.rdgo == C.rfgo)
-		hipLaunchKernelGGL(k_sw_ee_sys<true>, grid, block, lds, st, probs, nprob, reads, quals, stride, lens, windows,
-		                   ref_codes, ref_starts, C, enable8, cap, max_cols, S, ldsw, res, cands);
-	else
-		hipLaunchKernelGGL(k_sw_ee_sys<false>, grid, block, lds, st, probs, nprob, reads, quals, stride, lens,
-		                   windows, ref_codes, ref_starts, C, enable8, cap, max_cols, S, ldsw, res, cands);
+#define BT2G_SYS(SG, STO)                                                                                     \
+	hipLaunchKernelGGL((k_sw_ee_sys<SG, STO>), grid, block, lds, st, probs, nprob, reads, quals, stride, lens, \
+	                   windows, ref_codes, ref_starts, C, enable8, cap, max_cols, S, ldsw, res, cands, plane, hslot, \
+	                   hbytes)
+	const bool samego = C.rdgo == C.rfgo;
+	if(plane) {
+		if(samego) BT2G_SYS(true, true); else BT2G_SYS(false, true);
+	} else {
+		if(samego) BT2G_SYS(true, false); else BT2G_SYS(false, false);
+	}
+#undef BT2G_SYS
 }

@@ -220,6 +220,71 @@ int bt2g_sw_align_dev(bt2g_ctx* ctx, const uint8_t* reads, const uint8_t* quals,
  * wider than max_cols then fail with result.flag = -3). */
 int bt2g_reserve_sw(bt2g_ctx* ctx, uint32_t max_problems, uint32_t max_cols);
 
+/* ---- SW backtrace (row A21) ------------------------------------------------ */
+
+/* The DPRect fields the backtrace reads (dp_framer.h:62-93): columns trimmed
+ * off the rectangle's left end and the inclusive range of "core" diagonals
+ * (offsets from the untrimmed left end) an alignment must touch
+ * (aligner_swsse_ee_u8.cpp:1764-1800).  Seed extension: corel = maxgap,
+ * corer = 3*maxgap (dp_framer.cpp:116-125). */
+typedef struct {
+	int32_t triml, corel, corer, pad;
+} bt2g_sw_rect;
+
+/* One alignment returned by SwAligner::nextAlignment (aligner_sw.cpp:737-1146):
+ * the SwResult/AlnRes fields that SAM output needs. */
+typedef struct {
+	int32_t cand;     /* index of the candidate cell in the sorted list (cural_) */
+	int32_t score;    /* AlnScore::score_ */
+	int32_t off;      /* rectangle column of the leftmost aligned reference char
+	                     (reference offset = problem.refl + off) */
+	int32_t ns;       /* AlnScore::ns_: read or reference Ns aligned */
+	int32_t gaps;     /* AlnScore::gaps_ */
+	int32_t refns;    /* AlnRes::refns_ */
+	int32_t nedit;    /* edits in the alignment (> maxedit: only maxedit stored) */
+	int32_t trim5p;   /* soft trimming (local mode), AlnRes::trimmed5p(true) */
+	int32_t trim3p;
+	int32_t pad;
+} bt2g_sw_aln;
+
+/* Edit (edit.h:58-110): pos from the read's 5' end after trimming; type 1 =
+ * read gap, 2 = reference gap, 3 = mismatch; chr / qchr ASCII ('-' for gaps,
+ * IUPAC mask2dna for reference masks). */
+typedef struct {
+	uint32_t pos;
+	uint8_t  type, chr, qchr, pad;
+} bt2g_edit;
+
+/* SwAligner::align followed by the driver's loop of nextAlignment calls
+ * (aligner_sw_driver.cpp:1157-1180: until done() or an empty result) for every
+ * problem: the fill and candidates of bt2g_sw_align plus every alignment, in
+ * the order the reference returns them.  rects may be NULL (triml 0, every
+ * diagonal core).  Per problem p: naln[p] alignments at alns[p*maxaln ..]
+ * (the loop stops after maxaln; naln[p] = -4 if the problem needs an i16
+ * matrix but the reservation holds u8 only), edits of alignment k at
+ * edits[(p*maxaln + k)*maxedit ..]; fates (optional, NULL to skip):
+ * DpBtCandidate::fate of each candidate (aligner_sw_nuc.h:83-88) at
+ * fates[p*cap ..].  Candidates below the problem's minsc are skipped
+ * (FILT_SCORE) exactly as nextAlignment(minsc) does; a caller that tightens
+ * minsc between calls (aligner_sw_driver.cpp:1252-1290) truncates the list,
+ * since candidates are sorted by score. */
+int bt2g_sw_align_bt(bt2g_ctx* ctx, const uint8_t* reads, const uint8_t* quals, uint32_t stride,
+                     const uint32_t* lens, const bt2g_sw_problem* probs, uint32_t nprob, const uint8_t* windows,
+                     uint64_t windows_len, const bt2g_sw_rect* rects, const bt2g_scoring* sc, int enable8,
+                     uint32_t cap, bt2g_sw_result* res, bt2g_sw_cand* cands, uint32_t maxaln, uint32_t maxedit,
+                     int32_t* naln, bt2g_sw_aln* alns, bt2g_edit* edits, int8_t* fates);
+int bt2g_sw_align_bt_dev(bt2g_ctx* ctx, const uint8_t* reads, const uint8_t* quals, uint32_t stride,
+                         const uint32_t* lens, const bt2g_sw_problem* probs, uint32_t nprob, const uint8_t* windows,
+                         const bt2g_sw_rect* rects, const bt2g_scoring* sc, int enable8, uint32_t cap,
+                         bt2g_sw_result* res, bt2g_sw_cand* cands, uint32_t maxaln, uint32_t maxedit,
+                         int32_t* naln, bt2g_sw_aln* alns, bt2g_edit* edits, int8_t* fates, void* stream);
+
+/* Reserve the backtrace scratch (score plane + reportedThrough bits) for up to
+ * max_problems problems of <= max_rows x max_cols, so bt2g_sw_align_bt_dev
+ * neither allocates nor synchronises.  hbytes = 1 holds u8 fills only (end-to-end
+ * with enable8 and minsc >= -254, the default 150 bp case), 2 holds any. */
+int bt2g_reserve_sw_bt(bt2g_ctx* ctx, uint32_t max_problems, uint32_t max_rows, uint32_t max_cols, int hbytes);
+
 /* ---- bench batch glue (NOT reference seams) -------------------------------
  * Device-side glue used by bench.py between the seed-phase calls and
  * bt2g_sw_align_dev.  The reference's SwDriver::extendSeeds chooses hits with
@@ -255,7 +320,7 @@ int bt2g_bench_frame_dev(uint32_t n, const uint32_t* lens, const uint32_t* offs,
 /* ---- measurement --------------------------------------------------------- */
 /* Kernel timing with HIP events on the launch stream (off by default). */
 int bt2g_set_profiling(bt2g_ctx* ctx, int on);
-/* kernel ids: 0 exact_sweep, 1 seed_search, 2 one_mm, 3 get_offset, 4 sw_align */
+/* kernel ids: 0 exact_sweep, 1 seed_search, 2 one_mm, 3 get_offset, 4 sw_align, 5 sw_backtrace */
 int bt2g_kernel_stats(bt2g_ctx* ctx, int kernel, uint64_t* launches, double* total_ms);
 int bt2g_reset_stats(bt2g_ctx* ctx);
 

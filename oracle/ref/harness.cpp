@@ -506,3 +506,71 @@ int bt2ref_sw_bt(const char* seq, const char* qual, int fw, const uint8_t* rfmas
 }
 
 } // extern "C"
+
+// ---- batch backtrace for bench.py's cpu_baseline leg -------------------------
+extern "C" {
+
+// As bt2ref_sw_batch plus the SwDriver nextAlignment loop on every aligned
+// problem (seed-extension rectangle: triml 0, core diagonals [corel, corer]).
+// out: n x 8 = {aligned, ncand, naln, cand0, score0, off0, nedit0, edit checksum}
+// with the checksum over all alignments k and their edits e:
+//   sum (k+1) * (pos*131 + type*31 + chr*7 + qchr)   (mod 2^63)
+void bt2ref_sw_bt_batch(int n, const char** seqs, const char** quals, const uint8_t* fws, const uint8_t* rf,
+                        const int64_t* rf_off, const int32_t* ncols, const int64_t* minsc, const ScoreParams* sp,
+                        int corel, int corer, int64_t* out) {
+	Scoring sc = makeScoring(*sp);
+	SwAlignerX sw;
+	BTDnaString rdfw, rdrc;
+	BTString qufw, qurc;
+	std::vector<char> buf;
+	const char* last = nullptr;
+	RandomSource rnd;
+	rnd.init(0);
+	SwResult res;
+	for(int i = 0; i < n; i++) {
+		if(seqs[i] != last) {
+			rdfw.install(seqs[i], true);
+			rdrc = rdfw; rdrc.reverseComp();
+			qufw.install(quals[i]);
+			qurc = qufw; qurc.reverse();
+			sw.initRead(rdfw, rdrc, qufw, qurc, 0, rdfw.length(), sc);
+			last = seqs[i];
+		}
+		int ncol = ncols[i];
+		buf.assign(rf + rf_off[i], rf + rf_off[i] + ncol + 1);
+		buf.resize(ncol + 16, 0);
+		DPRect rect;
+		rect.refl = 0; rect.refr = ncol - 1; rect.refl_pretrim = 0; rect.refr_pretrim = ncol - 1;
+		rect.triml = rect.trimr = 0; rect.corel = corel; rect.corer = corer; rect.maxgap = 0;
+		sw.initRef(fws[i] != 0, 0, rect, buf.data(), 0, (size_t)ncol, (TRefOff)ncol + 1000, sc, minsc[i],
+		           true, 2000, 4, false, true);
+		TAlScore best = std::numeric_limits<TAlScore>::min();
+		bool aligned = sw.align(best);
+		int64_t* o = out + 8 * (size_t)i;
+		memset(o, 0, 8 * sizeof(int64_t));
+		o[0] = aligned; o[1] = (int64_t)sw.cands().size();
+		if(!aligned) continue;
+		int64_t na = 0;
+		uint64_t ck = 0;
+		while(!sw.done()) {
+			res.reset();
+			sw.nextAlignment(res, minsc[i], rnd);
+			if(res.empty()) break;
+			const AlnRes& a = res.alres;
+			if(na == 0) {
+				o[3] = (int64_t)sw.cural() - 1; o[4] = a.score().score(); o[5] = a.refoff();
+				o[6] = (int64_t)a.ned().size();
+			}
+			for(size_t e = 0; e < a.ned().size(); e++) {
+				const Edit& ed = a.ned()[e];
+				ck += (uint64_t)(na + 1) * ((uint64_t)ed.pos * 131 + (uint64_t)ed.type * 31 +
+				                            (uint64_t)ed.chr * 7 + (uint64_t)ed.qchr);
+			}
+			na++;
+		}
+		o[2] = na;
+		o[7] = (int64_t)(ck & 0x7fffffffffffffffULL);
+	}
+}
+
+} // extern "C"

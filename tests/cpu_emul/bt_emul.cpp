@@ -1,0 +1,32 @@
+// tests/cpu_emul/bt_emul.cpp -- TEST INFRASTRUCTURE ONLY.
+// Runs the backtrace kernel of bowtie2-server_amd/csrc/sw_backtrace.hip (the
+// same source file, compiled for the host against stub/hip/hip_runtime.h)
+// over a batch on the CPU, so tests/test_bt_emul.py can check its indexing and
+// its results against the oracle without a GPU.  The product never uses this.
+#include "../../bowtie2-server_amd/csrc/sw_backtrace.hip"
+#include <string.h>
+
+thread_local uint3v threadIdx, blockIdx;
+
+extern "C" int bt_emul_run(int kind, const bt2g_sw_problem* probs, uint32_t nprob, const uint8_t* reads,
+                           const uint8_t* quals, uint32_t stride, const uint32_t* lens, const uint8_t* windows,
+                           const bt2g_sw_rect* rects, const bt2g_sw_result* res, const bt2g_sw_cand* cands,
+                           uint32_t cap, const uint8_t* plane, uint64_t slot, uint32_t cstride, const int16_t* mat,
+                           const uint64_t* mat_off, uint32_t maxrow, uint32_t maxcol, const SwConst* C, int local,
+                           double ncl_const, double ncl_lin, uint32_t maxaln, uint32_t maxedit, int32_t* naln,
+                           bt2g_sw_aln* alns, bt2g_edit* edits, int8_t* fates) {
+	BtArgs a{};
+	a.probs = probs; a.nprob = nprob; a.reads = reads; a.quals = quals; a.stride = stride; a.lens = lens;
+	a.windows = windows; a.ref_codes = nullptr; a.ref_starts = nullptr; a.rects = rects;
+	a.res = res; a.cands = cands; a.cap = cap; a.plane = plane; a.slot = slot; a.cstride = cstride;
+	a.mat = mat; a.mat_off = mat_off;
+	a.mwords = sw_bt_mwords(maxcol); a.mrows = maxrow; a.mslot = sw_bt_mslot(maxrow, maxcol);
+	// garbage-filled scratch: the kernel must not rely on zeroed memory
+	std::vector<uint32_t> marks(a.mslot * nprob + 4, 0xdeadbeefu);
+	std::vector<int2> done((size_t)cap * nprob + 1, int2{-7, -7});
+	a.marks = marks.data(); a.done = done.data();
+	a.C = *C; a.local = local; a.ncl_const = ncl_const; a.ncl_lin = ncl_lin;
+	a.maxaln = maxaln; a.maxedit = maxedit; a.naln = naln; a.alns = alns; a.edits = edits; a.fates = fates;
+	launch_sw_bt(kind, a, nullptr);
+	return 0;
+}

@@ -1,0 +1,34 @@
+// tests/cpu_emul/stub/hip/hip_runtime.h -- TEST INFRASTRUCTURE ONLY.
+// The few HIP names the backtrace kernel source uses, so that
+// tests/cpu_emul/bt_emul.cpp can compile bowtie2-server_amd/csrc/sw_backtrace.hip
+// unchanged with g++ and run its kernel body lane by lane on the CPU (to catch
+// indexing faults before a GPU run).  Not a HIP implementation; never linked
+// into the product.
+#pragma once
+#include <stdint.h>
+#include <stddef.h>
+#define __device__
+#define __host__
+#define __global__
+#define __forceinline__ inline
+#define __launch_bounds__(...)
+#define __shared__ static
+struct dim3 { uint32_t x = 1, y = 1, z = 1; dim3(uint32_t a = 1, uint32_t b = 1, uint32_t c = 1) : x(a), y(b), z(c) {} };
+struct uint4 { uint32_t x, y, z, w; };
+struct int2 { int32_t x, y; };
+struct uint3v { uint32_t x = 0, y = 0, z = 0; };
+inline uint4 make_uint4(uint32_t a, uint32_t b, uint32_t c, uint32_t d) { return uint4{a, b, c, d}; }
+inline int2 make_int2(int32_t a, int32_t b) { return int2{a, b}; }
+extern thread_local uint3v threadIdx, blockIdx;
+typedef void* hipStream_t;
+typedef int hipError_t;
+template <typename K, typename... A>
+void emul_launch(K k, dim3 g, dim3 b, A... a) {
+	for(uint32_t bx = 0; bx < g.x; bx++)
+		for(uint32_t tx = 0; tx < b.x; tx++) {
+			blockIdx.x = bx;
+			threadIdx.x = tx;
+			k(a...);
+		}
+}
+#define hipLaunchKernelGGL(k, g, b, sh, st, ...) emul_launch(k, g, b, __VA_ARGS__)

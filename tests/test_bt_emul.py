@@ -1,0 +1,126 @@
+"""The backtrace kernel source (bowtie2-server_amd/csrc/sw_backtrace.hip),
+compiled for the host by tests/cpu_emul (stub HIP header, one kernel lane at a
+time), against the reference's alignments (sw_bt_* golden fixtures).  The
+fills are the oracle's (pinned to the reference by test_oracle_golden.py),
+laid out as the GPU fills leave them: the systolic fill's u8 score plane
+(kind 0) and the generic fill's H,E,F int16 triples (kind 2).  CPU only:
+catches indexing faults and logic errors before a GPU run."""
+import ctypes as C
+import os
+import subprocess
+
+import numpy as np
+import pytest
+
+from conftest import ROOT, load_golden
+
+EMUL = os.path.join(ROOT, "tests", "cpu_emul")
+LIB = os.path.join(EMUL, "libbt_emul.so")
+SRC = [os.path.join(EMUL, "bt_emul.cpp"), os.path.join(ROOT, "bowtie2-server_amd", "csrc", "sw_backtrace.hip"),
+       os.path.join(ROOT, "bowtie2-server_amd", "csrc", "bt2g_kernels.h")]
+CLANG = "/opt/rocm/lib/llvm/bin/clang++"
+
+
+class SwConst(C.Structure):
+    _fields_ = [(n, C.c_int32) for n in ("match", "npen", "gapbar", "rdgo", "rdge", "rfgo", "rfge")] + \
+               [("mmpen", C.c_int32 * 41)]
+
+
+def build():
+    if not os.path.exists(CLANG):
+        pytest.skip("clang++ missing")
+    if not os.path.exists(LIB) or os.path.getmtime(LIB) < max(os.path.getmtime(s) for s in SRC):
+        subprocess.check_call([CLANG, "-O1", "-g", "-std=c++17", "-fPIC", "-shared", "-Wno-unknown-attributes",
+                               "-I", os.path.join(EMUL, "stub"), "-I", os.path.join(ROOT, "include"),
+                               "-include", "vector", SRC[0], "-o", LIB])
+    return C.CDLL(LIB)
+
+
+def swconst(local):
+    c = SwConst(match=2 if local else 0, npen=1, gapbar=4, rdgo=8, rdge=3, rfgo=8, rfge=3)
+    for q in range(41):
+        c.mmpen[q] = 2 + int(np.float32(q) / np.float32(40.0) * 4)
+    return c
+
+
+def _p(a):
+    return None if a is None else C.c_void_p(a.ctypes.data)
+
+
+@pytest.fixture(scope="module")
+def lib():
+    return build()
+
+
+@pytest.mark.parametrize("src,kind", [("rand_ee", 0), ("log_ee", 0), ("rand_ee", 2), ("rand_loc", 2),
+                                      ("log_loc", 2)])
+def test_bt_kernel_source_on_cpu(lib, src, kind):
+    import bt2g
+    from oracle.oracle import Oracle
+    from test_oracle_golden import bt_expected, sw_problems
+    orc = Oracle()
+    g, b = load_golden("sw_" + src), load_golden("sw_bt_" + src)
+    local = bool(g["local"])
+    probs = np.zeros(len(g["rd_index"]), bt2g.SWPROB_DTYPE)
+    probs["read"], probs["fw"], probs["minsc"] = g["rd_index"], g["fw"], g["minsc"]
+    probs["win_off"] = g["rf_off"][:-1]
+    probs["ncol"] = np.diff(g["rf_off"]) - 1
+    n, cap = len(probs), 4096
+    res = np.zeros(n, bt2g.SWRES_DTYPE)
+    cands = np.zeros((n, cap), bt2g.SWCAND_DTYPE)
+    stride = g["reads"].shape[1]
+    S16 = 16 * ((stride + 15) // 16)
+    maxcol = int(probs["ncol"].max())
+    maxrow = int(g["lens"].max())
+    mats, offs, tot = [], [], 0
+    slot = S16 * maxcol
+    plane = np.zeros(slot * n if kind == 0 else 16, np.uint8)
+    keep = np.ones(n, bool)
+    for p, rd, q, rf, minsc, fw, out, cref in sw_problems(g):
+        o, c, m = orc.sw(rd, q, rf, minsc, local, want_mat=True, cap=cap)
+        res[p] = (o[0], max(o[1], -2**31), o[2], o[3], o[4], o[5], o[6], 0)
+        cands[p, :len(c)] = [tuple(x) for x in c]
+        L, ncol = len(rd), len(rf) - 1
+        offs.append(tot)
+        if m is None:
+            m = np.zeros((L, ncol, 3), np.int32)
+        mats.append(m.astype(np.int16).ravel())
+        tot += L * ncol * 3
+        if kind == 0:
+            if o[0] and not o[2]:
+                keep[p] = False          # i16 fill: not in a u8 plane (naln -4)
+                continue
+            blk = plane[p * slot:(p + 1) * slot].reshape(maxcol, S16)
+            blk[:ncol, S16 - L:] = m[:, :, 0].T
+    mat = np.concatenate(mats)
+    mat_off = np.array(offs, np.uint64)
+    rects = np.zeros(n, bt2g.SWRECT_DTYPE)
+    rects["triml"], rects["corel"], rects["corer"] = b["triml"], b["corel"], b["corer"]
+    maxaln, maxedit = 4096 if local else 256, 512
+    naln = np.zeros(n, np.int32)
+    alns = np.zeros((n, maxaln), bt2g.SWALN_DTYPE)
+    edits = np.zeros((n, maxaln, maxedit), bt2g.EDIT_DTYPE)
+    fates = np.zeros((n, cap), np.int8)
+    lens = np.ascontiguousarray(g["lens"], np.uint32)
+    lib.bt_emul_run(C.c_int(kind), _p(probs), C.c_uint32(n), _p(g["reads"]), _p(g["quals"]), C.c_uint32(stride),
+                    _p(lens), _p(g["rf"]), _p(rects), _p(res), _p(cands), C.c_uint32(cap), _p(plane),
+                    C.c_uint64(slot), C.c_uint32(S16), _p(mat), _p(mat_off), C.c_uint32(maxrow), C.c_uint32(maxcol),
+                    C.byref(swconst(local)), C.c_int(int(local)), C.c_double(0.0), C.c_double(0.15),
+                    C.c_uint32(maxaln), C.c_uint32(maxedit), _p(naln), _p(alns), _p(edits), _p(fates))
+    nal = 0
+    for p in range(n):
+        if not keep[p]:
+            assert naln[p] == -4
+            continue
+        ea, eeds, efates = bt_expected(b, p)
+        assert naln[p] == len(ea), (src, kind, p)
+        for k in range(len(ea)):
+            got = alns[p, k]
+            assert [got[f] for f in ("cand", "score", "off", "ns", "gaps", "refns", "nedit", "trim5p", "trim3p")] \
+                == [ea[k, i] for i in (0, 1, 2, 4, 5, 6, 7, 8, 9)], (src, kind, p, k)
+            e = edits[p, k, :int(ea[k, 7])]
+            assert np.array_equal(np.stack([e["pos"], e["type"], e["chr"], e["qchr"]], 1), eeds[k]), (src, p, k)
+        if len(efates):
+            assert np.array_equal(fates[p, :len(efates)], efates), (src, kind, p)
+        nal += len(ea)
+    assert nal > 40

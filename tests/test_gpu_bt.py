@@ -1,0 +1,167 @@
+"""GPU backtrace (bt2g_sw_align_bt: SwAligner::align + the nextAlignment loop,
+aligner_sw.cpp:737-1146) against the reference's own alignments (sw_bt_*
+golden fixtures made by the reference build) and against the CPU oracle on
+seed-extension problems that point into the HBM-resident reference.  Every
+field of every alignment, every edit and every candidate fate is compared
+bit-exactly (integer path, no tolerance)."""
+import numpy as np
+import pytest
+
+from conftest import get_index, load_golden
+from test_gpu_sw import golden_batch
+
+pytestmark = pytest.mark.gpu
+
+ALN_FIELDS = ("cand", "score", "off", "ns", "gaps", "refns", "nedit", "trim5p", "trim3p")
+# reference fixture columns: cand, score, off, refoff, ns, gaps, refns, nedit, trim5p, trim3p
+REF_COLS = (0, 1, 2, 4, 5, 6, 7, 8, 9)
+
+
+@pytest.fixture(scope="module")
+def eng():
+    import bt2g
+    e = bt2g.Engine(index=get_index("lambda"))
+    yield e
+    e.close()
+
+
+def _aln_rows(alns, k):
+    return np.stack([alns[f][:k] for f in ALN_FIELDS], 1).astype(np.int64)
+
+
+def _edit_rows(ed):
+    return np.stack([ed["pos"], ed["type"], ed["chr"], ed["qchr"]], 1).astype(np.int64)
+
+
+def check_against(naln, alns, edits, fates, res, exp_out, exp_alns, exp_edits, exp_fates, tag):
+    """exp_alns[p]: (k x 10) reference columns; exp_edits[p]: list of (e x 4)."""
+    n = len(naln)
+    for p in range(n):
+        ea = exp_alns[p]
+        assert naln[p] == len(ea), (tag, p, naln[p], len(ea))
+        if len(ea):
+            assert np.array_equal(_aln_rows(alns[p], len(ea)), ea[:, REF_COLS]), (tag, p)
+            for k in range(len(ea)):
+                ne = int(ea[k, 7])
+                assert np.array_equal(_edit_rows(edits[p, k, :ne]), exp_edits[p][k]), (tag, p, k)
+        if exp_fates is not None and res["aligned"][p]:
+            ef = exp_fates[p]
+            assert np.array_equal(fates[p, :len(ef)], ef), (tag, p)
+
+
+@pytest.mark.parametrize("src", ["rand_ee", "rand_loc", "log_ee", "log_loc"])
+def test_bt_golden(eng, src):
+    """Reference fixtures: the reference server's logged DP problems and random
+    ragged problems, each with its own rectangle trim / core diagonals."""
+    import bt2g
+    g, b = load_golden("sw_" + src), load_golden("sw_bt_" + src)
+    local = bool(g["local"])
+    probs = golden_batch(g)
+    n = len(probs)
+    rects = np.zeros(n, bt2g.SWRECT_DTYPE)
+    rects["triml"], rects["corel"], rects["corer"] = b["triml"], b["corel"], b["corer"]
+    res, cands, naln, alns, edits, fates = eng.sw_align_bt(g["reads"], g["quals"], g["lens"], probs,
+                                                           windows=g["rf"], rects=rects, local=local, cap=4096,
+                                                           maxaln=4096 if local else 256, maxedit=512)
+    assert np.array_equal(res["aligned"], b["out"][:, 0])
+    ea = [b["aln"][b["aln_off"][p]:b["aln_off"][p + 1]] for p in range(n)]
+    ee = [[b["edits"][b["edit_off"][k]:b["edit_off"][k + 1]] for k in range(b["aln_off"][p], b["aln_off"][p + 1])]
+          for p in range(n)]
+    ef = [b["fates"][b["fate_off"][p]:b["fate_off"][p + 1]] for p in range(n)]
+    check_against(naln, alns, edits, fates, res, b["out"], ea, ee, ef, src)
+    assert naln.sum() > 50
+
+
+def _synth_problems(gen, n, seed, length=150, maxgap=15, minsc=-90, sub=0.02, indel=0.3):
+    import bt2g
+    import synth
+    codes, quals, pos, fw = synth.reads(seed, gen, n, length, sub=sub, indel=indel)
+    rng = np.random.default_rng(seed)
+    probs = np.zeros(n, bt2g.SWPROB_DTYPE)
+    probs["read"] = np.arange(n)
+    probs["fw"] = fw.astype(np.int32)
+    refl = pos.astype(np.int64) - 2 * maxgap + rng.integers(-3, 4, n)
+    refl[:4] = [-2 * maxgap, -7, len(gen) - length - 10, len(gen) - length + 5]
+    probs["refl"] = refl
+    probs["win_off"] = -1
+    probs["ncol"] = length + 4 * maxgap
+    probs["minsc"] = minsc
+    rects = np.zeros(n, bt2g.SWRECT_DTYPE)
+    rects["triml"] = 0
+    rects["corel"], rects["corer"] = maxgap, 3 * maxgap
+    return codes, quals, np.full(n, length, np.uint32), probs, rects
+
+
+def _oracle_expect(orc, gen, codes, quals, probs, rects, local, sc=None, enable8=True):
+    ea, ee, ef = [], [], []
+    for p in range(len(probs)):
+        rd, q = codes[p], quals[p]
+        if not probs["fw"][p]:
+            rd, q = np.where(rd > 3, 4, 3 - rd)[::-1], q[::-1]
+        ncol = int(probs["ncol"][p])
+        o = np.arange(probs["refl"][p], probs["refl"][p] + ncol + 1)
+        cc = np.where((o >= 0) & (o < len(gen)), gen[np.clip(o, 0, len(gen) - 1)], 4).astype(np.int32)
+        rf = np.where(cc > 3, 16, 1 << np.minimum(cc, 3)).astype(np.uint8)
+        out, a, eds, fates = orc.sw_bt(rd, q, rf, int(probs["minsc"][p]), local, bool(probs["fw"][p]),
+                                       int(rects["triml"][p]), int(rects["corel"][p]), int(rects["corer"][p]),
+                                       enable8=enable8, maxaln=512, maxedit=512, sc=sc)
+        ea.append(a)
+        ee.append(eds)
+        ef.append(fates)
+    return ea, ee, ef
+
+
+@pytest.mark.parametrize("case", ["u8", "i16", "custom_scoring"])
+def test_bt_resident_vs_oracle(eng, case):
+    """Seed-extension problems (150 x 210, dp_framer.cpp:95-125 geometry) over the
+    resident reference, reads with substitutions, Ns and indels; windows off
+    both reference ends.  u8: the systolic fill's byte score plane; i16:
+    enable8 off (u16 plane); custom scoring: the generic fill's matrices."""
+    import bt2g
+    from oracle.oracle import Oracle, scoring as oscoring
+    orc = Oracle()
+    gen = get_index("lambda").ref_codes[0]
+    codes, quals, lens, probs, rects = _synth_problems(gen, 600, 17)
+    sc, osc, enable8 = None, None, True
+    if case == "i16":
+        enable8 = False
+    elif case == "custom_scoring":
+        sc = bt2g.scoring(False)
+        sc.rdg_const, sc.rdg_lin, sc.rfg_const, sc.rfg_lin, sc.mmp_max = 4, 2, 6, 1, 5
+        osc = oscoring(False)
+        osc.rdg_const, osc.rdg_lin, osc.rfg_const, osc.rfg_lin, osc.mmp_max = 4, 2, 6, 1, 5
+    res, cands, naln, alns, edits, fates = eng.sw_align_bt(codes, quals, lens, probs, rects=rects, cap=1024,
+                                                           maxaln=512, maxedit=512, sc=sc, enable8=enable8)
+    ea, ee, ef = _oracle_expect(orc, gen, codes, quals, probs, rects, False, sc=osc, enable8=enable8)
+    check_against(naln, alns, edits, fates, res, None, ea, ee, ef, case)
+    assert (naln > 0).sum() > 400
+    assert (alns["gaps"][:, 0] > 0).sum() > 20          # indel alignments were walked
+
+
+def test_bt_local_resident_vs_oracle(eng):
+    """--local scoring on the resident reference (soft trimming, dominance)."""
+    import bt2g
+    from oracle.oracle import Oracle
+    orc = Oracle()
+    gen = get_index("lambda").ref_codes[0]
+    # --score-min G,20,8 at 150 bp: (int)(20 + 8 ln 150) = 60
+    codes, quals, lens, probs, rects = _synth_problems(gen, 300, 23, minsc=60)
+    res, cands, naln, alns, edits, fates = eng.sw_align_bt(codes, quals, lens, probs, rects=rects, local=True,
+                                                           cap=4096, maxaln=512, maxedit=512)
+    ea, ee, ef = _oracle_expect(orc, gen, codes, quals, probs, rects, True)
+    check_against(naln, alns, edits, fates, res, None, ea, ee, ef, "local")
+    assert (naln > 0).sum() > 200
+
+
+def test_bt_maxaln_truncates(eng):
+    """maxaln bounds the loop: the first maxaln alignments equal the full run's."""
+    gen = get_index("lambda").ref_codes[0]
+    codes, quals, lens, probs, rects = _synth_problems(gen, 200, 31)
+    full = eng.sw_align_bt(codes, quals, lens, probs, rects=rects, cap=1024, maxaln=64, maxedit=256)
+    one = eng.sw_align_bt(codes, quals, lens, probs, rects=rects, cap=1024, maxaln=1, maxedit=256)
+    assert np.array_equal(one[2], np.minimum(full[2], 1))
+    has = full[2] > 0
+    assert np.array_equal(one[3][has, 0], full[3][has, 0])
+    for p in np.nonzero(has)[0]:
+        ne = int(full[3]["nedit"][p, 0])
+        assert np.array_equal(one[4][p, 0, :ne], full[4][p, 0, :ne]), p
