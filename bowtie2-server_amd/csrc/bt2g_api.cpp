@@ -600,7 +600,7 @@ int bt2g_sw_align_bt_dev(bt2g_ctx* c, const uint8_t* reads, const uint8_t* quals
 	int kind, rc;
 	uint32_t maxcol = 0, maxrow = stride;
 	const bool reserved = packed && c->bt_plane && nprob <= c->bt_max_prob && stride <= c->bt_max_stride &&
-	                      nprob <= c->sw_max_prob && c->sw_lists && c->bt_max_cols <= c->sw_max_cols;
+	                      nprob <= c->sw_max_prob && c->sw_lists && c->bt_max_cols == c->sw_max_cols;
 	if(reserved) {
 		// the fill marks problems wider than the reservation (flag -3, not aligned)
 		maxcol = c->bt_max_cols;
@@ -660,14 +660,14 @@ int bt2g_sw_align_bt_dev(bt2g_ctx* c, const uint8_t* reads, const uint8_t* quals
 		maxrow = 0;
 		for(uint32_t i = 0; i < nreads; i++) maxrow = hl[i] > maxrow ? hl[i] : maxrow;
 	}
-	a.mwords = sw_bt_mwords(maxcol);
-	a.mrows = maxrow;
+	a.mwords = sw_bt_tcols(maxcol);
+	a.mrows = sw_bt_trows(maxrow);
 	a.mslot = sw_bt_mslot(maxrow, maxcol);
 	if(!a.marks && (rc = talloc((void**)&a.marks, sizeof(uint32_t) * a.mslot * nprob))) return rc;
 	if(sc->local && (rc = talloc((void**)&a.done, sizeof(int2) * (size_t)cap * nprob))) return rc;
 	a.probs = probs; a.nprob = nprob; a.reads = reads; a.quals = quals; a.stride = stride; a.lens = lens;
 	a.windows = windows; a.ref_codes = c->ref_codes; a.ref_starts = c->ref_starts; a.rects = rects;
-	a.res = res; a.cands = cands; a.cap = cap; a.cstride = S16;
+	a.res = res; a.cands = cands; a.cap = cap; a.cstride = S16; a.pcols = maxcol;
 	a.C = C; a.local = sc->local; a.ncl_const = sc->ncl_const; a.ncl_lin = sc->ncl_lin;
 	a.maxaln = maxaln; a.maxedit = maxedit; a.naln = naln; a.alns = alns; a.edits = edits; a.fates = fates;
 	{

@@ -71,12 +71,13 @@ struct BtArgs {
 	uint32_t cap;
 	const uint8_t* plane;             // kinds 0/1: systolic score plane
 	uint64_t slot;                    //   bytes per problem
-	uint32_t cstride;                 //   rows per column
+	uint32_t cstride;                 //   rows per column (16-row blocks)
+	uint32_t pcols;                   //   columns per row block
 	const int16_t* mat;               // kind 2: H,E,F triples
 	const uint64_t* mat_off;
-	uint32_t* marks;                  // per problem (mslot words): reportedThrough bitmap of
-	uint64_t mslot;                   //   mrows x mwords words, then mrows first-walk intervals
-	uint32_t mwords, mrows;
+	uint32_t* marks;                  // per problem (mslot words): reportedThrough tiles
+	uint64_t mslot;
+	uint32_t mwords, mrows;           //   tiles per tile row, tile rows
 	int2* done;                       // local mode: cap (row, col) per problem
 	SwConst C;
 	int local;
@@ -89,10 +90,13 @@ struct BtArgs {
 };
 // kind: 0 u8 score plane, 1 u16 score plane, 2 generic H,E,F matrices
 void launch_sw_bt(int kind, const BtArgs& a, hipStream_t st);
-// words of backtrace mark scratch per problem of <= rows x cols
-inline uint32_t sw_bt_mwords(uint32_t cols) { return (((cols + 31u) / 32u) + 3u) & ~3u; }
+// backtrace mark scratch per problem of <= rows x cols: 8x8-cell bit tiles
+// (2 words each) + one valid bit per tile (sw_backtrace.hip)
+inline uint32_t sw_bt_tcols(uint32_t cols) { return (cols + 7u) / 8u; }
+inline uint32_t sw_bt_trows(uint32_t rows) { return (rows + 7u) / 8u; }
 inline uint64_t sw_bt_mslot(uint32_t rows, uint32_t cols) {
-	return (((uint64_t)rows * sw_bt_mwords(cols) + rows) + 3u) & ~(uint64_t)3u;
+	const uint64_t tc = sw_bt_tcols(cols), tr = sw_bt_trows(rows);
+	return (tr * tc * 2u + tr * ((tc + 31u) / 32u) + 3u) & ~(uint64_t)3u;
 }
 void launch_sort_cands(const bt2g_sw_result* res, bt2g_sw_cand* cands, uint32_t nprob, uint32_t cap,
                        uint32_t* big, uint32_t* nbig, hipStream_t st);

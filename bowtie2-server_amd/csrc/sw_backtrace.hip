@@ -25,12 +25,15 @@
 // moves need no scan at all: the F (E) value of the cell is known from the
 // move that entered it, and one of its two sources must match (both: the H one).
 //
-// reportedThrough: the first walk of a problem records, per row, the column
-// interval it crossed (a walk visits one contiguous run of columns per row);
-// later walks are checked against those intervals and against a bitmap whose
-// rows are cleared lazily over the range they reach (the bottom rows, for
-// end-to-end candidates).  All loads a step needs are issued together, so a
-// diagonal step costs one memory round trip.
+// Memory: 1M lanes each walking their own problem cannot share caches, so a
+// step must not touch memory: reportedThrough lives in 8x8 bit tiles of which
+// one is held in registers, the read / qualities / reference are read through
+// 4-byte register windows, and the u8 plane through a register copy of 4
+// columns x 16 rows (the plane is stored in 16-row blocks, sw_ee_packed.hip),
+// so a diagonal run reloads every 4 steps and the later, short walks of a
+// problem (all near its last rows) mostly hit registers.  Edits are written
+// by the first walk (which usually succeeds) and by a replay of any later
+// walk that succeeds.
 //
 // The reference's branch stack (btnstack_) never changes an outcome: every
 // popped frame restarts at a cell already marked reportedThrough, so a walk
@@ -58,24 +61,32 @@ __device__ __forceinline__ char mask2dna(int m) {
 enum { ST_H = 0, ST_E = 1, ST_F = 2 };
 
 // Score plane accessor: KIND 0 = u8 plane, 1 = u16 plane (systolic layout:
-// problem slot, column-major with cstride rows, bottom-aligned), 2 = int16
-// H,E,F triples at mat_off[p] (generic fill, row-major).
+// problem slot, 16-row blocks of pcols columns, rows bottom-aligned in the
+// strip stack (pad dead rows on top)), 2 = int16 H,E,F triples at mat_off[p]
+// (generic fill, row-major).
 template <int KIND>
 struct Plane {
-	const uint8_t* base;
-	uint32_t cstride, ncol;
+	const uint8_t* base;   // kinds 0/1: the problem's slot; 2: its matrix
+	uint32_t pcols, ncol, pad;
 	int32_t off;      // score = raw - off
+	__device__ __forceinline__ size_t idx(uint32_t r, uint32_t c) const {
+		const uint32_t rs = pad + r;
+		return ((size_t)(rs >> 4) * pcols + c) * 16u + (rs & 15u);
+	}
 	__device__ __forceinline__ int32_t h(uint32_t r, uint32_t c) const {
-		if(KIND == 0) return (int32_t)base[(size_t)c * cstride + r] - off;
-		if(KIND == 1) return (int32_t)((const uint16_t*)base)[(size_t)c * cstride + r] - off;
+		if(KIND == 0) return (int32_t)base[idx(r, c)] - off;
+		if(KIND == 1) return (int32_t)((const uint16_t*)base)[idx(r, c)] - off;
 		return (int32_t)((const int16_t*)base)[((size_t)r * ncol + c) * 3] - off;
 	}
 };
 
 }  // namespace
 
+#ifndef BT2G_BT_WAVES
+#define BT2G_BT_WAVES 3
+#endif
 template <int KIND>
-__global__ void __launch_bounds__(64)
+__global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(BT2G_BT_WAVES)))
 k_sw_bt(BtArgs A) {
 	const uint32_t p = blockIdx.x * 64u + threadIdx.x;
 	if(p >= A.nprob) return;
@@ -87,7 +98,8 @@ k_sw_bt(BtArgs A) {
 	const int variant = local ? (R.u8succ ? 2 : 3) : (R.u8succ ? 0 : 1);
 	Plane<KIND> pl;
 	pl.ncol = ncol;
-	pl.cstride = A.cstride;
+	pl.pcols = A.pcols;
+	pl.pad = 0;
 	uint32_t pad = 0;
 	const uint8_t* slot = nullptr;
 	if(KIND == 2) {
@@ -98,7 +110,9 @@ k_sw_bt(BtArgs A) {
 		const size_t es = KIND == 0 ? 1 : 2;
 		pad = A.cstride - nrow;
 		slot = A.plane + (size_t)p * A.slot;
-		pl.base = slot + (size_t)pad * es;
+		pl.base = slot;
+		pl.pad = pad;
+		(void)es;
 		pl.off = variant == 0 ? 0xff : 0xffff;
 	}
 	// SwAligner::initRead / initRef inputs of this problem
@@ -106,24 +120,8 @@ k_sw_bt(BtArgs A) {
 	const uint8_t* qu = A.quals + (size_t)P.read * A.stride;
 	const bool fw = P.fw != 0;
 	const SwConst& C = A.C;
-	auto readc = [&](uint32_t r) -> int {
-		if(fw) return rd[r];
-		const int c = rd[nrow - 1 - r];
-		return c > 3 ? 4 : 3 - c;
-	};
-	auto qual = [&](uint32_t r) -> int {
-		int q = (int)(fw ? qu[r] : qu[nrow - 1 - r]) - 33;
-		return q < 0 ? 0 : (q > 40 ? 40 : q);
-	};
 	uint64_t rs = 0, rlen = 0;
 	if(P.win_off < 0) { rs = A.ref_starts[P.refidx]; rlen = A.ref_starts[P.refidx + 1] - rs; }
-	auto refm = [&](uint32_t c) -> int {   // reference mask of column c (aligner_sw.cpp:171-253)
-		if(P.win_off >= 0) return A.windows[P.win_off + c];
-		const int64_t o = P.refl + (int64_t)c;
-		if(o < 0 || (uint64_t)o >= rlen) return 16;
-		const int code = A.ref_codes[rs + (uint64_t)o];
-		return code > 3 ? 16 : 1 << code;
-	};
 	// Scoring::score / Scoring::mm (scoring.h:232-254); match(30) is the bonus
 	auto sdiag = [&](int rc, int m, int q) -> int {
 		if(rc > 3 || m > 15) return -C.npen;
@@ -139,12 +137,11 @@ k_sw_bt(BtArgs A) {
 	auto col_hit = [&](uint32_t c, int32_t rlo, int32_t rhi, int32_t x, int32_t base, int32_t step) -> bool {
 		if(rlo > rhi) return false;
 		if(KIND == 0) {
-			// bytes [pad+rlo, pad+rhi] of column block c: aligned 16-B loads
-			const uint8_t* cb = slot + (size_t)c * A.cstride;
+			// stack rows [pad+rlo, pad+rhi] of column c: one 16-B load per row block
 			bool hit = false;
 #pragma unroll 1
 			for(int32_t o0 = ((int32_t)pad + rlo) & ~15; o0 <= (int32_t)pad + rhi; o0 += 16) {
-				const uint4 v = *(const uint4*)(cb + o0);
+				const uint4 v = *(const uint4*)(slot + ((size_t)(o0 >> 4) * A.pcols + c) * 16u);
 				const uint32_t wv[4] = {v.x, v.y, v.z, v.w};
 #pragma unroll
 				for(int b = 0; b < 16; b++) {
@@ -169,30 +166,88 @@ k_sw_bt(BtArgs A) {
 	}
 	int32_t triml = 0, corel = 0, corer = 0x7fffffff;
 	if(A.rects) { const bt2g_sw_rect rc = A.rects[p]; triml = rc.triml; corel = rc.corel; corer = rc.corer; }
-	// reportedThrough: the first walk's per-row column intervals + a lazily
-	// cleared bitmap for the cells of later walks
+	// reportedThrough: 8x8-cell bit tiles (one u64 each), one tile cached in
+	// registers at a time (a walk stays in a tile for several steps); a tile is
+	// valid once written back (valid bits per tile row, cleared here), so
+	// nothing else is ever cleared.
 	uint32_t* marks = A.marks + (size_t)p * A.mslot;
-	uint32_t* path1 = marks + (size_t)A.mwords * A.mrows;      // mrows words after the bitmap
-	const uint32_t mw = A.mwords;
-	int32_t mlo = 0x7fffffff, mhi = -1;      // bitmap rows cleared so far
-	int32_t p1lo = 0x7fffffff, p1hi = -1;    // rows holding first-walk intervals
-	auto clear_row = [&](int32_t r) {
-		uint4* q = (uint4*)(marks + (size_t)r * mw);
-		for(uint32_t w = 0; w < mw / 4; w++) q[w] = make_uint4(0, 0, 0, 0);
-	};
-	auto touch_rows = [&](int32_t r) {
-		if(mhi < 0) { mlo = mhi = r; clear_row(r); return; }
-		while(r > mhi) clear_row(++mhi);
-		while(r < mlo) clear_row(--mlo);
-	};
-	auto marked = [&](uint32_t r, uint32_t c) -> bool {
-		bool m = false;
-		if((int32_t)r >= p1lo && (int32_t)r <= p1hi) {
-			const uint32_t iv = path1[r];
-			m = c >= (iv & 0xffffu) && c <= (iv >> 16);
+	const uint32_t tcols = A.mwords, trows = A.mrows, vw = (tcols + 31u) / 32u;
+	uint32_t* valid = marks + (size_t)trows * tcols * 2u;
+	for(uint32_t i = 0; i < trows * vw; i++) valid[i] = 0u;
+	uint32_t ttr = 0xffffffffu, ttc = 0;
+	uint64_t tbits = 0;
+	bool tdirty = false;
+	auto tile_get = [&](uint32_t r, uint32_t c) {
+		const uint32_t tr = r >> 3, tc = c >> 3;
+		if(tr == ttr && tc == ttc) return;
+		if(tdirty) {
+			*(uint64_t*)(marks + ((size_t)ttr * tcols + ttc) * 2u) = tbits;
+			valid[ttr * vw + (ttc >> 5)] |= 1u << (ttc & 31u);
+			tdirty = false;
 		}
-		if((int32_t)r >= mlo && (int32_t)r <= mhi) m = m || ((marks[(size_t)r * mw + (c >> 5)] >> (c & 31)) & 1u);
-		return m;
+		ttr = tr;
+		ttc = tc;
+		const bool v = (valid[tr * vw + (tc >> 5)] >> (tc & 31u)) & 1u;
+		tbits = v ? *(const uint64_t*)(marks + ((size_t)tr * tcols + tc) * 2u) : 0ull;
+	};
+	auto tbit = [](uint32_t r, uint32_t c) -> uint64_t { return 1ull << (((r & 7u) << 3) | (c & 7u)); };
+	auto marked = [&](uint32_t r, uint32_t c) -> bool {
+		tile_get(r, c);
+		return (tbits & tbit(r, c)) != 0;
+	};
+	// 4-byte windows over the read, the qualities and the reference (aligned
+	// dwords: a walk moves one row / column at a time); a dword that would
+	// leave the array's extent [lo, hi) is not loaded (single byte instead)
+	struct Win { uint64_t a; uint32_t w; };
+	Win w_rd{~0ull, 0u}, w_q{~0ull, 0u}, w_rf{~0ull, 0u};
+	auto win = [&](Win& W, const uint8_t* ptr, const uint8_t* lo, const uint8_t* hi) -> int {
+		const uint64_t addr = (uint64_t)ptr, aa = addr & ~3ull;
+		if(aa != W.a) {
+			if(aa < (uint64_t)lo || aa + 4u > (uint64_t)hi) return *ptr;
+			W.a = aa;
+			W.w = *(const uint32_t*)aa;
+		}
+		return (int)((W.w >> ((addr & 3u) * 8u)) & 0xffu);
+	};
+	auto rd_at = [&](uint32_t r) -> int {   // read character of DP row r
+		const int raw = win(w_rd, rd + (fw ? r : nrow - 1 - r), rd, rd + nrow);
+		return fw ? raw : (raw > 3 ? 4 : 3 - raw);
+	};
+	auto q_at = [&](uint32_t r) -> int {
+		const int q = win(w_q, qu + (fw ? r : nrow - 1 - r), qu, qu + nrow) - 33;
+		return q < 0 ? 0 : (q > 40 ? 40 : q);
+	};
+	const uint8_t* wlo = P.win_off >= 0 ? A.windows + P.win_off : A.ref_codes + rs;
+	const uint8_t* whi = P.win_off >= 0 ? wlo + ncol + 1 : wlo + rlen;
+	auto rf_at = [&](uint32_t c) -> int {   // reference mask of column c (aligner_sw.cpp:171-253)
+		if(P.win_off >= 0) return win(w_rf, wlo + c, wlo, whi);
+		const int64_t o = P.refl + (int64_t)c;
+		if(o < 0 || (uint64_t)o >= rlen) return 16;
+		const int code = win(w_rf, wlo + (uint64_t)o, wlo, whi);
+		return code > 3 ? 16 : 1 << code;
+	};
+	// H of a cell; the u8 plane goes through a register copy of 4 columns x 16 rows
+	uint32_t cb = 0xffffffffu, cc0 = 0;
+	uint4 ch0 = make_uint4(0, 0, 0, 0), ch1 = ch0, ch2 = ch0, ch3 = ch0;   // named: no indexable array
+	auto hget = [&](uint32_t r, uint32_t c) -> int32_t {
+		if(KIND != 0) return pl.h(r, c);
+		const uint32_t rsx = pad + r, b = rsx >> 4;
+		if(b != cb || c < cc0 || c > cc0 + 3u) {
+			cb = b;
+			cc0 = c >= 3u ? c - 3u : 0u;
+			if(cc0 + 4u > A.pcols) cc0 = A.pcols >= 4u ? A.pcols - 4u : 0u;
+			const uint4* qp = (const uint4*)(slot + ((size_t)b * A.pcols + cc0) * 16u);
+			const uint4 z = make_uint4(0, 0, 0, 0);
+			ch0 = cc0 < A.pcols ? qp[0] : z;
+			ch1 = cc0 + 1u < A.pcols ? qp[1] : z;
+			ch2 = cc0 + 2u < A.pcols ? qp[2] : z;
+			ch3 = cc0 + 3u < A.pcols ? qp[3] : z;
+		}
+		const uint32_t u = c - cc0, di = (rsx & 15u) >> 2;
+		auto pick = [&](const uint4& v) -> uint32_t { return di == 0 ? v.x : di == 1 ? v.y : di == 2 ? v.z : v.w; };
+		const uint32_t d0 = pick(ch0), d1 = pick(ch1), d2 = pick(ch2), d3 = pick(ch3);
+		const uint32_t d = u == 0 ? d0 : u == 1 ? d1 : u == 2 ? d2 : d3;
+		return (int32_t)((d >> ((rsx & 3u) * 8u)) & 0xffu) - pl.off;
 	};
 	const uint32_t ncand = (uint32_t)R.ncand < A.cap ? (uint32_t)R.ncand : A.cap;
 	const bt2g_sw_cand* cl = A.cands + (size_t)p * A.cap;
@@ -202,8 +257,140 @@ k_sw_bt(BtArgs A) {
 	if(SQ == 0) SQ = 1;
 	int32_t nal = 0;
 	bool first = true;
+	// One backtrace from (row, col).  mark: set/check reportedThrough (off when
+	// replaying a successful walk to emit its edits; the path does not depend
+	// on the marks).  emit: write the edits (walk order) to ed.
+	struct Walk {
+		bool ok, core;
+		uint32_t row, col, ned;
+		int32_t score, ns, gaps;
+	};
+	auto walk = [&](uint32_t row, uint32_t col, bool mark, bool emit, bt2g_edit* ed) -> Walk {
+		Walk w{true, false, row, col, 0u, 0, 0, 0};
+		auto push = [&](uint32_t pos, int type, int chr, int qchr) {
+			if(emit && w.ned < A.maxedit) ed[w.ned] = bt2g_edit{pos, (uint8_t)type, (uint8_t)chr, (uint8_t)qchr, 0};
+			w.ned++;
+		};
+		int st = ST_H;
+		int32_t cur = hget(row, col);
+		while(true) {
+			if(mark) {
+				// reportedThrough (aligner_swsse_ee_u8.cpp:1331-1336, 1556)
+				tile_get(row, col);
+				const uint64_t bt = tbit(row, col);
+				if(tbits & bt) { w.ok = false; break; }
+				tbits |= bt;
+				tdirty = true;
+			}
+			{
+				const int32_t dg = (int32_t)col - (int32_t)row + triml;
+				w.core = w.core || (dg >= 0 && dg >= corel && dg <= corer);
+			}
+			if(row == 0) break;
+			const int rc = rd_at(row), m = rf_at(col), q = q_at(row);
+			int mv = -1;   // 0 diag, 1 ref open, 2 ref extend, 3 read open, 4 read extend
+			int32_t nxt = 0;
+			if(st == ST_H) {
+				const bool wantd = col > 0;
+				const int32_t hul = wantd ? hget(row - 1, col - 1) : 0;
+				// diag equality; local mode also wants H(up-left) > 0 (floorsc)
+				const bool deq = wantd && cur == hul + sdiag(rc, m, q);
+				if(deq && okv(hul)) { mv = 0; nxt = hul; }
+				if(mv < 0 && gaps_ok(row)) {
+					const int32_t hu = hget(row - 1, col);
+					const int32_t hl = col > 0 ? hget(row, col - 1) : 0;
+					// F(row-1, col) == cur + rfge: H(x-k, col) == cur + rfgo + k*rfge, x = row-1,
+					// rows x..x-k+1 outside the barrier, x-k >= 0
+					bool fup = false;
+					const int32_t x = (int32_t)row - 1;
+					if(okv(cur + rfge) && x >= gb && x <= (int32_t)nrow - gb - 1) {
+						int32_t kmax = x - gb + 1;
+						kmax = kmax < x ? kmax : x;
+						if(rfge > 0) {
+							const int32_t kh = (hmax(x - 1) - cur - rfgo) / rfge;   // need <= hmax
+							kmax = kh < kmax ? kh : kmax;
+						}
+						fup = col_hit(col, x - kmax, x - 1, x, cur + rfgo, rfge);
+					}
+					if(okv(hu) && cur == hu - rfgo) { mv = 1; nxt = hu; }
+					else if(fup) { mv = 2; nxt = cur + rfge; }
+					else if(col > 0) {
+						if(okv(hl) && cur == hl - rdgo) { mv = 3; nxt = hl; }
+						else if(!deq && (!local || cur > 0)) {
+							// above the floor, not diagonal, not from F: from E, and not
+							// by an open -- an extension
+							if(col > 1) { mv = 4; nxt = cur + rdge; }
+						} else if(col > 1 && okv(cur + rdge)) {
+							// H may come from a diagonal the walk may not take (local,
+							// H(up-left) == 0) or from the local floor: E(row, col-1) ==
+							// cur + rdge needs the row scan
+							const int32_t cc = (int32_t)col - 1;
+							const int32_t hm = hmax((int32_t)row);
+							for(int32_t k = 1; cc - k >= 0; k++) {
+								const int32_t need = cur + rdge + rdgo + (k - 1) * rdge;
+								if(need > hm) break;
+								if(pl.h(row, (uint32_t)(cc - k)) == need) { mv = 4; nxt = cur + rdge; break; }
+							}
+						}
+					}
+				}
+				if(mv < 0) break;   // empty cell: the alignment starts here
+			} else if(st == ST_E) {
+				if(col == 0) break;   // unreachable: E(row, 0) is the floor
+				const int32_t hl = hget(row, col - 1);
+				if(okv(hl) && hl - rdgo == cur) { mv = 3; nxt = hl; }
+				else { mv = 4; nxt = cur + rdge; }
+			} else {
+				const int32_t hu = hget(row - 1, col);
+				if(okv(hu) && hu - rfgo == cur) { mv = 1; nxt = hu; }
+				else { mv = 2; nxt = cur + rfge; }
+			}
+			if(mv == 0) {
+				const int mt = (m >= 16 || rc > 3) ? -1 : ((m >> rc) & 1);
+				if(mt != 1) {
+					push(row, 3, mask2dna(m), "ACGTN"[rc]);
+					w.score -= (rc > 3 || m > 15) ? C.npen : C.mmpen[q];
+				} else {
+					w.score += C.match;
+				}
+				if(mt == -1) w.ns++;
+				row--; col--;
+				st = ST_H;
+			} else if(mv <= 2) {
+				push(row, 2, '-', "ACGTN"[rc]);
+				w.score -= mv == 1 ? rfgo : rfge;
+				st = mv == 1 ? ST_H : ST_F;
+				row--; w.gaps++;
+			} else {
+				push(row + 1, 1, mask2dna(m), '-');
+				w.score -= mv == 3 ? rdgo : rdge;
+				st = mv == 3 ? ST_H : ST_E;
+				col--; w.gaps++;
+			}
+			cur = nxt;
+		}
+		w.row = row;
+		w.col = col;
+		if(w.ok && !w.core) w.ok = false;            // must touch a core diagonal
+		if(w.ok) {
+			const int rc = rd_at(row), m = rf_at(col);
+			const int mt = (m >= 16 || rc > 3) ? -1 : ((m >> rc) & 1);
+			if(mt != 1) {
+				push(row, 3, mask2dna(m), "ACGTN"[rc]);
+				w.score -= (rc > 3 || m > 15) ? C.npen : C.mmpen[q_at(row)];
+			} else {
+				w.score += C.match;
+			}
+			if(mt == -1) w.ns++;
+			if(w.ns > nceil) w.ok = false;
+		}
+		return w;
+	};
 	for(uint32_t ci = 0; ci < ncand; ci++) {
 		if(nal >= (int32_t)A.maxaln) break;
+#ifdef BT2G_BT_MAXWALK
+		if(!first && ci >= BT2G_BT_MAXWALK) break;      // timing experiments only
+#endif
 		const bt2g_sw_cand cd = cl[ci];
 		int8_t fate;
 		if(cd.score < P.minsc) {
@@ -223,154 +410,19 @@ k_sw_bt(BtArgs A) {
 			if(dom) {
 				fate = 4;                               // BT_CAND_FATE_FILT_DOMINATED
 			} else {
-				// ---- one backtrace from (row, col) ----
-				const bool rec = first;                 // first walk: record intervals
-				first = false;
+				// the first walk writes its edits as it goes (it usually succeeds);
+				// a later walk that succeeds is walked again to write them
 				bt2g_edit* ed = A.edits + ((size_t)p * A.maxaln + (size_t)nal) * A.maxedit;
-				uint32_t ned = 0;
-				auto push = [&](uint32_t pos, int type, int chr, int qchr) {
-					if(ned < A.maxedit) ed[ned] = bt2g_edit{pos, (uint8_t)type, (uint8_t)chr, (uint8_t)qchr, 0};
-					ned++;
-				};
-				uint32_t row = (uint32_t)cd.row, col = (uint32_t)cd.col;
-				const uint32_t origCol = col, trimEnd = nrow - row - 1;
-				int32_t score = 0, ns = 0, gaps = 0;
-				int st = ST_H;
-				int32_t cur = pl.h(row, col);
-				bool ok = true, core = false;
-				uint32_t irow = row, ilo = col, ihi = col;   // first walk: the open row interval
-				if(rec) p1hi = (int32_t)row;
-				while(true) {
-					// the loads of this step, issued together
-					const bool inP1 = !rec && (int32_t)row >= p1lo && (int32_t)row <= p1hi;
-					const bool inBM = !rec && (int32_t)row >= mlo && (int32_t)row <= mhi;
-					uint32_t* mwp = marks + (size_t)row * mw + (col >> 5);
-					const uint32_t iv = inP1 ? path1[row] : 0xffffu;
-					const uint32_t w = inBM ? *mwp : 0u;
-					const bool wantd = st == ST_H && row > 0 && col > 0;
-					const int32_t hul = wantd ? pl.h(row - 1, col - 1) : 0;
-					const int rc = readc(row), m = refm(col), q = qual(row);
-					const uint32_t bit = 1u << (col & 31);
-					// reportedThrough (aligner_swsse_ee_u8.cpp:1331-1336, 1556)
-					if((w & bit) || (col >= (iv & 0xffffu) && col <= (iv >> 16))) { ok = false; break; }
-					if(rec) {
-						if(row != irow) {
-							path1[irow] = ilo | (ihi << 16);
-							irow = row; ihi = col;
-						}
-						ilo = col;
-					} else {
-						if(!inBM) touch_rows((int32_t)row);
-						*mwp = w | bit;
-					}
-					{
-						const int32_t dg = (int32_t)col - (int32_t)row + triml;
-						core = core || (dg >= 0 && dg >= corel && dg <= corer);
-					}
-					if(row == 0) break;
-					int mv = -1;   // 0 diag, 1 ref open, 2 ref extend, 3 read open, 4 read extend
-					int32_t nxt = 0;
-					if(st == ST_H) {
-						// diag equality; local mode also wants H(up-left) > 0 (floorsc)
-						const bool deq = wantd && cur == hul + sdiag(rc, m, q);
-						if(deq && okv(hul)) { mv = 0; nxt = hul; }
-						if(mv < 0 && gaps_ok(row)) {
-							const int32_t hu = pl.h(row - 1, col);
-							const int32_t hl = col > 0 ? pl.h(row, col - 1) : 0;
-							// F(row-1, col) == cur + rfge: H(x-k, col) == cur + rfgo + k*rfge, x = row-1,
-							// rows x..x-k+1 outside the barrier, x-k >= 0
-							bool fup = false;
-							const int32_t x = (int32_t)row - 1;
-							if(okv(cur + rfge) && x >= gb && x <= (int32_t)nrow - gb - 1) {
-								int32_t kmax = x - gb + 1;
-								kmax = kmax < x ? kmax : x;
-								if(rfge > 0) {
-									const int32_t kh = (hmax(x - 1) - cur - rfgo) / rfge;   // need <= hmax
-									kmax = kh < kmax ? kh : kmax;
-								}
-								fup = col_hit(col, x - kmax, x - 1, x, cur + rfgo, rfge);
-							}
-							if(okv(hu) && cur == hu - rfgo) { mv = 1; nxt = hu; }
-							else if(fup) { mv = 2; nxt = cur + rfge; }
-							else if(col > 0) {
-								if(okv(hl) && cur == hl - rdgo) { mv = 3; nxt = hl; }
-								else if(!deq && (!local || cur > 0)) {
-									// above the floor, not diagonal, not from F: from E, and not
-									// by an open -- an extension
-									if(col > 1) { mv = 4; nxt = cur + rdge; }
-								} else if(col > 1 && okv(cur + rdge)) {
-									// H may come from a diagonal the walk may not take (local,
-									// H(up-left) == 0) or from the local floor: E(row, col-1) ==
-									// cur + rdge needs the row scan
-									const int32_t cc = (int32_t)col - 1;
-									const int32_t hm = hmax((int32_t)row);
-									for(int32_t k = 1; cc - k >= 0; k++) {
-										const int32_t need = cur + rdge + rdgo + (k - 1) * rdge;
-										if(need > hm) break;
-										if(pl.h(row, (uint32_t)(cc - k)) == need) { mv = 4; nxt = cur + rdge; break; }
-									}
-								}
-							}
-						}
-						if(mv < 0) break;   // empty cell: the alignment starts here
-					} else if(st == ST_E) {
-						if(col == 0) break;   // unreachable: E(row, 0) is the floor
-						const int32_t hl = pl.h(row, col - 1);
-						if(okv(hl) && hl - rdgo == cur) { mv = 3; nxt = hl; }
-						else { mv = 4; nxt = cur + rdge; }
-					} else {
-						const int32_t hu = pl.h(row - 1, col);
-						if(okv(hu) && hu - rfgo == cur) { mv = 1; nxt = hu; }
-						else { mv = 2; nxt = cur + rfge; }
-					}
-					if(mv == 0) {
-						const int mt = (m >= 16 || rc > 3) ? -1 : ((m >> rc) & 1);
-						if(mt != 1) {
-							push(row, 3, mask2dna(m), "ACGTN"[rc]);
-							score -= (rc > 3 || m > 15) ? C.npen : C.mmpen[q];
-						} else {
-							score += C.match;
-						}
-						if(mt == -1) ns++;
-						row--; col--;
-						st = ST_H;
-					} else if(mv <= 2) {
-						push(row, 2, '-', "ACGTN"[rc]);
-						score -= mv == 1 ? rfgo : rfge;
-						st = mv == 1 ? ST_H : ST_F;
-						row--; gaps++;
-					} else {
-						push(row + 1, 1, mask2dna(m), '-');
-						score -= mv == 3 ? rdgo : rdge;
-						st = mv == 3 ? ST_H : ST_E;
-						col--; gaps++;
-					}
-					cur = nxt;
-				}
-				if(rec) {
-					// close the first walk's record: rows [row, start] hold intervals
-					path1[irow] = ilo | (ihi << 16);
-					p1lo = (int32_t)row;
-				}
-				if(ok && !core) ok = false;              // must touch a core diagonal
-				if(ok) {
-					const int rc = readc(row), m = refm(col);
-					const int mt = (m >= 16 || rc > 3) ? -1 : ((m >> rc) & 1);
-					if(mt != 1) {
-						push(row, 3, mask2dna(m), "ACGTN"[rc]);
-						score -= (rc > 3 || m > 15) ? C.npen : C.mmpen[qual(row)];
-					} else {
-						score += C.match;
-					}
-					if(mt == -1) ns++;
-					if(ns > nceil) ok = false;
-				}
+				const uint32_t row0 = (uint32_t)cd.row, col0 = (uint32_t)cd.col;
+				Walk w = walk(row0, col0, true, first, ed);
+				if(w.ok && !first) (void)walk(row0, col0, false, true, ed);
+				first = false;
 				if(local) done[ndone++] = make_int2(cd.row, cd.col);
-				if(ok) {
-					const uint32_t trimBeg = row;
+				if(w.ok) {
+					const uint32_t trimBeg = w.row, trimEnd = nrow - row0 - 1;
 					// res.reverse(), AlnRes::setShape trim shift, invertEdits for !fw
 					// (aligner_result.cpp:101-117, 822-828; edit.cpp:50-78)
-					const uint32_t nst = ned < A.maxedit ? ned : A.maxedit;
+					const uint32_t ned = w.ned, nst = ned < A.maxedit ? ned : A.maxedit;
 					if(fw) {
 						for(uint32_t i = 0; i < nst / 2; i++) {
 							const bt2g_edit t = ed[i];
@@ -384,9 +436,9 @@ k_sw_bt(BtArgs A) {
 							ed[i].pos = sz - (ed[i].pos - trimBeg) - (ed[i].type == 1 ? 0u : 1u);
 					}
 					int32_t refns = 0;
-					for(uint32_t c = col; c <= origCol; c++) refns += refm(c) > 15;
+					for(uint32_t c = w.col; c <= col0; c++) refns += rf_at(c) > 15;
 					bt2g_sw_aln a;
-					a.cand = (int32_t)ci; a.score = score; a.off = (int32_t)col; a.ns = ns; a.gaps = gaps;
+					a.cand = (int32_t)ci; a.score = w.score; a.off = (int32_t)w.col; a.ns = w.ns; a.gaps = w.gaps;
 					a.refns = refns; a.nedit = (int32_t)ned;
 					a.trim5p = (int32_t)(fw ? trimBeg : trimEnd); a.trim3p = (int32_t)(fw ? trimEnd : trimBeg);
 					a.pad = 0;

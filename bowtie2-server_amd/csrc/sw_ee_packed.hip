@@ -84,8 +84,10 @@ struct Half {
 #define BT2G_SW_WAVES 3
 #endif
 // STORE: also write every cell's H to the score plane for the backtrace
-// (sw_backtrace.hip): problem pi's column j, stack rows 16k..16k+15 at
-// plane + pi*hslot + (j*16S + 16k)*hbytes; hbytes 1 keeps u8 fills only.
+// (sw_backtrace.hip), block-major: problem pi's stack rows 16k..16k+15 of
+// column j at plane + pi*hslot + ((k*max_cols + j)*16)*hbytes, so that a
+// backtrace step (up-left) usually stays inside one 128-B line; hbytes 1 keeps
+// u8 fills only.
 template <bool SAMEGO, bool STORE>
 __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(BT2G_SW_WAVES)))
 k_sw_ee_sys(const bt2g_sw_problem* __restrict__ probs, uint32_t nprob, const uint8_t* __restrict__ reads,
@@ -405,9 +407,16 @@ k_sw_ee_sys(const bt2g_sw_problem* __restrict__ probs, uint32_t nprob, const uin
 		};
 		if(__ballot(nfloor != 0)) rows(std::true_type{});
 		else rows(std::false_type{});
+#ifdef BT2G_SW_NOSTORE
+		if(false) {                                   // timing experiments only
+#else
 		if(STORE && in_group) {
+#endif
 			const bool s0 = h[0].live && (uint32_t)j < h[0].ncol, s1 = h[1].live && (uint32_t)j < h[1].ncol;
-			const size_t cell = (size_t)j * (16u * S) + 16u * k;
+			const size_t cell = ((size_t)k * max_cols + (uint32_t)j) * 16u;
+#ifdef BT2G_SW_STORE_TINY
+			const uint64_t hslot = 0;                 // timing experiments only: all writes in 64 KB
+#endif
 			if(hbytes == 1) {
 				// bytes of 16 rows per problem: low halves -> a, high halves -> b
 				uint32_t a[4], b[4];

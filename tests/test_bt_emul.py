@@ -90,8 +90,10 @@ def test_bt_kernel_source_on_cpu(lib, src, kind):
             if o[0] and not o[2]:
                 keep[p] = False          # i16 fill: not in a u8 plane (naln -4)
                 continue
-            blk = plane[p * slot:(p + 1) * slot].reshape(maxcol, S16)
-            blk[:ncol, S16 - L:] = m[:, :, 0].T
+            # block-major: [stack row // 16][column][stack row % 16]
+            stack = np.zeros((S16, maxcol), np.uint8)
+            stack[S16 - L:, :ncol] = m[:, :, 0]
+            plane[p * slot:(p + 1) * slot] = stack.reshape(S16 // 16, 16, maxcol).transpose(0, 2, 1).ravel()
     mat = np.concatenate(mats)
     mat_off = np.array(offs, np.uint64)
     rects = np.zeros(n, bt2g.SWRECT_DTYPE)
