@@ -13,6 +13,7 @@
 #define __forceinline__ inline
 #define __launch_bounds__(...)
 #define __shared__ static
+#define amdgpu_waves_per_eu(...) unused
 struct dim3 { uint32_t x = 1, y = 1, z = 1; dim3(uint32_t a = 1, uint32_t b = 1, uint32_t c = 1) : x(a), y(b), z(c) {} };
 struct uint4 { uint32_t x, y, z, w; };
 struct int2 { int32_t x, y; };
