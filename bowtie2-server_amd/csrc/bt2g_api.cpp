@@ -91,6 +91,16 @@ int upload(bt2g_ctx* c, T** dst, const T* src, size_t count) {
 	return BT2G_OK;
 }
 
+// the backtrace reads the reference through aligned 16-B windows: `pad` zero
+// bytes after the end keep the last window in bounds
+int upload_padded(bt2g_ctx* c, uint8_t** dst, const uint8_t* src, size_t count, size_t pad) {
+	int rc = dalloc(c, (void**)dst, count + pad);
+	if(rc) return rc;
+	if(count) HIPCHK(hipMemcpy(*dst, src, count, hipMemcpyHostToDevice));
+	HIPCHK(hipMemset(*dst + count, 0, pad));
+	return BT2G_OK;
+}
+
 hipEvent_t get_event(bt2g_ctx* c) {
 	if(!c->evpool.empty()) {
 		hipEvent_t e = c->evpool.back();
@@ -276,7 +286,7 @@ int bt2g_open_mem(const bt2g_index_mem* m, int device, bt2g_ctx** out) {
 		return fail(BT2G_ERR_HIP, "hipStreamCreate failed");
 	}
 	if((rc = make_dev_ebwt(c, m->fw, true, c->fw)) || (rc = make_dev_ebwt(c, m->bw, false, c->bw)) ||
-	   (rc = upload(c, &c->ref_codes, m->ref_codes, (size_t)m->ref_starts[m->nref])) ||
+	   (rc = upload_padded(c, &c->ref_codes, m->ref_codes, (size_t)m->ref_starts[m->nref], 64)) ||
 	   (rc = upload(c, &c->ref_starts, m->ref_starts, (size_t)m->nref + 1))) {
 		bt2g_close(c);
 		return rc;
@@ -606,7 +616,7 @@ int bt2g_sw_align_bt_dev(bt2g_ctx* c, const uint8_t* reads, const uint8_t* quals
 		maxcol = c->bt_max_cols;
 		kind = c->bt_hbytes == 1 ? 0 : 1;
 		a.plane = c->bt_plane;
-		a.slot = (uint64_t)S16 * maxcol * (uint64_t)c->bt_hbytes;
+		a.slot = sw_plane_slot(stride, maxcol, c->bt_hbytes);
 		a.marks = c->bt_marks;
 		maxrow = c->bt_max_stride;
 		if((rc = sw_align_impl(c, reads, quals, stride, lens, probs, nprob, windows, sc, enable8, cap, res, cands,
@@ -629,7 +639,7 @@ int bt2g_sw_align_bt_dev(bt2g_ctx* c, const uint8_t* reads, const uint8_t* quals
 		if(packed) {
 			const int hb = all8 ? 1 : 2;
 			kind = hb == 1 ? 0 : 1;
-			a.slot = (uint64_t)S16 * maxcol * (uint64_t)hb;
+			a.slot = sw_plane_slot(stride, maxcol, hb);
 			uint8_t* plane;
 			if((rc = talloc((void**)&plane, (size_t)a.slot * nprob))) return rc;
 			a.plane = plane;
@@ -668,6 +678,11 @@ int bt2g_sw_align_bt_dev(bt2g_ctx* c, const uint8_t* reads, const uint8_t* quals
 	a.probs = probs; a.nprob = nprob; a.reads = reads; a.quals = quals; a.stride = stride; a.lens = lens;
 	a.windows = windows; a.ref_codes = c->ref_codes; a.ref_starts = c->ref_starts; a.rects = rects;
 	a.res = res; a.cands = cands; a.cap = cap; a.cstride = S16; a.pcols = maxcol;
+#ifdef BT2G_SW_NOMASK
+	a.use_mask = 0;   // timing experiments only
+#else
+	a.use_mask = S16 <= 256u;
+#endif
 	a.C = C; a.local = sc->local; a.ncl_const = sc->ncl_const; a.ncl_lin = sc->ncl_lin;
 	a.maxaln = maxaln; a.maxedit = maxedit; a.naln = naln; a.alns = alns; a.edits = edits; a.fates = fates;
 	{
@@ -685,7 +700,7 @@ int bt2g_reserve_sw_bt(bt2g_ctx* c, uint32_t max_problems, uint32_t max_stride, 
 	if(int rc = bt2g_reserve_sw(c, max_problems, max_cols)) return rc;
 	if(c->bt_plane) { (void)hipFree(c->bt_plane); (void)hipFree(c->bt_marks); }
 	c->bt_plane = nullptr; c->bt_marks = nullptr;
-	const uint64_t slot = (uint64_t)sw_packed_rows(max_stride) * max_cols * (uint64_t)hbytes;
+	const uint64_t slot = sw_plane_slot(max_stride, max_cols, hbytes);
 	HIPCHK(hipMalloc((void**)&c->bt_plane, slot * max_problems));
 	HIPCHK(hipMalloc((void**)&c->bt_marks, sizeof(uint32_t) * sw_bt_mslot(max_stride, max_cols) * max_problems));
 	c->bt_max_prob = max_problems;

@@ -53,6 +53,11 @@ void launch_sw_ee_packed(const bt2g_sw_problem* probs, uint32_t nprob, const uin
                          hipStream_t st);
 // Rows per strip stack of the systolic fill (its score-plane column stride).
 inline uint32_t sw_packed_rows(uint32_t stride) { return 16u * ((stride + 15u) / 16u); }
+// Score-plane bytes per problem: 16-row blocks x cols x hbytes, then one u16
+// mask of written blocks per column (sw_ee_packed.hip)
+inline uint64_t sw_plane_slot(uint32_t stride, uint32_t cols, int hbytes) {
+	return (uint64_t)sw_packed_rows(stride) * cols * (uint64_t)hbytes + (((uint64_t)cols * 2u + 15u) & ~(uint64_t)15u);
+}
 
 // Backtrace (sw_backtrace.hip): one lane per problem.
 struct BtArgs {
@@ -73,6 +78,7 @@ struct BtArgs {
 	uint64_t slot;                    //   bytes per problem
 	uint32_t cstride;                 //   rows per column (16-row blocks)
 	uint32_t pcols;                   //   columns per row block
+	int use_mask;                     //   per-column masks of written blocks (<= 16 blocks)
 	const int16_t* mat;               // kind 2: H,E,F triples
 	const uint64_t* mat_off;
 	uint32_t* marks;                  // per problem (mslot words): reportedThrough tiles

@@ -67,15 +67,20 @@ enum { ST_H = 0, ST_E = 1, ST_F = 2 };
 template <int KIND>
 struct Plane {
 	const uint8_t* base;   // kinds 0/1: the problem's slot; 2: its matrix
+	const uint16_t* mask;  // kinds 0/1: written 16-row blocks per column (null: all)
 	uint32_t pcols, ncol, pad;
 	int32_t off;      // score = raw - off
 	__device__ __forceinline__ size_t idx(uint32_t r, uint32_t c) const {
 		const uint32_t rs = pad + r;
 		return ((size_t)(rs >> 4) * pcols + c) * 16u + (rs & 15u);
 	}
+	// unwritten blocks hold cells below minsc: they read as the floor (raw 0)
+	__device__ __forceinline__ bool blk(uint32_t r, uint32_t c) const {
+		return !mask || ((mask[c] >> ((pad + r) >> 4)) & 1u);
+	}
 	__device__ __forceinline__ int32_t h(uint32_t r, uint32_t c) const {
-		if(KIND == 0) return (int32_t)base[idx(r, c)] - off;
-		if(KIND == 1) return (int32_t)((const uint16_t*)base)[idx(r, c)] - off;
+		if(KIND == 0) return (blk(r, c) ? (int32_t)base[idx(r, c)] : 0) - off;
+		if(KIND == 1) return (blk(r, c) ? (int32_t)((const uint16_t*)base)[idx(r, c)] : 0) - off;
 		return (int32_t)((const int16_t*)base)[((size_t)r * ncol + c) * 3] - off;
 	}
 };
@@ -100,6 +105,7 @@ k_sw_bt(BtArgs A) {
 	pl.ncol = ncol;
 	pl.pcols = A.pcols;
 	pl.pad = 0;
+	pl.mask = nullptr;
 	uint32_t pad = 0;
 	const uint8_t* slot = nullptr;
 	if(KIND == 2) {
@@ -112,6 +118,7 @@ k_sw_bt(BtArgs A) {
 		slot = A.plane + (size_t)p * A.slot;
 		pl.base = slot;
 		pl.pad = pad;
+		if(A.use_mask) pl.mask = (const uint16_t*)(slot + (size_t)A.cstride * A.pcols * es);
 		(void)es;
 		pl.off = variant == 0 ? 0xff : 0xffff;
 	}
@@ -141,6 +148,7 @@ k_sw_bt(BtArgs A) {
 			bool hit = false;
 #pragma unroll 1
 			for(int32_t o0 = ((int32_t)pad + rlo) & ~15; o0 <= (int32_t)pad + rhi; o0 += 16) {
+				if(pl.mask && !((pl.mask[c] >> (o0 >> 4)) & 1u)) continue;   // below minsc: no hit
 				const uint4 v = *(const uint4*)(slot + ((size_t)(o0 >> 4) * A.pcols + c) * 16u);
 				const uint32_t wv[4] = {v.x, v.y, v.z, v.w};
 #pragma unroll
@@ -195,35 +203,39 @@ k_sw_bt(BtArgs A) {
 		tile_get(r, c);
 		return (tbits & tbit(r, c)) != 0;
 	};
-	// 4-byte windows over the read, the qualities and the reference (aligned
-	// dwords: a walk moves one row / column at a time); a dword that would
-	// leave the array's extent [lo, hi) is not loaded (single byte instead)
-	struct Win { uint64_t a; uint32_t w; };
-	Win w_rd{~0ull, 0u}, w_q{~0ull, 0u}, w_rf{~0ull, 0u};
+	// 16-byte windows over the read, the qualities and the reference (aligned
+	// uint4: a walk moves one row / column at a time); a window that would
+	// leave [lo, hi) is not loaded (single byte instead).  Reads and
+	// qualities: [buffer start, end of this row's stride); the resident
+	// reference is padded by bt2g_open; explicit windows: their own extent.
+	struct Win { uint64_t a; uint4 w; };
+	Win w_rd{~0ull, make_uint4(0, 0, 0, 0)}, w_q = w_rd, w_rf = w_rd;
 	auto win = [&](Win& W, const uint8_t* ptr, const uint8_t* lo, const uint8_t* hi) -> int {
-		const uint64_t addr = (uint64_t)ptr, aa = addr & ~3ull;
+		const uint64_t addr = (uint64_t)ptr, aa = addr & ~15ull;
 		if(aa != W.a) {
-			if(aa < (uint64_t)lo || aa + 4u > (uint64_t)hi) return *ptr;
+			if(aa < (uint64_t)lo || aa + 16u > (uint64_t)hi) return *ptr;
 			W.a = aa;
-			W.w = *(const uint32_t*)aa;
+			W.w = *(const uint4*)aa;
 		}
-		return (int)((W.w >> ((addr & 3u) * 8u)) & 0xffu);
+		const uint32_t di = (uint32_t)(addr >> 2) & 3u;
+		const uint32_t d = di == 0 ? W.w.x : di == 1 ? W.w.y : di == 2 ? W.w.z : W.w.w;
+		return (int)((d >> ((addr & 3u) * 8u)) & 0xffu);
 	};
 	auto rd_at = [&](uint32_t r) -> int {   // read character of DP row r
-		const int raw = win(w_rd, rd + (fw ? r : nrow - 1 - r), rd, rd + nrow);
+		const int raw = win(w_rd, rd + (fw ? r : nrow - 1 - r), A.reads, rd + A.stride);
 		return fw ? raw : (raw > 3 ? 4 : 3 - raw);
 	};
 	auto q_at = [&](uint32_t r) -> int {
-		const int q = win(w_q, qu + (fw ? r : nrow - 1 - r), qu, qu + nrow) - 33;
+		const int q = win(w_q, qu + (fw ? r : nrow - 1 - r), A.quals, qu + A.stride) - 33;
 		return q < 0 ? 0 : (q > 40 ? 40 : q);
 	};
-	const uint8_t* wlo = P.win_off >= 0 ? A.windows + P.win_off : A.ref_codes + rs;
-	const uint8_t* whi = P.win_off >= 0 ? wlo + ncol + 1 : wlo + rlen;
+	const uint8_t* wlo = P.win_off >= 0 ? A.windows + P.win_off : A.ref_codes;
+	const uint8_t* whi = P.win_off >= 0 ? wlo + ncol + 1 : A.ref_codes + rs + rlen + 16u;
 	auto rf_at = [&](uint32_t c) -> int {   // reference mask of column c (aligner_sw.cpp:171-253)
 		if(P.win_off >= 0) return win(w_rf, wlo + c, wlo, whi);
 		const int64_t o = P.refl + (int64_t)c;
 		if(o < 0 || (uint64_t)o >= rlen) return 16;
-		const int code = win(w_rf, wlo + (uint64_t)o, wlo, whi);
+		const int code = win(w_rf, A.ref_codes + rs + (uint64_t)o, wlo, whi);
 		return code > 3 ? 16 : 1 << code;
 	};
 	// H of a cell; the u8 plane goes through a register copy of 4 columns x 16 rows
@@ -237,11 +249,21 @@ k_sw_bt(BtArgs A) {
 			cc0 = c >= 3u ? c - 3u : 0u;
 			if(cc0 + 4u > A.pcols) cc0 = A.pcols >= 4u ? A.pcols - 4u : 0u;
 			const uint4* qp = (const uint4*)(slot + ((size_t)b * A.pcols + cc0) * 16u);
+			// chunks and their block masks in one round trip, dead blocks zeroed after
 			const uint4 z = make_uint4(0, 0, 0, 0);
 			ch0 = cc0 < A.pcols ? qp[0] : z;
 			ch1 = cc0 + 1u < A.pcols ? qp[1] : z;
 			ch2 = cc0 + 2u < A.pcols ? qp[2] : z;
 			ch3 = cc0 + 3u < A.pcols ? qp[3] : z;
+			if(pl.mask) {
+				const uint32_t m0 = pl.mask[cc0], m1 = cc0 + 1u < A.pcols ? pl.mask[cc0 + 1u] : 0u;
+				const uint32_t m2 = cc0 + 2u < A.pcols ? pl.mask[cc0 + 2u] : 0u;
+				const uint32_t m3 = cc0 + 3u < A.pcols ? pl.mask[cc0 + 3u] : 0u;
+				if(!((m0 >> b) & 1u)) ch0 = z;
+				if(!((m1 >> b) & 1u)) ch1 = z;
+				if(!((m2 >> b) & 1u)) ch2 = z;
+				if(!((m3 >> b) & 1u)) ch3 = z;
+			}
 		}
 		const uint32_t u = c - cc0, di = (rsx & 15u) >> 2;
 		auto pick = [&](const uint4& v) -> uint32_t { return di == 0 ? v.x : di == 1 ? v.y : di == 2 ? v.z : v.w; };
@@ -265,14 +287,13 @@ k_sw_bt(BtArgs A) {
 		uint32_t row, col, ned;
 		int32_t score, ns, gaps;
 	};
-	auto walk = [&](uint32_t row, uint32_t col, bool mark, bool emit, bt2g_edit* ed) -> Walk {
+	auto walk = [&](uint32_t row, uint32_t col, int32_t cur, bool mark, bool emit, bt2g_edit* ed) -> Walk {
 		Walk w{true, false, row, col, 0u, 0, 0, 0};
 		auto push = [&](uint32_t pos, int type, int chr, int qchr) {
 			if(emit && w.ned < A.maxedit) ed[w.ned] = bt2g_edit{pos, (uint8_t)type, (uint8_t)chr, (uint8_t)qchr, 0};
 			w.ned++;
 		};
 		int st = ST_H;
-		int32_t cur = hget(row, col);
 		while(true) {
 			if(mark) {
 				// reportedThrough (aligner_swsse_ee_u8.cpp:1331-1336, 1556)
@@ -292,7 +313,10 @@ k_sw_bt(BtArgs A) {
 			int32_t nxt = 0;
 			if(st == ST_H) {
 				const bool wantd = col > 0;
-				const int32_t hul = wantd ? hget(row - 1, col - 1) : 0;
+				// in gap-barrier rows H is the diagonal term itself when above the
+				// floor (E and F are the floor there): H(up-left) = cur - score, no load
+				const bool derive = !gaps_ok(row) && (!local || cur > 0);
+				const int32_t hul = !wantd ? 0 : derive ? cur - sdiag(rc, m, q) : hget(row - 1, col - 1);
 				// diag equality; local mode also wants H(up-left) > 0 (floorsc)
 				const bool deq = wantd && cur == hul + sdiag(rc, m, q);
 				if(deq && okv(hul)) { mv = 0; nxt = hul; }
@@ -414,8 +438,9 @@ k_sw_bt(BtArgs A) {
 				// a later walk that succeeds is walked again to write them
 				bt2g_edit* ed = A.edits + ((size_t)p * A.maxaln + (size_t)nal) * A.maxedit;
 				const uint32_t row0 = (uint32_t)cd.row, col0 = (uint32_t)cd.col;
-				Walk w = walk(row0, col0, true, first, ed);
-				if(w.ok && !first) (void)walk(row0, col0, false, true, ed);
+				// the candidate's score is its cell's H
+				Walk w = walk(row0, col0, cd.score, true, first, ed);
+				if(w.ok && !first) (void)walk(row0, col0, cd.score, false, true, ed);
 				first = false;
 				if(local) done[ndone++] = make_int2(cd.row, cd.col);
 				if(w.ok) {

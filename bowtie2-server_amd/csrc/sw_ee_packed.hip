@@ -83,13 +83,16 @@ struct Half {
 #ifndef BT2G_SW_WAVES
 #define BT2G_SW_WAVES 3
 #endif
+#ifndef BT2G_SW_WAVES_STORE
+#define BT2G_SW_WAVES_STORE 2      // the score-plane stores need registers: no spills at 2
+#endif
 // STORE: also write every cell's H to the score plane for the backtrace
 // (sw_backtrace.hip), block-major: problem pi's stack rows 16k..16k+15 of
 // column j at plane + pi*hslot + ((k*max_cols + j)*16)*hbytes, so that a
 // backtrace step (up-left) usually stays inside one 128-B line; hbytes 1 keeps
 // u8 fills only.
 template <bool SAMEGO, bool STORE>
-__global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(BT2G_SW_WAVES)))
+__global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(STORE ? BT2G_SW_WAVES_STORE : BT2G_SW_WAVES)))
 k_sw_ee_sys(const bt2g_sw_problem* __restrict__ probs, uint32_t nprob, const uint8_t* __restrict__ reads,
             const uint8_t* __restrict__ quals, uint32_t stride, const uint32_t* __restrict__ lens,
             const uint8_t* __restrict__ windows, const uint8_t* __restrict__ ref_codes,
@@ -340,13 +343,25 @@ k_sw_ee_sys(const bt2g_sw_problem* __restrict__ probs, uint32_t nprob, const uin
 		}
 	}
 #else
-	uint32_t hout = 0, fout = 0;
+	uint32_t hout = 0, fout = 0, mout = 0;
 	uint32_t nsel = in_group ? mysel[0] : 0u;
 	const uint32_t T = ncolmax + S - 1;
+	// score plane: a 16-row block is written only when one of its cells can be
+	// on a backtrace (H >= minsc: every value a walk compares for equality is
+	// at least its own score, sw_backtrace.hip); per column, a 16-bit mask of
+	// the written blocks (S <= 16; beyond that every block is written)
+#ifdef BT2G_SW_NOMASK
+	const bool use_mask = false;           // timing experiments only
+#else
+	const bool use_mask = S <= 16u;
+#endif
+	const uint32_t thr0 = h[0].row0 + (uint32_t)h[0].minsc, thr1 = h[1].row0 + (uint32_t)h[1].minsc;
+	uint8_t* const mplane = plane + (size_t)16u * S * max_cols * (size_t)hbytes;
 	for(uint32_t t = 0; t < T; t++) {
 		// the lane above computed this lane's column in the previous step (DPP wave_shr:1)
 		const uint32_t hin = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)hout, 0x138, 0xf, 0xf, false);
 		const uint32_t fin = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)fout, 0x138, 0xf, 0xf, false);
+		const uint32_t mskin = STORE ? (uint32_t)__builtin_amdgcn_update_dpp(0, (int)mout, 0x138, 0xf, 0xf, false) : 0u;
 		const int j = (int)t - (int)k;
 		if(j < 0 || j >= (int)ncolmax) continue;
 		const uint32_t sel = nsel;
@@ -412,8 +427,23 @@ k_sw_ee_sys(const bt2g_sw_problem* __restrict__ probs, uint32_t nprob, const uin
 #else
 		if(STORE && in_group) {
 #endif
-			const bool s0 = h[0].live && (uint32_t)j < h[0].ncol, s1 = h[1].live && (uint32_t)j < h[1].ncol;
+			bool s0 = h[0].live && (uint32_t)j < h[0].ncol, s1 = h[1].live && (uint32_t)j < h[1].ncol;
 			const size_t cell = ((size_t)k * max_cols + (uint32_t)j) * 16u;
+			if(use_mask) {
+				uint32_t mx = Hc[0];
+#pragma unroll
+				for(int i = 1; i < R; i++) mx = pmax(mx, Hc[i]);
+				s0 = s0 && (mx & 0xffffu) >= thr0;
+				s1 = s1 && (mx >> 16) >= thr1;
+				// block masks of column j travel down the group with the H hand-off
+				mout = (top ? 0u : mskin) | ((uint32_t)s0 << k) | ((uint32_t)s1 << (16u + k));
+				if(bottom) {
+					if(h[0].live && (uint32_t)j < h[0].ncol)
+						*(uint16_t*)(mplane + (size_t)h[0].pi * hslot + 2u * (uint32_t)j) = (uint16_t)(mout & 0xffffu);
+					if(h[1].live && (uint32_t)j < h[1].ncol)
+						*(uint16_t*)(mplane + (size_t)h[1].pi * hslot + 2u * (uint32_t)j) = (uint16_t)(mout >> 16);
+				}
+			}
 #ifdef BT2G_SW_STORE_TINY
 			const uint64_t hslot = 0;                 // timing experiments only: all writes in 64 KB
 #endif

@@ -73,7 +73,7 @@ def test_bt_kernel_source_on_cpu(lib, src, kind):
     maxcol = int(probs["ncol"].max())
     maxrow = int(g["lens"].max())
     mats, offs, tot = [], [], 0
-    slot = S16 * maxcol
+    slot = S16 * maxcol + ((maxcol * 2 + 15) & ~15)      # plane + per-column block masks
     plane = np.zeros(slot * n if kind == 0 else 16, np.uint8)
     keep = np.ones(n, bool)
     for p, rd, q, rf, minsc, fw, out, cref in sw_problems(g):
@@ -90,10 +90,20 @@ def test_bt_kernel_source_on_cpu(lib, src, kind):
             if o[0] and not o[2]:
                 keep[p] = False          # i16 fill: not in a u8 plane (naln -4)
                 continue
-            # block-major: [stack row // 16][column][stack row % 16]
-            stack = np.zeros((S16, maxcol), np.uint8)
+            # block-major: [stack row // 16][column][stack row % 16]; as the fill,
+            # only blocks holding a cell >= minsc are written (others garbage)
+            stack = np.full((S16, maxcol), 0xff, np.uint8)
             stack[S16 - L:, :ncol] = m[:, :, 0]
-            plane[p * slot:(p + 1) * slot] = stack.reshape(S16 // 16, 16, maxcol).transpose(0, 2, 1).ravel()
+            blocks = stack.reshape(S16 // 16, 16, maxcol)
+            live = blocks.max(1) >= 255 + minsc                      # (blocks, cols)
+            if S16 > 256:
+                live[:] = True                                       # no masks: all written
+            blocks = np.where(live[:, None, :], blocks, 0x5a)        # dead: garbage
+            plane[p * slot:p * slot + S16 * maxcol] = blocks.transpose(0, 2, 1).ravel()
+            if S16 <= 256:
+                masks = (live.astype(np.uint32) << np.arange(S16 // 16)[:, None].astype(np.uint32)).sum(0)
+                plane[p * slot + S16 * maxcol:p * slot + S16 * maxcol + 2 * maxcol] = \
+                    masks.astype(np.uint16).view(np.uint8)
     mat = np.concatenate(mats)
     mat_off = np.array(offs, np.uint64)
     rects = np.zeros(n, bt2g.SWRECT_DTYPE)
