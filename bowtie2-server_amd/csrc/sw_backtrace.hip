@@ -295,7 +295,11 @@ k_sw_bt(BtArgs A) {
 		};
 		int st = ST_H;
 		while(true) {
-			if(mark) {
+			// end-to-end: every candidate starts in the last row and the bottom
+			// gap-barrier rows allow only diagonal moves, so walks there stay on
+			// their own diagonals and can neither meet nor be met: no marks
+			const bool bottom_bar = !local && row + (uint32_t)gb >= nrow;
+			if(mark && !bottom_bar) {
 				// reportedThrough (aligner_swsse_ee_u8.cpp:1331-1336, 1556)
 				tile_get(row, col);
 				const uint64_t bt = tbit(row, col);
@@ -311,18 +315,27 @@ k_sw_bt(BtArgs A) {
 			const int rc = rd_at(row), m = rf_at(col), q = q_at(row);
 			int mv = -1;   // 0 diag, 1 ref open, 2 ref extend, 3 read open, 4 read extend
 			int32_t nxt = 0;
+			// in gap-barrier rows H is the diagonal term itself when above the
+			// floor (E and F are the floor there): H(up-left) = cur - score, no load
+			const bool derive = st == ST_H && !gaps_ok(row) && (!local || cur > 0);
+			// one plane read site for the neighbour the state tests first:
+			// H -> up-left, E -> left, F -> up
+			const bool need1 = st == ST_H ? (col > 0 && !derive) : (st == ST_E ? col > 0 : true);
+			const int32_t v1 = need1 ? hget(st == ST_E ? row : row - 1, st == ST_F ? col : col - 1) : 0;
 			if(st == ST_H) {
 				const bool wantd = col > 0;
-				// in gap-barrier rows H is the diagonal term itself when above the
-				// floor (E and F are the floor there): H(up-left) = cur - score, no load
-				const bool derive = !gaps_ok(row) && (!local || cur > 0);
-				const int32_t hul = !wantd ? 0 : derive ? cur - sdiag(rc, m, q) : hget(row - 1, col - 1);
+				const int32_t hul = !wantd ? 0 : derive ? cur - sdiag(rc, m, q) : v1;
 				// diag equality; local mode also wants H(up-left) > 0 (floorsc)
 				const bool deq = wantd && cur == hul + sdiag(rc, m, q);
 				if(deq && okv(hul)) { mv = 0; nxt = hul; }
 				if(mv < 0 && gaps_ok(row)) {
-					const int32_t hu = hget(row - 1, col);
-					const int32_t hl = col > 0 ? hget(row, col - 1) : 0;
+					int32_t hu = 0, hl = 0;
+#pragma unroll 1
+					for(int t = 0; t < 2; t++) {          // one read site for up and left
+						if(t == 1 && col == 0) break;
+						const int32_t v = hget(t == 0 ? row - 1 : row, t == 0 ? col : col - 1);
+						if(t == 0) hu = v; else hl = v;
+					}
 					// F(row-1, col) == cur + rfge: H(x-k, col) == cur + rfgo + k*rfge, x = row-1,
 					// rows x..x-k+1 outside the barrier, x-k >= 0
 					bool fup = false;
@@ -361,11 +374,11 @@ k_sw_bt(BtArgs A) {
 				if(mv < 0) break;   // empty cell: the alignment starts here
 			} else if(st == ST_E) {
 				if(col == 0) break;   // unreachable: E(row, 0) is the floor
-				const int32_t hl = hget(row, col - 1);
+				const int32_t hl = v1;
 				if(okv(hl) && hl - rdgo == cur) { mv = 3; nxt = hl; }
 				else { mv = 4; nxt = cur + rdge; }
 			} else {
-				const int32_t hu = hget(row - 1, col);
+				const int32_t hu = v1;
 				if(okv(hu) && hu - rfgo == cur) { mv = 1; nxt = hu; }
 				else { mv = 2; nxt = cur + rfge; }
 			}
@@ -419,7 +432,8 @@ k_sw_bt(BtArgs A) {
 		int8_t fate;
 		if(cd.score < P.minsc) {
 			fate = 5;                                   // BT_CAND_FATE_FILT_SCORE
-		} else if(marked((uint32_t)cd.row, (uint32_t)cd.col)) {
+		} else if((local || (uint32_t)cd.row + (uint32_t)gb < nrow) && marked((uint32_t)cd.row, (uint32_t)cd.col)) {
+			// (end-to-end starts in the bottom barrier rows are never marked: see walk)
 			fate = 3;                                   // BT_CAND_FATE_FILT_START
 		} else {
 			bool dom = false;
