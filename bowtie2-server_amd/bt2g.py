@@ -19,7 +19,7 @@ LIB_PATH = os.environ.get("BT2G_LIB", os.path.join(HERE, "libbt2g.so"))
 
 BT2G_OK = 0
 BT2G_ERR_OVERFLOW = -6
-K_EXACT_SWEEP, K_SEED_SEARCH, K_ONE_MM, K_GET_OFFSET, K_SW_ALIGN, K_SW_BACKTRACE = range(6)
+K_EXACT_SWEEP, K_SEED_SEARCH, K_ONE_MM, K_GET_OFFSET, K_SW_ALIGN, K_SW_BACKTRACE, K_UNGAPPED = range(7)
 
 
 class Scoring(C.Structure):
@@ -44,6 +44,9 @@ SWCAND_DTYPE = np.dtype([("row", "<i4"), ("col", "<i4"), ("score", "<i4")])
 SWRECT_DTYPE = np.dtype([("triml", "<i4"), ("corel", "<i4"), ("corer", "<i4"), ("pad", "<i4")])
 SWALN_DTYPE = np.dtype([(n, "<i4") for n in ("cand", "score", "off", "ns", "gaps", "refns", "nedit", "trim5p",
                                              "trim3p", "pad")])
+UGPROB_DTYPE = np.dtype([("read", "<u4"), ("fw", "<i4"), ("off", "<i8"), ("refidx", "<u4"), ("minsc", "<i4")])
+UGRES_DTYPE = np.dtype([("ret", "<i4"), ("score", "<i4"), ("refoff", "<i8")] +
+                       [(n, "<i4") for n in ("ns", "refns", "nedit", "trim5p", "trim3p", "pad")])
 EDIT_DTYPE = np.dtype([("pos", "<u4"), ("type", "u1"), ("chr", "u1"), ("qchr", "u1"), ("pad", "u1")])
 
 
@@ -108,6 +111,8 @@ def lib():
         L.bt2g_sw_align_bt_dev.argtypes = [vp, vp, vp, u32, vp, vp, u32, vp, vp, C.POINTER(Scoring), C.c_int, u32,
                                            vp, vp, u32, u32, vp, vp, vp, vp, vp]
         L.bt2g_reserve_sw_bt.argtypes = [vp, u32, u32, u32, C.c_int]
+        L.bt2g_ungapped.argtypes = [vp, vp, vp, u32, vp, vp, u32, C.POINTER(Scoring), C.c_int, u32, vp, vp]
+        L.bt2g_ungapped_dev.argtypes = [vp, vp, vp, u32, vp, vp, u32, C.POINTER(Scoring), C.c_int, u32, vp, vp, vp]
         L.bt2g_set_profiling.argtypes = [vp, C.c_int]
         L.bt2g_kernel_stats.argtypes = [vp, C.c_int, C.POINTER(u64), C.POINTER(C.c_double)]
         L.bt2g_reset_stats.argtypes = [vp]
@@ -266,6 +271,19 @@ class Engine:
                                     int(enable8), cap, _ptr(res), _ptr(cands), maxaln, maxedit, _ptr(naln),
                                     _ptr(alns), _ptr(edits), _ptr(fates)))
         return res, cands, naln, alns, edits, fates
+
+    def ungapped(self, reads, quals, lens, probs, local=False, ohang=False, maxedit=256, sc=None):
+        """SwAligner::ungappedAlign per problem (bt2g_ungapped): res (UGRES_DTYPE),
+        edits (n x maxedit EDIT_DTYPE)."""
+        reads, quals, lens = _c(reads, np.uint8), _c(quals, np.uint8), _c(lens, np.uint32)
+        probs = _c(probs, UGPROB_DTYPE)
+        n = len(probs)
+        res = np.zeros(n, UGRES_DTYPE)
+        edits = np.zeros((n, maxedit), EDIT_DTYPE)
+        sc = scoring(local) if sc is None else sc
+        _chk(lib().bt2g_ungapped(self.h, _ptr(reads), _ptr(quals), reads.shape[1], _ptr(lens), _ptr(probs), n,
+                                 C.byref(sc), int(ohang), maxedit, _ptr(res), _ptr(edits)))
+        return res, edits
 
     # ---- measurement -------------------------------------------------------
     def set_profiling(self, on=True):

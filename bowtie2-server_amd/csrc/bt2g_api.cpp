@@ -694,6 +694,24 @@ int bt2g_sw_align_bt_dev(bt2g_ctx* c, const uint8_t* reads, const uint8_t* quals
 	return BT2G_OK;
 }
 
+int bt2g_ungapped_dev(bt2g_ctx* c, const uint8_t* reads, const uint8_t* quals, uint32_t stride,
+                      const uint32_t* lens, const bt2g_ug_problem* probs, uint32_t n, const bt2g_scoring* sc,
+                      int ohang, uint32_t maxedit, bt2g_ug_result* res, bt2g_edit* edits, void* stream) {
+	if(!c || !sc || !res || (!edits && maxedit)) return fail(BT2G_ERR_ARG, "null argument");
+	if(int rc = check_reads(stride, n)) return rc;
+	if(n == 0) return BT2G_OK;
+	hipStream_t st = pick(c, stream);
+	SwConst C;
+	sw_fill_consts(*sc, C);
+	{
+		ProfScope ps(c, 6, st);
+		launch_ungapped(probs, n, reads, quals, stride, lens, c->ref_codes, c->ref_starts, C, sc->local, sc->ncl_const,
+		                sc->ncl_lin, ohang, maxedit, res, edits, st);
+	}
+	HIPCHK(hipGetLastError());
+	return BT2G_OK;
+}
+
 int bt2g_reserve_sw_bt(bt2g_ctx* c, uint32_t max_problems, uint32_t max_stride, uint32_t max_cols, int hbytes) {
 	if(!c || max_problems == 0 || max_cols == 0 || max_stride == 0 || (hbytes != 1 && hbytes != 2))
 		return fail(BT2G_ERR_ARG, "bad reservation");
@@ -929,6 +947,36 @@ int bt2g_sw_align_bt(bt2g_ctx* c, const uint8_t* reads, const uint8_t* quals, ui
 	for(uint32_t i = 0; i < nprob; i++)
 		if(res[i].ncand > (int32_t)cap) return fail(BT2G_ERR_OVERFLOW, "problem %u: %d candidates > cap %u", i,
 		                                             res[i].ncand, cap);
+	return BT2G_OK;
+}
+
+}  // extern "C"
+
+extern "C" {
+
+int bt2g_ungapped(bt2g_ctx* c, const uint8_t* reads, const uint8_t* quals, uint32_t stride, const uint32_t* lens,
+                  const bt2g_ug_problem* probs, uint32_t n, const bt2g_scoring* sc, int ohang, uint32_t maxedit,
+                  bt2g_ug_result* res, bt2g_edit* edits) {
+	if(!c) return fail(BT2G_ERR_ARG, "null ctx");
+	HIPCHK(hipSetDevice(c->device));
+	if(n == 0) return BT2G_OK;
+	uint32_t nreads = 0;
+	for(uint32_t i = 0; i < n; i++) nreads = probs[i].read + 1 > nreads ? probs[i].read + 1 : nreads;
+	Tmp t;
+	uint8_t *dr, *dq;
+	uint32_t* dl;
+	bt2g_ug_problem* dp;
+	bt2g_ug_result* dres;
+	bt2g_edit* ded;
+	int rc;
+	if((rc = t.up(&dr, reads, (size_t)nreads * stride)) || (rc = t.up(&dq, quals, (size_t)nreads * stride)) ||
+	   (rc = t.up(&dl, lens, nreads)) || (rc = t.up(&dp, probs, n)) ||
+	   (rc = t.up(&dres, (const bt2g_ug_result*)nullptr, n)) ||
+	   (rc = t.up(&ded, (const bt2g_edit*)nullptr, (size_t)n * maxedit)))
+		return rc;
+	if((rc = bt2g_ungapped_dev(c, dr, dq, stride, dl, dp, n, sc, ohang, maxedit, dres, ded, c->stream))) return rc;
+	HIPCHK(hipStreamSynchronize(c->stream));
+	if((rc = down(res, dres, n)) || (rc = down(edits, ded, (size_t)n * maxedit))) return rc;
 	return BT2G_OK;
 }
 

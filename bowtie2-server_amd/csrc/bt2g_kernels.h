@@ -106,3 +106,8 @@ inline uint64_t sw_bt_mslot(uint32_t rows, uint32_t cols) {
 }
 void launch_sort_cands(const bt2g_sw_result* res, bt2g_sw_cand* cands, uint32_t nprob, uint32_t cap,
                        uint32_t* big, uint32_t* nbig, hipStream_t st);
+
+void launch_ungapped(const bt2g_ug_problem* probs, uint32_t n, const uint8_t* reads, const uint8_t* quals,
+                     uint32_t stride, const uint32_t* lens, const uint8_t* ref_codes, const uint64_t* ref_starts,
+                     const SwConst& C, int local, double ncl_const, double ncl_lin, int ohang, uint32_t maxedit,
+                     bt2g_ug_result* res, bt2g_edit* edits, hipStream_t st);

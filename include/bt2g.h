@@ -285,6 +285,36 @@ int bt2g_sw_align_bt_dev(bt2g_ctx* ctx, const uint8_t* reads, const uint8_t* qua
  * with enable8 and minsc >= -254, the default 150 bp case), 2 holds any. */
 int bt2g_reserve_sw_bt(bt2g_ctx* ctx, uint32_t max_problems, uint32_t max_rows, uint32_t max_cols, int hbytes);
 
+/* ---- ungapped alignment (row A22) ----------------------------------------- */
+
+/* One SwAligner::ungappedAlign call (aligner_sw.cpp:286-494, called from
+ * aligner_sw_driver.cpp:1032-1073): the read (fw) or its reverse complement
+ * (!fw) against reference `refidx` starting at offset `off` (may be < 0). */
+typedef struct {
+	uint32_t read;
+	int32_t  fw;
+	int64_t  off;
+	uint32_t refidx;
+	int32_t  minsc;
+} bt2g_ug_problem;
+
+typedef struct {
+	int32_t ret;        /* ungappedAlign's return: 1 aligned, 0 not, -1 defer to DP (local) */
+	int32_t score;
+	int64_t refoff;     /* AlnRes::refoff() (coord.off + rowi) */
+	int32_t ns, refns, nedit, trim5p, trim3p, pad;
+} bt2g_ug_result;
+
+/* ungappedAlign for n problems with the scoring scheme sc (local or
+ * end-to-end); ohang = gReportOverhangs.  Edits of problem p (mismatches,
+ * 5'->3' after trimming) at edits[p*maxedit ..], nedit may exceed maxedit. */
+int bt2g_ungapped(bt2g_ctx* ctx, const uint8_t* reads, const uint8_t* quals, uint32_t stride, const uint32_t* lens,
+                  const bt2g_ug_problem* probs, uint32_t n, const bt2g_scoring* sc, int ohang, uint32_t maxedit,
+                  bt2g_ug_result* res, bt2g_edit* edits);
+int bt2g_ungapped_dev(bt2g_ctx* ctx, const uint8_t* reads, const uint8_t* quals, uint32_t stride,
+                      const uint32_t* lens, const bt2g_ug_problem* probs, uint32_t n, const bt2g_scoring* sc,
+                      int ohang, uint32_t maxedit, bt2g_ug_result* res, bt2g_edit* edits, void* stream);
+
 /* ---- bench batch glue (NOT reference seams) -------------------------------
  * Device-side glue used by bench.py between the seed-phase calls and
  * bt2g_sw_align_dev.  The reference's SwDriver::extendSeeds chooses hits with
@@ -320,7 +350,7 @@ int bt2g_bench_frame_dev(uint32_t n, const uint32_t* lens, const uint32_t* offs,
 /* ---- measurement --------------------------------------------------------- */
 /* Kernel timing with HIP events on the launch stream (off by default). */
 int bt2g_set_profiling(bt2g_ctx* ctx, int on);
-/* kernel ids: 0 exact_sweep, 1 seed_search, 2 one_mm, 3 get_offset, 4 sw_align, 5 sw_backtrace */
+/* kernel ids: 0 exact_sweep, 1 seed_search, 2 one_mm, 3 get_offset, 4 sw_align, 5 sw_backtrace, 6 ungapped */
 int bt2g_kernel_stats(bt2g_ctx* ctx, int kernel, uint64_t* launches, double* total_ms);
 int bt2g_reset_stats(bt2g_ctx* ctx);
 

@@ -20,6 +20,7 @@
  *     loc u8  aligner_swsse_loc_u8.cpp:75-159, 927-1336 (gather 1389-1500)
  *     loc i16 aligner_swsse_loc_i16.cpp:75-145, 938-1367 (gather 1420-1535)
  *     dispatch SwAligner::align aligner_sw.cpp:500-729; Scoring scoring.h:96-440
+ *   ungapped: SwAligner::ungappedAlign aligner_sw.cpp:286-494
  *   backtrace: SwAligner::nextAlignment aligner_sw.cpp:737-1146 with
  *     backtraceNucleotides{End2End,Local}Sse{U8,I16}
  *     (aligner_swsse_ee_u8.cpp:1283-1780, aligner_swsse_loc_u8.cpp:1588-2175,
@@ -1113,4 +1114,73 @@ int orc_sw_bt(const uint8_t* rd, const uint8_t* q33, int nrow, const uint8_t* rf
 	}
 	free(mat); free(cands);
 	return na;
+}
+
+/* ---------------------------------------------------------------------- */
+/* SwAligner::ungappedAlign (aligner_sw.cpp:286-494)                        */
+/* ---------------------------------------------------------------------- */
+/* rd/q33: the read as aligned (reverse-complemented when !fw); rf: reference
+ * codes 0..4 of positions rfi .. rfi+len-1 (4 off the reference); reflen:
+ * length of the reference.  out[10] = {ret, score, refoff, ns, refns, nedit,
+ * trim5p, trim3p, 0, 0}; edits (pos, type, chr, qchr) x nedit. */
+int orc_ungapped(const uint8_t* rd, const uint8_t* q33, int len, const uint8_t* rf, int64_t rfi, int64_t reflen,
+                 int64_t minsc, const orc_scoring* sc, int ohang, int fw, int64_t* out, int32_t* edits) {
+	memset(out, 0, 10 * sizeof(int64_t));
+	int nceil = (int)(sc->ncl_const + sc->ncl_lin * (double)len);
+	if(nceil < 0) nceil = 0;
+	int64_t rff = rfi + len;
+	int64_t leftNs = 0, rightNs = 0;
+	if(rfi < 0) { if(!ohang) return 0; leftNs = -rfi; }
+	if(rff > reflen) { if(!ohang) return 0; rightNs = rff - reflen; }
+	if(leftNs + rightNs > nceil) return 0;
+	int64_t score = 0;
+	int ns = 0;
+	size_t rowi = 0, rowf = (size_t)len - 1;
+	if(!sc->local) {
+		for(int i = 0; i < len; i++) {
+			int refm = 1 << rf[i];
+			if(rd[i] > 3 || refm > 15) ns++;
+			score += score_of(sc, rd[i], refm, q33[i] - 33);
+			if(score < minsc || ns > nceil) return 0;
+		}
+	} else {
+		int64_t floorsc = 0, scoreMax = 0;
+		size_t lastfloor = 0, sols = 0;
+		rowi = (size_t)-1;
+		for(int i = 0; i < len; i++) {
+			int refm = 1 << rf[i];
+			if(rd[i] > 3 || refm > 15) ns++;
+			score += score_of(sc, rd[i], refm, q33[i] - 33);
+			if(score >= minsc && score >= scoreMax) {
+				scoreMax = score;
+				rowf = (size_t)i;
+				if(rowi != lastfloor) { rowi = lastfloor; sols++; }
+			}
+			if(score <= floorsc) { score = floorsc; lastfloor = (size_t)i + 1; }
+		}
+		if(ns > nceil || scoreMax < minsc) return 0;
+		if(sols > 1) { out[0] = -1; return -1; }
+		score = scoreMax;
+	}
+	int ned = 0, refns = 0;
+	for(size_t i = rowi; i <= rowf; i++) {
+		if(rf[i] > 3 || rd[i] != rf[i]) {
+			int32_t* e = edits + 4 * ned;
+			e[0] = (int32_t)i; e[1] = 3; e[2] = mask2dna_c(1 << rf[i]); e[3] = "ACGTN"[rd[i]];
+			ned++;
+			if(rf[i] > 3) refns++;
+		}
+	}
+	size_t trimEnd = (size_t)len - 1 - rowf;
+	/* setShape: shift by the rows trimmed at the top; invertEdits for !fw */
+	for(int i = 0; i < ned; i++) edits[4 * i] -= (int32_t)rowi;
+	if(!fw) {
+		int32_t sz = len - (int32_t)rowi - (int32_t)trimEnd;
+		for(int i = 0; i < ned / 2; i++)
+			for(int k = 0; k < 4; k++) { int32_t t = edits[4 * i + k]; edits[4 * i + k] = edits[4 * (ned - 1 - i) + k]; edits[4 * (ned - 1 - i) + k] = t; }
+		for(int i = 0; i < ned; i++) edits[4 * i] = sz - edits[4 * i] - 1;
+	}
+	out[0] = 1; out[1] = score; out[2] = rfi + (int64_t)rowi; out[3] = ns; out[4] = refns; out[5] = ned;
+	out[6] = (int64_t)(fw ? rowi : trimEnd); out[7] = (int64_t)(fw ? trimEnd : rowi);
+	return 1;
 }

@@ -57,6 +57,9 @@ class Oracle:
         L.orc_bilf.argtypes = [C.POINTER(OrcEbwt), C.c_uint32, C.c_uint32, C.c_uint32] + [C.c_void_p] * 4
         L.orc_sw.argtypes = [C.c_void_p, C.c_void_p, C.c_int, C.c_void_p, C.c_int, C.c_int64,
                              C.POINTER(OrcScoring), C.c_int, C.c_int, C.c_void_p, C.c_void_p, C.c_void_p]
+        L.orc_ungapped.restype = C.c_int
+        L.orc_ungapped.argtypes = [C.c_void_p, C.c_void_p, C.c_int, C.c_void_p, C.c_int64, C.c_int64, C.c_int64,
+                                   C.POINTER(OrcScoring), C.c_int, C.c_int, C.c_void_p, C.c_void_p]
         L.orc_sw_bt.restype = C.c_int
         L.orc_sw_bt.argtypes = [C.c_void_p, C.c_void_p, C.c_int, C.c_void_p, C.c_int, C.c_int64,
                                 C.POINTER(OrcScoring), C.c_int, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int,
@@ -146,3 +149,16 @@ class Oracle:
         ed = edits.reshape(maxaln, maxedit, 4)
         eds = [ed[i, :min(int(aln[i, 7]), maxedit)].copy() for i in range(k)]
         return out[:7], aln, eds, fates[:min(int(out[6]), len(fates))].copy()
+
+    def ungapped(self, rd, q33, rf, rfi, reflen, minsc, local, fw=True, ohang=False, sc=None):
+        """SwAligner::ungappedAlign: rd/q33 as aligned, rf = reference codes at
+        rfi..rfi+len-1 (4 off the reference).  Returns (out[10], edits k x 4)."""
+        rd = np.ascontiguousarray(rd, np.uint8)
+        q33 = np.ascontiguousarray(q33, np.uint8)
+        rf = np.ascontiguousarray(rf, np.uint8)
+        out = np.zeros(10, np.int64)
+        ed = np.zeros(4 * (len(rd) + 1), np.int32)
+        sc = sc if sc is not None else scoring(local)
+        self.lib.orc_ungapped(_p(rd), _p(q33), len(rd), _p(rf), int(rfi), int(reflen), int(minsc), C.byref(sc),
+                              1 if ohang else 0, 1 if fw else 0, _p(out), _p(ed))
+        return out, ed[:4 * int(out[5])].reshape(-1, 4)

@@ -574,3 +574,46 @@ void bt2ref_sw_bt_batch(int n, const char** seqs, const char** quals, const uint
 }
 
 } // extern "C"
+
+// ---- ungapped alignment (row 8a A22) -----------------------------------------
+extern "C" {
+
+// SwAligner::ungappedAlign (aligner_sw.cpp:286-494) for n reads against the
+// loaded index's reference, each at (refidx[i], off[i]) on strand fw[i], with
+// the read (fw) or its reverse complement (as aligner_sw_driver.cpp:1034-1043).
+// out: n x 10 = {ret, score, refoff, ns, refns, nedit, trim5p, trim3p, 0, 0};
+// edits[(i*maxedit + e)*4 + {pos, type, chr, qchr}].
+void bt2ref_ungapped(void* vh, int n, const char** seqs, const char** quals, const uint8_t* fws,
+                     const uint32_t* refidx, const int64_t* off, const int64_t* minsc, const ScoreParams* sp,
+                     int ohang, int maxedit, int64_t* out, int32_t* edits) {
+	RefHandle* h = (RefHandle*)vh;
+	Scoring sc = makeScoring(*sp);
+	SwAligner sw(NULL);
+	SwResult res;
+	for(int i = 0; i < n; i++) {
+		BTDnaString rdfw(seqs[i], true), rdrc = rdfw;
+		rdrc.reverseComp();
+		BTString qfw(quals[i]), qrc = qfw;
+		qrc.reverse();
+		bool fw = fws[i] != 0;
+		Coord coord((TRefId)refidx[i], (TRefOff)off[i], fw);
+		size_t tlen = h->refs->approxLen(refidx[i]);
+		res.reset();
+		int ret = sw.ungappedAlign(fw ? rdfw : rdrc, fw ? qfw : qrc, coord, *h->refs, tlen, sc, ohang != 0,
+		                           minsc[i], res);
+		int64_t* o = out + 10 * (size_t)i;
+		memset(o, 0, 10 * sizeof(int64_t));
+		o[0] = ret;
+		if(ret == 1) {
+			const AlnRes& a = res.alres;
+			o[1] = a.score().score(); o[2] = a.refoff(); o[3] = a.score().ns(); o[4] = (int64_t)a.refNs();
+			o[5] = (int64_t)a.ned().size(); o[6] = (int64_t)a.trimmed5p(true); o[7] = (int64_t)a.trimmed3p(true);
+			for(size_t e = 0; e < a.ned().size() && (int)e < maxedit; e++) {
+				int32_t* q = edits + ((size_t)i * maxedit + e) * 4;
+				q[0] = (int32_t)a.ned()[e].pos; q[1] = a.ned()[e].type; q[2] = a.ned()[e].chr; q[3] = a.ned()[e].qchr;
+			}
+		}
+	}
+}
+
+} // extern "C"

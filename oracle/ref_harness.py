@@ -162,6 +162,25 @@ class RefIndex:
                              int(norc), cap, _p(out, C.c_int64), _p(counts, C.c_int32), _p(bw, C.c_uint64))
         return out.reshape(n, cap, 6), counts, bw
 
+    def ungapped(self, seqs, quals, fws, refidx, offs, minsc, local, ohang=False, maxedit=256):
+        """SwAligner::ungappedAlign per read.  Returns (out n x 10, edits list)."""
+        L = self.L
+        L.bt2ref_ungapped.argtypes = [C.c_void_p, C.c_int, C.POINTER(C.c_char_p), C.POINTER(C.c_char_p),
+                                      C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.POINTER(ScoreParams),
+                                      C.c_int, C.c_int, C.c_void_p, C.c_void_p]
+        n = len(seqs)
+        fws = np.ascontiguousarray(fws, np.uint8)
+        refidx = np.ascontiguousarray(refidx, np.uint32)
+        offs = np.ascontiguousarray(offs, np.int64)
+        minsc = np.ascontiguousarray(minsc, np.int64)
+        out = np.zeros((n, 10), np.int64)
+        ed = np.zeros((n, maxedit, 4), np.int32)
+        sp = score_params(local)
+        L.bt2ref_ungapped(self.h, n, _cstrs(seqs), _cstrs(quals), fws.ctypes.data, refidx.ctypes.data,
+                          offs.ctypes.data, minsc.ctypes.data, C.byref(sp), 1 if ohang else 0, maxedit,
+                          out.ctypes.data, ed.ctypes.data)
+        return out, [ed[i, :int(out[i, 5])].copy() for i in range(n)]
+
     def seed_search(self, seqs, quals, seedlen, interval, offset, maxseeds=64):
         n = len(seqs)
         out = np.zeros(n * 2 * maxseeds * 4, np.uint32)

@@ -123,3 +123,31 @@ def test_sw_backtrace(orc, src):
         assert np.array_equal(fates, efates), (src, p)
         nal += len(a)
     assert nal > 50
+
+
+def ug_cases(idx, g, mode):
+    """(read as aligned, quals as aligned, reference codes at off..off+L-1, ...) per fixture read."""
+    for i in range(len(g["fw"])):
+        rd, q = g["reads"][i], g["quals"][i]
+        fw = bool(g["fw"][i])
+        if not fw:
+            rd, q = np.where(rd > 3, 4, 3 - rd)[::-1], q[::-1]
+        ref = idx.ref_codes[int(g["refidx"][i])]
+        o = int(g["off"][i])
+        pos = np.arange(o, o + len(rd))
+        rf = np.where((pos >= 0) & (pos < len(ref)), ref[np.clip(pos, 0, len(ref) - 1)], 4).astype(np.uint8)
+        exp = g[mode + "_out"][i]
+        ee = g[mode + "_edits"][g[mode + "_edit_off"][i]:g[mode + "_edit_off"][i + 1]]
+        yield i, rd, q, rf, o, len(ref), int(g[mode + "_minsc"][i]), fw, exp, ee
+
+
+@pytest.mark.parametrize("name", ["lambda", "synth"])
+@pytest.mark.parametrize("mode", ["ee", "loc"])
+def test_ungapped(orc, name, mode):
+    """SwAligner::ungappedAlign (aligner_sw.cpp:286-494): return code, score,
+    offset, N counts, trims and edits equal the reference's."""
+    idx, g = get_index(name), load_golden("ug_" + name)
+    for i, rd, q, rf, o, reflen, minsc, fw, exp, ee in ug_cases(idx, g, mode):
+        out, ed = orc.ungapped(rd, q, rf, o, reflen, minsc, mode == "loc", fw)
+        assert np.array_equal(out[:8], exp[:8]), (name, mode, i, out, exp)
+        assert np.array_equal(ed, ee), (name, mode, i)
