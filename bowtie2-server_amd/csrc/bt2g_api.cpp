@@ -503,6 +503,13 @@ static bool sw_packed_ok(const bt2g_scoring& sc, const SwConst& C, const int16_t
 	return C.rdgo >= 0 && C.rdge >= 0 && C.rfgo >= 0 && C.rfge >= 0;
 }
 
+// the systolic fill's LDS holds (64/S) groups of (maxcol+1)|1 selector words
+static bool sw_use_packed(const bt2g_scoring& sc, const SwConst& C, const int16_t* mat, uint32_t stride,
+                          uint32_t maxcol) {
+	const uint32_t S = (stride + 15u) / 16u, lds = (64u / S) * ((maxcol + 1u) | 1u) * 4u;
+	return sw_packed_ok(sc, C, mat) && lds <= 65536u;
+}
+
 // Fill + gather + candidate sort.  plane != NULL (systolic path only): also
 // write the score plane for the backtrace.  maxcol_hint: widest problem when
 // the caller already knows it (0: read the problems back).
@@ -538,21 +545,21 @@ static int sw_align_impl(bt2g_ctx* c, const uint8_t* reads, const uint8_t* quals
 	uint32_t* satl = lists + 2 * (size_t)nprob;
 	{
 		ProfScope ps(c, 4, st);
-		const uint32_t S = (stride + 15u) / 16u, lds = (64u / S) * ((maxcol + 1u) | 1u) * 4u;
-		if(sw_packed_ok(*sc, C, mat) && lds <= 65536u) {
+		if(sw_use_packed(*sc, C, mat, stride, maxcol)) {
 			launch_sw_ee_packed(probs, nprob, reads, quals, stride, lens, windows, c->ref_codes, c->ref_starts, C,
 			                    enable8, cap, maxcol, res, cands, plane, hslot, hbytes, st);
 		} else {
+		const PlaneOut po{plane, hslot, maxcol};     // u16 score plane (hslot from sw_plane_slot(.., 2))
 		launch_sw_partition(probs, nprob, sc->local, enable8, list8, counts + 0, list16, counts + 1, st);
 		int v8 = sc->local ? 2 : 0, v16 = sc->local ? 3 : 1;
 		launch_sw_fill(v8, probs, nprob, list8, counts + 0, reads, quals, stride, lens, windows, c->ref_codes,
-		               c->ref_starts, C, cap, bnd, maxcol, res, cands, mat, mat_off, satl, counts + 2, st);
+		               c->ref_starts, C, cap, bnd, maxcol, res, cands, mat, mat_off, satl, counts + 2, po, st);
 		launch_sw_fill(v16, probs, nprob, list16, counts + 1, reads, quals, stride, lens, windows, c->ref_codes,
-		               c->ref_starts, C, cap, bnd, maxcol, res, cands, mat, mat_off, satl, counts + 3, st);
+		               c->ref_starts, C, cap, bnd, maxcol, res, cands, mat, mat_off, satl, counts + 3, po, st);
 		if(sc->local) {
 			// local u8 saturated -> i16 (aligner_sw.cpp:587-605)
 			launch_sw_fill(3, probs, nprob, satl, counts + 2, reads, quals, stride, lens, windows, c->ref_codes,
-			               c->ref_starts, C, cap, bnd, maxcol, res, cands, mat, mat_off, satl, counts + 3, st);
+			               c->ref_starts, C, cap, bnd, maxcol, res, cands, mat, mat_off, satl, counts + 3, po, st);
 		}
 		}
 		launch_sort_cands(res, cands, nprob, cap, list8, counts + 4, st);   // list8 is free again
@@ -599,7 +606,6 @@ int bt2g_sw_align_bt_dev(bt2g_ctx* c, const uint8_t* reads, const uint8_t* quals
 	SwConst C;
 	sw_fill_consts(*sc, C);
 	const uint32_t S16 = sw_packed_rows(stride);
-	const bool packed = sw_packed_ok(*sc, C, nullptr);
 	BtArgs a{};
 	std::vector<void*> tmp;
 	auto talloc = [&](void** p, size_t n) -> int {
@@ -607,21 +613,22 @@ int bt2g_sw_align_bt_dev(bt2g_ctx* c, const uint8_t* reads, const uint8_t* quals
 		tmp.push_back(*p);
 		return BT2G_OK;
 	};
-	int kind, rc;
+	int rc;
+	bool packed;
+	int hb;
+	uint8_t* plane = nullptr;
 	uint32_t maxcol = 0, maxrow = stride;
-	const bool reserved = packed && c->bt_plane && nprob <= c->bt_max_prob && stride <= c->bt_max_stride &&
-	                      nprob <= c->sw_max_prob && c->sw_lists && c->bt_max_cols == c->sw_max_cols;
+	const bool reserved = c->bt_plane && nprob <= c->bt_max_prob && stride <= c->bt_max_stride &&
+	                      nprob <= c->sw_max_prob && c->sw_lists && c->bt_max_cols == c->sw_max_cols &&
+	                      (sw_use_packed(*sc, C, nullptr, stride, c->bt_max_cols) || c->bt_hbytes == 2);
 	if(reserved) {
 		// the fill marks problems wider than the reservation (flag -3, not aligned)
 		maxcol = c->bt_max_cols;
-		kind = c->bt_hbytes == 1 ? 0 : 1;
-		a.plane = c->bt_plane;
-		a.slot = sw_plane_slot(stride, maxcol, c->bt_hbytes);
-		a.marks = c->bt_marks;
 		maxrow = c->bt_max_stride;
-		if((rc = sw_align_impl(c, reads, quals, stride, lens, probs, nprob, windows, sc, enable8, cap, res, cands,
-		                       nullptr, nullptr, c->bt_plane, a.slot, c->bt_hbytes, maxcol, st)))
-			return rc;
+		packed = sw_use_packed(*sc, C, nullptr, stride, maxcol);
+		hb = packed ? c->bt_hbytes : 2;
+		plane = c->bt_plane;
+		a.marks = c->bt_marks;
 	} else {
 		std::vector<bt2g_sw_problem> hp(nprob);
 		HIPCHK(hipMemcpyAsync(hp.data(), probs, sizeof(bt2g_sw_problem) * nprob, hipMemcpyDeviceToHost, st));
@@ -636,40 +643,21 @@ int bt2g_sw_align_bt_dev(bt2g_ctx* c, const uint8_t* reads, const uint8_t* quals
 		std::vector<uint32_t> hl(nreads);
 		HIPCHK(hipMemcpyAsync(hl.data(), lens, sizeof(uint32_t) * nreads, hipMemcpyDeviceToHost, st));
 		HIPCHK(hipStreamSynchronize(st));
-		if(packed) {
-			const int hb = all8 ? 1 : 2;
-			kind = hb == 1 ? 0 : 1;
-			a.slot = sw_plane_slot(stride, maxcol, hb);
-			uint8_t* plane;
-			if((rc = talloc((void**)&plane, (size_t)a.slot * nprob))) return rc;
-			a.plane = plane;
-			if((rc = sw_align_impl(c, reads, quals, stride, lens, probs, nprob, windows, sc, enable8, cap, res,
-			                       cands, nullptr, nullptr, plane, a.slot, hb, maxcol, st)))
-				return rc;
-		} else {
-			// generic fills: H,E,F int16 matrices per problem
-			kind = 2;
-			std::vector<uint64_t> off(nprob);
-			uint64_t tot = 0;
-			for(uint32_t i = 0; i < nprob; i++) {
-				off[i] = tot;
-				tot += (uint64_t)hl[hp[i].read] * hp[i].ncol * 3;
-			}
-			int16_t* mat;
-			uint64_t* moff;
-			if((rc = talloc((void**)&mat, (size_t)tot * 2)) || (rc = talloc((void**)&moff, sizeof(uint64_t) * nprob)))
-				return rc;
-			HIPCHK(hipMemcpyAsync(moff, off.data(), sizeof(uint64_t) * nprob, hipMemcpyHostToDevice, st));
-			a.mat = mat;
-			a.mat_off = moff;
-			if((rc = sw_align_impl(c, reads, quals, stride, lens, probs, nprob, windows, sc, enable8, cap, res,
-			                       cands, mat, moff, nullptr, 0, 0, maxcol, st)))
-				return rc;
-			HIPCHK(hipStreamSynchronize(st));   // keep `off` alive until the copy is done
-		}
 		maxrow = 0;
 		for(uint32_t i = 0; i < nreads; i++) maxrow = hl[i] > maxrow ? hl[i] : maxrow;
+		packed = sw_use_packed(*sc, C, nullptr, stride, maxcol);
+		hb = packed && all8 ? 1 : 2;
+		if((rc = talloc((void**)&plane, (size_t)sw_plane_slot(stride, maxcol, hb) * nprob))) return rc;
 	}
+	// systolic fill: bottom-aligned rows, u8 (hb 1) or u16 plane with block masks;
+	// one-problem-per-lane fills (local, other scorings): top-aligned u16 plane
+	const int kind = hb == 1 ? 0 : 1;
+	a.plane = plane;
+	a.slot = sw_plane_slot(stride, maxcol, hb);
+	a.plane_top = packed ? 0 : 1;
+	if((rc = sw_align_impl(c, reads, quals, stride, lens, probs, nprob, windows, sc, enable8, cap, res, cands,
+	                       nullptr, nullptr, plane, a.slot, hb, maxcol, st)))
+		return rc;
 	a.mwords = sw_bt_tcols(maxcol);
 	a.mrows = sw_bt_trows(maxrow);
 	a.mslot = sw_bt_mslot(maxrow, maxcol);
@@ -681,7 +669,7 @@ int bt2g_sw_align_bt_dev(bt2g_ctx* c, const uint8_t* reads, const uint8_t* quals
 #ifdef BT2G_SW_NOMASK
 	a.use_mask = 0;   // timing experiments only
 #else
-	a.use_mask = S16 <= 256u;
+	a.use_mask = packed && S16 <= 256u;
 #endif
 	a.C = C; a.local = sc->local; a.ncl_const = sc->ncl_const; a.ncl_lin = sc->ncl_lin;
 	a.maxaln = maxaln; a.maxedit = maxedit; a.naln = naln; a.alns = alns; a.edits = edits; a.fates = fates;

@@ -40,12 +40,20 @@ void launch_get_offset(const DevEbwt& e, const uint32_t* rows, uint32_t n, uint3
                        hipStream_t st);
 void launch_sw_partition(const bt2g_sw_problem* probs, uint32_t nprob, int local, int enable8, uint32_t* list8,
                          uint32_t* n8, uint32_t* list16, uint32_t* n16, hipStream_t st);
+// Score plane written by the one-problem-per-lane fills: u16 per cell (score
+// + 0x8000 for the i16 fills' offset domain), rows top-aligned in 16-row
+// blocks of pcols columns, hslot bytes per problem (null plane: none).
+struct PlaneOut {
+	uint8_t* plane;
+	uint64_t hslot;
+	uint32_t pcols;
+};
 void launch_sw_fill(int variant, const bt2g_sw_problem* probs, uint32_t nprob, const uint32_t* list,
                     const uint32_t* list_n, const uint8_t* reads, const uint8_t* quals, uint32_t stride,
                     const uint32_t* lens, const uint8_t* windows, const uint8_t* ref_codes,
                     const uint64_t* ref_starts, const SwConst& c, uint32_t cap, uint32_t* bnd,
                     uint32_t bnd_cols, bt2g_sw_result* res, bt2g_sw_cand* cands, int16_t* mat,
-                    const uint64_t* mat_off, uint32_t* sat_list, uint32_t* sat_n, hipStream_t st);
+                    const uint64_t* mat_off, uint32_t* sat_list, uint32_t* sat_n, PlaneOut po, hipStream_t st);
 void launch_sw_ee_packed(const bt2g_sw_problem* probs, uint32_t nprob, const uint8_t* reads, const uint8_t* quals,
                          uint32_t stride, const uint32_t* lens, const uint8_t* windows, const uint8_t* ref_codes,
                          const uint64_t* ref_starts, const SwConst& C, int enable8, uint32_t cap, uint32_t max_cols,
@@ -79,8 +87,7 @@ struct BtArgs {
 	uint32_t cstride;                 //   rows per column (16-row blocks)
 	uint32_t pcols;                   //   columns per row block
 	int use_mask;                     //   per-column masks of written blocks (<= 16 blocks)
-	const int16_t* mat;               // kind 2: H,E,F triples
-	const uint64_t* mat_off;
+	int plane_top;                    //   rows top-aligned (one-problem-per-lane fills)
 	uint32_t* marks;                  // per problem (mslot words): reportedThrough tiles
 	uint64_t mslot;
 	uint32_t mwords, mrows;           //   tiles per tile row, tile rows
@@ -94,7 +101,7 @@ struct BtArgs {
 	bt2g_edit* edits;
 	int8_t* fates;                    // may be null
 };
-// kind: 0 u8 score plane, 1 u16 score plane, 2 generic H,E,F matrices
+// kind: 0 u8 score plane, 1 u16 score plane
 void launch_sw_bt(int kind, const BtArgs& a, hipStream_t st);
 // backtrace mark scratch per problem of <= rows x cols: 8x8-cell bit tiles
 // (2 words each) + one valid bit per tile (sw_backtrace.hip)

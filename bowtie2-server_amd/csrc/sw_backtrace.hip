@@ -60,10 +60,10 @@ __device__ __forceinline__ char mask2dna(int m) {
 
 enum { ST_H = 0, ST_E = 1, ST_F = 2 };
 
-// Score plane accessor: KIND 0 = u8 plane, 1 = u16 plane (systolic layout:
-// problem slot, 16-row blocks of pcols columns, rows bottom-aligned in the
-// strip stack (pad dead rows on top)), 2 = int16 H,E,F triples at mat_off[p]
-// (generic fill, row-major).
+// Score plane accessor: KIND 0 = u8 plane, 1 = u16 plane (problem slot,
+// 16-row blocks of pcols columns; the systolic fill bottom-aligns the rows in
+// its strip stack (pad dead rows on top), the one-problem-per-lane fills
+// top-align them).
 template <int KIND>
 struct Plane {
 	const uint8_t* base;   // kinds 0/1: the problem's slot; 2: its matrix
@@ -80,8 +80,7 @@ struct Plane {
 	}
 	__device__ __forceinline__ int32_t h(uint32_t r, uint32_t c) const {
 		if(KIND == 0) return (blk(r, c) ? (int32_t)base[idx(r, c)] : 0) - off;
-		if(KIND == 1) return (blk(r, c) ? (int32_t)((const uint16_t*)base)[idx(r, c)] : 0) - off;
-		return (int32_t)((const int16_t*)base)[((size_t)r * ncol + c) * 3] - off;
+		return (blk(r, c) ? (int32_t)((const uint16_t*)base)[idx(r, c)] : 0) - off;
 	}
 };
 
@@ -108,19 +107,17 @@ k_sw_bt(BtArgs A) {
 	pl.mask = nullptr;
 	uint32_t pad = 0;
 	const uint8_t* slot = nullptr;
-	if(KIND == 2) {
-		pl.base = (const uint8_t*)(A.mat + A.mat_off[p]);
-		pl.off = variant == 0 ? 0xff : variant == 1 ? 0x7fff : variant == 2 ? 0 : -0x8000;
-	} else {
+	{
 		if(KIND == 0 && variant != 0) { A.naln[p] = -4; return; }   // i16 fill, u8-only plane
 		const size_t es = KIND == 0 ? 1 : 2;
-		pad = A.cstride - nrow;
+		pad = A.plane_top ? 0u : A.cstride - nrow;
 		slot = A.plane + (size_t)p * A.slot;
 		pl.base = slot;
 		pl.pad = pad;
 		if(A.use_mask) pl.mask = (const uint16_t*)(slot + (size_t)A.cstride * A.pcols * es);
-		(void)es;
-		pl.off = variant == 0 ? 0xff : 0xffff;
+		// u8 fill: 0xff + score; i16 end-to-end fill: 0xffff + score (offset-u16
+		// domain); local fills: the score itself
+		pl.off = variant == 0 ? 0xff : variant == 1 ? 0xffff : 0;
 	}
 	// SwAligner::initRead / initRef inputs of this problem
 	const uint8_t* rd = A.reads + (size_t)P.read * A.stride;
@@ -499,7 +496,6 @@ void launch_sw_bt(int kind, const BtArgs& a, hipStream_t st) {
 	const dim3 grid((a.nprob + 63u) / 64u), block(64);
 	switch(kind) {
 	case 0: hipLaunchKernelGGL(k_sw_bt<0>, grid, block, 0, st, a); break;
-	case 1: hipLaunchKernelGGL(k_sw_bt<1>, grid, block, 0, st, a); break;
-	default: hipLaunchKernelGGL(k_sw_bt<2>, grid, block, 0, st, a); break;
+	default: hipLaunchKernelGGL(k_sw_bt<1>, grid, block, 0, st, a); break;
 	}
 }

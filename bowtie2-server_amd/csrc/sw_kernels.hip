@@ -108,7 +108,7 @@ k_sw_fill(const bt2g_sw_problem* __restrict__ probs, uint32_t nprob, const uint3
           const uint8_t* __restrict__ ref_codes, const uint64_t* __restrict__ ref_starts, SwConst C,
           uint32_t cap, uint32_t* __restrict__ bnd, uint32_t bnd_cols, bt2g_sw_result* __restrict__ res,
           bt2g_sw_cand* __restrict__ cands, int16_t* __restrict__ mat, const uint64_t* __restrict__ mat_off,
-          uint32_t* __restrict__ sat_list, uint32_t* __restrict__ sat_n) {
+          uint32_t* __restrict__ sat_list, uint32_t* __restrict__ sat_n, PlaneOut po) {
 	using D = Dom<V>;
 	const uint32_t lane = threadIdx.x;
 	const uint32_t gi = blockIdx.x * 64u + lane;
@@ -185,6 +185,9 @@ k_sw_fill(const bt2g_sw_problem* __restrict__ probs, uint32_t nprob, const uint3
 			}
 			int cm = D::LO;
 			int fprev = fup, hprev = hup, diag = diag0;
+			uint32_t hs[R / 2];                    // the strip's H as u16 pairs (score plane)
+#pragma unroll
+			for(int k = 0; k < R / 2; k++) hs[k] = 0;
 #pragma unroll
 			for(int k = 0; k < R; k++) {
 				const uint32_t r = s0 + k;
@@ -205,6 +208,7 @@ k_sw_fill(const bt2g_sw_problem* __restrict__ probs, uint32_t nprob, const uint3
 					Hl[k] = h;
 					fprev = f; hprev = h;
 					cm = imax(cm, h);
+					hs[k / 2] |= (uint32_t)(uint16_t)(h + ((V & 1) ? 0x8000 : 0)) << (16 * (k & 1));
 					if(mymat && real) {
 						size_t o = ((size_t)r * ncol + j) * 3;
 						mymat[o] = (int16_t)h; mymat[o + 1] = (int16_t)eold; mymat[o + 2] = (int16_t)f;
@@ -234,6 +238,12 @@ k_sw_fill(const bt2g_sw_problem* __restrict__ probs, uint32_t nprob, const uint3
 						}
 					}
 				}
+			}
+			if(po.plane) {
+				// score plane (sw_backtrace.hip), rows top-aligned: this strip is block s0/16
+				uint4* d = (uint4*)(po.plane + (size_t)pi * po.hslot + (((size_t)(s0 / R) * po.pcols + j) * R) * 2u);
+				d[0] = make_uint4(hs[0], hs[1], hs[2], hs[3]);
+				d[1] = make_uint4(hs[4], hs[5], hs[6], hs[7]);
 			}
 			// hand the strip's last row and the column max to the next strip
 			bhf[(size_t)j * 64u + lane] = ((uint32_t)(uint16_t)(int16_t)hprev << 16) | (uint16_t)(int16_t)fprev;
@@ -442,22 +452,22 @@ void launch_sw_fill(int variant, const bt2g_sw_problem* probs, uint32_t nprob, c
                     const uint32_t* lens, const uint8_t* windows, const uint8_t* ref_codes,
                     const uint64_t* ref_starts, const SwConst& C, uint32_t cap, uint32_t* bnd,
                     uint32_t bnd_cols, bt2g_sw_result* res, bt2g_sw_cand* cands, int16_t* mat,
-                    const uint64_t* mat_off, uint32_t* sat_list, uint32_t* sat_n, hipStream_t st) {
+                    const uint64_t* mat_off, uint32_t* sat_list, uint32_t* sat_n, PlaneOut po, hipStream_t st) {
 	dim3 grid((nprob + 63) / 64), block(64);
 	if(nprob == 0) return;
 	switch(variant) {
 	case 0: hipLaunchKernelGGL(k_sw_fill<0>, grid, block, 0, st, probs, nprob, list, list_n, reads, quals, stride,
 	                           lens, windows, ref_codes, ref_starts, C, cap, bnd, bnd_cols, res, cands, mat, mat_off,
-	                           sat_list, sat_n); break;
+	                           sat_list, sat_n, po); break;
 	case 1: hipLaunchKernelGGL(k_sw_fill<1>, grid, block, 0, st, probs, nprob, list, list_n, reads, quals, stride,
 	                           lens, windows, ref_codes, ref_starts, C, cap, bnd, bnd_cols, res, cands, mat, mat_off,
-	                           sat_list, sat_n); break;
+	                           sat_list, sat_n, po); break;
 	case 2: hipLaunchKernelGGL(k_sw_fill<2>, grid, block, 0, st, probs, nprob, list, list_n, reads, quals, stride,
 	                           lens, windows, ref_codes, ref_starts, C, cap, bnd, bnd_cols, res, cands, mat, mat_off,
-	                           sat_list, sat_n); break;
+	                           sat_list, sat_n, po); break;
 	default: hipLaunchKernelGGL(k_sw_fill<3>, grid, block, 0, st, probs, nprob, list, list_n, reads, quals, stride,
 	                            lens, windows, ref_codes, ref_starts, C, cap, bnd, bnd_cols, res, cands, mat, mat_off,
-	                            sat_list, sat_n); break;
+	                            sat_list, sat_n, po); break;
 	}
 }
 

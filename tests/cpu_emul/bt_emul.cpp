@@ -11,15 +11,14 @@ thread_local uint3v threadIdx, blockIdx;
 extern "C" int bt_emul_run(int kind, const bt2g_sw_problem* probs, uint32_t nprob, const uint8_t* reads,
                            const uint8_t* quals, uint32_t stride, const uint32_t* lens, const uint8_t* windows,
                            const bt2g_sw_rect* rects, const bt2g_sw_result* res, const bt2g_sw_cand* cands,
-                           uint32_t cap, const uint8_t* plane, uint64_t slot, uint32_t cstride, const int16_t* mat,
-                           const uint64_t* mat_off, uint32_t maxrow, uint32_t maxcol, const SwConst* C, int local,
+                           uint32_t cap, const uint8_t* plane, uint64_t slot, uint32_t cstride, int plane_top, uint32_t maxrow, uint32_t maxcol, const SwConst* C, int local,
                            double ncl_const, double ncl_lin, uint32_t maxaln, uint32_t maxedit, int32_t* naln,
                            bt2g_sw_aln* alns, bt2g_edit* edits, int8_t* fates) {
 	BtArgs a{};
 	a.probs = probs; a.nprob = nprob; a.reads = reads; a.quals = quals; a.stride = stride; a.lens = lens;
 	a.windows = windows; a.ref_codes = nullptr; a.ref_starts = nullptr; a.rects = rects;
-	a.res = res; a.cands = cands; a.cap = cap; a.plane = plane; a.slot = slot; a.cstride = cstride; a.pcols = maxcol; a.use_mask = cstride <= 256u;
-	a.mat = mat; a.mat_off = mat_off;
+	a.res = res; a.cands = cands; a.cap = cap; a.plane = plane; a.slot = slot; a.cstride = cstride; a.pcols = maxcol; a.use_mask = !plane_top && cstride <= 256u;
+	a.plane_top = plane_top;
 	a.mwords = sw_bt_tcols(maxcol); a.mrows = sw_bt_trows(maxrow); a.mslot = sw_bt_mslot(maxrow, maxcol);
 	// garbage-filled scratch: the kernel must not rely on zeroed memory
 	std::vector<uint32_t> marks(a.mslot * nprob + 4, 0xdeadbeefu);

@@ -52,8 +52,8 @@ def lib():
     return build()
 
 
-@pytest.mark.parametrize("src,kind", [("rand_ee", 0), ("log_ee", 0), ("rand_ee", 2), ("rand_loc", 2),
-                                      ("log_loc", 2)])
+@pytest.mark.parametrize("src,kind", [("rand_ee", 0), ("log_ee", 0), ("rand_ee", 1), ("rand_loc", 1),
+                                      ("log_loc", 1)])
 def test_bt_kernel_source_on_cpu(lib, src, kind):
     import bt2g
     from oracle.oracle import Oracle
@@ -72,20 +72,23 @@ def test_bt_kernel_source_on_cpu(lib, src, kind):
     S16 = 16 * ((stride + 15) // 16)
     maxcol = int(probs["ncol"].max())
     maxrow = int(g["lens"].max())
-    mats, offs, tot = [], [], 0
-    slot = S16 * maxcol + ((maxcol * 2 + 15) & ~15)      # plane + per-column block masks
-    plane = np.zeros(slot * n if kind == 0 else 16, np.uint8)
+    es = 1 if kind == 0 else 2
+    slot = S16 * maxcol * es + ((maxcol * 2 + 15) & ~15)   # plane + per-column block masks
+    plane = np.zeros(slot * n, np.uint8)
     keep = np.ones(n, bool)
     for p, rd, q, rf, minsc, fw, out, cref in sw_problems(g):
         o, c, m = orc.sw(rd, q, rf, minsc, local, want_mat=True, cap=cap)
         res[p] = (o[0], max(o[1], -2**31), o[2], o[3], o[4], o[5], o[6], 0)
         cands[p, :len(c)] = [tuple(x) for x in c]
         L, ncol = len(rd), len(rf) - 1
-        offs.append(tot)
-        if m is None:
-            m = np.zeros((L, ncol, 3), np.int32)
-        mats.append(m.astype(np.int16).ravel())
-        tot += L * ncol * 3
+        if kind == 1:
+            # one-problem-per-lane fill layout: u16 (score + 0x8000 for i16
+            # fills), rows top-aligned, all blocks written, no masks
+            h = m[:, :, 0].astype(np.int64) + (0 if o[2] else 0x8000)
+            stack = np.zeros((S16, maxcol), np.uint16)
+            stack[:L, :ncol] = (h & 0xffff).astype(np.uint16)
+            plane[p * slot:p * slot + S16 * maxcol * 2] = \
+                stack.reshape(S16 // 16, 16, maxcol).transpose(0, 2, 1).ravel().view(np.uint8)
         if kind == 0:
             if o[0] and not o[2]:
                 keep[p] = False          # i16 fill: not in a u8 plane (naln -4)
@@ -104,8 +107,6 @@ def test_bt_kernel_source_on_cpu(lib, src, kind):
                 masks = (live.astype(np.uint32) << np.arange(S16 // 16)[:, None].astype(np.uint32)).sum(0)
                 plane[p * slot + S16 * maxcol:p * slot + S16 * maxcol + 2 * maxcol] = \
                     masks.astype(np.uint16).view(np.uint8)
-    mat = np.concatenate(mats)
-    mat_off = np.array(offs, np.uint64)
     rects = np.zeros(n, bt2g.SWRECT_DTYPE)
     rects["triml"], rects["corel"], rects["corer"] = b["triml"], b["corel"], b["corer"]
     maxaln, maxedit = 4096 if local else 256, 512
@@ -116,7 +117,7 @@ def test_bt_kernel_source_on_cpu(lib, src, kind):
     lens = np.ascontiguousarray(g["lens"], np.uint32)
     lib.bt_emul_run(C.c_int(kind), _p(probs), C.c_uint32(n), _p(g["reads"]), _p(g["quals"]), C.c_uint32(stride),
                     _p(lens), _p(g["rf"]), _p(rects), _p(res), _p(cands), C.c_uint32(cap), _p(plane),
-                    C.c_uint64(slot), C.c_uint32(S16), _p(mat), _p(mat_off), C.c_uint32(maxrow), C.c_uint32(maxcol),
+                    C.c_uint64(slot), C.c_uint32(S16), C.c_int(int(kind == 1)), C.c_uint32(maxrow), C.c_uint32(maxcol),
                     C.byref(swconst(local)), C.c_int(int(local)), C.c_double(0.0), C.c_double(0.15),
                     C.c_uint32(maxaln), C.c_uint32(maxedit), _p(naln), _p(alns), _p(edits), _p(fates))
     nal = 0
