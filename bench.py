@@ -46,6 +46,22 @@ for _p in (ROOT, PKG, os.path.join(PKG, "tools"), os.path.join(ROOT, "tests", "g
 
 HBM_PEAK_GBS = 8000.0          # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
 SEEDLEN, INTERVAL = 22, 15     # --sensitive, 150 bp: -L 22, -i S,1,1.15 -> 1+1.15*sqrt(150) = 15
+
+
+class Policy:
+    """Per-mode seed and score policy (bt2_search.cpp presets).
+    ee:    --end-to-end --sensitive: -L 22, -i S,1,1.15, --score-min L,-0.6,-0.6
+    local: --local --sensitive-local: -L 20, -i S,1,0.75, --score-min G,20,8, --ma 2"""
+
+    def __init__(self, mode, length):
+        import math
+        self.mode, self.local = mode, mode == "local"
+        if self.local:
+            self.seedlen, self.interval = 20, int(1 + 0.75 * math.sqrt(length))
+            self.minsc = int(20 + 8 * math.log(length))
+        else:
+            self.seedlen, self.interval = SEEDLEN, INTERVAL
+            self.minsc = int(-0.6 - 0.6 * length)
 MAXALN, MAXEDIT = 8, 64        # alignments kept per DP (the loop stops there); edits per alignment
                                # (150 bp, minsc -90, n-ceil 22: <= 22 N + 34 mismatches = 56)
 MAXGAP = 15                    # min(max(read gaps, ref gaps), maxhalf=15), dp_framer.cpp:95-100
@@ -98,9 +114,10 @@ def make_reads(parts, n, length, seed):
 class Pipeline:
     """The per-step GPU work (see module docstring), torch glue on one stream."""
 
-    def __init__(self, eng, idx, reads, quals, length):
+    def __init__(self, eng, idx, reads, quals, length, mode="ee"):
         import torch
         import bt2g
+        self.pol = pol = Policy(mode, length)
         self.torch, self.bt2g, self.L = torch, bt2g, bt2g.lib()
         self.eng = eng
         self.dev = reads.device
@@ -108,10 +125,10 @@ class Pipeline:
         self.len = length
         self.reads, self.quals = reads, quals
         self.lens = torch.full((self.n,), length, dtype=torch.int32, device=self.dev)
-        self.minsc = torch.full((self.n,), int(-0.6 - 0.6 * length), dtype=torch.int32, device=self.dev)
-        self.sc = bt2g.scoring(False)
+        self.minsc = torch.full((self.n,), pol.minsc, dtype=torch.int32, device=self.dev)
+        self.sc = bt2g.scoring(pol.local)
         n = self.n
-        self.maxseeds = 1 + (length - SEEDLEN) // INTERVAL
+        self.maxseeds = 1 + (length - pol.seedlen) // pol.interval
         self.sweep = torch.empty((n, 8), dtype=torch.int32, device=self.dev)
         self.mm_cap = 16
         self.mm_hits = torch.empty((n, self.mm_cap, 8), dtype=torch.int32, device=self.dev)
@@ -144,9 +161,12 @@ class Pipeline:
         self.max_probs = 2 * n
         self.probs = torch.zeros((self.max_probs, 5), dtype=torch.int64, device=self.dev)
         _chk = bt2g._chk
-        # fill + backtrace scratch: u8 score plane (end-to-end, minsc >= -254)
-        _chk(self.L.bt2g_reserve_sw_bt(eng.h, self.max_probs, length, self.ncol, 1))
-        self.sw_cap = 256
+        # fill + backtrace scratch: u8 score plane (end-to-end, minsc >= -254);
+        # u16 for the local fills
+        _chk(self.L.bt2g_reserve_sw_bt(eng.h, self.max_probs, length, self.ncol, 2 if pol.local else 1))
+        # candidate cells per DP: end-to-end gathers the last row only; local
+        # gathers every match-then-mismatch cell >= minsc (~1200 per 150 bp hit)
+        self.sw_cap = 2048 if pol.local else 256
         self.res = torch.empty((self.max_probs, 8), dtype=torch.int32, device=self.dev)
         self.cands = torch.empty((self.max_probs, self.sw_cap, 3), dtype=torch.int32, device=self.dev)
         # seed-extension rectangles: no trim, core diagonals [maxgap, 3*maxgap] (dp_framer.cpp:116-125)
@@ -181,7 +201,8 @@ class Pipeline:
         sel = torch.nonzero(~exact).squeeze(1)
         m = int(sel.numel())
         sreads = self.reads.index_select(0, sel)
-        chk(L.bt2g_seed_search_dev(h, self._p(sreads), stride, self._p(self.lens), m, SEEDLEN, INTERVAL, 0,
+        pol = self.pol
+        chk(L.bt2g_seed_search_dev(h, self._p(sreads), stride, self._p(self.lens), m, pol.seedlen, pol.interval, 0,
                                    self.maxseeds, self._p(self.seeds), self._p(self.nseeds), self._p(self.sd_ops),
                                    self._p(self.sd_loads), S))
         # 4. every read's hit rows (exact, 1-mm, seeds) -> one list, contiguous per read
@@ -190,7 +211,8 @@ class Pipeline:
         self.counters.zero_()
         P = self._p
         chk(L.bt2g_bench_collect_rows_dev(n, P(self.lens), P(self.sweep), P(self.mm_hits), P(self.mm_cnt),
-                                          self.mm_cap, P(self.seeds), P(self.inv), self.maxseeds, SEEDLEN, INTERVAL,
+                                          self.mm_cap, P(self.seeds), P(self.inv), self.maxseeds, pol.seedlen,
+                                          pol.interval,
                                           P(self.rows), P(self.meta), P(self.read_base), P(self.read_cnt),
                                           P(self.counters), self.row_cap, S))
         nrows = int(self.counters[0])
@@ -199,7 +221,7 @@ class Pipeline:
         # 6. joinedToTextOff + straddle filter + rectangles, <= 2 per read (device)
         chk(L.bt2g_bench_frame_dev(n, P(self.lens), P(self.offs), P(self.meta), P(self.read_base),
                                    P(self.read_cnt), P(self.fr[0]), P(self.fr[1]), P(self.fr[2]), P(self.fr[3]),
-                                   self.nfrag, MAXGAP, int(-0.6 - 0.6 * self.len), P(self.probs),
+                                   self.nfrag, MAXGAP, pol.minsc, P(self.probs),
                                    P(self.counters[1:]), self.max_probs, S))
         npb = min(int(self.counters[1]), self.max_probs)
         probs = self.probs[:npb]
@@ -208,7 +230,9 @@ class Pipeline:
                                    P(probs), npb, None, P(self.rects), C.byref(self.sc), 1, self.sw_cap,
                                    P(self.res), P(self.cands), self.maxaln, self.maxedit, P(self.naln),
                                    P(self.alns), P(self.edits), None, S))
-        aligned = exact.clone()
+        # end-to-end: an exact end-to-end hit is the alignment (EXTEND_PERFECT_SCORE);
+        # local: every read's hits, the exact ones included, go through the DP
+        aligned = torch.zeros_like(exact) if pol.local else exact.clone()
         al = self.naln[:npb] > 0
         aligned[probs.view(torch.int32)[:, 0][al].to(torch.int64)] = True
         ns = 0
@@ -273,7 +297,7 @@ def cpu_baseline(idx, reads, quals, pipe, sample, threads):
     L.bt2ref_sw_bt_batch.argtypes = [C.c_int, C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p,
                                      C.c_void_p, C.c_void_p, C.c_void_p, C.c_int, C.c_int, C.c_void_p]
     L.bt2ref_one_mm_gated.argtypes = [C.c_void_p, C.c_int, C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p,
-                                      C.c_void_p]
+                                      C.c_void_p, C.c_int]
     tmp = tempfile.mkdtemp(prefix="bt2bench_")
     base = os.path.join(tmp, "g")
     bi.write_index(base, idx)
@@ -310,8 +334,9 @@ def cpu_baseline(idx, reads, quals, pipe, sample, threads):
     tot = int(rc.sum())
     within = np.arange(tot) - np.repeat(np.cumsum(rc) - rc, rc)
     rows = rows_all[np.repeat(rb, rc) + within]
-    sp = score_params(False)
-    minsc = np.full(n, int(-0.6 - 0.6 * pipe.len), np.int64)
+    pol = pipe.pol
+    sp = score_params(pol.local)
+    minsc = np.full(n, pol.minsc, np.int64)
 
     def work(lo, hi):
         s, q = seqs[lo:hi], qs[lo:hi]
@@ -320,12 +345,13 @@ def cpu_baseline(idx, reads, quals, pipe, sample, threads):
         ex = R.exact_sweep(s, q, 2)
         cnt = np.zeros(hi - lo, np.int32)
         exu = np.ascontiguousarray(ex, np.uint64)
-        L.bt2ref_one_mm_gated(R.h, hi - lo, cs, cq, minsc[lo:hi].ctypes.data, exu.ctypes.data, cnt.ctypes.data)
+        L.bt2ref_one_mm_gated(R.h, hi - lo, cs, cq, minsc[lo:hi].ctypes.data, exu.ctypes.data, cnt.ctypes.data,
+                              int(pol.local))
         need = np.minimum(ex[:, 0], ex[:, 1]) != 0
         ss = [s[i] for i in np.nonzero(need)[0]]
         sq = [q[i] for i in np.nonzero(need)[0]]
         if ss:
-            R.seed_search(ss, sq, SEEDLEN, INTERVAL, 0, pipe.maxseeds)
+            R.seed_search(ss, sq, pol.seedlen, pol.interval, 0, pipe.maxseeds)
         return ex
 
     def work_rows(lo, hi):
@@ -344,7 +370,7 @@ def cpu_baseline(idx, reads, quals, pipe, sample, threads):
         cq = (C.c_char_p * k)(*[qs[r] for r in rid])
         offs = np.ascontiguousarray(rf_off[lo:hi + 1] - 0)
         nc = np.full(k, ncol, np.int32)
-        ms = np.full(k, int(-0.6 - 0.6 * pipe.len), np.int64)
+        ms = np.full(k, pol.minsc, np.int64)
         out = np.zeros((k, 8), np.int64)
         L.bt2ref_sw_bt_batch(k, cs, cq, fwv.ctypes.data, rf.ctypes.data, offs.ctypes.data, nc.ctypes.data,
                              ms.ctypes.data, C.byref(sp), MAXGAP, 3 * MAXGAP, out.ctypes.data)
@@ -390,6 +416,10 @@ def backtrace_parity(pipe, keep, sw_ref):
     bad = np.minimum(sw_ref[:, 2], pipe.maxaln) != naln
     bad |= (naln > 0) & (first != sw_ref[:, 3:7]).any(1)
     bad |= (naln < pipe.maxaln) & (ck != sw_ref[:, 7])
+    if os.environ.get("BT2G_BENCH_DEBUG"):
+        for i in np.nonzero(bad)[0][:8]:
+            print(f"[bt mismatch] dp {i}: gpu naln {naln[i]} first {first[i].tolist()} ck {ck[i]} | "
+                  f"ref {sw_ref[i].tolist()}", flush=True)
     return int(bad.sum())
 
 
@@ -400,6 +430,8 @@ def main():
     ap.add_argument("--warmup", type=int, default=1)
     ap.add_argument("--reads", type=int, default=1_000_000, help="reads per GPU per step")
     ap.add_argument("--read-len", type=int, default=150)
+    ap.add_argument("--mode", choices=("ee", "local"), default="ee",
+                    help="ee: BASELINE configs[1] (--end-to-end --sensitive); local: configs[3] (--local)")
     ap.add_argument("--genome-mb", type=float, default=1000.0)
     ap.add_argument("--cpu-sample", type=int, default=1_000_000)
     ap.add_argument("--cpu-threads", type=int, default=16)
@@ -444,7 +476,7 @@ def main():
     log(f"[rank {rank}] {args.reads} reads in {time.time()-t2:.1f}s; index resident: {info[12]/1e9:.2f} GB")
     reads = torch.from_numpy(reads_np).to(dev)
     quals = torch.from_numpy(quals_np).to(dev)
-    pipe = Pipeline(eng, idx, reads, quals, args.read_len)
+    pipe = Pipeline(eng, idx, reads, quals, args.read_len, args.mode)
 
     for _ in range(args.warmup):
         pipe.step()
@@ -478,7 +510,7 @@ def main():
     bytes_k = {
         # 64-B sides gathered + the read bytes each lane walks (2 strands)
         0: 64 * sweep_loads + 2 * n * args.read_len,
-        1: 64 * int(pipe.sd_loads[:last["m"]].to(torch.int64).sum()) + int(pipe.nseeds[:last["m"]].sum()) * 2 * (SEEDLEN + 12),
+        1: 64 * int(pipe.sd_loads[:last["m"]].to(torch.int64).sum()) + int(pipe.nseeds[:last["m"]].sum()) * 2 * (pipe.pol.seedlen + 12),
         2: 64 * int(pipe.mm_loads.to(torch.int64).sum()) + 4 * n * args.read_len,
         3: 64 * int(last["loads_off"].to(torch.int64).sum()) + 12 * last["nrows"],
         4: None,
@@ -496,7 +528,8 @@ def main():
         log(f"[rank {rank}] {names_k[k]:12s} {per_launch[k]:8.3f} ms/launch")
     naln_np = pipe.naln[:last["npb"]].cpu().numpy()
     bt_stats = {"alignments": int(naln_np.clip(0).sum()), "dps_with_alignment": int((naln_np > 0).sum()),
-                "dps_at_maxaln": int((naln_np >= pipe.maxaln).sum()), "maxaln": pipe.maxaln}
+                "dps_at_maxaln": int((naln_np >= pipe.maxaln).sum()), "maxaln": pipe.maxaln,
+                "dps_cand_overflow": int((naln_np == -5).sum())}
     log(f"[rank {rank}] SW: {last['npb']} DPs/step, {sw_gcups:.0f} GCUPS; aligned {n_aligned/(args.steps*world*args.reads):.4f}; backtrace {bt_stats}")
 
     # ---- CPU baseline: the reference on the host cores, rank 0, N=1 ---------
@@ -533,9 +566,10 @@ def main():
             "ms_per_step": elapsed / args.steps * 1e3, "higher_is_better": True, "scaling": "weak",
             "vs_baseline": None, "dtype": "u8/i16 DP, u32 FM", "data": "synthetic",
             "config": {"workload": f"{args.reads} synthetic {args.read_len} bp unpaired reads per GPU per step, "
-                                   f"--end-to-end --sensitive policy, vs a {args.genome_mb:.0f} Mbp synthetic "
+                                   f"{'--local --sensitive-local' if args.mode == 'local' else '--end-to-end --sensitive'}"
+                                   f" policy, vs a {args.genome_mb:.0f} Mbp synthetic "
                                    f"genome (hg38 unavailable offline); exact sweep + gated 1-mm + seed round 0 "
-                                   f"+ SA offsets + <=2 seed-extension DPs/read",
+                                   f"+ SA offsets + <=2 seed-extension DPs/read (fill + nextAlignment loop)",
                        "global_batch": args.reads * world, "seq_len": args.read_len, "parallelism": f"dp{world}",
                        "aligned_frac": n_aligned / total_reads},
             "roofline": {"bound": "hbm", "kernel": names_k[dom], "achieved": achieved, "peak": HBM_PEAK_GBS,

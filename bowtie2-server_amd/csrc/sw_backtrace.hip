@@ -96,6 +96,7 @@ k_sw_bt(BtArgs A) {
 	if(p >= A.nprob) return;
 	const bt2g_sw_result R = A.res[p];
 	if(!R.aligned || R.ncand <= 0) { A.naln[p] = 0; return; }
+	if((uint32_t)R.ncand > A.cap) { A.naln[p] = -5; return; }   // truncated list: not the reference's
 	const bt2g_sw_problem P = A.probs[p];
 	const uint32_t nrow = A.lens[P.read], ncol = P.ncol;
 	const bool local = A.local != 0;

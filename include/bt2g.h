@@ -261,7 +261,8 @@ typedef struct {
  * the order the reference returns them.  rects may be NULL (triml 0, every
  * diagonal core).  Per problem p: naln[p] alignments at alns[p*maxaln ..]
  * (the loop stops after maxaln; naln[p] = -4 if the problem needs an i16
- * matrix but the reservation holds u8 only), edits of alignment k at
+ * matrix but the reservation holds u8 only; -5 if its candidate list
+ * overflowed cap, so that the list is not the reference's), edits of alignment k at
  * edits[(p*maxaln + k)*maxedit ..]; fates (optional, NULL to skip):
  * DpBtCandidate::fate of each candidate (aligner_sw_nuc.h:83-88) at
  * fates[p*cap ..].  Candidates below the problem's minsc are skipped

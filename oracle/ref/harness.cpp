@@ -412,12 +412,12 @@ void bt2ref_sw_batch(int n, const char** seqs, const char** quals, const uint8_t
 // oneMmSearch gated by exactSweep exactly as bt2_search.cpp:3640-3667 chains them.
 // sweep: n x 8 from bt2ref_exact_sweep (mineFw, mineRc, ...).  counts[i] = hits.
 void bt2ref_one_mm_gated(void* vh, int n, const char** seqs, const char** quals, const int64_t* minsc,
-                         const uint64_t* sweep, int32_t* counts) {
+                         const uint64_t* sweep, int32_t* counts, int local) {
 	RefHandle* h = (RefHandle*)vh;
 	SeedAligner al;
 	SeedResults sr;
 	SeedSearchMetrics met;
-	ScoreParams sp = {0, 6, 2, 1, 5, 3, 5, 3, 4, 0, 0.0, 0.15};
+	ScoreParams sp = {local ? 2 : 0, 6, 2, 1, 5, 3, 5, 3, 4, local, 0.0, 0.15};
 	Scoring sc = makeScoring(sp);
 	for(int i = 0; i < n; i++) {
 		counts[i] = 0;
@@ -428,7 +428,7 @@ void bt2ref_one_mm_gated(void* vh, int n, const char** seqs, const char** quals,
 		Read rd("r", seqs[i], quals[i]);
 		sr.clear();
 		sr.nextRead(rd);
-		al.oneMmSearch(h->fw, h->bw, rd, sc, minsc[i], !yfw, !yrc, false, false, true, sr, met);
+		al.oneMmSearch(h->fw, h->bw, rd, sc, minsc[i], !yfw, !yrc, local != 0, false, true, sr, met);
 		counts[i] = (int32_t)sr.mm1EEHits().size();
 	}
 }
