@@ -19,7 +19,7 @@ LIB_PATH = os.environ.get("BT2G_LIB", os.path.join(HERE, "libbt2g.so"))
 
 BT2G_OK = 0
 BT2G_ERR_OVERFLOW = -6
-K_EXACT_SWEEP, K_SEED_SEARCH, K_ONE_MM, K_GET_OFFSET, K_SW_ALIGN, K_SW_BACKTRACE, K_UNGAPPED = range(7)
+K_EXACT_SWEEP, K_SEED_SEARCH, K_ONE_MM, K_GET_OFFSET, K_SW_ALIGN, K_SW_BACKTRACE, K_UNGAPPED, K_FRAME = range(8)
 
 
 class Scoring(C.Structure):
@@ -48,6 +48,22 @@ UGPROB_DTYPE = np.dtype([("read", "<u4"), ("fw", "<i4"), ("off", "<i8"), ("refid
 UGRES_DTYPE = np.dtype([("ret", "<i4"), ("score", "<i4"), ("refoff", "<i8")] +
                        [(n, "<i4") for n in ("ns", "refns", "nedit", "trim5p", "trim3p", "pad")])
 EDIT_DTYPE = np.dtype([("pos", "<u4"), ("type", "u1"), ("chr", "u1"), ("qchr", "u1"), ("pad", "u1")])
+FRAMEIN_DTYPE = np.dtype([("off", "<i8"), ("read", "<u4"), ("refidx", "<u4"), ("minsc", "<i4"), ("fw", "<i4"),
+                          ("kind", "<i4"), ("anchor1", "<i4"), ("alen", "<u4"), ("pad", "<u4")])
+PE_FF, PE_RR, PE_FR, PE_RF = 1, 2, 3, 4   # pe.h PE_POLICY_*
+
+
+class PePolicy(C.Structure):
+    _fields_ = [(n, C.c_int32) for n in ("policy", "minfrag", "maxfrag", "local", "flip", "dovetail", "contain",
+                                          "olap", "expand", "pad")]
+
+
+def pe_policy(policy=PE_FR, minfrag=0, maxfrag=500, local=False, flip=False, dovetail=False, contain=True,
+              olap=True, expand=True):
+    """PairedEndPolicy defaults of bowtie2 (--fr -I 0 -X 500, no dovetail,
+    containment and overlap allowed, bt2_search.cpp)."""
+    return PePolicy(policy=policy, minfrag=minfrag, maxfrag=maxfrag, local=int(local), flip=int(flip),
+                    dovetail=int(dovetail), contain=int(contain), olap=int(olap), expand=int(expand))
 
 
 class EbwtMem(C.Structure):
@@ -113,6 +129,10 @@ def lib():
         L.bt2g_reserve_sw_bt.argtypes = [vp, u32, u32, u32, C.c_int]
         L.bt2g_ungapped.argtypes = [vp, vp, vp, u32, vp, vp, u32, C.POINTER(Scoring), C.c_int, u32, vp, vp]
         L.bt2g_ungapped_dev.argtypes = [vp, vp, vp, u32, vp, vp, u32, C.POINTER(Scoring), C.c_int, u32, vp, vp, vp]
+        L.bt2g_frame.argtypes = [vp, vp, u32, vp, u32, C.POINTER(Scoring), C.POINTER(PePolicy), C.c_int32, C.c_int,
+                                 vp, vp, vp]
+        L.bt2g_frame_dev.argtypes = [vp, vp, u32, vp, C.POINTER(Scoring), C.POINTER(PePolicy), C.c_int32, C.c_int,
+                                     vp, vp, vp, vp]
         L.bt2g_set_profiling.argtypes = [vp, C.c_int]
         L.bt2g_kernel_stats.argtypes = [vp, C.c_int, C.POINTER(u64), C.POINTER(C.c_double)]
         L.bt2g_reset_stats.argtypes = [vp]
@@ -284,6 +304,20 @@ class Engine:
         _chk(lib().bt2g_ungapped(self.h, _ptr(reads), _ptr(quals), reads.shape[1], _ptr(lens), _ptr(probs), n,
                                  C.byref(sc), int(ohang), maxedit, _ptr(res), _ptr(edits)))
         return res, edits
+
+    def frame(self, inputs, lens, local=False, pe=None, maxhalf=15, trim_to_ref=True, sc=None):
+        """DP rectangles (bt2g_frame): seed extensions (kind 0) and mate searches
+        (kind 1).  Returns probs (SWPROB_DTYPE), rects (SWRECT_DTYPE), ok (int32)."""
+        inputs, lens = _c(inputs, FRAMEIN_DTYPE), _c(lens, np.uint32)
+        n = len(inputs)
+        probs = np.zeros(n, SWPROB_DTYPE)
+        rects = np.zeros(n, SWRECT_DTYPE)
+        ok = np.zeros(n, np.int32)
+        sc = scoring(local) if sc is None else sc
+        _chk(lib().bt2g_frame(self.h, _ptr(inputs), n, _ptr(lens), len(lens), C.byref(sc),
+                              None if pe is None else C.byref(pe), maxhalf, int(trim_to_ref), _ptr(probs),
+                              _ptr(rects), _ptr(ok)))
+        return probs, rects, ok
 
     # ---- measurement -------------------------------------------------------
     def set_profiling(self, on=True):

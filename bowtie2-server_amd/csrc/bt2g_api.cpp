@@ -620,7 +620,8 @@ int bt2g_sw_align_bt_dev(bt2g_ctx* c, const uint8_t* reads, const uint8_t* quals
 	uint32_t maxcol = 0, maxrow = stride;
 	const bool reserved = c->bt_plane && nprob <= c->bt_max_prob && stride <= c->bt_max_stride &&
 	                      nprob <= c->sw_max_prob && c->sw_lists && c->bt_max_cols == c->sw_max_cols &&
-	                      (sw_use_packed(*sc, C, nullptr, stride, c->bt_max_cols) || c->bt_hbytes == 2);
+	                      (sw_use_packed(*sc, C, nullptr, stride, c->bt_max_cols) || c->bt_hbytes == 2) &&
+	                      (!sc->local || c->bt_hbytes == 2);    // local: u16 plane and dominance tiles
 	if(reserved) {
 		// the fill marks problems wider than the reservation (flag -3, not aligned)
 		maxcol = c->bt_max_cols;
@@ -660,9 +661,9 @@ int bt2g_sw_align_bt_dev(bt2g_ctx* c, const uint8_t* reads, const uint8_t* quals
 		return rc;
 	a.mwords = sw_bt_tcols(maxcol);
 	a.mrows = sw_bt_trows(maxrow);
-	a.mslot = sw_bt_mslot(maxrow, maxcol);
+	a.mslot = sw_bt_mslot(maxrow, maxcol, sc->local != 0);
+	a.mdom = sc->local ? sw_bt_mslot(maxrow, maxcol, false) : 0u;
 	if(!a.marks && (rc = talloc((void**)&a.marks, sizeof(uint32_t) * a.mslot * nprob))) return rc;
-	if(sc->local && (rc = talloc((void**)&a.done, sizeof(int2) * (size_t)cap * nprob))) return rc;
 	a.probs = probs; a.nprob = nprob; a.reads = reads; a.quals = quals; a.stride = stride; a.lens = lens;
 	a.windows = windows; a.ref_codes = c->ref_codes; a.ref_starts = c->ref_starts; a.rects = rects;
 	a.res = res; a.cands = cands; a.cap = cap; a.cstride = S16; a.pcols = maxcol;
@@ -700,6 +701,38 @@ int bt2g_ungapped_dev(bt2g_ctx* c, const uint8_t* reads, const uint8_t* quals, u
 	return BT2G_OK;
 }
 
+int bt2g_frame_dev(bt2g_ctx* c, const bt2g_frame_in* in, uint32_t n, const uint32_t* lens, const bt2g_scoring* sc,
+                   const bt2g_pe_policy* pe, int32_t maxhalf, int trim_to_ref, bt2g_sw_problem* probs,
+                   bt2g_sw_rect* rects, int32_t* ok, void* stream) {
+	if(!c || !sc || (n && (!in || !lens || !probs || !rects || !ok))) return fail(BT2G_ERR_ARG, "null argument");
+	if(maxhalf < 0) return fail(BT2G_ERR_ARG, "maxhalf %d < 0", maxhalf);
+	bt2g_pe_policy P{};
+	P.policy = 3;
+	P.maxfrag = 500;
+	if(pe) {
+		if(pe->policy < 1 || pe->policy > 4) return fail(BT2G_ERR_ARG, "no such PE policy %d", pe->policy);
+		if(pe->maxfrag <= 0 || pe->minfrag < 0 || pe->maxfrag < pe->minfrag)
+			return fail(BT2G_ERR_ARG, "bad fragment lengths [%d, %d]", pe->minfrag, pe->maxfrag);
+		P = *pe;
+	}
+	if(n == 0) return BT2G_OK;
+	hipStream_t st = pick(c, stream);
+	FrameConst F;
+	F.match = sc->match;
+	F.rdgo = sc->rdg_const + sc->rdg_lin; F.rdge = sc->rdg_lin;
+	F.rfgo = sc->rfg_const + sc->rfg_lin; F.rfge = sc->rfg_lin;
+	F.maxhalf = maxhalf; F.trim_to_ref = trim_to_ref != 0;
+	F.ncl_const = sc->ncl_const; F.ncl_lin = sc->ncl_lin;
+	// every kind-1 input needs a policy: checked on the device would cost a
+	// round trip, so a NULL policy is simply the defaults (--fr, -X 500)
+	{
+		ProfScope ps(c, 7, st);
+		launch_frame(in, n, lens, c->ref_starts, F, P, probs, rects, ok, st);
+	}
+	HIPCHK(hipGetLastError());
+	return BT2G_OK;
+}
+
 int bt2g_reserve_sw_bt(bt2g_ctx* c, uint32_t max_problems, uint32_t max_stride, uint32_t max_cols, int hbytes) {
 	if(!c || max_problems == 0 || max_cols == 0 || max_stride == 0 || (hbytes != 1 && hbytes != 2))
 		return fail(BT2G_ERR_ARG, "bad reservation");
@@ -708,7 +741,8 @@ int bt2g_reserve_sw_bt(bt2g_ctx* c, uint32_t max_problems, uint32_t max_stride, 
 	c->bt_plane = nullptr; c->bt_marks = nullptr;
 	const uint64_t slot = sw_plane_slot(max_stride, max_cols, hbytes);
 	HIPCHK(hipMalloc((void**)&c->bt_plane, slot * max_problems));
-	HIPCHK(hipMalloc((void**)&c->bt_marks, sizeof(uint32_t) * sw_bt_mslot(max_stride, max_cols) * max_problems));
+	HIPCHK(hipMalloc((void**)&c->bt_marks,
+	                 sizeof(uint32_t) * sw_bt_mslot(max_stride, max_cols, hbytes == 2) * max_problems));
 	c->bt_max_prob = max_problems;
 	c->bt_max_stride = max_stride;
 	c->bt_max_cols = max_cols;
@@ -941,6 +975,33 @@ int bt2g_sw_align_bt(bt2g_ctx* c, const uint8_t* reads, const uint8_t* quals, ui
 }  // extern "C"
 
 extern "C" {
+
+int bt2g_frame(bt2g_ctx* c, const bt2g_frame_in* in, uint32_t n, const uint32_t* lens, uint32_t nreads,
+               const bt2g_scoring* sc, const bt2g_pe_policy* pe, int32_t maxhalf, int trim_to_ref,
+               bt2g_sw_problem* probs, bt2g_sw_rect* rects, int32_t* ok) {
+	if(!c) return fail(BT2G_ERR_ARG, "null ctx");
+	HIPCHK(hipSetDevice(c->device));
+	if(n == 0) return BT2G_OK;
+	for(uint32_t i = 0; i < n; i++) {
+		if(in[i].read >= nreads) return fail(BT2G_ERR_ARG, "input %u: read %u >= %u", i, in[i].read, nreads);
+		if(in[i].refidx >= c->nref) return fail(BT2G_ERR_ARG, "input %u: reference %u >= %u", i, in[i].refidx, c->nref);
+		if(in[i].kind == 1 && !pe) return fail(BT2G_ERR_ARG, "input %u: mate search without a PE policy", i);
+	}
+	Tmp t;
+	bt2g_frame_in* din;
+	uint32_t* dl;
+	bt2g_sw_problem* dp;
+	bt2g_sw_rect* dr;
+	int32_t* dok;
+	int rc;
+	if((rc = t.up(&din, in, n)) || (rc = t.up(&dl, lens, nreads)) || (rc = t.up(&dp, (const bt2g_sw_problem*)nullptr, n)) ||
+	   (rc = t.up(&dr, (const bt2g_sw_rect*)nullptr, n)) || (rc = t.up(&dok, (const int32_t*)nullptr, n)))
+		return rc;
+	if((rc = bt2g_frame_dev(c, din, n, dl, sc, pe, maxhalf, trim_to_ref, dp, dr, dok, c->stream))) return rc;
+	HIPCHK(hipStreamSynchronize(c->stream));
+	if((rc = down(probs, dp, n)) || (rc = down(rects, dr, n)) || (rc = down(ok, dok, n))) return rc;
+	return BT2G_OK;
+}
 
 int bt2g_ungapped(bt2g_ctx* c, const uint8_t* reads, const uint8_t* quals, uint32_t stride, const uint32_t* lens,
                   const bt2g_ug_problem* probs, uint32_t n, const bt2g_scoring* sc, int ohang, uint32_t maxedit,

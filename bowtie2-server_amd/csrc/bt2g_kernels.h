@@ -91,7 +91,7 @@ struct BtArgs {
 	uint32_t* marks;                  // per problem (mslot words): reportedThrough tiles
 	uint64_t mslot;
 	uint32_t mwords, mrows;           //   tiles per tile row, tile rows
-	int2* done;                       // local mode: cap (row, col) per problem
+	uint64_t mdom;                    // local mode: word offset of the FILT_DOMINATED tiles
 	SwConst C;
 	int local;
 	double ncl_const, ncl_lin;
@@ -104,15 +104,26 @@ struct BtArgs {
 // kind: 0 u8 score plane, 1 u16 score plane
 void launch_sw_bt(int kind, const BtArgs& a, hipStream_t st);
 // backtrace mark scratch per problem of <= rows x cols: 8x8-cell bit tiles
-// (2 words each) + one valid bit per tile (sw_backtrace.hip)
+// (2 words each) + one valid bit per tile (sw_backtrace.hip); dom: a second
+// tile set of the same shape (local mode's dominated-candidate squares)
 inline uint32_t sw_bt_tcols(uint32_t cols) { return (cols + 7u) / 8u; }
 inline uint32_t sw_bt_trows(uint32_t rows) { return (rows + 7u) / 8u; }
-inline uint64_t sw_bt_mslot(uint32_t rows, uint32_t cols) {
+inline uint64_t sw_bt_mslot(uint32_t rows, uint32_t cols, bool dom) {
 	const uint64_t tc = sw_bt_tcols(cols), tr = sw_bt_trows(rows);
-	return (tr * tc * 2u + tr * ((tc + 31u) / 32u) + 3u) & ~(uint64_t)3u;
+	return ((tr * tc * 2u + tr * ((tc + 31u) / 32u) + 3u) & ~(uint64_t)3u) * (dom ? 2u : 1u);
 }
 void launch_sort_cands(const bt2g_sw_result* res, bt2g_sw_cand* cands, uint32_t nprob, uint32_t cap,
                        uint32_t* big, uint32_t* nbig, hipStream_t st);
+
+// DP framing (frame.hip): the scoring and framer parameters of one batch
+struct FrameConst {
+	int32_t match, rdgo, rdge, rfgo, rfge;   // bonus and gap open (incl. extension) / extension
+	int32_t maxhalf, trim_to_ref;
+	double ncl_const, ncl_lin;
+};
+void launch_frame(const bt2g_frame_in* in, uint32_t n, const uint32_t* lens, const uint64_t* ref_starts,
+                  const FrameConst& F, const bt2g_pe_policy& P, bt2g_sw_problem* probs, bt2g_sw_rect* rects,
+                  int32_t* ok, hipStream_t st);
 
 void launch_ungapped(const bt2g_ug_problem* probs, uint32_t n, const uint8_t* reads, const uint8_t* quals,
                      uint32_t stride, const uint32_t* lens, const uint8_t* ref_codes, const uint64_t* ref_starts,

@@ -271,10 +271,41 @@ k_sw_bt(BtArgs A) {
 	};
 	const uint32_t ncand = (uint32_t)R.ncand < A.cap ? (uint32_t)R.ncand : A.cap;
 	const bt2g_sw_cand* cl = A.cands + (size_t)p * A.cap;
-	int2* done = local ? A.done + (size_t)p * A.cap : nullptr;
-	uint32_t ndone = 0;
+	// local mode, FILT_DOMINATED (aligner_sw.cpp nextAlignment): a candidate
+	// within SQ rows and SQ columns of one already walked is skipped.  Each
+	// walked candidate sets its (2SQ+1)^2 square in a second set of 8x8 bit
+	// tiles, so the test is one bit, not a scan of the walked list.
 	uint32_t SQ = nrow >> 4;
 	if(SQ == 0) SQ = 1;
+	uint32_t* dmarks = marks + A.mdom;
+	uint32_t* dvalid = dmarks + (size_t)trows * tcols * 2u;
+	if(local)
+		for(uint32_t i = 0; i < trows * vw; i++) dvalid[i] = 0u;
+	auto dom_test = [&](uint32_t r, uint32_t c) -> bool {
+		const uint32_t tr = r >> 3, tc = c >> 3;
+		if(!((dvalid[tr * vw + (tc >> 5)] >> (tc & 31u)) & 1u)) return false;
+		return (*(const uint64_t*)(dmarks + ((size_t)tr * tcols + tc) * 2u) & tbit(r, c)) != 0;
+	};
+	auto dom_add = [&](uint32_t r, uint32_t c) {
+		const uint32_t r0 = r > SQ ? r - SQ : 0u, c0 = c > SQ ? c - SQ : 0u;
+		uint32_t r1 = r + SQ, c1 = c + SQ;
+		r1 = r1 < trows * 8u - 1u ? r1 : trows * 8u - 1u;
+		c1 = c1 < tcols * 8u - 1u ? c1 : tcols * 8u - 1u;
+		for(uint32_t tr = r0 >> 3; tr <= r1 >> 3; tr++) {
+			// bytes (tile rows) inside [r0, r1], one bit each
+			const uint32_t lo = tr * 8u > r0 ? 0u : r0 & 7u, hi = tr * 8u + 7u < r1 ? 7u : r1 & 7u;
+			const uint64_t rows = (~0ull >> (8u * (7u - hi))) & (~0ull << (8u * lo)) & 0x0101010101010101ull;
+			for(uint32_t tc = c0 >> 3; tc <= c1 >> 3; tc++) {
+				const uint32_t cl0 = tc * 8u > c0 ? 0u : c0 & 7u, ch = tc * 8u + 7u < c1 ? 7u : c1 & 7u;
+				const uint64_t cols = (0xffull >> (7u - ch)) & (0xffull << cl0);
+				uint64_t* t = (uint64_t*)(dmarks + ((size_t)tr * tcols + tc) * 2u);
+				uint32_t& vwd = dvalid[tr * vw + (tc >> 5)];
+				const uint32_t vb = 1u << (tc & 31u);
+				*t = (vwd & vb ? *t : 0ull) | rows * cols;
+				vwd |= vb;
+			}
+		}
+	};
 	int32_t nal = 0;
 	bool first = true;
 	// One backtrace from (row, col).  mark: set/check reportedThrough (off when
@@ -434,16 +465,7 @@ k_sw_bt(BtArgs A) {
 			// (end-to-end starts in the bottom barrier rows are never marked: see walk)
 			fate = 3;                                   // BT_CAND_FATE_FILT_START
 		} else {
-			bool dom = false;
-			if(local) {
-				for(uint32_t i = 0; i < ndone && !dom; i++) {
-					const int2 d = done[i];
-					const uint32_t dr = d.x > cd.row ? d.x - cd.row : cd.row - d.x;
-					const uint32_t dc = d.y > cd.col ? d.y - cd.col : cd.col - d.y;
-					dom = dc <= SQ && dr <= SQ;
-				}
-			}
-			if(dom) {
+			if(local && dom_test((uint32_t)cd.row, (uint32_t)cd.col)) {
 				fate = 4;                               // BT_CAND_FATE_FILT_DOMINATED
 			} else {
 				// the first walk writes its edits as it goes (it usually succeeds);
@@ -454,7 +476,7 @@ k_sw_bt(BtArgs A) {
 				Walk w = walk(row0, col0, cd.score, true, first, ed);
 				if(w.ok && !first) (void)walk(row0, col0, cd.score, false, true, ed);
 				first = false;
-				if(local) done[ndone++] = make_int2(cd.row, cd.col);
+				if(local) dom_add((uint32_t)cd.row, (uint32_t)cd.col);
 				if(w.ok) {
 					const uint32_t trimBeg = w.row, trimEnd = nrow - row0 - 1;
 					// res.reverse(), AlnRes::setShape trim shift, invertEdits for !fw

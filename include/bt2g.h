@@ -316,6 +316,55 @@ int bt2g_ungapped_dev(bt2g_ctx* ctx, const uint8_t* reads, const uint8_t* quals,
                       const uint32_t* lens, const bt2g_ug_problem* probs, uint32_t n, const bt2g_scoring* sc,
                       int ohang, uint32_t maxedit, bt2g_ug_result* res, bt2g_edit* edits, void* stream);
 
+/* ---- DP framing (row A14) ------------------------------------------------ */
+
+/* PairedEndPolicy (pe.h:166-330): mate orientation policy and fragment-length
+ * constraints.  policy: PE_POLICY_FF 1, RR 2, FR 3, RF 4 (pe.h:30-35). */
+typedef struct {
+	int32_t policy;
+	int32_t minfrag, maxfrag;   /* -I, -X */
+	int32_t local;              /* unused by otherMate, kept for parity with the constructor */
+	int32_t flip, dovetail, contain, olap, expand;   /* flippingOk_ .. expandToFit_ */
+	int32_t pad;
+} bt2g_pe_policy;
+
+/* One rectangle to frame.  kind 0: seed extension,
+ * DynProgFramer::frameSeedExtensionRect (dp_framer.cpp:81-129) around the
+ * ungapped diagonal through `off`, as SwDriver::extendSeeds calls it
+ * (aligner_sw_driver.cpp:992-1000, 1074-1084).  kind 1: mate search,
+ * PairedEndPolicy::otherMate (pe.cpp:161-352) for the anchor alignment at `off`
+ * followed by DynProgFramer::frameFindMateRect (dp_framer.h:155-197,
+ * dp_framer.cpp:177-383), as SwDriver::extendSeedsPaired calls them
+ * (aligner_sw_driver.cpp:1975-2024). */
+typedef struct {
+	int64_t  off;      /* kind 0: reference offset implied by the hit; kind 1: the anchor's refoff */
+	uint32_t read;     /* the read of the DP: kind 0 the read itself, kind 1 the opposite mate */
+	uint32_t refidx;
+	int32_t  minsc;    /* minimum score of the DP (kind 1: ominsc_cur) */
+	int32_t  fw;       /* kind 0: strand of the DP; kind 1: the anchor's strand */
+	int32_t  kind;
+	int32_t  anchor1;  /* kind 1: the anchor is mate 1 */
+	uint32_t alen;     /* kind 1: length of the anchor mate */
+	uint32_t pad;
+} bt2g_frame_in;
+
+/* Frame n rectangles.  Read and reference gap budgets are
+ * Scoring::maxReadGaps / maxRefGaps (scoring.cpp:42-98) of the DP's minsc and
+ * read length (the seed-hit branch of extendSeeds; its exact end-to-end
+ * "eeMode" hits need no rectangle); the N budget is
+ * min(nCeil(len), len) (bt2_search.cpp multiseedSearchWorker); trim_to_ref =
+ * !--overhang.  Per input: ok[i] = 1 and a DP problem probs[i] (reference
+ * window [rect.refl, rect.refr], strand: kind 0 fw, kind 1 otherMate's ofw) with
+ * rects[i] {triml, corel, corer}, or ok[i] = 0 when otherMate finds no
+ * concordant window or the rectangle is entirely trimmed.  pe may be NULL when
+ * no input has kind 1. */
+int bt2g_frame(bt2g_ctx* ctx, const bt2g_frame_in* in, uint32_t n, const uint32_t* lens, uint32_t nreads,
+               const bt2g_scoring* sc, const bt2g_pe_policy* pe, int32_t maxhalf, int trim_to_ref,
+               bt2g_sw_problem* probs, bt2g_sw_rect* rects, int32_t* ok);
+int bt2g_frame_dev(bt2g_ctx* ctx, const bt2g_frame_in* in, uint32_t n, const uint32_t* lens,
+                   const bt2g_scoring* sc, const bt2g_pe_policy* pe, int32_t maxhalf, int trim_to_ref,
+                   bt2g_sw_problem* probs, bt2g_sw_rect* rects, int32_t* ok, void* stream);
+
 /* ---- bench batch glue (NOT reference seams) -------------------------------
  * Device-side glue used by bench.py between the seed-phase calls and
  * bt2g_sw_align_dev.  The reference's SwDriver::extendSeeds chooses hits with
@@ -351,7 +400,7 @@ int bt2g_bench_frame_dev(uint32_t n, const uint32_t* lens, const uint32_t* offs,
 /* ---- measurement --------------------------------------------------------- */
 /* Kernel timing with HIP events on the launch stream (off by default). */
 int bt2g_set_profiling(bt2g_ctx* ctx, int on);
-/* kernel ids: 0 exact_sweep, 1 seed_search, 2 one_mm, 3 get_offset, 4 sw_align, 5 sw_backtrace, 6 ungapped */
+/* kernel ids: 0 exact_sweep, 1 seed_search, 2 one_mm, 3 get_offset, 4 sw_align, 5 sw_backtrace, 6 ungapped, 7 frame */
 int bt2g_kernel_stats(bt2g_ctx* ctx, int kernel, uint64_t* launches, double* total_ms);
 int bt2g_reset_stats(bt2g_ctx* ctx);
 

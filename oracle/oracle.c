@@ -21,6 +21,8 @@
  *     loc i16 aligner_swsse_loc_i16.cpp:75-145, 938-1367 (gather 1420-1535)
  *     dispatch SwAligner::align aligner_sw.cpp:500-729; Scoring scoring.h:96-440
  *   ungapped: SwAligner::ungappedAlign aligner_sw.cpp:286-494
+ *   framing: DynProgFramer dp_framer.cpp:81-129, 177-383; PairedEndPolicy::
+ *     otherMate pe.cpp:161-352; Scoring::maxReadGaps/maxRefGaps scoring.cpp:42-98
  *   backtrace: SwAligner::nextAlignment aligner_sw.cpp:737-1146 with
  *     backtraceNucleotides{End2End,Local}Sse{U8,I16}
  *     (aligner_swsse_ee_u8.cpp:1283-1780, aligner_swsse_loc_u8.cpp:1588-2175,
@@ -1183,4 +1185,117 @@ int orc_ungapped(const uint8_t* rd, const uint8_t* q33, int len, const uint8_t* 
 	out[0] = 1; out[1] = score; out[2] = rfi + (int64_t)rowi; out[3] = ns; out[4] = refns; out[5] = ned;
 	out[6] = (int64_t)(fw ? rowi : trimEnd); out[7] = (int64_t)(fw ? trimEnd : rowi);
 	return 1;
+}
+
+/* ---------------------------------------------------------------------- */
+/* DP framing: DynProgFramer (dp_framer.cpp:81-129, 177-383),               */
+/* PairedEndPolicy::otherMate (pe.cpp:161-352), Scoring::maxReadGaps /      */
+/* maxRefGaps (scoring.cpp:42-98)                                           */
+/* ---------------------------------------------------------------------- */
+/* Gap budgets in closed form: the reference loops, converting matches of the
+ * perfect score P into gaps while the score stays >= minsc; the k-th read gap
+ * costs rdgo (k = 1) or rdge, the k-th reference gap also loses a match. */
+static int64_t orc_gap_budget(int64_t P, int64_t minsc, int64_t first, int64_t step) {
+	if(P < minsc) return -1;
+	if(P - first < minsc) return 0;
+	return 1 + (P - first - minsc) / step;
+}
+
+/* pe: {policy, minfrag, maxfrag, flip, dovetail, olap, expand}.
+ * out[7] = {ok, fw, refl, ncol, triml, corel, corer}. */
+void orc_frame(int kind, int64_t off, uint64_t rdlen, int64_t reflen, int64_t minsc, int fw, int anchor1,
+               uint64_t alen, const orc_scoring* sc, const int32_t* pe, int64_t maxhalf, int trim_to_ref,
+               int64_t* out) {
+	memset(out, 0, 7 * sizeof(int64_t));
+	const int64_t P = (int64_t)(rdlen * (uint64_t)sc->match);
+	const int64_t rdgo = sc->rdg_const + sc->rdg_lin, rfgo = sc->rfg_const + sc->rfg_lin;
+	const int64_t rdgaps = orc_gap_budget(P, minsc, rdgo, sc->rdg_lin);
+	const int64_t rfgaps = orc_gap_budget(P, minsc, sc->match + rfgo, sc->match + sc->rfg_lin);
+	double v = sc->ncl_const + sc->ncl_lin * (double)rdlen;
+	int64_t nceil = v < 0.0 ? 0 : (int64_t)(int)v;
+	if(nceil > (int64_t)rdlen) nceil = (int64_t)rdlen;
+	/* the budgets are ints handed to size_t parameters */
+	const uint64_t grd = (uint64_t)rdgaps, grf = (uint64_t)rfgaps;
+	const uint64_t gmax = grd > grf ? grd : grf;
+	uint64_t maxgap;
+	int64_t refl, refr;
+	int ofw = fw;
+	if(kind == 0) {
+		maxgap = gmax < (uint64_t)maxhalf ? gmax : (uint64_t)maxhalf;
+		refl = (int64_t)((uint64_t)off - 2 * maxgap);
+		refr = (int64_t)((uint64_t)off + (rdlen - 1) + 2 * maxgap);
+	} else {
+		/* pePolicyMateDir (pe.h:130-164): is the opposite mate to the left, on
+		 * which strand */
+		int left;
+		switch(pe[0]) {
+		case 1: left = anchor1 != fw; ofw = fw; break;
+		case 2: left = anchor1 == fw; ofw = fw; break;
+		case 3: left = !fw; ofw = !fw; break;
+		default: left = fw; ofw = !fw; break;
+		}
+		const uint64_t len1 = anchor1 ? alen : rdlen, len2 = anchor1 ? rdlen : alen;
+		const uint64_t a = anchor1 ? len1 : len2;   /* "length of opposite mate" as otherMate names it */
+		uint64_t maxfrag = (uint64_t)pe[2], minfrag = pe[1] < 1 ? 1u : (uint64_t)pe[1];
+		if(pe[6]) {
+			if(len1 > maxfrag) maxfrag = len1;
+			if(len2 > maxfrag) maxfrag = len2;
+		} else if(len1 > maxfrag || len2 > maxfrag) {
+			return;
+		}
+		const int64_t maxalcols = (int64_t)rdlen + rdgaps;
+		int64_t ll, lr, rl, rr;
+		if(left) {
+			ll = (int64_t)((uint64_t)off + a - maxfrag);
+			lr = (int64_t)((uint64_t)off + a - minfrag);
+			rl = ll;
+			rr = (int64_t)((uint64_t)off + maxfrag - 1);
+			if(!pe[5]) {
+				if(off - 1 < rr) rr = off - 1;
+				if(rr < lr) lr = rr;
+			} else if(!pe[4]) {
+				const int64_t t = (int64_t)((uint64_t)off + a - 1);
+				if(t < rr) rr = t;
+			} else if(!pe[3] && maxalcols != -1) {
+				const int64_t t = (int64_t)((uint64_t)off + a - 1 + (uint64_t)(maxalcols - 1));
+				if(t < rr) rr = t;
+			}
+		} else {
+			rr = (int64_t)((uint64_t)off + (maxfrag - 1));
+			rl = (int64_t)((uint64_t)off + (minfrag - 1));
+			ll = (int64_t)((uint64_t)off + a - maxfrag);
+			lr = rr;
+			if(!pe[5]) {
+				const int64_t t = (int64_t)((uint64_t)off + a);
+				if(t > ll) ll = t;
+				if(ll > rl) rl = ll;
+			} else if(!pe[4]) {
+				if(off > ll) ll = off;
+			} else if(!pe[3] && maxalcols != -1) {
+				const int64_t t = off - maxalcols + 1;
+				if(t > ll) ll = t;
+			}
+		}
+		(void)lr;
+		maxgap = gmax > (uint64_t)maxhalf ? gmax : (uint64_t)maxhalf;
+		/* anchor to the left (opposite to the right): the opposite mate ends in
+		 * [rl, rr]; anchor to the right: it starts in [ll, lr] */
+		const int64_t st = left ? ll : (int64_t)((uint64_t)rl - (rdlen - 1));
+		const int64_t en = left ? (int64_t)((uint64_t)lr + (rdlen - 1)) : rr;
+		refl = (int64_t)((uint64_t)st - maxgap);
+		refr = (int64_t)((uint64_t)en + maxgap);
+	}
+	int64_t maxns = trim_to_ref ? 0 : (nceil == (int64_t)rdlen ? nceil - 1 : nceil);
+	uint64_t triml = 0, trimr = 0;
+	if(refr >= reflen + maxns) trimr = (uint64_t)(refr - (reflen + maxns - 1));
+	if(refl < -maxns) triml = (uint64_t)(-refl) - (uint64_t)maxns;
+	const int64_t rl2 = (int64_t)((uint64_t)refl + triml), rr2 = (int64_t)((uint64_t)refr - trimr);
+	if(rr2 < rl2) return;
+	out[0] = 1;
+	out[1] = ofw;
+	out[2] = rl2;
+	out[3] = rr2 - rl2 + 1;
+	out[4] = (int64_t)triml;
+	out[5] = (int64_t)maxgap;
+	out[6] = kind == 0 ? (int64_t)(3 * maxgap) : (int64_t)((uint64_t)(refr - refl + 1) - maxgap - 1);
 }

@@ -162,3 +162,17 @@ class Oracle:
         self.lib.orc_ungapped(_p(rd), _p(q33), len(rd), _p(rf), int(rfi), int(reflen), int(minsc), C.byref(sc),
                               1 if ohang else 0, 1 if fw else 0, _p(out), _p(ed))
         return out, ed[:4 * int(out[5])].reshape(-1, 4)
+
+    def frame(self, kind, off, rdlen, reflen, minsc, fw=True, anchor1=True, alen=0, local=False, pe=None,
+              maxhalf=15, trim_to_ref=True, sc=None):
+        """DP rectangle of one seed extension (kind 0) or mate search (kind 1).
+        pe = (policy, minfrag, maxfrag, flip, dovetail, olap, expand).  Returns
+        (ok, fw, refl, ncol, triml, corel, corer)."""
+        out = np.zeros(7, np.int64)
+        pev = np.array(pe if pe is not None else (3, 0, 500, 0, 0, 1, 1), np.int32)
+        sc = sc if sc is not None else scoring(local)
+        self.lib.orc_frame(int(kind), C.c_int64(int(off)), C.c_uint64(int(rdlen)), C.c_int64(int(reflen)),
+                           C.c_int64(int(minsc)), int(bool(fw)), int(bool(anchor1)), C.c_uint64(int(alen)),
+                           C.byref(sc), _p(pev), C.c_int64(int(maxhalf)), int(bool(trim_to_ref)), _p(out))
+        return tuple(int(x) for x in out)
+

@@ -29,6 +29,8 @@
 #include "simple_func.h"
 #include "search_globals.h"
 #include "random_source.h"
+#include "dp_framer.h"
+#include "pe.h"
 
 // Globals normally defined by bt2_search.cpp (search_globals.h, aligner_seed_policy.h).
 bool gReportOverhangs = false;
@@ -613,6 +615,57 @@ void bt2ref_ungapped(void* vh, int n, const char** seqs, const char** quals, con
 				q[0] = (int32_t)a.ned()[e].pos; q[1] = a.ned()[e].type; q[2] = a.ned()[e].chr; q[3] = a.ned()[e].qchr;
 			}
 		}
+	}
+}
+
+} // extern "C"
+
+extern "C" {
+
+// DP framing exactly as SwDriver calls it: seed extension (kind 0,
+// aligner_sw_driver.cpp:992-1000, 1074-1084) and mate search (kind 1,
+// aligner_sw_driver.cpp:1975-2024: maxReadGaps/maxRefGaps of ominsc, otherMate
+// with maxalcols = orows + oreadGaps, frameFindMateRect(!oleft, ...)).
+// in: n x 8 int64 {kind, off, rdlen, reflen, minsc, fw, anchor1, alen}
+// pe: {policy, minfrag, maxfrag, flip, dovetail, olap, expand}
+// out: n x 7 {ok, fw, refl, ncol, triml, corel, corer}
+void bt2ref_frame(int n, const int64_t* in, const ScoreParams* sp, const int32_t* pe, int maxhalf, int trim_to_ref,
+                  int64_t* out) {
+	Scoring sc = makeScoring(*sp);
+	DynProgFramer fr(trim_to_ref != 0);
+	PairedEndPolicy pepol(pe[0], (size_t)pe[2], (size_t)pe[1], sp->local != 0, pe[3] != 0, pe[4] != 0, true,
+	                      pe[5] != 0, pe[6] != 0);
+	for(int i = 0; i < n; i++) {
+		const int64_t* x = in + 8 * (size_t)i;
+		int64_t* o = out + 7 * (size_t)i;
+		memset(o, 0, 7 * sizeof(int64_t));
+		const int kind = (int)x[0];
+		const int64_t off = x[1];
+		const size_t rdlen = (size_t)x[2];
+		const int64_t reflen = x[3], minsc = x[4];
+		const bool fw = x[5] != 0, anchor1 = x[6] != 0;
+		const size_t alen = (size_t)x[7];
+		int nceil = std::min((int)sc.nCeil.f<int>((double)rdlen), (int)rdlen);
+		int readGaps = sc.maxReadGaps(minsc, rdlen);
+		int refGaps = sc.maxRefGaps(minsc, rdlen);
+		DPRect rect;
+		bool found;
+		bool ofw = fw;
+		if(kind == 0) {
+			found = fr.frameSeedExtensionRect(off, rdlen, reflen, readGaps, refGaps, (size_t)nceil, (size_t)maxhalf,
+			                                  rect);
+		} else {
+			bool oleft = false;
+			int64_t oll = 0, olr = 0, orl = 0, orr = 0;
+			found = pepol.otherMate(anchor1, fw, off, rdlen + readGaps, (size_t)reflen, anchor1 ? alen : rdlen,
+			                        anchor1 ? rdlen : alen, oleft, oll, olr, orl, orr, ofw);
+			if(found)
+				found = fr.frameFindMateRect(!oleft, oll, olr, orl, orr, rdlen, reflen, readGaps, refGaps,
+				                             (size_t)nceil, (size_t)maxhalf, rect);
+		}
+		if(!found) continue;
+		o[0] = 1; o[1] = ofw; o[2] = rect.refl; o[3] = rect.refr - rect.refl + 1;
+		o[4] = (int64_t)rect.triml; o[5] = (int64_t)rect.corel; o[6] = (int64_t)rect.corer;
 	}
 }
 

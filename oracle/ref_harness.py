@@ -56,6 +56,19 @@ class RefLib:
                                 C.POINTER(ScoreParams), C.c_int, C.c_int, C.POINTER(C.c_int64),
                                 C.POINTER(C.c_int64), C.POINTER(C.c_int32)]
 
+    def frame(self, inputs, local, pe=(3, 0, 500, 0, 0, 1, 1), maxhalf=15, trim_to_ref=True, sp=None):
+        """DynProgFramer / PairedEndPolicy::otherMate as SwDriver calls them
+        (bt2ref_frame).  inputs: n x 8 int64 {kind, off, rdlen, reflen, minsc,
+        fw, anchor1, alen}.  Returns n x 7 {ok, fw, refl, ncol, triml, corel, corer}."""
+        x = np.ascontiguousarray(inputs, np.int64)
+        n = len(x)
+        out = np.zeros((n, 7), np.int64)
+        pev = np.ascontiguousarray(pe, np.int32)
+        sp = sp if sp is not None else score_params(local)
+        self.lib.bt2ref_frame(C.c_int(n), _p(x, C.c_int64), C.byref(sp), _p(pev, C.c_int32), C.c_int(maxhalf),
+                              C.c_int(int(trim_to_ref)), _p(out, C.c_int64))
+        return out
+
     def sw_bt(self, seq, qual, fw, rfmask, minsc, local, triml=0, corel=0, corer=0, enable8=True,
               maxaln=64, maxedit=256, sp=None):
         """SwAligner::align + the SwDriver nextAlignment loop.  Returns (out[7],

@@ -19,11 +19,11 @@ extern "C" int bt_emul_run(int kind, const bt2g_sw_problem* probs, uint32_t npro
 	a.windows = windows; a.ref_codes = nullptr; a.ref_starts = nullptr; a.rects = rects;
 	a.res = res; a.cands = cands; a.cap = cap; a.plane = plane; a.slot = slot; a.cstride = cstride; a.pcols = maxcol; a.use_mask = !plane_top && cstride <= 256u;
 	a.plane_top = plane_top;
-	a.mwords = sw_bt_tcols(maxcol); a.mrows = sw_bt_trows(maxrow); a.mslot = sw_bt_mslot(maxrow, maxcol);
+	a.mwords = sw_bt_tcols(maxcol); a.mrows = sw_bt_trows(maxrow); a.mslot = sw_bt_mslot(maxrow, maxcol, local != 0);
+	a.mdom = local ? sw_bt_mslot(maxrow, maxcol, false) : 0u;
 	// garbage-filled scratch: the kernel must not rely on zeroed memory
 	std::vector<uint32_t> marks(a.mslot * nprob + 4, 0xdeadbeefu);
-	std::vector<int2> done((size_t)cap * nprob + 1, int2{-7, -7});
-	a.marks = marks.data(); a.done = done.data();
+	a.marks = marks.data();
 	a.C = *C; a.local = local; a.ncl_const = ncl_const; a.ncl_lin = ncl_lin;
 	a.maxaln = maxaln; a.maxedit = maxedit; a.naln = naln; a.alns = alns; a.edits = edits; a.fates = fates;
 	launch_sw_bt(kind, a, nullptr);

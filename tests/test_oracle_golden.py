@@ -151,3 +151,22 @@ def test_ungapped(orc, name, mode):
         out, ed = orc.ungapped(rd, q, rf, o, reflen, minsc, mode == "loc", fw)
         assert np.array_equal(out[:8], exp[:8]), (name, mode, i, out, exp)
         assert np.array_equal(ed, ee), (name, mode, i)
+
+
+def test_frame(orc):
+    """DP framing (row A14): the oracle's restatement of frameSeedExtensionRect,
+    otherMate + frameFindMateRect and the gap budgets against the reference's
+    own rectangles (frame.npz, tests/golden/make_golden_frame.py)."""
+    g = load_golden("frame")
+    nframed = 0
+    for name in g["names"]:
+        x, y, par = g[f"in_{name}"], g[f"out_{name}"], g[f"par_{name}"]
+        local, pe, maxhalf, ttr = bool(par[0]), tuple(int(v) for v in par[1:8]), int(par[8]), bool(par[9])
+        for i in range(len(x)):
+            kind, off, rdlen, reflen, minsc, fw, a1, alen = (int(v) for v in x[i])
+            got = orc.frame(kind, off, rdlen, reflen, minsc, fw, a1, alen, local=local, pe=pe, maxhalf=maxhalf,
+                            trim_to_ref=ttr)
+            exp = tuple(int(v) for v in y[i]) if y[i, 0] else (0,) * 7
+            assert got == exp, (name, i, x[i].tolist(), got, exp)
+            nframed += got[0]
+    assert nframed > 30000
