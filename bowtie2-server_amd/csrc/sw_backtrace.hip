@@ -86,6 +86,14 @@ struct Plane {
 
 }  // namespace
 
+// work counters for the CPU emulation only (tests/cpu_emul, scripts)
+#ifdef BT2G_BT_COUNT
+extern unsigned long long bt_counts[8];
+#define BTC(i) (bt_counts[i]++)
+#else
+#define BTC(i) ((void)0)
+#endif
+
 #ifndef BT2G_BT_WAVES
 #define BT2G_BT_WAVES 3
 #endif
@@ -158,9 +166,23 @@ k_sw_bt(BtArgs A) {
 			}
 			return hit;
 		} else {
-			for(int32_t r = rhi; r >= rlo; r--)
-				if(pl.h((uint32_t)r, c) == base + (x - r) * step) return true;
-			return false;
+			// u16 plane: the 16 rows of a column block are 32 contiguous bytes
+			bool hit = false;
+#pragma unroll 1
+			for(int32_t o0 = ((int32_t)pad + rlo) & ~15; o0 <= (int32_t)pad + rhi && !hit; o0 += 16) {
+				if(pl.mask && !((pl.mask[c] >> (o0 >> 4)) & 1u)) continue;   // all below minsc / zero: no hit
+				BTC(2);
+				const uint4* q = (const uint4*)(slot + ((size_t)(o0 >> 4) * A.pcols + c) * 32u);
+				const uint4 v0 = q[0], v1 = q[1];
+				const uint32_t wv[8] = {v0.x, v0.y, v0.z, v0.w, v1.x, v1.y, v1.z, v1.w};
+#pragma unroll
+				for(int b = 0; b < 16; b++) {
+					const int32_t r = o0 + b - (int32_t)pad;
+					const int32_t val = (int32_t)((wv[b >> 1] >> (16 * (b & 1))) & 0xffffu) - pl.off;
+					hit = hit || (r >= rlo && r <= rhi && val == base + (x - r) * step);
+				}
+			}
+			return hit;
 		}
 	};
 	// N ceiling, Scoring::nCeil.f<int>(len) (simple_func.h:90-115)
@@ -240,7 +262,8 @@ k_sw_bt(BtArgs A) {
 	uint32_t cb = 0xffffffffu, cc0 = 0;
 	uint4 ch0 = make_uint4(0, 0, 0, 0), ch1 = ch0, ch2 = ch0, ch3 = ch0;   // named: no indexable array
 	auto hget = [&](uint32_t r, uint32_t c) -> int32_t {
-		if(KIND != 0) return pl.h(r, c);
+		BTC(7);
+		if(KIND != 0) return pl.h(r, c);   // u16 planes: direct (a chunk cache costs occupancy)
 		const uint32_t rsx = pad + r, b = rsx >> 4;
 		if(b != cb || c < cc0 || c > cc0 + 3u) {
 			cb = b;
@@ -323,7 +346,9 @@ k_sw_bt(BtArgs A) {
 			w.ned++;
 		};
 		int st = ST_H;
+		BTC(0);
 		while(true) {
+			BTC(1);
 			// end-to-end: every candidate starts in the last row and the bottom
 			// gap-barrier rows allow only diagonal moves, so walks there stay on
 			// their own diagonals and can neither meet nor be met: no marks
@@ -392,11 +417,23 @@ k_sw_bt(BtArgs A) {
 							// cur + rdge needs the row scan
 							const int32_t cc = (int32_t)col - 1;
 							const int32_t hm = hmax((int32_t)row);
-							for(int32_t k = 1; cc - k >= 0; k++) {
-								const int32_t need = cur + rdge + rdgo + (k - 1) * rdge;
-								if(need > hm) break;
-								if(pl.h(row, (uint32_t)(cc - k)) == need) { mv = 4; nxt = cur + rdge; break; }
+							// eight independent loads in flight per round (only existence matters)
+							bool found = false;
+#pragma unroll 1
+							for(int32_t k0 = 1; !found && cc - k0 >= 0 && cur + rdge + rdgo + (k0 - 1) * rdge <= hm;
+							    k0 += 8) {
+								int32_t v[8];
+								BTC(3);
+#pragma unroll
+								for(int u = 0; u < 8; u++)
+									v[u] = cc - (k0 + u) >= 0 ? pl.h(row, (uint32_t)(cc - (k0 + u))) : -1;
+#pragma unroll
+								for(int u = 0; u < 8; u++) {
+									const int32_t need = cur + rdge + rdgo + (k0 + u - 1) * rdge;
+									found = found || (cc - (k0 + u) >= 0 && need <= hm && v[u] == need);
+								}
 							}
+							if(found) { mv = 4; nxt = cur + rdge; }
 						}
 					}
 				}
@@ -454,18 +491,16 @@ k_sw_bt(BtArgs A) {
 	};
 	for(uint32_t ci = 0; ci < ncand; ci++) {
 		if(nal >= (int32_t)A.maxaln) break;
-#ifdef BT2G_BT_MAXWALK
-		if(!first && ci >= BT2G_BT_MAXWALK) break;      // timing experiments only
-#endif
 		const bt2g_sw_cand cd = cl[ci];
 		int8_t fate;
+		BTC(4);
 		if(cd.score < P.minsc) {
 			fate = 5;                                   // BT_CAND_FATE_FILT_SCORE
 		} else if((local || (uint32_t)cd.row + (uint32_t)gb < nrow) && marked((uint32_t)cd.row, (uint32_t)cd.col)) {
 			// (end-to-end starts in the bottom barrier rows are never marked: see walk)
 			fate = 3;                                   // BT_CAND_FATE_FILT_START
 		} else {
-			if(local && dom_test((uint32_t)cd.row, (uint32_t)cd.col)) {
+			if(local && (BTC(5), dom_test((uint32_t)cd.row, (uint32_t)cd.col))) {
 				fate = 4;                               // BT_CAND_FATE_FILT_DOMINATED
 			} else {
 				// the first walk writes its edits as it goes (it usually succeeds);
@@ -474,7 +509,7 @@ k_sw_bt(BtArgs A) {
 				const uint32_t row0 = (uint32_t)cd.row, col0 = (uint32_t)cd.col;
 				// the candidate's score is its cell's H
 				Walk w = walk(row0, col0, cd.score, true, first, ed);
-				if(w.ok && !first) (void)walk(row0, col0, cd.score, false, true, ed);
+				if(w.ok && !first) { BTC(6); (void)walk(row0, col0, cd.score, false, true, ed); }
 				first = false;
 				if(local) dom_add((uint32_t)cd.row, (uint32_t)cd.col);
 				if(w.ok) {

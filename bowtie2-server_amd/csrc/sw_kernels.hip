@@ -478,6 +478,9 @@ void launch_sort_cands(const bt2g_sw_result* res, bt2g_sw_cand* cands, uint32_t 
 	if(cap <= 64) return;
 	uint32_t P2 = 1;
 	while(P2 < cap) P2 <<= 1;
-	hipLaunchKernelGGL(k_sort_big, dim3(1024), dim3(256), P2 * sizeof(unsigned long long), st, res, cands, cap, big,
+	// enough workgroups to fill every CU's LDS (16 KB each at cap 2048); the
+	// queue length is only known on the device, idle groups exit at once
+	const uint32_t grid = nprob < 4096u ? nprob : 4096u;
+	hipLaunchKernelGGL(k_sort_big, dim3(grid), dim3(256), P2 * sizeof(unsigned long long), st, res, cands, cap, big,
 	                   nbig);
 }

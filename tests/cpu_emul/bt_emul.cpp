@@ -7,6 +7,10 @@
 #include <string.h>
 
 thread_local uint3v threadIdx, blockIdx;
+#ifdef BT2G_BT_COUNT
+unsigned long long bt_counts[8];
+extern "C" unsigned long long* bt_emul_counts() { return bt_counts; }
+#endif
 
 extern "C" int bt_emul_run(int kind, const bt2g_sw_problem* probs, uint32_t nprob, const uint8_t* reads,
                            const uint8_t* quals, uint32_t stride, const uint32_t* lens, const uint8_t* windows,
