@@ -50,13 +50,18 @@ SEEDLEN, INTERVAL = 22, 15     # --sensitive, 150 bp: -L 22, -i S,1,1.15 -> 1+1.
 
 class Policy:
     """Per-mode seed and score policy (bt2_search.cpp presets).
-    ee:    --end-to-end --sensitive: -L 22, -i S,1,1.15, --score-min L,-0.6,-0.6
-    local: --local --sensitive-local: -L 20, -i S,1,0.75, --score-min G,20,8, --ma 2"""
+    ee:     --end-to-end --sensitive: -L 22, -i S,1,1.15, --score-min L,-0.6,-0.6
+    local:  --local --sensitive-local: -L 20, -i S,1,0.75, --score-min G,20,8, --ma 2
+    paired: ee with the paired-end seed interval, --fr -I 0 -X 500 mate search"""
 
     def __init__(self, mode, length):
         import math
-        self.mode, self.local = mode, mode == "local"
-        if self.local:
+        self.mode, self.local, self.paired = mode, mode == "local", mode == "paired"
+        if self.paired:
+            # paired-end: the seed interval is boosted (bt2_search.cpp:3392-3395)
+            self.seedlen, self.interval = SEEDLEN, int(INTERVAL * 1.2 + 0.5)
+            self.minsc = int(-0.6 - 0.6 * length)
+        elif self.local:
             self.seedlen, self.interval = 20, int(1 + 0.75 * math.sqrt(length))
             self.minsc = int(20 + 8 * math.log(length))
         else:
@@ -65,6 +70,15 @@ class Policy:
 MAXALN, MAXEDIT = 8, 64        # alignments kept per DP (the loop stops there); edits per alignment
                                # (150 bp, minsc -90, n-ceil 22: <= 22 N + 34 mismatches = 56)
 MAXGAP = 15                    # min(max(read gaps, ref gaps), maxhalf=15), dp_framer.cpp:95-100
+MAXHALF = 15                   # --dpad (bt2_search.cpp:486)
+PE_MAXFRAG = 500               # -X (bt2_search.cpp:378); -I 0, --fr
+MATE_CHUNK = 262_144           # mate-search DPs per fill + backtrace call (their score planes: 114 KB each)
+
+
+def gap_budget(minsc, length):
+    """max(Scoring::maxReadGaps, maxRefGaps) (scoring.cpp:42-98) for the
+    default end-to-end scoring: gap open 8, extension 3, no match bonus."""
+    return 1 + (0 - 8 - minsc) // 3 if -8 >= minsc else 0
 
 
 def log(*a):
@@ -80,6 +94,29 @@ def make_genome(mb, seed=2024):
     cuts = np.linspace(0, n, nref + 1).astype(np.int64)
     parts = [g[cuts[i]:cuts[i + 1]] for i in range(nref)]
     return parts, [b"chr%d" % (i + 1) for i in range(nref)]
+
+
+def _reads_at(g, gpos, rc, length, rng):
+    """Reads whose forward-strand windows start at genome positions gpos
+    (BASELINE.md section 3 model: 1-bp indel in 5 %, 0.4 % substitutions,
+    0.05 % N, Phred 2..40), reverse-complemented where rc."""
+    n = len(gpos)
+    win = g[gpos[:, None] + np.arange(length + 1)[None, :]]
+    out = win[:, :length].copy()
+    ind = np.nonzero(rng.random(n) < 0.05)[0]
+    for i in ind:                                   # 1-bp indel in 5 % of reads
+        k = rng.integers(1, length - 1)
+        if rng.random() < 0.5:
+            out[i, k:] = win[i, k + 1:length + 1]
+        else:
+            out[i, k + 1:] = win[i, k:length - 1]
+            out[i, k] = rng.integers(0, 4)
+    out[rc] = np.where(out[rc] > 3, 4, 3 - out[rc])[:, ::-1]
+    m = rng.random((n, length)) < 0.004
+    out[m] = (out[m] + rng.integers(1, 4, m.sum(), dtype=np.uint8)) % 4
+    out[rng.random((n, length)) < 0.0005] = 4
+    quals = (rng.integers(2, 41, (n, length), dtype=np.uint8) + 33).astype(np.uint8)
+    return out.astype(np.uint8), quals
 
 
 def make_reads(parts, n, length, seed):
@@ -109,6 +146,25 @@ def make_reads(parts, n, length, seed):
     out[rng.random((n, length)) < 0.0005] = 4
     quals = (rng.integers(2, 41, (n, length), dtype=np.uint8) + 33).astype(np.uint8)
     return out.astype(np.uint8), quals
+
+
+def make_pairs(parts, n, length, seed):
+    """n read pairs (fragment ~N(300, 50) clipped to [200, 500],
+    mates 2 x length in --fr orientation, the fragment from either strand).
+    Returns 2n reads: mate 1 of pair i in row i, mate 2 in row n + i."""
+    rng = np.random.default_rng(seed)
+    sizes = np.array([len(p) for p in parts], np.int64)
+    ref = rng.choice(len(parts), n, p=sizes / sizes.sum())
+    frag = np.clip(np.rint(rng.normal(300, 50, n)), 200, 500).astype(np.int64)
+    frag = np.maximum(frag, length)
+    pos = (rng.random(n) * (sizes[ref] - frag - 2)).astype(np.int64)
+    starts = np.concatenate([[0], np.cumsum(sizes)])[:-1]
+    g = np.concatenate(parts)
+    left, right = starts[ref] + pos, starts[ref] + pos + frag - length
+    flip = rng.random(n) < 0.5                      # fragment from the reverse strand: mate 1 on the right
+    r1, q1 = _reads_at(g, np.where(flip, right, left), flip, length, rng)
+    r2, q2 = _reads_at(g, np.where(flip, left, right), ~flip, length, rng)
+    return np.concatenate([r1, r2]), np.concatenate([q1, q2])
 
 
 class Pipeline:
@@ -177,6 +233,25 @@ class Pipeline:
         self.alns = torch.empty((self.max_probs, self.maxaln, 10), dtype=torch.int32, device=self.dev)
         self.edits = torch.empty((self.max_probs, self.maxaln, self.maxedit, 2), dtype=torch.int32, device=self.dev)
         self.stats = {}
+        if pol.paired:
+            # mate search (SwDriver::extendSeedsPaired, aligner_sw_driver.cpp:1975-2100):
+            # its own context on the same index, reserved for the mate rectangles
+            # (otherMate + frameFindMateRect: maxfrag + len - 1 + 2 max(gaps, maxhalf) columns)
+            self.npairs = P = n // 2
+            self.mate_cols = PE_MAXFRAG + length - 1 + 2 * max(gap_budget(pol.minsc, length), MAXHALF)
+            self.mate_chunk = ch = min(P, MATE_CHUNK)
+            self.eng2 = bt2g.Engine(index=idx, device=self.dev.index or 0)
+            _chk(self.L.bt2g_reserve_sw_bt(self.eng2.h, ch, length, self.mate_cols, 1))
+            self.pe = bt2g.pe_policy()
+            self.fin = torch.zeros((P, 10), dtype=torch.int32, device=self.dev)     # bt2g_frame_in
+            self.mprobs = torch.zeros((P, 5), dtype=torch.int64, device=self.dev)
+            self.mrects = torch.zeros((P, 4), dtype=torch.int32, device=self.dev)
+            self.mok = torch.zeros(P, dtype=torch.int32, device=self.dev)
+            self.mres = torch.empty((ch, 8), dtype=torch.int32, device=self.dev)
+            self.mcands = torch.empty((ch, self.sw_cap, 3), dtype=torch.int32, device=self.dev)
+            self.mnaln = torch.empty(ch, dtype=torch.int32, device=self.dev)
+            self.malns = torch.empty((ch, self.maxaln, 10), dtype=torch.int32, device=self.dev)
+            self.medits = torch.empty((ch, self.maxaln, self.maxedit, 2), dtype=torch.int32, device=self.dev)
 
     def _p(self, t):
         return C.c_void_p(t.data_ptr())
@@ -240,7 +315,61 @@ class Pipeline:
             self.last = dict(sel=sel, rows=self.rows[:nrows], offs=self.offs[:nrows], probs=probs, npb=npb,
                              nrows=nrows, m=m, ns=ns, loads_off=self.loads_off[:nrows],
                              read_base=self.read_base, read_cnt=self.read_cnt)
+        if pol.paired:
+            return self.mates(probs, npb, aligned, keep, S)
         return aligned
+
+    def mates(self, probs, npb, aligned, keep, S):
+        """Mate search for every pair with an aligned mate: the first alignment of
+        mate 1 (else mate 2) is the anchor; otherMate + frameFindMateRect frame the
+        opposite mate's window (bt2g_frame_dev, on the device) and the mate DPs
+        run fill + nextAlignment loop in chunks.  Returns the pairs with an
+        aligned mate; counts the pairs whose mate search found the opposite mate."""
+        torch, L, chk, P = self.torch, self.L, self.bt2g._chk, self._p
+        npairs, dev = self.npairs, self.dev
+        rid = probs.view(torch.int32)[:, 0].to(torch.int64)
+        dpi = torch.arange(npb, device=dev)
+        al = self.naln[:npb] > 0
+        first = torch.full((self.n,), npb, dtype=torch.int64, device=dev)
+        first.scatter_reduce_(0, rid[al], dpi[al], reduce="amin")
+        f1, f2 = first[:npairs], first[npairs:]
+        has1, has2 = f1 < npb, f2 < npb
+        use = torch.nonzero(has1 | has2).squeeze(1)
+        a1 = has1[use]
+        dp = torch.where(a1, f1[use], f2[use])
+        pw = probs.view(torch.int32)
+        na = int(use.numel())
+        fin = self.fin[:na]
+        fin.zero_()
+        fin.view(torch.int64)[:, 0] = probs[dp, 1] + self.alns[dp, 0, 2].to(torch.int64)   # anchor refoff
+        fin[:, 2] = torch.where(a1, use + npairs, use).to(torch.int32)                       # opposite mate
+        fin[:, 3] = pw[dp, 6]                                                                # refidx
+        fin[:, 4] = self.pol.minsc
+        fin[:, 5] = pw[dp, 1]                                                                # anchor strand
+        fin[:, 6] = 1                                                                        # mate search
+        fin[:, 7] = a1.to(torch.int32)
+        fin[:, 8] = self.len
+        chk(L.bt2g_frame_dev(self.eng2.h, P(fin), na, P(self.lens), C.byref(self.sc), C.byref(self.pe), MAXHALF,
+                             1, P(self.mprobs), P(self.mrects), P(self.mok), S))
+        kept = torch.nonzero(self.mok[:na]).squeeze(1)
+        nm = int(kept.numel())
+        mp = self.mprobs[:na].index_select(0, kept)
+        mr = self.mrects[:na].index_select(0, kept)
+        if nm and int(mp.view(torch.int32)[:, 7].max()) > self.mate_cols:
+            raise RuntimeError("mate rectangle wider than the reservation")
+        found = torch.zeros(npairs, dtype=torch.bool, device=dev)
+        pair_of = use.index_select(0, kept)
+        for c0 in range(0, nm, self.mate_chunk):
+            c1 = min(nm, c0 + self.mate_chunk)
+            chk(L.bt2g_sw_align_bt_dev(self.eng2.h, P(self.reads), P(self.quals), self.len, P(self.lens),
+                                       P(mp[c0:c1]), c1 - c0, None, P(mr[c0:c1]), C.byref(self.sc), 1, self.sw_cap,
+                                       P(self.mres), P(self.mcands), self.maxaln, self.maxedit, P(self.mnaln),
+                                       P(self.malns), P(self.medits), None, S))
+            found[pair_of[c0:c1][self.mnaln[:c1 - c0] > 0]] = True
+        if keep:
+            self.last.update(m_anchors=na, m_dps=nm, m_found=int(found.sum()), m_probs=mp, m_rects=mr,
+                             m_pairs=pair_of, m_fin=fin.index_select(0, kept))
+        return aligned[:npairs] | aligned[npairs:]
 
 
 def pmc_traffic(fetch_csv, write_csv, kernel):
@@ -285,8 +414,10 @@ def shard_seed(rank):
 
 def cpu_baseline(idx, reads, quals, pipe, sample, threads):
     """Reference code (oracle/_ref/libbt2ref.so = /root/reference built by
-    oracle/ref/Makefile) on the same per-read work for `sample` reads, split
-    over `threads` host threads."""
+    oracle/ref/Makefile) on the same per-read work for `sample` reads (paired:
+    `sample` pairs, both mates, plus their mate searches), split over `threads`
+    host threads.  Returns (seconds, exact-sweep outputs, seed-extension DP
+    outputs, their problems, mate DP outputs or None)."""
     import bt2_index as bi
     import tempfile
     from oracle.ref_harness import RefLib, score_params
@@ -296,47 +427,82 @@ def cpu_baseline(idx, reads, quals, pipe, sample, threads):
     L.bt2ref_get_offsets.argtypes = [C.c_void_p, C.c_int, C.c_void_p, C.c_void_p]
     L.bt2ref_sw_bt_batch.argtypes = [C.c_int, C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p,
                                      C.c_void_p, C.c_void_p, C.c_void_p, C.c_int, C.c_int, C.c_void_p]
+    L.bt2ref_sw_bt_batch_rects.argtypes = [C.c_int, C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p,
+                                           C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p]
     L.bt2ref_one_mm_gated.argtypes = [C.c_void_p, C.c_int, C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p,
                                       C.c_void_p, C.c_int]
+    L.bt2ref_frame.argtypes = [C.c_int, C.c_void_p, C.c_void_p, C.c_void_p, C.c_int, C.c_int, C.c_void_p]
     tmp = tempfile.mkdtemp(prefix="bt2bench_")
     base = os.path.join(tmp, "g")
     bi.write_index(base, idx)
     R = lib.open(base)
     last = pipe.last
-    n = sample
-    asc = synth.to_ascii(reads[:n])
+    pol = pipe.pol
+    ids = np.arange(sample)
+    if pol.paired:
+        ids = np.concatenate([ids, pipe.npairs + ids])
+    n = len(ids)
+    asc = synth.to_ascii(reads[ids])
     seqs = [bytes(asc[i]) for i in range(n)]
-    qs = [bytes(quals[i]) for i in range(n)]
+    qs = [bytes(quals[i]) for i in ids]
     # the GPU's rows / DP problems that belong to the sampled reads
-    sel = last["sel"].cpu().numpy()
-    m = int(last["m"])
     probs = last["probs"].cpu().numpy()
     pr_read = probs.view(np.int32)[:, 0]
-    pr = probs[pr_read < n]
+    pr = probs[np.isin(pr_read, ids)]
     gen_codes = idx.ref_codes
+
+    def windows(ps, ncols):
+        # reference masks of each problem's window (what the GPU fetches itself)
+        rf_all, rf_off = [], [0]
+        for p, nc in zip(ps, ncols):
+            pw = p.view(np.int32)
+            refidx, refl = int(pw[6]), int(p[1])
+            g = gen_codes[refidx]
+            o = np.arange(refl, refl + nc + 1)
+            cc = np.where((o >= 0) & (o < len(g)), g[np.clip(o, 0, len(g) - 1)], 4)
+            rf_all.append((1 << cc).astype(np.uint8))
+            rf_off.append(rf_off[-1] + nc + 1)
+        rf = np.concatenate(rf_all) if rf_all else np.zeros(1, np.uint8)
+        return rf, np.array(rf_off, np.int64)
     ncol = pipe.ncol
-    # windows for the reference's SwAligner (same masks the GPU fetches itself)
-    rf_all, rf_off = [], [0]
-    for p in pr:
-        pw = p.view(np.int32)
-        refidx, refl = int(pw[6]), int(p[1])
-        g = gen_codes[refidx]
-        o = np.arange(refl, refl + ncol + 1)
-        cc = np.where((o >= 0) & (o < len(g)), g[np.clip(o, 0, len(g) - 1)], 4)
-        rf_all.append((1 << cc).astype(np.uint8))
-        rf_off.append(rf_off[-1] + ncol + 1)
-    rf = np.concatenate(rf_all) if rf_all else np.zeros(1, np.uint8)
-    rf_off = np.array(rf_off, np.int64)
+    rf, rf_off = windows(pr, [ncol] * len(pr))
     # the GPU's hit rows of the sampled reads (contiguous per read)
     rows_all = last["rows"].cpu().numpy().astype(np.uint32)
-    rb = last["read_base"][:n].cpu().numpy().astype(np.int64)
-    rc = last["read_cnt"][:n].cpu().numpy().astype(np.int64)
+    rb = last["read_base"].cpu().numpy().astype(np.int64)[ids]
+    rc = last["read_cnt"].cpu().numpy().astype(np.int64)[ids]
     tot = int(rc.sum())
     within = np.arange(tot) - np.repeat(np.cumsum(rc) - rc, rc)
     rows = rows_all[np.repeat(rb, rc) + within]
-    pol = pipe.pol
     sp = score_params(pol.local)
     minsc = np.full(n, pol.minsc, np.int64)
+    # mate searches of the sampled pairs: the GPU's anchors (framed again by the
+    # reference inside the timed region) and their rectangles' windows
+    mate = None
+    if pol.paired:
+        mpairs = last["m_pairs"].cpu().numpy()
+        sel_m = np.nonzero(mpairs < sample)[0]
+        mfin = last["m_fin"].cpu().numpy()[sel_m]
+        mp = last["m_probs"].cpu().numpy()[sel_m]
+        mr = np.ascontiguousarray(last["m_rects"].cpu().numpy()[sel_m])
+        fin64 = mfin.view(np.int64)
+        fw32 = mfin
+        opp = fw32[:, 2].astype(np.int64)
+        fx = np.zeros((len(sel_m), 8), np.int64)
+        fx[:, 0] = 1
+        fx[:, 1] = fin64[:, 0]
+        fx[:, 2] = pipe.len
+        fx[:, 3] = [len(gen_codes[r]) for r in fw32[:, 3]]
+        fx[:, 4] = pol.minsc
+        fx[:, 5] = fw32[:, 5]
+        fx[:, 6] = fw32[:, 7]
+        fx[:, 7] = pipe.len
+        mncol = mp.view(np.int32)[:, 7].astype(np.int64)
+        mrf, mrf_off = windows(mp, mncol)
+        pos_of = {int(r): i for i, r in enumerate(ids)}
+        mseq = [seqs[pos_of[int(r)]] for r in opp]
+        mq = [qs[pos_of[int(r)]] for r in opp]
+        mate = dict(fx=fx, mp=mp, mr=mr, mncol=mncol.astype(np.int32), rf=mrf, rf_off=mrf_off, seq=mseq, q=mq,
+                    fw=np.ascontiguousarray(mp.view(np.int32)[:, 1].astype(np.uint8)), sel=sel_m)
 
     def work(lo, hi):
         s, q = seqs[lo:hi], qs[lo:hi]
@@ -360,14 +526,15 @@ def cpu_baseline(idx, reads, quals, pipe, sample, threads):
         L.bt2ref_get_offsets(R.h, hi - lo, rr.ctypes.data, out.ctypes.data)
         return out
 
+    pos = np.searchsorted(ids, pr_read[np.isin(pr_read, ids)])
+
     def work_sw(lo, hi):
         k = hi - lo
         ps = pr[lo:hi]
-        rid = ps.view(np.int32)[:, 0]
         fwv = np.ascontiguousarray(ps.view(np.int32)[:, 1].astype(np.uint8))
         # the reference's SwAligner takes the read forward and its fw flag
-        cs = (C.c_char_p * k)(*[seqs[r] for r in rid])
-        cq = (C.c_char_p * k)(*[qs[r] for r in rid])
+        cs = (C.c_char_p * k)(*[seqs[r] for r in pos[lo:hi]])
+        cq = (C.c_char_p * k)(*[qs[r] for r in pos[lo:hi]])
         offs = np.ascontiguousarray(rf_off[lo:hi + 1] - 0)
         nc = np.full(k, ncol, np.int32)
         ms = np.full(k, pol.minsc, np.int64)
@@ -375,6 +542,23 @@ def cpu_baseline(idx, reads, quals, pipe, sample, threads):
         L.bt2ref_sw_bt_batch(k, cs, cq, fwv.ctypes.data, rf.ctypes.data, offs.ctypes.data, nc.ctypes.data,
                              ms.ctypes.data, C.byref(sp), MAXGAP, 3 * MAXGAP, out.ctypes.data)
         return out
+
+    def work_mate(lo, hi):
+        k = hi - lo
+        fx = np.ascontiguousarray(mate["fx"][lo:hi])
+        fo = np.zeros((k, 7), np.int64)
+        pev = np.array([3, 0, PE_MAXFRAG, 0, 0, 1, 1], np.int32)
+        L.bt2ref_frame(k, fx.ctypes.data, C.byref(sp), pev.ctypes.data, MAXHALF, 1, fo.ctypes.data)
+        cs = (C.c_char_p * k)(*mate["seq"][lo:hi])
+        cq = (C.c_char_p * k)(*mate["q"][lo:hi])
+        out = np.zeros((k, 8), np.int64)
+        ms = np.full(k, pol.minsc, np.int64)
+        L.bt2ref_sw_bt_batch_rects(k, cs, cq, mate["fw"][lo:].ctypes.data, mate["rf"].ctypes.data,
+                                   np.ascontiguousarray(mate["rf_off"][lo:hi + 1]).ctypes.data,
+                                   np.ascontiguousarray(mate["mncol"][lo:hi]).ctypes.data, ms.ctypes.data,
+                                   C.byref(sp), np.ascontiguousarray(mate["mr"][lo:hi]).ctypes.data,
+                                   out.ctypes.data)
+        return fo, out
 
     def split(total):
         b = np.linspace(0, total, threads + 1).astype(int)
@@ -385,42 +569,100 @@ def cpu_baseline(idx, reads, quals, pipe, sample, threads):
         exs = list(ex_.map(lambda a: work(*a), split(n)))
         list(ex_.map(lambda a: work_rows(*a), split(len(rows))))
         sws = list(ex_.map(lambda a: work_sw(*a), split(len(pr))))
+        mts = list(ex_.map(lambda a: work_mate(*a), split(len(mate["fx"])))) if mate else []
     dt = time.perf_counter() - t0
     R.close()
     ex_all = np.concatenate(exs)
     sw_all = np.concatenate(sws) if sws else np.zeros((0, 8), np.int64)
-    return dt, ex_all, sw_all, pr
+    if mate is not None:
+        mate["frame_ref"] = np.concatenate([m[0] for m in mts]) if mts else np.zeros((0, 7), np.int64)
+        mate["out_ref"] = np.concatenate([m[1] for m in mts]) if mts else np.zeros((0, 8), np.int64)
+    return dt, ex_all, sw_all, pr, mate
 
 
-def backtrace_parity(pipe, keep, sw_ref):
-    """GPU nextAlignment results of the sampled DPs vs the reference's
-    (bt2ref_sw_bt_batch): alignment count, first alignment (candidate, score,
-    offset, edit count) and a checksum over every alignment's edits.  Counts
-    DPs that differ; DPs that hit maxaln compare their first maxaln only."""
+def bt_mismatches(naln, alns, ed, ref, maxaln, maxedit):
+    """DPs whose GPU nextAlignment results differ from the reference's
+    (bt2ref_sw_bt_batch rows): alignment count, first alignment (candidate,
+    score, offset, edit count) and a checksum over every alignment's edits.  DPs
+    that hit maxaln compare their first maxaln only."""
     import torch
-    npb = pipe.last["npb"]
-    kp = torch.from_numpy(np.nonzero(keep)[0]).to(pipe.dev)
-    naln = pipe.naln[:npb].index_select(0, kp).to(torch.int64)
-    alns = pipe.alns[:npb].index_select(0, kp).to(torch.int64)
-    ed = pipe.edits[:npb].index_select(0, kp)
+    dev = naln.device
+    naln = naln.to(torch.int64)
+    alns = alns.to(torch.int64)
     pos = ed[..., 0].to(torch.int64)
     w = ed[..., 1].to(torch.int64) & 0xFFFFFFFF
     typ, chr_, qchr = w & 0xFF, (w >> 8) & 0xFF, (w >> 16) & 0xFF
-    k = torch.arange(pipe.maxaln, device=pipe.dev)[None, :, None]
-    e = torch.arange(pipe.maxedit, device=pipe.dev)[None, None, :]
+    k = torch.arange(maxaln, device=dev)[None, :, None]
+    e = torch.arange(maxedit, device=dev)[None, None, :]
     live = (k < naln[:, None, None]) & (e < alns[:, :, 6][:, :, None])
     term = (k + 1) * (pos * 131 + typ * 31 + chr_ * 7 + qchr)
     ck = (torch.where(live, term, torch.zeros_like(term)).sum((1, 2)) & 0x7FFFFFFFFFFFFFFF).cpu().numpy()
     naln = naln.cpu().numpy()
     first = alns[:, 0][:, [0, 1, 2, 6]].cpu().numpy()
-    bad = np.minimum(sw_ref[:, 2], pipe.maxaln) != naln
-    bad |= (naln > 0) & (first != sw_ref[:, 3:7]).any(1)
-    bad |= (naln < pipe.maxaln) & (ck != sw_ref[:, 7])
+    bad = np.minimum(ref[:, 2], maxaln) != naln
+    bad |= (naln > 0) & (first != ref[:, 3:7]).any(1)
+    bad |= (naln < maxaln) & (ck != ref[:, 7])
     if os.environ.get("BT2G_BENCH_DEBUG"):
         for i in np.nonzero(bad)[0][:8]:
             print(f"[bt mismatch] dp {i}: gpu naln {naln[i]} first {first[i].tolist()} ck {ck[i]} | "
-                  f"ref {sw_ref[i].tolist()}", flush=True)
+                  f"ref {ref[i].tolist()}", flush=True)
     return int(bad.sum())
+
+
+def backtrace_parity(pipe, keep, sw_ref):
+    """The sampled seed-extension DPs' nextAlignment results vs the reference's."""
+    import torch
+    npb = pipe.last["npb"]
+    kp = torch.from_numpy(np.nonzero(keep)[0]).to(pipe.dev)
+    return bt_mismatches(pipe.naln[:npb].index_select(0, kp), pipe.alns[:npb].index_select(0, kp),
+                         pipe.edits[:npb].index_select(0, kp), sw_ref, pipe.maxaln, pipe.maxedit)
+
+
+def mate_parity(pipe, mate):
+    """The sampled pairs' mate searches: rectangles (bt2g_frame vs the
+    reference's otherMate + frameFindMateRect) and the mate DPs' fill +
+    nextAlignment results, re-run on the GPU for the sample (outside the
+    timed steps) vs the reference's."""
+    import torch
+    bt2g, L = pipe.bt2g, pipe.L
+    mp, mr = mate["mp"], mate["mr"]
+    fr = mate["frame_ref"]
+    got = np.stack([np.ones(len(mp), np.int64), mp.view(np.int32)[:, 1], mp[:, 1], mp.view(np.int32)[:, 7],
+                    mr[:, 0], mr[:, 1], mr[:, 2]], 1)
+    frame_bad = int((got != fr).any(1).sum())
+    k = len(mp)
+    if k == 0:
+        return {"mate_dps": 0, "frame_mismatch": frame_bad, "mate_backtrace_mismatch": 0}
+    k = min(k, pipe.mate_chunk)
+    dev = pipe.dev
+    tp = torch.from_numpy(np.ascontiguousarray(mp[:k])).to(dev)
+    tr = torch.from_numpy(np.ascontiguousarray(mr[:k])).to(dev)
+    S = C.c_void_p(torch.cuda.current_stream().cuda_stream)
+    bt2g._chk(L.bt2g_sw_align_bt_dev(pipe.eng2.h, pipe._p(pipe.reads), pipe._p(pipe.quals), pipe.len,
+                                     pipe._p(pipe.lens), pipe._p(tp), k, None, pipe._p(tr), C.byref(pipe.sc), 1,
+                                     pipe.sw_cap, pipe._p(pipe.mres), pipe._p(pipe.mcands), pipe.maxaln,
+                                     pipe.maxedit, pipe._p(pipe.mnaln), pipe._p(pipe.malns), pipe._p(pipe.medits),
+                                     None, S))
+    torch.cuda.synchronize()
+    ref = mate["out_ref"][:k]
+    res = pipe.mres[:k].cpu().numpy()
+    sw_bad = int((res[:, 0] != ref[:, 0]).sum() + (res[:, 6] != ref[:, 1]).sum())
+    bt_bad = bt_mismatches(pipe.mnaln[:k], pipe.malns[:k], pipe.medits[:k], ref, pipe.maxaln, pipe.maxedit)
+    return {"mate_dps": k, "frame_mismatch": frame_bad, "mate_sw_mismatch": sw_bad,
+            "mate_backtrace_mismatch": bt_bad, "mate_ref_alignments": int(ref[:, 2].sum())}
+
+
+def workload(args):
+    genome = f"vs a {args.genome_mb:.0f} Mbp synthetic genome (hg38 unavailable offline)"
+    seed = ("exact sweep + gated 1-mm + seed round 0 + SA offsets + <=2 seed-extension DPs/read "
+            "(fill + nextAlignment loop)")
+    if args.mode == "paired":
+        return (f"{args.reads} synthetic 2 x {args.read_len} bp read pairs per GPU per step (BASELINE configs[2]), "
+                f"--end-to-end --sensitive, {genome}; both mates: {seed}; then per pair with an aligned mate one "
+                f"mate search: otherMate + frameFindMateRect (--fr -I 0 -X 500) + the mate DP "
+                f"({args.read_len} x <=705, fill + nextAlignment loop)")
+    mode = "--local --sensitive-local (configs[3])" if args.mode == "local" else "--end-to-end --sensitive (configs[1])"
+    return f"{args.reads} synthetic {args.read_len} bp unpaired reads per GPU per step, {mode} policy, {genome}; {seed}"
 
 
 def main():
@@ -428,10 +670,11 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=3)
     ap.add_argument("--warmup", type=int, default=1)
-    ap.add_argument("--reads", type=int, default=1_000_000, help="reads per GPU per step")
+    ap.add_argument("--reads", type=int, default=1_000_000, help="reads (paired: read pairs) per GPU per step")
     ap.add_argument("--read-len", type=int, default=150)
-    ap.add_argument("--mode", choices=("ee", "local"), default="ee",
-                    help="ee: BASELINE configs[1] (--end-to-end --sensitive); local: configs[3] (--local)")
+    ap.add_argument("--mode", choices=("ee", "local", "paired"), default="ee",
+                    help="ee: BASELINE configs[1] (--end-to-end --sensitive); local: configs[3] (--local); "
+                         "paired: configs[2] (2 x 150 bp pairs, --end-to-end, mate search)")
     ap.add_argument("--genome-mb", type=float, default=1000.0)
     ap.add_argument("--cpu-sample", type=int, default=1_000_000)
     ap.add_argument("--cpu-threads", type=int, default=16)
@@ -472,17 +715,22 @@ def main():
     eng = bt2g.Engine(index=idx, device=local)
     info = eng.info()
     t2 = time.time()
-    reads_np, quals_np = make_reads(parts, args.reads, args.read_len, seed=shard_seed(rank))
+    if args.mode == "paired":
+        reads_np, quals_np = make_pairs(parts, args.reads, args.read_len, seed=shard_seed(rank))
+    else:
+        reads_np, quals_np = make_reads(parts, args.reads, args.read_len, seed=shard_seed(rank))
     log(f"[rank {rank}] {args.reads} reads in {time.time()-t2:.1f}s; index resident: {info[12]/1e9:.2f} GB")
     reads = torch.from_numpy(reads_np).to(dev)
     quals = torch.from_numpy(quals_np).to(dev)
     pipe = Pipeline(eng, idx, reads, quals, args.read_len, args.mode)
 
+    engs = [eng] + ([pipe.eng2] if args.mode == "paired" else [])
     for _ in range(args.warmup):
         pipe.step()
     torch.cuda.synchronize()
-    eng.reset_stats()
-    eng.set_profiling(True)
+    for e in engs:
+        e.reset_stats()
+        e.set_profiling(True)
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
@@ -495,8 +743,10 @@ def main():
     if world > 1:
         dist.barrier()
     elapsed = time.perf_counter() - ts
-    eng.set_profiling(False)
+    for e in engs:
+        e.set_profiling(False)
     stats = {k: eng.kernel_stats(k) for k in range(6)}
+    mstats = {k: pipe.eng2.kernel_stats(k) for k in (4, 5, 7)} if args.mode == "paired" else {}
     elapsed, n_aligned = combine_ranks(elapsed, n_aligned, dev)
     total_reads = args.reads * args.steps * world
     value = total_reads / elapsed
@@ -505,7 +755,7 @@ def main():
     last = pipe.last
     names_k = ["exact_sweep", "seed_search", "one_mm", "get_offset", "sw_align", "sw_backtrace"]
     per_launch = {}
-    n = args.reads
+    n = pipe.n                                       # reads (paired: both mates)
     sweep_loads = int((pipe.sweep[:, 7].to(torch.int64) & 0xFFFFFFFF).sum())
     bytes_k = {
         # 64-B sides gathered + the read bytes each lane walks (2 strands)
@@ -531,6 +781,15 @@ def main():
                 "dps_at_maxaln": int((naln_np >= pipe.maxaln).sum()), "maxaln": pipe.maxaln,
                 "dps_cand_overflow": int((naln_np == -5).sum())}
     log(f"[rank {rank}] SW: {last['npb']} DPs/step, {sw_gcups:.0f} GCUPS; aligned {n_aligned/(args.steps*world*args.reads):.4f}; backtrace {bt_stats}")
+    mate_stats = None
+    if args.mode == "paired":
+        mk = {k: v[1] / args.steps for k, v in mstats.items()}          # ms per step
+        mcells = last["m_dps"] * args.read_len * pipe.mate_cols
+        mate_stats = {"anchors": last["m_anchors"], "mate_dps": last["m_dps"], "pairs_mate_found": last["m_found"],
+                      "frame_ms_per_step": mk[7], "fill_ms_per_step": mk[4], "backtrace_ms_per_step": mk[5],
+                      "fill_gcups": mcells / (mk[4] / 1e3) / 1e9 if mk[4] else None,
+                      "launches_per_step": mstats[4][0] / args.steps}
+        log(f"[rank {rank}] mate search: {mate_stats}")
 
     # ---- CPU baseline: the reference on the host cores, rank 0, N=1 ---------
     cpu = None
@@ -539,22 +798,32 @@ def main():
         threads = max(1, min(args.cpu_threads, os.cpu_count() or 1))
         sample = min(args.cpu_sample, args.reads)
         try:
-            dt, ex_ref, sw_ref, pr = cpu_baseline(idx, reads_np, quals_np, pipe, sample, threads)
-            cpu = {"value": sample / dt, "unit": "reads/s", "cores": threads, "kind": "reference",
-                   "sample": f"first {sample} reads of the batch through the reference's exactSweep, "
-                             f"gated oneMmSearch, searchAllSeeds, getOffset, SwAligner::align and the "
-                             f"nextAlignment loop on the same rows/DP problems ({len(pr)} DPs), {threads} threads"}
-            sw_gpu = pipe.sweep[:sample].cpu().numpy().astype(np.int64) & 0xFFFFFFFF
+            dt, ex_ref, sw_ref, pr, mate = cpu_baseline(idx, reads_np, quals_np, pipe, sample, threads)
+            paired = args.mode == "paired"
+            cpu = {"value": sample / dt, "unit": "read pairs/s" if paired else "reads/s", "cores": threads,
+                   "kind": "reference",
+                   "sample": f"first {sample} {'pairs (both mates)' if paired else 'reads'} of the batch through "
+                             f"the reference's exactSweep, gated oneMmSearch, searchAllSeeds, getOffset, "
+                             f"SwAligner::align and the nextAlignment loop on the same rows/DP problems "
+                             f"({len(pr)} DPs)"
+                             + (f", then otherMate + frameFindMateRect + the mate DPs ({len(mate['fx'])})"
+                                if paired else "") + f", {threads} threads"}
+            ids = np.arange(sample)
+            if paired:
+                ids = np.concatenate([ids, pipe.npairs + ids])
+            sw_gpu = pipe.sweep[torch.from_numpy(ids).to(dev)].cpu().numpy().astype(np.int64) & 0xFFFFFFFF
             mism = int((sw_gpu[:, [0, 1, 2, 3, 4, 5]] != ex_ref[:, [0, 1, 3, 4, 5, 6]].astype(np.int64)).any(1).sum())
             npb = pipe.last["npb"]
             res = pipe.res[:npb].cpu().numpy()
             pr_read = pipe.last["probs"].cpu().numpy().view(np.int32)[:, 0]
-            keep = pr_read < sample
+            keep = np.isin(pr_read, ids)
             rr = res[keep]
             sw_mism = int((rr[:, 0] != sw_ref[:, 0]).sum() + (rr[:, 6] != sw_ref[:, 1]).sum())
             bt_mism = backtrace_parity(pipe, keep, sw_ref)
             parity = {"exact_sweep_mismatch": mism, "sw_mismatch": sw_mism, "backtrace_mismatch": bt_mism,
-                      "reads": sample, "dps": int(len(sw_ref)), "ref_alignments": int(sw_ref[:, 2].sum())}
+                      "reads": int(len(ids)), "dps": int(len(sw_ref)), "ref_alignments": int(sw_ref[:, 2].sum())}
+            if paired:
+                parity.update(mate_parity(pipe, mate))
             log(f"[rank 0] cpu baseline {sample/dt:.0f} reads/s on {threads} threads ({dt:.1f}s); parity {parity}")
         except Exception as e:  # the reference build is optional on the box
             log(f"[rank 0] cpu baseline unavailable: {e!r}")
@@ -562,14 +831,11 @@ def main():
     if rank == 0:
         out = {
             "metric": "reads aligned/sec (whole node), 150 bp vs hg38, at 1/2/4/8 MI355X",
-            "value": value, "unit": "reads/s", "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
+            "value": value, "unit": "read pairs/s" if args.mode == "paired" else "reads/s", "n_gpus": world,
+            "steps": args.steps, "warmup": args.warmup,
             "ms_per_step": elapsed / args.steps * 1e3, "higher_is_better": True, "scaling": "weak",
             "vs_baseline": None, "dtype": "u8/i16 DP, u32 FM", "data": "synthetic",
-            "config": {"workload": f"{args.reads} synthetic {args.read_len} bp unpaired reads per GPU per step, "
-                                   f"{'--local --sensitive-local' if args.mode == 'local' else '--end-to-end --sensitive'}"
-                                   f" policy, vs a {args.genome_mb:.0f} Mbp synthetic "
-                                   f"genome (hg38 unavailable offline); exact sweep + gated 1-mm + seed round 0 "
-                                   f"+ SA offsets + <=2 seed-extension DPs/read (fill + nextAlignment loop)",
+            "config": {"workload": workload(args),
                        "global_batch": args.reads * world, "seq_len": args.read_len, "parallelism": f"dp{world}",
                        "aligned_frac": n_aligned / total_reads},
             "roofline": {"bound": "hbm", "kernel": names_k[dom], "achieved": achieved, "peak": HBM_PEAK_GBS,
@@ -582,11 +848,13 @@ def main():
             "side_loads_per_step": {names_k[k]: (bytes_k[k] // 64) for k in (0, 1, 2, 3) if bytes_k.get(k)},
             "sw_gcups": sw_gcups,
             "backtrace": bt_stats,
+            "mate_search": mate_stats,
             "cpu_baseline": cpu,
             "parity_sample": parity,
         }
         print(json.dumps(out), flush=True)
-    eng.close()
+    for e in engs[::-1]:
+        e.close()
     if world > 1:
         dist.destroy_process_group()
 

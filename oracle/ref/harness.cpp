@@ -517,9 +517,11 @@ extern "C" {
 // out: n x 8 = {aligned, ncand, naln, cand0, score0, off0, nedit0, edit checksum}
 // with the checksum over all alignments k and their edits e:
 //   sum (k+1) * (pos*131 + type*31 + chr*7 + qchr)   (mod 2^63)
-void bt2ref_sw_bt_batch(int n, const char** seqs, const char** quals, const uint8_t* fws, const uint8_t* rf,
-                        const int64_t* rf_off, const int32_t* ncols, const int64_t* minsc, const ScoreParams* sp,
-                        int corel, int corer, int64_t* out) {
+// As bt2ref_sw_bt_batch with a DPRect per problem: rects n x 4 = {triml,
+// corel, corer, 0} (bt2g_sw_rect; the window is the trimmed rectangle).
+void bt2ref_sw_bt_batch_rects(int n, const char** seqs, const char** quals, const uint8_t* fws, const uint8_t* rf,
+                              const int64_t* rf_off, const int32_t* ncols, const int64_t* minsc,
+                              const ScoreParams* sp, const int32_t* rects, int64_t* out) {
 	Scoring sc = makeScoring(*sp);
 	SwAlignerX sw;
 	BTDnaString rdfw, rdrc;
@@ -542,8 +544,10 @@ void bt2ref_sw_bt_batch(int n, const char** seqs, const char** quals, const uint
 		buf.assign(rf + rf_off[i], rf + rf_off[i] + ncol + 1);
 		buf.resize(ncol + 16, 0);
 		DPRect rect;
-		rect.refl = 0; rect.refr = ncol - 1; rect.refl_pretrim = 0; rect.refr_pretrim = ncol - 1;
-		rect.triml = rect.trimr = 0; rect.corel = corel; rect.corer = corer; rect.maxgap = 0;
+		const int32_t* rc = rects + 4 * (size_t)i;
+		rect.refl = 0; rect.refr = ncol - 1; rect.refl_pretrim = -(int64_t)rc[0]; rect.refr_pretrim = ncol - 1;
+		rect.triml = (size_t)rc[0]; rect.trimr = 0; rect.corel = (size_t)rc[1]; rect.corer = (size_t)rc[2];
+		rect.maxgap = 0;
 		sw.initRef(fws[i] != 0, 0, rect, buf.data(), 0, (size_t)ncol, (TRefOff)ncol + 1000, sc, minsc[i],
 		           true, 2000, 4, false, true);
 		TAlScore best = std::numeric_limits<TAlScore>::min();
@@ -573,6 +577,14 @@ void bt2ref_sw_bt_batch(int n, const char** seqs, const char** quals, const uint
 		o[2] = na;
 		o[7] = (int64_t)(ck & 0x7fffffffffffffffULL);
 	}
+}
+
+void bt2ref_sw_bt_batch(int n, const char** seqs, const char** quals, const uint8_t* fws, const uint8_t* rf,
+                        const int64_t* rf_off, const int32_t* ncols, const int64_t* minsc, const ScoreParams* sp,
+                        int corel, int corer, int64_t* out) {
+	std::vector<int32_t> rects(4 * (size_t)n);
+	for(int i = 0; i < n; i++) { rects[4 * i] = 0; rects[4 * i + 1] = corel; rects[4 * i + 2] = corer; rects[4 * i + 3] = 0; }
+	bt2ref_sw_bt_batch_rects(n, seqs, quals, fws, rf, rf_off, ncols, minsc, sp, rects.data(), out);
 }
 
 } // extern "C"
