@@ -824,7 +824,7 @@ def main():
                       "reads": int(len(ids)), "dps": int(len(sw_ref)), "ref_alignments": int(sw_ref[:, 2].sum())}
             if paired:
                 parity.update(mate_parity(pipe, mate))
-            log(f"[rank 0] cpu baseline {sample/dt:.0f} reads/s on {threads} threads ({dt:.1f}s); parity {parity}")
+            log(f"[rank 0] cpu baseline {sample/dt:.0f} {cpu['unit']} on {threads} threads ({dt:.1f}s); parity {parity}")
         except Exception as e:  # the reference build is optional on the box
             log(f"[rank 0] cpu baseline unavailable: {e!r}")
 
