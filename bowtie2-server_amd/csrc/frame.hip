@@ -164,7 +164,7 @@ __device__ bool other_mate(const bt2g_pe_policy& P, bool is1, bool fw, int64_t o
 }
 
 __global__ void __launch_bounds__(256)
-k_frame(const bt2g_frame_in* __restrict__ in, uint32_t n, const uint32_t* __restrict__ lens,
+k_frame_rect(const bt2g_frame_in* __restrict__ in, uint32_t n, const uint32_t* __restrict__ lens,
         const uint64_t* __restrict__ ref_starts, FrameConst F, bt2g_pe_policy P, bt2g_sw_problem* __restrict__ probs,
         bt2g_sw_rect* __restrict__ rects, int32_t* __restrict__ ok) {
 	const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
@@ -214,6 +214,6 @@ void launch_frame(const bt2g_frame_in* in, uint32_t n, const uint32_t* lens, con
                   const FrameConst& F, const bt2g_pe_policy& P, bt2g_sw_problem* probs, bt2g_sw_rect* rects,
                   int32_t* ok, hipStream_t st) {
 	if(n == 0) return;
-	hipLaunchKernelGGL(k_frame, dim3((n + 255u) / 256u), dim3(256), 0, st, in, n, lens, ref_starts, F, P, probs,
+	hipLaunchKernelGGL(k_frame_rect, dim3((n + 255u) / 256u), dim3(256), 0, st, in, n, lens, ref_starts, F, P, probs,
 	                   rects, ok);
 }
