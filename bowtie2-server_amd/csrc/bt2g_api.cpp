@@ -492,22 +492,28 @@ int bt2g_get_offset_dev(bt2g_ctx* c, const uint32_t* rows, uint32_t n, uint32_t*
 }
 
 // ---------------------------------------------------------------- SW engine
-// The packed two-problems-per-lane end-to-end fill covers the default
-// end-to-end scoring (no match bonus, penalties 1..255) without matrix
-// dumps; anything else runs the one-problem-per-lane fills.
-static bool sw_packed_ok(const bt2g_scoring& sc, const SwConst& C, const int16_t* mat) {
-	if(sc.local || mat || sc.match != 0 || sc.gapbar < 1 || C.npen < 0 || C.npen > 255) return false;
+// The packed two-problems-per-lane fill covers end-to-end scoring without a
+// match bonus and local scoring whose profile bytes (match + penalty) fit a
+// byte and whose scores cannot saturate i16, without matrix dumps; anything
+// else runs the one-problem-per-lane fills.
+static bool sw_packed_ok(const bt2g_scoring& sc, const SwConst& C, const int16_t* mat, uint32_t stride) {
+	if(mat || sc.gapbar < 1 || C.npen < 1 || C.npen > 255) return false;
 	for(int q = 0; q <= 40; q++)
 		if(C.mmpen[q] < 1 || C.mmpen[q] > 255) return false;   // non-zero profile marks a real row
-	if(C.npen < 1) return false;
-	return C.rdgo >= 0 && C.rdge >= 0 && C.rfgo >= 0 && C.rfge >= 0;
+	if(C.rdgo < 0 || C.rdge < 0 || C.rfgo < 0 || C.rfge < 0) return false;
+	if(!sc.local) return sc.match == 0;
+	if(C.match < 1 || C.match + C.npen > 255 || (uint64_t)stride * (uint64_t)C.match >= 32767u) return false;
+	for(int q = 0; q <= 40; q++)
+		if(C.match + C.mmpen[q] > 255) return false;
+	return true;
 }
 
-// the systolic fill's LDS holds (64/S) groups of (maxcol+1)|1 selector words
+// the systolic fill's LDS holds (64/S) groups of selector (and local) words
 static bool sw_use_packed(const bt2g_scoring& sc, const SwConst& C, const int16_t* mat, uint32_t stride,
                           uint32_t maxcol) {
-	const uint32_t S = (stride + 15u) / 16u, lds = (64u / S) * ((maxcol + 1u) | 1u) * 4u;
-	return sw_packed_ok(sc, C, mat) && lds <= 65536u;
+	const uint32_t S = (stride + 15u) / 16u;
+	const uint64_t lds = (uint64_t)(64u / S) * sw_packed_group_words(maxcol, sc.local != 0) * 4u;
+	return sw_packed_ok(sc, C, mat, stride) && lds <= 65536u;
 }
 
 // Fill + gather + candidate sort.  plane != NULL (systolic path only): also
@@ -546,8 +552,8 @@ static int sw_align_impl(bt2g_ctx* c, const uint8_t* reads, const uint8_t* quals
 	{
 		ProfScope ps(c, 4, st);
 		if(sw_use_packed(*sc, C, mat, stride, maxcol)) {
-			launch_sw_ee_packed(probs, nprob, reads, quals, stride, lens, windows, c->ref_codes, c->ref_starts, C,
-			                    enable8, cap, maxcol, res, cands, plane, hslot, hbytes, st);
+			launch_sw_packed(sc->local != 0, probs, nprob, reads, quals, stride, lens, windows, c->ref_codes,
+			                 c->ref_starts, C, enable8, cap, maxcol, res, cands, plane, hslot, hbytes, st);
 		} else {
 		const PlaneOut po{plane, hslot, maxcol};     // u16 score plane (hslot from sw_plane_slot(.., 2))
 		launch_sw_partition(probs, nprob, sc->local, enable8, list8, counts + 0, list16, counts + 1, st);
@@ -647,7 +653,7 @@ int bt2g_sw_align_bt_dev(bt2g_ctx* c, const uint8_t* reads, const uint8_t* quals
 		maxrow = 0;
 		for(uint32_t i = 0; i < nreads; i++) maxrow = hl[i] > maxrow ? hl[i] : maxrow;
 		packed = sw_use_packed(*sc, C, nullptr, stride, maxcol);
-		hb = packed && all8 ? 1 : 2;
+		hb = packed && all8 && !sc->local ? 1 : 2;
 		if((rc = talloc((void**)&plane, (size_t)sw_plane_slot(stride, maxcol, hb) * nprob))) return rc;
 	}
 	// systolic fill: bottom-aligned rows, u8 (hb 1) or u16 plane with block masks;
@@ -655,7 +661,7 @@ int bt2g_sw_align_bt_dev(bt2g_ctx* c, const uint8_t* reads, const uint8_t* quals
 	const int kind = hb == 1 ? 0 : 1;
 	a.plane = plane;
 	a.slot = sw_plane_slot(stride, maxcol, hb);
-	a.plane_top = packed ? 0 : 1;
+	a.plane_top = !packed ? 1 : sc->local ? 2 : 0;
 	if((rc = sw_align_impl(c, reads, quals, stride, lens, probs, nprob, windows, sc, enable8, cap, res, cands,
 	                       nullptr, nullptr, plane, a.slot, hb, maxcol, st)))
 		return rc;

@@ -54,11 +54,17 @@ void launch_sw_fill(int variant, const bt2g_sw_problem* probs, uint32_t nprob, c
                     const uint64_t* ref_starts, const SwConst& c, uint32_t cap, uint32_t* bnd,
                     uint32_t bnd_cols, bt2g_sw_result* res, bt2g_sw_cand* cands, int16_t* mat,
                     const uint64_t* mat_off, uint32_t* sat_list, uint32_t* sat_n, PlaneOut po, hipStream_t st);
-void launch_sw_ee_packed(const bt2g_sw_problem* probs, uint32_t nprob, const uint8_t* reads, const uint8_t* quals,
-                         uint32_t stride, const uint32_t* lens, const uint8_t* windows, const uint8_t* ref_codes,
-                         const uint64_t* ref_starts, const SwConst& C, int enable8, uint32_t cap, uint32_t max_cols,
-                         bt2g_sw_result* res, bt2g_sw_cand* cands, uint8_t* plane, uint64_t hslot, int hbytes,
-                         hipStream_t st);
+void launch_sw_packed(bool local, const bt2g_sw_problem* probs, uint32_t nprob, const uint8_t* reads,
+                      const uint8_t* quals, uint32_t stride, const uint32_t* lens, const uint8_t* windows,
+                      const uint8_t* ref_codes, const uint64_t* ref_starts, const SwConst& C, int enable8,
+                      uint32_t cap, uint32_t max_cols, bt2g_sw_result* res, bt2g_sw_cand* cands, uint8_t* plane,
+                      uint64_t hslot, int hbytes, hipStream_t st);
+// LDS words per problem pair of the systolic fill: per-column selectors, and in
+// local mode the i16 column maxima and the reference masks (u16) too
+inline uint32_t sw_packed_group_words(uint32_t max_cols, bool local) {
+	const uint32_t w = (max_cols + 1u) | 1u;
+	return local ? 2u * w + (w + 1u) / 2u : w;
+}
 // Rows per strip stack of the systolic fill (its score-plane column stride).
 inline uint32_t sw_packed_rows(uint32_t stride) { return 16u * ((stride + 15u) / 16u); }
 // Score-plane bytes per problem: 16-row blocks x cols x hbytes, then one u16
@@ -87,7 +93,7 @@ struct BtArgs {
 	uint32_t cstride;                 //   rows per column (16-row blocks)
 	uint32_t pcols;                   //   columns per row block
 	int use_mask;                     //   per-column masks of written blocks (<= 16 blocks)
-	int plane_top;                    //   rows top-aligned (one-problem-per-lane fills)
+	int plane_top;                    //   0 systolic end-to-end, 1 top-aligned (per-lane fills), 2 systolic local
 	uint32_t* marks;                  // per problem (mslot words): reportedThrough tiles
 	uint64_t mslot;
 	uint32_t mwords, mrows;           //   tiles per tile row, tile rows

@@ -119,7 +119,9 @@ k_sw_bt(BtArgs A) {
 	{
 		if(KIND == 0 && variant != 0) { A.naln[p] = -4; return; }   // i16 fill, u8-only plane
 		const size_t es = KIND == 0 ? 1 : 2;
-		pad = A.plane_top ? 0u : A.cstride - nrow;
+		// systolic end-to-end: last row at the stack bottom; one-problem-per-lane
+		// fills: top-aligned; systolic local: padded rows (round16) at the bottom
+		pad = A.plane_top == 1 ? 0u : A.cstride - (A.plane_top == 2 ? ((nrow + 15u) & ~15u) : nrow);
 		slot = A.plane + (size_t)p * A.slot;
 		pl.base = slot;
 		pl.pad = pad;

@@ -1,11 +1,14 @@
-// sw_ee_packed.hip -- end-to-end SW fill + last-row gather as a systolic
-// array of lanes, two problems per lane in packed 16-bit arithmetic (gfx950
-// VOP3P: v_pk_sub_u16 clamp, v_pk_max_u16, v_perm_b32).
+// sw_ee_packed.hip -- SW fills + candidate gather as a systolic array of
+// lanes, two problems per lane in packed 16-bit arithmetic (gfx950 VOP3P:
+// v_pk_sub_u16 clamp, v_pk_max_u16, v_perm_b32).
 //
-// Restates the end-to-end fills selected by SwAligner::align
-// (aligner_sw.cpp:500-620): aligner_swsse_ee_u8.cpp:775-1146 and
-// aligner_swsse_ee_i16.cpp:780-1200, plus the last-row candidate gather
-// (aligner_swsse_ee_u8.cpp:1176-1208), bit for bit.
+// Restates the fills selected by SwAligner::align (aligner_sw.cpp:500-620),
+// bit for bit: end-to-end aligner_swsse_ee_u8.cpp:775-1146 and
+// aligner_swsse_ee_i16.cpp:780-1200 with the last-row candidate gather
+// (aligner_swsse_ee_u8.cpp:1176-1208); local (LOCAL) aligner_swsse_loc_u8.cpp:
+// 927-1336 and aligner_swsse_loc_i16.cpp:938-1367 with their gathers
+// (aligner_swsse_loc_u8.cpp:1389-1500, aligner_swsse_loc_i16.cpp:1420-1535) and
+// the u8 -> i16 fallback on saturation (aligner_sw.cpp:570-605).
 //
 // Value domain.  Both reference domains run as unsigned 16-bit lanes with
 // unsigned saturation:
@@ -15,6 +18,22 @@
 //                                                    -> ROW0 = 0xffff, LO = 0
 // so a lane may pair a u8 problem with an i16 one; the reference's veto of
 // gap opens/extensions in the gap-barrier rows becomes an AND with 0 (LO).
+//
+// Local value domain: the score itself (floor 0 = the unsigned saturation of
+// the subtract).  The u8 local fill's bias cancels unless a cell would reach
+// 255 - bias, which is exactly its saturation test (column max + bias >= 255,
+// then the i16 fill runs), and the i16 fill's 0x8000 offset drops out: one
+// pass yields the H of both fills.  They differ only in the striped padding
+// rows below the last row (score 0, no gap barrier; up to a multiple of 16
+// rows for u8, of 8 for i16) that feed the per-column maxima driving
+// lastsolcol_ / colstop_; a problem's padded rows end at the bottom of the
+// strip stack and the bottom lane keeps both column maxima.  The diagonal term
+// is H(up-left) + match - pen', the query profile holding pen' = match - score
+// (0 for a match), so dead rows above the problem (profile = match) stay 0.
+// Candidate cells (>= minsc, a match whose down-right neighbour is not) are
+// found with per-character row bit masks, only in 16-row blocks whose maximum
+// reaches minsc, and appended through an LDS counter per problem (the
+// candidate sort that follows fixes the order).
 //
 // Layout.  A problem pair (low/high half of every register) is swept by a
 // group of S lanes (S = ceil(stride/16)); lane k of the group owns register
@@ -62,17 +81,8 @@ struct Half {
 	int64_t refl, win_off;
 	uint32_t nrow, ncol, pi, refidx;
 	int32_t minsc;
-	uint32_t row0;      // 0xff (u8 fill) or 0xffff (i16 fill)
+	uint32_t row0;      // end-to-end: 0xff (u8 fill) or 0xffff (i16 fill); local: 0
 	bool fw, live;
-	// reference character of column j (aligner_sw.cpp:171-253): 0..3, 4 = N / off the reference
-	__device__ __forceinline__ int refc(uint32_t j, const uint8_t* windows, const uint8_t* ref_codes,
-	                                    const uint64_t* ref_starts) const {
-		if(!live || j >= ncol) return 4;
-		if(win_off >= 0) return first5(windows[win_off + j]);
-		int64_t o = refl + (int64_t)j;
-		uint64_t s = ref_starts[refidx], e = ref_starts[refidx + 1];
-		return (o < 0 || (uint64_t)o >= e - s) ? 4 : ref_codes[s + (uint64_t)o];
-	}
 };
 
 }  // namespace
@@ -91,9 +101,9 @@ struct Half {
 // column j at plane + pi*hslot + ((k*max_cols + j)*16)*hbytes, so that a
 // backtrace step (up-left) usually stays inside one 128-B line; hbytes 1 keeps
 // u8 fills only.
-template <bool SAMEGO, bool STORE>
-__global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(STORE ? BT2G_SW_WAVES_STORE : BT2G_SW_WAVES)))
-k_sw_ee_sys(const bt2g_sw_problem* __restrict__ probs, uint32_t nprob, const uint8_t* __restrict__ reads,
+template <bool LOCAL, bool SAMEGO, bool STORE>
+__global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu((STORE || LOCAL) ? BT2G_SW_WAVES_STORE : BT2G_SW_WAVES)))
+k_sw_sys(const bt2g_sw_problem* __restrict__ probs, uint32_t nprob, const uint8_t* __restrict__ reads,
             const uint8_t* __restrict__ quals, uint32_t stride, const uint32_t* __restrict__ lens,
             const uint8_t* __restrict__ windows, const uint8_t* __restrict__ ref_codes,
             const uint64_t* __restrict__ ref_starts, SwConst C, int enable8, uint32_t cap, uint32_t max_cols,
@@ -111,7 +121,7 @@ k_sw_ee_sys(const bt2g_sw_problem* __restrict__ probs, uint32_t nprob, const uin
 		const uint32_t pi = base + (x ? G : 0u) + g;
 		H.live = in_group && pi < nprob;
 		H.nrow = H.ncol = 0;
-		H.row0 = 0xffu;
+		H.row0 = LOCAL ? 0u : 0xffu;
 		if(!H.live) continue;
 		H.pi = pi;
 		const bt2g_sw_problem p = probs[pi];
@@ -124,8 +134,9 @@ k_sw_ee_sys(const bt2g_sw_problem* __restrict__ probs, uint32_t nprob, const uin
 		H.win_off = p.win_off;
 		H.refidx = p.refidx;
 		H.minsc = p.minsc;
-		// u8 fill iff enable8 && minsc >= -254 (aligner_sw.cpp:516-519)
-		H.row0 = (enable8 && p.minsc >= -254) ? 0xffu : 0xffffu;
+		// end-to-end: u8 fill iff enable8 && minsc >= -254 (aligner_sw.cpp:516-519);
+		// local: both fills in one pass (score domain)
+		if(!LOCAL) H.row0 = (enable8 && p.minsc >= -254) ? 0xffu : 0xffffu;
 		if(H.ncol > max_cols || H.ncol == 0 || H.nrow == 0 || H.nrow > 16u * S) {
 			if(k == 0) {
 				bt2g_sw_result bad{};
@@ -137,6 +148,9 @@ k_sw_ee_sys(const bt2g_sw_problem* __restrict__ probs, uint32_t nprob, const uin
 			H.nrow = H.ncol = 0;
 		}
 	}
+	// strip-stack row of a problem's row 0: end-to-end, the last row at the stack
+	// bottom; local, the padding rows up to a multiple of 16 below it
+	auto top_of = [&](const Half& H) -> uint32_t { return 16u * S - (LOCAL ? ((H.nrow + 15u) & ~15u) : H.nrow); };
 	// wave-uniform sweep length
 	uint32_t ncolmax = h[0].ncol > h[1].ncol ? h[0].ncol : h[1].ncol;
 #pragma unroll
@@ -148,19 +162,30 @@ k_sw_ee_sys(const bt2g_sw_problem* __restrict__ probs, uint32_t nprob, const uin
 
 	// Scoring::mmpens (scoring.h:103-131) staged in LDS for per-lane lookups
 	__shared__ uint8_t mmq[48];
+	__shared__ uint32_t lcnt[128], lmaxc[128];     // LOCAL: candidates per problem, their largest column
 	if(lane <= 40) mmq[lane] = (uint8_t)C.mmpen[lane];
+	if(LOCAL) {
+		lcnt[lane] = lcnt[lane + 64u] = 0u;
+		lmaxc[lane] = lmaxc[lane + 64u] = 0u;
+	}
 	// this lane's rows: global row 16k+i of the stack; problem row = that - (16S - nrow).
 	// All read bytes and qualities are fetched first (independent loads, one
 	// wait), then turned into query-profile words.
 	uint32_t bq[2][R];
+	uint32_t below[2] = {5u, 5u};    // LOCAL: read character of the row under this lane's block (5: none)
 #pragma unroll
 	for(int x = 0; x < 2; x++) {
 		const Half& H = h[x];
-		const int64_t rx0 = (int64_t)(16u * k) - (int64_t)(16u * S - H.nrow);
+		const int64_t rx0 = (int64_t)(16u * k) - (int64_t)top_of(H);
+		if(LOCAL && H.live && rx0 + R >= 0 && rx0 + R < (int64_t)H.nrow) {
+			const uint32_t rb = (uint32_t)(rx0 + R);
+			const uint32_t c = H.rd[H.fw ? rb : H.nrow - 1u - rb];
+			below[x] = H.fw ? c : (c > 3u ? 4u : 3u - c);
+		}
 #pragma unroll
 		for(int i = 0; i < R; i++) {
 			const int64_t rx = rx0 + i;
-			const bool real = H.live && rx >= 0;
+			const bool real = H.live && rx >= 0 && rx < (int64_t)H.nrow;
 			const uint32_t o = real ? (H.fw ? (uint32_t)rx : H.nrow - 1 - (uint32_t)rx) : 0u;
 			const uint8_t* rdp = real ? H.rd : reads;
 			const uint8_t* qup = real ? H.qu : quals;
@@ -171,25 +196,53 @@ k_sw_ee_sys(const bt2g_sw_problem* __restrict__ probs, uint32_t nprob, const uin
 	const uint32_t row0p = h[0].row0 | (h[1].row0 << 16);
 	uint32_t PA[R], PB[R], M[R], E[R], Hc[R];   // M: 0 in gap-barrier rows (veto)
 	const int gb = C.gapbar;
+	const uint32_t match4 = (uint32_t)C.match * 0x01010101u;
+	// LOCAL: rows (bit i; +16 for the high problem) whose read character is c,
+	// real rows >= minrow (gather-eligible), the u8 fill's bias per problem
+	uint32_t rm0 = 0, rm1 = 0, rm2 = 0, rm3 = 0, rm4 = 0, rowok = 0;
+	uint32_t biasl[2] = {0u, 0u};
+	uint64_t minrow[2] = {~0ull, ~0ull};
+	if(LOCAL) {
+#pragma unroll
+		for(int x = 0; x < 2; x++)
+			minrow[x] = ((uint64_t)(int64_t)h[x].minsc + (uint64_t)C.match - 1u) / (uint64_t)(C.match > 0 ? C.match : 1) - 1u;
+	}
 #pragma unroll
 	for(int i = 0; i < R; i++) {
 		uint32_t pa = 0, pb = 0, v = 0, hi = 0;
 #pragma unroll
 		for(int x = 0; x < 2; x++) {
 			const Half& H = h[x];
-			const int64_t rx = (int64_t)(16u * k + i) - (int64_t)(16u * S - H.nrow);
-			uint32_t prof = 0, veto = 0, hinit = 0;
+			const int64_t rx = (int64_t)(16u * k + i) - (int64_t)top_of(H);
+			uint32_t prof = LOCAL ? match4 : 0u, veto = 0, hinit = 0;   // local dead/padding rows: score 0
 			if(H.live) {
-				if(rx < 0) {
-					hinit = H.row0;                  // dead row: H(col -1) = ROW0
+				if(rx < 0 || rx >= (int64_t)H.nrow) {
+					if(!LOCAL && rx < 0) hinit = H.row0;  // dead row: H(col -1) = ROW0
 				} else {
 					// {pen(A), pen(C), pen(G), pen(T)} (Scoring::score, scoring.h:237-262, no match bonus)
 					int c = (int)(bq[x][i] & 0xffu);
 					if(!H.fw) c = c > 3 ? 4 : 3 - c;
 					int q = (int)(bq[x][i] >> 8) - 33;
 					q = q < 0 ? 0 : (q > 40 ? 40 : q);
-					prof = c > 3 ? (uint32_t)C.npen * 0x01010101u
-					             : ((uint32_t)mmq[q] * 0x01010101u) & ~(0xffu << (8 * c));
+					if(LOCAL) {
+						// pen' = match - score: 0 for a match, match + mmpen / match + npen otherwise
+						prof = c > 3 ? (uint32_t)(C.match + C.npen) * 0x01010101u
+						             : (((uint32_t)(C.match + mmq[q]) * 0x01010101u) & ~(0xffu << (8 * c)));
+						const uint32_t bit = 1u << (i + 16 * x);
+						rm0 |= c == 0 ? bit : 0u;
+						rm1 |= c == 1 ? bit : 0u;
+						rm2 |= c == 2 ? bit : 0u;
+						rm3 |= c == 3 ? bit : 0u;
+						rm4 |= c > 3 ? bit : 0u;
+						if((uint64_t)rx >= minrow[x]) rowok |= bit;
+						// the u8 fill's bias: the largest penalty of the row's profile
+						const uint32_t bl = c > 3 ? (uint32_t)C.npen
+						                          : ((uint32_t)mmq[q] > (uint32_t)C.npen ? (uint32_t)mmq[q] : (uint32_t)C.npen);
+						biasl[x] = bl > biasl[x] ? bl : biasl[x];
+					} else {
+						prof = c > 3 ? (uint32_t)C.npen * 0x01010101u
+						             : ((uint32_t)mmq[q] * 0x01010101u) & ~(0xffu << (8 * c));
+					}
 					if(rx < gb || rx >= (int64_t)H.nrow - gb) veto = 0xffffu;
 				}
 			}
@@ -198,12 +251,34 @@ k_sw_ee_sys(const bt2g_sw_problem* __restrict__ probs, uint32_t nprob, const uin
 		}
 		PA[i] = pa; PB[i] = pb; M[i] = ~v; E[i] = 0; Hc[i] = hi;
 	}
+	// LOCAL: rows whose down-right neighbour's read character is c (next row real)
+	const uint32_t nm0 = ((rm0 >> 1) & 0x7fff7fffu) | (below[0] == 0u ? 0x8000u : 0u) | (below[1] == 0u ? 0x80000000u : 0u);
+	const uint32_t nm1 = ((rm1 >> 1) & 0x7fff7fffu) | (below[0] == 1u ? 0x8000u : 0u) | (below[1] == 1u ? 0x80000000u : 0u);
+	const uint32_t nm2 = ((rm2 >> 1) & 0x7fff7fffu) | (below[0] == 2u ? 0x8000u : 0u) | (below[1] == 2u ? 0x80000000u : 0u);
+	const uint32_t nm3 = ((rm3 >> 1) & 0x7fff7fffu) | (below[0] == 3u ? 0x8000u : 0u) | (below[1] == 3u ? 0x80000000u : 0u);
+	const uint32_t nm4 = ((rm4 >> 1) & 0x7fff7fffu) | (below[0] == 4u ? 0x8000u : 0u) | (below[1] == 4u ? 0x80000000u : 0u);
+	// LOCAL: the bias of each problem over its group's lanes; the bottom lane's
+	// u8-only padding rows (round16(nrow) - round8(nrow) = 8: its rows 8..15)
+	uint32_t bias[2] = {0u, 0u}, u8o = 0u;
+	if(LOCAL) {
+#pragma unroll
+		for(int x = 0; x < 2; x++) {
+			uint32_t b = 0u;
+			for(uint32_t t = 0; t < S; t++) {
+				const uint32_t o = (uint32_t)__shfl((int)biasl[x], (int)(g * S + t));
+				b = o > b ? o : b;
+			}
+			bias[x] = b;
+			const uint32_t r = h[x].nrow & 15u;
+			if(k == S - 1u && h[x].live && r != 0u && r <= 8u) u8o |= 0xffffu << (16 * x);
+		}
+	}
 	// H(row above this lane's first row, column -1): ROW0 if that row is dead
 	uint32_t hbprev = 0;
 	if(k > 0) {
 #pragma unroll
 		for(int x = 0; x < 2; x++) {
-			const int64_t rx = (int64_t)(16u * k) - 1 - (int64_t)(16u * S - h[x].nrow);
+			const int64_t rx = (int64_t)(16u * k) - 1 - (int64_t)top_of(h[x]);
 			if(h[x].live && rx < 0) hbprev |= h[x].row0 << (16 * x);
 		}
 	}
@@ -221,6 +296,10 @@ k_sw_ee_sys(const bt2g_sw_problem* __restrict__ probs, uint32_t nprob, const uin
 	// 'N' columns send the wave down the N row loop.
 	extern __shared__ uint32_t selw[];
 	uint32_t* mysel = selw + (size_t)g * ldsw;
+	uint32_t* mycm = selw + (size_t)(G + g) * ldsw;                                    // LOCAL: i16 column maxima
+	uint16_t* mymsk = (uint16_t*)(selw + (size_t)2u * G * ldsw) + (size_t)g * ldsw;      // LOCAL: reference masks
+	// local: also column ncol (the extra right column a gather's down-right test reads)
+	const uint32_t ncl = ncolmax + (LOCAL ? 1u : 0u);
 	if(in_group) {
 		const uint8_t* src[2];
 		int64_t lo[2], hi[2];
@@ -230,7 +309,7 @@ k_sw_ee_sys(const bt2g_sw_problem* __restrict__ probs, uint32_t nprob, const uin
 			const Half& H = h[x];
 			masks[x] = H.win_off >= 0;
 			lo[x] = 0;
-			hi[x] = H.ncol;
+			hi[x] = (int64_t)H.ncol + (LOCAL ? 1 : 0);
 			src[x] = reads;
 			if(!H.live) continue;
 			if(masks[x]) {
@@ -244,33 +323,40 @@ k_sw_ee_sys(const bt2g_sw_problem* __restrict__ probs, uint32_t nprob, const uin
 			}
 		}
 		// eight columns (two characters each) in flight per lane, then the selectors
-		for(uint32_t c0 = k; c0 < ncolmax; c0 += 8u * S) {
+		for(uint32_t c0 = k; c0 < ncl; c0 += 8u * S) {
 			uint32_t v[2][8];
 #pragma unroll
 			for(int u = 0; u < 8; u++) {
 				const int64_t c = (int64_t)c0 + (int64_t)u * S;
 #pragma unroll
 				for(int x = 0; x < 2; x++)
-					v[x][u] = (c >= lo[x] && c < hi[x]) ? src[x][c] : (c < (int64_t)h[x].ncol ? 0x100u : 0x200u);
+					v[x][u] = (c >= lo[x] && c < hi[x]) ? src[x][c]
+					        : (c < (int64_t)h[x].ncol + (LOCAL ? 1 : 0) ? 0x100u : 0x200u);
 			}
 #pragma unroll
 			for(int u = 0; u < 8; u++) {
 				const uint32_t c = c0 + (uint32_t)u * S;
-				if(c >= ncolmax) break;
-				uint32_t sel = 0x0c000c00u;
+				if(c >= ncl) break;
+				uint32_t sel = 0x0c000c00u, msk = 0u;
 #pragma unroll
 				for(int x = 0; x < 2; x++) {
 					// 0x100: off the reference (N); 0x200: filler
 					int code = v[x][u] == 0x100u ? 4 : v[x][u] == 0x200u ? 0
 					         : (masks[x] ? first5((int)v[x][u]) : (int)v[x][u]);
 					sel |= (code < 4 ? (uint32_t)(4 * x + code) : 0x0cu) << (16 * x);
+					// the gather's reference mask (aligner_sw.cpp:247-253: 1 << c, N -> 16)
+					const uint32_t m = v[x][u] == 0x100u ? 16u : v[x][u] == 0x200u ? 0u
+					                 : (masks[x] ? v[x][u] : (v[x][u] > 3u ? 16u : 1u << v[x][u]));
+					msk |= m << (8 * x);
 				}
 				mysel[c] = sel;
+				if(LOCAL) mymsk[c] = (uint16_t)msk;
 			}
 		}
 	}
 	__syncthreads();
 #if BT2G_SW_COLS == 2
+	static_assert(!LOCAL, "the two-column step is end-to-end only");
 	// Two columns per step: cell (i, j+1) only waits for (i, j)'s E and
 	// (i-1, j)'s H, so the two F chains of a step interleave (twice the ILP of
 	// the dependent row recurrence) and the lane-to-lane hand-off is halved.
@@ -343,25 +429,37 @@ k_sw_ee_sys(const bt2g_sw_problem* __restrict__ probs, uint32_t nprob, const uin
 		}
 	}
 #else
-	uint32_t hout = 0, fout = 0, mout = 0;
+	uint32_t hout = 0, fout = 0, mout = 0, cmout = 0;
 	uint32_t nsel = in_group ? mysel[0] : 0u;
 	const uint32_t T = ncolmax + S - 1;
 	// score plane: a 16-row block is written only when one of its cells can be
-	// on a backtrace (H >= minsc: every value a walk compares for equality is
-	// at least its own score, sw_backtrace.hip); per column, a 16-bit mask of
-	// the written blocks (S <= 16; beyond that every block is written)
+	// on a backtrace (end-to-end: H >= minsc, every value a walk compares for
+	// equality is at least its own score; local: H > 0, unwritten blocks read
+	// as 0, sw_backtrace.hip); per column, a 16-bit mask of the written blocks
+	// (S <= 16; beyond that every block is written)
 #ifdef BT2G_SW_NOMASK
 	const bool use_mask = false;           // timing experiments only
 #else
 	const bool use_mask = S <= 16u;
 #endif
-	const uint32_t thr0 = h[0].row0 + (uint32_t)h[0].minsc, thr1 = h[1].row0 + (uint32_t)h[1].minsc;
+	const uint32_t thr0 = LOCAL ? 1u : h[0].row0 + (uint32_t)h[0].minsc;
+	const uint32_t thr1 = LOCAL ? 1u : h[1].row0 + (uint32_t)h[1].minsc;
 	uint8_t* const mplane = plane + (size_t)16u * S * max_cols * (size_t)hbytes;
+	// LOCAL: a block is searched for candidates when its maximum reaches minsc
+	// (never for a problem without gather-eligible rows); cthr = minsc - 1 per half
+	uint32_t ctest[2];
+#pragma unroll
+	for(int x = 0; x < 2; x++)
+		ctest[x] = (LOCAL && ((rowok >> (16 * x)) & 0xffffu) != 0u && h[x].minsc > 0 && h[x].minsc <= 0xffff)
+		               ? (uint32_t)h[x].minsc : 0x10000u;
+	const uint32_t cthr = ((ctest[0] - 1u) & 0xffffu) | (((ctest[1] - 1u) & 0xffffu) << 16);
+	const uint32_t match2 = (uint32_t)C.match * 0x10001u, npm2 = (uint32_t)(C.match + C.npen) * 0x10001u;
 	for(uint32_t t = 0; t < T; t++) {
 		// the lane above computed this lane's column in the previous step (DPP wave_shr:1)
 		const uint32_t hin = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)hout, 0x138, 0xf, 0xf, false);
 		const uint32_t fin = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)fout, 0x138, 0xf, 0xf, false);
 		const uint32_t mskin = STORE ? (uint32_t)__builtin_amdgcn_update_dpp(0, (int)mout, 0x138, 0xf, 0xf, false) : 0u;
+		const uint32_t cmin = LOCAL ? (uint32_t)__builtin_amdgcn_update_dpp(0, (int)cmout, 0x138, 0xf, 0xf, false) : 0u;
 		const int j = (int)t - (int)k;
 		if(j < 0 || j >= (int)ncolmax) continue;
 		const uint32_t sel = nsel;
@@ -378,11 +476,12 @@ k_sw_ee_sys(const bt2g_sw_problem* __restrict__ probs, uint32_t nprob, const uin
 			hbprev = hup;
 		}
 		// An 'N' reference column costs npen in every real row (the selector
-		// picked 0 there) but nothing in dead rows, which must stay at ROW0.
+		// picked 0 there) but nothing in dead rows, which must stay at ROW0
+		// (local: pen' = match in dead and padding rows, match + npen in real ones).
 		// N columns are rare: the wave takes the slower row loop only when one of
 		// its lanes sees one.
-		const uint32_t nfloor = ((sel & 0xffu) == 0x0cu ? npen : 0u) |
-		                        (((sel >> 16) & 0xffu) == 0x0cu ? npen << 16 : 0u);
+		const uint32_t ncm = ((sel & 0xffu) == 0x0cu ? 0xffffu : 0u) | (((sel >> 16) & 0xffu) == 0x0cu ? 0xffff0000u : 0u);
+		const uint32_t nfloor = ncm & ((uint32_t)npen * 0x10001u);
 		uint32_t fprev = fup, hprev = SAMEGO ? psub(hup, rfgo2) : hup;
 		auto rows = [&](auto n_tag) {
 			constexpr bool NCOL = decltype(n_tag)::value;
@@ -390,14 +489,21 @@ k_sw_ee_sys(const bt2g_sw_problem* __restrict__ probs, uint32_t nprob, const uin
 			for(int i = 0; i < R; i++) {
 				uint32_t pen = __builtin_amdgcn_perm(PB[i], PA[i], sel);
 				if(NCOL) {
-					// real rows have a non-zero profile (sw_packed_ok: mmpen >= 1, npen >= 1);
-					// kept opaque so the masks are not hoisted into 16 more registers
+					// real rows: end-to-end a non-zero profile (sw_packed_ok: mmpen >= 1,
+					// npen >= 1), local one other than match4; kept opaque so the masks are
+					// not hoisted into 16 more registers
 					uint32_t pa = PA[i], pb = PB[i];
 					asm volatile("" : "+v"(pa), "+v"(pb));
-					const uint32_t real = (pa ? 0xffffu : 0u) | (pb ? 0xffff0000u : 0u);
-					pen = pmax(pen, nfloor & real);
+					if(LOCAL) {
+						const uint32_t real = (pa != match4 ? 0xffffu : 0u) | (pb != match4 ? 0xffff0000u : 0u);
+						pen = pmax(pen, ncm & ((npm2 & real) | (match2 & ~real)));
+					} else {
+						const uint32_t real = (pa ? 0xffffu : 0u) | (pb ? 0xffff0000u : 0u);
+						pen = pmax(pen, nfloor & real);
+					}
 				}
-				const uint32_t d = psub(diag, pen);
+				// local: H(up-left) + match - pen' (no carry between the halves: H < 2^15)
+				const uint32_t d = LOCAL ? psub(diag + match2, pen) : psub(diag, pen);
 				if(SAMEGO) {
 					// read and reference gap opens equal: H - open serves the F of the
 					// next row and the E of the next column (one subtract less)
@@ -420,8 +526,67 @@ k_sw_ee_sys(const bt2g_sw_problem* __restrict__ probs, uint32_t nprob, const uin
 				}
 			}
 		};
-		if(__ballot(nfloor != 0)) rows(std::true_type{});
+		if(__ballot(ncm != 0)) rows(std::true_type{});
 		else rows(std::false_type{});
+		// this lane's block maxima (rows 0..7 and all): block masks, local column maxima
+		uint32_t mlo = 0, mx = 0;
+		if(LOCAL || (STORE && use_mask)) {
+			mlo = Hc[0];
+#pragma unroll
+			for(int i = 1; i < R / 2; i++) mlo = pmax(mlo, Hc[i]);
+			uint32_t mhi = Hc[R / 2];
+#pragma unroll
+			for(int i = R / 2 + 1; i < R; i++) mhi = pmax(mhi, Hc[i]);
+			mx = pmax(mlo, mhi);
+		}
+		if(LOCAL) {
+			// column maxima down the group (the reference's vcolmax, padding rows
+			// included): u8 fill all rows, i16 fill without the u8-only padding rows
+			const uint32_t cm = top ? mx : pmax(cmin, mx);
+			cmout = cm;
+			if(bottom && in_group) {
+				const uint32_t m16 = (mlo & u8o) | (mx & ~u8o);
+				mysel[j] = cm;                  // the last reader of selector j has read it
+				mycm[j] = top ? m16 : pmax(cmin, m16);
+			}
+			// candidate cells of this block (aligner_swsse_loc_i16.cpp:1483-1520)
+			const bool g0 = h[0].live && (uint32_t)j < h[0].ncol && (mx & 0xffffu) >= ctest[0];
+			const bool g1 = h[1].live && (uint32_t)j < h[1].ncol && (mx >> 16) >= ctest[1];
+			if(g0 || g1) {
+				const uint32_t mj = mymsk[j], mj1 = mymsk[j + 1];
+				uint32_t ge = 0;
+#pragma unroll
+				for(int i = 0; i < R; i++) {
+					const uint32_t tt = psub(Hc[i], cthr);          // H >= minsc per half
+					ge |= ((tt & 0xffffu) ? 1u : 0u) << i;
+					ge |= ((tt >> 16) ? 1u : 0u) << (16 + i);
+				}
+				auto s2 = [](uint32_t m, int c) -> uint32_t {
+					return (((m >> c) & 1u) ? 0xffffu : 0u) | (((m >> (8 + c)) & 1u) ? 0xffff0000u : 0u);
+				};
+				// the cell is a match, its down-right neighbour (next row, next column) is not
+				const uint32_t mb = (rm0 & s2(mj, 0)) | (rm1 & s2(mj, 1)) | (rm2 & s2(mj, 2)) | (rm3 & s2(mj, 3)) |
+				                    (rm4 & s2(mj, 4));
+				const uint32_t nb = (nm0 & s2(mj1, 0)) | (nm1 & s2(mj1, 1)) | (nm2 & s2(mj1, 2)) | (nm3 & s2(mj1, 3)) |
+				                    (nm4 & s2(mj1, 4));
+				const uint32_t cand = ge & mb & ~nb & rowok & ((g0 ? 0xffffu : 0u) | (g1 ? 0xffff0000u : 0u));
+#pragma unroll
+				for(int x = 0; x < 2; x++) {
+					const uint32_t bits = (cand >> (16 * x)) & 0xffffu;
+					if(!bits) continue;
+					uint32_t slot = atomicAdd(&lcnt[2u * g + x], (uint32_t)__popc(bits));
+					atomicMax(&lmaxc[2u * g + x], (uint32_t)j);
+					bt2g_sw_cand* dst = cands + (size_t)h[x].pi * cap;
+					const int32_t rx0 = (int32_t)(16u * k) - (int32_t)top_of(h[x]);
+#pragma unroll
+					for(int i = 0; i < R; i++) {
+						if(!((bits >> i) & 1u)) continue;
+						if(slot < cap) dst[slot] = bt2g_sw_cand{rx0 + i, j, (int32_t)((Hc[i] >> (16 * x)) & 0xffffu)};
+						slot++;
+					}
+				}
+			}
+		}
 #ifdef BT2G_SW_NOSTORE
 		if(false) {                                   // timing experiments only
 #else
@@ -430,9 +595,6 @@ k_sw_ee_sys(const bt2g_sw_problem* __restrict__ probs, uint32_t nprob, const uin
 			bool s0 = h[0].live && (uint32_t)j < h[0].ncol, s1 = h[1].live && (uint32_t)j < h[1].ncol;
 			const size_t cell = ((size_t)k * max_cols + (uint32_t)j) * 16u;
 			if(use_mask) {
-				uint32_t mx = Hc[0];
-#pragma unroll
-				for(int i = 1; i < R; i++) mx = pmax(mx, Hc[i]);
 				s0 = s0 && (mx & 0xffffu) >= thr0;
 				s1 = s1 && (mx >> 16) >= thr1;
 				// block masks of column j travel down the group with the H hand-off
@@ -447,7 +609,7 @@ k_sw_ee_sys(const bt2g_sw_problem* __restrict__ probs, uint32_t nprob, const uin
 #ifdef BT2G_SW_STORE_TINY
 			const uint64_t hslot = 0;                 // timing experiments only: all writes in 64 KB
 #endif
-			if(hbytes == 1) {
+			if(!LOCAL && hbytes == 1) {
 				// bytes of 16 rows per problem: low halves -> a, high halves -> b
 				uint32_t a[4], b[4];
 #pragma unroll
@@ -482,11 +644,86 @@ k_sw_ee_sys(const bt2g_sw_problem* __restrict__ probs, uint32_t nprob, const uin
 		}
 		hout = Hc[R - 1];        // the strip's bottom row at column j (== hprev when !SAMEGO)
 		fout = fprev;
-		// the bottom lane is the last reader of column j's selector: the slot now
-		// keeps both problems' last-row H for the gather below
-		if(bottom && in_group) mysel[j] = hout;
+		// end-to-end: the bottom lane is the last reader of column j's selector:
+		// the slot now keeps both problems' last-row H for the gather below
+		if(!LOCAL && bottom && in_group) mysel[j] = hout;
 	}
 #endif
+	if(LOCAL) {
+		__syncthreads();                  // every lane's candidates are counted
+		if(!bottom || !in_group) return;
+		// SwAligner::align local outcome per problem: the u8 fill's column scan
+		// (saturation, early bail colstop_, lastsolcol_), the i16 fill's when
+		// the u8 one saturates (aligner_swsse_loc_u8.cpp:1278-1336,
+		// aligner_swsse_loc_i16.cpp:1296-1367, aligner_sw.cpp:570-605), as k_sw_fill
+#pragma unroll
+		for(int x = 0; x < 2; x++) {
+			if(!h[x].live) continue;
+			const int64_t minsc = h[x].minsc, match = C.match, bs = bias[x];
+			const uint32_t ncol = h[x].ncol;
+			int flag = 0;
+			int64_t best = 0, colstop = ncol, lastsol = 0;
+			auto pass = [&](bool u8) {
+				int64_t vmax = 0;
+				bool sat = false;
+				colstop = ncol;
+				lastsol = 0;
+				for(uint32_t j = 0; j < ncol; j++) {
+					const int64_t c = (int64_t)(((u8 ? mysel[j] : mycm[j]) >> (16 * x)) & 0xffffu);
+					vmax = c > vmax ? c : vmax;
+					if(u8 && c + bs >= 255) { sat = true; break; }
+					if(c < minsc) {
+						if(c + (int64_t)(ncol - j - 1u) * match < minsc) { colstop = j + 1; break; }
+					} else {
+						lastsol = j;
+					}
+				}
+				if(u8) {
+					if(sat || vmax + bs >= 255) { flag = -2; best = INT64_MIN; }
+					else if(vmax == 0 || vmax < minsc) { flag = -1; best = vmax; }
+					else { flag = 0; best = vmax; }
+				} else {
+					if(vmax == 0) { flag = -1; best = INT64_MIN; }       // native -32768
+					else if(vmax < minsc) { flag = -1; best = vmax; }
+					else { flag = 0; best = vmax; }
+				}
+			};
+			bt2g_sw_result out;
+			out.u8succ = out.i16succ = 0;
+			bool wide = !enable8;
+			if(enable8) {
+				pass(true);
+				if(flag == -2) wide = true;
+				else out.u8succ = flag == 0;
+			}
+			if(wide) {
+				pass(false);
+				out.i16succ = flag == 0;
+			}
+			out.flag = flag;
+			out.colstop = (int32_t)colstop;
+			out.lastsolcol = (int32_t)lastsol;
+			// gather only columns <= lastsolcol_; on overflow the count stays and the
+			// caller reports it (the stored subset is not the reference's)
+			uint32_t nc = lcnt[2u * g + x];
+			if(nc <= cap && lmaxc[2u * g + x] > (uint32_t)lastsol) {
+				bt2g_sw_cand* cl = cands + (size_t)h[x].pi * cap;
+				uint32_t kk = 0;
+				for(uint32_t i = 0; i < nc; i++) {
+					const bt2g_sw_cand c = cl[i];
+					if(c.col <= (int32_t)lastsol) cl[kk++] = c;
+				}
+				nc = kk;
+			}
+			const bool fail = best == INT64_MIN || best < minsc;
+			out.best = best == INT64_MIN ? INT32_MIN : (int32_t)best;
+			if(fail) nc = 0;
+			out.ncand = (int32_t)nc;
+			out.aligned = (!fail && nc > 0) ? 1 : 0;
+			res[h[x].pi] = out;
+		}
+		return;
+	}
 	if(!bottom || !in_group) return;
 	// last-row maximum and end-to-end candidates in column order
 	// (aligner_swsse_ee_u8.cpp:1096-1100, 1176-1208)
@@ -531,27 +768,34 @@ k_sw_ee_sys(const bt2g_sw_problem* __restrict__ probs, uint32_t nprob, const uin
 	}
 }
 
-// All problems, u8 and i16 fills together (no partition needed).
-void launch_sw_ee_packed(const bt2g_sw_problem* probs, uint32_t nprob, const uint8_t* reads, const uint8_t* quals,
-                         uint32_t stride, const uint32_t* lens, const uint8_t* windows, const uint8_t* ref_codes,
-                         const uint64_t* ref_starts, const SwConst& C, int enable8, uint32_t cap, uint32_t max_cols,
-                         bt2g_sw_result* res, bt2g_sw_cand* cands, uint8_t* plane, uint64_t hslot, int hbytes,
-                         hipStream_t st) {
+// All problems, u8 and i16 fills together (no partition needed); local: the
+// u8 and i16 local fills in one pass.
+void launch_sw_packed(bool local, const bt2g_sw_problem* probs, uint32_t nprob, const uint8_t* reads,
+                      const uint8_t* quals, uint32_t stride, const uint32_t* lens, const uint8_t* windows,
+                      const uint8_t* ref_codes, const uint64_t* ref_starts, const SwConst& C, int enable8,
+                      uint32_t cap, uint32_t max_cols, bt2g_sw_result* res, bt2g_sw_cand* cands, uint8_t* plane,
+                      uint64_t hslot, int hbytes, hipStream_t st) {
 	if(nprob == 0) return;
 	const uint32_t S = (stride + 15u) / 16u;     // <= 64 (stride <= BT2G_MAX_READ_LEN)
 	const uint32_t per_wave = 2u * (64u / S);
 	const uint32_t ldsw = (max_cols + 1u) | 1u;   // >= ncol+1 (column pairs); odd: groups hit different banks
 	const dim3 grid((nprob + per_wave - 1) / per_wave), block(64);
-	const size_t lds = (per_wave / 2) * ldsw * sizeof(uint32_t);
-#define BT2G_SYS(SG, STO)                                                                                     \
-	hipLaunchKernelGGL((k_sw_ee_sys<SG, STO>), grid, block, lds, st, probs, nprob, reads, quals, stride, lens, \
+	const size_t lds = (per_wave / 2) * sw_packed_group_words(max_cols, local) * sizeof(uint32_t);
+#define BT2G_SYS(LO, SG, STO)                                                                                 \
+	hipLaunchKernelGGL((k_sw_sys<LO, SG, STO>), grid, block, lds, st, probs, nprob, reads, quals, stride, lens, \
 	                   windows, ref_codes, ref_starts, C, enable8, cap, max_cols, S, ldsw, res, cands, plane, hslot, \
 	                   hbytes)
 	const bool samego = C.rdgo == C.rfgo;
-	if(plane) {
-		if(samego) BT2G_SYS(true, true); else BT2G_SYS(false, true);
+	if(local) {
+		if(plane) {
+			if(samego) BT2G_SYS(true, true, true); else BT2G_SYS(true, false, true);
+		} else {
+			if(samego) BT2G_SYS(true, true, false); else BT2G_SYS(true, false, false);
+		}
+	} else if(plane) {
+		if(samego) BT2G_SYS(false, true, true); else BT2G_SYS(false, false, true);
 	} else {
-		if(samego) BT2G_SYS(true, false); else BT2G_SYS(false, false);
+		if(samego) BT2G_SYS(false, true, false); else BT2G_SYS(false, false, false);
 	}
 #undef BT2G_SYS
 }

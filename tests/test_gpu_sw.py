@@ -155,3 +155,52 @@ def test_sw_packed_vs_per_lane(eng, gaps):
     assert np.array_equal(c_p, c_g)
     assert 0 < res_p["aligned"].sum() < n
     assert (res_p["i16succ"] == 1).sum() > 0 and (res_p["u8succ"] == 1).sum() > 0
+
+
+@pytest.mark.parametrize("gaps", ["default", "rdg5,3_rfg4,2"])
+def test_sw_packed_vs_per_lane_local(eng, gaps):
+    """The packed local fill (u8 and i16 local fills in one pass, column
+    maxima for both padding-row layouts, block-wise candidate gather) against
+    the one-problem-per-lane local fills on ragged problems: read lengths
+    1..200 (every nrow mod 16, so both u8-only padding cases), widths 1..300,
+    Ns, windows off both reference ends, low and high minsc (u8 saturation and
+    not)."""
+    import bt2g
+    idx = get_index("lambda")
+    gen = idx.ref_codes[0]
+    rng = np.random.default_rng(6)
+    n = 600
+    lens = rng.integers(1, 201, n).astype(np.uint32)
+    lens[:20] = np.arange(1, 21) + 140
+    stride = 200
+    codes = np.full((n, stride), 4, np.uint8)
+    quals = np.full((n, stride), 73, np.uint8)
+    pos = rng.integers(-50, len(gen) + 50, n)
+    fw = rng.random(n) < 0.5
+    for i in range(n):
+        L = int(lens[i])
+        o = np.arange(pos[i], pos[i] + L)
+        c = np.where((o >= 0) & (o < len(gen)), gen[np.clip(o, 0, len(gen) - 1)], 4)
+        m = rng.random(L) < 0.03
+        c[m] = rng.integers(0, 5, m.sum())
+        if not fw[i]:
+            c = np.where(c > 3, 4, 3 - c)[::-1]
+        codes[i, :L] = c
+        quals[i, :L] = rng.integers(33, 75, L)
+    probs = np.zeros(n, bt2g.SWPROB_DTYPE)
+    probs["read"] = np.arange(n)
+    probs["fw"] = fw
+    probs["ncol"] = np.clip(lens.astype(np.int64) + rng.integers(-20, 100, n), 1, 300)
+    probs["refl"] = pos - rng.integers(0, 40, n)
+    probs["win_off"] = -1
+    probs["minsc"] = np.where(rng.random(n) < 0.3, 10, (20 + 8 * np.log(np.maximum(lens, 2))).astype(np.int64))
+    sc = bt2g.scoring(True)
+    if gaps != "default":
+        sc.rfg_const, sc.rfg_lin = 4, 2
+    res_p, c_p, _ = eng.sw_align(codes, quals, lens, probs, cap=8192, sc=sc, local=True)
+    res_g, c_g, _ = eng.sw_align(codes, quals, lens, probs, cap=8192, want_mat=True, sc=sc, local=True)
+    for i in range(n):
+        assert tuple(res_p[i]) == tuple(res_g[i]), (i, res_p[i], res_g[i])
+    assert np.array_equal(c_p, c_g)
+    assert 0 < res_p["aligned"].sum() < n
+    assert (res_p["i16succ"] == 1).sum() > 0 and (res_p["u8succ"] == 1).sum() > 0
