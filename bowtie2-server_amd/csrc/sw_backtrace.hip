@@ -491,18 +491,33 @@ k_sw_bt(BtArgs A) {
 		}
 		return w;
 	};
+	uint32_t ndone = 0, wq0 = 0, wq1 = 0, wq2 = 0, wq3 = 0;   // walked candidates: row << 16 | col
 	for(uint32_t ci = 0; ci < ncand; ci++) {
 		if(nal >= (int32_t)A.maxaln) break;
 		const bt2g_sw_cand cd = cl[ci];
 		int8_t fate;
 		BTC(4);
+		// Local mode: most candidates (~95 % at 150 bp) lie within SQ of a walked
+		// one.  The squares of the first and the last three walked candidates
+		// are tested in registers first (exact: a hit is a dominated candidate);
+		// without a fates array the dominance test also runs before the start
+		// mark (either filter only skips the candidate; fates alone tell them apart).
+		const uint32_t cr = (uint32_t)cd.row, cc = (uint32_t)cd.col;
+		auto near = [&](uint32_t w) {
+			const uint32_t wr = w >> 16, wc = w & 0xffffu;
+			return (wr > cr ? wr - cr : cr - wr) <= SQ && (wc > cc ? wc - cc : cc - wc) <= SQ;
+		};
+		const bool dom_reg = local && ndone > 0 && (near(wq0) || near(wq1) || near(wq2) || near(wq3));
+		const bool dom_first = local && !A.fates && (dom_reg || (BTC(5), dom_test(cr, cc)));
 		if(cd.score < P.minsc) {
 			fate = 5;                                   // BT_CAND_FATE_FILT_SCORE
-		} else if((local || (uint32_t)cd.row + (uint32_t)gb < nrow) && marked((uint32_t)cd.row, (uint32_t)cd.col)) {
+		} else if(dom_first) {
+			fate = 4;                                   // BT_CAND_FATE_FILT_DOMINATED
+		} else if((local || cr + (uint32_t)gb < nrow) && marked(cr, cc)) {
 			// (end-to-end starts in the bottom barrier rows are never marked: see walk)
 			fate = 3;                                   // BT_CAND_FATE_FILT_START
 		} else {
-			if(local && (BTC(5), dom_test((uint32_t)cd.row, (uint32_t)cd.col))) {
+			if(local && A.fates && (dom_reg || (BTC(5), dom_test(cr, cc)))) {
 				fate = 4;                               // BT_CAND_FATE_FILT_DOMINATED
 			} else {
 				// the first walk writes its edits as it goes (it usually succeeds);
@@ -513,7 +528,14 @@ k_sw_bt(BtArgs A) {
 				Walk w = walk(row0, col0, cd.score, true, first, ed);
 				if(w.ok && !first) { BTC(6); (void)walk(row0, col0, cd.score, false, true, ed); }
 				first = false;
-				if(local) dom_add((uint32_t)cd.row, (uint32_t)cd.col);
+				if(local) {
+					dom_add(cr, cc);
+					// register copies: the first walked candidate stays, the others rotate
+					const uint32_t w = (cr << 16) | cc;
+					if(ndone == 0) wq0 = wq1 = wq2 = wq3 = w;
+					else { wq3 = wq2; wq2 = wq1; wq1 = w; }
+					ndone++;
+				}
 				if(w.ok) {
 					const uint32_t trimBeg = w.row, trimEnd = nrow - row0 - 1;
 					// res.reverse(), AlnRes::setShape trim shift, invertEdits for !fw
