@@ -233,6 +233,7 @@ class Pipeline:
         self.alns = torch.empty((self.max_probs, self.maxaln, 10), dtype=torch.int32, device=self.dev)
         self.edits = torch.empty((self.max_probs, self.maxaln, self.maxedit, 2), dtype=torch.int32, device=self.dev)
         self.stats = {}
+        self._timing = None
         if pol.paired:
             # mate search (SwDriver::extendSeedsPaired, aligner_sw_driver.cpp:1975-2100):
             # its own context on the same index, reserved for the mate rectangles
@@ -256,8 +257,19 @@ class Pipeline:
     def _p(self, t):
         return C.c_void_p(t.data_ptr())
 
+    def _mark(self, name):
+        """Phase boundary: the stream is drained here (measured faster than letting
+        the host run ahead into the next phase's glue: 196 vs 268-303 ms per paired
+        step); BT2G_BENCH_TIMING=1 also logs the phase times."""
+        self.torch.cuda.synchronize()
+        if self._timing is not None:
+            self._timing.append((name, time.perf_counter()))
+
     def step(self, keep=False):
         torch, L, bt2g = self.torch, self.L, self.bt2g
+        self._timing = [("start", time.perf_counter())] if os.environ.get("BT2G_BENCH_TIMING") else None
+        if self._timing is not None:
+            torch.cuda.synchronize()
         S = C.c_void_p(torch.cuda.current_stream().cuda_stream)
         h, n, stride = self.eng.h, self.n, self.len
         chk = bt2g._chk
@@ -270,6 +282,7 @@ class Pipeline:
                                     self._p(self.minsc), C.byref(self.sc), self._p(self.sweep), self.mm_cap,
                                     self._p(self.mm_hits), self._p(self.mm_cnt), self._p(self.mm_ops),
                                     self._p(self.mm_loads), S))
+        self._mark("sweep+1mm")
         sw = self.sweep.to(torch.int64) & u32
         exact = torch.minimum(sw[:, 0], sw[:, 1]) == 0
         # 3. seed round 0 for reads without an exact end-to-end hit
@@ -280,6 +293,7 @@ class Pipeline:
         chk(L.bt2g_seed_search_dev(h, self._p(sreads), stride, self._p(self.lens), m, pol.seedlen, pol.interval, 0,
                                    self.maxseeds, self._p(self.seeds), self._p(self.nseeds), self._p(self.sd_ops),
                                    self._p(self.sd_loads), S))
+        self._mark("seeds")
         # 4. every read's hit rows (exact, 1-mm, seeds) -> one list, contiguous per read
         self.inv.fill_(-1)
         self.inv[sel] = torch.arange(m, dtype=torch.int32, device=self.dev)
@@ -291,8 +305,10 @@ class Pipeline:
                                           P(self.rows), P(self.meta), P(self.read_base), P(self.read_cnt),
                                           P(self.counters), self.row_cap, S))
         nrows = int(self.counters[0])
+        self._mark("rows")
         # 5. SA rows -> joined-text offsets
         chk(L.bt2g_get_offset_dev(h, P(self.rows), nrows, P(self.offs), P(self.loads_off), S))
+        self._mark("offsets")
         # 6. joinedToTextOff + straddle filter + rectangles, <= 2 per read (device)
         chk(L.bt2g_bench_frame_dev(n, P(self.lens), P(self.offs), P(self.meta), P(self.read_base),
                                    P(self.read_cnt), P(self.fr[0]), P(self.fr[1]), P(self.fr[2]), P(self.fr[3]),
@@ -300,11 +316,13 @@ class Pipeline:
                                    P(self.counters[1:]), self.max_probs, S))
         npb = min(int(self.counters[1]), self.max_probs)
         probs = self.probs[:npb]
+        self._mark("frame")
         # 7. fill + candidates + the nextAlignment loop (backtraces)
         chk(L.bt2g_sw_align_bt_dev(h, P(self.reads), P(self.quals), stride, P(self.lens),
                                    P(probs), npb, None, P(self.rects), C.byref(self.sc), 1, self.sw_cap,
                                    P(self.res), P(self.cands), self.maxaln, self.maxedit, P(self.naln),
                                    P(self.alns), P(self.edits), None, S))
+        self._mark("sw")
         # end-to-end: an exact end-to-end hit is the alignment (EXTEND_PERFECT_SCORE);
         # local: every read's hits, the exact ones included, go through the DP
         aligned = torch.zeros_like(exact) if pol.local else exact.clone()
@@ -316,7 +334,11 @@ class Pipeline:
                              nrows=nrows, m=m, ns=ns, loads_off=self.loads_off[:nrows],
                              read_base=self.read_base, read_cnt=self.read_cnt)
         if pol.paired:
-            return self.mates(probs, npb, aligned, keep, S)
+            aligned = self.mates(probs, npb, aligned, keep, S)
+        self._mark("end")
+        if self._timing is not None:
+            t = self._timing
+            log("[timing] " + ", ".join(f"{t[i][0]} {1e3 * (t[i][1] - t[i - 1][1]):.1f}" for i in range(1, len(t))))
         return aligned
 
     def mates(self, probs, npb, aligned, keep, S):
@@ -349,6 +371,7 @@ class Pipeline:
         fin[:, 6] = 1                                                                        # mate search
         fin[:, 7] = a1.to(torch.int32)
         fin[:, 8] = self.len
+        self._mark("anchors")
         chk(L.bt2g_frame_dev(self.eng2.h, P(fin), na, P(self.lens), C.byref(self.sc), C.byref(self.pe), MAXHALF,
                              1, P(self.mprobs), P(self.mrects), P(self.mok), S))
         kept = torch.nonzero(self.mok[:na]).squeeze(1)
@@ -359,6 +382,7 @@ class Pipeline:
             raise RuntimeError("mate rectangle wider than the reservation")
         found = torch.zeros(npairs, dtype=torch.bool, device=dev)
         pair_of = use.index_select(0, kept)
+        self._mark("mate_frame")
         for c0 in range(0, nm, self.mate_chunk):
             c1 = min(nm, c0 + self.mate_chunk)
             chk(L.bt2g_sw_align_bt_dev(self.eng2.h, P(self.reads), P(self.quals), self.len, P(self.lens),
@@ -366,6 +390,7 @@ class Pipeline:
                                        P(self.mres), P(self.mcands), self.maxaln, self.maxedit, P(self.mnaln),
                                        P(self.malns), P(self.medits), None, S))
             found[pair_of[c0:c1][self.mnaln[:c1 - c0] > 0]] = True
+        self._mark("mate_dps")
         if keep:
             self.last.update(m_anchors=na, m_dps=nm, m_found=int(found.sum()), m_probs=mp, m_rects=mr,
                              m_pairs=pair_of, m_fin=fin.index_select(0, kept))
