@@ -261,7 +261,7 @@ class Pipeline:
         """Phase boundary: the stream is drained here (measured faster than letting
         the host run ahead into the next phase's glue: 196 vs 268-303 ms per paired
         step); BT2G_BENCH_TIMING=1 also logs the phase times."""
-        self.torch.cuda.synchronize()
+        self.torch.cuda.current_stream().synchronize()
         if self._timing is not None:
             self._timing.append((name, time.perf_counter()))
 
@@ -821,7 +821,7 @@ def main():
     parity = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         threads = max(1, min(args.cpu_threads, os.cpu_count() or 1))
-        sample = min(args.cpu_sample, args.reads)
+        sample = min(args.cpu_sample, pipe.npairs if args.mode == "paired" else pipe.n)
         try:
             dt, ex_ref, sw_ref, pr, mate = cpu_baseline(idx, reads_np, quals_np, pipe, sample, threads)
             paired = args.mode == "paired"
