@@ -12,7 +12,13 @@
 // --------------------------------------------------------------------------
 // exactSweep (aligner_seed.cpp:750-968): one lane = one (read, strand).
 // --------------------------------------------------------------------------
-__global__ void __launch_bounds__(256)
+#ifndef BT2G_SWEEP_WAVES
+#define BT2G_SWEEP_WAVES 7      // 8 (63 VGPRs, no spills) measured 4.47 vs 4.33 ms
+#endif
+#ifndef BT2G_SEED_WAVES
+#define BT2G_SEED_WAVES 4
+#endif
+__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(BT2G_SWEEP_WAVES)))
 k_exact_sweep(DevEbwt e, const uint8_t* __restrict__ reads, uint32_t stride, const uint32_t* __restrict__ lens,
               uint32_t n, uint32_t mine_max, int nofw, int norc, uint32_t* __restrict__ out) {
 	// lanes 2r, 2r+1: the two strands of read r (strand-homogeneous waves
@@ -117,7 +123,7 @@ k_exact_sweep(DevEbwt e, const uint8_t* __restrict__ reads, uint32_t stride, con
 // 214-358) + searchSeedBi for SEED_TYPE_EXACT (80-122, 1633-1714, 1854-2033).
 // One lane = one (read, strand, seed offset).
 // --------------------------------------------------------------------------
-__global__ void __launch_bounds__(256)
+__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(BT2G_SEED_WAVES)))
 k_seed_search(DevEbwt F, DevEbwt B, const uint8_t* __restrict__ reads, uint32_t stride,
               const uint32_t* __restrict__ lens, uint32_t n, uint32_t seedlen, uint32_t interval,
               uint32_t offset, uint32_t maxseeds, uint32_t* __restrict__ out, int32_t* __restrict__ nseeds,
