@@ -21,7 +21,7 @@ extern "C" int bt_emul_run(int kind, const bt2g_sw_problem* probs, uint32_t npro
 	BtArgs a{};
 	a.probs = probs; a.nprob = nprob; a.reads = reads; a.quals = quals; a.stride = stride; a.lens = lens;
 	a.windows = windows; a.ref_codes = nullptr; a.ref_starts = nullptr; a.rects = rects;
-	a.res = res; a.cands = cands; a.cap = cap; a.plane = plane; a.slot = slot; a.cstride = cstride; a.pcols = maxcol; a.use_mask = !plane_top && cstride <= 256u;
+	a.res = res; a.cands = cands; a.cap = cap; a.plane = plane; a.slot = slot; a.cstride = cstride; a.pcols = maxcol; a.use_mask = plane_top != 1 && cstride <= 256u;
 	a.plane_top = plane_top;
 	a.mwords = sw_bt_tcols(maxcol); a.mrows = sw_bt_trows(maxrow); a.mslot = sw_bt_mslot(maxrow, maxcol, local != 0);
 	a.mdom = local ? sw_bt_mslot(maxrow, maxcol, false) : 0u;

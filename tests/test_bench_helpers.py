@@ -1,0 +1,53 @@
+"""CPU checks of bench.py's host helpers: the paired read generator's
+geometry (fragments of 200..500, --fr mates) and the mate
+rectangle width budget (gap_budget, checked against the oracle's framer,
+itself pinned to the reference's rectangles by test_oracle_golden.py)."""
+import numpy as np
+
+import bench
+from test_oracle_golden import orc  # noqa: F401  (session oracle fixture)
+
+
+def test_gap_budget_matches_framer(orc):  # noqa: F811
+    for minsc in (0, -1, -8, -9, -11, -50, -90, -91, -200, -600):
+        # seed-extension rectangle with a huge maxhalf: corel = max(read gaps, ref gaps)
+        ok, fw, refl, ncol, triml, corel, corer = orc.frame(0, 10_000, 150, 100_000, minsc, maxhalf=10_000)
+        assert ok and corel == bench.gap_budget(minsc, 150), minsc
+
+
+def test_make_pairs_geometry():
+    parts, _ = bench.make_genome(0.5)
+    n, L = 400, 150
+    reads, quals = bench.make_pairs(parts, n, L, seed=3)
+    assert reads.shape == (2 * n, L) and quals.shape == (2 * n, L)
+    assert reads.max() <= 4 and quals.min() >= 33 + 2 and quals.max() <= 33 + 40
+    g = np.concatenate(parts)
+    # locate every mate exactly (ignoring mutated reads) and check the --fr fragment
+    # a cheaper check: most mate-1 / mate-2 pairs map within 500 bp of each other on opposite strands
+    def find(r):
+        rc = np.where(r > 3, 4, 3 - r)[::-1]
+        for strand, s in ((True, r), (False, rc)):
+            key = s[:24].tobytes()
+            hits = lookup_pos.get(key)
+            if hits is not None:
+                return strand, hits
+        return None
+    lookup_pos, seen = {}, set()
+    for i in range(len(g) - 24):
+        key = g[i:i + 24].tobytes()
+        if key in lookup_pos:
+            seen.add(key)                                # repeated 24-mer: ambiguous, skipped
+        lookup_pos[key] = i
+    for key in seen:
+        del lookup_pos[key]
+    good = 0
+    for i in range(n):
+        a, b = find(reads[i]), find(reads[n + i])
+        if a is None or b is None:
+            continue
+        (sa, pa), (sb, pb) = a, b
+        assert sa != sb                                  # --fr: opposite strands
+        frag = max(pa, pb) + L - min(pa, pb)
+        assert 150 <= frag <= 500 + 2, frag
+        good += 1
+    assert good > n // 2

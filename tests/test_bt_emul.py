@@ -3,7 +3,9 @@ compiled for the host by tests/cpu_emul (stub HIP header, one kernel lane at a
 time), against the reference's alignments (sw_bt_* golden fixtures).  The
 fills are the oracle's (pinned to the reference by test_oracle_golden.py),
 laid out as the GPU fills leave them: the systolic fill's u8 score plane
-(kind 0) and the generic fill's H,E,F int16 triples (kind 2).  CPU only:
+(kind 0), the one-problem-per-lane fills' top-aligned u16 plane (kind 1) and
+the systolic local fill's u16 plane (kind 2: rows padded to a multiple of 16
+at the stack bottom, only blocks holding a non-zero cell written).  CPU only:
 catches indexing faults and logic errors before a GPU run."""
 import ctypes as C
 import os
@@ -53,7 +55,7 @@ def lib():
 
 
 @pytest.mark.parametrize("src,kind", [("rand_ee", 0), ("log_ee", 0), ("rand_ee", 1), ("rand_loc", 1),
-                                      ("log_loc", 1)])
+                                      ("log_loc", 1), ("rand_loc", 2), ("log_loc", 2)])
 def test_bt_kernel_source_on_cpu(lib, src, kind):
     import bt2g
     from oracle.oracle import Oracle
@@ -73,6 +75,7 @@ def test_bt_kernel_source_on_cpu(lib, src, kind):
     maxcol = int(probs["ncol"].max())
     maxrow = int(g["lens"].max())
     es = 1 if kind == 0 else 2
+    plane_top = {0: 0, 1: 1, 2: 2}[kind]
     slot = S16 * maxcol * es + ((maxcol * 2 + 15) & ~15)   # plane + per-column block masks
     plane = np.zeros(slot * n, np.uint8)
     keep = np.ones(n, bool)
@@ -81,6 +84,22 @@ def test_bt_kernel_source_on_cpu(lib, src, kind):
         res[p] = (o[0], max(o[1], -2**31), o[2], o[3], o[4], o[5], o[6], 0)
         cands[p, :len(c)] = [tuple(x) for x in c]
         L, ncol = len(rd), len(rf) - 1
+        if kind == 2:
+            # systolic local layout: score domain, padded rows end at the stack
+            # bottom, blocks without a non-zero cell unwritten (garbage) + masks
+            top = S16 - ((L + 15) // 16) * 16
+            stack = np.zeros((S16, maxcol), np.uint16)
+            stack[top:top + L, :ncol] = ((m[:, :, 0].astype(np.int64) + (0 if o[2] else 0x8000)) & 0xffff)
+            blocks = stack.reshape(S16 // 16, 16, maxcol)
+            live = blocks.max(1) > 0
+            if S16 > 256:
+                live[:] = True
+            blocks = np.where(live[:, None, :], blocks, 0x5a5a).astype(np.uint16)
+            plane[p * slot:p * slot + S16 * maxcol * 2] = blocks.transpose(0, 2, 1).ravel().view(np.uint8)
+            if S16 <= 256:
+                masks = (live.astype(np.uint32) << np.arange(S16 // 16)[:, None].astype(np.uint32)).sum(0)
+                plane[p * slot + S16 * maxcol * 2:p * slot + S16 * maxcol * 2 + 2 * maxcol] = \
+                    masks.astype(np.uint16).view(np.uint8)
         if kind == 1:
             # one-problem-per-lane fill layout: u16 (score + 0x8000 for i16
             # fills), rows top-aligned, all blocks written, no masks
@@ -115,9 +134,9 @@ def test_bt_kernel_source_on_cpu(lib, src, kind):
     edits = np.zeros((n, maxaln, maxedit), bt2g.EDIT_DTYPE)
     fates = np.zeros((n, cap), np.int8)
     lens = np.ascontiguousarray(g["lens"], np.uint32)
-    lib.bt_emul_run(C.c_int(kind), _p(probs), C.c_uint32(n), _p(g["reads"]), _p(g["quals"]), C.c_uint32(stride),
+    lib.bt_emul_run(C.c_int(min(kind, 1)), _p(probs), C.c_uint32(n), _p(g["reads"]), _p(g["quals"]), C.c_uint32(stride),
                     _p(lens), _p(g["rf"]), _p(rects), _p(res), _p(cands), C.c_uint32(cap), _p(plane),
-                    C.c_uint64(slot), C.c_uint32(S16), C.c_int(int(kind == 1)), C.c_uint32(maxrow), C.c_uint32(maxcol),
+                    C.c_uint64(slot), C.c_uint32(S16), C.c_int(plane_top), C.c_uint32(maxrow), C.c_uint32(maxcol),
                     C.byref(swconst(local)), C.c_int(int(local)), C.c_double(0.0), C.c_double(0.15),
                     C.c_uint32(maxaln), C.c_uint32(maxedit), _p(naln), _p(alns), _p(edits), _p(fates))
     nal = 0
