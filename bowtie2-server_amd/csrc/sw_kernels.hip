@@ -402,12 +402,23 @@ k_sort_small(const bt2g_sw_result* __restrict__ res, bt2g_sw_cand* __restrict__ 
 	if(lane < n) c[lane] = cand_of(key);
 }
 
-// Lists longer than 64: one workgroup per queued problem, bitonic sort in LDS
-// (grid-stride over the queue, whose length is only known on the device).
+// Lists longer than 64: one workgroup per queued problem (grid-stride over
+// the queue, whose length is only known on the device).  Lists of >= 128 whose
+// scores span <= SORT_BUCKETS values (local mode: ~1200 candidates over a few
+// hundred scores) are counting-sorted by score (histogram, scan, scatter into
+// buckets, then each bucket -- a few candidates -- insertion-sorted by the full
+// key by one thread); others go through an LDS bitonic network.
+constexpr uint32_t SORT_BUCKETS = 2048;
 __global__ void __launch_bounds__(256)
-k_sort_big(const bt2g_sw_result* __restrict__ res, bt2g_sw_cand* __restrict__ cands, uint32_t cap,
-           const uint32_t* __restrict__ big, const uint32_t* __restrict__ nbig) {
+k_sort_big(const bt2g_sw_result* __restrict__ res, bt2g_sw_cand* __restrict__ cands, uint32_t cap, uint32_t P2max,
+           int counting, const uint32_t* __restrict__ big, const uint32_t* __restrict__ nbig) {
 	extern __shared__ __attribute__((aligned(16))) unsigned long long keys[];
+	unsigned long long* tmp = keys + P2max;
+	uint32_t* start = (uint32_t*)(tmp + P2max);
+	uint32_t* cur = start + SORT_BUCKETS;
+	__shared__ uint32_t part[256];
+	__shared__ int smin, smax;
+	const uint32_t tid = threadIdx.x;
 	const uint32_t nq = *nbig;
 	for(uint32_t qi = blockIdx.x; qi < nq; qi += gridDim.x) {
 		const uint32_t pi = big[qi];
@@ -416,22 +427,82 @@ k_sort_big(const bt2g_sw_result* __restrict__ res, bt2g_sw_cand* __restrict__ ca
 		uint32_t P2 = 1;
 		while(P2 < n) P2 <<= 1;
 		bt2g_sw_cand* c = cands + (size_t)pi * cap;
-		for(uint32_t i = threadIdx.x; i < P2; i += blockDim.x) keys[i] = i < n ? cand_key(c[i]) : ~0ull;
+		if(tid == 0) { smin = INT32_MAX; smax = INT32_MIN; }
 		__syncthreads();
-		for(uint32_t size = 2; size <= P2; size <<= 1) {
-			for(uint32_t stride = size >> 1; stride > 0; stride >>= 1) {
-				for(uint32_t i = threadIdx.x; i < P2; i += blockDim.x) {
-					const uint32_t jx = i ^ stride;
-					if(jx > i) {
-						const bool up = (i & size) == 0;
-						const unsigned long long a = keys[i], b = keys[jx];
-						if((a > b) == up) { keys[i] = b; keys[jx] = a; }
-					}
-				}
-				__syncthreads();
+		int lmin = INT32_MAX, lmax = INT32_MIN;
+		for(uint32_t i = tid; i < P2; i += blockDim.x) {
+			if(i < n) {
+				const bt2g_sw_cand x = c[i];
+				keys[i] = cand_key(x);
+				lmin = x.score < lmin ? x.score : lmin;
+				lmax = x.score > lmax ? x.score : lmax;
+			} else {
+				keys[i] = ~0ull;
 			}
 		}
-		for(uint32_t i = threadIdx.x; i < n; i += blockDim.x) c[i] = cand_of(keys[i]);
+		if(lmin <= lmax) { atomicMin(&smin, lmin); atomicMax(&smax, lmax); }
+		__syncthreads();
+		const int hi = smax;
+		const uint32_t range = (uint32_t)((int64_t)smax - (int64_t)smin + 1);
+		if(counting && n >= 128u && range <= SORT_BUCKETS) {
+			for(uint32_t b = tid; b < range; b += blockDim.x) cur[b] = 0u;
+			__syncthreads();
+			for(uint32_t i = tid; i < n; i += blockDim.x)
+				atomicAdd(&cur[(uint32_t)(hi - cand_of(keys[i]).score)], 1u);
+			__syncthreads();
+			// exclusive scan of the bucket counts (chunk per thread + block scan)
+			const uint32_t chunk = (range + 255u) / 256u, b0 = tid * chunk;
+			const uint32_t b1 = b0 + chunk < range ? b0 + chunk : range;
+			uint32_t sum = 0;
+			for(uint32_t b = b0; b < b1; b++) sum += cur[b];
+			part[tid] = sum;
+			__syncthreads();
+			for(uint32_t off = 1; off < 256u; off <<= 1) {
+				const uint32_t v = tid >= off ? part[tid - off] : 0u;
+				__syncthreads();
+				part[tid] += v;
+				__syncthreads();
+			}
+			uint32_t run = tid ? part[tid - 1] : 0u;
+			for(uint32_t b = b0; b < b1; b++) {
+				const uint32_t h = cur[b];
+				start[b] = run;
+				cur[b] = run;
+				run += h;
+			}
+			__syncthreads();
+			for(uint32_t i = tid; i < n; i += blockDim.x) {
+				const unsigned long long k = keys[i];
+				tmp[atomicAdd(&cur[(uint32_t)(hi - cand_of(k).score)], 1u)] = k;
+			}
+			__syncthreads();
+			for(uint32_t b = tid; b < range; b += blockDim.x) {
+				const uint32_t s0 = start[b], e0 = b + 1u < range ? start[b + 1u] : n;
+				for(uint32_t i = s0 + 1u; i < e0; i++) {
+					const unsigned long long x = tmp[i];
+					uint32_t j = i;
+					while(j > s0 && tmp[j - 1u] > x) { tmp[j] = tmp[j - 1u]; j--; }
+					tmp[j] = x;
+				}
+			}
+			__syncthreads();
+			for(uint32_t i = tid; i < n; i += blockDim.x) c[i] = cand_of(tmp[i]);
+		} else {
+			for(uint32_t size = 2; size <= P2; size <<= 1) {
+				for(uint32_t stride = size >> 1; stride > 0; stride >>= 1) {
+					for(uint32_t i = tid; i < P2; i += blockDim.x) {
+						const uint32_t jx = i ^ stride;
+						if(jx > i) {
+							const bool up = (i & size) == 0;
+							const unsigned long long a = keys[i], b = keys[jx];
+							if((a > b) == up) { keys[i] = b; keys[jx] = a; }
+						}
+					}
+					__syncthreads();
+				}
+			}
+			for(uint32_t i = tid; i < n; i += blockDim.x) c[i] = cand_of(keys[i]);
+		}
 		__syncthreads();
 	}
 }
@@ -478,9 +549,13 @@ void launch_sort_cands(const bt2g_sw_result* res, bt2g_sw_cand* cands, uint32_t 
 	if(cap <= 64) return;
 	uint32_t P2 = 1;
 	while(P2 < cap) P2 <<= 1;
-	// enough workgroups to fill every CU's LDS (16 KB each at cap 2048); the
+	// enough workgroups to fill every CU's LDS (48 KB each at cap 2048); the
 	// queue length is only known on the device, idle groups exit at once
 	const uint32_t grid = nprob < 4096u ? nprob : 4096u;
-	hipLaunchKernelGGL(k_sort_big, dim3(grid), dim3(256), P2 * sizeof(unsigned long long), st, res, cands, cap, big,
-	                   nbig);
+	// counting sort needs the keys twice plus the buckets (48 KB at cap 2048);
+	// larger caps keep the bitonic network only
+	size_t lds = 2u * P2 * sizeof(unsigned long long) + 2u * SORT_BUCKETS * sizeof(uint32_t);
+	const int counting = lds <= 65536u ? 1 : 0;
+	if(!counting) lds = P2 * sizeof(unsigned long long);
+	hipLaunchKernelGGL(k_sort_big, dim3(grid), dim3(256), lds, st, res, cands, cap, P2, counting, big, nbig);
 }
