@@ -71,6 +71,17 @@ __device__ __forceinline__ uint32_t pmax(uint32_t a, uint32_t b) {
 	                                                              __builtin_bit_cast(u16x2, b)));
 }
 
+// score-plane stores (BT2G_SW_NT_STORE: non-temporal, measured 4x slower fill: 57.8 vs 13.9 ms)
+__device__ __forceinline__ void st_plane(uint8_t* p, uint32_t x, uint32_t y, uint32_t z, uint32_t w) {
+#ifdef BT2G_SW_NT_STORE
+	typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+	u32x4 v = {x, y, z, w};
+	__builtin_nontemporal_store(v, (u32x4*)p);
+#else
+	*(uint4*)p = make_uint4(x, y, z, w);
+#endif
+}
+
 __device__ __forceinline__ int first5(int m) {
 	return (m & 1) ? 0 : (m & 2) ? 1 : (m & 4) ? 2 : (m & 8) ? 3 : 4;
 }
@@ -620,9 +631,9 @@ k_sw_sys(const bt2g_sw_problem* __restrict__ probs, uint32_t nprob, const uint8_
 					b[qd] = __builtin_amdgcn_perm(y1, y0, 0x07060302u);
 				}
 				if(s0 && h[0].row0 == 0xffu)
-					*(uint4*)(plane + (size_t)h[0].pi * hslot + cell) = make_uint4(a[0], a[1], a[2], a[3]);
+					st_plane(plane + (size_t)h[0].pi * hslot + cell, a[0], a[1], a[2], a[3]);
 				if(s1 && h[1].row0 == 0xffu)
-					*(uint4*)(plane + (size_t)h[1].pi * hslot + cell) = make_uint4(b[0], b[1], b[2], b[3]);
+					st_plane(plane + (size_t)h[1].pi * hslot + cell, b[0], b[1], b[2], b[3]);
 			} else {
 				uint32_t a[8], b[8];
 #pragma unroll
@@ -631,14 +642,14 @@ k_sw_sys(const bt2g_sw_problem* __restrict__ probs, uint32_t nprob, const uint8_
 					b[i] = __builtin_amdgcn_perm(Hc[2 * i + 1], Hc[2 * i], 0x07060302u);
 				}
 				if(s0) {
-					uint4* d = (uint4*)(plane + (size_t)h[0].pi * hslot + cell * 2u);
-					d[0] = make_uint4(a[0], a[1], a[2], a[3]);
-					d[1] = make_uint4(a[4], a[5], a[6], a[7]);
+					uint8_t* d = plane + (size_t)h[0].pi * hslot + cell * 2u;
+					st_plane(d, a[0], a[1], a[2], a[3]);
+					st_plane(d + 16, a[4], a[5], a[6], a[7]);
 				}
 				if(s1) {
-					uint4* d = (uint4*)(plane + (size_t)h[1].pi * hslot + cell * 2u);
-					d[0] = make_uint4(b[0], b[1], b[2], b[3]);
-					d[1] = make_uint4(b[4], b[5], b[6], b[7]);
+					uint8_t* d = plane + (size_t)h[1].pi * hslot + cell * 2u;
+					st_plane(d, b[0], b[1], b[2], b[3]);
+					st_plane(d + 16, b[4], b[5], b[6], b[7]);
 				}
 			}
 		}
