@@ -97,7 +97,7 @@ extern unsigned long long bt_counts[8];
 #ifndef BT2G_BT_WAVES
 #define BT2G_BT_WAVES 3
 #endif
-template <int KIND>
+template <int KIND, bool FLAT>
 __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(BT2G_BT_WAVES)))
 k_sw_bt(BtArgs A) {
 	const uint32_t p = blockIdx.x * 64u + threadIdx.x;
@@ -333,41 +333,105 @@ k_sw_bt(BtArgs A) {
 	};
 	int32_t nal = 0;
 	bool first = true;
-	// One backtrace from (row, col).  mark: set/check reportedThrough (off when
-	// replaying a successful walk to emit its edits; the path does not depend
-	// on the marks).  emit: write the edits (walk order) to ed.
+	// FLAT (local mode): the candidate loop and the walks run as ONE loop: an
+	// iteration either filters a candidate or takes one walk step, so a lane
+	// never waits for the longest walk of its wave at every candidate (nested
+	// loops reconverge at each walk's end; flat, a wave runs for the longest
+	// lane's total): 3.8x faster with local's ~1,200 candidates and 55 uneven
+	// walks per DP.  End-to-end (48 similar candidates) keeps each walk in an
+	// inner loop, whose iterations are cheaper (measured 31.5 vs 34.4 ms).
+	// A walk: one backtrace from (row0, col0); wmark: set/check reportedThrough
+	// (off when replaying a successful walk to emit its edits -- the path does
+	// not depend on the marks); wemit: write the edits (walk order) to ed.
 	struct Walk {
 		bool ok, core;
 		uint32_t row, col, ned;
 		int32_t score, ns, gaps;
 	};
-	auto walk = [&](uint32_t row, uint32_t col, int32_t cur, bool mark, bool emit, bt2g_edit* ed) -> Walk {
-		Walk w{true, false, row, col, 0u, 0, 0, 0};
-		auto push = [&](uint32_t pos, int type, int chr, int qchr) {
-			if(emit && w.ned < A.maxedit) ed[w.ned] = bt2g_edit{pos, (uint8_t)type, (uint8_t)chr, (uint8_t)qchr, 0};
-			w.ned++;
-		};
-		int st = ST_H;
+	Walk w{true, false, 0u, 0u, 0u, 0, 0, 0};
+	bool walking = false, wmark = false, wemit = false, replay = false;
+	uint32_t row = 0, col = 0, row0 = 0, col0 = 0;
+	int32_t cur = 0;
+	int st = ST_H;
+	bt2g_edit* ed = A.edits;
+	auto push = [&](uint32_t pos, int type, int chr, int qchr) {
+		if(wemit && w.ned < A.maxedit) ed[w.ned] = bt2g_edit{pos, (uint8_t)type, (uint8_t)chr, (uint8_t)qchr, 0};
+		w.ned++;
+	};
+	auto start_walk = [&](bool mark, bool emit) {
+		w = Walk{true, false, row0, col0, 0u, 0, 0, 0};
+		row = row0; col = col0; st = ST_H;
+		wmark = mark; wemit = emit;
+		walking = true;
 		BTC(0);
-		while(true) {
-			BTC(1);
+	};
+	uint32_t ndone = 0, wq0 = 0, wq1 = 0, wq2 = 0, wq3 = 0;   // walked candidates: row << 16 | col
+	uint32_t ci = 0;
+	int32_t cscore = 0;
+	while(true) {
+		if(!walking) {
+			if(ci >= ncand || nal >= (int32_t)A.maxaln) break;
+			const bt2g_sw_cand cd = cl[ci];
+			int8_t fate = 0;
+			BTC(4);
+			// Local mode: most candidates (~95 % at 150 bp) lie within SQ of a walked
+			// one.  The squares of the first and the last three walked candidates
+			// are tested in registers first (exact: a hit is a dominated candidate);
+			// without a fates array the dominance test also runs before the start
+			// mark (either filter only skips the candidate; fates alone tell them apart).
+			const uint32_t cr = (uint32_t)cd.row, cc = (uint32_t)cd.col;
+			auto near = [&](uint32_t wv) {
+				const uint32_t wr = wv >> 16, wc = wv & 0xffffu;
+				return (wr > cr ? wr - cr : cr - wr) <= SQ && (wc > cc ? wc - cc : cc - wc) <= SQ;
+			};
+			const bool dom_reg = local && ndone > 0 && (near(wq0) || near(wq1) || near(wq2) || near(wq3));
+			const bool dom_first = local && !A.fates && (dom_reg || (BTC(5), dom_test(cr, cc)));
+			if(cd.score < P.minsc) {
+				fate = 5;                                   // BT_CAND_FATE_FILT_SCORE
+			} else if(dom_first) {
+				fate = 4;                                   // BT_CAND_FATE_FILT_DOMINATED
+			} else if((local || cr + (uint32_t)gb < nrow) && marked(cr, cc)) {
+				// (end-to-end starts in the bottom barrier rows are never marked: see walk)
+				fate = 3;                                   // BT_CAND_FATE_FILT_START
+			} else if(local && A.fates && (dom_reg || (BTC(5), dom_test(cr, cc)))) {
+				fate = 4;                                   // BT_CAND_FATE_FILT_DOMINATED
+			}
+			if(fate) {
+				if(A.fates) A.fates[(size_t)p * A.cap + ci] = fate;
+				ci++;
+				continue;
+			}
+			// the first walk writes its edits as it goes (it usually succeeds);
+			// a later walk that succeeds is walked again to write them.  The
+			// candidate's score is its cell's H.
+			ed = A.edits + ((size_t)p * A.maxaln + (size_t)nal) * A.maxedit;
+			row0 = cr; col0 = cc; cur = cd.score; cscore = cd.score;
+			replay = false;
+			start_walk(true, first);
+		}
+		// ---- one walk step (FLAT), or the whole walk --------------------------
+		bool ended = false;
+		do {
+		BTC(1);
+		{
 			// end-to-end: every candidate starts in the last row and the bottom
 			// gap-barrier rows allow only diagonal moves, so walks there stay on
 			// their own diagonals and can neither meet nor be met: no marks
 			const bool bottom_bar = !local && row + (uint32_t)gb >= nrow;
-			if(mark && !bottom_bar) {
+			if(wmark && !bottom_bar) {
 				// reportedThrough (aligner_swsse_ee_u8.cpp:1331-1336, 1556)
 				tile_get(row, col);
 				const uint64_t bt = tbit(row, col);
-				if(tbits & bt) { w.ok = false; break; }
-				tbits |= bt;
-				tdirty = true;
+				if(tbits & bt) { w.ok = false; ended = true; }
+				else { tbits |= bt; tdirty = true; }
 			}
-			{
-				const int32_t dg = (int32_t)col - (int32_t)row + triml;
-				w.core = w.core || (dg >= 0 && dg >= corel && dg <= corer);
-			}
-			if(row == 0) break;
+		}
+		if(!ended) {
+			const int32_t dg = (int32_t)col - (int32_t)row + triml;
+			w.core = w.core || (dg >= 0 && dg >= corel && dg <= corer);
+			if(row == 0) ended = true;
+		}
+		if(!ended) {
 			const int rc = rd_at(row), m = rf_at(col), q = q_at(row);
 			int mv = -1;   // 0 diag, 1 ref open, 2 ref extend, 3 read open, 4 read extend
 			int32_t nxt = 0;
@@ -439,9 +503,9 @@ k_sw_bt(BtArgs A) {
 						}
 					}
 				}
-				if(mv < 0) break;   // empty cell: the alignment starts here
+				if(mv < 0) ended = true;   // empty cell: the alignment starts here
 			} else if(st == ST_E) {
-				if(col == 0) break;   // unreachable: E(row, 0) is the floor
+				if(col == 0) ended = true;   // unreachable: E(row, 0) is the floor
 				const int32_t hl = v1;
 				if(okv(hl) && hl - rdgo == cur) { mv = 3; nxt = hl; }
 				else { mv = 4; nxt = cur + rdge; }
@@ -450,30 +514,35 @@ k_sw_bt(BtArgs A) {
 				if(okv(hu) && hu - rfgo == cur) { mv = 1; nxt = hu; }
 				else { mv = 2; nxt = cur + rfge; }
 			}
-			if(mv == 0) {
-				const int mt = (m >= 16 || rc > 3) ? -1 : ((m >> rc) & 1);
-				if(mt != 1) {
-					push(row, 3, mask2dna(m), "ACGTN"[rc]);
-					w.score -= (rc > 3 || m > 15) ? C.npen : C.mmpen[q];
+			if(!ended) {
+				if(mv == 0) {
+					const int mt = (m >= 16 || rc > 3) ? -1 : ((m >> rc) & 1);
+					if(mt != 1) {
+						push(row, 3, mask2dna(m), "ACGTN"[rc]);
+						w.score -= (rc > 3 || m > 15) ? C.npen : C.mmpen[q];
+					} else {
+						w.score += C.match;
+					}
+					if(mt == -1) w.ns++;
+					row--; col--;
+					st = ST_H;
+				} else if(mv <= 2) {
+					push(row, 2, '-', "ACGTN"[rc]);
+					w.score -= mv == 1 ? rfgo : rfge;
+					st = mv == 1 ? ST_H : ST_F;
+					row--; w.gaps++;
 				} else {
-					w.score += C.match;
+					push(row + 1, 1, mask2dna(m), '-');
+					w.score -= mv == 3 ? rdgo : rdge;
+					st = mv == 3 ? ST_H : ST_E;
+					col--; w.gaps++;
 				}
-				if(mt == -1) w.ns++;
-				row--; col--;
-				st = ST_H;
-			} else if(mv <= 2) {
-				push(row, 2, '-', "ACGTN"[rc]);
-				w.score -= mv == 1 ? rfgo : rfge;
-				st = mv == 1 ? ST_H : ST_F;
-				row--; w.gaps++;
-			} else {
-				push(row + 1, 1, mask2dna(m), '-');
-				w.score -= mv == 3 ? rdgo : rdge;
-				st = mv == 3 ? ST_H : ST_E;
-				col--; w.gaps++;
+				cur = nxt;
 			}
-			cur = nxt;
 		}
+		} while(!FLAT && !ended);
+		if(!ended) continue;
+		// ---- the walk ended --------------------------------------------------
 		w.row = row;
 		w.col = col;
 		if(w.ok && !w.core) w.ok = false;            // must touch a core diagonal
@@ -489,86 +558,57 @@ k_sw_bt(BtArgs A) {
 			if(mt == -1) w.ns++;
 			if(w.ns > nceil) w.ok = false;
 		}
-		return w;
-	};
-	uint32_t ndone = 0, wq0 = 0, wq1 = 0, wq2 = 0, wq3 = 0;   // walked candidates: row << 16 | col
-	for(uint32_t ci = 0; ci < ncand; ci++) {
-		if(nal >= (int32_t)A.maxaln) break;
-		const bt2g_sw_cand cd = cl[ci];
+		if(w.ok && !first && !replay) {
+			// a later walk that succeeded: walk it again, unmarked, writing its edits
+			BTC(6);
+			replay = true;
+			cur = cscore;
+			start_walk(false, true);
+			continue;
+		}
+		walking = false;
+		first = false;
 		int8_t fate;
-		BTC(4);
-		// Local mode: most candidates (~95 % at 150 bp) lie within SQ of a walked
-		// one.  The squares of the first and the last three walked candidates
-		// are tested in registers first (exact: a hit is a dominated candidate);
-		// without a fates array the dominance test also runs before the start
-		// mark (either filter only skips the candidate; fates alone tell them apart).
-		const uint32_t cr = (uint32_t)cd.row, cc = (uint32_t)cd.col;
-		auto near = [&](uint32_t w) {
-			const uint32_t wr = w >> 16, wc = w & 0xffffu;
-			return (wr > cr ? wr - cr : cr - wr) <= SQ && (wc > cc ? wc - cc : cc - wc) <= SQ;
-		};
-		const bool dom_reg = local && ndone > 0 && (near(wq0) || near(wq1) || near(wq2) || near(wq3));
-		const bool dom_first = local && !A.fates && (dom_reg || (BTC(5), dom_test(cr, cc)));
-		if(cd.score < P.minsc) {
-			fate = 5;                                   // BT_CAND_FATE_FILT_SCORE
-		} else if(dom_first) {
-			fate = 4;                                   // BT_CAND_FATE_FILT_DOMINATED
-		} else if((local || cr + (uint32_t)gb < nrow) && marked(cr, cc)) {
-			// (end-to-end starts in the bottom barrier rows are never marked: see walk)
-			fate = 3;                                   // BT_CAND_FATE_FILT_START
-		} else {
-			if(local && A.fates && (dom_reg || (BTC(5), dom_test(cr, cc)))) {
-				fate = 4;                               // BT_CAND_FATE_FILT_DOMINATED
+		if(local) {
+			dom_add(row0, col0);
+			// register copies: the first walked candidate stays, the others rotate
+			const uint32_t wv = (row0 << 16) | col0;
+			if(ndone == 0) wq0 = wq1 = wq2 = wq3 = wv;
+			else { wq3 = wq2; wq2 = wq1; wq1 = wv; }
+			ndone++;
+		}
+		if(w.ok) {
+			const uint32_t trimBeg = w.row, trimEnd = nrow - row0 - 1;
+			// res.reverse(), AlnRes::setShape trim shift, invertEdits for !fw
+			// (aligner_result.cpp:101-117, 822-828; edit.cpp:50-78)
+			const uint32_t ned = w.ned, nst = ned < A.maxedit ? ned : A.maxedit;
+			if(fw) {
+				for(uint32_t i = 0; i < nst / 2; i++) {
+					const bt2g_edit t = ed[i];
+					ed[i] = ed[nst - 1 - i];
+					ed[nst - 1 - i] = t;
+				}
+				for(uint32_t i = 0; i < nst; i++) ed[i].pos -= trimBeg;
 			} else {
-				// the first walk writes its edits as it goes (it usually succeeds);
-				// a later walk that succeeds is walked again to write them
-				bt2g_edit* ed = A.edits + ((size_t)p * A.maxaln + (size_t)nal) * A.maxedit;
-				const uint32_t row0 = (uint32_t)cd.row, col0 = (uint32_t)cd.col;
-				// the candidate's score is its cell's H
-				Walk w = walk(row0, col0, cd.score, true, first, ed);
-				if(w.ok && !first) { BTC(6); (void)walk(row0, col0, cd.score, false, true, ed); }
-				first = false;
-				if(local) {
-					dom_add(cr, cc);
-					// register copies: the first walked candidate stays, the others rotate
-					const uint32_t w = (cr << 16) | cc;
-					if(ndone == 0) wq0 = wq1 = wq2 = wq3 = w;
-					else { wq3 = wq2; wq2 = wq1; wq1 = w; }
-					ndone++;
-				}
-				if(w.ok) {
-					const uint32_t trimBeg = w.row, trimEnd = nrow - row0 - 1;
-					// res.reverse(), AlnRes::setShape trim shift, invertEdits for !fw
-					// (aligner_result.cpp:101-117, 822-828; edit.cpp:50-78)
-					const uint32_t ned = w.ned, nst = ned < A.maxedit ? ned : A.maxedit;
-					if(fw) {
-						for(uint32_t i = 0; i < nst / 2; i++) {
-							const bt2g_edit t = ed[i];
-							ed[i] = ed[nst - 1 - i];
-							ed[nst - 1 - i] = t;
-						}
-						for(uint32_t i = 0; i < nst; i++) ed[i].pos -= trimBeg;
-					} else {
-						const uint32_t sz = nrow - trimBeg - trimEnd;
-						for(uint32_t i = 0; i < nst; i++)
-							ed[i].pos = sz - (ed[i].pos - trimBeg) - (ed[i].type == 1 ? 0u : 1u);
-					}
-					int32_t refns = 0;
-					for(uint32_t c = w.col; c <= col0; c++) refns += rf_at(c) > 15;
-					bt2g_sw_aln a;
-					a.cand = (int32_t)ci; a.score = w.score; a.off = (int32_t)w.col; a.ns = w.ns; a.gaps = w.gaps;
-					a.refns = refns; a.nedit = (int32_t)ned;
-					a.trim5p = (int32_t)(fw ? trimBeg : trimEnd); a.trim3p = (int32_t)(fw ? trimEnd : trimBeg);
-					a.pad = 0;
-					A.alns[(size_t)p * A.maxaln + (size_t)nal] = a;
-					nal++;
-					fate = 1;                               // BT_CAND_FATE_SUCCEEDED
-				} else {
-					fate = 2;                               // BT_CAND_FATE_FAILED
-				}
+				const uint32_t sz = nrow - trimBeg - trimEnd;
+				for(uint32_t i = 0; i < nst; i++)
+					ed[i].pos = sz - (ed[i].pos - trimBeg) - (ed[i].type == 1 ? 0u : 1u);
 			}
+			int32_t refns = 0;
+			for(uint32_t c = w.col; c <= col0; c++) refns += rf_at(c) > 15;
+			bt2g_sw_aln a;
+			a.cand = (int32_t)ci; a.score = w.score; a.off = (int32_t)w.col; a.ns = w.ns; a.gaps = w.gaps;
+			a.refns = refns; a.nedit = (int32_t)ned;
+			a.trim5p = (int32_t)(fw ? trimBeg : trimEnd); a.trim3p = (int32_t)(fw ? trimEnd : trimBeg);
+			a.pad = 0;
+			A.alns[(size_t)p * A.maxaln + (size_t)nal] = a;
+			nal++;
+			fate = 1;                                       // BT_CAND_FATE_SUCCEEDED
+		} else {
+			fate = 2;                                       // BT_CAND_FATE_FAILED
 		}
 		if(A.fates) A.fates[(size_t)p * A.cap + ci] = fate;
+		ci++;
 	}
 	A.naln[p] = nal;
 }
@@ -576,8 +616,11 @@ k_sw_bt(BtArgs A) {
 void launch_sw_bt(int kind, const BtArgs& a, hipStream_t st) {
 	if(a.nprob == 0) return;
 	const dim3 grid((a.nprob + 63u) / 64u), block(64);
-	switch(kind) {
-	case 0: hipLaunchKernelGGL(k_sw_bt<0>, grid, block, 0, st, a); break;
-	default: hipLaunchKernelGGL(k_sw_bt<1>, grid, block, 0, st, a); break;
+	if(a.local) {
+		if(kind == 0) hipLaunchKernelGGL((k_sw_bt<0, true>), grid, block, 0, st, a);
+		else hipLaunchKernelGGL((k_sw_bt<1, true>), grid, block, 0, st, a);
+	} else {
+		if(kind == 0) hipLaunchKernelGGL((k_sw_bt<0, false>), grid, block, 0, st, a);
+		else hipLaunchKernelGGL((k_sw_bt<1, false>), grid, block, 0, st, a);
 	}
 }
