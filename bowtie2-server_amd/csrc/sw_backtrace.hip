@@ -97,6 +97,9 @@ extern unsigned long long bt_counts[8];
 #ifndef BT2G_BT_WAVES
 #define BT2G_BT_WAVES 3
 #endif
+#ifndef BT2G_BT_EE_STEPS
+#define BT2G_BT_EE_STEPS 0xffffffffu   // end-to-end: a whole walk per iteration (4, 8, 16: same 32 ms)
+#endif
 template <int KIND, bool FLAT>
 __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(BT2G_BT_WAVES)))
 k_sw_bt(BtArgs A) {
@@ -409,8 +412,9 @@ k_sw_bt(BtArgs A) {
 			replay = false;
 			start_walk(true, first);
 		}
-		// ---- one walk step (FLAT), or the whole walk --------------------------
+		// ---- one walk step (FLAT), or up to BT2G_BT_EE_STEPS steps ---------------
 		bool ended = false;
+		uint32_t ks = 0;
 		do {
 		BTC(1);
 		{
@@ -540,7 +544,7 @@ k_sw_bt(BtArgs A) {
 				cur = nxt;
 			}
 		}
-		} while(!FLAT && !ended);
+		} while(!ended && ++ks < (FLAT ? 1u : (uint32_t)BT2G_BT_EE_STEPS));
 		if(!ended) continue;
 		// ---- the walk ended --------------------------------------------------
 		w.row = row;
