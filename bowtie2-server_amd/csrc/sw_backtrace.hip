@@ -620,7 +620,12 @@ k_sw_bt(BtArgs A) {
 void launch_sw_bt(int kind, const BtArgs& a, hipStream_t st) {
 	if(a.nprob == 0) return;
 	const dim3 grid((a.nprob + 63u) / 64u), block(64);
-	if(a.local) {
+#ifdef BT2G_BT_FLAT_ALL
+	const bool flat = true;                 // timing experiments only (end-to-end and mate DPs: slower)
+#else
+	const bool flat = a.local != 0;
+#endif
+	if(flat) {
 		if(kind == 0) hipLaunchKernelGGL((k_sw_bt<0, true>), grid, block, 0, st, a);
 		else hipLaunchKernelGGL((k_sw_bt<1, true>), grid, block, 0, st, a);
 	} else {
