@@ -66,6 +66,10 @@ __device__ __forceinline__ uint32_t psub(uint32_t a, uint32_t b) {
 	return __builtin_bit_cast(uint32_t, __builtin_elementwise_sub_sat(__builtin_bit_cast(u16x2, a),
 	                                                                  __builtin_bit_cast(u16x2, b)));
 }
+__device__ __forceinline__ uint32_t pmin(uint32_t a, uint32_t b) {
+	return __builtin_bit_cast(uint32_t, __builtin_elementwise_min(__builtin_bit_cast(u16x2, a),
+	                                                              __builtin_bit_cast(u16x2, b)));
+}
 __device__ __forceinline__ uint32_t pmax(uint32_t a, uint32_t b) {
 	return __builtin_bit_cast(uint32_t, __builtin_elementwise_max(__builtin_bit_cast(u16x2, a),
 	                                                              __builtin_bit_cast(u16x2, b)));
@@ -565,13 +569,11 @@ k_sw_sys(const bt2g_sw_problem* __restrict__ probs, uint32_t nprob, const uint8_
 			const bool g1 = h[1].live && (uint32_t)j < h[1].ncol && (mx >> 16) >= ctest[1];
 			if(g0 || g1) {
 				const uint32_t mj = mymsk[j], mj1 = mymsk[j + 1];
+				// H >= minsc per half as one bit per half: min(H -sat (minsc-1), 1) is
+				// 0 or 1 in each half, shifted to bit i / 16 + i (3 ops per row pair)
 				uint32_t ge = 0;
 #pragma unroll
-				for(int i = 0; i < R; i++) {
-					const uint32_t tt = psub(Hc[i], cthr);          // H >= minsc per half
-					ge |= ((tt & 0xffffu) ? 1u : 0u) << i;
-					ge |= ((tt >> 16) ? 1u : 0u) << (16 + i);
-				}
+				for(int i = 0; i < R; i++) ge |= pmin(psub(Hc[i], cthr), 0x00010001u) << i;
 				auto s2 = [](uint32_t m, int c) -> uint32_t {
 					return (((m >> c) & 1u) ? 0xffffu : 0u) | (((m >> (8 + c)) & 1u) ? 0xffff0000u : 0u);
 				};
