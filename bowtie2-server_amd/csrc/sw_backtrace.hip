@@ -370,11 +370,14 @@ k_sw_bt(BtArgs A) {
 	};
 	uint32_t ndone = 0, wq0 = 0, wq1 = 0, wq2 = 0, wq3 = 0;   // walked candidates: row << 16 | col
 	uint32_t ci = 0;
+	// the next candidate is loaded one ahead (its load overlaps the current walk)
+	bt2g_sw_cand nxt_cd = ncand ? cl[0] : bt2g_sw_cand{0, 0, 0};
 	int32_t cscore = 0;
 	while(true) {
 		if(!walking) {
 			if(ci >= ncand || nal >= (int32_t)A.maxaln) break;
-			const bt2g_sw_cand cd = cl[ci];
+			const bt2g_sw_cand cd = nxt_cd;
+			nxt_cd = cl[ci + 1u < ncand ? ci + 1u : ci];
 			int8_t fate = 0;
 			BTC(4);
 			// Local mode: most candidates (~95 % at 150 bp) lie within SQ of a walked
