@@ -419,7 +419,7 @@ def _build_ebwt_torch(t, sa, flags, rstarts, plen, off_rate=4, ftab_chars=10, li
     side_bwt_len = side_bwt_sz * 4
     num_sides = (n // 4 + 1 + side_bwt_sz - 1) // side_bwt_sz
     tot = num_sides * side_bwt_len
-    zoff = int(torch.nonzero(sa == 0)[0, 0])
+    zoff = int(_nonzero_big(sa == 0)[0])
     bwt = torch.zeros(tot, dtype=torch.uint8, device=dev)
     prev = (sa - 1).clamp_(min=0)
     bwt[: n + 1] = t[prev]
@@ -455,7 +455,7 @@ def _build_ebwt_torch(t, sa, flags, rstarts, plen, off_rate=4, ftab_chars=10, li
     ftab = torch.zeros(ftab_len, dtype=torch.int64, device=dev)
     ftab[1:] += torch.bincount(key, minlength=ftab_len - 1)[: ftab_len - 1]
     # short suffixes (n - sa < ftab_chars): absorbed by the next long suffix's bucket
-    short_rows = torch.nonzero((n - sa) < ftab_chars).squeeze(1).cpu().numpy()
+    short_rows = _nonzero_big((n - sa) < ftab_chars).cpu().numpy()
     absorb = np.zeros(ftab_len, dtype=np.int64)
     short_set = set(int(r) for r in short_rows)
     for r in short_rows:
@@ -486,6 +486,57 @@ def _build_ebwt_torch(t, sa, flags, rstarts, plen, off_rate=4, ftab_chars=10, li
                 ftab=out.astype(np.uint32), eftab=eftab.astype(np.uint32), offs=offs)
 
 
+_CHUNK = 1 << 30      # torch sort / nonzero take at most INT_MAX elements
+
+
+def _nonzero_big(mask):
+    """torch.nonzero(mask).squeeze(1) for masks longer than INT_MAX."""
+    import torch
+    n = int(mask.numel())
+    if n <= _CHUNK:
+        return torch.nonzero(mask).squeeze(1)
+    parts = [torch.nonzero(mask[i:i + _CHUNK]).squeeze(1) + i for i in range(0, n, _CHUNK)]
+    return torch.cat(parts)
+
+
+def _cummax_big(x):
+    """torch.cummax(x, 0).values in chunks, carrying the running maximum."""
+    import torch
+    n = int(x.numel())
+    if n <= _CHUNK:
+        return torch.cummax(x, 0).values
+    out = torch.empty_like(x)
+    carry = None
+    for i in range(0, n, _CHUNK):
+        c = torch.cummax(x[i:i + _CHUNK], 0).values
+        if carry is not None:
+            c = torch.maximum(c, carry)
+        out[i:i + _CHUNK] = c
+        carry = c[-1]
+    return out
+
+
+def _sort_big(key, top_shift):
+    """torch.sort(key) for more than INT_MAX non-negative keys: bucket by the
+    bits above top_shift (key order), sort every bucket on its own."""
+    import torch
+    n = int(key.numel())
+    if n <= _CHUNK:
+        return torch.sort(key)
+    b = (key >> top_shift).to(torch.uint8)          # < 64 buckets
+    nb = int(b.max()) + 1
+    keys, perms = [], []
+    for v in range(nb):
+        idx = _nonzero_big(b == v)
+        if idx.numel() == 0:
+            continue
+        k, o = torch.sort(key[idx])
+        keys.append(k)
+        perms.append(idx[o])
+        del idx, k, o
+    return torch.cat(keys), torch.cat(perms)
+
+
 def _suffix_array_torch(t):
     """suffix_array() on a device tensor; returns an int64 device tensor."""
     import torch
@@ -498,7 +549,8 @@ def _suffix_array_torch(t):
     for k in range(K):
         key.mul_(8).add_(sym[k:k + n + 1])
     del sym
-    key, sa = torch.sort(key)
+    # 21 symbols x 3 bits = 63 bits; beyond INT_MAX keys the first two symbols bucket the sort
+    key, sa = _sort_big(key, 3 * (K - 2))
     newgrp = torch.ones(n + 1, dtype=torch.bool, device=dev)
     newgrp[1:] = key[1:] != key[:-1]
     del key
@@ -506,14 +558,14 @@ def _suffix_array_torch(t):
     while True:
         single = newgrp.clone()
         single[:-1] &= newgrp[1:]
-        unresolved = torch.nonzero(~single).squeeze(1)
+        unresolved = _nonzero_big(~single)
         del single
         if unresolved.numel() == 0:
             break
         idx = torch.arange(n + 1, device=dev)
         grpstart = torch.where(newgrp, idx, torch.zeros_like(idx))
         del idx
-        grpstart = torch.cummax(grpstart, 0).values
+        grpstart = _cummax_big(grpstart)
         rank = torch.full((n + 1 + h,), -1, dtype=torch.int64, device=dev)
         rank[sa] = grpstart
         pos = sa[unresolved]
