@@ -5,5 +5,5 @@ tag=${1:-r01}
 export TMPDIR=/tmp
 cd $GRAFT_REPO_ROOT
 mkdir -p gpurun_out
-timeout -k 10 600 python -u bench.py > gpurun_out/${tag}_bench.log 2>&1
+timeout -k 10 700 python -u bench.py --index-cache /tmp/bench_idx > gpurun_out/${tag}_bench.log 2>&1
 timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/${tag}_prof -o run -- python3 bench.py --no-cpu-baseline --index-cache /tmp/bench_idx > gpurun_out/${tag}_prof.log 2>&1
