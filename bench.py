@@ -60,20 +60,29 @@ class Policy:
     """Per-mode seed and score policy (bt2_search.cpp presets).
     ee:     --end-to-end --sensitive: -L 22, -i S,1,1.15, --score-min L,-0.6,-0.6
     local:  --local --sensitive-local: -L 20, -i S,1,0.75, --score-min G,20,8, --ma 2
-    paired: ee with the paired-end seed interval, --fr -I 0 -X 500 mate search"""
+    paired: ee with the paired-end seed interval, --fr -I 0 -X 500 mate search
+    preset "very-sensitive" (BASELINE configs[4]): -L 20, -i S,1,0.50 in every mode
+    (bt2_search.cpp preset table; --very-sensitive-local has the same seed
+    policy).  Its -D 20 -R 3 extension / re-seed limits belong to the host
+    driver loop (row A11), which the bench does not model: round 0 only."""
 
-    def __init__(self, mode, length):
+    def __init__(self, mode, length, preset="sensitive"):
         import math
         self.mode, self.local, self.paired = mode, mode == "local", mode == "paired"
+        self.preset = preset
+        if preset == "very-sensitive":
+            seedlen, interval = 20, int(1 + 0.50 * math.sqrt(length))
+        elif self.local:
+            seedlen, interval = 20, int(1 + 0.75 * math.sqrt(length))
+        else:
+            seedlen, interval = SEEDLEN, int(1 + 1.15 * math.sqrt(length))
         if self.paired:
             # paired-end: the seed interval is boosted (bt2_search.cpp:3392-3395)
-            self.seedlen, self.interval = SEEDLEN, int(INTERVAL * 1.2 + 0.5)
-            self.minsc = int(-0.6 - 0.6 * length)
-        elif self.local:
-            self.seedlen, self.interval = 20, int(1 + 0.75 * math.sqrt(length))
+            interval = int(interval * 1.2 + 0.5)
+        self.seedlen, self.interval = seedlen, interval
+        if self.local:
             self.minsc = int(20 + 8 * math.log(length))
         else:
-            self.seedlen, self.interval = SEEDLEN, INTERVAL
             self.minsc = int(-0.6 - 0.6 * length)
 MAXALN, MAXEDIT = 8, 64        # alignments kept per DP (the loop stops there); edits per alignment
                                # (150 bp, minsc -90, n-ceil 22: <= 22 N + 34 mismatches = 56)
@@ -178,10 +187,10 @@ def make_pairs(parts, n, length, seed):
 class Pipeline:
     """The per-step GPU work (see module docstring), torch glue on one stream."""
 
-    def __init__(self, eng, idx, reads, quals, length, mode="ee"):
+    def __init__(self, eng, idx, reads, quals, length, mode="ee", preset="sensitive"):
         import torch
         import bt2g
-        self.pol = pol = Policy(mode, length)
+        self.pol = pol = Policy(mode, length, preset)
         self.torch, self.bt2g, self.L = torch, bt2g, bt2g.lib()
         self.eng = eng
         self.dev = reads.device
@@ -686,16 +695,22 @@ def mate_parity(pipe, mate):
 
 
 def workload(args):
-    genome = (f"vs a {args.genome_mb:.0f} Mbp synthetic genome (hg38-size; hg38 itself is unavailable offline), "
+    size = "hg38-size; " if args.genome_mb >= 3000 else ""
+    genome = (f"vs a {args.genome_mb:.0f} Mbp synthetic genome ({size}hg38 itself is unavailable offline), "
               f"index built like bowtie2-build (offRate 4, ftabChars 10)")
+    vs = args.preset == "very-sensitive"
     seed = ("exact sweep + gated 1-mm + seed round 0 + SA offsets + <=2 seed-extension DPs/read "
             "(fill + nextAlignment loop)")
     if args.mode == "paired":
-        return (f"{args.reads} synthetic 2 x {args.read_len} bp read pairs per GPU per step (BASELINE configs[2]), "
-                f"--end-to-end --sensitive, {genome}; both mates: {seed}; then per pair with an aligned mate one "
+        cfg = "BASELINE configs[4] policy, --end-to-end --very-sensitive" if vs else \
+            "BASELINE configs[2], --end-to-end --sensitive"
+        return (f"{args.reads} synthetic 2 x {args.read_len} bp read pairs per GPU per step ({cfg}), "
+                f"{genome}; both mates: {seed}; then per pair with an aligned mate one "
                 f"mate search: otherMate + frameFindMateRect (--fr -I 0 -X 500) + the mate DP "
                 f"({args.read_len} x <=705, fill + nextAlignment loop)")
     mode = "--local --sensitive-local (configs[3])" if args.mode == "local" else "--end-to-end --sensitive (configs[1])"
+    if vs:
+        mode = "--local --very-sensitive-local" if args.mode == "local" else "--end-to-end --very-sensitive"
     return f"{args.reads} synthetic {args.read_len} bp unpaired reads per GPU per step, {mode} policy, {genome}; {seed}"
 
 
@@ -709,6 +724,9 @@ def main():
     ap.add_argument("--mode", choices=("ee", "local", "paired"), default="ee",
                     help="ee: BASELINE configs[1] (--end-to-end --sensitive); local: configs[3] (--local); "
                          "paired: configs[2] (2 x 150 bp pairs, --end-to-end, mate search)")
+    ap.add_argument("--preset", choices=("sensitive", "very-sensitive"), default="sensitive",
+                    help="seed policy; very-sensitive: -L 20 -i S,1,0.50 (with --mode paired: BASELINE "
+                         "configs[4]'s policy, sharded by torchrun across GPUs)")
     ap.add_argument("--genome-mb", type=float, default=3100.0,
                     help="synthetic genome size (default: hg38's 3.1 Gbp; the index is built on the GPU, ~160 s)")
     ap.add_argument("--cpu-sample", type=int, default=1_000_000)
@@ -757,7 +775,7 @@ def main():
     log(f"[rank {rank}] {args.reads} reads in {time.time()-t2:.1f}s; index resident: {info[12]/1e9:.2f} GB")
     reads = torch.from_numpy(reads_np).to(dev)
     quals = torch.from_numpy(quals_np).to(dev)
-    pipe = Pipeline(eng, idx, reads, quals, args.read_len, args.mode)
+    pipe = Pipeline(eng, idx, reads, quals, args.read_len, args.mode, args.preset)
 
     engs = [eng] + ([pipe.eng2] if args.mode == "paired" else [])
     for _ in range(args.warmup):

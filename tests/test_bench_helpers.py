@@ -51,3 +51,16 @@ def test_make_pairs_geometry():
         assert 150 <= frag <= 500 + 2, frag
         good += 1
     assert good > n // 2
+
+
+def test_policy_seed_geometry():
+    """Seed length / interval / count per strand at 150 bp (SURVEY.md 8a row A9:
+    --sensitive 22/15 -> 9 seeds, --very-sensitive 20/7 -> 19, paired-end
+    interval boost (int)(ival * 1.2 + 0.5), bt2_search.cpp:3392-3395)."""
+    want = {("ee", "sensitive"): (22, 15, 9), ("ee", "very-sensitive"): (20, 7, 19),
+            ("local", "sensitive"): (20, 10, 14), ("local", "very-sensitive"): (20, 7, 19),
+            ("paired", "sensitive"): (22, 18, 8), ("paired", "very-sensitive"): (20, 8, 17)}
+    for (mode, preset), (L, ival, nseeds) in want.items():
+        p = bench.Policy(mode, 150, preset)
+        assert (p.seedlen, p.interval, 1 + (150 - p.seedlen) // p.interval) == (L, ival, nseeds), (mode, preset)
+        assert p.minsc == (60 if mode == "local" else -90)
