@@ -631,14 +631,18 @@ def bt_mismatches(naln, alns, ed, ref, maxaln, maxedit):
     dev = naln.device
     naln = naln.to(torch.int64)
     alns = alns.to(torch.int64)
-    pos = ed[..., 0].to(torch.int64)
-    w = ed[..., 1].to(torch.int64) & 0xFFFFFFFF
-    typ, chr_, qchr = w & 0xFF, (w >> 8) & 0xFF, (w >> 16) & 0xFF
     k = torch.arange(maxaln, device=dev)[None, :, None]
     e = torch.arange(maxedit, device=dev)[None, None, :]
-    live = (k < naln[:, None, None]) & (e < alns[:, :, 6][:, :, None])
-    term = (k + 1) * (pos * 131 + typ * 31 + chr_ * 7 + qchr)
-    ck = (torch.where(live, term, torch.zeros_like(term)).sum((1, 2)) & 0x7FFFFFFFFFFFFFFF).cpu().numpy()
+    cks = []
+    for s0 in range(0, len(naln), 65536):          # int64 temporaries: 4 KB per DP per tensor
+        s1 = min(s0 + 65536, len(naln))
+        pos = ed[s0:s1, ..., 0].to(torch.int64)
+        w = ed[s0:s1, ..., 1].to(torch.int64) & 0xFFFFFFFF
+        typ, chr_, qchr = w & 0xFF, (w >> 8) & 0xFF, (w >> 16) & 0xFF
+        live = (k < naln[s0:s1, None, None]) & (e < alns[s0:s1, :, 6][:, :, None])
+        term = (k + 1) * (pos * 131 + typ * 31 + chr_ * 7 + qchr)
+        cks.append((torch.where(live, term, torch.zeros_like(term)).sum((1, 2)) & 0x7FFFFFFFFFFFFFFF).cpu().numpy())
+    ck = np.concatenate(cks) if cks else np.zeros(0, np.int64)
     naln = naln.cpu().numpy()
     first = alns[:, 0][:, [0, 1, 2, 6]].cpu().numpy()
     bad = np.minimum(ref[:, 2], maxaln) != naln
@@ -655,9 +659,14 @@ def backtrace_parity(pipe, keep, sw_ref):
     """The sampled seed-extension DPs' nextAlignment results vs the reference's."""
     import torch
     npb = pipe.last["npb"]
-    kp = torch.from_numpy(np.nonzero(keep)[0]).to(pipe.dev)
-    return bt_mismatches(pipe.naln[:npb].index_select(0, kp), pipe.alns[:npb].index_select(0, kp),
-                         pipe.edits[:npb].index_select(0, kp), sw_ref, pipe.maxaln, pipe.maxedit)
+    kp_all = np.nonzero(keep)[0]
+    bad = 0
+    for s0 in range(0, len(kp_all), 262144):       # bounded copies of the edit rows
+        kp = torch.from_numpy(kp_all[s0:s0 + 262144]).to(pipe.dev)
+        bad += bt_mismatches(pipe.naln[:npb].index_select(0, kp), pipe.alns[:npb].index_select(0, kp),
+                             pipe.edits[:npb].index_select(0, kp), sw_ref[s0:s0 + 262144], pipe.maxaln,
+                             pipe.maxedit)
+    return bad
 
 
 def mate_parity(pipe, mate):

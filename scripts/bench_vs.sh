@@ -7,3 +7,5 @@ O=gpurun_out/vs
 mkdir -p $O
 timeout -k 10 900 python -u bench.py --mode paired --preset very-sensitive --reads 1250000 --cpu-sample 250000 > $O/bench.log 2>&1
 echo bench ok
+timeout -k 10 300 python -u -c "import __graft_entry__ as g; g.smoke()" > $O/smoke.log 2>&1
+echo smoke ok
