@@ -97,11 +97,6 @@ extern unsigned long long bt_counts[8];
 #ifndef BT2G_BT_WAVES
 #define BT2G_BT_WAVES 3
 #endif
-#ifdef BT2G_BT_DEFER
-#define BT2G_BT_DEFER_ON true
-#else
-#define BT2G_BT_DEFER_ON false
-#endif
 #ifndef BT2G_BT_EE_STEPS
 #define BT2G_BT_EE_STEPS 0xffffffffu   // end-to-end: a whole walk per iteration (4, 8, 16: same 32 ms)
 #endif
@@ -359,10 +354,6 @@ k_sw_bt(BtArgs A) {
 	};
 	Walk w{true, false, 0u, 0u, 0u, 0, 0, 0};
 	bool walking = false, wmark = false, wemit = false, replay = false;
-	// deferred gap tests (end-to-end, BT2G_BT_DEFER): a lane whose diagonal test
-	// fails parks at its cell until the wave evaluates its parked lanes together
-	constexpr bool DEFER = !FLAT && BT2G_BT_DEFER_ON;
-	bool parked = false, pdeq = false;
 	uint32_t row = 0, col = 0, row0 = 0, col0 = 0;
 	int32_t cur = 0;
 	int st = ST_H;
@@ -376,7 +367,6 @@ k_sw_bt(BtArgs A) {
 		row = row0; col = col0; st = ST_H;
 		wmark = mark; wemit = emit;
 		walking = true;
-		parked = false;
 		BTC(0);
 	};
 	uint32_t ndone = 0, wq0 = 0, wq1 = 0, wq2 = 0, wq3 = 0;   // walked candidates: row << 16 | col
@@ -439,11 +429,7 @@ k_sw_bt(BtArgs A) {
 		uint32_t ks = 0;
 		do {
 		BTC(1);
-		const bool resume = parked;       // its mark, core and row-0 test were done when it parked
-		int mv = -1;   // 0 diag, 1 ref open, 2 ref extend, 3 read open, 4 read extend
-		int32_t nxt = 0;
-		bool gap_now = false, deq = pdeq;
-		if(!resume) {
+		{
 			// end-to-end: every candidate starts in the last row and the bottom
 			// gap-barrier rows allow only diagonal moves, so walks there stay on
 			// their own diagonals and can neither meet nor be met: no marks
@@ -456,13 +442,15 @@ k_sw_bt(BtArgs A) {
 				else { tbits |= bt; tdirty = true; }
 			}
 		}
-		if(!ended && !resume) {
+		if(!ended) {
 			const int32_t dg = (int32_t)col - (int32_t)row + triml;
 			w.core = w.core || (dg >= 0 && dg >= corel && dg <= corer);
 			if(row == 0) ended = true;
 		}
-		const int rc = ended ? 0 : rd_at(row), m = ended ? 0 : rf_at(col), q = ended ? 0 : q_at(row);
-		if(!ended && !resume) {
+		if(!ended) {
+			const int rc = rd_at(row), m = rf_at(col), q = q_at(row);
+			int mv = -1;   // 0 diag, 1 ref open, 2 ref extend, 3 read open, 4 read extend
+			int32_t nxt = 0;
 			// in gap-barrier rows H is the diagonal term itself when above the
 			// floor (E and F are the floor there): H(up-left) = cur - score, no load
 			const bool derive = st == ST_H && !gaps_ok(row) && (!local || cur > 0);
@@ -474,12 +462,64 @@ k_sw_bt(BtArgs A) {
 				const bool wantd = col > 0;
 				const int32_t hul = !wantd ? 0 : derive ? cur - sdiag(rc, m, q) : v1;
 				// diag equality; local mode also wants H(up-left) > 0 (floorsc)
-				deq = wantd && cur == hul + sdiag(rc, m, q);
+				const bool deq = wantd && cur == hul + sdiag(rc, m, q);
 				if(deq && okv(hul)) { mv = 0; nxt = hul; }
 				if(mv < 0 && gaps_ok(row)) {
-					if(DEFER) { parked = true; pdeq = deq; }   // evaluated with the wave's other parked lanes
-					else gap_now = true;
-				} else if(mv < 0) ended = true;   // empty cell: the alignment starts here
+					int32_t hu = 0, hl = 0;
+#pragma unroll 1
+					for(int t = 0; t < 2; t++) {          // one read site for up and left
+						if(t == 1 && col == 0) break;
+						const int32_t v = hget(t == 0 ? row - 1 : row, t == 0 ? col : col - 1);
+						if(t == 0) hu = v; else hl = v;
+					}
+					// F(row-1, col) == cur + rfge: H(x-k, col) == cur + rfgo + k*rfge, x = row-1,
+					// rows x..x-k+1 outside the barrier, x-k >= 0
+					bool fup = false;
+					const int32_t x = (int32_t)row - 1;
+					if(okv(cur + rfge) && x >= gb && x <= (int32_t)nrow - gb - 1) {
+						int32_t kmax = x - gb + 1;
+						kmax = kmax < x ? kmax : x;
+						if(rfge > 0) {
+							const int32_t kh = (hmax(x - 1) - cur - rfgo) / rfge;   // need <= hmax
+							kmax = kh < kmax ? kh : kmax;
+						}
+						fup = col_hit(col, x - kmax, x - 1, x, cur + rfgo, rfge);
+					}
+					if(okv(hu) && cur == hu - rfgo) { mv = 1; nxt = hu; }
+					else if(fup) { mv = 2; nxt = cur + rfge; }
+					else if(col > 0) {
+						if(okv(hl) && cur == hl - rdgo) { mv = 3; nxt = hl; }
+						else if(!deq && (!local || cur > 0)) {
+							// above the floor, not diagonal, not from F: from E, and not
+							// by an open -- an extension
+							if(col > 1) { mv = 4; nxt = cur + rdge; }
+						} else if(col > 1 && okv(cur + rdge)) {
+							// H may come from a diagonal the walk may not take (local,
+							// H(up-left) == 0) or from the local floor: E(row, col-1) ==
+							// cur + rdge needs the row scan
+							const int32_t cc = (int32_t)col - 1;
+							const int32_t hm = hmax((int32_t)row);
+							// eight independent loads in flight per round (only existence matters)
+							bool found = false;
+#pragma unroll 1
+							for(int32_t k0 = 1; !found && cc - k0 >= 0 && cur + rdge + rdgo + (k0 - 1) * rdge <= hm;
+							    k0 += 8) {
+								int32_t v[8];
+								BTC(3);
+#pragma unroll
+								for(int u = 0; u < 8; u++)
+									v[u] = cc - (k0 + u) >= 0 ? pl.h(row, (uint32_t)(cc - (k0 + u))) : -1;
+#pragma unroll
+								for(int u = 0; u < 8; u++) {
+									const int32_t need = cur + rdge + rdgo + (k0 + u - 1) * rdge;
+									found = found || (cc - (k0 + u) >= 0 && need <= hm && v[u] == need);
+								}
+							}
+							if(found) { mv = 4; nxt = cur + rdge; }
+						}
+					}
+				}
+				if(mv < 0) ended = true;   // empty cell: the alignment starts here
 			} else if(st == ST_E) {
 				if(col == 0) ended = true;   // unreachable: E(row, 0) is the floor
 				const int32_t hl = v1;
@@ -490,96 +530,31 @@ k_sw_bt(BtArgs A) {
 				if(okv(hu) && hu - rfgo == cur) { mv = 1; nxt = hu; }
 				else { mv = 2; nxt = cur + rfge; }
 			}
-		}
-#ifdef BT2G_BT_DEFER
-		if(DEFER) {
-			// parked lanes run the gap tests together: once 16 have parked, or when
-			// no lane of the wave can take a diagonal step (exact: per-lane
-			// semantics are unchanged, only the schedule)
-			const uint64_t pm = __ballot(parked && !ended), am = __ballot(!parked && !ended);
-			if(parked && (__popcll(pm) >= 16 || am == 0)) { gap_now = true; parked = false; }
-		}
-#endif
-		if(gap_now && !ended) {
-			int32_t hu = 0, hl = 0;
-#pragma unroll 1
-			for(int t = 0; t < 2; t++) {          // one read site for up and left
-				if(t == 1 && col == 0) break;
-				const int32_t v = hget(t == 0 ? row - 1 : row, t == 0 ? col : col - 1);
-				if(t == 0) hu = v; else hl = v;
-			}
-			// F(row-1, col) == cur + rfge: H(x-k, col) == cur + rfgo + k*rfge, x = row-1,
-			// rows x..x-k+1 outside the barrier, x-k >= 0
-			bool fup = false;
-			const int32_t x = (int32_t)row - 1;
-			if(okv(cur + rfge) && x >= gb && x <= (int32_t)nrow - gb - 1) {
-				int32_t kmax = x - gb + 1;
-				kmax = kmax < x ? kmax : x;
-				if(rfge > 0) {
-					const int32_t kh = (hmax(x - 1) - cur - rfgo) / rfge;   // need <= hmax
-					kmax = kh < kmax ? kh : kmax;
-				}
-				fup = col_hit(col, x - kmax, x - 1, x, cur + rfgo, rfge);
-			}
-			if(okv(hu) && cur == hu - rfgo) { mv = 1; nxt = hu; }
-			else if(fup) { mv = 2; nxt = cur + rfge; }
-			else if(col > 0) {
-				if(okv(hl) && cur == hl - rdgo) { mv = 3; nxt = hl; }
-				else if(!deq && (!local || cur > 0)) {
-					// above the floor, not diagonal, not from F: from E, and not
-					// by an open -- an extension
-					if(col > 1) { mv = 4; nxt = cur + rdge; }
-				} else if(col > 1 && okv(cur + rdge)) {
-					// H may come from a diagonal the walk may not take (local,
-					// H(up-left) == 0) or from the local floor: E(row, col-1) ==
-					// cur + rdge needs the row scan
-					const int32_t cc = (int32_t)col - 1;
-					const int32_t hm = hmax((int32_t)row);
-					// eight independent loads in flight per round (only existence matters)
-					bool found = false;
-#pragma unroll 1
-					for(int32_t k0 = 1; !found && cc - k0 >= 0 && cur + rdge + rdgo + (k0 - 1) * rdge <= hm;
-					    k0 += 8) {
-						int32_t v[8];
-						BTC(3);
-#pragma unroll
-						for(int u = 0; u < 8; u++)
-							v[u] = cc - (k0 + u) >= 0 ? pl.h(row, (uint32_t)(cc - (k0 + u))) : -1;
-#pragma unroll
-						for(int u = 0; u < 8; u++) {
-							const int32_t need = cur + rdge + rdgo + (k0 + u - 1) * rdge;
-							found = found || (cc - (k0 + u) >= 0 && need <= hm && v[u] == need);
-						}
+			if(!ended) {
+				if(mv == 0) {
+					const int mt = (m >= 16 || rc > 3) ? -1 : ((m >> rc) & 1);
+					if(mt != 1) {
+						push(row, 3, mask2dna(m), "ACGTN"[rc]);
+						w.score -= (rc > 3 || m > 15) ? C.npen : C.mmpen[q];
+					} else {
+						w.score += C.match;
 					}
-					if(found) { mv = 4; nxt = cur + rdge; }
-				}
-			}
-			if(mv < 0) ended = true;   // empty cell: the alignment starts here
-		}
-		if(!ended && mv >= 0) {
-			if(mv == 0) {
-				const int mt = (m >= 16 || rc > 3) ? -1 : ((m >> rc) & 1);
-				if(mt != 1) {
-					push(row, 3, mask2dna(m), "ACGTN"[rc]);
-					w.score -= (rc > 3 || m > 15) ? C.npen : C.mmpen[q];
+					if(mt == -1) w.ns++;
+					row--; col--;
+					st = ST_H;
+				} else if(mv <= 2) {
+					push(row, 2, '-', "ACGTN"[rc]);
+					w.score -= mv == 1 ? rfgo : rfge;
+					st = mv == 1 ? ST_H : ST_F;
+					row--; w.gaps++;
 				} else {
-					w.score += C.match;
+					push(row + 1, 1, mask2dna(m), '-');
+					w.score -= mv == 3 ? rdgo : rdge;
+					st = mv == 3 ? ST_H : ST_E;
+					col--; w.gaps++;
 				}
-				if(mt == -1) w.ns++;
-				row--; col--;
-				st = ST_H;
-			} else if(mv <= 2) {
-				push(row, 2, '-', "ACGTN"[rc]);
-				w.score -= mv == 1 ? rfgo : rfge;
-				st = mv == 1 ? ST_H : ST_F;
-				row--; w.gaps++;
-			} else {
-				push(row + 1, 1, mask2dna(m), '-');
-				w.score -= mv == 3 ? rdgo : rdge;
-				st = mv == 3 ? ST_H : ST_E;
-				col--; w.gaps++;
+				cur = nxt;
 			}
-			cur = nxt;
 		}
 		} while(!ended && ++ks < (FLAT ? 1u : (uint32_t)BT2G_BT_EE_STEPS));
 		if(!ended) continue;

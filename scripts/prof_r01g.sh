@@ -1,11 +1,11 @@
 # Round-1 final evidence (r01g): GPU tests, kernel-trace stats, separate FETCH_SIZE / WRITE_SIZE
 # passes, then the bench line with roofline.traffic from those passes.
-# Usage (on the GPU box): bash scripts/prof_r01g.sh
+# Usage (on the GPU box): bash scripts/prof_r01g.sh [tag]
 set -e
 cd /tmp && export TMPDIR=/tmp
 cd $GRAFT_REPO_ROOT
 mkdir -p gpurun_out
-O=gpurun_out/r01g
+O=gpurun_out/${1:-r01g}
 mkdir -p $O
 B="bench.py --no-cpu-baseline --index-cache /tmp/bench_idx"
 timeout -k 10 400 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread > $O/tests.log 2>&1
