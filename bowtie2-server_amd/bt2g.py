@@ -320,6 +320,14 @@ class Engine:
         return probs, rects, ok
 
     # ---- measurement -------------------------------------------------------
+    def reserve_sw(self, max_problems, max_cols):
+        """Persistent fill scratch (bt2g_reserve_sw)."""
+        _chk(lib().bt2g_reserve_sw(self.h, max_problems, max_cols))
+
+    def reserve_sw_bt(self, max_problems, max_rows, max_cols, hbytes):
+        """Persistent fill + backtrace scratch (bt2g_reserve_sw_bt)."""
+        _chk(lib().bt2g_reserve_sw_bt(self.h, max_problems, max_rows, max_cols, hbytes))
+
     def set_profiling(self, on=True):
         _chk(lib().bt2g_set_profiling(self.h, int(on)))
 

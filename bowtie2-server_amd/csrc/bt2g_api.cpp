@@ -332,6 +332,7 @@ int bt2g_close(bt2g_ctx* c) {
 	for(hipEvent_t e : c->evpool) (void)hipEventDestroy(e);
 	for(void* p : c->owned) (void)hipFree(p);
 	if(c->sw_lists) { (void)hipFree(c->sw_lists); (void)hipFree(c->sw_counts); (void)hipFree(c->sw_bnd); }
+	if(c->bt_plane) { (void)hipFree(c->bt_plane); (void)hipFree(c->bt_marks); }
 	if(c->stream) (void)hipStreamDestroy(c->stream);
 	delete c;
 	return BT2G_OK;
@@ -532,7 +533,11 @@ static int sw_align_impl(bt2g_ctx* c, const uint8_t* reads, const uint8_t* quals
 	uint32_t maxcol = maxcol_hint;
 	const bool reserved = nprob <= c->sw_max_prob && c->sw_lists && (maxcol == 0 || maxcol <= c->sw_max_cols);
 	if(reserved) {
-		lists = c->sw_lists; counts = c->sw_counts; bnd = c->sw_bnd; maxcol = c->sw_max_cols;
+		// the reserved boundary scratch is sw_max_cols wide; a caller's width hint
+		// (the backtrace's score-plane pitch) stays the launch width, since the
+		// plane was laid out with it
+		lists = c->sw_lists; counts = c->sw_counts; bnd = c->sw_bnd;
+		if(maxcol == 0) maxcol = c->sw_max_cols;
 	} else {
 		if(maxcol == 0) {
 			// widest problem decides the boundary buffer width (problems live on the device)
@@ -743,12 +748,24 @@ int bt2g_reserve_sw_bt(bt2g_ctx* c, uint32_t max_problems, uint32_t max_stride, 
 	if(!c || max_problems == 0 || max_cols == 0 || max_stride == 0 || (hbytes != 1 && hbytes != 2))
 		return fail(BT2G_ERR_ARG, "bad reservation");
 	if(int rc = bt2g_reserve_sw(c, max_problems, max_cols)) return rc;
+	// bt2g_reserve_sw synchronised the device: the old scratch is idle
 	if(c->bt_plane) { (void)hipFree(c->bt_plane); (void)hipFree(c->bt_marks); }
 	c->bt_plane = nullptr; c->bt_marks = nullptr;
+	c->bt_max_prob = c->bt_max_stride = c->bt_max_cols = 0;
+	c->bt_hbytes = 0;
 	const uint64_t slot = sw_plane_slot(max_stride, max_cols, hbytes);
-	HIPCHK(hipMalloc((void**)&c->bt_plane, slot * max_problems));
-	HIPCHK(hipMalloc((void**)&c->bt_marks,
-	                 sizeof(uint32_t) * sw_bt_mslot(max_stride, max_cols, hbytes == 2) * max_problems));
+	uint8_t* plane = nullptr;
+	uint32_t* marks = nullptr;
+	hipError_t e = hipMalloc((void**)&plane, slot * max_problems);
+	if(e == hipSuccess)
+		e = hipMalloc((void**)&marks, sizeof(uint32_t) * sw_bt_mslot(max_stride, max_cols, hbytes == 2) * max_problems);
+	if(e != hipSuccess) {
+		if(plane) (void)hipFree(plane);
+		return fail(BT2G_ERR_NOMEM, "bt2g_reserve_sw_bt: %s", hipGetErrorString(e));
+	}
+	// commit only after every allocation succeeded
+	c->bt_plane = plane;
+	c->bt_marks = marks;
 	c->bt_max_prob = max_problems;
 	c->bt_max_stride = max_stride;
 	c->bt_max_cols = max_cols;
@@ -762,10 +779,20 @@ int bt2g_reserve_sw(bt2g_ctx* c, uint32_t max_problems, uint32_t max_cols) {
 	HIPCHK(hipDeviceSynchronize());   // the old scratch may be in use on any stream
 	if(c->sw_lists) { (void)hipFree(c->sw_lists); (void)hipFree(c->sw_counts); (void)hipFree(c->sw_bnd); }
 	c->sw_lists = c->sw_counts = c->sw_bnd = nullptr;
+	c->sw_max_prob = c->sw_max_cols = 0;
 	size_t nblk = ((size_t)max_problems + 63) / 64;
-	HIPCHK(hipMalloc((void**)&c->sw_lists, sizeof(uint32_t) * (size_t)max_problems * 3));
-	HIPCHK(hipMalloc((void**)&c->sw_counts, sizeof(uint32_t) * 8));
-	HIPCHK(hipMalloc((void**)&c->sw_bnd, sizeof(uint32_t) * nblk * (size_t)max_cols * 64 * 2));
+	uint32_t *lists = nullptr, *counts = nullptr, *bnd = nullptr;
+	hipError_t e = hipMalloc((void**)&lists, sizeof(uint32_t) * (size_t)max_problems * 3);
+	if(e == hipSuccess) e = hipMalloc((void**)&counts, sizeof(uint32_t) * 8);
+	if(e == hipSuccess) e = hipMalloc((void**)&bnd, sizeof(uint32_t) * nblk * (size_t)max_cols * 64 * 2);
+	if(e != hipSuccess) {
+		if(lists) (void)hipFree(lists);
+		if(counts) (void)hipFree(counts);
+		return fail(BT2G_ERR_NOMEM, "bt2g_reserve_sw: %s", hipGetErrorString(e));
+	}
+	c->sw_lists = lists;
+	c->sw_counts = counts;
+	c->sw_bnd = bnd;
 	c->sw_max_prob = max_problems;
 	c->sw_max_cols = max_cols;
 	return BT2G_OK;

@@ -165,3 +165,43 @@ def test_bt_maxaln_truncates(eng):
     for p in np.nonzero(has)[0]:
         ne = int(full[3]["nedit"][p, 0])
         assert np.array_equal(one[4][p, 0, :ne], full[4][p, 0, :ne]), p
+
+
+@pytest.mark.parametrize("case", ["reserve_sw", "reserve_bt_u8_then_local", "reserve_narrow_stride"])
+def test_bt_after_reservation(case):
+    """Backtrace calls after bt2g_reserve_sw / bt2g_reserve_sw_bt whose
+    reservation does not match the call: the score plane keeps the
+    call's own pitch, so the results equal the unreserved run's and the oracle's."""
+    import bt2g
+    from oracle.oracle import Oracle
+    orc = Oracle()
+    gen = get_index("lambda").ref_codes[0]
+    local = case == "reserve_bt_u8_then_local"
+    codes, quals, lens, probs, rects = _synth_problems(gen, 256, 41, minsc=60 if local else -90)
+    with bt2g.Engine(index=get_index("lambda")) as e:
+        if case == "reserve_sw":
+            e.reserve_sw(1024, 400)          # wider than the problems (210 columns)
+        elif case == "reserve_bt_u8_then_local":
+            e.reserve_sw_bt(1024, 150, 210, 1)
+        else:
+            e.reserve_sw_bt(1024, 100, 210, 1)   # stride 150 > reserved rows
+        res, cands, naln, alns, edits, fates = e.sw_align_bt(codes, quals, lens, probs, rects=rects, local=local,
+                                                             cap=4096, maxaln=512, maxedit=512)
+    ea, ee, ef = _oracle_expect(orc, gen, codes, quals, probs, rects, local)
+    check_against(naln, alns, edits, fates, res, None, ea, ee, ef, case)
+    assert (naln > 0).sum() > 150
+
+
+def test_close_frees_reserved_scratch():
+    """bt2g_close releases the backtrace scratch of bt2g_reserve_sw_bt:
+    repeated open / reserve / close cycles do not lose device memory."""
+    import torch
+    import bt2g
+    idx = get_index("lambda")
+    free = []
+    for _ in range(4):
+        with bt2g.Engine(index=idx) as e:
+            e.reserve_sw_bt(200_000, 150, 210, 1)     # ~8 GB of plane + marks
+        torch.cuda.synchronize()
+        free.append(torch.cuda.mem_get_info()[0])
+    assert max(free) - min(free) < (1 << 30), free
