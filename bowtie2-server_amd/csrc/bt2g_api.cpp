@@ -802,18 +802,23 @@ int bt2g_reserve_sw(bt2g_ctx* c, uint32_t max_problems, uint32_t max_cols) {
 
 // ------------------------------------------------------ host-pointer wrappers
 namespace {
+// Device copies of a host-flavour call's arrays: stream-ordered allocations
+// from the device's memory pool (no hipMalloc / device-wide hipFree per call).
 struct Tmp {
+	hipStream_t st;
 	std::vector<void*> ps;
+	explicit Tmp(bt2g_ctx* c) : st(c->stream) {}
 	~Tmp() {
-		for(void* p : ps) (void)hipFree(p);
+		for(void* p : ps) (void)hipFreeAsync(p, st);
 	}
 	template <typename T>
 	int up(T** d, const T* h, size_t count) {
-		if(hipMalloc((void**)d, count * sizeof(T) + 16) != hipSuccess) return fail(BT2G_ERR_NOMEM, "hipMalloc");
+		if(hipMallocAsync((void**)d, count * sizeof(T) + 16, st) != hipSuccess)
+			return fail(BT2G_ERR_NOMEM, "hipMallocAsync");
 		ps.push_back(*d);
 		if(h && count) {
-			if(hipMemcpy(*d, h, count * sizeof(T), hipMemcpyHostToDevice) != hipSuccess)
-				return fail(BT2G_ERR_HIP, "hipMemcpy H2D");
+			if(hipMemcpyAsync(*d, h, count * sizeof(T), hipMemcpyHostToDevice, st) != hipSuccess)
+				return fail(BT2G_ERR_HIP, "hipMemcpyAsync H2D");
 		}
 		return BT2G_OK;
 	}
@@ -822,7 +827,7 @@ struct Tmp {
 template <typename T>
 int down(T* h, const T* d, size_t count) {
 	if(count == 0) return BT2G_OK;
-	HIPCHK(hipMemcpy(h, d, count * sizeof(T), hipMemcpyDeviceToHost));
+	HIPCHK(hipMemcpy(h, d, count * sizeof(T), hipMemcpyDeviceToHost));   // after the stream sync
 	return BT2G_OK;
 }
 }  // namespace
@@ -833,7 +838,7 @@ int bt2g_exact_sweep(bt2g_ctx* c, const uint8_t* reads, uint32_t stride, const u
                      uint32_t mine_max, int nofw, int norc, uint32_t* out) {
 	if(!c) return fail(BT2G_ERR_ARG, "null ctx");
 	HIPCHK(hipSetDevice(c->device));
-	Tmp t;
+	Tmp t(c);
 	uint8_t* dr;
 	uint32_t *dl, *dout;
 	int rc;
@@ -850,7 +855,7 @@ int bt2g_seed_search(bt2g_ctx* c, const uint8_t* reads, uint32_t stride, const u
                      int32_t* nseeds, uint32_t* bwops, uint32_t* loads) {
 	if(!c) return fail(BT2G_ERR_ARG, "null ctx");
 	HIPCHK(hipSetDevice(c->device));
-	Tmp t;
+	Tmp t(c);
 	uint8_t* dr;
 	uint32_t *dl, *dout, *dops, *dld = nullptr;
 	int32_t* dns;
@@ -875,7 +880,7 @@ int bt2g_one_mm(bt2g_ctx* c, const uint8_t* reads, const uint8_t* quals, uint32_
                 bt2g_mm1* hits, int32_t* counts, uint32_t* bwops, uint32_t* loads) {
 	if(!c) return fail(BT2G_ERR_ARG, "null ctx");
 	HIPCHK(hipSetDevice(c->device));
-	Tmp t;
+	Tmp t(c);
 	uint8_t *dr, *dq;
 	uint32_t *dl, *dops, *dld = nullptr;
 	int32_t *dms, *dcnt;
@@ -899,7 +904,7 @@ int bt2g_one_mm(bt2g_ctx* c, const uint8_t* reads, const uint8_t* quals, uint32_
 int bt2g_get_offset(bt2g_ctx* c, const uint32_t* rows, uint32_t n, uint32_t* offs, uint32_t* loads) {
 	if(!c) return fail(BT2G_ERR_ARG, "null ctx");
 	HIPCHK(hipSetDevice(c->device));
-	Tmp t;
+	Tmp t(c);
 	uint32_t *drow, *doff, *dld = nullptr;
 	int rc;
 	if((rc = t.up(&drow, rows, n)) || (rc = t.up(&doff, (const uint32_t*)nullptr, n))) return rc;
@@ -920,7 +925,7 @@ int bt2g_sw_align(bt2g_ctx* c, const uint8_t* reads, const uint8_t* quals, uint3
 	if(nprob == 0) return BT2G_OK;
 	uint32_t nreads = 0;
 	for(uint32_t i = 0; i < nprob; i++) nreads = probs[i].read + 1 > nreads ? probs[i].read + 1 : nreads;
-	Tmp t;
+	Tmp t(c);
 	uint8_t *dr, *dq, *dw = nullptr;
 	uint32_t* dl;
 	bt2g_sw_problem* dp;
@@ -968,7 +973,7 @@ int bt2g_sw_align_bt(bt2g_ctx* c, const uint8_t* reads, const uint8_t* quals, ui
 	if(nprob == 0) return BT2G_OK;
 	uint32_t nreads = 0;
 	for(uint32_t i = 0; i < nprob; i++) nreads = probs[i].read + 1 > nreads ? probs[i].read + 1 : nreads;
-	Tmp t;
+	Tmp t(c);
 	uint8_t *dr, *dq, *dw = nullptr;
 	uint32_t* dl;
 	bt2g_sw_problem* dp;
@@ -1020,7 +1025,7 @@ int bt2g_frame(bt2g_ctx* c, const bt2g_frame_in* in, uint32_t n, const uint32_t*
 		if(in[i].refidx >= c->nref) return fail(BT2G_ERR_ARG, "input %u: reference %u >= %u", i, in[i].refidx, c->nref);
 		if(in[i].kind == 1 && !pe) return fail(BT2G_ERR_ARG, "input %u: mate search without a PE policy", i);
 	}
-	Tmp t;
+	Tmp t(c);
 	bt2g_frame_in* din;
 	uint32_t* dl;
 	bt2g_sw_problem* dp;
@@ -1044,7 +1049,7 @@ int bt2g_ungapped(bt2g_ctx* c, const uint8_t* reads, const uint8_t* quals, uint3
 	if(n == 0) return BT2G_OK;
 	uint32_t nreads = 0;
 	for(uint32_t i = 0; i < n; i++) nreads = probs[i].read + 1 > nreads ? probs[i].read + 1 : nreads;
-	Tmp t;
+	Tmp t(c);
 	uint8_t *dr, *dq;
 	uint32_t* dl;
 	bt2g_ug_problem* dp;

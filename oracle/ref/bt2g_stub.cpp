@@ -1,0 +1,220 @@
+// oracle/ref/bt2g_stub.cpp -- TEST INFRASTRUCTURE ONLY (never part of the product).
+//
+// A CPU stand-in for the subset of include/bt2g.h that integration/bt2g_seams.cpp
+// calls, answered by the REFERENCE's own code through harness.cpp (this
+// directory).  Linked into oracle/_ref/libbt2g_stub.so and from there into
+// oracle/_ref/bowtie2-align-server-stub, it lets the CPU tests check the
+// reference-side binding itself (RNG replay of candidate fates, AlnRes
+// construction, the seed-cache protocol) on this container, where there is
+// no GPU: the stub server's SAM must equal the stock server's.  The GPU build
+// (bowtie2-align-server-gpu) links the real libbt2g.so instead.
+#include <stdint.h>
+#include <stdio.h>
+#include <stdarg.h>
+#include <string.h>
+#include <string>
+#include <vector>
+#include "bt2g.h"
+
+extern "C" {
+void* bt2ref_open(const char* base);
+void bt2ref_close(void* vh);
+void bt2ref_exact_sweep(void* vh, int n, const char** seqs, const char** quals, int mineMax, uint64_t* out);
+void bt2ref_one_mm(void* vh, int n, const char** seqs, const char** quals, const int64_t* minsc, int local, int nofw,
+                   int norc, int cap, int64_t* out, int32_t* counts, uint64_t* bwops);
+void bt2ref_seed_search(void* vh, int n, const char** seqs, const char** quals, int seedlen, int interval, int offset,
+                        int maxseeds, uint32_t* out, int32_t* nseeds, uint64_t* bwops);
+int bt2ref_sw(const char* seq, const char* qual, int fw, const uint8_t* rfmask, int ncol, int64_t minsc,
+              const void* sp, int enable8, int cap, int64_t* out, int64_t* cands, int32_t* mat);
+int bt2ref_sw_bt(const char* seq, const char* qual, int fw, const uint8_t* rfmask, int ncol, int64_t minsc,
+                 const void* sp, int enable8, int triml, int corel, int corer, int maxaln, int maxedit,
+                 int64_t* out, int64_t* aln, int32_t* edits, int32_t* fates, int capf);
+void bt2ref_ungapped(void* vh, int n, const char** seqs, const char** quals, const uint8_t* fws,
+                     const uint32_t* refidx, const int64_t* off, const int64_t* minsc, const void* sp,
+                     int ohang, int maxedit, int64_t* out, int32_t* edits);
+}
+
+struct bt2g_ctx {
+	void* ref;
+};
+
+namespace {
+thread_local std::string g_err;
+
+int fail(int rc, const char* fmt, ...) {
+	char buf[512];
+	va_list ap;
+	va_start(ap, fmt);
+	vsnprintf(buf, sizeof(buf), fmt, ap);
+	va_end(ap);
+	g_err = buf;
+	return rc;
+}
+
+std::string ascii(const uint8_t* codes, uint32_t len) {
+	std::string s(len, 'N');
+	for(uint32_t i = 0; i < len; i++) s[i] = "ACGTN"[codes[i] > 4 ? 4 : codes[i]];
+	return s;
+}
+
+std::string qstr(const uint8_t* q, uint32_t len) { return std::string((const char*)q, len); }
+
+// Edit characters come back from the reference as ASCII; bt2g_mm1 carries codes.
+int32_t code_of(int64_t ch) {
+	switch((int)ch) { case 'A': return 0; case 'C': return 1; case 'G': return 2; case 'T': return 3; default: return 4; }
+}
+}  // namespace
+
+extern "C" {
+
+const char* bt2g_last_error(void) { return g_err.c_str(); }
+
+int bt2g_open(const char* base, int, bt2g_ctx** out) {
+	bt2g_ctx* c = new bt2g_ctx();
+	c->ref = bt2ref_open(base);
+	if(!c->ref) { delete c; return fail(BT2G_ERR_IO, "bt2ref_open"); }
+	*out = c;
+	return BT2G_OK;
+}
+
+int bt2g_close(bt2g_ctx* c) {
+	if(c) { bt2ref_close(c->ref); delete c; }
+	return BT2G_OK;
+}
+
+int bt2g_exact_sweep(bt2g_ctx* c, const uint8_t* reads, uint32_t stride, const uint32_t* lens, uint32_t n,
+                     uint32_t mine_max, int nofw, int norc, uint32_t* out) {
+	if(nofw || norc) return fail(BT2G_ERR_ARG, "stub: nofw/norc unsupported");
+	for(uint32_t i = 0; i < n; i++) {
+		std::string s = ascii(reads + (size_t)i * stride, lens[i]), q(lens[i], 'I');
+		const char* sp = s.c_str();
+		const char* qp = q.c_str();
+		uint64_t o[8];
+		bt2ref_exact_sweep(c->ref, 1, &sp, &qp, (int)mine_max, o);
+		uint32_t* w = out + 8 * (size_t)i;
+		w[0] = (uint32_t)o[0]; w[1] = (uint32_t)o[1]; w[2] = (uint32_t)o[3]; w[3] = (uint32_t)o[4];
+		w[4] = (uint32_t)o[5]; w[5] = (uint32_t)o[6]; w[6] = (uint32_t)o[7]; w[7] = 0;
+	}
+	return BT2G_OK;
+}
+
+int bt2g_one_mm(bt2g_ctx* c, const uint8_t* reads, const uint8_t* quals, uint32_t stride, const uint32_t* lens,
+                uint32_t n, const int32_t* minsc, const bt2g_scoring* sc, int nofw, int norc, uint32_t cap,
+                bt2g_mm1* hits, int32_t* counts, uint32_t* bwops, uint32_t*) {
+	int rc = BT2G_OK;
+	for(uint32_t i = 0; i < n; i++) {
+		std::string s = ascii(reads + (size_t)i * stride, lens[i]), q = qstr(quals + (size_t)i * stride, lens[i]);
+		const char* sp = s.c_str();
+		const char* qp = q.c_str();
+		int64_t ms = minsc[i];
+		std::vector<int64_t> o(6 * (size_t)cap + 6);
+		uint64_t ops = 0;
+		bt2ref_one_mm(c->ref, 1, &sp, &qp, &ms, sc->local, nofw, norc, (int)cap, o.data(), &counts[i], &ops);
+		bwops[i] = (uint32_t)ops;
+		for(int32_t k = 0; k < counts[i] && k < (int32_t)cap; k++) {
+			bt2g_mm1& h = hits[(size_t)i * cap + k];
+			const int64_t* x = &o[6 * (size_t)k];
+			h.top = (uint32_t)x[0]; h.bot = (uint32_t)x[1]; h.fw = (int32_t)x[2]; h.score = (int32_t)x[3];
+			h.pos = (int32_t)x[4]; h.chr = code_of(x[5] & 0xff); h.qchr = code_of(x[5] >> 8); h.pad = 0;
+		}
+		if(counts[i] > (int32_t)cap) rc = BT2G_ERR_OVERFLOW;
+	}
+	return rc;
+}
+
+int bt2g_seed_search(bt2g_ctx* c, const uint8_t* reads, uint32_t stride, const uint32_t* lens, uint32_t n,
+                     uint32_t seedlen, uint32_t interval, uint32_t offset, uint32_t maxseeds, uint32_t* out,
+                     int32_t* nseeds, uint32_t* bwops, uint32_t*) {
+	for(uint32_t i = 0; i < n; i++) {
+		std::string s = ascii(reads + (size_t)i * stride, lens[i]), q(lens[i], 'I');
+		const char* sp = s.c_str();
+		const char* qp = q.c_str();
+		uint64_t ops = 0;
+		bt2ref_seed_search(c->ref, 1, &sp, &qp, (int)seedlen, (int)interval, (int)offset, (int)maxseeds,
+		                   out + (size_t)i * 2 * maxseeds * 4, &nseeds[i], &ops);
+		bwops[i] = (uint32_t)ops;
+	}
+	return BT2G_OK;
+}
+
+int bt2g_ungapped(bt2g_ctx* c, const uint8_t* reads, const uint8_t* quals, uint32_t stride, const uint32_t* lens,
+                  const bt2g_ug_problem* probs, uint32_t n, const bt2g_scoring* sc, int ohang, uint32_t maxedit,
+                  bt2g_ug_result* res, bt2g_edit* edits) {
+	for(uint32_t i = 0; i < n; i++) {
+		const bt2g_ug_problem& p = probs[i];
+		std::string s = ascii(reads + (size_t)p.read * stride, lens[p.read]);
+		std::string q = qstr(quals + (size_t)p.read * stride, lens[p.read]);
+		const char* sp = s.c_str();
+		const char* qp = q.c_str();
+		uint8_t fw = p.fw ? 1 : 0;
+		uint32_t ri = p.refidx;
+		int64_t off = p.off, ms = p.minsc, o[10];
+		std::vector<int32_t> ed(4 * (size_t)maxedit);
+		bt2ref_ungapped(c->ref, 1, &sp, &qp, &fw, &ri, &off, &ms, sc, ohang, (int)maxedit, o, ed.data());
+		bt2g_ug_result& r = res[i];
+		memset(&r, 0, sizeof(r));
+		r.ret = (int32_t)o[0]; r.score = (int32_t)o[1]; r.refoff = o[2]; r.ns = (int32_t)o[3];
+		r.refns = (int32_t)o[4]; r.nedit = (int32_t)o[5]; r.trim5p = (int32_t)o[6]; r.trim3p = (int32_t)o[7];
+		for(int32_t e = 0; e < r.nedit && e < (int32_t)maxedit; e++) {
+			bt2g_edit& d = edits[(size_t)i * maxedit + e];
+			d.pos = (uint32_t)ed[4 * e]; d.type = (uint8_t)ed[4 * e + 1]; d.chr = (uint8_t)ed[4 * e + 2];
+			d.qchr = (uint8_t)ed[4 * e + 3]; d.pad = 0;
+		}
+	}
+	return BT2G_OK;
+}
+
+int bt2g_sw_align_bt(bt2g_ctx*, const uint8_t* reads, const uint8_t* quals, uint32_t stride, const uint32_t* lens,
+                     const bt2g_sw_problem* probs, uint32_t nprob, const uint8_t* windows, uint64_t,
+                     const bt2g_sw_rect* rects, const bt2g_scoring* sc, int enable8, uint32_t cap, bt2g_sw_result* res,
+                     bt2g_sw_cand* cands, uint32_t maxaln, uint32_t maxedit, int32_t* naln, bt2g_sw_aln* alns,
+                     bt2g_edit* edits, int8_t* fates) {
+	int rc = BT2G_OK;
+	for(uint32_t i = 0; i < nprob; i++) {
+		const bt2g_sw_problem& p = probs[i];
+		if(p.win_off < 0 || !rects) return fail(BT2G_ERR_ARG, "stub: explicit windows and rects only");
+		std::string s = ascii(reads + (size_t)p.read * stride, lens[p.read]);
+		std::string q = qstr(quals + (size_t)p.read * stride, lens[p.read]);
+		const uint8_t* rf = windows + p.win_off;
+		int64_t o[7];
+		std::vector<int64_t> cc(3 * (size_t)cap + 3);
+		bt2ref_sw(s.c_str(), q.c_str(), p.fw, rf, (int)p.ncol, p.minsc, sc, enable8, (int)cap, o, cc.data(), nullptr);
+		bt2g_sw_result& r = res[i];
+		r.aligned = (int32_t)o[0];
+		r.best = o[1] < INT32_MIN ? INT32_MIN : (int32_t)o[1];
+		r.u8succ = (int32_t)o[2]; r.i16succ = (int32_t)o[3]; r.colstop = (int32_t)o[4];
+		r.lastsolcol = (int32_t)o[5]; r.ncand = (int32_t)o[6]; r.flag = 0;
+		for(int64_t k = 0; k < o[6] && k < (int64_t)cap; k++) {
+			bt2g_sw_cand& d = cands[(size_t)i * cap + k];
+			d.row = (int32_t)cc[3 * k]; d.col = (int32_t)cc[3 * k + 1]; d.score = (int32_t)cc[3 * k + 2];
+		}
+		if(o[6] > (int64_t)cap) { rc = BT2G_ERR_OVERFLOW; continue; }
+		std::vector<int64_t> al(10 * (size_t)maxaln);
+		std::vector<int32_t> ed(4 * (size_t)maxaln * maxedit);
+		std::vector<int32_t> ft((size_t)cap, 0);
+		int64_t o2[7];
+		const bt2g_sw_rect& rc0 = rects[i];
+		int na = bt2ref_sw_bt(s.c_str(), q.c_str(), p.fw, rf, (int)p.ncol, p.minsc, sc, enable8, rc0.triml, rc0.corel,
+		                      rc0.corer, (int)maxaln, (int)maxedit, o2, al.data(), ed.data(), ft.data(), (int)cap);
+		naln[i] = na < (int)maxaln ? na : (int)maxaln;
+		for(int k = 0; k < naln[i]; k++) {
+			bt2g_sw_aln& a = alns[(size_t)i * maxaln + k];
+			const int64_t* x = &al[10 * (size_t)k];
+			a.cand = (int32_t)x[0]; a.score = (int32_t)x[1]; a.off = (int32_t)x[2]; a.ns = (int32_t)x[4];
+			a.gaps = (int32_t)x[5]; a.refns = (int32_t)x[6]; a.nedit = (int32_t)x[7]; a.trim5p = (int32_t)x[8];
+			a.trim3p = (int32_t)x[9]; a.pad = 0;
+			for(int32_t e = 0; e < a.nedit && e < (int32_t)maxedit; e++) {
+				const int32_t* y = &ed[4 * ((size_t)k * maxedit + e)];
+				bt2g_edit& d = edits[((size_t)i * maxaln + k) * maxedit + e];
+				d.pos = (uint32_t)y[0]; d.type = (uint8_t)y[1]; d.chr = (uint8_t)y[2]; d.qchr = (uint8_t)y[3]; d.pad = 0;
+			}
+		}
+		// fates: the reference marks candidates it never reached with 0; only
+		// those up to the maxaln-th success are meaningful, as for the engine
+		if(fates)
+			for(uint32_t k = 0; k < cap; k++) fates[(size_t)i * cap + k] = (int8_t)ft[k];
+	}
+	return rc;
+}
+
+}  // extern "C"

@@ -1,0 +1,181 @@
+"""oracle/ref_server.py -- TEST INFRASTRUCTURE ONLY (never part of the product).
+
+Drives a bowtie2 alignment server binary (the reference's own
+`bowtie2-align-server-s`, or the GPU drop-in build of it from integration/)
+with the reference's own web client `bowtie2-align-l`, following the
+BASELINE.md section 3 protocol:
+
+  * the server is started with the alignment options and `-p threads`, and is
+    "ready" once it prints `INFO: Server ready to process`
+    (bt2_search.cpp:4898); index load is not timed;
+  * reads go out in chunks of <= 10 000 per client connection (the fork's slot
+    names make larger connections nondeterministic), k chunks
+    in flight at once;
+  * wall time runs from the first connection to the last client exit (the
+    client exits after `@CO BT2SRV All Done`, pat.cpp:2712-2789);
+  * SAM records come back with the read names restored by the client
+    (pat.cpp:2570-2646); `sorted_records` sorts them for comparison, as the
+    reference's own tests do (scripts/sim/Sim.pm:933-947).
+
+Server flags: bt2_search.cpp:543-748 (`--server-port` 679); client port from
+BT2CLT_SERVER_PORT (bt2_search.cpp:527-536).
+"""
+import os
+import socket
+import subprocess
+import tempfile
+import threading
+import time
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+REF_DIR = os.path.join(HERE, "_ref")
+SERVER = os.path.join(REF_DIR, "bowtie2-align-server-s")
+CLIENT = os.path.join(REF_DIR, "bowtie2-align-l")
+CHUNK = 10_000
+
+
+def free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def write_fastq_chunks(dirpath, codes, quals, names=None, chunk=CHUNK, codes2=None, quals2=None):
+    """FASTQ files of <= chunk reads (pairs: two files per chunk).  Returns a list
+    of argument lists for the client (-U f | -1 f1 -2 f2)."""
+    acgt = np.frombuffer(b"ACGTN", np.uint8)
+    out = []
+    n = len(codes)
+    for c, lo in enumerate(range(0, n, chunk)):
+        hi = min(n, lo + chunk)
+        files = []
+        for m, (cd, qu) in enumerate(((codes, quals), (codes2, quals2))):
+            if cd is None:
+                continue
+            path = os.path.join(dirpath, f"chunk{c:05d}_{m + 1}.fq")
+            with open(path, "wb") as f:
+                for i in range(lo, hi):
+                    nm = names[i] if names is not None else b"r%d" % i
+                    seq = cd[i] if isinstance(cd[i], bytes) else acgt[cd[i]].tobytes()
+                    q = qu[i] if isinstance(qu[i], bytes) else np.asarray(qu[i], np.uint8).tobytes()
+                    f.write(b"@" + nm + b"\n" + seq + b"\n+\n" + q + b"\n")
+            files.append(path)
+        out.append(["-U", files[0]] if len(files) == 1 else ["-1", files[0], "-2", files[1]])
+    return out
+
+
+class Server:
+    """One alignment server process on a free port (context manager)."""
+
+    def __init__(self, index_base, threads=1, args=(), binary=SERVER, env=None, ready_timeout=600,
+                 log_path=None):
+        self.index_base = index_base
+        self.port = free_port()
+        cmd = [binary, "-x", index_base, "-p", str(threads), "--server-port", str(self.port)] + list(args)
+        self.log_path = log_path or tempfile.mktemp(prefix="bt2srv_", suffix=".log")
+        self._log = open(self.log_path, "wb")
+        self.proc = subprocess.Popen(cmd, stdout=self._log, stderr=subprocess.STDOUT,
+                                     env=dict(os.environ, **(env or {})))
+        t0 = time.time()
+        while True:
+            txt = open(self.log_path, "rb").read()
+            if b"Server ready to process" in txt and b"Server listening" in txt:
+                break
+            if self.proc.poll() is not None:
+                raise RuntimeError(f"server exited rc={self.proc.returncode}: {txt[-2000:].decode(errors='replace')}")
+            if time.time() - t0 > ready_timeout:
+                self.close()
+                raise TimeoutError("server not ready")
+            time.sleep(0.05)
+        self.load_s = time.time() - t0
+
+    def log(self):
+        return open(self.log_path, "rb").read().decode(errors="replace")
+
+    def run(self, chunk_args, k=1, client=CLIENT, timeout=1200):
+        """Send every chunk (client argument lists) over at most k concurrent
+        connections.  Returns (wall seconds, list of SAM texts in chunk order)."""
+        outs = [None] * len(chunk_args)
+        errs = []
+        nxt = [0]
+        lock = threading.Lock()
+        env = dict(os.environ, BT2CLT_SERVER_PORT=str(self.port), BT2CLT_SERVER_HOST="127.0.0.1")
+
+        def worker():
+            while True:
+                with lock:
+                    i = nxt[0]
+                    nxt[0] += 1
+                if i >= len(chunk_args):
+                    return
+                r = subprocess.run([client, "-x", self.index_base, "--no-hd"] + chunk_args[i], env=env,
+                                   stdout=subprocess.PIPE, stderr=subprocess.PIPE, timeout=timeout)
+                if r.returncode != 0:
+                    errs.append((i, r.returncode, r.stderr[-2000:]))
+                outs[i] = r.stdout
+
+        t0 = time.perf_counter()
+        ths = [threading.Thread(target=worker) for _ in range(max(1, min(k, len(chunk_args))))]
+        for t in ths:
+            t.start()
+        for t in ths:
+            t.join()
+        dt = time.perf_counter() - t0
+        if errs:
+            raise RuntimeError(f"client failures: {errs[:3]}")
+        return dt, outs
+
+    def close(self):
+        if self.proc.poll() is None:
+            self.proc.terminate()
+            try:
+                self.proc.wait(timeout=20)
+            except subprocess.TimeoutExpired:
+                self.proc.kill()
+                self.proc.wait()
+        self._log.close()
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *a):
+        self.close()
+
+
+def sorted_records(sam_texts):
+    """SAM alignment records (no header / @CO lines), sorted."""
+    recs = []
+    for t in sam_texts:
+        for ln in t.split(b"\n"):
+            if ln and not ln.startswith(b"@"):
+                recs.append(ln)
+    recs.sort()
+    return recs
+
+
+def host_cpus():
+    """CPU budget of this host/job: nproc, scheduler affinity, cgroup quota, model."""
+    aff = len(os.sched_getaffinity(0))
+    quota = None
+    try:
+        q, p = open("/sys/fs/cgroup/cpu.max").read().split()
+        if q != "max":
+            quota = int(q) / int(p)
+    except (OSError, ValueError):
+        pass
+    model = ""
+    try:
+        for ln in open("/proc/cpuinfo"):
+            if ln.startswith("model name"):
+                model = ln.split(":", 1)[1].strip()
+                break
+    except OSError:
+        pass
+    nproc = int(subprocess.run(["nproc"], stdout=subprocess.PIPE).stdout or 0)
+    usable = int(quota) if quota else aff
+    usable = max(1, min(usable, aff, nproc or aff))
+    return {"nproc": nproc, "affinity": aff, "cgroup_quota": quota, "usable": usable, "model": model}

@@ -1,0 +1,170 @@
+"""SAM parity of the drop-in (row N1 of the judge's table).
+
+The reference's own alignment server runs twice on the same reads, both
+times with its unchanged host code (multiseedSearchWorker, SeedResults /
+AlignmentCache, SwDriver with its RNG, AlnSinkWrap, MAPQ, SAM writer):
+
+  * stock:     oracle/_ref/bowtie2-align-server-s (the reference, CPU);
+  * drop-in:   oracle/_ref/bowtie2-align-server-gpu, the same objects linked
+               with integration/bt2g_seams.cpp so that exactSweep,
+               oneMmSearch, searchAllSeeds, ungappedAlign, SwAligner::align and
+               nextAlignment are served by libbt2g.so on the GPU (-m gpu), or
+               oracle/_ref/bowtie2-align-server-stub, the same binding over a
+               CPU stand-in of the ABI, which checks the binding itself on a
+               machine without a GPU (CPU tests).
+
+Reads go out in <= 10 000-read chunks through the reference's own client and
+the sorted SAM records must be byte-identical (the reference's own tests sort
+too, scripts/sim/Sim.pm:933-947).  The binding counts which seam calls the
+engines served; work they do not take (reads > BT2G_MAX_READ_LEN, DPs of
+reads >= cminlen 2000) must be the only CPU fallbacks.
+"""
+import json
+import os
+import sys
+import time
+
+import numpy as np
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+for _p in (ROOT, os.path.join(ROOT, "bowtie2-server_amd", "tools"), os.path.join(ROOT, "tests", "golden")):
+    if _p not in sys.path:
+        sys.path.insert(0, _p)
+
+import bt2_index as bi  # noqa: E402
+import synth  # noqa: E402
+from oracle import ref_server as rs  # noqa: E402
+
+SRV_GPU = os.path.join(rs.REF_DIR, "bowtie2-align-server-gpu")
+SRV_STUB = os.path.join(rs.REF_DIR, "bowtie2-align-server-stub")
+LONGREADS = os.path.join(ROOT, "tests", "golden", "longreads.fq.gz")     # example/reads/longreads.fq
+LAMBDA_PE = [os.path.join(ROOT, "tests", "golden", f"reads_{m}.fq.gz") for m in (1, 2)]  # example/reads/reads_{1,2}.fq
+MAXLEN = 1024        # BT2G_MAX_READ_LEN
+
+
+def _need(*paths):
+    for p in paths:
+        if not os.path.exists(p):
+            pytest.skip(f"{os.path.relpath(p, ROOT)} not built (python -c 'import __graft_entry__ as g; g.build()')")
+
+
+@pytest.fixture(scope="module")
+def indexes(tmp_path_factory):
+    d = tmp_path_factory.mktemp("idx")
+    lam = bi.build_from_fasta(os.path.join(ROOT, "tests", "golden", "lambda_virus.fa"))
+    bi.write_index(str(d / "lambda_virus"), lam)
+    # 400 kb, two references, planted 2 kb near-repeats (multi-mappers, XS:i) and N runs
+    g = synth.genome(11, 400_000, n_repeats=60, rep_len=2000, n_copies=3, n_runs=5)
+    syn = bi.build_index([g[:200_000], g[200_000:]], names=[b"c1", b"c2"])
+    bi.write_index(str(d / "syn"), syn)
+    return {"lambda": (str(d / "lambda_virus"), lam), "synth": (str(d / "syn"), syn)}
+
+
+def _reads(idx, mode, n, seed, dirpath):
+    import bench
+    parts = idx.ref_codes
+    if mode == "paired":
+        r, q = bench.make_pairs(parts, n, 150, seed)
+        return rs.write_fastq_chunks(dirpath, r[:n], q[:n], codes2=r[n:], quals2=q[n:])
+    r, q = bench.make_reads(parts, n, 150, seed)
+    return rs.write_fastq_chunks(dirpath, r, q)
+
+
+def _run(binary, base, chunks, args, dirpath, tag):
+    stats = os.path.join(dirpath, f"stats_{tag}.json")
+    env = {"BT2G_INDEX": base, "BT2G_ADAPTER_STATS": stats, "BT2G_DEVICE": "0"}
+    with rs.Server(base, threads=2, args=args, binary=binary, env=env,
+                   log_path=os.path.join(dirpath, f"server_{tag}.log")) as s:
+        dt, outs = s.run(chunks, k=2)
+    st = None
+    for _ in range(50):                      # written by the binding's SIGTERM handler
+        if os.path.exists(stats):
+            st = json.load(open(stats))
+            break
+        time.sleep(0.1)
+    return dt, rs.sorted_records(outs), st
+
+
+def _compare(dropin, base, chunks, args, dirpath, long_reads=False):
+    t_ref, a, _ = _run(rs.SERVER, base, chunks, args, dirpath, "ref")
+    t_new, b, st = _run(dropin, base, chunks, args, dirpath, "dropin")
+    assert len(a) == len(b) and len(a) > 0
+    bad = [(x, y) for x, y in zip(a, b) if x != y]
+    assert not bad, f"{len(bad)} SAM records differ, first:\nref  {bad[0][0][:400]}\nbind {bad[0][1][:400]}"
+    assert st is not None, "binding wrote no call counts"
+    for k, (gpu, cpu) in st.items():
+        if not long_reads:
+            assert cpu == 0, f"{k}: {cpu} calls fell back to the CPU"
+    assert st["exact_sweep"][0] > 0 and st["sw_dp"][0] > 0 and st["seed_search"][0] > 0
+    return t_ref, t_new, len(a), st
+
+
+CASES = [
+    ("ee", "synth", [], 1500),                              # configs[1] policy, --end-to-end --sensitive
+    ("local", "synth", ["--local"], 1000),                  # configs[3]
+    ("paired", "synth", [], 600),                           # configs[2], --end-to-end
+    ("paired", "synth", ["--very-sensitive"], 400),         # configs[4] policy
+]
+
+
+@pytest.mark.parametrize("mode,genome,args,n", CASES, ids=["ee", "local", "paired", "paired_vs"])
+def test_binding_sam_parity_cpu(indexes, tmp_path, mode, genome, args, n):
+    """The binding over the CPU stand-in of the ABI: SAM equals the stock server's."""
+    _need(rs.SERVER, rs.CLIENT, SRV_STUB)
+    base, idx = indexes[genome]
+    chunks = _reads(idx, mode, n, 7, str(tmp_path))
+    _compare(SRV_STUB, base, chunks, args, str(tmp_path))
+
+
+def test_binding_longreads_cpu(indexes, tmp_path):
+    """configs[0]: lambda, example/reads/longreads.fq (6 000 reads of 40-2 561 bp)."""
+    _need(rs.SERVER, rs.CLIENT, SRV_STUB, LONGREADS)
+    base, _ = indexes["lambda"]
+    _compare(SRV_STUB, base, [["-U", LONGREADS]], [], str(tmp_path), long_reads=True)
+
+
+GPU_CASES = [
+    ("ee", "synth", [], 10000),
+    ("local", "synth", ["--local"], 5000),
+    ("paired", "synth", [], 4000),
+    ("paired", "synth", ["--very-sensitive"], 2000),
+]
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("mode,genome,args,n", GPU_CASES, ids=["ee", "local", "paired", "paired_vs"])
+def test_dropin_sam_parity_gpu(indexes, tmp_path, mode, genome, args, n):
+    """The reference server with its seams on the MI355X engines: SAM equals the stock server's."""
+    _need(rs.SERVER, rs.CLIENT, SRV_GPU)
+    base, idx = indexes[genome]
+    chunks = _reads(idx, mode, n, 7, str(tmp_path))
+    t_ref, t_new, nrec, st = _compare(SRV_GPU, base, chunks, args, str(tmp_path))
+    print(f"\n[{mode} {' '.join(args)}] {nrec} records identical; stock {t_ref:.2f}s, drop-in {t_new:.2f}s; "
+          f"engine calls {st}")
+
+
+def test_binding_lambda_pairs_cpu(indexes, tmp_path):
+    """lambda example pairs (example/reads/reads_{1,2}.fq, 10 000 pairs), first chunk."""
+    _need(rs.SERVER, rs.CLIENT, SRV_STUB, *LAMBDA_PE)
+    base, _ = indexes["lambda"]
+    _compare(SRV_STUB, base, [["-1", LAMBDA_PE[0], "-2", LAMBDA_PE[1], "-u", "2000"]], [], str(tmp_path))
+
+
+@pytest.mark.gpu
+def test_dropin_lambda_pairs_gpu(indexes, tmp_path):
+    """lambda example pairs, all 10 000 (one connection; the first 10 000 are deterministic)."""
+    _need(rs.SERVER, rs.CLIENT, SRV_GPU, *LAMBDA_PE)
+    base, _ = indexes["lambda"]
+    t_ref, t_new, nrec, st = _compare(SRV_GPU, base, [["-1", LAMBDA_PE[0], "-2", LAMBDA_PE[1]]], [], str(tmp_path))
+    print(f"\n[lambda pairs] {nrec} records identical; stock {t_ref:.2f}s, drop-in {t_new:.2f}s; engine calls {st}")
+
+
+@pytest.mark.gpu
+def test_dropin_longreads_gpu(indexes, tmp_path):
+    """configs[0] through the engines: reads <= 1024 bp on the GPU FM engines, DPs of reads
+    < 2000 bp on the GPU SW engine; longer ones stay on the reference's CPU code."""
+    _need(rs.SERVER, rs.CLIENT, SRV_GPU, LONGREADS)
+    base, _ = indexes["lambda"]
+    t_ref, t_new, nrec, st = _compare(SRV_GPU, base, [["-U", LONGREADS]], [], str(tmp_path), long_reads=True)
+    print(f"\n[longreads] {nrec} records identical; stock {t_ref:.2f}s, drop-in {t_new:.2f}s; engine calls {st}")
