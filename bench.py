@@ -242,9 +242,12 @@ class Pipeline:
         self.sw_cap = 2048 if pol.local else 256
         self.res = torch.empty((self.max_probs, 8), dtype=torch.int32, device=self.dev)
         self.cands = torch.empty((self.max_probs, self.sw_cap, 3), dtype=torch.int32, device=self.dev)
-        # seed-extension rectangles: no trim, core diagonals [maxgap, 3*maxgap] (dp_framer.cpp:116-125)
-        self.rects = torch.zeros((self.max_probs, 4), dtype=torch.int32, device=self.dev)
-        self.rects[:, 1], self.rects[:, 2] = MAXGAP, 3 * MAXGAP
+        # seed-extension frame inputs (bt2g_frame_in) -> rectangles of DynProgFramer::
+        # frameSeedExtensionRect (trimmed at the reference ends, core diagonals; dp_framer.cpp:81-129)
+        self.fin0 = torch.zeros((self.max_probs, 10), dtype=torch.int32, device=self.dev)
+        self.probs0 = torch.zeros((self.max_probs, 5), dtype=torch.int64, device=self.dev)
+        self.rects0 = torch.zeros((self.max_probs, 4), dtype=torch.int32, device=self.dev)
+        self.fok = torch.zeros(self.max_probs, dtype=torch.int32, device=self.dev)
         self.maxaln, self.maxedit = MAXALN, MAXEDIT
         self.naln = torch.empty(self.max_probs, dtype=torch.int32, device=self.dev)
         self.alns = torch.empty((self.max_probs, self.maxaln, 10), dtype=torch.int32, device=self.dev)
@@ -326,13 +329,21 @@ class Pipeline:
         # 5. SA rows -> joined-text offsets
         chk(L.bt2g_get_offset_dev(h, P(self.rows), nrows, P(self.offs), P(self.loads_off), S))
         self._mark("offsets")
-        # 6. joinedToTextOff + straddle filter + rectangles, <= 2 per read (device)
+        # 6. joinedToTextOff + straddle filter, <= 2 diagonals per read (device), framed by
+        #    frameSeedExtensionRect (bt2g_frame_dev kind 0)
         chk(L.bt2g_bench_frame_dev(n, P(self.lens), P(self.offs), P(self.meta), P(self.read_base),
                                    P(self.read_cnt), P(self.fr[0]), P(self.fr[1]), P(self.fr[2]), P(self.fr[3]),
-                                   self.nfrag, MAXGAP, pol.minsc, P(self.probs),
+                                   self.nfrag, pol.minsc, P(self.fin0),
                                    P(self.counters[1:]), self.max_probs, S))
-        npb = min(int(self.counters[1]), self.max_probs)
-        probs = self.probs[:npb]
+        nfin = min(int(self.counters[1]), self.max_probs)
+        chk(L.bt2g_frame_dev(h, P(self.fin0), nfin, P(self.lens), C.byref(self.sc), None, MAXHALF, 1,
+                             P(self.probs0), P(self.rects0), P(self.fok), S))
+        okp = torch.nonzero(self.fok[:nfin]).squeeze(1)
+        npb = int(okp.numel())
+        if npb == nfin:
+            probs, self.rects = self.probs0[:npb], self.rects0[:npb]
+        else:                                           # rectangles trimmed away entirely
+            probs, self.rects = self.probs0.index_select(0, okp), self.rects0.index_select(0, okp)
         self._mark("frame")
         # 7. fill + candidates + the nextAlignment loop (backtraces)
         chk(L.bt2g_sw_align_bt_dev(h, P(self.reads), P(self.quals), stride, P(self.lens),
@@ -348,8 +359,8 @@ class Pipeline:
         ns = 0
         if keep:
             self.last = dict(sel=sel, rows=self.rows[:nrows], offs=self.offs[:nrows], probs=probs, npb=npb,
-                             nrows=nrows, m=m, ns=ns, loads_off=self.loads_off[:nrows],
-                             read_base=self.read_base, read_cnt=self.read_cnt)
+                             rects=self.rects, nrows=nrows, m=m, ns=ns, loads_off=self.loads_off[:nrows],
+                             meta=self.meta[:nrows], read_base=self.read_base, read_cnt=self.read_cnt)
         if pol.paired:
             aligned = self.mates(probs, npb, aligned, keep, S)
         self._mark("end")
@@ -458,27 +469,22 @@ def cpu_baseline(idx, reads, quals, pipe, sample, threads):
     """Reference code (oracle/_ref/libbt2ref.so = /root/reference built by
     oracle/ref/Makefile) on the same per-read work for `sample` reads (paired:
     `sample` pairs, both mates, plus their mate searches), split over `threads`
-    host threads.  Returns (seconds, exact-sweep outputs, seed-extension DP
-    outputs, their problems, mate DP outputs or None)."""
+    host threads.  The seed-extension chain runs on the reference's OWN
+    intermediates (oracle/ref_chain.py: its exact sweep, 1-mm hits, seeds, hit
+    rows, getOffset, joinedToTextOff, frameSeedExtensionRect, SwAligner), never
+    on the GPU's; the mate searches start from the GPU's anchors (reference
+    framing + DPs).  Returns (seconds, chain outputs, mate outputs or None,
+    per-stage seconds)."""
     import bt2_index as bi
     import tempfile
-    from oracle.ref_harness import RefLib, score_params
     import synth
-    lib = RefLib()
-    L = lib.lib
-    L.bt2ref_get_offsets.argtypes = [C.c_void_p, C.c_int, C.c_void_p, C.c_void_p]
-    L.bt2ref_sw_bt_batch.argtypes = [C.c_int, C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p,
-                                     C.c_void_p, C.c_void_p, C.c_void_p, C.c_int, C.c_int, C.c_void_p]
-    L.bt2ref_sw_bt_batch_rects.argtypes = [C.c_int, C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p,
-                                           C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p]
-    L.bt2ref_one_mm_gated.argtypes = [C.c_void_p, C.c_int, C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p,
-                                      C.c_void_p, C.c_int]
-    L.bt2ref_frame.argtypes = [C.c_int, C.c_void_p, C.c_void_p, C.c_void_p, C.c_int, C.c_int, C.c_void_p]
+    from oracle.ref_chain import RefChain
+    from oracle.ref_harness import score_params
     tmp = tempfile.mkdtemp(prefix="bt2bench_")
     base = os.path.join(tmp, "g")
     bi.write_index(base, idx)
-    R = lib.open(base)
-    last = pipe.last
+    chain = RefChain(base)
+    L, R = chain.L, chain.R
     pol = pipe.pol
     ids = np.arange(sample)
     if pol.paired:
@@ -487,139 +493,119 @@ def cpu_baseline(idx, reads, quals, pipe, sample, threads):
     asc = synth.to_ascii(reads[ids])
     seqs = [bytes(asc[i]) for i in range(n)]
     qs = [bytes(quals[i]) for i in ids]
-    # the GPU's rows / DP problems that belong to the sampled reads
-    probs = last["probs"].cpu().numpy()
-    pr_read = probs.view(np.int32)[:, 0]
-    pr = probs[np.isin(pr_read, ids)]
-    gen_codes = idx.ref_codes
-
-    def windows(ps, ncols):
-        # reference masks of each problem's window (what the GPU fetches itself)
-        rf_all, rf_off = [], [0]
-        for p, nc in zip(ps, ncols):
-            pw = p.view(np.int32)
-            refidx, refl = int(pw[6]), int(p[1])
-            g = gen_codes[refidx]
-            o = np.arange(refl, refl + nc + 1)
-            cc = np.where((o >= 0) & (o < len(g)), g[np.clip(o, 0, len(g) - 1)], 4)
-            rf_all.append((1 << cc).astype(np.uint8))
-            rf_off.append(rf_off[-1] + nc + 1)
-        rf = np.concatenate(rf_all) if rf_all else np.zeros(1, np.uint8)
-        return rf, np.array(rf_off, np.int64)
-    ncol = pipe.ncol
-    rf, rf_off = windows(pr, [ncol] * len(pr))
-    # the GPU's hit rows of the sampled reads (contiguous per read)
-    rows_all = last["rows"].cpu().numpy().astype(np.uint32)
-    rb = last["read_base"].cpu().numpy().astype(np.int64)[ids]
-    rc = last["read_cnt"].cpu().numpy().astype(np.int64)[ids]
-    tot = int(rc.sum())
-    within = np.arange(tot) - np.repeat(np.cumsum(rc) - rc, rc)
-    rows = rows_all[np.repeat(rb, rc) + within]
-    sp = score_params(pol.local)
-    minsc = np.full(n, pol.minsc, np.int64)
-    # mate searches of the sampled pairs: the GPU's anchors (framed again by the
-    # reference inside the timed region) and their rectangles' windows
+    lens = np.full(n, pipe.len, np.int64)
+    ref = chain.run(seqs, qs, lens, pol, pipe.maxseeds, pipe.mm_cap, MAXHALF, idx.ref_codes, threads)
+    ref["ids"] = ids
+    dt = sum(chain.secs.values())
+    secs = dict(chain.secs)
     mate = None
     if pol.paired:
+        # mate searches of the sampled pairs from the GPU's anchors: the reference frames
+        # them again (otherMate + frameFindMateRect) and runs the mate DPs
+        sp = score_params(pol.local)
+        last = pipe.last
+        gen_codes = idx.ref_codes
+        L.bt2ref_sw_bt_batch_rects.argtypes = [C.c_int, C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p,
+                                               C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p]
         mpairs = last["m_pairs"].cpu().numpy()
         sel_m = np.nonzero(mpairs < sample)[0]
         mfin = last["m_fin"].cpu().numpy()[sel_m]
         mp = last["m_probs"].cpu().numpy()[sel_m]
         mr = np.ascontiguousarray(last["m_rects"].cpu().numpy()[sel_m])
         fin64 = mfin.view(np.int64)
-        fw32 = mfin
-        opp = fw32[:, 2].astype(np.int64)
+        opp = mfin[:, 2].astype(np.int64)
         fx = np.zeros((len(sel_m), 8), np.int64)
         fx[:, 0] = 1
         fx[:, 1] = fin64[:, 0]
         fx[:, 2] = pipe.len
-        fx[:, 3] = [len(gen_codes[r]) for r in fw32[:, 3]]
+        fx[:, 3] = [len(gen_codes[r]) for r in mfin[:, 3]]
         fx[:, 4] = pol.minsc
-        fx[:, 5] = fw32[:, 5]
-        fx[:, 6] = fw32[:, 7]
+        fx[:, 5] = mfin[:, 5]
+        fx[:, 6] = mfin[:, 7]
         fx[:, 7] = pipe.len
         mncol = mp.view(np.int32)[:, 7].astype(np.int64)
-        mrf, mrf_off = windows(mp, mncol)
+        rf_all, rf_off = [], [0]
+        for p_, nc in zip(mp, mncol):
+            refidx, refl = int(p_.view(np.int32)[6]), int(p_[1])
+            g = gen_codes[refidx]
+            o = np.arange(refl, refl + nc + 1)
+            cc = np.where((o >= 0) & (o < len(g)), g[np.clip(o, 0, len(g) - 1)], 4)
+            rf_all.append((1 << cc).astype(np.uint8))
+            rf_off.append(rf_off[-1] + nc + 1)
+        mrf = np.concatenate(rf_all) if rf_all else np.zeros(1, np.uint8)
+        mrf_off = np.array(rf_off, np.int64)
         pos_of = {int(r): i for i, r in enumerate(ids)}
         mseq = [seqs[pos_of[int(r)]] for r in opp]
         mq = [qs[pos_of[int(r)]] for r in opp]
-        mate = dict(fx=fx, mp=mp, mr=mr, mncol=mncol.astype(np.int32), rf=mrf, rf_off=mrf_off, seq=mseq, q=mq,
-                    fw=np.ascontiguousarray(mp.view(np.int32)[:, 1].astype(np.uint8)), sel=sel_m)
+        mfw = np.ascontiguousarray(mp.view(np.int32)[:, 1].astype(np.uint8))
+        mnc32 = np.ascontiguousarray(mncol.astype(np.int32))
 
-    def work(lo, hi):
-        s, q = seqs[lo:hi], qs[lo:hi]
-        cs = (C.c_char_p * len(s))(*s)
-        cq = (C.c_char_p * len(q))(*q)
-        ex = R.exact_sweep(s, q, 2)
-        cnt = np.zeros(hi - lo, np.int32)
-        exu = np.ascontiguousarray(ex, np.uint64)
-        L.bt2ref_one_mm_gated(R.h, hi - lo, cs, cq, minsc[lo:hi].ctypes.data, exu.ctypes.data, cnt.ctypes.data,
-                              int(pol.local))
-        need = np.minimum(ex[:, 0], ex[:, 1]) != 0
-        ss = [s[i] for i in np.nonzero(need)[0]]
-        sq = [q[i] for i in np.nonzero(need)[0]]
-        if ss:
-            R.seed_search(ss, sq, pol.seedlen, pol.interval, 0, pipe.maxseeds)
-        return ex
+        def work_mate(lo, hi):
+            k = hi - lo
+            fxk = np.ascontiguousarray(fx[lo:hi])
+            fo = np.zeros((k, 7), np.int64)
+            pev = np.array([3, 0, PE_MAXFRAG, 0, 0, 1, 1], np.int32)
+            L.bt2ref_frame(k, fxk.ctypes.data, C.byref(sp), pev.ctypes.data, MAXHALF, 1, fo.ctypes.data)
+            out = np.zeros((k, 8), np.int64)
+            ms = np.full(k, pol.minsc, np.int64)
+            L.bt2ref_sw_bt_batch_rects(k, (C.c_char_p * k)(*mseq[lo:hi]), (C.c_char_p * k)(*mq[lo:hi]),
+                                       mfw[lo:].ctypes.data, mrf.ctypes.data,
+                                       np.ascontiguousarray(mrf_off[lo:hi + 1]).ctypes.data,
+                                       mnc32[lo:].ctypes.data, ms.ctypes.data, C.byref(sp),
+                                       np.ascontiguousarray(mr[lo:hi]).ctypes.data, out.ctypes.data)
+            return fo, out
 
-    def work_rows(lo, hi):
-        out = np.zeros(hi - lo, np.uint32)
-        rr = np.ascontiguousarray(rows[lo:hi])
-        L.bt2ref_get_offsets(R.h, hi - lo, rr.ctypes.data, out.ctypes.data)
-        return out
-
-    pos = np.searchsorted(ids, pr_read[np.isin(pr_read, ids)])
-
-    def work_sw(lo, hi):
-        k = hi - lo
-        ps = pr[lo:hi]
-        fwv = np.ascontiguousarray(ps.view(np.int32)[:, 1].astype(np.uint8))
-        # the reference's SwAligner takes the read forward and its fw flag
-        cs = (C.c_char_p * k)(*[seqs[r] for r in pos[lo:hi]])
-        cq = (C.c_char_p * k)(*[qs[r] for r in pos[lo:hi]])
-        offs = np.ascontiguousarray(rf_off[lo:hi + 1] - 0)
-        nc = np.full(k, ncol, np.int32)
-        ms = np.full(k, pol.minsc, np.int64)
-        out = np.zeros((k, 8), np.int64)
-        L.bt2ref_sw_bt_batch(k, cs, cq, fwv.ctypes.data, rf.ctypes.data, offs.ctypes.data, nc.ctypes.data,
-                             ms.ctypes.data, C.byref(sp), MAXGAP, 3 * MAXGAP, out.ctypes.data)
-        return out
-
-    def work_mate(lo, hi):
-        k = hi - lo
-        fx = np.ascontiguousarray(mate["fx"][lo:hi])
-        fo = np.zeros((k, 7), np.int64)
-        pev = np.array([3, 0, PE_MAXFRAG, 0, 0, 1, 1], np.int32)
-        L.bt2ref_frame(k, fx.ctypes.data, C.byref(sp), pev.ctypes.data, MAXHALF, 1, fo.ctypes.data)
-        cs = (C.c_char_p * k)(*mate["seq"][lo:hi])
-        cq = (C.c_char_p * k)(*mate["q"][lo:hi])
-        out = np.zeros((k, 8), np.int64)
-        ms = np.full(k, pol.minsc, np.int64)
-        L.bt2ref_sw_bt_batch_rects(k, cs, cq, mate["fw"][lo:].ctypes.data, mate["rf"].ctypes.data,
-                                   np.ascontiguousarray(mate["rf_off"][lo:hi + 1]).ctypes.data,
-                                   np.ascontiguousarray(mate["mncol"][lo:hi]).ctypes.data, ms.ctypes.data,
-                                   C.byref(sp), np.ascontiguousarray(mate["mr"][lo:hi]).ctypes.data,
-                                   out.ctypes.data)
-        return fo, out
-
-    def split(total):
-        b = np.linspace(0, total, threads + 1).astype(int)
-        return [(int(b[i]), int(b[i + 1])) for i in range(threads) if b[i + 1] > b[i]]
-
-    t0 = time.perf_counter()
-    with cf.ThreadPoolExecutor(threads) as ex_:
-        exs = list(ex_.map(lambda a: work(*a), split(n)))
-        list(ex_.map(lambda a: work_rows(*a), split(len(rows))))
-        sws = list(ex_.map(lambda a: work_sw(*a), split(len(pr))))
-        mts = list(ex_.map(lambda a: work_mate(*a), split(len(mate["fx"])))) if mate else []
-    dt = time.perf_counter() - t0
-    R.close()
-    ex_all = np.concatenate(exs)
-    sw_all = np.concatenate(sws) if sws else np.zeros((0, 8), np.int64)
-    if mate is not None:
+        t0 = time.perf_counter()
+        with cf.ThreadPoolExecutor(threads) as ex_:
+            b_ = np.linspace(0, len(fx), threads + 1).astype(int)
+            mts = list(ex_.map(lambda a: work_mate(*a),
+                               [(int(b_[i]), int(b_[i + 1])) for i in range(threads) if b_[i + 1] > b_[i]]))
+        secs["mate_search"] = time.perf_counter() - t0
+        dt += secs["mate_search"]
+        mate = dict(mp=mp, mr=mr, sel=sel_m)
         mate["frame_ref"] = np.concatenate([m[0] for m in mts]) if mts else np.zeros((0, 7), np.int64)
         mate["out_ref"] = np.concatenate([m[1] for m in mts]) if mts else np.zeros((0, 8), np.int64)
-    return dt, ex_all, sw_all, pr, mate
+    chain.close()
+    return dt, ref, mate, secs
+
+
+def gpu_chain(pipe, ids):
+    """The GPU's buffers of the sampled reads, in the shapes oracle/ref_chain.compare expects."""
+    import torch
+    dev = pipe.dev
+    last = pipe.last
+    tid = torch.from_numpy(ids).to(dev)
+    n_all = pipe.n
+    pos = np.full(n_all, -1, np.int64)
+    pos[ids] = np.arange(len(ids))
+    g = {"sweep": pipe.sweep.index_select(0, tid).cpu().numpy(),
+         "mm_cnt": pipe.mm_cnt.index_select(0, tid).cpu().numpy(),
+         "mm_hits": pipe.mm_hits.index_select(0, tid).cpu().numpy()}
+    sd = np.zeros((len(ids), 2, pipe.maxseeds, 4), np.uint32)
+    inv = pipe.inv.cpu().numpy()[ids]
+    has = inv >= 0
+    if has.any():
+        sd[has] = pipe.seeds[:last["m"]].cpu().numpy()[inv[has]].view(np.uint32)
+    g["seeds"] = sd
+    # hit rows of the sampled reads: contiguous per read at read_base
+    rb = last["read_base"].cpu().numpy().astype(np.int64)[ids]
+    rc = last["read_cnt"].cpu().numpy().astype(np.int64)[ids]
+    tot = int(rc.sum())
+    within = np.arange(tot) - np.repeat(np.cumsum(rc) - rc, rc)
+    at = np.repeat(rb, rc) + within
+    g["rows"] = last["rows"].cpu().numpy()[at]
+    g["offs"] = last["offs"].cpu().numpy()[at]
+    g["row_read"] = np.repeat(np.arange(len(ids)), rc)
+    pr = last["probs"].cpu().numpy()
+    rt = last["rects"].cpu().numpy()
+    pw = pr.view(np.int32)
+    r_all = pw[:, 0].astype(np.int64)
+    keep = pos[r_all] >= 0
+    g["probs"] = dict(read=pos[r_all[keep]], fw=pw[keep, 1].astype(np.int64), refidx=pw[keep, 6].astype(np.int64),
+                      refl=pr[keep, 1], ncol=pw[keep, 7].astype(np.int64), triml=rt[keep, 0].astype(np.int64),
+                      corel=rt[keep, 1].astype(np.int64), corer=rt[keep, 2].astype(np.int64))
+    g["probs_index"] = np.nonzero(keep)[0]
+    return g
 
 
 def bt_mismatches(naln, alns, ed, ref, maxaln, maxedit):
@@ -655,11 +641,11 @@ def bt_mismatches(naln, alns, ed, ref, maxaln, maxedit):
     return int(bad.sum())
 
 
-def backtrace_parity(pipe, keep, sw_ref):
-    """The sampled seed-extension DPs' nextAlignment results vs the reference's."""
+def backtrace_parity(pipe, kp_all, sw_ref):
+    """The seed-extension DPs kp_all (GPU problem indices) nextAlignment results
+    vs the reference's rows sw_ref (same order)."""
     import torch
     npb = pipe.last["npb"]
-    kp_all = np.nonzero(keep)[0]
     bad = 0
     for s0 in range(0, len(kp_all), 262144):       # bounded copies of the edit rows
         kp = torch.from_numpy(kp_all[s0:s0 + 262144]).to(pipe.dev)
@@ -683,7 +669,7 @@ def mate_parity(pipe, mate):
     frame_bad = int((got != fr).any(1).sum())
     k = len(mp)
     if k == 0:
-        return {"mate_dps": 0, "frame_mismatch": frame_bad, "mate_backtrace_mismatch": 0}
+        return {"mate_dps": 0, "mate_frame_mismatch": frame_bad, "mate_backtrace_mismatch": 0}
     k = min(k, pipe.mate_chunk)
     dev = pipe.dev
     tp = torch.from_numpy(np.ascontiguousarray(mp[:k])).to(dev)
@@ -699,7 +685,7 @@ def mate_parity(pipe, mate):
     res = pipe.mres[:k].cpu().numpy()
     sw_bad = int((res[:, 0] != ref[:, 0]).sum() + (res[:, 6] != ref[:, 1]).sum())
     bt_bad = bt_mismatches(pipe.mnaln[:k], pipe.malns[:k], pipe.medits[:k], ref, pipe.maxaln, pipe.maxedit)
-    return {"mate_dps": k, "frame_mismatch": frame_bad, "mate_sw_mismatch": sw_bad,
+    return {"mate_dps": k, "mate_frame_mismatch": frame_bad, "mate_sw_mismatch": sw_bad,
             "mate_backtrace_mismatch": bt_bad, "mate_ref_alignments": int(ref[:, 2].sum())}
 
 
@@ -739,7 +725,8 @@ def main():
     ap.add_argument("--genome-mb", type=float, default=3100.0,
                     help="synthetic genome size (default: hg38's 3.1 Gbp; the index is built on the GPU, ~160 s)")
     ap.add_argument("--cpu-sample", type=int, default=1_000_000)
-    ap.add_argument("--cpu-threads", type=int, default=16)
+    ap.add_argument("--cpu-threads", type=int, default=0, help="0: the usable cores of the host (cgroup quota / "
+                                                                   "affinity)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--index-cache", default="", help="reuse/write the built index at this base path")
     ap.add_argument("--pmc-fetch", default="", help="rocprofv3 --pmc FETCH_SIZE counter_collection.csv of this "
@@ -857,37 +844,44 @@ def main():
     cpu = None
     parity = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        threads = max(1, min(args.cpu_threads, os.cpu_count() or 1))
+        from oracle import ref_server as rs
+        from oracle.ref_chain import compare
+        host = rs.host_cpus()
+        threads = args.cpu_threads or host["usable"]
         sample = min(args.cpu_sample, pipe.npairs if args.mode == "paired" else pipe.n)
         try:
-            dt, ex_ref, sw_ref, pr, mate = cpu_baseline(idx, reads_np, quals_np, pipe, sample, threads)
+            dt, ref, mate, secs = cpu_baseline(idx, reads_np, quals_np, pipe, sample, threads)
             paired = args.mode == "paired"
             cpu = {"value": sample / dt, "unit": "read pairs/s" if paired else "reads/s", "cores": threads,
-                   "kind": "reference",
+                   "kind": "reference", "host": host, "stage_seconds": secs,
                    "sample": f"first {sample} {'pairs (both mates)' if paired else 'reads'} of the batch through "
-                             f"the reference's exactSweep, gated oneMmSearch, searchAllSeeds, getOffset, "
-                             f"SwAligner::align and the nextAlignment loop on the same rows/DP problems "
-                             f"({len(pr)} DPs)"
-                             + (f", then otherMate + frameFindMateRect + the mate DPs ({len(mate['fx'])})"
-                                if paired else "") + f", {threads} threads"}
-            ids = np.arange(sample)
-            if paired:
-                ids = np.concatenate([ids, pipe.npairs + ids])
-            sw_gpu = pipe.sweep[torch.from_numpy(ids).to(dev)].cpu().numpy().astype(np.int64) & 0xFFFFFFFF
-            mism = int((sw_gpu[:, [0, 1, 2, 3, 4, 5]] != ex_ref[:, [0, 1, 3, 4, 5, 6]].astype(np.int64)).any(1).sum())
-            npb = pipe.last["npb"]
-            res = pipe.res[:npb].cpu().numpy()
-            pr_read = pipe.last["probs"].cpu().numpy().view(np.int32)[:, 0]
-            keep = np.isin(pr_read, ids)
-            rr = res[keep]
-            sw_mism = int((rr[:, 0] != sw_ref[:, 0]).sum() + (rr[:, 6] != sw_ref[:, 1]).sum())
-            bt_mism = backtrace_parity(pipe, keep, sw_ref)
-            parity = {"exact_sweep_mismatch": mism, "sw_mismatch": sw_mism, "backtrace_mismatch": bt_mism,
-                      "reads": int(len(ids)), "dps": int(len(sw_ref)), "ref_alignments": int(sw_ref[:, 2].sum())}
+                             f"the reference's own chain: exactSweep, gated oneMmSearch, searchAllSeeds, getOffset "
+                             f"of its own hit rows, joinedToTextOff, frameSeedExtensionRect of the bench's two "
+                             f"diagonals per read, SwAligner::align and the nextAlignment loop "
+                             f"({len(ref['sw'])} DPs)"
+                             + (f", then otherMate + frameFindMateRect + the mate DPs of the GPU's anchors "
+                                f"({len(mate['out_ref'])})" if paired else "")
+                             + f"; {threads} threads = the usable cores of this host ({host['model']})"}
+            g = gpu_chain(pipe, ref["ids"])
+            parity = compare(ref, g)
+            parity["reads"] = int(len(ref["ids"]))
+            if parity["frame_mismatch"] == 0:
+                # the same rectangles on both sides: pair them up and compare fill + backtraces
+                rp, gp = ref["probs"], g["probs"]
+                kr = np.lexsort([rp[k] for k in ("refl", "refidx", "fw", "read")])
+                kg = np.lexsort([gp[k] for k in ("refl", "refidx", "fw", "read")])
+                gidx = g["probs_index"][kg]
+                sw_ref = ref["sw"][kr]
+                res = pipe.res[:pipe.last["npb"]].cpu().numpy()[gidx]
+                parity["sw_mismatch"] = int((res[:, 0] != sw_ref[:, 0]).sum() + (res[:, 6] != sw_ref[:, 1]).sum())
+                parity["backtrace_mismatch"] = backtrace_parity(pipe, gidx, sw_ref)
+                parity["ref_alignments"] = int(sw_ref[:, 2].sum())
             if paired:
                 parity.update(mate_parity(pipe, mate))
             log(f"[rank 0] cpu baseline {sample/dt:.0f} {cpu['unit']} on {threads} threads ({dt:.1f}s); parity {parity}")
         except Exception as e:  # the reference build is optional on the box
+            import traceback
+            traceback.print_exc()
             log(f"[rank 0] cpu baseline unavailable: {e!r}")
 
     if rank == 0:

@@ -114,7 +114,7 @@ def lib():
         L.bt2g_reserve_sw.argtypes = [vp, u32, u32]
         L.bt2g_bench_collect_rows_dev.argtypes = [u32, vp, vp, vp, vp, u32, vp, vp, u32, u32, u32, vp, vp, vp, vp, vp,
                                                   u32, vp]
-        L.bt2g_bench_frame_dev.argtypes = [u32, vp, vp, vp, vp, vp, vp, vp, vp, vp, u32, C.c_int32, C.c_int32, vp, vp,
+        L.bt2g_bench_frame_dev.argtypes = [u32, vp, vp, vp, vp, vp, vp, vp, vp, vp, u32, C.c_int32, vp, vp,
                                            u32, vp]
         L.bt2g_get_offset.argtypes = [vp, vp, u32, vp, vp]
         L.bt2g_get_offset_dev.argtypes = [vp, vp, u32, vp, vp, vp]

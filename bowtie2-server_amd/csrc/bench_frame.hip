@@ -7,9 +7,10 @@
 // limits (aligner_sw_driver.cpp:756-1297).  The bench's policy is documented
 // in DESIGN.md section 5: one rectangle per distinct (read, strand, reference,
 // diagonal), at most two per read, the two smallest by (strand, reference,
-// diagonal); the rectangle itself is DynProgFramer::frameSeedExtensionRect
-// (dp_framer.cpp:81-129) with maxgap 15: refl = start - 2*maxgap,
-// width = len + 4*maxgap.
+// diagonal).  k_frame emits seed-extension frame inputs (kind 0); the
+// rectangles themselves come from bt2g_frame_dev, the restatement of
+// DynProgFramer::frameSeedExtensionRect (dp_framer.cpp:81-129) with its
+// trimming at the reference ends and its core diagonals.
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 #include "bt2g_kernels.h"
@@ -84,15 +85,16 @@ k_collect_rows(uint32_t n, const uint32_t* __restrict__ lens, const uint32_t* __
 }
 
 // One thread per read: joined offsets -> (reference, offset) (Ebwt::joinedToTextOff,
-// bt2_idx.cpp:54), drop hits straddling a fragment end, read start on the
-// reference, two smallest distinct (strand, reference, start) -> rectangles.
+// bt2_idx.cpp:54, rejecting hits that straddle a fragment end), read start on
+// the reference, two smallest distinct (strand, reference, start) -> frame
+// inputs for bt2g_frame_dev.
 __global__ void __launch_bounds__(256)
 k_frame(uint32_t n, const uint32_t* __restrict__ lens, const uint32_t* __restrict__ offs,
         const uint32_t* __restrict__ meta, const uint32_t* __restrict__ read_base,
         const uint32_t* __restrict__ read_cnt, const uint32_t* __restrict__ fr_joff,
         const uint32_t* __restrict__ fr_tid, const uint32_t* __restrict__ fr_toff,
-        const uint32_t* __restrict__ fr_end, uint32_t nfrag, int32_t maxgap, int32_t minsc,
-        bt2g_sw_problem* __restrict__ probs, uint32_t* __restrict__ nprob, uint32_t cap) {
+        const uint32_t* __restrict__ fr_end, uint32_t nfrag, int32_t minsc,
+        bt2g_frame_in* __restrict__ fin, uint32_t* __restrict__ nprob, uint32_t cap) {
 	const uint32_t r = blockIdx.x * blockDim.x + threadIdx.x;
 	const bool valid = r < n;
 	const uint64_t NONE = ~0ull;
@@ -127,17 +129,17 @@ k_frame(uint32_t n, const uint32_t* __restrict__ lens, const uint32_t* __restric
 	for(uint32_t i = 0; i < np; i++) {
 		if(base + i >= cap) break;
 		const uint64_t key = i ? k2 : k1;
-		bt2g_sw_problem p;
-		p.read = r;
-		p.fw = (int32_t)(key >> 62);
-		const int64_t start = (int64_t)(key & ((1ull << 40) - 1)) - (1ll << 39);
-		p.refl = start - 2 * maxgap;
-		p.win_off = -1;
-		p.refidx = (uint32_t)((key >> 40) & 0x3fffffu);
-		p.ncol = len + 4u * (uint32_t)maxgap;
-		p.minsc = minsc;
-		p.pad = 0;
-		probs[base + i] = p;
+		bt2g_frame_in f;
+		f.off = (int64_t)(key & ((1ull << 40) - 1)) - (1ll << 39);
+		f.read = r;
+		f.refidx = (uint32_t)((key >> 40) & 0x3fffffu);
+		f.minsc = minsc;
+		f.fw = (int32_t)(key >> 62);
+		f.kind = 0;
+		f.anchor1 = 0;
+		f.alen = 0;
+		f.pad = 0;
+		fin[base + i] = f;
 	}
 }
 
@@ -158,12 +160,11 @@ int bt2g_bench_collect_rows_dev(uint32_t n, const uint32_t* lens, const uint32_t
 int bt2g_bench_frame_dev(uint32_t n, const uint32_t* lens, const uint32_t* offs, const uint32_t* meta,
                          const uint32_t* read_base, const uint32_t* read_cnt, const uint32_t* fr_joff,
                          const uint32_t* fr_tid, const uint32_t* fr_toff, const uint32_t* fr_end, uint32_t nfrag,
-                         int32_t maxgap, int32_t minsc, bt2g_sw_problem* probs, uint32_t* nprob, uint32_t cap,
-                         void* stream) {
+                         int32_t minsc, bt2g_frame_in* fin, uint32_t* nprob, uint32_t cap, void* stream) {
 	if(n == 0) return BT2G_OK;
 	if(nfrag == 0) return BT2G_ERR_ARG;
 	hipLaunchKernelGGL(k_frame, dim3((n + 255) / 256), dim3(256), 0, (hipStream_t)stream, n, lens, offs, meta,
-	                   read_base, read_cnt, fr_joff, fr_tid, fr_toff, fr_end, nfrag, maxgap, minsc, probs, nprob, cap);
+	                   read_base, read_cnt, fr_joff, fr_tid, fr_toff, fr_end, nfrag, minsc, fin, nprob, cap);
 	return hipGetLastError() == hipSuccess ? BT2G_OK : BT2G_ERR_HIP;
 }
 

@@ -382,16 +382,16 @@ int bt2g_bench_collect_rows_dev(uint32_t n, const uint32_t* lens, const uint32_t
                                 uint32_t maxseeds, uint32_t seedlen, uint32_t interval, uint32_t* rows,
                                 uint32_t* meta, uint32_t* read_base, uint32_t* read_cnt, uint32_t* total,
                                 uint32_t cap, void* stream);
-/* Rows' joined offsets (bt2g_get_offset_dev) -> seed-extension rectangles
- * (dp_framer.cpp:81-129, maxgap): one per distinct (strand, reference,
- * diagonal), the two smallest per read; fragments as in the .1.bt2 rstarts
- * (joined offset, text id, text offset) plus each fragment's joined end.
- * *nprob (zeroed by the caller) receives the problem count. */
+/* Rows' joined offsets (bt2g_get_offset_dev) -> seed-extension frame inputs
+ * (kind 0, off = the read's start on the reference) for bt2g_frame_dev: one
+ * per distinct (strand, reference, diagonal), the two smallest per read;
+ * fragments as in the .1.bt2 rstarts (joined offset, text id, text offset) plus
+ * each fragment's joined end.  *nprob (zeroed by the caller) receives the
+ * count. */
 int bt2g_bench_frame_dev(uint32_t n, const uint32_t* lens, const uint32_t* offs, const uint32_t* meta,
                          const uint32_t* read_base, const uint32_t* read_cnt, const uint32_t* fr_joff,
                          const uint32_t* fr_tid, const uint32_t* fr_toff, const uint32_t* fr_end, uint32_t nfrag,
-                         int32_t maxgap, int32_t minsc, bt2g_sw_problem* probs, uint32_t* nprob, uint32_t cap,
-                         void* stream);
+                         int32_t minsc, bt2g_frame_in* fin, uint32_t* nprob, uint32_t cap, void* stream);
 
 /* ---- multi-GPU ----------------------------------------------------------- */
 /* The only collective of the path: the caller sums these

@@ -28,9 +28,17 @@
 //   SwAligner::nextAlignment     aligner_sw.cpp:737-1146        and every backtrace, with candidate fates)
 //
 // The GPU context is opened on first use from $BT2G_INDEX (the index base the
-// server was started with) on device $BT2G_DEVICE (default 0).  Calls are
-// serialised by one mutex: this binding demonstrates the drop-in and its
-// exactness; it is not the throughput path (bench.py batches instead).
+// server was started with) on device $BT2G_DEVICE (default 0).
+//
+// Batching across worker threads: each seam call becomes a request that the
+// calling worker thread blocks on; one dispatcher thread drains the pending
+// requests of a seam (grouped by their batch-wide arguments) into ONE bt2g_*
+// call and wakes the workers.  The reference's per-read control flow stays
+// exactly as written -- every read still runs in its own worker thread in
+// program order -- so running the server with many workers (-p 256 ... 1024)
+// turns the reference's one-read-at-a-time schedule into GPU batches of
+// hundreds of reads/DPs without changing any decision.  BT2G_BATCH=0 serves
+// every call synchronously instead.
 #include <stdint.h>
 #include <stdio.h>
 #include <stdlib.h>
@@ -38,8 +46,11 @@
 #include <signal.h>
 #include <unistd.h>
 #include <fcntl.h>
+#include <semaphore.h>
 #include <atomic>
+#include <condition_variable>
 #include <mutex>
+#include <thread>
 #include <vector>
 #include <limits>
 
@@ -57,7 +68,7 @@ bt2g_ctx* g_ctx = nullptr;
 
 enum { ST_EXACT, ST_1MM, ST_SEEDS, ST_UG, ST_DP, ST_N };
 const char* const ST_NAMES[ST_N] = {"exact_sweep", "one_mm", "seed_search", "ungapped", "sw_dp"};
-std::atomic<uint64_t> g_gpu[ST_N], g_cpu[ST_N];
+std::atomic<uint64_t> g_gpu[ST_N], g_cpu[ST_N], g_batches[ST_N];
 char g_stats_path[4096];
 
 void write_stats() {
@@ -66,8 +77,9 @@ void write_stats() {
 	int n = 0;
 	n += snprintf(buf + n, sizeof(buf) - n, "{");
 	for(int i = 0; i < ST_N; i++)
-		n += snprintf(buf + n, sizeof(buf) - n, "%s\"%s\": [%llu, %llu]", i ? ", " : "", ST_NAMES[i],
-		              (unsigned long long)g_gpu[i].load(), (unsigned long long)g_cpu[i].load());
+		n += snprintf(buf + n, sizeof(buf) - n, "%s\"%s\": [%llu, %llu, %llu]", i ? ", " : "", ST_NAMES[i],
+		              (unsigned long long)g_gpu[i].load(), (unsigned long long)g_cpu[i].load(),
+		              (unsigned long long)g_batches[i].load());
 	n += snprintf(buf + n, sizeof(buf) - n, "}\n");
 	int fd = open(g_stats_path, O_WRONLY | O_CREAT | O_TRUNC, 0644);
 	if(fd >= 0) {
@@ -158,6 +170,323 @@ struct Row {
 	}
 };
 
+// ---- requests and the dispatcher ---------------------------------------------
+struct Req {
+	int kind;
+	uint64_t key;        // batch-wide arguments: requests with equal keys share one call
+	int rc = 0;
+	sem_t sem;
+	Req(int k, uint64_t ky) : kind(k), key(ky) { sem_init(&sem, 0, 0); }
+	~Req() { sem_destroy(&sem); }
+};
+
+struct ExactReq : Req {      // bt2g_exact_sweep
+	Row r;
+	uint32_t mine_max;
+	int nofw, norc;
+	uint32_t out[8];
+	ExactReq(uint32_t mm, int f, int c) : Req(ST_EXACT, ((uint64_t)mm << 2) | (uint64_t)(f << 1) | (uint64_t)c),
+	                                      mine_max(mm), nofw(f), norc(c) {}
+};
+
+struct MmReq : Req {         // bt2g_one_mm
+	Row r;
+	int32_t minsc;
+	int nofw, norc;
+	bt2g_scoring sc;
+	std::vector<bt2g_mm1> hits;
+	int32_t cnt = 0;
+	uint32_t ops = 0;
+	MmReq(int f, int c, const bt2g_scoring& s)
+		: Req(ST_1MM, (uint64_t)(f << 1) | (uint64_t)c | ((uint64_t)s.local << 2)), nofw(f), norc(c), sc(s) {}
+};
+
+struct SeedReq : Req {       // bt2g_seed_search
+	Row r;
+	uint32_t seedlen, per, off, nof;
+	std::vector<uint32_t> out;
+	int32_t ns = 0;
+	uint32_t ops = 0;
+	SeedReq(uint32_t L, uint32_t p, uint32_t o, uint32_t n)
+		: Req(ST_SEEDS, ((uint64_t)L << 48) | ((uint64_t)p << 24) | (uint64_t)o), seedlen(L), per(p), off(o), nof(n) {}
+};
+
+struct UgReq : Req {         // bt2g_ungapped
+	Row r;
+	bt2g_ug_problem p;
+	bt2g_scoring sc;
+	int ohang;
+	bt2g_ug_result o;
+	std::vector<bt2g_edit> ed;
+	UgReq(const bt2g_scoring& s, int oh) : Req(ST_UG, (uint64_t)oh | ((uint64_t)s.local << 1)), sc(s), ohang(oh) {}
+};
+
+struct DpReq : Req {         // bt2g_sw_align_bt
+	Row r;
+	bt2g_sw_problem p;
+	bt2g_sw_rect rect;
+	std::vector<uint8_t> win;
+	bt2g_scoring sc;
+	int enable8;
+	uint32_t cap, maxaln, maxedit;
+	bt2g_sw_result o;
+	std::vector<bt2g_sw_cand> cands;
+	std::vector<int8_t> fates;
+	std::vector<bt2g_sw_aln> alns;
+	std::vector<bt2g_edit> edits;
+	int32_t naln = 0;
+	DpReq(const bt2g_scoring& s, int e8) : Req(ST_DP, (uint64_t)e8 | ((uint64_t)s.local << 1)), sc(s), enable8(e8) {}
+};
+
+// Rows of a batch as one [n][stride] array (stride = longest read).
+struct Pack {
+	std::vector<uint8_t> codes, quals;
+	std::vector<uint32_t> lens;
+	uint32_t stride = 1;
+	template <typename R>
+	void build(const std::vector<R*>& v) {
+		stride = 1;
+		for(R* q : v) stride = std::max(stride, q->r.len);
+		codes.assign(v.size() * (size_t)stride, 4);
+		quals.assign(v.size() * (size_t)stride, 'I');
+		lens.resize(v.size());
+		for(size_t i = 0; i < v.size(); i++) {
+			lens[i] = v[i]->r.len;
+			memcpy(&codes[i * stride], v[i]->r.codes.data(), v[i]->r.len);
+			memcpy(&quals[i * stride], v[i]->r.quals.data(), v[i]->r.len);
+		}
+	}
+};
+
+int run_exact(const std::vector<ExactReq*>& v) {
+	Pack pk;
+	pk.build(v);
+	std::vector<uint32_t> out(8 * v.size());
+	int rc = bt2g_exact_sweep(ctx(), pk.codes.data(), pk.stride, pk.lens.data(), (uint32_t)v.size(), v[0]->mine_max,
+	                          v[0]->nofw, v[0]->norc, out.data());
+	if(rc) return rc;
+	for(size_t i = 0; i < v.size(); i++) memcpy(v[i]->out, &out[8 * i], sizeof(v[i]->out));
+	return BT2G_OK;
+}
+
+int run_mm(const std::vector<MmReq*>& v, uint32_t cap = 16) {
+	Pack pk;
+	pk.build(v);
+	const size_t n = v.size();
+	std::vector<int32_t> ms(n), cnt(n);
+	std::vector<uint32_t> ops(n);
+	std::vector<bt2g_mm1> h(n * cap);
+	for(size_t i = 0; i < n; i++) ms[i] = v[i]->minsc;
+	int rc = bt2g_one_mm(ctx(), pk.codes.data(), pk.quals.data(), pk.stride, pk.lens.data(), (uint32_t)n, ms.data(),
+	                     &v[0]->sc, v[0]->nofw, v[0]->norc, cap, h.data(), cnt.data(), ops.data(), nullptr);
+	if(rc && rc != BT2G_ERR_OVERFLOW) return rc;
+	for(size_t i = 0; i < n; i++) {
+		if(cnt[i] > (int32_t)cap) {          // more hits than the batch slots: this read again, alone
+			std::vector<MmReq*> one{v[i]};
+			if((rc = run_mm(one, (uint32_t)cnt[i]))) return rc;
+			continue;
+		}
+		v[i]->cnt = cnt[i];
+		v[i]->ops = ops[i];
+		v[i]->hits.assign(h.begin() + i * cap, h.begin() + i * cap + cnt[i]);
+	}
+	return BT2G_OK;
+}
+
+int run_seeds(const std::vector<SeedReq*>& v) {
+	Pack pk;
+	pk.build(v);
+	const size_t n = v.size();
+	uint32_t maxs = 1;
+	for(SeedReq* q : v) maxs = std::max(maxs, q->nof);
+	std::vector<uint32_t> out(n * 2 * maxs * 4), ops(n);
+	std::vector<int32_t> ns(n);
+	int rc = bt2g_seed_search(ctx(), pk.codes.data(), pk.stride, pk.lens.data(), (uint32_t)n, v[0]->seedlen, v[0]->per,
+	                          v[0]->off, maxs, out.data(), ns.data(), ops.data(), nullptr);
+	if(rc) return rc;
+	for(size_t i = 0; i < n; i++) {
+		SeedReq* q = v[i];
+		q->ns = ns[i];
+		q->ops = ops[i];
+		q->out.assign(2 * (size_t)q->nof * 4, 0);
+		for(int f = 0; f < 2; f++)
+			for(uint32_t k = 0; k < q->nof && k < maxs; k++)
+				memcpy(&q->out[((size_t)f * q->nof + k) * 4], &out[((i * 2 + f) * maxs + k) * 4], 16);
+	}
+	return BT2G_OK;
+}
+
+int run_ug(const std::vector<UgReq*>& v) {
+	Pack pk;
+	pk.build(v);
+	const size_t n = v.size();
+	const uint32_t maxedit = pk.stride + 1;
+	std::vector<bt2g_ug_problem> P(n);
+	std::vector<bt2g_ug_result> R(n);
+	std::vector<bt2g_edit> E(n * maxedit);
+	for(size_t i = 0; i < n; i++) {
+		P[i] = v[i]->p;
+		P[i].read = (uint32_t)i;
+	}
+	int rc = bt2g_ungapped(ctx(), pk.codes.data(), pk.quals.data(), pk.stride, pk.lens.data(), P.data(), (uint32_t)n,
+	                       &v[0]->sc, v[0]->ohang, maxedit, R.data(), E.data());
+	if(rc) return rc;
+	for(size_t i = 0; i < n; i++) {
+		v[i]->o = R[i];
+		v[i]->ed.assign(E.begin() + i * maxedit, E.begin() + (i + 1) * maxedit);
+	}
+	return BT2G_OK;
+}
+
+// Fill + gather + the nextAlignment loop for every DP of the batch.  A DP
+// whose candidate list outgrew `cap`, or that may have more than `maxaln`
+// alignments, runs again alone with room for all of them.
+int run_dp(const std::vector<DpReq*>& v, uint32_t cap = 0, uint32_t maxaln = 8) {
+	Pack pk;
+	pk.build(v);
+	const size_t n = v.size();
+	if(cap == 0) cap = v[0]->sc.local ? 2048 : 512;
+	const uint32_t maxedit = 2 * pk.stride + 8;
+	std::vector<bt2g_sw_problem> P(n);
+	std::vector<bt2g_sw_rect> RC(n);
+	std::vector<uint8_t> W;
+	for(size_t i = 0; i < n; i++) {
+		P[i] = v[i]->p;
+		P[i].read = (uint32_t)i;
+		P[i].win_off = (int64_t)W.size();
+		W.insert(W.end(), v[i]->win.begin(), v[i]->win.end());
+		RC[i] = v[i]->rect;
+	}
+	std::vector<bt2g_sw_result> R(n);
+	std::vector<bt2g_sw_cand> C(n * cap);
+	std::vector<int8_t> F(n * cap);
+	std::vector<int32_t> NA(n);
+	std::vector<bt2g_sw_aln> A(n * maxaln);
+	std::vector<bt2g_edit> E(n * maxaln * (size_t)maxedit);
+	int rc = bt2g_sw_align_bt(ctx(), pk.codes.data(), pk.quals.data(), pk.stride, pk.lens.data(), P.data(),
+	                          (uint32_t)n, W.data(), W.size(), RC.data(), &v[0]->sc, v[0]->enable8, cap, R.data(),
+	                          C.data(), maxaln, maxedit, NA.data(), A.data(), E.data(), F.data());
+	if(rc && rc != BT2G_ERR_OVERFLOW) return rc;
+	for(size_t i = 0; i < n; i++) {
+		DpReq* q = v[i];
+		if(R[i].ncand > (int32_t)cap || (NA[i] == (int32_t)maxaln && R[i].ncand > (int32_t)maxaln)) {
+			std::vector<DpReq*> one{q};
+			if((rc = run_dp(one, std::max<uint32_t>(cap, (uint32_t)R[i].ncand),
+			                std::max<uint32_t>(maxaln, (uint32_t)R[i].ncand))))
+				return rc;
+			continue;
+		}
+		q->o = R[i];
+		q->naln = NA[i];
+		q->cap = cap;
+		q->maxaln = maxaln;
+		q->maxedit = maxedit;
+		q->cands.assign(C.begin() + i * cap, C.begin() + i * cap + std::max(0, R[i].ncand));
+		q->fates.assign(F.begin() + i * cap, F.begin() + (i + 1) * cap);
+		q->alns.assign(A.begin() + i * maxaln, A.begin() + (i + 1) * maxaln);
+		q->edits.assign(E.begin() + i * maxaln * (size_t)maxedit, E.begin() + (i + 1) * maxaln * (size_t)maxedit);
+	}
+	return BT2G_OK;
+}
+
+int run_group(int kind, const std::vector<Req*>& g) {
+	switch(kind) {
+	case ST_EXACT: { std::vector<ExactReq*> v; for(Req* r : g) v.push_back(static_cast<ExactReq*>(r)); return run_exact(v); }
+	case ST_1MM:   { std::vector<MmReq*> v;    for(Req* r : g) v.push_back(static_cast<MmReq*>(r));    return run_mm(v); }
+	case ST_SEEDS: { std::vector<SeedReq*> v;  for(Req* r : g) v.push_back(static_cast<SeedReq*>(r));  return run_seeds(v); }
+	case ST_UG:    { std::vector<UgReq*> v;    for(Req* r : g) v.push_back(static_cast<UgReq*>(r));    return run_ug(v); }
+	default:       { std::vector<DpReq*> v;    for(Req* r : g) v.push_back(static_cast<DpReq*>(r));    return run_dp(v); }
+	}
+}
+
+const size_t MAX_BATCH = 8192;
+
+class Dispatcher {
+public:
+	// Serve one request: queued for the dispatcher thread (batching on) or
+	// run at once under the context lock.
+	void submit(Req* r) {
+		if(!batching()) {
+			std::lock_guard<std::mutex> lk(g_mu);
+			r->rc = run_group(r->kind, std::vector<Req*>{r});
+			g_batches[r->kind]++;
+		} else {
+			{
+				std::lock_guard<std::mutex> lk(mu_);
+				q_[r->kind].push_back(r);
+			}
+			cv_.notify_one();
+			while(sem_wait(&r->sem) != 0) {}
+		}
+		if(r->rc) die(ST_NAMES[r->kind], r->rc);
+	}
+
+private:
+	bool batching() {
+		std::call_once(once_, [this] {
+			const char* b = getenv("BT2G_BATCH");
+			on_ = !(b && b[0] == '0');
+			if(on_) {
+				std::lock_guard<std::mutex> lk(g_mu);
+				ctx();
+				std::thread(&Dispatcher::loop, this).detach();
+			}
+		});
+		return on_;
+	}
+
+	void loop() {
+		int next = 0;
+		std::vector<Req*> take;
+		for(;;) {
+			int kind = -1;
+			{
+				std::unique_lock<std::mutex> lk(mu_);
+				cv_.wait(lk, [this] {
+					for(int k = 0; k < ST_N; k++)
+						if(!q_[k].empty()) return true;
+					return false;
+				});
+				for(int d = 0; d < ST_N && kind < 0; d++) {         // round robin over the seams
+					int k = (next + d) % ST_N;
+					if(!q_[k].empty()) kind = k;
+				}
+				next = (kind + 1) % ST_N;
+				std::vector<Req*>& q = q_[kind];
+				const size_t m = std::min(q.size(), MAX_BATCH);
+				take.assign(q.begin(), q.begin() + m);
+				q.erase(q.begin(), q.begin() + m);
+			}
+			// group by the batch-wide arguments, keeping arrival order within a group
+			std::vector<bool> done(take.size(), false);
+			for(size_t i = 0; i < take.size(); i++) {
+				if(done[i]) continue;
+				std::vector<Req*> g;
+				for(size_t j = i; j < take.size(); j++)
+					if(!done[j] && take[j]->key == take[i]->key) { g.push_back(take[j]); done[j] = true; }
+				int rc;
+				{
+					std::lock_guard<std::mutex> lk(g_mu);
+					rc = run_group(kind, g);
+				}
+				g_batches[kind]++;
+				for(Req* r : g) {
+					r->rc = rc;
+					sem_post(&r->sem);
+				}
+			}
+		}
+	}
+
+	std::once_flag once_;
+	bool on_ = false;
+	std::mutex mu_;
+	std::condition_variable cv_;
+	std::vector<Req*> q_[ST_N];
+};
+
+Dispatcher g_disp;
+
 // AlnRes from an engine alignment: edits already in their final (5'->3',
 // post-trim) positions, so they are shifted by the leading trim before
 // setShape, which subtracts it (aligner_result.cpp:101-108).
@@ -186,13 +515,14 @@ struct DpState {
 	uint32_t next = 0;         // next engine alignment to hand out
 };
 
-thread_local std::vector<std::pair<const void*, DpState>> t_dp;
+// one entry per SwAligner of the worker thread (sw and osw, bt2_search.cpp:3130)
+thread_local std::vector<std::pair<const void*, DpState*>> t_dp;
 
 DpState& dp_state(const void* sw) {
 	for(auto& p : t_dp)
-		if(p.first == sw) return p.second;
-	t_dp.emplace_back(sw, DpState());
-	return t_dp.back().second;
+		if(p.first == sw) return *p.second;
+	t_dp.emplace_back(sw, new DpState());
+	return *t_dp.back().second;
 }
 
 // Protected-member access (no added members: same layout as the base).
@@ -210,8 +540,6 @@ struct SwAlignerAcc : public SwAligner {
 	size_t rdlen() const { return rdf_ - rdi_; }
 	size_t cminlen() const { return cperMinlen_; }
 };
-
-const uint32_t MAXALN0 = 64;
 
 }  // namespace
 
@@ -243,14 +571,10 @@ size_t __wrap__ZN11SeedAligner10exactSweepERK4EbwtRK4ReadRK7ScoringbbmRmS9_bR11S
 		return __real__ZN11SeedAligner10exactSweepERK4EbwtRK4ReadRK7ScoringbbmRmS9_bR11SeedResultsR17SeedSearchMetrics(
 			self, ebwt, read, sc, nofw, norc, mineMax, mineFw, mineRc, repex, hits, met);
 	}
-	Row r;
-	r.set(read.patFw, read.qual);
-	uint32_t out[8];
-	{
-		std::lock_guard<std::mutex> lk(g_mu);
-		int rc = bt2g_exact_sweep(ctx(), r.codes.data(), r.len, &r.len, 1, (uint32_t)mineMax, nofw, norc, out);
-		if(rc) die("bt2g_exact_sweep", rc);
-	}
+	ExactReq q((uint32_t)mineMax, nofw ? 1 : 0, norc ? 1 : 0);
+	q.r.set(read.patFw, read.qual);
+	g_disp.submit(&q);
+	const uint32_t* out = q.out;
 	count(ST_EXACT, true);
 	// outputs exactly as the tail of exactSweep (aligner_seed.cpp:944-967)
 	if(!nofw) mineFw = out[0];
@@ -284,22 +608,13 @@ bool __wrap__ZN11SeedAligner11oneMmSearchEPK4EbwtS2_RK4ReadRK7ScoringlbbbbbR11Se
 		return __real__ZN11SeedAligner11oneMmSearchEPK4EbwtS2_RK4ReadRK7ScoringlbbbbbR11SeedResultsR17SeedSearchMetrics(
 			self, ebwtFw, ebwtBw, read, sc, minsc, nofw, norc, local, repex, rep1mm, hits, met);
 	}
-	Row r;
-	r.set(read.patFw, read.qual);
-	int32_t ms = (int32_t)minsc, cnt = 0;
-	uint32_t ops = 0;
-	std::vector<bt2g_mm1> h(64);
-	{
-		std::lock_guard<std::mutex> lk(g_mu);
-		int rc = bt2g_one_mm(ctx(), r.codes.data(), r.quals.data(), r.len, &r.len, 1, &ms, &bs, nofw, norc,
-		                     (uint32_t)h.size(), h.data(), &cnt, &ops, nullptr);
-		if(rc == BT2G_ERR_OVERFLOW) {
-			h.resize((size_t)cnt);
-			rc = bt2g_one_mm(ctx(), r.codes.data(), r.quals.data(), r.len, &r.len, 1, &ms, &bs, nofw, norc,
-			                 (uint32_t)h.size(), h.data(), &cnt, &ops, nullptr);
-		}
-		if(rc) die("bt2g_one_mm", rc);
-	}
+	MmReq q(nofw ? 1 : 0, norc ? 1 : 0, bs);
+	q.r.set(read.patFw, read.qual);
+	q.minsc = (int32_t)minsc;
+	g_disp.submit(&q);
+	const std::vector<bt2g_mm1>& h = q.hits;
+	const int32_t cnt = q.cnt;
+	const uint32_t ops = q.ops;
 	count(ST_1MM, true);
 	static_cast<SeedAlignerAcc*>(self)->add_ops(ops);
 	for(int32_t k = 0; k < cnt; k++) {
@@ -335,17 +650,12 @@ void __wrap__ZN11SeedAligner14searchAllSeedsERK5EListI4SeedLi128EEPK4EbwtS7_RK4R
 	const uint32_t off = (uint32_t)sr.idx2off(0);
 	uint32_t per = nof > 1 ? (uint32_t)(sr.idx2off(1) - sr.idx2off(0))
 	                       : (uint32_t)(len > off + seedlen ? len - off - seedlen + 1 : 1);
-	Row r;
-	r.set(read.patFw, read.qual);
-	std::vector<uint32_t> out(2 * nof * 4);
-	int32_t ns = 0;
-	uint32_t ops = 0;
-	{
-		std::lock_guard<std::mutex> lk(g_mu);
-		int rc = bt2g_seed_search(ctx(), r.codes.data(), r.len, &r.len, 1, (uint32_t)seeds[0].len, per, off,
-		                          (uint32_t)nof, out.data(), &ns, &ops, nullptr);
-		if(rc) die("bt2g_seed_search", rc);
-	}
+	SeedReq q((uint32_t)seeds[0].len, per, off, (uint32_t)nof);
+	q.r.set(read.patFw, read.qual);
+	g_disp.submit(&q);
+	const std::vector<uint32_t>& out = q.out;
+	const int32_t ns = q.ns;
+	const uint32_t ops = q.ops;
 	if((size_t)ns != nof) {
 		fprintf(stderr, "bt2g adapter: seed offsets differ (engine %d, reference %zu)\n", ns, nof);
 		throw 1;
@@ -401,23 +711,16 @@ int __wrap__ZN9SwAligner13ungappedAlignERK20SDnaStringExpandableILi1024ELi2EERK1
 			self, rd, qu, coord, refs, reflen, sc, ohang, minsc, res);
 	}
 	const bool fw = coord.fw();
-	Row r;
-	r.set_fw_of(rd, qu, fw);
-	bt2g_ug_problem p;
-	memset(&p, 0, sizeof(p));
-	p.read = 0;
-	p.fw = fw ? 1 : 0;
-	p.off = coord.off();
-	p.refidx = (uint32_t)coord.ref();
-	p.minsc = (int32_t)minsc;
-	bt2g_ug_result o;
-	std::vector<bt2g_edit> ed(len + 1);
-	{
-		std::lock_guard<std::mutex> lk(g_mu);
-		int rc = bt2g_ungapped(ctx(), r.codes.data(), r.quals.data(), r.len, &r.len, &p, 1, &bs, ohang ? 1 : 0,
-		                       (uint32_t)ed.size(), &o, ed.data());
-		if(rc) die("bt2g_ungapped", rc);
-	}
+	UgReq q(bs, ohang ? 1 : 0);
+	q.r.set_fw_of(rd, qu, fw);
+	memset(&q.p, 0, sizeof(q.p));
+	q.p.fw = fw ? 1 : 0;
+	q.p.off = coord.off();
+	q.p.refidx = (uint32_t)coord.ref();
+	q.p.minsc = (int32_t)minsc;
+	g_disp.submit(&q);
+	const bt2g_ug_result& o = q.o;
+	const std::vector<bt2g_edit>& ed = q.ed;
 	count(ST_UG, true);
 	res.alres.reset();
 	if(o.ret != 1) return o.ret;
@@ -462,46 +765,27 @@ bool SwAlignerAcc::gpu_align(TAlScore& best, bool& served) {
 	   minsc_ > std::numeric_limits<int32_t>::max())
 		return false;
 	DpState& st = dp_state(this);
-	Row r;
-	r.set(*rdfw_, *qufw_);
-	bt2g_sw_problem p;
+	DpReq q(bs, (enable8_ && !readSse16_) ? 1 : 0);
+	q.r.set(*rdfw_, *qufw_);
+	bt2g_sw_problem& p = q.p;
 	memset(&p, 0, sizeof(p));
-	p.read = 0;
 	p.fw = fw_ ? 1 : 0;
-	p.refl = 0;
-	p.win_off = 0;
 	p.refidx = (uint32_t)refidx_;
 	p.ncol = (uint32_t)ncol;
 	p.minsc = (int32_t)minsc_;
-	bt2g_sw_rect rect;
-	rect.triml = (int32_t)rect_->triml;
-	rect.corel = (int32_t)rect_->corel;
-	rect.corer = (int32_t)rect_->corer;
-	rect.pad = 0;
-	std::vector<uint8_t> win(ncol + 1);
-	for(size_t i = 0; i <= ncol; i++) win[i] = (uint8_t)rf_[rfi_ + i];
-	bt2g_sw_result o;
-	uint32_t cap = 1024;
-	uint32_t maxaln = MAXALN0;
-	const uint32_t maxedit = (uint32_t)(2 * rdlen + 8);
-	std::vector<bt2g_sw_cand> cands;
-	for(;;) {
-		cands.assign(cap, bt2g_sw_cand());
-		st.fates.assign(cap, 0);
-		st.alns.assign(maxaln, bt2g_sw_aln());
-		st.edits.assign((size_t)maxaln * maxedit, bt2g_edit());
-		int rc;
-		{
-			std::lock_guard<std::mutex> lk(g_mu);
-			rc = bt2g_sw_align_bt(ctx(), r.codes.data(), r.quals.data(), r.len, &r.len, &p, 1, win.data(), win.size(),
-			                      &rect, &bs, (enable8_ && !readSse16_) ? 1 : 0, cap, &o, cands.data(), maxaln,
-			                      maxedit, &st.naln, st.alns.data(), st.edits.data(), st.fates.data());
-		}
-		if(rc == BT2G_ERR_OVERFLOW && o.ncand > (int32_t)cap) { cap = (uint32_t)o.ncand; continue; }
-		if(rc) die("bt2g_sw_align_bt", rc);
-		if(st.naln == (int32_t)maxaln && maxaln < (uint32_t)o.ncand) { maxaln = (uint32_t)o.ncand; continue; }
-		break;
-	}
+	q.rect.triml = (int32_t)rect_->triml;
+	q.rect.corel = (int32_t)rect_->corel;
+	q.rect.corer = (int32_t)rect_->corer;
+	q.rect.pad = 0;
+	q.win.assign((const uint8_t*)rf_ + rfi_, (const uint8_t*)rf_ + rfi_ + ncol + 1);
+	g_disp.submit(&q);
+	const bt2g_sw_result& o = q.o;
+	st.naln = q.naln;
+	st.fates.swap(q.fates);
+	st.alns.swap(q.alns);
+	st.edits.swap(q.edits);
+	const std::vector<bt2g_sw_cand>& cands = q.cands;
+	const uint32_t maxedit = q.maxedit;
 	if(st.naln < 0) {
 		fprintf(stderr, "bt2g adapter: sw_align_bt status %d\n", st.naln);
 		throw 1;

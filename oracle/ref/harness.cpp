@@ -435,6 +435,51 @@ void bt2ref_one_mm_gated(void* vh, int n, const char** seqs, const char** quals,
 	}
 }
 
+// As bt2ref_one_mm_gated, also returning the hits in discovery order (6 words
+// each, as bt2ref_one_mm: top, bot, fw, score, edit pos, edit chr | qchr << 8;
+// chr / qchr ASCII) at out[(i*cap + k)*6].
+void bt2ref_one_mm_gated_hits(void* vh, int n, const char** seqs, const char** quals, const int64_t* minsc,
+                              const uint64_t* sweep, int32_t* counts, int local, int cap, int64_t* out) {
+	RefHandle* h = (RefHandle*)vh;
+	SeedAligner al;
+	SeedResults sr;
+	SeedSearchMetrics met;
+	ScoreParams sp = {local ? 2 : 0, 6, 2, 1, 5, 3, 5, 3, 4, local, 0.0, 0.15};
+	Scoring sc = makeScoring(sp);
+	for(int i = 0; i < n; i++) {
+		counts[i] = 0;
+		uint64_t mfw = sweep[8 * (size_t)i], mrc = sweep[8 * (size_t)i + 1];
+		if(std::min(mfw, mrc) == 0) continue;
+		bool yfw = mfw <= 1, yrc = mrc <= 1;
+		if(!(yfw || yrc)) continue;
+		Read rd("r", seqs[i], quals[i]);
+		sr.clear();
+		sr.nextRead(rd);
+		al.oneMmSearch(h->fw, h->bw, rd, sc, minsc[i], !yfw, !yrc, local != 0, false, true, sr, met);
+		const EList<EEHit>& hits = sr.mm1EEHits();
+		counts[i] = (int32_t)hits.size();
+		for(size_t j = 0; j < hits.size() && (int)j < cap; j++) {
+			int64_t* o = out + ((size_t)i * cap + j) * 6;
+			o[0] = hits[j].top; o[1] = hits[j].bot; o[2] = hits[j].fw ? 1 : 0; o[3] = hits[j].score;
+			o[4] = hits[j].e1.pos; o[5] = (int64_t)hits[j].e1.chr | ((int64_t)hits[j].e1.qchr << 8);
+		}
+	}
+}
+
+// Ebwt::joinedToTextOff (bt2_idx.cpp:54) for n joined offsets with hit length
+// qlens[i]: out[3i..] = {tidx (-1 when rejected as straddling), textoff, tlen}.
+void bt2ref_joined_to_text_off(void* vh, int n, const uint32_t* offs, const uint32_t* qlens, int reject,
+                               int64_t* out) {
+	RefHandle* h = (RefHandle*)vh;
+	for(int i = 0; i < n; i++) {
+		TIndexOffU tidx = 0, toff = 0, tlen = 0;
+		bool straddled = false;
+		h->fw->joinedToTextOff(qlens[i], offs[i], tidx, toff, tlen, reject != 0, straddled);
+		int64_t* o = out + 3 * (size_t)i;
+		o[0] = tidx == OFF_MASK ? -1 : (int64_t)tidx; o[1] = toff; o[2] = tlen;
+	}
+}
+
 } // extern "C"
 
 // ---- backtrace (row 8a A21) --------------------------------------------------

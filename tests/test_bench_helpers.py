@@ -64,3 +64,49 @@ def test_policy_seed_geometry():
         p = bench.Policy(mode, 150, preset)
         assert (p.seedlen, p.interval, 1 + (150 - p.seedlen) // p.interval) == (L, ival, nseeds), (mode, preset)
         assert p.minsc == (60 if mode == "local" else -90)
+
+
+def test_ref_chain_compare_cpu():
+    """oracle/ref_chain: the reference's own seed-extension chain runs on a small
+    synthetic index, and compare() reports zero for identical buffers and
+    counts a planted difference at every stage."""
+    import os
+    import tempfile
+    import pytest
+    import numpy as np
+    import bench
+    import bt2_index as bi
+    import synth
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    if not os.path.exists(os.path.join(root, "oracle", "_ref", "libbt2ref.so")):
+        pytest.skip("oracle/_ref not built")
+    from oracle.ref_chain import RefChain, compare
+    g = synth.genome(5, 120_000, n_repeats=20, rep_len=2000, n_copies=3, n_runs=3)
+    idx = bi.build_index([g[:60_000], g[60_000:]], names=[b"a", b"b"])
+    base = os.path.join(tempfile.mkdtemp(), "g")
+    bi.write_index(base, idx)
+    r, q = bench.make_reads(idx.ref_codes, 400, 150, 3)
+    seqs = [bytes(a) for a in synth.to_ascii(r)]
+    pol = bench.Policy("ee", 150)
+    ch = RefChain(base)
+    ref = ch.run(seqs, [bytes(x) for x in q], np.full(400, 150), pol, 1 + (150 - pol.seedlen) // pol.interval, 16,
+                 15, idx.ref_codes, 2)
+    ch.close()
+    assert ref["sw"][:, 2].sum() > 300                    # most reads align
+    lut = np.full(256, 4)
+    lut[[65, 67, 71, 84]] = [0, 1, 2, 3]
+    h = ref["mm_hits"]
+    mh = np.zeros(h.shape[:2] + (8,), np.int64)
+    mh[:, :, :5] = h[:, :, :5]
+    mh[:, :, 5], mh[:, :, 6] = lut[h[:, :, 5] & 255], lut[(h[:, :, 5] >> 8) & 255]
+    gpu = {"sweep": ref["ex"][:, [0, 1, 3, 4, 5, 6, 7, 2]].astype(np.int64), "mm_cnt": ref["mm_cnt"].copy(),
+           "mm_hits": mh, "seeds": ref["seeds"].copy(), "rows": ref["rows"]["row"].copy(), "offs": ref["offs"].copy(),
+           "row_read": ref["rows"]["read"], "probs": {k: v.copy() for k, v in ref["probs"].items()}}
+    c = compare(ref, gpu)
+    assert all(c[k] == 0 for k in ("exact_sweep_mismatch", "one_mm_mismatch", "seed_mismatch", "row_mismatch",
+                                   "offset_mismatch", "frame_mismatch")), c
+    gpu["offs"][3] += 1
+    gpu["probs"]["refl"][5] += 1
+    gpu["sweep"][7, 0] += 1
+    c = compare(ref, gpu)
+    assert c["offset_mismatch"] == 1 and c["frame_mismatch"] == 1 and c["exact_sweep_mismatch"] == 1, c
