@@ -102,11 +102,19 @@ def log(*a):
     print(*a, file=sys.stderr, flush=True)
 
 
-def make_genome(mb, seed=2024):
+def make_genome(mb, seed=2024, model="hg38like"):
+    """Synthetic genome of mb Mbp in 8 references (2 below 8 Mbp).  model
+    "hg38like" (default): tests/golden/synth.genome_hg38like -- Alu/L1-like
+    interspersed repeat families with 3-20 % divergence, segmental duplications,
+    microsatellites and N gaps at hg38's genome fractions; "simple": random
+    sequence with planted 2 kb near-duplicates (round 1's bench genome)."""
     import synth
     n = int(mb * 1_000_000)
-    g = synth.genome(seed, n, n_repeats=max(1, n // 200_000), rep_len=2000, n_copies=3,
-                     n_runs=max(1, n // 2_000_000))
+    if model == "hg38like":
+        g = synth.genome_hg38like(seed, n)
+    else:
+        g = synth.genome(seed, n, n_repeats=max(1, n // 200_000), rep_len=2000, n_copies=3,
+                         n_runs=max(1, n // 2_000_000))
     nref = 8 if n >= 8_000_000 else 2
     cuts = np.linspace(0, n, nref + 1).astype(np.int64)
     parts = [g[cuts[i]:cuts[i + 1]] for i in range(nref)]
@@ -136,15 +144,28 @@ def _reads_at(g, gpos, rc, length, rng):
     return out.astype(np.uint8), quals
 
 
+def _n_free_starts(rng, g, sizes, starts, n, span):
+    """n fragment starts uniform over the genome's positions whose next `span`
+    bases lie in one reference and hold no N (uniform over
+    non-N positions)."""
+    isn = np.concatenate([[0], np.cumsum(g == 4, dtype=np.int64)])
+    out = np.empty(0, np.int64)
+    while len(out) < n:
+        m = int((n - len(out)) * 1.2) + 16
+        ref = rng.choice(len(sizes), m, p=sizes / sizes.sum())
+        pos = starts[ref] + (rng.random(m) * (sizes[ref] - span - 2)).astype(np.int64)
+        ok = isn[pos + span] == isn[pos]
+        out = np.concatenate([out, pos[ok]])
+    return out[:n]
+
+
 def make_reads(parts, n, length, seed):
     """Vectorised version of tests/golden/synth.reads (BASELINE.md section 3 model)."""
     rng = np.random.default_rng(seed)
     sizes = np.array([len(p) for p in parts], np.int64)
-    ref = rng.choice(len(parts), n, p=sizes / sizes.sum())
-    pos = (rng.random(n) * (sizes[ref] - length - 2)).astype(np.int64)
     starts = np.concatenate([[0], np.cumsum(sizes)])[:-1]
     g = np.concatenate(parts)
-    gpos = starts[ref] + pos
+    gpos = _n_free_starts(rng, g, sizes, starts, n, length + 1)
     win = g[gpos[:, None] + np.arange(length + 1)[None, :]]
     out = win[:, :length].copy()
     ind = np.nonzero(rng.random(n) < 0.05)[0]
@@ -171,13 +192,12 @@ def make_pairs(parts, n, length, seed):
     Returns 2n reads: mate 1 of pair i in row i, mate 2 in row n + i."""
     rng = np.random.default_rng(seed)
     sizes = np.array([len(p) for p in parts], np.int64)
-    ref = rng.choice(len(parts), n, p=sizes / sizes.sum())
     frag = np.clip(np.rint(rng.normal(300, 50, n)), 200, 500).astype(np.int64)
     frag = np.maximum(frag, length)
-    pos = (rng.random(n) * (sizes[ref] - frag - 2)).astype(np.int64)
     starts = np.concatenate([[0], np.cumsum(sizes)])[:-1]
     g = np.concatenate(parts)
-    left, right = starts[ref] + pos, starts[ref] + pos + frag - length
+    left = _n_free_starts(rng, g, sizes, starts, n, 502)
+    right = left + frag - length
     flip = rng.random(n) < 0.5                      # fragment from the reverse strand: mate 1 on the right
     r1, q1 = _reads_at(g, np.where(flip, right, left), flip, length, rng)
     r2, q2 = _reads_at(g, np.where(flip, left, right), ~flip, length, rng)
@@ -691,7 +711,10 @@ def mate_parity(pipe, mate):
 
 def workload(args):
     size = "hg38-size; " if args.genome_mb >= 3000 else ""
-    genome = (f"vs a {args.genome_mb:.0f} Mbp synthetic genome ({size}hg38 itself is unavailable offline), "
+    model = ("hg38-like repeat landscape: Alu/L1-like families at 10 %/17 % with 3-20 % divergence, segmental "
+             "duplications, microsatellites, N gaps" if args.genome_model == "hg38like" else
+             "random sequence with planted 2 kb near-repeats")
+    genome = (f"vs a {args.genome_mb:.0f} Mbp synthetic genome ({size}{model}; hg38 itself is unavailable offline), "
               f"index built like bowtie2-build (offRate 4, ftabChars 10)")
     vs = args.preset == "very-sensitive"
     seed = ("exact sweep + gated 1-mm + seed round 0 + SA offsets + <=2 seed-extension DPs/read "
@@ -724,6 +747,7 @@ def main():
                          "configs[4]'s policy, sharded by torchrun across GPUs)")
     ap.add_argument("--genome-mb", type=float, default=3100.0,
                     help="synthetic genome size (default: hg38's 3.1 Gbp; the index is built on the GPU, ~160 s)")
+    ap.add_argument("--genome-model", choices=("hg38like", "simple"), default="hg38like")
     ap.add_argument("--cpu-sample", type=int, default=1_000_000)
     ap.add_argument("--cpu-threads", type=int, default=0, help="0: the usable cores of the host (cgroup quota / "
                                                                    "affinity)")
@@ -748,7 +772,7 @@ def main():
         dist.init_process_group("nccl", device_id=dev)
 
     t0 = time.time()
-    parts, names = make_genome(args.genome_mb)
+    parts, names = make_genome(args.genome_mb, model=args.genome_model)
     log(f"[rank {rank}] genome {sum(len(p) for p in parts)/1e6:.0f} Mbp in {time.time()-t0:.1f}s")
     t1 = time.time()
     cache = args.index_cache
@@ -840,6 +864,25 @@ def main():
                       "launches_per_step": mstats[4][0] / args.steps}
         log(f"[rank {rank}] mate search: {mate_stats}")
 
+    # ---- the repeat landscape the last step saw (rank 0's batch) -------------
+    def hist(x):
+        edges = [1, 2, 11, 101, 1001, 1 << 62]
+        x = x.cpu().numpy() if hasattr(x, "cpu") else np.asarray(x)
+        return {f"{lo}-{hi - 1}" if hi - lo > 1 else str(lo): int(((x >= lo) & (x < hi)).sum())
+                for lo, hi in zip(edges[:-1], edges[1:])}
+    swl = pipe.sweep.to(torch.int64) & 0xFFFFFFFF
+    exr = torch.minimum(swl[:, 0], swl[:, 1]) == 0
+    ex_sz = torch.where(swl[:, 3] > swl[:, 2], swl[:, 3] - swl[:, 2], swl[:, 5] - swl[:, 4])[exr]
+    sdl = pipe.seeds[:last["m"]].to(torch.int64) & 0xFFFFFFFF
+    sd_sz = (sdl[..., 1] - sdl[..., 0]).flatten()
+    sd_sz = sd_sz[sd_sz > 0]
+    dpr = torch.bincount(last["probs"].view(torch.int32)[:, 0].to(torch.int64), minlength=pipe.n)
+    landscape = {"exact_hit_range_sizes": hist(ex_sz), "seed_hit_range_sizes": hist(sd_sz),
+                 "seed_hit_range_mean": float(sd_sz.double().mean()) if sd_sz.numel() else 0.0,
+                 "dps_per_read": {str(k): int(v) for k, v in enumerate(torch.bincount(dpr).tolist())},
+                 "hit_rows_per_read": float(last["nrows"] / pipe.n)}
+    log(f"[rank {rank}] landscape {landscape}")
+
     # ---- CPU baseline: the reference on the host cores, rank 0, N=1 ---------
     cpu = None
     parity = None
@@ -909,6 +952,7 @@ def main():
                             "unit": "T lane-ops/s", "frac": sw_gcups * VALU_OPS_PER_CELL / 1e3 / VALU_PEAK_TOPS,
                             "ops_per_cell": VALU_OPS_PER_CELL} if args.mode == "ee" else None,
             "backtrace": bt_stats,
+            "landscape": landscape,
             "mate_search": mate_stats,
             "cpu_baseline": cpu,
             "parity_sample": parity,

@@ -276,7 +276,13 @@ void bt2ref_seed_search(void* vh, int n, const char** seqs, const char** quals,
 	PerReadMetrics prm;
 	ScoreParams sp = {0, 6, 2, 1, 5, 3, 5, 3, 4, 0, 0.0, 0.15};
 	Scoring sc = makeScoring(sp);
-	AlignmentCache scCurrent(16 * 1024 * 1024, false);
+	// Engine-level parity: a current-read cache large enough never to run out.
+	// The server's default (--seed-cache-sz 20 MB, bt2_search.cpp:484) drops a
+	// seed hit when its SA range no longer fits the per-read pool
+	// (aligner_cache.cpp:82-96) -- giant ranges of e.g. poly-A 22-mers at hg38
+	// scale; that resource limit is reproduced by the drop-in server, which runs
+	// the reference's own cache code (integration/bt2g_seams.cpp), not here.
+	AlignmentCache scCurrent((size_t)1 << 30, false);
 	AlignmentCacheIface ca(&scCurrent, NULL, NULL);
 	EList<Seed> seeds;
 	Constraint gc = Constraint::penaltyFuncBased(sc.scoreMin);
