@@ -881,6 +881,13 @@ def main():
                  "seed_hit_range_mean": float(sd_sz.double().mean()) if sd_sz.numel() else 0.0,
                  "dps_per_read": {str(k): int(v) for k, v in enumerate(torch.bincount(dpr).tolist())},
                  "hit_rows_per_read": float(last["nrows"] / pipe.n)}
+    mmo = pipe.mm_ops.to(torch.int64)
+    mmo = mmo[mmo > 0].double()
+    if mmo.numel():
+        q = torch.quantile(mmo[:1 << 24], torch.tensor([0.5, 0.9, 0.99, 0.999], dtype=torch.float64,
+                                                       device=mmo.device)).tolist()
+        landscape["one_mm_ops_per_read"] = {"reads": int(mmo.numel()), "mean": float(mmo.mean()), "p50": q[0],
+                                            "p90": q[1], "p99": q[2], "p999": q[3], "max": float(mmo.max())}
     log(f"[rank {rank}] landscape {landscape}")
 
     # ---- CPU baseline: the reference on the host cores, rank 0, N=1 ---------

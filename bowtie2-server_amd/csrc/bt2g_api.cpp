@@ -418,6 +418,7 @@ struct OneMmScratch {
 	uint32_t* items = nullptr;
 	uint4* near_state = nullptr;
 	uint32_t* near_dep = nullptr;
+	MmBranch* brq = nullptr;
 };
 }  // namespace
 
@@ -437,6 +438,10 @@ static int one_mm_impl(bt2g_ctx* c, const uint8_t* reads, const uint8_t* quals, 
 	HIPCHK(hipMallocAsync((void**)&s.items, sizeof(uint32_t) * (size_t)n * 4, st));
 	HIPCHK(hipMallocAsync((void**)&s.near_state, sizeof(uint4) * (size_t)n * 4, st));
 	HIPCHK(hipMallocAsync((void**)&s.near_dep, sizeof(uint32_t) * (size_t)n * 4, st));
+	// far-half branches queued for the branch kernel: 4 per read on average
+	// (hg38-like reads: ~1); a full queue degrades to walking in place
+	const uint32_t brq_cap = n * 4 + 1024;
+	HIPCHK(hipMallocAsync((void**)&s.brq, sizeof(MmBranch) * (size_t)brq_cap, st));
 	HIPCHK(hipMemsetAsync(s.ovf, 0, sizeof(int32_t) * 8, st));
 	HIPCHK(hipMemsetAsync(bwops, 0, sizeof(uint32_t) * n, st));
 	if(loads) HIPCHK(hipMemsetAsync(loads, 0, sizeof(uint32_t) * n, st));
@@ -444,7 +449,7 @@ static int one_mm_impl(bt2g_ctx* c, const uint8_t* reads, const uint8_t* quals, 
 		ProfScope ps(c, 2, st);
 		launch_one_mm(c->fw, c->bw, reads, quals, stride, lens, n, minsc, *sc, nofw, norc, gate, cap, s.items,
 		              (uint32_t*)s.ovf + 1, s.near_state, s.near_dep, s.slots, s.slot_counts, hits, counts, bwops,
-		              loads, s.ovf, st);
+		              loads, s.ovf, s.brq, brq_cap, st);
 	}
 	HIPCHK(hipGetLastError());
 	int32_t ovf = 0;
@@ -455,6 +460,7 @@ static int one_mm_impl(bt2g_ctx* c, const uint8_t* reads, const uint8_t* quals, 
 	HIPCHK(hipFreeAsync(s.items, st));
 	HIPCHK(hipFreeAsync(s.near_state, st));
 	HIPCHK(hipFreeAsync(s.near_dep, st));
+	HIPCHK(hipFreeAsync(s.brq, st));
 	if(sync_overflow) {
 		HIPCHK(hipStreamSynchronize(st));
 		if(ovf) return fail(BT2G_ERR_OVERFLOW, "one-mismatch hits exceed cap %u", cap);

@@ -207,8 +207,10 @@ k_seed_search(DevEbwt F, DevEbwt B, const uint8_t* __restrict__ reads, uint32_t 
 // per-(read, strand, index) slots are concatenated here in the reference's
 // loop order (fw/BWT, fw/BWT', rc/BWT, rc/BWT').
 // --------------------------------------------------------------------------
-// Concatenate the 4 per-direction slots of each read in discovery order.
-__global__ void k_one_mm_compact(const bt2g_mm1* __restrict__ slots, const int32_t* __restrict__ slot_counts,
+// Concatenate the 4 per-direction slots of each read in discovery order.  A
+// slot's hits arrive out of order (branches finish in the branch kernel), each
+// tagged with its discovery number in `pad`: they are put back in order here.
+__global__ void k_one_mm_compact(bt2g_mm1* __restrict__ slots, const int32_t* __restrict__ slot_counts,
                                  uint32_t n, uint32_t cap, bt2g_mm1* __restrict__ hits, int32_t* __restrict__ counts,
                                  int32_t* __restrict__ overflow) {
 	uint32_t r = blockIdx.x * blockDim.x + threadIdx.x;
@@ -216,10 +218,22 @@ __global__ void k_one_mm_compact(const bt2g_mm1* __restrict__ slots, const int32
 	int32_t k = 0;
 	bool ovf = false;
 	for(int s = 0; s < 4; s++) {
-		int32_t c = slot_counts[(size_t)r * 4 + s];
+		const int32_t c = slot_counts[(size_t)r * 4 + s];
 		if((uint32_t)c > cap) ovf = true;
-		for(int32_t i = 0; i < c && i < (int32_t)cap; i++) {
-			if((uint32_t)k < cap) hits[(size_t)r * cap + k] = slots[((size_t)r * 4 + s) * cap + i];
+		bt2g_mm1* sl = slots + ((size_t)r * 4 + s) * cap;
+		const int32_t m = c < (int32_t)cap ? c : (int32_t)cap;
+		for(int32_t i = 1; i < m; i++) {                 // insertion sort by discovery number (m <= cap)
+			const bt2g_mm1 h = sl[i];
+			int32_t j = i - 1;
+			while(j >= 0 && (uint32_t)sl[j].pad > (uint32_t)h.pad) { sl[j + 1] = sl[j]; j--; }
+			sl[j + 1] = h;
+		}
+		for(int32_t i = 0; i < m; i++) {
+			if((uint32_t)k < cap) {
+				bt2g_mm1 h = sl[i];
+				h.pad = 0;
+				hits[(size_t)r * cap + k] = h;
+			}
 			k++;
 		}
 		if((uint32_t)c > cap) k += c - (int32_t)cap;
@@ -280,9 +294,10 @@ void launch_one_mm(const DevEbwt& F, const DevEbwt& B, const uint8_t* reads, con
                    const uint32_t* lens, uint32_t n, const int32_t* minsc, const bt2g_scoring& sc, int nofw,
                    int norc, const uint32_t* gate, uint32_t cap, uint32_t* items, uint32_t* counters,
                    uint4* near_state, uint32_t* near_dep, bt2g_mm1* slots, int32_t* slot_counts, bt2g_mm1* hits,
-                   int32_t* counts, uint32_t* ops, uint32_t* loads, int32_t* overflow, hipStream_t st) {
+                   int32_t* counts, uint32_t* ops, uint32_t* loads, int32_t* overflow, MmBranch* brq,
+                   uint32_t brq_cap, hipStream_t st) {
 	launch_one_mm_q(F, B, reads, quals, stride, lens, n, minsc, sc, nofw, norc, gate, cap, items, counters,
-	                near_state, near_dep, slots, slot_counts, ops, loads, st);
+	                near_state, near_dep, slots, slot_counts, ops, loads, brq, brq_cap, st);
 	hipLaunchKernelGGL(k_one_mm_compact, dim3((n + 255) / 256), dim3(256), 0, st, slots, slot_counts, n, cap, hits,
 	                   counts, overflow);
 }

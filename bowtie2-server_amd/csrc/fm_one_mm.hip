@@ -8,10 +8,16 @@
 // small state machine over its item -- near half exact, far half with one
 // mismatch, one branch walk per alternative base -- performing exactly one LF
 // operation (one or two 64-B side gathers) per loop iteration, so lanes in
-// different phases still issue their gathers together.  Hits go to per-item
-// slots in discovery order;
-// k_one_mm_compact concatenates the four slots of a read in the reference's
-// loop order (fw/BWT, fw/BWT', rc/BWT, rc/BWT').
+// different phases still issue their gathers together.  A far-half
+// alternative that survives its mismatch step is not walked in place: it goes
+// to a global branch queue (k_one_mm_branch walks every queued branch in its
+// own lane), so an item in a high-copy repeat -- thousands of LF steps of
+// branch walks one after another in the reference -- no longer holds its wave
+// for the whole kernel (hg38-like genome: p50 161 but max 16 379 LF ops per
+// read).  Each candidate carries its discovery number; hits land in per-item
+// slots in completion order and k_one_mm_compact restores the reference's
+// order and concatenates the four slots of a read in its loop order
+// (fw/BWT, fw/BWT', rc/BWT, rc/BWT').
 #include "fm_device.h"
 #include "bt2g_kernels.h"
 #include "dev_util.h"
@@ -194,7 +200,8 @@ k_one_mm_q(DevEbwt F, DevEbwt B, const uint8_t* __restrict__ reads, const uint8_
            double ncl_const, double ncl_lin, const uint32_t* __restrict__ items,
            const uint32_t* __restrict__ nitems_p, const uint4* __restrict__ st4,
            const uint32_t* __restrict__ sdep, uint32_t cap, bt2g_mm1* __restrict__ slots, int32_t* __restrict__ slot_counts, uint32_t* __restrict__ ops_out,
-           uint32_t* __restrict__ loads_out) {
+           uint32_t* __restrict__ loads_out, MmBranch* __restrict__ brq, uint32_t* __restrict__ brq_n,
+           uint32_t brq_cap) {
 	const uint32_t nitems = *nitems_p;
 	const int64_t matchsc = (int64_t)((float)P.match + 0.5f);
 
@@ -223,6 +230,7 @@ k_one_mm_q(DevEbwt F, DevEbwt B, const uint8_t* __restrict__ reads, const uint8_
 	bool match = true;
 	uint32_t topm = 0, botm = 0, topmp = 0, botmp = 0;        // branch range (+ mirror)
 	int32_t nh = 0;
+	uint32_t dseq = 0, bseq = 0;                // discovery numbers: next, and the in-place branch's
 	uint32_t ops = 0, loads = 0;
 #pragma unroll
 	for(int i = 0; i < 16; i++) alt_s[i][tid] = 0;
@@ -239,8 +247,7 @@ k_one_mm_q(DevEbwt F, DevEbwt B, const uint8_t* __restrict__ reads, const uint8_
 						if(j == rdc || B_(j) == T_(j)) continue;
 						depm = dep + 1;
 						topm = T_(j); botm = B_(j); topmp = TP_(j); botmp = BP_(j);
-						if(depm < len) { started = true; break; }
-						// branch complete at the last base: report (no further LF step)
+						// the hit this alternative would report (aligner_seed.cpp:1166-1290)
 						uint32_t off5p = dep;
 						if(fw == ebwtfw) off5p = len - off5p - 1;
 						int64_t score = (int64_t)(len - 1) * matchsc;
@@ -256,11 +263,34 @@ k_one_mm_q(DevEbwt F, DevEbwt B, const uint8_t* __restrict__ reads, const uint8_
 								else lb += matchsc;
 							}
 						}
-						if(valid && score >= minsc) {
+						valid = valid && score >= minsc;
+						const uint32_t myseq = dseq++;
+						if(depm < len) {
+							// hand the walk to the branch kernel; walk in place when the queue is full
+							const uint32_t q = atomicAdd(brq_n, 1u);
+							if(q < brq_cap) {
+								MmBranch b;
+								b.rng = make_uint4(topm, botm, topmp, botmp);
+								b.slot = slot;
+								b.seq = myseq;
+								b.meta = depm | ((uint32_t)j << 16) | ((uint32_t)rdc << 20) | ((valid ? 1u : 0u) << 24) |
+								         ((ebwtfw ? 1u : 0u) << 25);
+								b.score = (int32_t)score;
+								b.off5p = (int32_t)off5p;
+								b.pad[0] = b.pad[1] = b.pad[2] = 0;
+								brq[q] = b;
+								continue;
+							}
+							bseq = myseq;
+							started = true;
+							break;
+						}
+						// branch complete at the last base: report (no further LF step)
+						if(valid) {
 							if((uint32_t)nh < cap)
 								slots[(size_t)slot * cap + nh] = bt2g_mm1{ebwtfw ? topm : topmp, ebwtfw ? botm : botmp,
 								                                          fw ? 1 : 0, (int32_t)score, (int32_t)off5p,
-								                                          j, rdc, 0};
+								                                          j, rdc, (int32_t)myseq};
 							nh++;
 						}
 					}
@@ -300,6 +330,7 @@ k_one_mm_q(DevEbwt F, DevEbwt B, const uint8_t* __restrict__ reads, const uint8_
 			nceil = (int)(ncl_const + ncl_lin * (double)len);
 			if(nceil < 0) nceil = 0;
 			nh = 0;
+			dseq = 0;
 			ops = loads = 0;
 			// seq = fw ? (ebwtfw ? patFw : patFwRev) : (ebwtfw ? patRc : patRcRev)
 			seq = SeqView{rd, len, fw ? !ebwtfw : ebwtfw, !fw};
@@ -396,7 +427,7 @@ k_one_mm_q(DevEbwt F, DevEbwt B, const uint8_t* __restrict__ reads, const uint8_
 					if((uint32_t)nh < cap)
 						slots[(size_t)slot * cap + nh] = bt2g_mm1{ebwtfw ? topm : topmp, ebwtfw ? botm : botmp,
 						                                          fw ? 1 : 0, (int32_t)score, (int32_t)off5p, j, rdc,
-						                                          0};
+						                                          (int32_t)bseq};
 					nh++;
 				}
 				j++;
@@ -406,11 +437,67 @@ k_one_mm_q(DevEbwt F, DevEbwt B, const uint8_t* __restrict__ reads, const uint8_
 	}
 }
 
+// Walk every queued far-half branch to the read's end (or its death), one
+// lane per branch: exact steps on the read's remaining bases with the same LF
+// operations and op counting as the in-place walk (ST_BR above).  A completed
+// valid branch appends its hit to its slot (after the far kernel's own hits,
+// slot_counts[] is the slot's running count).
+__global__ void __launch_bounds__(256)
+k_one_mm_branch(DevEbwt F, DevEbwt B, const uint8_t* __restrict__ reads, uint32_t stride,
+                const uint32_t* __restrict__ lens, const MmBranch* __restrict__ brq,
+                const uint32_t* __restrict__ brq_n, uint32_t brq_cap, uint32_t cap, bt2g_mm1* __restrict__ slots,
+                int32_t* __restrict__ slot_counts, uint32_t* __restrict__ ops_out, uint32_t* __restrict__ loads_out) {
+	const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+	const uint32_t nq = *brq_n < brq_cap ? *brq_n : brq_cap;
+	if(i >= nq) return;
+	const MmBranch b = brq[i];
+	const bool ebwtfw = (b.meta >> 25) & 1u;
+	const DevEbwt& E = ebwtfw ? F : B;
+	const uint32_t r = b.slot >> 2;
+	const bool fw = ((b.slot >> 1) & 1u) == 0;
+	const uint32_t len = lens[r];
+	const SeqView seq{reads + (size_t)r * stride, len, fw ? !ebwtfw : ebwtfw, !fw};
+	uint32_t topm = b.rng.x, botm = b.rng.y, topmp = b.rng.z, botmp = b.rng.w;
+	uint32_t depm = b.meta & 0xffffu;
+	uint32_t ops = 0, loads = 0;
+	bool done = false;
+	while(depm < len) {
+		const int c = seq[len - depm - 1];
+		ops++;
+		bool dead;
+		if(botm - topm > 1) {
+			uint32_t ot[4] = {0, 0, 0, 0}, ob[4] = {0, 0, 0, 0}, otp[4], obp[4];
+			otp[0] = topmp;
+			loads += bi_step(E, topm, botm, topmp, ot, ob, otp, obp);
+			topm = at4(ot, c); botm = at4(ob, c); topmp = at4(otp, c); botmp = at4(obp, c);
+			dead = botm <= topm;
+		} else {
+			SideData s1;
+			load_side(E, topm / 192u, s1);
+			loads++;
+			const int rowl = side_rowL(s1, topm % 192u);
+			dead = rowl != c || topm == E.zoff;
+			if(!dead) { topm = occ1(E, s1, topm, rowl); botm = topm + 1; }
+		}
+		if(dead) break;
+		if(++depm == len) done = true;
+	}
+	if(done && ((b.meta >> 24) & 1u)) {
+		const int32_t p = atomicAdd(&slot_counts[b.slot], 1);
+		if((uint32_t)p < cap)
+			slots[(size_t)b.slot * cap + p] = bt2g_mm1{ebwtfw ? topm : topmp, ebwtfw ? botm : botmp, fw ? 1 : 0,
+			                                           b.score, b.off5p, (int32_t)((b.meta >> 16) & 0xfu),
+			                                           (int32_t)((b.meta >> 20) & 0xfu), (int32_t)b.seq};
+	}
+	if(ops) atomicAdd(&ops_out[r], ops);
+	if(ops && loads_out) atomicAdd(&loads_out[r], loads);
+}
+
 void launch_one_mm_q(const DevEbwt& F, const DevEbwt& B, const uint8_t* reads, const uint8_t* quals, uint32_t stride,
                      const uint32_t* lens, uint32_t n, const int32_t* minsc, const bt2g_scoring& sc, int nofw,
                      int norc, const uint32_t* gate, uint32_t cap, uint32_t* items, uint32_t* counters,
                      uint4* near_state, uint32_t* near_dep, bt2g_mm1* slots, int32_t* slot_counts, uint32_t* ops,
-                     uint32_t* loads, hipStream_t st) {
+                     uint32_t* loads, MmBranch* brq, uint32_t brq_cap, hipStream_t st) {
 	MmParams P{sc.match, sc.mmp_max, sc.mmp_min, sc.npen, sc.local, 0, 0};
 	// counters[0]/[2] = item counts of the BWT / BWT' lists (zeroed by the caller)
 	hipLaunchKernelGGL(k_one_mm_items, dim3((n + 255) / 256), dim3(256), 0, st, reads, stride, lens, n, gate, nofw,
@@ -423,8 +510,10 @@ void launch_one_mm_q(const DevEbwt& F, const DevEbwt& B, const uint8_t* reads, c
 	                   counters + 2, near_state + half, near_dep + half, ops, loads);
 	hipLaunchKernelGGL(k_one_mm_q<true>, dim3(grid), dim3(256), 0, st, F, B, reads, quals, stride, lens, minsc, P,
 	                   sc.ncl_const, sc.ncl_lin, items, counters, near_state, near_dep, cap, slots, slot_counts, ops,
-	                   loads);
+	                   loads, brq, counters + 4, brq_cap);
 	hipLaunchKernelGGL(k_one_mm_q<false>, dim3(grid), dim3(256), 0, st, F, B, reads, quals, stride, lens, minsc, P,
 	                   sc.ncl_const, sc.ncl_lin, items + half, counters + 2, near_state + half, near_dep + half, cap,
-	                   slots, slot_counts, ops, loads);
+	                   slots, slot_counts, ops, loads, brq, counters + 4, brq_cap);
+	hipLaunchKernelGGL(k_one_mm_branch, dim3((brq_cap + 255) / 256), dim3(256), 0, st, F, B, reads, stride, lens, brq,
+	                   counters + 4, brq_cap, cap, slots, slot_counts, ops, loads);
 }

@@ -140,8 +140,9 @@ typedef struct {
  * bt2_search.cpp:3654-3667 calls it (aligner_seed.h:1731-1743,
  * aligner_seed.cpp:973-1323).  Hits are returned per read in the reference's
  * discovery order: hits[i*cap .. i*cap+counts[i]), counts[i] may exceed cap
- * (then BT2G_ERR_OVERFLOW is returned and only cap hits are stored).  bwops and
- * loads (optional) as for bt2g_seed_search. */
+ * (then BT2G_ERR_OVERFLOW is returned and cap of the hits are stored, which
+ * ones unspecified: call again with cap >= counts[i] for the ordered list).
+ * bwops and loads (optional) as for bt2g_seed_search. */
 int bt2g_one_mm(bt2g_ctx* ctx, const uint8_t* reads, const uint8_t* quals, uint32_t stride, const uint32_t* lens,
                 uint32_t n, const int32_t* minsc, const bt2g_scoring* sc, int nofw, int norc, uint32_t cap,
                 bt2g_mm1* hits, int32_t* counts, uint32_t* bwops, uint32_t* loads);
