@@ -419,6 +419,10 @@ struct OneMmScratch {
 	uint4* near_state = nullptr;
 	uint32_t* near_dep = nullptr;
 	MmBranch* brq = nullptr;
+	uint32_t* fb_items = nullptr;
+	uint4* fb_st4 = nullptr;
+	uint32_t* fb_sdep = nullptr;
+	uint32_t* slot_flag = nullptr;
 };
 }  // namespace
 
@@ -434,22 +438,26 @@ static int one_mm_impl(bt2g_ctx* c, const uint8_t* reads, const uint8_t* quals, 
 	OneMmScratch s;
 	HIPCHK(hipMallocAsync((void**)&s.slots, sizeof(bt2g_mm1) * (size_t)n * 4 * cap, st));
 	HIPCHK(hipMallocAsync((void**)&s.slot_counts, sizeof(int32_t) * (size_t)n * 4, st));
-	HIPCHK(hipMallocAsync((void**)&s.ovf, sizeof(int32_t) * 8, st));
+	HIPCHK(hipMallocAsync((void**)&s.ovf, sizeof(int32_t) * 16, st));
 	HIPCHK(hipMallocAsync((void**)&s.items, sizeof(uint32_t) * (size_t)n * 4, st));
 	HIPCHK(hipMallocAsync((void**)&s.near_state, sizeof(uint4) * (size_t)n * 4, st));
 	HIPCHK(hipMallocAsync((void**)&s.near_dep, sizeof(uint32_t) * (size_t)n * 4, st));
-	// far-half branches queued for the branch kernel: 4 per read on average
-	// (hg38-like reads: ~1); a full queue degrades to walking in place
-	const uint32_t brq_cap = n * 4 + 1024;
+	// far-half branches queued for the branch kernel (16 per read: an item that
+	// meets a full queue is redone whole by the in-place state machine)
+	const uint32_t brq_cap = n * 16 + 1024;
 	HIPCHK(hipMallocAsync((void**)&s.brq, sizeof(MmBranch) * (size_t)brq_cap, st));
-	HIPCHK(hipMemsetAsync(s.ovf, 0, sizeof(int32_t) * 8, st));
+	HIPCHK(hipMallocAsync((void**)&s.fb_items, sizeof(uint32_t) * (size_t)n * 4, st));
+	HIPCHK(hipMallocAsync((void**)&s.fb_st4, sizeof(uint4) * (size_t)n * 4, st));
+	HIPCHK(hipMallocAsync((void**)&s.fb_sdep, sizeof(uint32_t) * (size_t)n * 4, st));
+	HIPCHK(hipMallocAsync((void**)&s.slot_flag, sizeof(uint32_t) * (size_t)n * 4, st));
+	HIPCHK(hipMemsetAsync(s.ovf, 0, sizeof(int32_t) * 16, st));
 	HIPCHK(hipMemsetAsync(bwops, 0, sizeof(uint32_t) * n, st));
 	if(loads) HIPCHK(hipMemsetAsync(loads, 0, sizeof(uint32_t) * n, st));
 	{
 		ProfScope ps(c, 2, st);
 		launch_one_mm(c->fw, c->bw, reads, quals, stride, lens, n, minsc, *sc, nofw, norc, gate, cap, s.items,
 		              (uint32_t*)s.ovf + 1, s.near_state, s.near_dep, s.slots, s.slot_counts, hits, counts, bwops,
-		              loads, s.ovf, s.brq, brq_cap, st);
+		              loads, s.ovf, s.brq, brq_cap, s.fb_items, s.fb_st4, s.fb_sdep, s.slot_flag, st);
 	}
 	HIPCHK(hipGetLastError());
 	int32_t ovf = 0;
@@ -461,6 +469,10 @@ static int one_mm_impl(bt2g_ctx* c, const uint8_t* reads, const uint8_t* quals, 
 	HIPCHK(hipFreeAsync(s.near_state, st));
 	HIPCHK(hipFreeAsync(s.near_dep, st));
 	HIPCHK(hipFreeAsync(s.brq, st));
+	HIPCHK(hipFreeAsync(s.fb_items, st));
+	HIPCHK(hipFreeAsync(s.fb_st4, st));
+	HIPCHK(hipFreeAsync(s.fb_sdep, st));
+	HIPCHK(hipFreeAsync(s.slot_flag, st));
 	if(sync_overflow) {
 		HIPCHK(hipStreamSynchronize(st));
 		if(ovf) return fail(BT2G_ERR_OVERFLOW, "one-mismatch hits exceed cap %u", cap);

@@ -36,20 +36,24 @@ struct MmBranch {
 	int32_t off5p;      // the mismatch's offset from the 5' end
 	uint32_t pad[3];
 };
-// items: n*4 u32 scratch; counters: 6 u32 zeroed by the caller (item counts
-// at [0] / [2], branch queue head at [4]); near_state / near_dep: n*4 each;
-// brq: brq_cap branch records (a full queue falls back to walking in place)
+// items: n*4 u32 scratch; counters: 8 u32 zeroed by the caller (item counts
+// at [0] / [2], branch queue head at [4], fallback item counts at [5] / [6]);
+// near_state / near_dep / fb_items / fb_st4 / fb_sdep / slot_flag: n*4 each;
+// brq: brq_cap branch records (items meeting a full queue are redone whole by
+// the in-place state machine k_one_mm_q)
 void launch_one_mm_q(const DevEbwt& F, const DevEbwt& B, const uint8_t* reads, const uint8_t* quals, uint32_t stride,
                      const uint32_t* lens, uint32_t n, const int32_t* minsc, const bt2g_scoring& sc, int nofw,
                      int norc, const uint32_t* gate, uint32_t cap, uint32_t* items, uint32_t* counters,
                      uint4* near_state, uint32_t* near_dep, bt2g_mm1* slots, int32_t* slot_counts, uint32_t* ops,
-                     uint32_t* loads, MmBranch* brq, uint32_t brq_cap, hipStream_t st);
+                     uint32_t* loads, MmBranch* brq, uint32_t brq_cap, uint32_t* fb_items, uint4* fb_st4,
+                     uint32_t* fb_sdep, uint32_t* slot_flag, hipStream_t st);
 void launch_one_mm(const DevEbwt& F, const DevEbwt& B, const uint8_t* reads, const uint8_t* quals, uint32_t stride,
                    const uint32_t* lens, uint32_t n, const int32_t* minsc, const bt2g_scoring& sc, int nofw,
                    int norc, const uint32_t* gate, uint32_t cap, uint32_t* items, uint32_t* counters,
                    uint4* near_state, uint32_t* near_dep, bt2g_mm1* slots, int32_t* slot_counts, bt2g_mm1* hits,
                    int32_t* counts, uint32_t* ops, uint32_t* loads, int32_t* overflow, MmBranch* brq,
-                   uint32_t brq_cap, hipStream_t st);
+                   uint32_t brq_cap, uint32_t* fb_items, uint4* fb_st4, uint32_t* fb_sdep, uint32_t* slot_flag,
+                   hipStream_t st);
 void launch_get_offset(const DevEbwt& e, const uint32_t* rows, uint32_t n, uint32_t* offs, uint32_t* loads,
                        hipStream_t st);
 void launch_sw_partition(const bt2g_sw_problem* probs, uint32_t nprob, int local, int enable8, uint32_t* list8,

@@ -44,3 +44,17 @@ __device__ __forceinline__ uint32_t block_alloc(uint32_t count, uint32_t* counte
 	__syncthreads();   // the shared words may be reused by the next call
 	return base;
 }
+
+// One slot of *counter for every lane active at this call site, with ONE
+// atomic per wave (a lone queue word sustains only ~90 atomics/us chip-wide:
+// per-lane atomics on it serialise a whole kernel).  Lanes of a wave that
+// reach the call together get consecutive slots in lane order.
+__device__ __forceinline__ uint32_t wave_alloc1(uint32_t* counter) {
+	const uint64_t m = __ballot(1);
+	const uint32_t lane = threadIdx.x & 63u;
+	const int leader = __builtin_ctzll(m);
+	uint32_t base = 0;
+	if((int)lane == leader) base = atomicAdd(counter, (uint32_t)__popcll(m));
+	base = (uint32_t)__shfl((int)base, leader);
+	return base + (uint32_t)__popcll(m & ((1ull << lane) - 1ull));
+}

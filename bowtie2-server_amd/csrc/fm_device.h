@@ -212,3 +212,36 @@ struct SeqView {
 		return cmp ? (c > 3 ? 4 : 3 - c) : c;
 	}
 };
+
+// A walk's next read base through a 16-byte register window: the LF loops
+// consume one base per step in a fixed direction, so the read row is loaded
+// once per 16 steps instead of one byte load per step inside the dependent
+// gather chain.  `lo`/`hi` bound the row (windows never cross them: a window
+// that would is replaced by single-byte loads).
+struct ReadWin {
+	const uint8_t* lo;
+	const uint8_t* hi;
+	uint64_t a = ~0ull;
+	uint4 w = make_uint4(0, 0, 0, 0);
+	__device__ __forceinline__ int at(const uint8_t* ptr) {
+		const uint64_t addr = (uint64_t)ptr, aa = addr & ~15ull;
+		if(aa != a) {
+			if(aa < (uint64_t)lo || aa + 16u > (uint64_t)hi) return *ptr;
+			a = aa;
+			w = *(const uint4*)aa;
+		}
+		const uint32_t di = (uint32_t)(addr >> 2) & 3u;
+		const uint32_t d = di == 0 ? w.x : di == 1 ? w.y : di == 2 ? w.z : w.w;
+		return (int)((d >> ((addr & 3u) * 8u)) & 0xffu);
+	}
+};
+
+// SeqView read through a ReadWin (row bounds [lo, hi)).
+struct SeqWin {
+	SeqView v;
+	ReadWin w;
+	__device__ __forceinline__ int operator[](uint32_t i) {
+		const int c = w.at(v.p + (v.rev ? v.len - 1 - i : i));
+		return v.cmp ? (c > 3 ? 4 : 3 - c) : c;
+	}
+};

@@ -29,6 +29,13 @@ k_exact_sweep(DevEbwt e, const uint8_t* __restrict__ reads, uint32_t stride, con
 	const bool active = valid && !((strand == 0 && nofw) || (strand == 1 && norc));
 	const uint32_t len = active ? lens[r] : 0;
 	SeqView seq{reads + (size_t)(active ? r : 0) * stride, len, strand == 1, strand == 1};
+	// the LF loop's base at depth dep: fw row[len-dep-1], rc comp(row[dep]), via a register window
+	ReadWin rw{reads, reads + (size_t)n * stride};
+	const uint8_t* row = seq.p;
+	auto base_at = [&](uint32_t d) -> int {
+		const int c = rw.at(row + (strand == 1 ? d : len - d - 1));
+		return strand == 1 ? (c > 3 ? 4 : 3 - c) : c;
+	};
 	const uint32_t flen = e.ftab_chars;
 	uint32_t dep = 0, nedit = 0, top = 0, bot = 0, mine = 0;
 	uint32_t bwops = 0, loads = 0;
@@ -64,7 +71,7 @@ k_exact_sweep(DevEbwt e, const uint8_t* __restrict__ reads, uint32_t stride, con
 			doinit = false;
 		}
 		if(dep < len) {
-			int c = seq[len - dep - 1];
+			const int c = base_at(dep);
 			if(c > 3) {
 				top = bot = 0;
 			} else if(bot - top > 1) {
@@ -295,9 +302,11 @@ void launch_one_mm(const DevEbwt& F, const DevEbwt& B, const uint8_t* reads, con
                    int norc, const uint32_t* gate, uint32_t cap, uint32_t* items, uint32_t* counters,
                    uint4* near_state, uint32_t* near_dep, bt2g_mm1* slots, int32_t* slot_counts, bt2g_mm1* hits,
                    int32_t* counts, uint32_t* ops, uint32_t* loads, int32_t* overflow, MmBranch* brq,
-                   uint32_t brq_cap, hipStream_t st) {
+                   uint32_t brq_cap, uint32_t* fb_items, uint4* fb_st4, uint32_t* fb_sdep, uint32_t* slot_flag,
+                   hipStream_t st) {
 	launch_one_mm_q(F, B, reads, quals, stride, lens, n, minsc, sc, nofw, norc, gate, cap, items, counters,
-	                near_state, near_dep, slots, slot_counts, ops, loads, brq, brq_cap, st);
+	                near_state, near_dep, slots, slot_counts, ops, loads, brq, brq_cap, fb_items, fb_st4, fb_sdep,
+	                slot_flag, st);
 	hipLaunchKernelGGL(k_one_mm_compact, dim3((n + 255) / 256), dim3(256), 0, st, slots, slot_counts, n, cap, hits,
 	                   counts, overflow);
 }

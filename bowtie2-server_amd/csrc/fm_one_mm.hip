@@ -164,8 +164,9 @@ k_one_mm_near(DevEbwt F, DevEbwt B, const uint8_t* __restrict__ reads, uint32_t 
 		}
 		alive = bot != top;
 	}
+	SeqWin sw{seq, ReadWin{seq.p, seq.p + stride}};
 	while(alive && dep < nea) {
-		const int c = seq[len - dep - 1];
+		const int c = sw[len - dep - 1];
 		ops++;
 		if(bot - top > 1) {
 			uint32_t t[4] = {0, 0, 0, 0}, b[4] = {0, 0, 0, 0}, tp[4], bp[4];
@@ -267,7 +268,7 @@ k_one_mm_q(DevEbwt F, DevEbwt B, const uint8_t* __restrict__ reads, const uint8_
 						const uint32_t myseq = dseq++;
 						if(depm < len) {
 							// hand the walk to the branch kernel; walk in place when the queue is full
-							const uint32_t q = atomicAdd(brq_n, 1u);
+							const uint32_t q = wave_alloc1(brq_n);
 							if(q < brq_cap) {
 								MmBranch b;
 								b.rng = make_uint4(topm, botm, topmp, botmp);
@@ -437,6 +438,150 @@ k_one_mm_q(DevEbwt F, DevEbwt B, const uint8_t* __restrict__ reads, const uint8_
 	}
 }
 
+// Far half, lean form (aligner_seed.cpp:1110-1315): the main path's LF steps
+// with the read's base at every far depth, and for each non-empty alternative
+// base the hit it would make -- queued for k_one_mm_branch when the walk has
+// bases left, reported at once when the mismatch is the last base.  No branch
+// is walked here, so the loop is as lean as the near half's (the state
+// machine k_one_mm_q, which also walks branches in place, only runs for the
+// rare items that meet a full queue: they are handed over whole, and their
+// queued branches are dropped by the branch kernel via slot_flag).
+#ifndef BT2G_MM_FAR_WAVES
+#define BT2G_MM_FAR_WAVES 3      // 4 and 5 spill (84 / 152 B per lane)
+#endif
+template <bool EBWTFW>
+__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(BT2G_MM_FAR_WAVES)))
+k_one_mm_far(DevEbwt F, DevEbwt B, const uint8_t* __restrict__ reads, const uint8_t* __restrict__ quals,
+             uint32_t stride, const uint32_t* __restrict__ lens, const int32_t* __restrict__ minscs, MmParams P,
+             double ncl_const, double ncl_lin, const uint32_t* __restrict__ items,
+             const uint32_t* __restrict__ nitems_p, const uint4* __restrict__ st4, const uint32_t* __restrict__ sdep,
+             uint32_t cap, bt2g_mm1* __restrict__ slots, int32_t* __restrict__ slot_counts,
+             uint32_t* __restrict__ ops_out, uint32_t* __restrict__ loads_out, MmBranch* __restrict__ brq,
+             uint32_t* __restrict__ brq_n, uint32_t brq_cap, uint32_t* __restrict__ fb_items,
+             uint4* __restrict__ fb_st4, uint32_t* __restrict__ fb_sdep, uint32_t* __restrict__ fb_n,
+             uint32_t* __restrict__ slot_flag) {
+	const uint32_t qi = blockIdx.x * blockDim.x + threadIdx.x;
+	if(qi >= *nitems_p) return;
+	constexpr bool ebwtfw = EBWTFW;
+	const DevEbwt& E = EBWTFW ? F : B;
+	const uint32_t item = items[qi];
+	const uint32_t r = item >> 3;
+	const uint32_t fwi = (item >> 2) & 1u, ebi = (item >> 1) & 1u;
+	const bool hasn = item & 1u;
+	const bool fw = fwi == 0;
+	const uint32_t slot = r * 4 + fwi * 2 + ebi;
+	const uint32_t sd = sdep[qi];
+	if(!(sd >> 31)) { slot_counts[slot] = 0; return; }           // the near half died
+	const uint32_t len = lens[r];
+	const uint8_t* qd = quals + (size_t)r * stride;
+	const int64_t minsc = minscs[r];
+	int nceil = (int)(ncl_const + ncl_lin * (double)len);
+	if(nceil < 0) nceil = 0;
+	const int64_t matchsc = (int64_t)((float)P.match + 0.5f);
+	// seq = fw ? (ebwtfw ? patFw : patFwRev) : (ebwtfw ? patRc : patRcRev)
+	const SeqView sv{reads + (size_t)r * stride, len, fw ? !ebwtfw : ebwtfw, !fw};
+	SeqWin seq{sv, ReadWin{sv.p, sv.p + stride}};
+	const bool qrev = fw ? !ebwtfw : ebwtfw;
+	const uint4 q4 = st4[qi];
+	uint32_t top = q4.x, bot = q4.y, topp = q4.z, botp = q4.w;
+	uint32_t dep = sd & 0x7fffffffu;
+	int32_t nh = 0;
+	uint32_t dseq = 0, ops = 0, loads = 0;
+	bool handed = false;
+	while(dep < len) {
+		const int rdc = seq[len - dep - 1];
+		const int quc = qd[qrev ? dep : len - dep - 1];
+		if(rdc > 3 && nceil == 0) break;
+		if(bot - top <= 1 && top == E.zoff) break;                // mapLF1 would hit '$'
+		ops++;
+		uint32_t ot[4], ob[4], otp[4], obp[4];
+		int clo = 0, chi = 3;
+		bool match;
+		if(bot - top > 1) {
+#pragma unroll
+			for(int i = 0; i < 4; i++) ot[i] = ob[i] = 0;
+			otp[0] = topp;
+			loads += bi_step(E, top, bot, topp, ot, ob, otp, obp);
+			match = rdc < 4;
+		} else {
+			SideData s1;
+			load_side(E, top / 192u, s1);
+			loads++;
+			const int rowl = side_rowL(s1, top % 192u);
+			const uint32_t lf1 = occ1(E, s1, top, rowl);
+#pragma unroll
+			for(int i = 0; i < 4; i++) { ot[i] = lf1; ob[i] = lf1 + 1; otp[i] = topp; obp[i] = botp; }
+			clo = chi = rowl;
+			match = rowl == rdc;
+		}
+		// alternatives clo..chi at this depth (aligner_seed.cpp:1166-1290); with an N in
+		// the read only the N itself may be the mismatch
+		if(!hasn || rdc > 3) {
+#pragma unroll 1
+			for(int j = clo; j <= chi; j++) {
+				if(j == rdc || at4(ob, j) == at4(ot, j)) continue;
+				const uint32_t depm = dep + 1;
+				uint32_t off5p = dep;
+				if(fw == ebwtfw) off5p = len - off5p - 1;
+				int64_t score = (int64_t)(len - 1) * matchsc;
+				const int pen = rdc > 3 ? -P.npen : -mmpen_q(P, quc - 33);
+				score += pen;
+				bool valid = true;
+				if(P.local) {
+					int64_t lf = 0, lb = 0;
+					for(uint32_t i = 0; i < len; i++) {
+						if(i == dep) { if(lf + pen <= 0) { valid = false; break; } lf += pen; }
+						else lf += matchsc;
+						if(len - i - 1 == dep) { if(lb + pen <= 0) { valid = false; break; } lb += pen; }
+						else lb += matchsc;
+					}
+				}
+				valid = valid && score >= minsc;
+				const uint32_t myseq = dseq++;
+				const uint32_t tm = at4(ot, j), bm = at4(ob, j), tpm = at4(otp, j), bpm = at4(obp, j);
+				if(depm < len) {
+					const uint32_t q = wave_alloc1(brq_n);
+					if(q >= brq_cap) { handed = true; break; }
+					MmBranch b;
+					b.rng = make_uint4(tm, bm, tpm, bpm);
+					b.slot = slot;
+					b.seq = myseq;
+					b.meta = depm | ((uint32_t)j << 16) | ((uint32_t)rdc << 20) | ((valid ? 1u : 0u) << 24) |
+					         ((ebwtfw ? 1u : 0u) << 25);
+					b.score = (int32_t)score;
+					b.off5p = (int32_t)off5p;
+					b.pad[0] = b.pad[1] = b.pad[2] = 0;
+					brq[q] = b;
+				} else if(valid) {                       // the mismatch is the last base
+					if((uint32_t)nh < cap)
+						slots[(size_t)slot * cap + nh] = bt2g_mm1{ebwtfw ? tm : tpm, ebwtfw ? bm : bpm, fw ? 1 : 0,
+						                                          (int32_t)score, (int32_t)off5p, j, rdc,
+						                                          (int32_t)myseq};
+					nh++;
+				}
+			}
+		}
+		if(handed) break;
+		if(match) {
+			top = at4(ot, rdc); bot = at4(ob, rdc); topp = at4(otp, rdc); botp = at4(obp, rdc);
+		}
+		if(!(bot > top && match && dep != len - 1)) break;
+		dep++;
+	}
+	if(handed) {
+		// queue full: the whole item goes to the in-place state machine
+		slot_flag[slot] = 1u;
+		const uint32_t f = wave_alloc1(fb_n);
+		fb_items[f] = item;
+		fb_st4[f] = q4;
+		fb_sdep[f] = sd;
+		return;
+	}
+	slot_counts[slot] = nh;
+	if(ops) atomicAdd(&ops_out[r], ops);
+	if(ops && loads_out) atomicAdd(&loads_out[r], loads);
+}
+
 // Walk every queued far-half branch to the read's end (or its death), one
 // lane per branch: exact steps on the read's remaining bases with the same LF
 // operations and op counting as the in-place walk (ST_BR above).  A completed
@@ -446,17 +591,20 @@ __global__ void __launch_bounds__(256)
 k_one_mm_branch(DevEbwt F, DevEbwt B, const uint8_t* __restrict__ reads, uint32_t stride,
                 const uint32_t* __restrict__ lens, const MmBranch* __restrict__ brq,
                 const uint32_t* __restrict__ brq_n, uint32_t brq_cap, uint32_t cap, bt2g_mm1* __restrict__ slots,
-                int32_t* __restrict__ slot_counts, uint32_t* __restrict__ ops_out, uint32_t* __restrict__ loads_out) {
+                int32_t* __restrict__ slot_counts, uint32_t* __restrict__ ops_out, uint32_t* __restrict__ loads_out,
+                const uint32_t* __restrict__ slot_flag) {
 	const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
 	const uint32_t nq = *brq_n < brq_cap ? *brq_n : brq_cap;
 	if(i >= nq) return;
 	const MmBranch b = brq[i];
+	if(slot_flag[b.slot]) return;                 // its item was redone whole by the state machine
 	const bool ebwtfw = (b.meta >> 25) & 1u;
 	const DevEbwt& E = ebwtfw ? F : B;
 	const uint32_t r = b.slot >> 2;
 	const bool fw = ((b.slot >> 1) & 1u) == 0;
 	const uint32_t len = lens[r];
-	const SeqView seq{reads + (size_t)r * stride, len, fw ? !ebwtfw : ebwtfw, !fw};
+	const SeqView sv{reads + (size_t)r * stride, len, fw ? !ebwtfw : ebwtfw, !fw};
+	SeqWin seq{sv, ReadWin{sv.p, sv.p + stride}};
 	uint32_t topm = b.rng.x, botm = b.rng.y, topmp = b.rng.z, botmp = b.rng.w;
 	uint32_t depm = b.meta & 0xffffu;
 	uint32_t ops = 0, loads = 0;
@@ -497,7 +645,8 @@ void launch_one_mm_q(const DevEbwt& F, const DevEbwt& B, const uint8_t* reads, c
                      const uint32_t* lens, uint32_t n, const int32_t* minsc, const bt2g_scoring& sc, int nofw,
                      int norc, const uint32_t* gate, uint32_t cap, uint32_t* items, uint32_t* counters,
                      uint4* near_state, uint32_t* near_dep, bt2g_mm1* slots, int32_t* slot_counts, uint32_t* ops,
-                     uint32_t* loads, MmBranch* brq, uint32_t brq_cap, hipStream_t st) {
+                     uint32_t* loads, MmBranch* brq, uint32_t brq_cap, uint32_t* fb_items, uint4* fb_st4,
+                     uint32_t* fb_sdep, uint32_t* slot_flag, hipStream_t st) {
 	MmParams P{sc.match, sc.mmp_max, sc.mmp_min, sc.npen, sc.local, 0, 0};
 	// counters[0]/[2] = item counts of the BWT / BWT' lists (zeroed by the caller)
 	hipLaunchKernelGGL(k_one_mm_items, dim3((n + 255) / 256), dim3(256), 0, st, reads, stride, lens, n, gate, nofw,
@@ -508,12 +657,23 @@ void launch_one_mm_q(const DevEbwt& F, const DevEbwt& B, const uint8_t* reads, c
 	                   near_state, near_dep, ops, loads);
 	hipLaunchKernelGGL(k_one_mm_near<false>, dim3(grid), dim3(256), 0, st, F, B, reads, stride, lens, items + half,
 	                   counters + 2, near_state + half, near_dep + half, ops, loads);
-	hipLaunchKernelGGL(k_one_mm_q<true>, dim3(grid), dim3(256), 0, st, F, B, reads, quals, stride, lens, minsc, P,
+	// far halves (lean; branches to the queue), then the state machine for the items that met a
+	// full queue (counters[5] / [6]; it walks in place: no queue, its own dummy head counters[7]),
+	// then every queued branch
+	(void)hipMemsetAsync(slot_flag, 0, sizeof(uint32_t) * (size_t)n * 4, st);
+	hipLaunchKernelGGL(k_one_mm_far<true>, dim3(grid), dim3(256), 0, st, F, B, reads, quals, stride, lens, minsc, P,
 	                   sc.ncl_const, sc.ncl_lin, items, counters, near_state, near_dep, cap, slots, slot_counts, ops,
-	                   loads, brq, counters + 4, brq_cap);
-	hipLaunchKernelGGL(k_one_mm_q<false>, dim3(grid), dim3(256), 0, st, F, B, reads, quals, stride, lens, minsc, P,
+	                   loads, brq, counters + 4, brq_cap, fb_items, fb_st4, fb_sdep, counters + 5, slot_flag);
+	hipLaunchKernelGGL(k_one_mm_far<false>, dim3(grid), dim3(256), 0, st, F, B, reads, quals, stride, lens, minsc, P,
 	                   sc.ncl_const, sc.ncl_lin, items + half, counters + 2, near_state + half, near_dep + half, cap,
-	                   slots, slot_counts, ops, loads, brq, counters + 4, brq_cap);
+	                   slots, slot_counts, ops, loads, brq, counters + 4, brq_cap, fb_items + half, fb_st4 + half,
+	                   fb_sdep + half, counters + 6, slot_flag);
+	hipLaunchKernelGGL(k_one_mm_q<true>, dim3(grid), dim3(256), 0, st, F, B, reads, quals, stride, lens, minsc, P,
+	                   sc.ncl_const, sc.ncl_lin, fb_items, counters + 5, fb_st4, fb_sdep, cap, slots, slot_counts, ops,
+	                   loads, brq, counters + 7, 0u);
+	hipLaunchKernelGGL(k_one_mm_q<false>, dim3(grid), dim3(256), 0, st, F, B, reads, quals, stride, lens, minsc, P,
+	                   sc.ncl_const, sc.ncl_lin, fb_items + half, counters + 6, fb_st4 + half, fb_sdep + half, cap,
+	                   slots, slot_counts, ops, loads, brq, counters + 7, 0u);
 	hipLaunchKernelGGL(k_one_mm_branch, dim3((brq_cap + 255) / 256), dim3(256), 0, st, F, B, reads, stride, lens, brq,
-	                   counters + 4, brq_cap, cap, slots, slot_counts, ops, loads);
+	                   counters + 4, brq_cap, cap, slots, slot_counts, ops, loads, slot_flag);
 }
