@@ -586,7 +586,44 @@ def cpu_baseline(idx, reads, quals, pipe, sample, threads):
         mate["frame_ref"] = np.concatenate([m[0] for m in mts]) if mts else np.zeros((0, 7), np.int64)
         mate["out_ref"] = np.concatenate([m[1] for m in mts]) if mts else np.zeros((0, 8), np.int64)
     chain.close()
+    ref["index_base"] = base
     return dt, ref, mate, secs
+
+
+def server_baseline(base, reads, quals, pol, sample, threads, workers, args_srv, log_dir):
+    """The north-star comparison on the reference's real schedule (BASELINE.md
+    section 3): the stock reference server (oracle/_ref/bowtie2-align-server-s,
+    -p <usable cores>) and the same server with its seams bound to the engines
+    (integration/bt2g_seams.cpp -> oracle/_ref/bowtie2-align-server-gpu, -p
+    <workers>) on the same `sample` reads (pairs) and index, driven by the
+    reference's own client in <= 10 000-read connections, 8 at a time; sorted
+    SAM compared record by record."""
+    from oracle import ref_server as rs
+    n = sample
+    if pol.paired:
+        P = len(reads) // 2
+        chunks = rs.write_fastq_chunks(log_dir, reads[:n], quals[:n], codes2=reads[P:P + n], quals2=quals[P:P + n])
+    else:
+        chunks = rs.write_fastq_chunks(log_dir, reads[:n], quals[:n])
+    out, sams = {}, {}
+    for tag, binary, th in (("stock", rs.SERVER, threads),
+                            ("dropin", os.path.join(rs.REF_DIR, "bowtie2-align-server-gpu"), workers)):
+        stats = os.path.join(log_dir, f"stats_{tag}.json")
+        env = {"BT2G_INDEX": base, "BT2G_ADAPTER_STATS": stats, "BT2G_DEVICE": "0"}
+        with rs.Server(base, threads=th, args=args_srv, binary=binary, env=env,
+                       log_path=os.path.join(log_dir, f"server_{tag}.log")) as srv:
+            dt, outs = srv.run(chunks, k=8)
+        sams[tag] = rs.sorted_records(outs)
+        out[tag] = {"rate": n / dt, "seconds": dt, "threads": th, "records": len(sams[tag])}
+        time.sleep(0.5)
+        if os.path.exists(stats):
+            import json as _j
+            out[tag]["engine_calls"] = _j.load(open(stats))
+    a, b = sams["stock"], sams["dropin"]
+    out["sam_identical"] = a == b
+    out["sam_records_differing"] = sum(1 for x, y in zip(a, b) if x != y) + abs(len(a) - len(b))
+    out["dropin_vs_stock"] = out["dropin"]["rate"] / out["stock"]["rate"]
+    return out
 
 
 def gpu_chain(pipe, ids):
@@ -752,6 +789,9 @@ def main():
     ap.add_argument("--cpu-threads", type=int, default=0, help="0: the usable cores of the host (cgroup quota / "
                                                                    "affinity)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--server-sample", type=int, default=200_000,
+                    help="reads (pairs) timed through the stock reference server and the drop-in server (0: skip)")
+    ap.add_argument("--server-workers", type=int, default=512, help="drop-in server worker threads (-p)")
     ap.add_argument("--index-cache", default="", help="reuse/write the built index at this base path")
     ap.add_argument("--pmc-fetch", default="", help="rocprofv3 --pmc FETCH_SIZE counter_collection.csv of this "
                                                     "command: fills roofline.traffic")
@@ -929,6 +969,30 @@ def main():
             if paired:
                 parity.update(mate_parity(pipe, mate))
             log(f"[rank 0] cpu baseline {sample/dt:.0f} {cpu['unit']} on {threads} threads ({dt:.1f}s); parity {parity}")
+            if args.server_sample:
+              try:
+                import tempfile
+                srv_args = ["--local"] if args.mode == "local" else []
+                if args.preset == "very-sensitive":
+                    srv_args.append("--very-sensitive-local" if args.mode == "local" else "--very-sensitive")
+                srv = server_baseline(ref["index_base"], reads_np, quals_np, pol,
+                                      min(args.server_sample, sample), threads, args.server_workers, srv_args,
+                                      tempfile.mkdtemp(prefix="bt2srv_"))
+                cpu["reference_server"] = {"value": srv["stock"]["rate"], "unit": cpu["unit"], "cores": threads,
+                                           "sample": f"first {min(args.server_sample, sample)} of the batch, "
+                                                     f"<= 10 000 per client connection, 8 connections at a time",
+                                           **{k: v for k, v in srv["stock"].items() if k != "rate"}}
+                cpu["dropin_server"] = {"value": srv["dropin"]["rate"], "unit": cpu["unit"],
+                                        "sam_identical_to_reference": srv["sam_identical"],
+                                        "sam_records_differing": srv["sam_records_differing"],
+                                        "vs_reference_server": srv["dropin_vs_stock"],
+                                        **{k: v for k, v in srv["dropin"].items() if k != "rate"}}
+                log(f"[rank 0] reference server {srv['stock']['rate']:.0f}, drop-in {srv['dropin']['rate']:.0f} "
+                    f"{cpu['unit']}; SAM identical {srv['sam_identical']}")
+              except Exception as e:       # the servers are checkers: their failure must not hide the rest
+                import traceback
+                traceback.print_exc()
+                cpu["reference_server"] = {"error": repr(e)[:500]}
         except Exception as e:  # the reference build is optional on the box
             import traceback
             traceback.print_exc()

@@ -100,6 +100,7 @@ def lib():
         L.bt2g_open.argtypes = [C.c_char_p, C.c_int, C.POINTER(vp)]
         L.bt2g_open_mem.argtypes = [C.POINTER(IndexMem), C.c_int, C.POINTER(vp)]
         L.bt2g_close.argtypes = [vp]
+        L.bt2g_open_shared.argtypes = [vp, C.POINTER(vp)]
         L.bt2g_info.argtypes = [vp, vp, C.c_int]
         L.bt2g_exact_sweep.argtypes = [vp, vp, u32, vp, u32, u32, C.c_int, C.c_int, vp]
         L.bt2g_exact_sweep_dev.argtypes = [vp, vp, u32, vp, u32, u32, C.c_int, C.c_int, vp, vp]
@@ -191,6 +192,14 @@ class Engine:
             self._keep = None
         else:
             _chk(lib().bt2g_open(index_base.encode(), device, C.byref(self.h)))
+
+    def shared(self):
+        """A second Engine on this one's index and device (bt2g_open_shared): its
+        own stream and scratch, for another thread.  Close it before this one."""
+        e = Engine.__new__(Engine)
+        e.h = C.c_void_p()
+        _chk(lib().bt2g_open_shared(self.h, C.byref(e.h)))
+        return e
 
     def close(self):
         if self.h:

@@ -9,9 +9,13 @@
 #include <stdio.h>
 #include <string.h>
 
+#include <algorithm>
 #include <cstdarg>
+#include <cstdlib>
 #include <fstream>
+#include <mutex>
 #include <string>
+#include <unordered_map>
 #include <vector>
 
 #include "bt2g_kernels.h"
@@ -70,9 +74,164 @@ struct bt2g_ctx {
 	int bt_hbytes = 0;
 	uint8_t* bt_plane = nullptr;
 	uint32_t* bt_marks = nullptr;
+	// host-wrapper scratch (Arena): one device block reused call after call
+	uint8_t* arena = nullptr;
+	size_t arena_cap = 0, arena_used = 0, arena_need = 0;
+	int arena_depth = 0;
+	std::vector<void*> arena_spill;
+	struct GuardRec { void* p; size_t n; int line; };
+	std::vector<GuardRec> arena_guards;
+	// pinned host staging for the wrappers' copies (same growth rule as the arena)
+	uint8_t* pin = nullptr;
+	size_t pin_cap = 0, pin_used = 0, pin_need = 0;
 };
 
 namespace {
+
+// Device scratch.  Inside a host-pointer wrapper (Arena below) blocks come from
+// the context's arena: the wrappers synchronise before they return, so the
+// arena is simply rewound for the next call, and no allocator is shared by the
+// threads that drive their own contexts.  The device-pointer calls (which a
+// caller may enqueue on any stream, without waiting) take stream-ordered blocks
+// from the device's memory pool.
+//
+// With BT2G_GUARD=1 (a debugging mode) every block gets a 4 KiB tail of 0xA5
+// bytes that is checked when the block is released: a kernel writing past the
+// end of its buffer is reported with the source line that allocated it.
+const size_t GUARD_BYTES = 4096;
+
+bool guard_on() {
+	static const bool on = [] {
+		const char* g = getenv("BT2G_GUARD");
+		return g && g[0] == '1';
+	}();
+	return on;
+}
+
+struct GuardInfo {
+	size_t n;
+	int line;
+};
+std::mutex g_guard_mu;
+std::unordered_map<void*, GuardInfo> g_guard;
+
+// compare a guard tail (after the stream it was used on has drained)
+bool guard_check(void* p, size_t n, int line) {
+	std::vector<uint8_t> tail(GUARD_BYTES);
+	if(hipMemcpy(tail.data(), (char*)p + n, GUARD_BYTES, hipMemcpyDeviceToHost) != hipSuccess) return false;
+	for(size_t i = 0; i < GUARD_BYTES; i++)
+		if(tail[i] != 0xA5) {
+			fprintf(stderr, "bt2g guard: block of %zu bytes from bt2g_api.cpp:%d overwritten at +%zu\n", n, line,
+			        n + i);
+			return false;
+		}
+	return true;
+}
+
+hipError_t amalloc(bt2g_ctx* c, void** p, size_t n, hipStream_t st, int line = __builtin_LINE()) {
+	const size_t g = guard_on() ? GUARD_BYTES : 0;
+	hipError_t e;
+	if(c->arena_depth > 0) {
+		const size_t need = (n + g + 255) & ~(size_t)255;
+		if(c->arena_used + need <= c->arena_cap) {
+			*p = c->arena + c->arena_used;
+			c->arena_used += need;
+			c->arena_need = std::max(c->arena_need, c->arena_used);
+		} else {
+			// too small for this call: a block of its own now, a bigger arena next call
+			c->arena_need = std::max(c->arena_need, c->arena_used + need);
+			if((e = hipMalloc(p, n + g)) != hipSuccess) return e;
+			c->arena_spill.push_back(*p);
+		}
+		if(g) {
+			if((e = hipMemsetAsync((char*)*p + n, 0xA5, g, st)) != hipSuccess) return e;
+			c->arena_guards.push_back(bt2g_ctx::GuardRec{*p, n, line});
+		}
+		return hipSuccess;
+	}
+	if((e = hipMallocAsync(p, n + g, st)) != hipSuccess) return e;
+	if(g) {
+		if((e = hipMemsetAsync((char*)*p + n, 0xA5, g, st)) != hipSuccess) return e;
+		std::lock_guard<std::mutex> lk(g_guard_mu);
+		g_guard[*p] = GuardInfo{n, line};
+	}
+	return hipSuccess;
+}
+
+hipError_t afree(bt2g_ctx* c, void* p, hipStream_t st) {
+	if(c->arena_depth > 0) return hipSuccess;    // released when the wrapper's Arena ends
+	if(guard_on() && p) {
+		GuardInfo gi{0, 0};
+		{
+			std::lock_guard<std::mutex> lk(g_guard_mu);
+			auto it = g_guard.find(p);
+			if(it != g_guard.end()) {
+				gi = it->second;
+				g_guard.erase(it);
+			}
+		}
+		if(gi.line) {
+			hipError_t e = hipStreamSynchronize(st);
+			if(e != hipSuccess) return e;
+			guard_check(p, gi.n, gi.line);
+		}
+	}
+	return hipFreeAsync(p, st);
+}
+
+// Scope of one host-pointer wrapper call on context c (not re-entrant across
+// threads: a context is driven by one thread at a time).
+struct Arena {
+	bt2g_ctx* c;
+	hipStream_t st;
+	explicit Arena(bt2g_ctx* cx) : c(cx), st(cx->stream) {
+		if(c->arena_depth++ > 0) return;
+		c->arena_used = 0;
+		if(c->arena_need > c->arena_cap) {
+			// nothing of an earlier call is in flight: it synchronised before returning
+			if(c->arena) (void)hipFree(c->arena);
+			c->arena = nullptr;
+			size_t cap = std::max<size_t>(c->arena_need + c->arena_need / 4, (size_t)64 << 20);
+			if(hipMalloc((void**)&c->arena, cap) == hipSuccess) {
+				c->arena_cap = cap;
+			} else {
+				c->arena = nullptr;
+				c->arena_cap = 0;
+			}
+		}
+		c->pin_used = 0;
+		if(c->pin_need > c->pin_cap) {
+			if(c->pin) (void)hipHostFree(c->pin);
+			c->pin = nullptr;
+			size_t cap = std::max<size_t>(c->pin_need + c->pin_need / 4, (size_t)16 << 20);
+			if(hipHostMalloc((void**)&c->pin, cap, hipHostMallocDefault) == hipSuccess) {
+				c->pin_cap = cap;
+			} else {
+				c->pin = nullptr;
+				c->pin_cap = 0;
+			}
+		}
+	}
+	// pinned staging of `n` bytes for this call (nullptr: copy through pageable memory)
+	uint8_t* pinned(size_t n) {
+		const size_t need = (n + 63) & ~(size_t)63;
+		c->pin_need = std::max(c->pin_need, c->pin_used + need);
+		if(c->pin_used + need > c->pin_cap) return nullptr;
+		uint8_t* p = c->pin + c->pin_used;
+		c->pin_used += need;
+		return p;
+	}
+	~Arena() {
+		if(--c->arena_depth > 0) return;
+		(void)hipStreamSynchronize(st);   // an early error return may leave work in flight
+		for(auto& g : c->arena_guards) guard_check(g.p, g.n, g.line);
+		c->arena_guards.clear();
+		for(void* p : c->arena_spill) (void)hipFree(p);
+		c->arena_spill.clear();
+		c->arena_used = 0;
+		c->pin_used = 0;
+	}
+};
 
 int dalloc(bt2g_ctx* c, void** p, size_t n) {
 	if(n == 0) n = 16;
@@ -278,6 +437,15 @@ int bt2g_open_mem(const bt2g_index_mem* m, int device, bt2g_ctx** out) {
 	HIPCHK(hipGetDeviceCount(&ndev));
 	if(device < 0 || device >= ndev) return fail(BT2G_ERR_ARG, "device %d of %d", device, ndev);
 	HIPCHK(hipSetDevice(device));
+	// $BT2G_SYNC: how a host thread waits for the device (blocking | yield | spin);
+	// a process with many threads driving contexts wants its cores back (blocking)
+	if(const char* sy = getenv("BT2G_SYNC")) {
+		unsigned fl = !strcmp(sy, "blocking") ? hipDeviceScheduleBlockingSync
+		            : !strcmp(sy, "yield")    ? hipDeviceScheduleYield
+		            : !strcmp(sy, "spin")     ? hipDeviceScheduleSpin
+		                                      : hipDeviceScheduleAuto;
+		(void)hipSetDeviceFlags(fl);
+	}
 	bt2g_ctx* c = new bt2g_ctx();
 	c->device = device;
 	int rc;
@@ -292,6 +460,26 @@ int bt2g_open_mem(const bt2g_index_mem* m, int device, bt2g_ctx** out) {
 		return rc;
 	}
 	c->nref = m->nref;
+	*out = c;
+	return BT2G_OK;
+}
+
+int bt2g_open_shared(bt2g_ctx* base, bt2g_ctx** out) {
+	if(!base || !out) return fail(BT2G_ERR_ARG, "null argument");
+	HIPCHK(hipSetDevice(base->device));
+	bt2g_ctx* c = new bt2g_ctx();
+	c->device = base->device;
+	if(hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess) {
+		delete c;
+		return fail(BT2G_ERR_HIP, "hipStreamCreate failed");
+	}
+	// the index stays owned by `base` (c->owned is empty)
+	c->fw = base->fw;
+	c->bw = base->bw;
+	c->ref_codes = base->ref_codes;
+	c->ref_starts = base->ref_starts;
+	c->nref = base->nref;
+	c->num_sides = base->num_sides;
 	*out = c;
 	return BT2G_OK;
 }
@@ -333,6 +521,8 @@ int bt2g_close(bt2g_ctx* c) {
 	for(void* p : c->owned) (void)hipFree(p);
 	if(c->sw_lists) { (void)hipFree(c->sw_lists); (void)hipFree(c->sw_counts); (void)hipFree(c->sw_bnd); }
 	if(c->bt_plane) { (void)hipFree(c->bt_plane); (void)hipFree(c->bt_marks); }
+	if(c->arena) (void)hipFree(c->arena);
+	if(c->pin) (void)hipHostFree(c->pin);
 	if(c->stream) (void)hipStreamDestroy(c->stream);
 	delete c;
 	return BT2G_OK;
@@ -436,20 +626,20 @@ static int one_mm_impl(bt2g_ctx* c, const uint8_t* reads, const uint8_t* quals, 
 	if(n == 0) return BT2G_OK;
 	hipStream_t st = pick(c, stream);
 	OneMmScratch s;
-	HIPCHK(hipMallocAsync((void**)&s.slots, sizeof(bt2g_mm1) * (size_t)n * 4 * cap, st));
-	HIPCHK(hipMallocAsync((void**)&s.slot_counts, sizeof(int32_t) * (size_t)n * 4, st));
-	HIPCHK(hipMallocAsync((void**)&s.ovf, sizeof(int32_t) * 16, st));
-	HIPCHK(hipMallocAsync((void**)&s.items, sizeof(uint32_t) * (size_t)n * 4, st));
-	HIPCHK(hipMallocAsync((void**)&s.near_state, sizeof(uint4) * (size_t)n * 4, st));
-	HIPCHK(hipMallocAsync((void**)&s.near_dep, sizeof(uint32_t) * (size_t)n * 4, st));
+	HIPCHK(amalloc(c, (void**)&s.slots, sizeof(bt2g_mm1) * (size_t)n * 4 * cap, st));
+	HIPCHK(amalloc(c, (void**)&s.slot_counts, sizeof(int32_t) * (size_t)n * 4, st));
+	HIPCHK(amalloc(c, (void**)&s.ovf, sizeof(int32_t) * 16, st));
+	HIPCHK(amalloc(c, (void**)&s.items, sizeof(uint32_t) * (size_t)n * 4, st));
+	HIPCHK(amalloc(c, (void**)&s.near_state, sizeof(uint4) * (size_t)n * 4, st));
+	HIPCHK(amalloc(c, (void**)&s.near_dep, sizeof(uint32_t) * (size_t)n * 4, st));
 	// far-half branches queued for the branch kernel (16 per read: an item that
 	// meets a full queue is redone whole by the in-place state machine)
 	const uint32_t brq_cap = n * 16 + 1024;
-	HIPCHK(hipMallocAsync((void**)&s.brq, sizeof(MmBranch) * (size_t)brq_cap, st));
-	HIPCHK(hipMallocAsync((void**)&s.fb_items, sizeof(uint32_t) * (size_t)n * 4, st));
-	HIPCHK(hipMallocAsync((void**)&s.fb_st4, sizeof(uint4) * (size_t)n * 4, st));
-	HIPCHK(hipMallocAsync((void**)&s.fb_sdep, sizeof(uint32_t) * (size_t)n * 4, st));
-	HIPCHK(hipMallocAsync((void**)&s.slot_flag, sizeof(uint32_t) * (size_t)n * 4, st));
+	HIPCHK(amalloc(c, (void**)&s.brq, sizeof(MmBranch) * (size_t)brq_cap, st));
+	HIPCHK(amalloc(c, (void**)&s.fb_items, sizeof(uint32_t) * (size_t)n * 4, st));
+	HIPCHK(amalloc(c, (void**)&s.fb_st4, sizeof(uint4) * (size_t)n * 4, st));
+	HIPCHK(amalloc(c, (void**)&s.fb_sdep, sizeof(uint32_t) * (size_t)n * 4, st));
+	HIPCHK(amalloc(c, (void**)&s.slot_flag, sizeof(uint32_t) * (size_t)n * 4, st));
 	HIPCHK(hipMemsetAsync(s.ovf, 0, sizeof(int32_t) * 16, st));
 	HIPCHK(hipMemsetAsync(bwops, 0, sizeof(uint32_t) * n, st));
 	if(loads) HIPCHK(hipMemsetAsync(loads, 0, sizeof(uint32_t) * n, st));
@@ -462,17 +652,17 @@ static int one_mm_impl(bt2g_ctx* c, const uint8_t* reads, const uint8_t* quals, 
 	HIPCHK(hipGetLastError());
 	int32_t ovf = 0;
 	if(sync_overflow) HIPCHK(hipMemcpyAsync(&ovf, s.ovf, sizeof(int32_t), hipMemcpyDeviceToHost, st));
-	HIPCHK(hipFreeAsync(s.slots, st));
-	HIPCHK(hipFreeAsync(s.slot_counts, st));
-	HIPCHK(hipFreeAsync(s.ovf, st));
-	HIPCHK(hipFreeAsync(s.items, st));
-	HIPCHK(hipFreeAsync(s.near_state, st));
-	HIPCHK(hipFreeAsync(s.near_dep, st));
-	HIPCHK(hipFreeAsync(s.brq, st));
-	HIPCHK(hipFreeAsync(s.fb_items, st));
-	HIPCHK(hipFreeAsync(s.fb_st4, st));
-	HIPCHK(hipFreeAsync(s.fb_sdep, st));
-	HIPCHK(hipFreeAsync(s.slot_flag, st));
+	HIPCHK(afree(c, s.slots, st));
+	HIPCHK(afree(c, s.slot_counts, st));
+	HIPCHK(afree(c, s.ovf, st));
+	HIPCHK(afree(c, s.items, st));
+	HIPCHK(afree(c, s.near_state, st));
+	HIPCHK(afree(c, s.near_dep, st));
+	HIPCHK(afree(c, s.brq, st));
+	HIPCHK(afree(c, s.fb_items, st));
+	HIPCHK(afree(c, s.fb_st4, st));
+	HIPCHK(afree(c, s.fb_sdep, st));
+	HIPCHK(afree(c, s.slot_flag, st));
 	if(sync_overflow) {
 		HIPCHK(hipStreamSynchronize(st));
 		if(ovf) return fail(BT2G_ERR_OVERFLOW, "one-mismatch hits exceed cap %u", cap);
@@ -564,9 +754,9 @@ static int sw_align_impl(bt2g_ctx* c, const uint8_t* reads, const uint8_t* quals
 			HIPCHK(hipStreamSynchronize(st));
 			for(auto& p : hp) maxcol = p.ncol > maxcol ? p.ncol : maxcol;
 		}
-		HIPCHK(hipMallocAsync((void**)&lists, sizeof(uint32_t) * (size_t)nprob * 3, st));
-		HIPCHK(hipMallocAsync((void**)&counts, sizeof(uint32_t) * 8, st));
-		HIPCHK(hipMallocAsync((void**)&bnd, sizeof(uint32_t) * nblk * (size_t)maxcol * 64 * 2, st));
+		HIPCHK(amalloc(c, (void**)&lists, sizeof(uint32_t) * (size_t)nprob * 3, st));
+		HIPCHK(amalloc(c, (void**)&counts, sizeof(uint32_t) * 8, st));
+		HIPCHK(amalloc(c, (void**)&bnd, sizeof(uint32_t) * nblk * (size_t)maxcol * 64 * 2, st));
 	}
 	HIPCHK(hipMemsetAsync(counts, 0, sizeof(uint32_t) * 8, st));
 	uint32_t* list8 = lists;
@@ -595,9 +785,9 @@ static int sw_align_impl(bt2g_ctx* c, const uint8_t* reads, const uint8_t* quals
 	}
 	HIPCHK(hipGetLastError());
 	if(!reserved) {
-		HIPCHK(hipFreeAsync(lists, st));
-		HIPCHK(hipFreeAsync(counts, st));
-		HIPCHK(hipFreeAsync(bnd, st));
+		HIPCHK(afree(c, lists, st));
+		HIPCHK(afree(c, counts, st));
+		HIPCHK(afree(c, bnd, st));
 	}
 	return BT2G_OK;
 }
@@ -638,7 +828,7 @@ int bt2g_sw_align_bt_dev(bt2g_ctx* c, const uint8_t* reads, const uint8_t* quals
 	BtArgs a{};
 	std::vector<void*> tmp;
 	auto talloc = [&](void** p, size_t n) -> int {
-		HIPCHK(hipMallocAsync(p, n ? n : 16, st));
+		HIPCHK(amalloc(c, p, n ? n : 16, st));
 		tmp.push_back(*p);
 		return BT2G_OK;
 	};
@@ -708,7 +898,7 @@ int bt2g_sw_align_bt_dev(bt2g_ctx* c, const uint8_t* reads, const uint8_t* quals
 		launch_sw_bt(kind, a, st);
 	}
 	HIPCHK(hipGetLastError());
-	for(void* p : tmp) HIPCHK(hipFreeAsync(p, st));
+	for(void* p : tmp) HIPCHK(afree(c, p, st));
 	return BT2G_OK;
 }
 
@@ -820,34 +1010,51 @@ int bt2g_reserve_sw(bt2g_ctx* c, uint32_t max_problems, uint32_t max_cols) {
 
 // ------------------------------------------------------ host-pointer wrappers
 namespace {
-// Device copies of a host-flavour call's arrays: stream-ordered allocations
-// from the device's memory pool (no hipMalloc / device-wide hipFree per call).
+// Device copies of a host-flavour call's arrays, in the context's arena (the
+// Arena scope also covers the scratch of the device-pointer call it makes).
+// Both directions go through the context's pinned staging, on the context's
+// stream: one stream synchronisation per call (finish), no null-stream copy
+// that would wait on the other contexts' work.
 struct Tmp {
+	Arena ar;
+	bt2g_ctx* c;
 	hipStream_t st;
-	std::vector<void*> ps;
-	explicit Tmp(bt2g_ctx* c) : st(c->stream) {}
-	~Tmp() {
-		for(void* p : ps) (void)hipFreeAsync(p, st);
-	}
+	struct Out { void* h; const void* pin; size_t n; };
+	std::vector<Out> outs;
+	explicit Tmp(bt2g_ctx* cx) : ar(cx), c(cx), st(cx->stream) {}
 	template <typename T>
 	int up(T** d, const T* h, size_t count) {
-		if(hipMallocAsync((void**)d, count * sizeof(T) + 16, st) != hipSuccess)
-			return fail(BT2G_ERR_NOMEM, "hipMallocAsync");
-		ps.push_back(*d);
+		const size_t bytes = count * sizeof(T);
+		if(amalloc(c, (void**)d, bytes + 16, st) != hipSuccess)
+			return fail(BT2G_ERR_NOMEM, "device scratch (%zu bytes)", bytes + 16);
 		if(h && count) {
-			if(hipMemcpyAsync(*d, h, count * sizeof(T), hipMemcpyHostToDevice, st) != hipSuccess)
+			const void* src = h;
+			if(uint8_t* pn = ar.pinned(bytes)) {
+				memcpy(pn, h, bytes);
+				src = pn;
+			}
+			if(hipMemcpyAsync(*d, src, bytes, hipMemcpyHostToDevice, st) != hipSuccess)
 				return fail(BT2G_ERR_HIP, "hipMemcpyAsync H2D");
 		}
 		return BT2G_OK;
 	}
+	// enqueue a result copy (valid after finish)
+	template <typename T>
+	int down(T* h, const T* d, size_t count) {
+		const size_t bytes = count * sizeof(T);
+		if(bytes == 0) return BT2G_OK;
+		uint8_t* pn = ar.pinned(bytes);
+		HIPCHK(hipMemcpyAsync(pn ? (void*)pn : (void*)h, d, bytes, hipMemcpyDeviceToHost, st));
+		if(pn) outs.push_back(Out{h, pn, bytes});
+		return BT2G_OK;
+	}
+	int finish() {
+		HIPCHK(hipStreamSynchronize(st));
+		for(const Out& o : outs) memcpy(o.h, o.pin, o.n);
+		outs.clear();
+		return BT2G_OK;
+	}
 };
-
-template <typename T>
-int down(T* h, const T* d, size_t count) {
-	if(count == 0) return BT2G_OK;
-	HIPCHK(hipMemcpy(h, d, count * sizeof(T), hipMemcpyDeviceToHost));   // after the stream sync
-	return BT2G_OK;
-}
 }  // namespace
 
 extern "C" {
@@ -864,8 +1071,8 @@ int bt2g_exact_sweep(bt2g_ctx* c, const uint8_t* reads, uint32_t stride, const u
 	   (rc = t.up(&dout, (const uint32_t*)nullptr, (size_t)n * 8)))
 		return rc;
 	if((rc = bt2g_exact_sweep_dev(c, dr, stride, dl, n, mine_max, nofw, norc, dout, c->stream))) return rc;
-	HIPCHK(hipStreamSynchronize(c->stream));
-	return down(out, dout, (size_t)n * 8);
+	if((rc = t.down(out, dout, (size_t)n * 8))) return rc;
+	return t.finish();
 }
 
 int bt2g_seed_search(bt2g_ctx* c, const uint8_t* reads, uint32_t stride, const uint32_t* lens, uint32_t n,
@@ -887,10 +1094,9 @@ int bt2g_seed_search(bt2g_ctx* c, const uint8_t* reads, uint32_t stride, const u
 	if((rc = bt2g_seed_search_dev(c, dr, stride, dl, n, seedlen, interval, offset, maxseeds, dout, dns, dops, dld,
 	                              c->stream)))
 		return rc;
-	HIPCHK(hipStreamSynchronize(c->stream));
-	if((rc = down(out, dout, no)) || (rc = down(nseeds, dns, n)) || (rc = down(bwops, dops, n))) return rc;
-	if(loads && (rc = down(loads, dld, n))) return rc;
-	return BT2G_OK;
+	if((rc = t.down(out, dout, no)) || (rc = t.down(nseeds, dns, n)) || (rc = t.down(bwops, dops, n))) return rc;
+	if(loads && (rc = t.down(loads, dld, n))) return rc;
+	return t.finish();
 }
 
 int bt2g_one_mm(bt2g_ctx* c, const uint8_t* reads, const uint8_t* quals, uint32_t stride, const uint32_t* lens,
@@ -912,10 +1118,10 @@ int bt2g_one_mm(bt2g_ctx* c, const uint8_t* reads, const uint8_t* quals, uint32_
 	if(loads && (rc = t.up(&dld, (const uint32_t*)nullptr, n))) return rc;
 	int rc2 = bt2g_one_mm_dev(c, dr, dq, stride, dl, n, dms, sc, nofw, norc, cap, dh, dcnt, dops, dld, c->stream);
 	if(rc2 && rc2 != BT2G_ERR_OVERFLOW) return rc2;
-	HIPCHK(hipStreamSynchronize(c->stream));
-	if((rc = down(hits, dh, (size_t)n * cap)) || (rc = down(counts, dcnt, n)) || (rc = down(bwops, dops, n)))
+	if((rc = t.down(hits, dh, (size_t)n * cap)) || (rc = t.down(counts, dcnt, n)) || (rc = t.down(bwops, dops, n)))
 		return rc;
-	if(loads && (rc = down(loads, dld, n))) return rc;
+	if(loads && (rc = t.down(loads, dld, n))) return rc;
+	if((rc = t.finish())) return rc;
 	return rc2;
 }
 
@@ -928,10 +1134,9 @@ int bt2g_get_offset(bt2g_ctx* c, const uint32_t* rows, uint32_t n, uint32_t* off
 	if((rc = t.up(&drow, rows, n)) || (rc = t.up(&doff, (const uint32_t*)nullptr, n))) return rc;
 	if(loads && (rc = t.up(&dld, (const uint32_t*)nullptr, n))) return rc;
 	if((rc = bt2g_get_offset_dev(c, drow, n, doff, dld, c->stream))) return rc;
-	HIPCHK(hipStreamSynchronize(c->stream));
-	if((rc = down(offs, doff, n))) return rc;
-	if(loads && (rc = down(loads, dld, n))) return rc;
-	return BT2G_OK;
+	if((rc = t.down(offs, doff, n))) return rc;
+	if(loads && (rc = t.down(loads, dld, n))) return rc;
+	return t.finish();
 }
 
 int bt2g_sw_align(bt2g_ctx* c, const uint8_t* reads, const uint8_t* quals, uint32_t stride, const uint32_t* lens,
@@ -968,9 +1173,9 @@ int bt2g_sw_align(bt2g_ctx* c, const uint8_t* reads, const uint8_t* quals, uint3
 	}
 	if((rc = bt2g_sw_align_dev(c, dr, dq, stride, dl, dp, nprob, dw, sc, enable8, cap, dres, dc, dm, dmo, c->stream)))
 		return rc;
-	HIPCHK(hipStreamSynchronize(c->stream));
-	if((rc = down(res, dres, nprob)) || (rc = down(cands, dc, (size_t)nprob * cap))) return rc;
-	if(mat && (rc = down(mat, dm, matn))) return rc;
+	if((rc = t.down(res, dres, nprob)) || (rc = t.down(cands, dc, (size_t)nprob * cap))) return rc;
+	if(mat && (rc = t.down(mat, dm, matn))) return rc;
+	if((rc = t.finish())) return rc;
 	for(uint32_t i = 0; i < nprob; i++)
 		if(res[i].ncand > (int32_t)cap) return fail(BT2G_ERR_OVERFLOW, "problem %u: %d candidates > cap %u", i,
 		                                             res[i].ncand, cap);
@@ -1017,11 +1222,11 @@ int bt2g_sw_align_bt(bt2g_ctx* c, const uint8_t* reads, const uint8_t* quals, ui
 	if((rc = bt2g_sw_align_bt_dev(c, dr, dq, stride, dl, dp, nprob, dw, drc, sc, enable8, cap, dres, dc, maxaln,
 	                              maxedit, dna, dal, ded, dft, c->stream)))
 		return rc;
-	HIPCHK(hipStreamSynchronize(c->stream));
-	if((rc = down(res, dres, nprob)) || (rc = down(cands, dc, (size_t)nprob * cap)) || (rc = down(naln, dna, nprob)) ||
-	   (rc = down(alns, dal, na)) || (rc = down(edits, ded, na * maxedit)))
+	if((rc = t.down(res, dres, nprob)) || (rc = t.down(cands, dc, (size_t)nprob * cap)) ||
+	   (rc = t.down(naln, dna, nprob)) || (rc = t.down(alns, dal, na)) || (rc = t.down(edits, ded, na * maxedit)))
 		return rc;
-	if(fates && (rc = down(fates, dft, (size_t)nprob * cap))) return rc;
+	if(fates && (rc = t.down(fates, dft, (size_t)nprob * cap))) return rc;
+	if((rc = t.finish())) return rc;
 	for(uint32_t i = 0; i < nprob; i++)
 		if(res[i].ncand > (int32_t)cap) return fail(BT2G_ERR_OVERFLOW, "problem %u: %d candidates > cap %u", i,
 		                                             res[i].ncand, cap);
@@ -1054,9 +1259,8 @@ int bt2g_frame(bt2g_ctx* c, const bt2g_frame_in* in, uint32_t n, const uint32_t*
 	   (rc = t.up(&dr, (const bt2g_sw_rect*)nullptr, n)) || (rc = t.up(&dok, (const int32_t*)nullptr, n)))
 		return rc;
 	if((rc = bt2g_frame_dev(c, din, n, dl, sc, pe, maxhalf, trim_to_ref, dp, dr, dok, c->stream))) return rc;
-	HIPCHK(hipStreamSynchronize(c->stream));
-	if((rc = down(probs, dp, n)) || (rc = down(rects, dr, n)) || (rc = down(ok, dok, n))) return rc;
-	return BT2G_OK;
+	if((rc = t.down(probs, dp, n)) || (rc = t.down(rects, dr, n)) || (rc = t.down(ok, dok, n))) return rc;
+	return t.finish();
 }
 
 int bt2g_ungapped(bt2g_ctx* c, const uint8_t* reads, const uint8_t* quals, uint32_t stride, const uint32_t* lens,
@@ -1080,9 +1284,8 @@ int bt2g_ungapped(bt2g_ctx* c, const uint8_t* reads, const uint8_t* quals, uint3
 	   (rc = t.up(&ded, (const bt2g_edit*)nullptr, (size_t)n * maxedit)))
 		return rc;
 	if((rc = bt2g_ungapped_dev(c, dr, dq, stride, dl, dp, n, sc, ohang, maxedit, dres, ded, c->stream))) return rc;
-	HIPCHK(hipStreamSynchronize(c->stream));
-	if((rc = down(res, dres, n)) || (rc = down(edits, ded, (size_t)n * maxedit))) return rc;
-	return BT2G_OK;
+	if((rc = t.down(res, dres, n)) || (rc = t.down(edits, ded, (size_t)n * maxedit))) return rc;
+	return t.finish();
 }
 
 }  // extern "C"

@@ -48,6 +48,7 @@
 #include <fcntl.h>
 #include <semaphore.h>
 #include <atomic>
+#include <chrono>
 #include <condition_variable>
 #include <mutex>
 #include <thread>
@@ -69,18 +70,34 @@ bt2g_ctx* g_ctx = nullptr;
 enum { ST_EXACT, ST_1MM, ST_SEEDS, ST_UG, ST_DP, ST_N };
 const char* const ST_NAMES[ST_N] = {"exact_sweep", "one_mm", "seed_search", "ungapped", "sw_dp"};
 std::atomic<uint64_t> g_gpu[ST_N], g_cpu[ST_N], g_batches[ST_N];
+std::atomic<uint64_t> g_call_us[ST_N], g_wait_us[ST_N];   // engine time per seam; request round trips
+// $BT2G_ADAPTER_PROF=1: kernel time per engine kernel id (bt2g_kernel_stats), all dispatchers
+const int NKERN = 8;
+const char* const KERN_NAMES[NKERN] = {"exact_sweep", "seed_search", "one_mm", "get_offset", "sw_align",
+                                       "sw_backtrace", "ungapped", "frame"};
+std::atomic<uint64_t> g_kern_n[NKERN], g_kern_us[NKERN];
+
+uint64_t now_us() {
+	return (uint64_t)std::chrono::duration_cast<std::chrono::microseconds>(
+		std::chrono::steady_clock::now().time_since_epoch()).count();
+}
 char g_stats_path[4096];
 
 void write_stats() {
 	if(!g_stats_path[0]) return;
-	char buf[1024];
+	char buf[4096];
 	int n = 0;
 	n += snprintf(buf + n, sizeof(buf) - n, "{");
 	for(int i = 0; i < ST_N; i++)
-		n += snprintf(buf + n, sizeof(buf) - n, "%s\"%s\": [%llu, %llu, %llu]", i ? ", " : "", ST_NAMES[i],
-		              (unsigned long long)g_gpu[i].load(), (unsigned long long)g_cpu[i].load(),
-		              (unsigned long long)g_batches[i].load());
-	n += snprintf(buf + n, sizeof(buf) - n, "}\n");
+		n += snprintf(buf + n, sizeof(buf) - n, "%s\"%s\": [%llu, %llu, %llu, %.1f, %.1f]", i ? ", " : "",
+		              ST_NAMES[i], (unsigned long long)g_gpu[i].load(), (unsigned long long)g_cpu[i].load(),
+		              (unsigned long long)g_batches[i].load(), g_call_us[i].load() / 1000.0,
+		              g_wait_us[i].load() / 1000.0);
+	n += snprintf(buf + n, sizeof(buf) - n, ", \"kernels\": {");
+	for(int i = 0; i < NKERN; i++)
+		n += snprintf(buf + n, sizeof(buf) - n, "%s\"%s\": [%llu, %.1f]", i ? ", " : "", KERN_NAMES[i],
+		              (unsigned long long)g_kern_n[i].load(), g_kern_us[i].load() / 1000.0);
+	n += snprintf(buf + n, sizeof(buf) - n, "}}\n");
 	int fd = open(g_stats_path, O_WRONLY | O_CREAT | O_TRUNC, 0644);
 	if(fd >= 0) {
 		ssize_t w = write(fd, buf, (size_t)n);
@@ -104,6 +121,24 @@ void die(const char* what, int rc) {
 	throw 1;   // the reference's error convention (bt2_search.cpp:5598-5620)
 }
 
+// $BT2G_ADAPTER_STATS: where the call counts go (written on SIGTERM too).
+void init_env() {
+	static std::once_flag once;
+	std::call_once(once, [] {
+		// dispatcher threads sleep in their stream waits: the server's workers need the cores
+		setenv("BT2G_SYNC", "blocking", 0);
+		const char* sp = getenv("BT2G_ADAPTER_STATS");
+		if(sp) {
+			strncpy(g_stats_path, sp, sizeof(g_stats_path) - 1);
+			signal(SIGTERM, on_term);
+		}
+		if(!getenv("BT2G_INDEX")) {
+			fprintf(stderr, "bt2g adapter: BT2G_INDEX is not set\n");
+			throw 1;
+		}
+	});
+}
+
 // Opened lazily under g_mu.
 bt2g_ctx* ctx() {
 	if(g_ctx) return g_ctx;
@@ -113,15 +148,17 @@ bt2g_ctx* ctx() {
 		throw 1;
 	}
 	const char* dev = getenv("BT2G_DEVICE");
-	const char* sp = getenv("BT2G_ADAPTER_STATS");
-	if(sp) {
-		strncpy(g_stats_path, sp, sizeof(g_stats_path) - 1);
-		signal(SIGTERM, on_term);
-	}
+	init_env();
 	int rc = bt2g_open(base, dev ? atoi(dev) : 0, &g_ctx);
 	if(rc) die("bt2g_open", rc);
 	return g_ctx;
 }
+
+// The batching dispatcher threads each own a context on the one index
+// (bt2g_open_shared: own HIP stream and scratch), so the seams' batches run
+// concurrently on the GPU; the synchronous path uses the base context under g_mu.
+thread_local bt2g_ctx* t_ctx = nullptr;
+bt2g_ctx* cur_ctx() { return t_ctx ? t_ctx : ctx(); }
 
 // bt2g_scoring of a reference Scoring object (scoring.h:442-460).  Only the
 // models the engines implement: quality-aware mismatches, constant N penalty.
@@ -175,6 +212,7 @@ struct Req {
 	int kind;
 	uint64_t key;        // batch-wide arguments: requests with equal keys share one call
 	int rc = 0;
+	char err[256] = {0}; // bt2g_last_error() of the thread that ran the call
 	sem_t sem;
 	Req(int k, uint64_t ky) : kind(k), key(ky) { sem_init(&sem, 0, 0); }
 	~Req() { sem_destroy(&sem); }
@@ -262,7 +300,7 @@ int run_exact(const std::vector<ExactReq*>& v) {
 	Pack pk;
 	pk.build(v);
 	std::vector<uint32_t> out(8 * v.size());
-	int rc = bt2g_exact_sweep(ctx(), pk.codes.data(), pk.stride, pk.lens.data(), (uint32_t)v.size(), v[0]->mine_max,
+	int rc = bt2g_exact_sweep(cur_ctx(), pk.codes.data(), pk.stride, pk.lens.data(), (uint32_t)v.size(), v[0]->mine_max,
 	                          v[0]->nofw, v[0]->norc, out.data());
 	if(rc) return rc;
 	for(size_t i = 0; i < v.size(); i++) memcpy(v[i]->out, &out[8 * i], sizeof(v[i]->out));
@@ -277,7 +315,7 @@ int run_mm(const std::vector<MmReq*>& v, uint32_t cap = 16) {
 	std::vector<uint32_t> ops(n);
 	std::vector<bt2g_mm1> h(n * cap);
 	for(size_t i = 0; i < n; i++) ms[i] = v[i]->minsc;
-	int rc = bt2g_one_mm(ctx(), pk.codes.data(), pk.quals.data(), pk.stride, pk.lens.data(), (uint32_t)n, ms.data(),
+	int rc = bt2g_one_mm(cur_ctx(), pk.codes.data(), pk.quals.data(), pk.stride, pk.lens.data(), (uint32_t)n, ms.data(),
 	                     &v[0]->sc, v[0]->nofw, v[0]->norc, cap, h.data(), cnt.data(), ops.data(), nullptr);
 	if(rc && rc != BT2G_ERR_OVERFLOW) return rc;
 	for(size_t i = 0; i < n; i++) {
@@ -301,7 +339,7 @@ int run_seeds(const std::vector<SeedReq*>& v) {
 	for(SeedReq* q : v) maxs = std::max(maxs, q->nof);
 	std::vector<uint32_t> out(n * 2 * maxs * 4), ops(n);
 	std::vector<int32_t> ns(n);
-	int rc = bt2g_seed_search(ctx(), pk.codes.data(), pk.stride, pk.lens.data(), (uint32_t)n, v[0]->seedlen, v[0]->per,
+	int rc = bt2g_seed_search(cur_ctx(), pk.codes.data(), pk.stride, pk.lens.data(), (uint32_t)n, v[0]->seedlen, v[0]->per,
 	                          v[0]->off, maxs, out.data(), ns.data(), ops.data(), nullptr);
 	if(rc) return rc;
 	for(size_t i = 0; i < n; i++) {
@@ -328,7 +366,7 @@ int run_ug(const std::vector<UgReq*>& v) {
 		P[i] = v[i]->p;
 		P[i].read = (uint32_t)i;
 	}
-	int rc = bt2g_ungapped(ctx(), pk.codes.data(), pk.quals.data(), pk.stride, pk.lens.data(), P.data(), (uint32_t)n,
+	int rc = bt2g_ungapped(cur_ctx(), pk.codes.data(), pk.quals.data(), pk.stride, pk.lens.data(), P.data(), (uint32_t)n,
 	                       &v[0]->sc, v[0]->ohang, maxedit, R.data(), E.data());
 	if(rc) return rc;
 	for(size_t i = 0; i < n; i++) {
@@ -363,7 +401,7 @@ int run_dp(const std::vector<DpReq*>& v, uint32_t cap = 0, uint32_t maxaln = 8) 
 	std::vector<int32_t> NA(n);
 	std::vector<bt2g_sw_aln> A(n * maxaln);
 	std::vector<bt2g_edit> E(n * maxaln * (size_t)maxedit);
-	int rc = bt2g_sw_align_bt(ctx(), pk.codes.data(), pk.quals.data(), pk.stride, pk.lens.data(), P.data(),
+	int rc = bt2g_sw_align_bt(cur_ctx(), pk.codes.data(), pk.quals.data(), pk.stride, pk.lens.data(), P.data(),
 	                          (uint32_t)n, W.data(), W.size(), RC.data(), &v[0]->sc, v[0]->enable8, cap, R.data(),
 	                          C.data(), maxaln, maxedit, NA.data(), A.data(), E.data(), F.data());
 	if(rc && rc != BT2G_ERR_OVERFLOW) return rc;
@@ -400,64 +438,94 @@ int run_group(int kind, const std::vector<Req*>& g) {
 }
 
 const size_t MAX_BATCH = 8192;
+const size_t BATCH_TARGET = 256;         // requests that make a batch worth launching at once
+const int BATCH_WINDOW_US = 300;         // longest wait for them after the first arrives
 
 class Dispatcher {
 public:
-	// Serve one request: queued for the dispatcher thread (batching on) or
-	// run at once under the context lock.
+	// Serve one request: queued for its seam's dispatcher thread (batching on)
+	// or run at once under the shared context's lock.
 	void submit(Req* r) {
+		const uint64_t t0 = now_us();
 		if(!batching()) {
 			std::lock_guard<std::mutex> lk(g_mu);
 			r->rc = run_group(r->kind, std::vector<Req*>{r});
+			if(r->rc) strncpy(r->err, bt2g_last_error(), sizeof(r->err) - 1);
 			g_batches[r->kind]++;
 		} else {
+			Q& q = q_[r->kind];
 			{
-				std::lock_guard<std::mutex> lk(mu_);
-				q_[r->kind].push_back(r);
+				std::lock_guard<std::mutex> lk(q.mu);
+				q.v.push_back(r);
 			}
-			cv_.notify_one();
+			q.cv.notify_one();
 			while(sem_wait(&r->sem) != 0) {}
 		}
-		if(r->rc) die(ST_NAMES[r->kind], r->rc);
+		g_wait_us[r->kind] += now_us() - t0;
+		if(r->rc) {
+			fprintf(stderr, "bt2g adapter: %s failed (%d): %s\n", ST_NAMES[r->kind], r->rc, r->err);
+			throw 1;
+		}
 	}
 
 private:
+	struct Q {
+		std::mutex mu;
+		std::condition_variable cv;
+		std::vector<Req*> v;
+	};
+
 	bool batching() {
 		std::call_once(once_, [this] {
 			const char* b = getenv("BT2G_BATCH");
 			on_ = !(b && b[0] == '0');
 			if(on_) {
-				std::lock_guard<std::mutex> lk(g_mu);
-				ctx();
-				std::thread(&Dispatcher::loop, this).detach();
+				init_env();
+				{
+					std::lock_guard<std::mutex> lk(g_mu);
+					ctx();                          // the base context, before any dispatcher
+				}
+				// dispatchers per seam: $BT2G_SEAM_THREADS (default 2; the DP seam, whose
+				// batches take longest, twice that)
+				const char* t = getenv("BT2G_SEAM_THREADS");
+				const int per = std::max(1, t ? atoi(t) : 2);
+				for(int k = 0; k < ST_N; k++)
+					for(int i = 0; i < (k == ST_DP ? 2 * per : per); i++)
+						std::thread(&Dispatcher::loop, this, k).detach();
 			}
 		});
 		return on_;
 	}
 
-	void loop() {
-		int next = 0;
+	// Dispatcher threads of a seam share its queue: each drains it into batches,
+	// grouped by the batch-wide arguments (arrival order kept within a group), on
+	// its own context.
+	void loop(int kind) {
+		int rc0 = bt2g_open_shared(g_ctx, &t_ctx);
+		if(rc0) {
+			fprintf(stderr, "bt2g adapter: bt2g_open_shared (%s dispatcher) failed (%d): %s\n", ST_NAMES[kind], rc0,
+			        bt2g_last_error());
+			t_ctx = nullptr;                 // fall back to the shared context under g_mu
+		}
+		const char* pf = getenv("BT2G_ADAPTER_PROF");
+		const bool prof = t_ctx && pf && pf[0] == '1';
+		if(prof) bt2g_set_profiling(t_ctx, 1);
+		uint64_t seen_n[NKERN] = {0};
+		double seen_ms[NKERN] = {0};
+		Q& q = q_[kind];
 		std::vector<Req*> take;
 		for(;;) {
-			int kind = -1;
 			{
-				std::unique_lock<std::mutex> lk(mu_);
-				cv_.wait(lk, [this] {
-					for(int k = 0; k < ST_N; k++)
-						if(!q_[k].empty()) return true;
-					return false;
-				});
-				for(int d = 0; d < ST_N && kind < 0; d++) {         // round robin over the seams
-					int k = (next + d) % ST_N;
-					if(!q_[k].empty()) kind = k;
-				}
-				next = (kind + 1) % ST_N;
-				std::vector<Req*>& q = q_[kind];
-				const size_t m = std::min(q.size(), MAX_BATCH);
-				take.assign(q.begin(), q.begin() + m);
-				q.erase(q.begin(), q.begin() + m);
+				std::unique_lock<std::mutex> lk(q.mu);
+				q.cv.wait(lk, [&q] { return !q.v.empty(); });
+				// a short window for the batch to fill: every call costs a few copies and a
+				// stream sync, which a batch of one or two requests does not amortise
+				q.cv.wait_for(lk, std::chrono::microseconds(BATCH_WINDOW_US),
+				              [&q] { return q.v.size() >= BATCH_TARGET; });
+				const size_t m = std::min(q.v.size(), MAX_BATCH);
+				take.assign(q.v.begin(), q.v.begin() + m);
+				q.v.erase(q.v.begin(), q.v.begin() + m);
 			}
-			// group by the batch-wide arguments, keeping arrival order within a group
 			std::vector<bool> done(take.size(), false);
 			for(size_t i = 0; i < take.size(); i++) {
 				if(done[i]) continue;
@@ -465,13 +533,28 @@ private:
 				for(size_t j = i; j < take.size(); j++)
 					if(!done[j] && take[j]->key == take[i]->key) { g.push_back(take[j]); done[j] = true; }
 				int rc;
-				{
+				const uint64_t t0 = now_us();
+				if(t_ctx) {
+					rc = run_group(kind, g);
+				} else {
 					std::lock_guard<std::mutex> lk(g_mu);
 					rc = run_group(kind, g);
+				}
+				g_call_us[kind] += now_us() - t0;
+				for(int k = 0; prof && k < NKERN; k++) {
+					uint64_t ln = 0;
+					double ms = 0;
+					if(bt2g_kernel_stats(t_ctx, k, &ln, &ms) == BT2G_OK && ln > seen_n[k]) {
+						g_kern_n[k] += ln - seen_n[k];
+						g_kern_us[k] += (uint64_t)((ms - seen_ms[k]) * 1000.0);
+						seen_n[k] = ln;
+						seen_ms[k] = ms;
+					}
 				}
 				g_batches[kind]++;
 				for(Req* r : g) {
 					r->rc = rc;
+					if(rc) snprintf(r->err, sizeof(r->err), "%s (batch of %zu)", bt2g_last_error(), g.size());
 					sem_post(&r->sem);
 				}
 			}
@@ -480,9 +563,7 @@ private:
 
 	std::once_flag once_;
 	bool on_ = false;
-	std::mutex mu_;
-	std::condition_variable cv_;
-	std::vector<Req*> q_[ST_N];
+	Q q_[ST_N];
 };
 
 Dispatcher g_disp;
@@ -513,7 +594,43 @@ struct DpState {
 	uint32_t maxedit = 0;
 	int32_t naln = 0;
 	uint32_t next = 0;         // next engine alignment to hand out
+	// the problem as sent to the engine (for $BT2G_ADAPTER_DUMP on a mismatch)
+	Row row;
+	bt2g_sw_problem prob;
+	bt2g_sw_rect rect;
+	std::vector<uint8_t> win;
+	int enable8 = 1;
 };
+
+// One engine/reference disagreement as a JSON line in $BT2G_ADAPTER_DUMP:
+// everything needed to replay the DP through the oracle and the reference.
+void dump_dp(const DpState& st, const std::vector<DpBtCandidate>& cands, size_t cural, int64_t minsc_now,
+             const char* why) {
+	const char* path = getenv("BT2G_ADAPTER_DUMP");
+	if(!path) return;
+	static std::mutex mu;
+	std::lock_guard<std::mutex> lk(mu);
+	FILE* f = fopen(path, "a");
+	if(!f) return;
+	fprintf(f, "{\"why\": \"%s\", \"cural\": %zu, \"minsc_now\": %lld, \"fw\": %d, \"ncol\": %u, \"minsc\": %d, "
+	           "\"rect\": [%d, %d, %d], \"enable8\": %d, \"read\": \"", why, cural, (long long)minsc_now,
+	        st.prob.fw, st.prob.ncol, st.prob.minsc, st.rect.triml, st.rect.corel, st.rect.corer, st.enable8);
+	for(uint32_t i = 0; i < st.row.len; i++) fputc("ACGTN"[st.row.codes[i] > 4 ? 4 : st.row.codes[i]], f);
+	fprintf(f, "\", \"qual\": \"");
+	for(uint32_t i = 0; i < st.row.len; i++) fputc(st.row.quals[i] == '"' || st.row.quals[i] == '\\' ? 'I' : st.row.quals[i], f);
+	fprintf(f, "\", \"win\": [");
+	for(size_t i = 0; i < st.win.size(); i++) fprintf(f, "%s%d", i ? ", " : "", st.win[i]);
+	fprintf(f, "], \"cands\": [");
+	for(size_t i = 0; i < cands.size(); i++)
+		fprintf(f, "%s[%zu, %zu, %lld, %d]", i ? ", " : "", (size_t)cands[i].row, (size_t)cands[i].col,
+		        (long long)cands[i].score, i < st.fates.size() ? st.fates[i] : -9);
+	fprintf(f, "], \"alns\": [");
+	for(int32_t k = 0; k < st.naln; k++)
+		fprintf(f, "%s[%d, %d, %d, %d]", k ? ", " : "", st.alns[k].cand, st.alns[k].score, st.alns[k].off,
+		        st.alns[k].nedit);
+	fprintf(f, "]}\n");
+	fclose(f);
+}
 
 // one entry per SwAligner of the worker thread (sw and osw, bt2_search.cpp:3130)
 thread_local std::vector<std::pair<const void*, DpState*>> t_dp;
@@ -780,6 +897,13 @@ bool SwAlignerAcc::gpu_align(TAlScore& best, bool& served) {
 	q.win.assign((const uint8_t*)rf_ + rfi_, (const uint8_t*)rf_ + rfi_ + ncol + 1);
 	g_disp.submit(&q);
 	const bt2g_sw_result& o = q.o;
+	if(getenv("BT2G_ADAPTER_DUMP")) {
+		st.row = q.r;
+		st.prob = q.p;
+		st.rect = q.rect;
+		st.win = q.win;
+		st.enable8 = q.enable8;
+	}
 	st.naln = q.naln;
 	st.fates.swap(q.fates);
 	st.alns.swap(q.alns);
@@ -838,6 +962,9 @@ bool SwAlignerAcc::gpu_next(SwResult& res, TAlScore minsc, RandomSource& rnd, Dp
 		if(f == BT_CAND_FATE_FILT_DOMINATED) { c.fate = f; nbtfiltdo_++; cural_++; continue; }
 		if(f != BT_CAND_FATE_SUCCEEDED && f != BT_CAND_FATE_FAILED) {
 			fprintf(stderr, "bt2g adapter: candidate %zu of %zu has no engine fate (%d)\n", cural_, candsz, f);
+			std::vector<DpBtCandidate> cv(btncand_.size());
+			for(size_t i = 0; i < btncand_.size(); i++) cv[i] = btncand_[i];
+			dump_dp(st, cv, cural_, minsc, "no fate");
 			throw 1;
 		}
 		const uint32_t reseed = rnd.nextU32() + 1;
@@ -851,11 +978,17 @@ bool SwAlignerAcc::gpu_next(SwResult& res, TAlScore minsc, RandomSource& rnd, Dp
 		if(f == BT_CAND_FATE_FAILED) { cural_++; continue; }
 		if(st.next >= (uint32_t)st.naln) {
 			fprintf(stderr, "bt2g adapter: engine returned %d alignments, reference wants more\n", st.naln);
+			std::vector<DpBtCandidate> cv(btncand_.size());
+			for(size_t i = 0; i < btncand_.size(); i++) cv[i] = btncand_[i];
+			dump_dp(st, cv, cural_, minsc, "too few alignments");
 			throw 1;
 		}
 		const bt2g_sw_aln& a = st.alns[st.next];
 		if(a.cand != (int32_t)cural_ || a.nedit > (int32_t)st.maxedit) {
 			fprintf(stderr, "bt2g adapter: alignment %u is candidate %d, expected %zu\n", st.next, a.cand, cural_);
+			std::vector<DpBtCandidate> cv(btncand_.size());
+			for(size_t i = 0; i < btncand_.size(); i++) cv[i] = btncand_[i];
+			dump_dp(st, cv, cural_, minsc, "alignment order");
 			throw 1;
 		}
 		const bt2g_edit* ed = &st.edits[(size_t)st.next * st.maxedit];

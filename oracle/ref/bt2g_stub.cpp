@@ -36,6 +36,7 @@ void bt2ref_ungapped(void* vh, int n, const char** seqs, const char** quals, con
 
 struct bt2g_ctx {
 	void* ref;
+	std::string base;
 };
 
 namespace {
@@ -73,6 +74,17 @@ int bt2g_open(const char* base, int, bt2g_ctx** out) {
 	bt2g_ctx* c = new bt2g_ctx();
 	c->ref = bt2ref_open(base);
 	if(!c->ref) { delete c; return fail(BT2G_ERR_IO, "bt2ref_open"); }
+	c->base = base;
+	*out = c;
+	return BT2G_OK;
+}
+
+int bt2g_open_shared(bt2g_ctx* base, bt2g_ctx** out) {
+	if(!base || !out) return fail(BT2G_ERR_ARG, "null argument");
+	bt2g_ctx* c = new bt2g_ctx();
+	c->ref = bt2ref_open(base->base.c_str());   // the harness index is driven by one thread
+	if(!c->ref) { delete c; return fail(BT2G_ERR_IO, "bt2ref_open"); }
+	c->base = base->base;
 	*out = c;
 	return BT2G_OK;
 }
@@ -215,6 +227,15 @@ int bt2g_sw_align_bt(bt2g_ctx*, const uint8_t* reads, const uint8_t* quals, uint
 			for(uint32_t k = 0; k < cap; k++) fates[(size_t)i * cap + k] = (int8_t)ft[k];
 	}
 	return rc;
+}
+
+// kernel timing: nothing runs on a device here
+int bt2g_set_profiling(bt2g_ctx*, int) { return BT2G_OK; }
+
+int bt2g_kernel_stats(bt2g_ctx*, int, uint64_t* launches, double* total_ms) {
+	if(launches) *launches = 0;
+	if(total_ms) *total_ms = 0;
+	return BT2G_OK;
 }
 
 }  // extern "C"

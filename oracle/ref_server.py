@@ -118,6 +118,7 @@ class Server:
                     errs.append((i, r.returncode, r.stderr[-2000:]))
                 outs[i] = r.stdout
 
+        c0 = self.cpu_seconds()
         t0 = time.perf_counter()
         ths = [threading.Thread(target=worker) for _ in range(max(1, min(k, len(chunk_args))))]
         for t in ths:
@@ -125,9 +126,18 @@ class Server:
         for t in ths:
             t.join()
         dt = time.perf_counter() - t0
+        self.last_cpu_s = self.cpu_seconds() - c0        # server CPU time (all threads) over the run
         if errs:
             raise RuntimeError(f"client failures: {errs[:3]}")
         return dt, outs
+
+    def cpu_seconds(self):
+        """User + system CPU seconds of the server process so far (/proc/<pid>/stat)."""
+        try:
+            f = open(f"/proc/{self.proc.pid}/stat").read().rsplit(")", 1)[1].split()
+            return (int(f[11]) + int(f[12])) / os.sysconf("SC_CLK_TCK")
+        except (OSError, ValueError, IndexError):
+            return float("nan")
 
     def close(self):
         if self.proc.poll() is None:

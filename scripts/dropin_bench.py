@@ -85,7 +85,8 @@ def main():
             dt, outs = s.run(chunks, k=a.k)
         sams[tag] = rs.sorted_records(outs)
         unit = "pairs/s" if a.mode == "paired" else "reads/s"
-        out[tag] = {"seconds": dt, "rate": a.reads / dt, "unit": unit, "threads": th, "records": len(sams[tag])}
+        out[tag] = {"seconds": dt, "rate": a.reads / dt, "unit": unit, "threads": th, "records": len(sams[tag]),
+                    "server_cpu_s": s.last_cpu_s, "server_cores_busy": s.last_cpu_s / dt}
         time.sleep(0.5)
         if os.path.exists(stats):
             out[tag]["engine_calls"] = json.load(open(stats))
