@@ -49,6 +49,7 @@
 #include <semaphore.h>
 #include <atomic>
 #include <chrono>
+#include <pthread.h>
 #include <condition_variable>
 #include <mutex>
 #include <thread>
@@ -501,6 +502,11 @@ private:
 	// grouped by the batch-wide arguments (arrival order kept within a group), on
 	// its own context.
 	void loop(int kind) {
+		{
+			char nm[16];
+			snprintf(nm, sizeof(nm), "bt2g-%.10s", ST_NAMES[kind]);
+			pthread_setname_np(pthread_self(), nm);
+		}
 		int rc0 = bt2g_open_shared(g_ctx, &t_ctx);
 		if(rc0) {
 			fprintf(stderr, "bt2g adapter: bt2g_open_shared (%s dispatcher) failed (%d): %s\n", ST_NAMES[kind], rc0,

@@ -127,9 +127,32 @@ class Server:
             t.join()
         dt = time.perf_counter() - t0
         self.last_cpu_s = self.cpu_seconds() - c0        # server CPU time (all threads) over the run
+        self.last_threads = self.thread_cpu()
         if errs:
             raise RuntimeError(f"client failures: {errs[:3]}")
         return dt, outs
+
+    def thread_cpu(self):
+        """{thread name: [threads, CPU seconds, busiest thread's CPU seconds]} of the server."""
+        out = {}
+        tck = os.sysconf("SC_CLK_TCK")
+        try:
+            tids = os.listdir(f"/proc/{self.proc.pid}/task")
+        except OSError:
+            return out
+        for t in tids:
+            try:
+                txt = open(f"/proc/{self.proc.pid}/task/{t}/stat").read()
+            except OSError:
+                continue
+            name = txt[txt.index("(") + 1:txt.rindex(")")]
+            f = txt.rsplit(")", 1)[1].split()
+            cs = (int(f[11]) + int(f[12])) / tck
+            e = out.setdefault(name, [0, 0.0, 0.0])
+            e[0] += 1
+            e[1] += cs
+            e[2] = max(e[2], cs)
+        return out
 
     def cpu_seconds(self):
         """User + system CPU seconds of the server process so far (/proc/<pid>/stat)."""

@@ -86,7 +86,8 @@ def main():
         sams[tag] = rs.sorted_records(outs)
         unit = "pairs/s" if a.mode == "paired" else "reads/s"
         out[tag] = {"seconds": dt, "rate": a.reads / dt, "unit": unit, "threads": th, "records": len(sams[tag]),
-                    "server_cpu_s": s.last_cpu_s, "server_cores_busy": s.last_cpu_s / dt}
+                    "server_cpu_s": s.last_cpu_s, "server_cores_busy": s.last_cpu_s / dt,
+                    "server_threads_cpu": s.last_threads}
         time.sleep(0.5)
         if os.path.exists(stats):
             out[tag]["engine_calls"] = json.load(open(stats))
