@@ -485,7 +485,7 @@ def shard_seed(rank):
     return 42 + rank
 
 
-def cpu_baseline(idx, reads, quals, pipe, sample, threads):
+def cpu_baseline(idx, reads, quals, pipe, sample, threads, base=None):
     """Reference code (oracle/_ref/libbt2ref.so = /root/reference built by
     oracle/ref/Makefile) on the same per-read work for `sample` reads (paired:
     `sample` pairs, both mates, plus their mate searches), split over `threads`
@@ -500,9 +500,9 @@ def cpu_baseline(idx, reads, quals, pipe, sample, threads):
     import synth
     from oracle.ref_chain import RefChain
     from oracle.ref_harness import score_params
-    tmp = tempfile.mkdtemp(prefix="bt2bench_")
-    base = os.path.join(tmp, "g")
-    bi.write_index(base, idx)
+    if not base or not os.path.exists(base + ".rev.2.bt2"):
+        base = os.path.join(tempfile.mkdtemp(prefix="bt2bench_"), "g")
+        bi.write_index(base, idx)
     chain = RefChain(base)
     L, R = chain.L, chain.R
     pol = pipe.pol
@@ -792,7 +792,9 @@ def main():
     ap.add_argument("--server-sample", type=int, default=200_000,
                     help="reads (pairs) timed through the stock reference server and the drop-in server (0: skip)")
     ap.add_argument("--server-workers", type=int, default=512, help="drop-in server worker threads (-p)")
-    ap.add_argument("--index-cache", default="", help="reuse/write the built index at this base path")
+    ap.add_argument("--index-cache", default="auto",
+                    help="reuse/write the built index at this base path ('auto': under $TMPDIR keyed by the "
+                         "genome model and size; '': always build)")
     ap.add_argument("--pmc-fetch", default="", help="rocprofv3 --pmc FETCH_SIZE counter_collection.csv of this "
                                                     "command: fills roofline.traffic")
     ap.add_argument("--pmc-write", default="", help="same for WRITE_SIZE")
@@ -816,12 +818,26 @@ def main():
     log(f"[rank {rank}] genome {sum(len(p) for p in parts)/1e6:.0f} Mbp in {time.time()-t0:.1f}s")
     t1 = time.time()
     cache = args.index_cache
+    if cache == "auto":
+        import tempfile
+        cache = os.path.join(tempfile.gettempdir(), "bt2g_bench_index",
+                             f"{args.genome_model}_{args.genome_mb:g}mb", "g")
     if cache and os.path.exists(cache + ".rev.2.bt2"):
         idx = bi.read_index(cache)                  # same seed -> same genome -> same index
+        log(f"[rank {rank}] index read from {cache}")
     else:
         idx = bi.build_index_device(parts, names=names, device=str(dev))
-        if cache:
-            bi.write_index(cache, idx)
+        if cache and rank == 0:
+            # written beside, then renamed into place: a reader never sees half an index
+            import shutil
+            d = os.path.dirname(cache)
+            tmpd = f"{d}.tmp{os.getpid()}"
+            os.makedirs(tmpd, exist_ok=True)
+            bi.write_index(os.path.join(tmpd, os.path.basename(cache)), idx)
+            if os.path.isdir(d):
+                shutil.rmtree(d, ignore_errors=True)
+            os.makedirs(os.path.dirname(d), exist_ok=True)
+            os.rename(tmpd, d)
     torch.cuda.synchronize()
     log(f"[rank {rank}] index built on GPU in {time.time()-t1:.1f}s")
     torch.cuda.empty_cache()
@@ -889,6 +905,19 @@ def main():
     sw_gcups = sw_cells / (per_launch.get(4, float("nan")) / 1e3) / 1e9
     for k in per_launch:
         log(f"[rank {rank}] {names_k[k]:12s} {per_launch[k]:8.3f} ms/launch")
+    prof = getattr(bt2g.lib(), "bt2g_bt_prof_read", None) if "prof" in bt2g.LIB_PATH else None
+    if prof is not None and stats[5][0]:
+        # profiling build of the backtrace (scripts/bt_bench.py): counters per launch
+        import ctypes
+        cnt = (ctypes.c_ulonglong * 16)()
+        prof(cnt)
+        nl = stats[5][0]
+        names_p = ["walks", "steps", "colhit16_blocks", "escan_rounds", "candidates", "dom_tests", "replays",
+                   "hget", "chunk_reloads", "tile_loads", "tile_writebacks", "colhit8_blocks", "dps_walked", "",
+                   "", "wave_steps"]
+        d = {k: int(v) // nl for k, v in zip(names_p, cnt) if k}
+        d["lane_utilization"] = d["steps"] / max(1, d["wave_steps"])
+        log(f"[rank {rank}] bt_prof per launch (all launches since start / {nl}): {d}")
     naln_np = pipe.naln[:last["npb"]].cpu().numpy()
     bt_stats = {"alignments": int(naln_np.clip(0).sum()), "dps_with_alignment": int((naln_np > 0).sum()),
                 "dps_at_maxaln": int((naln_np >= pipe.maxaln).sum()), "maxaln": pipe.maxaln,
@@ -940,7 +969,7 @@ def main():
         threads = args.cpu_threads or host["usable"]
         sample = min(args.cpu_sample, pipe.npairs if args.mode == "paired" else pipe.n)
         try:
-            dt, ref, mate, secs = cpu_baseline(idx, reads_np, quals_np, pipe, sample, threads)
+            dt, ref, mate, secs = cpu_baseline(idx, reads_np, quals_np, pipe, sample, threads, base=cache or None)
             paired = args.mode == "paired"
             cpu = {"value": sample / dt, "unit": "read pairs/s" if paired else "reads/s", "cores": threads,
                    "kind": "reference", "host": host, "stage_seconds": secs,

@@ -878,10 +878,12 @@ int bt2g_sw_align_bt_dev(bt2g_ctx* c, const uint8_t* reads, const uint8_t* quals
 	if((rc = sw_align_impl(c, reads, quals, stride, lens, probs, nprob, windows, sc, enable8, cap, res, cands,
 	                       nullptr, nullptr, plane, a.slot, hb, maxcol, st)))
 		return rc;
+	a.rwords = sw_bt_rcols(maxrow, maxcol);
+	a.rrows = sw_bt_rrows(maxrow);
 	a.mwords = sw_bt_tcols(maxcol);
 	a.mrows = sw_bt_trows(maxrow);
 	a.mslot = sw_bt_mslot(maxrow, maxcol, sc->local != 0);
-	a.mdom = sc->local ? sw_bt_mslot(maxrow, maxcol, false) : 0u;
+	a.mdom = sc->local ? sw_bt_mdom(maxrow, maxcol) : 0u;
 	if(!a.marks && (rc = talloc((void**)&a.marks, sizeof(uint32_t) * a.mslot * nprob))) return rc;
 	a.probs = probs; a.nprob = nprob; a.reads = reads; a.quals = quals; a.stride = stride; a.lens = lens;
 	a.windows = windows; a.ref_codes = c->ref_codes; a.ref_starts = c->ref_starts; a.rects = rects;

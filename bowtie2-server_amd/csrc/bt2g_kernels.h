@@ -114,7 +114,8 @@ struct BtArgs {
 	int plane_top;                    //   0 systolic end-to-end, 1 top-aligned (per-lane fills), 2 systolic local
 	uint32_t* marks;                  // per problem (mslot words): reportedThrough tiles
 	uint64_t mslot;
-	uint32_t mwords, mrows;           //   tiles per tile row, tile rows
+	uint32_t rwords, rrows;           //   reportedThrough: diagonal tiles per tile row, tile rows
+	uint32_t mwords, mrows;           //   FILT_DOMINATED squares: 8x8 tiles per tile row, tile rows
 	uint64_t mdom;                    // local mode: word offset of the FILT_DOMINATED tiles
 	SwConst C;
 	int local;
@@ -127,14 +128,23 @@ struct BtArgs {
 };
 // kind: 0 u8 score plane, 1 u16 score plane
 void launch_sw_bt(int kind, const BtArgs& a, hipStream_t st);
-// backtrace mark scratch per problem of <= rows x cols: 8x8-cell bit tiles
-// (2 words each) + one valid bit per tile (sw_backtrace.hip); dom: a second
-// tile set of the same shape (local mode's dominated-candidate squares)
+// backtrace mark scratch per problem of <= rows x cols (sw_backtrace.hip):
+// reportedThrough in 64-bit tiles of 16 rows x 4 diagonals (a diagonal run
+// stays in one tile for up to 16 steps) + one valid bit per tile; dom (local
+// mode's dominated-candidate squares): 8x8-cell tiles + valid bits.
+inline uint32_t sw_bt_rcols(uint32_t rows, uint32_t cols) { return (cols + rows + 3u) / 4u; }
+inline uint32_t sw_bt_rrows(uint32_t rows) { return (rows + 15u) / 16u; }
 inline uint32_t sw_bt_tcols(uint32_t cols) { return (cols + 7u) / 8u; }
 inline uint32_t sw_bt_trows(uint32_t rows) { return (rows + 7u) / 8u; }
+inline uint64_t sw_bt_tiles_words(uint64_t tr, uint64_t tc) {
+	return (tr * tc * 2u + tr * ((tc + 31u) / 32u) + 3u) & ~(uint64_t)3u;
+}
+// word offset of the dom tiles = the reportedThrough part
+inline uint64_t sw_bt_mdom(uint32_t rows, uint32_t cols) {
+	return sw_bt_tiles_words(sw_bt_rrows(rows), sw_bt_rcols(rows, cols));
+}
 inline uint64_t sw_bt_mslot(uint32_t rows, uint32_t cols, bool dom) {
-	const uint64_t tc = sw_bt_tcols(cols), tr = sw_bt_trows(rows);
-	return ((tr * tc * 2u + tr * ((tc + 31u) / 32u) + 3u) & ~(uint64_t)3u) * (dom ? 2u : 1u);
+	return sw_bt_mdom(rows, cols) + (dom ? sw_bt_tiles_words(sw_bt_trows(rows), sw_bt_tcols(cols)) : 0u);
 }
 void launch_sort_cands(const bt2g_sw_result* res, bt2g_sw_cand* cands, uint32_t nprob, uint32_t cap,
                        uint32_t* big, uint32_t* nbig, hipStream_t st);

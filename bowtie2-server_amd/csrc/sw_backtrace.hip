@@ -86,10 +86,19 @@ struct Plane {
 
 }  // namespace
 
-// work counters for the CPU emulation only (tests/cpu_emul, scripts)
+// work counters for the CPU emulation (tests/cpu_emul) and, with
+// BT2G_BT_PROF, for a profiling build of the kernel (bt2g_bt_prof_read):
+// 0 walks, 1 steps, 2 col_hit u16 block loads, 3 E-scan rounds, 4 candidates,
+// 5 dominance tests, 6 replays, 7 hget calls, 8 u8 chunk reloads, 9 tile loads,
+// 10 tile write-backs, 11 col_hit u8 block loads, 12 DPs walked; 15: sum over
+// waves of 64 x the wave's largest per-lane step count
 #ifdef BT2G_BT_COUNT
-extern unsigned long long bt_counts[8];
+extern unsigned long long bt_counts[16];
 #define BTC(i) (bt_counts[i]++)
+#elif defined(BT2G_BT_PROF)
+__device__ unsigned long long g_bt_prof[16];
+__device__ unsigned int g_bt_wave_max[1u << 16];
+#define BTC(i) (pc[i]++)
 #else
 #define BTC(i) ((void)0)
 #endif
@@ -105,6 +114,17 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(BT2G_BT
 k_sw_bt(BtArgs A) {
 	const uint32_t p = blockIdx.x * 64u + threadIdx.x;
 	if(p >= A.nprob) return;
+#ifdef BT2G_BT_PROF
+	uint32_t pc[13] = {0};
+	struct Flush {
+		uint32_t* pc;
+		__device__ ~Flush() {
+			for(int i = 0; i < 13; i++)
+				if(pc[i]) atomicAdd(&g_bt_prof[i], (unsigned long long)pc[i]);
+			atomicMax(&g_bt_wave_max[blockIdx.x & 0xffffu], pc[1]);
+		}
+	} flush_{pc};
+#endif
 	const bt2g_sw_result R = A.res[p];
 	if(!R.aligned || R.ncand <= 0) { A.naln[p] = 0; return; }
 	if((uint32_t)R.ncand > A.cap) { A.naln[p] = -5; return; }   // truncated list: not the reference's
@@ -160,6 +180,7 @@ k_sw_bt(BtArgs A) {
 #pragma unroll 1
 			for(int32_t o0 = ((int32_t)pad + rlo) & ~15; o0 <= (int32_t)pad + rhi; o0 += 16) {
 				if(pl.mask && !((pl.mask[c] >> (o0 >> 4)) & 1u)) continue;   // below minsc: no hit
+				BTC(11);
 				const uint4 v = *(const uint4*)(slot + ((size_t)(o0 >> 4) * A.pcols + c) * 16u);
 				const uint32_t wv[4] = {v.x, v.y, v.z, v.w};
 #pragma unroll
@@ -199,35 +220,52 @@ k_sw_bt(BtArgs A) {
 	}
 	int32_t triml = 0, corel = 0, corer = 0x7fffffff;
 	if(A.rects) { const bt2g_sw_rect rc = A.rects[p]; triml = rc.triml; corel = rc.corel; corer = rc.corer; }
-	// reportedThrough: 8x8-cell bit tiles (one u64 each), one tile cached in
-	// registers at a time (a walk stays in a tile for several steps); a tile is
-	// valid once written back (valid bits per tile row, cleared here), so
-	// nothing else is ever cleared.  (Valid bits in LDS instead: measured
-	// slower, 34.6 vs 32.8 ms end-to-end, 155 vs 144 ms local.)
+	// reportedThrough: bit tiles of 16 rows x 4 diagonals (one u64 each; a
+	// walk is mostly a diagonal run, which stays in a tile for up to 16 steps
+	// -- 8x8 cell tiles changed every ~4), one tile cached in registers at a
+	// time.  A tile is valid once written back (one valid bit per tile, cleared
+	// here; the current valid word is cached in a register too), so nothing
+	// else is ever cleared.  (Valid bits in LDS instead: measured slower.)
 	uint32_t* marks = A.marks + (size_t)p * A.mslot;
-	const uint32_t tcols = A.mwords, trows = A.mrows, vw = (tcols + 31u) / 32u;
+	const uint32_t tcols = A.rwords, trows = A.rrows, vw = (tcols + 31u) / 32u;
 	uint32_t* valid = marks + (size_t)trows * tcols * 2u;
 	for(uint32_t i = 0; i < trows * vw; i++) valid[i] = 0u;
 	uint32_t ttr = 0xffffffffu, ttc = 0;
 	uint64_t tbits = 0;
 	bool tdirty = false;
+	uint32_t vidx = 0xffffffffu, vval = 0u;
+	bool vdirty = false;
+	auto vword = [&](uint32_t i) -> uint32_t& {
+		if(i != vidx) {
+			if(vdirty) valid[vidx] = vval;
+			vdirty = false;
+			vidx = i;
+			vval = valid[i];
+		}
+		return vval;
+	};
+	const uint32_t dg0 = nrow - 1u;            // diagonal index of (r, c): c - r + nrow - 1 >= 0
 	auto tile_get = [&](uint32_t r, uint32_t c) {
-		const uint32_t tr = r >> 3, tc = c >> 3;
+		const uint32_t tr = r >> 4, tc = (c + dg0 - r) >> 2;
 		if(tr == ttr && tc == ttc) return;
 		if(tdirty) {
+			BTC(10);
 			*(uint64_t*)(marks + ((size_t)ttr * tcols + ttc) * 2u) = tbits;
-			valid[ttr * vw + (ttc >> 5)] |= 1u << (ttc & 31u);
+			vword(ttr * vw + (ttc >> 5)) |= 1u << (ttc & 31u);
+			vdirty = true;
 			tdirty = false;
 		}
 		ttr = tr;
 		ttc = tc;
-		const bool v = (valid[tr * vw + (tc >> 5)] >> (tc & 31u)) & 1u;
+		BTC(9);
+		const bool v = (vword(tr * vw + (tc >> 5)) >> (tc & 31u)) & 1u;
 		tbits = v ? *(const uint64_t*)(marks + ((size_t)tr * tcols + tc) * 2u) : 0ull;
 	};
+	auto rbit = [&](uint32_t r, uint32_t c) -> uint64_t { return 1ull << (((r & 15u) << 2) | ((c + dg0 - r) & 3u)); };
 	auto tbit = [](uint32_t r, uint32_t c) -> uint64_t { return 1ull << (((r & 7u) << 3) | (c & 7u)); };
 	auto marked = [&](uint32_t r, uint32_t c) -> bool {
 		tile_get(r, c);
-		return (tbits & tbit(r, c)) != 0;
+		return (tbits & rbit(r, c)) != 0;
 	};
 	// 16-byte windows over the read, the qualities and the reference (aligned
 	// uint4: a walk moves one row / column at a time); a window that would
@@ -272,6 +310,7 @@ k_sw_bt(BtArgs A) {
 		if(KIND != 0) return pl.h(r, c);   // u16 planes: direct (a chunk cache costs occupancy)
 		const uint32_t rsx = pad + r, b = rsx >> 4;
 		if(b != cb || c < cc0 || c > cc0 + 3u) {
+			BTC(8);
 			cb = b;
 			cc0 = c >= 3u ? c - 3u : 0u;
 			if(cc0 + 4u > A.pcols) cc0 = A.pcols >= 4u ? A.pcols - 4u : 0u;
@@ -307,19 +346,20 @@ k_sw_bt(BtArgs A) {
 	uint32_t SQ = nrow >> 4;
 	if(SQ == 0) SQ = 1;
 	uint32_t* dmarks = marks + A.mdom;
-	uint32_t* dvalid = dmarks + (size_t)trows * tcols * 2u;
+	const uint32_t dtcols = A.mwords, dtrows = A.mrows, dvw = (dtcols + 31u) / 32u;
+	uint32_t* dvalid = dmarks + (size_t)dtrows * dtcols * 2u;
 	if(local)
-		for(uint32_t i = 0; i < trows * vw; i++) dvalid[i] = 0u;
+		for(uint32_t i = 0; i < dtrows * dvw; i++) dvalid[i] = 0u;
 	auto dom_test = [&](uint32_t r, uint32_t c) -> bool {
 		const uint32_t tr = r >> 3, tc = c >> 3;
-		if(!((dvalid[tr * vw + (tc >> 5)] >> (tc & 31u)) & 1u)) return false;
-		return (*(const uint64_t*)(dmarks + ((size_t)tr * tcols + tc) * 2u) & tbit(r, c)) != 0;
+		if(!((dvalid[tr * dvw + (tc >> 5)] >> (tc & 31u)) & 1u)) return false;
+		return (*(const uint64_t*)(dmarks + ((size_t)tr * dtcols + tc) * 2u) & tbit(r, c)) != 0;
 	};
 	auto dom_add = [&](uint32_t r, uint32_t c) {
 		const uint32_t r0 = r > SQ ? r - SQ : 0u, c0 = c > SQ ? c - SQ : 0u;
 		uint32_t r1 = r + SQ, c1 = c + SQ;
-		r1 = r1 < trows * 8u - 1u ? r1 : trows * 8u - 1u;
-		c1 = c1 < tcols * 8u - 1u ? c1 : tcols * 8u - 1u;
+		r1 = r1 < dtrows * 8u - 1u ? r1 : dtrows * 8u - 1u;
+		c1 = c1 < dtcols * 8u - 1u ? c1 : dtcols * 8u - 1u;
 		for(uint32_t tr = r0 >> 3; tr <= r1 >> 3; tr++) {
 			// bytes (tile rows) inside [r0, r1], one bit each
 			const uint32_t lo = tr * 8u > r0 ? 0u : r0 & 7u, hi = tr * 8u + 7u < r1 ? 7u : r1 & 7u;
@@ -327,8 +367,8 @@ k_sw_bt(BtArgs A) {
 			for(uint32_t tc = c0 >> 3; tc <= c1 >> 3; tc++) {
 				const uint32_t cl0 = tc * 8u > c0 ? 0u : c0 & 7u, ch = tc * 8u + 7u < c1 ? 7u : c1 & 7u;
 				const uint64_t cols = (0xffull >> (7u - ch)) & (0xffull << cl0);
-				uint64_t* t = (uint64_t*)(dmarks + ((size_t)tr * tcols + tc) * 2u);
-				uint32_t& vwd = dvalid[tr * vw + (tc >> 5)];
+				uint64_t* t = (uint64_t*)(dmarks + ((size_t)tr * dtcols + tc) * 2u);
+				uint32_t& vwd = dvalid[tr * dvw + (tc >> 5)];
 				const uint32_t vb = 1u << (tc & 31u);
 				*t = (vwd & vb ? *t : 0ull) | rows * cols;
 				vwd |= vb;
@@ -337,6 +377,7 @@ k_sw_bt(BtArgs A) {
 	};
 	int32_t nal = 0;
 	bool first = true;
+	BTC(12);
 	// FLAT (local mode): the candidate loop and the walks run as ONE loop: an
 	// iteration either filters a candidate or takes one walk step, so a lane
 	// never waits for the longest walk of its wave at every candidate (nested
@@ -437,7 +478,7 @@ k_sw_bt(BtArgs A) {
 			if(wmark && !bottom_bar) {
 				// reportedThrough (aligner_swsse_ee_u8.cpp:1331-1336, 1556)
 				tile_get(row, col);
-				const uint64_t bt = tbit(row, col);
+				const uint64_t bt = rbit(row, col);
 				if(tbits & bt) { w.ok = false; ended = true; }
 				else { tbits |= bt; tdirty = true; }
 			}
@@ -633,6 +674,25 @@ k_sw_bt(BtArgs A) {
 	}
 	A.naln[p] = nal;
 }
+
+#ifdef BT2G_BT_PROF
+// profiling build: counters since the last call (then cleared); out[15] is the
+// wave-divergence sum described above
+extern "C" int bt2g_bt_prof_read(unsigned long long* out) {
+	unsigned long long h[16];
+	static unsigned int w[1u << 16];
+	if(hipMemcpyFromSymbol(h, HIP_SYMBOL(g_bt_prof), sizeof(h)) != hipSuccess) return -1;
+	if(hipMemcpyFromSymbol(w, HIP_SYMBOL(g_bt_wave_max), sizeof(w)) != hipSuccess) return -1;
+	h[15] = 0;
+	for(uint32_t i = 0; i < (1u << 16); i++) h[15] += 64ull * w[i];
+	for(int i = 0; i < 16; i++) out[i] = h[i];
+	const unsigned long long z[16] = {0};
+	(void)hipMemcpyToSymbol(HIP_SYMBOL(g_bt_prof), z, sizeof(z));
+	static const unsigned int zw[1u << 16] = {0};
+	(void)hipMemcpyToSymbol(HIP_SYMBOL(g_bt_wave_max), zw, sizeof(zw));
+	return 0;
+}
+#endif
 
 void launch_sw_bt(int kind, const BtArgs& a, hipStream_t st) {
 	if(a.nprob == 0) return;

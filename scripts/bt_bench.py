@@ -80,6 +80,19 @@ def run():
 
 run()
 torch.cuda.synchronize()
+prof = getattr(bt2g.lib(), "bt2g_bt_prof_read", None) if "prof" in bt2g.LIB_PATH else None
+if prof is not None:
+    # profiling build (make -C bowtie2-server_amd exp V=btprof FLAGS=-DBT2G_BT_PROF=1): work counters of one launch
+    cnt = (C.c_ulonglong * 16)()
+    prof(cnt)
+    run()
+    torch.cuda.synchronize()
+    prof(cnt)
+    names = ["walks", "steps", "colhit16_blocks", "escan_rounds", "candidates", "dom_tests", "replays", "hget",
+             "chunk_reloads", "tile_loads", "tile_writebacks", "colhit8_blocks", "dps_walked", "", "", "wave_steps"]
+    d = {k: int(v) for k, v in zip(names, cnt) if k}
+    d["lane_utilization"] = d["steps"] / max(1, d["wave_steps"])
+    print("bt_prof", d, flush=True)
 eng.reset_stats()
 eng.set_profiling(True)
 for _ in range(a.iters):

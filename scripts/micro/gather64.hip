@@ -27,7 +27,10 @@ __global__ void __launch_bounds__(256) k_indep(const u32x4* __restrict__ t, uint
 	}
 	out[gid] = acc;
 }
-// dependent chain: next side index from the loaded data (pointer chase)
+// dependent chain: next side index from the loaded data (pointer chase).  The
+// lane id enters every step's address, and the table holds distinct words
+// (k_fill): with a constant table the loaded words cancelled and every lane
+// chased the same line, i.e. the "chain" rows measured a cache hit.
 __global__ void __launch_bounds__(256) k_chain(const u32x4* __restrict__ t, uint32_t nside, uint32_t iters,
                                                uint32_t* out) {
 	uint32_t gid = blockIdx.x * blockDim.x + threadIdx.x;
@@ -35,9 +38,13 @@ __global__ void __launch_bounds__(256) k_chain(const u32x4* __restrict__ t, uint
 	for(uint32_t it = 0; it < iters; it++) {
 		u32x4 a = t[(size_t)s * 4], b = t[(size_t)s * 4 + 1], c = t[(size_t)s * 4 + 2], d = t[(size_t)s * 4 + 3];
 		acc += a.x ^ b.y ^ c.z ^ d.w;
-		s = hash(acc + it) % nside;
+		s = hash(acc ^ (gid * 0x9e3779b9u) ^ it) % nside;
 	}
 	out[gid] = acc;
+}
+__global__ void k_fill(uint32_t* t, size_t n) {
+	for(size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < n; i += (size_t)gridDim.x * blockDim.x)
+		t[i] = hash((uint32_t)i * 2654435761u + 12345u);
 }
 int main() {
 	const size_t bytes = 2ull << 30;   // 2 GiB table
@@ -45,7 +52,8 @@ int main() {
 	u32x4* t;
 	uint32_t* o;
 	(void)hipMalloc(&t, bytes);
-	(void)hipMemset(t, 1, bytes);
+	hipLaunchKernelGGL(k_fill, dim3(4096), dim3(256), 0, 0, (uint32_t*)t, bytes / 4);
+	(void)hipDeviceSynchronize();
 	(void)hipMalloc(&o, 64u << 20);
 	hipEvent_t e0, e1;
 	(void)hipEventCreate(&e0); (void)hipEventCreate(&e1);

@@ -8,7 +8,7 @@
 
 thread_local uint3v threadIdx, blockIdx;
 #ifdef BT2G_BT_COUNT
-unsigned long long bt_counts[8];
+unsigned long long bt_counts[16];
 extern "C" unsigned long long* bt_emul_counts() { return bt_counts; }
 #endif
 
@@ -23,8 +23,9 @@ extern "C" int bt_emul_run(int kind, const bt2g_sw_problem* probs, uint32_t npro
 	a.windows = windows; a.ref_codes = nullptr; a.ref_starts = nullptr; a.rects = rects;
 	a.res = res; a.cands = cands; a.cap = cap; a.plane = plane; a.slot = slot; a.cstride = cstride; a.pcols = maxcol; a.use_mask = plane_top != 1 && cstride <= 256u;
 	a.plane_top = plane_top;
+	a.rwords = sw_bt_rcols(maxrow, maxcol); a.rrows = sw_bt_rrows(maxrow);
 	a.mwords = sw_bt_tcols(maxcol); a.mrows = sw_bt_trows(maxrow); a.mslot = sw_bt_mslot(maxrow, maxcol, local != 0);
-	a.mdom = local ? sw_bt_mslot(maxrow, maxcol, false) : 0u;
+	a.mdom = local ? sw_bt_mdom(maxrow, maxcol) : 0u;
 	// garbage-filled scratch: the kernel must not rely on zeroed memory
 	std::vector<uint32_t> marks(a.mslot * nprob + 4, 0xdeadbeefu);
 	a.marks = marks.data();
