@@ -128,12 +128,14 @@ struct BtArgs {
 };
 // kind: 0 u8 score plane, 1 u16 score plane
 void launch_sw_bt(int kind, const BtArgs& a, hipStream_t st);
+
 // backtrace mark scratch per problem of <= rows x cols (sw_backtrace.hip):
-// reportedThrough in 64-bit tiles of 16 rows x 4 diagonals (a diagonal run
-// stays in one tile for up to 16 steps) + one valid bit per tile; dom (local
-// mode's dominated-candidate squares): 8x8-cell tiles + valid bits.
-inline uint32_t sw_bt_rcols(uint32_t rows, uint32_t cols) { return (cols + rows + 3u) / 4u; }
-inline uint32_t sw_bt_rrows(uint32_t rows) { return (rows + 15u) / 16u; }
+// reportedThrough in 8x8-cell bit tiles (2 words each) + one valid bit per
+// tile; dom (local mode's dominated-candidate squares): a second set of the
+// same shape.  (16-row x 4-diagonal reportedThrough tiles: 9 % more tile
+// loads, the short failing walks are not diagonal runs.)
+inline uint32_t sw_bt_rcols(uint32_t rows, uint32_t cols) { (void)rows; return (cols + 7u) / 8u; }
+inline uint32_t sw_bt_rrows(uint32_t rows) { return (rows + 7u) / 8u; }
 inline uint32_t sw_bt_tcols(uint32_t cols) { return (cols + 7u) / 8u; }
 inline uint32_t sw_bt_trows(uint32_t rows) { return (rows + 7u) / 8u; }
 inline uint64_t sw_bt_tiles_words(uint64_t tr, uint64_t tc) {

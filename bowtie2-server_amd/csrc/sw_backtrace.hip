@@ -109,7 +109,9 @@ __device__ unsigned int g_bt_wave_max[1u << 16];
 #ifndef BT2G_BT_EE_STEPS
 #define BT2G_BT_EE_STEPS 0xffffffffu   // end-to-end: a whole walk per iteration (4, 8, 16: same 32 ms)
 #endif
-template <int KIND, bool FLAT>
+// LOCAL: the alignment mode, compile-time (each mode's kernel keeps only its
+// own filters and moves); FLAT: the loop shape, flat for local (see below)
+template <int KIND, bool LOCAL, bool FLAT = LOCAL>
 __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(BT2G_BT_WAVES)))
 k_sw_bt(BtArgs A) {
 	const uint32_t p = blockIdx.x * 64u + threadIdx.x;
@@ -130,7 +132,7 @@ k_sw_bt(BtArgs A) {
 	if((uint32_t)R.ncand > A.cap) { A.naln[p] = -5; return; }   // truncated list: not the reference's
 	const bt2g_sw_problem P = A.probs[p];
 	const uint32_t nrow = A.lens[P.read], ncol = P.ncol;
-	const bool local = A.local != 0;
+	constexpr bool local = LOCAL;
 	const int variant = local ? (R.u8succ ? 2 : 3) : (R.u8succ ? 0 : 1);
 	Plane<KIND> pl;
 	pl.ncol = ncol;
@@ -220,12 +222,11 @@ k_sw_bt(BtArgs A) {
 	}
 	int32_t triml = 0, corel = 0, corer = 0x7fffffff;
 	if(A.rects) { const bt2g_sw_rect rc = A.rects[p]; triml = rc.triml; corel = rc.corel; corer = rc.corer; }
-	// reportedThrough: bit tiles of 16 rows x 4 diagonals (one u64 each; a
-	// walk is mostly a diagonal run, which stays in a tile for up to 16 steps
-	// -- 8x8 cell tiles changed every ~4), one tile cached in registers at a
-	// time.  A tile is valid once written back (one valid bit per tile, cleared
-	// here; the current valid word is cached in a register too), so nothing
-	// else is ever cleared.  (Valid bits in LDS instead: measured slower.)
+	// reportedThrough: 8x8-cell bit tiles (one u64 each), one tile cached in
+	// registers at a time (a walk stays in a tile for several steps); a tile is
+	// valid once written back (one valid bit per tile, cleared here; the current
+	// valid word is cached in a register too), so nothing else is ever cleared.
+	// (Valid bits in LDS instead: measured slower.)
 	uint32_t* marks = A.marks + (size_t)p * A.mslot;
 	const uint32_t tcols = A.rwords, trows = A.rrows, vw = (tcols + 31u) / 32u;
 	uint32_t* valid = marks + (size_t)trows * tcols * 2u;
@@ -244,9 +245,8 @@ k_sw_bt(BtArgs A) {
 		}
 		return vval;
 	};
-	const uint32_t dg0 = nrow - 1u;            // diagonal index of (r, c): c - r + nrow - 1 >= 0
 	auto tile_get = [&](uint32_t r, uint32_t c) {
-		const uint32_t tr = r >> 4, tc = (c + dg0 - r) >> 2;
+		const uint32_t tr = r >> 3, tc = c >> 3;
 		if(tr == ttr && tc == ttc) return;
 		if(tdirty) {
 			BTC(10);
@@ -261,8 +261,8 @@ k_sw_bt(BtArgs A) {
 		const bool v = (vword(tr * vw + (tc >> 5)) >> (tc & 31u)) & 1u;
 		tbits = v ? *(const uint64_t*)(marks + ((size_t)tr * tcols + tc) * 2u) : 0ull;
 	};
-	auto rbit = [&](uint32_t r, uint32_t c) -> uint64_t { return 1ull << (((r & 15u) << 2) | ((c + dg0 - r) & 3u)); };
 	auto tbit = [](uint32_t r, uint32_t c) -> uint64_t { return 1ull << (((r & 7u) << 3) | (c & 7u)); };
+	auto rbit = tbit;
 	auto marked = [&](uint32_t r, uint32_t c) -> bool {
 		tile_get(r, c);
 		return (tbits & rbit(r, c)) != 0;
@@ -697,14 +697,9 @@ extern "C" int bt2g_bt_prof_read(unsigned long long* out) {
 void launch_sw_bt(int kind, const BtArgs& a, hipStream_t st) {
 	if(a.nprob == 0) return;
 	const dim3 grid((a.nprob + 63u) / 64u), block(64);
-#ifdef BT2G_BT_FLAT_ALL
-	const bool flat = true;                 // timing experiments only (end-to-end and mate DPs: slower)
-#else
-	const bool flat = a.local != 0;
-#endif
-	if(flat) {
-		if(kind == 0) hipLaunchKernelGGL((k_sw_bt<0, true>), grid, block, 0, st, a);
-		else hipLaunchKernelGGL((k_sw_bt<1, true>), grid, block, 0, st, a);
+	if(a.local) {
+		// local fills leave a u16 plane
+		hipLaunchKernelGGL((k_sw_bt<1, true>), grid, block, 0, st, a);
 	} else {
 		if(kind == 0) hipLaunchKernelGGL((k_sw_bt<0, false>), grid, block, 0, st, a);
 		else hipLaunchKernelGGL((k_sw_bt<1, false>), grid, block, 0, st, a);
