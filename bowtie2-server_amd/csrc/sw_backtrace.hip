@@ -98,6 +98,7 @@ extern unsigned long long bt_counts[16];
 #elif defined(BT2G_BT_PROF)
 __device__ unsigned long long g_bt_prof[16];
 __device__ unsigned int g_bt_wave_max[1u << 16];
+__device__ unsigned long long g_bt_wave_t0[1u << 16], g_bt_wave_t1[1u << 16];   // wall_clock64 ticks
 #define BTC(i) (pc[i]++)
 #else
 #define BTC(i) ((void)0)
@@ -118,12 +119,14 @@ k_sw_bt(BtArgs A) {
 	if(p >= A.nprob) return;
 #ifdef BT2G_BT_PROF
 	uint32_t pc[13] = {0};
+	if(threadIdx.x == 0) g_bt_wave_t0[blockIdx.x & 0xffffu] = wall_clock64();
 	struct Flush {
 		uint32_t* pc;
 		__device__ ~Flush() {
 			for(int i = 0; i < 13; i++)
 				if(pc[i]) atomicAdd(&g_bt_prof[i], (unsigned long long)pc[i]);
 			atomicMax(&g_bt_wave_max[blockIdx.x & 0xffffu], pc[1]);
+			atomicMax(&g_bt_wave_t1[blockIdx.x & 0xffffu], (unsigned long long)wall_clock64());
 		}
 	} flush_{pc};
 #endif
@@ -258,8 +261,11 @@ k_sw_bt(BtArgs A) {
 		ttr = tr;
 		ttc = tc;
 		BTC(9);
+		// the tile is loaded with (not after) its valid word: one round trip; an
+		// invalid tile's stale bits are dropped
+		const uint64_t tl = *(const uint64_t*)(marks + ((size_t)tr * tcols + tc) * 2u);
 		const bool v = (vword(tr * vw + (tc >> 5)) >> (tc & 31u)) & 1u;
-		tbits = v ? *(const uint64_t*)(marks + ((size_t)tr * tcols + tc) * 2u) : 0ull;
+		tbits = v ? tl : 0ull;
 	};
 	auto tbit = [](uint32_t r, uint32_t c) -> uint64_t { return 1ull << (((r & 7u) << 3) | (c & 7u)); };
 	auto rbit = tbit;
@@ -322,9 +328,16 @@ k_sw_bt(BtArgs A) {
 			ch2 = cc0 + 2u < A.pcols ? qp[2] : z;
 			ch3 = cc0 + 3u < A.pcols ? qp[3] : z;
 			if(pl.mask) {
-				const uint32_t m0 = pl.mask[cc0], m1 = cc0 + 1u < A.pcols ? pl.mask[cc0 + 1u] : 0u;
-				const uint32_t m2 = cc0 + 2u < A.pcols ? pl.mask[cc0 + 2u] : 0u;
-				const uint32_t m3 = cc0 + 3u < A.pcols ? pl.mask[cc0 + 3u] : 0u;
+				// the four columns' block masks from one or two aligned 8-B loads (not four)
+				const uint32_t ma = cc0 & ~3u, sh = cc0 & 3u;
+				const uint2 lo = *(const uint2*)(pl.mask + ma);
+				const uint2 hi = sh && ma + 4u < A.pcols ? *(const uint2*)(pl.mask + ma + 4u) : make_uint2(0u, 0u);
+				const uint32_t mw[4] = {lo.x, lo.y, hi.x, hi.y};   // two masks per word
+				auto mk = [&](uint32_t k) -> uint32_t {
+					const uint32_t j = sh + k;                     // column cc0 + k = ma + j
+					return cc0 + k < A.pcols ? (mw[j >> 1] >> ((j & 1u) * 16u)) & 0xffffu : 0u;
+				};
+				const uint32_t m0 = mk(0), m1 = mk(1), m2 = mk(2), m3 = mk(3);
 				if(!((m0 >> b) & 1u)) ch0 = z;
 				if(!((m1 >> b) & 1u)) ch1 = z;
 				if(!((m2 >> b) & 1u)) ch2 = z;
@@ -678,6 +691,16 @@ k_sw_bt(BtArgs A) {
 #ifdef BT2G_BT_PROF
 // profiling build: counters since the last call (then cleared); out[15] is the
 // wave-divergence sum described above
+// per-wave start / end (wall_clock64 ticks, 100 MHz) of the last launch, for
+// waves 0..n-1 (n <= 65536)
+extern "C" int bt2g_bt_prof_waves(unsigned long long* t0, unsigned long long* t1, unsigned int* steps, uint32_t n) {
+	if(n > (1u << 16)) return -1;
+	if(hipMemcpyFromSymbol(t0, HIP_SYMBOL(g_bt_wave_t0), sizeof(unsigned long long) * n) != hipSuccess) return -1;
+	if(hipMemcpyFromSymbol(t1, HIP_SYMBOL(g_bt_wave_t1), sizeof(unsigned long long) * n) != hipSuccess) return -1;
+	if(hipMemcpyFromSymbol(steps, HIP_SYMBOL(g_bt_wave_max), sizeof(unsigned int) * n) != hipSuccess) return -1;
+	return 0;
+}
+
 extern "C" int bt2g_bt_prof_read(unsigned long long* out) {
 	unsigned long long h[16];
 	static unsigned int w[1u << 16];
@@ -690,6 +713,8 @@ extern "C" int bt2g_bt_prof_read(unsigned long long* out) {
 	(void)hipMemcpyToSymbol(HIP_SYMBOL(g_bt_prof), z, sizeof(z));
 	static const unsigned int zw[1u << 16] = {0};
 	(void)hipMemcpyToSymbol(HIP_SYMBOL(g_bt_wave_max), zw, sizeof(zw));
+	static const unsigned long long zt[1u << 16] = {0};
+	(void)hipMemcpyToSymbol(HIP_SYMBOL(g_bt_wave_t1), zt, sizeof(zt));
 	return 0;
 }
 #endif

@@ -87,12 +87,27 @@ if prof is not None:
     prof(cnt)
     run()
     torch.cuda.synchronize()
+    nw = min((n + 63) // 64, 1 << 16)
+    t0 = np.zeros(nw, np.uint64); t1 = np.zeros(nw, np.uint64); ws = np.zeros(nw, np.uint32)
+    wok = bt2g.lib().bt2g_bt_prof_waves(t0.ctypes.data_as(C.c_void_p), t1.ctypes.data_as(C.c_void_p),
+                                        ws.ctypes.data_as(C.c_void_p), C.c_uint32(nw)) == 0
     prof(cnt)
     names = ["walks", "steps", "colhit16_blocks", "escan_rounds", "candidates", "dom_tests", "replays", "hget",
              "chunk_reloads", "tile_loads", "tile_writebacks", "colhit8_blocks", "dps_walked", "", "", "wave_steps"]
     d = {k: int(v) for k, v in zip(names, cnt) if k}
     d["lane_utilization"] = d["steps"] / max(1, d["wave_steps"])
     print("bt_prof", d, flush=True)
+    if wok:
+        ok = t1 > 0
+        t0, t1, ws = t0[ok].astype(np.float64), t1[ok].astype(np.float64), ws[ok]
+        dur = (t1 - t0) / 100.0                      # us (100 MHz)
+        span = (t1.max() - t0.min()) / 100.0
+        q = np.percentile(dur, [50, 90, 99, 100])
+        print(f"bt_waves n={ok.sum()} span {span:.0f} us; wave duration us p50 {q[0]:.0f} p90 {q[1]:.0f} "
+              f"p99 {q[2]:.0f} max {q[3]:.0f}; sum {dur.sum()/1e6:.2f} wave-s; us per wave-step "
+              f"{(dur / np.maximum(ws, 1)).mean():.2f}; concurrent waves ~{dur.sum() / max(span, 1):.0f}", flush=True)
+        late = t0 > t0.min() + 0.5 * (t1.max() - t0.min())
+        print(f"bt_waves started in the 2nd half of the span: {late.sum()}, their steps p50 {np.median(ws[late]) if late.any() else 0}", flush=True)
 eng.reset_stats()
 eng.set_profiling(True)
 for _ in range(a.iters):

@@ -17,6 +17,8 @@
 struct dim3 { uint32_t x = 1, y = 1, z = 1; dim3(uint32_t a = 1, uint32_t b = 1, uint32_t c = 1) : x(a), y(b), z(c) {} };
 struct uint4 { uint32_t x, y, z, w; };
 struct int2 { int32_t x, y; };
+struct uint2 { uint32_t x, y; };
+inline uint2 make_uint2(uint32_t a, uint32_t b) { return uint2{a, b}; }
 struct uint3v { uint32_t x = 0, y = 0, z = 0; };
 inline uint4 make_uint4(uint32_t a, uint32_t b, uint32_t c, uint32_t d) { return uint4{a, b, c, d}; }
 inline int2 make_int2(int32_t a, int32_t b) { return int2{a, b}; }
