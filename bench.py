@@ -590,7 +590,7 @@ def cpu_baseline(idx, reads, quals, pipe, sample, threads, base=None):
     return dt, ref, mate, secs
 
 
-def server_baseline(base, reads, quals, pol, sample, threads, workers, args_srv, log_dir):
+def server_baseline(base, reads, quals, pol, sample, threads, workers, args_srv, log_dir, dropin_binary=None):
     """The north-star comparison on the reference's real schedule (BASELINE.md
     section 3): the stock reference server (oracle/_ref/bowtie2-align-server-s,
     -p <usable cores>) and the same server with its seams bound to the engines
@@ -607,14 +607,16 @@ def server_baseline(base, reads, quals, pol, sample, threads, workers, args_srv,
         chunks = rs.write_fastq_chunks(log_dir, reads[:n], quals[:n])
     out, sams = {}, {}
     for tag, binary, th in (("stock", rs.SERVER, threads),
-                            ("dropin", os.path.join(rs.REF_DIR, "bowtie2-align-server-gpu"), workers)):
+                            ("dropin", dropin_binary or os.path.join(rs.REF_DIR, "bowtie2-align-server-gpu"),
+                             workers)):
         stats = os.path.join(log_dir, f"stats_{tag}.json")
         env = {"BT2G_INDEX": base, "BT2G_ADAPTER_STATS": stats, "BT2G_DEVICE": "0"}
         with rs.Server(base, threads=th, args=args_srv, binary=binary, env=env,
                        log_path=os.path.join(log_dir, f"server_{tag}.log")) as srv:
             dt, outs = srv.run(chunks, k=8)
         sams[tag] = rs.sorted_records(outs)
-        out[tag] = {"rate": n / dt, "seconds": dt, "threads": th, "records": len(sams[tag])}
+        out[tag] = {"rate": n / dt, "seconds": dt, "threads": th, "records": len(sams[tag]),
+                    "server_cpu_s": srv.last_cpu_s, "server_cores_busy": srv.last_cpu_s / dt}
         time.sleep(0.5)
         if os.path.exists(stats):
             import json as _j
@@ -791,7 +793,7 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--server-sample", type=int, default=200_000,
                     help="reads (pairs) timed through the stock reference server and the drop-in server (0: skip)")
-    ap.add_argument("--server-workers", type=int, default=512, help="drop-in server worker threads (-p)")
+    ap.add_argument("--server-workers", type=int, default=1024, help="drop-in server worker threads (-p)")
     ap.add_argument("--index-cache", default="auto",
                     help="reuse/write the built index at this base path ('auto': under $TMPDIR keyed by the "
                          "genome model and size; '': always build)")
@@ -1004,7 +1006,7 @@ def main():
                 srv_args = ["--local"] if args.mode == "local" else []
                 if args.preset == "very-sensitive":
                     srv_args.append("--very-sensitive-local" if args.mode == "local" else "--very-sensitive")
-                srv = server_baseline(ref["index_base"], reads_np, quals_np, pol,
+                srv = server_baseline(ref["index_base"], reads_np, quals_np, pipe.pol,
                                       min(args.server_sample, sample), threads, args.server_workers, srv_args,
                                       tempfile.mkdtemp(prefix="bt2srv_"))
                 cpu["reference_server"] = {"value": srv["stock"]["rate"], "unit": cpu["unit"], "cores": threads,

@@ -110,3 +110,29 @@ def test_ref_chain_compare_cpu():
     gpu["sweep"][7, 0] += 1
     c = compare(ref, gpu)
     assert c["offset_mismatch"] == 1 and c["frame_mismatch"] == 1 and c["exact_sweep_mismatch"] == 1, c
+
+
+def test_server_baseline_cpu():
+    """bench.server_baseline end to end on CPU: the stock reference server and the
+    drop-in binding over the CPU stand-in (bowtie2-align-server-stub) on 300
+    reads of a small synthetic index; identical sorted SAM, both rates set."""
+    import os
+    import tempfile
+    import pytest
+    import bench
+    import bt2_index as bi
+    import synth
+    from oracle import ref_server as rs
+    stub = os.path.join(rs.REF_DIR, "bowtie2-align-server-stub")
+    if not (os.path.exists(rs.SERVER) and os.path.exists(stub)):
+        pytest.skip("oracle/_ref servers not built")
+    g = synth.genome(7, 100_000, n_repeats=10, rep_len=1500, n_copies=3, n_runs=2)
+    idx = bi.build_index([g], names=[b"chr"])
+    d = tempfile.mkdtemp()
+    base = os.path.join(d, "g")
+    bi.write_index(base, idx)
+    r, q = bench.make_reads(idx.ref_codes, 300, 150, 5)
+    out = bench.server_baseline(base, r, q, bench.Policy("ee", 150), 300, 2, 8, [], d, dropin_binary=stub)
+    assert out["sam_identical"] and out["sam_records_differing"] == 0
+    assert out["stock"]["records"] == 300 and out["dropin"]["rate"] > 0
+    assert out["dropin"]["engine_calls"]["exact_sweep"][0] > 0
