@@ -907,6 +907,26 @@ def main():
     sw_gcups = sw_cells / (per_launch.get(4, float("nan")) / 1e3) / 1e9
     for k in per_launch:
         log(f"[rank {rank}] {names_k[k]:12s} {per_launch[k]:8.3f} ms/launch")
+    mmprof = getattr(bt2g.lib(), "bt2g_mm_prof_waves", None) if "prof" in bt2g.LIB_PATH else None
+    if mmprof is not None:
+        # profiling build of the 1-mm far kernels (-DBT2G_MM_PROF): waves of the last launch
+        import ctypes
+        t0 = np.zeros(2 << 16, np.uint64); t1 = np.zeros(2 << 16, np.uint64); ws = np.zeros(2 << 16, np.uint32)
+        if mmprof(t0.ctypes.data_as(ctypes.c_void_p), t1.ctypes.data_as(ctypes.c_void_p),
+                  ws.ctypes.data_as(ctypes.c_void_p)) == 0:
+            for h, nm in ((0, "far<true>"), (1, "far<false>")):
+                a0, a1, st_ = t0[h << 16:(h + 1) << 16], t1[h << 16:(h + 1) << 16], ws[h << 16:(h + 1) << 16]
+                ok = a1 > 0
+                if not ok.any():
+                    continue
+                a0, a1, st_ = a0[ok].astype(np.float64), a1[ok].astype(np.float64), st_[ok]
+                dur = (a1 - a0) / 100.0
+                q = np.percentile(dur, [50, 90, 99, 100])
+                qs = np.percentile(st_, [50, 90, 99, 100])
+                log(f"[rank {rank}] mm_prof {nm}: {ok.sum()} waves, span {(a1.max() - a0.min()) / 100:.0f} us, "
+                    f"start spread {(a0.max() - a0.min()) / 100:.0f} us; wave us p50/90/99/max "
+                    f"{q[0]:.0f}/{q[1]:.0f}/{q[2]:.0f}/{q[3]:.0f}; max-lane LF steps p50/90/99/max "
+                    f"{qs[0]:.0f}/{qs[1]:.0f}/{qs[2]:.0f}/{qs[3]:.0f}")
     prof = getattr(bt2g.lib(), "bt2g_bt_prof_read", None) if "prof" in bt2g.LIB_PATH else None
     if prof is not None and stats[5][0]:
         # profiling build of the backtrace (scripts/bt_bench.py): counters per launch

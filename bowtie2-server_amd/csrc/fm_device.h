@@ -60,7 +60,10 @@ struct SideData {
 
 __device__ __forceinline__ void load_side(const DevEbwt& e, uint32_t side, SideData& s) {
 	typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
-	const u32x4* p = reinterpret_cast<const u32x4*>(e.sides + (size_t)side * 64u);
+	// global address space, stated: through a DevEbwt picked at run time the
+	// pointer is generic, and flat loads make every later wait a full drain
+	typedef const __attribute__((address_space(1))) u32x4 gu32x4;
+	const gu32x4* p = (const gu32x4*)(e.sides + (size_t)side * 64u);
 	u32x4 a = p[0], b = p[1], c = p[2], d = p[3];
 	s.w[0] = a.x; s.w[1] = a.y; s.w[2] = a.z; s.w[3] = a.w;
 	s.w[4] = b.x; s.w[5] = b.y; s.w[6] = b.z; s.w[7] = b.w;
@@ -228,7 +231,7 @@ struct ReadWin {
 		if(aa != a) {
 			if(aa < (uint64_t)lo || aa + 16u > (uint64_t)hi) return *ptr;
 			a = aa;
-			w = *(const uint4*)aa;
+			w = *(const uint4*)(ptr - (addr & 15u));   // pointer provenance: global, not flat
 		}
 		const uint32_t di = (uint32_t)(addr >> 2) & 3u;
 		const uint32_t d = di == 0 ? w.x : di == 1 ? w.y : di == 2 ? w.z : w.w;

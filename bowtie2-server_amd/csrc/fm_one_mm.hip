@@ -446,6 +446,23 @@ k_one_mm_q(DevEbwt F, DevEbwt B, const uint8_t* __restrict__ reads, const uint8_
 // machine k_one_mm_q, which also walks branches in place, only runs for the
 // rare items that meet a full queue: they are handed over whole, and their
 // queued branches are dropped by the branch kernel via slot_flag).
+#ifdef BT2G_MM_PROF
+// profiling build: per far-kernel wave, first start / last end (wall_clock64)
+// and the largest per-lane LF-step count, [EBWTFW ? 0 : 65536] + wave index
+__device__ unsigned long long g_mm_t0[2u << 16], g_mm_t1[2u << 16];
+__device__ unsigned int g_mm_steps[2u << 16];
+extern "C" int bt2g_mm_prof_waves(unsigned long long* t0, unsigned long long* t1, unsigned int* steps) {
+	if(hipMemcpyFromSymbol(t0, HIP_SYMBOL(g_mm_t0), sizeof(unsigned long long) * (2u << 16)) != hipSuccess) return -1;
+	if(hipMemcpyFromSymbol(t1, HIP_SYMBOL(g_mm_t1), sizeof(unsigned long long) * (2u << 16)) != hipSuccess) return -1;
+	if(hipMemcpyFromSymbol(steps, HIP_SYMBOL(g_mm_steps), sizeof(unsigned int) * (2u << 16)) != hipSuccess) return -1;
+	static unsigned long long z[2u << 16];
+	static unsigned int zs[2u << 16];
+	(void)hipMemcpyToSymbol(HIP_SYMBOL(g_mm_t0), z, sizeof(z));
+	(void)hipMemcpyToSymbol(HIP_SYMBOL(g_mm_t1), z, sizeof(z));
+	(void)hipMemcpyToSymbol(HIP_SYMBOL(g_mm_steps), zs, sizeof(zs));
+	return 0;
+}
+#endif
 #ifndef BT2G_MM_FAR_WAVES
 #define BT2G_MM_FAR_WAVES 3      // 4 and 5 spill (84 / 152 B per lane)
 #endif
@@ -462,6 +479,19 @@ k_one_mm_far(DevEbwt F, DevEbwt B, const uint8_t* __restrict__ reads, const uint
              uint32_t* __restrict__ slot_flag) {
 	const uint32_t qi = blockIdx.x * blockDim.x + threadIdx.x;
 	if(qi >= *nitems_p) return;
+#ifdef BT2G_MM_PROF
+	const uint32_t wslot = (EBWTFW ? 0u : 65536u) + ((qi >> 6) & 0xffffu);
+	if((qi & 63u) == 0) g_mm_t0[wslot] = wall_clock64();
+	uint32_t prof_ops = 0;
+	struct Flush {
+		uint32_t w;
+		uint32_t* ops;
+		__device__ ~Flush() {
+			atomicMax(&g_mm_t1[w], (unsigned long long)wall_clock64());
+			atomicMax(&g_mm_steps[w], *ops);
+		}
+	} flush_{wslot, &prof_ops};
+#endif
 	constexpr bool ebwtfw = EBWTFW;
 	const DevEbwt& E = EBWTFW ? F : B;
 	const uint32_t item = items[qi];
@@ -494,6 +524,9 @@ k_one_mm_far(DevEbwt F, DevEbwt B, const uint8_t* __restrict__ reads, const uint
 		if(rdc > 3 && nceil == 0) break;
 		if(bot - top <= 1 && top == E.zoff) break;                // mapLF1 would hit '$'
 		ops++;
+#ifdef BT2G_MM_PROF
+		prof_ops = ops;
+#endif
 		uint32_t ot[4], ob[4], otp[4], obp[4];
 		int clo = 0, chi = 3;
 		bool match;

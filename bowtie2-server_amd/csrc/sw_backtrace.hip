@@ -241,16 +241,25 @@ k_sw_bt(BtArgs A) {
 	bool vdirty = false;
 	auto vword = [&](uint32_t i) -> uint32_t& {
 		if(i != vidx) {
+			// load before the write-back: a wave's loads wait for every older
+			// vector-memory op, stores included (vmcnt is in order)
+			const uint32_t nv = valid[i];
 			if(vdirty) valid[vidx] = vval;
 			vdirty = false;
 			vidx = i;
-			vval = valid[i];
+			vval = nv;
 		}
 		return vval;
 	};
 	auto tile_get = [&](uint32_t r, uint32_t c) {
 		const uint32_t tr = r >> 3, tc = c >> 3;
 		if(tr == ttr && tc == ttc) return;
+		BTC(9);
+		// the new tile is loaded first, with (not after) its valid word, and the
+		// old one written back after: one round trip, not a store acknowledgement
+		// and then a load (vmcnt counts loads and stores in order); an invalid
+		// tile's stale bits are dropped
+		const uint64_t tl = *(const uint64_t*)(marks + ((size_t)tr * tcols + tc) * 2u);
 		if(tdirty) {
 			BTC(10);
 			*(uint64_t*)(marks + ((size_t)ttr * tcols + ttc) * 2u) = tbits;
@@ -260,10 +269,6 @@ k_sw_bt(BtArgs A) {
 		}
 		ttr = tr;
 		ttc = tc;
-		BTC(9);
-		// the tile is loaded with (not after) its valid word: one round trip; an
-		// invalid tile's stale bits are dropped
-		const uint64_t tl = *(const uint64_t*)(marks + ((size_t)tr * tcols + tc) * 2u);
 		const bool v = (vword(tr * vw + (tc >> 5)) >> (tc & 31u)) & 1u;
 		tbits = v ? tl : 0ull;
 	};
@@ -285,7 +290,9 @@ k_sw_bt(BtArgs A) {
 		if(aa != W.a) {
 			if(aa < (uint64_t)lo || aa + 16u > (uint64_t)hi) return *ptr;
 			W.a = aa;
-			W.w = *(const uint4*)aa;
+			// through the kernel-argument pointer (global address space), not an
+			// integer cast: a flat load would make every later wait a full drain
+			W.w = *(const uint4*)(ptr - (addr & 15u));
 		}
 		const uint32_t di = (uint32_t)(addr >> 2) & 3u;
 		const uint32_t d = di == 0 ? W.w.x : di == 1 ? W.w.y : di == 2 ? W.w.z : W.w.w;

@@ -345,7 +345,7 @@ k_sw_sys(const bt2g_sw_problem* __restrict__ probs, uint32_t nprob, const uint8_
 				const int64_t c = (int64_t)c0 + (int64_t)u * S;
 #pragma unroll
 				for(int x = 0; x < 2; x++)
-					v[x][u] = (c >= lo[x] && c < hi[x]) ? src[x][c]
+					v[x][u] = (c >= lo[x] && c < hi[x]) ? ((const __attribute__((address_space(1))) uint8_t*)src[x])[c]
 					        : (c < (int64_t)h[x].ncol + (LOCAL ? 1 : 0) ? 0x100u : 0x200u);
 			}
 #pragma unroll

@@ -27,7 +27,7 @@ struct Win16 {
 		if(aa != a) {
 			if(aa < (uint64_t)lo || aa + 16u > (uint64_t)hi) return *p;
 			a = aa;
-			w = *(const uint4*)aa;
+			w = *(const uint4*)(p - (addr & 15u));     // pointer provenance: global, not flat
 		}
 		const uint32_t di = (uint32_t)(addr >> 2) & 3u;
 		const uint32_t d = di == 0 ? w.x : di == 1 ? w.y : di == 2 ? w.z : w.w;
