@@ -28,8 +28,9 @@
 // Memory: 1M lanes each walking their own problem cannot share caches, so a
 // step must not touch memory: reportedThrough lives in 8x8 bit tiles of which
 // one is held in registers, the read / qualities / reference are read through
-// 4-byte register windows, and the u8 plane through a register copy of 4
-// columns x 16 rows (the plane is stored in 16-row blocks, sw_ee_packed.hip),
+// 16-byte windows and the u8 plane through a copy of 4 columns x 16 rows (the
+// plane is stored in 16-row blocks, sw_ee_packed.hip), both in the lane's
+// region of LDS,
 // so a diagonal run reloads every 4 steps and the later, short walks of a
 // problem (all near its last rows) mostly hit registers.  Edits are written
 // by the first walk (which usually succeeds) and by a replay of any later
@@ -105,7 +106,7 @@ __device__ unsigned long long g_bt_wave_t0[1u << 16], g_bt_wave_t1[1u << 16];   
 #endif
 
 #ifndef BT2G_BT_WAVES
-#define BT2G_BT_WAVES 3
+#define BT2G_BT_WAVES 4      // with the LDS caches: 3 waves 41.3 ms, 4 (12 B/lane spilled) 36.9, 5 (124 B) 43.8
 #endif
 #ifndef BT2G_BT_EE_STEPS
 #define BT2G_BT_EE_STEPS 0xffffffffu   // end-to-end: a whole walk per iteration (4, 8, 16: same 32 ms)
@@ -283,41 +284,47 @@ k_sw_bt(BtArgs A) {
 	// leave [lo, hi) is not loaded (single byte instead).  Reads and
 	// qualities: [buffer start, end of this row's stride); the resident
 	// reference is padded by bt2g_open; explicit windows: their own extent.
-	struct Win { uint64_t a; uint4 w; };
-	Win w_rd{~0ull, make_uint4(0, 0, 0, 0)}, w_q = w_rd, w_rf = w_rd;
-	auto win = [&](Win& W, const uint8_t* ptr, const uint8_t* lo, const uint8_t* hi) -> int {
+	// The window bytes and the u8 plane chunk below live in LDS, 29 dwords per
+	// lane (odd stride: the 64 lanes' regions start in different banks): LDS
+	// reads wait on their own counter, not behind the walk's global loads, and
+	// the 40 VGPRs they took are what kept the kernel at 3 waves/SIMD with
+	// spills (measured: 2 waves 61 ms, 3 waves 48.8 ms, 4 waves + spills 46.6).
+	__shared__ uint32_t s_cache[64u * 29u];
+	uint32_t* const myc = s_cache + threadIdx.x * 29u;
+	uint64_t w_rd = ~0ull, w_q = ~0ull, w_rf = ~0ull;   // address of the window each slot holds
+	auto win = [&](uint64_t& Wa, uint32_t k, const uint8_t* ptr, const uint8_t* lo, const uint8_t* hi) -> int {
 		const uint64_t addr = (uint64_t)ptr, aa = addr & ~15ull;
-		if(aa != W.a) {
+		if(aa != Wa) {
 			if(aa < (uint64_t)lo || aa + 16u > (uint64_t)hi) return *ptr;
-			W.a = aa;
+			Wa = aa;
 			// through the kernel-argument pointer (global address space), not an
 			// integer cast: a flat load would make every later wait a full drain
-			W.w = *(const uint4*)(ptr - (addr & 15u));
+			const uint4 v = *(const uint4*)(ptr - (addr & 15u));
+			uint32_t* d = myc + 16u + 4u * k;
+			d[0] = v.x; d[1] = v.y; d[2] = v.z; d[3] = v.w;
 		}
-		const uint32_t di = (uint32_t)(addr >> 2) & 3u;
-		const uint32_t d = di == 0 ? W.w.x : di == 1 ? W.w.y : di == 2 ? W.w.z : W.w.w;
-		return (int)((d >> ((addr & 3u) * 8u)) & 0xffu);
+		return ((const uint8_t*)(myc + 16u + 4u * k))[addr & 15u];
 	};
 	auto rd_at = [&](uint32_t r) -> int {   // read character of DP row r
-		const int raw = win(w_rd, rd + (fw ? r : nrow - 1 - r), A.reads, rd + A.stride);
+		const int raw = win(w_rd, 0u, rd + (fw ? r : nrow - 1 - r), A.reads, rd + A.stride);
 		return fw ? raw : (raw > 3 ? 4 : 3 - raw);
 	};
 	auto q_at = [&](uint32_t r) -> int {
-		const int q = win(w_q, qu + (fw ? r : nrow - 1 - r), A.quals, qu + A.stride) - 33;
+		const int q = win(w_q, 1u, qu + (fw ? r : nrow - 1 - r), A.quals, qu + A.stride) - 33;
 		return q < 0 ? 0 : (q > 40 ? 40 : q);
 	};
 	const uint8_t* wlo = P.win_off >= 0 ? A.windows + P.win_off : A.ref_codes;
 	const uint8_t* whi = P.win_off >= 0 ? wlo + ncol + 1 : A.ref_codes + rs + rlen + 16u;
 	auto rf_at = [&](uint32_t c) -> int {   // reference mask of column c (aligner_sw.cpp:171-253)
-		if(P.win_off >= 0) return win(w_rf, wlo + c, wlo, whi);
+		if(P.win_off >= 0) return win(w_rf, 2u, wlo + c, wlo, whi);
 		const int64_t o = P.refl + (int64_t)c;
 		if(o < 0 || (uint64_t)o >= rlen) return 16;
-		const int code = win(w_rf, A.ref_codes + rs + (uint64_t)o, wlo, whi);
+		const int code = win(w_rf, 2u, A.ref_codes + rs + (uint64_t)o, wlo, whi);
 		return code > 3 ? 16 : 1 << code;
 	};
-	// H of a cell; the u8 plane goes through a register copy of 4 columns x 16 rows
+	// H of a cell; the u8 plane goes through a copy of 4 columns x 16 rows in
+	// the lane's LDS region (dwords 0..15: column cc0 + u at 4u..4u+3)
 	uint32_t cb = 0xffffffffu, cc0 = 0;
-	uint4 ch0 = make_uint4(0, 0, 0, 0), ch1 = ch0, ch2 = ch0, ch3 = ch0;   // named: no indexable array
 	auto hget = [&](uint32_t r, uint32_t c) -> int32_t {
 		BTC(7);
 		if(KIND != 0) return pl.h(r, c);   // u16 planes: direct (a chunk cache costs occupancy)
@@ -330,10 +337,10 @@ k_sw_bt(BtArgs A) {
 			const uint4* qp = (const uint4*)(slot + ((size_t)b * A.pcols + cc0) * 16u);
 			// chunks and their block masks in one round trip, dead blocks zeroed after
 			const uint4 z = make_uint4(0, 0, 0, 0);
-			ch0 = cc0 < A.pcols ? qp[0] : z;
-			ch1 = cc0 + 1u < A.pcols ? qp[1] : z;
-			ch2 = cc0 + 2u < A.pcols ? qp[2] : z;
-			ch3 = cc0 + 3u < A.pcols ? qp[3] : z;
+			uint4 ch0 = cc0 < A.pcols ? qp[0] : z;
+			uint4 ch1 = cc0 + 1u < A.pcols ? qp[1] : z;
+			uint4 ch2 = cc0 + 2u < A.pcols ? qp[2] : z;
+			uint4 ch3 = cc0 + 3u < A.pcols ? qp[3] : z;
 			if(pl.mask) {
 				// the four columns' block masks from one or two aligned 8-B loads (not four)
 				const uint32_t ma = cc0 & ~3u, sh = cc0 & 3u;
@@ -350,12 +357,12 @@ k_sw_bt(BtArgs A) {
 				if(!((m2 >> b) & 1u)) ch2 = z;
 				if(!((m3 >> b) & 1u)) ch3 = z;
 			}
+			myc[0] = ch0.x; myc[1] = ch0.y; myc[2] = ch0.z; myc[3] = ch0.w;
+			myc[4] = ch1.x; myc[5] = ch1.y; myc[6] = ch1.z; myc[7] = ch1.w;
+			myc[8] = ch2.x; myc[9] = ch2.y; myc[10] = ch2.z; myc[11] = ch2.w;
+			myc[12] = ch3.x; myc[13] = ch3.y; myc[14] = ch3.z; myc[15] = ch3.w;
 		}
-		const uint32_t u = c - cc0, di = (rsx & 15u) >> 2;
-		auto pick = [&](const uint4& v) -> uint32_t { return di == 0 ? v.x : di == 1 ? v.y : di == 2 ? v.z : v.w; };
-		const uint32_t d0 = pick(ch0), d1 = pick(ch1), d2 = pick(ch2), d3 = pick(ch3);
-		const uint32_t d = u == 0 ? d0 : u == 1 ? d1 : u == 2 ? d2 : d3;
-		return (int32_t)((d >> ((rsx & 3u) * 8u)) & 0xffu) - pl.off;
+		return (int32_t)((const uint8_t*)myc)[(c - cc0) * 16u + (rsx & 15u)] - pl.off;
 	};
 	const uint32_t ncand = (uint32_t)R.ncand < A.cap ? (uint32_t)R.ncand : A.cap;
 	const bt2g_sw_cand* cl = A.cands + (size_t)p * A.cap;
