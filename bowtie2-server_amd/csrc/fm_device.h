@@ -204,6 +204,23 @@ __device__ __forceinline__ int bi_step(const DevEbwt& e, uint32_t top, uint32_t 
 	return loads;
 }
 
+// bi_step without the mirror ranges (a caller that needs few of them derives
+// them: mirror top of character j = topp + sum of the range sizes below j)
+__device__ __forceinline__ int bi_step_tb(const DevEbwt& e, uint32_t top, uint32_t bot, uint32_t t[4], uint32_t b[4]) {
+	const uint32_t st = top / 192u, sb = bot / 192u;
+	SideData s1;
+	load_side(e, st, s1);
+	occ4(e, s1, top, t);
+	if(sb == st) {
+		occ4(e, s1, bot, b);
+		return 1;
+	}
+	SideData s2;
+	load_side(e, sb, s2);
+	occ4(e, s2, bot, b);
+	return 2;
+}
+
 // A read (or its reverse complement / reversal) as the reference's BTDnaString
 // views: patFw (rev=0,cmp=0), patRc (1,1), patFwRev (1,0), patRcRev (0,1).
 struct SeqView {
@@ -234,7 +251,9 @@ struct ReadWin {
 			w = *(const uint4*)(ptr - (addr & 15u));   // pointer provenance: global, not flat
 		}
 		const uint32_t di = (uint32_t)(addr >> 2) & 3u;
-		const uint32_t d = di == 0 ? w.x : di == 1 ? w.y : di == 2 ? w.z : w.w;
+		uint32_t x0 = w.x, x1 = w.y, x2 = w.z, x3 = w.w;
+		asm volatile("" : "+v"(x0), "+v"(x1), "+v"(x2), "+v"(x3));   // a select, not a scratch array
+		const uint32_t d = di == 0 ? x0 : di == 1 ? x1 : di == 2 ? x2 : x3;
 		return (int)((d >> ((addr & 3u) * 8u)) & 0xffu);
 	}
 };

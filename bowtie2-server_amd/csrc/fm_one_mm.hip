@@ -35,7 +35,9 @@ enum : int { ST_IDLE = 0, ST_FAR, ST_ALT, ST_BR, ST_DONE };
 
 // register-array access by a data-dependent index without going through scratch
 __device__ __forceinline__ uint32_t at4(const uint32_t a[4], int i) {
-	return i == 0 ? a[0] : i == 1 ? a[1] : i == 2 ? a[2] : a[3];
+	uint32_t x0 = a[0], x1 = a[1], x2 = a[2], x3 = a[3];
+	asm volatile("" : "+v"(x0), "+v"(x1), "+v"(x2), "+v"(x3));   // the compiler would index a stack copy
+	return i == 0 ? x0 : i == 1 ? x1 : i == 2 ? x2 : x3;
 }
 __device__ __forceinline__ void set4(uint32_t a[4], int i, uint32_t v) {
 #pragma unroll
@@ -463,6 +465,9 @@ extern "C" int bt2g_mm_prof_waves(unsigned long long* t0, unsigned long long* t1
 	return 0;
 }
 #endif
+#ifndef MM_BRBUF
+#define MM_BRBUF 160             // staged far-half branches per wave (48 B each, LDS)
+#endif
 #ifndef BT2G_MM_FAR_WAVES
 #define BT2G_MM_FAR_WAVES 3      // 4 and 5 spill (84 / 152 B per lane)
 #endif
@@ -478,6 +483,15 @@ k_one_mm_far(DevEbwt F, DevEbwt B, const uint8_t* __restrict__ reads, const uint
              uint4* __restrict__ fb_st4, uint32_t* __restrict__ fb_sdep, uint32_t* __restrict__ fb_n,
              uint32_t* __restrict__ slot_flag) {
 	const uint32_t qi = blockIdx.x * blockDim.x + threadIdx.x;
+	// Far-half branches are staged in LDS per wave and go to the global queue in
+	// one allocation and a coalesced copy when the wave is done: a global atomic
+	// (whose return the store waits for) and a store inside the LF loop made
+	// every later side load of the wave wait behind them (vmcnt is in order) --
+	// ~13 us per LF step with most waves pushing at some step.
+	__shared__ MmBranch s_br[4][MM_BRBUF];
+	__shared__ uint32_t s_brn[4];
+	const uint32_t wv = threadIdx.x >> 6;
+	if((threadIdx.x & 63u) == 0) s_brn[wv] = 0;
 	if(qi >= *nitems_p) return;
 #ifdef BT2G_MM_PROF
 	const uint32_t wslot = (EBWTFW ? 0u : 65536u) + ((qi >> 6) & 0xffffu);
@@ -527,14 +541,12 @@ k_one_mm_far(DevEbwt F, DevEbwt B, const uint8_t* __restrict__ reads, const uint
 #ifdef BT2G_MM_PROF
 		prof_ops = ops;
 #endif
-		uint32_t ot[4], ob[4], otp[4], obp[4];
+		uint32_t ot[4], ob[4];
 		int clo = 0, chi = 3;
 		bool match;
-		if(bot - top > 1) {
-#pragma unroll
-			for(int i = 0; i < 4; i++) ot[i] = ob[i] = 0;
-			otp[0] = topp;
-			loads += bi_step(E, top, bot, topp, ot, ob, otp, obp);
+		const bool single = bot - top <= 1;
+		if(!single) {
+			loads += bi_step_tb(E, top, bot, ot, ob);
 			match = rdc < 4;
 		} else {
 			SideData s1;
@@ -543,10 +555,19 @@ k_one_mm_far(DevEbwt F, DevEbwt B, const uint8_t* __restrict__ reads, const uint
 			const int rowl = side_rowL(s1, top % 192u);
 			const uint32_t lf1 = occ1(E, s1, top, rowl);
 #pragma unroll
-			for(int i = 0; i < 4; i++) { ot[i] = lf1; ob[i] = lf1 + 1; otp[i] = topp; obp[i] = botp; }
+			for(int i = 0; i < 4; i++) { ot[i] = lf1; ob[i] = lf1 + 1; }
 			clo = chi = rowl;
 			match = rowl == rdc;
 		}
+		// mirror range of character j (mapBiLFEx's prefix sums; a single row keeps its mirror)
+		auto mirror = [&](int jj, uint32_t& mt, uint32_t& mb) {
+			if(single) { mt = topp; mb = botp; return; }
+			uint32_t acc = topp;
+#pragma unroll
+			for(int i = 0; i < 3; i++) acc += i < jj ? ob[i] - ot[i] : 0u;
+			mt = acc;
+			mb = acc + (at4(ob, jj) - at4(ot, jj));
+		};
 		// alternatives clo..chi at this depth (aligner_seed.cpp:1166-1290); with an N in
 		// the read only the N itself may be the mismatch
 		if(!hasn || rdc > 3) {
@@ -571,20 +592,28 @@ k_one_mm_far(DevEbwt F, DevEbwt B, const uint8_t* __restrict__ reads, const uint
 				}
 				valid = valid && score >= minsc;
 				const uint32_t myseq = dseq++;
-				const uint32_t tm = at4(ot, j), bm = at4(ob, j), tpm = at4(otp, j), bpm = at4(obp, j);
+				uint32_t tpm, bpm;
+				mirror(j, tpm, bpm);
+				const uint32_t tm = at4(ot, j), bm = at4(ob, j);
 				if(depm < len) {
-					const uint32_t q = wave_alloc1(brq_n);
-					if(q >= brq_cap) { handed = true; break; }
-					MmBranch b;
-					b.rng = make_uint4(tm, bm, tpm, bpm);
-					b.slot = slot;
-					b.seq = myseq;
-					b.meta = depm | ((uint32_t)j << 16) | ((uint32_t)rdc << 20) | ((valid ? 1u : 0u) << 24) |
-					         ((ebwtfw ? 1u : 0u) << 25);
-					b.score = (int32_t)score;
-					b.off5p = (int32_t)off5p;
-					b.pad[0] = b.pad[1] = b.pad[2] = 0;
-					brq[q] = b;
+					// MmBranch as three 16-B words; pad[0] = the item (for a queue
+					// overflow at the flush)
+					const uint32_t meta = depm | ((uint32_t)j << 16) | ((uint32_t)rdc << 20) | ((valid ? 1u : 0u) << 24) |
+					                      ((ebwtfw ? 1u : 0u) << 25);
+					const uint4 w0 = make_uint4(tm, bm, tpm, bpm);
+					const uint4 w1 = make_uint4(slot, myseq, meta, (uint32_t)(int32_t)score);
+					const uint4 w2 = make_uint4((uint32_t)(int32_t)off5p, qi, 0u, 0u);
+					const uint32_t k = atomicAdd(&s_brn[wv], 1u);
+					if(k < MM_BRBUF) {
+						uint4* dst = (uint4*)&s_br[wv][k];
+						dst[0] = w0; dst[1] = w1; dst[2] = w2;
+					} else {
+						// the wave's LDS buffer is full: straight to the global queue
+						const uint32_t q = atomicAdd(brq_n, 1u);
+						if(q >= brq_cap) { handed = true; break; }
+						uint4* dst = (uint4*)&brq[q];
+						dst[0] = w0; dst[1] = w1; dst[2] = w2;
+					}
 				} else if(valid) {                       // the mismatch is the last base
 					if((uint32_t)nh < cap)
 						slots[(size_t)slot * cap + nh] = bt2g_mm1{ebwtfw ? tm : tpm, ebwtfw ? bm : bpm, fw ? 1 : 0,
@@ -596,11 +625,43 @@ k_one_mm_far(DevEbwt F, DevEbwt B, const uint8_t* __restrict__ reads, const uint
 		}
 		if(handed) break;
 		if(match) {
-			top = at4(ot, rdc); bot = at4(ob, rdc); topp = at4(otp, rdc); botp = at4(obp, rdc);
+			uint32_t mt, mb;
+			mirror(rdc, mt, mb);
+			top = at4(ot, rdc); bot = at4(ob, rdc); topp = mt; botp = mb;
 		}
 		if(!(bot > top && match && dep != len - 1)) break;
 		dep++;
 	}
+	// flush the wave's staged branches (every lane still running is here)
+	bool overflow = false;
+	{
+		const uint32_t n = s_brn[wv] < MM_BRBUF ? s_brn[wv] : MM_BRBUF;
+		if(n) {
+			const uint64_t act = __ballot(1);
+			const uint32_t me = threadIdx.x & 63u, lead = (uint32_t)__ffsll((long long)act) - 1u;
+			uint32_t qb = 0;
+			if(me == lead) qb = atomicAdd(brq_n, n);
+			qb = (uint32_t)__shfl((int)qb, (int)lead);
+			const uint32_t rank = (uint32_t)__popcll(act & ((1ull << me) - 1ull)), na = (uint32_t)__popcll(act);
+			for(uint32_t i = rank; i < n; i += na) {
+				const uint4* src = (const uint4*)&s_br[wv][i];
+				const uint4 w0 = src[0], w1 = src[1], w2 = src[2];
+				if(qb + i < brq_cap) {
+					uint4* dst = (uint4*)&brq[qb + i];
+					dst[0] = w0; dst[1] = w1; dst[2] = w2;
+				} else if(atomicExch(&slot_flag[w1.x], 1u) == 0u) {
+					// queue full: the entry's item is redone whole by the in-place state
+					// machine (its queued branches are skipped by their slot flag)
+					const uint32_t f = atomicAdd(fb_n, 1u);
+					fb_items[f] = items[w2.y];
+					fb_st4[f] = st4[w2.y];
+					fb_sdep[f] = sdep[w2.y];
+				}
+			}
+			overflow = qb + n > brq_cap;
+		}
+	}
+	if(overflow && !handed && atomicAdd(&slot_flag[slot], 0u)) return;   // redone by the state machine
 	if(handed) {
 		// queue full: the whole item goes to the in-place state machine
 		slot_flag[slot] = 1u;
@@ -620,6 +681,7 @@ k_one_mm_far(DevEbwt F, DevEbwt B, const uint8_t* __restrict__ reads, const uint
 // operations and op counting as the in-place walk (ST_BR above).  A completed
 // valid branch appends its hit to its slot (after the far kernel's own hits,
 // slot_counts[] is the slot's running count).
+template <bool EBWTFW>
 __global__ void __launch_bounds__(256)
 k_one_mm_branch(DevEbwt F, DevEbwt B, const uint8_t* __restrict__ reads, uint32_t stride,
                 const uint32_t* __restrict__ lens, const MmBranch* __restrict__ brq,
@@ -630,9 +692,12 @@ k_one_mm_branch(DevEbwt F, DevEbwt B, const uint8_t* __restrict__ reads, uint32_
 	const uint32_t nq = *brq_n < brq_cap ? *brq_n : brq_cap;
 	if(i >= nq) return;
 	const MmBranch b = brq[i];
-	if(slot_flag[b.slot]) return;                 // its item was redone whole by the state machine
+	// one launch per index direction: the index a lane walks is then uniform (a
+	// per-lane choice between the two DevEbwt arguments put both on the stack)
 	const bool ebwtfw = (b.meta >> 25) & 1u;
-	const DevEbwt& E = ebwtfw ? F : B;
+	if(ebwtfw != EBWTFW) return;
+	if(slot_flag[b.slot]) return;                 // its item was redone whole by the state machine
+	const DevEbwt& E = EBWTFW ? F : B;
 	const uint32_t r = b.slot >> 2;
 	const bool fw = ((b.slot >> 1) & 1u) == 0;
 	const uint32_t len = lens[r];
@@ -707,6 +772,8 @@ void launch_one_mm_q(const DevEbwt& F, const DevEbwt& B, const uint8_t* reads, c
 	hipLaunchKernelGGL(k_one_mm_q<false>, dim3(grid), dim3(256), 0, st, F, B, reads, quals, stride, lens, minsc, P,
 	                   sc.ncl_const, sc.ncl_lin, fb_items + half, counters + 6, fb_st4 + half, fb_sdep + half, cap,
 	                   slots, slot_counts, ops, loads, brq, counters + 7, 0u);
-	hipLaunchKernelGGL(k_one_mm_branch, dim3((brq_cap + 255) / 256), dim3(256), 0, st, F, B, reads, stride, lens, brq,
-	                   counters + 4, brq_cap, cap, slots, slot_counts, ops, loads, slot_flag);
+	hipLaunchKernelGGL(k_one_mm_branch<true>, dim3((brq_cap + 255) / 256), dim3(256), 0, st, F, B, reads, stride,
+	                   lens, brq, counters + 4, brq_cap, cap, slots, slot_counts, ops, loads, slot_flag);
+	hipLaunchKernelGGL(k_one_mm_branch<false>, dim3((brq_cap + 255) / 256), dim3(256), 0, st, F, B, reads, stride,
+	                   lens, brq, counters + 4, brq_cap, cap, slots, slot_counts, ops, loads, slot_flag);
 }
