@@ -768,7 +768,7 @@ static int sw_align_impl(bt2g_ctx* c, const uint8_t* reads, const uint8_t* quals
 			launch_sw_packed(sc->local != 0, probs, nprob, reads, quals, stride, lens, windows, c->ref_codes,
 			                 c->ref_starts, C, enable8, cap, maxcol, res, cands, plane, hslot, hbytes, st);
 		} else {
-		const PlaneOut po{plane, hslot, maxcol};     // u16 score plane (hslot from sw_plane_slot(.., 2))
+		const PlaneOut po{plane, hslot, sw_plane_pitch(maxcol)};   // u16 score plane (hslot from sw_plane_slot(.., 2))
 		launch_sw_partition(probs, nprob, sc->local, enable8, list8, counts + 0, list16, counts + 1, st);
 		int v8 = sc->local ? 2 : 0, v16 = sc->local ? 3 : 1;
 		launch_sw_fill(v8, probs, nprob, list8, counts + 0, reads, quals, stride, lens, windows, c->ref_codes,
@@ -887,7 +887,7 @@ int bt2g_sw_align_bt_dev(bt2g_ctx* c, const uint8_t* reads, const uint8_t* quals
 	if(!a.marks && (rc = talloc((void**)&a.marks, sizeof(uint32_t) * a.mslot * nprob))) return rc;
 	a.probs = probs; a.nprob = nprob; a.reads = reads; a.quals = quals; a.stride = stride; a.lens = lens;
 	a.windows = windows; a.ref_codes = c->ref_codes; a.ref_starts = c->ref_starts; a.rects = rects;
-	a.res = res; a.cands = cands; a.cap = cap; a.cstride = S16; a.pcols = maxcol;
+	a.res = res; a.cands = cands; a.cap = cap; a.cstride = S16; a.pcols = sw_plane_pitch(maxcol);
 #ifdef BT2G_SW_NOMASK
 	a.use_mask = 0;   // timing experiments only
 #else

@@ -85,10 +85,15 @@ inline uint32_t sw_packed_group_words(uint32_t max_cols, bool local) {
 }
 // Rows per strip stack of the systolic fill (its score-plane column stride).
 inline uint32_t sw_packed_rows(uint32_t stride) { return 16u * ((stride + 15u) / 16u); }
-// Score-plane bytes per problem: 16-row blocks x cols x hbytes, then one u16
-// mask of written blocks per column (sw_ee_packed.hip)
+// Score-plane column pitch: a multiple of 4, so that the u8 fill's 4-column
+// bursts (64 B) start on 64-B boundaries
+__host__ __device__ inline uint32_t sw_plane_pitch(uint32_t cols) { return (cols + 3u) & ~3u; }
+// Score-plane bytes per problem: 16-row blocks x pitch x hbytes, then one u16
+// mask of written blocks per column (sw_ee_packed.hip); a multiple of 64 B
 inline uint64_t sw_plane_slot(uint32_t stride, uint32_t cols, int hbytes) {
-	return (uint64_t)sw_packed_rows(stride) * cols * (uint64_t)hbytes + (((uint64_t)cols * 2u + 15u) & ~(uint64_t)15u);
+	const uint64_t pc = sw_plane_pitch(cols);
+	return ((uint64_t)sw_packed_rows(stride) * pc * (uint64_t)hbytes + ((pc * 2u + 15u) & ~(uint64_t)15u) + 63u) &
+	       ~(uint64_t)63u;
 }
 
 // Backtrace (sw_backtrace.hip): one lane per problem.

@@ -459,7 +459,11 @@ k_sw_sys(const bt2g_sw_problem* __restrict__ probs, uint32_t nprob, const uint8_
 #endif
 	const uint32_t thr0 = LOCAL ? 1u : h[0].row0 + (uint32_t)h[0].minsc;
 	const uint32_t thr1 = LOCAL ? 1u : h[1].row0 + (uint32_t)h[1].minsc;
-	uint8_t* const mplane = plane + (size_t)16u * S * max_cols * (size_t)hbytes;
+	const uint32_t pitch = sw_plane_pitch(max_cols);       // plane columns per 16-row block
+	uint8_t* const mplane = plane + (size_t)16u * S * pitch * (size_t)hbytes;
+	// (staging 4 columns per lane in LDS and writing 64-B bursts measured
+	// slower: 17.2 vs 15.4 ms; stores into an L2-resident 64 KB instead of the
+	// plane: 12.4 ms, no stores 10.0 ms)
 	// LOCAL: a block is searched for candidates when its maximum reaches minsc
 	// (never for a problem without gather-eligible rows); cthr = minsc - 1 per half
 	uint32_t ctest[2];
@@ -606,7 +610,7 @@ k_sw_sys(const bt2g_sw_problem* __restrict__ probs, uint32_t nprob, const uint8_
 		if(STORE && in_group) {
 #endif
 			bool s0 = h[0].live && (uint32_t)j < h[0].ncol, s1 = h[1].live && (uint32_t)j < h[1].ncol;
-			const size_t cell = ((size_t)k * max_cols + (uint32_t)j) * 16u;
+			const size_t cell = ((size_t)k * pitch + (uint32_t)j) * 16u;
 			if(use_mask) {
 				s0 = s0 && (mx & 0xffffu) >= thr0;
 				s1 = s1 && (mx >> 16) >= thr1;
