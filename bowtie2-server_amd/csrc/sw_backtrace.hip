@@ -105,6 +105,12 @@ __device__ unsigned long long g_bt_wave_t0[1u << 16], g_bt_wave_t1[1u << 16];   
 #define BTC(i) ((void)0)
 #endif
 
+// u8 plane columns held in the lane's LDS chunk; LDS dwords per lane (the
+// chunk, then the read / quality / reference windows; odd: banks differ by lane)
+#ifndef BT_CHUNK
+#define BT_CHUNK 4u      // 4: 36.7 ms, 6: 36.8, 8: 39.8 (LDS occupancy)
+#endif
+#define BT_LDSW ((4u * BT_CHUNK + 12u) | 1u)
 #ifndef BT2G_BT_WAVES
 #define BT2G_BT_WAVES 4      // with the LDS caches: 3 waves 41.3 ms, 4 (12 B/lane spilled) 36.9, 5 (124 B) 43.8
 #endif
@@ -289,8 +295,8 @@ k_sw_bt(BtArgs A) {
 	// reads wait on their own counter, not behind the walk's global loads, and
 	// the 40 VGPRs they took are what kept the kernel at 3 waves/SIMD with
 	// spills (measured: 2 waves 61 ms, 3 waves 48.8 ms, 4 waves + spills 46.6).
-	__shared__ uint32_t s_cache[64u * 29u];
-	uint32_t* const myc = s_cache + threadIdx.x * 29u;
+	__shared__ uint32_t s_cache[64u * BT_LDSW];
+	uint32_t* const myc = s_cache + threadIdx.x * BT_LDSW;
 	uint64_t w_rd = ~0ull, w_q = ~0ull, w_rf = ~0ull;   // address of the window each slot holds
 	auto win = [&](uint64_t& Wa, uint32_t k, const uint8_t* ptr, const uint8_t* lo, const uint8_t* hi) -> int {
 		const uint64_t addr = (uint64_t)ptr, aa = addr & ~15ull;
@@ -300,10 +306,10 @@ k_sw_bt(BtArgs A) {
 			// through the kernel-argument pointer (global address space), not an
 			// integer cast: a flat load would make every later wait a full drain
 			const uint4 v = *(const uint4*)(ptr - (addr & 15u));
-			uint32_t* d = myc + 16u + 4u * k;
+			uint32_t* d = myc + 4u * BT_CHUNK + 4u * k;
 			d[0] = v.x; d[1] = v.y; d[2] = v.z; d[3] = v.w;
 		}
-		return ((const uint8_t*)(myc + 16u + 4u * k))[addr & 15u];
+		return ((const uint8_t*)(myc + 4u * BT_CHUNK + 4u * k))[addr & 15u];
 	};
 	auto rd_at = [&](uint32_t r) -> int {   // read character of DP row r
 		const int raw = win(w_rd, 0u, rd + (fw ? r : nrow - 1 - r), A.reads, rd + A.stride);
@@ -322,45 +328,48 @@ k_sw_bt(BtArgs A) {
 		const int code = win(w_rf, 2u, A.ref_codes + rs + (uint64_t)o, wlo, whi);
 		return code > 3 ? 16 : 1 << code;
 	};
-	// H of a cell; the u8 plane goes through a copy of 4 columns x 16 rows in
-	// the lane's LDS region (dwords 0..15: column cc0 + u at 4u..4u+3)
+	// H of a cell; the u8 plane goes through a copy of BT_CHUNK columns x 16
+	// rows in the lane's LDS region (column cc0 + u at dwords 4u..4u+3)
 	uint32_t cb = 0xffffffffu, cc0 = 0;
 	auto hget = [&](uint32_t r, uint32_t c) -> int32_t {
 		BTC(7);
 		if(KIND != 0) return pl.h(r, c);   // u16 planes: direct (a chunk cache costs occupancy)
 		const uint32_t rsx = pad + r, b = rsx >> 4;
-		if(b != cb || c < cc0 || c > cc0 + 3u) {
+		if(b != cb || c < cc0 || c > cc0 + (BT_CHUNK - 1u)) {
 			BTC(8);
 			cb = b;
-			cc0 = c >= 3u ? c - 3u : 0u;
-			if(cc0 + 4u > A.pcols) cc0 = A.pcols >= 4u ? A.pcols - 4u : 0u;
+			// the walk moves left: the chunk ends at column c
+			cc0 = c >= BT_CHUNK - 1u ? c - (BT_CHUNK - 1u) : 0u;
+			if(cc0 + BT_CHUNK > A.pcols) cc0 = A.pcols >= BT_CHUNK ? A.pcols - BT_CHUNK : 0u;
 			const uint4* qp = (const uint4*)(slot + ((size_t)b * A.pcols + cc0) * 16u);
 			// chunks and their block masks in one round trip, dead blocks zeroed after
 			const uint4 z = make_uint4(0, 0, 0, 0);
-			uint4 ch0 = cc0 < A.pcols ? qp[0] : z;
-			uint4 ch1 = cc0 + 1u < A.pcols ? qp[1] : z;
-			uint4 ch2 = cc0 + 2u < A.pcols ? qp[2] : z;
-			uint4 ch3 = cc0 + 3u < A.pcols ? qp[3] : z;
+			uint4 ch[BT_CHUNK];
+#pragma unroll
+			for(uint32_t u = 0; u < BT_CHUNK; u++) ch[u] = cc0 + u < A.pcols ? qp[u] : z;
 			if(pl.mask) {
-				// the four columns' block masks from one or two aligned 8-B loads (not four)
-				const uint32_t ma = cc0 & ~3u, sh = cc0 & 3u;
-				const uint2 lo = *(const uint2*)(pl.mask + ma);
-				const uint2 hi = sh && ma + 4u < A.pcols ? *(const uint2*)(pl.mask + ma + 4u) : make_uint2(0u, 0u);
-				const uint32_t mw[4] = {lo.x, lo.y, hi.x, hi.y};   // two masks per word
-				auto mk = [&](uint32_t k) -> uint32_t {
-					const uint32_t j = sh + k;                     // column cc0 + k = ma + j
-					return cc0 + k < A.pcols ? (mw[j >> 1] >> ((j & 1u) * 16u)) & 0xffffu : 0u;
-				};
-				const uint32_t m0 = mk(0), m1 = mk(1), m2 = mk(2), m3 = mk(3);
-				if(!((m0 >> b) & 1u)) ch0 = z;
-				if(!((m1 >> b) & 1u)) ch1 = z;
-				if(!((m2 >> b) & 1u)) ch2 = z;
-				if(!((m3 >> b) & 1u)) ch3 = z;
+				// the columns' block masks from one or two aligned 16-B loads (8 masks each)
+				const uint32_t ma = cc0 & ~7u, sh = cc0 & 7u;
+				const uint4 lo = *(const uint4*)(pl.mask + ma);
+				const uint4 hi = sh + BT_CHUNK > 8u && ma + 8u < A.pcols ? *(const uint4*)(pl.mask + ma + 8u)
+				                                                         : make_uint4(0u, 0u, 0u, 0u);
+				uint32_t mw[8] = {lo.x, lo.y, lo.z, lo.w, hi.x, hi.y, hi.z, hi.w};   // two masks per word
+				asm volatile("" : "+v"(mw[0]), "+v"(mw[1]), "+v"(mw[2]), "+v"(mw[3]), "+v"(mw[4]), "+v"(mw[5]),
+				             "+v"(mw[6]), "+v"(mw[7]));
+#pragma unroll
+				for(uint32_t u = 0; u < BT_CHUNK; u++) {
+					const uint32_t jw = sh + u;                       // column cc0 + u = ma + jw
+					uint32_t w = mw[0];
+#pragma unroll
+					for(uint32_t q = 1; q < 8; q++) w = (jw >> 1) == q ? mw[q] : w;
+					const uint32_t m = cc0 + u < A.pcols ? (w >> ((jw & 1u) * 16u)) & 0xffffu : 0u;
+					if(!((m >> b) & 1u)) ch[u] = z;
+				}
 			}
-			myc[0] = ch0.x; myc[1] = ch0.y; myc[2] = ch0.z; myc[3] = ch0.w;
-			myc[4] = ch1.x; myc[5] = ch1.y; myc[6] = ch1.z; myc[7] = ch1.w;
-			myc[8] = ch2.x; myc[9] = ch2.y; myc[10] = ch2.z; myc[11] = ch2.w;
-			myc[12] = ch3.x; myc[13] = ch3.y; myc[14] = ch3.z; myc[15] = ch3.w;
+#pragma unroll
+			for(uint32_t u = 0; u < BT_CHUNK; u++) {
+				myc[4u * u] = ch[u].x; myc[4u * u + 1u] = ch[u].y; myc[4u * u + 2u] = ch[u].z; myc[4u * u + 3u] = ch[u].w;
+			}
 		}
 		return (int32_t)((const uint8_t*)myc)[(c - cc0) * 16u + (rsx & 15u)] - pl.off;
 	};
