@@ -305,6 +305,34 @@ class Pipeline:
         if self._timing is not None:
             self._timing.append((name, time.perf_counter()))
 
+    def _overflow(self, h, probs, rects, npb, res, naln, alns, edits, S):
+        """DPs whose candidate list outgrew the call's cap (naln -5, the engine's
+        'list truncated' mark) are run again with room for all of them, as the
+        reference keeps every candidate (SwAligner::align; the drop-in binding
+        does the same): the local fill finds > 2048 candidates in some repeat
+        windows of the hg38-like genome."""
+        torch, L, bt2g = self.torch, self.L, self.bt2g
+        over = torch.nonzero(naln[:npb] == -5).squeeze(1)
+        k = int(over.numel())
+        if k == 0:
+            return
+        cap = min(8192, int(res[:npb, 6].index_select(0, over).max()))
+        dev, P = self.dev, self._p
+        r2 = torch.empty((k, 8), dtype=torch.int32, device=dev)
+        c2 = torch.empty((k, cap, 3), dtype=torch.int32, device=dev)
+        n2 = torch.empty(k, dtype=torch.int32, device=dev)
+        a2 = torch.empty((k, self.maxaln, 10), dtype=torch.int32, device=dev)
+        e2 = torch.empty((k, self.maxaln, self.maxedit, 2), dtype=torch.int32, device=dev)
+        p2, q2 = probs.index_select(0, over).contiguous(), rects.index_select(0, over).contiguous()
+        bt2g._chk(L.bt2g_sw_align_bt_dev(h, P(self.reads), P(self.quals), self.len, P(self.lens), P(p2), k, None,
+                                         P(q2), C.byref(self.sc), 1, cap, P(r2), P(c2), self.maxaln, self.maxedit,
+                                         P(n2), P(a2), P(e2), None, S))
+        res[over] = r2
+        naln[over] = n2
+        alns[over] = a2
+        edits[over] = e2
+        self.stats["cand_overflow_reruns"] = self.stats.get("cand_overflow_reruns", 0) + k
+
     def step(self, keep=False):
         torch, L, bt2g = self.torch, self.L, self.bt2g
         self._timing = [("start", time.perf_counter())] if os.environ.get("BT2G_BENCH_TIMING") else None
@@ -370,6 +398,7 @@ class Pipeline:
                                    P(probs), npb, None, P(self.rects), C.byref(self.sc), 1, self.sw_cap,
                                    P(self.res), P(self.cands), self.maxaln, self.maxedit, P(self.naln),
                                    P(self.alns), P(self.edits), None, S))
+        self._overflow(h, probs, self.rects, npb, self.res, self.naln, self.alns, self.edits, S)
         self._mark("sw")
         # end-to-end: an exact end-to-end hit is the alignment (EXTEND_PERFECT_SCORE);
         # local: every read's hits, the exact ones included, go through the DP
@@ -437,6 +466,8 @@ class Pipeline:
                                        P(mp[c0:c1]), c1 - c0, None, P(mr[c0:c1]), C.byref(self.sc), 1, self.sw_cap,
                                        P(self.mres), P(self.mcands), self.maxaln, self.maxedit, P(self.mnaln),
                                        P(self.malns), P(self.medits), None, S))
+            self._overflow(self.eng2.h, mp[c0:c1], mr[c0:c1], c1 - c0, self.mres, self.mnaln, self.malns,
+                           self.medits, S)
             found[pair_of[c0:c1][self.mnaln[:c1 - c0] > 0]] = True
         self._mark("mate_dps")
         if keep:
@@ -700,6 +731,30 @@ def bt_mismatches(naln, alns, ed, ref, maxaln, maxedit):
     return int(bad.sum())
 
 
+def chain_parity(pipe, ref, mate):
+    """Stage-by-stage comparison of the GPU's buffers of the last kept step with
+    the reference's own chain on the same reads (cpu_baseline): every count
+    ending in "_mismatch" is 0 when the two agree."""
+    from oracle.ref_chain import compare
+    g = gpu_chain(pipe, ref["ids"])
+    parity = compare(ref, g)
+    parity["reads"] = int(len(ref["ids"]))
+    if parity["frame_mismatch"] == 0:
+        # the same rectangles on both sides: pair them up and compare fill + backtraces
+        rp, gp = ref["probs"], g["probs"]
+        kr = np.lexsort([rp[k] for k in ("refl", "refidx", "fw", "read")])
+        kg = np.lexsort([gp[k] for k in ("refl", "refidx", "fw", "read")])
+        gidx = g["probs_index"][kg]
+        sw_ref = ref["sw"][kr]
+        res = pipe.res[:pipe.last["npb"]].cpu().numpy()[gidx]
+        parity["sw_mismatch"] = int((res[:, 0] != sw_ref[:, 0]).sum() + (res[:, 6] != sw_ref[:, 1]).sum())
+        parity["backtrace_mismatch"] = backtrace_parity(pipe, gidx, sw_ref)
+        parity["ref_alignments"] = int(sw_ref[:, 2].sum())
+    if pipe.pol.paired:
+        parity.update(mate_parity(pipe, mate))
+    return parity
+
+
 def backtrace_parity(pipe, kp_all, sw_ref):
     """The seed-extension DPs kp_all (GPU problem indices) nextAlignment results
     vs the reference's rows sw_ref (same order)."""
@@ -943,7 +998,8 @@ def main():
     naln_np = pipe.naln[:last["npb"]].cpu().numpy()
     bt_stats = {"alignments": int(naln_np.clip(0).sum()), "dps_with_alignment": int((naln_np > 0).sum()),
                 "dps_at_maxaln": int((naln_np >= pipe.maxaln).sum()), "maxaln": pipe.maxaln,
-                "dps_cand_overflow": int((naln_np == -5).sum())}
+                "dps_cand_overflow": int((naln_np == -5).sum()),
+                "cand_overflow_reruns_total": int(pipe.stats.get("cand_overflow_reruns", 0))}
     log(f"[rank {rank}] SW: {last['npb']} DPs/step, {sw_gcups:.0f} GCUPS; aligned {n_aligned/(args.steps*world*args.reads):.4f}; backtrace {bt_stats}")
     mate_stats = None
     if args.mode == "paired":
@@ -1003,22 +1059,7 @@ def main():
                              + (f", then otherMate + frameFindMateRect + the mate DPs of the GPU's anchors "
                                 f"({len(mate['out_ref'])})" if paired else "")
                              + f"; {threads} threads = the usable cores of this host ({host['model']})"}
-            g = gpu_chain(pipe, ref["ids"])
-            parity = compare(ref, g)
-            parity["reads"] = int(len(ref["ids"]))
-            if parity["frame_mismatch"] == 0:
-                # the same rectangles on both sides: pair them up and compare fill + backtraces
-                rp, gp = ref["probs"], g["probs"]
-                kr = np.lexsort([rp[k] for k in ("refl", "refidx", "fw", "read")])
-                kg = np.lexsort([gp[k] for k in ("refl", "refidx", "fw", "read")])
-                gidx = g["probs_index"][kg]
-                sw_ref = ref["sw"][kr]
-                res = pipe.res[:pipe.last["npb"]].cpu().numpy()[gidx]
-                parity["sw_mismatch"] = int((res[:, 0] != sw_ref[:, 0]).sum() + (res[:, 6] != sw_ref[:, 1]).sum())
-                parity["backtrace_mismatch"] = backtrace_parity(pipe, gidx, sw_ref)
-                parity["ref_alignments"] = int(sw_ref[:, 2].sum())
-            if paired:
-                parity.update(mate_parity(pipe, mate))
+            parity = chain_parity(pipe, ref, mate)
             log(f"[rank 0] cpu baseline {sample/dt:.0f} {cpu['unit']} on {threads} threads ({dt:.1f}s); parity {parity}")
             if args.server_sample:
               try:
