@@ -37,7 +37,11 @@ extern "C" {
 #define BT2G_ERR_NOMEM    -5
 #define BT2G_ERR_OVERFLOW -6
 
-#define BT2G_MAX_READ_LEN 1024
+/* Longest read the engines take (the reference checkpoints DPs of reads of
+ * >= --cp-min (default 2000) bases; the checkpointed path stays on the CPU).
+ * Reads up to 1024 bases go through the systolic fills; longer ones through
+ * the one-problem-per-lane fills and a u16 score plane. */
+#define BT2G_MAX_READ_LEN 2048
 
 typedef struct bt2g_ctx bt2g_ctx;
 

@@ -274,7 +274,10 @@ struct DpReq : Req {         // bt2g_sw_align_bt
 	std::vector<bt2g_sw_aln> alns;
 	std::vector<bt2g_edit> edits;
 	int32_t naln = 0;
-	DpReq(const bt2g_scoring& s, int e8) : Req(ST_DP, (uint64_t)e8 | ((uint64_t)s.local << 1)), sc(s), enable8(e8) {}
+	bool cpu = false;            // more candidates than the engine takes (> 8192): the CPU path
+	// reads longer than 1024 bases batch apart (another fill; a batch is padded to its longest read)
+	DpReq(const bt2g_scoring& s, int e8, bool lng)
+		: Req(ST_DP, (uint64_t)e8 | ((uint64_t)s.local << 1) | ((uint64_t)lng << 2)), sc(s), enable8(e8) {}
 };
 
 // Rows of a batch as one [n][stride] array (stride = longest read).
@@ -408,6 +411,10 @@ int run_dp(const std::vector<DpReq*>& v, uint32_t cap = 0, uint32_t maxaln = 8) 
 	if(rc && rc != BT2G_ERR_OVERFLOW) return rc;
 	for(size_t i = 0; i < n; i++) {
 		DpReq* q = v[i];
+		if(R[i].ncand > 8192) {      // beyond the engine's candidate capacity
+			q->cpu = true;
+			continue;
+		}
 		if(R[i].ncand > (int32_t)cap || (NA[i] == (int32_t)maxaln && R[i].ncand > (int32_t)maxaln)) {
 			std::vector<DpReq*> one{q};
 			if((rc = run_dp(one, std::max<uint32_t>(cap, (uint32_t)R[i].ncand),
@@ -888,7 +895,7 @@ bool SwAlignerAcc::gpu_align(TAlScore& best, bool& served) {
 	   minsc_ > std::numeric_limits<int32_t>::max())
 		return false;
 	DpState& st = dp_state(this);
-	DpReq q(bs, (enable8_ && !readSse16_) ? 1 : 0);
+	DpReq q(bs, (enable8_ && !readSse16_) ? 1 : 0, rdlen > 1024);
 	q.r.set(*rdfw_, *qufw_);
 	bt2g_sw_problem& p = q.p;
 	memset(&p, 0, sizeof(p));
@@ -902,6 +909,7 @@ bool SwAlignerAcc::gpu_align(TAlScore& best, bool& served) {
 	q.rect.pad = 0;
 	q.win.assign((const uint8_t*)rf_ + rfi_, (const uint8_t*)rf_ + rfi_ + ncol + 1);
 	g_disp.submit(&q);
+	if(q.cpu) return false;      // served = false: the reference's align() runs
 	const bt2g_sw_result& o = q.o;
 	if(getenv("BT2G_ADAPTER_DUMP")) {
 		st.row = q.r;

@@ -11,7 +11,7 @@ O=gpurun_out/${2:-r02}
 mkdir -p $O
 B="bench.py --no-cpu-baseline --server-sample 0"
 if [ "$1" = prof ]; then
-  timeout -k 10 420 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread > $O/gpu_tests.log 2>&1
+  timeout -k 10 720 python -u -m pytest tests -m gpu -x -q --timeout 600 --timeout-method thread > $O/gpu_tests.log 2>&1
   echo tests ok
   timeout -s KILL 360 rocprofv3 --pmc FETCH_SIZE --output-format csv -d $O/pmc_fetch -o run -- python3 $B --steps 1 --warmup 0 > $O/pmc_fetch.log 2>&1
   echo fetch ok

@@ -40,7 +40,7 @@ SRV_GPU = os.path.join(rs.REF_DIR, "bowtie2-align-server-gpu")
 SRV_STUB = os.path.join(rs.REF_DIR, "bowtie2-align-server-stub")
 LONGREADS = os.path.join(ROOT, "tests", "golden", "longreads.fq.gz")     # example/reads/longreads.fq
 LAMBDA_PE = [os.path.join(ROOT, "tests", "golden", f"reads_{m}.fq.gz") for m in (1, 2)]  # example/reads/reads_{1,2}.fq
-MAXLEN = 1024        # BT2G_MAX_READ_LEN
+MAXLEN = 2048        # BT2G_MAX_READ_LEN
 
 
 def _need(*paths):
