@@ -74,6 +74,9 @@ struct bt2g_ctx {
 	int bt_hbytes = 0;
 	uint8_t* bt_plane = nullptr;
 	uint32_t* bt_marks = nullptr;
+	// the 1-mm search's second stream (the BWT' direction) and its fork/join events
+	hipStream_t aux = nullptr;
+	hipEvent_t mm_ev[4] = {nullptr, nullptr, nullptr, nullptr};
 	// host-wrapper scratch (Arena): one device block reused call after call
 	uint8_t* arena = nullptr;
 	size_t arena_cap = 0, arena_used = 0, arena_need = 0;
@@ -523,6 +526,9 @@ int bt2g_close(bt2g_ctx* c) {
 	if(c->bt_plane) { (void)hipFree(c->bt_plane); (void)hipFree(c->bt_marks); }
 	if(c->arena) (void)hipFree(c->arena);
 	if(c->pin) (void)hipHostFree(c->pin);
+	for(hipEvent_t& e : c->mm_ev)
+		if(e) (void)hipEventDestroy(e);
+	if(c->aux) (void)hipStreamDestroy(c->aux);
 	if(c->stream) (void)hipStreamDestroy(c->stream);
 	delete c;
 	return BT2G_OK;
@@ -625,6 +631,17 @@ static int one_mm_impl(bt2g_ctx* c, const uint8_t* reads, const uint8_t* quals, 
 	if(cap == 0) return fail(BT2G_ERR_ARG, "cap must be > 0");
 	if(n == 0) return BT2G_OK;
 	hipStream_t st = pick(c, stream);
+	if(!c->aux) {
+		// the second direction's stream (created once; without it the directions run in turn)
+		bool ok = hipStreamCreateWithFlags(&c->aux, hipStreamNonBlocking) == hipSuccess;
+		for(int i = 0; ok && i < 4; i++) ok = hipEventCreateWithFlags(&c->mm_ev[i], hipEventDisableTiming) == hipSuccess;
+		if(!ok) {
+			for(hipEvent_t& e : c->mm_ev)
+				if(e) { (void)hipEventDestroy(e); e = nullptr; }
+			if(c->aux) (void)hipStreamDestroy(c->aux);
+			c->aux = nullptr;
+		}
+	}
 	OneMmScratch s;
 	HIPCHK(amalloc(c, (void**)&s.slots, sizeof(bt2g_mm1) * (size_t)n * 4 * cap, st));
 	HIPCHK(amalloc(c, (void**)&s.slot_counts, sizeof(int32_t) * (size_t)n * 4, st));
@@ -647,7 +664,7 @@ static int one_mm_impl(bt2g_ctx* c, const uint8_t* reads, const uint8_t* quals, 
 		ProfScope ps(c, 2, st);
 		launch_one_mm(c->fw, c->bw, reads, quals, stride, lens, n, minsc, *sc, nofw, norc, gate, cap, s.items,
 		              (uint32_t*)s.ovf + 1, s.near_state, s.near_dep, s.slots, s.slot_counts, hits, counts, bwops,
-		              loads, s.ovf, s.brq, brq_cap, s.fb_items, s.fb_st4, s.fb_sdep, s.slot_flag, st);
+		              loads, s.ovf, s.brq, brq_cap, s.fb_items, s.fb_st4, s.fb_sdep, s.slot_flag, st, c->aux, c->aux ? c->mm_ev : nullptr);
 	}
 	HIPCHK(hipGetLastError());
 	int32_t ovf = 0;

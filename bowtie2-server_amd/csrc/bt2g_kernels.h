@@ -46,14 +46,18 @@ void launch_one_mm_q(const DevEbwt& F, const DevEbwt& B, const uint8_t* reads, c
                      int norc, const uint32_t* gate, uint32_t cap, uint32_t* items, uint32_t* counters,
                      uint4* near_state, uint32_t* near_dep, bt2g_mm1* slots, int32_t* slot_counts, uint32_t* ops,
                      uint32_t* loads, MmBranch* brq, uint32_t brq_cap, uint32_t* fb_items, uint4* fb_st4,
-                     uint32_t* fb_sdep, uint32_t* slot_flag, hipStream_t st);
+                     uint32_t* fb_sdep, uint32_t* slot_flag, hipStream_t st, hipStream_t st2 = nullptr,
+                     hipEvent_t* ev = nullptr);
+// st2 / ev (4 events, optional): the second index direction's kernels on st2
+// (fork from st, join back): each direction's kernels last as long as their
+// longest walk, so the two directions overlap instead of running back to back
 void launch_one_mm(const DevEbwt& F, const DevEbwt& B, const uint8_t* reads, const uint8_t* quals, uint32_t stride,
                    const uint32_t* lens, uint32_t n, const int32_t* minsc, const bt2g_scoring& sc, int nofw,
                    int norc, const uint32_t* gate, uint32_t cap, uint32_t* items, uint32_t* counters,
                    uint4* near_state, uint32_t* near_dep, bt2g_mm1* slots, int32_t* slot_counts, bt2g_mm1* hits,
                    int32_t* counts, uint32_t* ops, uint32_t* loads, int32_t* overflow, MmBranch* brq,
                    uint32_t brq_cap, uint32_t* fb_items, uint4* fb_st4, uint32_t* fb_sdep, uint32_t* slot_flag,
-                   hipStream_t st);
+                   hipStream_t st, hipStream_t st2 = nullptr, hipEvent_t* ev = nullptr);
 void launch_get_offset(const DevEbwt& e, const uint32_t* rows, uint32_t n, uint32_t* offs, uint32_t* loads,
                        hipStream_t st);
 void launch_sw_partition(const bt2g_sw_problem* probs, uint32_t nprob, int local, int enable8, uint32_t* list8,

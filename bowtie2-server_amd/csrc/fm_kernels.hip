@@ -303,10 +303,10 @@ void launch_one_mm(const DevEbwt& F, const DevEbwt& B, const uint8_t* reads, con
                    uint4* near_state, uint32_t* near_dep, bt2g_mm1* slots, int32_t* slot_counts, bt2g_mm1* hits,
                    int32_t* counts, uint32_t* ops, uint32_t* loads, int32_t* overflow, MmBranch* brq,
                    uint32_t brq_cap, uint32_t* fb_items, uint4* fb_st4, uint32_t* fb_sdep, uint32_t* slot_flag,
-                   hipStream_t st) {
+                   hipStream_t st, hipStream_t st2, hipEvent_t* ev) {
 	launch_one_mm_q(F, B, reads, quals, stride, lens, n, minsc, sc, nofw, norc, gate, cap, items, counters,
 	                near_state, near_dep, slots, slot_counts, ops, loads, brq, brq_cap, fb_items, fb_st4, fb_sdep,
-	                slot_flag, st);
+	                slot_flag, st, st2, ev);
 	hipLaunchKernelGGL(k_one_mm_compact, dim3((n + 255) / 256), dim3(256), 0, st, slots, slot_counts, n, cap, hits,
 	                   counts, overflow);
 }

@@ -729,36 +729,54 @@ void launch_one_mm_q(const DevEbwt& F, const DevEbwt& B, const uint8_t* reads, c
                      int norc, const uint32_t* gate, uint32_t cap, uint32_t* items, uint32_t* counters,
                      uint4* near_state, uint32_t* near_dep, bt2g_mm1* slots, int32_t* slot_counts, uint32_t* ops,
                      uint32_t* loads, MmBranch* brq, uint32_t brq_cap, uint32_t* fb_items, uint4* fb_st4,
-                     uint32_t* fb_sdep, uint32_t* slot_flag, hipStream_t st) {
+                     uint32_t* fb_sdep, uint32_t* slot_flag, hipStream_t st, hipStream_t st2, hipEvent_t* ev) {
 	MmParams P{sc.match, sc.mmp_max, sc.mmp_min, sc.npen, sc.local, 0, 0};
+	// the BWT' direction's kernels on s2 (st2, forked from st and joined back), or after the BWT ones on st
+	const bool two = st2 != nullptr && ev != nullptr;
+	hipStream_t s2 = two ? st2 : st;
 	// counters[0]/[2] = item counts of the BWT / BWT' lists (zeroed by the caller)
 	hipLaunchKernelGGL(k_one_mm_items, dim3((n + 255) / 256), dim3(256), 0, st, reads, stride, lens, n, gate, nofw,
 	                   norc, items, counters, slot_counts);
 	const uint32_t grid = (2 * n + 255) / 256;   // list capacity; lanes past the count exit
 	const size_t half = 2 * (size_t)n;
+	(void)hipMemsetAsync(slot_flag, 0, sizeof(uint32_t) * (size_t)n * 4, st);
+	if(two) {
+		(void)hipEventRecord(ev[0], st);
+		(void)hipStreamWaitEvent(s2, ev[0], 0);
+	}
+	// near half, far half (lean; branches to the queue, shared by both directions),
+	// then the state machine for the items that met a full queue (counters[5] / [6];
+	// it walks in place: no queue, its own dummy head counters[7])
 	hipLaunchKernelGGL(k_one_mm_near<true>, dim3(grid), dim3(256), 0, st, F, B, reads, stride, lens, items, counters,
 	                   near_state, near_dep, ops, loads);
-	hipLaunchKernelGGL(k_one_mm_near<false>, dim3(grid), dim3(256), 0, st, F, B, reads, stride, lens, items + half,
+	hipLaunchKernelGGL(k_one_mm_near<false>, dim3(grid), dim3(256), 0, s2, F, B, reads, stride, lens, items + half,
 	                   counters + 2, near_state + half, near_dep + half, ops, loads);
-	// far halves (lean; branches to the queue), then the state machine for the items that met a
-	// full queue (counters[5] / [6]; it walks in place: no queue, its own dummy head counters[7]),
-	// then every queued branch
-	(void)hipMemsetAsync(slot_flag, 0, sizeof(uint32_t) * (size_t)n * 4, st);
 	hipLaunchKernelGGL(k_one_mm_far<true>, dim3(grid), dim3(256), 0, st, F, B, reads, quals, stride, lens, minsc, P,
 	                   sc.ncl_const, sc.ncl_lin, items, counters, near_state, near_dep, cap, slots, slot_counts, ops,
 	                   loads, brq, counters + 4, brq_cap, fb_items, fb_st4, fb_sdep, counters + 5, slot_flag);
-	hipLaunchKernelGGL(k_one_mm_far<false>, dim3(grid), dim3(256), 0, st, F, B, reads, quals, stride, lens, minsc, P,
+	hipLaunchKernelGGL(k_one_mm_far<false>, dim3(grid), dim3(256), 0, s2, F, B, reads, quals, stride, lens, minsc, P,
 	                   sc.ncl_const, sc.ncl_lin, items + half, counters + 2, near_state + half, near_dep + half, cap,
 	                   slots, slot_counts, ops, loads, brq, counters + 4, brq_cap, fb_items + half, fb_st4 + half,
 	                   fb_sdep + half, counters + 6, slot_flag);
 	hipLaunchKernelGGL(k_one_mm_q<true>, dim3(grid), dim3(256), 0, st, F, B, reads, quals, stride, lens, minsc, P,
 	                   sc.ncl_const, sc.ncl_lin, fb_items, counters + 5, fb_st4, fb_sdep, cap, slots, slot_counts, ops,
 	                   loads, brq, counters + 7, 0u);
-	hipLaunchKernelGGL(k_one_mm_q<false>, dim3(grid), dim3(256), 0, st, F, B, reads, quals, stride, lens, minsc, P,
+	hipLaunchKernelGGL(k_one_mm_q<false>, dim3(grid), dim3(256), 0, s2, F, B, reads, quals, stride, lens, minsc, P,
 	                   sc.ncl_const, sc.ncl_lin, fb_items + half, counters + 6, fb_st4 + half, fb_sdep + half, cap,
 	                   slots, slot_counts, ops, loads, brq, counters + 7, 0u);
+	if(two) {
+		// every branch is queued (both far kernels) before either branch kernel runs
+		(void)hipEventRecord(ev[1], s2);
+		(void)hipStreamWaitEvent(st, ev[1], 0);
+		(void)hipEventRecord(ev[2], st);
+		(void)hipStreamWaitEvent(s2, ev[2], 0);
+	}
 	hipLaunchKernelGGL(k_one_mm_branch<true>, dim3((brq_cap + 255) / 256), dim3(256), 0, st, F, B, reads, stride,
 	                   lens, brq, counters + 4, brq_cap, cap, slots, slot_counts, ops, loads, slot_flag);
-	hipLaunchKernelGGL(k_one_mm_branch<false>, dim3((brq_cap + 255) / 256), dim3(256), 0, st, F, B, reads, stride,
+	hipLaunchKernelGGL(k_one_mm_branch<false>, dim3((brq_cap + 255) / 256), dim3(256), 0, s2, F, B, reads, stride,
 	                   lens, brq, counters + 4, brq_cap, cap, slots, slot_counts, ops, loads, slot_flag);
+	if(two) {
+		(void)hipEventRecord(ev[3], s2);
+		(void)hipStreamWaitEvent(st, ev[3], 0);
+	}
 }
