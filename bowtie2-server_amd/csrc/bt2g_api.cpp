@@ -889,12 +889,15 @@ int bt2g_sw_align_bt_dev(bt2g_ctx* c, const uint8_t* reads, const uint8_t* quals
 	}
 	// systolic fill: bottom-aligned rows, u8 (hb 1) or u16 plane with block masks;
 	// one-problem-per-lane fills (local, other scorings): top-aligned u16 plane
-	const int kind = hb == 1 ? 0 : 1;
+	// u8 fills: the fill writes the walk's decision per cell (kind 2, 4 bits);
+	// BT2G_BT_HPLANE=1 keeps the H score plane (kind 0) for A/B runs
+	static const bool hplane = [] { const char* e = getenv("BT2G_BT_HPLANE"); return e && *e == '1'; }();
+	const int kind = hb == 1 ? (hplane || sc->local ? 0 : 2) : 1;
 	a.plane = plane;
 	a.slot = sw_plane_slot(stride, maxcol, hb);
 	a.plane_top = !packed ? 1 : sc->local ? 2 : 0;
 	if((rc = sw_align_impl(c, reads, quals, stride, lens, probs, nprob, windows, sc, enable8, cap, res, cands,
-	                       nullptr, nullptr, plane, a.slot, hb, maxcol, st)))
+	                       nullptr, nullptr, plane, a.slot, kind == 2 ? 3 : hb, maxcol, st)))
 		return rc;
 	a.rwords = sw_bt_rcols(maxrow, maxcol);
 	a.rrows = sw_bt_rrows(maxrow);

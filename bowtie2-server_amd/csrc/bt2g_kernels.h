@@ -135,7 +135,7 @@ struct BtArgs {
 	bt2g_edit* edits;
 	int8_t* fates;                    // may be null
 };
-// kind: 0 u8 score plane, 1 u16 score plane
+// kind: 0 u8 score plane, 1 u16 score plane, 2 decision nibbles (end-to-end u8 fills)
 void launch_sw_bt(int kind, const BtArgs& a, hipStream_t st);
 
 // backtrace mark scratch per problem of <= rows x cols (sw_backtrace.hip):

@@ -152,8 +152,8 @@ k_sw_bt(BtArgs A) {
 	uint32_t pad = 0;
 	const uint8_t* slot = nullptr;
 	{
-		if(KIND == 0 && variant != 0) { A.naln[p] = -4; return; }   // i16 fill, u8-only plane
-		const size_t es = KIND == 0 ? 1 : 2;
+		if(KIND != 1 && variant != 0) { A.naln[p] = -4; return; }   // i16 fill, u8-only plane
+		const size_t es = KIND == 1 ? 2 : 1;   // kind 2: the u8 plane's layout, 8 B per block column
 		// systolic end-to-end: last row at the stack bottom; one-problem-per-lane
 		// fills: top-aligned; systolic local: padded rows (round16) at the bottom
 		pad = A.plane_top == 1 ? 0u : A.cstride - (A.plane_top == 2 ? ((nrow + 15u) & ~15u) : nrow);
@@ -373,6 +373,11 @@ k_sw_bt(BtArgs A) {
 		}
 		return (int32_t)((const uint8_t*)myc)[(c - cc0) * 16u + (rsx & 15u)] - pl.off;
 	};
+	// KIND 2: the decision nibbles (sw_ee_packed.hip DEC) through a copy of
+	// BT_DCH columns x 16 rows (8 B per column) in the lane's LDS region, loaded
+	// in the walk step together with its reportedThrough tile (one round trip)
+	constexpr uint32_t BT_DCH = 2u * BT_CHUNK;
+	uint32_t db = 0xffffffffu, dc0 = 0;
 	const uint32_t ncand = (uint32_t)R.ncand < A.cap ? (uint32_t)R.ncand : A.cap;
 	const bt2g_sw_cand* cl = A.cands + (size_t)p * A.cap;
 	// local mode, FILT_DOMINATED (aligner_sw.cpp nextAlignment): a candidate
@@ -505,8 +510,83 @@ k_sw_bt(BtArgs A) {
 		bool ended = false;
 		uint32_t ks = 0;
 		do {
-		BTC(1);
-		{
+		uint32_t nb2 = 0;   // KIND 2: the cell's decision nibble
+		if constexpr(KIND == 2) {
+			// Gap-barrier rows allow diagonal moves only (E and F are vetoed there):
+			// no nibble.  The bottom ones are never marked (see below).  Every load
+			// of the step (tile, its valid word, the nibble chunk and its block
+			// masks) is issued before any store or use: one round trip per step.
+			const bool bbar = row + (uint32_t)gb >= nrow, bar = bbar || row < (uint32_t)gb;
+			const bool mk = wmark && !bbar;
+			const uint32_t tr = row >> 3, tc = col >> 3;
+			const bool tnew = mk && (tr != ttr || tc != ttc);
+			const uint32_t vi = tr * vw + (tc >> 5);
+			const bool vnew = tnew && vi != vidx;
+			uint64_t tl = 0;
+			uint32_t nv = 0;
+			if(tnew) tl = *(const uint64_t*)(marks + ((size_t)tr * tcols + tc) * 2u);
+			if(vnew) nv = valid[vi];
+			const bool needd = (st != ST_H || !bar) && row > 0;
+			const uint32_t rsx = pad + row, b = rsx >> 4;
+			const bool dnew = needd && (b != db || col < dc0 || col > dc0 + (BT_DCH - 1u));
+			// (leaving the inner loop at the first step that needs a load, so that
+			// a wave's loads go out together: measured slower, 28.2 vs 25.1 ms)
+			BTC(1);
+			uint4 ch[BT_DCH / 2u];
+			uint32_t ndc0 = dc0;
+			if(dnew) {
+				// the walk moves left: the chunk ends near column col (even start: 16-B loads)
+				ndc0 = (col >= BT_DCH - 2u ? col - (BT_DCH - 2u) : 0u) & ~1u;
+				if(ndc0 + BT_DCH > A.pcols) ndc0 = A.pcols >= BT_DCH ? A.pcols - BT_DCH : 0u;
+				const uint4* qp = (const uint4*)(slot + ((size_t)b * A.pcols + ndc0) * 8u);
+#pragma unroll
+				for(uint32_t u = 0; u < BT_DCH / 2u; u++) ch[u] = ndc0 + 2u * u < A.pcols ? qp[u] : make_uint4(0u, 0u, 0u, 0u);
+			}
+			if(tnew) {
+				BTC(9);
+				// the cached valid word is the old tile's (it was switched in with it)
+				if(tdirty) {
+					BTC(10);
+					*(uint64_t*)(marks + ((size_t)ttr * tcols + ttc) * 2u) = tbits;
+					vval |= 1u << (ttc & 31u);
+					vdirty = true;
+					tdirty = false;
+				}
+				if(vnew) {
+					if(vdirty) valid[vidx] = vval;
+					vidx = vi;
+					vval = nv;
+					vdirty = false;
+				}
+				ttr = tr;
+				ttc = tc;
+				tbits = ((vval >> (tc & 31u)) & 1u) ? tl : 0ull;
+			}
+			if(dnew) {
+				BTC(8);
+				db = b;
+				dc0 = ndc0;
+				// (no block masks: a walked cell is >= the candidate's score >= minsc,
+				// so its block was written; unwritten columns of a chunk are never read)
+#pragma unroll
+				for(uint32_t u = 0; u < BT_DCH / 2u; u++) {
+					myc[4u * u] = ch[u].x; myc[4u * u + 1u] = ch[u].y; myc[4u * u + 2u] = ch[u].z; myc[4u * u + 3u] = ch[u].w;
+				}
+			}
+			if(mk) {
+				// reportedThrough (aligner_swsse_ee_u8.cpp:1331-1336, 1556)
+				const uint64_t bt = rbit(row, col);
+				if(tbits & bt) { w.ok = false; ended = true; }
+				else { tbits |= bt; tdirty = true; }
+			}
+			if(needd) {
+				// row 4q+i of the block is nibble 4q+3-i of the column's 8 bytes
+				const uint32_t rr = rsx & 15u, nbi = (rr & ~3u) + 3u - (rr & 3u);
+				const uint32_t by = ((const uint8_t*)myc)[(col - dc0) * 8u + (nbi >> 1)];
+				nb2 = (by >> (4u * (nbi & 1u))) & 15u;
+			}
+		} else {
+			BTC(1);
 			// end-to-end: every candidate starts in the last row and the bottom
 			// gap-barrier rows allow only diagonal moves, so walks there stay on
 			// their own diagonals and can neither meet nor be met: no marks
@@ -525,9 +605,32 @@ k_sw_bt(BtArgs A) {
 			if(row == 0) ended = true;
 		}
 		if(!ended) {
-			const int rc = rd_at(row), m = rf_at(col), q = q_at(row);
+			int rc = 0, m = 0, q = 0;
 			int mv = -1;   // 0 diag, 1 ref open, 2 ref extend, 3 read open, 4 read extend
 			int32_t nxt = 0;
+			if constexpr(KIND == 2) {
+			// the fill's decision (sw_ee_packed.hip DEC): bit 0 not diag, bit 1 not
+			// from F, bit 2 F not opened from H(up), bit 3 E not opened from H(left)
+			const uint32_t nb = nb2;
+			if(st == ST_H) {
+				if(!gaps_ok(row)) { if(col > 0) mv = 0; }   // barrier rows: diagonal only
+				else if(!(nb & 1u) && col > 0) mv = 0;
+				else if(gaps_ok(row)) {
+					if(!(nb & 2u)) mv = (nb & 4u) ? 2 : 1;
+					else if(col > 0) mv = (nb & 8u) ? 4 : 3;
+				}
+				if(mv < 0) ended = true;   // empty cell: the alignment starts here
+			} else if(st == ST_E) {
+				if(col == 0) ended = true;   // unreachable: E(row, 0) is the floor
+				mv = (nb & 8u) ? 4 : 3;
+			} else {
+				mv = (nb & 4u) ? 2 : 1;
+			}
+			// characters only for a walk that writes its edits (a failing walk
+			// needs none; a later walk that succeeds is replayed with them)
+			if(!ended && wemit) { rc = rd_at(row); m = rf_at(col); if(mv == 0) q = q_at(row); }
+			} else {
+			rc = rd_at(row); m = rf_at(col); q = q_at(row);
 			// in gap-barrier rows H is the diagonal term itself when above the
 			// floor (E and F are the floor there): H(up-left) = cur - score, no load
 			const bool derive = st == ST_H && !gaps_ok(row) && (!local || cur > 0);
@@ -607,6 +710,7 @@ k_sw_bt(BtArgs A) {
 				if(okv(hu) && hu - rfgo == cur) { mv = 1; nxt = hu; }
 				else { mv = 2; nxt = cur + rfge; }
 			}
+			}   // KIND
 			if(!ended) {
 				if(mv == 0) {
 					const int mt = (m >= 16 || rc > 3) ? -1 : ((m >> rc) & 1);
@@ -639,7 +743,7 @@ k_sw_bt(BtArgs A) {
 		w.row = row;
 		w.col = col;
 		if(w.ok && !w.core) w.ok = false;            // must touch a core diagonal
-		if(w.ok) {
+		if(w.ok && (KIND != 2 || wemit)) {
 			const int rc = rd_at(row), m = rf_at(col);
 			const int mt = (m >= 16 || rc > 3) ? -1 : ((m >> rc) & 1);
 			if(mt != 1) {
@@ -750,6 +854,7 @@ void launch_sw_bt(int kind, const BtArgs& a, hipStream_t st) {
 		hipLaunchKernelGGL((k_sw_bt<1, true>), grid, block, 0, st, a);
 	} else {
 		if(kind == 0) hipLaunchKernelGGL((k_sw_bt<0, false>), grid, block, 0, st, a);
+		else if(kind == 2) hipLaunchKernelGGL((k_sw_bt<2, false>), grid, block, 0, st, a);
 		else hipLaunchKernelGGL((k_sw_bt<1, false>), grid, block, 0, st, a);
 	}
 }

@@ -116,7 +116,17 @@ struct Half {
 // column j at plane + pi*hslot + ((k*max_cols + j)*16)*hbytes, so that a
 // backtrace step (up-left) usually stays inside one 128-B line; hbytes 1 keeps
 // u8 fills only.
-template <bool LOCAL, bool SAMEGO, bool STORE>
+// DEC (end-to-end, u8 fills): instead of H, the backtrace's decision at every
+// cell as a nibble (the "decision plane", 8 B per 16-row block column, row
+// 4q+i as nibble 4q+3-i, little-endian nibbles): the reference's walk
+// (aligner_swsse_ee_u8.cpp:1357-1540) picks, in H state, diag > H-up > F-up >
+// H-left > E-left, in F state H-up > F-up, in E state H-left > E-left; with
+// H = max(diag, E, F) and every walked cell above the floor that is
+//   bit 0  H != diag              bit 1  H != F
+//   bit 2  F != H(up) - rfgo      bit 3  E != H(left) - rdgo
+// (F-up / E-left being then the other source of F / E).  A walk step reads
+// one nibble and no neighbour, no column or row scan (sw_backtrace.hip KIND 2).
+template <bool LOCAL, bool SAMEGO, bool STORE, bool DEC = false>
 __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu((STORE || LOCAL) ? BT2G_SW_WAVES_STORE : BT2G_SW_WAVES)))
 k_sw_sys(const bt2g_sw_problem* __restrict__ probs, uint32_t nprob, const uint8_t* __restrict__ reads,
             const uint8_t* __restrict__ quals, uint32_t stride, const uint32_t* __restrict__ lens,
@@ -359,6 +369,11 @@ k_sw_sys(const bt2g_sw_problem* __restrict__ probs, uint32_t nprob, const uint8_
 					int code = v[x][u] == 0x100u ? 4 : v[x][u] == 0x200u ? 0
 					         : (masks[x] ? first5((int)v[x][u]) : (int)v[x][u]);
 					sel |= (code < 4 ? (uint32_t)(4 * x + code) : 0x0cu) << (16 * x);
+					// DEC: an ambiguous reference mask (IUPAC, caller windows only) in the
+					// otherwise unused selector byte: the fill scores its first base
+					// (firsts5) but the walk's diagonal test matches any of its bases
+					if(DEC && masks[x] && v[x][u] < 16u && __popc(v[x][u]) > 1)
+						sel = (sel & ~(0xff00u << (16 * x))) | ((0x80u | v[x][u]) << (8 + 16 * x));
 					// the gather's reference mask (aligner_sw.cpp:247-253: 1 << c, N -> 16)
 					const uint32_t m = v[x][u] == 0x100u ? 16u : v[x][u] == 0x200u ? 0u
 					                 : (masks[x] ? v[x][u] : (v[x][u] > 3u ? 16u : 1u << v[x][u]));
@@ -473,6 +488,21 @@ k_sw_sys(const bt2g_sw_problem* __restrict__ probs, uint32_t nprob, const uint8_
 		               ? (uint32_t)h[x].minsc : 0x10000u;
 	const uint32_t cthr = ((ctest[0] - 1u) & 0xffffu) | (((ctest[1] - 1u) & 0xffffu) << 16);
 	const uint32_t match2 = (uint32_t)C.match * 0x10001u, npm2 = (uint32_t)(C.match + C.npen) * 0x10001u;
+	// DEC: this column's decision nibbles (rows 4q..4q+3 in Dw[q], row 4q+i in
+	// nibble 3-i of each half: Horner steps by 16, an inline constant) and the
+	// E bits of the next column, known one column early (Dn, bit 0 of each
+	// nibble until the column's end)
+	uint32_t Dw[4] = {0u, 0u, 0u, 0u}, Dn[4] = {0u, 0u, 0u, 0u};
+	const uint32_t one2 = 0x00010001u;
+	// (t* are 0 / 1 per half: 32-bit shifts never carry a bit across the halves
+	// within 4 rows, and v_lshl_or_b32 issues at the full rate)
+	auto dec_cell = [&](int i, uint32_t t0, uint32_t t1, uint32_t t2) {
+		const uint32_t nb = (t2 << 2) | (t1 << 1) | t0;
+		Dw[i >> 2] = (i & 3) ? (Dw[i >> 2] << 4) | nb : nb;
+	};
+	auto dec_next = [&](int i, uint32_t t3) {
+		Dn[i >> 2] = (i & 3) ? (Dn[i >> 2] << 4) | t3 : t3;
+	};
 	for(uint32_t t = 0; t < T; t++) {
 		// the lane above computed this lane's column in the previous step (DPP wave_shr:1)
 		const uint32_t hin = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)hout, 0x138, 0xf, 0xf, false);
@@ -481,8 +511,16 @@ k_sw_sys(const bt2g_sw_problem* __restrict__ probs, uint32_t nprob, const uint8_
 		const uint32_t cmin = LOCAL ? (uint32_t)__builtin_amdgcn_update_dpp(0, (int)cmout, 0x138, 0xf, 0xf, false) : 0u;
 		const int j = (int)t - (int)k;
 		if(j < 0 || j >= (int)ncolmax) continue;
-		const uint32_t sel = nsel;
+		const uint32_t selx = nsel;
+		// DEC: ambiguous columns of this step (bytes 1 / 3 of the selector); their
+		// diagonal term for the decision nibble is H(up-left) - the smallest
+		// profile penalty over the mask's bases (Scoring::score with the mask)
+		const bool amb = DEC && __ballot((selx & 0x80008000u) != 0u);
+		const uint32_t sel = DEC ? ((selx & 0x00ff00ffu) | 0x0c000c00u) : selx;
 		if(in_group) nsel = mysel[(uint32_t)j + 1 < ncolmax ? j + 1 : j];   // next step's column
+		uint32_t Dp[4];   // DEC: bit 3 of this column's nibbles (from the previous column)
+#pragma unroll
+		for(int q = 0; q < 4; q++) Dp[q] = DEC ? Dn[q] << 3 : 0u;
 		uint32_t hup, fup, diag;
 		if(top) {
 			hup = 0;
@@ -502,8 +540,9 @@ k_sw_sys(const bt2g_sw_problem* __restrict__ probs, uint32_t nprob, const uint8_
 		const uint32_t ncm = ((sel & 0xffu) == 0x0cu ? 0xffffu : 0u) | (((sel >> 16) & 0xffu) == 0x0cu ? 0xffff0000u : 0u);
 		const uint32_t nfloor = ncm & ((uint32_t)npen * 0x10001u);
 		uint32_t fprev = fup, hprev = SAMEGO ? psub(hup, rfgo2) : hup;
-		auto rows = [&](auto n_tag) {
+		auto rows = [&](auto n_tag, auto a_tag) {
 			constexpr bool NCOL = decltype(n_tag)::value;
+			constexpr bool AMB = DEC && decltype(a_tag)::value;
 #pragma unroll
 			for(int i = 0; i < R; i++) {
 				uint32_t pen = __builtin_amdgcn_perm(PB[i], PA[i], sel);
@@ -523,21 +562,51 @@ k_sw_sys(const bt2g_sw_problem* __restrict__ probs, uint32_t nprob, const uint8_
 				}
 				// local: H(up-left) + match - pen' (no carry between the halves: H < 2^15)
 				const uint32_t d = LOCAL ? psub(diag + match2, pen) : psub(diag, pen);
+				uint32_t dwalk = d;   // DEC: the walk's diagonal term
+				if(AMB) {
+					// (rare: recomputed per row rather than held in registers)
+					uint32_t pm = 0xffffffffu;
+#pragma unroll
+					for(int c = 0; c < 4; c++) {
+						const uint32_t nm = (((selx >> (8 + c)) & 1u) ? 0u : 0xffffu) | (((selx >> (24 + c)) & 1u) ? 0u : 0xffff0000u);
+						pm = pmin(pm, __builtin_amdgcn_perm(PB[i], PA[i], 0x0c000c00u | (uint32_t)c | ((4u + (uint32_t)c) << 16)) | nm);
+					}
+					const uint32_t ah = ((selx & 0x8000u) ? 0xffffu : 0u) | ((selx & 0x80000000u) ? 0xffff0000u : 0u);
+					dwalk = (psub(diag, pm) & ah) | (d & ~ah);
+				}
 				if(SAMEGO) {
 					// read and reference gap opens equal: H - open serves the F of the
 					// next row and the E of the next column (one subtract less)
 					const uint32_t f = pmax(psub(fprev, rfge2), hprev) & M[i];
 					const uint32_t hh = pmax(pmax(d, E[i]), f);
 					const uint32_t hg = psub(hh, rdgo2);
-					E[i] = pmax(psub(E[i], rdge2), hg & M[i]);
+					if(DEC) {
+						// hprev: H(up) - rfgo
+						dec_cell(i, pmin(psub(hh, dwalk), one2), pmin(psub(hh, f), one2), pmin(psub(f, hprev), one2));
+						const uint32_t hgm = hg & M[i];
+						const uint32_t en = pmax(psub(E[i], rdge2), hgm);
+						dec_next(i, pmin(psub(en, hgm), one2));
+						E[i] = en;
+					} else {
+						E[i] = pmax(psub(E[i], rdge2), hg & M[i]);
+					}
 					diag = Hc[i];
 					Hc[i] = hh;
 					fprev = f;
 					hprev = hg;          // carries H - open
 				} else {
-					const uint32_t f = pmax(psub(fprev, rfge2), psub(hprev, rfgo2)) & M[i];
+					const uint32_t huo = psub(hprev, rfgo2);
+					const uint32_t f = pmax(psub(fprev, rfge2), huo) & M[i];
 					const uint32_t hh = pmax(pmax(d, E[i]), f);
-					E[i] = pmax(psub(E[i], rdge2), psub(hh, rdgo2) & M[i]);
+					if(DEC) {
+						dec_cell(i, pmin(psub(hh, dwalk), one2), pmin(psub(hh, f), one2), pmin(psub(f, huo), one2));
+						const uint32_t hgm = psub(hh, rdgo2) & M[i];
+						const uint32_t en = pmax(psub(E[i], rdge2), hgm);
+						dec_next(i, pmin(psub(en, hgm), one2));
+						E[i] = en;
+					} else {
+						E[i] = pmax(psub(E[i], rdge2), psub(hh, rdgo2) & M[i]);
+					}
 					diag = Hc[i];
 					Hc[i] = hh;
 					fprev = f;
@@ -545,8 +614,13 @@ k_sw_sys(const bt2g_sw_problem* __restrict__ probs, uint32_t nprob, const uint8_
 				}
 			}
 		};
-		if(__ballot(ncm != 0)) rows(std::true_type{});
-		else rows(std::false_type{});
+		if(amb) {
+			if(__ballot(ncm != 0)) rows(std::true_type{}, std::true_type{});
+			else rows(std::false_type{}, std::true_type{});
+		} else {
+			if(__ballot(ncm != 0)) rows(std::true_type{}, std::false_type{});
+			else rows(std::false_type{}, std::false_type{});
+		}
 		// this lane's block maxima (rows 0..7 and all): block masks, local column maxima
 		uint32_t mlo = 0, mx = 0;
 		if(LOCAL || (STORE && use_mask)) {
@@ -626,7 +700,18 @@ k_sw_sys(const bt2g_sw_problem* __restrict__ probs, uint32_t nprob, const uint8_
 #ifdef BT2G_SW_STORE_TINY
 			const uint64_t hslot = 0;                 // timing experiments only: all writes in 64 KB
 #endif
-			if(!LOCAL && hbytes == 1) {
+			if(DEC) {
+				// the decision nibbles of 16 rows: 8 B per problem
+#pragma unroll
+				for(int q = 0; q < 4; q++) Dw[q] |= Dp[q];
+				const uint32_t a0 = __builtin_amdgcn_perm(Dw[1], Dw[0], 0x05040100u);
+				const uint32_t a1 = __builtin_amdgcn_perm(Dw[3], Dw[2], 0x05040100u);
+				const uint32_t b0 = __builtin_amdgcn_perm(Dw[1], Dw[0], 0x07060302u);
+				const uint32_t b1 = __builtin_amdgcn_perm(Dw[3], Dw[2], 0x07060302u);
+				const size_t cell8 = ((size_t)k * pitch + (uint32_t)j) * 8u;
+				if(s0 && h[0].row0 == 0xffu) *(uint2*)(plane + (size_t)h[0].pi * hslot + cell8) = make_uint2(a0, a1);
+				if(s1 && h[1].row0 == 0xffu) *(uint2*)(plane + (size_t)h[1].pi * hslot + cell8) = make_uint2(b0, b1);
+			} else if(!LOCAL && hbytes == 1) {
 				// bytes of 16 rows per problem: low halves -> a, high halves -> b
 				uint32_t a[4], b[4];
 #pragma unroll
@@ -798,8 +883,8 @@ void launch_sw_packed(bool local, const bt2g_sw_problem* probs, uint32_t nprob, 
 	const uint32_t ldsw = (max_cols + 1u) | 1u;   // >= ncol+1 (column pairs); odd: groups hit different banks
 	const dim3 grid((nprob + per_wave - 1) / per_wave), block(64);
 	const size_t lds = (per_wave / 2) * sw_packed_group_words(max_cols, local) * sizeof(uint32_t);
-#define BT2G_SYS(LO, SG, STO)                                                                                 \
-	hipLaunchKernelGGL((k_sw_sys<LO, SG, STO>), grid, block, lds, st, probs, nprob, reads, quals, stride, lens, \
+#define BT2G_SYS(LO, SG, STO, ...)                                                                             \
+	hipLaunchKernelGGL((k_sw_sys<LO, SG, STO, ##__VA_ARGS__>), grid, block, lds, st, probs, nprob, reads, quals, stride, lens, \
 	                   windows, ref_codes, ref_starts, C, enable8, cap, max_cols, S, ldsw, res, cands, plane, hslot, \
 	                   hbytes)
 	const bool samego = C.rdgo == C.rfgo;
@@ -809,6 +894,10 @@ void launch_sw_packed(bool local, const bt2g_sw_problem* probs, uint32_t nprob, 
 		} else {
 			if(samego) BT2G_SYS(true, true, false); else BT2G_SYS(true, false, false);
 		}
+	} else if(plane && hbytes == 3) {
+		// decision nibbles (the plane's u8 layout: masks after 16S x pitch bytes)
+		hbytes = 1;
+		if(samego) BT2G_SYS(false, true, true, true); else BT2G_SYS(false, false, true, true);
 	} else if(plane) {
 		if(samego) BT2G_SYS(false, true, true); else BT2G_SYS(false, false, true);
 	} else {

@@ -23,6 +23,8 @@ ap.add_argument("--n", type=int, default=1_000_000)
 ap.add_argument("--iters", type=int, default=3)
 ap.add_argument("--genome-mb", type=float, default=20)
 ap.add_argument("--maxaln", type=int, default=8)
+ap.add_argument("--save", default="", help="write naln/alns/edits (npz) for an A/B comparison")
+ap.add_argument("--compare", default="", help="compare with a --save file")
 a = ap.parse_args()
 parts, names = bench.make_genome(a.genome_mb)
 g = parts[0]
@@ -120,4 +122,18 @@ nal = naln.cpu().numpy()
 nc = res[:, 6].cpu().numpy()
 print(f"lib={os.path.basename(bt2g.LIB_PATH)} n={n} fill {f[1]/f[0]:.3f} ms  backtrace {b[1]/b[0]:.3f} ms  "
       f"aligned {(nal > 0).mean():.4f} alns {nal.clip(0).sum()} mean ncand {nc.mean():.1f}", flush=True)
+if a.save or a.compare:
+    out = {"naln": nal, "alns": alns.cpu().numpy(), "edits": edits.cpu().numpy()}
+    k = out["naln"].clip(0)
+    mask = np.arange(maxaln)[None, :] < k[:, None]
+    out["alns"] = np.where(mask[:, :, None], out["alns"], 0)
+    ne = out["alns"][:, :, 6]
+    emask = np.arange(maxedit)[None, None, :] < ne[:, :, None]
+    out["edits"] = np.where(emask[:, :, :, None], out["edits"], 0)
+    if a.save:
+        np.savez_compressed(a.save, **out)
+    if a.compare:
+        ref = np.load(a.compare)
+        bad = {key: int((ref[key] != out[key]).reshape(n, -1).any(1).sum()) for key in out}
+        print("compare vs", a.compare, "problems differing:", bad, flush=True)
 eng.close()

@@ -24,6 +24,7 @@ inline uint4 make_uint4(uint32_t a, uint32_t b, uint32_t c, uint32_t d) { return
 inline int2 make_int2(int32_t a, int32_t b) { return int2{a, b}; }
 extern thread_local uint3v threadIdx, blockIdx;
 typedef void* hipStream_t;
+typedef void* hipEvent_t;
 typedef int hipError_t;
 template <typename K, typename... A>
 void emul_launch(K k, dim3 g, dim3 b, A... a) {

@@ -54,8 +54,35 @@ def lib():
     return build()
 
 
+def decision_nibbles(h, e, f, rd, q33, rf, sc):
+    """The end-to-end u8 fill's decision plane (sw_ee_packed.hip DEC) from the
+    oracle's H/E/F (u8 domain): bit 0 H != diag, bit 1 H != F, bit 2 F !=
+    H(up) - rfgo, bit 3 E != H(left) - rdgo; row 0 / column 0 terms the
+    reference never reads are left set."""
+    L, ncol = h.shape
+    h, e, f = (x.astype(np.int64) for x in (h, e, f))
+    qq = np.clip(q33.astype(np.int64) - 33, 0, 40)
+    mm = np.array([sc.mmpen[i] for i in range(41)], np.int64)
+    rc = rd.astype(np.int64)[:, None]
+    m = rf[:ncol].astype(np.int64)[None, :]
+    n_ = (rc > 3) | (m > 15)
+    sdiag = np.where(n_, -sc.npen, np.where((m >> np.minimum(rc, 3)) & 1, sc.match, -mm[qq][:, None]))
+    up_left = np.full((L, ncol), -10 ** 6, np.int64)
+    up_left[1:, 1:] = h[:-1, :-1]
+    up = np.full((L, ncol), -10 ** 6, np.int64)
+    up[1:, :] = h[:-1, :]
+    left = np.full((L, ncol), -10 ** 6, np.int64)
+    left[:, 1:] = h[:, :-1]
+    nib = (h != up_left + sdiag).astype(np.uint8)
+    nib |= (h != f).astype(np.uint8) << 1
+    nib |= (f != up - sc.rfgo).astype(np.uint8) << 2
+    nib |= (e != left - sc.rdgo).astype(np.uint8) << 3
+    return nib
+
+
 @pytest.mark.parametrize("src,kind", [("rand_ee", 0), ("log_ee", 0), ("rand_ee", 1), ("rand_loc", 1),
-                                      ("log_loc", 1), ("rand_loc", 2), ("log_loc", 2)])
+                                      ("log_loc", 1), ("rand_loc", 2), ("log_loc", 2), ("rand_ee", 3),
+                                      ("log_ee", 3)])
 def test_bt_kernel_source_on_cpu(lib, src, kind):
     import bt2g
     from oracle.oracle import Oracle
@@ -74,8 +101,8 @@ def test_bt_kernel_source_on_cpu(lib, src, kind):
     S16 = 16 * ((stride + 15) // 16)
     maxcol = int(probs["ncol"].max())
     maxrow = int(g["lens"].max())
-    es = 1 if kind == 0 else 2
-    plane_top = {0: 0, 1: 1, 2: 2}[kind]
+    es = 1 if kind in (0, 3) else 2
+    plane_top = {0: 0, 1: 1, 2: 2, 3: 0}[kind]
     slot = S16 * maxcol * es + ((maxcol * 2 + 15) & ~15)   # plane + per-column block masks
     plane = np.zeros(slot * n, np.uint8)
     keep = np.ones(n, bool)
@@ -108,6 +135,29 @@ def test_bt_kernel_source_on_cpu(lib, src, kind):
             stack[:L, :ncol] = (h & 0xffff).astype(np.uint16)
             plane[p * slot:p * slot + S16 * maxcol * 2] = \
                 stack.reshape(S16 // 16, 16, maxcol).transpose(0, 2, 1).ravel().view(np.uint8)
+        if kind == 3:
+            # decision nibbles (kernel kind 2): block-major [stack row // 16][column]
+            # [8 B: row 4q+i is nibble 4q+3-i, little-endian], same block masks as kind 0
+            if o[0] and not o[2]:
+                keep[p] = False
+                continue
+            nib = decision_nibbles(m[:, :, 0], m[:, :, 1], m[:, :, 2], rd, q, rf, swconst(False))
+            stack = np.full((S16, maxcol), 0xf, np.uint8)
+            stack[S16 - L:, :ncol] = nib
+            hs = np.full((S16, maxcol), 0xff, np.uint8)
+            hs[S16 - L:, :ncol] = m[:, :, 0]
+            live = hs.reshape(S16 // 16, 16, maxcol).max(1) >= 255 + minsc
+            if S16 > 256:
+                live[:] = True
+            perm = np.array([4 * (n >> 2) + 3 - (n & 3) for n in range(16)])   # nibble n holds row perm[n]
+            blocks = stack.reshape(S16 // 16, 16, maxcol)[:, perm, :].reshape(S16 // 16, 8, 2, maxcol)
+            packed = (blocks[:, :, 0, :] | (blocks[:, :, 1, :] << 4)).astype(np.uint8)   # (blk, 8, col)
+            packed = np.where(live[:, None, :], packed, 0xa5)
+            plane[p * slot:p * slot + S16 * maxcol // 2] = packed.transpose(0, 2, 1).ravel()
+            if S16 <= 256:
+                masks = (live.astype(np.uint32) << np.arange(S16 // 16)[:, None].astype(np.uint32)).sum(0)
+                plane[p * slot + S16 * maxcol:p * slot + S16 * maxcol + 2 * maxcol] = \
+                    masks.astype(np.uint16).view(np.uint8)
         if kind == 0:
             if o[0] and not o[2]:
                 keep[p] = False          # i16 fill: not in a u8 plane (naln -4)
@@ -134,7 +184,7 @@ def test_bt_kernel_source_on_cpu(lib, src, kind):
     edits = np.zeros((n, maxaln, maxedit), bt2g.EDIT_DTYPE)
     fates = np.zeros((n, cap), np.int8)
     lens = np.ascontiguousarray(g["lens"], np.uint32)
-    lib.bt_emul_run(C.c_int(min(kind, 1)), _p(probs), C.c_uint32(n), _p(g["reads"]), _p(g["quals"]), C.c_uint32(stride),
+    lib.bt_emul_run(C.c_int({0: 0, 1: 1, 2: 1, 3: 2}[kind]), _p(probs), C.c_uint32(n), _p(g["reads"]), _p(g["quals"]), C.c_uint32(stride),
                     _p(lens), _p(g["rf"]), _p(rects), _p(res), _p(cands), C.c_uint32(cap), _p(plane),
                     C.c_uint64(slot), C.c_uint32(S16), C.c_int(plane_top), C.c_uint32(maxrow), C.c_uint32(maxcol),
                     C.byref(swconst(local)), C.c_int(int(local)), C.c_double(0.0), C.c_double(0.15),
