@@ -134,6 +134,7 @@ struct BtArgs {
 	bt2g_sw_aln* alns;
 	bt2g_edit* edits;
 	int8_t* fates;                    // may be null
+	uint32_t* queue;                  // null: one DP per lane; else a zeroed counter: lanes take DPs from it
 };
 // kind: 0 u8 score plane, 1 u16 score plane, 2 decision nibbles (end-to-end u8 fills)
 void launch_sw_bt(int kind, const BtArgs& a, hipStream_t st);

@@ -5,6 +5,7 @@
 // its results against the oracle without a GPU.  The product never uses this.
 #include "../../bowtie2-server_amd/csrc/sw_backtrace.hip"
 #include <string.h>
+#include <stdlib.h>
 
 thread_local uint3v threadIdx, blockIdx;
 #ifdef BT2G_BT_COUNT
@@ -31,6 +32,11 @@ extern "C" int bt_emul_run(int kind, const bt2g_sw_problem* probs, uint32_t npro
 	a.marks = marks.data();
 	a.C = *C; a.local = local; a.ncl_const = ncl_const; a.ncl_lin = ncl_lin;
 	a.maxaln = maxaln; a.maxedit = maxedit; a.naln = naln; a.alns = alns; a.edits = edits; a.fates = fates;
+	// DP queue (the lanes of the emulation run one after another: lane 0 of each
+	// block takes every DP left; BT_EMUL_STATIC=1: one DP per lane)
+	uint32_t queue = 0;
+	const char* st = getenv("BT_EMUL_STATIC");
+	a.queue = st && *st == '1' ? nullptr : &queue;
 	launch_sw_bt(kind, a, nullptr);
 	return 0;
 }

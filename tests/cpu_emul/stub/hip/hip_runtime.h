@@ -36,3 +36,9 @@ void emul_launch(K k, dim3 g, dim3 b, A... a) {
 		}
 }
 #define hipLaunchKernelGGL(k, g, b, sh, st, ...) emul_launch(k, g, b, __VA_ARGS__)
+// wave intrinsics for one lane at a time: the lane is its own wave
+inline uint64_t __ballot(int pr) { return pr ? (1ull << threadIdx.x) : 0ull; }
+inline int __ffsll(unsigned long long x) { return __builtin_ffsll((long long)x); }
+inline int __popcll(unsigned long long x) { return __builtin_popcountll(x); }
+inline int __shfl(int v, int) { return v; }
+inline uint32_t atomicAdd(uint32_t* a, uint32_t v) { const uint32_t o = *a; *a += v; return o; }
