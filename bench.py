@@ -46,13 +46,15 @@ for _p in (ROOT, PKG, os.path.join(PKG, "tools"), os.path.join(ROOT, "tests", "g
 
 HBM_PEAK_GBS = 8000.0          # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
 # SW fill (VALU-bound): VALU lane-ops issued per DP cell by the systolic
-# end-to-end fill incl. its score plane (profiles/r01d_pmc_sw.csv: 5.71e9
-# SQ_INSTS_VALU x 64 lanes / 3.29e10 cells per launch), and the issue-rate
-# ceiling of its instruction mix: packed u16 / v_perm ops issue at half rate,
-# 37 T lane-ops/s measured on the box (profiles/r01_valu_rates.txt; full-rate
-# ops 70 T)
-VALU_OPS_PER_CELL = 11.1
-VALU_PEAK_TOPS = 37.0
+# end-to-end fill incl. its decision plane (r02n, scripts/pmc_fill.sh: 1.31e10
+# SQ_INSTS_VALU x 64 lanes / 3.15e10 cells per launch; 11.9 with the H score
+# plane, BT2G_BT_HPLANE=1), against two ceilings: the chip's VALU peak (256
+# CUs x 128 lanes x 2.4 GHz = 78.6 T lane-ops/s) and the issue rate measured
+# on the box for packed u16 / v_perm ops, which issue at half rate (37 T;
+# profiles/r01_valu_rates.txt, full-rate ops 70 T)
+VALU_OPS_PER_CELL = 11.9 if os.environ.get("BT2G_BT_HPLANE") == "1" else 26.6
+VALU_PEAK_TOPS = 78.6
+VALU_PACKED_TOPS = 37.0
 SEEDLEN, INTERVAL = 22, 15     # --sensitive, 150 bp: -L 22, -i S,1,1.15 -> 1+1.15*sqrt(150) = 15
 
 
@@ -1110,9 +1112,10 @@ def main():
             "side_loads_per_step": {names_k[k]: (bytes_k[k] // 64) for k in (0, 1, 2, 3) if bytes_k.get(k)},
             "sw_gcups": sw_gcups,
             # the SW fill against its VALU ceiling (north_star: VALU utilisation of the SW kernel)
-            "sw_roofline": {"bound": "valu", "kernel": "sw_align (systolic fill + score plane + candidate sort)",
+            "sw_roofline": {"bound": "valu", "kernel": "sw_align (systolic fill + decision plane + candidate sort)",
                             "achieved": sw_gcups * VALU_OPS_PER_CELL / 1e3, "peak": VALU_PEAK_TOPS,
                             "unit": "T lane-ops/s", "frac": sw_gcups * VALU_OPS_PER_CELL / 1e3 / VALU_PEAK_TOPS,
+                            "frac_packed_issue": sw_gcups * VALU_OPS_PER_CELL / 1e3 / VALU_PACKED_TOPS,
                             "ops_per_cell": VALU_OPS_PER_CELL} if args.mode == "ee" else None,
             "backtrace": bt_stats,
             "landscape": landscape,
