@@ -635,10 +635,12 @@ k_sw_bt(BtArgs A) {
 				else { tbits |= bt; tdirty = true; }
 			}
 			if(needd) {
-				// row 4q+i of the block is nibble 4q+3-i of the column's 8 bytes
-				const uint32_t rr = rsx & 15u, nbi = (rr & ~3u) + 3u - (rr & 3u);
-				const uint32_t by = ((const uint8_t*)myc)[(col - dc0) * 8u + (nbi >> 1)];
-				nb2 = (by >> (4u * (nbi & 1u))) & 15u;
+				// row 8w+i of the block: word w of the column's 8 bytes, bits 0-2 of
+				// the decision at 3(7-i)+2, +1, +0, bit 3 at 24+7-i (sw_ee_packed.hip)
+				const uint32_t rr = rsx & 15u, i7 = 7u - (rr & 7u);
+				const uint32_t wd = myc[(col - dc0) * 2u + (rr >> 3)];
+				const uint32_t t = wd >> (3u * i7);
+				nb2 = ((t >> 2) & 1u) | ((t & 2u)) | ((t & 1u) << 2) | (((wd >> (24u + i7)) & 1u) << 3);
 			}
 		} else {
 			BTC(1);

@@ -86,6 +86,22 @@ __device__ __forceinline__ void st_plane(uint8_t* p, uint32_t x, uint32_t y, uin
 #endif
 }
 
+// DEC: acc * 2 + (a != b) for the low / high 16-bit halves -- a compare into
+// VCC and an add-with-carry that shifts the bit in: two full-rate ops per bit
+// (v_pk_* ops issue at half rate; the compiler's form of a per-half test took
+// about twice the instructions)
+__device__ __forceinline__ uint32_t shl_ne_lo(uint32_t acc, uint32_t a, uint32_t b) {
+	uint32_t r;
+	asm("v_cmp_ne_u16_e32 vcc, %1, %2\n\tv_addc_co_u32_e32 %0, vcc, %3, %3, vcc" : "=v"(r) : "v"(a), "v"(b), "v"(acc) : "vcc");
+	return r;
+}
+__device__ __forceinline__ uint32_t shl_ne_hi(uint32_t acc, uint32_t a, uint32_t b) {
+	uint32_t r;
+	asm("v_cmp_ne_u16_sdwa vcc, %1, %2 src0_sel:WORD_1 src1_sel:WORD_1\n\tv_addc_co_u32_e32 %0, vcc, %3, %3, vcc"
+	    : "=v"(r) : "v"(a), "v"(b), "v"(acc) : "vcc");
+	return r;
+}
+
 __device__ __forceinline__ int first5(int m) {
 	return (m & 1) ? 0 : (m & 2) ? 1 : (m & 4) ? 2 : (m & 8) ? 3 : 4;
 }
@@ -117,8 +133,9 @@ struct Half {
 // backtrace step (up-left) usually stays inside one 128-B line; hbytes 1 keeps
 // u8 fills only.
 // DEC (end-to-end, u8 fills): instead of H, the backtrace's decision at every
-// cell as a nibble (the "decision plane", 8 B per 16-row block column, row
-// 4q+i as nibble 4q+3-i, little-endian nibbles): the reference's walk
+// cell as 4 bits (the "decision plane", 8 B per 16-row block column: word
+// w = row >> 3 holds, for row 8w+i, bits 0 / 1 / 2 below at bits 3(7-i)+2 /
+// 3(7-i)+1 / 3(7-i) and bit 3 at bit 24+7-i): the reference's walk
 // (aligner_swsse_ee_u8.cpp:1357-1540) picks, in H state, diag > H-up > F-up >
 // H-left > E-left, in F state H-up > F-up, in E state H-left > E-left; with
 // H = max(diag, E, F) and every walked cell above the floor that is
@@ -488,20 +505,18 @@ k_sw_sys(const bt2g_sw_problem* __restrict__ probs, uint32_t nprob, const uint8_
 		               ? (uint32_t)h[x].minsc : 0x10000u;
 	const uint32_t cthr = ((ctest[0] - 1u) & 0xffffu) | (((ctest[1] - 1u) & 0xffffu) << 16);
 	const uint32_t match2 = (uint32_t)C.match * 0x10001u, npm2 = (uint32_t)(C.match + C.npen) * 0x10001u;
-	// DEC: this column's decision nibbles (rows 4q..4q+3 in Dw[q], row 4q+i in
-	// nibble 3-i of each half: Horner steps by 16, an inline constant) and the
-	// E bits of the next column, known one column early (Dn, bit 0 of each
-	// nibble until the column's end)
-	uint32_t Dw[4] = {0u, 0u, 0u, 0u}, Dn[4] = {0u, 0u, 0u, 0u};
-	const uint32_t one2 = 0x00010001u;
-	// (t* are 0 / 1 per half: 32-bit shifts never carry a bit across the halves
-	// within 4 rows, and v_lshl_or_b32 issues at the full rate)
-	auto dec_cell = [&](int i, uint32_t t0, uint32_t t1, uint32_t t2) {
-		const uint32_t nb = (t2 << 2) | (t1 << 1) | t0;
-		Dw[i >> 2] = (i & 3) ? (Dw[i >> 2] << 4) | nb : nb;
+	// DEC: this column's decision bits per problem (rows 0-7 / 8-15 shifted into
+	// DA/DB[0] / [1], 3 bits a row) and the E bits of the next column, known one
+	// column early (NA / NB, one bit a row; older bits shift out and are masked)
+	uint32_t DA[2] = {0u, 0u}, DB[2] = {0u, 0u}, NA = 0u, NB = 0u;
+	auto dec_cell = [&](int i, uint32_t hh, uint32_t dw, uint32_t f, uint32_t hu) {
+		const int w = i >> 3;
+		DA[w] = shl_ne_lo(shl_ne_lo(shl_ne_lo(DA[w], hh, dw), hh, f), f, hu);
+		DB[w] = shl_ne_hi(shl_ne_hi(shl_ne_hi(DB[w], hh, dw), hh, f), f, hu);
 	};
-	auto dec_next = [&](int i, uint32_t t3) {
-		Dn[i >> 2] = (i & 3) ? (Dn[i >> 2] << 4) | t3 : t3;
+	auto dec_next = [&](uint32_t en, uint32_t hgm) {
+		NA = shl_ne_lo(NA, en, hgm);
+		NB = shl_ne_hi(NB, en, hgm);
 	};
 	for(uint32_t t = 0; t < T; t++) {
 		// the lane above computed this lane's column in the previous step (DPP wave_shr:1)
@@ -518,9 +533,7 @@ k_sw_sys(const bt2g_sw_problem* __restrict__ probs, uint32_t nprob, const uint8_
 		const bool amb = DEC && __ballot((selx & 0x80008000u) != 0u);
 		const uint32_t sel = DEC ? ((selx & 0x00ff00ffu) | 0x0c000c00u) : selx;
 		if(in_group) nsel = mysel[(uint32_t)j + 1 < ncolmax ? j + 1 : j];   // next step's column
-		uint32_t Dp[4];   // DEC: bit 3 of this column's nibbles (from the previous column)
-#pragma unroll
-		for(int q = 0; q < 4; q++) Dp[q] = DEC ? Dn[q] << 3 : 0u;
+		const uint32_t XA = NA, XB = NB;   // DEC: bit 3 of this column's cells (previous column)
 		uint32_t hup, fup, diag;
 		if(top) {
 			hup = 0;
@@ -581,11 +594,10 @@ k_sw_sys(const bt2g_sw_problem* __restrict__ probs, uint32_t nprob, const uint8_
 					const uint32_t hh = pmax(pmax(d, E[i]), f);
 					const uint32_t hg = psub(hh, rdgo2);
 					if(DEC) {
-						// hprev: H(up) - rfgo
-						dec_cell(i, pmin(psub(hh, dwalk), one2), pmin(psub(hh, f), one2), pmin(psub(f, hprev), one2));
+						dec_cell(i, hh, dwalk, f, hprev);   // hprev: H(up) - rfgo
 						const uint32_t hgm = hg & M[i];
 						const uint32_t en = pmax(psub(E[i], rdge2), hgm);
-						dec_next(i, pmin(psub(en, hgm), one2));
+						dec_next(en, hgm);
 						E[i] = en;
 					} else {
 						E[i] = pmax(psub(E[i], rdge2), hg & M[i]);
@@ -599,10 +611,10 @@ k_sw_sys(const bt2g_sw_problem* __restrict__ probs, uint32_t nprob, const uint8_
 					const uint32_t f = pmax(psub(fprev, rfge2), huo) & M[i];
 					const uint32_t hh = pmax(pmax(d, E[i]), f);
 					if(DEC) {
-						dec_cell(i, pmin(psub(hh, dwalk), one2), pmin(psub(hh, f), one2), pmin(psub(f, huo), one2));
+						dec_cell(i, hh, dwalk, f, huo);
 						const uint32_t hgm = psub(hh, rdgo2) & M[i];
 						const uint32_t en = pmax(psub(E[i], rdge2), hgm);
-						dec_next(i, pmin(psub(en, hgm), one2));
+						dec_next(en, hgm);
 						E[i] = en;
 					} else {
 						E[i] = pmax(psub(E[i], rdge2), psub(hh, rdgo2) & M[i]);
@@ -701,13 +713,12 @@ k_sw_sys(const bt2g_sw_problem* __restrict__ probs, uint32_t nprob, const uint8_
 			const uint64_t hslot = 0;                 // timing experiments only: all writes in 64 KB
 #endif
 			if(DEC) {
-				// the decision nibbles of 16 rows: 8 B per problem
-#pragma unroll
-				for(int q = 0; q < 4; q++) Dw[q] |= Dp[q];
-				const uint32_t a0 = __builtin_amdgcn_perm(Dw[1], Dw[0], 0x05040100u);
-				const uint32_t a1 = __builtin_amdgcn_perm(Dw[3], Dw[2], 0x05040100u);
-				const uint32_t b0 = __builtin_amdgcn_perm(Dw[1], Dw[0], 0x07060302u);
-				const uint32_t b1 = __builtin_amdgcn_perm(Dw[3], Dw[2], 0x07060302u);
+				// the decision bits of 16 rows: 8 B per problem (24 shifted-in bits a
+				// word; the E bits of rows 0-7 / 8-15 are bits 15-8 / 7-0 of XA, XB)
+				const uint32_t a0 = (DA[0] & 0xffffffu) | ((XA << 16) & 0xff000000u);
+				const uint32_t a1 = (DA[1] & 0xffffffu) | (XA << 24);
+				const uint32_t b0 = (DB[0] & 0xffffffu) | ((XB << 16) & 0xff000000u);
+				const uint32_t b1 = (DB[1] & 0xffffffu) | (XB << 24);
 				const size_t cell8 = ((size_t)k * pitch + (uint32_t)j) * 8u;
 				if(s0 && h[0].row0 == 0xffu) *(uint2*)(plane + (size_t)h[0].pi * hslot + cell8) = make_uint2(a0, a1);
 				if(s1 && h[1].row0 == 0xffu) *(uint2*)(plane + (size_t)h[1].pi * hslot + cell8) = make_uint2(b0, b1);

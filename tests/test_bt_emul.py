@@ -136,8 +136,8 @@ def test_bt_kernel_source_on_cpu(lib, src, kind):
             plane[p * slot:p * slot + S16 * maxcol * 2] = \
                 stack.reshape(S16 // 16, 16, maxcol).transpose(0, 2, 1).ravel().view(np.uint8)
         if kind == 3:
-            # decision nibbles (kernel kind 2): block-major [stack row // 16][column]
-            # [8 B: row 4q+i is nibble 4q+3-i, little-endian], same block masks as kind 0
+            # decision bits (kernel kind 2): block-major [stack row // 16][column][2 words],
+            # same block masks as kind 0
             if o[0] and not o[2]:
                 keep[p] = False
                 continue
@@ -149,11 +149,14 @@ def test_bt_kernel_source_on_cpu(lib, src, kind):
             live = hs.reshape(S16 // 16, 16, maxcol).max(1) >= 255 + minsc
             if S16 > 256:
                 live[:] = True
-            perm = np.array([4 * (n >> 2) + 3 - (n & 3) for n in range(16)])   # nibble n holds row perm[n]
-            blocks = stack.reshape(S16 // 16, 16, maxcol)[:, perm, :].reshape(S16 // 16, 8, 2, maxcol)
-            packed = (blocks[:, :, 0, :] | (blocks[:, :, 1, :] << 4)).astype(np.uint8)   # (blk, 8, col)
-            packed = np.where(live[:, None, :], packed, 0xa5)
-            plane[p * slot:p * slot + S16 * maxcol // 2] = packed.transpose(0, 2, 1).ravel()
+            # word w of a block column: row 8w+i's bits 0/1/2 at 3(7-i)+2/+1/+0, bit 3 at 24+7-i
+            st = stack.astype(np.uint32).reshape(S16 // 16, 2, 8, maxcol)            # (blk, w, i, col)
+            sh = (3 * (7 - np.arange(8)))[None, None, :, None].astype(np.uint32)
+            b0, b1, b2, b3 = st & 1, (st >> 1) & 1, (st >> 2) & 1, (st >> 3) & 1
+            words = ((b0 << (sh + 2)) | (b1 << (sh + 1)) | (b2 << sh) |
+                     (b3 << (24 + 7 - np.arange(8)).astype(np.uint32)[None, None, :, None])).sum(2).astype(np.uint32)
+            words = np.where(live[:, None, :], words, 0xa5a5a5a5).astype(np.uint32)   # (blk, w, col)
+            plane[p * slot:p * slot + S16 * maxcol // 2] = words.transpose(0, 2, 1).ravel().view(np.uint8)
             if S16 <= 256:
                 masks = (live.astype(np.uint32) << np.arange(S16 // 16)[:, None].astype(np.uint32)).sum(0)
                 plane[p * slot + S16 * maxcol:p * slot + S16 * maxcol + 2 * maxcol] = \
