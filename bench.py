@@ -46,13 +46,13 @@ for _p in (ROOT, PKG, os.path.join(PKG, "tools"), os.path.join(ROOT, "tests", "g
 
 HBM_PEAK_GBS = 8000.0          # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
 # SW fill (VALU-bound): VALU lane-ops issued per DP cell by the systolic
-# end-to-end fill incl. its decision plane (r02n, scripts/pmc_fill.sh: 1.31e10
-# SQ_INSTS_VALU x 64 lanes / 3.15e10 cells per launch; 11.9 with the H score
-# plane, BT2G_BT_HPLANE=1), against two ceilings: the chip's VALU peak (256
+# end-to-end fill incl. its decision plane (r02o, scripts/pmc_fill.sh:
+# SQ_INSTS_VALU x 64 lanes / 3.15e10 cells per launch = 22.0; 11.9 with the H
+# score plane, BT2G_BT_HPLANE=1), against two ceilings: the chip's VALU peak (256
 # CUs x 128 lanes x 2.4 GHz = 78.6 T lane-ops/s) and the issue rate measured
 # on the box for packed u16 / v_perm ops, which issue at half rate (37 T;
 # profiles/r01_valu_rates.txt, full-rate ops 70 T)
-VALU_OPS_PER_CELL = 11.9 if os.environ.get("BT2G_BT_HPLANE") == "1" else 26.6
+VALU_OPS_PER_CELL = 11.9 if os.environ.get("BT2G_BT_HPLANE") == "1" else 22.0
 VALU_PEAK_TOPS = 78.6
 VALU_PACKED_TOPS = 37.0
 SEEDLEN, INTERVAL = 22, 15     # --sensitive, 150 bp: -L 22, -i S,1,1.15 -> 1+1.15*sqrt(150) = 15
