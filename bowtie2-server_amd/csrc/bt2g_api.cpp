@@ -892,7 +892,9 @@ int bt2g_sw_align_bt_dev(bt2g_ctx* c, const uint8_t* reads, const uint8_t* quals
 	// u8 fills: the fill writes the walk's decision per cell (kind 2, 4 bits);
 	// BT2G_BT_HPLANE=1 keeps the H score plane (kind 0) for A/B runs
 	static const bool hplane = [] { const char* e = getenv("BT2G_BT_HPLANE"); return e && *e == '1'; }();
-	const int kind = hb == 1 ? (hplane || sc->local ? 0 : 2) : 1;
+	// (wide DPs -- mate searches, 150 x 705 -- keep the H plane: the decision bits
+	// cost fill work per cell, and their walks touch a small share of the cells)
+	const int kind = hb == 1 ? (hplane || sc->local || maxcol > 2u * maxrow ? 0 : 2) : 1;
 	a.plane = plane;
 	a.slot = sw_plane_slot(stride, maxcol, hb);
 	a.plane_top = !packed ? 1 : sc->local ? 2 : 0;

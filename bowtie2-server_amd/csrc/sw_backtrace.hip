@@ -122,11 +122,8 @@ __device__ unsigned long long g_bt_wave_t0[1u << 16], g_bt_wave_t1[1u << 16];   
 template <int KIND, bool LOCAL, bool FLAT = LOCAL>
 __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(BT2G_BT_WAVES)))
 k_sw_bt(BtArgs A) {
-	// DPs: one per lane, or (A.queue) the next unclaimed one whenever a lane is
-	// done with a DP -- the DP, candidate and walk loops are one loop, so a lane
-	// never waits for the slowest DP of its wave (launch_sw_bt)
-	uint32_t p = blockIdx.x * 64u + threadIdx.x;
-	bool first_dp = true;
+	const uint32_t p = blockIdx.x * 64u + threadIdx.x;
+	if(p >= A.nprob) return;
 #ifdef BT2G_BT_PROF
 	uint32_t pc[13] = {0};
 	if(threadIdx.x == 0) g_bt_wave_t0[blockIdx.x & 0xffffu] = wall_clock64();
@@ -140,27 +137,41 @@ k_sw_bt(BtArgs A) {
 		}
 	} flush_{pc};
 #endif
-	// the current DP's state (set when the lane takes it, in the loop below)
-	bt2g_sw_result R{};
-	bt2g_sw_problem P{};
-	uint32_t nrow = 0, ncol = 0;
+	const bt2g_sw_result R = A.res[p];
+	if(!R.aligned || R.ncand <= 0) { A.naln[p] = 0; return; }
+	if((uint32_t)R.ncand > A.cap) { A.naln[p] = -5; return; }   // truncated list: not the reference's
+	const bt2g_sw_problem P = A.probs[p];
+	const uint32_t nrow = A.lens[P.read], ncol = P.ncol;
 	constexpr bool local = LOCAL;
-	int variant = 0;
+	const int variant = local ? (R.u8succ ? 2 : 3) : (R.u8succ ? 0 : 1);
 	Plane<KIND> pl;
-	pl.base = nullptr;
-	pl.ncol = 0;
+	pl.ncol = ncol;
 	pl.pcols = A.pcols;
 	pl.pad = 0;
-	pl.off = 0;
 	pl.mask = nullptr;
 	uint32_t pad = 0;
 	const uint8_t* slot = nullptr;
+	{
+		if(KIND != 1 && variant != 0) { A.naln[p] = -4; return; }   // i16 fill, u8-only plane
+		const size_t es = KIND == 1 ? 2 : 1;   // kind 2: the u8 plane's layout, 8 B per block column
+		// systolic end-to-end: last row at the stack bottom; one-problem-per-lane
+		// fills: top-aligned; systolic local: padded rows (round16) at the bottom
+		pad = A.plane_top == 1 ? 0u : A.cstride - (A.plane_top == 2 ? ((nrow + 15u) & ~15u) : nrow);
+		slot = A.plane + (size_t)p * A.slot;
+		pl.base = slot;
+		pl.pad = pad;
+		if(A.use_mask) pl.mask = (const uint16_t*)(slot + (size_t)A.cstride * A.pcols * es);
+		// u8 fill: 0xff + score; i16 end-to-end fill: 0xffff + score (offset-u16
+		// domain); local fills: the score itself
+		pl.off = variant == 0 ? 0xff : variant == 1 ? 0xffff : 0;
+	}
 	// SwAligner::initRead / initRef inputs of this problem
-	const uint8_t* rd = nullptr;
-	const uint8_t* qu = nullptr;
-	bool fw = true;
+	const uint8_t* rd = A.reads + (size_t)P.read * A.stride;
+	const uint8_t* qu = A.quals + (size_t)P.read * A.stride;
+	const bool fw = P.fw != 0;
 	const SwConst& C = A.C;
 	uint64_t rs = 0, rlen = 0;
+	if(P.win_off < 0) { rs = A.ref_starts[P.refidx]; rlen = A.ref_starts[P.refidx + 1] - rs; }
 	// Scoring::score / Scoring::mm (scoring.h:232-254); match(30) is the bonus
 	auto sdiag = [&](int rc, int m, int q) -> int {
 		if(rc > 3 || m > 15) return -C.npen;
@@ -212,16 +223,24 @@ k_sw_bt(BtArgs A) {
 			return hit;
 		}
 	};
-	int32_t nceil = 0;   // N ceiling, Scoring::nCeil.f<int>(len) (simple_func.h:90-115)
+	// N ceiling, Scoring::nCeil.f<int>(len) (simple_func.h:90-115)
+	int32_t nceil;
+	{
+		double v = A.ncl_const + A.ncl_lin * (double)nrow;
+		v = v < 0.0 ? 0.0 : v;
+		nceil = v >= 2147483647.0 ? 2147483647 : (int32_t)v;
+	}
 	int32_t triml = 0, corel = 0, corer = 0x7fffffff;
+	if(A.rects) { const bt2g_sw_rect rc = A.rects[p]; triml = rc.triml; corel = rc.corel; corer = rc.corer; }
 	// reportedThrough: 8x8-cell bit tiles (one u64 each), one tile cached in
 	// registers at a time (a walk stays in a tile for several steps); a tile is
 	// valid once written back (one valid bit per tile, cleared here; the current
 	// valid word is cached in a register too), so nothing else is ever cleared.
 	// (Valid bits in LDS instead: measured slower.)
-	uint32_t* marks = nullptr;
+	uint32_t* marks = A.marks + (size_t)p * A.mslot;
 	const uint32_t tcols = A.rwords, trows = A.rrows, vw = (tcols + 31u) / 32u;
-	uint32_t* valid = nullptr;
+	uint32_t* valid = marks + (size_t)trows * tcols * 2u;
+	for(uint32_t i = 0; i < trows * vw; i++) valid[i] = 0u;
 	uint32_t ttr = 0xffffffffu, ttc = 0;
 	uint64_t tbits = 0;
 	bool tdirty = false;
@@ -300,8 +319,8 @@ k_sw_bt(BtArgs A) {
 		const int q = win(w_q, 1u, qu + (fw ? r : nrow - 1 - r), A.quals, qu + A.stride) - 33;
 		return q < 0 ? 0 : (q > 40 ? 40 : q);
 	};
-	const uint8_t* wlo = nullptr;
-	const uint8_t* whi = nullptr;
+	const uint8_t* wlo = P.win_off >= 0 ? A.windows + P.win_off : A.ref_codes;
+	const uint8_t* whi = P.win_off >= 0 ? wlo + ncol + 1 : A.ref_codes + rs + rlen + 16u;
 	auto rf_at = [&](uint32_t c) -> int {   // reference mask of column c (aligner_sw.cpp:171-253)
 		if(P.win_off >= 0) return win(w_rf, 2u, wlo + c, wlo, whi);
 		const int64_t o = P.refl + (int64_t)c;
@@ -359,16 +378,19 @@ k_sw_bt(BtArgs A) {
 	// in the walk step together with its reportedThrough tile (one round trip)
 	constexpr uint32_t BT_DCH = 2u * BT_CHUNK;
 	uint32_t db = 0xffffffffu, dc0 = 0;
-	uint32_t ncand = 0;
-	const bt2g_sw_cand* cl = nullptr;
+	const uint32_t ncand = (uint32_t)R.ncand < A.cap ? (uint32_t)R.ncand : A.cap;
+	const bt2g_sw_cand* cl = A.cands + (size_t)p * A.cap;
 	// local mode, FILT_DOMINATED (aligner_sw.cpp nextAlignment): a candidate
 	// within SQ rows and SQ columns of one already walked is skipped.  Each
 	// walked candidate sets its (2SQ+1)^2 square in a second set of 8x8 bit
 	// tiles, so the test is one bit, not a scan of the walked list.
-	uint32_t SQ = 1;
-	uint32_t* dmarks = nullptr;
+	uint32_t SQ = nrow >> 4;
+	if(SQ == 0) SQ = 1;
+	uint32_t* dmarks = marks + A.mdom;
 	const uint32_t dtcols = A.mwords, dtrows = A.mrows, dvw = (dtcols + 31u) / 32u;
-	uint32_t* dvalid = nullptr;
+	uint32_t* dvalid = dmarks + (size_t)dtrows * dtcols * 2u;
+	if(local)
+		for(uint32_t i = 0; i < dtrows * dvw; i++) dvalid[i] = 0u;
 	auto dom_test = [&](uint32_t r, uint32_t c) -> bool {
 		const uint32_t tr = r >> 3, tc = c >> 3;
 		if(!((dvalid[tr * dvw + (tc >> 5)] >> (tc & 31u)) & 1u)) return false;
@@ -396,6 +418,7 @@ k_sw_bt(BtArgs A) {
 	};
 	int32_t nal = 0;
 	bool first = true;
+	BTC(12);
 	// FLAT (local mode): the candidate loop and the walks run as ONE loop: an
 	// iteration either filters a candidate or takes one walk step, so a lane
 	// never waits for the longest walk of its wave at every candidate (nested
@@ -434,89 +457,11 @@ k_sw_bt(BtArgs A) {
 #endif
 	uint32_t ci = 0;
 	// the next candidate is loaded one ahead (its load overlaps the current walk)
-	bt2g_sw_cand nxt_cd{0, 0, 0};
+	bt2g_sw_cand nxt_cd = ncand ? cl[0] : bt2g_sw_cand{0, 0, 0};
 	int32_t cscore = 0;
-	bool have = false;   // the lane holds a DP
 	while(true) {
-		if(!have) {
-			// ---- take the next DP ------------------------------------------------
-			if(A.queue) {
-				// one atomic per wave for all its lanes that need a DP now
-				const uint64_t need = __ballot(1);
-				const uint32_t lead = (uint32_t)__ffsll((unsigned long long)need) - 1u;
-				uint32_t base = 0;
-				if(threadIdx.x == lead) base = atomicAdd(A.queue, (uint32_t)__popcll(need));
-				base = (uint32_t)__shfl((int)base, (int)lead);
-				p = base + (uint32_t)__popcll(need & ((1ull << threadIdx.x) - 1ull));
-			} else if(!first_dp) {
-				break;
-			}
-			first_dp = false;
-			if(p >= A.nprob) break;
-			R = A.res[p];
-			if(!R.aligned || R.ncand <= 0) { A.naln[p] = 0; continue; }
-			if((uint32_t)R.ncand > A.cap) { A.naln[p] = -5; continue; }   // truncated list: not the reference's
-			P = A.probs[p];
-			nrow = A.lens[P.read];
-			ncol = P.ncol;
-			variant = local ? (R.u8succ ? 2 : 3) : (R.u8succ ? 0 : 1);
-			if(KIND != 1 && variant != 0) { A.naln[p] = -4; continue; }   // i16 fill, u8-only plane
-			{
-				const size_t es = KIND == 1 ? 2 : 1;   // kind 2: the u8 plane's layout, 8 B per block column
-				// systolic end-to-end: last row at the stack bottom; one-problem-per-lane
-				// fills: top-aligned; systolic local: padded rows (round16) at the bottom
-				pad = A.plane_top == 1 ? 0u : A.cstride - (A.plane_top == 2 ? ((nrow + 15u) & ~15u) : nrow);
-				slot = A.plane + (size_t)p * A.slot;
-				pl.base = slot;
-				pl.ncol = ncol;
-				pl.pad = pad;
-				pl.mask = A.use_mask ? (const uint16_t*)(slot + (size_t)A.cstride * A.pcols * es) : nullptr;
-				// u8 fill: 0xff + score; i16 end-to-end fill: 0xffff + score (offset-u16
-				// domain); local fills: the score itself
-				pl.off = variant == 0 ? 0xff : variant == 1 ? 0xffff : 0;
-			}
-			rd = A.reads + (size_t)P.read * A.stride;
-			qu = A.quals + (size_t)P.read * A.stride;
-			fw = P.fw != 0;
-			rs = rlen = 0;
-			if(P.win_off < 0) { rs = A.ref_starts[P.refidx]; rlen = A.ref_starts[P.refidx + 1] - rs; }
-			{
-				double v = A.ncl_const + A.ncl_lin * (double)nrow;
-				v = v < 0.0 ? 0.0 : v;
-				nceil = v >= 2147483647.0 ? 2147483647 : (int32_t)v;
-			}
-			triml = 0; corel = 0; corer = 0x7fffffff;
-			if(A.rects) { const bt2g_sw_rect rc = A.rects[p]; triml = rc.triml; corel = rc.corel; corer = rc.corer; }
-			marks = A.marks + (size_t)p * A.mslot;
-			valid = marks + (size_t)trows * tcols * 2u;
-			for(uint32_t i = 0; i < trows * vw; i++) valid[i] = 0u;
-			ttr = 0xffffffffu; ttc = 0; tbits = 0; tdirty = false;
-			vidx = 0xffffffffu; vval = 0u; vdirty = false;
-			w_rd = w_q = w_rf = ~0ull;
-			wlo = P.win_off >= 0 ? A.windows + P.win_off : A.ref_codes;
-			whi = P.win_off >= 0 ? wlo + ncol + 1 : A.ref_codes + rs + rlen + 16u;
-			cb = 0xffffffffu; cc0 = 0;
-			db = 0xffffffffu; dc0 = 0;
-			ncand = (uint32_t)R.ncand < A.cap ? (uint32_t)R.ncand : A.cap;
-			cl = A.cands + (size_t)p * A.cap;
-			if(local) {
-				SQ = nrow >> 4;
-				if(SQ == 0) SQ = 1;
-				dmarks = marks + A.mdom;
-				dvalid = dmarks + (size_t)dtrows * dtcols * 2u;
-				for(uint32_t i = 0; i < dtrows * dvw; i++) dvalid[i] = 0u;
-			}
-			nal = 0;
-			first = true;
-			walking = false;
-			ndone = 0;
-			ci = 0;
-			nxt_cd = cl[0];
-			BTC(12);
-			have = true;
-		}
 		if(!walking) {
-			if(ci >= ncand || nal >= (int32_t)A.maxaln) { A.naln[p] = nal; have = false; continue; }
+			if(ci >= ncand || nal >= (int32_t)A.maxaln) break;
 			const bt2g_sw_cand cd = nxt_cd;
 			nxt_cd = cl[ci + 1u < ncand ? ci + 1u : ci];
 			int8_t fate = 0;
@@ -869,6 +814,7 @@ k_sw_bt(BtArgs A) {
 		if(A.fates) A.fates[(size_t)p * A.cap + ci] = fate;
 		ci++;
 	}
+	A.naln[p] = nal;
 }
 
 #ifdef BT2G_BT_PROF
@@ -904,11 +850,7 @@ extern "C" int bt2g_bt_prof_read(unsigned long long* out) {
 
 void launch_sw_bt(int kind, const BtArgs& a, hipStream_t st) {
 	if(a.nprob == 0) return;
-	// with a queue: about the resident waves of the chip (256 CUs x 4 SIMDs x
-	// BT2G_BT_WAVES), each lane taking DPs until none is left
-	uint32_t nb = (a.nprob + 63u) / 64u;
-	if(a.queue && nb > 1024u * BT2G_BT_WAVES) nb = 1024u * BT2G_BT_WAVES;
-	const dim3 grid(nb), block(64);
+	const dim3 grid((a.nprob + 63u) / 64u), block(64);
 	if(a.local) {
 		// local fills leave a u16 plane
 		hipLaunchKernelGGL((k_sw_bt<1, true>), grid, block, 0, st, a);
