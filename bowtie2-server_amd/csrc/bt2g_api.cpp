@@ -1266,6 +1266,71 @@ int bt2g_sw_align_bt(bt2g_ctx* c, const uint8_t* reads, const uint8_t* quals, ui
 	return BT2G_OK;
 }
 
+int bt2g_sw_align_bt_packed(bt2g_ctx* c, const uint8_t* reads, const uint8_t* quals, uint32_t stride,
+                            const uint32_t* lens, const bt2g_sw_problem* probs, uint32_t nprob,
+                            const uint8_t* windows, uint64_t windows_len, const bt2g_sw_rect* rects,
+                            const bt2g_scoring* sc, int enable8, uint32_t cap, bt2g_sw_result* res, uint32_t maxaln,
+                            uint32_t maxedit, int32_t* naln, bt2g_sw_aln* alns, bt2g_sw_cand* cands, int8_t* fates,
+                            bt2g_edit* edits, uint64_t* totals) {
+	if(!c) return fail(BT2G_ERR_ARG, "null ctx");
+	if(!totals) return fail(BT2G_ERR_ARG, "null totals");
+	HIPCHK(hipSetDevice(c->device));
+	totals[0] = totals[1] = totals[2] = 0;
+	if(nprob == 0) return BT2G_OK;
+	uint32_t nreads = 0;
+	for(uint32_t i = 0; i < nprob; i++) nreads = probs[i].read + 1 > nreads ? probs[i].read + 1 : nreads;
+	Tmp t(c);
+	uint8_t *dr, *dq, *dw = nullptr;
+	uint32_t *dl, *dcnt, *doff;
+	bt2g_sw_problem* dp;
+	bt2g_sw_rect* drc = nullptr;
+	bt2g_sw_result* dres;
+	bt2g_sw_cand *dc, *dpc;
+	int32_t* dna;
+	bt2g_sw_aln* dal;
+	bt2g_edit *ded, *dpe;
+	int8_t *dft = nullptr, *dpf = nullptr;
+	int rc;
+	const size_t na = (size_t)nprob * maxaln;
+	if((rc = t.up(&dr, reads, (size_t)nreads * stride)) || (rc = t.up(&dq, quals, (size_t)nreads * stride)) ||
+	   (rc = t.up(&dl, lens, nreads)) || (rc = t.up(&dp, probs, nprob)) ||
+	   (rc = t.up(&dres, (const bt2g_sw_result*)nullptr, nprob)) ||
+	   (rc = t.up(&dc, (const bt2g_sw_cand*)nullptr, (size_t)nprob * cap)) ||
+	   (rc = t.up(&dna, (const int32_t*)nullptr, nprob)) || (rc = t.up(&dal, (const bt2g_sw_aln*)nullptr, na)) ||
+	   (rc = t.up(&ded, (const bt2g_edit*)nullptr, na * maxedit)) ||
+	   (rc = t.up(&dcnt, (const uint32_t*)nullptr, 3 * (size_t)nprob)) ||
+	   (rc = t.up(&doff, (const uint32_t*)nullptr, 3 * (size_t)nprob + 3)) ||
+	   (rc = t.up(&dpc, (const bt2g_sw_cand*)nullptr, (size_t)nprob * cap)) ||
+	   (rc = t.up(&dpe, (const bt2g_edit*)nullptr, na * maxedit)))
+		return rc;
+	if(windows && windows_len && (rc = t.up(&dw, windows, windows_len))) return rc;
+	if(rects && (rc = t.up(&drc, rects, nprob))) return rc;
+	if(fates && ((rc = t.up(&dft, (const int8_t*)nullptr, (size_t)nprob * cap)) ||
+	             (rc = t.up(&dpf, (const int8_t*)nullptr, (size_t)nprob * cap))))
+		return rc;
+	if((rc = bt2g_sw_align_bt_dev(c, dr, dq, stride, dl, dp, nprob, dw, drc, sc, enable8, cap, dres, dc, maxaln,
+	                              maxedit, dna, dal, ded, dft, c->stream)))
+		return rc;
+	launch_sw_pack(dres, dna, dal, dc, dft, ded, nprob, cap, maxaln, maxedit, dcnt, doff, dpc, dpf, dpe, c->stream);
+	HIPCHK(hipGetLastError());
+	uint32_t tot[3];
+	if((rc = t.down(res, dres, nprob)) || (rc = t.down(naln, dna, nprob)) || (rc = t.down(alns, dal, na)) ||
+	   (rc = t.down(tot, doff + 3 * (size_t)nprob, 3)))
+		return rc;
+	if((rc = t.finish())) return rc;
+	if((rc = t.down(cands, dpc, tot[0])) || (fates && (rc = t.down(fates, dpf, tot[0]))) ||
+	   (rc = t.down(edits, dpe, tot[2])))
+		return rc;
+	if((rc = t.finish())) return rc;
+	totals[0] = tot[0];
+	totals[1] = tot[1];
+	totals[2] = tot[2];
+	for(uint32_t i = 0; i < nprob; i++)
+		if(res[i].ncand > (int32_t)cap) return fail(BT2G_ERR_OVERFLOW, "problem %u: %d candidates > cap %u", i,
+		                                             res[i].ncand, cap);
+	return BT2G_OK;
+}
+
 }  // extern "C"
 
 extern "C" {

@@ -158,6 +158,12 @@ inline uint64_t sw_bt_mdom(uint32_t rows, uint32_t cols) {
 inline uint64_t sw_bt_mslot(uint32_t rows, uint32_t cols, bool dom) {
 	return sw_bt_mdom(rows, cols) + (dom ? sw_bt_tiles_words(sw_bt_trows(rows), sw_bt_tcols(cols)) : 0u);
 }
+// sw_pack.hip: outputs of launch_sw_bt packed per problem (cnt: 3n scratch,
+// off: 3n + 3, totals last) into pc / pf (fates, may be null) / pe
+void launch_sw_pack(const bt2g_sw_result* res, const int32_t* naln, const bt2g_sw_aln* alns,
+                    const bt2g_sw_cand* cands, const int8_t* fates, const bt2g_edit* edits, uint32_t n, uint32_t cap,
+                    uint32_t maxaln, uint32_t maxedit, uint32_t* cnt, uint32_t* off, bt2g_sw_cand* pc, int8_t* pf,
+                    bt2g_edit* pe, hipStream_t st);
 void launch_sort_cands(const bt2g_sw_result* res, bt2g_sw_cand* cands, uint32_t nprob, uint32_t cap,
                        uint32_t* big, uint32_t* nbig, hipStream_t st);
 

@@ -290,6 +290,23 @@ int bt2g_sw_align_bt_dev(bt2g_ctx* ctx, const uint8_t* reads, const uint8_t* qua
                          bt2g_sw_result* res, bt2g_sw_cand* cands, uint32_t maxaln, uint32_t maxedit,
                          int32_t* naln, bt2g_sw_aln* alns, bt2g_edit* edits, int8_t* fates, void* stream);
 
+/* bt2g_sw_align_bt for host callers, with the variable-length outputs packed:
+ * res, naln and alns (nprob x maxaln slots) as there; the sorted candidates of
+ * every problem (min(ncand, cap) each), their fates (optional) and the edits of
+ * every returned alignment (min(nedit, maxedit) each) back to back in problem
+ * (and alignment) order in cands / fates / edits, which must hold nprob*cap,
+ * nprob*cap and nprob*maxaln*maxedit entries; only the first totals[0]
+ * candidates, totals[1] alignments and totals[2] edits are written.  Per-problem
+ * offsets follow from res/naln/alns by prefix sums.  Same seams as
+ * bt2g_sw_align_bt (aligner_sw.cpp:500-1146); what it saves is the copy of the
+ * unused slots (~26 KB per 150 bp end-to-end DP at cap 512, maxaln 8). */
+int bt2g_sw_align_bt_packed(bt2g_ctx* ctx, const uint8_t* reads, const uint8_t* quals, uint32_t stride,
+                            const uint32_t* lens, const bt2g_sw_problem* probs, uint32_t nprob,
+                            const uint8_t* windows, uint64_t windows_len, const bt2g_sw_rect* rects,
+                            const bt2g_scoring* sc, int enable8, uint32_t cap, bt2g_sw_result* res, uint32_t maxaln,
+                            uint32_t maxedit, int32_t* naln, bt2g_sw_aln* alns, bt2g_sw_cand* cands, int8_t* fates,
+                            bt2g_edit* edits, uint64_t* totals);
+
 /* Reserve the backtrace scratch (score plane + reportedThrough bits) for up to
  * max_problems problems of <= max_rows x max_cols, so bt2g_sw_align_bt_dev
  * neither allocates nor synchronises.  hbytes = 1 holds u8 fills only (end-to-end

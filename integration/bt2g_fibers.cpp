@@ -1,0 +1,534 @@
+// integration/bt2g_fibers.cpp -- the reference's search workers as user-mode
+// fibers: the drop-in's batch-first schedule.
+//
+// The reference runs one OS thread per search worker (`-p N` workers spawned
+// by multiseedSearch, bt2_search.cpp:4913-4925), each aligning one read at a
+// time (multiseedSearchWorker, bt2_search.cpp:3050-4197).  With the engines
+// under it, every seam call (exactSweep, oneMmSearch, searchAllSeeds,
+// ungappedAlign, SwAligner::align) becomes a batched GPU call, so the worker
+// waits at each seam; as OS threads that is a futex sleep and a wake with cold
+// caches per seam call -- ~0.7 ms of host CPU per read in round 2, 4x the
+// stock server's whole alignment.
+//
+// Here every worker the reference spawns becomes a fiber: its own stack, run
+// by one of a few carrier threads (one per core).  A seam call queues its
+// request in the carrier's outbox and switches back to the carrier, which runs
+// the next runnable fiber; once every runnable fiber has had its turn the
+// outbox goes to the seam dispatchers in one hand-off, and fibers whose
+// requests completed come back through the carrier's inbox.  The reference's
+// per-read control flow is untouched (each worker still runs its own reads in
+// program order, with its own RNG, SeedResults, SwDriver and AlnSinkWrap), so
+// the SAM is the reference's; what changes is that thousands of reads are in
+// flight on a handful of OS threads and a seam round trip costs a user-mode
+// context switch instead of a sleep/wake pair.
+//
+// Interception (integration/Makefile, -Wl,--wrap):
+//   std::thread::_M_start_thread  the worker spawn (the reference's
+//                                 std::thread(multiseedSearchWorker, tps) at
+//                                 bt2_search.cpp:4921): a thread whose state
+//                                 is a void(*)(void*) call becomes a fiber;
+//                                 every other thread (listener, connection
+//                                 threads, pat.h:2104,2163) is created as usual
+//   std::thread::detach           of a fiber's handle: nothing to detach
+//   nanosleep                     the SLEEP(10) after each spawn
+//                                 (bt2_search.cpp:4924): skipped for fibers
+//   std::condition_variable::wait a fiber waiting for reads
+//   + notify_one / notify_all     (LockedQueueCV::pop, pat.h:1996-2002) must
+//                                 not block its carrier: it registers on the
+//                                 condition variable, releases the lock and
+//                                 yields; a notify on that variable hands it
+//                                 back to its carrier, and it returns (the
+//                                 caller's predicate loop re-checks, as after
+//                                 any wake-up)
+//
+// $BT2G_FIBERS=0 keeps OS threads; $BT2G_CARRIERS sets the carrier count
+// (default: the CPUs this process may use); $BT2G_FIBER_STACK the stack size
+// in KiB (default 256; the worker's frame is 21 KiB, -fstack-usage).
+#include "bt2g_fibers.h"
+
+#include <errno.h>
+#include <malloc.h>
+#include <pthread.h>
+#include <sched.h>
+#include <stdint.h>
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+#include <sys/mman.h>
+#include <time.h>
+#include <unistd.h>
+
+#include <atomic>
+#include <chrono>
+#include <condition_variable>
+#include <memory>
+#include <mutex>
+#include <thread>
+#include <typeinfo>
+#include <unordered_map>
+#include <vector>
+
+// ---- context switch (x86-64 System V) -----------------------------------------
+// bt2gf_switch(save, to): push the callee-saved registers, the MXCSR and the
+// x87 control word, store the stack pointer at *save, load `to` and pop the
+// same frame from it.  A new fiber's stack is laid out as such a frame whose
+// return address is bt2gf_entry, which calls r13(r12).
+extern "C" void bt2gf_switch(void** save, void* to);
+extern "C" void bt2gf_entry();
+asm(R"(
+	.text
+	.globl bt2gf_switch
+	.type bt2gf_switch,@function
+bt2gf_switch:
+	pushq %rbp
+	pushq %rbx
+	pushq %r12
+	pushq %r13
+	pushq %r14
+	pushq %r15
+	subq $8, %rsp
+	stmxcsr (%rsp)
+	fnstcw 4(%rsp)
+	movq %rsp, (%rdi)
+	movq %rsi, %rsp
+	ldmxcsr (%rsp)
+	fldcw 4(%rsp)
+	addq $8, %rsp
+	popq %r15
+	popq %r14
+	popq %r13
+	popq %r12
+	popq %rbx
+	popq %rbp
+	ret
+	.size bt2gf_switch,.-bt2gf_switch
+
+	.globl bt2gf_entry
+	.type bt2gf_entry,@function
+bt2gf_entry:
+	movq %r12, %rdi
+	callq *%r13
+	ud2
+	.size bt2gf_entry,.-bt2gf_entry
+)");
+
+namespace bt2gf {
+namespace {
+
+// READY: runnable; BLOCKED: its request is with the dispatchers, or it waits on a
+// condition variable -- wake_many brings it back either way; PARKED: a timed
+// sleep, polled by its carrier; DONE: the work returned
+enum State { READY, BLOCKED, PARKED, DONE };
+
+struct Carrier;
+
+struct Fiber {
+	void* sp = nullptr;              // saved stack pointer while suspended
+	void* stack = nullptr;
+	size_t stack_bytes = 0;
+	std::thread::_State* work = nullptr;
+	Carrier* home = nullptr;
+	State state = READY;
+	uint64_t wake_at_ns = 0;          // PARKED by nanosleep: not before this time
+	const void* cv = nullptr;         // the condition variable it waits on
+};
+
+uint64_t now_ns() {
+	timespec ts;
+	clock_gettime(CLOCK_MONOTONIC, &ts);
+	return (uint64_t)ts.tv_sec * 1000000000ull + (uint64_t)ts.tv_nsec;
+}
+
+const bool g_dbg = getenv("BT2G_FIBER_DEBUG") != nullptr;
+#define FDBG(...) do { if(g_dbg) fprintf(stderr, __VA_ARGS__); } while(0)
+
+FlushFn g_flush = nullptr;
+InitFn g_init = nullptr;
+
+struct Carrier {
+	std::thread th;
+	void* sched_sp = nullptr;        // the scheduler's context while a fiber runs
+	Fiber* cur = nullptr;
+	std::vector<Fiber*> ready, round, parked;
+	std::vector<void*> outbox;
+	// fibers handed to this carrier: new ones and those whose requests completed
+	std::mutex mu;
+	std::condition_variable cv;
+	std::vector<Fiber*> inbox;
+	bool sleeping = false;
+
+	void run();
+	void flush() {
+		if(outbox.empty()) return;
+		FDBG("carrier %p: flush %zu\n", (void*)this, outbox.size());
+		g_flush(outbox.data(), outbox.size());
+		outbox.clear();
+	}
+};
+
+thread_local Carrier* t_carrier = nullptr;   // set on carrier threads only
+thread_local int t_skip_sleep = 0;            // spawns whose SLEEP(10) is skipped
+
+std::mutex g_mu;                              // carriers, fiber handles
+// fibers waiting on each condition variable (woken by its notify_one/_all)
+std::mutex g_cv_mu;
+std::unordered_map<const void*, std::vector<Fiber*>> g_cv_waiters;
+std::vector<Carrier*> g_carriers;
+size_t g_next_carrier = 0;
+// fibers' std::thread ids: tagged in the top 16 bits (a pthread_t is a user-space
+// address, below 2^47)
+const uintptr_t FIBER_HANDLE_TAG = 0xF1BE;
+uintptr_t g_next_handle = 0;
+
+size_t stack_bytes() {
+	static const size_t sz = [] {
+		const char* e = getenv("BT2G_FIBER_STACK");
+		size_t kb = e ? (size_t)atol(e) : 256;
+		if(kb < 64) kb = 64;
+		return kb << 10;
+	}();
+	return sz;
+}
+
+// CPUs this process may use: the affinity mask, capped by a cgroup v2 CPU
+// quota (the GPU box gives a 16-CPU quota over a 256-CPU affinity mask)
+size_t usable_cpus() {
+	size_t n = 0;
+	cpu_set_t set;
+	if(sched_getaffinity(0, sizeof(set), &set) == 0) n = (size_t)CPU_COUNT(&set);
+	if(n == 0) {
+		long m = sysconf(_SC_NPROCESSORS_ONLN);
+		n = m > 0 ? (size_t)m : 1;
+	}
+	if(FILE* f = fopen("/sys/fs/cgroup/cpu.max", "r")) {
+		char q[64] = {0};
+		unsigned long period = 0;
+		if(fscanf(f, "%63s %lu", q, &period) == 2 && strcmp(q, "max") != 0 && period > 0) {
+			const size_t cap = (size_t)((strtoul(q, nullptr, 10) + period - 1) / period);
+			if(cap > 0 && cap < n) n = cap;
+		}
+		fclose(f);
+	}
+	return n;
+}
+
+size_t n_carriers() {
+	const char* e = getenv("BT2G_CARRIERS");
+	if(e && atoi(e) > 0) return (size_t)atoi(e);
+	return usable_cpus();
+}
+
+[[noreturn]] void fiber_main(Fiber* f);
+
+void switch_to(Carrier* c, Fiber* f) {
+	c->cur = f;
+	f->state = READY;
+	bt2gf_switch(&c->sched_sp, f->sp);
+	c->cur = nullptr;
+}
+
+// Back to the carrier's scheduler, leaving the fiber in state `st`.
+void suspend(Fiber* f, State st) {
+	f->state = st;
+	bt2gf_switch(&f->sp, f->home->sched_sp);
+}
+
+void fiber_main(Fiber* f) {
+	f->work->_M_run();
+	delete f->work;
+	f->work = nullptr;
+	suspend(f, DONE);
+	abort();   // a finished fiber is never resumed
+}
+
+}  // namespace
+}  // namespace bt2gf
+extern "C" void bt2g_prof_thread();
+namespace bt2gf {
+namespace {
+
+void Carrier::run() {
+	t_carrier = this;
+	bt2g_prof_thread();
+	char nm[16];
+	snprintf(nm, sizeof(nm), "bt2g-carrier");
+	pthread_setname_np(pthread_self(), nm);
+	uint64_t last_poll = 0;
+	for(;;) {
+		{
+			std::lock_guard<std::mutex> lk(mu);
+			if(!inbox.empty()) {
+				ready.insert(ready.end(), inbox.begin(), inbox.end());
+				inbox.clear();
+			}
+		}
+		if(!parked.empty()) {
+			// timed sleeps: re-run them when due (checked when nothing else is
+			// runnable, and at least every 100 us)
+			const uint64_t t = now_ns();
+			if(ready.empty() || t - last_poll > 100000) {
+				last_poll = t;
+				size_t k = 0;
+				for(Fiber* f : parked) {
+					if(f->wake_at_ns && f->wake_at_ns > t) parked[k++] = f;
+					else ready.push_back(f);
+				}
+				parked.resize(k);
+			}
+		}
+		if(ready.empty()) {
+			flush();
+			std::unique_lock<std::mutex> lk(mu);
+			sleeping = true;
+			if(parked.empty()) cv.wait(lk, [this] { return !inbox.empty(); });
+			else cv.wait_for(lk, std::chrono::microseconds(100), [this] { return !inbox.empty(); });
+			sleeping = false;
+			continue;
+		}
+		round.swap(ready);
+		for(Fiber* f : round) {
+			FDBG("carrier %p: run fiber %p\n", (void*)this, (void*)f);
+			switch_to(this, f);
+			FDBG("carrier %p: fiber %p -> state %d\n", (void*)this, (void*)f, (int)f->state);
+			switch(f->state) {
+			case READY: ready.push_back(f); break;
+			case PARKED: parked.push_back(f); break;
+			case BLOCKED: break;        // its request is in the outbox; wake_many brings it back
+			case DONE:
+				munmap(f->stack, f->stack_bytes);
+				delete f;
+				break;
+			}
+		}
+		round.clear();
+		flush();
+	}
+}
+
+Carrier* pick_carrier() {
+	// under g_mu
+	if(g_carriers.empty()) {
+		const size_t n = n_carriers();
+		for(size_t i = 0; i < n; i++) g_carriers.push_back(new Carrier());
+		for(Carrier* c : g_carriers) c->th = std::thread(&Carrier::run, c);
+		for(Carrier* c : g_carriers) c->th.detach();
+	}
+	Carrier* c = g_carriers[g_next_carrier % g_carriers.size()];
+	g_next_carrier++;
+	return c;
+}
+
+Fiber* make_fiber(std::thread::_State* work) {
+	Fiber* f = new Fiber();
+	f->work = work;
+	const size_t page = (size_t)sysconf(_SC_PAGESIZE);
+	f->stack_bytes = stack_bytes() + page;
+	void* mem = mmap(nullptr, f->stack_bytes, PROT_READ | PROT_WRITE,
+	                 MAP_PRIVATE | MAP_ANONYMOUS | MAP_NORESERVE | MAP_STACK, -1, 0);
+	if(mem == MAP_FAILED) {
+		fprintf(stderr, "bt2g fibers: cannot map a %zu-byte stack: %s\n", f->stack_bytes, strerror(errno));
+		abort();
+	}
+	mprotect(mem, page, PROT_NONE);   // guard page: an overflow faults instead of corrupting
+	f->stack = mem;
+	// initial frame popped by bt2gf_switch: [mxcsr|fpucw][r15][r14][r13][r12][rbx][rbp][ret];
+	// after its ret rsp == top (16-aligned), as before a call: bt2gf_entry's call is aligned
+	uintptr_t top = ((uintptr_t)mem + f->stack_bytes) & ~(uintptr_t)15;
+	uint64_t* sp = (uint64_t*)top;
+	*--sp = (uint64_t)(uintptr_t)&bt2gf_entry;   // ret
+	*--sp = 0;                                   // rbp
+	*--sp = 0;                                   // rbx
+	*--sp = (uint64_t)(uintptr_t)f;              // r12: argument
+	*--sp = (uint64_t)(uintptr_t)&fiber_main;    // r13: function
+	*--sp = 0;                                   // r14
+	*--sp = 0;                                   // r15
+	uint32_t csr[2] = {0x1f80u, 0x037fu};        // default MXCSR, x87 control word
+	__asm__ volatile("stmxcsr %0" : "=m"(csr[0]));
+	__asm__ volatile("fnstcw %0" : "=m"(csr[1]));
+	--sp;
+	memcpy(sp, csr, 8);
+	f->sp = sp;
+	return f;
+}
+
+Fiber* cur_fiber() { return t_carrier ? t_carrier->cur : nullptr; }
+
+// Allocator settings for thousands of workers on a few threads: no heap
+// trimming and no mmap for blocks below 32 MB (the dispatchers' batch buffers
+// and the workers' per-read lists otherwise cycle pages through mprotect /
+// madvise and page faults).
+struct MallocTuning {
+	MallocTuning() {
+		if(!enabled()) return;
+		mallopt(M_MMAP_THRESHOLD, 32 << 20);
+		mallopt(M_TRIM_THRESHOLD, 1 << 30);
+		mallopt(M_TOP_PAD, 16 << 20);
+	}
+} g_malloc_tuning;
+
+}  // namespace
+
+void* self() { return cur_fiber(); }
+
+bool enabled() {
+	static const bool on = [] {
+		const char* e = getenv("BT2G_FIBERS");
+		return !(e && e[0] == '0');
+	}();
+	return on;
+}
+
+void set_flush(FlushFn fn) { g_flush = fn; }
+void set_init(InitFn fn) { g_init = fn; }
+
+void block_on(void* req) {
+	Fiber* f = cur_fiber();
+	f->home->outbox.push_back(req);
+	suspend(f, BLOCKED);
+}
+
+void wake_many(void* const* fibers, size_t n) {
+	// grouped per carrier: one lock (and at most one wake-up) per carrier
+	thread_local std::vector<std::pair<Carrier*, std::vector<Fiber*>>> groups;
+	for(size_t i = 0; i < n; i++) {
+		Fiber* f = static_cast<Fiber*>(fibers[i]);
+		size_t g = 0;
+		while(g < groups.size() && groups[g].first != f->home) g++;
+		if(g == groups.size()) groups.emplace_back(f->home, std::vector<Fiber*>());
+		groups[g].second.push_back(f);
+	}
+	for(auto& g : groups) {
+		if(g.second.empty()) continue;
+		Carrier* c = g.first;
+		bool notify;
+		{
+			std::lock_guard<std::mutex> lk(c->mu);
+			c->inbox.insert(c->inbox.end(), g.second.begin(), g.second.end());
+			notify = c->sleeping;
+		}
+		if(notify) c->cv.notify_one();
+		g.second.clear();
+	}
+}
+
+}  // namespace bt2gf
+
+// ---- interception ---------------------------------------------------------------
+using namespace bt2gf;
+
+extern "C" {
+
+void __real__ZNSt6thread15_M_start_threadESt10unique_ptrINS_6_StateESt14default_deleteIS1_EEPFvvE(
+	std::thread* self, std::unique_ptr<std::thread::_State> st, void (*dep)());
+void __real__ZNSt6thread6detachEv(std::thread* self);
+void __real__ZNSt18condition_variable4waitERSt11unique_lockISt5mutexE(std::condition_variable* cv,
+                                                                      std::unique_lock<std::mutex>& lk);
+int __real_nanosleep(const struct timespec* req, struct timespec* rem);
+
+// std::thread's constructor: the search workers (a void(*)(void*) and its
+// argument: std::thread(multiseedSearchWorker, (void*)&tps[i])) become fibers.
+void __wrap__ZNSt6thread15_M_start_threadESt10unique_ptrINS_6_StateESt14default_deleteIS1_EEPFvvE(
+	std::thread* self, std::unique_ptr<std::thread::_State> st, void (*dep)()) {
+	static const char* const WORKER = "NSt6thread11_State_implINS_8_InvokerISt5tupleIJPFvPvES3_EEEEEE";
+	FDBG("start_thread: %s\n", st ? typeid(*st).name() : "null");
+	if(!enabled() || !st || strcmp(typeid(*st).name(), WORKER) != 0) {
+		__real__ZNSt6thread15_M_start_threadESt10unique_ptrINS_6_StateESt14default_deleteIS1_EEPFvvE(
+			self, std::move(st), dep);
+		return;
+	}
+	static std::once_flag once;
+	std::call_once(once, [] {
+		if(g_init) g_init();
+		if(!g_flush) {
+			fprintf(stderr, "bt2g fibers: no seam dispatcher registered\n");
+			abort();
+		}
+	});
+	Fiber* f = make_fiber(st.release());
+	uintptr_t handle;
+	Carrier* c;
+	{
+		std::lock_guard<std::mutex> lk(g_mu);
+		c = pick_carrier();
+		f->home = c;
+		handle = ((uintptr_t)FIBER_HANDLE_TAG << 48) | ++g_next_handle;
+	}
+	*reinterpret_cast<std::thread::native_handle_type*>(self) = (std::thread::native_handle_type)handle;
+	t_skip_sleep++;
+	void* one = f;
+	wake_many(&one, 1);
+}
+
+void __wrap__ZNSt6thread6detachEv(std::thread* self) {
+	const uintptr_t h = (uintptr_t) * reinterpret_cast<std::thread::native_handle_type*>(self);
+	if((h >> 48) == FIBER_HANDLE_TAG) {      // a fiber's handle: nothing to detach
+		*reinterpret_cast<std::thread::native_handle_type*>(self) = 0;
+		return;
+	}
+	__real__ZNSt6thread6detachEv(self);
+}
+
+void __wrap__ZNSt18condition_variable4waitERSt11unique_lockISt5mutexE(std::condition_variable* cv,
+                                                                      std::unique_lock<std::mutex>& lk) {
+	Fiber* f = cur_fiber();
+	if(!f) {
+		__real__ZNSt18condition_variable4waitERSt11unique_lockISt5mutexE(cv, lk);
+		return;
+	}
+	// registered while the caller still holds the lock: a notifier that changes
+	// the predicate's state under that lock cannot notify before we are on the list
+	f->cv = cv;
+	{
+		std::lock_guard<std::mutex> g(g_cv_mu);
+		g_cv_waiters[cv].push_back(f);
+	}
+	lk.unlock();
+	suspend(f, BLOCKED);
+	lk.lock();
+}
+
+// notify: fibers waiting on `cv` go back to their carriers, then the OS threads
+static void wake_cv_fibers(const void* cv, bool all) {
+	std::vector<Fiber*> w;
+	{
+		std::lock_guard<std::mutex> g(g_cv_mu);
+		auto it = g_cv_waiters.find(cv);
+		if(it == g_cv_waiters.end() || it->second.empty()) return;
+		if(all) {
+			w.swap(it->second);
+		} else {
+			w.push_back(it->second.front());
+			it->second.erase(it->second.begin());
+		}
+	}
+	wake_many(reinterpret_cast<void* const*>(w.data()), w.size());
+}
+
+void __real__ZNSt18condition_variable10notify_allEv(std::condition_variable* cv);
+void __real__ZNSt18condition_variable10notify_oneEv(std::condition_variable* cv);
+
+void __wrap__ZNSt18condition_variable10notify_allEv(std::condition_variable* cv) {
+	wake_cv_fibers(cv, true);
+	__real__ZNSt18condition_variable10notify_allEv(cv);
+}
+
+void __wrap__ZNSt18condition_variable10notify_oneEv(std::condition_variable* cv) {
+	wake_cv_fibers(cv, false);
+	__real__ZNSt18condition_variable10notify_oneEv(cv);
+}
+
+int __wrap_nanosleep(const struct timespec* req, struct timespec* rem) {
+	if(t_skip_sleep > 0) {          // the spawn loop's SLEEP(10) after a fiber was created
+		t_skip_sleep--;
+		return 0;
+	}
+	Fiber* f = cur_fiber();
+	if(!f || !req) return __real_nanosleep(req, rem);
+	f->wake_at_ns = now_ns() + (uint64_t)req->tv_sec * 1000000000ull + (uint64_t)req->tv_nsec;
+	suspend(f, PARKED);
+	f->wake_at_ns = 0;
+	if(rem) rem->tv_sec = rem->tv_nsec = 0;
+	return 0;
+}
+
+}  // extern "C"

@@ -55,6 +55,8 @@
 #include <thread>
 #include <vector>
 #include <limits>
+#include <memory>
+#include <unordered_map>
 
 #include "aligner_seed.h"
 #include "aligner_cache.h"
@@ -62,6 +64,9 @@
 #include "read.h"
 #include "scoring.h"
 #include "bt2g.h"
+#include "bt2g_fibers.h"
+
+extern "C" void bt2g_prof_thread();   // bt2g_prof.cpp: CPU samples of this thread ($BT2G_SAMPLE)
 
 namespace {
 
@@ -182,14 +187,14 @@ bool to_scoring(const Scoring& sc, bt2g_scoring& o) {
 	return true;
 }
 
-// A read as one row of codes (0..4) and Phred+33 qualities.
+// A read as one row of codes (0..4) and Phred+33 qualities, inline: requests
+// live on the caller's (fiber's) stack and allocate nothing.
 struct Row {
-	std::vector<uint8_t> codes, quals;
 	uint32_t len = 0;
+	uint8_t codes[BT2G_MAX_READ_LEN];
+	uint8_t quals[BT2G_MAX_READ_LEN];
 	void set(const BTDnaString& s, const BTString& q) {
-		len = (uint32_t)s.length();
-		codes.resize(len ? len : 1);
-		quals.resize(len ? len : 1);
+		len = (uint32_t)std::min<size_t>(s.length(), BT2G_MAX_READ_LEN);
 		for(uint32_t i = 0; i < len; i++) {
 			codes[i] = (uint8_t)s[i];
 			quals[i] = (uint8_t)q[i];
@@ -208,15 +213,38 @@ struct Row {
 	}
 };
 
+// Outputs owned by the requester: up to N inline, a heap vector beyond.  The
+// dispatcher writes them; keeping them inline means no block allocated by a
+// dispatcher thread is freed by a carrier thread (glibc arena locks: 30 % of
+// the host CPU in r03a).
+template <typename T, size_t N>
+struct Out {
+	T inl[N];
+	std::vector<T> big;
+	size_t n = 0;
+	void assign(const T* p, size_t k) {
+		n = k;
+		T* d = inl;
+		if(k > N) {
+			big.assign(p, p + k);
+			return;
+		}
+		if(k) memcpy(d, p, k * sizeof(T));
+	}
+	const T* data() const { return n > N ? big.data() : inl; }
+	size_t size() const { return n; }
+	const T& operator[](size_t i) const { return data()[i]; }
+};
+
 // ---- requests and the dispatcher ---------------------------------------------
 struct Req {
 	int kind;
 	uint64_t key;        // batch-wide arguments: requests with equal keys share one call
 	int rc = 0;
 	char err[256] = {0}; // bt2g_last_error() of the thread that ran the call
+	void* fiber = nullptr;   // the waiting fiber (bt2g_fibers.cpp), else an OS thread on sem
 	sem_t sem;
-	Req(int k, uint64_t ky) : kind(k), key(ky) { sem_init(&sem, 0, 0); }
-	~Req() { sem_destroy(&sem); }
+	Req(int k, uint64_t ky) : kind(k), key(ky) {}
 };
 
 struct ExactReq : Req {      // bt2g_exact_sweep
@@ -233,7 +261,7 @@ struct MmReq : Req {         // bt2g_one_mm
 	int32_t minsc;
 	int nofw, norc;
 	bt2g_scoring sc;
-	std::vector<bt2g_mm1> hits;
+	Out<bt2g_mm1, 32> hits;
 	int32_t cnt = 0;
 	uint32_t ops = 0;
 	MmReq(int f, int c, const bt2g_scoring& s)
@@ -243,7 +271,7 @@ struct MmReq : Req {         // bt2g_one_mm
 struct SeedReq : Req {       // bt2g_seed_search
 	Row r;
 	uint32_t seedlen, per, off, nof;
-	std::vector<uint32_t> out;
+	Out<uint32_t, 2 * 32 * 4> out;    // [strand][seed offset][topf, botf, topb, botb]
 	int32_t ns = 0;
 	uint32_t ops = 0;
 	SeedReq(uint32_t L, uint32_t p, uint32_t o, uint32_t n)
@@ -256,9 +284,11 @@ struct UgReq : Req {         // bt2g_ungapped
 	bt2g_scoring sc;
 	int ohang;
 	bt2g_ug_result o;
-	std::vector<bt2g_edit> ed;
+	Out<bt2g_edit, 64> ed;
 	UgReq(const bt2g_scoring& s, int oh) : Req(ST_UG, (uint64_t)oh | ((uint64_t)s.local << 1)), sc(s), ohang(oh) {}
 };
+
+struct DpState;
 
 struct DpReq : Req {         // bt2g_sw_align_bt
 	Row r;
@@ -269,18 +299,37 @@ struct DpReq : Req {         // bt2g_sw_align_bt
 	int enable8;
 	uint32_t cap, maxaln, maxedit;
 	bt2g_sw_result o;
-	std::vector<bt2g_sw_cand> cands;
-	std::vector<int8_t> fates;
-	std::vector<bt2g_sw_aln> alns;
-	std::vector<bt2g_edit> edits;
+	DpState* st;                 // the SwAligner's state: receives candidates, fates, alignments, edits
 	int32_t naln = 0;
 	bool cpu = false;            // more candidates than the engine takes (> 8192): the CPU path
 	// reads longer than 1024 bases batch apart (another fill; a batch is padded to its longest read)
-	DpReq(const bt2g_scoring& s, int e8, bool lng)
-		: Req(ST_DP, (uint64_t)e8 | ((uint64_t)s.local << 1) | ((uint64_t)lng << 2)), sc(s), enable8(e8) {}
+	DpReq(const bt2g_scoring& s, int e8, bool lng, DpState* state)
+		: Req(ST_DP, (uint64_t)e8 | ((uint64_t)s.local << 1) | ((uint64_t)lng << 2)), sc(s), enable8(e8), st(state) {}
 };
 
-// Rows of a batch as one [n][stride] array (stride = longest read).
+// Per-SwAligner state between align() and the nextAlignment() calls (one per
+// SwAligner of each worker; its vectors keep their capacity read after read).
+struct DpState {
+	bool gpu = false;          // served by the engine (else the reference's CPU path)
+	bool u8 = false;           // u8 fill succeeded (RNG re-seed rule, aligner_sw.cpp:877 vs 932)
+	std::vector<bt2g_sw_cand> cands;   // the sorted candidates
+	std::vector<int8_t> fates; // engine's DpBtCandidate::fate per candidate
+	std::vector<bt2g_sw_aln> alns;
+	std::vector<bt2g_edit> edits;   // of every alignment, back to back
+	uint32_t maxedit = 0;
+	int32_t naln = 0;
+	uint32_t next = 0;         // next engine alignment to hand out
+	size_t next_edit = 0;      // its first edit
+	// the problem as sent to the engine (for $BT2G_ADAPTER_DUMP on a mismatch)
+	Row row;
+	bt2g_sw_problem prob;
+	bt2g_sw_rect rect;
+	std::vector<uint8_t> win;
+	int enable8 = 1;
+};
+
+// Rows of a batch as one [n][stride] array (stride = longest read); one per
+// dispatcher thread, reused call after call.
 struct Pack {
 	std::vector<uint8_t> codes, quals;
 	std::vector<uint32_t> lens;
@@ -289,21 +338,29 @@ struct Pack {
 	void build(const std::vector<R*>& v) {
 		stride = 1;
 		for(R* q : v) stride = std::max(stride, q->r.len);
-		codes.assign(v.size() * (size_t)stride, 4);
-		quals.assign(v.size() * (size_t)stride, 'I');
+		codes.resize(v.size() * (size_t)stride);
+		quals.resize(v.size() * (size_t)stride);
 		lens.resize(v.size());
 		for(size_t i = 0; i < v.size(); i++) {
-			lens[i] = v[i]->r.len;
-			memcpy(&codes[i * stride], v[i]->r.codes.data(), v[i]->r.len);
-			memcpy(&quals[i * stride], v[i]->r.quals.data(), v[i]->r.len);
+			const uint32_t L = v[i]->r.len;
+			lens[i] = L;
+			uint8_t* c = &codes[i * stride];
+			uint8_t* q = &quals[i * stride];
+			memcpy(c, v[i]->r.codes, L);
+			memcpy(q, v[i]->r.quals, L);
+			if(L < stride) {
+				memset(c + L, 4, stride - L);
+				memset(q + L, 'I', stride - L);
+			}
 		}
 	}
 };
 
 int run_exact(const std::vector<ExactReq*>& v) {
-	Pack pk;
+	thread_local Pack pk;
+	thread_local std::vector<uint32_t> out;
 	pk.build(v);
-	std::vector<uint32_t> out(8 * v.size());
+	out.resize(8 * v.size());
 	int rc = bt2g_exact_sweep(cur_ctx(), pk.codes.data(), pk.stride, pk.lens.data(), (uint32_t)v.size(), v[0]->mine_max,
 	                          v[0]->nofw, v[0]->norc, out.data());
 	if(rc) return rc;
@@ -312,125 +369,195 @@ int run_exact(const std::vector<ExactReq*>& v) {
 }
 
 int run_mm(const std::vector<MmReq*>& v, uint32_t cap = 16) {
-	Pack pk;
-	pk.build(v);
+	struct B {
+		Pack pk;
+		std::vector<int32_t> ms, cnt;
+		std::vector<uint32_t> ops;
+		std::vector<bt2g_mm1> h;
+	};
+	thread_local B b;
+	b.pk.build(v);
 	const size_t n = v.size();
-	std::vector<int32_t> ms(n), cnt(n);
-	std::vector<uint32_t> ops(n);
-	std::vector<bt2g_mm1> h(n * cap);
-	for(size_t i = 0; i < n; i++) ms[i] = v[i]->minsc;
-	int rc = bt2g_one_mm(cur_ctx(), pk.codes.data(), pk.quals.data(), pk.stride, pk.lens.data(), (uint32_t)n, ms.data(),
-	                     &v[0]->sc, v[0]->nofw, v[0]->norc, cap, h.data(), cnt.data(), ops.data(), nullptr);
+	b.ms.resize(n);
+	b.cnt.resize(n);
+	b.ops.resize(n);
+	b.h.resize(n * cap);
+	for(size_t i = 0; i < n; i++) b.ms[i] = v[i]->minsc;
+	int rc = bt2g_one_mm(cur_ctx(), b.pk.codes.data(), b.pk.quals.data(), b.pk.stride, b.pk.lens.data(), (uint32_t)n,
+	                     b.ms.data(), &v[0]->sc, v[0]->nofw, v[0]->norc, cap, b.h.data(), b.cnt.data(), b.ops.data(),
+	                     nullptr);
 	if(rc && rc != BT2G_ERR_OVERFLOW) return rc;
+	std::vector<std::pair<MmReq*, uint32_t>> again;    // more hits than the batch slots: alone, after
 	for(size_t i = 0; i < n; i++) {
-		if(cnt[i] > (int32_t)cap) {          // more hits than the batch slots: this read again, alone
-			std::vector<MmReq*> one{v[i]};
-			if((rc = run_mm(one, (uint32_t)cnt[i]))) return rc;
+		if(b.cnt[i] > (int32_t)cap) {
+			again.emplace_back(v[i], (uint32_t)b.cnt[i]);
 			continue;
 		}
-		v[i]->cnt = cnt[i];
-		v[i]->ops = ops[i];
-		v[i]->hits.assign(h.begin() + i * cap, h.begin() + i * cap + cnt[i]);
+		v[i]->cnt = b.cnt[i];
+		v[i]->ops = b.ops[i];
+		v[i]->hits.assign(&b.h[i * cap], (size_t)b.cnt[i]);
+	}
+	for(auto& qa : again) {
+		std::vector<MmReq*> one{qa.first};
+		if((rc = run_mm(one, qa.second))) return rc;
 	}
 	return BT2G_OK;
 }
 
 int run_seeds(const std::vector<SeedReq*>& v) {
-	Pack pk;
-	pk.build(v);
+	struct B {
+		Pack pk;
+		std::vector<uint32_t> out, ops;
+		std::vector<int32_t> ns;
+		std::vector<uint32_t> tmp;
+	};
+	thread_local B b;
+	b.pk.build(v);
 	const size_t n = v.size();
 	uint32_t maxs = 1;
 	for(SeedReq* q : v) maxs = std::max(maxs, q->nof);
-	std::vector<uint32_t> out(n * 2 * maxs * 4), ops(n);
-	std::vector<int32_t> ns(n);
-	int rc = bt2g_seed_search(cur_ctx(), pk.codes.data(), pk.stride, pk.lens.data(), (uint32_t)n, v[0]->seedlen, v[0]->per,
-	                          v[0]->off, maxs, out.data(), ns.data(), ops.data(), nullptr);
+	b.out.resize(n * 2 * maxs * 4);
+	b.ops.resize(n);
+	b.ns.resize(n);
+	int rc = bt2g_seed_search(cur_ctx(), b.pk.codes.data(), b.pk.stride, b.pk.lens.data(), (uint32_t)n, v[0]->seedlen,
+	                          v[0]->per, v[0]->off, maxs, b.out.data(), b.ns.data(), b.ops.data(), nullptr);
 	if(rc) return rc;
 	for(size_t i = 0; i < n; i++) {
 		SeedReq* q = v[i];
-		q->ns = ns[i];
-		q->ops = ops[i];
-		q->out.assign(2 * (size_t)q->nof * 4, 0);
+		q->ns = b.ns[i];
+		q->ops = b.ops[i];
+		b.tmp.assign(2 * (size_t)q->nof * 4, 0);
 		for(int f = 0; f < 2; f++)
 			for(uint32_t k = 0; k < q->nof && k < maxs; k++)
-				memcpy(&q->out[((size_t)f * q->nof + k) * 4], &out[((i * 2 + f) * maxs + k) * 4], 16);
+				memcpy(&b.tmp[((size_t)f * q->nof + k) * 4], &b.out[((i * 2 + f) * maxs + k) * 4], 16);
+		q->out.assign(b.tmp.data(), b.tmp.size());
 	}
 	return BT2G_OK;
 }
 
 int run_ug(const std::vector<UgReq*>& v) {
-	Pack pk;
-	pk.build(v);
+	struct B {
+		Pack pk;
+		std::vector<bt2g_ug_problem> P;
+		std::vector<bt2g_ug_result> R;
+		std::vector<bt2g_edit> E;
+	};
+	thread_local B b;
+	b.pk.build(v);
 	const size_t n = v.size();
-	const uint32_t maxedit = pk.stride + 1;
-	std::vector<bt2g_ug_problem> P(n);
-	std::vector<bt2g_ug_result> R(n);
-	std::vector<bt2g_edit> E(n * maxedit);
+	const uint32_t maxedit = b.pk.stride + 1;
+	b.P.resize(n);
+	b.R.resize(n);
+	b.E.resize(n * maxedit);
 	for(size_t i = 0; i < n; i++) {
-		P[i] = v[i]->p;
-		P[i].read = (uint32_t)i;
+		b.P[i] = v[i]->p;
+		b.P[i].read = (uint32_t)i;
 	}
-	int rc = bt2g_ungapped(cur_ctx(), pk.codes.data(), pk.quals.data(), pk.stride, pk.lens.data(), P.data(), (uint32_t)n,
-	                       &v[0]->sc, v[0]->ohang, maxedit, R.data(), E.data());
+	int rc = bt2g_ungapped(cur_ctx(), b.pk.codes.data(), b.pk.quals.data(), b.pk.stride, b.pk.lens.data(), b.P.data(),
+	                       (uint32_t)n, &v[0]->sc, v[0]->ohang, maxedit, b.R.data(), b.E.data());
 	if(rc) return rc;
 	for(size_t i = 0; i < n; i++) {
-		v[i]->o = R[i];
-		v[i]->ed.assign(E.begin() + i * maxedit, E.begin() + (i + 1) * maxedit);
+		v[i]->o = b.R[i];
+		const int32_t ne = b.R[i].ret == 1 ? std::min<int32_t>(std::max<int32_t>(b.R[i].nedit, 0), (int32_t)maxedit) : 0;
+		v[i]->ed.assign(&b.E[i * maxedit], (size_t)ne);
 	}
 	return BT2G_OK;
 }
 
-// Fill + gather + the nextAlignment loop for every DP of the batch.  A DP
-// whose candidate list outgrew `cap`, or that may have more than `maxaln`
-// alignments, runs again alone with room for all of them.
-int run_dp(const std::vector<DpReq*>& v, uint32_t cap = 0, uint32_t maxaln = 8) {
+// Fill + gather + the nextAlignment loop for every DP of the batch
+// (bt2g_sw_align_bt_packed: only the candidates, fates and edits the problems
+// produced come back).  A DP whose candidate list outgrew `cap`, or that may
+// have more than `maxaln` alignments, runs again alone with room for all of them.
+struct DpBufs {      // per dispatcher thread, grown as needed, never shrunk
 	Pack pk;
+	std::vector<bt2g_sw_problem> P;
+	std::vector<bt2g_sw_rect> RC;
+	std::vector<uint8_t> W;
+	std::vector<bt2g_sw_result> R;
+	std::vector<int32_t> NA;
+	std::vector<bt2g_sw_aln> A;
+	std::unique_ptr<bt2g_sw_cand[]> C;
+	std::unique_ptr<int8_t[]> F;
+	std::unique_ptr<bt2g_edit[]> E;
+	size_t ncap = 0, necap = 0;
+};
+
+int run_dp(const std::vector<DpReq*>& v, uint32_t cap = 0, uint32_t maxaln = 8) {
+	thread_local DpBufs b;
+	Pack& pk = b.pk;
 	pk.build(v);
 	const size_t n = v.size();
 	if(cap == 0) cap = v[0]->sc.local ? 2048 : 512;
 	const uint32_t maxedit = 2 * pk.stride + 8;
-	std::vector<bt2g_sw_problem> P(n);
-	std::vector<bt2g_sw_rect> RC(n);
-	std::vector<uint8_t> W;
+	b.P.resize(n);
+	b.RC.resize(n);
+	b.W.clear();
 	for(size_t i = 0; i < n; i++) {
-		P[i] = v[i]->p;
-		P[i].read = (uint32_t)i;
-		P[i].win_off = (int64_t)W.size();
-		W.insert(W.end(), v[i]->win.begin(), v[i]->win.end());
-		RC[i] = v[i]->rect;
+		b.P[i] = v[i]->p;
+		b.P[i].read = (uint32_t)i;
+		b.P[i].win_off = (int64_t)b.W.size();
+		b.W.insert(b.W.end(), v[i]->win.begin(), v[i]->win.end());
+		b.RC[i] = v[i]->rect;
 	}
-	std::vector<bt2g_sw_result> R(n);
-	std::vector<bt2g_sw_cand> C(n * cap);
-	std::vector<int8_t> F(n * cap);
-	std::vector<int32_t> NA(n);
-	std::vector<bt2g_sw_aln> A(n * maxaln);
-	std::vector<bt2g_edit> E(n * maxaln * (size_t)maxedit);
-	int rc = bt2g_sw_align_bt(cur_ctx(), pk.codes.data(), pk.quals.data(), pk.stride, pk.lens.data(), P.data(),
-	                          (uint32_t)n, W.data(), W.size(), RC.data(), &v[0]->sc, v[0]->enable8, cap, R.data(),
-	                          C.data(), maxaln, maxedit, NA.data(), A.data(), E.data(), F.data());
+	b.R.resize(n);
+	b.NA.resize(n);
+	b.A.resize(n * maxaln);
+	// packed outputs: worst-case capacity, only the used prefix is ever touched
+	if(b.ncap < n * (size_t)cap) {
+		b.ncap = n * (size_t)cap;
+		b.C.reset(new bt2g_sw_cand[b.ncap]);
+		b.F.reset(new int8_t[b.ncap]);
+	}
+	if(b.necap < n * (size_t)maxaln * maxedit) {
+		b.necap = n * (size_t)maxaln * maxedit;
+		b.E.reset(new bt2g_edit[b.necap]);
+	}
+	uint64_t tot[3] = {0, 0, 0};
+	int rc = bt2g_sw_align_bt_packed(cur_ctx(), pk.codes.data(), pk.quals.data(), pk.stride, pk.lens.data(), b.P.data(),
+	                                 (uint32_t)n, b.W.data(), b.W.size(), b.RC.data(), &v[0]->sc, v[0]->enable8, cap,
+	                                 b.R.data(), maxaln, maxedit, b.NA.data(), b.A.data(), b.C.get(), b.F.get(),
+	                                 b.E.get(), tot);
 	if(rc && rc != BT2G_ERR_OVERFLOW) return rc;
+	std::vector<std::pair<DpReq*, uint32_t>> again;      // (their own calls below reuse b)
+	size_t oc = 0, oe = 0;
 	for(size_t i = 0; i < n; i++) {
 		DpReq* q = v[i];
-		if(R[i].ncand > 8192) {      // beyond the engine's candidate capacity
+		const bt2g_sw_result& r = b.R[i];
+		const uint32_t nc = (uint32_t)std::min<int64_t>(std::max<int32_t>(r.ncand, 0), cap);
+		const uint32_t na = (uint32_t)std::min<int64_t>(std::max<int32_t>(b.NA[i], 0), maxaln);
+		uint32_t ne = 0;
+		for(uint32_t k = 0; k < na; k++)
+			ne += (uint32_t)std::min<int64_t>(std::max<int32_t>(b.A[i * maxaln + k].nedit, 0), maxedit);
+		const size_t c0 = oc, e0 = oe;
+		oc += nc;
+		oe += ne;
+		if(r.ncand > 8192) {         // beyond the engine's candidate capacity
 			q->cpu = true;
 			continue;
 		}
-		if(R[i].ncand > (int32_t)cap || (NA[i] == (int32_t)maxaln && R[i].ncand > (int32_t)maxaln)) {
-			std::vector<DpReq*> one{q};
-			if((rc = run_dp(one, std::max<uint32_t>(cap, (uint32_t)R[i].ncand),
-			                std::max<uint32_t>(maxaln, (uint32_t)R[i].ncand))))
-				return rc;
+		if(r.ncand > (int32_t)cap || (b.NA[i] == (int32_t)maxaln && r.ncand > (int32_t)maxaln)) {
+			again.emplace_back(q, (uint32_t)r.ncand);
 			continue;
 		}
-		q->o = R[i];
-		q->naln = NA[i];
+		q->o = r;
+		q->naln = b.NA[i];
 		q->cap = cap;
 		q->maxaln = maxaln;
 		q->maxedit = maxedit;
-		q->cands.assign(C.begin() + i * cap, C.begin() + i * cap + std::max(0, R[i].ncand));
-		q->fates.assign(F.begin() + i * cap, F.begin() + (i + 1) * cap);
-		q->alns.assign(A.begin() + i * maxaln, A.begin() + (i + 1) * maxaln);
-		q->edits.assign(E.begin() + i * maxaln * (size_t)maxedit, E.begin() + (i + 1) * maxaln * (size_t)maxedit);
+		DpState* st = q->st;
+		st->cands.assign(b.C.get() + c0, b.C.get() + c0 + nc);
+		st->fates.assign(b.F.get() + c0, b.F.get() + c0 + nc);
+		st->alns.assign(b.A.begin() + i * maxaln, b.A.begin() + i * maxaln + na);
+		st->edits.assign(b.E.get() + e0, b.E.get() + e0 + ne);
+	}
+	if(oc != tot[0] || oe != tot[2]) {
+		fprintf(stderr, "bt2g adapter: packed DP outputs %llu/%llu, expected %zu/%zu\n", (unsigned long long)tot[0],
+		        (unsigned long long)tot[2], oc, oe);
+		return BT2G_ERR_FORMAT;
+	}
+	for(auto& qa : again) {
+		std::vector<DpReq*> one{qa.first};
+		if((rc = run_dp(one, std::max<uint32_t>(cap, qa.second), std::max<uint32_t>(maxaln, qa.second)))) return rc;
 	}
 	return BT2G_OK;
 }
@@ -446,8 +573,16 @@ int run_group(int kind, const std::vector<Req*>& g) {
 }
 
 const size_t MAX_BATCH = 8192;
-const size_t BATCH_TARGET = 256;         // requests that make a batch worth launching at once
-const int BATCH_WINDOW_US = 300;         // longest wait for them after the first arrives
+// requests that make a batch worth launching at once ($BT2G_BATCH_TARGET), and
+// the longest wait for them after the first arrives ($BT2G_BATCH_WINDOW_US)
+size_t env_or(const char* name, size_t dflt) {
+	const char* e = getenv(name);
+	return e && atol(e) > 0 ? (size_t)atol(e) : dflt;
+}
+// (fiber workers hand requests over a carrier round at a time, in bursts: a
+// shorter window, a larger target)
+const size_t BATCH_TARGET = env_or("BT2G_BATCH_TARGET", bt2gf::enabled() ? 1024 : 256);
+const int BATCH_WINDOW_US = (int)env_or("BT2G_BATCH_WINDOW_US", bt2gf::enabled() ? 200 : 300);
 
 class Dispatcher {
 public:
@@ -455,12 +590,18 @@ public:
 	// or run at once under the shared context's lock.
 	void submit(Req* r) {
 		const uint64_t t0 = now_us();
-		if(!batching()) {
+		if(void* f = bt2gf::self()) {
+			// a fiber (bt2g_fibers.cpp): the carrier hands the request over with the
+			// rest of its round (flush below) and resumes the fiber when it is done
+			r->fiber = f;
+			bt2gf::block_on(r);
+		} else if(!batching()) {
 			std::lock_guard<std::mutex> lk(g_mu);
 			r->rc = run_group(r->kind, std::vector<Req*>{r});
 			if(r->rc) strncpy(r->err, bt2g_last_error(), sizeof(r->err) - 1);
 			g_batches[r->kind]++;
 		} else {
+			sem_init(&r->sem, 0, 0);
 			Q& q = q_[r->kind];
 			{
 				std::lock_guard<std::mutex> lk(q.mu);
@@ -468,6 +609,7 @@ public:
 			}
 			q.cv.notify_one();
 			while(sem_wait(&r->sem) != 0) {}
+			sem_destroy(&r->sem);
 		}
 		g_wait_us[r->kind] += now_us() - t0;
 		if(r->rc) {
@@ -475,6 +617,26 @@ public:
 			throw 1;
 		}
 	}
+
+	void start() { (void)batching(); }
+
+	// A carrier's round of fiber requests (bt2gf::set_flush): one lock per seam.
+	static void flush(void* const* reqs, size_t n) {
+		Dispatcher& d = instance();
+		for(int k = 0; k < ST_N; k++) {
+			bool any = false;
+			for(size_t i = 0; i < n && !any; i++) any = static_cast<Req*>(reqs[i])->kind == k;
+			if(!any) continue;
+			Q& q = d.q_[k];
+			{
+				std::lock_guard<std::mutex> lk(q.mu);
+				for(size_t i = 0; i < n; i++)
+					if(static_cast<Req*>(reqs[i])->kind == k) q.v.push_back(static_cast<Req*>(reqs[i]));
+			}
+			q.cv.notify_one();
+		}
+	}
+	static Dispatcher& instance();
 
 private:
 	struct Q {
@@ -487,6 +649,10 @@ private:
 		std::call_once(once_, [this] {
 			const char* b = getenv("BT2G_BATCH");
 			on_ = !(b && b[0] == '0');
+			if(!on_ && bt2gf::enabled()) {
+				fprintf(stderr, "bt2g adapter: fibers need batching (BT2G_BATCH=0 with BT2G_FIBERS=1)\n");
+				throw 1;
+			}
 			if(on_) {
 				init_env();
 				{
@@ -509,6 +675,7 @@ private:
 	// grouped by the batch-wide arguments (arrival order kept within a group), on
 	// its own context.
 	void loop(int kind) {
+		bt2g_prof_thread();
 		{
 			char nm[16];
 			snprintf(nm, sizeof(nm), "bt2g-%.10s", ST_NAMES[kind]);
@@ -527,6 +694,7 @@ private:
 		double seen_ms[NKERN] = {0};
 		Q& q = q_[kind];
 		std::vector<Req*> take;
+		std::vector<void*> wake;
 		for(;;) {
 			{
 				std::unique_lock<std::mutex> lk(q.mu);
@@ -565,11 +733,14 @@ private:
 					}
 				}
 				g_batches[kind]++;
+				wake.clear();
 				for(Req* r : g) {
 					r->rc = rc;
 					if(rc) snprintf(r->err, sizeof(r->err), "%s (batch of %zu)", bt2g_last_error(), g.size());
-					sem_post(&r->sem);
+					if(r->fiber) wake.push_back(r->fiber);
+					else sem_post(&r->sem);
 				}
+				if(!wake.empty()) bt2gf::wake_many(wake.data(), wake.size());
 			}
 		}
 	}
@@ -580,6 +751,16 @@ private:
 };
 
 Dispatcher g_disp;
+Dispatcher& Dispatcher::instance() { return g_disp; }
+
+// fibers (bt2g_fibers.cpp): their requests reach the dispatchers a carrier round
+// at a time; the context and dispatchers start before the first fiber runs
+struct FiberHooks {
+	FiberHooks() {
+		bt2gf::set_flush(&Dispatcher::flush);
+		bt2gf::set_init([] { g_disp.start(); });
+	}
+} g_fiber_hooks;
 
 // AlnRes from an engine alignment: edits already in their final (5'->3',
 // post-trim) positions, so they are shifted by the leading trim before
@@ -597,23 +778,6 @@ void fill_alnres(AlnRes& a, const bt2g_edit* ed, uint32_t nedit, int64_t score, 
 	a.setRefNs(refns);
 }
 
-// Per-SwAligner state between align() and the nextAlignment() calls.
-struct DpState {
-	bool gpu = false;          // served by the engine (else the reference's CPU path)
-	bool u8 = false;           // u8 fill succeeded (RNG re-seed rule, aligner_sw.cpp:877 vs 932)
-	std::vector<int8_t> fates; // engine's DpBtCandidate::fate per candidate
-	std::vector<bt2g_sw_aln> alns;
-	std::vector<bt2g_edit> edits;
-	uint32_t maxedit = 0;
-	int32_t naln = 0;
-	uint32_t next = 0;         // next engine alignment to hand out
-	// the problem as sent to the engine (for $BT2G_ADAPTER_DUMP on a mismatch)
-	Row row;
-	bt2g_sw_problem prob;
-	bt2g_sw_rect rect;
-	std::vector<uint8_t> win;
-	int enable8 = 1;
-};
 
 // One engine/reference disagreement as a JSON line in $BT2G_ADAPTER_DUMP:
 // everything needed to replay the DP through the oracle and the reference.
@@ -645,14 +809,14 @@ void dump_dp(const DpState& st, const std::vector<DpBtCandidate>& cands, size_t 
 	fclose(f);
 }
 
-// one entry per SwAligner of the worker thread (sw and osw, bt2_search.cpp:3130)
-thread_local std::vector<std::pair<const void*, DpState*>> t_dp;
+// one entry per SwAligner of the worker (sw and osw, bt2_search.cpp:3130); a
+// carrier thread holds those of all its fibers
+thread_local std::unordered_map<const void*, DpState*> t_dp;
 
 DpState& dp_state(const void* sw) {
-	for(auto& p : t_dp)
-		if(p.first == sw) return *p.second;
-	t_dp.emplace_back(sw, new DpState());
-	return *t_dp.back().second;
+	DpState*& p = t_dp[sw];
+	if(!p) p = new DpState();
+	return *p;
 }
 
 // Protected-member access (no added members: same layout as the base).
@@ -742,7 +906,7 @@ bool __wrap__ZN11SeedAligner11oneMmSearchEPK4EbwtS2_RK4ReadRK7ScoringlbbbbbR11Se
 	q.r.set(read.patFw, read.qual);
 	q.minsc = (int32_t)minsc;
 	g_disp.submit(&q);
-	const std::vector<bt2g_mm1>& h = q.hits;
+	const auto& h = q.hits;
 	const int32_t cnt = q.cnt;
 	const uint32_t ops = q.ops;
 	count(ST_1MM, true);
@@ -783,7 +947,7 @@ void __wrap__ZN11SeedAligner14searchAllSeedsERK5EListI4SeedLi128EEPK4EbwtS7_RK4R
 	SeedReq q((uint32_t)seeds[0].len, per, off, (uint32_t)nof);
 	q.r.set(read.patFw, read.qual);
 	g_disp.submit(&q);
-	const std::vector<uint32_t>& out = q.out;
+	const auto& out = q.out;
 	const int32_t ns = q.ns;
 	const uint32_t ops = q.ops;
 	if((size_t)ns != nof) {
@@ -850,7 +1014,7 @@ int __wrap__ZN9SwAligner13ungappedAlignERK20SDnaStringExpandableILi1024ELi2EERK1
 	q.p.minsc = (int32_t)minsc;
 	g_disp.submit(&q);
 	const bt2g_ug_result& o = q.o;
-	const std::vector<bt2g_edit>& ed = q.ed;
+	const auto& ed = q.ed;
 	count(ST_UG, true);
 	res.alres.reset();
 	if(o.ret != 1) return o.ret;
@@ -895,7 +1059,7 @@ bool SwAlignerAcc::gpu_align(TAlScore& best, bool& served) {
 	   minsc_ > std::numeric_limits<int32_t>::max())
 		return false;
 	DpState& st = dp_state(this);
-	DpReq q(bs, (enable8_ && !readSse16_) ? 1 : 0, rdlen > 1024);
+	DpReq q(bs, (enable8_ && !readSse16_) ? 1 : 0, rdlen > 1024, &st);
 	q.r.set(*rdfw_, *qufw_);
 	bt2g_sw_problem& p = q.p;
 	memset(&p, 0, sizeof(p));
@@ -911,7 +1075,8 @@ bool SwAlignerAcc::gpu_align(TAlScore& best, bool& served) {
 	g_disp.submit(&q);
 	if(q.cpu) return false;      // served = false: the reference's align() runs
 	const bt2g_sw_result& o = q.o;
-	if(getenv("BT2G_ADAPTER_DUMP")) {
+	static const bool dump = getenv("BT2G_ADAPTER_DUMP") != nullptr;
+	if(dump) {
 		st.row = q.r;
 		st.prob = q.p;
 		st.rect = q.rect;
@@ -919,10 +1084,7 @@ bool SwAlignerAcc::gpu_align(TAlScore& best, bool& served) {
 		st.enable8 = q.enable8;
 	}
 	st.naln = q.naln;
-	st.fates.swap(q.fates);
-	st.alns.swap(q.alns);
-	st.edits.swap(q.edits);
-	const std::vector<bt2g_sw_cand>& cands = q.cands;
+	const std::vector<bt2g_sw_cand>& cands = st.cands;   // (written by run_dp)
 	const uint32_t maxedit = q.maxedit;
 	if(st.naln < 0) {
 		fprintf(stderr, "bt2g adapter: sw_align_bt status %d\n", st.naln);
@@ -933,6 +1095,7 @@ bool SwAlignerAcc::gpu_align(TAlScore& best, bool& served) {
 	st.gpu = true;
 	st.maxedit = maxedit;
 	st.next = 0;
+	st.next_edit = 0;
 	// SwAligner::align's own state (aligner_sw.cpp:505-512, 677-729)
 	state_ = 2;   // STATE_ALIGNED (private enum, aligner_sw.h:197-201)
 	btncand_.clear();
@@ -1005,7 +1168,8 @@ bool SwAlignerAcc::gpu_next(SwResult& res, TAlScore minsc, RandomSource& rnd, Dp
 			dump_dp(st, cv, cural_, minsc, "alignment order");
 			throw 1;
 		}
-		const bt2g_edit* ed = &st.edits[(size_t)st.next * st.maxedit];
+		const bt2g_edit* ed = st.edits.data() + st.next_edit;
+		st.next_edit += (size_t)a.nedit;
 		st.next++;
 		const size_t rdlen = rdf_ - rdi_;
 		// backtraceNucleotides*: setScore / setShape / setRefNs (aligner_swsse_ee_u8.cpp:1822-1847)

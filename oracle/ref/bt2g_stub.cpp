@@ -229,6 +229,39 @@ int bt2g_sw_align_bt(bt2g_ctx*, const uint8_t* reads, const uint8_t* quals, uint
 	return rc;
 }
 
+// the packed flavour (include/bt2g.h): the unpacked call, then packed here
+int bt2g_sw_align_bt_packed(bt2g_ctx* c, const uint8_t* reads, const uint8_t* quals, uint32_t stride,
+                            const uint32_t* lens, const bt2g_sw_problem* probs, uint32_t nprob,
+                            const uint8_t* windows, uint64_t wl, const bt2g_sw_rect* rects, const bt2g_scoring* sc,
+                            int enable8, uint32_t cap, bt2g_sw_result* res, uint32_t maxaln, uint32_t maxedit,
+                            int32_t* naln, bt2g_sw_aln* alns, bt2g_sw_cand* cands, int8_t* fates, bt2g_edit* edits,
+                            uint64_t* totals) {
+	std::vector<bt2g_sw_cand> C((size_t)nprob * cap);
+	std::vector<int8_t> F((size_t)nprob * cap);
+	std::vector<bt2g_edit> E((size_t)nprob * maxaln * maxedit);
+	int rc = bt2g_sw_align_bt(c, reads, quals, stride, lens, probs, nprob, windows, wl, rects, sc, enable8, cap, res,
+	                          C.data(), maxaln, maxedit, naln, alns, E.data(), F.data());
+	if(rc && rc != BT2G_ERR_OVERFLOW) return rc;
+	uint64_t tc = 0, ta = 0, te = 0;
+	for(uint32_t i = 0; i < nprob; i++) {
+		const uint32_t nc = (uint32_t)std::min<int64_t>(std::max<int32_t>(res[i].ncand, 0), cap);
+		for(uint32_t k = 0; k < nc; k++, tc++) {
+			cands[tc] = C[(size_t)i * cap + k];
+			if(fates) fates[tc] = F[(size_t)i * cap + k];
+		}
+		const uint32_t na = (uint32_t)std::min<int64_t>(std::max<int32_t>(naln[i], 0), maxaln);
+		ta += na;
+		for(uint32_t k = 0; k < na; k++) {
+			const uint32_t ne = (uint32_t)std::min<int64_t>(std::max<int32_t>(alns[(size_t)i * maxaln + k].nedit, 0), maxedit);
+			for(uint32_t e = 0; e < ne; e++) edits[te++] = E[((size_t)i * maxaln + k) * maxedit + e];
+		}
+	}
+	totals[0] = tc;
+	totals[1] = ta;
+	totals[2] = te;
+	return rc;
+}
+
 // kernel timing: nothing runs on a device here
 int bt2g_set_profiling(bt2g_ctx*, int) { return BT2G_OK; }
 

@@ -1,0 +1,63 @@
+#!/usr/bin/env python3
+"""Per-function totals of a $BT2G_SAMPLE dump (integration/bt2g_prof.cpp).
+
+  python scripts/prof_symbolize.py samples.txt [--top 40]
+"""
+import argparse
+import collections
+import subprocess
+
+
+def load_segments(path):
+    """(p_offset, p_vaddr, p_filesz) of the executable LOAD segments."""
+    out = subprocess.run(["readelf", "-lW", path], stdout=subprocess.PIPE, stderr=subprocess.DEVNULL,
+                         text=True).stdout
+    segs = []
+    for ln in out.splitlines():
+        f = ln.split()
+        if f and f[0] == "LOAD":
+            segs.append((int(f[1], 16), int(f[2], 16), int(f[4], 16)))
+    return segs
+
+
+def to_vaddr(segs, off):
+    for o, v, n in segs:
+        if o <= off < o + n:
+            return off - o + v
+    return off
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("dump")
+    ap.add_argument("--top", type=int, default=40)
+    a = ap.parse_args()
+    by_path = collections.defaultdict(list)
+    total = 0
+    for ln in open(a.dump):
+        if ln.startswith("#"):
+            continue
+        p, off, c = ln.split()
+        by_path[p].append((int(off, 16), int(c)))
+        total += int(c)
+    funcs = collections.Counter()
+    for p, items in by_path.items():
+        if p in ("?", "[vdso]") or p.startswith("["):
+            for _, c in items:
+                funcs[p] += c
+            continue
+        segs = load_segments(p)
+        addrs = [hex(to_vaddr(segs, o)) for o, _ in items]
+        out = subprocess.run(["addr2line", "-f", "-C", "-e", p] + addrs, stdout=subprocess.PIPE,
+                             stderr=subprocess.DEVNULL, text=True).stdout.splitlines()
+        names = out[0::2]
+        lib = p.rsplit("/", 1)[-1]
+        for (o, c), nm in zip(items, names):
+            funcs[f"{nm[:110]} [{lib}]"] += c
+    print(f"{total} samples")
+    for nm, c in funcs.most_common(a.top):
+        print(f"{100.0 * c / total:6.2f}%  {c:7d}  {nm}")
+
+
+if __name__ == "__main__":
+    main()
