@@ -646,7 +646,7 @@ def server_baseline(base, reads, quals, pol, sample, threads, workers, args_srv,
         env = {"BT2G_INDEX": base, "BT2G_ADAPTER_STATS": stats, "BT2G_DEVICE": "0"}
         with rs.Server(base, threads=th, args=args_srv, binary=binary, env=env,
                        log_path=os.path.join(log_dir, f"server_{tag}.log")) as srv:
-            dt, outs = srv.run(chunks, k=8)
+            dt, outs = srv.run(chunks, k=8, warmup=chunks[:1])
         sams[tag] = rs.sorted_records(outs)
         out[tag] = {"rate": n / dt, "seconds": dt, "threads": th, "records": len(sams[tag]),
                     "server_cpu_s": srv.last_cpu_s, "server_cores_busy": srv.last_cpu_s / dt}

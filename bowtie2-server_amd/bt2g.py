@@ -118,6 +118,10 @@ def lib():
         L.bt2g_bench_frame_dev.argtypes = [u32, vp, vp, vp, vp, vp, vp, vp, vp, vp, u32, C.c_int32, vp, vp,
                                            u32, vp]
         L.bt2g_get_offset.argtypes = [vp, vp, u32, vp, vp]
+        L.bt2g_extend.argtypes = [vp, vp, u32, vp, u32, vp, u32, vp]
+        L.bt2g_extend_dev.argtypes = [vp, vp, u32, vp, vp, u32, vp, vp]
+        L.bt2g_sw_align_bt_packed.argtypes = [vp, vp, vp, u32, vp, vp, u32, vp, u64, vp, C.POINTER(Scoring), C.c_int,
+                                              u32, vp, u32, u32, vp, vp, vp, vp, vp, vp]
         L.bt2g_get_offset_dev.argtypes = [vp, vp, u32, vp, vp, vp]
         L.bt2g_sw_align.argtypes = [vp, vp, vp, u32, vp, vp, u32, vp, u64, C.POINTER(Scoring), C.c_int, u32, vp, vp,
                                     vp, vp]
@@ -249,6 +253,16 @@ class Engine:
                                C.byref(sc), int(nofw), int(norc), cap, _ptr(hits), _ptr(cnt), _ptr(ops), _ptr(loads))
         _chk(rc)
         return hits, cnt, ops, loads
+
+    def extend(self, reads, lens, ranges):
+        """SwDriver::extend per seed-hit range; ranges n x 8 = (read, fw, off, len,
+        topf, botf, topb, botb).  Returns n x 4 (nlex, nrex, LF steps, 0)."""
+        reads, lens = _c(reads, np.uint8), _c(lens, np.uint32)
+        rg = _c(ranges, np.uint32)
+        out = np.zeros((len(rg), 4), np.uint32)
+        _chk(lib().bt2g_extend(self.h, _ptr(reads), reads.shape[1], _ptr(lens), len(lens), _ptr(rg), len(rg),
+                               _ptr(out)))
+        return out
 
     def get_offset(self, rows):
         rows = _c(rows, np.uint32)

@@ -9,6 +9,8 @@
 #include <stdio.h>
 #include <string.h>
 
+#include <time.h>
+
 #include <algorithm>
 #include <cstdarg>
 #include <cstdlib>
@@ -87,9 +89,40 @@ struct bt2g_ctx {
 	// pinned host staging for the wrappers' copies (same growth rule as the arena)
 	uint8_t* pin = nullptr;
 	size_t pin_cap = 0, pin_used = 0, pin_need = 0;
+	// $BT2G_SYNC=poll: host waits query an event and sleep between queries
+	hipEvent_t poll_ev = nullptr;
 };
 
 namespace {
+
+// How a host thread waits for its stream.  $BT2G_SYNC=poll: record an event and
+// query it, sleeping $BT2G_POLL_US (default 20) between queries -- no CPU burnt
+// in the runtime's wait loop, which a process with a CPU quota and many busy
+// threads (the drop-in server) cannot spare; otherwise hipStreamSynchronize.
+bool poll_sync() {
+	static const bool on = [] {
+		const char* e = getenv("BT2G_SYNC");
+		return e && !strcmp(e, "poll");
+	}();
+	return on;
+}
+
+hipError_t stream_wait(bt2g_ctx* c, hipStream_t st) {
+	if(!poll_sync()) return hipStreamSynchronize(st);
+	static const long us = [] {
+		const char* e = getenv("BT2G_POLL_US");
+		return e && atol(e) > 0 ? atol(e) : 20L;
+	}();
+	hipError_t e;
+	if(!c->poll_ev && (e = hipEventCreateWithFlags(&c->poll_ev, hipEventDisableTiming)) != hipSuccess) return e;
+	if((e = hipEventRecord(c->poll_ev, st)) != hipSuccess) return e;
+	for(;;) {
+		e = hipEventQuery(c->poll_ev);
+		if(e != hipErrorNotReady) return e;
+		timespec ts{0, us * 1000L};
+		nanosleep(&ts, nullptr);
+	}
+}
 
 // Device scratch.  Inside a host-pointer wrapper (Arena below) blocks come from
 // the context's arena: the wrappers synchronise before they return, so the
@@ -226,7 +259,7 @@ struct Arena {
 	}
 	~Arena() {
 		if(--c->arena_depth > 0) return;
-		(void)hipStreamSynchronize(st);   // an early error return may leave work in flight
+		(void)stream_wait(c, st);   // an early error return may leave work in flight
 		for(auto& g : c->arena_guards) guard_check(g.p, g.n, g.line);
 		c->arena_guards.clear();
 		for(void* p : c->arena_spill) (void)hipFree(p);
@@ -529,6 +562,7 @@ int bt2g_close(bt2g_ctx* c) {
 	for(hipEvent_t& e : c->mm_ev)
 		if(e) (void)hipEventDestroy(e);
 	if(c->aux) (void)hipStreamDestroy(c->aux);
+	if(c->poll_ev) (void)hipEventDestroy(c->poll_ev);
 	if(c->stream) (void)hipStreamDestroy(c->stream);
 	delete c;
 	return BT2G_OK;
@@ -681,7 +715,7 @@ static int one_mm_impl(bt2g_ctx* c, const uint8_t* reads, const uint8_t* quals, 
 	HIPCHK(afree(c, s.fb_sdep, st));
 	HIPCHK(afree(c, s.slot_flag, st));
 	if(sync_overflow) {
-		HIPCHK(hipStreamSynchronize(st));
+		HIPCHK(stream_wait(c, st));
 		if(ovf) return fail(BT2G_ERR_OVERFLOW, "one-mismatch hits exceed cap %u", cap);
 	}
 	return BT2G_OK;
@@ -712,6 +746,20 @@ int bt2g_get_offset_dev(bt2g_ctx* c, const uint32_t* rows, uint32_t n, uint32_t*
 	{
 		ProfScope ps(c, 3, st);
 		launch_get_offset(c->fw, rows, n, offs, loads, st);
+	}
+	HIPCHK(hipGetLastError());
+	return BT2G_OK;
+}
+
+int bt2g_extend_dev(bt2g_ctx* c, const uint8_t* reads, uint32_t stride, const uint32_t* lens, const bt2g_ext_in* in,
+                    uint32_t n, bt2g_ext_out* out, void* stream) {
+	if(!c) return fail(BT2G_ERR_ARG, "null ctx");
+	if(int rc = check_reads(stride, n)) return rc;
+	if(n == 0) return BT2G_OK;
+	hipStream_t st = pick(c, stream);
+	{
+		ProfScope ps(c, 3, st);
+		launch_extend(c->fw, c->bw, c->bw.sides != nullptr, reads, stride, lens, in, n, out, st);
 	}
 	HIPCHK(hipGetLastError());
 	return BT2G_OK;
@@ -769,7 +817,7 @@ static int sw_align_impl(bt2g_ctx* c, const uint8_t* reads, const uint8_t* quals
 			// widest problem decides the boundary buffer width (problems live on the device)
 			std::vector<bt2g_sw_problem> hp(nprob);
 			HIPCHK(hipMemcpyAsync(hp.data(), probs, sizeof(bt2g_sw_problem) * nprob, hipMemcpyDeviceToHost, st));
-			HIPCHK(hipStreamSynchronize(st));
+			HIPCHK(stream_wait(c, st));
 			for(auto& p : hp) maxcol = p.ncol > maxcol ? p.ncol : maxcol;
 		}
 		HIPCHK(amalloc(c, (void**)&lists, sizeof(uint32_t) * (size_t)nprob * 3, st));
@@ -829,11 +877,32 @@ int bt2g_sw_align_dev(bt2g_ctx* c, const uint8_t* reads, const uint8_t* quals, u
 	                     mat_off, nullptr, 0, 0, 0, pick(c, stream));
 }
 
-int bt2g_sw_align_bt_dev(bt2g_ctx* c, const uint8_t* reads, const uint8_t* quals, uint32_t stride,
-                         const uint32_t* lens, const bt2g_sw_problem* probs, uint32_t nprob, const uint8_t* windows,
-                         const bt2g_sw_rect* rects, const bt2g_scoring* sc, int enable8, uint32_t cap,
-                         bt2g_sw_result* res, bt2g_sw_cand* cands, uint32_t maxaln, uint32_t maxedit,
-                         int32_t* naln, bt2g_sw_aln* alns, bt2g_edit* edits, int8_t* fates, void* stream) {
+}  // extern "C"
+
+// What a host caller knows about its problems without reading them back from
+// the device: widest window, longest read, whether every minsc fits the u8 fill.
+struct SwHint {
+	uint32_t maxcol, maxrow;
+	bool all8;
+};
+
+static SwHint sw_hint(const bt2g_sw_problem* probs, uint32_t nprob, const uint32_t* lens, int enable8) {
+	SwHint h{0, 0, enable8 != 0};
+	for(uint32_t i = 0; i < nprob; i++) {
+		h.maxcol = probs[i].ncol > h.maxcol ? probs[i].ncol : h.maxcol;
+		const uint32_t L = lens[probs[i].read];
+		h.maxrow = L > h.maxrow ? L : h.maxrow;
+		h.all8 = h.all8 && probs[i].minsc >= -254;
+	}
+	return h;
+}
+
+static int sw_align_bt_impl(bt2g_ctx* c, const uint8_t* reads, const uint8_t* quals, uint32_t stride,
+                            const uint32_t* lens, const bt2g_sw_problem* probs, uint32_t nprob, const uint8_t* windows,
+                            const bt2g_sw_rect* rects, const bt2g_scoring* sc, int enable8, uint32_t cap,
+                            bt2g_sw_result* res, bt2g_sw_cand* cands, uint32_t maxaln, uint32_t maxedit,
+                            int32_t* naln, bt2g_sw_aln* alns, bt2g_edit* edits, int8_t* fates, void* stream,
+                            const SwHint* hint) {
 	if(!c) return fail(BT2G_ERR_ARG, "null argument");
 	if(int rc = sw_args_ok(sc, cap)) return rc;
 	if(int rc = check_reads(stride, nprob)) return rc;
@@ -868,21 +937,28 @@ int bt2g_sw_align_bt_dev(bt2g_ctx* c, const uint8_t* reads, const uint8_t* quals
 		plane = c->bt_plane;
 		a.marks = c->bt_marks;
 	} else {
-		std::vector<bt2g_sw_problem> hp(nprob);
-		HIPCHK(hipMemcpyAsync(hp.data(), probs, sizeof(bt2g_sw_problem) * nprob, hipMemcpyDeviceToHost, st));
-		uint32_t nreads = 0;
-		HIPCHK(hipStreamSynchronize(st));
 		bool all8 = enable8 != 0;
-		for(auto& p : hp) {
-			maxcol = p.ncol > maxcol ? p.ncol : maxcol;
-			nreads = p.read + 1 > nreads ? p.read + 1 : nreads;
-			all8 = all8 && p.minsc >= -254;
+		if(hint) {
+			maxcol = hint->maxcol;
+			maxrow = hint->maxrow;
+			all8 = hint->all8;
+		} else {
+			// problems and lengths live on the device: read them back (two syncs)
+			std::vector<bt2g_sw_problem> hp(nprob);
+			HIPCHK(hipMemcpyAsync(hp.data(), probs, sizeof(bt2g_sw_problem) * nprob, hipMemcpyDeviceToHost, st));
+			uint32_t nreads = 0;
+			HIPCHK(stream_wait(c, st));
+			for(auto& p : hp) {
+				maxcol = p.ncol > maxcol ? p.ncol : maxcol;
+				nreads = p.read + 1 > nreads ? p.read + 1 : nreads;
+				all8 = all8 && p.minsc >= -254;
+			}
+			std::vector<uint32_t> hl(nreads);
+			HIPCHK(hipMemcpyAsync(hl.data(), lens, sizeof(uint32_t) * nreads, hipMemcpyDeviceToHost, st));
+			HIPCHK(stream_wait(c, st));
+			maxrow = 0;
+			for(uint32_t i = 0; i < nreads; i++) maxrow = hl[i] > maxrow ? hl[i] : maxrow;
 		}
-		std::vector<uint32_t> hl(nreads);
-		HIPCHK(hipMemcpyAsync(hl.data(), lens, sizeof(uint32_t) * nreads, hipMemcpyDeviceToHost, st));
-		HIPCHK(hipStreamSynchronize(st));
-		maxrow = 0;
-		for(uint32_t i = 0; i < nreads; i++) maxrow = hl[i] > maxrow ? hl[i] : maxrow;
 		packed = sw_use_packed(*sc, C, nullptr, stride, maxcol);
 		hb = packed && all8 && !sc->local ? 1 : 2;
 		if((rc = talloc((void**)&plane, (size_t)sw_plane_slot(stride, maxcol, hb) * nprob))) return rc;
@@ -933,6 +1009,17 @@ int bt2g_sw_align_bt_dev(bt2g_ctx* c, const uint8_t* reads, const uint8_t* quals
 	HIPCHK(hipGetLastError());
 	for(void* p : tmp) HIPCHK(afree(c, p, st));
 	return BT2G_OK;
+}
+
+extern "C" {
+
+int bt2g_sw_align_bt_dev(bt2g_ctx* c, const uint8_t* reads, const uint8_t* quals, uint32_t stride,
+                         const uint32_t* lens, const bt2g_sw_problem* probs, uint32_t nprob, const uint8_t* windows,
+                         const bt2g_sw_rect* rects, const bt2g_scoring* sc, int enable8, uint32_t cap,
+                         bt2g_sw_result* res, bt2g_sw_cand* cands, uint32_t maxaln, uint32_t maxedit,
+                         int32_t* naln, bt2g_sw_aln* alns, bt2g_edit* edits, int8_t* fates, void* stream) {
+	return sw_align_bt_impl(c, reads, quals, stride, lens, probs, nprob, windows, rects, sc, enable8, cap, res, cands,
+	                        maxaln, maxedit, naln, alns, edits, fates, stream, nullptr);
 }
 
 int bt2g_ungapped_dev(bt2g_ctx* c, const uint8_t* reads, const uint8_t* quals, uint32_t stride,
@@ -1082,7 +1169,7 @@ struct Tmp {
 		return BT2G_OK;
 	}
 	int finish() {
-		HIPCHK(hipStreamSynchronize(st));
+		HIPCHK(stream_wait(c, st));
 		for(const Out& o : outs) memcpy(o.h, o.pin, o.n);
 		outs.clear();
 		return BT2G_OK;
@@ -1149,13 +1236,42 @@ int bt2g_one_mm(bt2g_ctx* c, const uint8_t* reads, const uint8_t* quals, uint32_
 	   (rc = t.up(&dcnt, (const int32_t*)nullptr, n)) || (rc = t.up(&dops, (const uint32_t*)nullptr, n)))
 		return rc;
 	if(loads && (rc = t.up(&dld, (const uint32_t*)nullptr, n))) return rc;
-	int rc2 = bt2g_one_mm_dev(c, dr, dq, stride, dl, n, dms, sc, nofw, norc, cap, dh, dcnt, dops, dld, c->stream);
-	if(rc2 && rc2 != BT2G_ERR_OVERFLOW) return rc2;
+	// (the overflow shows in the counts copied back: no sync of its own)
+	if((rc = one_mm_impl(c, dr, dq, stride, dl, n, dms, sc, nofw, norc, nullptr, cap, dh, dcnt, dops, dld, c->stream,
+	                     false)))
+		return rc;
 	if((rc = t.down(hits, dh, (size_t)n * cap)) || (rc = t.down(counts, dcnt, n)) || (rc = t.down(bwops, dops, n)))
 		return rc;
 	if(loads && (rc = t.down(loads, dld, n))) return rc;
 	if((rc = t.finish())) return rc;
-	return rc2;
+	for(uint32_t i = 0; i < n; i++)
+		if(counts[i] > (int32_t)cap) return fail(BT2G_ERR_OVERFLOW, "one-mismatch hits exceed cap %u", cap);
+	return BT2G_OK;
+}
+
+int bt2g_extend(bt2g_ctx* c, const uint8_t* reads, uint32_t stride, const uint32_t* lens, uint32_t nreads,
+                const bt2g_ext_in* in, uint32_t n, bt2g_ext_out* out) {
+	if(!c) return fail(BT2G_ERR_ARG, "null ctx");
+	HIPCHK(hipSetDevice(c->device));
+	if(n == 0) return BT2G_OK;
+	for(uint32_t i = 0; i < n; i++) {
+		if(in[i].read >= nreads) return fail(BT2G_ERR_ARG, "range %u: read %u >= %u", i, in[i].read, nreads);
+		const uint32_t L = lens[in[i].read];
+		if(L > stride || in[i].off + in[i].len > L || in[i].botf <= in[i].topf || in[i].botb - in[i].topb != in[i].botf - in[i].topf)
+			return fail(BT2G_ERR_ARG, "range %u: bad seed hit", i);
+	}
+	Tmp t(c);
+	uint8_t* dr;
+	uint32_t* dl;
+	bt2g_ext_in* din;
+	bt2g_ext_out* dout;
+	int rc;
+	if((rc = t.up(&dr, reads, (size_t)nreads * stride)) || (rc = t.up(&dl, lens, nreads)) || (rc = t.up(&din, in, n)) ||
+	   (rc = t.up(&dout, (const bt2g_ext_out*)nullptr, n)))
+		return rc;
+	if((rc = bt2g_extend_dev(c, dr, stride, dl, din, n, dout, c->stream))) return rc;
+	if((rc = t.down(out, dout, n))) return rc;
+	return t.finish();
 }
 
 int bt2g_get_offset(bt2g_ctx* c, const uint32_t* rows, uint32_t n, uint32_t* offs, uint32_t* loads) {
@@ -1252,8 +1368,9 @@ int bt2g_sw_align_bt(bt2g_ctx* c, const uint8_t* reads, const uint8_t* quals, ui
 	if(windows && windows_len && (rc = t.up(&dw, windows, windows_len))) return rc;
 	if(rects && (rc = t.up(&drc, rects, nprob))) return rc;
 	if(fates && (rc = t.up(&dft, (const int8_t*)nullptr, (size_t)nprob * cap))) return rc;
-	if((rc = bt2g_sw_align_bt_dev(c, dr, dq, stride, dl, dp, nprob, dw, drc, sc, enable8, cap, dres, dc, maxaln,
-	                              maxedit, dna, dal, ded, dft, c->stream)))
+	const SwHint hint = sw_hint(probs, nprob, lens, enable8);
+	if((rc = sw_align_bt_impl(c, dr, dq, stride, dl, dp, nprob, dw, drc, sc, enable8, cap, dres, dc, maxaln, maxedit,
+	                          dna, dal, ded, dft, c->stream, &hint)))
 		return rc;
 	if((rc = t.down(res, dres, nprob)) || (rc = t.down(cands, dc, (size_t)nprob * cap)) ||
 	   (rc = t.down(naln, dna, nprob)) || (rc = t.down(alns, dal, na)) || (rc = t.down(edits, ded, na * maxedit)))
@@ -1308,8 +1425,9 @@ int bt2g_sw_align_bt_packed(bt2g_ctx* c, const uint8_t* reads, const uint8_t* qu
 	if(fates && ((rc = t.up(&dft, (const int8_t*)nullptr, (size_t)nprob * cap)) ||
 	             (rc = t.up(&dpf, (const int8_t*)nullptr, (size_t)nprob * cap))))
 		return rc;
-	if((rc = bt2g_sw_align_bt_dev(c, dr, dq, stride, dl, dp, nprob, dw, drc, sc, enable8, cap, dres, dc, maxaln,
-	                              maxedit, dna, dal, ded, dft, c->stream)))
+	const SwHint hint = sw_hint(probs, nprob, lens, enable8);
+	if((rc = sw_align_bt_impl(c, dr, dq, stride, dl, dp, nprob, dw, drc, sc, enable8, cap, dres, dc, maxaln, maxedit,
+	                          dna, dal, ded, dft, c->stream, &hint)))
 		return rc;
 	launch_sw_pack(dres, dna, dal, dc, dft, ded, nprob, cap, maxaln, maxedit, dcnt, doff, dpc, dpf, dpe, c->stream);
 	HIPCHK(hipGetLastError());

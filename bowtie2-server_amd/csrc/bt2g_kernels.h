@@ -58,6 +58,8 @@ void launch_one_mm(const DevEbwt& F, const DevEbwt& B, const uint8_t* reads, con
                    int32_t* counts, uint32_t* ops, uint32_t* loads, int32_t* overflow, MmBranch* brq,
                    uint32_t brq_cap, uint32_t* fb_items, uint4* fb_st4, uint32_t* fb_sdep, uint32_t* slot_flag,
                    hipStream_t st, hipStream_t st2 = nullptr, hipEvent_t* ev = nullptr);
+void launch_extend(const DevEbwt& F, const DevEbwt& B, int has_bw, const uint8_t* reads, uint32_t stride,
+                   const uint32_t* lens, const bt2g_ext_in* in, uint32_t n, bt2g_ext_out* out, hipStream_t st);
 void launch_get_offset(const DevEbwt& e, const uint32_t* rows, uint32_t n, uint32_t* offs, uint32_t* loads,
                        hipStream_t st);
 void launch_sw_partition(const bt2g_sw_problem* probs, uint32_t nprob, int local, int enable8, uint32_t* list8,

@@ -315,3 +315,76 @@ void launch_get_offset(const DevEbwt& e, const uint32_t* rows, uint32_t n, uint3
                        hipStream_t st) {
 	hipLaunchKernelGGL(k_get_offset, dim3((n + 255) / 256), dim3(256), 0, st, e, rows, n, offs, loads);
 }
+
+// --------------------------------------------------------------------------
+// SwDriver::extend (aligner_sw_driver.cpp:299-483): one lane = one seed-hit
+// range.  Left: the range walks leftward in the forward index while it keeps
+// its size and its one extending character agrees with the read (an N in the
+// read takes any single character); right: the same in the mirror index.
+// A one-row range steps by mapLF1 (bt2_idx.h:2451-2470, no step from the '$'
+// row); the loop stops at 255 positions per side, as the reference does.
+// --------------------------------------------------------------------------
+__device__ __forceinline__ uint32_t ext_walk(const DevEbwt& e, uint32_t top, uint32_t bot, const uint8_t* row,
+                                             uint32_t rdlen, bool fw, uint32_t lim, uint32_t i0, int dir,
+                                             uint32_t& fmops) {
+	uint32_t n = 0;
+	for(uint32_t ii = 0; ii < lim; ii++) {
+		const uint32_t i = (uint32_t)((int64_t)i0 + (int64_t)dir * ii);
+		int rdc = fw ? row[i] : row[rdlen - 1 - i];
+		if(!fw) rdc = rdc > 3 ? 4 : 3 - rdc;
+		fmops++;
+		if(bot - top > 1) {
+			uint32_t t[4], b[4];
+			bi_step_tb(e, top, bot, t, b);
+			int nonz = -1;
+			bool abort = false;
+			const uint32_t orig = bot - top;
+			for(int j = 0; j < 4; j++) {
+				if(b[j] > t[j]) {
+					if(nonz >= 0) { abort = true; break; }
+					nonz = j;
+					top = t[j];
+					bot = b[j];
+				}
+			}
+			if(abort || (nonz != rdc && rdc <= 3) || bot - top < orig) break;
+		} else {
+			int c = -1;
+			if(top != e.zoff) {
+				SideData s;
+				load_side(e, top / 192u, s);
+				c = side_rowL(s, top % 192u);
+				top = occ1(e, s, top, c);
+			}
+			if(c != rdc && rdc <= 3) break;
+			bot = top + 1;
+		}
+		if(++n == 255u) break;
+	}
+	return n;
+}
+
+__global__ void __launch_bounds__(256)
+k_extend(DevEbwt F, DevEbwt B, int has_bw, const uint8_t* __restrict__ reads, uint32_t stride,
+         const uint32_t* __restrict__ lens, const bt2g_ext_in* __restrict__ in, uint32_t n, bt2g_ext_out* __restrict__ out) {
+	const uint32_t k = blockIdx.x * blockDim.x + threadIdx.x;
+	if(k >= n) return;
+	const bt2g_ext_in q = in[k];
+	const uint32_t rdlen = lens[q.read];
+	const uint8_t* row = reads + (size_t)q.read * stride;
+	const bool fw = q.fw != 0;
+	uint32_t fmops = 0, nlex = 0, nrex = 0;
+	// left, forward index (aligner_sw_driver.cpp:335-408)
+	uint32_t lim = fw ? q.off : rdlen - q.len - q.off;
+	if(lim > 0) nlex = ext_walk(F, q.topf, q.botf, row, rdlen, fw, lim, fw ? q.off - 1 : rdlen - q.off - q.len - 1, -1, fmops);
+	// right, mirror index (aligner_sw_driver.cpp:411-475)
+	lim = fw ? rdlen - q.len - q.off : q.off;
+	if(lim > 0 && has_bw) nrex = ext_walk(B, q.topb, q.botb, row, rdlen, fw, lim, fw ? q.len + q.off : rdlen - q.off, 1, fmops);
+	out[k] = bt2g_ext_out{nlex, nrex, fmops, 0u};
+}
+
+void launch_extend(const DevEbwt& F, const DevEbwt& B, int has_bw, const uint8_t* reads, uint32_t stride,
+                   const uint32_t* lens, const bt2g_ext_in* in, uint32_t n, bt2g_ext_out* out, hipStream_t st) {
+	if(n == 0) return;
+	hipLaunchKernelGGL(k_extend, dim3((n + 255) / 256), dim3(256), 0, st, F, B, has_bw, reads, stride, lens, in, n, out);
+}

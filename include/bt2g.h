@@ -176,6 +176,32 @@ int bt2g_get_offset(bt2g_ctx* ctx, const uint32_t* rows, uint32_t n, uint32_t* o
 int bt2g_get_offset_dev(bt2g_ctx* ctx, const uint32_t* rows, uint32_t n, uint32_t* offs, uint32_t* loads,
                         void* stream);
 
+/* One seed-hit range to extend (SwDriver::extend's arguments,
+ * aligner_sw_driver.cpp:299-312): the seed at `off` from the 5' end of the read
+ * (fw) or of its reverse complement (!fw), `len` long, with SA range
+ * [topf, botf) in the forward index and [topb, botb) in the mirror index. */
+typedef struct {
+	uint32_t read;       /* row in reads/lens */
+	int32_t  fw;
+	uint32_t off, len;
+	uint32_t topf, botf, topb, botb;
+} bt2g_ext_in;
+
+typedef struct {
+	uint32_t nlex, nrex; /* positions the hit extends to the left / right without an edit */
+	uint32_t fmops;      /* LF steps taken (PerReadMetrics::nSdFmops increments) */
+	uint32_t pad;
+} bt2g_ext_out;
+
+/* SwDriver::extend (aligner_sw_driver.cpp:299-483), called by
+ * prioritizeSATups (aligner_sw_driver.cpp:574-589) for every seed-hit range:
+ * walks the range outward, left in the forward index and right in the mirror
+ * index, while it stays the same size and agrees with the read. */
+int bt2g_extend(bt2g_ctx* ctx, const uint8_t* reads, uint32_t stride, const uint32_t* lens, uint32_t nreads,
+                const bt2g_ext_in* in, uint32_t n, bt2g_ext_out* out);
+int bt2g_extend_dev(bt2g_ctx* ctx, const uint8_t* reads, uint32_t stride, const uint32_t* lens,
+                    const bt2g_ext_in* in, uint32_t n, bt2g_ext_out* out, void* stream);
+
 /* ---- SW engine ----------------------------------------------------------- */
 
 /* One dynamic-programming problem (SwAligner::initRead + initRef,

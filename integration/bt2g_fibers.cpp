@@ -243,13 +243,13 @@ void fiber_main(Fiber* f) {
 
 }  // namespace
 }  // namespace bt2gf
-extern "C" void bt2g_prof_thread();
+extern "C" void bt2g_prof_thread(int role);
 namespace bt2gf {
 namespace {
 
 void Carrier::run() {
 	t_carrier = this;
-	bt2g_prof_thread();
+	bt2g_prof_thread(1);
 	char nm[16];
 	snprintf(nm, sizeof(nm), "bt2g-carrier");
 	pthread_setname_np(pthread_self(), nm);
@@ -354,13 +354,13 @@ Fiber* make_fiber(std::thread::_State* work) {
 Fiber* cur_fiber() { return t_carrier ? t_carrier->cur : nullptr; }
 
 // Allocator settings for thousands of workers on a few threads: no heap
-// trimming and no mmap for blocks below 32 MB (the dispatchers' batch buffers
+// trimming and no mmap for blocks below 4 MB (the dispatchers' batch buffers
 // and the workers' per-read lists otherwise cycle pages through mprotect /
 // madvise and page faults).
 struct MallocTuning {
 	MallocTuning() {
 		if(!enabled()) return;
-		mallopt(M_MMAP_THRESHOLD, 32 << 20);
+		mallopt(M_MMAP_THRESHOLD, 4 << 20);   // (the workers' 20 MB cache pools: mmap, untouched)
 		mallopt(M_TRIM_THRESHOLD, 1 << 30);
 		mallopt(M_TOP_PAD, 16 << 20);
 	}

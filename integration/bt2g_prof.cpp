@@ -14,6 +14,7 @@
 #include <sys/syscall.h>
 #include <sys/time.h>
 #include <time.h>
+#include <malloc.h>
 #include <ucontext.h>
 #include <unistd.h>
 
@@ -27,11 +28,38 @@ namespace {
 const size_t NSLOT = 1u << 20;
 std::atomic<uint64_t>* g_pc = nullptr;     // key: instruction pointer (0 = empty)
 std::atomic<uint32_t>* g_cnt = nullptr;
+// (pc, word at the stack pointer) pairs: for a sample inside a frameless leaf
+// (a libc syscall wrapper) that word is its caller's return address
+std::atomic<uint64_t>* g_pc2 = nullptr;
+std::atomic<uint64_t>* g_ret2 = nullptr;
+std::atomic<uint32_t>* g_cnt2 = nullptr;
 std::atomic<uint64_t> g_lost{0};
+thread_local uint64_t t_role = 0;           // 1 carrier, 2 dispatcher (folded into the pair table)
+
+void count_pair(uint64_t pc, uint64_t ret) {
+	size_t h = (size_t)(((pc ^ (ret * 0xC2B2AE3D27D4EB4Full)) * 0x9E3779B97F4A7C15ull) >> 44) & (NSLOT - 1);
+	for(size_t probe = 0; probe < 64; probe++, h = (h + 1) & (NSLOT - 1)) {
+		uint64_t k = g_pc2[h].load(std::memory_order_relaxed);
+		if(k == pc && g_ret2[h].load(std::memory_order_relaxed) == ret) {
+			g_cnt2[h].fetch_add(1, std::memory_order_relaxed);
+			return;
+		}
+		if(k == 0) {
+			uint64_t z = 0;
+			if(g_pc2[h].compare_exchange_strong(z, pc)) {
+				g_ret2[h].store(ret, std::memory_order_relaxed);
+				g_cnt2[h].fetch_add(1, std::memory_order_relaxed);
+				return;
+			}
+		}
+	}
+}
 
 void on_prof(int, siginfo_t*, void* uc) {
 	const uint64_t pc = (uint64_t)((ucontext_t*)uc)->uc_mcontext.gregs[REG_RIP];
 	if(!pc) return;
+	const uint64_t sp = (uint64_t)((ucontext_t*)uc)->uc_mcontext.gregs[REG_RSP];
+	if(sp) count_pair(pc, *(const uint64_t*)sp ^ (t_role << 60));
 	size_t h = (size_t)((pc * 0x9E3779B97F4A7C15ull) >> 44) & (NSLOT - 1);
 	for(size_t probe = 0; probe < 64; probe++, h = (h + 1) & (NSLOT - 1)) {
 		uint64_t k = g_pc[h].load(std::memory_order_relaxed);
@@ -72,6 +100,24 @@ void dump(const char* path) {
 	FILE* o = fopen(tmp.c_str(), "w");
 	if(!o) return;
 	fprintf(o, "# lost %llu\n", (unsigned long long)g_lost.load());
+	auto where = [&](uint64_t a, char* buf, size_t n) {
+		for(const Map& x : maps)
+			if(a >= x.lo && a < x.hi) {
+				snprintf(buf, n, "%s %lx", x.path.c_str(), (unsigned long)(a - x.lo + x.off));
+				return;
+			}
+		snprintf(buf, n, "? %lx", (unsigned long)a);
+	};
+	for(size_t i = 0; i < NSLOT; i++) {
+		uint64_t pc = g_pc2[i].load(std::memory_order_relaxed);
+		if(!pc) continue;
+		char a[4200], b[4200];
+		where(pc, a, sizeof(a));
+		const uint64_t rr = g_ret2[i].load(std::memory_order_relaxed);
+		where(rr & ~(0xFull << 60), b, sizeof(b));
+		fprintf(o, "#pair %s %s %u %llu\n", a, b, g_cnt2[i].load(std::memory_order_relaxed),
+		        (unsigned long long)(rr >> 60));
+	}
 	for(size_t i = 0; i < NSLOT; i++) {
 		uint64_t pc = g_pc[i].load(std::memory_order_relaxed);
 		if(!pc) continue;
@@ -92,6 +138,9 @@ struct Sampler {
 		if(!path || !*path) return;
 		g_pc = new std::atomic<uint64_t>[NSLOT]();
 		g_cnt = new std::atomic<uint32_t>[NSLOT]();
+		g_pc2 = new std::atomic<uint64_t>[NSLOT]();
+		g_ret2 = new std::atomic<uint64_t>[NSLOT]();
+		g_cnt2 = new std::atomic<uint32_t>[NSLOT]();
 		struct sigaction sa;
 		memset(&sa, 0, sizeof(sa));
 		sa.sa_sigaction = on_prof;
@@ -99,9 +148,15 @@ struct Sampler {
 		sigaction(SIGPROF, &sa, nullptr);
 		std::string p(path);
 		std::thread([p] {
-			for(;;) {
+			for(int k = 0;; k++) {
 				sleep(2);
 				dump(p.c_str());
+				// the allocator's arenas over time (system bytes per heap)
+				if(FILE* f = fopen((p + ".malloc").c_str(), "a")) {
+					fprintf(f, "<!-- t=%d -->\n", 2 * (k + 1));
+					malloc_info(0, f);
+					fclose(f);
+				}
 			}
 		}).detach();
 	}
@@ -110,8 +165,9 @@ struct Sampler {
 }  // namespace
 
 // Sample the calling thread's CPU time (no-op unless $BT2G_SAMPLE is set).
-extern "C" void bt2g_prof_thread() {
+extern "C" void bt2g_prof_thread(int role) {
 	if(!g_pc) return;
+	t_role = (uint64_t)role & 0xF;
 	sigevent sev;
 	memset(&sev, 0, sizeof(sev));
 	sev.sigev_notify = SIGEV_THREAD_ID;

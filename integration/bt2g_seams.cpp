@@ -57,24 +57,28 @@
 #include <limits>
 #include <memory>
 #include <unordered_map>
+#include <algorithm>
 
 #include "aligner_seed.h"
 #include "aligner_cache.h"
 #include "aligner_sw.h"
 #include "read.h"
 #include "scoring.h"
+#include "aligner_sw_driver.h"
 #include "bt2g.h"
 #include "bt2g_fibers.h"
+#include "bt2g_gw_spec.h"
 
-extern "C" void bt2g_prof_thread();   // bt2g_prof.cpp: CPU samples of this thread ($BT2G_SAMPLE)
+extern "C" void bt2g_prof_thread(int role);   // bt2g_prof.cpp: CPU samples of this thread ($BT2G_SAMPLE)
 
 namespace {
 
 std::mutex g_mu;
 bt2g_ctx* g_ctx = nullptr;
 
-enum { ST_EXACT, ST_1MM, ST_SEEDS, ST_UG, ST_DP, ST_N };
-const char* const ST_NAMES[ST_N] = {"exact_sweep", "one_mm", "seed_search", "ungapped", "sw_dp"};
+enum { ST_EXACT, ST_1MM, ST_SEEDS, ST_UG, ST_DP, ST_EXT, ST_OFF, ST_N };
+const char* const ST_NAMES[ST_N] = {"exact_sweep", "one_mm", "seed_search", "ungapped", "sw_dp", "extend",
+                                    "get_offset"};
 std::atomic<uint64_t> g_gpu[ST_N], g_cpu[ST_N], g_batches[ST_N];
 std::atomic<uint64_t> g_call_us[ST_N], g_wait_us[ST_N];   // engine time per seam; request round trips
 // $BT2G_ADAPTER_PROF=1: kernel time per engine kernel id (bt2g_kernel_stats), all dispatchers
@@ -131,8 +135,9 @@ void die(const char* what, int rc) {
 void init_env() {
 	static std::once_flag once;
 	std::call_once(once, [] {
-		// dispatcher threads sleep in their stream waits: the server's workers need the cores
-		setenv("BT2G_SYNC", "blocking", 0);
+		// dispatcher threads sleep in their stream waits: the server's workers need the
+		// cores (the runtime's blocking wait still spins: r03d, 21 % of the CPU)
+		setenv("BT2G_SYNC", "poll", 0);
 		const char* sp = getenv("BT2G_ADAPTER_STATS");
 		if(sp) {
 			strncpy(g_stats_path, sp, sizeof(g_stats_path) - 1);
@@ -326,6 +331,20 @@ struct DpState {
 	bt2g_sw_rect rect;
 	std::vector<uint8_t> win;
 	int enable8 = 1;
+};
+
+struct ExtReq : Req {         // bt2g_extend: every seed-hit range of one read
+	Row r;
+	std::vector<bt2g_ext_in> in;       // (.read is set by the dispatcher)
+	Out<bt2g_ext_out, 64> out;
+	ExtReq() : Req(ST_EXT, 0) {}
+};
+
+struct OffReq : Req {         // bt2g_get_offset: the SA rows one read's walks resolve
+	Row r;                        // (unused: no read data)
+	std::vector<uint32_t> rows;
+	Out<uint32_t, 128> offs;
+	OffReq() : Req(ST_OFF, 0) { r.len = 0; }
 };
 
 // Rows of a batch as one [n][stride] array (stride = longest read); one per
@@ -562,12 +581,58 @@ int run_dp(const std::vector<DpReq*>& v, uint32_t cap = 0, uint32_t maxaln = 8) 
 	return BT2G_OK;
 }
 
+int run_ext(const std::vector<ExtReq*>& v) {
+	struct B {
+		Pack pk;
+		std::vector<bt2g_ext_in> in;
+		std::vector<bt2g_ext_out> out;
+	};
+	thread_local B b;
+	b.pk.build(v);
+	b.in.clear();
+	for(size_t i = 0; i < v.size(); i++)
+		for(const bt2g_ext_in& q : v[i]->in) {
+			b.in.push_back(q);
+			b.in.back().read = (uint32_t)i;
+		}
+	b.out.resize(b.in.size());
+	int rc = bt2g_extend(cur_ctx(), b.pk.codes.data(), b.pk.stride, b.pk.lens.data(), (uint32_t)v.size(), b.in.data(),
+	                     (uint32_t)b.in.size(), b.out.data());
+	if(rc) return rc;
+	size_t k = 0;
+	for(ExtReq* q : v) {
+		q->out.assign(&b.out[k], q->in.size());
+		k += q->in.size();
+	}
+	return BT2G_OK;
+}
+
+int run_off(const std::vector<OffReq*>& v) {
+	struct B {
+		std::vector<uint32_t> rows, offs;
+	};
+	thread_local B b;
+	b.rows.clear();
+	for(OffReq* q : v) b.rows.insert(b.rows.end(), q->rows.begin(), q->rows.end());
+	b.offs.resize(b.rows.size());
+	int rc = bt2g_get_offset(cur_ctx(), b.rows.data(), (uint32_t)b.rows.size(), b.offs.data(), nullptr);
+	if(rc) return rc;
+	size_t k = 0;
+	for(OffReq* q : v) {
+		q->offs.assign(&b.offs[k], q->rows.size());
+		k += q->rows.size();
+	}
+	return BT2G_OK;
+}
+
 int run_group(int kind, const std::vector<Req*>& g) {
 	switch(kind) {
 	case ST_EXACT: { std::vector<ExactReq*> v; for(Req* r : g) v.push_back(static_cast<ExactReq*>(r)); return run_exact(v); }
 	case ST_1MM:   { std::vector<MmReq*> v;    for(Req* r : g) v.push_back(static_cast<MmReq*>(r));    return run_mm(v); }
 	case ST_SEEDS: { std::vector<SeedReq*> v;  for(Req* r : g) v.push_back(static_cast<SeedReq*>(r));  return run_seeds(v); }
 	case ST_UG:    { std::vector<UgReq*> v;    for(Req* r : g) v.push_back(static_cast<UgReq*>(r));    return run_ug(v); }
+	case ST_EXT:   { std::vector<ExtReq*> v;   for(Req* r : g) v.push_back(static_cast<ExtReq*>(r));   return run_ext(v); }
+	case ST_OFF:   { std::vector<OffReq*> v;   for(Req* r : g) v.push_back(static_cast<OffReq*>(r));   return run_off(v); }
 	default:       { std::vector<DpReq*> v;    for(Req* r : g) v.push_back(static_cast<DpReq*>(r));    return run_dp(v); }
 	}
 }
@@ -675,7 +740,7 @@ private:
 	// grouped by the batch-wide arguments (arrival order kept within a group), on
 	// its own context.
 	void loop(int kind) {
-		bt2g_prof_thread();
+		bt2g_prof_thread(2);
 		{
 			char nm[16];
 			snprintf(nm, sizeof(nm), "bt2g-%.10s", ST_NAMES[kind]);
@@ -1181,4 +1246,256 @@ bool SwAlignerAcc::gpu_next(SwResult& res, TAlScore minsc, RandomSource& rnd, Dp
 		return true;
 	}
 	return false;
+}
+
+// ---- SwDriver: seed-hit extension and SA-row resolution ----------------------
+//
+// prioritizeSATups (aligner_sw_driver.cpp:490-738) extends every seed-hit range
+// with SwDriver::extend (299-483, LF walks left in the forward index and right
+// in the mirror index), and both it and eeSaTups (66-290) hand the ranges they
+// choose to GroupWalk2S, whose advanceElement (group_walk.h:1161-1216) walks LF
+// until an SA sample to resolve a row's text offset.  On the reference's host
+// these walks are cache misses into a 3 GB index.  Here:
+//   * before the reference's prioritizeSATups runs, every range it will look at
+//     (SeedResults::hitsByRank + AlignmentCacheIface::queryQval, in its own
+//     order) is extended on the GPU in one request (bt2g_extend); the
+//     reference's extend calls then read those results (extend below);
+//   * GroupWalk2S::init only records the range (the explicit specialisations
+//     declared by bt2g_gw_spec.h); when prioritizeSATups / eeSaTups return,
+//     every unresolved row of the ranges they set up is resolved on the GPU in
+//     one request (bt2g_get_offset == Ebwt::getOffset, bt2_idx.cpp:150-171) and
+//     written into the range's offset list in the alignment cache, where the
+//     reference's walk leaves it too; advanceElement reads it (or, for a row
+//     that could not be batched, calls Ebwt::getOffset on the CPU).
+// Results are the reference's; the walk metrics (WalkMetrics, per-read LF op
+// counts of the walks) are not reproduced -- they reach no SAM field unless
+// --read-times / --metrics are given.
+extern "C" {
+void bt2g_real__ZN8SwDriver16prioritizeSATupsERK4ReadR11SeedResultsRK4EbwtPS6_RK16BitPairReferenceimbbbmR19AlignmentCacheIfaceR12RandomSourceR11WalkMetricsR14PerReadMetricsRmb(
+	SwDriver*, const Read&, SeedResults&, const Ebwt&, const Ebwt*, const BitPairReference&, int, size_t, bool, bool, bool,
+	size_t, AlignmentCacheIface&, RandomSource&, WalkMetrics&, PerReadMetrics&, size_t&, bool);
+bool bt2g_real__ZN8SwDriver8eeSaTupsERK4ReadR11SeedResultsRK4EbwtRK16BitPairReferenceR12RandomSourceR11WalkMetricsR9SwMetricsRmmb(
+	SwDriver*, const Read&, SeedResults&, const Ebwt&, const BitPairReference&, RandomSource&, WalkMetrics&, SwMetrics&,
+	size_t&, size_t, bool);
+void bt2g_real__ZN8SwDriver6extendERK4ReadRK4EbwtPS4_jjjjbmmR14PerReadMetricsRmS9_(
+	SwDriver*, const Read&, const Ebwt&, const Ebwt*, TIndexOffU, TIndexOffU, TIndexOffU, TIndexOffU, bool, size_t,
+	size_t, PerReadMetrics&, size_t&, size_t&);
+}
+
+namespace {
+
+bool drv_engine() {
+	static const bool on = [] {
+		const char* e = getenv("BT2G_DRIVER_SEAMS");
+		return !(e && e[0] == '0');
+	}();
+	return on;
+}
+
+// extend() results of the read being prioritised (valid during one
+// prioritizeSATups call on this thread: filled after the request's fiber
+// switch, and no switch happens inside the reference's prioritizeSATups)
+struct ExtTable {
+	bool on = false;
+	std::vector<bt2g_ext_in> keys;
+	std::vector<bt2g_ext_out> vals;
+};
+thread_local ExtTable t_ext;
+
+// ranges handed to GroupWalk2S::init during one prioritizeSATups / eeSaTups call
+struct GwRange {
+	TIndexOffU topf;
+	size_t size;
+	TSlice offs;
+};
+struct GwTable {
+	bool on = false;
+	std::vector<GwRange> ranges;
+};
+thread_local GwTable t_gw;
+
+const size_t MAX_ROWS = 8192;    // rows per read per request (the rest: CPU getOffset)
+
+void resolve_rows(const Ebwt& ebwtFw) {
+	t_gw.on = false;
+	if(t_gw.ranges.empty()) return;
+	// this fiber's ranges: the request below yields, and the carrier's other
+	// fibers reuse t_gw meanwhile
+	std::vector<GwRange> ranges;
+	ranges.swap(t_gw.ranges);
+	OffReq q;
+	std::vector<std::pair<size_t, size_t>> where;    // (range, element) of each row
+	for(size_t r = 0; r < ranges.size(); r++) {
+		GwRange& x = ranges[r];
+		for(size_t j = 0; j < x.size && q.rows.size() < MAX_ROWS; j++)
+			if(x.offs[j] == OFF_MASK) {
+				q.rows.push_back((uint32_t)(x.topf + j));
+				where.emplace_back(r, j);
+			}
+	}
+	if(!q.rows.empty()) {
+		g_disp.submit(&q);
+		count(ST_OFF, true);
+		for(size_t k = 0; k < where.size(); k++) ranges[where[k].first].offs[where[k].second] = q.offs[k];
+	}
+	(void)ebwtFw;
+}
+
+}  // namespace
+
+template <>
+void GroupWalk2S<TSlice, 16>::init(const Ebwt& ebwtFw, const BitPairReference& ref, SARangeWithOffs<TSlice>& sa,
+                                   RandomSource& rnd, WalkMetrics& met) {
+	(void)ebwtFw; (void)ref; (void)rnd; (void)met;
+	reset();
+	elt_ += sa.size();
+	if(t_gw.on) t_gw.ranges.push_back(GwRange{sa.topf, sa.size(), sa.offs});
+}
+
+template <>
+bool GroupWalk2S<TSlice, 16>::advanceElement(TIndexOffU elt, const Ebwt& ebwtFw, const BitPairReference& ref,
+                                             SARangeWithOffs<TSlice>& sa, GroupWalkState& gws, WalkResult& res,
+                                             WalkMetrics& met, PerReadMetrics& prm) {
+	(void)ref; (void)gws; (void)prm;
+	if(sa.offs[elt] == OFF_MASK) {       // not batched: the reference's getOffset on the CPU
+		sa.offs[elt] = ebwtFw.getOffset(sa.topf + elt);
+		count(ST_OFF, false);
+	}
+	met.reports++;
+	res.init(0, false, 0, elt, sa.topf + elt, (TIndexOffU)sa.len, sa.offs[elt]);
+	rep_++;
+	return true;
+}
+
+void SwDriver::prioritizeSATups(const Read& read, SeedResults& sh, const Ebwt& ebwtFw, const Ebwt* ebwtBw,
+                                const BitPairReference& ref, int seedmms, size_t maxelt, bool doExtend, bool lensq,
+                                bool szsq, size_t nsm, AlignmentCacheIface& ca, RandomSource& rnd, WalkMetrics& wlm,
+                                PerReadMetrics& prm, size_t& nelt_out, bool all) {
+	const bool eng = drv_engine();
+	t_ext.on = false;
+	if(eng && doExtend && ebwtBw != NULL && read.length() > 0 && read.length() <= BT2G_MAX_READ_LEN) {
+		// every range the loop at aligner_sw_driver.cpp:519-604 visits, in its order
+		ExtReq q;
+		q.r.set(read.patFw, read.qual);
+		EList<SATuple, 16> sat;
+		const size_t nonz = sh.nonzeroOffsets();
+		for(size_t i = 0; i < nonz; i++) {
+			bool fw = true;
+			uint32_t offidx = 0, rdoff = 0, seedlen = 0;
+			QVal qv = sh.hitsByRank(i, offidx, rdoff, fw, seedlen);
+			size_t nr = 0, ne = 0;
+			sat.clear();
+			ca.queryQval(qv, sat, nr, ne);
+			for(size_t j = 0; j < sat.size(); j++) {
+				const TIndexOffU sz = (TIndexOffU)sat[j].size();
+				bt2g_ext_in x;
+				x.read = 0;
+				x.fw = fw ? 1 : 0;
+				x.off = rdoff;
+				x.len = seedlen;
+				x.topf = sat[j].topf;
+				x.botf = sat[j].topf + sz;
+				x.topb = sat[j].topb;
+				x.botb = sat[j].topb + sz;
+				if(sz > 0 && rdoff + seedlen <= read.length()) q.in.push_back(x);
+			}
+		}
+		if(!q.in.empty()) {
+			g_disp.submit(&q);
+			count(ST_EXT, true);
+			t_ext.keys.assign(q.in.begin(), q.in.end());
+			t_ext.vals.assign(q.out.data(), q.out.data() + q.out.size());
+			t_ext.on = true;
+		}
+	}
+	t_gw.ranges.clear();
+	t_gw.on = eng;
+	bt2g_real__ZN8SwDriver16prioritizeSATupsERK4ReadR11SeedResultsRK4EbwtPS6_RK16BitPairReferenceimbbbmR19AlignmentCacheIfaceR12RandomSourceR11WalkMetricsR14PerReadMetricsRmb(
+		this, read, sh, ebwtFw, ebwtBw, ref, seedmms, maxelt, doExtend, lensq, szsq, nsm, ca, rnd, wlm, prm, nelt_out, all);
+	t_ext.on = false;
+	resolve_rows(ebwtFw);
+}
+
+bool SwDriver::eeSaTups(const Read& rd, SeedResults& sh, const Ebwt& ebwt, const BitPairReference& ref,
+                        RandomSource& rnd, WalkMetrics& wlm, SwMetrics& swmSeed, size_t& nelt_out, size_t maxelt,
+                        bool all) {
+	t_gw.ranges.clear();
+	t_gw.on = drv_engine();
+	bool ret = bt2g_real__ZN8SwDriver8eeSaTupsERK4ReadR11SeedResultsRK4EbwtRK16BitPairReferenceR12RandomSourceR11WalkMetricsR9SwMetricsRmmb(
+		this, rd, sh, ebwt, ref, rnd, wlm, swmSeed, nelt_out, maxelt, all);
+	resolve_rows(ebwt);
+	return ret;
+}
+
+void SwDriver::extend(const Read& rd, const Ebwt& ebwtFw, const Ebwt* ebwtBw, TIndexOffU topf, TIndexOffU botf,
+                      TIndexOffU topb, TIndexOffU botb, bool fw, size_t off, size_t len, PerReadMetrics& prm,
+                      size_t& nlex, size_t& nrex) {
+	if(t_ext.on) {
+		const std::vector<bt2g_ext_in>& K = t_ext.keys;
+		for(size_t i = 0; i < K.size(); i++) {
+			const bt2g_ext_in& k = K[i];
+			if(k.topf == topf && k.botf == botf && k.topb == topb && k.botb == botb && (k.fw != 0) == fw && k.off == off &&
+			   k.len == len) {
+				nlex += t_ext.vals[i].nlex;
+				nrex += t_ext.vals[i].nrex;
+				prm.nSdFmops += t_ext.vals[i].fmops;
+				return;
+			}
+		}
+	}
+	count(ST_EXT, false);
+	bt2g_real__ZN8SwDriver6extendERK4ReadRK4EbwtPS4_jjjjbmmR14PerReadMetricsRmS9_(
+		this, rd, ebwtFw, ebwtBw, topf, botf, topb, botb, fw, off, len, prm, nlex, nrex);
+}
+
+// ---- AlignmentCache::addOnTheFlyImpl (aligner_cache.cpp:55-104) ---------------
+// Registers a seed hit's SA range in the current-read cache and appends one
+// OFF_MASK offset slot per row to salist_ -- one PList::add per row in the
+// reference, i.e. a function call and a capacity check per element; on an
+// hg38-scale genome a seed in a repeat family has a range of 10^5 rows, and
+// this loop was 18 % of the drop-in's host CPU (r03f).  Restated here with the
+// same result, pool use and failure point: PList::add for the first slot of
+// every page (which takes the page from the pool, or fails exactly where the
+// reference's loop fails), plain stores for the rest of the page.
+namespace {
+struct TSAListFill : public PList<TIndexOffU, CACHE_PAGE_SZ> {
+	// n copies of v, as n calls of add(p, v): returns how many were added
+	size_t add_fill(Pool& p, size_t n, TIndexOffU v) {
+		const size_t per = (size_t)CACHE_PAGE_SZ / sizeof(TIndexOffU);
+		size_t done = 0;
+		while(done < n) {
+			if(!add(p, v)) return done;
+			done++;
+			const size_t k = std::min(per - cur_, n - done);
+			std::fill(pages_[curPage_] + cur_, pages_[curPage_] + cur_ + k, v);
+			cur_ += k;
+			done += k;
+		}
+		return done;
+	}
+};
+}  // namespace
+
+bool AlignmentCache::addOnTheFlyImpl(QVal& qv, const SAKey& sak, TIndexOffU topf, TIndexOffU botf, TIndexOffU topb,
+                                     TIndexOffU botb) {
+	(void)botb;
+	bool added = true;
+	if(!qv.valid()) qv.init((uint32_t)qlist_.size(), 0, 0);
+	qv.addRange(botf - topf);
+	if(!qlist_.add(pool(), sak)) return false;
+	SANode* s = samap_.add(pool(), sak, &added);
+	if(s == NULL) return false;
+	if(added) {
+		s->payload.i = (TIndexOffU)salist_.size();
+		s->payload.len = botf - topf;
+		s->payload.topf = topf;
+		s->payload.topb = topb;
+		const size_t n = botf - topf;
+		const size_t k = static_cast<TSAListFill&>(salist_).add_fill(pool(), n, OFF_MASK);
+		if(k < n) {
+			s->payload.len = (TIndexOffU)k;
+			return false;
+		}
+	}
+	return true;
 }

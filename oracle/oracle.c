@@ -221,6 +221,61 @@ uint32_t orc_get_offset(const orc_ebwt* e, uint32_t row) {
 }
 
 /* ---------------------------------------------------------------------- */
+/* SwDriver::extend (aligner_sw_driver.cpp:299-483): how far a seed-hit     */
+/* range extends left (forward index) and right (mirror index) without an  */
+/* edit.  seq: the read's codes (patFw); fw: seed on the read (1) or on its */
+/* reverse complement (0); off/len: the seed from the 5' end.               */
+/* out: nlex, nrex, LF steps (PerReadMetrics::nSdFmops increments).         */
+/* ---------------------------------------------------------------------- */
+static uint32_t ext_walk(const orc_ebwt* e, uint32_t top, uint32_t bot, const uint8_t* seq, uint32_t rdlen, int fw,
+                         uint32_t lim, int64_t i0, int dir, uint32_t* fmops) {
+	uint32_t n = 0;
+	orc_locus tl, bl;
+	init_locs(top, bot, &tl, &bl);
+	for(uint32_t ii = 0; ii < lim; ii++) {
+		int64_t i = i0 + (int64_t)dir * ii;
+		int rdc = fw ? seq[i] : seq[rdlen - 1 - i];
+		if(!fw) rdc = rdc > 3 ? 4 : 3 - rdc;      /* patRc */
+		(*fmops)++;
+		if(bl.bp >= 0) {
+			uint32_t t[4] = {0, 0, 0, 0}, b[4] = {0, 0, 0, 0}, tp[4] = {0, 0, 0, 0}, bp[4] = {0, 0, 0, 0};
+			map_bilf_ex(e, &tl, &bl, t, b, tp, bp);
+			int nonz = -1, abort_ = 0;
+			uint32_t orig = bot - top;
+			for(int j = 0; j < 4; j++) {
+				if(b[j] > t[j]) {
+					if(nonz >= 0) { abort_ = 1; break; }
+					nonz = j;
+					top = t[j];
+					bot = b[j];
+				}
+			}
+			if(abort_ || (nonz != rdc && rdc <= 3) || bot - top < orig) break;
+		} else {
+			int c = map_lf1(e, &top, &tl);
+			if(c != rdc && rdc <= 3) break;
+			bot = top + 1;
+		}
+		if(++n == 255u) break;
+		init_locs(top, bot, &tl, &bl);
+	}
+	return n;
+}
+
+void orc_extend(const orc_ebwt* fwi, const orc_ebwt* bwi, const uint8_t* seq, uint32_t rdlen, int fw, uint32_t off,
+                uint32_t len, uint32_t topf, uint32_t botf, uint32_t topb, uint32_t botb, uint32_t* out) {
+	init_lut();
+	uint32_t fmops = 0, nlex = 0, nrex = 0;
+	uint32_t lim = fw ? off : rdlen - len - off;
+	if(lim > 0) nlex = ext_walk(fwi, topf, botf, seq, rdlen, fw, lim, fw ? (int64_t)off - 1 : (int64_t)rdlen - off - len - 1, -1, &fmops);
+	lim = fw ? rdlen - len - off : off;
+	if(lim > 0 && bwi) nrex = ext_walk(bwi, topb, botb, seq, rdlen, fw, lim, fw ? (int64_t)len + off : (int64_t)rdlen - off, 1, &fmops);
+	out[0] = nlex;
+	out[1] = nrex;
+	out[2] = fmops;
+}
+
+/* ---------------------------------------------------------------------- */
 /* exactSweep (aligner_seed.cpp:750-968), one strand at a time.            */
 /* ---------------------------------------------------------------------- */
 static void sweep_strand(const orc_ebwt* e, const uint8_t* seq, uint32_t len, uint32_t mine_max,

@@ -55,6 +55,8 @@ class Oracle:
         L.orc_get_offset.restype = C.c_uint32
         L.orc_get_offset.argtypes = [C.POINTER(OrcEbwt), C.c_uint32]
         L.orc_bilf.argtypes = [C.POINTER(OrcEbwt), C.c_uint32, C.c_uint32, C.c_uint32] + [C.c_void_p] * 4
+        L.orc_extend.argtypes = [C.POINTER(OrcEbwt), C.POINTER(OrcEbwt), C.c_void_p, C.c_uint32, C.c_int,
+                                 C.c_uint32, C.c_uint32, C.c_uint32, C.c_uint32, C.c_uint32, C.c_uint32, C.c_void_p]
         L.orc_sw.argtypes = [C.c_void_p, C.c_void_p, C.c_int, C.c_void_p, C.c_int, C.c_int64,
                              C.POINTER(OrcScoring), C.c_int, C.c_int, C.c_void_p, C.c_void_p, C.c_void_p]
         L.orc_ungapped.restype = C.c_int
@@ -107,6 +109,14 @@ class Oracle:
 
     def get_offset(self, fe, row):
         return self.lib.orc_get_offset(C.byref(fe), row)
+
+    def extend(self, fe, be, seq, fw, off, ln, topf, botf, topb, botb):
+        """SwDriver::extend of one seed-hit range -> (nlex, nrex, LF steps)."""
+        seq = np.ascontiguousarray(seq, np.uint8)
+        out = np.zeros(3, np.uint32)
+        self.lib.orc_extend(C.byref(fe), C.byref(be) if be is not None else None, seq.ctypes.data, len(seq),
+                            int(fw), off, ln, topf, botf, topb, botb, out.ctypes.data)
+        return out
 
     def bilf(self, e, top, bot, topp):
         arrs = [np.zeros(4, np.uint32) for _ in range(4)]

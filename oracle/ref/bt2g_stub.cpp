@@ -29,6 +29,9 @@ int bt2ref_sw(const char* seq, const char* qual, int fw, const uint8_t* rfmask, 
 int bt2ref_sw_bt(const char* seq, const char* qual, int fw, const uint8_t* rfmask, int ncol, int64_t minsc,
                  const void* sp, int enable8, int triml, int corel, int corer, int maxaln, int maxedit,
                  int64_t* out, int64_t* aln, int32_t* edits, int32_t* fates, int capf);
+void bt2ref_extend(void* vh, int n, const char** seqs, const char** quals, const int32_t* fw, const uint32_t* off,
+                   const uint32_t* len, const uint32_t* tb, uint32_t* out);
+void bt2ref_get_offsets(void* vh, int n, const uint32_t* rows, uint32_t* out);
 void bt2ref_ungapped(void* vh, int n, const char** seqs, const char** quals, const uint8_t* fws,
                      const uint32_t* refidx, const int64_t* off, const int64_t* minsc, const void* sp,
                      int ohang, int maxedit, int64_t* out, int32_t* edits);
@@ -227,6 +230,28 @@ int bt2g_sw_align_bt(bt2g_ctx*, const uint8_t* reads, const uint8_t* quals, uint
 			for(uint32_t k = 0; k < cap; k++) fates[(size_t)i * cap + k] = (int8_t)ft[k];
 	}
 	return rc;
+}
+
+int bt2g_extend(bt2g_ctx* c, const uint8_t* reads, uint32_t stride, const uint32_t* lens, uint32_t nreads,
+                const bt2g_ext_in* in, uint32_t n, bt2g_ext_out* out) {
+	for(uint32_t i = 0; i < n; i++) {
+		const bt2g_ext_in& q = in[i];
+		if(q.read >= nreads) return fail(BT2G_ERR_ARG, "stub: bad read");
+		std::string s = ascii(reads + (size_t)q.read * stride, lens[q.read]);
+		std::string qq(lens[q.read], 'I');
+		const char* sp = s.c_str();
+		const char* qp = qq.c_str();
+		uint32_t tb[4] = {q.topf, q.botf, q.topb, q.botb}, o[3];
+		bt2ref_extend(c->ref, 1, &sp, &qp, &q.fw, &q.off, &q.len, tb, o);
+		out[i].nlex = o[0]; out[i].nrex = o[1]; out[i].fmops = o[2]; out[i].pad = 0;
+	}
+	return BT2G_OK;
+}
+
+int bt2g_get_offset(bt2g_ctx* c, const uint32_t* rows, uint32_t n, uint32_t* offs, uint32_t* loads) {
+	bt2ref_get_offsets(c->ref, (int)n, rows, offs);
+	if(loads) memset(loads, 0, sizeof(uint32_t) * n);
+	return BT2G_OK;
 }
 
 // the packed flavour (include/bt2g.h): the unpacked call, then packed here

@@ -31,6 +31,7 @@
 #include "random_source.h"
 #include "dp_framer.h"
 #include "pe.h"
+#include "aligner_sw_driver.h"
 
 // Globals normally defined by bt2_search.cpp (search_globals.h, aligner_seed_policy.h).
 bool gReportOverhangs = false;
@@ -732,4 +733,36 @@ void bt2ref_frame(int n, const int64_t* in, const ScoreParams* sp, const int32_t
 	}
 }
 
+} // extern "C"
+
+// SwDriver::extend (aligner_sw_driver.cpp:299-483, protected) on seed-hit
+// ranges: per range {fw, off, len} and {topf, botf, topb, botb}; out per range
+// {nlex, nrex, nSdFmops increments}.
+namespace {
+struct SwDriverX : public SwDriver {
+	SwDriverX() : SwDriver(1 << 20) {}
+	void ext(const Read& rd, const Ebwt& f, const Ebwt* b, uint32_t tf, uint32_t bf, uint32_t tb, uint32_t bb, bool fw,
+	         size_t off, size_t len, PerReadMetrics& prm, size_t& nlex, size_t& nrex) {
+		extend(rd, f, b, tf, bf, tb, bb, fw, off, len, prm, nlex, nrex);
+	}
+};
+}  // namespace
+
+extern "C" {
+void bt2ref_extend(void* vh, int n, const char** seqs, const char** quals, const int32_t* fw, const uint32_t* off,
+                   const uint32_t* len, const uint32_t* tb, uint32_t* out) {
+	RefHandle* h = (RefHandle*)vh;
+	SwDriverX sd;
+	for(int i = 0; i < n; i++) {
+		Read rd("r", seqs[i], quals[i]);
+		PerReadMetrics prm;
+		prm.reset();
+		size_t nlex = 0, nrex = 0;
+		sd.ext(rd, *h->fw, h->bw, tb[4 * i], tb[4 * i + 1], tb[4 * i + 2], tb[4 * i + 3], fw[i] != 0, off[i], len[i], prm,
+		       nlex, nrex);
+		out[3 * i] = (uint32_t)nlex;
+		out[3 * i + 1] = (uint32_t)nrex;
+		out[3 * i + 2] = (uint32_t)prm.nSdFmops;
+	}
+}
 } // extern "C"

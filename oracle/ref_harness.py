@@ -194,6 +194,21 @@ class RefIndex:
                           out.ctypes.data, ed.ctypes.data)
         return out, [ed[i, :int(out[i, 5])].copy() for i in range(n)]
 
+    def extend(self, seqs, quals, fw, off, ln, tb):
+        """SwDriver::extend per range (seqs[i] the read of range i): tb n x 4 =
+        (topf, botf, topb, botb).  Returns n x 3 (nlex, nrex, nSdFmops)."""
+        L = self.L
+        L.bt2ref_extend.argtypes = [C.c_void_p, C.c_int, C.POINTER(C.c_char_p), C.POINTER(C.c_char_p)] + [C.c_void_p] * 5
+        n = len(seqs)
+        fw = np.ascontiguousarray(fw, np.int32)
+        off = np.ascontiguousarray(off, np.uint32)
+        ln = np.ascontiguousarray(ln, np.uint32)
+        tb = np.ascontiguousarray(tb, np.uint32)
+        out = np.zeros((n, 3), np.uint32)
+        L.bt2ref_extend(self.h, n, _cstrs(seqs), _cstrs(quals), fw.ctypes.data, off.ctypes.data, ln.ctypes.data,
+                        tb.ctypes.data, out.ctypes.data)
+        return out
+
     def seed_search(self, seqs, quals, seedlen, interval, offset, maxseeds=64):
         n = len(seqs)
         out = np.zeros(n * 2 * maxseeds * 4, np.uint32)

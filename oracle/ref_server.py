@@ -96,9 +96,13 @@ class Server:
     def log(self):
         return open(self.log_path, "rb").read().decode(errors="replace")
 
-    def run(self, chunk_args, k=1, client=CLIENT, timeout=1200):
+    def run(self, chunk_args, k=1, client=CLIENT, timeout=1200, warmup=()):
         """Send every chunk (client argument lists) over at most k concurrent
-        connections.  Returns (wall seconds, list of SAM texts in chunk order)."""
+        connections.  Returns (wall seconds, list of SAM texts in chunk order).
+        `warmup`: chunks sent first, untimed, output dropped (a long-running
+        server past its start-up: workers spawned, per-worker state allocated)."""
+        if warmup:
+            self.run(list(warmup), k=min(k, len(warmup)), client=client, timeout=timeout)
         outs = [None] * len(chunk_args)
         errs = []
         nxt = [0]
@@ -127,6 +131,7 @@ class Server:
             t.join()
         dt = time.perf_counter() - t0
         self.last_cpu_s = self.cpu_seconds() - c0        # server CPU time (all threads) over the run
+        self.last_rss_gb = self.rss_gb()
         self.last_threads = self.thread_cpu()
         if errs:
             raise RuntimeError(f"client failures: {errs[:3]}")
@@ -153,6 +158,16 @@ class Server:
             e[1] += cs
             e[2] = max(e[2], cs)
         return out
+
+    def rss_gb(self):
+        """Resident memory of the server (GB)."""
+        try:
+            for ln in open(f"/proc/{self.proc.pid}/status"):
+                if ln.startswith("VmRSS:"):
+                    return int(ln.split()[1]) / 1e6
+        except (OSError, ValueError):
+            pass
+        return float("nan")
 
     def cpu_seconds(self):
         """User + system CPU seconds of the server process so far (/proc/<pid>/stat)."""

@@ -41,6 +41,7 @@ def main():
     ap.add_argument("--cpu-threads", type=int, default=0, help="stock server -p (0: usable host cores)")
     ap.add_argument("--workdir", default="/tmp/dropin_bench")
     ap.add_argument("--skip-stock", action="store_true")
+    ap.add_argument("--warmup-chunks", type=int, default=1, help="chunks sent untimed first (both servers)")
     ap.add_argument("--dropin-binary", default="", help="default oracle/_ref/bowtie2-align-server-gpu "
                                                        "(-stub: the binding over the CPU stand-in)")
     a = ap.parse_args()
@@ -82,11 +83,11 @@ def main():
         with rs.Server(base, threads=th, args=a.args, binary=binary, env=env,
                        log_path=os.path.join(a.workdir, f"server_{tag}.log")) as s:
             log(f"{tag}: server ready in {s.load_s:.1f}s (-p {th})")
-            dt, outs = s.run(chunks, k=a.k)
+            dt, outs = s.run(chunks, k=a.k, warmup=chunks[:a.warmup_chunks])
         sams[tag] = rs.sorted_records(outs)
         unit = "pairs/s" if a.mode == "paired" else "reads/s"
         out[tag] = {"seconds": dt, "rate": a.reads / dt, "unit": unit, "threads": th, "records": len(sams[tag]),
-                    "server_cpu_s": s.last_cpu_s, "server_cores_busy": s.last_cpu_s / dt,
+                    "server_cpu_s": s.last_cpu_s, "server_cores_busy": s.last_cpu_s / dt, "server_rss_gb": s.last_rss_gb,
                     "server_threads_cpu": s.last_threads}
         time.sleep(0.5)
         if os.path.exists(stats):

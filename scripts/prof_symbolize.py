@@ -31,7 +31,11 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("dump")
     ap.add_argument("--top", type=int, default=40)
+    ap.add_argument("--callers-of", default="", help="function name: list the callers of its samples "
+                    "(from the (pc, [rsp]) pairs; meaningful for frameless leaves such as syscall wrappers)")
     a = ap.parse_args()
+    if a.callers_of:
+        return callers(a)
     by_path = collections.defaultdict(list)
     total = 0
     for ln in open(a.dump):
@@ -57,6 +61,47 @@ def main():
     print(f"{total} samples")
     for nm, c in funcs.most_common(a.top):
         print(f"{100.0 * c / total:6.2f}%  {c:7d}  {nm}")
+
+
+def symbolize(pairs):
+    """{(path, off): name} for a list of (path, off)."""
+    by = collections.defaultdict(set)
+    for p, o in pairs:
+        by[p].add(o)
+    out = {}
+    for p, offs in by.items():
+        offs = sorted(offs)
+        if p == "?" or p.startswith("["):
+            for o in offs:
+                out[(p, o)] = p
+            continue
+        segs = load_segments(p)
+        res = subprocess.run(["addr2line", "-f", "-C", "-e", p] + [hex(to_vaddr(segs, o)) for o in offs],
+                             stdout=subprocess.PIPE, stderr=subprocess.DEVNULL, text=True).stdout.splitlines()
+        for o, nm in zip(offs, res[0::2]):
+            out[(p, o)] = f"{nm[:100]} [{p.rsplit('/', 1)[-1]}]"
+    return out
+
+
+def callers(a):
+    rows = []
+    for ln in open(a.dump):
+        if ln.startswith("#pair "):
+            f = ln.split()
+            rows.append(((f[1], int(f[2], 16)), (f[3], int(f[4], 16)), int(f[5]), int(f[6]) if len(f) > 6 else 0))
+    names = symbolize([r[0] for r in rows] + [r[1] for r in rows])
+    cnt = collections.Counter()
+    roles = collections.Counter()
+    tot = 0
+    for pc, ret, c, role in rows:
+        roles[role] += c
+        if a.callers_of in names[pc]:
+            cnt[f"{['?', 'carrier', 'dispatcher'][role] if role < 3 else role}: {names[ret]}"] += c
+            tot += c
+    print(f"samples by thread role (1 carrier, 2 dispatcher): {dict(roles)}")
+    print(f"{tot} samples in {a.callers_of}")
+    for nm, c in cnt.most_common(a.top):
+        print(f"{c:7d}  {nm}")
 
 
 if __name__ == "__main__":

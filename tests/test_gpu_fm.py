@@ -64,6 +64,15 @@ def test_one_mm_golden(engines, name, mode):
 
 
 @pytest.mark.parametrize("name", ["lambda", "synth"])
+def test_extend_golden(engines, name):
+    """SwDriver::extend (k_extend) on every seed hit of the reference's seed search."""
+    g = load_golden("ext_" + name)
+    rg = g["ranges"]
+    out = engines[name].extend(g["reads"], g["lens"], rg)
+    assert np.array_equal(out[:, :3], g["out"])
+
+
+@pytest.mark.parametrize("name", ["lambda", "synth"])
 def test_get_offset_golden(engines, name):
     g = load_golden("fm_" + name)
     offs, loads = engines[name].get_offset(g["off_rows"])

@@ -70,6 +70,19 @@ def test_get_offset_and_bilf(orc, name):
     assert idx.fw.length > 0
 
 
+@pytest.mark.parametrize("name", ["lambda", "synth"])
+def test_extend(orc, name):
+    """SwDriver::extend on every seed hit the reference's seed search found (ext_<name>.npz)."""
+    g = load_golden("ext_" + name)
+    fe, be = _ebwts(orc, name)
+    bad = 0
+    for k, (r, fw, off, ln, tf, bf, tb, bb) in enumerate(g["ranges"]):
+        seq = g["reads"][r, :g["lens"][r]]
+        got = orc.extend(fe, be, seq, int(fw), int(off), int(ln), int(tf), int(bf), int(tb), int(bb))
+        bad += int(not np.array_equal(got, g["out"][k]))
+    assert bad == 0
+
+
 def sw_problems(g):
     """Yield (read codes as aligned, quals as aligned, rfmask, minsc, fw, expected out, expected cands)."""
     for p in range(len(g["rd_index"])):
