@@ -54,6 +54,11 @@ HBM_PEAK_GBS = 8000.0          # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
 # profiles/r01_valu_rates.txt, full-rate ops 70 T)
 VALU_OPS_PER_CELL = 11.9 if os.environ.get("BT2G_BT_HPLANE") == "1" else 22.0
 VALU_PEAK_TOPS = 78.6
+# algorithmic integer ops per DP cell: H = max(Hdiag - pen, E, F),
+# E = max(E - ext, H - open), F likewise, with the gap-barrier vetoes
+SW_OPS_PER_CELL = 10
+# the kernel whose PMC counters make roofline.traffic (per bench kernel id)
+PMC_KERNEL = {0: "k_exact_sweep", 1: "k_seed_search", 2: "k_one_mm", 3: "k_get_offset", 4: "k_sw_sys"}
 VALU_PACKED_TOPS = 37.0
 SEEDLEN, INTERVAL = 22, 15     # --sensitive, 150 bp: -L 22, -i S,1,1.15 -> 1+1.15*sqrt(150) = 15
 
@@ -499,6 +504,19 @@ def pmc_traffic(fetch_csv, write_csv, kernel):
     return total
 
 
+def real_schedule(cpu):
+    """The north-star rate: the reference server bound to the
+    engines (integration/, the drop-in) on the reference's own schedule, through
+    its own client, SAM compared with the stock server's on the same reads."""
+    if not cpu or "dropin_server" not in cpu or "reference_server" not in cpu \
+            or "value" not in cpu.get("reference_server", {}):
+        return None
+    d, r = cpu["dropin_server"], cpu["reference_server"]
+    return {"dropin_value": d["value"], "stock_value": r["value"], "unit": d["unit"],
+            "vs_stock": d["value"] / r["value"], "sam_identical": d.get("sam_identical_to_reference"),
+            "stock_cores": r.get("cores"), "sample": r.get("sample")}
+
+
 def combine_ranks(elapsed, n_aligned, dev):
     """Max of the per-rank times, sum of the aligned-read counters: the path's
     only collective (RCCL on the GPUs, gloo in the CPU tests)."""
@@ -643,7 +661,7 @@ def server_baseline(base, reads, quals, pol, sample, threads, workers, args_srv,
                             ("dropin", dropin_binary or os.path.join(rs.REF_DIR, "bowtie2-align-server-gpu"),
                              workers)):
         stats = os.path.join(log_dir, f"stats_{tag}.json")
-        env = {"BT2G_INDEX": base, "BT2G_ADAPTER_STATS": stats, "BT2G_DEVICE": "0"}
+        env = rs.dropin_env(base, stats)
         with rs.Server(base, threads=th, args=args_srv, binary=binary, env=env,
                        log_path=os.path.join(log_dir, f"server_{tag}.log")) as srv:
             dt, outs = srv.run(chunks, k=8, warmup=chunks[:1])
@@ -958,10 +976,16 @@ def main():
         launches, ms = stats[k]
         if launches:
             per_launch[k] = ms / launches
-    dom = max((k for k in per_launch if k < 4), key=lambda k: per_launch[k])
-    achieved = bytes_k[dom] / (per_launch[dom] / 1e3) / 1e9
     sw_cells = last["npb"] * args.read_len * pipe.ncol
     sw_gcups = sw_cells / (per_launch.get(4, float("nan")) / 1e3) / 1e9
+    # the dominant kernel: the longest per step among those with an algorithmic
+    # work figure: FM kernels in bytes (HBM-bound), the SW fill
+    # in integer ops, SW_OPS_PER_CELL per DP cell (VALU-bound)
+    work_k = dict(bytes_k)
+    work_k[4] = sw_cells * SW_OPS_PER_CELL if 4 in per_launch else None
+    step_ms = {k: stats[k][1] / args.steps for k in per_launch}
+    dom = max((k for k in per_launch if work_k.get(k)), key=lambda k: step_ms[k])
+    achieved = work_k[dom] / (per_launch[dom] / 1e3) / (1e12 if dom == 4 else 1e9)
     for k in per_launch:
         log(f"[rank {rank}] {names_k[k]:12s} {per_launch[k]:8.3f} ms/launch")
     mmprof = getattr(bt2g.lib(), "bt2g_mm_prof_waves", None) if "prof" in bt2g.LIB_PATH else None
@@ -1102,21 +1126,35 @@ def main():
             "config": {"workload": workload(args),
                        "global_batch": args.reads * world, "seq_len": args.read_len, "parallelism": f"dp{world}",
                        "aligned_frac": n_aligned / total_reads},
-            "roofline": {"bound": "hbm", "kernel": names_k[dom], "achieved": achieved, "peak": HBM_PEAK_GBS,
-                         "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS,
-                         "traffic": pmc_traffic(args.pmc_fetch, args.pmc_write, "k_" + names_k[dom]),
-                         "bytes_per_launch": bytes_k[dom], "ms_per_launch": per_launch[dom]},
+            "roofline": dict({"bound": "hbm", "kernel": names_k[dom], "achieved": achieved, "peak": HBM_PEAK_GBS,
+                              "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS, "bytes_per_launch": bytes_k[dom]}
+                             if dom != 4 else
+                             {"bound": "valu", "kernel": "sw_align (systolic fill + decision plane, candidate sort)",
+                              "achieved": achieved, "peak": VALU_PEAK_TOPS, "unit": "T int-ops/s",
+                              "frac": achieved / VALU_PEAK_TOPS, "ops_per_cell": SW_OPS_PER_CELL,
+                              "cells_per_launch": sw_cells, "gcups": sw_gcups,
+                              "issued_valu_lane_ops_per_cell": VALU_OPS_PER_CELL},
+                             ms_per_launch=per_launch[dom], ms_per_step=step_ms[dom],
+                             traffic=pmc_traffic(args.pmc_fetch, args.pmc_write, PMC_KERNEL[dom])),
+            "aligned_per_s": n_aligned / elapsed,
+            "schedule": "bench chain: exact sweep, gated 1-mm search, round-0 exact seeds, getOffset of each hit "
+                        "range's top row, <= 2 seed-extension DPs per read (fixed policy), fill + nextAlignment "
+                        "loop; the reference's real schedule (RNG-driven prioritisation, streaks, re-seeding, "
+                        "SAM) is timed by real_schedule",
+            "real_schedule": real_schedule(cpu),
             "kernels_ms": {names_k[k]: per_launch[k] for k in per_launch},
             "kernels_gbs": {names_k[k]: bytes_k[k] / (per_launch[k] / 1e3) / 1e9 for k in per_launch
                             if bytes_k.get(k)},
             "side_loads_per_step": {names_k[k]: (bytes_k[k] // 64) for k in (0, 1, 2, 3) if bytes_k.get(k)},
             "sw_gcups": sw_gcups,
             # the SW fill against its VALU ceiling (north_star: VALU utilisation of the SW kernel)
-            "sw_roofline": {"bound": "valu", "kernel": "sw_align (systolic fill + decision plane + candidate sort)",
-                            "achieved": sw_gcups * VALU_OPS_PER_CELL / 1e3, "peak": VALU_PEAK_TOPS,
-                            "unit": "T lane-ops/s", "frac": sw_gcups * VALU_OPS_PER_CELL / 1e3 / VALU_PEAK_TOPS,
-                            "frac_packed_issue": sw_gcups * VALU_OPS_PER_CELL / 1e3 / VALU_PACKED_TOPS,
-                            "ops_per_cell": VALU_OPS_PER_CELL} if args.mode == "ee" else None,
+            # issued (not algorithmic) VALU work of the fill: its instruction mix, from
+            # the PMC pass scripts/pmc_fill.sh (a constant measured on another run)
+            "sw_issue": {"issued_valu_lane_ops_per_cell": VALU_OPS_PER_CELL,
+                         "issued_T_lane_ops_per_s": sw_gcups * VALU_OPS_PER_CELL / 1e3,
+                         "of_valu_peak": sw_gcups * VALU_OPS_PER_CELL / 1e3 / VALU_PEAK_TOPS,
+                         "of_packed_issue_ceiling": sw_gcups * VALU_OPS_PER_CELL / 1e3 / VALU_PACKED_TOPS}
+            if args.mode == "ee" else None,
             "backtrace": bt_stats,
             "landscape": landscape,
             "mate_search": mate_stats,

@@ -207,7 +207,7 @@ class Engine:
 
     def close(self):
         if self.h:
-            lib().bt2g_close(self.h)
+            _chk(lib().bt2g_close(self.h))     # fails while shared() contexts are open
             self.h = C.c_void_p()
 
     def __enter__(self):

@@ -4,6 +4,7 @@
 // batch calls into kernel launches on a HIP stream, and provides the
 // host-pointer convenience wrappers.  No exception crosses the ABI; errors are
 // status codes plus a thread-local message (bt2g_last_error).
+#include <atomic>
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 #include <stdio.h>
@@ -59,6 +60,10 @@ struct bt2g_ctx {
 	uint32_t nref = 0;
 	uint64_t num_sides = 0;
 	uint64_t hbm_bytes = 0;
+	// contexts opened on this one's index (bt2g_open_shared) and still open; the
+	// index owner cannot close before them.  `base`: the owner of a shared context
+	std::atomic<int> shares{0};
+	bt2g_ctx* base = nullptr;
 	// profiling
 	bool prof = false;
 	struct Pending { int kid; hipEvent_t a, b; };
@@ -89,6 +94,9 @@ struct bt2g_ctx {
 	// pinned host staging for the wrappers' copies (same growth rule as the arena)
 	uint8_t* pin = nullptr;
 	size_t pin_cap = 0, pin_used = 0, pin_need = 0;
+	// device mirror of `pin` (same size and offsets): a call's inputs are staged
+	// in `pin` and reach the device in one copy, its outputs come back in one
+	uint8_t* pin_dev = nullptr;
 	// $BT2G_SYNC=poll: host waits query an event and sleep between queries
 	hipEvent_t poll_ev = nullptr;
 };
@@ -238,12 +246,17 @@ struct Arena {
 		c->pin_used = 0;
 		if(c->pin_need > c->pin_cap) {
 			if(c->pin) (void)hipHostFree(c->pin);
+			if(c->pin_dev) (void)hipFree(c->pin_dev);
 			c->pin = nullptr;
+			c->pin_dev = nullptr;
 			size_t cap = std::max<size_t>(c->pin_need + c->pin_need / 4, (size_t)16 << 20);
-			if(hipHostMalloc((void**)&c->pin, cap, hipHostMallocDefault) == hipSuccess) {
+			if(hipHostMalloc((void**)&c->pin, cap, hipHostMallocDefault) == hipSuccess &&
+			   hipMalloc((void**)&c->pin_dev, cap) == hipSuccess) {
 				c->pin_cap = cap;
 			} else {
+				if(c->pin) (void)hipHostFree(c->pin);
 				c->pin = nullptr;
+				c->pin_dev = nullptr;
 				c->pin_cap = 0;
 			}
 		}
@@ -516,6 +529,9 @@ int bt2g_open_shared(bt2g_ctx* base, bt2g_ctx** out) {
 	c->ref_starts = base->ref_starts;
 	c->nref = base->nref;
 	c->num_sides = base->num_sides;
+	c->hbm_bytes = base->hbm_bytes;
+	c->base = base;
+	base->shares++;
 	*out = c;
 	return BT2G_OK;
 }
@@ -550,6 +566,9 @@ int bt2g_open(const char* index_base, int device, bt2g_ctx** out) {
 
 int bt2g_close(bt2g_ctx* c) {
 	if(!c) return BT2G_OK;
+	if(c->shares.load() > 0)
+		return fail(BT2G_ERR_ARG, "%d shared context(s) still use this index: close them first", c->shares.load());
+	if(c->base) c->base->shares--;
 	(void)hipSetDevice(c->device);
 	if(c->stream) (void)hipStreamSynchronize(c->stream);
 	drain_prof(c);
@@ -559,6 +578,7 @@ int bt2g_close(bt2g_ctx* c) {
 	if(c->bt_plane) { (void)hipFree(c->bt_plane); (void)hipFree(c->bt_marks); }
 	if(c->arena) (void)hipFree(c->arena);
 	if(c->pin) (void)hipHostFree(c->pin);
+	if(c->pin_dev) (void)hipFree(c->pin_dev);
 	for(hipEvent_t& e : c->mm_ev)
 		if(e) (void)hipEventDestroy(e);
 	if(c->aux) (void)hipStreamDestroy(c->aux);
@@ -685,7 +705,10 @@ static int one_mm_impl(bt2g_ctx* c, const uint8_t* reads, const uint8_t* quals, 
 	HIPCHK(amalloc(c, (void**)&s.near_dep, sizeof(uint32_t) * (size_t)n * 4, st));
 	// far-half branches queued for the branch kernel (16 per read: an item that
 	// meets a full queue is redone whole by the in-place state machine)
-	const uint32_t brq_cap = n * 16 + 1024;
+	// ($BT2G_MM_BRQ_CAP: a smaller queue, for the tests of the overflow paths)
+	uint32_t brq_cap = n * 16 + 1024;
+	if(const char* e = getenv("BT2G_MM_BRQ_CAP"))
+		if(atol(e) > 0 && (uint32_t)atol(e) < brq_cap) brq_cap = (uint32_t)atol(e);
 	HIPCHK(amalloc(c, (void**)&s.brq, sizeof(MmBranch) * (size_t)brq_cap, st));
 	HIPCHK(amalloc(c, (void**)&s.fb_items, sizeof(uint32_t) * (size_t)n * 4, st));
 	HIPCHK(amalloc(c, (void**)&s.fb_st4, sizeof(uint4) * (size_t)n * 4, st));
@@ -1130,32 +1153,65 @@ int bt2g_reserve_sw(bt2g_ctx* c, uint32_t max_problems, uint32_t max_cols) {
 
 // ------------------------------------------------------ host-pointer wrappers
 namespace {
-// Device copies of a host-flavour call's arrays, in the context's arena (the
-// Arena scope also covers the scratch of the device-pointer call it makes).
-// Both directions go through the context's pinned staging, on the context's
-// stream: one stream synchronisation per call (finish), no null-stream copy
-// that would wait on the other contexts' work.
+// Device copies of a host-flavour call's arrays.  Inputs are staged in the
+// context's pinned block and placed at the same offsets of its device mirror,
+// so that send() moves them all in ONE copy; outputs declared with out() get a
+// slot in the same mirror, and finish() brings every one of them back in ONE
+// copy.  Scratch (up() without host data) comes from the arena.  Everything on
+// the context's stream, one stream synchronisation per finish(): no null-stream
+// copy that would wait on the other contexts' work.  When the pinned block is
+// too small (its first use, or a bigger call) the arrays are copied one by one
+// and the block grows for the next call.
 struct Tmp {
 	Arena ar;
 	bt2g_ctx* c;
 	hipStream_t st;
 	struct Out { void* h; const void* pin; size_t n; };
 	std::vector<Out> outs;
+	size_t sent = 0;                      // pinned bytes already on the device
+	size_t mo_lo = SIZE_MAX, mo_hi = 0;   // mirrored outputs still to bring back
+	bool pending = false;                 // staged inputs not yet sent
 	explicit Tmp(bt2g_ctx* cx) : ar(cx), c(cx), st(cx->stream) {}
 	template <typename T>
 	int up(T** d, const T* h, size_t count) {
 		const size_t bytes = count * sizeof(T);
+		// (pinned() also records the size the block needs: it grows for the next call)
+		if(uint8_t* pn = h && count ? ar.pinned(bytes) : nullptr) {
+			memcpy(pn, h, bytes);
+			*d = (T*)(c->pin_dev + (pn - c->pin));
+			pending = true;
+			return BT2G_OK;
+		}
 		if(amalloc(c, (void**)d, bytes + 16, st) != hipSuccess)
 			return fail(BT2G_ERR_NOMEM, "device scratch (%zu bytes)", bytes + 16);
-		if(h && count) {
-			const void* src = h;
-			if(uint8_t* pn = ar.pinned(bytes)) {
-				memcpy(pn, h, bytes);
-				src = pn;
-			}
-			if(hipMemcpyAsync(*d, src, bytes, hipMemcpyHostToDevice, st) != hipSuccess)
-				return fail(BT2G_ERR_HIP, "hipMemcpyAsync H2D");
+		if(h && count && hipMemcpyAsync(*d, h, bytes, hipMemcpyHostToDevice, st) != hipSuccess)
+			return fail(BT2G_ERR_HIP, "hipMemcpyAsync H2D");
+		return BT2G_OK;
+	}
+	// the staged inputs to the device (before the first launch that reads them)
+	int send() {
+		if(c->pin_used > sent) {
+			HIPCHK(hipMemcpyAsync(c->pin_dev + sent, c->pin + sent, c->pin_used - sent, hipMemcpyHostToDevice, st));
+			sent = c->pin_used;
 		}
+		pending = false;
+		return BT2G_OK;
+	}
+	// a device output that finish() copies to h (`count` elements)
+	template <typename T>
+	int out(T** d, T* h, size_t count) {
+		const size_t bytes = count * sizeof(T);
+		uint8_t* pn = bytes ? ar.pinned(bytes) : nullptr;
+		if(!pn) {
+			int rc = up(d, (const T*)nullptr, count);
+			if(rc == BT2G_OK && bytes) rc = down(h, *d, count);
+			return rc;
+		}
+		*d = (T*)(c->pin_dev + (pn - c->pin));
+		const size_t o = (size_t)(pn - c->pin);
+		mo_lo = std::min(mo_lo, o);
+		mo_hi = std::max(mo_hi, o + bytes);
+		outs.push_back(Out{h, pn, bytes});
 		return BT2G_OK;
 	}
 	// enqueue a result copy (valid after finish)
@@ -1169,6 +1225,12 @@ struct Tmp {
 		return BT2G_OK;
 	}
 	int finish() {
+		if(pending) return fail(BT2G_ERR_ARG, "internal: inputs staged but never sent");
+		if(mo_hi > mo_lo) {
+			HIPCHK(hipMemcpyAsync(c->pin + mo_lo, c->pin_dev + mo_lo, mo_hi - mo_lo, hipMemcpyDeviceToHost, st));
+			mo_lo = SIZE_MAX;
+			mo_hi = 0;
+		}
 		HIPCHK(stream_wait(c, st));
 		for(const Out& o : outs) memcpy(o.h, o.pin, o.n);
 		outs.clear();
@@ -1188,10 +1250,9 @@ int bt2g_exact_sweep(bt2g_ctx* c, const uint8_t* reads, uint32_t stride, const u
 	uint32_t *dl, *dout;
 	int rc;
 	if((rc = t.up(&dr, reads, (size_t)n * stride)) || (rc = t.up(&dl, lens, n)) ||
-	   (rc = t.up(&dout, (const uint32_t*)nullptr, (size_t)n * 8)))
+	   (rc = t.out(&dout, out, (size_t)n * 8)) || (rc = t.send()))
 		return rc;
 	if((rc = bt2g_exact_sweep_dev(c, dr, stride, dl, n, mine_max, nofw, norc, dout, c->stream))) return rc;
-	if((rc = t.down(out, dout, (size_t)n * 8))) return rc;
 	return t.finish();
 }
 
@@ -1206,16 +1267,14 @@ int bt2g_seed_search(bt2g_ctx* c, const uint8_t* reads, uint32_t stride, const u
 	int32_t* dns;
 	int rc;
 	size_t no = (size_t)n * 2 * maxseeds * 4;
-	if((rc = t.up(&dr, reads, (size_t)n * stride)) || (rc = t.up(&dl, lens, n)) ||
-	   (rc = t.up(&dout, (const uint32_t*)nullptr, no)) || (rc = t.up(&dns, (const int32_t*)nullptr, n)) ||
-	   (rc = t.up(&dops, (const uint32_t*)nullptr, n)))
+	if((rc = t.up(&dr, reads, (size_t)n * stride)) || (rc = t.up(&dl, lens, n)) || (rc = t.out(&dout, out, no)) ||
+	   (rc = t.out(&dns, nseeds, n)) || (rc = t.out(&dops, bwops, n)))
 		return rc;
-	if(loads && (rc = t.up(&dld, (const uint32_t*)nullptr, n))) return rc;
+	if(loads && (rc = t.out(&dld, loads, n))) return rc;
+	if((rc = t.send())) return rc;
 	if((rc = bt2g_seed_search_dev(c, dr, stride, dl, n, seedlen, interval, offset, maxseeds, dout, dns, dops, dld,
 	                              c->stream)))
 		return rc;
-	if((rc = t.down(out, dout, no)) || (rc = t.down(nseeds, dns, n)) || (rc = t.down(bwops, dops, n))) return rc;
-	if(loads && (rc = t.down(loads, dld, n))) return rc;
 	return t.finish();
 }
 
@@ -1231,18 +1290,15 @@ int bt2g_one_mm(bt2g_ctx* c, const uint8_t* reads, const uint8_t* quals, uint32_
 	bt2g_mm1* dh;
 	int rc;
 	if((rc = t.up(&dr, reads, (size_t)n * stride)) || (rc = t.up(&dq, quals, (size_t)n * stride)) ||
-	   (rc = t.up(&dl, lens, n)) || (rc = t.up(&dms, minsc, n)) ||
-	   (rc = t.up(&dh, (const bt2g_mm1*)nullptr, (size_t)n * cap)) ||
-	   (rc = t.up(&dcnt, (const int32_t*)nullptr, n)) || (rc = t.up(&dops, (const uint32_t*)nullptr, n)))
+	   (rc = t.up(&dl, lens, n)) || (rc = t.up(&dms, minsc, n)) || (rc = t.out(&dh, hits, (size_t)n * cap)) ||
+	   (rc = t.out(&dcnt, counts, n)) || (rc = t.out(&dops, bwops, n)))
 		return rc;
-	if(loads && (rc = t.up(&dld, (const uint32_t*)nullptr, n))) return rc;
+	if(loads && (rc = t.out(&dld, loads, n))) return rc;
+	if((rc = t.send())) return rc;
 	// (the overflow shows in the counts copied back: no sync of its own)
 	if((rc = one_mm_impl(c, dr, dq, stride, dl, n, dms, sc, nofw, norc, nullptr, cap, dh, dcnt, dops, dld, c->stream,
 	                     false)))
 		return rc;
-	if((rc = t.down(hits, dh, (size_t)n * cap)) || (rc = t.down(counts, dcnt, n)) || (rc = t.down(bwops, dops, n)))
-		return rc;
-	if(loads && (rc = t.down(loads, dld, n))) return rc;
 	if((rc = t.finish())) return rc;
 	for(uint32_t i = 0; i < n; i++)
 		if(counts[i] > (int32_t)cap) return fail(BT2G_ERR_OVERFLOW, "one-mismatch hits exceed cap %u", cap);
@@ -1267,10 +1323,9 @@ int bt2g_extend(bt2g_ctx* c, const uint8_t* reads, uint32_t stride, const uint32
 	bt2g_ext_out* dout;
 	int rc;
 	if((rc = t.up(&dr, reads, (size_t)nreads * stride)) || (rc = t.up(&dl, lens, nreads)) || (rc = t.up(&din, in, n)) ||
-	   (rc = t.up(&dout, (const bt2g_ext_out*)nullptr, n)))
+	   (rc = t.out(&dout, out, n)) || (rc = t.send()))
 		return rc;
 	if((rc = bt2g_extend_dev(c, dr, stride, dl, din, n, dout, c->stream))) return rc;
-	if((rc = t.down(out, dout, n))) return rc;
 	return t.finish();
 }
 
@@ -1280,11 +1335,10 @@ int bt2g_get_offset(bt2g_ctx* c, const uint32_t* rows, uint32_t n, uint32_t* off
 	Tmp t(c);
 	uint32_t *drow, *doff, *dld = nullptr;
 	int rc;
-	if((rc = t.up(&drow, rows, n)) || (rc = t.up(&doff, (const uint32_t*)nullptr, n))) return rc;
-	if(loads && (rc = t.up(&dld, (const uint32_t*)nullptr, n))) return rc;
+	if((rc = t.up(&drow, rows, n)) || (rc = t.out(&doff, offs, n))) return rc;
+	if(loads && (rc = t.out(&dld, loads, n))) return rc;
+	if((rc = t.send())) return rc;
 	if((rc = bt2g_get_offset_dev(c, drow, n, doff, dld, c->stream))) return rc;
-	if((rc = t.down(offs, doff, n))) return rc;
-	if(loads && (rc = t.down(loads, dld, n))) return rc;
 	return t.finish();
 }
 
@@ -1312,14 +1366,16 @@ int bt2g_sw_align(bt2g_ctx* c, const uint8_t* reads, const uint8_t* quals, uint3
 	   (rc = t.up(&dc, (const bt2g_sw_cand*)nullptr, (size_t)nprob * cap)))
 		return rc;
 	if(windows && windows_len && (rc = t.up(&dw, windows, windows_len))) return rc;
+	if(mat && (rc = t.up(&dmo, mat_off, nprob))) return rc;
 	size_t matn = 0;
 	if(mat) {
 		for(uint32_t i = 0; i < nprob; i++) {
 			size_t e = mat_off[i] + (size_t)lens[probs[i].read] * probs[i].ncol * 3;
 			matn = e > matn ? e : matn;
 		}
-		if((rc = t.up(&dm, (const int16_t*)nullptr, matn)) || (rc = t.up(&dmo, mat_off, nprob))) return rc;
+		if((rc = t.up(&dm, (const int16_t*)nullptr, matn))) return rc;
 	}
+	if((rc = t.send())) return rc;
 	if((rc = bt2g_sw_align_dev(c, dr, dq, stride, dl, dp, nprob, dw, sc, enable8, cap, dres, dc, dm, dmo, c->stream)))
 		return rc;
 	if((rc = t.down(res, dres, nprob)) || (rc = t.down(cands, dc, (size_t)nprob * cap))) return rc;
@@ -1368,6 +1424,7 @@ int bt2g_sw_align_bt(bt2g_ctx* c, const uint8_t* reads, const uint8_t* quals, ui
 	if(windows && windows_len && (rc = t.up(&dw, windows, windows_len))) return rc;
 	if(rects && (rc = t.up(&drc, rects, nprob))) return rc;
 	if(fates && (rc = t.up(&dft, (const int8_t*)nullptr, (size_t)nprob * cap))) return rc;
+	if((rc = t.send())) return rc;
 	const SwHint hint = sw_hint(probs, nprob, lens, enable8);
 	if((rc = sw_align_bt_impl(c, dr, dq, stride, dl, dp, nprob, dw, drc, sc, enable8, cap, dres, dc, maxaln, maxedit,
 	                          dna, dal, ded, dft, c->stream, &hint)))
@@ -1409,32 +1466,31 @@ int bt2g_sw_align_bt_packed(bt2g_ctx* c, const uint8_t* reads, const uint8_t* qu
 	int8_t *dft = nullptr, *dpf = nullptr;
 	int rc;
 	const size_t na = (size_t)nprob * maxaln;
+	uint32_t tot[3];
 	if((rc = t.up(&dr, reads, (size_t)nreads * stride)) || (rc = t.up(&dq, quals, (size_t)nreads * stride)) ||
-	   (rc = t.up(&dl, lens, nreads)) || (rc = t.up(&dp, probs, nprob)) ||
-	   (rc = t.up(&dres, (const bt2g_sw_result*)nullptr, nprob)) ||
+	   (rc = t.up(&dl, lens, nreads)) || (rc = t.up(&dp, probs, nprob)))
+		return rc;
+	if(windows && windows_len && (rc = t.up(&dw, windows, windows_len))) return rc;
+	if(rects && (rc = t.up(&drc, rects, nprob))) return rc;
+	if((rc = t.out(&dres, res, nprob)) || (rc = t.out(&dna, naln, nprob)) || (rc = t.out(&dal, alns, na)) ||
 	   (rc = t.up(&dc, (const bt2g_sw_cand*)nullptr, (size_t)nprob * cap)) ||
-	   (rc = t.up(&dna, (const int32_t*)nullptr, nprob)) || (rc = t.up(&dal, (const bt2g_sw_aln*)nullptr, na)) ||
 	   (rc = t.up(&ded, (const bt2g_edit*)nullptr, na * maxedit)) ||
 	   (rc = t.up(&dcnt, (const uint32_t*)nullptr, 3 * (size_t)nprob)) ||
 	   (rc = t.up(&doff, (const uint32_t*)nullptr, 3 * (size_t)nprob + 3)) ||
 	   (rc = t.up(&dpc, (const bt2g_sw_cand*)nullptr, (size_t)nprob * cap)) ||
 	   (rc = t.up(&dpe, (const bt2g_edit*)nullptr, na * maxedit)))
 		return rc;
-	if(windows && windows_len && (rc = t.up(&dw, windows, windows_len))) return rc;
-	if(rects && (rc = t.up(&drc, rects, nprob))) return rc;
 	if(fates && ((rc = t.up(&dft, (const int8_t*)nullptr, (size_t)nprob * cap)) ||
 	             (rc = t.up(&dpf, (const int8_t*)nullptr, (size_t)nprob * cap))))
 		return rc;
+	if((rc = t.send())) return rc;
 	const SwHint hint = sw_hint(probs, nprob, lens, enable8);
 	if((rc = sw_align_bt_impl(c, dr, dq, stride, dl, dp, nprob, dw, drc, sc, enable8, cap, dres, dc, maxaln, maxedit,
 	                          dna, dal, ded, dft, c->stream, &hint)))
 		return rc;
 	launch_sw_pack(dres, dna, dal, dc, dft, ded, nprob, cap, maxaln, maxedit, dcnt, doff, dpc, dpf, dpe, c->stream);
 	HIPCHK(hipGetLastError());
-	uint32_t tot[3];
-	if((rc = t.down(res, dres, nprob)) || (rc = t.down(naln, dna, nprob)) || (rc = t.down(alns, dal, na)) ||
-	   (rc = t.down(tot, doff + 3 * (size_t)nprob, 3)))
-		return rc;
+	if((rc = t.down(tot, doff + 3 * (size_t)nprob, 3))) return rc;
 	if((rc = t.finish())) return rc;
 	if((rc = t.down(cands, dpc, tot[0])) || (fates && (rc = t.down(fates, dpf, tot[0]))) ||
 	   (rc = t.down(edits, dpe, tot[2])))
@@ -1471,11 +1527,10 @@ int bt2g_frame(bt2g_ctx* c, const bt2g_frame_in* in, uint32_t n, const uint32_t*
 	bt2g_sw_rect* dr;
 	int32_t* dok;
 	int rc;
-	if((rc = t.up(&din, in, n)) || (rc = t.up(&dl, lens, nreads)) || (rc = t.up(&dp, (const bt2g_sw_problem*)nullptr, n)) ||
-	   (rc = t.up(&dr, (const bt2g_sw_rect*)nullptr, n)) || (rc = t.up(&dok, (const int32_t*)nullptr, n)))
+	if((rc = t.up(&din, in, n)) || (rc = t.up(&dl, lens, nreads)) || (rc = t.out(&dp, probs, n)) ||
+	   (rc = t.out(&dr, rects, n)) || (rc = t.out(&dok, ok, n)) || (rc = t.send()))
 		return rc;
 	if((rc = bt2g_frame_dev(c, din, n, dl, sc, pe, maxhalf, trim_to_ref, dp, dr, dok, c->stream))) return rc;
-	if((rc = t.down(probs, dp, n)) || (rc = t.down(rects, dr, n)) || (rc = t.down(ok, dok, n))) return rc;
 	return t.finish();
 }
 
@@ -1495,12 +1550,10 @@ int bt2g_ungapped(bt2g_ctx* c, const uint8_t* reads, const uint8_t* quals, uint3
 	bt2g_edit* ded;
 	int rc;
 	if((rc = t.up(&dr, reads, (size_t)nreads * stride)) || (rc = t.up(&dq, quals, (size_t)nreads * stride)) ||
-	   (rc = t.up(&dl, lens, nreads)) || (rc = t.up(&dp, probs, n)) ||
-	   (rc = t.up(&dres, (const bt2g_ug_result*)nullptr, n)) ||
-	   (rc = t.up(&ded, (const bt2g_edit*)nullptr, (size_t)n * maxedit)))
+	   (rc = t.up(&dl, lens, nreads)) || (rc = t.up(&dp, probs, n)) || (rc = t.out(&dres, res, n)) ||
+	   (rc = t.out(&ded, edits, (size_t)n * maxedit)) || (rc = t.send()))
 		return rc;
 	if((rc = bt2g_ungapped_dev(c, dr, dq, stride, dl, dp, n, sc, ohang, maxedit, dres, ded, c->stream))) return rc;
-	if((rc = t.down(res, dres, n)) || (rc = t.down(edits, ded, (size_t)n * maxedit))) return rc;
 	return t.finish();
 }
 

@@ -617,6 +617,10 @@ k_one_mm_far(DevEbwt F, DevEbwt B, const uint8_t* __restrict__ reads, const uint
 		if(!(bot > top && match && dep != len - 1)) break;
 		dep++;
 	}
+	// a lane that met the full queue claims its item before the flush, so the
+	// flush skips the item's staged entries (their slot flag is set) and the
+	// item reaches the state machine's list exactly once (below)
+	const bool claimed = handed && atomicExch(&slot_flag[slot], 1u) == 0u;
 	// flush the wave's staged branches (every lane still running is here)
 	bool overflow = false;
 	{
@@ -648,12 +652,14 @@ k_one_mm_far(DevEbwt F, DevEbwt B, const uint8_t* __restrict__ reads, const uint
 	}
 	if(overflow && !handed && atomicAdd(&slot_flag[slot], 0u)) return;   // redone by the state machine
 	if(handed) {
-		// queue full: the whole item goes to the in-place state machine
-		slot_flag[slot] = 1u;
-		const uint32_t f = wave_alloc1(fb_n);
-		fb_items[f] = item;
-		fb_st4[f] = q4;
-		fb_sdep[f] = sd;
+		// queue full: the whole item goes to the in-place state machine (unless the
+		// flush of another lane's entries already sent it there)
+		if(claimed) {
+			const uint32_t f = wave_alloc1(fb_n);
+			fb_items[f] = item;
+			fb_st4[f] = q4;
+			fb_sdep[f] = sd;
+		}
 		return;
 	}
 	slot_counts[slot] = nh;

@@ -96,10 +96,12 @@ int bt2g_open(const char* index_base, int device, bt2g_ctx** out);
 /* Same from arrays already in host memory. */
 int bt2g_open_mem(const bt2g_index_mem* m, int device, bt2g_ctx** out);
 /* A second context on `base`'s device and index: its own stream and scratch,
- * no second copy of the index.  Every such context is closed before `base`.
+ * no second copy of the index.  Every such context is closed before `base`:
+ * bt2g_close(base) fails with BT2G_ERR_ARG while one is open.
  * Contexts are not thread-safe; one thread drives each (the drop-in binding
  * gives every dispatcher thread its own, integration/bt2g_seams.cpp). */
 int bt2g_open_shared(bt2g_ctx* base, bt2g_ctx** out);
+/* Release a context (a shared one first, then the index owner). */
 int bt2g_close(bt2g_ctx* ctx);
 /* out: [len, zoff_fw, zoff_bw, fchr0..4, ftab_chars, off_rate, num_sides,
  *       nref, hbm_bytes]  (n <= 13 words written) */

@@ -1349,6 +1349,10 @@ void GroupWalk2S<TSlice, 16>::init(const Ebwt& ebwtFw, const BitPairReference& r
 	(void)ebwtFw; (void)ref; (void)rnd; (void)met;
 	reset();
 	elt_ += sa.size();
+	// the range's offset slots as the cache would hold them before any walk
+	// (AlignmentCache::addOnTheFlyImpl above only reserves them); rows resolved
+	// earlier in this read are resolved again, to the same offsets
+	for(size_t j = 0; j < sa.size(); j++) sa.offs[j] = OFF_MASK;
 	if(t_gw.on) t_gw.ranges.push_back(GwRange{sa.topf, sa.size(), sa.offs});
 }
 
@@ -1451,23 +1455,30 @@ void SwDriver::extend(const Read& rd, const Ebwt& ebwtFw, const Ebwt* ebwtBw, TI
 // ---- AlignmentCache::addOnTheFlyImpl (aligner_cache.cpp:55-104) ---------------
 // Registers a seed hit's SA range in the current-read cache and appends one
 // OFF_MASK offset slot per row to salist_ -- one PList::add per row in the
-// reference, i.e. a function call and a capacity check per element; on an
-// hg38-scale genome a seed in a repeat family has a range of 10^5 rows, and
-// this loop was 18 % of the drop-in's host CPU (r03f).  Restated here with the
-// same result, pool use and failure point: PList::add for the first slot of
-// every page (which takes the page from the pool, or fails exactly where the
-// reference's loop fails), plain stores for the rest of the page.
+// reference; on an hg38-scale genome a seed in a repeat family has a range of
+// 10^5 rows, and every worker's 20 MB pool gets written (r03f: the loop was
+// 18 % of the drop-in's host CPU; r03h at 3.1 Gbp: its page-wise restatement's
+// fill still 12.5 %, page faults included, and 38 GB resident over 2 048
+// workers).  The slots' contents are read by GroupWalk2S alone (group_walk.h:
+// 368-372, 508), whose init / advanceElement the binding specialises: init
+// writes OFF_MASK over exactly the rows of the range it is handed (below), so
+// here the slots are only reserved.  Reserving keeps the reference's pool use
+// and failure point: PList::ensure(pool, 1) wherever the reference's add() of
+// that row would take a page (or fail), the rest of the page by the count.
 namespace {
 struct TSAListFill : public PList<TIndexOffU, CACHE_PAGE_SZ> {
-	// n copies of v, as n calls of add(p, v): returns how many were added
-	size_t add_fill(Pool& p, size_t n, TIndexOffU v) {
+	// the effect of n calls of add(p, v) on the pool and the list's length,
+	// without writing the slots: returns how many were added
+	size_t reserve(Pool& p, size_t n) {
 		const size_t per = (size_t)CACHE_PAGE_SZ / sizeof(TIndexOffU);
 		size_t done = 0;
 		while(done < n) {
-			if(!add(p, v)) return done;
-			done++;
+			if(!ensure(p, 1)) return done;
+			if(cur_ == per) {
+				cur_ = 0;
+				curPage_++;
+			}
 			const size_t k = std::min(per - cur_, n - done);
-			std::fill(pages_[curPage_] + cur_, pages_[curPage_] + cur_ + k, v);
 			cur_ += k;
 			done += k;
 		}
@@ -1491,7 +1502,7 @@ bool AlignmentCache::addOnTheFlyImpl(QVal& qv, const SAKey& sak, TIndexOffU topf
 		s->payload.topf = topf;
 		s->payload.topb = topb;
 		const size_t n = botf - topf;
-		const size_t k = static_cast<TSAListFill&>(salist_).add_fill(pool(), n, OFF_MASK);
+		const size_t k = static_cast<TSAListFill&>(salist_).reserve(pool(), n);
 		if(k < n) {
 			s->payload.len = (TIndexOffU)k;
 			return false;

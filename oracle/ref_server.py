@@ -36,6 +36,20 @@ CLIENT = os.path.join(REF_DIR, "bowtie2-align-l")
 CHUNK = 10_000
 
 
+def dropin_env(index_base, stats_path=None, device=0):
+    """Environment of the drop-in server (integration/): the index its engines
+    open, where the binding writes its call counts, and one HIP hardware queue
+    per stream -- the binding drives ~20 streams (a context per seam
+    dispatcher), and with HIP's default of 4 hardware queues a 0.07 ms kernel
+    waits behind other seams' kernels on a shared queue (r03h: ~2 ms of every
+    engine call).  GPU_MAX_HW_QUEUES from the caller's environment wins."""
+    env = {"BT2G_INDEX": index_base, "BT2G_DEVICE": str(device),
+           "GPU_MAX_HW_QUEUES": os.environ.get("GPU_MAX_HW_QUEUES", "24")}
+    if stats_path:
+        env["BT2G_ADAPTER_STATS"] = stats_path
+    return env
+
+
 def free_port():
     s = socket.socket()
     s.bind(("127.0.0.1", 0))

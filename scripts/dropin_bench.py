@@ -79,7 +79,7 @@ def main():
     runs.append(("dropin", a.dropin_binary or os.path.join(rs.REF_DIR, "bowtie2-align-server-gpu"), a.gpu_workers))
     for tag, binary, th in runs:
         stats = os.path.join(a.workdir, f"stats_{tag}.json")
-        env = {"BT2G_INDEX": base, "BT2G_ADAPTER_STATS": stats, "BT2G_DEVICE": "0"}
+        env = rs.dropin_env(base, stats)
         with rs.Server(base, threads=th, args=a.args, binary=binary, env=env,
                        log_path=os.path.join(a.workdir, f"server_{tag}.log")) as s:
             log(f"{tag}: server ready in {s.load_s:.1f}s (-p {th})")

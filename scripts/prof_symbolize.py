@@ -5,7 +5,18 @@
 """
 import argparse
 import collections
+import os
 import subprocess
+
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def local(path):
+    """A GPU box's path of a repository file, mapped into this checkout."""
+    if os.path.exists(path) or "/repo/" not in path:
+        return path
+    return os.path.join(ROOT, path.split("/repo/", 1)[1])
 
 
 def load_segments(path):
@@ -31,11 +42,15 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("dump")
     ap.add_argument("--top", type=int, default=40)
+    ap.add_argument("--role", type=int, default=0, help="only samples of this thread role (1 carrier, "
+                    "2 dispatcher), from the (pc, [rsp]) pair table")
     ap.add_argument("--callers-of", default="", help="function name: list the callers of its samples "
                     "(from the (pc, [rsp]) pairs; meaningful for frameless leaves such as syscall wrappers)")
     a = ap.parse_args()
     if a.callers_of:
         return callers(a)
+    if a.role:
+        return by_role(a)
     by_path = collections.defaultdict(list)
     total = 0
     for ln in open(a.dump):
@@ -50,9 +65,9 @@ def main():
             for _, c in items:
                 funcs[p] += c
             continue
-        segs = load_segments(p)
+        segs = load_segments(local(p))
         addrs = [hex(to_vaddr(segs, o)) for o, _ in items]
-        out = subprocess.run(["addr2line", "-f", "-C", "-e", p] + addrs, stdout=subprocess.PIPE,
+        out = subprocess.run(["addr2line", "-f", "-C", "-e", local(p)] + addrs, stdout=subprocess.PIPE,
                              stderr=subprocess.DEVNULL, text=True).stdout.splitlines()
         names = out[0::2]
         lib = p.rsplit("/", 1)[-1]
@@ -75,12 +90,29 @@ def symbolize(pairs):
             for o in offs:
                 out[(p, o)] = p
             continue
-        segs = load_segments(p)
-        res = subprocess.run(["addr2line", "-f", "-C", "-e", p] + [hex(to_vaddr(segs, o)) for o in offs],
+        segs = load_segments(local(p))
+        res = subprocess.run(["addr2line", "-f", "-C", "-e", local(p)] + [hex(to_vaddr(segs, o)) for o in offs],
                              stdout=subprocess.PIPE, stderr=subprocess.DEVNULL, text=True).stdout.splitlines()
         for o, nm in zip(offs, res[0::2]):
             out[(p, o)] = f"{nm[:100]} [{p.rsplit('/', 1)[-1]}]"
     return out
+
+
+def by_role(a):
+    rows = []
+    for ln in open(a.dump):
+        if ln.startswith("#pair "):
+            f = ln.split()
+            if len(f) > 6 and int(f[6]) == a.role:
+                rows.append(((f[1], int(f[2], 16)), int(f[5])))
+    names = symbolize([r[0] for r in rows])
+    cnt = collections.Counter()
+    for pc, c in rows:
+        cnt[names[pc]] += c
+    tot = sum(cnt.values())
+    print(f"{tot} samples of role {a.role}")
+    for nm, c in cnt.most_common(a.top):
+        print(f"{100.0 * c / max(tot, 1):6.2f}%  {c:7d}  {nm}")
 
 
 def callers(a):

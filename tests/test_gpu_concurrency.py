@@ -36,13 +36,14 @@ def test_shared_contexts_threads_match_serial():
     lens = np.full(n, 150, np.uint32)
     minsc = np.full(n, -60, np.int32)
     base = bt2g.Engine(index=idx)
+    engines = []
     try:
         # batches of ragged sizes, as the dispatchers form them
         rng = np.random.default_rng(5)
         cuts = np.unique(np.concatenate([[0, n], rng.integers(1, n, 40)]))
         slices = [slice(int(a), int(b)) for a, b in zip(cuts[:-1], cuts[1:])]
         want = [_work(base, reads, quals, lens, minsc, sl) for sl in slices]
-        engines = [base.shared() for _ in range(6)]
+        engines += [base.shared() for _ in range(6)]
         got = [None] * (len(slices) * len(engines))
         errs = []
 
@@ -66,7 +67,25 @@ def test_shared_contexts_threads_match_serial():
                 assert g is not None, (t, k)
                 for a, b in zip(g, w):
                     assert np.array_equal(a, b), (t, k)
+    finally:
         for e in engines:
             e.close()
-    finally:
         base.close()
+
+
+def test_shared_context_close_order():
+    """A shared context reports the index's HBM bytes, and the index owner cannot
+    be closed while a shared context still uses its index."""
+    import bt2g
+    base = bt2g.Engine(index=get_index("lambda"))
+    sh = base.shared()
+    try:
+        assert sh.info()[12] == base.info()[12] > 0
+        with pytest.raises(bt2g.Bt2gError):
+            base.close()
+        assert base.h                               # still open and usable
+        assert base.info()[0] == sh.info()[0]
+    finally:
+        sh.close()
+        base.close()
+    assert not base.h

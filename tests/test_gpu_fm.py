@@ -114,6 +114,23 @@ def test_large_batch_vs_oracle(engines, orc):
                 tuple(int(v) for v in h_cpu[i, k])
 
 
+@pytest.mark.parametrize("brq_cap", [1, 7, 64])
+def test_one_mm_branch_queue_overflow(engines, brq_cap, monkeypatch):
+    """A branch queue far too small for the batch ($BT2G_MM_BRQ_CAP): items whose
+    branches do not fit go to the in-place state machine, each exactly once, so
+    hits, counts and bwops equal the normal path's (a lane that met
+    the full queue while its wave's flush also overflowed was queued twice)."""
+    g = load_golden("fm_synth")
+    e = engines["synth"]
+    args = (g["reads"], g["quals"], g["lens"], g["mmminsc_ee"], False)
+    h0, c0, o0, _ = e.one_mm(*args)
+    monkeypatch.setenv("BT2G_MM_BRQ_CAP", str(brq_cap))
+    h1, c1, o1, _ = e.one_mm(*args)
+    assert np.array_equal(c0, c1) and np.array_equal(o0, o1)
+    for i in np.nonzero(c0)[0]:
+        assert np.array_equal(h0[i, :c0[i]], h1[i, :c0[i]]), i
+
+
 def test_open_from_files_and_edge_cases(tmp_path):
     import bt2g
     import bt2_index as bi

@@ -73,7 +73,7 @@ def _reads(idx, mode, n, seed, dirpath):
 
 def _run(binary, base, chunks, args, dirpath, tag):
     stats = os.path.join(dirpath, f"stats_{tag}.json")
-    env = {"BT2G_INDEX": base, "BT2G_ADAPTER_STATS": stats, "BT2G_DEVICE": "0"}
+    env = rs.dropin_env(base, stats)
     with rs.Server(base, threads=2, args=args, binary=binary, env=env,
                    log_path=os.path.join(dirpath, f"server_{tag}.log")) as s:
         dt, outs = s.run(chunks, k=2)
