@@ -517,18 +517,32 @@ def real_schedule(cpu):
             "stock_cores": r.get("cores"), "sample": r.get("sample")}
 
 
-def combine_ranks(elapsed, n_aligned, dev):
+def combine_ranks(elapsed, n_aligned, dev, eng=None):
     """Max of the per-rank times, sum of the aligned-read counters: the path's
-    only collective (RCCL on the GPUs, gloo in the CPU tests)."""
+    only collective.  On the GPUs the counters go through the
+    engines' own RCCL all-reduce (bt2g_allreduce_counts, communicator from
+    comm_setup); the max of the times, a harness figure, through torch.distributed
+    (RCCL); in the CPU tests both through gloo."""
     import torch
     import torch.distributed as dist
     if not (dist.is_available() and dist.is_initialized()) or dist.get_world_size() == 1:
         return elapsed, n_aligned
     el = torch.tensor([elapsed], dtype=torch.float64, device=dev)
-    na = torch.tensor([float(n_aligned)], dtype=torch.float64, device=dev)
     dist.all_reduce(el, op=dist.ReduceOp.MAX)
+    if eng is not None:
+        return float(el[0]), int(eng.allreduce_counts([n_aligned])[0])
+    na = torch.tensor([float(n_aligned)], dtype=torch.float64, device=dev)
     dist.all_reduce(na, op=dist.ReduceOp.SUM)
     return float(el[0]), int(na[0])
+
+
+def comm_setup(eng, rank, world):
+    """The engines' communicator over the ranks: rank 0 makes the RCCL id, the
+    others receive it over torch.distributed, every rank joins (bt2g_comm_init)."""
+    import torch.distributed as dist
+    obj = [eng.comm_unique_id() if rank == 0 else None]
+    dist.broadcast_object_list(obj, src=0)
+    eng.comm_init(world, rank, obj[0])
 
 
 def shard_seed(rank):
@@ -919,6 +933,8 @@ def main():
     log(f"[rank {rank}] index built on GPU in {time.time()-t1:.1f}s")
     torch.cuda.empty_cache()
     eng = bt2g.Engine(index=idx, device=local)
+    if world > 1:
+        comm_setup(eng, rank, world)
     info = eng.info()
     t2 = time.time()
     if args.mode == "paired":
@@ -953,7 +969,7 @@ def main():
         e.set_profiling(False)
     stats = {k: eng.kernel_stats(k) for k in range(6)}
     mstats = {k: pipe.eng2.kernel_stats(k) for k in (4, 5, 7)} if args.mode == "paired" else {}
-    elapsed, n_aligned = combine_ranks(elapsed, n_aligned, dev)
+    elapsed, n_aligned = combine_ranks(elapsed, n_aligned, dev, eng if world > 1 else None)
     total_reads = args.reads * args.steps * world
     value = total_reads / elapsed
 

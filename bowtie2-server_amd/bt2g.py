@@ -141,6 +141,9 @@ def lib():
         L.bt2g_set_profiling.argtypes = [vp, C.c_int]
         L.bt2g_kernel_stats.argtypes = [vp, C.c_int, C.POINTER(u64), C.POINTER(C.c_double)]
         L.bt2g_reset_stats.argtypes = [vp]
+        L.bt2g_comm_unique_id.argtypes = [vp]
+        L.bt2g_comm_init.argtypes = [vp, C.c_int, C.c_int, vp]
+        L.bt2g_allreduce_counts.argtypes = [vp, vp, u32]
         _lib = L
     return _lib
 
@@ -204,6 +207,24 @@ class Engine:
         e.h = C.c_void_p()
         _chk(lib().bt2g_open_shared(self.h, C.byref(e.h)))
         return e
+
+    # ---- multi-GPU: the ranks' one collective (RCCL) -----------------------
+    @staticmethod
+    def comm_unique_id():
+        """A communicator id (bytes) for comm_init; made by one rank, sent to the others."""
+        buf = (C.c_uint8 * 128)()
+        _chk(lib().bt2g_comm_unique_id(C.cast(buf, C.c_void_p)))
+        return bytes(buf)
+
+    def comm_init(self, nranks, rank, uid):
+        buf = (C.c_uint8 * 128).from_buffer_copy(uid)
+        _chk(lib().bt2g_comm_init(self.h, nranks, rank, C.cast(buf, C.c_void_p)))
+
+    def allreduce_counts(self, counts):
+        """Sum of a u64 counter vector over the ranks of comm_init (collective)."""
+        a = np.ascontiguousarray(np.asarray(counts, dtype=np.uint64)).copy()
+        _chk(lib().bt2g_allreduce_counts(self.h, _ptr(a), len(a)))
+        return a
 
     def close(self):
         if self.h:

@@ -5,6 +5,7 @@
 // host-pointer convenience wrappers.  No exception crosses the ABI; errors are
 // status codes plus a thread-local message (bt2g_last_error).
 #include <atomic>
+#include <dlfcn.h>
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 #include <stdio.h>
@@ -99,6 +100,8 @@ struct bt2g_ctx {
 	uint8_t* pin_dev = nullptr;
 	// $BT2G_SYNC=poll: host waits query an event and sleep between queries
 	hipEvent_t poll_ev = nullptr;
+	// the ranks' communicator (bt2g_comm_init): an RCCL ncclComm_t
+	void* comm = nullptr;
 };
 
 namespace {
@@ -564,6 +567,8 @@ int bt2g_open(const char* index_base, int device, bt2g_ctx** out) {
 	return bt2g_open_mem(&m, device, out);
 }
 
+static int rccl_destroy(void* comm);   // (multi-GPU section below)
+
 int bt2g_close(bt2g_ctx* c) {
 	if(!c) return BT2G_OK;
 	if(c->shares.load() > 0)
@@ -583,6 +588,7 @@ int bt2g_close(bt2g_ctx* c) {
 		if(e) (void)hipEventDestroy(e);
 	if(c->aux) (void)hipStreamDestroy(c->aux);
 	if(c->poll_ev) (void)hipEventDestroy(c->poll_ev);
+	if(c->comm) (void)rccl_destroy(c->comm);
 	if(c->stream) (void)hipStreamDestroy(c->stream);
 	delete c;
 	return BT2G_OK;
@@ -1168,6 +1174,8 @@ struct Tmp {
 	hipStream_t st;
 	struct Out { void* h; const void* pin; size_t n; };
 	std::vector<Out> outs;
+	struct Late { void* h; const void* d; size_t n; };
+	std::vector<Late> late;               // outputs outside the mirror (copied at finish)
 	size_t sent = 0;                      // pinned bytes already on the device
 	size_t mo_lo = SIZE_MAX, mo_hi = 0;   // mirrored outputs still to bring back
 	bool pending = false;                 // staged inputs not yet sent
@@ -1203,8 +1211,10 @@ struct Tmp {
 		const size_t bytes = count * sizeof(T);
 		uint8_t* pn = bytes ? ar.pinned(bytes) : nullptr;
 		if(!pn) {
+			// no mirror slot (the block grows for the next call): arena output, copied
+			// back by finish() after the work that writes it
 			int rc = up(d, (const T*)nullptr, count);
-			if(rc == BT2G_OK && bytes) rc = down(h, *d, count);
+			if(rc == BT2G_OK && bytes) late.push_back(Late{(void*)h, (const void*)*d, bytes});
 			return rc;
 		}
 		*d = (T*)(c->pin_dev + (pn - c->pin));
@@ -1231,6 +1241,8 @@ struct Tmp {
 			mo_lo = SIZE_MAX;
 			mo_hi = 0;
 		}
+		for(const Late& l : late) HIPCHK(hipMemcpyAsync(l.h, l.d, l.n, hipMemcpyDeviceToHost, st));
+		late.clear();
 		HIPCHK(stream_wait(c, st));
 		for(const Out& o : outs) memcpy(o.h, o.pin, o.n);
 		outs.clear();
@@ -1555,6 +1567,93 @@ int bt2g_ungapped(bt2g_ctx* c, const uint8_t* reads, const uint8_t* quals, uint3
 		return rc;
 	if((rc = bt2g_ungapped_dev(c, dr, dq, stride, dl, dp, n, sc, ohang, maxedit, dres, ded, c->stream))) return rc;
 	return t.finish();
+}
+
+}  // extern "C"
+
+// ------------------------------------------------------------- multi-GPU
+// RCCL entry points, resolved from librccl.so.1 on first use (no link-time
+// dependency for the single-GPU path).  Signatures as rccl.h declares them.
+namespace {
+struct Rccl {
+	bool ok = false;
+	int (*get_unique_id)(void* id) = nullptr;
+	void* init_rank = nullptr;
+	int (*all_reduce)(const void*, void*, size_t, int, int, void*, hipStream_t) = nullptr;
+	int (*destroy)(void*) = nullptr;
+	const char* (*err)(int) = nullptr;
+};
+struct Id128 { char b[BT2G_COMM_ID_BYTES]; };
+const int NCCL_UINT64 = 5, NCCL_SUM = 0;     // ncclUint64, ncclSum (rccl.h)
+
+Rccl& rccl() {
+	static Rccl r = [] {
+		Rccl x;
+		void* h = dlopen("librccl.so.1", RTLD_NOW | RTLD_LOCAL);
+		if(!h) h = dlopen("/opt/rocm/lib/librccl.so.1", RTLD_NOW | RTLD_LOCAL);
+		if(!h) return x;
+		x.get_unique_id = (int (*)(void*))dlsym(h, "ncclGetUniqueId");
+		x.init_rank = dlsym(h, "ncclCommInitRank");
+		x.all_reduce = (int (*)(const void*, void*, size_t, int, int, void*, hipStream_t))dlsym(h, "ncclAllReduce");
+		x.destroy = (int (*)(void*))dlsym(h, "ncclCommDestroy");
+		x.err = (const char* (*)(int))dlsym(h, "ncclGetErrorString");
+		x.ok = x.get_unique_id && x.init_rank && x.all_reduce && x.destroy && x.err;
+		return x;
+	}();
+	return r;
+}
+}  // namespace
+
+static int rccl_destroy(void* comm) {
+	Rccl& r = rccl();
+	return r.ok ? r.destroy(comm) : 0;
+}
+
+extern "C" {
+
+int bt2g_comm_unique_id(uint8_t* id) {
+	if(!id) return fail(BT2G_ERR_ARG, "null id");
+	Rccl& r = rccl();
+	if(!r.ok) return fail(BT2G_ERR_HIP, "RCCL (librccl.so.1) not available");
+	if(int e = r.get_unique_id(id)) return fail(BT2G_ERR_HIP, "ncclGetUniqueId: %s", r.err(e));
+	return BT2G_OK;
+}
+
+int bt2g_comm_init(bt2g_ctx* c, int nranks, int rank, const uint8_t* id) {
+	if(!c || !id || nranks < 1 || rank < 0 || rank >= nranks) return fail(BT2G_ERR_ARG, "bad communicator arguments");
+	Rccl& r = rccl();
+	if(!r.ok) return fail(BT2G_ERR_HIP, "RCCL (librccl.so.1) not available");
+	if(c->comm) return fail(BT2G_ERR_ARG, "context already has a communicator");
+	HIPCHK(hipSetDevice(c->device));
+	Id128 uid;
+	memcpy(uid.b, id, BT2G_COMM_ID_BYTES);
+	auto init = (int (*)(void**, int, Id128, int))r.init_rank;
+	if(int e = init(&c->comm, nranks, uid, rank)) {
+		c->comm = nullptr;
+		return fail(BT2G_ERR_HIP, "ncclCommInitRank: %s", r.err(e));
+	}
+	return BT2G_OK;
+}
+
+int bt2g_allreduce_counts(bt2g_ctx* c, uint64_t* counts, uint32_t k) {
+	if(!c || (!counts && k)) return fail(BT2G_ERR_ARG, "null argument");
+	if(!c->comm) return fail(BT2G_ERR_ARG, "no communicator (bt2g_comm_init)");
+	if(k == 0) return BT2G_OK;
+	HIPCHK(hipSetDevice(c->device));
+	Rccl& r = rccl();
+	uint64_t* d = nullptr;
+	HIPCHK(hipMalloc((void**)&d, sizeof(uint64_t) * k));
+	int rc = BT2G_OK;
+	if(hipMemcpyAsync(d, counts, sizeof(uint64_t) * k, hipMemcpyHostToDevice, c->stream) != hipSuccess) {
+		rc = fail(BT2G_ERR_HIP, "hipMemcpyAsync H2D");
+	} else if(int e = r.all_reduce(d, d, k, NCCL_UINT64, NCCL_SUM, c->comm, c->stream)) {
+		rc = fail(BT2G_ERR_HIP, "ncclAllReduce: %s", r.err(e));
+	} else if(hipMemcpyAsync(counts, d, sizeof(uint64_t) * k, hipMemcpyDeviceToHost, c->stream) != hipSuccess ||
+	          stream_wait(c, c->stream) != hipSuccess) {
+		rc = fail(BT2G_ERR_HIP, "all-reduce result copy");
+	}
+	(void)hipFree(d);
+	return rc;
 }
 
 }  // extern "C"

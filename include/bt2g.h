@@ -449,8 +449,21 @@ int bt2g_bench_frame_dev(uint32_t n, const uint32_t* lens, const uint32_t* offs,
                          int32_t minsc, bt2g_frame_in* fin, uint32_t* nprob, uint32_t cap, void* stream);
 
 /* ---- multi-GPU ----------------------------------------------------------- */
-/* The only collective of the path: the caller sums these
- * counters over ranks (RCCL all-reduce in bench.py / the server). */
+/* The only collective of the path: reads shard across ranks
+ * (one process per GPU, a full index replica each) and the ranks sum a few
+ * counters at the end -- RCCL over xGMI.  Where the reference has one process
+ * (the server's OutputQueue / metrics, bt2_search.cpp:4913-4925 spawning every
+ * worker in it) nothing needs reducing; these serve a sharded deployment.
+ *   bt2g_comm_unique_id: one rank creates the communicator id (128 bytes) and
+ *                        hands it to the others out of band;
+ *   bt2g_comm_init:      every rank joins (collective; ctx's device);
+ *   bt2g_allreduce_counts: counts[0..k) summed over the ranks, in place
+ *                        (collective, synchronous on ctx's stream).
+ * RCCL (librccl.so.1) is loaded on first use; BT2G_ERR_HIP if it is absent. */
+#define BT2G_COMM_ID_BYTES 128
+int bt2g_comm_unique_id(uint8_t* id);
+int bt2g_comm_init(bt2g_ctx* ctx, int nranks, int rank, const uint8_t* id);
+int bt2g_allreduce_counts(bt2g_ctx* ctx, uint64_t* counts, uint32_t k);
 
 /* ---- measurement --------------------------------------------------------- */
 /* Kernel timing with HIP events on the launch stream (off by default). */

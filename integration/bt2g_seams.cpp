@@ -28,7 +28,9 @@
 //   SwAligner::nextAlignment     aligner_sw.cpp:737-1146        and every backtrace, with candidate fates)
 //
 // The GPU context is opened on first use from $BT2G_INDEX (the index base the
-// server was started with) on device $BT2G_DEVICE (default 0).
+// server was started with) on device $BT2G_DEVICE (default 0); with
+// $BT2G_DEVICES="0,1,..." every listed device holds a replica of the index and
+// the seams' dispatchers of all devices drain the same request queues.
 //
 // Batching across worker threads: each seam call becomes a request that the
 // calling worker thread blocks on; one dispatcher thread drains the pending
@@ -150,6 +152,30 @@ void init_env() {
 	});
 }
 
+// The devices the dispatchers use: $BT2G_DEVICES (comma-separated, e.g.
+// "0,1,2,3"; default $BT2G_DEVICE, else 0), one full index replica each
+// (reads are independent, no exchange).  The first is g_ctx.
+std::vector<int> devices() {
+	std::vector<int> d;
+	if(const char* e = getenv("BT2G_DEVICES")) {
+		for(const char* p = e; *p;) {
+			char* end = nullptr;
+			long v = strtol(p, &end, 10);
+			if(end == p) break;
+			d.push_back((int)v);
+			p = *end == ',' ? end + 1 : end;
+		}
+	}
+	if(d.empty()) {
+		const char* dev = getenv("BT2G_DEVICE");
+		d.push_back(dev ? atoi(dev) : 0);
+	}
+	return d;
+}
+
+// Index replicas of the devices after the first (opened with the dispatchers).
+std::vector<bt2g_ctx*> g_replicas;
+
 // Opened lazily under g_mu.
 bt2g_ctx* ctx() {
 	if(g_ctx) return g_ctx;
@@ -158,16 +184,15 @@ bt2g_ctx* ctx() {
 		fprintf(stderr, "bt2g adapter: BT2G_INDEX is not set\n");
 		throw 1;
 	}
-	const char* dev = getenv("BT2G_DEVICE");
 	init_env();
-	int rc = bt2g_open(base, dev ? atoi(dev) : 0, &g_ctx);
+	int rc = bt2g_open(base, devices()[0], &g_ctx);
 	if(rc) die("bt2g_open", rc);
 	return g_ctx;
 }
 
-// The batching dispatcher threads each own a context on the one index
+// The batching dispatcher threads each own a context on one replica
 // (bt2g_open_shared: own HIP stream and scratch), so the seams' batches run
-// concurrently on the GPU; the synchronous path uses the base context under g_mu.
+// concurrently on the GPUs; the synchronous path uses the base context under g_mu.
 thread_local bt2g_ctx* t_ctx = nullptr;
 bt2g_ctx* cur_ctx() { return t_ctx ? t_ctx : ctx(); }
 
@@ -724,13 +749,30 @@ private:
 					std::lock_guard<std::mutex> lk(g_mu);
 					ctx();                          // the base context, before any dispatcher
 				}
-				// dispatchers per seam: $BT2G_SEAM_THREADS (default 2; the DP seam, whose
-				// batches take longest, twice that)
+				// one index replica per further device, loaded concurrently
+				const std::vector<int> devs = devices();
+				std::vector<bt2g_ctx*> bases{g_ctx};
+				g_replicas.assign(devs.size() - 1, nullptr);
+				{
+					std::vector<std::thread> ld;
+					std::vector<int> rcs(devs.size(), 0);
+					for(size_t i = 1; i < devs.size(); i++)
+						ld.emplace_back([&, i] { rcs[i] = bt2g_open(getenv("BT2G_INDEX"), devs[i], &g_replicas[i - 1]); });
+					for(std::thread& t : ld) t.join();
+					for(size_t i = 1; i < devs.size(); i++) {
+						if(rcs[i]) die("bt2g_open (replica)", rcs[i]);
+						bases.push_back(g_replicas[i - 1]);
+					}
+				}
+				// dispatchers per seam and device: $BT2G_SEAM_THREADS (default 2; the DP
+				// seam, whose batches take longest, twice that); all of a seam's
+				// dispatchers drain the one queue, so the devices share its load
 				const char* t = getenv("BT2G_SEAM_THREADS");
 				const int per = std::max(1, t ? atoi(t) : 2);
-				for(int k = 0; k < ST_N; k++)
-					for(int i = 0; i < (k == ST_DP ? 2 * per : per); i++)
-						std::thread(&Dispatcher::loop, this, k).detach();
+				for(bt2g_ctx* b : bases)
+					for(int k = 0; k < ST_N; k++)
+						for(int i = 0; i < (k == ST_DP ? 2 * per : per); i++)
+							std::thread(&Dispatcher::loop, this, k, b).detach();
 			}
 		});
 		return on_;
@@ -739,14 +781,14 @@ private:
 	// Dispatcher threads of a seam share its queue: each drains it into batches,
 	// grouped by the batch-wide arguments (arrival order kept within a group), on
 	// its own context.
-	void loop(int kind) {
+	void loop(int kind, bt2g_ctx* base) {
 		bt2g_prof_thread(2);
 		{
 			char nm[16];
 			snprintf(nm, sizeof(nm), "bt2g-%.10s", ST_NAMES[kind]);
 			pthread_setname_np(pthread_self(), nm);
 		}
-		int rc0 = bt2g_open_shared(g_ctx, &t_ctx);
+		int rc0 = bt2g_open_shared(base, &t_ctx);
 		if(rc0) {
 			fprintf(stderr, "bt2g adapter: bt2g_open_shared (%s dispatcher) failed (%d): %s\n", ST_NAMES[kind], rc0,
 			        bt2g_last_error());

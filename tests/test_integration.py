@@ -71,9 +71,9 @@ def _reads(idx, mode, n, seed, dirpath):
     return rs.write_fastq_chunks(dirpath, r, q)
 
 
-def _run(binary, base, chunks, args, dirpath, tag):
+def _run(binary, base, chunks, args, dirpath, tag, extra_env=None):
     stats = os.path.join(dirpath, f"stats_{tag}.json")
-    env = rs.dropin_env(base, stats)
+    env = dict(rs.dropin_env(base, stats), **(extra_env or {}))
     with rs.Server(base, threads=2, args=args, binary=binary, env=env,
                    log_path=os.path.join(dirpath, f"server_{tag}.log")) as s:
         dt, outs = s.run(chunks, k=2)
@@ -86,9 +86,9 @@ def _run(binary, base, chunks, args, dirpath, tag):
     return dt, rs.sorted_records(outs), st
 
 
-def _compare(dropin, base, chunks, args, dirpath, long_reads=False):
+def _compare(dropin, base, chunks, args, dirpath, long_reads=False, extra_env=None):
     t_ref, a, _ = _run(rs.SERVER, base, chunks, args, dirpath, "ref")
-    t_new, b, st = _run(dropin, base, chunks, args, dirpath, "dropin")
+    t_new, b, st = _run(dropin, base, chunks, args, dirpath, "dropin", extra_env)
     assert len(a) == len(b) and len(a) > 0
     bad = [(x, y) for x, y in zip(a, b) if x != y]
     assert not bad, f"{len(bad)} SAM records differ, first:\nref  {bad[0][0][:400]}\nbind {bad[0][1][:400]}"
@@ -120,6 +120,16 @@ def test_binding_sam_parity_cpu(indexes, tmp_path, mode, genome, args, n):
     _compare(SRV_STUB, base, chunks, args, str(tmp_path))
 
 
+@pytest.mark.parametrize("mode,args,n", [("ee", [], 1500), ("paired", [], 600)], ids=["ee", "paired"])
+def test_binding_multi_device_cpu(indexes, tmp_path, mode, args, n):
+    """$BT2G_DEVICES with two devices: every seam's dispatchers on both index
+    replicas drain one queue; SAM equals the stock server's."""
+    _need(rs.SERVER, rs.CLIENT, SRV_STUB)
+    base, idx = indexes["synth"]
+    chunks = _reads(idx, mode, n, 9, str(tmp_path))
+    _compare(SRV_STUB, base, chunks, args, str(tmp_path), extra_env={"BT2G_DEVICES": "0,1"})
+
+
 def test_binding_longreads_cpu(indexes, tmp_path):
     """configs[0]: lambda, example/reads/longreads.fq (6 000 reads of 40-2 561 bp)."""
     _need(rs.SERVER, rs.CLIENT, SRV_STUB, LONGREADS)
@@ -145,6 +155,17 @@ def test_dropin_sam_parity_gpu(indexes, tmp_path, mode, genome, args, n):
     t_ref, t_new, nrec, st = _compare(SRV_GPU, base, chunks, args, str(tmp_path))
     print(f"\n[{mode} {' '.join(args)}] {nrec} records identical; stock {t_ref:.2f}s, drop-in {t_new:.2f}s; "
           f"engine calls {st}")
+
+
+@pytest.mark.gpu
+def test_dropin_two_replicas_gpu(indexes, tmp_path):
+    """BT2G_DEVICES="0,0": two index replicas (on the box's one GPU), the seams'
+    dispatchers of both serving one queue -- the multi-GPU server's sharing."""
+    _need(rs.SERVER, rs.CLIENT, SRV_GPU)
+    base, idx = indexes["synth"]
+    chunks = _reads(idx, "ee", 10000, 9, str(tmp_path))
+    t_ref, t_new, nrec, st = _compare(SRV_GPU, base, chunks, [], str(tmp_path), extra_env={"BT2G_DEVICES": "0,0"})
+    print(f"\n[two replicas] {nrec} records identical; stock {t_ref:.2f}s, drop-in {t_new:.2f}s")
 
 
 def test_binding_lambda_pairs_cpu(indexes, tmp_path):
