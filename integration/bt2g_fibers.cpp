@@ -212,6 +212,23 @@ size_t usable_cpus() {
 	return n;
 }
 
+// a carrier's outbox goes to the dispatchers when it holds $BT2G_FLUSH_N
+// requests or its oldest waited $BT2G_FLUSH_US (defaults 64, 100 us)
+size_t flush_n() {
+	static const size_t n = [] {
+		const char* e = getenv("BT2G_FLUSH_N");
+		return e && atol(e) > 0 ? (size_t)atol(e) : (size_t)64;
+	}();
+	return n;
+}
+uint64_t flush_ns() {
+	static const uint64_t ns = [] {
+		const char* e = getenv("BT2G_FLUSH_US");
+		return (e && atol(e) > 0 ? (uint64_t)atol(e) : (uint64_t)100) * 1000ull;
+	}();
+	return ns;
+}
+
 size_t n_carriers() {
 	const char* e = getenv("BT2G_CARRIERS");
 	if(e && atoi(e) > 0) return (size_t)atoi(e);
@@ -286,8 +303,19 @@ void Carrier::run() {
 			continue;
 		}
 		round.swap(ready);
+		uint64_t t_flush = now_ns();
 		for(Fiber* f : round) {
 			FDBG("carrier %p: run fiber %p\n", (void*)this, (void*)f);
+			// requests leave during the round, not only at its end: a long round
+			// (hundreds of fibers) would otherwise hold the first ones' requests
+			// back for its whole length
+			if(!outbox.empty()) {
+				const uint64_t t = now_ns();
+				if(outbox.size() >= flush_n() || t - t_flush >= flush_ns()) {
+					flush();
+					t_flush = t;
+				}
+			}
 			switch_to(this, f);
 			FDBG("carrier %p: fiber %p -> state %d\n", (void*)this, (void*)f, (int)f->state);
 			switch(f->state) {
@@ -376,6 +404,11 @@ bool enabled() {
 		return !(e && e[0] == '0');
 	}();
 	return on;
+}
+
+size_t count() {
+	std::lock_guard<std::mutex> lk(g_mu);
+	return (size_t)g_next_handle;
 }
 
 void set_flush(FlushFn fn) { g_flush = fn; }
@@ -515,6 +548,28 @@ void __wrap__ZNSt18condition_variable10notify_allEv(std::condition_variable* cv)
 void __wrap__ZNSt18condition_variable10notify_oneEv(std::condition_variable* cv) {
 	wake_cv_fibers(cv, false);
 	__real__ZNSt18condition_variable10notify_oneEv(cv);
+}
+
+// pthread_mutex_lock (std::mutex::lock of the reference's objects and the
+// binding): a fiber must not block its carrier -- a contended lock would stop
+// every other fiber of that carrier, and a condition-variable wake-up of many
+// fibers (LockedQueueCV::push notifies all, pat.h:1981-1985) makes them all
+// re-lock the queue's mutex at once.  A fiber tries the lock, spins briefly,
+// then yields to its carrier and tries again on the carrier's next round.
+int __real_pthread_mutex_lock(pthread_mutex_t* m);
+
+int __wrap_pthread_mutex_lock(pthread_mutex_t* m) {
+	Fiber* f = cur_fiber();
+	if(!f) return __real_pthread_mutex_lock(m);
+	for(int spin = 0;; spin++) {
+		const int r = pthread_mutex_trylock(m);
+		if(r != EBUSY) return r;
+		if(spin < 64) {
+			__builtin_ia32_pause();
+			continue;
+		}
+		suspend(f, READY);
+	}
 }
 
 int __wrap_nanosleep(const struct timespec* req, struct timespec* rem) {

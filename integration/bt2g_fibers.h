@@ -31,6 +31,9 @@ void set_init(InitFn fn);
 // Whether the drop-in runs its workers as fibers ($BT2G_FIBERS, default on).
 bool enabled();
 
+// Fibers created so far (the server's search workers).
+size_t count();
+
 }  // namespace bt2gf
 
 #endif

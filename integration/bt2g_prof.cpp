@@ -13,6 +13,7 @@
 #include <string.h>
 #include <sys/syscall.h>
 #include <sys/time.h>
+#include <sys/uio.h>
 #include <time.h>
 #include <malloc.h>
 #include <ucontext.h>
@@ -34,6 +35,11 @@ std::atomic<uint64_t>* g_pc2 = nullptr;
 std::atomic<uint64_t>* g_ret2 = nullptr;
 std::atomic<uint32_t>* g_cnt2 = nullptr;
 std::atomic<uint64_t> g_lost{0};
+// the executable's text: for a sample outside it (libc, the HIP runtime), the
+// first stack word that points into it is recorded as the sample's "exe caller"
+// (role 8 + role in the pair table) -- which of the server's functions led to
+// a hot spot in a library (mprotect <- sysmalloc <- malloc <- ?)
+uint64_t g_text_lo = 0, g_text_hi = 0;
 thread_local uint64_t t_role = 0;           // 1 carrier, 2 dispatcher (folded into the pair table)
 
 void count_pair(uint64_t pc, uint64_t ret) {
@@ -60,6 +66,17 @@ void on_prof(int, siginfo_t*, void* uc) {
 	if(!pc) return;
 	const uint64_t sp = (uint64_t)((ucontext_t*)uc)->uc_mcontext.gregs[REG_RSP];
 	if(sp) count_pair(pc, *(const uint64_t*)sp ^ (t_role << 60));
+	if(sp && g_text_hi && (pc < g_text_lo || pc >= g_text_hi)) {
+		// the stack words above sp, read without faulting past the stack's end
+		uint64_t w[256];
+		iovec loc{w, sizeof(w)}, rem{(void*)sp, sizeof(w)};
+		const ssize_t got = process_vm_readv(getpid(), &loc, 1, &rem, 1, 0);
+		for(ssize_t i = 0; got > 0 && i < got / 8; i++)
+			if(w[i] >= g_text_lo && w[i] < g_text_hi) {
+				count_pair(pc, w[i] ^ ((t_role | 8) << 60));
+				break;
+			}
+	}
 	size_t h = (size_t)((pc * 0x9E3779B97F4A7C15ull) >> 44) & (NSLOT - 1);
 	for(size_t probe = 0; probe < 64; probe++, h = (h + 1) & (NSLOT - 1)) {
 		uint64_t k = g_pc[h].load(std::memory_order_relaxed);
@@ -146,6 +163,21 @@ struct Sampler {
 		sa.sa_sigaction = on_prof;
 		sa.sa_flags = SA_SIGINFO | SA_RESTART;
 		sigaction(SIGPROF, &sa, nullptr);
+		char exe[4096] = {0};
+		if(readlink("/proc/self/exe", exe, sizeof(exe) - 1) > 0)
+			if(FILE* f = fopen("/proc/self/maps", "r")) {
+				char line[4096];
+				while(fgets(line, sizeof(line), f)) {
+					unsigned long lo, hi, off, ino;
+					char perm[8], dev[16], pth[3000] = {0};
+					if(sscanf(line, "%lx-%lx %7s %lx %15s %lu %2999s", &lo, &hi, perm, &off, dev, &ino, pth) == 7 &&
+					   perm[2] == 'x' && !strcmp(pth, exe)) {
+						g_text_lo = lo;
+						g_text_hi = hi;
+					}
+				}
+				fclose(f);
+			}
 		std::string p(path);
 		std::thread([p] {
 			for(int k = 0;; k++) {

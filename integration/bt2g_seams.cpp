@@ -83,6 +83,10 @@ const char* const ST_NAMES[ST_N] = {"exact_sweep", "one_mm", "seed_search", "ung
                                     "get_offset"};
 std::atomic<uint64_t> g_gpu[ST_N], g_cpu[ST_N], g_batches[ST_N];
 std::atomic<uint64_t> g_call_us[ST_N], g_wait_us[ST_N];   // engine time per seam; request round trips
+// of a round trip: from submit until a dispatcher takes the request (queue: the
+// carrier's round, the batch window, earlier batches), and from the request's
+// completion until its fiber runs again (resume: the carrier's ready queue)
+std::atomic<uint64_t> g_queue_us[ST_N], g_resume_us[ST_N];
 // $BT2G_ADAPTER_PROF=1: kernel time per engine kernel id (bt2g_kernel_stats), all dispatchers
 const int NKERN = 8;
 const char* const KERN_NAMES[NKERN] = {"exact_sweep", "seed_search", "one_mm", "get_offset", "sw_align",
@@ -105,6 +109,13 @@ void write_stats() {
 		              ST_NAMES[i], (unsigned long long)g_gpu[i].load(), (unsigned long long)g_cpu[i].load(),
 		              (unsigned long long)g_batches[i].load(), g_call_us[i].load() / 1000.0,
 		              g_wait_us[i].load() / 1000.0);
+	n += snprintf(buf + n, sizeof(buf) - n, ", \"queue_ms\": [");
+	for(int i = 0; i < ST_N; i++)
+		n += snprintf(buf + n, sizeof(buf) - n, "%s%.1f", i ? ", " : "", g_queue_us[i].load() / 1000.0);
+	n += snprintf(buf + n, sizeof(buf) - n, "], \"resume_ms\": [");
+	for(int i = 0; i < ST_N; i++)
+		n += snprintf(buf + n, sizeof(buf) - n, "%s%.1f", i ? ", " : "", g_resume_us[i].load() / 1000.0);
+	n += snprintf(buf + n, sizeof(buf) - n, "]");
 	n += snprintf(buf + n, sizeof(buf) - n, ", \"kernels\": {");
 	for(int i = 0; i < NKERN; i++)
 		n += snprintf(buf + n, sizeof(buf) - n, "%s\"%s\": [%llu, %.1f]", i ? ", " : "", KERN_NAMES[i],
@@ -273,6 +284,7 @@ struct Req {
 	int rc = 0;
 	char err[256] = {0}; // bt2g_last_error() of the thread that ran the call
 	void* fiber = nullptr;   // the waiting fiber (bt2g_fibers.cpp), else an OS thread on sem
+	uint64_t t_sub = 0, t_take = 0, t_done = 0;   // submit, taken by a dispatcher, completed (us)
 	sem_t sem;
 	Req(int k, uint64_t ky) : kind(k), key(ky) {}
 };
@@ -680,6 +692,7 @@ public:
 	// or run at once under the shared context's lock.
 	void submit(Req* r) {
 		const uint64_t t0 = now_us();
+		r->t_sub = t0;
 		if(void* f = bt2gf::self()) {
 			// a fiber (bt2g_fibers.cpp): the carrier hands the request over with the
 			// rest of its round (flush below) and resumes the fiber when it is done
@@ -701,7 +714,10 @@ public:
 			while(sem_wait(&r->sem) != 0) {}
 			sem_destroy(&r->sem);
 		}
-		g_wait_us[r->kind] += now_us() - t0;
+		const uint64_t t1 = now_us();
+		g_wait_us[r->kind] += t1 - t0;
+		if(r->t_take) g_queue_us[r->kind] += r->t_take - t0;
+		if(r->t_done) g_resume_us[r->kind] += t1 - r->t_done;
 		if(r->rc) {
 			fprintf(stderr, "bt2g adapter: %s failed (%d): %s\n", ST_NAMES[r->kind], r->rc, r->err);
 			throw 1;
@@ -814,6 +830,8 @@ private:
 				take.assign(q.v.begin(), q.v.begin() + m);
 				q.v.erase(q.v.begin(), q.v.begin() + m);
 			}
+			const uint64_t tk = now_us();
+			for(Req* r : take) r->t_take = tk;
 			std::vector<bool> done(take.size(), false);
 			for(size_t i = 0; i < take.size(); i++) {
 				if(done[i]) continue;
@@ -841,7 +859,9 @@ private:
 				}
 				g_batches[kind]++;
 				wake.clear();
+				const uint64_t td = now_us();
 				for(Req* r : g) {
+					r->t_done = td;
 					r->rc = rc;
 					if(rc) snprintf(r->err, sizeof(r->err), "%s (batch of %zu)", bt2g_last_error(), g.size());
 					if(r->fiber) wake.push_back(r->fiber);
@@ -1385,6 +1405,44 @@ void resolve_rows(const Ebwt& ebwtFw) {
 
 }  // namespace
 
+namespace {
+struct TSAListFill : public PList<TIndexOffU, CACHE_PAGE_SZ> {
+	// the effect of n calls of add(p, v) on the pool and the list's length,
+	// without writing the slots: returns how many were added
+	size_t reserve(Pool& p, size_t n) {
+		const size_t per = (size_t)CACHE_PAGE_SZ / sizeof(TIndexOffU);
+		size_t done = 0;
+		while(done < n) {
+			if(!ensure(p, 1)) return done;
+			if(cur_ == per) {
+				cur_ = 0;
+				curPage_++;
+			}
+			const size_t k = std::min(per - cur_, n - done);
+			cur_ += k;
+			done += k;
+		}
+		return done;
+	}
+	// slots [i, i + n) set to v, a page at a time
+	void fill(size_t i, size_t n, TIndexOffU v) {
+		const size_t per = (size_t)CACHE_PAGE_SZ / sizeof(TIndexOffU);
+		while(n) {
+			const size_t pg = i / per, off = i % per, k = std::min(per - off, n);
+			std::fill(pages_[pg] + off, pages_[pg] + off + k, v);
+			i += k;
+			n -= k;
+		}
+	}
+};
+// the slice's list and position (protected in PListSlice)
+struct TSliceAcc : public TSlice {
+	void fill(TIndexOffU v) {
+		if(len_) static_cast<TSAListFill*>(list_)->fill(i_, len_, v);
+	}
+};
+}  // namespace
+
 template <>
 void GroupWalk2S<TSlice, 16>::init(const Ebwt& ebwtFw, const BitPairReference& ref, SARangeWithOffs<TSlice>& sa,
                                    RandomSource& rnd, WalkMetrics& met) {
@@ -1394,7 +1452,7 @@ void GroupWalk2S<TSlice, 16>::init(const Ebwt& ebwtFw, const BitPairReference& r
 	// the range's offset slots as the cache would hold them before any walk
 	// (AlignmentCache::addOnTheFlyImpl above only reserves them); rows resolved
 	// earlier in this read are resolved again, to the same offsets
-	for(size_t j = 0; j < sa.size(); j++) sa.offs[j] = OFF_MASK;
+	static_cast<TSliceAcc&>(sa.offs).fill(OFF_MASK);
 	if(t_gw.on) t_gw.ranges.push_back(GwRange{sa.topf, sa.size(), sa.offs});
 }
 
@@ -1507,27 +1565,6 @@ void SwDriver::extend(const Read& rd, const Ebwt& ebwtFw, const Ebwt* ebwtBw, TI
 // here the slots are only reserved.  Reserving keeps the reference's pool use
 // and failure point: PList::ensure(pool, 1) wherever the reference's add() of
 // that row would take a page (or fail), the rest of the page by the count.
-namespace {
-struct TSAListFill : public PList<TIndexOffU, CACHE_PAGE_SZ> {
-	// the effect of n calls of add(p, v) on the pool and the list's length,
-	// without writing the slots: returns how many were added
-	size_t reserve(Pool& p, size_t n) {
-		const size_t per = (size_t)CACHE_PAGE_SZ / sizeof(TIndexOffU);
-		size_t done = 0;
-		while(done < n) {
-			if(!ensure(p, 1)) return done;
-			if(cur_ == per) {
-				cur_ = 0;
-				curPage_++;
-			}
-			const size_t k = std::min(per - cur_, n - done);
-			cur_ += k;
-			done += k;
-		}
-		return done;
-	}
-};
-}  // namespace
 
 bool AlignmentCache::addOnTheFlyImpl(QVal& qv, const SAKey& sak, TIndexOffU topf, TIndexOffU botf, TIndexOffU topb,
                                      TIndexOffU botb) {

@@ -22,7 +22,11 @@ for f in sys.argv[1:]:
         ec = x.get("engine_calls")
         if not ec:
             continue
+        names = [k for k in ec if isinstance(ec[k], list) and k not in ("queue_ms", "resume_ms")]
         for k, v in ec.items():
+            if k in ("queue_ms", "resume_ms"):
+                print(f"   {k} per call: " + ", ".join(f"{n}:{q / max(ec[n][0], 1):.2f}" for n, q in zip(names, v)))
+                continue
             if k == "kernels":
                 kk = {a: f"{b[1] / max(b[0], 1):.3f}ms x{b[0]}" for a, b in v.items() if b[0]}
                 if kk:

@@ -128,7 +128,8 @@ def callers(a):
     for pc, ret, c, role in rows:
         roles[role] += c
         if a.callers_of in names[pc]:
-            cnt[f"{['?', 'carrier', 'dispatcher'][role] if role < 3 else role}: {names[ret]}"] += c
+            tag = {1: "carrier", 2: "dispatcher", 9: "carrier (exe caller)", 10: "dispatcher (exe caller)"}
+            cnt[f"{tag.get(role, role)}: {names[ret]}"] += c
             tot += c
     print(f"samples by thread role (1 carrier, 2 dispatcher): {dict(roles)}")
     print(f"{tot} samples in {a.callers_of}")

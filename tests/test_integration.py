@@ -94,7 +94,7 @@ def _compare(dropin, base, chunks, args, dirpath, long_reads=False, extra_env=No
     assert not bad, f"{len(bad)} SAM records differ, first:\nref  {bad[0][0][:400]}\nbind {bad[0][1][:400]}"
     assert st is not None, "binding wrote no call counts"
     for k, v in st.items():
-        if k == "kernels":
+        if k in ("kernels", "queue_ms", "resume_ms"):       # (not seams: timing breakdowns)
             continue
         gpu, cpu = v[0], v[1]                    # calls served by the engine / by the CPU path
         if not long_reads:
