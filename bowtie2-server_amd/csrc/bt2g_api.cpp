@@ -98,6 +98,9 @@ struct bt2g_ctx {
 	// device mirror of `pin` (same size and offsets): a call's inputs are staged
 	// in `pin` and reach the device in one copy, its outputs come back in one
 	uint8_t* pin_dev = nullptr;
+	// the device's view of `pin` itself (hipHostGetDevicePointer): kernels write
+	// small variable-size outputs straight into host memory
+	uint8_t* pin_dview = nullptr;
 	// $BT2G_SYNC=poll: host waits query an event and sleep between queries
 	hipEvent_t poll_ev = nullptr;
 	// the ranks' communicator (bt2g_comm_init): an RCCL ncclComm_t
@@ -254,12 +257,15 @@ struct Arena {
 			c->pin_dev = nullptr;
 			size_t cap = std::max<size_t>(c->pin_need + c->pin_need / 4, (size_t)16 << 20);
 			if(hipHostMalloc((void**)&c->pin, cap, hipHostMallocDefault) == hipSuccess &&
-			   hipMalloc((void**)&c->pin_dev, cap) == hipSuccess) {
+			   hipMalloc((void**)&c->pin_dev, cap) == hipSuccess &&
+			   hipHostGetDevicePointer((void**)&c->pin_dview, c->pin, 0) == hipSuccess) {
 				c->pin_cap = cap;
 			} else {
 				if(c->pin) (void)hipHostFree(c->pin);
+				if(c->pin_dev) (void)hipFree(c->pin_dev);
 				c->pin = nullptr;
 				c->pin_dev = nullptr;
+				c->pin_dview = nullptr;
 				c->pin_cap = 0;
 			}
 		}
@@ -1178,6 +1184,7 @@ struct Tmp {
 	std::vector<Late> late;               // outputs outside the mirror (copied at finish)
 	size_t sent = 0;                      // pinned bytes already on the device
 	size_t mo_lo = SIZE_MAX, mo_hi = 0;   // mirrored outputs still to bring back
+	size_t map_lo = SIZE_MAX;             // lowest pinned offset a kernel writes directly
 	bool pending = false;                 // staged inputs not yet sent
 	explicit Tmp(bt2g_ctx* cx) : ar(cx), c(cx), st(cx->stream) {}
 	template <typename T>
@@ -1204,6 +1211,17 @@ struct Tmp {
 		}
 		pending = false;
 		return BT2G_OK;
+	}
+	// a block of pinned host memory that kernels write directly (no copy back):
+	// the device's pointer to it, *h the host's; nullptr when the block is too
+	// small this call.  Called after the call's out()s.
+	template <typename T>
+	T* mapped(size_t count, T** h) {
+		uint8_t* pn = ar.pinned(count * sizeof(T) + 16);
+		if(!pn) return nullptr;
+		map_lo = std::min(map_lo, (size_t)(pn - c->pin));
+		*h = (T*)pn;
+		return (T*)(c->pin_dview + (pn - c->pin));
 	}
 	// a device output that finish() copies to h (`count` elements)
 	template <typename T>
@@ -1236,6 +1254,8 @@ struct Tmp {
 	}
 	int finish() {
 		if(pending) return fail(BT2G_ERR_ARG, "internal: inputs staged but never sent");
+		// (the mirror's copy back must not cover host memory a kernel wrote)
+		if(mo_hi > mo_lo && mo_hi > map_lo) return fail(BT2G_ERR_ARG, "internal: out() after mapped()");
 		if(mo_hi > mo_lo) {
 			HIPCHK(hipMemcpyAsync(c->pin + mo_lo, c->pin_dev + mo_lo, mo_hi - mo_lo, hipMemcpyDeviceToHost, st));
 			mo_lo = SIZE_MAX;
@@ -1488,13 +1508,25 @@ int bt2g_sw_align_bt_packed(bt2g_ctx* c, const uint8_t* reads, const uint8_t* qu
 	   (rc = t.up(&dc, (const bt2g_sw_cand*)nullptr, (size_t)nprob * cap)) ||
 	   (rc = t.up(&ded, (const bt2g_edit*)nullptr, na * maxedit)) ||
 	   (rc = t.up(&dcnt, (const uint32_t*)nullptr, 3 * (size_t)nprob)) ||
-	   (rc = t.up(&doff, (const uint32_t*)nullptr, 3 * (size_t)nprob + 3)) ||
-	   (rc = t.up(&dpc, (const bt2g_sw_cand*)nullptr, (size_t)nprob * cap)) ||
-	   (rc = t.up(&dpe, (const bt2g_edit*)nullptr, na * maxedit)))
+	   (rc = t.up(&doff, (const uint32_t*)nullptr, 3 * (size_t)nprob + 3)))
 		return rc;
-	if(fates && ((rc = t.up(&dft, (const int8_t*)nullptr, (size_t)nprob * cap)) ||
-	             (rc = t.up(&dpf, (const int8_t*)nullptr, (size_t)nprob * cap))))
-		return rc;
+	if(fates && (rc = t.up(&dft, (const int8_t*)nullptr, (size_t)nprob * cap))) return rc;
+	// the packed outputs go straight to pinned host memory when it has room (one
+	// synchronisation per call); else to the device, copied back once the
+	// totals are known (two)
+	bt2g_sw_cand* hpc = nullptr;
+	int8_t* hpf = nullptr;
+	bt2g_edit* hpe = nullptr;
+	dpc = t.mapped((size_t)nprob * cap, &hpc);
+	dpe = dpc ? t.mapped(na * maxedit, &hpe) : nullptr;
+	dpf = dpe && fates ? t.mapped((size_t)nprob * cap, &hpf) : nullptr;
+	const bool direct = dpc && dpe && (dpf || !fates);
+	if(!direct) {
+		if((rc = t.up(&dpc, (const bt2g_sw_cand*)nullptr, (size_t)nprob * cap)) ||
+		   (rc = t.up(&dpe, (const bt2g_edit*)nullptr, na * maxedit)) ||
+		   (fates && (rc = t.up(&dpf, (const int8_t*)nullptr, (size_t)nprob * cap))))
+			return rc;
+	}
 	if((rc = t.send())) return rc;
 	const SwHint hint = sw_hint(probs, nprob, lens, enable8);
 	if((rc = sw_align_bt_impl(c, dr, dq, stride, dl, dp, nprob, dw, drc, sc, enable8, cap, dres, dc, maxaln, maxedit,
@@ -1504,10 +1536,16 @@ int bt2g_sw_align_bt_packed(bt2g_ctx* c, const uint8_t* reads, const uint8_t* qu
 	HIPCHK(hipGetLastError());
 	if((rc = t.down(tot, doff + 3 * (size_t)nprob, 3))) return rc;
 	if((rc = t.finish())) return rc;
-	if((rc = t.down(cands, dpc, tot[0])) || (fates && (rc = t.down(fates, dpf, tot[0]))) ||
-	   (rc = t.down(edits, dpe, tot[2])))
-		return rc;
-	if((rc = t.finish())) return rc;
+	if(direct) {
+		memcpy(cands, hpc, sizeof(bt2g_sw_cand) * tot[0]);
+		if(fates) memcpy(fates, hpf, tot[0]);
+		memcpy(edits, hpe, sizeof(bt2g_edit) * tot[2]);
+	} else {
+		if((rc = t.down(cands, dpc, tot[0])) || (fates && (rc = t.down(fates, dpf, tot[0]))) ||
+		   (rc = t.down(edits, dpe, tot[2])))
+			return rc;
+		if((rc = t.finish())) return rc;
+	}
 	totals[0] = tot[0];
 	totals[1] = tot[1];
 	totals[2] = tot[2];

@@ -1,0 +1,224 @@
+// integration/bt2g_alloc.cpp -- the drop-in's operator new / delete: per-thread
+// caches of freed blocks by size class.
+//
+// The reference allocates with new / new[] (EList, SStringExpandable, the
+// per-connection read buffers PatternSourceServiceFactory::align creates and
+// destroys, pat.cpp:2030-2075).  Under fibers the server holds thousands of
+// workers on a few carrier threads, and the per-connection buffers are built
+// on the connection's thread, grown on the carriers (PatternSourcePerThread::
+// finalize) and freed on the connection's thread again.  glibc's arenas take
+// that badly: frees into another thread's arena contend for its lock, and a
+// heap that empties completely is unmapped (heap_trim ignores
+// M_TRIM_THRESHOLD for that case) and re-created later one mprotect per
+// allocation that does not fit -- r03k at 3.1 Gbp: mprotect 19 %, malloc
+// internals 7 % of the carriers' CPU.
+//
+// Replacing the global operator new / delete (the standard's replaceable
+// allocation functions: the executable's definitions serve every object and
+// library of the process) with size-class caches removes both: a freed block
+// goes to the freeing thread's cache, blocks beyond a cache's cap move to a
+// shared depot in batches (one lock per batch), and a thread that finds its
+// cache empty takes a batch from the depot before it asks malloc.  Memory is
+// never returned to the system -- the server's working set is stable once the
+// first connections have run.  Blocks above 256 KiB (the alignment caches'
+// pools) go to malloc / free directly.  $BT2G_ALLOC=0 keeps glibc's allocator.
+#include <errno.h>
+#include <stdint.h>
+#include <stdlib.h>
+#include <string.h>
+
+#include <atomic>
+#include <new>
+
+namespace {
+
+const int NCLASS = 15;                  // 16 B .. 256 KiB
+const size_t MAXSZ = (size_t)16 << (NCLASS - 1);
+const size_t HDR = 16;                  // keeps the default new alignment (16)
+const uint32_t MAGIC_CACHED = 0xB72C0DE5u, MAGIC_MALLOC = 0xB72C0DE6u;
+const int BATCH = 32;                   // blocks moved to / from the depot at once
+
+struct Hdr {
+	uint32_t magic;
+	uint32_t cls;
+	uint64_t pad;
+};
+static_assert(sizeof(Hdr) == HDR, "header size");
+
+struct Node {
+	Node* next;
+};
+
+inline int cls_of(size_t n) {
+	size_t s = 16;
+	int c = 0;
+	while(s < n) {
+		s <<= 1;
+		c++;
+	}
+	return c;
+}
+inline size_t size_of(int c) { return (size_t)16 << c; }
+// blocks a thread keeps per class before half go to the depot (~4 MiB per class)
+inline int cap_of(int c) {
+	const size_t v = ((size_t)4 << 20) / size_of(c);
+	return v < 64 ? 64 : (v > 4096 ? 4096 : (int)v);
+}
+
+bool enabled() {
+	static const bool on = [] {
+		const char* e = getenv("BT2G_ALLOC");
+		return !(e && e[0] == '0');
+	}();
+	return on;
+}
+
+// a spin lock: held for a few list operations, and never yields (the drop-in
+// wraps pthread_mutex_lock to yield a fiber; an allocation must not)
+struct Spin {
+	std::atomic_flag f = ATOMIC_FLAG_INIT;
+	void lock() {
+		while(f.test_and_set(std::memory_order_acquire)) __builtin_ia32_pause();
+	}
+	void unlock() { f.clear(std::memory_order_release); }
+};
+struct Guard {
+	Spin& s;
+	explicit Guard(Spin& x) : s(x) { s.lock(); }
+	~Guard() { s.unlock(); }
+};
+
+struct Depot {
+	Spin mu[NCLASS];
+	Node* head[NCLASS] = {};
+	size_t n[NCLASS] = {};
+};
+Depot& depot() {
+	static Depot* d = new (malloc(sizeof(Depot))) Depot();   // never destroyed (used until exit)
+	return *d;
+}
+
+thread_local bool t_dead = false;       // the thread's cache is gone (thread exit)
+
+struct Cache {
+	Node* head[NCLASS] = {};
+	int n[NCLASS] = {};
+	~Cache() {
+		// a thread that ends (the server makes one per connection) leaves its blocks
+		// to the others; frees by later thread-exit destructors go to the depot
+		t_dead = true;
+		for(int c = 0; c < NCLASS; c++) {
+			if(!head[c]) continue;
+			Node* tail = head[c];
+			while(tail->next) tail = tail->next;
+			Depot& d = depot();
+			Guard lk(d.mu[c]);
+			tail->next = d.head[c];
+			d.head[c] = head[c];
+			d.n[c] += (size_t)n[c];
+			head[c] = nullptr;
+			n[c] = 0;
+		}
+	}
+};
+thread_local Cache t_cache;
+
+void* fresh(int c) {
+	void* p = malloc(HDR + size_of(c));
+	if(!p) return nullptr;
+	Hdr* h = (Hdr*)p;
+	h->magic = MAGIC_CACHED;
+	h->cls = (uint32_t)c;
+	return (char*)p + HDR;
+}
+
+void* alloc(size_t n) {
+	if(n == 0) n = 1;
+	if(!enabled() || n > MAXSZ) {
+		void* p = malloc(HDR + n);
+		if(!p) return nullptr;
+		((Hdr*)p)->magic = MAGIC_MALLOC;
+		return (char*)p + HDR;
+	}
+	const int c = cls_of(n);
+	if(!t_dead) {
+		Cache& tc = t_cache;
+		if(!tc.head[c]) {
+			// refill from the depot (one lock for a batch)
+			Depot& d = depot();
+			Guard lk(d.mu[c]);
+			for(int i = 0; i < BATCH && d.head[c]; i++) {
+				Node* b = d.head[c];
+				d.head[c] = b->next;
+				d.n[c]--;
+				b->next = tc.head[c];
+				tc.head[c] = b;
+				tc.n[c]++;
+			}
+		}
+		if(Node* b = tc.head[c]) {
+			tc.head[c] = b->next;
+			tc.n[c]--;
+			return b;
+		}
+	}
+	return fresh(c);
+}
+
+void release(void* p) {
+	if(!p) return;
+	Hdr* h = (Hdr*)((char*)p - HDR);
+	if(h->magic == MAGIC_MALLOC) {
+		free(h);
+		return;
+	}
+	if(h->magic != MAGIC_CACHED || h->cls >= (uint32_t)NCLASS) abort();   // not ours: a heap corruption
+	const int c = (int)h->cls;
+	Node* b = (Node*)p;
+	if(t_dead) {
+		Depot& d = depot();
+		Guard lk(d.mu[c]);
+		b->next = d.head[c];
+		d.head[c] = b;
+		d.n[c]++;
+		return;
+	}
+	Cache& tc = t_cache;
+	b->next = tc.head[c];
+	tc.head[c] = b;
+	if(++tc.n[c] > cap_of(c)) {
+		// half of the cache to the depot
+		const int k = tc.n[c] / 2;
+		Node* first = tc.head[c];
+		Node* last = first;
+		for(int i = 1; i < k; i++) last = last->next;
+		tc.head[c] = last->next;
+		tc.n[c] -= k;
+		Depot& d = depot();
+		Guard lk(d.mu[c]);
+		last->next = d.head[c];
+		d.head[c] = first;
+		d.n[c] += (size_t)k;
+	}
+}
+
+}  // namespace
+
+void* operator new(size_t n) {
+	void* p = alloc(n);
+	if(!p) throw std::bad_alloc();
+	return p;
+}
+void* operator new[](size_t n) {
+	void* p = alloc(n);
+	if(!p) throw std::bad_alloc();
+	return p;
+}
+void* operator new(size_t n, const std::nothrow_t&) noexcept { return alloc(n); }
+void* operator new[](size_t n, const std::nothrow_t&) noexcept { return alloc(n); }
+void operator delete(void* p) noexcept { release(p); }
+void operator delete[](void* p) noexcept { release(p); }
+void operator delete(void* p, size_t) noexcept { release(p); }
+void operator delete[](void* p, size_t) noexcept { release(p); }
+void operator delete(void* p, const std::nothrow_t&) noexcept { release(p); }
+void operator delete[](void* p, const std::nothrow_t&) noexcept { release(p); }

@@ -131,6 +131,7 @@ struct Fiber {
 	State state = READY;
 	uint64_t wake_at_ns = 0;          // PARKED by nanosleep: not before this time
 	const void* cv = nullptr;         // the condition variable it waits on
+	void* user = nullptr;             // bt2gf::local()
 };
 
 uint64_t now_ns() {
@@ -398,6 +399,11 @@ struct MallocTuning {
 
 void* self() { return cur_fiber(); }
 
+void** local() {
+	Fiber* f = cur_fiber();
+	return f ? &f->user : nullptr;
+}
+
 bool enabled() {
 	static const bool on = [] {
 		const char* e = getenv("BT2G_FIBERS");
@@ -417,6 +423,12 @@ void set_init(InitFn fn) { g_init = fn; }
 void block_on(void* req) {
 	Fiber* f = cur_fiber();
 	f->home->outbox.push_back(req);
+	suspend(f, BLOCKED);
+}
+
+void block_on_many(void* const* reqs, size_t n) {
+	Fiber* f = cur_fiber();
+	f->home->outbox.insert(f->home->outbox.end(), reqs, reqs + n);
 	suspend(f, BLOCKED);
 }
 

@@ -15,6 +15,10 @@ void* self();
 // carrier has had its turn) and suspend until wake(self) is called for it.
 void block_on(void* req);
 
+// The same for n requests at once; the fiber resumes at the first wake(self)
+// (the seam side wakes it once, when the last of them completed).
+void block_on_many(void* const* reqs, size_t n);
+
 // Resume fibers whose requests completed (any thread; grouped per carrier).
 void wake_many(void* const* fibers, size_t n);
 
@@ -33,6 +37,10 @@ bool enabled();
 
 // Fibers created so far (the server's search workers).
 size_t count();
+
+// A pointer-sized slot of the running fiber for its caller's use (nullptr on an
+// ordinary thread): state that must not be shared by the fibers of a carrier.
+void** local();
 
 }  // namespace bt2gf
 

@@ -87,6 +87,9 @@ std::atomic<uint64_t> g_call_us[ST_N], g_wait_us[ST_N];   // engine time per sea
 // carrier's round, the batch window, earlier batches), and from the request's
 // completion until its fiber runs again (resume: the carrier's ready queue)
 std::atomic<uint64_t> g_queue_us[ST_N], g_resume_us[ST_N];
+// speculative DP prefetch: group requests, DPs prefetched, align() calls served
+// by them, and (BT2G_SPEC_VERIFY) served ones that differed from align()'s own
+std::atomic<uint64_t> g_spec_dps{0}, g_spec_hits{0}, g_spec_groups{0}, g_spec_verify_bad{0};
 // $BT2G_ADAPTER_PROF=1: kernel time per engine kernel id (bt2g_kernel_stats), all dispatchers
 const int NKERN = 8;
 const char* const KERN_NAMES[NKERN] = {"exact_sweep", "seed_search", "one_mm", "get_offset", "sw_align",
@@ -116,6 +119,9 @@ void write_stats() {
 	for(int i = 0; i < ST_N; i++)
 		n += snprintf(buf + n, sizeof(buf) - n, "%s%.1f", i ? ", " : "", g_resume_us[i].load() / 1000.0);
 	n += snprintf(buf + n, sizeof(buf) - n, "]");
+	n += snprintf(buf + n, sizeof(buf) - n, ", \"spec\": [%llu, %llu, %llu, %llu]",
+	              (unsigned long long)g_spec_groups.load(), (unsigned long long)g_spec_dps.load(),
+	              (unsigned long long)g_spec_hits.load(), (unsigned long long)g_spec_verify_bad.load());
 	n += snprintf(buf + n, sizeof(buf) - n, ", \"kernels\": {");
 	for(int i = 0; i < NKERN; i++)
 		n += snprintf(buf + n, sizeof(buf) - n, "%s\"%s\": [%llu, %.1f]", i ? ", " : "", KERN_NAMES[i],
@@ -285,6 +291,7 @@ struct Req {
 	char err[256] = {0}; // bt2g_last_error() of the thread that ran the call
 	void* fiber = nullptr;   // the waiting fiber (bt2g_fibers.cpp), else an OS thread on sem
 	uint64_t t_sub = 0, t_take = 0, t_done = 0;   // submit, taken by a dispatcher, completed (us)
+	std::atomic<int>* group = nullptr;   // submit_group: requests still to complete (the last wakes)
 	sem_t sem;
 	Req(int k, uint64_t ky) : kind(k), key(ky) {}
 };
@@ -551,8 +558,10 @@ int run_dp(const std::vector<DpReq*>& v, uint32_t cap = 0, uint32_t maxaln = 8) 
 	for(size_t i = 0; i < n; i++) {
 		b.P[i] = v[i]->p;
 		b.P[i].read = (uint32_t)i;
-		b.P[i].win_off = (int64_t)b.W.size();
-		b.W.insert(b.W.end(), v[i]->win.begin(), v[i]->win.end());
+		if(v[i]->p.win_off >= 0) {     // the caller's window (align(): initRef's); else the resident reference
+			b.P[i].win_off = (int64_t)b.W.size();
+			b.W.insert(b.W.end(), v[i]->win.begin(), v[i]->win.end());
+		}
 		b.RC[i] = v[i]->rect;
 	}
 	b.R.resize(n);
@@ -724,6 +733,36 @@ public:
 		}
 	}
 
+	// Several requests of one worker at once (a fiber waits once, for all).
+	void submit_group(Req* const* v, size_t n) {
+		if(n == 0) return;
+		void* f = bt2gf::self();
+		if(!f) {
+			for(size_t i = 0; i < n; i++) submit(v[i]);
+			return;
+		}
+		std::atomic<int> left((int)n);
+		const uint64_t t0 = now_us();
+		for(size_t i = 0; i < n; i++) {
+			v[i]->fiber = f;
+			v[i]->group = &left;
+			v[i]->t_sub = t0;
+		}
+		bt2gf::block_on_many(reinterpret_cast<void* const*>(v), n);
+		const uint64_t t1 = now_us();
+		for(size_t i = 0; i < n; i++) {
+			Req* r = v[i];
+			r->group = nullptr;
+			g_wait_us[r->kind] += t1 - t0;
+			if(r->t_take) g_queue_us[r->kind] += r->t_take - t0;
+			if(r->t_done) g_resume_us[r->kind] += t1 - r->t_done;
+			if(r->rc) {
+				fprintf(stderr, "bt2g adapter: %s failed (%d): %s\n", ST_NAMES[r->kind], r->rc, r->err);
+				throw 1;
+			}
+		}
+	}
+
 	void start() { (void)batching(); }
 
 	// A carrier's round of fiber requests (bt2gf::set_flush): one lock per seam.
@@ -780,15 +819,22 @@ private:
 						bases.push_back(g_replicas[i - 1]);
 					}
 				}
-				// dispatchers per seam and device: $BT2G_SEAM_THREADS (default 2; the DP
-				// seam, whose batches take longest, twice that); all of a seam's
-				// dispatchers drain the one queue, so the devices share its load
+				// dispatchers per seam and device: $BT2G_SEAM_THREADS (default 1; the DP
+				// seam, whose batches take longest, twice that), or per seam
+				// $BT2G_SEAM_THREADS_<seam> (e.g. BT2G_SEAM_THREADS_one_mm=2); all of a
+				// seam's dispatchers drain the one queue, so the devices share its load.
+				// (r03i at 3.1 Gbp: 2 per seam 25.2k reads/s, 1 per seam 28.6k -- the
+				// streams' kernels slow each other more than they overlap)
 				const char* t = getenv("BT2G_SEAM_THREADS");
-				const int per = std::max(1, t ? atoi(t) : 2);
+				const int per = std::max(1, t ? atoi(t) : 1);
 				for(bt2g_ctx* b : bases)
-					for(int k = 0; k < ST_N; k++)
-						for(int i = 0; i < (k == ST_DP ? 2 * per : per); i++)
-							std::thread(&Dispatcher::loop, this, k, b).detach();
+					for(int k = 0; k < ST_N; k++) {
+						char nm[64];
+						snprintf(nm, sizeof(nm), "BT2G_SEAM_THREADS_%s", ST_NAMES[k]);
+						const char* tk = getenv(nm);
+						const int nk = tk && atoi(tk) > 0 ? atoi(tk) : (k == ST_DP ? 2 * per : per);
+						for(int i = 0; i < nk; i++) std::thread(&Dispatcher::loop, this, k, b).detach();
+					}
 			}
 		});
 		return on_;
@@ -864,8 +910,13 @@ private:
 					r->t_done = td;
 					r->rc = rc;
 					if(rc) snprintf(r->err, sizeof(r->err), "%s (batch of %zu)", bt2g_last_error(), g.size());
-					if(r->fiber) wake.push_back(r->fiber);
-					else sem_post(&r->sem);
+					// (a request's last access here: the decrement that completes a group
+					// lets its fiber resume and release the requests)
+					if(r->fiber) {
+						if(!r->group || r->group->fetch_sub(1) == 1) wake.push_back(r->fiber);
+					} else {
+						sem_post(&r->sem);
+					}
 				}
 				if(!wake.empty()) bt2gf::wake_many(wake.data(), wake.size());
 			}
@@ -1171,6 +1222,15 @@ bool __wrap__ZN9SwAligner13nextAlignmentER8SwResultlR12RandomSource(SwAligner* s
 
 }  // extern "C"
 
+// the speculative DP prefetch (below): align()'s DP among those it ran
+namespace {
+struct SpecEntry;
+SpecEntry* spec_find(const DpReq& q, int64_t refl);
+void spec_use(DpReq& q, SpecEntry* e);
+void spec_check(const DpReq& q, SpecEntry* e);
+bool spec_verify();
+}  // namespace
+
 // align(): the engine's fill + gather + sort and the whole nextAlignment loop
 // of this DP, on the window initRef built (rf_[rfi_ .. rff_] plus the extra
 // right column, aligner_sw.cpp:171-253) and the DPRect's trim and core
@@ -1198,8 +1258,14 @@ bool SwAlignerAcc::gpu_align(TAlScore& best, bool& served) {
 	q.rect.corel = (int32_t)rect_->corel;
 	q.rect.corer = (int32_t)rect_->corer;
 	q.rect.pad = 0;
-	q.win.assign((const uint8_t*)rf_ + rfi_, (const uint8_t*)rf_ + rfi_ + ncol + 1);
-	g_disp.submit(&q);
+	SpecEntry* se = spec_find(q, rect_->refl);
+	if(se && !spec_verify()) {
+		spec_use(q, se);
+	} else {
+		q.win.assign((const uint8_t*)rf_ + rfi_, (const uint8_t*)rf_ + rfi_ + ncol + 1);
+		g_disp.submit(&q);
+		if(se) spec_check(q, se);
+	}
 	if(q.cpu) return false;      // served = false: the reference's align() runs
 	const bt2g_sw_result& o = q.o;
 	static const bool dump = getenv("BT2G_ADAPTER_DUMP") != nullptr;
@@ -1362,7 +1428,7 @@ struct ExtTable {
 	std::vector<bt2g_ext_in> keys;
 	std::vector<bt2g_ext_out> vals;
 };
-thread_local ExtTable t_ext;
+
 
 // ranges handed to GroupWalk2S::init during one prioritizeSATups / eeSaTups call
 struct GwRange {
@@ -1374,17 +1440,243 @@ struct GwTable {
 	bool on = false;
 	std::vector<GwRange> ranges;
 };
-thread_local GwTable t_gw;
+// per worker (fiber): a fiber may be suspended inside the reference's
+// prioritizeSATups (a contended lock yields, bt2g_fibers.cpp), and the other
+// fibers of its carrier must not see its tables
+const size_t SPEC_MAX = 32;
+
+struct SpecEntry {
+	int32_t fw, minsc, enable8;
+	uint32_t refidx, ncol;
+	int64_t refl;
+	bt2g_sw_rect rect;
+	bool ready = false, used = false;
+	bt2g_sw_result o;
+	int32_t naln = 0;
+	uint32_t cap = 0, maxaln = 0, maxedit = 0;
+	bool cpu = false;
+	DpState st;
+};
+
+struct SpecCtx {
+	bool on = false;               // inside an unpaired extendSeeds call
+	const Read* rd = nullptr;
+	const Scoring* sc = nullptr;
+	TAlScore minsc = 0;
+	int nceil = 0;
+	size_t maxhalf = 0, cminlen = 0;
+	bool doUngapped = false, enable8 = true;
+	std::vector<SpecEntry*> entries;   // this extendSeeds call's prefetched DPs
+	std::vector<SpecEntry*> spare;
+	void clear() {
+		for(SpecEntry* e : entries) spare.push_back(e);
+		entries.clear();
+	}
+};
+struct DrvState {
+	ExtTable ext;
+	GwTable gw;
+	SpecCtx spec;
+};
+DrvState& drv() {
+	void** slot = bt2gf::local();
+	if(!slot) {
+		thread_local DrvState t;
+		return t;
+	}
+	if(!*slot) *slot = new DrvState();
+	return *static_cast<DrvState*>(*slot);
+}
+
+// ---- speculative DP prefetch --------------------------------------------------
+// SwDriver::extendSeeds (aligner_sw_driver.cpp:756-1297) resolves one seed-hit
+// element at a time and, for each new diagonal, frames a rectangle and runs a
+// DP (initRef + align) -- one engine round trip per DP, 5.5 per read at
+// 3.1 Gbp (r03l), each waiting on a whole batch.  But once prioritizeSATups
+// has chosen the ranges and their rows are resolved, every DP the loop can
+// request at the current minimum score is known up to the loop's random visit
+// order: for each element, joinedToTextOff + frameSeedExtensionRect with the
+// loop's own arguments (aligner_sw_driver.cpp:935-1105).  So right there the
+// binding frames them all (distinct diagonals, at most SPEC_MAX) and runs them
+// in one group request; align() then takes its DP's result from here when the
+// problem is the same one (same strand, reference, rectangle, minimum score,
+// u8 choice; the read is fixed for the extendSeeds call), else asks the
+// engine as before.  The prefetched problems read the reference from HBM
+// (the engine's resident copy) where align()'s own request carries initRef's
+// window: the same bytes (rectangle trimming at reference ends, Ns outside
+// them, masks 1 << code; pinned at full size by bench.py's parity sample, and
+// here by BT2G_SPEC_VERIFY=1, which runs every hit again as a normal request
+// and counts differences).  Nothing the reference decides changes: align()
+// returns what the engine computes for that problem either way.
+SpecCtx& spec() {
+	DrvState& d = drv();
+	return d.spec;
+}
+
+bool spec_enabled() {
+	static const bool on = [] {
+		const char* e = getenv("BT2G_SPEC");
+		return !(e && e[0] == '0') && bt2gf::enabled();
+	}();
+	return on;
+}
+bool spec_verify() {
+	static const bool on = getenv("BT2G_SPEC_VERIFY") != nullptr;
+	return on;
+}
+
+// SwDriver's ranges (protected members; no added members: same layout)
+struct SwDriverAcc : public SwDriver {
+	const EList<SATupleAndPos, 16>& sp() const { return satpos_; }
+};
+
+void spec_prefetch(const SwDriver* sd, const Ebwt& ebwtFw) {
+	SpecCtx& x = spec();
+	x.clear();
+	const Read& rd = *x.rd;
+	const size_t rdlen = rd.length();
+	bt2g_scoring bs;
+	if(rdlen == 0 || rdlen > BT2G_MAX_READ_LEN || rdlen >= x.cminlen || !to_scoring(*x.sc, bs) ||
+	   x.minsc < std::numeric_limits<int32_t>::min() || x.minsc > std::numeric_limits<int32_t>::max())
+		return;
+	const Scoring& sc = *x.sc;
+	const int readGaps = sc.maxReadGaps(x.minsc, rdlen), refGaps = sc.maxRefGaps(x.minsc, rdlen);
+	if(x.doUngapped && readGaps == 0 && refGaps == 0) return;   // the loop's ungapped path, no DP
+	DynProgFramer dpframe(!gReportOverhangs);
+	const EList<SATupleAndPos, 16>& sp = static_cast<const SwDriverAcc*>(sd)->sp();
+	struct Diag { uint32_t tidx; int64_t refoff; bool fw; };
+	std::vector<Diag> seen;
+	std::vector<DpReq*> reqs;
+	std::vector<std::unique_ptr<DpReq>> own;
+	for(size_t i = 0; i < sp.size() && x.entries.size() < SPEC_MAX; i++) {
+		const SATuple& sat = sp[i].sat;
+		const bool fw = sp[i].pos.fw;
+		uint32_t rdoff = sp[i].pos.rdoff;
+		const uint32_t seedhitlen = sp[i].pos.seedlen;
+		if(!fw) rdoff = (uint32_t)(rdlen - rdoff - seedhitlen);
+		for(size_t elt = 0; elt < sat.size() && x.entries.size() < SPEC_MAX; elt++) {
+			const TIndexOffU off = sat.offs[elt];
+			if(off == OFF_MASK) continue;
+			TIndexOffU tidx = 0, toff = 0, tlen = 0;
+			bool straddled = false;
+			ebwtFw.joinedToTextOff(sat.key.len, off, tidx, toff, tlen, false, straddled);
+			if(tidx == OFF_MASK) continue;
+			const int64_t refoff = (int64_t)toff - rdoff;
+			bool dup = false;
+			for(const Diag& d : seen) dup = dup || (d.tidx == tidx && d.refoff == refoff && d.fw == fw);
+			if(dup) continue;
+			seen.push_back(Diag{tidx, refoff, fw});
+			DPRect rect;
+			if(!dpframe.frameSeedExtensionRect(refoff, rdlen, tlen, readGaps, refGaps, (size_t)x.nceil, x.maxhalf, rect))
+				continue;
+			SpecEntry* e;
+			if(!x.spare.empty()) {
+				e = x.spare.back();
+				x.spare.pop_back();
+			} else {
+				e = new SpecEntry();
+			}
+			e->fw = fw ? 1 : 0;
+			e->minsc = (int32_t)x.minsc;
+			e->enable8 = x.enable8 ? 1 : 0;
+			e->refidx = (uint32_t)tidx;
+			e->ncol = (uint32_t)(rect.refr + 1 - rect.refl);
+			e->refl = rect.refl;
+			e->rect.triml = (int32_t)rect.triml;
+			e->rect.corel = (int32_t)rect.corel;
+			e->rect.corer = (int32_t)rect.corer;
+			e->rect.pad = 0;
+			e->ready = e->used = false;
+			x.entries.push_back(e);
+			DpReq* q = new DpReq(bs, e->enable8, rdlen > 1024, &e->st);
+			own.emplace_back(q);
+			q->r.set(rd.patFw, rd.qual);
+			memset(&q->p, 0, sizeof(q->p));
+			q->p.fw = e->fw;
+			q->p.refidx = e->refidx;
+			q->p.ncol = e->ncol;
+			q->p.minsc = e->minsc;
+			q->p.refl = e->refl;
+			q->p.win_off = -1;          // the engine's resident reference
+			q->rect = e->rect;
+			reqs.push_back(q);
+		}
+	}
+	if(reqs.empty()) return;
+	g_disp.submit_group(reinterpret_cast<Req* const*>(reqs.data()), reqs.size());
+	g_spec_groups++;
+	g_spec_dps += reqs.size();
+	for(size_t k = 0; k < reqs.size(); k++) {
+		SpecEntry* e = x.entries[k];
+		const DpReq* q = reqs[k];
+		e->o = q->o;
+		e->naln = q->naln;
+		e->cap = q->cap;
+		e->maxaln = q->maxaln;
+		e->maxedit = q->maxedit;
+		e->cpu = q->cpu;
+		e->ready = true;
+	}
+}
+
+}  // namespace
+
+namespace {
+
+// align()'s DP among the prefetched ones (nullptr: not prefetched)
+SpecEntry* spec_find(const DpReq& q, int64_t refl) {
+	if(!spec_enabled() || !bt2gf::self()) return nullptr;
+	SpecCtx& x = spec();
+	if(!x.on) return nullptr;
+	for(SpecEntry* e : x.entries)
+		if(e->ready && !e->used && !e->cpu && e->fw == q.p.fw && e->refidx == q.p.refidx && e->ncol == q.p.ncol &&
+		   e->minsc == q.p.minsc && e->enable8 == q.enable8 && e->refl == refl && e->rect.triml == q.rect.triml &&
+		   e->rect.corel == q.rect.corel && e->rect.corer == q.rect.corer)
+			return e;
+	return nullptr;
+}
+
+// its outputs moved into q and q's DpState, as run_dp leaves them
+void spec_use(DpReq& q, SpecEntry* e) {
+	e->used = true;
+	g_spec_hits++;
+	q.o = e->o;
+	q.naln = e->naln;
+	q.cap = e->cap;
+	q.maxaln = e->maxaln;
+	q.maxedit = e->maxedit;
+	q.cpu = false;
+	DpState& st = *q.st;
+	st.cands.swap(e->st.cands);
+	st.fates.swap(e->st.fates);
+	st.alns.swap(e->st.alns);
+	st.edits.swap(e->st.edits);
+}
+
+// BT2G_SPEC_VERIFY: the prefetched answer against align()'s own request
+void spec_check(const DpReq& q, SpecEntry* e) {
+	e->used = true;
+	g_spec_hits++;
+	const DpState& st = *q.st;
+	auto same = [](const void* a, const void* b, size_t n) { return n == 0 || memcmp(a, b, n) == 0; };
+	const bool ok = same(&e->o, &q.o, sizeof(q.o)) && e->naln == q.naln && e->st.cands.size() == st.cands.size() &&
+	                same(e->st.cands.data(), st.cands.data(), sizeof(bt2g_sw_cand) * st.cands.size()) &&
+	                e->st.fates == st.fates && e->st.alns.size() == st.alns.size() &&
+	                same(e->st.alns.data(), st.alns.data(), sizeof(bt2g_sw_aln) * st.alns.size()) &&
+	                e->st.edits.size() == st.edits.size() &&
+	                same(e->st.edits.data(), st.edits.data(), sizeof(bt2g_edit) * st.edits.size());
+	if(!ok) g_spec_verify_bad++;
+}
+
 
 const size_t MAX_ROWS = 8192;    // rows per read per request (the rest: CPU getOffset)
 
 void resolve_rows(const Ebwt& ebwtFw) {
-	t_gw.on = false;
-	if(t_gw.ranges.empty()) return;
-	// this fiber's ranges: the request below yields, and the carrier's other
-	// fibers reuse t_gw meanwhile
+	drv().gw.on = false;
+	if(drv().gw.ranges.empty()) return;
+	// the ranges leave the table before the request below yields
 	std::vector<GwRange> ranges;
-	ranges.swap(t_gw.ranges);
+	ranges.swap(drv().gw.ranges);
 	OffReq q;
 	std::vector<std::pair<size_t, size_t>> where;    // (range, element) of each row
 	for(size_t r = 0; r < ranges.size(); r++) {
@@ -1453,7 +1745,7 @@ void GroupWalk2S<TSlice, 16>::init(const Ebwt& ebwtFw, const BitPairReference& r
 	// (AlignmentCache::addOnTheFlyImpl above only reserves them); rows resolved
 	// earlier in this read are resolved again, to the same offsets
 	static_cast<TSliceAcc&>(sa.offs).fill(OFF_MASK);
-	if(t_gw.on) t_gw.ranges.push_back(GwRange{sa.topf, sa.size(), sa.offs});
+	if(drv().gw.on) drv().gw.ranges.push_back(GwRange{sa.topf, sa.size(), sa.offs});
 }
 
 template <>
@@ -1476,7 +1768,7 @@ void SwDriver::prioritizeSATups(const Read& read, SeedResults& sh, const Ebwt& e
                                 bool szsq, size_t nsm, AlignmentCacheIface& ca, RandomSource& rnd, WalkMetrics& wlm,
                                 PerReadMetrics& prm, size_t& nelt_out, bool all) {
 	const bool eng = drv_engine();
-	t_ext.on = false;
+	drv().ext.on = false;
 	if(eng && doExtend && ebwtBw != NULL && read.length() > 0 && read.length() <= BT2G_MAX_READ_LEN) {
 		// every range the loop at aligner_sw_driver.cpp:519-604 visits, in its order
 		ExtReq q;
@@ -1507,24 +1799,25 @@ void SwDriver::prioritizeSATups(const Read& read, SeedResults& sh, const Ebwt& e
 		if(!q.in.empty()) {
 			g_disp.submit(&q);
 			count(ST_EXT, true);
-			t_ext.keys.assign(q.in.begin(), q.in.end());
-			t_ext.vals.assign(q.out.data(), q.out.data() + q.out.size());
-			t_ext.on = true;
+			drv().ext.keys.assign(q.in.begin(), q.in.end());
+			drv().ext.vals.assign(q.out.data(), q.out.data() + q.out.size());
+			drv().ext.on = true;
 		}
 	}
-	t_gw.ranges.clear();
-	t_gw.on = eng;
+	drv().gw.ranges.clear();
+	drv().gw.on = eng;
 	bt2g_real__ZN8SwDriver16prioritizeSATupsERK4ReadR11SeedResultsRK4EbwtPS6_RK16BitPairReferenceimbbbmR19AlignmentCacheIfaceR12RandomSourceR11WalkMetricsR14PerReadMetricsRmb(
 		this, read, sh, ebwtFw, ebwtBw, ref, seedmms, maxelt, doExtend, lensq, szsq, nsm, ca, rnd, wlm, prm, nelt_out, all);
-	t_ext.on = false;
+	drv().ext.on = false;
 	resolve_rows(ebwtFw);
+	if(spec_enabled() && spec().on) spec_prefetch(this, ebwtFw);
 }
 
 bool SwDriver::eeSaTups(const Read& rd, SeedResults& sh, const Ebwt& ebwt, const BitPairReference& ref,
                         RandomSource& rnd, WalkMetrics& wlm, SwMetrics& swmSeed, size_t& nelt_out, size_t maxelt,
                         bool all) {
-	t_gw.ranges.clear();
-	t_gw.on = drv_engine();
+	drv().gw.ranges.clear();
+	drv().gw.on = drv_engine();
 	bool ret = bt2g_real__ZN8SwDriver8eeSaTupsERK4ReadR11SeedResultsRK4EbwtRK16BitPairReferenceR12RandomSourceR11WalkMetricsR9SwMetricsRmmb(
 		this, rd, sh, ebwt, ref, rnd, wlm, swmSeed, nelt_out, maxelt, all);
 	resolve_rows(ebwt);
@@ -1534,15 +1827,15 @@ bool SwDriver::eeSaTups(const Read& rd, SeedResults& sh, const Ebwt& ebwt, const
 void SwDriver::extend(const Read& rd, const Ebwt& ebwtFw, const Ebwt* ebwtBw, TIndexOffU topf, TIndexOffU botf,
                       TIndexOffU topb, TIndexOffU botb, bool fw, size_t off, size_t len, PerReadMetrics& prm,
                       size_t& nlex, size_t& nrex) {
-	if(t_ext.on) {
-		const std::vector<bt2g_ext_in>& K = t_ext.keys;
+	if(drv().ext.on) {
+		const std::vector<bt2g_ext_in>& K = drv().ext.keys;
 		for(size_t i = 0; i < K.size(); i++) {
 			const bt2g_ext_in& k = K[i];
 			if(k.topf == topf && k.botf == botf && k.topb == topb && k.botb == botb && (k.fw != 0) == fw && k.off == off &&
 			   k.len == len) {
-				nlex += t_ext.vals[i].nlex;
-				nrex += t_ext.vals[i].nrex;
-				prm.nSdFmops += t_ext.vals[i].fmops;
+				nlex += drv().ext.vals[i].nlex;
+				nrex += drv().ext.vals[i].nrex;
+				prm.nSdFmops += drv().ext.vals[i].fmops;
 				return;
 			}
 		}
@@ -1588,4 +1881,53 @@ bool AlignmentCache::addOnTheFlyImpl(QVal& qv, const SAKey& sak, TIndexOffU topf
 		}
 	}
 	return true;
+}
+
+// ---- SwDriver::extendSeeds (aligner_sw_driver.cpp:756-1297) -------------------
+// The unpaired extension loop, unchanged; the binding only records the
+// arguments its DPs are framed with, for the speculative prefetch above.
+extern "C" int __real__ZN8SwDriver11extendSeedsER4ReadbR11SeedResultsRK4EbwtPS5_RK16BitPairReferenceR9SwAlignerRK7ScoringiiiRlimbmmmmmbbmmbiR19AlignmentCacheIfaceR12RandomSourceR11WalkMetricsR9SwMetricsR14PerReadMetricsP11AlnSinkWrapbRb(
+	SwDriver*, Read&, bool, SeedResults&, const Ebwt&, const Ebwt*, const BitPairReference&, SwAligner&, const Scoring&,
+	int, int, int, TAlScore&, int, size_t, bool, size_t, size_t, size_t, size_t, size_t, bool, bool, size_t, size_t, bool,
+	int, AlignmentCacheIface&, RandomSource&, WalkMetrics&, SwMetrics&, PerReadMetrics&, AlnSinkWrap*, bool, bool&);
+
+extern "C" int __wrap__ZN8SwDriver11extendSeedsER4ReadbR11SeedResultsRK4EbwtPS5_RK16BitPairReferenceR9SwAlignerRK7ScoringiiiRlimbmmmmmbbmmbiR19AlignmentCacheIfaceR12RandomSourceR11WalkMetricsR9SwMetricsR14PerReadMetricsP11AlnSinkWrapbRb(
+	SwDriver* self, Read& rd, bool mate1, SeedResults& sh, const Ebwt& ebwtFw, const Ebwt* ebwtBw,
+	const BitPairReference& ref, SwAligner& swa, const Scoring& sc, int seedmms, int seedlen, int seedival,
+	TAlScore& minsc, int nceil, size_t maxhalf, bool doUngapped, size_t maxIters, size_t maxUg, size_t maxDp,
+	size_t maxUgStreak, size_t maxDpStreak, bool doExtend, bool enable8, size_t cminlen, size_t cpow2, bool doTri,
+	int tighten, AlignmentCacheIface& ca, RandomSource& rnd, WalkMetrics& wlm, SwMetrics& swmSeed,
+	PerReadMetrics& prm, AlnSinkWrap* msink, bool reportImmediately, bool& exhaustive) {
+	const bool sp = spec_enabled() && bt2gf::self() != nullptr;
+	if(sp) {
+		SpecCtx& x = spec();
+		x.clear();
+		x.on = true;
+		x.rd = &rd;
+		x.sc = &sc;
+		x.minsc = minsc;          // (the loop may tighten it later: those DPs miss)
+		x.nceil = nceil;
+		x.maxhalf = maxhalf;
+		x.cminlen = cminlen;
+		x.doUngapped = doUngapped;
+		x.enable8 = enable8;
+	}
+	int ret;
+	try {
+		ret = __real__ZN8SwDriver11extendSeedsER4ReadbR11SeedResultsRK4EbwtPS5_RK16BitPairReferenceR9SwAlignerRK7ScoringiiiRlimbmmmmmbbmmbiR19AlignmentCacheIfaceR12RandomSourceR11WalkMetricsR9SwMetricsR14PerReadMetricsP11AlnSinkWrapbRb(
+			self, rd, mate1, sh, ebwtFw, ebwtBw, ref, swa, sc, seedmms, seedlen, seedival, minsc, nceil, maxhalf,
+			doUngapped, maxIters, maxUg, maxDp, maxUgStreak, maxDpStreak, doExtend, enable8, cminlen, cpow2, doTri,
+			tighten, ca, rnd, wlm, swmSeed, prm, msink, reportImmediately, exhaustive);
+	} catch(...) {
+		if(sp) {
+			spec().on = false;
+			spec().clear();
+		}
+		throw;
+	}
+	if(sp) {
+		spec().on = false;
+		spec().clear();
+	}
+	return ret;
 }

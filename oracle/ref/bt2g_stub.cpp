@@ -32,6 +32,8 @@ int bt2ref_sw_bt(const char* seq, const char* qual, int fw, const uint8_t* rfmas
 void bt2ref_extend(void* vh, int n, const char** seqs, const char** quals, const int32_t* fw, const uint32_t* off,
                    const uint32_t* len, const uint32_t* tb, uint32_t* out);
 void bt2ref_get_offsets(void* vh, int n, const uint32_t* rows, uint32_t* out);
+int bt2ref_get_stretch(void* vh, uint32_t refidx, uint64_t off, uint64_t len, uint8_t* dst);
+uint64_t bt2ref_ref_len(void* vh, uint32_t refidx);
 void bt2ref_ungapped(void* vh, int n, const char** seqs, const char** quals, const uint8_t* fws,
                      const uint32_t* refidx, const int64_t* off, const int64_t* minsc, const void* sp,
                      int ohang, int maxedit, int64_t* out, int32_t* edits);
@@ -179,7 +181,7 @@ int bt2g_ungapped(bt2g_ctx* c, const uint8_t* reads, const uint8_t* quals, uint3
 	return BT2G_OK;
 }
 
-int bt2g_sw_align_bt(bt2g_ctx*, const uint8_t* reads, const uint8_t* quals, uint32_t stride, const uint32_t* lens,
+int bt2g_sw_align_bt(bt2g_ctx* c, const uint8_t* reads, const uint8_t* quals, uint32_t stride, const uint32_t* lens,
                      const bt2g_sw_problem* probs, uint32_t nprob, const uint8_t* windows, uint64_t,
                      const bt2g_sw_rect* rects, const bt2g_scoring* sc, int enable8, uint32_t cap, bt2g_sw_result* res,
                      bt2g_sw_cand* cands, uint32_t maxaln, uint32_t maxedit, int32_t* naln, bt2g_sw_aln* alns,
@@ -187,10 +189,26 @@ int bt2g_sw_align_bt(bt2g_ctx*, const uint8_t* reads, const uint8_t* quals, uint
 	int rc = BT2G_OK;
 	for(uint32_t i = 0; i < nprob; i++) {
 		const bt2g_sw_problem& p = probs[i];
-		if(p.win_off < 0 || !rects) return fail(BT2G_ERR_ARG, "stub: explicit windows and rects only");
+		if(!rects) return fail(BT2G_ERR_ARG, "stub: rects required");
 		std::string s = ascii(reads + (size_t)p.read * stride, lens[p.read]);
 		std::string q = qstr(quals + (size_t)p.read * stride, lens[p.read]);
+		// the caller's window, or (win_off < 0) the reference's own bases at
+		// [refl, refl + ncol], N outside the reference, as masks (initRef's window)
+		std::vector<uint8_t> own;
 		const uint8_t* rf = windows + p.win_off;
+		if(p.win_off < 0) {
+			own.assign((size_t)p.ncol + 1, 16);
+			const int64_t rl = (int64_t)bt2ref_ref_len(c->ref, p.refidx);
+			for(uint32_t j = 0; j <= p.ncol; j++) {
+				const int64_t pos = p.refl + (int64_t)j;
+				if(pos >= 0 && pos < rl) {
+					uint8_t b;
+					bt2ref_get_stretch(c->ref, p.refidx, (uint64_t)pos, 1, &b);
+					own[j] = (uint8_t)(1u << (b > 4 ? 4 : b));
+				}
+			}
+			rf = own.data();
+		}
 		int64_t o[7];
 		std::vector<int64_t> cc(3 * (size_t)cap + 3);
 		bt2ref_sw(s.c_str(), q.c_str(), p.fw, rf, (int)p.ncol, p.minsc, sc, enable8, (int)cap, o, cc.data(), nullptr);

@@ -202,6 +202,12 @@ int bt2ref_get_stretch(void* vh, uint32_t refidx, uint64_t off, uint64_t len, ui
 	return 0;
 }
 
+// Length of reference `refidx` (BitPairReference::approxLen, Ns included).
+uint64_t bt2ref_ref_len(void* vh, uint32_t refidx) {
+	RefHandle* h = (RefHandle*)vh;
+	return (uint64_t)h->refs->approxLen(refidx);
+}
+
 // SeedAligner::exactSweep over n reads (ASCII seq/qual, NUL-terminated).
 // out per read: mineFw, mineRc, nelt, exact fw [top,bot), exact rc [top,bot), bwops
 void bt2ref_exact_sweep(void* vh, int n, const char** seqs, const char** quals,

@@ -22,8 +22,11 @@ for f in sys.argv[1:]:
         ec = x.get("engine_calls")
         if not ec:
             continue
-        names = [k for k in ec if isinstance(ec[k], list) and k not in ("queue_ms", "resume_ms")]
+        names = [k for k in ec if isinstance(ec[k], list) and k not in ("queue_ms", "resume_ms", "spec")]
         for k, v in ec.items():
+            if k == "spec":
+                print(f"   spec prefetch: groups {v[0]}, DPs {v[1]}, hits {v[2]}, verify mismatches {v[3]}")
+                continue
             if k in ("queue_ms", "resume_ms"):
                 print(f"   {k} per call: " + ", ".join(f"{n}:{q / max(ec[n][0], 1):.2f}" for n, q in zip(names, v)))
                 continue

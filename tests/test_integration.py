@@ -94,12 +94,14 @@ def _compare(dropin, base, chunks, args, dirpath, long_reads=False, extra_env=No
     assert not bad, f"{len(bad)} SAM records differ, first:\nref  {bad[0][0][:400]}\nbind {bad[0][1][:400]}"
     assert st is not None, "binding wrote no call counts"
     for k, v in st.items():
-        if k in ("kernels", "queue_ms", "resume_ms"):       # (not seams: timing breakdowns)
+        if k in ("kernels", "queue_ms", "resume_ms", "spec"):   # (not seams: timing breakdowns, prefetch counts)
             continue
         gpu, cpu = v[0], v[1]                    # calls served by the engine / by the CPU path
         if not long_reads:
             assert cpu == 0, f"{k}: {cpu} calls fell back to the CPU"
     assert st["exact_sweep"][0] > 0 and st["sw_dp"][0] > 0 and st["seed_search"][0] > 0
+    if "spec" in st:
+        assert st["spec"][3] == 0, f"{st['spec'][3]} prefetched DPs differed from align()'s own (BT2G_SPEC_VERIFY)"
     return t_ref, t_new, len(a), st
 
 
