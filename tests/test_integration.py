@@ -132,6 +132,17 @@ def test_binding_multi_device_cpu(indexes, tmp_path, mode, args, n):
     _compare(SRV_STUB, base, chunks, args, str(tmp_path), extra_env={"BT2G_DEVICES": "0,1"})
 
 
+def test_binding_spec_prefetch_cpu(indexes, tmp_path):
+    """$BT2G_SPEC=1 (speculative DP prefetch, off by default): align() takes prefetched
+    results only for identical problems; BT2G_SPEC_VERIFY re-runs each and counts differences."""
+    _need(rs.SERVER, rs.CLIENT, SRV_STUB)
+    base, idx = indexes["synth"]
+    chunks = _reads(idx, "ee", 1500, 11, str(tmp_path))
+    _, _, _, st = _compare(SRV_STUB, base, chunks, [], str(tmp_path),
+                           extra_env={"BT2G_SPEC": "1", "BT2G_SPEC_VERIFY": "1"})
+    assert st["spec"][2] > 0, "no align() call was served by a prefetched DP"
+
+
 def test_binding_longreads_cpu(indexes, tmp_path):
     """configs[0]: lambda, example/reads/longreads.fq (6 000 reads of 40-2 561 bp)."""
     _need(rs.SERVER, rs.CLIENT, SRV_STUB, LONGREADS)
