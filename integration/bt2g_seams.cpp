@@ -157,6 +157,13 @@ void init_env() {
 		// dispatcher threads sleep in their stream waits: the server's workers need the
 		// cores (the runtime's blocking wait still spins: r03d, 21 % of the CPU)
 		setenv("BT2G_SYNC", "poll", 0);
+		// one HIP hardware queue per stream (a context per seam dispatcher, ~10
+		// streams): with HIP's default of 4 -- also what the GPU box exports -- a
+		// 0.05 ms seed-search kernel waits behind other seams' DP kernels on a shared
+		// in-order queue (r03p at 3.1 Gbp: 29.4k -> 43.6k reads/s with 16 queues).
+		// Set before the first HIP call of the process; $BT2G_HW_QUEUES overrides.
+		const char* hq = getenv("BT2G_HW_QUEUES");
+		setenv("GPU_MAX_HW_QUEUES", hq && atoi(hq) > 0 ? hq : "16", 1);
 		const char* sp = getenv("BT2G_ADAPTER_STATS");
 		if(sp) {
 			strncpy(g_stats_path, sp, sizeof(g_stats_path) - 1);

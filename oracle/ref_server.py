@@ -38,13 +38,12 @@ CHUNK = 10_000
 
 def dropin_env(index_base, stats_path=None, device=0):
     """Environment of the drop-in server (integration/): the index its engines
-    open, where the binding writes its call counts, and one HIP hardware queue
-    per stream -- the binding drives ~20 streams (a context per seam
-    dispatcher), and with HIP's default of 4 hardware queues a 0.07 ms kernel
-    waits behind other seams' kernels on a shared queue (r03h: ~2 ms of every
-    engine call).  GPU_MAX_HW_QUEUES from the caller's environment wins."""
-    env = {"BT2G_INDEX": index_base, "BT2G_DEVICE": str(device),
-           "GPU_MAX_HW_QUEUES": os.environ.get("GPU_MAX_HW_QUEUES", "24")}
+    open and where the binding writes its call counts.  (The binding sets one
+    HIP hardware queue per stream itself, GPU_MAX_HW_QUEUES=16 before its first
+    HIP call, whatever the caller's environment says -- the GPU box exports 4;
+    BT2G_HW_QUEUES overrides -- and the server is started with it too.)"""
+    hq = os.environ.get("BT2G_HW_QUEUES", "16")
+    env = {"BT2G_INDEX": index_base, "BT2G_DEVICE": str(device), "BT2G_HW_QUEUES": hq, "GPU_MAX_HW_QUEUES": hq}
     if stats_path:
         env["BT2G_ADAPTER_STATS"] = stats_path
     return env
