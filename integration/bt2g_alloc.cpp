@@ -20,8 +20,12 @@
 // shared depot in batches (one lock per batch), and a thread that finds its
 // cache empty takes a batch from the depot before it asks malloc.  Memory is
 // never returned to the system -- the server's working set is stable once the
-// first connections have run.  Blocks above 256 KiB (the alignment caches'
-// pools) go to malloc / free directly.  $BT2G_ALLOC=0 keeps glibc's allocator.
+// first connections have run.  Blocks up to 64 MiB are cached too (power-of-two
+// classes): freed big blocks (the alignment caches' pools, grown ELists) had
+// gone back to glibc, which trimmed the heap and grew it again one mprotect per
+// allocation (r03p at 3.1 Gbp: mprotect 14 % of the carriers' CPU, all of it
+// under this allocator's malloc calls).  Larger blocks go to malloc / free
+// directly.  $BT2G_ALLOC=0 keeps glibc's allocator.
 #include <errno.h>
 #include <stdint.h>
 #include <stdlib.h>
@@ -32,7 +36,7 @@
 
 namespace {
 
-const int NCLASS = 15;                  // 16 B .. 256 KiB
+const int NCLASS = 23;                  // 16 B .. 64 MiB
 const size_t MAXSZ = (size_t)16 << (NCLASS - 1);
 const size_t HDR = 16;                  // keeps the default new alignment (16)
 const uint32_t MAGIC_CACHED = 0xB72C0DE5u, MAGIC_MALLOC = 0xB72C0DE6u;
@@ -59,8 +63,13 @@ inline int cls_of(size_t n) {
 	return c;
 }
 inline size_t size_of(int c) { return (size_t)16 << c; }
-// blocks a thread keeps per class before half go to the depot (~4 MiB per class)
+// blocks a thread keeps per class before half go to the depot (~4 MiB per class
+// up to 256 KiB blocks, at least 64 of them; ~16 MiB and at least 2 beyond)
 inline int cap_of(int c) {
+	if(size_of(c) > ((size_t)256 << 10)) {
+		const size_t v = ((size_t)16 << 20) / size_of(c);
+		return v < 2 ? 2 : (int)v;
+	}
 	const size_t v = ((size_t)4 << 20) / size_of(c);
 	return v < 64 ? 64 : (v > 4096 ? 4096 : (int)v);
 }
@@ -147,7 +156,8 @@ void* alloc(size_t n) {
 			// refill from the depot (one lock for a batch)
 			Depot& d = depot();
 			Guard lk(d.mu[c]);
-			for(int i = 0; i < BATCH && d.head[c]; i++) {
+			const int nb = BATCH < cap_of(c) ? BATCH : cap_of(c);
+			for(int i = 0; i < nb && d.head[c]; i++) {
 				Node* b = d.head[c];
 				d.head[c] = b->next;
 				d.n[c]--;

@@ -42,6 +42,11 @@ size_t count();
 // ordinary thread): state that must not be shared by the fibers of a carrier.
 void** local();
 
+// $BT2G_MUTEX_PROF=<path>: contended pthread_mutex_lock call sites of fibers
+// (note: the wrapper; dump: "offset count" lines, written at SIGTERM)
+void mutex_prof_note(void* ra);
+void mutex_prof_dump();
+
 }  // namespace bt2gf
 
 #endif

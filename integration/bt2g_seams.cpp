@@ -137,6 +137,7 @@ void write_stats() {
 
 void on_term(int) {
 	write_stats();
+	bt2gf::mutex_prof_dump();
 	_exit(0);
 }
 

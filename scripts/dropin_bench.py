@@ -42,6 +42,9 @@ def main():
     ap.add_argument("--workdir", default="/tmp/dropin_bench")
     ap.add_argument("--skip-stock", action="store_true")
     ap.add_argument("--warmup-chunks", type=int, default=1, help="chunks sent untimed first (both servers)")
+    ap.add_argument("--dropin-args", default="",
+                    help="extra server options for the drop-in only, one string (throughput knobs that do not "
+                         "change alignments, e.g. --dropin-args='--reads-per-batch 4')")
     ap.add_argument("--dropin-binary", default="", help="default oracle/_ref/bowtie2-align-server-gpu "
                                                        "(-stub: the binding over the CPU stand-in)")
     a = ap.parse_args()
@@ -73,14 +76,15 @@ def main():
         chunks = rs.write_fastq_chunks(a.workdir, r, q)
     cpus = rs.host_cpus()
     threads = a.cpu_threads or cpus["usable"]
-    out = {"reads": a.reads, "mode": a.mode, "args": a.args, "genome_mb": a.genome_mb, "k": a.k, "host": cpus}
+    out = {"reads": a.reads, "mode": a.mode, "args": a.args, "dropin_args": a.dropin_args, "genome_mb": a.genome_mb,
+           "k": a.k, "host": cpus}
     sams = {}
     runs = [] if a.skip_stock else [("stock", rs.SERVER, threads)]
     runs.append(("dropin", a.dropin_binary or os.path.join(rs.REF_DIR, "bowtie2-align-server-gpu"), a.gpu_workers))
     for tag, binary, th in runs:
         stats = os.path.join(a.workdir, f"stats_{tag}.json")
         env = rs.dropin_env(base, stats)
-        with rs.Server(base, threads=th, args=a.args, binary=binary, env=env,
+        with rs.Server(base, threads=th, args=a.args + (a.dropin_args.split() if tag == "dropin" else []), binary=binary, env=env,
                        log_path=os.path.join(a.workdir, f"server_{tag}.log")) as s:
             log(f"{tag}: server ready in {s.load_s:.1f}s (-p {th})")
             dt, outs = s.run(chunks, k=a.k, warmup=chunks[:a.warmup_chunks])
