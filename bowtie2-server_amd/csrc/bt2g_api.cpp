@@ -821,8 +821,8 @@ static bool sw_packed_ok(const bt2g_scoring& sc, const SwConst& C, const int16_t
 static bool sw_use_packed(const bt2g_scoring& sc, const SwConst& C, const int16_t* mat, uint32_t stride,
                           uint32_t maxcol) {
 	const uint32_t S = (stride + 15u) / 16u;
-	if(S > 64u) return false;                      // one problem pair's rows across one wave at most
-	const uint64_t lds = (uint64_t)(64u / S) * sw_packed_group_words(maxcol, sc.local != 0) * 4u;
+	if(S > 128u) return false;                     // one problem pair's rows across two waves at most
+	const uint64_t lds = (uint64_t)(S > 64u ? 1u : 64u / S) * sw_packed_group_words(maxcol, sc.local != 0) * 4u;
 	return sw_packed_ok(sc, C, mat, stride) && lds <= 65536u;
 }
 

@@ -143,8 +143,12 @@ struct Half {
 //   bit 2  F != H(up) - rfgo      bit 3  E != H(left) - rdgo
 // (F-up / E-left being then the other source of F / E).  A walk step reads
 // one nibble and no neighbour, no column or row scan (sw_backtrace.hip KIND 2).
-template <bool LOCAL, bool SAMEGO, bool STORE, bool DEC = false>
-__global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu((STORE || LOCAL) ? BT2G_SW_WAVES_STORE : BT2G_SW_WAVES)))
+// WIDE (reads of 1025..2048 bases, S = 65..128): one problem pair per
+// workgroup of two waves; lane 63 hands its bottom row to lane 64 through LDS
+// (double-buffered, one barrier per step) where the DPP shift stops at the wave
+// edge.  (Before: one problem per lane in k_sw_fill, ~200 ms per 2 kb DP.)
+template <bool LOCAL, bool SAMEGO, bool STORE, bool DEC = false, bool WIDE = false>
+__global__ void __launch_bounds__(WIDE ? 128 : 64) __attribute__((amdgpu_waves_per_eu((STORE || LOCAL) ? BT2G_SW_WAVES_STORE : BT2G_SW_WAVES)))
 k_sw_sys(const bt2g_sw_problem* __restrict__ probs, uint32_t nprob, const uint8_t* __restrict__ reads,
             const uint8_t* __restrict__ quals, uint32_t stride, const uint32_t* __restrict__ lens,
             const uint8_t* __restrict__ windows, const uint8_t* __restrict__ ref_codes,
@@ -152,9 +156,9 @@ k_sw_sys(const bt2g_sw_problem* __restrict__ probs, uint32_t nprob, const uint8_
             uint32_t S, uint32_t ldsw, bt2g_sw_result* __restrict__ res, bt2g_sw_cand* __restrict__ cands,
             uint8_t* __restrict__ plane, uint64_t hslot, int hbytes) {
 	const uint32_t lane = threadIdx.x;
-	const uint32_t G = 64u / S;                  // problem pairs per wave
-	const uint32_t g = lane / S, k = lane % S;
-	const bool in_group = g < G;
+	const uint32_t G = WIDE ? 1u : 64u / S;      // problem pairs per wave (WIDE: per workgroup)
+	const uint32_t g = WIDE ? 0u : lane / S, k = WIDE ? lane : lane % S;
+	const bool in_group = WIDE ? lane < S : g < G;
 	const uint32_t base = blockIdx.x * 2u * G;
 	Half h[2];
 #pragma unroll
@@ -206,7 +210,7 @@ k_sw_sys(const bt2g_sw_problem* __restrict__ probs, uint32_t nprob, const uint8_
 	__shared__ uint8_t mmq[48];
 	__shared__ uint32_t lcnt[128], lmaxc[128];     // LOCAL: candidates per problem, their largest column
 	if(lane <= 40) mmq[lane] = (uint8_t)C.mmpen[lane];
-	if(LOCAL) {
+	if(LOCAL && lane < 64u) {
 		lcnt[lane] = lcnt[lane + 64u] = 0u;
 		lmaxc[lane] = lmaxc[lane + 64u] = 0u;
 	}
@@ -303,12 +307,26 @@ k_sw_sys(const bt2g_sw_problem* __restrict__ probs, uint32_t nprob, const uint8_
 	// u8-only padding rows (round16(nrow) - round8(nrow) = 8: its rows 8..15)
 	uint32_t bias[2] = {0u, 0u}, u8o = 0u;
 	if(LOCAL) {
+		__shared__ uint32_t wbias[2];         // WIDE: the group spans both waves
+		if(WIDE) {
+			if(lane < 2u) wbias[lane] = 0u;
+			__syncthreads();
+			if(in_group) {
+				atomicMax(&wbias[0], biasl[0]);
+				atomicMax(&wbias[1], biasl[1]);
+			}
+			__syncthreads();
+		}
 #pragma unroll
 		for(int x = 0; x < 2; x++) {
 			uint32_t b = 0u;
-			for(uint32_t t = 0; t < S; t++) {
-				const uint32_t o = (uint32_t)__shfl((int)biasl[x], (int)(g * S + t));
-				b = o > b ? o : b;
+			if(WIDE) {
+				b = wbias[x];
+			} else {
+				for(uint32_t t = 0; t < S; t++) {
+					const uint32_t o = (uint32_t)__shfl((int)biasl[x], (int)(g * S + t));
+					b = o > b ? o : b;
+				}
 			}
 			bias[x] = b;
 			const uint32_t r = h[x].nrow & 15u;
@@ -520,10 +538,24 @@ k_sw_sys(const bt2g_sw_problem* __restrict__ probs, uint32_t nprob, const uint8_
 	};
 	for(uint32_t t = 0; t < T; t++) {
 		// the lane above computed this lane's column in the previous step (DPP wave_shr:1)
-		const uint32_t hin = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)hout, 0x138, 0xf, 0xf, false);
-		const uint32_t fin = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)fout, 0x138, 0xf, 0xf, false);
-		const uint32_t mskin = STORE ? (uint32_t)__builtin_amdgcn_update_dpp(0, (int)mout, 0x138, 0xf, 0xf, false) : 0u;
-		const uint32_t cmin = LOCAL ? (uint32_t)__builtin_amdgcn_update_dpp(0, (int)cmout, 0x138, 0xf, 0xf, false) : 0u;
+		uint32_t hin = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)hout, 0x138, 0xf, 0xf, false);
+		uint32_t fin = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)fout, 0x138, 0xf, 0xf, false);
+		uint32_t mskin = STORE ? (uint32_t)__builtin_amdgcn_update_dpp(0, (int)mout, 0x138, 0xf, 0xf, false) : 0u;
+		uint32_t cmin = LOCAL ? (uint32_t)__builtin_amdgcn_update_dpp(0, (int)cmout, 0x138, 0xf, 0xf, false) : 0u;
+		if constexpr(WIDE) {
+			// across the wave edge: lane 63's previous step to lane 64 (a slot is
+			// rewritten two steps later, after lane 64 has passed the next barrier)
+			__shared__ uint32_t xch[2][4];
+			if(lane == 63u) {
+				uint32_t* b = xch[t & 1u];
+				b[0] = hout; b[1] = fout; b[2] = mout; b[3] = cmout;
+			}
+			__syncthreads();
+			if(lane == 64u) {
+				const uint32_t* b = xch[t & 1u];
+				hin = b[0]; fin = b[1]; mskin = b[2]; cmin = b[3];
+			}
+		}
 		const int j = (int)t - (int)k;
 		if(j < 0 || j >= (int)ncolmax) continue;
 		const uint32_t selx = nsel;
@@ -882,37 +914,52 @@ k_sw_sys(const bt2g_sw_problem* __restrict__ probs, uint32_t nprob, const uint8_
 }
 
 // All problems, u8 and i16 fills together (no partition needed); local: the
-// u8 and i16 local fills in one pass.
-void launch_sw_packed(bool local, const bt2g_sw_problem* probs, uint32_t nprob, const uint8_t* reads,
-                      const uint8_t* quals, uint32_t stride, const uint32_t* lens, const uint8_t* windows,
-                      const uint8_t* ref_codes, const uint64_t* ref_starts, const SwConst& C, int enable8,
-                      uint32_t cap, uint32_t max_cols, bt2g_sw_result* res, bt2g_sw_cand* cands, uint8_t* plane,
-                      uint64_t hslot, int hbytes, hipStream_t st) {
-	if(nprob == 0) return;
-	const uint32_t S = (stride + 15u) / 16u;     // <= 64 (stride <= BT2G_MAX_READ_LEN)
-	const uint32_t per_wave = 2u * (64u / S);
+// u8 and i16 local fills in one pass.  Reads up to 1024 bases: a wave holds
+// 64/S problem pairs; 1025..2048 bases: a two-wave workgroup per pair (WIDE).
+template <bool WIDE>
+static void launch_sys(bool local, const bt2g_sw_problem* probs, uint32_t nprob, const uint8_t* reads,
+                       const uint8_t* quals, uint32_t stride, const uint32_t* lens, const uint8_t* windows,
+                       const uint8_t* ref_codes, const uint64_t* ref_starts, const SwConst& C, int enable8,
+                       uint32_t cap, uint32_t max_cols, bt2g_sw_result* res, bt2g_sw_cand* cands, uint8_t* plane,
+                       uint64_t hslot, int hbytes, hipStream_t st) {
+	const uint32_t S = (stride + 15u) / 16u;     // <= 128 (stride <= BT2G_MAX_READ_LEN)
+	const uint32_t per_block = WIDE ? 2u : 2u * (64u / S);
 	const uint32_t ldsw = (max_cols + 1u) | 1u;   // >= ncol+1 (column pairs); odd: groups hit different banks
-	const dim3 grid((nprob + per_wave - 1) / per_wave), block(64);
-	const size_t lds = (per_wave / 2) * sw_packed_group_words(max_cols, local) * sizeof(uint32_t);
-#define BT2G_SYS(LO, SG, STO, ...)                                                                             \
-	hipLaunchKernelGGL((k_sw_sys<LO, SG, STO, ##__VA_ARGS__>), grid, block, lds, st, probs, nprob, reads, quals, stride, lens, \
-	                   windows, ref_codes, ref_starts, C, enable8, cap, max_cols, S, ldsw, res, cands, plane, hslot, \
-	                   hbytes)
+	const dim3 grid((nprob + per_block - 1) / per_block), block(WIDE ? 128 : 64);
+	const size_t lds = (per_block / 2) * sw_packed_group_words(max_cols, local) * sizeof(uint32_t);
+#define BT2G_SYS(LO, SG, STO, DE)                                                                              \
+	hipLaunchKernelGGL((k_sw_sys<LO, SG, STO, DE, WIDE>), grid, block, lds, st, probs, nprob, reads, quals, stride, \
+	                   lens, windows, ref_codes, ref_starts, C, enable8, cap, max_cols, S, ldsw, res, cands, plane,  \
+	                   hslot, hbytes)
 	const bool samego = C.rdgo == C.rfgo;
 	if(local) {
 		if(plane) {
-			if(samego) BT2G_SYS(true, true, true); else BT2G_SYS(true, false, true);
+			if(samego) BT2G_SYS(true, true, true, false); else BT2G_SYS(true, false, true, false);
 		} else {
-			if(samego) BT2G_SYS(true, true, false); else BT2G_SYS(true, false, false);
+			if(samego) BT2G_SYS(true, true, false, false); else BT2G_SYS(true, false, false, false);
 		}
 	} else if(plane && hbytes == 3) {
 		// decision nibbles (the plane's u8 layout: masks after 16S x pitch bytes)
 		hbytes = 1;
 		if(samego) BT2G_SYS(false, true, true, true); else BT2G_SYS(false, false, true, true);
 	} else if(plane) {
-		if(samego) BT2G_SYS(false, true, true); else BT2G_SYS(false, false, true);
+		if(samego) BT2G_SYS(false, true, true, false); else BT2G_SYS(false, false, true, false);
 	} else {
-		if(samego) BT2G_SYS(false, true, false); else BT2G_SYS(false, false, false);
+		if(samego) BT2G_SYS(false, true, false, false); else BT2G_SYS(false, false, false, false);
 	}
 #undef BT2G_SYS
+}
+
+void launch_sw_packed(bool local, const bt2g_sw_problem* probs, uint32_t nprob, const uint8_t* reads,
+                      const uint8_t* quals, uint32_t stride, const uint32_t* lens, const uint8_t* windows,
+                      const uint8_t* ref_codes, const uint64_t* ref_starts, const SwConst& C, int enable8,
+                      uint32_t cap, uint32_t max_cols, bt2g_sw_result* res, bt2g_sw_cand* cands, uint8_t* plane,
+                      uint64_t hslot, int hbytes, hipStream_t st) {
+	if(nprob == 0) return;
+	if((stride + 15u) / 16u > 64u)
+		launch_sys<true>(local, probs, nprob, reads, quals, stride, lens, windows, ref_codes, ref_starts, C, enable8,
+		                 cap, max_cols, res, cands, plane, hslot, hbytes, st);
+	else
+		launch_sys<false>(local, probs, nprob, reads, quals, stride, lens, windows, ref_codes, ref_starts, C, enable8,
+		                  cap, max_cols, res, cands, plane, hslot, hbytes, st);
 }

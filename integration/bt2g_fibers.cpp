@@ -61,6 +61,7 @@
 #include <atomic>
 #include <chrono>
 #include <condition_variable>
+#include <deque>
 #include <memory>
 #include <mutex>
 #include <thread>
@@ -174,6 +175,14 @@ std::mutex g_mu;                              // carriers, fiber handles
 // fibers waiting on each condition variable (woken by its notify_one/_all)
 std::mutex g_cv_mu;
 std::unordered_map<const void*, std::vector<Fiber*>> g_cv_waiters;
+// fibers a notify_all released but did not wake yet: each woken fiber wakes
+// the next once it holds the lock again (the "baton"), so they re-take the
+// mutex one after another instead of all at once -- every one still returns
+// from its wait, as notify_all requires.  (The reference's ready queue of
+// reads notifies all its waiters per pushed element, pat.h:1981-1985: with
+// thousands of idle workers that herd was 4.2M contended lock attempts per
+// 400k reads at --reads-per-batch 1, r03r.)
+std::unordered_map<const void*, std::deque<Fiber*>> g_cv_baton;
 std::vector<Carrier*> g_carriers;
 size_t g_next_carrier = 0;
 // fibers' std::thread ids: tagged in the top 16 bits (a pthread_t is a user-space
@@ -513,6 +522,20 @@ void __wrap__ZNSt6thread6detachEv(std::thread* self) {
 	__real__ZNSt6thread6detachEv(self);
 }
 
+// a fiber woken from `cv` holds the lock again: the next fiber a notify_all released goes
+static void pass_baton(const void* cv) {
+	Fiber* w = nullptr;
+	{
+		std::lock_guard<std::mutex> g(g_cv_mu);
+		auto it = g_cv_baton.find(cv);
+		if(it == g_cv_baton.end() || it->second.empty()) return;
+		w = it->second.front();
+		it->second.pop_front();
+	}
+	void* one = w;
+	wake_many(&one, 1);
+}
+
 void __wrap__ZNSt18condition_variable4waitERSt11unique_lockISt5mutexE(std::condition_variable* cv,
                                                                       std::unique_lock<std::mutex>& lk) {
 	Fiber* f = cur_fiber();
@@ -530,23 +553,27 @@ void __wrap__ZNSt18condition_variable4waitERSt11unique_lockISt5mutexE(std::condi
 	lk.unlock();
 	suspend(f, BLOCKED);
 	lk.lock();
+	pass_baton(cv);
 }
 
 // notify: fibers waiting on `cv` go back to their carriers, then the OS threads
+// (notify_all: the first now, the rest through the baton)
 static void wake_cv_fibers(const void* cv, bool all) {
-	std::vector<Fiber*> w;
+	Fiber* w = nullptr;
 	{
 		std::lock_guard<std::mutex> g(g_cv_mu);
 		auto it = g_cv_waiters.find(cv);
 		if(it == g_cv_waiters.end() || it->second.empty()) return;
-		if(all) {
-			w.swap(it->second);
-		} else {
-			w.push_back(it->second.front());
-			it->second.erase(it->second.begin());
+		w = it->second.front();
+		it->second.erase(it->second.begin());
+		if(all && !it->second.empty()) {
+			std::deque<Fiber*>& b = g_cv_baton[cv];
+			b.insert(b.end(), it->second.begin(), it->second.end());
+			it->second.clear();
 		}
 	}
-	wake_many(reinterpret_cast<void* const*>(w.data()), w.size());
+	void* one = w;
+	wake_many(&one, 1);
 }
 
 void __real__ZNSt18condition_variable10notify_allEv(std::condition_variable* cv);

@@ -205,3 +205,21 @@ def test_close_frees_reserved_scratch():
         torch.cuda.synchronize()
         free.append(torch.cuda.mem_get_info()[0])
     assert max(free) - min(free) < (1 << 30), free
+
+
+@pytest.mark.parametrize("local", [False, True], ids=["ee", "local"])
+def test_bt_long_reads_vs_oracle(eng, local):
+    """Reads of 1100..2048 bases (the two-wave systolic fill and its u16 plane):
+    every alignment, edit and candidate fate of the nextAlignment loop equals
+    the oracle's."""
+    from oracle.oracle import Oracle
+    orc = Oracle()
+    gen = get_index("lambda").ref_codes[0]
+    for L in (1100, 2048):
+        minsc = int(20 + 8 * np.log(L)) if local else int(-(0.6 + 0.6 * L))
+        codes, quals, lens, probs, rects = _synth_problems(gen, 16, 40 + L, length=L, maxgap=30, minsc=minsc)
+        res, cands, naln, alns, edits, fates = eng.sw_align_bt(codes, quals, lens, probs, rects=rects, local=local,
+                                                               cap=8192, maxaln=512, maxedit=2 * L + 8)
+        ea, ee, ef = _oracle_expect(orc, gen, codes, quals, probs, rects, local)
+        check_against(naln, alns, edits, fates, res, None, ea, ee, ef, f"long{L}")
+        assert (naln > 0).sum() > 8

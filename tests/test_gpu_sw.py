@@ -204,3 +204,54 @@ def test_sw_packed_vs_per_lane_local(eng, gaps):
     assert np.array_equal(c_p, c_g)
     assert 0 < res_p["aligned"].sum() < n
     assert (res_p["i16succ"] == 1).sum() > 0 and (res_p["u8succ"] == 1).sum() > 0
+
+
+@pytest.mark.parametrize("local", [False, True], ids=["ee", "local"])
+def test_sw_packed_wide_vs_per_lane(eng, local):
+    """Reads of 1025..2048 bases: the two-wave systolic fill (WIDE, S = 65..128
+    lanes per problem pair, lane 63 -> 64 through LDS) against the
+    one-problem-per-lane fill on ragged long problems (configs[0]'s longreads.fq
+    reach 2561 bp; the engines take up to BT2G_MAX_READ_LEN = 2048)."""
+    import bt2g
+    idx = get_index("lambda")
+    gen = idx.ref_codes[0]
+    rng = np.random.default_rng(8)
+    n = 48
+    stride = 2048
+    lens = rng.integers(1025, 2049, n).astype(np.uint32)
+    lens[:6] = [1025, 1040, 1500, 2047, 2048, 600]      # a short read in a wide batch too
+    codes = np.full((n, stride), 4, np.uint8)
+    quals = np.full((n, stride), 73, np.uint8)
+    pos = rng.integers(-50, len(gen) - 1000, n)
+    fw = rng.random(n) < 0.5
+    for i in range(n):
+        L = int(lens[i])
+        o = np.arange(pos[i], pos[i] + L)
+        c = np.where((o >= 0) & (o < len(gen)), gen[np.clip(o, 0, len(gen) - 1)], 4)
+        m = rng.random(L) < 0.03
+        c[m] = rng.integers(0, 5, m.sum())
+        if not fw[i]:
+            c = np.where(c > 3, 4, 3 - c)[::-1]
+        codes[i, :L] = c
+        quals[i, :L] = rng.integers(33, 75, L)
+    probs = np.zeros(n, bt2g.SWPROB_DTYPE)
+    probs["read"] = np.arange(n)
+    probs["fw"] = fw
+    probs["ncol"] = np.clip(lens.astype(np.int64) + rng.integers(-20, 100, n), 1, 2200)
+    probs["refl"] = pos - rng.integers(0, 40, n)
+    probs["win_off"] = -1
+    if local:
+        probs["minsc"] = np.where(rng.random(n) < 0.3, 10, (20 + 8 * np.log(lens)).astype(np.int64))
+        sc = bt2g.scoring(True)
+    else:
+        probs["minsc"] = np.where(rng.random(n) < 0.3, -(0.6 + 2.5 * lens).astype(np.int64),
+                                  -(0.6 + 0.6 * lens).astype(np.int64))
+        probs["minsc"][:2] = [-200, -254]                # u8 fills of long reads
+        sc = bt2g.scoring(False)
+    cap = 8192
+    res_p, c_p, _ = eng.sw_align(codes, quals, lens, probs, cap=cap, sc=sc, local=local)
+    res_g, c_g, _ = eng.sw_align(codes, quals, lens, probs, cap=cap, want_mat=True, sc=sc, local=local)
+    for i in range(n):
+        assert tuple(res_p[i]) == tuple(res_g[i]), (i, res_p[i], res_g[i])
+    assert np.array_equal(c_p, c_g)
+    assert res_p["aligned"].sum() > n // 3
