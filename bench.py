@@ -655,14 +655,17 @@ def cpu_baseline(idx, reads, quals, pipe, sample, threads, base=None):
     return dt, ref, mate, secs
 
 
-def server_baseline(base, reads, quals, pol, sample, threads, workers, args_srv, log_dir, dropin_binary=None):
+def server_baseline(base, reads, quals, pol, sample, threads, workers, args_srv, log_dir, dropin_binary=None,
+                    dropin_args=()):
     """The north-star comparison on the reference's real schedule (BASELINE.md
     section 3): the stock reference server (oracle/_ref/bowtie2-align-server-s,
     -p <usable cores>) and the same server with its seams bound to the engines
     (integration/bt2g_seams.cpp -> oracle/_ref/bowtie2-align-server-gpu, -p
     <workers>) on the same `sample` reads (pairs) and index, driven by the
     reference's own client in <= 10 000-read connections, 8 at a time; sorted
-    SAM compared record by record."""
+    SAM compared record by record.  `dropin_args`: server options of the
+    drop-in only that change no alignment (--reads-per-batch: a worker aligns
+    its batch's reads one after another)."""
     from oracle import ref_server as rs
     n = sample
     if pol.paired:
@@ -676,11 +679,13 @@ def server_baseline(base, reads, quals, pol, sample, threads, workers, args_srv,
                              workers)):
         stats = os.path.join(log_dir, f"stats_{tag}.json")
         env = rs.dropin_env(base, stats)
-        with rs.Server(base, threads=th, args=args_srv, binary=binary, env=env,
+        with rs.Server(base, threads=th, args=list(args_srv) + (list(dropin_args) if tag == "dropin" else []),
+                       binary=binary, env=env,
                        log_path=os.path.join(log_dir, f"server_{tag}.log")) as srv:
-            dt, outs = srv.run(chunks, k=8, warmup=chunks[:1])
+            dt, outs = srv.run(chunks, k=8, warmup=chunks[:4])   # (the drop-in sizes its caches and staging first)
         sams[tag] = rs.sorted_records(outs)
         out[tag] = {"rate": n / dt, "seconds": dt, "threads": th, "records": len(sams[tag]),
+                    "server_args": list(args_srv) + (list(dropin_args) if tag == "dropin" else []),
                     "server_cpu_s": srv.last_cpu_s, "server_cores_busy": srv.last_cpu_s / dt}
         time.sleep(0.5)
         if os.path.exists(stats):
@@ -882,7 +887,9 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--server-sample", type=int, default=200_000,
                     help="reads (pairs) timed through the stock reference server and the drop-in server (0: skip)")
-    ap.add_argument("--server-workers", type=int, default=1024, help="drop-in server worker threads (-p)")
+    ap.add_argument("--server-workers", type=int, default=4096, help="drop-in server workers (-p; fibers)")
+    ap.add_argument("--server-dropin-args", default="--reads-per-batch 4",
+                    help="drop-in server options that change no alignment (one string)")
     ap.add_argument("--index-cache", default="auto",
                     help="reuse/write the built index at this base path ('auto': under $TMPDIR keyed by the "
                          "genome model and size; '': always build)")
@@ -1111,7 +1118,7 @@ def main():
                     srv_args.append("--very-sensitive-local" if args.mode == "local" else "--very-sensitive")
                 srv = server_baseline(ref["index_base"], reads_np, quals_np, pipe.pol,
                                       min(args.server_sample, sample), threads, args.server_workers, srv_args,
-                                      tempfile.mkdtemp(prefix="bt2srv_"))
+                                      tempfile.mkdtemp(prefix="bt2srv_"), dropin_args=args.server_dropin_args.split())
                 cpu["reference_server"] = {"value": srv["stock"]["rate"], "unit": cpu["unit"], "cores": threads,
                                            "sample": f"first {min(args.server_sample, sample)} of the batch, "
                                                      f"<= 10 000 per client connection, 8 connections at a time",

@@ -832,7 +832,8 @@ private:
 				// $BT2G_SEAM_THREADS_<seam> (e.g. BT2G_SEAM_THREADS_one_mm=2); all of a
 				// seam's dispatchers drain the one queue, so the devices share its load.
 				// (r03i at 3.1 Gbp: 2 per seam 25.2k reads/s, 1 per seam 28.6k -- the
-				// streams' kernels slow each other more than they overlap)
+				// streams' kernels slow each other more than they overlap; with 16 HW
+				// queues the DP seam gains from 4: r03q 40.7k -> 43.2k, r03t 54.8k)
 				const char* t = getenv("BT2G_SEAM_THREADS");
 				const int per = std::max(1, t ? atoi(t) : 1);
 				for(bt2g_ctx* b : bases)
@@ -840,7 +841,7 @@ private:
 						char nm[64];
 						snprintf(nm, sizeof(nm), "BT2G_SEAM_THREADS_%s", ST_NAMES[k]);
 						const char* tk = getenv(nm);
-						const int nk = tk && atoi(tk) > 0 ? atoi(tk) : (k == ST_DP ? 2 * per : per);
+						const int nk = tk && atoi(tk) > 0 ? atoi(tk) : (k == ST_DP ? 4 * per : per);
 						for(int i = 0; i < nk; i++) std::thread(&Dispatcher::loop, this, k, b).detach();
 					}
 			}

@@ -216,8 +216,10 @@ def test_bt_long_reads_vs_oracle(eng, local):
     orc = Oracle()
     gen = get_index("lambda").ref_codes[0]
     for L in (1100, 2048):
-        minsc = int(20 + 8 * np.log(L)) if local else int(-(0.6 + 0.6 * L))
-        codes, quals, lens, probs, rects = _synth_problems(gen, 16, 40 + L, length=L, maxgap=30, minsc=minsc)
+        # (local: a minsc near 1.8 x length keeps the candidate list under the cap of 8192)
+        minsc = int(1.8 * L) if local else int(-(0.6 + 0.6 * L))
+        codes, quals, lens, probs, rects = _synth_problems(gen, 16, 40 + L, length=L, maxgap=30, minsc=minsc,
+                                                           sub=0.005 if local else 0.02)
         res, cands, naln, alns, edits, fates = eng.sw_align_bt(codes, quals, lens, probs, rects=rects, local=local,
                                                                cap=8192, maxaln=512, maxedit=2 * L + 8)
         ea, ee, ef = _oracle_expect(orc, gen, codes, quals, probs, rects, local)
