@@ -932,6 +932,11 @@ static SwHint sw_hint(const bt2g_sw_problem* probs, uint32_t nprob, const uint32
 	return h;
 }
 
+static bool bt_hplane() {
+	static const bool on = [] { const char* e = getenv("BT2G_BT_HPLANE"); return e && *e == '1'; }();
+	return on;
+}
+
 static int sw_align_bt_impl(bt2g_ctx* c, const uint8_t* reads, const uint8_t* quals, uint32_t stride,
                             const uint32_t* lens, const bt2g_sw_problem* probs, uint32_t nprob, const uint8_t* windows,
                             const bt2g_sw_rect* rects, const bt2g_scoring* sc, int enable8, uint32_t cap,
@@ -996,16 +1001,19 @@ static int sw_align_bt_impl(bt2g_ctx* c, const uint8_t* reads, const uint8_t* qu
 		}
 		packed = sw_use_packed(*sc, C, nullptr, stride, maxcol);
 		hb = packed && all8 && !sc->local ? 1 : 2;
+		// end-to-end systolic fills, u8 and i16 alike (long reads: minsc < -254), write
+		// the walk's decisions (kind 2, the u8 plane's layout)
+		if(packed && !sc->local && !bt_hplane() && maxcol <= 2u * maxrow) hb = 1;
 		if((rc = talloc((void**)&plane, (size_t)sw_plane_slot(stride, maxcol, hb) * nprob))) return rc;
 	}
 	// systolic fill: bottom-aligned rows, u8 (hb 1) or u16 plane with block masks;
 	// one-problem-per-lane fills (local, other scorings): top-aligned u16 plane
-	// u8 fills: the fill writes the walk's decision per cell (kind 2, 4 bits);
-	// BT2G_BT_HPLANE=1 keeps the H score plane (kind 0) for A/B runs
-	static const bool hplane = [] { const char* e = getenv("BT2G_BT_HPLANE"); return e && *e == '1'; }();
+	// end-to-end systolic fills: the fill writes the walk's decision per cell (kind
+	// 2, 4 bits); BT2G_BT_HPLANE=1 keeps the H score plane (kind 0) for A/B runs
 	// (wide DPs -- mate searches, 150 x 705 -- keep the H plane: the decision bits
 	// cost fill work per cell, and their walks touch a small share of the cells)
-	const int kind = hb == 1 ? (hplane || sc->local || maxcol > 2u * maxrow ? 0 : 2) : 1;
+	const bool dec = packed && !sc->local && !bt_hplane() && maxcol <= 2u * maxrow && (!reserved || hb == 1);
+	const int kind = dec ? 2 : hb == 1 ? 0 : 1;
 	a.plane = plane;
 	a.slot = sw_plane_slot(stride, maxcol, hb);
 	a.plane_top = !packed ? 1 : sc->local ? 2 : 0;

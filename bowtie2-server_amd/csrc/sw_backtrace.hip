@@ -152,7 +152,7 @@ k_sw_bt(BtArgs A) {
 	uint32_t pad = 0;
 	const uint8_t* slot = nullptr;
 	{
-		if(KIND != 1 && variant != 0) { A.naln[p] = -4; return; }   // i16 fill, u8-only plane
+		if(KIND == 0 && variant != 0) { A.naln[p] = -4; return; }   // i16 fill, u8-only plane
 		const size_t es = KIND == 1 ? 2 : 1;   // kind 2: the u8 plane's layout, 8 B per block column
 		// systolic end-to-end: last row at the stack bottom; one-problem-per-lane
 		// fills: top-aligned; systolic local: padded rows (round16) at the bottom

@@ -752,8 +752,9 @@ k_sw_sys(const bt2g_sw_problem* __restrict__ probs, uint32_t nprob, const uint8_
 				const uint32_t b0 = (DB[0] & 0xffffffu) | ((XB << 16) & 0xff000000u);
 				const uint32_t b1 = (DB[1] & 0xffffffu) | (XB << 24);
 				const size_t cell8 = ((size_t)k * pitch + (uint32_t)j) * 8u;
-				if(s0 && h[0].row0 == 0xffu) *(uint2*)(plane + (size_t)h[0].pi * hslot + cell8) = make_uint2(a0, a1);
-				if(s1 && h[1].row0 == 0xffu) *(uint2*)(plane + (size_t)h[1].pi * hslot + cell8) = make_uint2(b0, b1);
+				// (u8 and i16 fills alike: the decisions do not depend on the width)
+				if(s0) *(uint2*)(plane + (size_t)h[0].pi * hslot + cell8) = make_uint2(a0, a1);
+				if(s1) *(uint2*)(plane + (size_t)h[1].pi * hslot + cell8) = make_uint2(b0, b1);
 			} else if(!LOCAL && hbytes == 1) {
 				// bytes of 16 rows per problem: low halves -> a, high halves -> b
 				uint32_t a[4], b[4];
