@@ -132,7 +132,6 @@ struct Fiber {
 	State state = READY;
 	uint64_t wake_at_ns = 0;          // PARKED by nanosleep: not before this time
 	const void* cv = nullptr;         // the condition variable it waits on
-	const void* baton = nullptr;      // woken from this cv's baton: pass it on at the next unlock
 	void* user = nullptr;             // bt2gf::local()
 };
 
@@ -176,11 +175,10 @@ std::mutex g_mu;                              // carriers, fiber handles
 // fibers waiting on each condition variable (woken by its notify_one/_all)
 std::mutex g_cv_mu;
 std::unordered_map<const void*, std::vector<Fiber*>> g_cv_waiters;
-// fibers a notify_all released but did not wake yet: it wakes two, and each
-// woken fiber wakes the next when it next releases a mutex (the "baton": after
-// its predicate check, or inside its next wait), so they re-take the mutex a
-// few at a time instead of all at once -- every one still returns from its
-// wait, as notify_all requires.  (The reference's ready queue of
+// fibers a notify_all released but did not wake yet: each woken fiber wakes
+// the next once it holds the lock again (the "baton"), so they re-take the
+// mutex one after another instead of all at once -- every one still returns
+// from its wait, as notify_all requires.  (The reference's ready queue of
 // reads notifies all its waiters per pushed element, pat.h:1981-1985: with
 // thousands of idle workers that herd was 4.2M contended lock attempts per
 // 400k reads at --reads-per-batch 1, r03r.)
@@ -545,15 +543,6 @@ void __wrap__ZNSt18condition_variable4waitERSt11unique_lockISt5mutexE(std::condi
 		__real__ZNSt18condition_variable4waitERSt11unique_lockISt5mutexE(cv, lk);
 		return;
 	}
-	// a baton this fiber holds goes on first: between its registration below and
-	// its suspension the fiber must not yield (a mutex wait would park it READY
-	// while a notify may already have queued it: it would run twice), and the
-	// unlocks in that window would pass the baton through contended locks
-	if(f->baton) {
-		const void* b = f->baton;
-		f->baton = nullptr;
-		pass_baton(b);
-	}
 	// registered while the caller still holds the lock: a notifier that changes
 	// the predicate's state under that lock cannot notify before we are on the list
 	f->cv = cv;
@@ -564,15 +553,13 @@ void __wrap__ZNSt18condition_variable4waitERSt11unique_lockISt5mutexE(std::condi
 	lk.unlock();
 	suspend(f, BLOCKED);
 	lk.lock();
-	if(f->baton) pass_baton(f->baton);   // (a second baton while holding one: pass the older)
-	f->baton = cv;
+	pass_baton(cv);
 }
 
 // notify: fibers waiting on `cv` go back to their carriers, then the OS threads
 // (notify_all: the first now, the rest through the baton)
 static void wake_cv_fibers(const void* cv, bool all) {
 	Fiber* w = nullptr;
-	Fiber* w2 = nullptr;
 	{
 		std::lock_guard<std::mutex> g(g_cv_mu);
 		auto it = g_cv_waiters.find(cv);
@@ -583,12 +570,10 @@ static void wake_cv_fibers(const void* cv, bool all) {
 			std::deque<Fiber*>& b = g_cv_baton[cv];
 			b.insert(b.end(), it->second.begin(), it->second.end());
 			it->second.clear();
-			w2 = b.front();
-			b.pop_front();
 		}
 	}
-	void* two[2] = {w, w2};
-	wake_many(two, w2 ? 2 : 1);
+	void* one = w;
+	wake_many(&one, 1);
 }
 
 void __real__ZNSt18condition_variable10notify_allEv(std::condition_variable* cv);
@@ -611,20 +596,6 @@ void __wrap__ZNSt18condition_variable10notify_oneEv(std::condition_variable* cv)
 // re-lock the queue's mutex at once.  A fiber tries the lock, spins briefly,
 // then yields to its carrier and tries again on the carrier's next round.
 int __real_pthread_mutex_lock(pthread_mutex_t* m);
-
-int __real_pthread_mutex_unlock(pthread_mutex_t* m);
-
-// a fiber holding a notify_all baton hands it on once it has let go of a lock
-int __wrap_pthread_mutex_unlock(pthread_mutex_t* m) {
-	const int r = __real_pthread_mutex_unlock(m);
-	Fiber* f = cur_fiber();
-	if(f && f->baton) {
-		const void* cv = f->baton;
-		f->baton = nullptr;
-		pass_baton(cv);
-	}
-	return r;
-}
 
 int __wrap_pthread_mutex_lock(pthread_mutex_t* m) {
 	Fiber* f = cur_fiber();

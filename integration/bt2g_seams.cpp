@@ -90,6 +90,9 @@ std::atomic<uint64_t> g_queue_us[ST_N], g_resume_us[ST_N];
 // speculative DP prefetch: group requests, DPs prefetched, align() calls served
 // by them, and (BT2G_SPEC_VERIFY) served ones that differed from align()'s own
 std::atomic<uint64_t> g_spec_dps{0}, g_spec_hits{0}, g_spec_groups{0}, g_spec_verify_bad{0};
+// seed-phase prefetch: 1-mm searches / seed searches run with the exact sweep,
+// those the seams took, and (BT2G_SEEDPF_VERIFY) taken ones that differed
+std::atomic<uint64_t> g_pf[6];
 // $BT2G_ADAPTER_PROF=1: kernel time per engine kernel id (bt2g_kernel_stats), all dispatchers
 const int NKERN = 8;
 const char* const KERN_NAMES[NKERN] = {"exact_sweep", "seed_search", "one_mm", "get_offset", "sw_align",
@@ -122,6 +125,10 @@ void write_stats() {
 	n += snprintf(buf + n, sizeof(buf) - n, ", \"spec\": [%llu, %llu, %llu, %llu]",
 	              (unsigned long long)g_spec_groups.load(), (unsigned long long)g_spec_dps.load(),
 	              (unsigned long long)g_spec_hits.load(), (unsigned long long)g_spec_verify_bad.load());
+	n += snprintf(buf + n, sizeof(buf) - n, ", \"pf\": [%llu, %llu, %llu, %llu, %llu, %llu]",
+	              (unsigned long long)g_pf[0].load(), (unsigned long long)g_pf[1].load(),
+	              (unsigned long long)g_pf[2].load(), (unsigned long long)g_pf[3].load(),
+	              (unsigned long long)g_pf[4].load(), (unsigned long long)g_pf[5].load());
 	n += snprintf(buf + n, sizeof(buf) - n, ", \"kernels\": {");
 	for(int i = 0; i < NKERN; i++)
 		n += snprintf(buf + n, sizeof(buf) - n, "%s\"%s\": [%llu, %.1f]", i ? ", " : "", KERN_NAMES[i],
@@ -304,11 +311,13 @@ struct Req {
 	Req(int k, uint64_t ky) : kind(k), key(ky) {}
 };
 
+struct MmReq;
 struct ExactReq : Req {      // bt2g_exact_sweep
 	Row r;
 	uint32_t mine_max;
 	int nofw, norc;
 	uint32_t out[8];
+	MmReq* mm = nullptr;         // seed-phase prefetch: the gated 1-mm search to run after the sweep
 	ExactReq(uint32_t mm, int f, int c) : Req(ST_EXACT, ((uint64_t)mm << 2) | (uint64_t)(f << 1) | (uint64_t)c),
 	                                      mine_max(mm), nofw(f), norc(c) {}
 };
@@ -321,6 +330,7 @@ struct MmReq : Req {         // bt2g_one_mm
 	Out<bt2g_mm1, 32> hits;
 	int32_t cnt = 0;
 	uint32_t ops = 0;
+	bool pf_ran = false;         // (prefetch) the exact sweep's dispatcher ran it
 	MmReq(int f, int c, const bt2g_scoring& s)
 		: Req(ST_1MM, (uint64_t)(f << 1) | (uint64_t)c | ((uint64_t)s.local << 2)), nofw(f), norc(c), sc(s) {}
 };
@@ -427,6 +437,8 @@ struct Pack {
 	}
 };
 
+int run_mm(const std::vector<MmReq*>& v, uint32_t cap);
+
 int run_exact(const std::vector<ExactReq*>& v) {
 	thread_local Pack pk;
 	thread_local std::vector<uint32_t> out;
@@ -436,10 +448,31 @@ int run_exact(const std::vector<ExactReq*>& v) {
 	                          v[0]->nofw, v[0]->norc, out.data());
 	if(rc) return rc;
 	for(size_t i = 0; i < v.size(); i++) memcpy(v[i]->out, &out[8 * i], sizeof(v[i]->out));
+	// seed-phase prefetch: the 1-mm search the worker asks next, gated as
+	// bt2_search.cpp:3640-3667 gates it (a strand whose sweep found <= 1 edit;
+	// reads with exact hits too: most are not done after extending them, stub
+	// run at 20 Mbp: 25 k of 30 k reads asked); run here, in the same round trip
+	std::vector<MmReq*> mm[8];
+	for(ExactReq* q : v) {
+		if(!q->mm) continue;
+		const bool yfw = !q->nofw && q->out[0] <= 1, yrc = !q->norc && q->out[1] <= 1;
+		if(!yfw && !yrc) continue;
+		MmReq* m = q->mm;
+		m->nofw = yfw ? 0 : 1;
+		m->norc = yrc ? 0 : 1;
+		m->key = (uint64_t)(m->nofw << 1) | (uint64_t)m->norc | ((uint64_t)m->sc.local << 2);
+		mm[m->key & 7u].push_back(m);
+	}
+	for(int k = 0; k < 8; k++) {
+		if(mm[k].empty()) continue;
+		if(run_mm(mm[k], 16) != BT2G_OK) continue;     // (not fatal: the seam asks again)
+		for(MmReq* m : mm[k]) m->pf_ran = true;
+		g_pf[0] += mm[k].size();
+	}
 	return BT2G_OK;
 }
 
-int run_mm(const std::vector<MmReq*>& v, uint32_t cap = 16) {
+int run_mm(const std::vector<MmReq*>& v, uint32_t cap) {
 	struct B {
 		Pack pk;
 		std::vector<int32_t> ms, cnt;
@@ -682,7 +715,7 @@ int run_off(const std::vector<OffReq*>& v) {
 int run_group(int kind, const std::vector<Req*>& g) {
 	switch(kind) {
 	case ST_EXACT: { std::vector<ExactReq*> v; for(Req* r : g) v.push_back(static_cast<ExactReq*>(r)); return run_exact(v); }
-	case ST_1MM:   { std::vector<MmReq*> v;    for(Req* r : g) v.push_back(static_cast<MmReq*>(r));    return run_mm(v); }
+	case ST_1MM:   { std::vector<MmReq*> v;    for(Req* r : g) v.push_back(static_cast<MmReq*>(r));    return run_mm(v, 16); }
 	case ST_SEEDS: { std::vector<SeedReq*> v;  for(Req* r : g) v.push_back(static_cast<SeedReq*>(r));  return run_seeds(v); }
 	case ST_UG:    { std::vector<UgReq*> v;    for(Req* r : g) v.push_back(static_cast<UgReq*>(r));    return run_ug(v); }
 	case ST_EXT:   { std::vector<ExtReq*> v;   for(Req* r : g) v.push_back(static_cast<ExtReq*>(r));   return run_ext(v); }
@@ -949,6 +982,99 @@ struct FiberHooks {
 	}
 } g_fiber_hooks;
 
+// ---- seed-phase prefetch -------------------------------------------------------
+// A read's seed phase is three round trips one after another: exactSweep,
+// then (no exact hit, <= 1 edit on a strand) oneMmSearch, then the first seed
+// round's searchAllSeeds (bt2_search.cpp:3450-3906) -- nearly every read that
+// is not done after its exact hits reaches the seed round.  Their arguments
+// are functions of the read length and the server's fixed options
+// (scoreMin, the seed interval and length: bt2_search.cpp:3287-3400), which
+// the seams learn from their own calls.  So with the exact sweep the binding
+// also asks for the read's round-0 seed search (in parallel, on the seed
+// dispatcher) and, in the sweep's own dispatcher call right after the sweep,
+// the gated 1-mm search.  A seam takes a prefetched result only when its
+// request is the identical one (same read, same arguments: checked), else
+// asks the engine as before -- nothing the reference decides changes.
+// $BT2G_SEEDPF=0 turns it off; BT2G_SEEDPF_VERIFY=1 re-runs every taken
+// result as an ordinary request and counts differences.
+bool seedpf_enabled() {
+	static const bool on = [] {
+		const char* e = getenv("BT2G_SEEDPF");
+		return !(e && e[0] == '0') && bt2gf::enabled();
+	}();
+	return on;
+}
+bool seedpf_verify() {
+	static const bool on = getenv("BT2G_SEEDPF_VERIFY") != nullptr;
+	return on;
+}
+
+// learned per read length (the latest value seen; a prediction is only ever
+// used after the seam has checked it)
+struct Learned {
+	std::atomic<uint8_t> st[BT2G_MAX_READ_LEN + 1];
+	std::atomic<int64_t> v[BT2G_MAX_READ_LEN + 1];
+	Learned() {
+		for(auto& x : st) x.store(0);
+		for(auto& x : v) x.store(0);
+	}
+	void learn(size_t len, int64_t val) {
+		if(len > BT2G_MAX_READ_LEN) return;
+		if(st[len].load(std::memory_order_relaxed) == 1 && v[len].load(std::memory_order_relaxed) == val) return;
+		v[len].store(val, std::memory_order_relaxed);
+		st[len].store(1, std::memory_order_release);
+	}
+	bool get(size_t len, int64_t& val) const {
+		if(len > BT2G_MAX_READ_LEN || st[len].load(std::memory_order_acquire) != 1) return false;
+		val = v[len].load(std::memory_order_relaxed);
+		return true;
+	}
+};
+Learned g_mm_minsc;            // oneMmSearch's minsc
+Learned g_sd_par;              // round 0's (seed length << 40 | interval << 20 | offsets)
+std::mutex g_pf_mu;
+std::atomic<int> g_pf_sc_st{0};   // the 1-mm scoring: 0 unknown, 1 known, 2 varies
+bt2g_scoring g_pf_sc;
+void learn_scoring(const bt2g_scoring& sc) {
+	const int st = g_pf_sc_st.load(std::memory_order_acquire);
+	if(st == 2) return;
+	if(st == 1) {
+		if(memcmp(&sc, &g_pf_sc, sizeof(sc)) != 0) g_pf_sc_st.store(2, std::memory_order_release);   // (not one scheme)
+		return;
+	}
+	std::lock_guard<std::mutex> lk(g_pf_mu);
+	if(g_pf_sc_st.load() == 0) {
+		g_pf_sc = sc;
+		g_pf_sc_st.store(1, std::memory_order_release);
+	}
+}
+
+// One prefetched read (per fiber: two, for a pair's mates).
+struct SeedPf {
+	bool live = false;
+	uint32_t len = 0;
+	uint8_t codes[BT2G_MAX_READ_LEN], quals[BT2G_MAX_READ_LEN];
+	std::unique_ptr<MmReq> mm;
+	std::unique_ptr<SeedReq> sd;
+	bool mm_ok = false, sd_ok = false;
+	bool same(const Read& rd) const {
+		if(!live || rd.length() != len) return false;
+		for(uint32_t i = 0; i < len; i++)
+			if(codes[i] != (uint8_t)rd.patFw[i] || quals[i] != (uint8_t)rd.qual[i]) return false;
+		return true;
+	}
+};
+struct SeedPfState {
+	SeedPf slot[2];
+	unsigned next = 0;
+	SeedPf* find(const Read& rd) {
+		for(SeedPf& x : slot)
+			if(x.same(rd)) return &x;
+		return nullptr;
+	}
+};
+SeedPfState& seed_pf();      // per fiber (DrvState below)
+
 // AlnRes from an engine alignment: edits already in their final (5'->3',
 // post-trim) positions, so they are shifted by the leading trim before
 // setShape, which subtracts it (aligner_result.cpp:101-108).
@@ -1054,7 +1180,48 @@ size_t __wrap__ZN11SeedAligner10exactSweepERK4EbwtRK4ReadRK7ScoringbbmRmS9_bR11S
 	}
 	ExactReq q((uint32_t)mineMax, nofw ? 1 : 0, norc ? 1 : 0);
 	q.r.set(read.patFw, read.qual);
-	g_disp.submit(&q);
+	SeedPf* pf = nullptr;
+	if(seedpf_enabled() && bt2gf::self() && q.r.len == len) {
+		SeedPfState& ps = seed_pf();
+		pf = ps.find(read);
+		if(!pf) pf = &ps.slot[ps.next++ & 1u];
+		pf->live = true;
+		pf->len = (uint32_t)len;
+		memcpy(pf->codes, q.r.codes, len);
+		memcpy(pf->quals, q.r.quals, len);
+		pf->mm_ok = pf->sd_ok = false;
+	}
+	Req* extra = nullptr;
+	if(pf) {
+		int64_t minsc = 0, par = 0;
+		if(g_pf_sc_st.load(std::memory_order_acquire) == 1 && g_mm_minsc.get(len, minsc)) {
+			if(!pf->mm) pf->mm.reset(new MmReq(0, 0, g_pf_sc));
+			MmReq* m = pf->mm.get();
+			m->sc = g_pf_sc;
+			m->r = q.r;
+			m->minsc = (int32_t)minsc;
+			m->pf_ran = false;
+			m->rc = 0;
+			q.mm = m;
+		}
+		if(g_sd_par.get(len, par)) {
+			const uint32_t L = (uint32_t)(par >> 40), per = (uint32_t)((par >> 20) & 0xfffff), nof = (uint32_t)(par & 0xfffff);
+			if(!pf->sd) pf->sd.reset(new SeedReq(L, per, 0, nof));
+			SeedReq* sq = pf->sd.get();
+			*sq = SeedReq(L, per, 0, nof);          // (fresh request state; the Row is copied below)
+			sq->r = q.r;
+			extra = sq;
+		}
+	}
+	if(extra) {
+		Req* g2[2] = {&q, extra};
+		g_disp.submit_group(g2, 2);
+		pf->sd_ok = true;
+		g_pf[1]++;
+	} else {
+		g_disp.submit(&q);
+	}
+	if(pf && q.mm) pf->mm_ok = q.mm->pf_ran;
 	const uint32_t* out = q.out;
 	count(ST_EXACT, true);
 	// outputs exactly as the tail of exactSweep (aligner_seed.cpp:944-967)
@@ -1090,12 +1257,32 @@ bool __wrap__ZN11SeedAligner11oneMmSearchEPK4EbwtS2_RK4ReadRK7ScoringlbbbbbR11Se
 			self, ebwtFw, ebwtBw, read, sc, minsc, nofw, norc, local, repex, rep1mm, hits, met);
 	}
 	MmReq q(nofw ? 1 : 0, norc ? 1 : 0, bs);
-	q.r.set(read.patFw, read.qual);
-	q.minsc = (int32_t)minsc;
-	g_disp.submit(&q);
-	const auto& h = q.hits;
-	const int32_t cnt = q.cnt;
-	const uint32_t ops = q.ops;
+	const MmReq* src = &q;
+	if(seedpf_enabled() && bt2gf::self()) {
+		learn_scoring(bs);
+		g_mm_minsc.learn(len, minsc);
+		SeedPf* pf = seed_pf().find(read);
+		if(pf && pf->mm_ok) {
+			pf->mm_ok = false;
+			const MmReq* m = pf->mm.get();
+			if(m->minsc == (int32_t)minsc && m->nofw == q.nofw && m->norc == q.norc &&
+			   memcmp(&m->sc, &bs, sizeof(bs)) == 0) {
+				src = m;
+				g_pf[2]++;
+			}
+		}
+	}
+	if(src == &q || seedpf_verify()) {
+		q.r.set(read.patFw, read.qual);
+		q.minsc = (int32_t)minsc;
+		g_disp.submit(&q);
+		if(src != &q && (src->cnt != q.cnt || src->ops != q.ops || src->hits.size() != q.hits.size() ||
+		                 memcmp(src->hits.data(), q.hits.data(), sizeof(bt2g_mm1) * q.hits.size()) != 0))
+			g_pf[4]++;
+	}
+	const auto& h = src->hits;
+	const int32_t cnt = src->cnt;
+	const uint32_t ops = src->ops;
 	count(ST_1MM, true);
 	static_cast<SeedAlignerAcc*>(self)->add_ops(ops);
 	for(int32_t k = 0; k < cnt; k++) {
@@ -1132,11 +1319,29 @@ void __wrap__ZN11SeedAligner14searchAllSeedsERK5EListI4SeedLi128EEPK4EbwtS7_RK4R
 	uint32_t per = nof > 1 ? (uint32_t)(sr.idx2off(1) - sr.idx2off(0))
 	                       : (uint32_t)(len > off + seedlen ? len - off - seedlen + 1 : 1);
 	SeedReq q((uint32_t)seeds[0].len, per, off, (uint32_t)nof);
-	q.r.set(read.patFw, read.qual);
-	g_disp.submit(&q);
-	const auto& out = q.out;
-	const int32_t ns = q.ns;
-	const uint32_t ops = q.ops;
+	const SeedReq* src = &q;
+	if(seedpf_enabled() && bt2gf::self()) {
+		if(off == 0) g_sd_par.learn(len, ((int64_t)seeds[0].len << 40) | ((int64_t)per << 20) | (int64_t)nof);
+		SeedPf* pf = seed_pf().find(read);
+		if(pf && pf->sd_ok) {
+			pf->sd_ok = false;
+			const SeedReq* sq = pf->sd.get();
+			if(sq->seedlen == (uint32_t)seeds[0].len && sq->per == per && sq->off == off && sq->nof == (uint32_t)nof) {
+				src = sq;
+				g_pf[3]++;
+			}
+		}
+	}
+	if(src == &q || seedpf_verify()) {
+		q.r.set(read.patFw, read.qual);
+		g_disp.submit(&q);
+		if(src != &q && (src->ns != q.ns || src->ops != q.ops || src->out.size() != q.out.size() ||
+		                 memcmp(src->out.data(), q.out.data(), sizeof(uint32_t) * q.out.size()) != 0))
+			g_pf[5]++;
+	}
+	const auto& out = src->out;
+	const int32_t ns = src->ns;
+	const uint32_t ops = src->ops;
 	if((size_t)ns != nof) {
 		fprintf(stderr, "bt2g adapter: seed offsets differ (engine %d, reference %zu)\n", ns, nof);
 		throw 1;
@@ -1486,6 +1691,7 @@ struct DrvState {
 	ExtTable ext;
 	GwTable gw;
 	SpecCtx spec;
+	SeedPfState pf;
 };
 DrvState& drv() {
 	void** slot = bt2gf::local();
@@ -1496,6 +1702,8 @@ DrvState& drv() {
 	if(!*slot) *slot = new DrvState();
 	return *static_cast<DrvState*>(*slot);
 }
+
+SeedPfState& seed_pf() { return drv().pf; }
 
 // ---- speculative DP prefetch --------------------------------------------------
 // SwDriver::extendSeeds (aligner_sw_driver.cpp:756-1297) resolves one seed-hit

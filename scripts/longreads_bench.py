@@ -30,8 +30,10 @@ def main():
     ap.add_argument("--cpu-threads", type=int, default=0, help="stock server -p (0: usable host cores)")
     ap.add_argument("--dropin-binary", default=os.path.join(rs.REF_DIR, "bowtie2-align-server-gpu"))
     ap.add_argument("--repeat", type=int, default=1, help="connections of the whole file, one at a time")
+    ap.add_argument("--workdir", default="", help="index, server logs (default: a fresh temporary directory)")
     a = ap.parse_args()
-    d = tempfile.mkdtemp(prefix="bt2lr_")
+    d = a.workdir or tempfile.mkdtemp(prefix="bt2lr_")
+    os.makedirs(d, exist_ok=True)
     base = os.path.join(d, "lambda_virus")
     bi.write_index(base, bi.build_from_fasta(os.path.join(ROOT, "tests", "golden", "lambda_virus.fa")))
     reads = os.path.join(ROOT, "tests", "golden", "longreads.fq.gz")

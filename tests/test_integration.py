@@ -94,7 +94,7 @@ def _compare(dropin, base, chunks, args, dirpath, long_reads=False, extra_env=No
     assert not bad, f"{len(bad)} SAM records differ, first:\nref  {bad[0][0][:400]}\nbind {bad[0][1][:400]}"
     assert st is not None, "binding wrote no call counts"
     for k, v in st.items():
-        if k in ("kernels", "queue_ms", "resume_ms", "spec"):   # (not seams: timing breakdowns, prefetch counts)
+        if k in ("kernels", "queue_ms", "resume_ms", "spec", "pf"):   # (not seams: timing breakdowns, prefetch counts)
             continue
         gpu, cpu = v[0], v[1]                    # calls served by the engine / by the CPU path
         if not long_reads:
@@ -102,6 +102,8 @@ def _compare(dropin, base, chunks, args, dirpath, long_reads=False, extra_env=No
     assert st["exact_sweep"][0] > 0 and st["sw_dp"][0] > 0 and st["seed_search"][0] > 0
     if "spec" in st:
         assert st["spec"][3] == 0, f"{st['spec'][3]} prefetched DPs differed from align()'s own (BT2G_SPEC_VERIFY)"
+    if "pf" in st:
+        assert st["pf"][4] == 0 and st["pf"][5] == 0, f"seed-phase prefetch differed (BT2G_SEEDPF_VERIFY): {st['pf']}"
     return t_ref, t_new, len(a), st
 
 
@@ -141,6 +143,16 @@ def test_binding_spec_prefetch_cpu(indexes, tmp_path):
     _, _, _, st = _compare(SRV_STUB, base, chunks, [], str(tmp_path),
                            extra_env={"BT2G_SPEC": "1", "BT2G_SPEC_VERIFY": "1"})
     assert st["spec"][2] > 0, "no align() call was served by a prefetched DP"
+
+
+def test_binding_seed_prefetch_cpu(indexes, tmp_path):
+    """Seed-phase prefetch (default on): the gated 1-mm search and the first seed
+    round ride with the exact sweep; BT2G_SEEDPF_VERIFY re-runs every taken result."""
+    _need(rs.SERVER, rs.CLIENT, SRV_STUB)
+    base, idx = indexes["synth"]
+    chunks = _reads(idx, "ee", 1500, 13, str(tmp_path))
+    _, _, _, st = _compare(SRV_STUB, base, chunks, [], str(tmp_path), extra_env={"BT2G_SEEDPF_VERIFY": "1"})
+    assert st["pf"][2] > 0 and st["pf"][3] > 0, f"no prefetched result was taken: {st['pf']}"
 
 
 def test_binding_longreads_cpu(indexes, tmp_path):
