@@ -736,6 +736,8 @@ size_t env_or(const char* name, size_t dflt) {
 const size_t BATCH_TARGET = env_or("BT2G_BATCH_TARGET", bt2gf::enabled() ? 1024 : 256);
 const int BATCH_WINDOW_US = (int)env_or("BT2G_BATCH_WINDOW_US", bt2gf::enabled() ? 200 : 300);
 
+bool seedpf_enabled();
+
 class Dispatcher {
 public:
 	// Serve one request: queued for its seam's dispatcher thread (batching on)
@@ -874,7 +876,10 @@ private:
 						char nm[64];
 						snprintf(nm, sizeof(nm), "BT2G_SEAM_THREADS_%s", ST_NAMES[k]);
 						const char* tk = getenv(nm);
-						const int nk = tk && atoi(tk) > 0 ? atoi(tk) : (k == ST_DP ? 4 * per : per);
+						// (the exact sweep's dispatcher also runs the prefetched 1-mm searches:
+						// two of them, r03x: one was saturated, 3.9 ms per call)
+						const int nk = tk && atoi(tk) > 0 ? atoi(tk)
+						                                  : (k == ST_DP ? 4 * per : k == ST_EXACT && seedpf_enabled() ? 2 * per : per);
 						for(int i = 0; i < nk; i++) std::thread(&Dispatcher::loop, this, k, b).detach();
 					}
 			}
