@@ -438,6 +438,7 @@ struct Pack {
 };
 
 int run_mm(const std::vector<MmReq*>& v, uint32_t cap);
+void enqueue_1mm(const std::vector<MmReq*>& v);   // onto the 1-mm seam's queue (Dispatcher below)
 
 int run_exact(const std::vector<ExactReq*>& v) {
 	thread_local Pack pk;
@@ -451,23 +452,30 @@ int run_exact(const std::vector<ExactReq*>& v) {
 	// seed-phase prefetch: the 1-mm search the worker asks next, gated as
 	// bt2_search.cpp:3640-3667 gates it (a strand whose sweep found <= 1 edit;
 	// reads with exact hits too: most are not done after extending them, stub
-	// run at 20 Mbp: 25 k of 30 k reads asked); run here, in the same round trip
-	std::vector<MmReq*> mm[8];
+	// run at 20 Mbp: 25 k of 30 k reads asked), goes to the 1-mm seam's queue
+	// in the same round trip: the request's group (the worker's wait) grows by
+	// one before the sweep's request completes.  (Run in this dispatcher's own
+	// call instead it saturated the sweep's dispatcher, r03x / r03y.)
+	std::vector<MmReq*> mm;
 	for(ExactReq* q : v) {
-		if(!q->mm) continue;
+		if(!q->mm || !q->group) continue;
 		const bool yfw = !q->nofw && q->out[0] <= 1, yrc = !q->norc && q->out[1] <= 1;
 		if(!yfw && !yrc) continue;
 		MmReq* m = q->mm;
 		m->nofw = yfw ? 0 : 1;
 		m->norc = yrc ? 0 : 1;
 		m->key = (uint64_t)(m->nofw << 1) | (uint64_t)m->norc | ((uint64_t)m->sc.local << 2);
-		mm[m->key & 7u].push_back(m);
+		m->fiber = q->fiber;
+		m->group = q->group;
+		m->pf_ran = true;
+		m->rc = 0;
+		m->t_sub = now_us();
+		q->group->fetch_add(1);
+		mm.push_back(m);
 	}
-	for(int k = 0; k < 8; k++) {
-		if(mm[k].empty()) continue;
-		if(run_mm(mm[k], 16) != BT2G_OK) continue;     // (not fatal: the seam asks again)
-		for(MmReq* m : mm[k]) m->pf_ran = true;
-		g_pf[0] += mm[k].size();
+	if(!mm.empty()) {
+		g_pf[0] += mm.size();
+		enqueue_1mm(mm);
 	}
 	return BT2G_OK;
 }
@@ -826,6 +834,17 @@ public:
 	}
 	static Dispatcher& instance();
 
+	// requests a dispatcher hands on to another seam (their waiters' groups
+	// already count them)
+	void enqueue(int kind, Req* const* reqs, size_t n) {
+		Q& q = q_[kind];
+		{
+			std::lock_guard<std::mutex> lk(q.mu);
+			q.v.insert(q.v.end(), reqs, reqs + n);
+		}
+		q.cv.notify_one();
+	}
+
 private:
 	struct Q {
 		std::mutex mu;
@@ -977,6 +996,9 @@ private:
 
 Dispatcher g_disp;
 Dispatcher& Dispatcher::instance() { return g_disp; }
+void enqueue_1mm(const std::vector<MmReq*>& v) {
+	g_disp.enqueue(ST_1MM, reinterpret_cast<Req* const*>(v.data()), v.size());
+}
 
 // fibers (bt2g_fibers.cpp): their requests reach the dispatchers a carrier round
 // at a time; the context and dispatchers start before the first fiber runs
@@ -1223,10 +1245,13 @@ size_t __wrap__ZN11SeedAligner10exactSweepERK4EbwtRK4ReadRK7ScoringbbmRmS9_bR11S
 		g_disp.submit_group(g2, 2);
 		pf->sd_ok = true;
 		g_pf[1]++;
+	} else if(q.mm) {
+		Req* g1[1] = {&q};
+		g_disp.submit_group(g1, 1);    // (a group: the dispatcher may add the 1-mm request to it)
 	} else {
 		g_disp.submit(&q);
 	}
-	if(pf && q.mm) pf->mm_ok = q.mm->pf_ran;
+	if(pf && q.mm) pf->mm_ok = q.mm->pf_ran && q.mm->rc == 0;
 	const uint32_t* out = q.out;
 	count(ST_EXACT, true);
 	// outputs exactly as the tail of exactSweep (aligner_seed.cpp:944-967)
