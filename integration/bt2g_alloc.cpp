@@ -27,12 +27,15 @@
 // under this allocator's malloc calls).  Larger blocks go to malloc / free
 // directly.  $BT2G_ALLOC=0 keeps glibc's allocator.
 #include <errno.h>
+#include <execinfo.h>
+#include <stdio.h>
 #include <stdint.h>
 #include <stdlib.h>
 #include <string.h>
 
 #include <atomic>
 #include <new>
+#include <string>
 
 namespace {
 
@@ -132,7 +135,16 @@ struct Cache {
 };
 thread_local Cache t_cache;
 
+// $BT2G_ALLOC_STATS=<path>: blocks taken from malloc per class (fresh), from
+// the depot, and big ones; written by bt2g_alloc_stats_dump (at SIGTERM)
+std::atomic<uint64_t> g_fresh[NCLASS + 1], g_refill[NCLASS], g_topot[NCLASS], g_big[48];
+bool stats_on() {
+	static const bool on = getenv("BT2G_ALLOC_STATS") != nullptr;
+	return on;
+}
+
 void* fresh(int c) {
+	if(stats_on()) g_fresh[c].fetch_add(1, std::memory_order_relaxed);
 	void* p = malloc(HDR + size_of(c));
 	if(!p) return nullptr;
 	Hdr* h = (Hdr*)p;
@@ -144,6 +156,17 @@ void* fresh(int c) {
 void* alloc(size_t n) {
 	if(n == 0) n = 1;
 	if(!enabled() || n > MAXSZ) {
+		if(stats_on()) {
+			g_fresh[NCLASS].fetch_add(1, std::memory_order_relaxed);
+			int b = 0;
+			while(b < 47 && ((size_t)1 << b) < n) b++;
+			if(g_big[b].fetch_add(1, std::memory_order_relaxed) == 0 && b >= 30 && getenv("BT2G_ALLOC_TRACE")) {
+				void* bt[24];
+				const int k = backtrace(bt, 24);
+				fprintf(stderr, "bt2g alloc: %zu bytes\n", n);
+				backtrace_symbols_fd(bt, k, 2);
+			}
+		}
 		void* p = malloc(HDR + n);
 		if(!p) return nullptr;
 		((Hdr*)p)->magic = MAGIC_MALLOC;
@@ -157,6 +180,7 @@ void* alloc(size_t n) {
 			Depot& d = depot();
 			Guard lk(d.mu[c]);
 			const int nb = BATCH < cap_of(c) ? BATCH : cap_of(c);
+			if(stats_on()) g_refill[c].fetch_add(1, std::memory_order_relaxed);
 			for(int i = 0; i < nb && d.head[c]; i++) {
 				Node* b = d.head[c];
 				d.head[c] = b->next;
@@ -199,6 +223,7 @@ void release(void* p) {
 	if(++tc.n[c] > cap_of(c)) {
 		// half of the cache to the depot
 		const int k = tc.n[c] / 2;
+		if(stats_on()) g_topot[c].fetch_add((uint64_t)k, std::memory_order_relaxed);
 		Node* first = tc.head[c];
 		Node* last = first;
 		for(int i = 1; i < k; i++) last = last->next;
@@ -213,6 +238,20 @@ void release(void* p) {
 }
 
 }  // namespace
+
+extern "C" void bt2g_alloc_stats_dump() {
+	const char* path = getenv("BT2G_ALLOC_STATS");
+	if(!path) return;
+	FILE* f = fopen(path, "w");
+	if(!f) return;
+	for(int c = 0; c <= NCLASS; c++)
+		fprintf(f, "%s %llu %llu %llu %llu\n", c < NCLASS ? std::to_string(size_of(c)).c_str() : "big",
+		        (unsigned long long)g_fresh[c].load(), c < NCLASS ? (unsigned long long)g_refill[c].load() : 0ull,
+		        c < NCLASS ? (unsigned long long)g_topot[c].load() : 0ull, c < NCLASS ? (unsigned long long)depot().n[c] : 0ull);
+	for(int b = 0; b < 48; b++)
+		if(g_big[b].load()) fprintf(f, "big<=2^%d %llu\n", b, (unsigned long long)g_big[b].load());
+	fclose(f);
+}
 
 void* operator new(size_t n) {
 	void* p = alloc(n);

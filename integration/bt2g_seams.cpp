@@ -142,8 +142,11 @@ void write_stats() {
 	}
 }
 
+extern "C" void bt2g_alloc_stats_dump();   // bt2g_alloc.cpp ($BT2G_ALLOC_STATS)
+
 void on_term(int) {
 	write_stats();
+	bt2g_alloc_stats_dump();
 	bt2gf::mutex_prof_dump();
 	_exit(0);
 }

@@ -1,0 +1,18 @@
+#!/bin/bash
+# r03aa: per-connection read-ahead depth (PatternSourcePerThread buffers built and freed per
+# connection: 4097 by default at -p 4096, of which a 10 000-read connection at --reads-per-batch 4
+# uses 2 500) with the allocator's malloc fallbacks counted
+set -o pipefail
+cd "$GRAFT_REPO_ROOT" || exit 1
+O=gpurun_out/r03aa
+mkdir -p $O /tmp/db3100
+run() {   # tag workers extra-args...
+  local tag=$1 w=$2; shift 2
+  BT2G_ALLOC_STATS=$PWD/$O/alloc_$tag.txt BT2G_SAMPLE=$PWD/$O/samp_$tag.txt timeout -k 10 900 python -u scripts/dropin_bench.py --genome-mb 3100 \
+    --k 8 --gpu-workers $w --workdir /tmp/db3100 "$@" > $O/$tag.json 2> $O/$tag.log || return 1
+  python scripts/prof_symbolize.py $O/samp_$tag.txt --role 1 --top 40 > $O/prof_$tag.txt
+}
+run g4096 4096 --reads 400000 --warmup-chunks 12 --dropin-args='--reads-per-batch 4' || exit 1
+BT2G_READAHEAD=2049 run g4096ra2049 4096 --reads 400000 --warmup-chunks 12 --skip-stock --dropin-args='--reads-per-batch 4' || exit 1
+BT2G_READAHEAD=1025 run g4096ra1025 4096 --reads 400000 --warmup-chunks 12 --skip-stock --dropin-args='--reads-per-batch 4' || exit 1
+echo done
