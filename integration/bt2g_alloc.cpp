@@ -143,14 +143,31 @@ bool stats_on() {
 	return on;
 }
 
+// A class's new blocks come from 1 MiB slabs (one malloc for many blocks;
+// blocks of 64 KiB and up one at a time): the rest of a slab goes to the
+// calling thread's cache.  Blocks are never returned, so slabs never are.
+const size_t SLAB = (size_t)1 << 20;
+
 void* fresh(int c) {
 	if(stats_on()) g_fresh[c].fetch_add(1, std::memory_order_relaxed);
-	void* p = malloc(HDR + size_of(c));
+	const size_t bsz = HDR + size_of(c);
+	const size_t nb = size_of(c) < ((size_t)64 << 10) && !t_dead ? SLAB / bsz : 1;
+	char* p = (char*)malloc(bsz * nb);
 	if(!p) return nullptr;
-	Hdr* h = (Hdr*)p;
-	h->magic = MAGIC_CACHED;
-	h->cls = (uint32_t)c;
-	return (char*)p + HDR;
+	for(size_t i = 0; i < nb; i++) {
+		Hdr* h = (Hdr*)(p + i * bsz);
+		h->magic = MAGIC_CACHED;
+		h->cls = (uint32_t)c;
+	}
+	// blocks 1..nb-1 to this thread's cache (it was empty: the caller found no block)
+	Cache& tc = t_cache;
+	for(size_t i = nb; i-- > 1;) {
+		Node* b = (Node*)(p + i * bsz + HDR);
+		b->next = tc.head[c];
+		tc.head[c] = b;
+		tc.n[c]++;
+	}
+	return p + HDR;
 }
 
 void* alloc(size_t n) {
