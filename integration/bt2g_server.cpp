@@ -14,11 +14,16 @@
 //
 // A buffer feeds one worker at a time, so nthreads + 1 buffers let one
 // connection alone keep every worker busy -- the minimum the reference's own
-// comment asks for (bt2_search.cpp:4858).  Fewer would make workers wait for
-// buffers, and a buffer's return notifies every waiter (notify_all,
-// pat.h:1981-1985): measured (stub server, 1 024 workers, nthreads / 4 + 1)
-// 3.7x slower.  So: nthreads + 1 per connection ($BT2G_READAHEAD overrides),
-// never more than the reference's own number.  Which buffer a batch lands in
+// comment asks for (bt2_search.cpp:4858).  But every connection builds all of
+// them up front, and a 10 000-read connection at --reads-per-batch 4 uses at
+// most 2 500: with 4 096 workers the unused ones were most of the server's
+// allocator traffic.  Since notify_all wakes waiting fibers one after another
+// (bt2g_fibers.cpp), workers waiting for buffers are cheap, and with several
+// connections in flight (the benchmark protocol runs 8) nthreads / 4 + 1 per
+// connection keeps them busy: r03aa/r03ab at 3.1 Gbp, 4 096 workers, 1 025 vs
+// 4 097 buffers 61.5k vs 58.1k and 63.2k vs 60.8k reads/s, host CPU 55 vs 75
+// s.  (One client alone gets a quarter of the workers.)  $BT2G_READAHEAD
+// overrides; never more than the reference's own number.  Which buffer a batch lands in
 // does not change any alignment (each read's RNG is seeded from the read
 // itself), so the SAM is the stock server's -- the SAM-parity tests check it.
 //
@@ -73,7 +78,8 @@ bool PatternSourceServiceFactory::align(int fd, long data_size) {
 	if(const char* e = getenv("BT2G_READAHEAD")) {
 		if(atol(e) > 0) depth = (unsigned int)atol(e);
 	} else if(bt2gf::enabled() && bt2gf::count() > 0) {
-		depth = (unsigned int)(bt2gf::count() + 1);
+		const size_t n = bt2gf::count();
+		depth = (unsigned int)std::max(n / 4 + 1, std::min<size_t>(n + 1, 64));   // (few workers: all of them)
 	}
 	if(depth < n_readahead_) const_cast<unsigned int&>(n_readahead_) = depth;
 	return bt2g_real__ZN27PatternSourceServiceFactory5alignEil(this, fd, data_size);
