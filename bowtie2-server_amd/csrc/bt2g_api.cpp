@@ -507,11 +507,11 @@ int bt2g_open_mem(const bt2g_index_mem* m, int device, bt2g_ctx** out) {
 	// the device's stream-ordered pool keeps what the _dev calls free
 	// (hipMallocAsync scratch): with the default release threshold of 0 every
 	// synchronisation may hand it back to the driver and the next call maps it
-	// again ($BT2G_POOL_KEEP=0: the default behaviour, for A/B runs)
+	// again ($BT2G_POOL_KEEP=1 keeps it; opt-in until measured on the paired step)
 	{
 		const char* pk = getenv("BT2G_POOL_KEEP");
 		hipMemPool_t pool;
-		if(!(pk && pk[0] == '0') && hipDeviceGetDefaultMemPool(&pool, device) == hipSuccess) {
+		if(pk && pk[0] == '1' && hipDeviceGetDefaultMemPool(&pool, device) == hipSuccess) {
 			uint64_t keep = UINT64_MAX;
 			(void)hipMemPoolSetAttribute(pool, hipMemPoolAttrReleaseThreshold, &keep);
 		}
