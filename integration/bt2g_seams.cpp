@@ -70,6 +70,7 @@
 #include "bt2g.h"
 #include "bt2g_fibers.h"
 #include "bt2g_gw_spec.h"
+#include "bt2g_refspec.h"
 
 extern "C" void bt2g_prof_thread(int role);   // bt2g_prof.cpp: CPU samples of this thread ($BT2G_SAMPLE)
 
@@ -1950,44 +1951,6 @@ void resolve_rows(const Ebwt& ebwtFw) {
 
 }  // namespace
 
-namespace {
-struct TSAListFill : public PList<TIndexOffU, CACHE_PAGE_SZ> {
-	// the effect of n calls of add(p, v) on the pool and the list's length,
-	// without writing the slots: returns how many were added
-	size_t reserve(Pool& p, size_t n) {
-		const size_t per = (size_t)CACHE_PAGE_SZ / sizeof(TIndexOffU);
-		size_t done = 0;
-		while(done < n) {
-			if(!ensure(p, 1)) return done;
-			if(cur_ == per) {
-				cur_ = 0;
-				curPage_++;
-			}
-			const size_t k = std::min(per - cur_, n - done);
-			cur_ += k;
-			done += k;
-		}
-		return done;
-	}
-	// slots [i, i + n) set to v, a page at a time
-	void fill(size_t i, size_t n, TIndexOffU v) {
-		const size_t per = (size_t)CACHE_PAGE_SZ / sizeof(TIndexOffU);
-		while(n) {
-			const size_t pg = i / per, off = i % per, k = std::min(per - off, n);
-			std::fill(pages_[pg] + off, pages_[pg] + off + k, v);
-			i += k;
-			n -= k;
-		}
-	}
-};
-// the slice's list and position (protected in PListSlice)
-struct TSliceAcc : public TSlice {
-	void fill(TIndexOffU v) {
-		if(len_) static_cast<TSAListFill*>(list_)->fill(i_, len_, v);
-	}
-};
-}  // namespace
-
 template <>
 void GroupWalk2S<TSlice, 16>::init(const Ebwt& ebwtFw, const BitPairReference& ref, SARangeWithOffs<TSlice>& sa,
                                    RandomSource& rnd, WalkMetrics& met) {
@@ -1997,7 +1960,7 @@ void GroupWalk2S<TSlice, 16>::init(const Ebwt& ebwtFw, const BitPairReference& r
 	// the range's offset slots as the cache would hold them before any walk
 	// (AlignmentCache::addOnTheFlyImpl above only reserves them); rows resolved
 	// earlier in this read are resolved again, to the same offsets
-	static_cast<TSliceAcc&>(sa.offs).fill(OFF_MASK);
+	static_cast<bt2gref::TSliceAcc&>(sa.offs).fill(OFF_MASK);
 	if(drv().gw.on) drv().gw.ranges.push_back(GwRange{sa.topf, sa.size(), sa.offs});
 }
 
@@ -2098,43 +2061,7 @@ void SwDriver::extend(const Read& rd, const Ebwt& ebwtFw, const Ebwt* ebwtBw, TI
 		this, rd, ebwtFw, ebwtBw, topf, botf, topb, botb, fw, off, len, prm, nlex, nrex);
 }
 
-// ---- AlignmentCache::addOnTheFlyImpl (aligner_cache.cpp:55-104) ---------------
-// Registers a seed hit's SA range in the current-read cache and appends one
-// OFF_MASK offset slot per row to salist_ -- one PList::add per row in the
-// reference; on an hg38-scale genome a seed in a repeat family has a range of
-// 10^5 rows, and every worker's 20 MB pool gets written (r03f: the loop was
-// 18 % of the drop-in's host CPU; r03h at 3.1 Gbp: its page-wise restatement's
-// fill still 12.5 %, page faults included, and 38 GB resident over 2 048
-// workers).  The slots' contents are read by GroupWalk2S alone (group_walk.h:
-// 368-372, 508), whose init / advanceElement the binding specialises: init
-// writes OFF_MASK over exactly the rows of the range it is handed (below), so
-// here the slots are only reserved.  Reserving keeps the reference's pool use
-// and failure point: PList::ensure(pool, 1) wherever the reference's add() of
-// that row would take a page (or fail), the rest of the page by the count.
-
-bool AlignmentCache::addOnTheFlyImpl(QVal& qv, const SAKey& sak, TIndexOffU topf, TIndexOffU botf, TIndexOffU topb,
-                                     TIndexOffU botb) {
-	(void)botb;
-	bool added = true;
-	if(!qv.valid()) qv.init((uint32_t)qlist_.size(), 0, 0);
-	qv.addRange(botf - topf);
-	if(!qlist_.add(pool(), sak)) return false;
-	SANode* s = samap_.add(pool(), sak, &added);
-	if(s == NULL) return false;
-	if(added) {
-		s->payload.i = (TIndexOffU)salist_.size();
-		s->payload.len = botf - topf;
-		s->payload.topf = topf;
-		s->payload.topb = topb;
-		const size_t n = botf - topf;
-		const size_t k = static_cast<TSAListFill&>(salist_).reserve(pool(), n);
-		if(k < n) {
-			s->payload.len = (TIndexOffU)k;
-			return false;
-		}
-	}
-	return true;
-}
+// ---- AlignmentCache::addOnTheFlyImpl (aligner_cache.cpp:55-104): bt2g_refspec.h
 
 // ---- SwDriver::extendSeeds (aligner_sw_driver.cpp:756-1297) -------------------
 // The unpaired extension loop, unchanged; the binding only records the

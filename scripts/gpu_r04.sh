@@ -1,0 +1,22 @@
+#!/bin/bash
+# Round-4 GPU steps, one gpurun call each:
+#   bash scripts/gpu_r04.sh gap TAG     kernel + HIP API trace of --mode paired (default path), gap summary
+#   bash scripts/gpu_r04.sh tests TAG   the GPU test suite and smoke()
+#   bash scripts/gpu_r04.sh batch TAG   the batch-first server vs the stock server (dropin_bench.py)
+set -o pipefail
+cd /tmp && export TMPDIR=/tmp
+cd "$GRAFT_REPO_ROOT" || exit 1
+O=gpurun_out/${2:-r04}
+mkdir -p $O
+case "$1" in
+gap)
+  timeout -k 10 600 rocprofv3 --kernel-trace --hip-trace --output-format csv -d $O/ptrace -o run -- \
+    python3 bench.py --mode paired --no-cpu-baseline --server-sample 0 --steps 2 --warmup 1 > $O/paired.json 2> $O/paired.log || { tail -20 $O/paired.log; exit 1; }
+  python3 scripts/gap_trace.py $O/ptrace 15 > $O/gap.txt 2>&1; cat $O/gap.txt | head -80
+  find $O/ptrace -name "*.csv" -size +20M -delete ;;
+tests)
+  timeout -k 10 1000 python -u -m pytest tests -m gpu -x -v --timeout 600 --timeout-method thread > $O/gpu_tests.log 2>&1 || { tail -20 $O/gpu_tests.log; exit 1; }
+  tail -2 $O/gpu_tests.log
+  timeout -k 10 300 python -u -c "import __graft_entry__ as g; g.smoke()" > $O/smoke.log 2>&1 || { tail $O/smoke.log; exit 1; }
+  echo smoke ok ;;
+esac
