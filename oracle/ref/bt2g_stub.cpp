@@ -22,6 +22,10 @@ void bt2ref_close(void* vh);
 void bt2ref_exact_sweep(void* vh, int n, const char** seqs, const char** quals, int mineMax, uint64_t* out);
 void bt2ref_one_mm(void* vh, int n, const char** seqs, const char** quals, const int64_t* minsc, int local, int nofw,
                    int norc, int cap, int64_t* out, int32_t* counts, uint64_t* bwops);
+void bt2ref_one_mm_sc(void* vh, int n, const char** seqs, const char** quals, const int64_t* minsc, int local,
+                      int nofw, int norc, int cap, int64_t* out, int32_t* counts, uint64_t* bwops, const void* sp);
+void bt2ref_exact_sweep_fr(void* vh, int n, const char** seqs, const char** quals, int mineMax, int nofw, int norc,
+                           uint64_t* out);
 void bt2ref_seed_search(void* vh, int n, const char** seqs, const char** quals, int seedlen, int interval, int offset,
                         int maxseeds, uint32_t* out, int32_t* nseeds, uint64_t* bwops);
 int bt2ref_sw(const char* seq, const char* qual, int fw, const uint8_t* rfmask, int ncol, int64_t minsc,
@@ -101,13 +105,12 @@ int bt2g_close(bt2g_ctx* c) {
 
 int bt2g_exact_sweep(bt2g_ctx* c, const uint8_t* reads, uint32_t stride, const uint32_t* lens, uint32_t n,
                      uint32_t mine_max, int nofw, int norc, uint32_t* out) {
-	if(nofw || norc) return fail(BT2G_ERR_ARG, "stub: nofw/norc unsupported");
 	for(uint32_t i = 0; i < n; i++) {
 		std::string s = ascii(reads + (size_t)i * stride, lens[i]), q(lens[i], 'I');
 		const char* sp = s.c_str();
 		const char* qp = q.c_str();
 		uint64_t o[8];
-		bt2ref_exact_sweep(c->ref, 1, &sp, &qp, (int)mine_max, o);
+		bt2ref_exact_sweep_fr(c->ref, 1, &sp, &qp, (int)mine_max, nofw, norc, o);
 		uint32_t* w = out + 8 * (size_t)i;
 		w[0] = (uint32_t)o[0]; w[1] = (uint32_t)o[1]; w[2] = (uint32_t)o[3]; w[3] = (uint32_t)o[4];
 		w[4] = (uint32_t)o[5]; w[5] = (uint32_t)o[6]; w[6] = (uint32_t)o[7]; w[7] = 0;
@@ -126,7 +129,7 @@ int bt2g_one_mm(bt2g_ctx* c, const uint8_t* reads, const uint8_t* quals, uint32_
 		int64_t ms = minsc[i];
 		std::vector<int64_t> o(6 * (size_t)cap + 6);
 		uint64_t ops = 0;
-		bt2ref_one_mm(c->ref, 1, &sp, &qp, &ms, sc->local, nofw, norc, (int)cap, o.data(), &counts[i], &ops);
+		bt2ref_one_mm_sc(c->ref, 1, &sp, &qp, &ms, sc->local, nofw, norc, (int)cap, o.data(), &counts[i], &ops, sc);
 		bwops[i] = (uint32_t)ops;
 		for(int32_t k = 0; k < counts[i] && k < (int32_t)cap; k++) {
 			bt2g_mm1& h = hits[(size_t)i * cap + k];

@@ -210,8 +210,17 @@ uint64_t bt2ref_ref_len(void* vh, uint32_t refidx) {
 
 // SeedAligner::exactSweep over n reads (ASCII seq/qual, NUL-terminated).
 // out per read: mineFw, mineRc, nelt, exact fw [top,bot), exact rc [top,bot), bwops
+void bt2ref_exact_sweep_fr(void* vh, int n, const char** seqs, const char** quals,
+                           int mineMax, int nofw, int norc, uint64_t* out);
+
 void bt2ref_exact_sweep(void* vh, int n, const char** seqs, const char** quals,
                         int mineMax, uint64_t* out /* 8 per read */) {
+	bt2ref_exact_sweep_fr(vh, n, seqs, quals, mineMax, 0, 0, out);
+}
+
+// The same with --nofw / --norc.
+void bt2ref_exact_sweep_fr(void* vh, int n, const char** seqs, const char** quals,
+                           int mineMax, int nofw, int norc, uint64_t* out /* 8 per read */) {
 	RefHandle* h = (RefHandle*)vh;
 	SeedAlignerX al;
 	SeedResults sr;
@@ -225,7 +234,7 @@ void bt2ref_exact_sweep(void* vh, int n, const char** seqs, const char** quals,
 		size_t mineFw = 0, mineRc = 0;
 		met.reset();
 		uint64_t ops0 = al.ops();
-		size_t nelt = al.exactSweep(*h->fw, rd, sc, false, false, (size_t)mineMax,
+		size_t nelt = al.exactSweep(*h->fw, rd, sc, nofw != 0, norc != 0, (size_t)mineMax,
 		                            mineFw, mineRc, true, sr, met);
 		uint64_t* o = out + 8 * (size_t)i;
 		o[0] = mineFw; o[1] = mineRc; o[2] = nelt;
@@ -238,14 +247,26 @@ void bt2ref_exact_sweep(void* vh, int n, const char** seqs, const char** quals,
 // SeedAligner::oneMmSearch (rep1mm, no repex, as bt2_search.cpp:3654-3667).
 // Writes hits in discovery order: 6 words each (top, bot, fw, score, edit pos, edit chr|readc<<8).
 // counts[i] = number of hits for read i (capped at cap per read).  out stride = cap*6.
+void bt2ref_one_mm_sc(void* vh, int n, const char** seqs, const char** quals,
+                      const int64_t* minsc, int local, int nofw, int norc,
+                      int cap, int64_t* out, int32_t* counts, uint64_t* bwops, const void* spp);
+
 void bt2ref_one_mm(void* vh, int n, const char** seqs, const char** quals,
                    const int64_t* minsc, int local, int nofw, int norc,
                    int cap, int64_t* out, int32_t* counts, uint64_t* bwops) {
+	bt2ref_one_mm_sc(vh, n, seqs, quals, minsc, local, nofw, norc, cap, out, counts, bwops, NULL);
+}
+
+// The same with a scoring scheme (ScoreParams*; NULL: the defaults of `local`).
+void bt2ref_one_mm_sc(void* vh, int n, const char** seqs, const char** quals,
+                      const int64_t* minsc, int local, int nofw, int norc,
+                      int cap, int64_t* out, int32_t* counts, uint64_t* bwops, const void* spp) {
 	RefHandle* h = (RefHandle*)vh;
 	SeedAlignerX al;
 	SeedResults sr;
 	SeedSearchMetrics met;
 	ScoreParams sp = {local ? 2 : 0, 6, 2, 1, 5, 3, 5, 3, 4, local, 0.0, 0.15};
+	if(spp) sp = *(const ScoreParams*)spp;
 	Scoring sc = makeScoring(sp);
 	for(int i = 0; i < n; i++) {
 		Read rd("r", seqs[i], quals[i]);

@@ -1,0 +1,166 @@
+"""SAM parity of the batch-first driver (integration/bt2g_batch.cpp).
+
+The reference's alignment server with its search workers replaced by batch
+driver threads: every read's worker logic (multiseedSearchWorker's per-read
+body, SwDriver::extendSeeds) runs as a resumable state machine and the
+engines take one call per stage for all reads in flight.  Its SAM must equal
+the stock server's on the same reads (sorted records, <= 10 000 reads per
+connection):
+
+  * -stub (CPU tests): oracle/_ref/bowtie2-align-server-batch-stub, the driver
+    over the CPU stand-in of the ABI (the reference answers every engine call),
+    which checks the driver's own logic -- the restated control flow, RNG
+    order, DP table reuse across minimum scores, CPU fallbacks;
+  * GPU: oracle/_ref/bowtie2-align-server-batch on libbt2g.so.
+"""
+import json
+import os
+import sys
+import time
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+for _p in (ROOT, os.path.join(ROOT, "bowtie2-server_amd", "tools"), os.path.join(ROOT, "tests", "golden")):
+    if _p not in sys.path:
+        sys.path.insert(0, _p)
+
+import bt2_index as bi  # noqa: E402
+import synth  # noqa: E402
+from oracle import ref_server as rs  # noqa: E402
+
+SRV_BATCH = os.path.join(rs.REF_DIR, "bowtie2-align-server-batch")
+SRV_BATCH_STUB = os.path.join(rs.REF_DIR, "bowtie2-align-server-batch-stub")
+LONGREADS = os.path.join(ROOT, "tests", "golden", "longreads.fq.gz")     # example/reads/longreads.fq
+
+
+def _need(*paths):
+    for p in paths:
+        if not os.path.exists(p):
+            pytest.skip(f"{os.path.relpath(p, ROOT)} not built (python -c 'import __graft_entry__ as g; g.build()')")
+
+
+@pytest.fixture(scope="module")
+def indexes(tmp_path_factory):
+    d = tmp_path_factory.mktemp("idx")
+    lam = bi.build_from_fasta(os.path.join(ROOT, "tests", "golden", "lambda_virus.fa"))
+    bi.write_index(str(d / "lambda_virus"), lam)
+    # 400 kb, two references, planted 2 kb near-repeats (multi-mappers, XS:i) and N runs
+    g = synth.genome(11, 400_000, n_repeats=60, rep_len=2000, n_copies=3, n_runs=5)
+    syn = bi.build_index([g[:200_000], g[200_000:]], names=[b"c1", b"c2"])
+    bi.write_index(str(d / "syn"), syn)
+    return {"lambda": str(d / "lambda_virus"), "synth": (str(d / "syn"), syn)}
+
+
+def _reads(idx, n, seed, dirpath, read_len=150):
+    import bench
+    r, q = bench.make_reads(idx.ref_codes, n, read_len, seed)
+    return rs.write_fastq_chunks(dirpath, r, q)
+
+
+def _run(binary, base, chunks, args, dirpath, tag, threads=2, env_extra=None):
+    stats = os.path.join(dirpath, f"stats_{tag}.json")
+    env = dict(rs.dropin_env(base, stats), **(env_extra or {}))
+    with rs.Server(base, threads=threads, args=args, binary=binary, env=env,
+                   log_path=os.path.join(dirpath, f"server_{tag}.log")) as s:
+        dt, outs = s.run(chunks, k=2)
+    st = None
+    for _ in range(50):                      # written by the driver's SIGTERM handler
+        if os.path.exists(stats):
+            st = json.load(open(stats))
+            break
+        time.sleep(0.1)
+    return dt, rs.sorted_records(outs), st
+
+
+def compare(binary, base, chunks, args, dirpath, threads=2, env_extra=None, cpu_ok=()):
+    t_ref, a, _ = _run(rs.SERVER, base, chunks, args, dirpath, "ref")
+    t_new, b, st = _run(binary, base, chunks, args, dirpath, "batch", threads, env_extra)
+    assert len(a) == len(b) and len(a) > 0
+    bad = [(x, y) for x, y in zip(a, b) if x != y]
+    assert not bad, f"{len(bad)} SAM records differ, first:\nref   {bad[0][0][:400]}\nbatch {bad[0][1][:400]}"
+    assert st is not None and st.get("driver") == "batch", "driver wrote no counts"
+    assert st["reads"] > 0 and st["exact_sweep"][0] > 0
+    for k in ("exact_sweep", "one_mm", "seed_search", "extend", "get_offset", "ungapped", "sw_dp"):
+        if k not in cpu_ok:
+            assert st[k][1] == 0, f"{k}: {st[k][1]} CPU fallbacks"
+    return t_ref, t_new, len(a), st
+
+
+CASES = [
+    ("sensitive", [], 1500),                       # configs[1] policy
+    ("local", ["--local"], 1000),                  # configs[3]
+    ("very_sensitive", ["--very-sensitive"], 800),
+    ("k5", ["-k", "5"], 800),                      # -k mode (no -M tightening)
+    ("mp_rdg", ["--mp", "4,2", "--rdg", "4,2", "--score-min", "L,-0.8,-0.8"], 800),
+    ("norc", ["--norc"], 600),
+]
+
+
+@pytest.mark.parametrize("name,args,n", CASES, ids=[c[0] for c in CASES])
+def test_batch_sam_parity_cpu(indexes, tmp_path, name, args, n):
+    _need(rs.SERVER, rs.CLIENT, SRV_BATCH_STUB)
+    base, idx = indexes["synth"]
+    chunks = _reads(idx, n, 7, str(tmp_path))
+    _, _, nrec, st = compare(SRV_BATCH_STUB, base, chunks, args, str(tmp_path))
+    assert st["sw_dp"][0] > 0
+
+
+def test_batch_no_speculation_cpu(indexes, tmp_path):
+    """BT2G_SPEC_DPS=1: every DP asked when the loop reaches it (no table reuse)."""
+    _need(rs.SERVER, rs.CLIENT, SRV_BATCH_STUB)
+    base, idx = indexes["synth"]
+    chunks = _reads(idx, 800, 17, str(tmp_path))
+    _, _, _, st = compare(SRV_BATCH_STUB, base, chunks, [], str(tmp_path), env_extra={"BT2G_SPEC_DPS": "1"})
+    assert st["dp"][0] == 0
+
+
+def test_batch_cpu_fallback_cpu(indexes, tmp_path):
+    """-N 1 seeds (the engine's seed search is exact-only) and --ignore-quals (a
+    mismatch model the engines do not implement): the driver runs the
+    reference's own code for those stages; SAM unchanged."""
+    _need(rs.SERVER, rs.CLIENT, SRV_BATCH_STUB)
+    base, idx = indexes["synth"]
+    chunks = _reads(idx, 500, 19, str(tmp_path))
+    compare(SRV_BATCH_STUB, base, chunks, ["-N", "1", "--ignore-quals"], str(tmp_path),
+            cpu_ok=("seed_search", "one_mm", "ungapped", "sw_dp"))
+
+
+def test_batch_longreads_cpu(indexes, tmp_path):
+    """configs[0]: lambda, example/reads/longreads.fq (6 000 reads of 40-2 561 bp)."""
+    _need(rs.SERVER, rs.CLIENT, SRV_BATCH_STUB, LONGREADS)
+    compare(SRV_BATCH_STUB, indexes["lambda"], [["-U", LONGREADS]], [], str(tmp_path),
+            cpu_ok=("exact_sweep", "seed_search", "extend", "sw_dp"))
+
+
+def test_batch_many_drivers_cpu(indexes, tmp_path):
+    """-p 6 drivers, two devices (BT2G_DEVICES=0,1: an index replica each)."""
+    _need(rs.SERVER, rs.CLIENT, SRV_BATCH_STUB)
+    base, idx = indexes["synth"]
+    chunks = _reads(idx, 3000, 23, str(tmp_path))
+    compare(SRV_BATCH_STUB, base, chunks, [], str(tmp_path), threads=6, env_extra={"BT2G_DEVICES": "0,1"})
+
+
+GPU_CASES = [
+    ("sensitive", [], 20000),
+    ("local", ["--local"], 10000),
+    ("very_sensitive", ["--very-sensitive"], 5000),
+]
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("name,args,n", GPU_CASES, ids=[c[0] for c in GPU_CASES])
+def test_batch_sam_parity_gpu(indexes, tmp_path, name, args, n):
+    _need(rs.SERVER, rs.CLIENT, SRV_BATCH)
+    base, idx = indexes["synth"]
+    chunks = _reads(idx, n, 7, str(tmp_path))
+    t_ref, t_new, nrec, st = compare(SRV_BATCH, base, chunks, args, str(tmp_path), threads=8)
+    print(f"\n[{name}] {nrec} records identical; stock {t_ref:.2f}s, batch {t_new:.2f}s; {st}")
+
+
+@pytest.mark.gpu
+def test_batch_longreads_gpu(indexes, tmp_path):
+    _need(rs.SERVER, rs.CLIENT, SRV_BATCH, LONGREADS)
+    t_ref, t_new, nrec, st = compare(SRV_BATCH, indexes["lambda"], [["-U", LONGREADS]], [], str(tmp_path),
+                                     cpu_ok=("exact_sweep", "seed_search", "extend", "sw_dp"))
+    print(f"\n[longreads] {nrec} records identical; stock {t_ref:.2f}s, batch {t_new:.2f}s; {st}")
