@@ -1203,6 +1203,7 @@ struct Tmp {
 	struct Late { void* h; const void* d; size_t n; };
 	std::vector<Late> late;               // outputs outside the mirror (copied at finish)
 	size_t sent = 0;                      // pinned bytes already on the device
+	size_t in_hi = 0;                     // end of the highest staged input (outputs past it are not sent)
 	size_t mo_lo = SIZE_MAX, mo_hi = 0;   // mirrored outputs still to bring back
 	size_t map_lo = SIZE_MAX;             // lowest pinned offset a kernel writes directly
 	bool pending = false;                 // staged inputs not yet sent
@@ -1214,6 +1215,7 @@ struct Tmp {
 		if(uint8_t* pn = h && count ? ar.pinned(bytes) : nullptr) {
 			memcpy(pn, h, bytes);
 			*d = (T*)(c->pin_dev + (pn - c->pin));
+			in_hi = std::max(in_hi, (size_t)(pn - c->pin) + bytes);
 			pending = true;
 			return BT2G_OK;
 		}
@@ -1225,9 +1227,12 @@ struct Tmp {
 	}
 	// the staged inputs to the device (before the first launch that reads them)
 	int send() {
-		if(c->pin_used > sent) {
-			HIPCHK(hipMemcpyAsync(c->pin_dev + sent, c->pin + sent, c->pin_used - sent, hipMemcpyHostToDevice, st));
-			sent = c->pin_used;
+		// only the staged inputs: the out() slots and mapped() blocks after them are
+		// written by the kernels (the whole used span was copied, up to
+		// several MB of worst-case candidate / edit slots per DP batch)
+		if(in_hi > sent) {
+			HIPCHK(hipMemcpyAsync(c->pin_dev + sent, c->pin + sent, in_hi - sent, hipMemcpyHostToDevice, st));
+			sent = in_hi;
 		}
 		pending = false;
 		return BT2G_OK;

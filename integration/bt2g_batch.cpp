@@ -23,9 +23,11 @@
 // rankSeedHits, SwDriver::eeSaTups and prioritizeSATups with their RNG
 // draws); what is restated are the two control loops that do wait:
 //
-//   Driver::step_read   multiseedSearchWorker's per-read body, unpaired
-//                       (bt2_search.cpp:3266-4160)
-//   SwDriverB::ext_step SwDriver::extendSeeds (aligner_sw_driver.cpp:756-1297)
+//   Driver::step_read          multiseedSearchWorker's per-read body, unpaired
+//                              and paired (bt2_search.cpp:3266-4160)
+//   SwDriverB::ext_step        SwDriver::extendSeeds (aligner_sw_driver.cpp:756-1297)
+//   SwDriverB::ext_step_paired SwDriver::extendSeedsPaired, mate search included
+//                              (aligner_sw_driver.cpp:1385-2402)
 //
 // and the replay of SwAligner::nextAlignment's RNG draws from the engine's
 // candidate fates (aligner_sw.cpp:737-1146).
@@ -80,6 +82,7 @@
 #include "aln_sink.h"
 #include "dp_framer.h"
 #include "pat.h"
+#include "pe.h"
 #include "read.h"
 #include "scoring.h"
 #include "simple_func.h"
@@ -147,8 +150,10 @@ extern bool        R_metricsStderr       __asm__("_ZL13metricsStderr");
 extern OutFileBuf* R_metricsOfb          __asm__("_ZL20multiseed_metricsOfb");
 extern std::string R_logDps              __asm__("_ZL6logDps");
 extern std::string R_logDpsOpp           __asm__("_ZL9logDpsOpp");
-extern bool gReportDiscordant;           // bt2_search.cpp:127-128 (global there)
+extern bool gReportDiscordant;           // bt2_search.cpp:118-128 (globals there)
 extern bool gReportMixed;
+extern bool gMate1fw, gMate2fw, gFlippedMatesOK, gDovetailMatesOK, gContainMatesOK, gOlapMatesOK, gExpandToFrag;
+extern int gMinInsert, gMaxInsert;
 
 namespace {
 
@@ -329,6 +334,7 @@ thread_local std::atomic<uint64_t>* t_cpu_ext = nullptr;
 // One engine DP: SwAligner::initRead + initRef + align and every
 // nextAlignment walk of it (bt2g_sw_align_bt), keyed by the problem.
 struct DpRes {
+	int mate = 0;          // the read of the DP (its row in the slot)
 	int32_t fw = 0;
 	uint32_t refidx = 0;
 	int64_t refl = 0;
@@ -336,6 +342,7 @@ struct DpRes {
 	bt2g_sw_rect rect{};
 	int32_t minsc = 0;
 	TRefOff tlen = 0;
+	bool extend = true;    // seed extension (else mate search), SwAligner::initRef's `extend`
 	bool ready = false, cpu = false;
 	bt2g_sw_result o{};
 	int32_t naln = 0;
@@ -345,36 +352,66 @@ struct DpRes {
 	std::vector<bt2g_sw_aln> alns;
 	std::vector<bt2g_edit> edits;
 	DPRect drect;          // for the CPU path (reads the engine does not take)
+	bool same_problem(int m, bool f, uint32_t ti, const DPRect& r) const {
+		return mate == m && fw == (f ? 1 : 0) && refidx == ti && refl == r.refl &&
+		       ncol == (uint32_t)(r.refr + 1 - r.refl) && rect.triml == (int32_t)r.triml &&
+		       rect.corel == (int32_t)r.corel && rect.corer == (int32_t)r.corer;
+	}
 };
 
 bool u8_regime(int64_t minsc) { return R_enable8 && minsc >= -254; }
 
+// The SwAligner after align(): the engine's candidate list replayed by
+// nextAlignment (or, for a DP the engine does not take, the driver thread's
+// own SwAligner).
+struct Replay {
+	DpRes* dp = nullptr;
+	size_t cural = 0;
+	uint32_t next = 0;
+	size_t next_edit = 0;
+	bool cpu = false;
+	void start(DpRes* d) {
+		dp = d;
+		cural = 0;
+		next = 0;
+		next_edit = 0;
+		cpu = d->cpu;
+	}
+};
+
 struct Driver;
 struct Slot;
 
-// ---- SwDriver::extendSeeds as a resumable state machine -----------------------
-// (aligner_sw_driver.cpp:756-1297, unpaired).  Members of the reference's
-// SwDriver (satpos_, gws_, rands_, eehits_, seenDiags1_, redAnchor_, res*_)
-// are used as the reference uses them; the loop's locals live here so that
-// it can stop where it needs an engine result and resume there.
+// ---- SwDriver::extendSeeds / extendSeedsPaired as resumable state machines ----
+// (aligner_sw_driver.cpp:756-1297 and 1385-2402).  Members of the reference's
+// SwDriver (satpos_, gws_, rands_, eehits_, seenDiags*_, red*_, res*_,
+// mateStreaks_) are used as the reference uses them; the loops' locals live
+// here so that a loop can stop where it needs an engine result and resume
+// there.
 enum { EXTEND_BLOCKED = 0 };
 enum { FOUND_NONE_ = 0, FOUND_EE_, FOUND_UNGAPPED_ };
+enum { X_START = 0, X_AFTER_EE_ROWS, X_AFTER_EXT, X_AFTER_PRIO_ROWS, X_AFTER_UG, X_AFTER_DP, X_AFTER_MDP };
 
 struct SwDriverB : public SwDriver {
 	explicit SwDriverB(size_t bytes) : SwDriver(bytes) {}
 
-	// extendSeeds arguments (bt2_search.cpp:3559-3593 / 3741-3775 / 4017-4051)
+	// extendSeeds / extendSeedsPaired arguments (bt2_search.cpp:3505-3593 and twins)
+	int mate = 0;                  // the anchor mate (0: mate 1)
+	bool paired = false, anchor1 = true, oppFilt = false;
 	int seedmms = 0, seedlen = 0, seedival = 0;
 	TAlScore* minsc = nullptr;
-	int nceil = 0;
-	size_t maxIters = 0, maxUg = 0, maxDp = 0, maxUgStreak = 0, maxDpStreak = 0;
+	TAlScore* ominsc = nullptr;
+	int nceil = 0, onceil = 0;
+	bool nofw = false, norc = false;
+	size_t maxIters = 0, maxUg = 0, maxDp = 0, maxEeStreak = 0, maxUgStreak = 0, maxDpStreak = 0, maxMateStreak = 0;
+	bool swMateImmediately = true;
 	bool* exhaustive = nullptr;
 	// loop state
-	int pc = 0;
+	int pc = X_START;
 	bool all = false, eeMode = false, firstEe = false, firstExtend = false;
-	size_t nonz = 0, nelt = 0, neltLeft = 0, rows = 0, eltsDone = 0, rdlen = 0;
-	TAlScore perfectScore = 0;
-	size_t i = 0, riter = 0;
+	size_t nonz = 0, nelt = 0, neltLeft = 0, rows = 0, orows = 0, eltsDone = 0, rdlen = 0, ordlen = 0;
+	TAlScore perfectScore = 0, operfectScore = 0, bestPairScore = 0;
+	size_t i = 0;
 	bool is_small = false, fw = false, first = false;
 	uint32_t rdoff = 0, seedhitlen = 0;
 	TIndexOffU tidx = 0, toff = 0, tlen = 0;
@@ -386,25 +423,33 @@ struct SwDriverB : public SwDriver {
 	bool found = false;
 	DPRect rect;
 	int ug_ret = 0;
-	// the DP in replay (the reference's SwAligner after align())
-	DpRes* dp = nullptr;
-	size_t cural = 0;
-	uint32_t dp_next = 0;
-	size_t dp_next_edit = 0;
+	Replay a;                      // the anchor's DP (SwAligner swa)
 	bool firstInner = true;
-	bool cpu_dp = false;       // replayed by the driver thread's own SwAligner
+	int res_kind = 0;              // the anchor result in hand: FOUND_EE_ / FOUND_UNGAPPED_ / FOUND_NONE_ (resGap_)
+	// the opposite mate (extendSeedsPaired)
+	Replay o;                      // the opposite mate's DP (SwAligner oswa)
+	bool foundConcordant = false, foundMate = false, didAnchor = false;
+	TRefOff off = 0;
+	TAlScore ominsc_cur = 0;
+	int oreadGaps = 0, orefGaps = 0;
+	bool oleft = false, ofw = false;
+	int64_t oll = 0, olr = 0, orl = 0, orr = 0;
+	DPRect orect;
 
-	int ext_step(Driver& d, Slot& s);
-	bool replay_next(Driver& d, Slot& s, SwResult& res);
-	bool need_dp(Driver& d, Slot& s, int& out);
+	SwResult* res_ptr() { return res_kind == FOUND_EE_ ? &resEe_ : res_kind == FOUND_UNGAPPED_ ? &resUngap_ : &resGap_; }
+	EIvalMergeListBinned& seenDiags() { return anchor1 ? seenDiags1_ : seenDiags2_; }
+
+	int ext_step(Driver& d, Slot& s);          // extendSeeds
+	int ext_step_paired(Driver& d, Slot& s);   // extendSeedsPaired
+	bool need_dp(Driver& d, Slot& s, int m, bool f, TIndexOffU ti, TRefOff tl, const DPRect& r, TAlScore ms,
+	             bool extend, bool spec, bool force_cpu, Replay& rp);
 	void speculate(Driver& d, Slot& s, std::vector<DpRes*>& out, size_t k);
-
-	// protected reference members, for the driver
-	EList<SATupleAndPos, 16>& sp() { return satpos_; }
+	bool replay_next(Driver& d, Slot& s, Replay& rp, bool opp, TAlScore ms, SwResult& res);
+	bool replay_done(Driver& d, const Replay& rp, bool opp) const;
+	bool dp_found(Driver& d, Slot& s, Replay& rp, bool opp, TAlScore ms, TAlScore& bestCell);
 };
 
-// One read in flight.  Owns the reference's per-read objects a worker thread
-// owns (bt2_search.cpp:3086-3176), reused read after read.
+// A connection's read buffer the driver holds (PSFactory::ReadAhead's element).
 struct Elem {
 	ReadElement re;
 	int live = 0;
@@ -412,10 +457,37 @@ struct Elem {
 };
 
 enum {
-	P_START = 0, P_AFTER_EXACT, P_AFTER_EXT_EXACT, P_1MM, P_AFTER_1MM, P_AFTER_EXT_1MM, P_ROUND, P_AFTER_SEEDS,
-	P_ROUND_EXT, P_AFTER_EXT_SEEDS, P_FINISH
+	P_START = 0, P_AFTER_EXACT, P_EXT_EXACT, P_1MM, P_AFTER_1MM, P_EXT_1MM, P_ROUND, P_AFTER_SEEDS, P_EXT_SEEDS,
+	P_FINISH
 };
 
+// Engine results of one mate.
+struct MateRes {
+	uint32_t sweep[8] = {0};
+	bool sweep_asked = false;
+	int32_t mm_minsc = 0;
+	int mm_nofw = 0, mm_norc = 0;
+	bool mm_asked = false;
+	std::vector<bt2g_mm1> mm;
+	int32_t mm_cnt = 0;
+	uint32_t mm_ops = 0;
+	// seed search (a round's; round 0's asked with the exact sweep, its arguments
+	// being known when the read is set up)
+	bool sd_ready = false;
+	uint32_t sd_L = 0, sd_per = 0, sd_off = 0, sd_nof = 0;
+	std::vector<uint32_t> sd_out;      // [strand][offset][topf, botf, topb, botb]
+	int32_t sd_ns = 0;
+	uint32_t sd_ops = 0;
+	// row in this round's engine call
+	uint64_t row_stamp = ~0ull;
+	uint32_t row = 0;
+	// seeds instantiated this round (instantiateSeeds, aligner_seed.cpp:556-580)
+	uint64_t valid_fw = 0, valid_rc = 0;
+	std::vector<uint64_t> valid_big;   // (reads with more than 64 seed offsets per strand)
+};
+
+// One read (pair) in flight.  Owns the reference's per-read objects a worker
+// thread owns (bt2_search.cpp:3086-3176), reused read after read.
 struct Slot {
 	Slot(const ReportingParams& rp, Mapq& mapq, size_t tid)
 		: scCurrent((uint64_t)R_seedCacheCurrentMB * 1024 * 1024, false),
@@ -429,52 +501,38 @@ struct Slot {
 	AlnSinkWrap msinkwrap;
 	RandomSource rnd;
 	PerReadMetrics prm;
-	EList<Seed> seeds;
+	EList<Seed> seeds[2];
 	Constraint gc = Constraint::penaltyFuncBased(R_scoreMin);   // (a Seed points at it)
 	EList<uint32_t> offIdx2off;
 	RefTables tab;
 
-	// the read
+	// the read (pair)
 	Elem* el = nullptr;
-	Read* rd = nullptr;
-	Read* rdb = nullptr;     // the buffer's mate-2 slot (empty: unpaired)
+	Read* rds[2] = {nullptr, nullptr};
 	TReadId rdid = 0;
 	AlnSink* msink = nullptr;
+	bool paired = false;
 
 	// multiseedSearchWorker's per-read locals (bt2_search.cpp:3283-3451, 3814-3823)
 	int pc = P_START;
-	size_t rdlen = 0;
-	TAlScore minsc = 0;
+	size_t rdlens[2] = {0, 0};
+	TAlScore minsc[2] = {0, 0};
 	bool nfilt[2] = {true, true}, scfilt[2] = {true, true}, lenfilt[2] = {true, true}, qcfilt[2] = {true, true};
-	bool filt = true, nofw = false, norc = false, done = false, exhaustive[2] = {false, false};
-	bool yfw = false, yrc = false;
-	int nceil = 0, interval = 0;
-	size_t streak = 0, mxDp = 0, mxUg = 0, mxIter = 0, nrounds = 0, nelt = 0;
-	size_t minedfw = 0, minedrc = 0;
-	int seedlen = 0;
-	size_t roundi = 0, offset = 0;
+	bool filt[2] = {true, true}, nofw[2] = {false, false}, norc[2] = {false, false}, done[2] = {false, false};
+	bool exhaustive[2] = {false, false}, yfw[2] = {false, false}, yrc[2] = {false, false};
+	int nceil[2] = {0, 0}, interval[2] = {0, 0}, seedlens[2] = {0, 0};
+	size_t streak[2] = {0, 0}, mtStreak[2] = {0, 0}, mxDp[2] = {0, 0}, mxUg[2] = {0, 0}, mxIter[2] = {0, 0};
+	size_t nrounds[2] = {0, 0}, nelt[2] = {0, 0}, minedfw[2] = {0, 0}, minedrc[2] = {0, 0};
+	size_t matemap[2] = {0, 1};
+	size_t matei = 0, roundi = 0;
 	size_t seedsTried = 0, seedsTriedMS[4] = {0, 0, 0, 0};
 	size_t nUniqueSeeds = 0, nRepeatSeeds = 0, seedHitTot = 0;
 	size_t nUniqueSeedsMS[4] = {0, 0, 0, 0}, nRepeatSeedsMS[4] = {0, 0, 0, 0}, seedHitTotMS[4] = {0, 0, 0, 0};
-	uint64_t valid_fw = 0, valid_rc = 0;   // seeds instantiated this round (instantiateSeeds, aligner_seed.cpp:556-580)
-	std::vector<uint64_t> valid_big;       // (reads with more than 64 seed offsets per strand)
+	size_t round_off[2] = {0, 0};       // this round's seed offset per mate
+	bool round_go[2] = {false, false};  // (the round searches this mate unless an earlier one stops it)
 
-	// engine results
-	uint32_t sweep[8] = {0};
-	bool mm_asked = false;
-	int32_t mm_minsc = 0;
-	int mm_nofw = 0, mm_norc = 0;
-	std::vector<bt2g_mm1> mm;
-	int32_t mm_cnt = 0;
-	uint32_t mm_ops = 0;
-	// seed search (the round-0 one asked with the exact sweep: its arguments are
-	// known when the read is set up)
-	bool sd_ready = false;
-	uint32_t sd_L = 0, sd_per = 0, sd_off = 0, sd_nof = 0;
-	std::vector<uint32_t> sd_out;      // [strand][offset][topf, botf, topb, botb]
-	int32_t sd_ns = 0;
-	uint32_t sd_ops = 0;
-	// pending requests of this slot's extension loop
+	MateRes mr[2];
+	// pending requests of the extension loop (its anchor: sd.mate)
 	std::vector<bt2g_ext_in> ext_in;
 	std::vector<bt2g_ext_out> ext_out;
 	std::vector<uint32_t> off_rows, off_vals;
@@ -482,7 +540,7 @@ struct Slot {
 	bt2g_ug_problem ug_p{};
 	bt2g_ug_result ug_r{};
 	std::vector<bt2g_edit> ug_ed;
-	// the read's DP table (speculative and asked DPs)
+	// the read's DP table (asked and speculative DPs)
 	std::vector<std::unique_ptr<DpRes>> dps;
 	size_t ndps = 0;
 	DpRes* new_dp() {
@@ -492,9 +550,6 @@ struct Slot {
 		r->naln = 0;
 		return r;
 	}
-	// per-round row in the engine call's read pack
-	uint64_t row_stamp = ~0ull;
-	uint32_t row = 0;
 };
 
 // Reads packed as rows of one engine call.
@@ -523,9 +578,14 @@ struct Pack {
 	uint32_t n() const { return (uint32_t)lens.size(); }
 };
 
+struct Rq {
+	Slot* s;
+	int m;         // mate
+};
+
 // ---- one driver thread --------------------------------------------------------
 struct Driver {
-	explicit Driver(int tid_) : tid(tid_), swcpu(nullptr) {}
+	explicit Driver(int tid_) : tid(tid_), swcpu(nullptr), oswcpu(nullptr) {}
 	int tid;
 	bt2g_ctx* ctx = nullptr;
 	const Scoring* sc = nullptr;
@@ -536,12 +596,13 @@ struct Driver {
 	const BitPairReference* ref = nullptr;
 	std::unique_ptr<ReportingParams> rp;
 	std::unique_ptr<Mapq> mapq;
+	std::unique_ptr<PairedEndPolicy> pepol;
 	// per-thread reference objects (CPU paths; metrics)
 	SeedAligner al;
-	SwAligner swcpu;
+	SwAligner swcpu, oswcpu;
 	SeedSearchMetrics sdm;
 	WalkMetrics wlm;
-	SwMetrics swmSeed;
+	SwMetrics swmSeed, swmMate;
 	ReportingMetrics rpm;
 	// slots
 	std::vector<std::unique_ptr<Slot>> all;
@@ -553,7 +614,7 @@ struct Driver {
 	std::deque<Elem*> inbox;
 	size_t held = 0, max_held = 64;
 	// requests of this round
-	std::vector<Slot*> rq[K_N];
+	std::vector<Rq> rq[K_N];
 	std::vector<std::pair<Slot*, DpRes*>> rq_dp;
 	uint64_t stamp = 0;
 	size_t spec_k = 16;
@@ -565,53 +626,58 @@ struct Driver {
 	void step_read(Slot& s);
 	void setup_read(Slot& s);
 	void gpu_phase();
-	void prefetch_seeds(Slot& s);
+	void prefetch_seeds(Slot& s, int mate);
+	uint32_t row_of(Pack& pk, Slot& s, int m);
 
 	// engine calls of a round
-	int call_exact();
-	int call_1mm();
-	int call_seeds();
-	int call_ext();
-	int call_off();
-	int call_ug();
-	int call_dp();
-	int run_dp(const std::vector<std::pair<Slot*, DpRes*>>& v, uint32_t cap, uint32_t maxaln);
-	void cpu_dp(Slot& s, DpRes& r);
+	void call_exact();
+	void call_1mm();
+	void call_seeds();
+	void call_ext();
+	void call_off();
+	void call_ug();
+	void call_dp();
+	void run_dp(const std::vector<std::pair<Slot*, DpRes*>>& v, uint32_t cap, uint32_t maxaln);
+	void cpu_dp(Slot& s, DpRes& r, SwAligner& sw);
 
 	// helpers
-	bool seeds_valid(const Slot& s, bool fw, size_t i) const;
-	void set_valid(Slot& s, bool fw, size_t i);
+	bool seeds_valid(const MateRes& m, bool fw, size_t i) const;
+	void set_valid(MateRes& m, bool fw, size_t i);
 	void resolve_rows_request(Slot& s);
-	int after_seeds(Slot& s);
+	void after_seeds(Slot& s, int mate);
+	int instantiate(Slot& s, int mate, size_t offset);
+	bool engine_read(const Slot& s, int m) const { return s.rdlens[m] > 0 && s.rdlens[m] <= BT2G_MAX_READ_LEN; }
+	int ext(Slot& s) { return s.sd.paired ? s.sd.ext_step_paired(*this, s) : s.sd.ext_step(*this, s); }
 };
 
-uint32_t row_of(Pack& pk, Slot& s, uint64_t stamp) {
-	if(s.row_stamp != stamp) {
-		s.row_stamp = stamp;
-		s.row = pk.add(*s.rd);
+uint32_t Driver::row_of(Pack& pk, Slot& s, int m) {
+	MateRes& x = s.mr[m];
+	if(x.row_stamp != stamp) {
+		x.row_stamp = stamp;
+		x.row = pk.add(*s.rds[m]);
 	}
-	return s.row;
+	return x.row;
 }
 
 // ---- the engine calls of one round ---------------------------------------------
-int Driver::call_exact() {
-	// grouped by (nofw, norc): batch-wide arguments of bt2g_exact_sweep
-	std::vector<Slot*>& v = rq[K_EXACT];
-	if(v.empty()) return 0;
+// (grouped by each call's batch-wide arguments)
+void Driver::call_exact() {
+	std::vector<Rq>& v = rq[K_EXACT];
+	if(v.empty()) return;
 	thread_local Pack pk;
 	thread_local std::vector<uint32_t> out;
 	for(int g = 0; g < 4; g++) {
 		const bool nf = (g & 2) != 0, nr = (g & 1) != 0;
-		std::vector<Slot*> sub;
+		std::vector<Rq> sub;
 		uint32_t stride = 1;
-		for(Slot* s : v)
-			if(s->nofw == nf && s->norc == nr) {
-				sub.push_back(s);
-				stride = std::max<uint32_t>(stride, (uint32_t)s->rdlen);
+		for(const Rq& q : v)
+			if(q.s->nofw[q.m] == nf && q.s->norc[q.m] == nr) {
+				sub.push_back(q);
+				stride = std::max<uint32_t>(stride, (uint32_t)q.s->rdlens[q.m]);
 			}
 		if(sub.empty()) continue;
 		pk.reset(stride);
-		for(Slot* s : sub) pk.add(*s->rd);
+		for(const Rq& q : sub) pk.add(*q.s->rds[q.m]);
 		out.resize(8 * sub.size());
 		const uint64_t t0 = now_us();
 		int rc = bt2g_exact_sweep(ctx, pk.codes.data(), pk.stride, pk.lens.data(), pk.n(), 2, nf ? 1 : 0, nr ? 1 : 0,
@@ -619,27 +685,26 @@ int Driver::call_exact() {
 		g_call_us[K_EXACT] += now_us() - t0;
 		g_calls[K_EXACT]++;
 		if(rc) die("bt2g_exact_sweep", rc);
-		for(size_t i = 0; i < sub.size(); i++) memcpy(sub[i]->sweep, &out[8 * i], sizeof(sub[i]->sweep));
+		for(size_t i = 0; i < sub.size(); i++) memcpy(sub[i].s->mr[sub[i].m].sweep, &out[8 * i], 8 * sizeof(uint32_t));
 	}
 	g_req[K_EXACT] += v.size();
-	return 0;
 }
 
-int Driver::call_1mm() {
-	std::vector<Slot*>& v = rq[K_1MM];
-	if(v.empty()) return 0;
+void Driver::call_1mm() {
+	std::vector<Rq>& v = rq[K_1MM];
+	if(v.empty()) return;
 	thread_local Pack pk;
 	thread_local std::vector<int32_t> ms, cnt;
 	thread_local std::vector<uint32_t> ops;
 	thread_local std::vector<bt2g_mm1> h;
 	for(int g = 0; g < 4; g++) {
 		const int nf = (g >> 1) & 1, nr = g & 1;
-		std::vector<Slot*> sub;
+		std::vector<Rq> sub;
 		uint32_t stride = 1;
-		for(Slot* s : v)
-			if(s->mm_nofw == nf && s->mm_norc == nr) {
-				sub.push_back(s);
-				stride = std::max<uint32_t>(stride, (uint32_t)s->rdlen);
+		for(const Rq& q : v)
+			if(q.s->mr[q.m].mm_nofw == nf && q.s->mr[q.m].mm_norc == nr) {
+				sub.push_back(q);
+				stride = std::max<uint32_t>(stride, (uint32_t)q.s->rdlens[q.m]);
 			}
 		if(sub.empty()) continue;
 		uint32_t cap = 16;
@@ -651,8 +716,8 @@ int Driver::call_1mm() {
 			ops.resize(n);
 			h.resize(n * (size_t)cap);
 			for(size_t i = 0; i < n; i++) {
-				pk.add(*sub[i]->rd);
-				ms[i] = sub[i]->mm_minsc;
+				pk.add(*sub[i].s->rds[sub[i].m]);
+				ms[i] = sub[i].s->mr[sub[i].m].mm_minsc;
 			}
 			const uint64_t t0 = now_us();
 			int rc = bt2g_one_mm(ctx, pk.codes.data(), pk.quals.data(), pk.stride, pk.lens.data(), (uint32_t)n, ms.data(),
@@ -660,18 +725,18 @@ int Driver::call_1mm() {
 			g_call_us[K_1MM] += now_us() - t0;
 			g_calls[K_1MM]++;
 			if(rc && rc != BT2G_ERR_OVERFLOW) die("bt2g_one_mm", rc);
-			std::vector<Slot*> again;
+			std::vector<Rq> again;
 			uint32_t cap2 = cap;
 			for(size_t i = 0; i < n; i++) {
-				Slot* s = sub[i];
+				MateRes& x = sub[i].s->mr[sub[i].m];
 				if(cnt[i] > (int32_t)cap) {        // more hits than the slots: all of them, in order, next pass
-					again.push_back(s);
+					again.push_back(sub[i]);
 					cap2 = std::max<uint32_t>(cap2, (uint32_t)cnt[i]);
 					continue;
 				}
-				s->mm_cnt = cnt[i];
-				s->mm_ops = ops[i];
-				s->mm.assign(&h[i * cap], &h[i * cap] + cnt[i]);
+				x.mm_cnt = cnt[i];
+				x.mm_ops = ops[i];
+				x.mm.assign(&h[i * cap], &h[i * cap] + cnt[i]);
 			}
 			sub.swap(again);
 			cap = cap2;
@@ -679,70 +744,68 @@ int Driver::call_1mm() {
 		if(!sub.empty()) die("bt2g_one_mm (rerun)", BT2G_ERR_OVERFLOW);
 	}
 	g_req[K_1MM] += v.size();
-	return 0;
 }
 
-int Driver::call_seeds() {
-	std::vector<Slot*>& v = rq[K_SEEDS];
-	if(v.empty()) return 0;
+void Driver::call_seeds() {
+	std::vector<Rq>& v = rq[K_SEEDS];
+	if(v.empty()) return;
 	thread_local Pack pk;
 	thread_local std::vector<uint32_t> out, ops;
 	thread_local std::vector<int32_t> ns;
 	std::vector<bool> taken(v.size(), false);
 	for(size_t a = 0; a < v.size(); a++) {
 		if(taken[a]) continue;
-		Slot* s0 = v[a];
-		std::vector<Slot*> sub;
+		const MateRes& x0 = v[a].s->mr[v[a].m];
+		std::vector<Rq> sub;
 		uint32_t stride = 1, maxs = 1;
 		for(size_t b = a; b < v.size(); b++) {
-			Slot* s = v[b];
-			if(taken[b] || s->sd_L != s0->sd_L || s->sd_per != s0->sd_per || s->sd_off != s0->sd_off) continue;
+			const MateRes& x = v[b].s->mr[v[b].m];
+			if(taken[b] || x.sd_L != x0.sd_L || x.sd_per != x0.sd_per || x.sd_off != x0.sd_off) continue;
 			taken[b] = true;
-			sub.push_back(s);
-			stride = std::max<uint32_t>(stride, (uint32_t)s->rdlen);
-			maxs = std::max(maxs, s->sd_nof);
+			sub.push_back(v[b]);
+			stride = std::max<uint32_t>(stride, (uint32_t)v[b].s->rdlens[v[b].m]);
+			maxs = std::max(maxs, x.sd_nof);
 		}
 		pk.reset(stride);
-		for(Slot* s : sub) pk.add(*s->rd);
+		for(const Rq& q : sub) pk.add(*q.s->rds[q.m]);
 		const size_t n = sub.size();
 		out.resize(n * 2 * maxs * 4);
 		ops.resize(n);
 		ns.resize(n);
 		const uint64_t t0 = now_us();
-		int rc = bt2g_seed_search(ctx, pk.codes.data(), pk.stride, pk.lens.data(), (uint32_t)n, s0->sd_L, s0->sd_per,
-		                          s0->sd_off, maxs, out.data(), ns.data(), ops.data(), nullptr);
+		int rc = bt2g_seed_search(ctx, pk.codes.data(), pk.stride, pk.lens.data(), (uint32_t)n, x0.sd_L, x0.sd_per,
+		                          x0.sd_off, maxs, out.data(), ns.data(), ops.data(), nullptr);
 		g_call_us[K_SEEDS] += now_us() - t0;
 		g_calls[K_SEEDS]++;
 		if(rc) die("bt2g_seed_search", rc);
 		for(size_t i = 0; i < n; i++) {
-			Slot* s = sub[i];
-			s->sd_ns = ns[i];
-			s->sd_ops = ops[i];
-			s->sd_out.assign(2 * (size_t)s->sd_nof * 4, 0);
+			MateRes& x = sub[i].s->mr[sub[i].m];
+			x.sd_ns = ns[i];
+			x.sd_ops = ops[i];
+			x.sd_out.assign(2 * (size_t)x.sd_nof * 4, 0);
 			for(int f = 0; f < 2; f++)
-				for(uint32_t k = 0; k < s->sd_nof && k < maxs; k++)
-					memcpy(&s->sd_out[((size_t)f * s->sd_nof + k) * 4], &out[((i * 2 + f) * maxs + k) * 4], 16);
-			s->sd_ready = true;
+				for(uint32_t k = 0; k < x.sd_nof && k < maxs; k++)
+					memcpy(&x.sd_out[((size_t)f * x.sd_nof + k) * 4], &out[((i * 2 + f) * maxs + k) * 4], 16);
+			x.sd_ready = true;
 		}
 	}
 	g_req[K_SEEDS] += v.size();
-	return 0;
 }
 
-int Driver::call_ext() {
-	std::vector<Slot*>& v = rq[K_EXT];
-	if(v.empty()) return 0;
+void Driver::call_ext() {
+	std::vector<Rq>& v = rq[K_EXT];
+	if(v.empty()) return;
 	thread_local Pack pk;
 	thread_local std::vector<bt2g_ext_in> in;
 	thread_local std::vector<bt2g_ext_out> out;
 	uint32_t stride = 1;
-	for(Slot* s : v) stride = std::max<uint32_t>(stride, (uint32_t)s->rdlen);
+	for(const Rq& q : v) stride = std::max<uint32_t>(stride, (uint32_t)q.s->rdlens[q.m]);
 	pk.reset(stride);
 	in.clear();
-	for(Slot* s : v) {
-		const uint32_t r = pk.add(*s->rd);
-		for(const bt2g_ext_in& q : s->ext_in) {
-			in.push_back(q);
+	for(const Rq& q : v) {
+		const uint32_t r = pk.add(*q.s->rds[q.m]);
+		for(const bt2g_ext_in& x : q.s->ext_in) {
+			in.push_back(x);
 			in.back().read = r;
 		}
 	}
@@ -754,20 +817,19 @@ int Driver::call_ext() {
 	g_calls[K_EXT]++;
 	if(rc) die("bt2g_extend", rc);
 	size_t k = 0;
-	for(Slot* s : v) {
-		s->ext_out.assign(out.begin() + k, out.begin() + k + s->ext_in.size());
-		k += s->ext_in.size();
+	for(const Rq& q : v) {
+		q.s->ext_out.assign(out.begin() + k, out.begin() + k + q.s->ext_in.size());
+		k += q.s->ext_in.size();
 	}
 	g_req[K_EXT] += v.size();
-	return 0;
 }
 
-int Driver::call_off() {
-	std::vector<Slot*>& v = rq[K_OFF];
-	if(v.empty()) return 0;
+void Driver::call_off() {
+	std::vector<Rq>& v = rq[K_OFF];
+	if(v.empty()) return;
 	thread_local std::vector<uint32_t> rows, offs;
 	rows.clear();
-	for(Slot* s : v) rows.insert(rows.end(), s->off_rows.begin(), s->off_rows.end());
+	for(const Rq& q : v) rows.insert(rows.end(), q.s->off_rows.begin(), q.s->off_rows.end());
 	offs.resize(rows.size());
 	const uint64_t t0 = now_us();
 	int rc = bt2g_get_offset(ctx, rows.data(), (uint32_t)rows.size(), offs.data(), nullptr);
@@ -775,7 +837,8 @@ int Driver::call_off() {
 	g_calls[K_OFF]++;
 	if(rc) die("bt2g_get_offset", rc);
 	size_t k = 0;
-	for(Slot* s : v) {
+	for(const Rq& q : v) {
+		Slot* s = q.s;
 		// into the ranges' offset slots in the cache, where the reference's walks leave them
 		for(size_t j = 0; j < s->off_rows.size(); j++) {
 			const std::pair<size_t, size_t>& w = s->off_where[j];
@@ -785,23 +848,22 @@ int Driver::call_off() {
 		s->tab.gw.clear();
 	}
 	g_req[K_OFF] += v.size();
-	return 0;
 }
 
-int Driver::call_ug() {
-	std::vector<Slot*>& v = rq[K_UG];
-	if(v.empty()) return 0;
+void Driver::call_ug() {
+	std::vector<Rq>& v = rq[K_UG];
+	if(v.empty()) return;
 	thread_local Pack pk;
 	thread_local std::vector<bt2g_ug_problem> P;
 	thread_local std::vector<bt2g_ug_result> R;
 	thread_local std::vector<bt2g_edit> E;
 	uint32_t stride = 1;
-	for(Slot* s : v) stride = std::max<uint32_t>(stride, (uint32_t)s->rdlen);
+	for(const Rq& q : v) stride = std::max<uint32_t>(stride, (uint32_t)q.s->rdlens[q.m]);
 	pk.reset(stride);
 	P.resize(v.size());
 	for(size_t i = 0; i < v.size(); i++) {
-		P[i] = v[i]->ug_p;
-		P[i].read = pk.add(*v[i]->rd);
+		P[i] = v[i].s->ug_p;
+		P[i].read = pk.add(*v[i].s->rds[v[i].m]);
 	}
 	const uint32_t maxedit = stride + 1;
 	R.resize(v.size());
@@ -813,19 +875,18 @@ int Driver::call_ug() {
 	g_calls[K_UG]++;
 	if(rc) die("bt2g_ungapped", rc);
 	for(size_t i = 0; i < v.size(); i++) {
-		v[i]->ug_r = R[i];
+		v[i].s->ug_r = R[i];
 		const int32_t ne = R[i].ret == 1 ? std::min<int32_t>(std::max<int32_t>(R[i].nedit, 0), (int32_t)maxedit) : 0;
-		v[i]->ug_ed.assign(&E[i * maxedit], &E[i * maxedit] + ne);
+		v[i].s->ug_ed.assign(&E[i * maxedit], &E[i * maxedit] + ne);
 	}
 	g_req[K_UG] += v.size();
-	return 0;
 }
 
 // Fill + gather + the nextAlignment loop for every DP of the batch
 // (bt2g_sw_align_bt_packed).  A DP whose candidate list outgrew `cap`, or that
 // may have more than `maxaln` alignments, runs again alone with room for all;
 // one with more candidates than the engine takes goes to the CPU when used.
-int Driver::run_dp(const std::vector<std::pair<Slot*, DpRes*>>& v, uint32_t cap, uint32_t maxaln) {
+void Driver::run_dp(const std::vector<std::pair<Slot*, DpRes*>>& v, uint32_t cap, uint32_t maxaln) {
 	struct B {
 		Pack pk;
 		std::vector<bt2g_sw_problem> P;
@@ -839,9 +900,9 @@ int Driver::run_dp(const std::vector<std::pair<Slot*, DpRes*>>& v, uint32_t cap,
 	};
 	thread_local B b;
 	uint32_t stride = 1;
-	for(auto& q : v) stride = std::max<uint32_t>(stride, (uint32_t)q.first->rdlen);
+	for(auto& q : v) stride = std::max<uint32_t>(stride, (uint32_t)q.first->rdlens[q.second->mate]);
 	b.pk.reset(stride);
-	const uint64_t st = ++stamp;
+	++stamp;
 	const size_t n = v.size();
 	b.P.resize(n);
 	b.RC.resize(n);
@@ -849,7 +910,7 @@ int Driver::run_dp(const std::vector<std::pair<Slot*, DpRes*>>& v, uint32_t cap,
 		const DpRes& r = *v[i].second;
 		bt2g_sw_problem& p = b.P[i];
 		memset(&p, 0, sizeof(p));
-		p.read = row_of(b.pk, *v[i].first, st);
+		p.read = row_of(b.pk, *v[i].first, r.mate);
 		p.fw = r.fw;
 		p.refl = r.refl;
 		p.win_off = -1;                 // the engine's HBM-resident reference (initRef's window)
@@ -915,98 +976,98 @@ int Driver::run_dp(const std::vector<std::pair<Slot*, DpRes*>>& v, uint32_t cap,
 		        (unsigned long long)tot[2], oc, oe);
 		abort();
 	}
-	if(!again.empty()) return run_dp(again, cap2, maxaln2);
-	return 0;
+	if(!again.empty()) run_dp(again, cap2, maxaln2);
 }
 
-int Driver::call_dp() {
-	if(rq_dp.empty()) return 0;
+void Driver::call_dp() {
+	if(rq_dp.empty()) return;
 	g_req[K_DP] += rq_dp.size();
 	// long reads (> 1024 bases) batch apart: a batch is padded to its longest read
 	std::vector<std::pair<Slot*, DpRes*>> sh, lg;
-	for(auto& q : rq_dp) (q.first->rdlen > 1024 ? lg : sh).push_back(q);
+	for(auto& q : rq_dp) (q.first->rdlens[q.second->mate] > 1024 ? lg : sh).push_back(q);
 	const uint32_t cap = R_localAlign ? 2048 : 512;
 	if(!sh.empty()) run_dp(sh, cap, 8);
 	if(!lg.empty()) run_dp(lg, cap, 8);
-	return 0;
 }
 
 // A DP the engine does not take (reads at or above --cp-min, longer than
 // BT2G_MAX_READ_LEN, or more candidates than the engine holds): the
 // reference's own SwAligner, when the extension loop reaches it
-// (aligner_sw_driver.cpp:1104-1139).
-void Driver::cpu_dp(Slot& s, DpRes& r) {
-	const Read& rd = *s.rd;
-	swcpu.reset();
-	swcpu.initRead(rd.patFw, rd.patRc, rd.qual, rd.qualRev, 0, rd.length(), *sc);
+// (aligner_sw_driver.cpp:1104-1139, 2029-2079).
+void Driver::cpu_dp(Slot& s, DpRes& r, SwAligner& sw) {
+	const Read& rd = *s.rds[r.mate];
+	sw.reset();
+	sw.initRead(rd.patFw, rd.patRc, rd.qual, rd.qualRev, 0, rd.length(), *sc);
 	size_t nsInLeftShift = 0;
-	swcpu.initRef(r.fw != 0, r.refidx, r.drect, const_cast<BitPairReference&>(*ref), r.tlen, *sc, r.minsc, R_enable8,
-	              R_cminlen, R_cpow2, R_doTri, true, 0, nsInLeftShift);
+	sw.initRef(r.fw != 0, r.refidx, r.drect, const_cast<BitPairReference&>(*ref), r.tlen, *sc, r.minsc, R_enable8,
+	           R_cminlen, R_cpow2, R_doTri, r.extend, 0, nsInLeftShift);
 	TAlScore best = std::numeric_limits<TAlScore>::min();
-	r.o.aligned = swcpu.align(best) ? 1 : 0;
+	r.o.aligned = sw.align(best) ? 1 : 0;
 	r.o.best = best == std::numeric_limits<TAlScore>::min() ? std::numeric_limits<int32_t>::min() : (int32_t)best;
 	g_cpu[K_DP]++;
 }
 
-// ---- the extension loop ----------------------------------------------------------
-enum {
-	X_START = 0, X_AFTER_EE_ROWS, X_AFTER_EXT, X_AFTER_PRIO_ROWS, X_AFTER_UG, X_AFTER_DP
-};
+// ---- the extension loops ---------------------------------------------------------
 
-// The DP the loop needs now (framed at the current minsc): from the read's
-// table, or requested with up to spec_k - 1 speculative others.  Returns true
-// when it is available (d.dp set), false when the slot must wait.
-bool SwDriverB::need_dp(Driver& d, Slot& s, int& out) {
-	(void)out;
-	const int64_t ms = *minsc;
-	const int32_t nc = (int32_t)(rect.refr + 1 - rect.refl);
-	for(size_t k = 0; k < s.ndps; k++) {
-		DpRes* r = s.dps[k].get();
-		if(!r->ready || r->fw != (fw ? 1 : 0) || r->refidx != (uint32_t)tidx || r->refl != rect.refl ||
-		   r->ncol != (uint32_t)nc || r->rect.triml != (int32_t)rect.triml || r->rect.corel != (int32_t)rect.corel ||
-		   r->rect.corer != (int32_t)rect.corer)
-			continue;
-		bool ok = r->minsc == ms;
-		if(!ok && !R_localAlign && r->minsc < ms && u8_regime(r->minsc) == u8_regime(ms)) ok = true;
+// The DP the loop needs now: from the read's table, or requested (with up to
+// spec_k - 1 speculative others for a seed extension).  Returns true when it is
+// available (rp started), false when the slot must wait for this round's
+// engine call.
+//
+// force_cpu: a mate search under an anchor the driver thread's own SwAligner
+// is replaying -- no wait may come between (another slot would take that
+// SwAligner), so the mate DP runs on the CPU too.
+bool SwDriverB::need_dp(Driver& d, Slot& s, int m, bool f, TIndexOffU ti, TRefOff tl, const DPRect& r, TAlScore ms,
+                        bool extend, bool spec, bool force_cpu, Replay& rp) {
+	for(size_t k = 0; k < s.ndps && !force_cpu; k++) {
+		DpRes* x = s.dps[k].get();
+		if(!x->ready || !x->same_problem(m, f, (uint32_t)ti, r)) continue;
+		bool ok = x->minsc == ms;
+		if(!ok && !R_localAlign && !x->cpu && x->minsc < ms && u8_regime(x->minsc) == u8_regime(ms)) ok = true;
 		if(!ok) continue;
-		dp = r;
+		rp.start(x);
 		g_dp_used++;
-		if(r->minsc != ms) g_dp_reuse++;
+		if(x->minsc != ms) g_dp_reuse++;
 		return true;
 	}
 	g_dp_miss++;
-	DpRes* r = s.new_dp();
-	r->fw = fw ? 1 : 0;
-	r->refidx = (uint32_t)tidx;
-	r->refl = rect.refl;
-	r->ncol = (uint32_t)nc;
-	r->rect.triml = (int32_t)rect.triml;
-	r->rect.corel = (int32_t)rect.corel;
-	r->rect.corer = (int32_t)rect.corer;
-	r->rect.pad = 0;
-	r->minsc = (int32_t)ms;
-	r->tlen = tlen;
-	r->drect = rect;
-	const bool engine = d.bsc_ok && rdlen > 0 && rdlen <= BT2G_MAX_READ_LEN && rdlen < R_cminlen &&
+	DpRes* x = s.new_dp();
+	x->mate = m;
+	x->fw = f ? 1 : 0;
+	x->refidx = (uint32_t)ti;
+	x->refl = r.refl;
+	x->ncol = (uint32_t)(r.refr + 1 - r.refl);
+	x->rect.triml = (int32_t)r.triml;
+	x->rect.corel = (int32_t)r.corel;
+	x->rect.corer = (int32_t)r.corer;
+	x->rect.pad = 0;
+	x->minsc = (int32_t)ms;
+	x->tlen = tl;
+	x->extend = extend;
+	x->drect = r;
+	const size_t len = s.rdlens[m];
+	const bool engine = !force_cpu && d.bsc_ok && len > 0 && len <= BT2G_MAX_READ_LEN && len < R_cminlen &&
 	                    ms >= std::numeric_limits<int32_t>::min() && ms <= std::numeric_limits<int32_t>::max();
 	if(!engine) {
-		r->cpu = true;
-		r->ready = true;
-		dp = r;
+		x->cpu = true;
+		x->ready = true;
+		rp.start(x);
 		return true;
 	}
-	std::vector<DpRes*> spec;
-	if(d.spec_k > 1) speculate(d, s, spec, d.spec_k - 1);
-	d.rq_dp.emplace_back(&s, r);
-	for(DpRes* q : spec) d.rq_dp.emplace_back(&s, q);
-	g_dp_spec += spec.size();
-	dp = r;
+	d.rq_dp.emplace_back(&s, x);
+	if(spec && d.spec_k > 1) {
+		std::vector<DpRes*> more;
+		speculate(d, s, more, d.spec_k - 1);
+		for(DpRes* q : more) d.rq_dp.emplace_back(&s, q);
+		g_dp_spec += more.size();
+	}
+	rp.dp = x;
 	return false;
 }
 
-// Up to k more DPs this extension loop may ask for at the current minsc: one
-// per element of the prioritised ranges whose row is resolved, on a diagonal
-// not yet seen, framed exactly as the loop frames it
+// Up to k more seed-extension DPs this loop may ask for at the current minsc:
+// one per element of the prioritised ranges whose row is resolved, on a
+// diagonal not yet seen, framed exactly as the loop frames it
 // (aligner_sw_driver.cpp:937-1097).
 void SwDriverB::speculate(Driver& d, Slot& s, std::vector<DpRes*>& out, size_t k) {
 	const int64_t ms = *minsc;
@@ -1022,105 +1083,129 @@ void SwDriverB::speculate(Driver& d, Slot& s, std::vector<DpRes*>& out, size_t k
 		uint32_t ro = p.pos.rdoff;
 		if(!f) ro = (uint32_t)(rdlen - ro - p.pos.seedlen);
 		for(size_t e = 0; e < p.sat.size() && out.size() < k; e++) {
-			const TIndexOffU off = p.sat.offs[e];
-			if(off == OFF_MASK) continue;
+			const TIndexOffU so = p.sat.offs[e];
+			if(so == OFF_MASK) continue;
 			TIndexOffU ti = 0, to = 0, tl = 0;
 			bool straddled = false;
-			d.ebwtFw->joinedToTextOff(p.sat.key.len, off, ti, to, tl, false, straddled);
+			d.ebwtFw->joinedToTextOff(p.sat.key.len, so, ti, to, tl, false, straddled);
 			if(ti == OFF_MASK) continue;
 			const int64_t ro64 = (int64_t)to - ro;
 			Coord c(ti, ro64, f);
-			if(seenDiags1_.locusPresent(c)) continue;
+			if(seenDiags().locusPresent(c)) continue;
 			bool dup = (ti == tidx && ro64 == refoff && f == fw);
 			for(const Diag& x : seen) dup = dup || (x.t == ti && x.o == ro64 && x.f == f);
 			if(dup) continue;
 			seen.push_back(Diag{(uint32_t)ti, ro64, f});
 			DPRect r;
 			if(!dpframe.frameSeedExtensionRect(ro64, rdlen, tl, rg, fg, (size_t)nceil, R_maxhalf, r)) continue;
-			const int32_t nc = (int32_t)(r.refr + 1 - r.refl);
 			bool have = false;
 			for(size_t q = 0; q < s.ndps && !have; q++) {
 				const DpRes* x = s.dps[q].get();
-				have = x->fw == (f ? 1 : 0) && x->refidx == (uint32_t)ti && x->refl == r.refl && x->ncol == (uint32_t)nc &&
-				       x->rect.triml == (int32_t)r.triml && x->rect.corel == (int32_t)r.corel &&
-				       x->rect.corer == (int32_t)r.corer && x->minsc == (int32_t)ms;
+				have = x->same_problem(mate, f, (uint32_t)ti, r) && x->minsc == (int32_t)ms;
 			}
 			if(have) continue;
 			DpRes* q = s.new_dp();
+			q->mate = mate;
 			q->fw = f ? 1 : 0;
 			q->refidx = (uint32_t)ti;
 			q->refl = r.refl;
-			q->ncol = (uint32_t)nc;
+			q->ncol = (uint32_t)(r.refr + 1 - r.refl);
 			q->rect.triml = (int32_t)r.triml;
 			q->rect.corel = (int32_t)r.corel;
 			q->rect.corer = (int32_t)r.corer;
 			q->rect.pad = 0;
 			q->minsc = (int32_t)ms;
 			q->tlen = tl;
+			q->extend = true;
 			q->drect = r;
 			out.push_back(q);
 		}
 	}
 }
 
+// SwAligner::align's outcome (aligner_sw.cpp:677-729) at minsc `ms` from the
+// table entry (computed at a minsc <= ms, same fill width: see the header).
+bool SwDriverB::dp_found(Driver& d, Slot& s, Replay& rp, bool opp, TAlScore ms, TAlScore& bestCell) {
+	DpRes& r = *rp.dp;
+	if(rp.cpu) {
+		r.minsc = (int32_t)ms;
+		d.cpu_dp(s, r, opp ? d.oswcpu : d.swcpu);
+		bestCell = r.o.best == std::numeric_limits<int32_t>::min() ? std::numeric_limits<TAlScore>::min()
+		                                                            : (TAlScore)r.o.best;
+		return r.o.aligned != 0;
+	}
+	bestCell = r.o.best == std::numeric_limits<int32_t>::min() ? std::numeric_limits<TAlScore>::min()
+	                                                            : (TAlScore)r.o.best;
+	if(!r.o.aligned) return false;
+	for(const bt2g_sw_cand& c : r.cands)
+		if(c.score >= ms) return true;
+	return false;
+}
+
+bool SwDriverB::replay_done(Driver& d, const Replay& rp, bool opp) const {
+	if(rp.cpu) return (opp ? d.oswcpu : d.swcpu).done();
+	return rp.cural == rp.dp->cands.size();
+}
+
 // nextAlignment(): the candidate list walked as aligner_sw.cpp:758-1140 walks
-// it, with the engine's fate for each candidate: below `minsc` FILT_SCORE
-// (the caller may have tightened it since align()); FILT_START and
-// FILT_DOMINATED consume no randomness; every tried candidate draws
-// rnd.nextU32() and re-seeds rnd as the u8 / i16 branches do.
-bool SwDriverB::replay_next(Driver& d, Slot& s, SwResult& res) {
-	if(cpu_dp) return d.swcpu.nextAlignment(res, *minsc, s.rnd);
-	DpRes& r = *dp;
+// it, with the engine's fate for each candidate: below `ms` FILT_SCORE (the
+// caller may have tightened it since align()); FILT_START and FILT_DOMINATED
+// consume no randomness; every tried candidate draws rnd.nextU32() and
+// re-seeds rnd as the u8 / i16 branches do.
+bool SwDriverB::replay_next(Driver& d, Slot& s, Replay& rp, bool opp, TAlScore ms, SwResult& res) {
+	if(rp.cpu) return (opp ? d.oswcpu : d.swcpu).nextAlignment(res, ms, s.rnd);
+	DpRes& r = *rp.dp;
 	const size_t candsz = r.cands.size();
 	const bool u8 = r.o.u8succ != 0;
-	while(cural < candsz) {
-		const bt2g_sw_cand& c = r.cands[cural];
-		if(c.score < *minsc) {
-			cural++;
+	const size_t len = s.rdlens[r.mate];
+	while(rp.cural < candsz) {
+		const bt2g_sw_cand& c = r.cands[rp.cural];
+		if(c.score < ms) {
+			rp.cural++;
 			continue;
 		}
-		const int f = r.fates[cural];
+		const int f = r.fates[rp.cural];
 		if(f == BT_CAND_FATE_FILT_START || f == BT_CAND_FATE_FILT_DOMINATED) {
-			cural++;
+			rp.cural++;
 			continue;
 		}
 		if(f != BT_CAND_FATE_SUCCEEDED && f != BT_CAND_FATE_FAILED) {
-			fprintf(stderr, "bt2g batch: candidate %zu of %zu has no engine fate (%d)\n", cural, candsz, f);
+			fprintf(stderr, "bt2g batch: candidate %zu of %zu has no engine fate (%d)\n", rp.cural, candsz, f);
 			abort();
 		}
 		const uint32_t reseed = s.rnd.nextU32() + 1;
 		res.reset();
 		s.rnd.init(u8 ? reseed + 1 : reseed);
 		if(f == BT_CAND_FATE_FAILED) {
-			cural++;
+			rp.cural++;
 			continue;
 		}
-		if(dp_next >= (uint32_t)r.naln) {
+		if(rp.next >= (uint32_t)r.naln) {
 			fprintf(stderr, "bt2g batch: engine returned %d alignments, reference wants more\n", r.naln);
 			abort();
 		}
-		const bt2g_sw_aln& a = r.alns[dp_next];
-		if(a.cand != (int32_t)cural || a.nedit > (int32_t)r.maxedit) {
-			fprintf(stderr, "bt2g batch: alignment %u is candidate %d, expected %zu\n", dp_next, a.cand, cural);
+		const bt2g_sw_aln& a = r.alns[rp.next];
+		if(a.cand != (int32_t)rp.cural || a.nedit > (int32_t)r.maxedit) {
+			fprintf(stderr, "bt2g batch: alignment %u is candidate %d, expected %zu\n", rp.next, a.cand, rp.cural);
 			abort();
 		}
-		const bt2g_edit* ed = r.edits.data() + dp_next_edit;
-		dp_next_edit += (size_t)a.nedit;
-		dp_next++;
+		const bt2g_edit* ed = r.edits.data() + rp.next_edit;
+		rp.next_edit += (size_t)a.nedit;
+		rp.next++;
 		// backtraceNucleotides*: setScore / setShape / setRefNs (aligner_swsse_ee_u8.cpp:1822-1847)
-		const int based = (int)(rdlen - (size_t)a.trim5p - (size_t)a.trim3p - (size_t)a.nedit);
+		const int based = (int)(len - (size_t)a.trim5p - (size_t)a.trim3p - (size_t)a.nedit);
 		fill_alnres(res.alres, ed, (uint32_t)a.nedit, a.score, a.ns, a.gaps, based, (TRefId)r.refidx,
-		            (TRefOff)a.off + r.refl, (TRefOff)r.tlen, r.fw != 0, rdlen, (size_t)a.trim5p, (size_t)a.trim3p,
+		            (TRefOff)a.off + r.refl, (TRefOff)r.tlen, r.fw != 0, len, (size_t)a.trim5p, (size_t)a.trim3p,
 		            (size_t)a.refns);
-		cural++;
+		rp.cural++;
 		return true;
 	}
 	res.reset();
 	return false;
 }
 
-// The read's rows handed to GroupWalk2S::init by the call that just returned,
-// as one engine request (bt2g_get_offset == Ebwt::getOffset, bt2_idx.cpp:150-171).
+// The rows handed to GroupWalk2S::init by the call that just returned, as one
+// engine request (bt2g_get_offset == Ebwt::getOffset, bt2_idx.cpp:150-171).
 void Driver::resolve_rows_request(Slot& s) {
 	const size_t MAX_ROWS = 8192;          // per read (the rest: Ebwt::getOffset in advanceElement)
 	s.off_rows.clear();
@@ -1137,12 +1222,183 @@ void Driver::resolve_rows_request(Slot& s) {
 		s.tab.gw.clear();
 		return;
 	}
-	rq[K_OFF].push_back(&s);
+	rq[K_OFF].push_back(Rq{&s, s.sd.mate});
 }
 
+// The preamble of both loops' first pass: eeSaTups for end-to-end hits, or
+// SwDriver::extend for every seed-hit range + prioritizeSATups; then the rows
+// they hand GroupWalk2S resolved.  Expanded into each loop (below) so that
+// their resume points stay in one function each.
+#define BT2GB_EE_SETUP(LABEL_ROWS)                                                                     \
+	s.tab.gw.clear();                                                                                  \
+	s.tab.gw_on = true;                                                                                \
+	t_tab = &s.tab;                                                                                    \
+	eeMode = eeSaTups(rd, s.shs[mate], ebwtFw, ref, s.rnd, d.wlm, d.swmSeed, nelt, maxIters, all);     \
+	s.tab.gw_on = false;                                                                               \
+	t_tab = nullptr;                                                                                   \
+	d.resolve_rows_request(s);                                                                         \
+	if(!s.off_rows.empty()) {                                                                          \
+		pc = X_AFTER_EE_ROWS;                                                                          \
+		return EXTEND_BLOCKED;                                                                         \
+	}                                                                                                  \
+	LABEL_ROWS:;
+
+// every range the loop at aligner_sw_driver.cpp:519-604 visits, in its order,
+// extended on the engine first (SwDriver::extend below reads the results)
+static void ext_request(Driver& d, Slot& s, SwDriverB& x) {
+	s.ext_in.clear();
+	const size_t len = s.rdlens[x.mate];
+	if(!(R_doExtend && d.ebwtBw != NULL && len > 0 && len <= BT2G_MAX_READ_LEN)) return;
+	EList<SATuple, 16> sat;
+	for(size_t k = 0; k < x.nonz; k++) {
+		bool f = true;
+		uint32_t offidx = 0, ro = 0, sl = 0;
+		QVal qv = s.shs[x.mate].hitsByRank(k, offidx, ro, f, sl);
+		size_t nr = 0, ne = 0;
+		sat.clear();
+		s.ca.queryQval(qv, sat, nr, ne);
+		for(size_t j = 0; j < sat.size(); j++) {
+			const TIndexOffU sz = (TIndexOffU)sat[j].size();
+			bt2g_ext_in q;
+			q.read = 0;
+			q.fw = f ? 1 : 0;
+			q.off = ro;
+			q.len = sl;
+			q.topf = sat[j].topf;
+			q.botf = sat[j].topf + sz;
+			q.topb = sat[j].topb;
+			q.botb = sat[j].topb + sz;
+			if(sz > 0 && ro + sl <= len) s.ext_in.push_back(q);
+		}
+	}
+}
+
+#define BT2GB_PRIO_SETUP(LABEL_EXT, LABEL_ROWS)                                                        \
+	ext_request(d, s, *this);                                                                          \
+	if(!s.ext_in.empty()) {                                                                            \
+		d.rq[K_EXT].push_back(Rq{&s, mate});                                                           \
+		pc = X_AFTER_EXT;                                                                              \
+		return EXTEND_BLOCKED;                                                                         \
+	}                                                                                                  \
+	s.ext_out.clear();                                                                                 \
+	LABEL_EXT:                                                                                         \
+	s.tab.ext_on = !s.ext_in.empty();                                                                  \
+	s.tab.ext_keys.swap(s.ext_in);                                                                     \
+	s.tab.ext_vals.swap(s.ext_out);                                                                    \
+	s.tab.ext_next = 0;                                                                                \
+	s.tab.gw.clear();                                                                                  \
+	s.tab.gw_on = true;                                                                                \
+	t_tab = &s.tab;                                                                                    \
+	t_cpu_ext = &g_cpu[K_EXT];                                                                         \
+	prioritizeSATups(rd, s.shs[mate], ebwtFw, d.ebwtBw, ref, seedmms, maxIters, R_doExtend, true, true, 5, \
+	                 s.ca, s.rnd, d.wlm, s.prm, nelt, all);                                            \
+	s.tab.ext_on = false;                                                                              \
+	s.tab.gw_on = false;                                                                               \
+	t_tab = nullptr;                                                                                   \
+	d.resolve_rows_request(s);                                                                         \
+	if(!s.off_rows.empty()) {                                                                          \
+		pc = X_AFTER_PRIO_ROWS;                                                                        \
+		return EXTEND_BLOCKED;                                                                         \
+	}                                                                                                  \
+	LABEL_ROWS:;
+
+// Resolve the next element's offset and its reference coordinates
+// (aligner_sw_driver.cpp:924-952, 1626-1651).
+#define BT2GB_NEXT_ELEMENT()                                                                           \
+	{                                                                                                  \
+		WalkResult wr;                                                                                 \
+		const size_t elt = rands_[i].next(s.rnd);                                                      \
+		SARangeWithOffs<TSlice> sa;                                                                    \
+		sa.topf = satpos_[i].sat.topf;                                                                 \
+		sa.len = satpos_[i].sat.key.len;                                                               \
+		sa.offs = satpos_[i].sat.offs;                                                                 \
+		gws_[i].advanceElement((TIndexOffU)elt, ebwtFw, ref, sa, gwstate_, wr, d.wlm, s.prm);          \
+		eltsDone++;                                                                                    \
+		BT2GB_NELT_DEC;                                                                                \
+		tidx = 0;                                                                                      \
+		toff = 0;                                                                                      \
+		tlen = 0;                                                                                      \
+		bool straddled = false;                                                                        \
+		ebwtFw.joinedToTextOff(wr.elt.len, wr.toff, tidx, toff, tlen, eeMode, straddled);              \
+	}
+
+// Ask the engine for the ungapped alignment at refcoord (or run the
+// reference's on the CPU) and leave ungappedAlign's return in ug_ret
+// (aligner_sw_driver.cpp:1033-1043, 1742-1752).
+#define BT2GB_UNGAPPED(LABEL)                                                                          \
+	resUngap_.reset();                                                                                 \
+	if(d.bsc_ok && rdlen > 0 && rdlen <= BT2G_MAX_READ_LEN) {                                          \
+		memset(&s.ug_p, 0, sizeof(s.ug_p));                                                            \
+		s.ug_p.fw = fw ? 1 : 0;                                                                        \
+		s.ug_p.off = refcoord.off();                                                                   \
+		s.ug_p.refidx = (uint32_t)refcoord.ref();                                                      \
+		s.ug_p.minsc = (int32_t)*minsc;                                                                \
+		d.rq[K_UG].push_back(Rq{&s, mate});                                                            \
+		pc = X_AFTER_UG;                                                                               \
+		return EXTEND_BLOCKED;                                                                         \
+	LABEL:                                                                                             \
+		resUngap_.alres.reset();                                                                       \
+		ug_ret = s.ug_r.ret;                                                                           \
+		if(s.ug_r.ret == 1)                                                                            \
+			fill_alnres(resUngap_.alres, s.ug_ed.data(), (uint32_t)s.ug_r.nedit, s.ug_r.score, s.ug_r.ns, 0, \
+			            (int)(rdlen - (size_t)s.ug_r.nedit), refcoord.ref(), s.ug_r.refoff, (TRefOff)tlen, fw, \
+			            rdlen, (size_t)s.ug_r.trim5p, (size_t)s.ug_r.trim3p, (size_t)s.ug_r.refns);           \
+	} else {                                                                                           \
+		d.swcpu.reset();                                                                               \
+		ug_ret = d.swcpu.ungappedAlign(fw ? rd.patFw : rd.patRc, fw ? rd.qual : rd.qualRev, refcoord, ref, tlen, \
+		                               sc, gReportOverhangs, *minsc, resUngap_);                        \
+		g_cpu[K_UG]++;                                                                                 \
+	}
+
+// The report and -M tightening after an unpaired alignment
+// (aligner_sw_driver.cpp:1245-1285).
+static void tighten_unp(SwDriverB& x, AlnSinkWrap* msink) {
+	if(R_tighten > 0 && msink->Mmode() && msink->hasSecondBestUnp1()) {
+		TAlScore& m = *x.minsc;
+		if(R_tighten == 1) {
+			if(msink->bestUnp1() >= m) {
+				m = msink->bestUnp1();
+				if(m < x.perfectScore && msink->bestUnp1() == msink->secondBestUnp1()) m++;
+			}
+		} else if(R_tighten == 2) {
+			if(msink->secondBestUnp1() >= m) {
+				m = msink->secondBestUnp1();
+				if(m < x.perfectScore) m++;
+			}
+		} else {
+			TAlScore diff = msink->bestUnp1() - msink->secondBestUnp1();
+			TAlScore bot = msink->secondBestUnp1() + ((diff * 3) / 4);
+			if(bot >= m) {
+				m = bot;
+				if(m < x.perfectScore) m++;
+			}
+		}
+	}
+}
+
+// The paired score a concordant alignment must now reach under -M tightening
+// (aligner_sw_driver.cpp:1455-1473, 1948-1966, 2226-2244).
+static bool pair_floor(const SwDriverB& x, AlnSinkWrap* msink, TAlScore& ps) {
+	if(!(R_tighten > 0 && msink->Mmode() && msink->hasSecondBestPair())) return false;
+	if(R_tighten == 1) {
+		ps = msink->bestPair();
+	} else if(R_tighten == 2) {
+		ps = msink->secondBestPair();
+	} else {
+		TAlScore diff = msink->bestPair() - msink->secondBestPair();
+		ps = msink->secondBestPair() + (diff * 3) / 4;
+	}
+	if(R_tighten == 1 && ps < x.bestPairScore && msink->bestPair() == msink->secondBestPair()) ps++;
+	if(R_tighten >= 2 && ps < x.bestPairScore) ps++;
+	return true;
+}
+
+#define BT2GB_NELT_DEC if(!eeMode) neltLeft--
+
+// SwDriver::extendSeeds (aligner_sw_driver.cpp:756-1297).
 int SwDriverB::ext_step(Driver& d, Slot& s) {
 	AlnSinkWrap* msink = &s.msinkwrap;
-	const Read& rd = *s.rd;
+	const Read& rd = *s.rds[mate];
 	const Scoring& sc = *d.sc;
 	const Ebwt& ebwtFw = *d.ebwtFw;
 	const BitPairReference& ref = *d.ref;
@@ -1159,8 +1415,8 @@ int SwDriverB::ext_step(Driver& d, Slot& s) {
 	all = msink->allHits();
 	rdlen = rd.length();
 	perfectScore = sc.perfectScore(rdlen);
-	nonz = s.shs[0].nonzeroOffsets();
-	eeMode = s.shs[0].numE2eHits() > 0;
+	nonz = s.shs[mate].nonzeroOffsets();
+	eeMode = s.shs[mate].numE2eHits() > 0;
 	firstEe = true;
 	firstExtend = true;
 	s.prm.nEeFail = 0;
@@ -1170,23 +1426,11 @@ int SwDriverB::ext_step(Driver& d, Slot& s) {
 	neltLeft = 0;
 	rows = rdlen;
 	eltsDone = 0;
-	s.ndps = 0;
 	while(true) {
 		if(eeMode) {
 			if(firstEe) {
 				firstEe = false;
-				s.tab.gw.clear();
-				s.tab.gw_on = true;
-				t_tab = &s.tab;
-				eeMode = eeSaTups(rd, s.shs[0], ebwtFw, ref, s.rnd, d.wlm, d.swmSeed, nelt, maxIters, all);
-				s.tab.gw_on = false;
-				t_tab = nullptr;
-				d.resolve_rows_request(s);
-				if(!s.off_rows.empty()) {
-					pc = X_AFTER_EE_ROWS;
-					return EXTEND_BLOCKED;
-				}
-			after_ee_rows:;
+				BT2GB_EE_SETUP(after_ee_rows)
 			} else {
 				eeMode = false;
 			}
@@ -1196,60 +1440,7 @@ int SwDriverB::ext_step(Driver& d, Slot& s) {
 			if(*minsc == perfectScore) return EXTEND_PERFECT_SCORE;
 			if(firstExtend) {
 				nelt = 0;
-				// every range the loop at aligner_sw_driver.cpp:519-604 visits, in its
-				// order, extended on the engine first (SwDriver::extend reads them)
-				s.ext_in.clear();
-				if(R_doExtend && d.ebwtBw != NULL && rdlen > 0 && rdlen <= BT2G_MAX_READ_LEN) {
-					EList<SATuple, 16>& sat = satups_;
-					for(size_t k = 0; k < nonz; k++) {
-						bool f = true;
-						uint32_t offidx = 0, ro = 0, sl = 0;
-						QVal qv = s.shs[0].hitsByRank(k, offidx, ro, f, sl);
-						size_t nr = 0, ne = 0;
-						sat.clear();
-						s.ca.queryQval(qv, sat, nr, ne);
-						for(size_t j = 0; j < sat.size(); j++) {
-							const TIndexOffU sz = (TIndexOffU)sat[j].size();
-							bt2g_ext_in x;
-							x.read = 0;
-							x.fw = f ? 1 : 0;
-							x.off = ro;
-							x.len = sl;
-							x.topf = sat[j].topf;
-							x.botf = sat[j].topf + sz;
-							x.topb = sat[j].topb;
-							x.botb = sat[j].topb + sz;
-							if(sz > 0 && ro + sl <= rdlen) s.ext_in.push_back(x);
-						}
-					}
-					sat.clear();
-				}
-				if(!s.ext_in.empty()) {
-					d.rq[K_EXT].push_back(&s);
-					pc = X_AFTER_EXT;
-					return EXTEND_BLOCKED;
-				}
-				s.ext_out.clear();
-			after_ext:
-				s.tab.ext_on = !s.ext_in.empty();
-				s.tab.ext_keys.swap(s.ext_in);
-				s.tab.ext_vals.swap(s.ext_out);
-				s.tab.ext_next = 0;
-				s.tab.gw.clear();
-				s.tab.gw_on = true;
-				t_tab = &s.tab;
-				t_cpu_ext = &g_cpu[K_EXT];
-				prioritizeSATups(rd, s.shs[0], ebwtFw, d.ebwtBw, ref, seedmms, maxIters, R_doExtend, true, true, 5, s.ca,
-				                 s.rnd, d.wlm, s.prm, nelt, all);
-				s.tab.ext_on = false;
-				s.tab.gw_on = false;
-				t_tab = nullptr;
-				d.resolve_rows_request(s);
-				if(!s.off_rows.empty()) {
-					pc = X_AFTER_PRIO_ROWS;
-					return EXTEND_BLOCKED;
-				}
-			after_prio_rows:
+				BT2GB_PRIO_SETUP(after_ext, after_prio_rows)
 				neltLeft = nelt;
 				firstExtend = false;
 			}
@@ -1263,9 +1454,7 @@ int SwDriverB::ext_step(Driver& d, Slot& s) {
 			seedhitlen = satpos_[i].pos.seedlen;
 			if(!fw) rdoff = (uint32_t)(rdlen - rdoff - seedhitlen);
 			first = true;
-			riter = 0;
 			while(!rands_[i].done() && (first || is_small || eeMode)) {
-				riter++;
 				if(*minsc == perfectScore) {
 					if(!eeMode || eehits_[i].score < perfectScore) return EXTEND_PERFECT_SCORE;
 				} else if(eeMode && eehits_[i].score < *minsc) {
@@ -1276,23 +1465,7 @@ int SwDriverB::ext_step(Driver& d, Slot& s) {
 				if(s.prm.nExIters >= maxIters) return EXTEND_EXCEEDED_HARD_LIMIT;
 				s.prm.nExIters++;
 				first = false;
-				{
-					// resolve the next element's offset (aligner_sw_driver.cpp:924-952)
-					WalkResult wr;
-					const size_t elt = rands_[i].next(s.rnd);
-					SARangeWithOffs<TSlice> sa;
-					sa.topf = satpos_[i].sat.topf;
-					sa.len = satpos_[i].sat.key.len;
-					sa.offs = satpos_[i].sat.offs;
-					gws_[i].advanceElement((TIndexOffU)elt, ebwtFw, ref, sa, gwstate_, wr, d.wlm, s.prm);
-					eltsDone++;
-					if(!eeMode) neltLeft--;
-					tidx = 0;
-					toff = 0;
-					tlen = 0;
-					bool straddled = false;
-					ebwtFw.joinedToTextOff(wr.elt.len, wr.toff, tidx, toff, tlen, eeMode, straddled);
-				}
+				BT2GB_NEXT_ELEMENT()
 				if(tidx == OFF_MASK) continue;   // the seed hit straddled a reference boundary
 				refoff = (int64_t)toff - rdoff;
 				refcoord.init(tidx, refoff, fw);
@@ -1321,34 +1494,10 @@ int SwDriverB::ext_step(Driver& d, Slot& s) {
 					if(h.mms() > 0) resEe_.alres.ned().push_back(h.e1);
 					state = FOUND_EE_;
 					found = true;
-					Interval refival(refcoord, 1);
-					seenDiags1_.add(refival);
+					seenDiags1_.add(Interval(refcoord, 1));
 				} else if(R_doUngapped && ungapped) {
-					resUngap_.reset();
-					if(d.bsc_ok && rdlen > 0 && rdlen <= BT2G_MAX_READ_LEN) {
-						memset(&s.ug_p, 0, sizeof(s.ug_p));
-						s.ug_p.fw = fw ? 1 : 0;
-						s.ug_p.off = refcoord.off();
-						s.ug_p.refidx = (uint32_t)refcoord.ref();
-						s.ug_p.minsc = (int32_t)*minsc;
-						d.rq[K_UG].push_back(&s);
-						pc = X_AFTER_UG;
-						return EXTEND_BLOCKED;
-					after_ug:
-						resUngap_.alres.reset();
-						ug_ret = s.ug_r.ret;
-						if(s.ug_r.ret == 1)
-							fill_alnres(resUngap_.alres, s.ug_ed.data(), (uint32_t)s.ug_r.nedit, s.ug_r.score, s.ug_r.ns, 0,
-							            (int)(rdlen - (size_t)s.ug_r.nedit), refcoord.ref(), s.ug_r.refoff, (TRefOff)tlen,
-							            fw, rdlen, (size_t)s.ug_r.trim5p, (size_t)s.ug_r.trim3p, (size_t)s.ug_r.refns);
-					} else {
-						d.swcpu.reset();
-						ug_ret = d.swcpu.ungappedAlign(fw ? rd.patFw : rd.patRc, fw ? rd.qual : rd.qualRev, refcoord, ref, tlen,
-						                               sc, gReportOverhangs, *minsc, resUngap_);
-						g_cpu[K_UG]++;
-					}
-					Interval refival(refcoord, 1);
-					seenDiags1_.add(refival);
+					BT2GB_UNGAPPED(after_ug)
+					seenDiags1_.add(Interval(refcoord, 1));
 					s.prm.nExUgs++;
 					if(ug_ret == 0) {
 						s.prm.nExUgFails++;
@@ -1384,50 +1533,30 @@ int SwDriverB::ext_step(Driver& d, Slot& s) {
 						rect.initIval(refival);
 						seenDiags1_.add(refival);
 					}
-					{
-						int unused = 0;
-						if(!need_dp(d, s, unused)) {
-							pc = X_AFTER_DP;
-							return EXTEND_BLOCKED;
-						}
+					if(!need_dp(d, s, mate, fw, tidx, tlen, rect, *minsc, true, true, false, a)) {
+						pc = X_AFTER_DP;
+						return EXTEND_BLOCKED;
 					}
 				after_dp:
-					// SwAligner::align's outcome (aligner_sw.cpp:677-729) at this minsc
-					cpu_dp = dp->cpu;
-					cural = 0;
-					dp_next = 0;
-					dp_next_edit = 0;
-					if(cpu_dp) {
-						dp->minsc = (int32_t)*minsc;
-						d.cpu_dp(s, *dp);
-						found = dp->o.aligned != 0;
-					} else {
-						found = false;
-						if(dp->o.aligned)
-							for(const bt2g_sw_cand& c : dp->cands)
-								if(c.score >= *minsc) {
-									found = true;
-									break;
-								}
+					a.start(a.dp);
+					{
+						TAlScore bestCell = std::numeric_limits<TAlScore>::min();
+						found = dp_found(d, s, a, false, *minsc, bestCell);
+						d.swmSeed.tallyGappedDp(readGaps, refGaps);
+						s.prm.nExDps++;
+						if(!found) {
+							s.prm.nExDpFails++;
+							s.prm.nDpFail++;
+							if(s.prm.nDpFail >= maxDpStreak) return EXTEND_EXCEEDED_SOFT_LIMIT;
+							if(bestCell > std::numeric_limits<TAlScore>::min() && bestCell > s.prm.bestLtMinscMate1)
+								s.prm.bestLtMinscMate1 = bestCell;
+							continue;     // look for more anchor alignments
+						}
 					}
-					d.swmSeed.tallyGappedDp(readGaps, refGaps);
-					s.prm.nExDps++;
-					if(!found) {
-						s.prm.nExDpFails++;
-						s.prm.nDpFail++;
-						if(s.prm.nDpFail >= maxDpStreak) return EXTEND_EXCEEDED_SOFT_LIMIT;
-						const TAlScore bestCell = dp->o.best == std::numeric_limits<int32_t>::min()
-						                              ? std::numeric_limits<TAlScore>::min()
-						                              : (TAlScore)dp->o.best;
-						if(bestCell > std::numeric_limits<TAlScore>::min() && bestCell > s.prm.bestLtMinscMate1)
-							s.prm.bestLtMinscMate1 = bestCell;
-						continue;     // look for more anchor alignments
-					} else {
-						s.prm.nExDpSuccs++;
-						s.prm.nDpLastSucc = s.prm.nExDps - 1;
-						if(s.prm.nDpFail > s.prm.nDpFailStreak) s.prm.nDpFailStreak = s.prm.nDpFail;
-						s.prm.nDpFail = 0;
-					}
+					s.prm.nExDpSuccs++;
+					s.prm.nDpLastSucc = s.prm.nExDps - 1;
+					if(s.prm.nDpFail > s.prm.nDpFailStreak) s.prm.nDpFailStreak = s.prm.nDpFail;
+					s.prm.nDpFail = 0;
 				}
 				// aligner_sw_driver.cpp:1161-1287
 				firstInner = true;
@@ -1441,8 +1570,8 @@ int SwDriverB::ext_step(Driver& d, Slot& s) {
 						res = &resUngap_;
 					} else {
 						resGap_.reset();
-						if(cpu_dp ? d.swcpu.done() : cural == dp->cands.size()) break;
-						replay_next(d, s, resGap_);
+						if(replay_done(d, a, false)) break;
+						replay_next(d, s, a, false, *minsc, resGap_);
 						found = !resGap_.empty();
 						if(!found) break;
 						res = &resGap_;
@@ -1457,34 +1586,420 @@ int SwDriverB::ext_step(Driver& d, Slot& s) {
 					if(redAnchor_.overlap(res->alres)) continue;
 					redAnchor_.add(res->alres);
 					res->alres.setParams(seedmms, seedlen, seedival, *minsc);
-					if(msink->report(0, &res->alres, NULL)) return EXTEND_POLICY_FULFILLED;
-					if(R_tighten > 0 && msink->Mmode() && msink->hasSecondBestUnp1()) {
-						TAlScore& m = *minsc;
-						if(R_tighten == 1) {
-							if(msink->bestUnp1() >= m) {
-								m = msink->bestUnp1();
-								if(m < perfectScore && msink->bestUnp1() == msink->secondBestUnp1()) m++;
-							}
-						} else if(R_tighten == 2) {
-							if(msink->secondBestUnp1() >= m) {
-								m = msink->secondBestUnp1();
-								if(m < perfectScore) m++;
-							}
-						} else {
-							TAlScore diff = msink->bestUnp1() - msink->secondBestUnp1();
-							TAlScore bot = msink->secondBestUnp1() + ((diff * 3) / 4);
-							if(bot >= m) {
-								m = bot;
-								if(m < perfectScore) m++;
-							}
-						}
-					}
+					if(msink->report(0, anchor1 ? &res->alres : NULL, anchor1 ? NULL : &res->alres))
+						return EXTEND_POLICY_FULFILLED;
+					tighten_unp(*this, msink);
 				}
 			}
 		}
 	}
 	return EXTEND_EXHAUSTED_CANDIDATES;
 }
+
+#undef BT2GB_NELT_DEC
+#define BT2GB_NELT_DEC neltLeft--
+
+// SwDriver::extendSeedsPaired (aligner_sw_driver.cpp:1385-2402), with
+// swMateImmediately and reportImmediately true as multiseedSearchWorker calls it.
+int SwDriverB::ext_step_paired(Driver& d, Slot& s) {
+	AlnSinkWrap* msink = &s.msinkwrap;
+	const Read& rd = *s.rds[mate];
+	const Read& ord = *s.rds[mate ^ 1];
+	const Scoring& sc = *d.sc;
+	const Ebwt& ebwtFw = *d.ebwtFw;
+	const BitPairReference& ref = *d.ref;
+	const PairedEndPolicy& pepol = *d.pepol;
+	const bool mixed = gReportMixed, discord = gReportDiscordant;
+	switch(pc) {
+	case X_START: break;
+	case X_AFTER_EE_ROWS: goto after_ee_rows;
+	case X_AFTER_EXT: goto after_ext;
+	case X_AFTER_PRIO_ROWS: goto after_prio_rows;
+	case X_AFTER_UG: goto after_ug;
+	case X_AFTER_DP: goto after_dp;
+	case X_AFTER_MDP: goto after_mdp;
+	default: abort();
+	}
+	// aligner_sw_driver.cpp:1435-1504
+	all = msink->allHits();
+	rdlen = rd.length();
+	ordlen = ord.length();
+	perfectScore = sc.perfectScore(rdlen);
+	operfectScore = sc.perfectScore(ordlen);
+	bestPairScore = perfectScore + operfectScore;
+	{
+		TAlScore ps;
+		if(pair_floor(*this, msink, ps)) {
+			TAlScore nc = ps - operfectScore;
+			if(nc > *minsc) *minsc = nc;
+		}
+	}
+	nonz = s.shs[mate].nonzeroOffsets();
+	eeMode = s.shs[mate].numE2eHits() > 0;
+	firstEe = true;
+	firstExtend = true;
+	s.prm.nEeFail = 0;
+	s.prm.nUgFail = 0;
+	s.prm.nDpFail = 0;
+	nelt = 0;
+	neltLeft = 0;
+	rows = rdlen;
+	orows = ordlen;
+	eltsDone = 0;
+	while(true) {
+		if(eeMode) {
+			if(firstEe) {
+				firstEe = false;
+				BT2GB_EE_SETUP(after_ee_rows)
+				neltLeft = nelt;
+				mateStreaks_.resize(gws_.size());
+				mateStreaks_.fill(0);
+			} else {
+				eeMode = false;
+			}
+		}
+		if(!eeMode) {
+			if(nonz == 0) return EXTEND_EXHAUSTED_CANDIDATES;
+			if(msink->Mmode() && *minsc == perfectScore) return EXTEND_PERFECT_SCORE;
+			if(firstExtend) {
+				nelt = 0;
+				BT2GB_PRIO_SETUP(after_ext, after_prio_rows)
+				neltLeft = nelt;
+				firstExtend = false;
+				mateStreaks_.resize(gws_.size());
+				mateStreaks_.fill(0);
+			}
+			if(neltLeft == 0) break;
+		}
+		for(i = 0; i < gws_.size(); i++) {
+			if(eeMode && eehits_[i].score < *minsc) return EXTEND_PERFECT_SCORE;
+			is_small = satpos_[i].sat.size() < 5;
+			fw = satpos_[i].pos.fw;
+			rdoff = satpos_[i].pos.rdoff;
+			seedhitlen = satpos_[i].pos.seedlen;
+			if(!fw) rdoff = (uint32_t)(rdlen - rdoff - seedhitlen);
+			first = true;
+			while(!rands_[i].done() && (first || is_small || eeMode)) {
+				if(*minsc == perfectScore) {
+					if(!eeMode || eehits_[i].score < perfectScore) return EXTEND_PERFECT_SCORE;
+				} else if(eeMode && eehits_[i].score < *minsc) {
+					break;
+				}
+				if(s.prm.nExDps >= maxDp || s.prm.nMateDps >= maxDp) return EXTEND_EXCEEDED_HARD_LIMIT;
+				if(s.prm.nExUgs >= maxUg || s.prm.nMateUgs >= maxUg) return EXTEND_EXCEEDED_HARD_LIMIT;
+				if(s.prm.nExIters >= maxIters) return EXTEND_EXCEEDED_HARD_LIMIT;
+				if(eeMode && s.prm.nEeFail >= maxEeStreak) return EXTEND_EXCEEDED_SOFT_LIMIT;
+				if(!eeMode && s.prm.nDpFail >= maxDpStreak) return EXTEND_EXCEEDED_SOFT_LIMIT;
+				if(!eeMode && s.prm.nUgFail >= maxUgStreak) return EXTEND_EXCEEDED_SOFT_LIMIT;
+				if(mateStreaks_[i] >= maxMateStreak) {
+					rands_[i].setDone();       // don't try this seed range anymore
+					break;
+				}
+				s.prm.nExIters++;
+				first = false;
+				BT2GB_NEXT_ELEMENT()
+				if(tidx == OFF_MASK) continue;
+				refoff = (int64_t)toff - rdoff;
+				refcoord.init(tidx, refoff, fw);
+				if(seenDiags().locusPresent(refcoord)) {
+					s.prm.nRedundants++;
+					d.swmSeed.rshit++;
+					continue;
+				}
+				readGaps = 0;
+				refGaps = 0;
+				ungapped = false;
+				if(!eeMode) {
+					readGaps = sc.maxReadGaps(*minsc, rdlen);
+					refGaps = sc.maxRefGaps(*minsc, rdlen);
+					ungapped = (readGaps == 0 && refGaps == 0);
+				}
+				state = FOUND_NONE_;
+				found = false;
+				if(eeMode) {
+					resEe_.reset();
+					resEe_.alres.reset();
+					const EEHit& h = eehits_[i];
+					resEe_.alres.setScore(AlnScore(h.score, (int)(rdlen - h.mms()), h.mms(), h.ns(), 0));
+					resEe_.alres.setShape(refcoord.ref(), refcoord.off(), tlen, fw, rdlen, true, 0, 0, true, 0, 0);
+					resEe_.alres.setRefNs(h.refns());
+					if(h.mms() > 0) resEe_.alres.ned().push_back(h.e1);
+					state = FOUND_EE_;
+					found = true;
+					seenDiags().add(Interval(refcoord, 1));
+					s.prm.nExEes++;
+					s.prm.nEeFail++;        // failed until proven successful
+					s.prm.nExEeFails++;
+				} else if(R_doUngapped && ungapped) {
+					BT2GB_UNGAPPED(after_ug)
+					seenDiags().add(Interval(refcoord, 1));
+					s.prm.nExUgs++;
+					s.prm.nUgFail++;        // failed until proven successful
+					s.prm.nExUgFails++;
+					if(ug_ret == 0) {
+						d.swmSeed.ungapfail++;
+						continue;
+					} else if(ug_ret == -1) {
+						d.swmSeed.ungapnodec++;
+					} else {
+						found = true;
+						state = FOUND_UNGAPPED_;
+						d.swmSeed.ungapsucc++;
+					}
+				}
+				if(state == FOUND_NONE_) {
+					DynProgFramer dpframe(!gReportOverhangs);
+					found = dpframe.frameSeedExtensionRect(refoff, rows, tlen, readGaps, refGaps, (size_t)nceil, R_maxhalf,
+					                                       rect);
+					seenDiags().add(Interval(refcoord, 1));
+					if(!found) continue;
+				}
+				if(state == FOUND_NONE_) {
+					{
+						Interval refival(tidx, 0, fw, 0);
+						rect.initIval(refival);
+						seenDiags().add(refival);
+					}
+					if(!need_dp(d, s, mate, fw, tidx, tlen, rect, *minsc, true, true, false, a)) {
+						pc = X_AFTER_DP;
+						return EXTEND_BLOCKED;
+					}
+				after_dp:
+					a.start(a.dp);
+					{
+						TAlScore bestCell = std::numeric_limits<TAlScore>::min();
+						found = dp_found(d, s, a, false, *minsc, bestCell);
+						d.swmSeed.tallyGappedDp(readGaps, refGaps);
+						s.prm.nExDps++;
+						s.prm.nDpFail++;        // failed until proven successful
+						s.prm.nExDpFails++;
+						if(!found) {
+							TAlScore& bl = anchor1 ? s.prm.bestLtMinscMate1 : s.prm.bestLtMinscMate2;
+							if(bestCell > std::numeric_limits<TAlScore>::min() && bestCell > bl) bl = bestCell;
+							continue;           // look for more anchor alignments
+						}
+					}
+				}
+				// aligner_sw_driver.cpp:1851-2353
+				firstInner = true;
+				foundConcordant = false;
+				while(true) {
+					if(state == FOUND_EE_) {
+						if(!firstInner) break;
+						res_kind = FOUND_EE_;
+					} else if(state == FOUND_UNGAPPED_) {
+						if(!firstInner) break;
+						res_kind = FOUND_UNGAPPED_;
+					} else {
+						resGap_.reset();
+						if(replay_done(d, a, false)) break;
+						replay_next(d, s, a, false, *minsc, resGap_);
+						found = !resGap_.empty();
+						if(!found) break;
+						res_kind = FOUND_NONE_;
+					}
+					firstInner = false;
+					{
+						SwResult* res = res_ptr();
+						Interval refival(tidx, 0, fw, tlen);
+						if(gReportOverhangs && !refival.containsIgnoreOrient(res->alres.refival())) {
+							res->alres.clipOutside(true, 0, tlen);
+							if(res->alres.refExtent() == 0) continue;
+						}
+						if(!refival.overlapsIgnoreOrient(res->alres.refival())) continue;
+						if(redAnchor_.overlap(res->alres)) continue;
+						redAnchor_.add(res->alres);
+						res->alres.setParams(seedmms, seedlen, seedival, *minsc);
+						foundMate = false;
+						off = res->alres.refoff();
+					}
+					if(msink->state().doneWithMate(!anchor1) && !msink->state().doneWithMate(anchor1))
+						swMateImmediately = false;   // done with the opposite mate, not with the anchor
+					if(found && swMateImmediately) {
+						oleft = false;
+						ofw = false;
+						oll = olr = orl = orr = 0;
+						foundMate = !oppFilt;
+						ominsc_cur = *ominsc;
+						oreadGaps = 0;
+						orefGaps = 0;
+						if(foundMate) {
+							ominsc_cur = *ominsc;
+							TAlScore ps;
+							if(pair_floor(*this, msink, ps)) {
+								TAlScore nc = ps - res_ptr()->alres.score().score();
+								if(nc > ominsc_cur) ominsc_cur = nc;
+							}
+							oreadGaps = sc.maxReadGaps(ominsc_cur, ordlen);
+							orefGaps = sc.maxRefGaps(ominsc_cur, ordlen);
+							foundMate = pepol.otherMate(anchor1, fw, off, orows + oreadGaps, tlen,
+							                            anchor1 ? rd.length() : ord.length(),
+							                            anchor1 ? ord.length() : rd.length(), oleft, oll, olr, orl, orr, ofw);
+						}
+						if(foundMate) {
+							DynProgFramer dpframe(!gReportOverhangs);
+							foundMate = dpframe.frameFindMateRect(!oleft, oll, olr, orl, orr, orows, tlen, oreadGaps,
+							                                      orefGaps, (size_t)onceil, R_maxhalf, orect);
+						}
+						if(foundMate) {
+							oresGap_.reset();
+							if(!need_dp(d, s, mate ^ 1, ofw, tidx, tlen, orect, ominsc_cur, false, false, a.cpu && res_kind == FOUND_NONE_, o)) {
+								pc = X_AFTER_MDP;
+								return EXTEND_BLOCKED;
+							}
+						after_mdp:
+							o.start(o.dp);
+							{
+								TAlScore bestCell = std::numeric_limits<TAlScore>::min();
+								foundMate = dp_found(d, s, o, true, ominsc_cur, bestCell);
+								s.prm.nMateDps++;
+								d.swmMate.tallyGappedDp(oreadGaps, orefGaps);
+								if(!foundMate) {
+									TAlScore& bl = anchor1 ? s.prm.bestLtMinscMate2 : s.prm.bestLtMinscMate1;
+									if(bestCell > std::numeric_limits<TAlScore>::min() && bestCell > bl) bl = bestCell;
+								}
+							}
+						}
+						didAnchor = false;
+						do {
+							oresGap_.reset();
+							if(foundMate && replay_done(d, o, true)) {
+								foundMate = false;
+							} else if(foundMate) {
+								replay_next(d, s, o, true, ominsc_cur, oresGap_);
+								foundMate = !oresGap_.empty();
+							}
+							SwResult* res = res_ptr();
+							Interval refival(tidx, 0, fw, tlen);
+							if(foundMate) {
+								if(!redAnchor_.overlap(oresGap_.alres)) redAnchor_.add(oresGap_.alres);
+								oresGap_.alres.setParams(seedmms, seedlen, seedival, *ominsc);
+								if(gReportOverhangs && !refival.containsIgnoreOrient(oresGap_.alres.refival())) {
+									oresGap_.alres.clipOutside(true, 0, tlen);
+									foundMate = oresGap_.alres.refExtent() > 0;
+								}
+								if(foundMate && ((!gReportOverhangs && !refival.containsIgnoreOrient(oresGap_.alres.refival())) ||
+								                 !refival.overlapsIgnoreOrient(oresGap_.alres.refival())))
+									foundMate = false;
+							}
+							int pairCl = PE_ALS_DISCORD;
+							if(foundMate) {
+								const TRefOff off1 = anchor1 ? off : oresGap_.alres.refoff();
+								const TRefOff off2 = anchor1 ? oresGap_.alres.refoff() : off;
+								const size_t len1 = anchor1 ? res->alres.refExtent() : oresGap_.alres.refExtent();
+								const size_t len2 = anchor1 ? oresGap_.alres.refExtent() : res->alres.refExtent();
+								const bool fw1 = anchor1 ? res->alres.fw() : oresGap_.alres.fw();
+								const bool fw2 = anchor1 ? oresGap_.alres.fw() : res->alres.fw();
+								pairCl = pepol.peClassifyPair(off1, len1, fw1, off2, len2, fw2);
+							}
+							if(msink->state().doneConcordant()) foundMate = false;
+							if(foundMate) {
+								bool doneUnpaired = false;
+								if(!anchor1 || !didAnchor) {
+									if(anchor1) didAnchor = true;
+									const AlnRes& r1 = anchor1 ? res->alres : oresGap_.alres;
+									if(!redMate1_.overlap(r1)) {
+										redMate1_.add(r1);
+										if(msink->report(0, &r1, NULL)) doneUnpaired = true;
+									}
+								}
+								if(anchor1 || !didAnchor) {
+									if(!anchor1) didAnchor = true;
+									const AlnRes& r2 = anchor1 ? oresGap_.alres : res->alres;
+									if(!redMate2_.overlap(r2)) {
+										redMate2_.add(r2);
+										if(msink->report(0, NULL, &r2)) doneUnpaired = true;
+									}
+								}
+								bool donePaired = false;
+								if(pairCl != PE_ALS_DISCORD) {
+									foundConcordant = true;
+									if(msink->report(0, anchor1 ? &res->alres : &oresGap_.alres,
+									                 anchor1 ? &oresGap_.alres : &res->alres)) {
+										donePaired = true;
+									} else {
+										TAlScore ps;
+										if(pair_floor(*this, msink, ps)) {
+											TAlScore nc = ps - operfectScore;
+											if(nc > *minsc) {
+												*minsc = nc;
+												if(*minsc > res->alres.score().score()) break;   // done with this anchor
+											}
+										}
+									}
+								}
+								if(donePaired || doneUnpaired) return EXTEND_POLICY_FULFILLED;
+								if(msink->state().doneWithMate(anchor1)) return EXTEND_POLICY_FULFILLED;
+							} else if((mixed || discord) && !didAnchor) {
+								didAnchor = true;
+								if(!msink->state().doneUnpaired(anchor1)) {
+									const AlnRes& r = res->alres;
+									RedundantAlns& red = anchor1 ? redMate1_ : redMate2_;
+									const AlnRes* r1 = anchor1 ? &res->alres : NULL;
+									const AlnRes* r2 = anchor1 ? NULL : &res->alres;
+									if(!red.overlap(r)) {
+										red.add(r);
+										if(msink->report(0, r1, r2)) return EXTEND_POLICY_FULFILLED;
+									}
+								}
+								if(msink->state().doneWithMate(anchor1)) return EXTEND_POLICY_FULFILLED;
+							}
+						} while(!oresGap_.empty());
+					} else if(found) {
+						// an anchor alignment, no opposite-mate search (probably done with it)
+						if(mixed || discord) {
+							SwResult* res = res_ptr();
+							if(!msink->state().doneUnpaired(anchor1)) {
+								const AlnRes& r = res->alres;
+								RedundantAlns& red = anchor1 ? redMate1_ : redMate2_;
+								const AlnRes* r1 = anchor1 ? &res->alres : NULL;
+								const AlnRes* r2 = anchor1 ? NULL : &res->alres;
+								if(!red.overlap(r)) {
+									red.add(r);
+									if(msink->report(0, r1, r2)) return EXTEND_POLICY_FULFILLED;
+								}
+							}
+							if(msink->state().doneWithMate(anchor1)) return EXTEND_POLICY_FULFILLED;
+						}
+					}
+				}
+				if(foundConcordant) {
+					s.prm.nMateDpSuccs++;
+					mateStreaks_[i] = 0;
+					if(state == FOUND_UNGAPPED_) {
+						s.prm.nExUgFails--;
+						s.prm.nExUgSuccs++;
+						s.prm.nUgLastSucc = s.prm.nExUgs - 1;
+						if(s.prm.nUgFail > s.prm.nUgFailStreak) s.prm.nUgFailStreak = s.prm.nUgFail;
+						s.prm.nUgFail = 0;
+					} else if(state == FOUND_EE_) {
+						s.prm.nExEeFails--;
+						s.prm.nExEeSuccs++;
+						s.prm.nEeLastSucc = s.prm.nExEes - 1;
+						if(s.prm.nEeFail > s.prm.nEeFailStreak) s.prm.nEeFailStreak = s.prm.nEeFail;
+						s.prm.nEeFail = 0;
+					} else {
+						s.prm.nExDpFails--;
+						s.prm.nExDpSuccs++;
+						s.prm.nDpLastSucc = s.prm.nExDps - 1;
+						if(s.prm.nDpFail > s.prm.nDpFailStreak) s.prm.nDpFailStreak = s.prm.nDpFail;
+						s.prm.nDpFail = 0;
+					}
+				} else {
+					s.prm.nMateDpFails++;
+					mateStreaks_[i]++;
+				}
+			}
+		}
+	}
+	return EXTEND_EXHAUSTED_CANDIDATES;
+}
+
+#undef BT2GB_NELT_DEC
+#undef BT2GB_EE_SETUP
+#undef BT2GB_PRIO_SETUP
+#undef BT2GB_NEXT_ELEMENT
+#undef BT2GB_UNGAPPED
 
 }  // namespace
 
@@ -1493,31 +2008,11 @@ extern "C" {
 void bt2g_real__ZN8SwDriver6extendERK4ReadRK4EbwtPS4_jjjjbmmR14PerReadMetricsRmS9_(
 	SwDriver*, const Read&, const Ebwt&, const Ebwt*, TIndexOffU, TIndexOffU, TIndexOffU, TIndexOffU, bool, size_t,
 	size_t, PerReadMetrics&, size_t&, size_t&);
-void bt2g_real__ZN8SwDriver16prioritizeSATupsERK4ReadR11SeedResultsRK4EbwtPS6_RK16BitPairReferenceimbbbmR19AlignmentCacheIfaceR12RandomSourceR11WalkMetricsR14PerReadMetricsRmb(
-	SwDriver*, const Read&, SeedResults&, const Ebwt&, const Ebwt*, const BitPairReference&, int, size_t, bool, bool, bool,
-	size_t, AlignmentCacheIface&, RandomSource&, WalkMetrics&, PerReadMetrics&, size_t&, bool);
-bool bt2g_real__ZN8SwDriver8eeSaTupsERK4ReadR11SeedResultsRK4EbwtRK16BitPairReferenceR12RandomSourceR11WalkMetricsR9SwMetricsRmmb(
-	SwDriver*, const Read&, SeedResults&, const Ebwt&, const BitPairReference&, RandomSource&, WalkMetrics&, SwMetrics&,
-	size_t&, size_t, bool);
-}
-
-void SwDriver::prioritizeSATups(const Read& read, SeedResults& sh, const Ebwt& ebwtFw, const Ebwt* ebwtBw,
-                                const BitPairReference& ref, int seedmms, size_t maxelt, bool doExtend, bool lensq,
-                                bool szsq, size_t nsm, AlignmentCacheIface& ca, RandomSource& rnd, WalkMetrics& wlm,
-                                PerReadMetrics& prm, size_t& nelt_out, bool all) {
-	bt2g_real__ZN8SwDriver16prioritizeSATupsERK4ReadR11SeedResultsRK4EbwtPS6_RK16BitPairReferenceimbbbmR19AlignmentCacheIfaceR12RandomSourceR11WalkMetricsR14PerReadMetricsRmb(
-		this, read, sh, ebwtFw, ebwtBw, ref, seedmms, maxelt, doExtend, lensq, szsq, nsm, ca, rnd, wlm, prm, nelt_out, all);
-}
-
-bool SwDriver::eeSaTups(const Read& rd, SeedResults& sh, const Ebwt& ebwt, const BitPairReference& ref,
-                        RandomSource& rnd, WalkMetrics& wlm, SwMetrics& swmSeed, size_t& nelt_out, size_t maxelt,
-                        bool all) {
-	return bt2g_real__ZN8SwDriver8eeSaTupsERK4ReadR11SeedResultsRK4EbwtRK16BitPairReferenceR12RandomSourceR11WalkMetricsR9SwMetricsRmmb(
-		this, rd, sh, ebwt, ref, rnd, wlm, swmSeed, nelt_out, maxelt, all);
 }
 
 // SwDriver::extend (aligner_sw_driver.cpp:299-483) from the engine's results for
-// this read (asked in the same order prioritizeSATups calls it), else the CPU.
+// this read (asked in the order prioritizeSATups calls it), else the CPU.
+// (prioritizeSATups and eeSaTups are the reference's own definitions.)
 void SwDriver::extend(const Read& rd, const Ebwt& ebwtFw, const Ebwt* ebwtBw, TIndexOffU topf, TIndexOffU botf,
                       TIndexOffU topb, TIndexOffU botb, bool fw, size_t off, size_t len, PerReadMetrics& prm,
                       size_t& nlex, size_t& nrex) {
@@ -1572,21 +2067,21 @@ bool GroupWalk2S<TSlice, 16>::advanceElement(TIndexOffU elt, const Ebwt& ebwtFw,
 
 namespace {
 
-// ---- multiseedSearchWorker's per-read body (bt2_search.cpp:3266-4160), unpaired
-bool Driver::seeds_valid(const Slot& s, bool fw, size_t i) const {
-	if(i < 64) return ((fw ? s.valid_fw : s.valid_rc) >> i) & 1;
+// ---- multiseedSearchWorker's per-read body (bt2_search.cpp:3266-4160) ----------
+bool Driver::seeds_valid(const MateRes& m, bool fw, size_t i) const {
+	if(i < 64) return ((fw ? m.valid_fw : m.valid_rc) >> i) & 1;
 	const size_t k = (i - 64) * 2 + (fw ? 0 : 1);
-	return k / 64 < s.valid_big.size() && ((s.valid_big[k / 64] >> (k % 64)) & 1);
+	return k / 64 < m.valid_big.size() && ((m.valid_big[k / 64] >> (k % 64)) & 1);
 }
 
-void Driver::set_valid(Slot& s, bool fw, size_t i) {
+void Driver::set_valid(MateRes& m, bool fw, size_t i) {
 	if(i < 64) {
-		(fw ? s.valid_fw : s.valid_rc) |= 1ull << i;
+		(fw ? m.valid_fw : m.valid_rc) |= 1ull << i;
 		return;
 	}
 	const size_t k = (i - 64) * 2 + (fw ? 0 : 1);
-	if(s.valid_big.size() <= k / 64) s.valid_big.resize(k / 64 + 1, 0);
-	s.valid_big[k / 64] |= 1ull << (k % 64);
+	if(m.valid_big.size() <= k / 64) m.valid_big.resize(k / 64 + 1, 0);
+	m.valid_big[k / 64] |= 1ull << (k % 64);
 }
 
 // Per-read setup (bt2_search.cpp:3266-3451).
@@ -1595,115 +2090,151 @@ void Driver::setup_read(Slot& s) {
 	s.prm.doFmString = false;
 	if(R_sam_print_xt) gettimeofday(&s.prm.tv_beg, &s.prm.tz_beg);
 	s.ca.nextRead();
-	const Read& rd = *s.rd;
-	s.rdlen = rd.length();
-	s.msinkwrap.nextRead(s.msink, s.rd, NULL, s.rdid, sc->qualitiesMatter());
-	TAlScore minsc = std::numeric_limits<TAlScore>::max();
+	const bool paired = s.paired;
+	const Read& ra = *s.rds[0];
+	const Read& rb = *s.rds[1];
+	s.rdlens[0] = ra.length();
+	s.rdlens[1] = paired ? rb.length() : 0;
+	s.msinkwrap.nextRead(s.msink, &ra, paired ? &rb : NULL, s.rdid, sc->qualitiesMatter());
+	s.minsc[0] = s.minsc[1] = std::numeric_limits<TAlScore>::max();
 	if(R_bwaSwLike) {
 		float a = (float)sc->match(30);
 		float T = R_bwaSwLikeT, c = R_bwaSwLikeC;
-		minsc = (TAlScore)max<float>(a * T, a * c * log(s.rdlen));
+		s.minsc[0] = (TAlScore)max<float>(a * T, a * c * log(s.rdlens[0]));
+		if(paired) s.minsc[1] = (TAlScore)max<float>(a * T, a * c * log(s.rdlens[1]));
 	} else {
-		minsc = R_scoreMin.f<TAlScore>(s.rdlen);
+		s.minsc[0] = R_scoreMin.f<TAlScore>(s.rdlens[0]);
+		if(paired) s.minsc[1] = R_scoreMin.f<TAlScore>(s.rdlens[1]);
 		if(R_localAlign) {
-			if(minsc < 0) minsc = 0;
+			if(s.minsc[0] < 0) s.minsc[0] = 0;
+			if(paired && s.minsc[1] < 0) s.minsc[1] = 0;
 		} else {
-			if(minsc > 0) minsc = 0;
+			if(s.minsc[0] > 0) s.minsc[0] = 0;
+			if(paired && s.minsc[1] > 0) s.minsc[1] = 0;
 		}
 	}
-	s.minsc = minsc;
 	size_t readns[2] = {0, 0};
-	sc->nFilterPair(&rd.patFw, NULL, readns[0], readns[1], s.nfilt[0], s.nfilt[1]);
-	s.scfilt[0] = sc->scoreFilter(minsc, s.rdlen);
-	s.scfilt[1] = sc->scoreFilter(std::numeric_limits<TAlScore>::max(), 0);
+	sc->nFilterPair(&ra.patFw, paired ? &rb.patFw : NULL, readns[0], readns[1], s.nfilt[0], s.nfilt[1]);
+	s.scfilt[0] = sc->scoreFilter(s.minsc[0], s.rdlens[0]);
+	s.scfilt[1] = sc->scoreFilter(s.minsc[1], s.rdlens[1]);
 	s.lenfilt[0] = s.lenfilt[1] = true;
-	if(s.rdlen <= (size_t)R_multiseedMms || s.rdlen < 2) s.lenfilt[0] = false;
-	if(s.rdlen < 2) s.lenfilt[0] = false;
+	if(s.rdlens[0] <= (size_t)R_multiseedMms || s.rdlens[0] < 2) s.lenfilt[0] = false;
+	if((s.rdlens[1] <= (size_t)R_multiseedMms || s.rdlens[1] < 2) && paired) s.lenfilt[1] = false;
+	if(s.rdlens[0] < 2) s.lenfilt[0] = false;
+	if(s.rdlens[1] < 2 && paired) s.lenfilt[1] = false;
 	s.qcfilt[0] = s.qcfilt[1] = true;
 	if(R_qcFilter) {
-		s.qcfilt[0] = (rd.filter != '0');
-		s.qcfilt[1] = (s.rdb->filter != '0');
+		s.qcfilt[0] = (ra.filter != '0');
+		s.qcfilt[1] = (rb.filter != '0');
 	}
-	s.filt = s.nfilt[0] && s.scfilt[0] && s.lenfilt[0] && s.qcfilt[0];
-	s.prm.nFilt += (s.filt ? 0 : 1) + ((s.nfilt[1] && s.scfilt[1] && s.lenfilt[1] && s.qcfilt[1]) ? 0 : 1);
-	s.sd.nextRead(false, s.rdlen, 0);
-	s.minedfw = s.minedrc = 0;
-	s.nofw = gNofw;
-	s.norc = gNorc;
-	s.nceil = std::min(R_nCeil.f<int>((double)s.rdlen), (int)s.rdlen);
+	for(int m = 0; m < 2; m++) s.filt[m] = s.nfilt[m] && s.scfilt[m] && s.lenfilt[m] && s.qcfilt[m];
+	s.prm.nFilt += (s.filt[0] ? 0 : 1) + (s.filt[1] ? 0 : 1);
+	s.sd.nextRead(paired, s.rdlens[0], s.rdlens[1]);
+	s.minedfw[0] = s.minedfw[1] = s.minedrc[0] = s.minedrc[1] = 0;
+	s.nofw[0] = paired ? (gMate1fw ? gNofw : gNorc) : gNofw;
+	s.norc[0] = paired ? (gMate1fw ? gNorc : gNofw) : gNorc;
+	s.nofw[1] = paired ? (gMate2fw ? gNofw : gNorc) : gNofw;
+	s.norc[1] = paired ? (gMate2fw ? gNorc : gNofw) : gNorc;
+	s.nceil[0] = std::min(R_nCeil.f<int>((double)s.rdlens[0]), (int)s.rdlens[0]);
+	s.nceil[1] = paired ? std::min(R_nCeil.f<int>((double)s.rdlens[1]), (int)s.rdlens[1]) : 0;
 	s.exhaustive[0] = s.exhaustive[1] = false;
-	s.rnd.init(rd.seed);      // (pairPostFilt is false for an unpaired read)
-	s.interval = std::max(R_msIval.f<int>((double)s.rdlen), 1);
-	s.streak = R_maxDpStreak;
-	s.mxDp = R_maxDp;
-	s.mxUg = R_maxUg;
-	s.mxIter = R_maxIters;
-	if(R_allHits) {
-		s.streak = s.mxDp = s.mxUg = s.mxIter = std::numeric_limits<size_t>::max();
-	} else if(R_khits > 1) {
-		s.streak += (R_khits - 1) * R_maxStreakIncr;
-		s.mxDp += (R_khits - 1) * R_maxItersIncr;
-		s.mxUg += (R_khits - 1) * R_maxItersIncr;
-		s.mxIter += (R_khits - 1) * R_maxItersIncr;
+	s.matemap[0] = 0;
+	s.matemap[1] = 1;
+	const bool pairPostFilt = s.filt[0] && s.filt[1];
+	if(pairPostFilt) s.rnd.init(ra.seed ^ rb.seed);
+	else s.rnd.init(ra.seed);
+	s.interval[0] = s.interval[1] = 0;
+	for(int m = 0; m < (paired ? 2 : 1); m++) {
+		s.interval[m] = R_msIval.f<int>((double)s.rdlens[m]);
+		if(s.filt[0] && s.filt[1]) s.interval[m] = (int)(s.interval[m] * 1.2 + 0.5);   // boost for pairs
+		s.interval[m] = std::max(s.interval[m], 1);
 	}
-	s.prm.maxDPFails = s.streak;
-	s.nrounds = R_nSeedRounds;
-	if(s.filt) {
-		s.shs[0].clear();
-		s.shs[0].nextRead(rd);
+	for(int m = 0; m < 2; m++) {
+		s.streak[m] = R_maxDpStreak;
+		s.mtStreak[m] = R_maxMateStreak;
+		s.mxDp[m] = R_maxDp;
+		s.mxUg[m] = R_maxUg;
+		s.mxIter[m] = R_maxIters;
+		if(R_allHits) {
+			s.streak[m] = s.mtStreak[m] = s.mxDp[m] = s.mxUg[m] = s.mxIter[m] = std::numeric_limits<size_t>::max();
+		} else if(R_khits > 1) {
+			s.streak[m] += (R_khits - 1) * R_maxStreakIncr;
+			s.mtStreak[m] += (R_khits - 1) * R_maxStreakIncr;
+			s.mxDp[m] += (R_khits - 1) * R_maxItersIncr;
+			s.mxUg[m] += (R_khits - 1) * R_maxItersIncr;
+			s.mxIter[m] += (R_khits - 1) * R_maxItersIncr;
+		}
 	}
-	s.done = !s.filt;
-	s.nelt = 0;
-	s.sd_ready = false;
-	s.mm_asked = false;
-	s.seedlen = R_multiseedLen;
+	if(s.filt[0] && s.filt[1]) {
+		s.streak[0] = (size_t)ceil((double)s.streak[0] / 2.0);
+		s.streak[1] = (size_t)ceil((double)s.streak[1] / 2.0);
+	}
+	s.prm.maxDPFails = s.streak[0];
+	s.nrounds[0] = s.nrounds[1] = R_nSeedRounds;
+	if(s.filt[0] && s.filt[1]) {
+		s.nrounds[0] = (size_t)ceil((double)s.nrounds[0] / 2.0);
+		s.nrounds[1] = (size_t)ceil((double)s.nrounds[1] / 2.0);
+	}
+	for(int m = 0; m < (paired ? 2 : 1); m++) {
+		if(s.filt[m]) {
+			s.shs[m].clear();
+			s.shs[m].nextRead(*s.rds[m]);
+		}
+	}
+	s.done[0] = !s.filt[0];
+	s.done[1] = !s.filt[1];
+	s.nelt[0] = s.nelt[1] = 0;
+	for(int m = 0; m < 2; m++) {
+		MateRes& x = s.mr[m];
+		x.sd_ready = false;
+		x.sweep_asked = false;
+		x.mm_asked = false;
+	}
 	s.seedsTried = 0;
 	for(int k = 0; k < 4; k++) s.seedsTriedMS[k] = s.nUniqueSeedsMS[k] = s.nRepeatSeedsMS[k] = s.seedHitTotMS[k] = 0;
 	s.nUniqueSeeds = s.nRepeatSeeds = s.seedHitTot = 0;
 	s.ndps = 0;
 }
 
-// (the engine takes the read?)
-bool engine_read(const Slot& s) { return s.rdlen > 0 && s.rdlen <= BT2G_MAX_READ_LEN; }
-
 // instantiateSeeds (aligner_seed.cpp:498-587) for exact seeds: offsets,
 // sequences and qualities into SeedResults; which seeds instantiate (an N
 // disqualifies an exact seed: Constraint::canN, aligner_seed.h:88-92).
 // Returns the number instantiated.
-int instantiate(Driver& d, Slot& s) {
-	const Read& rd = *s.rd;
-	const int len = s.seeds[0].len;
+int Driver::instantiate(Slot& s, int mate, size_t offset) {
+	const Read& rd = *s.rds[mate];
+	MateRes& x = s.mr[mate];
+	const int len = s.seeds[mate][0].len;
+	const int per = s.interval[mate];
 	int nseeds = 1;
-	if((int)rd.length() - (int)s.offset > len) nseeds += ((int)rd.length() - (int)s.offset - len) / s.interval;
+	if((int)rd.length() - (int)offset > len) nseeds += ((int)rd.length() - (int)offset - len) / per;
 	s.offIdx2off.clear();
-	for(int i = 0; i < nseeds; i++) s.offIdx2off.push_back(s.interval * i + (int)s.offset);
-	SeedResults& sr = s.shs[0];
+	for(int i = 0; i < nseeds; i++) s.offIdx2off.push_back(per * i + (int)offset);
+	SeedResults& sr = s.shs[mate];
 	sr.reset(rd, s.offIdx2off, nseeds);
-	s.valid_fw = s.valid_rc = 0;
-	s.valid_big.clear();
-	int ninst = 0;
-	int inst_fw = 0, inst_rc = 0;
+	x.valid_fw = x.valid_rc = 0;
+	x.valid_big.clear();
+	int ninst = 0, inst_fw = 0, inst_rc = 0;
 	for(int fwi = 0; fwi < 2; fwi++) {
 		const bool fw = fwi == 0;
-		if((fw && s.nofw) || (!fw && s.norc)) continue;
+		if((fw && s.nofw[mate]) || (!fw && s.norc[mate])) continue;
 		for(int i = 0; i < nseeds; i++) {
-			const int depth = i * s.interval + (int)s.offset;
+			const int depth = i * per + (int)offset;
 			const int sl = std::min<int>(len, (int)rd.length());
-			d.al.instantiateSeq(rd, sr.seqs(fw)[i], sr.quals(fw)[i], sl, depth, fw);
+			al.instantiateSeq(rd, sr.seqs(fw)[i], sr.quals(fw)[i], sl, depth, fw);
 			bool ok = true;
 			const BTDnaString& q = sr.seqs(fw)[i];
 			for(int k = 0; k < sl && ok; k++) ok = (int)q[k] < 4;
 			if(ok) {
-				d.set_valid(s, fw, (size_t)i);
+				set_valid(x, fw, (size_t)i);
 				ninst++;
 				(fw ? inst_fw : inst_rc)++;
 			} else {
-				d.sdm.filteredseed++;
+				sdm.filteredseed++;
 			}
 		}
 	}
-	s.seedsTriedMS[0] = (size_t)inst_fw;
-	s.seedsTriedMS[1] = (size_t)inst_rc;
+	s.seedsTriedMS[mate * 2 + 0] = (size_t)inst_fw;
+	s.seedsTriedMS[mate * 2 + 1] = (size_t)inst_rc;
 	return ninst;
 }
 
@@ -1711,23 +2242,24 @@ int instantiate(Driver& d, Slot& s) {
 // the engine's seed ranges: strand fw then rc, offsets ascending;
 // SeedSearchCache::addOnTheFly for a hit (reportHit, aligner_seed.cpp:1576-1630),
 // beginAlign / addAllCached / finishAlign, SeedResults::add.
-int Driver::after_seeds(Slot& s) {
-	SeedResults& sr = s.shs[0];
+void Driver::after_seeds(Slot& s, int mate) {
+	SeedResults& sr = s.shs[mate];
+	MateRes& x = s.mr[mate];
 	const size_t nof = sr.numOffs();
-	if((size_t)s.sd_ns != nof) {
-		fprintf(stderr, "bt2g batch: seed offsets differ (engine %d, reference %zu)\n", s.sd_ns, nof);
+	if((size_t)x.sd_ns != nof) {
+		fprintf(stderr, "bt2g batch: seed offsets differ (engine %d, reference %zu)\n", x.sd_ns, nof);
 		abort();
 	}
 	uint64_t possearches = 0, seedsearches = 0, ooms = 0;
 	for(int fwi = 0; fwi < 2; fwi++) {
 		const bool fw = fwi == 0;
 		for(size_t i = 0; i < nof; i++) {
-			if(!seeds_valid(s, fw, i)) continue;
+			if(!seeds_valid(x, fw, i)) continue;
 			possearches++;
 			seedsearches++;
 			const BTDnaString& seq = sr.seqs(fw)[i];
 			SeedSearchCache srcache(seq, sr.quals(fw)[i]);
-			const uint32_t* q = &s.sd_out[((size_t)fwi * nof + i) * 4];
+			const uint32_t* q = &x.sd_out[((size_t)fwi * nof + i) * 4];
 			if(q[1] > q[0]) srcache.addOnTheFly(seq, q[0], q[1], q[2], q[3]);
 			if(srcache.beginAlign(s.ca) == -1) {
 				ooms++;
@@ -1749,271 +2281,387 @@ int Driver::after_seeds(Slot& s) {
 	s.prm.nSeedEltsRc = sr.numEltsRc();
 	s.prm.seedMedian = (uint64_t)(sr.medianHitsPerSeed() + 0.5);
 	s.prm.seedMean = (uint64_t)sr.averageHitsPerSeed();
-	s.prm.nSdFmops += s.sd_ops;
+	s.prm.nSdFmops += x.sd_ops;
 	sdm.seedsearch += seedsearches;
 	sdm.nrange += sr.numRanges();
 	sdm.nelt += sr.numElts();
 	sdm.possearch += possearches;
 	sdm.ooms += ooms;
-	sdm.bwops += s.sd_ops;
-	return 0;
+	sdm.bwops += x.sd_ops;
+	x.sd_ready = false;
 }
 
-// Start one extendSeeds call (bt2_search.cpp:3559-3593 and its two twins).
-void start_ext(Slot& s, int seedmms, int seedlen, int seedival) {
+// A round's seed search, asked ahead: (round 0) with the exact sweep, its
+// arguments being functions of the read and the server's options; (later
+// rounds, pairs) both mates' searches in the round's one wait.  The round
+// takes a result only when its own arguments are the same.
+void Driver::prefetch_seeds(Slot& s, int mate) {
+	if(R_seedSumm || R_nSeedRounds == 0 || R_multiseedMms != 0 || ebwtBw == NULL || !engine_read(s, mate)) return;
+	MateRes& x = s.mr[mate];
+	const int L = R_multiseedLen;
+	const size_t off = s.round_off[mate];
+	int nseeds = 1;
+	if((int)s.rdlens[mate] - (int)off > L) nseeds += ((int)s.rdlens[mate] - (int)off - L) / s.interval[mate];
+	if(x.sd_ready && x.sd_L == (uint32_t)L && x.sd_per == (uint32_t)s.interval[mate] && x.sd_off == (uint32_t)off &&
+	   x.sd_nof == (uint32_t)nseeds)
+		return;
+	x.sd_L = (uint32_t)L;
+	x.sd_per = (uint32_t)s.interval[mate];
+	x.sd_off = (uint32_t)off;
+	x.sd_nof = (uint32_t)nseeds;
+	x.sd_ready = false;
+	rq[K_SEEDS].push_back(Rq{&s, mate});
+}
+
+// Start one extendSeeds / extendSeedsPaired call for anchor `mate`
+// (bt2_search.cpp:3505-3593, 3687-3775, 3963-4051).
+void start_ext(Slot& s, int mate, int seedmms, int seedlen, int seedival) {
 	SwDriverB& x = s.sd;
 	x.pc = X_START;
+	x.mate = mate;
+	x.paired = s.paired;
+	x.anchor1 = mate == 0;
+	x.oppFilt = !s.filt[mate ^ 1];
 	x.seedmms = seedmms;
 	x.seedlen = seedlen;
 	x.seedival = seedival;
-	x.minsc = &s.minsc;
-	x.nceil = s.nceil;
-	x.maxIters = s.mxIter;
-	x.maxUg = s.mxUg;
-	x.maxDp = s.mxDp;
-	x.maxUgStreak = s.streak;
-	x.maxDpStreak = s.streak;
-	x.exhaustive = &s.exhaustive[0];
+	x.minsc = &s.minsc[mate];
+	x.ominsc = &s.minsc[mate ^ 1];
+	x.nceil = s.nceil[mate];
+	x.onceil = s.nceil[mate ^ 1];
+	x.nofw = s.nofw[mate];
+	x.norc = s.norc[mate];
+	x.maxIters = s.mxIter[mate];
+	x.maxUg = s.mxUg[mate];
+	x.maxDp = s.mxDp[mate];
+	x.maxEeStreak = s.streak[mate];
+	x.maxUgStreak = s.streak[mate];
+	x.maxDpStreak = s.streak[mate];
+	x.maxMateStreak = s.mtStreak[mate];
+	x.swMateImmediately = true;
+	x.exhaustive = &s.exhaustive[mate];
 }
 
 // extendSeeds' return code as the worker handles it (bt2_search.cpp:3601-3629).
-void after_ext(Driver& d, Slot& s, int ret, bool perfect_check) {
+void after_ext(Driver& d, Slot& s, int mate, int ret, bool perfect_check) {
 	if(ret == EXTEND_EXHAUSTED_CANDIDATES) {
 	} else if(ret == EXTEND_POLICY_FULFILLED) {
-		if(s.msinkwrap.state().doneWithMate(true)) s.done = true;
+		if(s.msinkwrap.state().doneWithMate(mate == 0)) s.done[mate] = true;
+		if(s.msinkwrap.state().doneWithMate(mate == 1)) s.done[mate ^ 1] = true;
 	} else if(ret == EXTEND_PERFECT_SCORE) {
-		s.done = true;
+		s.done[mate] = true;
 	} else if(ret == EXTEND_EXCEEDED_HARD_LIMIT) {
-		s.done = true;
+		s.done[mate] = true;
 	} else if(ret == EXTEND_EXCEEDED_SOFT_LIMIT) {
 	} else {
 		fprintf(stderr, "Bad return value: %d\n", ret);
 		throw 1;
 	}
-	if(perfect_check && !s.done) {
-		const TAlScore perfectScore = d.sc->perfectScore(s.rdlen);
-		if(s.minsc == perfectScore) s.done = true;
+	if(perfect_check && !s.done[mate]) {
+		const TAlScore perfectScore = d.sc->perfectScore(s.rdlens[mate]);
+		if(s.minsc[mate] == perfectScore) s.done[mate] = true;
 	}
 }
 
 void Driver::step_read(Slot& s) {
-	const Read& rd = *s.rd;
+	const bool paired = s.paired;
+	const size_t nmates = paired ? 2 : 1;
+	const size_t eePeEeltLimit = std::numeric_limits<size_t>::max();
 	int ret = 0;
+	size_t mate = 0;
 	switch(s.pc) {
 	case P_START: break;
 	case P_AFTER_EXACT: goto after_exact;
-	case P_AFTER_EXT_EXACT: goto after_ext_exact;
+	case P_EXT_EXACT: mate = s.matemap[s.matei]; goto ext_exact;
 	case P_AFTER_1MM: goto after_1mm;
-	case P_AFTER_EXT_1MM: goto after_ext_1mm;
+	case P_EXT_1MM: mate = s.matemap[s.matei]; goto ext_1mm;
 	case P_AFTER_SEEDS: goto after_seeds_l;
-	case P_AFTER_EXT_SEEDS: goto after_ext_seeds;
+	case P_EXT_SEEDS: mate = s.matemap[s.matei]; goto ext_seeds;
 	default: abort();
 	}
 	setup_read(s);
-	// exact end-to-end alignments (bt2_search.cpp:3453-3482)
+	// exact end-to-end alignments (bt2_search.cpp:3453-3631)
 	if(R_doExactUpFront) {
-		if(!(!s.filt || s.done || s.msinkwrap.state().doneWithMate(true))) {
-			swmSeed.exatts++;
-			if(engine_read(s)) {
-				rq[K_EXACT].push_back(&s);
-				prefetch_seeds(s);
+		{
+			bool asked = false;
+			for(size_t mi = 0; mi < nmates; mi++) {
+				const size_t m = s.matemap[mi];
+				if(!s.filt[m] || s.done[m] || s.msinkwrap.state().doneWithMate(m == 0)) continue;
+				swmSeed.exatts++;
+				if(engine_read(s, (int)m)) {
+					rq[K_EXACT].push_back(Rq{&s, (int)m});
+					s.mr[m].sweep_asked = true;
+					s.round_off[m] = 0;
+					prefetch_seeds(s, (int)m);
+					asked = true;
+				} else {
+					s.nelt[m] = al.exactSweep(*ebwtFw, *s.rds[m], *sc, s.nofw[m], s.norc[m], 2, s.minedfw[m], s.minedrc[m],
+					                          true, s.shs[m], sdm);
+					g_cpu[K_EXACT]++;
+					const size_t bestmin = std::min(s.minedfw[m], s.minedrc[m]);
+					if(bestmin == 0) sdm.bestmin0++;
+					else if(bestmin == 1) sdm.bestmin1++;
+					else sdm.bestmin2++;
+				}
+			}
+			if(asked) {
 				s.pc = P_AFTER_EXACT;
 				return;
 			}
-			s.nelt = al.exactSweep(*ebwtFw, rd, *sc, s.nofw, s.norc, 2, s.minedfw, s.minedrc, true, s.shs[0], sdm);
-			g_cpu[K_EXACT]++;
-			goto exact_done;
-		after_exact:
-			{
-				const uint32_t* out = s.sweep;
-				if(!s.nofw) s.minedfw = out[0];
-				if(!s.norc) s.minedrc = out[1];
-				sdm.bwops += out[6];
-				size_t nelt = 0;
-				const int64_t score = (int64_t)s.rdlen * sc->match();
-				if(!s.nofw && out[0] == 0 && out[3] > out[2]) {
-					s.shs[0].addExactEeFw(out[2], out[3], NULL, NULL, true, score);
-					nelt += out[3] - out[2];
-				}
-				if(!s.norc && out[1] == 0 && out[5] > out[4]) {
-					s.shs[0].addExactEeRc(out[4], out[5], NULL, NULL, false, score);
-					nelt += out[5] - out[4];
-				}
-				s.nelt = nelt;
-			}
-		exact_done:
-			{
-				size_t bestmin = std::min(s.minedfw, s.minedrc);
-				if(bestmin == 0) sdm.bestmin0++;
-				else if(bestmin == 1) sdm.bestmin1++;
-				else sdm.bestmin2++;
-			}
 		}
-		if(!R_seedSumm) {
-			if(s.nelt == 0) {
-				s.shs[0].clearExactE2eHits();
-			} else if(s.msinkwrap.state().doneWithMate(true)) {
-				s.shs[0].clearExactE2eHits();
-				s.done = true;
-			} else {
-				start_ext(s, -1, 0, 0);
-				ret = s.sd.ext_step(*this, s);
-				if(ret == EXTEND_BLOCKED) {
-					s.pc = P_AFTER_EXT_EXACT;
-					return;
-				}
-				goto have_ext_exact;
-			after_ext_exact:
-				ret = s.sd.ext_step(*this, s);
-				if(ret == EXTEND_BLOCKED) return;
-			have_ext_exact:
-				s.shs[0].clearExactE2eHits();
-				after_ext(*this, s, ret, true);
+	after_exact:
+		for(size_t m = 0; m < 2; m++) {
+			MateRes& x = s.mr[m];
+			if(!x.sweep_asked) continue;
+			x.sweep_asked = false;
+			const uint32_t* out = x.sweep;
+			if(!s.nofw[m]) s.minedfw[m] = out[0];
+			if(!s.norc[m]) s.minedrc[m] = out[1];
+			sdm.bwops += out[6];
+			size_t ne = 0;
+			const int64_t score = (int64_t)s.rdlens[m] * sc->match();
+			if(!s.nofw[m] && out[0] == 0 && out[3] > out[2]) {
+				s.shs[m].addExactEeFw(out[2], out[3], NULL, NULL, true, score);
+				ne += out[3] - out[2];
 			}
+			if(!s.norc[m] && out[1] == 0 && out[5] > out[4]) {
+				s.shs[m].addExactEeRc(out[4], out[5], NULL, NULL, false, score);
+				ne += out[5] - out[4];
+			}
+			s.nelt[m] = ne;
+			const size_t bestmin = std::min(s.minedfw[m], s.minedrc[m]);
+			if(bestmin == 0) sdm.bestmin0++;
+			else if(bestmin == 1) sdm.bestmin1++;
+			else sdm.bestmin2++;
+		}
+		s.matemap[0] = 0;
+		s.matemap[1] = 1;
+		if(s.nelt[0] > 0 && s.nelt[1] > 0 && s.nelt[0] > s.nelt[1]) {   // the mate with fewer exact hits first
+			s.matemap[0] = 1;
+			s.matemap[1] = 0;
+		}
+		for(s.matei = 0; s.matei < (R_seedSumm ? 0u : 2u); s.matei++) {
+			mate = s.matemap[s.matei];
+			if(s.nelt[mate] == 0 || s.nelt[mate] > eePeEeltLimit) {
+				s.shs[mate].clearExactE2eHits();
+				continue;
+			}
+			if(s.msinkwrap.state().doneWithMate(mate == 0)) {
+				s.shs[mate].clearExactE2eHits();
+				s.done[mate] = true;
+				continue;
+			}
+			start_ext(s, (int)mate, -1, 0, 0);
+		ext_exact:
+			ret = ext(s);
+			if(ret == EXTEND_BLOCKED) {
+				s.pc = P_EXT_EXACT;
+				return;
+			}
+			s.shs[mate].clearExactE2eHits();
+			after_ext(*this, s, (int)mate, ret, true);
 		}
 	}
 	// 1-mismatch end-to-end alignments (bt2_search.cpp:3633-3813)
 	if(R_do1mmUpFront && !R_seedSumm) {
-		if(!s.filt || s.done) {
-			s.shs[0].clear1mmE2eHits();
-			s.nelt = 0;
-		} else {
-			s.nelt = 0;
-			s.yfw = s.minedfw <= 1 && !s.nofw;
-			s.yrc = s.minedrc <= 1 && !s.norc;
-			if(s.yfw || s.yrc) {
-				swmSeed.mm1atts++;
-				if(engine_read(s) && bsc_ok && s.minsc >= std::numeric_limits<int32_t>::min() &&
-				   s.minsc <= std::numeric_limits<int32_t>::max() && R_localAlign == !sc->monotone) {
-					s.mm_nofw = s.yfw ? 0 : 1;
-					s.mm_norc = s.yrc ? 0 : 1;
-					s.mm_minsc = (int32_t)s.minsc;
-					rq[K_1MM].push_back(&s);
-					s.pc = P_AFTER_1MM;
-					return;
-				after_1mm:
-					sdm.bwops += s.mm_ops;
-					for(int32_t k = 0; k < s.mm_cnt; k++) {
-						const bt2g_mm1& h = s.mm[k];
-						Edit e((uint32_t)h.pos, h.chr, h.qchr, EDIT_TYPE_MM, false);
-						s.shs[0].add1mmEe(h.top, h.bot, &e, NULL, h.fw != 0, h.score);
-					}
-				} else {
-					al.oneMmSearch(ebwtFw, ebwtBw, rd, *sc, s.minsc, !s.yfw, !s.yrc, R_localAlign, false, true, s.shs[0], sdm);
-					g_cpu[K_1MM]++;
+		{
+			bool asked = false;
+			for(size_t mi = 0; mi < nmates; mi++) {
+				const size_t m = s.matemap[mi];
+				if(!s.filt[m] || s.done[m] || s.nelt[m] > eePeEeltLimit) {
+					s.shs[m].clear1mmE2eHits();
+					s.nelt[m] = 0;
+					continue;
 				}
-				s.nelt = s.shs[0].num1mmE2eHits();
+				s.nelt[m] = 0;
+				s.yfw[m] = s.minedfw[m] <= 1 && !s.nofw[m];
+				s.yrc[m] = s.minedrc[m] <= 1 && !s.norc[m];
+				if(s.yfw[m] || s.yrc[m]) {
+					swmSeed.mm1atts++;
+					if(engine_read(s, (int)m) && bsc_ok && s.minsc[m] >= std::numeric_limits<int32_t>::min() &&
+					   s.minsc[m] <= std::numeric_limits<int32_t>::max() && R_localAlign == !sc->monotone) {
+						MateRes& x = s.mr[m];
+						x.mm_nofw = s.yfw[m] ? 0 : 1;
+						x.mm_norc = s.yrc[m] ? 0 : 1;
+						x.mm_minsc = (int32_t)s.minsc[m];
+						x.mm_asked = true;
+						rq[K_1MM].push_back(Rq{&s, (int)m});
+						asked = true;
+					} else {
+						al.oneMmSearch(ebwtFw, ebwtBw, *s.rds[m], *sc, s.minsc[m], !s.yfw[m], !s.yrc[m], R_localAlign, false,
+						               true, s.shs[m], sdm);
+						g_cpu[K_1MM]++;
+						s.nelt[m] = s.shs[m].num1mmE2eHits();
+					}
+				}
+			}
+			if(asked) {
+				s.pc = P_AFTER_1MM;
+				return;
 			}
 		}
-		if(s.nelt > 0) {
-			if(s.msinkwrap.state().doneWithMate(true)) {
-				s.done = true;
-			} else {
-				start_ext(s, -1, 0, 0);
-				ret = s.sd.ext_step(*this, s);
-				if(ret == EXTEND_BLOCKED) {
-					s.pc = P_AFTER_EXT_1MM;
-					return;
-				}
-				goto have_ext_1mm;
-			after_ext_1mm:
-				ret = s.sd.ext_step(*this, s);
-				if(ret == EXTEND_BLOCKED) return;
-			have_ext_1mm:
-				s.shs[0].clear1mmE2eHits();
-				after_ext(*this, s, ret, true);
+	after_1mm:
+		for(size_t m = 0; m < 2; m++) {
+			MateRes& x = s.mr[m];
+			if(!x.mm_asked) continue;
+			x.mm_asked = false;
+			sdm.bwops += x.mm_ops;
+			for(int32_t k = 0; k < x.mm_cnt; k++) {
+				const bt2g_mm1& h = x.mm[k];
+				Edit e((uint32_t)h.pos, h.chr, h.qchr, EDIT_TYPE_MM, false);
+				s.shs[m].add1mmEe(h.top, h.bot, &e, NULL, h.fw != 0, h.score);
 			}
+			s.nelt[m] = s.shs[m].num1mmE2eHits();
+		}
+		s.matemap[0] = 0;
+		s.matemap[1] = 1;
+		if(s.nelt[0] > 0 && s.nelt[1] > 0 && s.nelt[0] > s.nelt[1]) {
+			s.matemap[0] = 1;
+			s.matemap[1] = 0;
+		}
+		for(s.matei = 0; s.matei < (R_seedSumm ? 0u : 2u); s.matei++) {
+			mate = s.matemap[s.matei];
+			if(s.nelt[mate] == 0 || s.nelt[mate] > eePeEeltLimit) continue;
+			if(s.msinkwrap.state().doneWithMate(mate == 0)) {
+				s.done[mate] = true;
+				continue;
+			}
+			start_ext(s, (int)mate, -1, 0, 0);
+		ext_1mm:
+			ret = ext(s);
+			if(ret == EXTEND_BLOCKED) {
+				s.pc = P_EXT_1MM;
+				return;
+			}
+			s.shs[mate].clear1mmE2eHits();
+			after_ext(*this, s, (int)mate, ret, true);
 		}
 	}
 	// seed rounds (bt2_search.cpp:3814-4090)
-	s.seedlen = R_multiseedLen;
-	s.nrounds = std::min<size_t>(s.nrounds, (size_t)s.interval);
+	s.seedlens[0] = s.seedlens[1] = R_multiseedLen;
+	s.nrounds[0] = std::min<size_t>(s.nrounds[0], (size_t)s.interval[0]);
+	s.nrounds[1] = std::min<size_t>(s.nrounds[1], (size_t)s.interval[1]);
 	for(s.roundi = 0; s.roundi < R_nSeedRounds; s.roundi++) {
 		s.ca.nextRead();
 		s.shs[0].clearSeeds();
 		s.shs[1].clearSeeds();
-		if(s.done || s.msinkwrap.state().doneWithMate(true)) {
-			s.done = true;
-		} else if(s.roundi >= s.nrounds || s.interval <= (int)s.roundi) {
-			// not doing this round
-		} else {
-			s.offset = ((size_t)s.interval * s.roundi) / s.nrounds;
+		{
+			// which mates this round searches (until one stops it), and their engine
+			// searches asked together
+			bool asked = false;
+			for(size_t mi = 0; mi < nmates; mi++) {
+				const size_t m = s.matemap[mi];
+				s.round_go[m] = false;
+				if(s.done[m] || s.msinkwrap.state().doneWithMate(m == 0)) continue;
+				if(s.roundi >= s.nrounds[m] || s.interval[m] <= (int)s.roundi) continue;
+				s.round_off[m] = ((size_t)s.interval[m] * s.roundi) / s.nrounds[m];
+				s.seeds[m].clear();
+				Seed::mmSeeds(R_multiseedMms, s.seedlens[m], s.seeds[m], s.gc);
+				if(s.round_off[m] > 0 && s.seeds[m][0].len + s.round_off[m] > s.rds[m]->length()) continue;
+				s.round_go[m] = true;
+				const size_t before = rq[K_SEEDS].size();
+				prefetch_seeds(s, (int)m);
+				asked = asked || rq[K_SEEDS].size() > before;
+			}
+			if(asked) {
+				s.pc = P_AFTER_SEEDS;
+				return;
+			}
+		}
+	after_seeds_l:
+		for(s.matei = 0; s.matei < nmates; s.matei++) {
+			mate = s.matemap[s.matei];
+			if(s.done[mate] || s.msinkwrap.state().doneWithMate(mate == 0)) {
+				s.done[mate] = true;
+				continue;
+			}
+			if(!s.round_go[mate]) continue;    // not this round (its count, its interval, or off the end)
 			swmSeed.sdatts++;
-			s.seeds.clear();
-			Seed::mmSeeds(R_multiseedMms, s.seedlen, s.seeds, s.gc);
-			if(s.offset > 0 && s.seeds[0].len + s.offset > rd.length()) goto round_summary;
-			if(!engine_read(s) || R_multiseedMms != 0 || ebwtBw == NULL) {
+			const Read& rd = *s.rds[mate];
+			if(!engine_read(s, (int)mate) || R_multiseedMms != 0 || ebwtBw == NULL) {
 				// the reference's own seed search on the host (instantiateSeeds +
 				// searchAllSeeds, bt2_search.cpp:3873-3913)
 				std::pair<int, int> instFw, instRc;
-				std::pair<int, int> inst = al.instantiateSeeds(s.seeds, s.offset, s.interval, rd, *sc, s.nofw, s.norc, s.ca,
-				                                               s.shs[0], sdm, instFw, instRc);
+				std::pair<int, int> inst = al.instantiateSeeds(s.seeds[mate], s.round_off[mate], s.interval[mate], rd, *sc,
+				                                               s.nofw[mate], s.norc[mate], s.ca, s.shs[mate], sdm, instFw,
+				                                               instRc);
 				if(inst.first + inst.second == 0) {
-					s.done = true;
-					goto round_summary;
+					s.done[mate] = true;
+					break;
 				}
 				s.seedsTried += (inst.first + inst.second);
-				s.seedsTriedMS[0] = instFw.first + instFw.second;
-				s.seedsTriedMS[1] = instRc.first + instRc.second;
-				al.searchAllSeeds(s.seeds, ebwtFw, ebwtBw, rd, *sc, s.ca, s.shs[0], sdm, s.prm);
+				s.seedsTriedMS[mate * 2 + 0] = instFw.first + instFw.second;
+				s.seedsTriedMS[mate * 2 + 1] = instRc.first + instRc.second;
+				al.searchAllSeeds(s.seeds[mate], ebwtFw, ebwtBw, rd, *sc, s.ca, s.shs[mate], sdm, s.prm);
 				g_cpu[K_SEEDS]++;
 			} else {
-				{
-					const int inst = instantiate(*this, s);
-					if(inst == 0) {
-						s.done = true;
-						goto round_summary;
-					}
-					s.seedsTried += (size_t)inst;
+				const int inst = instantiate(s, (int)mate, s.round_off[mate]);
+				if(inst == 0) {
+					s.done[mate] = true;
+					break;
 				}
-				if(!(s.sd_ready && s.sd_L == (uint32_t)s.seeds[0].len && s.sd_per == (uint32_t)s.interval &&
-				     s.sd_off == (uint32_t)s.offset && s.sd_nof == (uint32_t)s.shs[0].numOffs())) {
-					s.sd_ready = false;
-					s.sd_L = (uint32_t)s.seeds[0].len;
-					s.sd_per = (uint32_t)s.interval;
-					s.sd_off = (uint32_t)s.offset;
-					s.sd_nof = (uint32_t)s.shs[0].numOffs();
-					rq[K_SEEDS].push_back(&s);
-					s.pc = P_AFTER_SEEDS;
-					return;
+				s.seedsTried += (size_t)inst;
+				const MateRes& x = s.mr[mate];
+				if(!(x.sd_ready && x.sd_L == (uint32_t)s.seeds[mate][0].len && x.sd_per == (uint32_t)s.interval[mate] &&
+				     x.sd_off == (uint32_t)s.round_off[mate] && x.sd_nof == (uint32_t)s.shs[mate].numOffs())) {
+					fprintf(stderr, "bt2g batch: seed search of the round not asked\n");
+					abort();
 				}
-			after_seeds_l:
-				s.sd_ready = false;
-				after_seeds(s);
+				after_seeds(s, (int)mate);
 			}
-			if(s.shs[0].empty()) s.done = true;
+			if(s.shs[mate].empty()) {
+				s.done[mate] = true;
+				break;
+			}
 		}
-	round_summary:
-		if(!s.shs[0].empty()) {
-			s.nUniqueSeeds += s.shs[0].numUniqueSeeds();
-			s.nUniqueSeedsMS[0] += s.shs[0].numUniqueSeedsStrand(true);
-			s.nUniqueSeedsMS[1] += s.shs[0].numUniqueSeedsStrand(false);
-			s.nRepeatSeeds += s.shs[0].numRepeatSeeds();
-			s.nRepeatSeedsMS[0] += s.shs[0].numRepeatSeedsStrand(true);
-			s.nRepeatSeedsMS[1] += s.shs[0].numRepeatSeedsStrand(false);
-			s.seedHitTot += s.shs[0].numElts();
-			s.seedHitTotMS[0] += s.shs[0].numEltsFw();
-			s.seedHitTotMS[1] += s.shs[0].numEltsRc();
-			swmSeed.sdsucc++;
+		for(size_t m = 0; m < 2; m++) {
+			if(!s.shs[m].empty()) {
+				s.nUniqueSeeds += s.shs[m].numUniqueSeeds();
+				s.nUniqueSeedsMS[m * 2 + 0] += s.shs[m].numUniqueSeedsStrand(true);
+				s.nUniqueSeedsMS[m * 2 + 1] += s.shs[m].numUniqueSeedsStrand(false);
+				s.nRepeatSeeds += s.shs[m].numRepeatSeeds();
+				s.nRepeatSeedsMS[m * 2 + 0] += s.shs[m].numRepeatSeedsStrand(true);
+				s.nRepeatSeedsMS[m * 2 + 1] += s.shs[m].numRepeatSeedsStrand(false);
+				s.seedHitTot += s.shs[m].numElts();
+				s.seedHitTotMS[m * 2 + 0] += s.shs[m].numEltsFw();
+				s.seedHitTotMS[m * 2 + 1] += s.shs[m].numEltsRc();
+			}
 		}
-		if(s.done || s.msinkwrap.state().doneWithMate(true)) {
-			s.done = true;
-		} else if(!R_seedSumm && !s.shs[0].empty()) {
-			s.shs[0].rankSeedHits(s.rnd, s.msinkwrap.allHits());
-			start_ext(s, R_multiseedMms, s.seedlen, s.interval);
-			ret = s.sd.ext_step(*this, s);
+		{
+			double uniqFactor[2] = {0.0f, 0.0f};
+			for(size_t m = 0; m < 2; m++) {
+				if(!s.shs[m].empty()) {
+					swmSeed.sdsucc++;
+					uniqFactor[m] = s.shs[m].uniquenessFactor();
+				}
+			}
+			s.matemap[0] = 0;
+			s.matemap[1] = 1;
+			if(!s.shs[0].empty() && !s.shs[1].empty() && uniqFactor[1] > uniqFactor[0]) {
+				s.matemap[0] = 1;
+				s.matemap[1] = 0;
+			}
+		}
+		for(s.matei = 0; s.matei < nmates; s.matei++) {
+			mate = s.matemap[s.matei];
+			if(s.done[mate] || s.msinkwrap.state().doneWithMate(mate == 0)) {
+				s.done[mate] = true;
+				continue;
+			}
+			if(R_seedSumm) continue;
+			if(s.shs[mate].empty()) continue;
+			s.shs[mate].rankSeedHits(s.rnd, s.msinkwrap.allHits());
+			start_ext(s, (int)mate, R_multiseedMms, s.seedlens[mate], s.interval[mate]);
+		ext_seeds:
+			ret = ext(s);
 			if(ret == EXTEND_BLOCKED) {
-				s.pc = P_AFTER_EXT_SEEDS;
+				s.pc = P_EXT_SEEDS;
 				return;
 			}
-			goto have_ext_seeds;
-		after_ext_seeds:
-			ret = s.sd.ext_step(*this, s);
-			if(ret == EXTEND_BLOCKED) return;
-		have_ext_seeds:
-			after_ext(*this, s, ret, false);
+			after_ext(*this, s, (int)mate, ret, false);
 		}
-		if(!s.done && s.shs[0].averageHitsPerSeed() < R_seedBoostThresh) s.done = true;
+		for(size_t m = 0; m < 2; m++)
+			if(!s.done[m] && s.shs[m].averageHitsPerSeed() < R_seedBoostThresh) s.done[m] = true;
 	}
 	// per-read seed statistics (bt2_search.cpp:4091-4124) and the SAM record
 	if(s.seedsTried > 0) {
@@ -2038,10 +2686,12 @@ void Driver::step_read(Slot& s) {
 	}
 	{
 		size_t totnucs = 0;
-		if(s.filt) {
-			size_t len = s.rdlen;
-			if(!s.nofw && !s.norc) len *= 2;
-			totnucs += len;
+		for(size_t m = 0; m < nmates; m++) {
+			if(s.filt[m]) {
+				size_t len = s.rdlens[m];
+				if(!s.nofw[m] && !s.norc[m]) len *= 2;
+				totnucs += len;
+			}
 		}
 		s.prm.seedsPerNuc = totnucs > 0 ? ((float)s.seedsTried / totnucs) : -1;
 		for(int k = 0; k < 4; k++) s.prm.seedsPerNucMS[k] = totnucs > 0 ? ((float)s.seedsTriedMS[k] / totnucs) : -1;
@@ -2052,28 +2702,8 @@ void Driver::step_read(Slot& s) {
 	s.pc = P_FINISH;
 }
 
-}  // namespace
-
-namespace {
-
-// The first seed round's search, asked with the exact sweep: its arguments are
-// functions of the read and the server's options (round 0: offset 0, the
-// read's interval, bt2_search.cpp:3814-3906).  The round takes it only if its
-// own arguments are the same (checked in step_read).
-void Driver::prefetch_seeds(Slot& s) {
-	if(R_seedSumm || R_nSeedRounds == 0 || R_multiseedMms != 0 || ebwtBw == NULL) return;
-	const int L = R_multiseedLen;
-	int nseeds = 1;
-	if((int)s.rdlen > L) nseeds += ((int)s.rdlen - L) / s.interval;
-	s.sd_L = (uint32_t)L;
-	s.sd_per = (uint32_t)s.interval;
-	s.sd_off = 0;
-	s.sd_nof = (uint32_t)nseeds;
-	s.sd_ready = false;
-	rq[K_SEEDS].push_back(&s);
-}
-
 void Driver::gpu_phase() {
+	++stamp;
 	call_exact();
 	call_seeds();
 	call_1mm();
@@ -2124,10 +2754,6 @@ void Driver::admit(Elem* e) {
 		first = false;
 		if(!e->re.readResult.first) continue;
 		Read& ra = ps->read_a();
-		if(!ps->read_b().empty()) {
-			fprintf(stderr, "bt2g batch: paired reads are served by the fiber drop-in (bowtie2-align-server-gpu)\n");
-			abort();
-		}
 		if(ra.rdid < R_skipReads || ra.rdid >= R_qUpto) continue;
 		Slot* s;
 		if(freel.empty()) {
@@ -2138,8 +2764,9 @@ void Driver::admit(Elem* e) {
 			freel.pop_back();
 		}
 		s->el = e;
-		s->rd = &ra;
-		s->rdb = &ps->read_b();
+		s->rds[0] = &ra;
+		s->rds[1] = &ps->read_b();
+		s->paired = !ps->read_b().empty();
 		s->rdid = ra.rdid;
 		s->msink = &ps->msink();
 		s->pc = P_START;
@@ -2172,6 +2799,14 @@ void Driver::run_loop() {
 	rp.reset(new ReportingParams(R_allHits ? std::numeric_limits<THitInt>::max() : R_khits, R_mhits, 0, R_msample,
 	                             gReportDiscordant, gReportMixed));
 	mapq.reset(new_mapq(R_mapqv, R_scoreMin, *sc));
+	// the worker's paired-end policy (bt2_search.cpp:3148-3169)
+	int pepolFlag;
+	if(gMate1fw && gMate2fw) pepolFlag = PE_POLICY_FF;
+	else if(gMate1fw && !gMate2fw) pepolFlag = PE_POLICY_FR;
+	else if(!gMate1fw && gMate2fw) pepolFlag = PE_POLICY_RF;
+	else pepolFlag = PE_POLICY_RR;
+	pepol.reset(new PairedEndPolicy(pepolFlag, gMaxInsert, gMinInsert, R_localAlign, gFlippedMatesOK, gDovetailMatesOK,
+	                                gContainMatesOK, gOlapMatesOK, gExpandToFrag));
 	max_held = env_or("BT2G_BATCH_ELEMS", 64);
 	spec_k = env_or("BT2G_SPEC_DPS", 16);
 	{

@@ -8,12 +8,27 @@ cd /tmp && export TMPDIR=/tmp
 cd "$GRAFT_REPO_ROOT" || exit 1
 O=gpurun_out/${2:-r04}
 mkdir -p $O
+# heartbeat: long index builds print nothing for minutes
+( while sleep 50; do date +%T >> $O/heartbeat; done ) &
+HB=$!
+trap "kill $HB 2>/dev/null" EXIT
 case "$1" in
 gap)
   timeout -k 10 600 rocprofv3 --kernel-trace --hip-trace --output-format csv -d $O/ptrace -o run -- \
     python3 bench.py --mode paired --no-cpu-baseline --server-sample 0 --steps 2 --warmup 1 > $O/paired.json 2> $O/paired.log || { tail -20 $O/paired.log; exit 1; }
   python3 scripts/gap_trace.py $O/ptrace 15 > $O/gap.txt 2>&1; cat $O/gap.txt | head -80
   find $O/ptrace -name "*.csv" -size +20M -delete ;;
+batch)
+  # the batch-first server (integration/bt2g_batch.cpp) vs the stock server, configs[1] policy,
+  # 3.1 Gbp hg38-like genome, 200 k reads, <= 10 k per connection, 8 connections
+  for p in ${3:-32}; do
+    timeout -k 10 900 python3 -u scripts/dropin_bench.py --genome-mb 3100 --reads 200000 --workdir /tmp/db \
+      --dropin-binary oracle/_ref/bowtie2-align-server-batch --gpu-workers $p $SKIP > $O/batch_p$p.json 2> $O/batch_p$p.log \
+      || { tail -30 $O/batch_p$p.log; tail -30 /tmp/db/server_dropin.log; exit 1; }
+    cp /tmp/db/server_dropin.log $O/server_p$p.log
+    SKIP=--skip-stock
+    python3 -c "import json,sys; d=json.load(open('$O/batch_p$p.json')); print($p, {k: d[k] for k in ('sam_identical','speedup') if k in d}, d['dropin']['rate'], d['dropin']['server_cpu_s'], d['dropin'].get('engine_calls'))"
+  done ;;
 tests)
   timeout -k 10 1000 python -u -m pytest tests -m gpu -x -v --timeout 600 --timeout-method thread > $O/gpu_tests.log 2>&1 || { tail -20 $O/gpu_tests.log; exit 1; }
   tail -2 $O/gpu_tests.log

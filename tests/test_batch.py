@@ -32,6 +32,7 @@ from oracle import ref_server as rs  # noqa: E402
 SRV_BATCH = os.path.join(rs.REF_DIR, "bowtie2-align-server-batch")
 SRV_BATCH_STUB = os.path.join(rs.REF_DIR, "bowtie2-align-server-batch-stub")
 LONGREADS = os.path.join(ROOT, "tests", "golden", "longreads.fq.gz")     # example/reads/longreads.fq
+LAMBDA_PE = [os.path.join(ROOT, "tests", "golden", f"reads_{m}.fq.gz") for m in (1, 2)]  # example/reads/reads_{1,2}.fq
 
 
 def _need(*paths):
@@ -52,8 +53,11 @@ def indexes(tmp_path_factory):
     return {"lambda": str(d / "lambda_virus"), "synth": (str(d / "syn"), syn)}
 
 
-def _reads(idx, n, seed, dirpath, read_len=150):
+def _reads(idx, n, seed, dirpath, read_len=150, paired=False):
     import bench
+    if paired:
+        r, q = bench.make_pairs(idx.ref_codes, n, read_len, seed)
+        return rs.write_fastq_chunks(dirpath, r[:n], q[:n], codes2=r[n:], quals2=q[n:])
     r, q = bench.make_reads(idx.ref_codes, n, read_len, seed)
     return rs.write_fastq_chunks(dirpath, r, q)
 
@@ -106,6 +110,33 @@ def test_batch_sam_parity_cpu(indexes, tmp_path, name, args, n):
     assert st["sw_dp"][0] > 0
 
 
+PAIRED_CASES = [
+    ("paired", [], 800),                           # configs[2] policy, --end-to-end
+    ("paired_vs", ["--very-sensitive"], 500),      # configs[4] policy
+    ("paired_local", ["--local"], 400),
+    ("paired_nomixed", ["-I", "100", "-X", "300", "--no-mixed"], 400),
+    ("paired_ff_nodisc", ["--ff", "--no-discordant"], 300),
+    ("paired_k3", ["-k", "3"], 300),
+]
+
+
+@pytest.mark.parametrize("name,args,n", PAIRED_CASES, ids=[c[0] for c in PAIRED_CASES])
+def test_batch_sam_parity_paired_cpu(indexes, tmp_path, name, args, n):
+    """extendSeedsPaired restated (anchor + mate-search DPs): SAM equals the stock server's."""
+    _need(rs.SERVER, rs.CLIENT, SRV_BATCH_STUB)
+    base, idx = indexes["synth"]
+    chunks = _reads(idx, n, 29, str(tmp_path), paired=True)
+    _, _, _, st = compare(SRV_BATCH_STUB, base, chunks, args, str(tmp_path))
+    assert st["sw_dp"][0] > 0
+
+
+def test_batch_lambda_pairs_cpu(indexes, tmp_path):
+    """lambda example pairs (example/reads/reads_{1,2}.fq), the first 2 000."""
+    _need(rs.SERVER, rs.CLIENT, SRV_BATCH_STUB, *LAMBDA_PE)
+    compare(SRV_BATCH_STUB, indexes["lambda"], [["-1", LAMBDA_PE[0], "-2", LAMBDA_PE[1], "-u", "2000"]], [],
+            str(tmp_path))
+
+
 def test_batch_no_speculation_cpu(indexes, tmp_path):
     """BT2G_SPEC_DPS=1: every DP asked when the loop reaches it (no table reuse)."""
     _need(rs.SERVER, rs.CLIENT, SRV_BATCH_STUB)
@@ -142,20 +173,28 @@ def test_batch_many_drivers_cpu(indexes, tmp_path):
 
 
 GPU_CASES = [
-    ("sensitive", [], 20000),
-    ("local", ["--local"], 10000),
-    ("very_sensitive", ["--very-sensitive"], 5000),
+    ("sensitive", [], 20000, False),
+    ("local", ["--local"], 10000, False),
+    ("very_sensitive", ["--very-sensitive"], 5000, False),
+    ("paired", [], 8000, True),
+    ("paired_vs", ["--very-sensitive"], 4000, True),
 ]
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("name,args,n", GPU_CASES, ids=[c[0] for c in GPU_CASES])
-def test_batch_sam_parity_gpu(indexes, tmp_path, name, args, n):
+@pytest.mark.parametrize("name,args,n,paired", GPU_CASES, ids=[c[0] for c in GPU_CASES])
+def test_batch_sam_parity_gpu(indexes, tmp_path, name, args, n, paired):
     _need(rs.SERVER, rs.CLIENT, SRV_BATCH)
     base, idx = indexes["synth"]
-    chunks = _reads(idx, n, 7, str(tmp_path))
+    chunks = _reads(idx, n, 7, str(tmp_path), paired=paired)
     t_ref, t_new, nrec, st = compare(SRV_BATCH, base, chunks, args, str(tmp_path), threads=8)
     print(f"\n[{name}] {nrec} records identical; stock {t_ref:.2f}s, batch {t_new:.2f}s; {st}")
+
+
+@pytest.mark.gpu
+def test_batch_lambda_pairs_gpu(indexes, tmp_path):
+    _need(rs.SERVER, rs.CLIENT, SRV_BATCH, *LAMBDA_PE)
+    compare(SRV_BATCH, indexes["lambda"], [["-1", LAMBDA_PE[0], "-2", LAMBDA_PE[1]]], [], str(tmp_path), threads=8)
 
 
 @pytest.mark.gpu
