@@ -168,6 +168,30 @@ struct Carrier {
 	}
 };
 
+}  // namespace
+}  // namespace bt2gf
+extern "C" int __real_pthread_mutex_lock(pthread_mutex_t* m);
+namespace bt2gf {
+namespace {
+
+// The scheduler's own mutexes (a carrier's inbox lock, the condition-variable
+// tables, the carrier list) are taken with the real pthread_mutex_lock: never
+// through the fiber-yielding wrapper below.  A fiber that yielded while in the
+// middle of scheduler code would let another fiber of its carrier run the same
+// code on the same thread-local state (r03w: a fiber suspended at a contended
+// carrier lock inside wake_many, another fiber's wake_many reallocated the
+// thread-local grouping vector, the first resumed on a dangling reference and
+// the server died -- "once in ~6 runs" with the unlock-time baton, which called
+// wake_many from fibers at every unlock; the lock-time baton had the same
+// window, less often).
+struct RealGuard {
+	pthread_mutex_t* m;
+	explicit RealGuard(std::mutex& mu) : m(mu.native_handle()) { __real_pthread_mutex_lock(m); }
+	~RealGuard() { pthread_mutex_unlock(m); }
+	RealGuard(const RealGuard&) = delete;
+	RealGuard& operator=(const RealGuard&) = delete;
+};
+
 thread_local Carrier* t_carrier = nullptr;   // set on carrier threads only
 thread_local int t_skip_sleep = 0;            // spawns whose SLEEP(10) is skipped
 
@@ -283,7 +307,7 @@ void Carrier::run() {
 	uint64_t last_poll = 0;
 	for(;;) {
 		{
-			std::lock_guard<std::mutex> lk(mu);
+			RealGuard lk(mu);
 			if(!inbox.empty()) {
 				ready.insert(ready.end(), inbox.begin(), inbox.end());
 				inbox.clear();
@@ -422,7 +446,7 @@ bool enabled() {
 }
 
 size_t count() {
-	std::lock_guard<std::mutex> lk(g_mu);
+	RealGuard lk(g_mu);
 	return (size_t)g_next_handle;
 }
 
@@ -442,8 +466,10 @@ void block_on_many(void* const* reqs, size_t n) {
 }
 
 void wake_many(void* const* fibers, size_t n) {
-	// grouped per carrier: one lock (and at most one wake-up) per carrier
-	thread_local std::vector<std::pair<Carrier*, std::vector<Fiber*>>> groups;
+	// grouped per carrier: one lock (and at most one wake-up) per carrier.  (On
+	// the caller's stack: a thread-local list is shared by every fiber of the
+	// carrier, see RealGuard.)
+	std::vector<std::pair<Carrier*, std::vector<Fiber*>>> groups;
 	for(size_t i = 0; i < n; i++) {
 		Fiber* f = static_cast<Fiber*>(fibers[i]);
 		size_t g = 0;
@@ -456,12 +482,11 @@ void wake_many(void* const* fibers, size_t n) {
 		Carrier* c = g.first;
 		bool notify;
 		{
-			std::lock_guard<std::mutex> lk(c->mu);
+			RealGuard lk(c->mu);
 			c->inbox.insert(c->inbox.end(), g.second.begin(), g.second.end());
 			notify = c->sleeping;
 		}
 		if(notify) c->cv.notify_one();
-		g.second.clear();
 	}
 }
 
@@ -502,7 +527,7 @@ void __wrap__ZNSt6thread15_M_start_threadESt10unique_ptrINS_6_StateESt14default_
 	uintptr_t handle;
 	Carrier* c;
 	{
-		std::lock_guard<std::mutex> lk(g_mu);
+		RealGuard lk(g_mu);
 		c = pick_carrier();
 		f->home = c;
 		handle = ((uintptr_t)FIBER_HANDLE_TAG << 48) | ++g_next_handle;
@@ -526,7 +551,7 @@ void __wrap__ZNSt6thread6detachEv(std::thread* self) {
 static void pass_baton(const void* cv) {
 	Fiber* w = nullptr;
 	{
-		std::lock_guard<std::mutex> g(g_cv_mu);
+		RealGuard g(g_cv_mu);
 		auto it = g_cv_baton.find(cv);
 		if(it == g_cv_baton.end() || it->second.empty()) return;
 		w = it->second.front();
@@ -547,7 +572,7 @@ void __wrap__ZNSt18condition_variable4waitERSt11unique_lockISt5mutexE(std::condi
 	// the predicate's state under that lock cannot notify before we are on the list
 	f->cv = cv;
 	{
-		std::lock_guard<std::mutex> g(g_cv_mu);
+		RealGuard g(g_cv_mu);
 		g_cv_waiters[cv].push_back(f);
 	}
 	lk.unlock();
@@ -561,7 +586,7 @@ void __wrap__ZNSt18condition_variable4waitERSt11unique_lockISt5mutexE(std::condi
 static void wake_cv_fibers(const void* cv, bool all) {
 	Fiber* w = nullptr;
 	{
-		std::lock_guard<std::mutex> g(g_cv_mu);
+		RealGuard g(g_cv_mu);
 		auto it = g_cv_waiters.find(cv);
 		if(it == g_cv_waiters.end() || it->second.empty()) return;
 		w = it->second.front();
