@@ -60,6 +60,7 @@
 #include <sys/time.h>
 #include <pthread.h>
 #include <signal.h>
+#include <execinfo.h>
 #include <unistd.h>
 
 #include <algorithm>
@@ -73,6 +74,7 @@
 #include <string>
 #include <thread>
 #include <typeinfo>
+#include <unordered_map>
 #include <vector>
 
 #include "aligner_cache.h"
@@ -155,6 +157,8 @@ extern bool gReportMixed;
 extern bool gMate1fw, gMate2fw, gFlippedMatesOK, gDovetailMatesOK, gContainMatesOK, gOlapMatesOK, gExpandToFrag;
 extern int gMinInsert, gMaxInsert;
 
+extern "C" void bt2g_prof_thread(int role);   // bt2g_prof.cpp: CPU samples of this thread ($BT2G_SAMPLE)
+
 namespace {
 
 typedef PatternSourceServiceFactory::ReadElement ReadElement;
@@ -215,6 +219,18 @@ void on_term(int) {
 	_exit(0);
 }
 
+// A fault in a driver thread: its stack on stderr (the server's log), then die.
+void on_fault(int sig) {
+	void* pcs[64];
+	const int n = backtrace(pcs, 64);
+	char msg[64];
+	const int k = snprintf(msg, sizeof(msg), "bt2g batch: signal %d, stack:\n", sig);
+	if(write(2, msg, (size_t)k) < 0) {}
+	backtrace_symbols_fd(pcs, n, 2);
+	signal(sig, SIG_DFL);
+	raise(sig);
+}
+
 // Environment of the engines, set before any thread starts (static
 // initialiser): the runtime reads it at its first HIP call.
 struct EnvInit {
@@ -227,6 +243,9 @@ struct EnvInit {
 		char b[16];
 		snprintf(b, sizeof(b), "%ld", q);
 		setenv("GPU_MAX_HW_QUEUES", b, 1);
+		signal(SIGSEGV, on_fault);
+		signal(SIGBUS, on_fault);
+		signal(SIGABRT, on_fault);
 		if(const char* sp = getenv("BT2G_ADAPTER_STATS")) {
 			strncpy(g_stats_path, sp, sizeof(g_stats_path) - 1);
 			signal(SIGTERM, on_term);
@@ -449,12 +468,27 @@ struct SwDriverB : public SwDriver {
 	bool dp_found(Driver& d, Slot& s, Replay& rp, bool opp, TAlScore ms, TAlScore& bestCell);
 };
 
-// A connection's read buffer the driver holds (PSFactory::ReadAhead's element).
+// A connection's read buffer the driver took from the factory's ready queue
+// (PSFactory::ReadAhead's element).  Its reads are copied into slots and the
+// buffer goes back to its connection soon -- but a connection ends (its
+// AlnSinkSam and OutputQueue are destroyed, pat.cpp:2016-2086) once every
+// buffer of it has come back after its input ran out, so one buffer per
+// connection, the latest, is held until every read of the connection taken so
+// far has finished (Conn below).
 struct Elem {
 	ReadElement re;
-	int live = 0;
+	const void* conn = nullptr;     // the connection: its AlnSink
 	explicit Elem(const ReadElement& r) : re(r) {}
 };
+
+// Per connection: buffers taken and not returned + reads in flight, and the
+// held buffer.
+struct Conn {
+	long live = 0;
+	Elem* last = nullptr;
+};
+std::mutex g_conn_mu;
+std::unordered_map<const void*, Conn> g_conns;
 
 enum {
 	P_START = 0, P_AFTER_EXACT, P_EXT_EXACT, P_1MM, P_AFTER_1MM, P_EXT_1MM, P_ROUND, P_AFTER_SEEDS, P_EXT_SEEDS,
@@ -506,9 +540,10 @@ struct Slot {
 	EList<uint32_t> offIdx2off;
 	RefTables tab;
 
-	// the read (pair)
-	Elem* el = nullptr;
-	Read* rds[2] = {nullptr, nullptr};
+	// the read (pair): copies of the buffer's reads
+	Read rdbuf[2];
+	const void* conn = nullptr;
+	Read* rds[2] = {&rdbuf[0], &rdbuf[1]};
 	TReadId rdid = 0;
 	AlnSink* msink = nullptr;
 	bool paired = false;
@@ -612,7 +647,8 @@ struct Driver {
 	std::mutex in_mu;
 	std::condition_variable in_cv, room_cv;
 	std::deque<Elem*> inbox;
-	size_t held = 0, max_held = 64;
+	size_t max_slots = 2048;         // reads in flight per driver ($BT2G_BATCH_SLOTS)
+	std::atomic<size_t> active_a{0}; // `active` for the feeder
 	// requests of this round
 	std::vector<Rq> rq[K_N];
 	std::vector<std::pair<Slot*, DpRes*>> rq_dp;
@@ -2717,14 +2753,19 @@ void Driver::gpu_phase() {
 
 void Driver::feeder() {
 	pthread_setname_np(pthread_self(), "bt2g-feed");
+	bt2g_prof_thread(2);
 	for(;;) {
 		{
 			std::unique_lock<std::mutex> lk(in_mu);
-			room_cv.wait(lk, [this] { return held < max_held; });
-			held++;
+			room_cv.wait(lk, [this] { return inbox.size() < 4 && active_a.load() < max_slots; });
 		}
 		ReadElement re = R_factory->nextReadPair();      // blocks until a connection has reads
 		Elem* e = new Elem(re);
+		e->conn = &re.ps->msink();
+		{
+			std::lock_guard<std::mutex> lk(g_conn_mu);
+			g_conns[e->conn].live++;
+		}
 		{
 			std::lock_guard<std::mutex> lk(in_mu);
 			inbox.push_back(e);
@@ -2733,21 +2774,31 @@ void Driver::feeder() {
 	}
 }
 
-void finish_elem(Driver& d, Elem* e) {
-	R_factory->returnUnready(e->re);      // back to its connection (PSFactory::ReadAhead's destructor)
-	delete e;
+// One reference fewer for connection `c` (a buffer returned or a read
+// finished); its held last buffer goes back when nothing else is left.
+void conn_done(const void* c, long n) {
+	Elem* ret = nullptr;
 	{
-		std::lock_guard<std::mutex> lk(d.in_mu);
-		d.held--;
+		std::lock_guard<std::mutex> lk(g_conn_mu);
+		auto it = g_conns.find(c);
+		it->second.live -= n;
+		if(it->second.last && it->second.live == 1) {
+			ret = it->second.last;
+			g_conns.erase(it);     // (before the connection may end and its AlnSink's address be reused)
+		}
 	}
-	d.room_cv.notify_one();
+	if(ret) {
+		R_factory->returnUnready(ret->re);
+		delete ret;
+	}
 }
 
 // The reads of one buffer, in the order the reference's worker takes them
-// (bt2_search.cpp:3201-3211, 4174: the buffer is read to its end).
+// (bt2_search.cpp:3201-3211, 4174: the buffer is read to its end), copied into
+// slots.
 void Driver::admit(Elem* e) {
 	PatternSourcePerThread* ps = e->re.ps;
-	e->live = 1;
+	long n = 0;
 	bool first = true;
 	do {
 		if(!first) e->re.nextReadPair();
@@ -2763,27 +2814,46 @@ void Driver::admit(Elem* e) {
 			s = freel.back();
 			freel.pop_back();
 		}
-		s->el = e;
-		s->rds[0] = &ra;
-		s->rds[1] = &ps->read_b();
+		s->rdbuf[0] = ra;
+		s->rdbuf[1] = ps->read_b();
 		s->paired = !ps->read_b().empty();
 		s->rdid = ra.rdid;
 		s->msink = &ps->msink();
+		s->conn = e->conn;
 		s->pc = P_START;
-		e->live++;
+		n++;
 		active++;
 		run.push_back(s);
 	} while(ps->nextReadPairReady());
-	if(--e->live == 0) finish_elem(*this, e);
+	// this buffer is held; the one held before goes back (a connection cannot end
+	// while one of its buffers is held, whether or not the input has ended --
+	// the last batch is not always marked, pat.cpp:161-192)
+	const void* conn = e->conn;
+	Elem* prev;
+	{
+		std::lock_guard<std::mutex> lk(g_conn_mu);
+		Conn& c = g_conns[conn];
+		c.live += n;
+		prev = c.last;
+		c.last = e;
+	}
+	if(prev) {
+		R_factory->returnUnready(prev->re);
+		delete prev;
+		conn_done(conn, 1);
+	} else {
+		conn_done(conn, 0);                   // (returned now if none of its reads is in flight)
+	}
+	active_a.store(active);
 }
 
 void Driver::release(Slot* s) {
-	Elem* e = s->el;
-	s->el = nullptr;
 	active--;
 	freel.push_back(s);
 	if(((++g_reads) & 0xffff) == 0) write_stats();
-	if(--e->live == 0) finish_elem(*this, e);
+	conn_done(s->conn, 1);
+	s->conn = nullptr;
+	if(active_a.exchange(active) >= max_slots && active < max_slots) room_cv.notify_one();
 }
 
 void Driver::run_loop() {
@@ -2807,12 +2877,13 @@ void Driver::run_loop() {
 	else pepolFlag = PE_POLICY_RR;
 	pepol.reset(new PairedEndPolicy(pepolFlag, gMaxInsert, gMinInsert, R_localAlign, gFlippedMatesOK, gDovetailMatesOK,
 	                                gContainMatesOK, gOlapMatesOK, gExpandToFrag));
-	max_held = env_or("BT2G_BATCH_ELEMS", 64);
+	max_slots = env_or("BT2G_BATCH_SLOTS", 2048);
 	spec_k = env_or("BT2G_SPEC_DPS", 16);
 	{
 		char nm[16];
 		snprintf(nm, sizeof(nm), "bt2g-drv%d", tid);
 		pthread_setname_np(pthread_self(), nm);
+		bt2g_prof_thread(1);
 	}
 	std::thread(&Driver::feeder, this).detach();
 	for(;;) {
@@ -2823,6 +2894,7 @@ void Driver::run_loop() {
 			got.swap(inbox);
 		}
 		for(Elem* e : got) admit(e);
+		if(!got.empty()) room_cv.notify_one();
 		const uint64_t t0 = now_us();
 		for(size_t k = 0; k < run.size(); k++) {
 			Slot* s = run[k];

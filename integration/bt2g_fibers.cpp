@@ -192,6 +192,15 @@ struct RealGuard {
 	RealGuard& operator=(const RealGuard&) = delete;
 };
 
+// BT2GF_R03W (test builds only, tests/test_fibers.py): the round-3 scheduler
+// -- the scheduler's mutexes through the yielding wrapper and wake_many's
+// grouping list thread-local -- so that the stress test can show the race.
+#ifdef BT2GF_R03W
+typedef std::lock_guard<std::mutex> SchedGuard;
+#else
+typedef RealGuard SchedGuard;
+#endif
+
 thread_local Carrier* t_carrier = nullptr;   // set on carrier threads only
 thread_local int t_skip_sleep = 0;            // spawns whose SLEEP(10) is skipped
 
@@ -469,7 +478,11 @@ void wake_many(void* const* fibers, size_t n) {
 	// grouped per carrier: one lock (and at most one wake-up) per carrier.  (On
 	// the caller's stack: a thread-local list is shared by every fiber of the
 	// carrier, see RealGuard.)
+#ifdef BT2GF_R03W
+	thread_local std::vector<std::pair<Carrier*, std::vector<Fiber*>>> groups;
+#else
 	std::vector<std::pair<Carrier*, std::vector<Fiber*>>> groups;
+#endif
 	for(size_t i = 0; i < n; i++) {
 		Fiber* f = static_cast<Fiber*>(fibers[i]);
 		size_t g = 0;
@@ -482,11 +495,14 @@ void wake_many(void* const* fibers, size_t n) {
 		Carrier* c = g.first;
 		bool notify;
 		{
-			RealGuard lk(c->mu);
+			SchedGuard lk(c->mu);
 			c->inbox.insert(c->inbox.end(), g.second.begin(), g.second.end());
 			notify = c->sleeping;
 		}
 		if(notify) c->cv.notify_one();
+#ifdef BT2GF_R03W
+		g.second.clear();
+#endif
 	}
 }
 
@@ -551,7 +567,7 @@ void __wrap__ZNSt6thread6detachEv(std::thread* self) {
 static void pass_baton(const void* cv) {
 	Fiber* w = nullptr;
 	{
-		RealGuard g(g_cv_mu);
+		SchedGuard g(g_cv_mu);
 		auto it = g_cv_baton.find(cv);
 		if(it == g_cv_baton.end() || it->second.empty()) return;
 		w = it->second.front();
@@ -572,7 +588,7 @@ void __wrap__ZNSt18condition_variable4waitERSt11unique_lockISt5mutexE(std::condi
 	// the predicate's state under that lock cannot notify before we are on the list
 	f->cv = cv;
 	{
-		RealGuard g(g_cv_mu);
+		SchedGuard g(g_cv_mu);
 		g_cv_waiters[cv].push_back(f);
 	}
 	lk.unlock();
@@ -586,7 +602,7 @@ void __wrap__ZNSt18condition_variable4waitERSt11unique_lockISt5mutexE(std::condi
 static void wake_cv_fibers(const void* cv, bool all) {
 	Fiber* w = nullptr;
 	{
-		RealGuard g(g_cv_mu);
+		SchedGuard g(g_cv_mu);
 		auto it = g_cv_waiters.find(cv);
 		if(it == g_cv_waiters.end() || it->second.empty()) return;
 		w = it->second.front();
