@@ -158,6 +158,7 @@ extern bool gMate1fw, gMate2fw, gFlippedMatesOK, gDovetailMatesOK, gContainMates
 extern int gMinInsert, gMaxInsert;
 
 extern "C" void bt2g_prof_thread(int role);   // bt2g_prof.cpp: CPU samples of this thread ($BT2G_SAMPLE)
+extern "C" void bt2g_prof_role(int role);     // (samples tagged 3: stepping reads, 1: engine calls)
 
 namespace {
 
@@ -2896,6 +2897,7 @@ void Driver::run_loop() {
 		for(Elem* e : got) admit(e);
 		if(!got.empty()) room_cv.notify_one();
 		const uint64_t t0 = now_us();
+		bt2g_prof_role(3);
 		for(size_t k = 0; k < run.size(); k++) {
 			Slot* s = run[k];
 			step_read(*s);
@@ -2904,6 +2906,7 @@ void Driver::run_loop() {
 		}
 		run.clear();
 		const uint64_t t1 = now_us();
+		bt2g_prof_role(1);
 		gpu_phase();
 		const uint64_t t2 = now_us();
 		run.swap(next);

@@ -213,3 +213,6 @@ extern "C" void bt2g_prof_thread(int role) {
 	it.it_value = it.it_interval;
 	timer_settime(t, 0, &it, nullptr);
 }
+
+// Change the calling thread's role tag (which phase its samples belong to).
+extern "C" void bt2g_prof_role(int role) { t_role = (uint64_t)role & 0xF; }
