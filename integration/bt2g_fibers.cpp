@@ -133,6 +133,10 @@ struct Fiber {
 	uint64_t wake_at_ns = 0;          // PARKED by nanosleep: not before this time
 	const void* cv = nullptr;         // the condition variable it waits on
 	void* user = nullptr;             // bt2gf::local()
+	// on a carrier's inbox (set by wake_many, cleared when the carrier takes it):
+	// a second wake-up before that is a scheduler bug -- checked, it would run the
+	// fiber twice
+	std::atomic<bool> queued{false};
 };
 
 uint64_t now_ns() {
@@ -318,6 +322,7 @@ void Carrier::run() {
 		{
 			RealGuard lk(mu);
 			if(!inbox.empty()) {
+				for(Fiber* f : inbox) f->queued.store(false, std::memory_order_relaxed);
 				ready.insert(ready.end(), inbox.begin(), inbox.end());
 				inbox.clear();
 			}
@@ -485,6 +490,10 @@ void wake_many(void* const* fibers, size_t n) {
 #endif
 	for(size_t i = 0; i < n; i++) {
 		Fiber* f = static_cast<Fiber*>(fibers[i]);
+		if(f->queued.exchange(true, std::memory_order_relaxed)) {
+			fprintf(stderr, "bt2g fibers: fiber %p woken twice\n", (void*)f);
+			abort();
+		}
 		size_t g = 0;
 		while(g < groups.size() && groups[g].first != f->home) g++;
 		if(g == groups.size()) groups.emplace_back(f->home, std::vector<Fiber*>());

@@ -147,7 +147,10 @@ class Server:
         self.last_rss_gb = self.rss_gb()
         self.last_threads = self.thread_cpu()
         if errs:
-            raise RuntimeError(f"client failures: {errs[:3]}")
+            # the server's own output (kept in its log file, which outlives the
+            # server): why a connection failed is usually there, not in the client's
+            raise RuntimeError(f"client failures: {errs[:3]}\nserver rc={self.proc.poll()} "
+                               f"(log {self.log_path}), tail:\n{self.log()[-4000:]}")
         return dt, outs
 
     def thread_cpu(self):
