@@ -162,10 +162,10 @@ void die(const char* what, int rc) {
 	throw 1;   // the reference's error convention (bt2_search.cpp:5598-5620)
 }
 
-// $BT2G_ADAPTER_STATS: where the call counts go (written on SIGTERM too).
-void init_env() {
-	static std::once_flag once;
-	std::call_once(once, [] {
+// The HIP runtime's settings, from a static initializer: before main, so before
+// any thread exists (setenv is not safe against a concurrent getenv).
+struct EnvInit {
+	EnvInit() {
 		// dispatcher threads sleep in their stream waits: the server's workers need the
 		// cores (the runtime's blocking wait still spins: r03d, 21 % of the CPU)
 		setenv("BT2G_SYNC", "poll", 0);
@@ -173,9 +173,20 @@ void init_env() {
 		// streams): with HIP's default of 4 -- also what the GPU box exports -- a
 		// 0.05 ms seed-search kernel waits behind other seams' DP kernels on a shared
 		// in-order queue (r03p at 3.1 Gbp: 29.4k -> 43.6k reads/s with 16 queues).
-		// Set before the first HIP call of the process; $BT2G_HW_QUEUES overrides.
+		// $BT2G_HW_QUEUES overrides, clamped to the runtime's 1..32.
 		const char* hq = getenv("BT2G_HW_QUEUES");
-		setenv("GPU_MAX_HW_QUEUES", hq && atoi(hq) > 0 ? hq : "16", 1);
+		int q = hq && atoi(hq) > 0 ? atoi(hq) : 16;
+		if(q > 32) q = 32;
+		char buf[16];
+		snprintf(buf, sizeof(buf), "%d", q);
+		setenv("GPU_MAX_HW_QUEUES", buf, 1);
+	}
+} g_env_init;
+
+// $BT2G_ADAPTER_STATS: where the call counts go (written on SIGTERM too).
+void init_env() {
+	static std::once_flag once;
+	std::call_once(once, [] {
 		const char* sp = getenv("BT2G_ADAPTER_STATS");
 		if(sp) {
 			strncpy(g_stats_path, sp, sizeof(g_stats_path) - 1);

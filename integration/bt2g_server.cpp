@@ -74,13 +74,20 @@ extern "C" bool bt2g_real__ZN27PatternSourceServiceFactory5alignEil(PatternSourc
                                                                    long data_size);
 
 bool PatternSourceServiceFactory::align(int fd, long data_size) {
-	unsigned int depth = n_readahead_;
-	if(const char* e = getenv("BT2G_READAHEAD")) {
-		if(atol(e) > 0) depth = (unsigned int)atol(e);
-	} else if(bt2gf::enabled() && bt2gf::count() > 0) {
-		const size_t n = bt2gf::count();
-		depth = (unsigned int)std::max(n / 4 + 1, std::min<size_t>(n + 1, 64));   // (few workers: all of them)
-	}
-	if(depth < n_readahead_) const_cast<unsigned int&>(n_readahead_) = depth;
+	// Set once, by the first connection, before it reads the member (the workers
+	// exist by then: the server accepts connections after spawning them).  The
+	// member is const in pat.h; it is read through `this` at every connection
+	// (pat.cpp's align), never folded: the one write here is what changes it.
+	static std::once_flag once;
+	std::call_once(once, [this] {
+		unsigned int depth = n_readahead_;
+		if(const char* e = getenv("BT2G_READAHEAD")) {
+			if(atol(e) > 0) depth = (unsigned int)atol(e);
+		} else if(bt2gf::enabled() && bt2gf::count() > 0) {
+			const size_t n = bt2gf::count();
+			depth = (unsigned int)std::max(n / 4 + 1, std::min<size_t>(n + 1, 64));   // (few workers: all of them)
+		}
+		if(depth < n_readahead_) const_cast<unsigned int&>(n_readahead_) = depth;
+	});
 	return bt2g_real__ZN27PatternSourceServiceFactory5alignEil(this, fd, data_size);
 }
