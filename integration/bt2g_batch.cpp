@@ -215,9 +215,32 @@ void write_stats() {
 	}
 }
 
+extern "C" void bt2g_alloc_stats_dump();   // bt2g_alloc.cpp ($BT2G_ALLOC_STATS)
+
+// $BT2G_EXIT_CLEAN=1: SIGTERM ends the process through exit() (atexit handlers
+// run: a profiler preloaded into the server writes its trace), from a thread
+// of its own rather than the signal handler.
+std::atomic<bool> g_term{false};
+bool exit_clean() {
+	static const bool on = [] { const char* e = getenv("BT2G_EXIT_CLEAN"); return e && *e == '1'; }();
+	return on;
+}
+
 void on_term(int) {
+	if(exit_clean()) {
+		g_term.store(true);
+		return;
+	}
 	write_stats();
+	bt2g_alloc_stats_dump();
 	_exit(0);
+}
+
+void term_watch() {
+	while(!g_term.load()) usleep(10000);
+	write_stats();
+	bt2g_alloc_stats_dump();
+	exit(0);
 }
 
 // A fault in a driver thread: its stack on stderr (the server's log), then die.
@@ -2885,6 +2908,10 @@ void Driver::run_loop() {
 		snprintf(nm, sizeof(nm), "bt2g-drv%d", tid);
 		pthread_setname_np(pthread_self(), nm);
 		bt2g_prof_thread(1);
+	}
+	if(exit_clean()) {
+		static std::once_flag once;
+		std::call_once(once, [] { std::thread(term_watch).detach(); });
 	}
 	std::thread(&Driver::feeder, this).detach();
 	for(;;) {

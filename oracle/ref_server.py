@@ -85,10 +85,12 @@ class Server:
     """One alignment server process on a free port (context manager)."""
 
     def __init__(self, index_base, threads=1, args=(), binary=SERVER, env=None, ready_timeout=600,
-                 log_path=None):
+                 log_path=None, prefix=()):
+        """`prefix`: a launcher put before the server's command line that runs the
+        server in its own process (rocprofv3 ... --)."""
         self.index_base = index_base
         self.port = free_port()
-        cmd = [binary, "-x", index_base, "-p", str(threads), "--server-port", str(self.port)] + list(args)
+        cmd = list(prefix) + [binary, "-x", index_base, "-p", str(threads), "--server-port", str(self.port)] + list(args)
         self.log_path = log_path or tempfile.mktemp(prefix="bt2srv_", suffix=".log")
         self._log = open(self.log_path, "wb")
         self.proc = subprocess.Popen(cmd, stdout=self._log, stderr=subprocess.STDOUT,

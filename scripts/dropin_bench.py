@@ -47,6 +47,8 @@ def main():
                          "change alignments, e.g. --dropin-args='--reads-per-batch 4')")
     ap.add_argument("--dropin-binary", default="", help="default oracle/_ref/bowtie2-align-server-gpu "
                                                        "(-stub: the binding over the CPU stand-in)")
+    ap.add_argument("--dropin-prefix", default="", help="a launcher before the drop-in's command line, one string "
+                    "(e.g. 'rocprofv3 --kernel-trace --stats -d DIR --'; the server gets BT2G_EXIT_CLEAN=1)")
     a = ap.parse_args()
 
     import bench
@@ -84,8 +86,11 @@ def main():
     for tag, binary, th in runs:
         stats = os.path.join(a.workdir, f"stats_{tag}.json")
         env = rs.dropin_env(base, stats)
+        prefix = a.dropin_prefix.split() if tag == "dropin" else []
+        if prefix:
+            env["BT2G_EXIT_CLEAN"] = "1"
         with rs.Server(base, threads=th, args=a.args + (a.dropin_args.split() if tag == "dropin" else []), binary=binary, env=env,
-                       log_path=os.path.join(a.workdir, f"server_{tag}.log")) as s:
+                       log_path=os.path.join(a.workdir, f"server_{tag}.log"), prefix=prefix) as s:
             log(f"{tag}: server ready in {s.load_s:.1f}s (-p {th})")
             dt, outs = s.run(chunks, k=a.k, warmup=chunks[:a.warmup_chunks])
         sams[tag] = rs.sorted_records(outs)

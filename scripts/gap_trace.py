@@ -43,6 +43,15 @@ def main():
     gaps.sort(reverse=True)
     idle = sum(g[0] for g in gaps) / 1e6
     print(f"kernels {len(kt)}  span {span:.1f} ms  idle {idle:.1f} ms in {len(gaps)} gaps")
+    # kernels by name: launches, total and mean duration; how many run at once
+    byk = {}
+    for s, e, name in kt:
+        v = byk.setdefault(name, [0, 0])
+        v[0] += 1
+        v[1] += e - s
+    print(f"sum of kernel durations {sum(v[1] for v in byk.values()) / 1e6:.1f} ms (busy {span - idle:.1f} ms)")
+    for name, (n, t) in sorted(byk.items(), key=lambda x: -x[1][1])[:20]:
+        print(f"  {t / 1e6:10.2f} ms  {n:8d} x {t / n / 1e3:9.1f} us  {name}")
     for g, a, b, nxt in gaps[:top]:
         print(f"gap {g/1e6:8.2f} ms at +{(a-t0)/1e6:9.2f} ms, next kernel {nxt}")
         ov = [(min(e, b) - max(s, a), f, tid, e - s) for s, e, f, tid in calls if s < b and e > a]

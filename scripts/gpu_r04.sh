@@ -29,6 +29,17 @@ batch)
     SKIP=--skip-stock
     python3 -c "import json,sys; d=json.load(open('$O/batch_p$p.json')); print($p, {k: d[k] for k in ('sam_identical','speedup') if k in d}, d['dropin']['rate'], d['dropin']['server_cpu_s'], d['dropin'].get('engine_calls'))"
   done ;;
+ktrace)
+  # kernel trace of the batch server (rocprofv3 in front of the server's command line; the server
+  # exits through exit() at SIGTERM so that the trace is written)
+  p=${3:-16}
+  timeout -k 10 900 python3 -u scripts/dropin_bench.py --genome-mb 3100 --reads ${4:-100000} --workdir /tmp/db \
+    --dropin-binary oracle/_ref/bowtie2-align-server-batch --gpu-workers $p --skip-stock \
+    --dropin-prefix "rocprofv3 --kernel-trace --stats --output-format csv -d $PWD/$O/ktrace -o run --" \
+    > $O/ktrace_p$p.json 2> $O/ktrace_p$p.log || { tail -30 $O/ktrace_p$p.log; tail -30 /tmp/db/server_dropin.log; exit 1; }
+  cp /tmp/db/server_dropin.log $O/server_ktrace.log
+  python3 scripts/gap_trace.py $O/ktrace 10 > $O/ktrace_gap.txt 2>&1; head -60 $O/ktrace_gap.txt
+  find $O/ktrace -name "*.csv" -size +40M -delete ;;
 tests)
   timeout -k 10 1000 python -u -m pytest tests -m gpu -x -v --timeout 600 --timeout-method thread > $O/gpu_tests.log 2>&1 || { tail -20 $O/gpu_tests.log; exit 1; }
   tail -2 $O/gpu_tests.log
