@@ -149,6 +149,14 @@ void dump(const char* path) {
 	rename(tmp.c_str(), path);
 }
 
+// $BT2G_SAMPLE_ALL=1: one process-wide CPU-time timer (ITIMER_PROF) instead of
+// per-thread ones -- every thread is sampled, the runtime's and the reference's
+// connection threads included (role 0 unless registered)
+bool sample_all() {
+	static const bool on = [] { const char* e = getenv("BT2G_SAMPLE_ALL"); return e && *e == '1'; }();
+	return on;
+}
+
 struct Sampler {
 	Sampler() {
 		const char* path = getenv("BT2G_SAMPLE");
@@ -178,6 +186,13 @@ struct Sampler {
 				}
 				fclose(f);
 			}
+		if(sample_all()) {
+			itimerval it;
+			it.it_interval.tv_sec = 0;
+			it.it_interval.tv_usec = 1000;
+			it.it_value = it.it_interval;
+			setitimer(ITIMER_PROF, &it, nullptr);
+		}
 		std::string p(path);
 		std::thread([p] {
 			for(int k = 0;; k++) {
@@ -200,6 +215,7 @@ struct Sampler {
 extern "C" void bt2g_prof_thread(int role) {
 	if(!g_pc) return;
 	t_role = (uint64_t)role & 0xF;
+	if(sample_all()) return;             // the process timer samples every thread
 	sigevent sev;
 	memset(&sev, 0, sizeof(sev));
 	sev.sigev_notify = SIGEV_THREAD_ID;
