@@ -32,6 +32,7 @@
 #include <stdint.h>
 #include <stdlib.h>
 #include <string.h>
+#include <sys/mman.h>
 
 #include <atomic>
 #include <new>
@@ -148,11 +149,38 @@ bool stats_on() {
 // calling thread's cache.  Blocks are never returned, so slabs never are.
 const size_t SLAB = (size_t)1 << 20;
 
+// Blocks of 1 MiB and up come from one reserved, never-committed address range
+// (MAP_NORESERVE; pages are backed when first touched): a malloc'd block that
+// big is a mapping of its own, and the batch driver's slots each hold one
+// (the reference's 20 MB alignment cache pool, ds.h Pool, mostly untouched) --
+// tens of thousands of slots would pass the kernel's limit on mappings
+// (vm.max_map_count, 65 530).  $BT2G_ARENA_GB sizes the range (default
+// 8192); when it cannot be reserved, or is used up, malloc as before.
+char* arena_take(size_t bytes) {
+	static const size_t cap = [] {
+		const char* e = getenv("BT2G_ARENA_GB");
+		const long gb = e ? atol(e) : 8192;
+		return gb > 0 ? (size_t)gb << 30 : (size_t)0;
+	}();
+	static char* const base = [] {
+		if(!cap) return (char*)nullptr;
+		void* m = mmap(nullptr, cap, PROT_READ | PROT_WRITE, MAP_PRIVATE | MAP_ANONYMOUS | MAP_NORESERVE, -1, 0);
+		return m == MAP_FAILED ? (char*)nullptr : (char*)m;
+	}();
+	static std::atomic<size_t> used{0};
+	if(!base) return nullptr;
+	bytes = (bytes + 4095) & ~(size_t)4095;
+	const size_t o = used.fetch_add(bytes, std::memory_order_relaxed);
+	if(o + bytes > cap) return nullptr;
+	return base + o;
+}
+
 void* fresh(int c) {
 	if(stats_on()) g_fresh[c].fetch_add(1, std::memory_order_relaxed);
 	const size_t bsz = HDR + size_of(c);
 	const size_t nb = size_of(c) < ((size_t)64 << 10) && !t_dead ? SLAB / bsz : 1;
-	char* p = (char*)malloc(bsz * nb);
+	char* p = size_of(c) >= ((size_t)1 << 20) ? arena_take(bsz) : nullptr;
+	if(!p) p = (char*)malloc(bsz * nb);
 	if(!p) return nullptr;
 	for(size_t i = 0; i < nb; i++) {
 		Hdr* h = (Hdr*)(p + i * bsz);

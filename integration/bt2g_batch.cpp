@@ -64,6 +64,7 @@
 #include <unistd.h>
 
 #include <algorithm>
+#include <array>
 #include <atomic>
 #include <chrono>
 #include <condition_variable>
@@ -642,6 +643,45 @@ struct Rq {
 	int m;         // mate
 };
 
+// ---- engine services -------------------------------------------------------------
+// The engine calls of a round, by kind.  With $BT2G_SERVICES (default on) each
+// kind has a thread of its own per device (a context and stream of its own):
+// the drivers hand it their requests of the round and wait; it takes whatever
+// every driver has pending, makes ONE call for all of it and returns the
+// results to the slots.  So a round's calls of the different kinds run at the
+// same time (a round waits for its slowest kind, not for their sum), and the
+// calls carry the requests of every driver (fewer, bigger launches, and one
+// stream per kind instead of one per driver and kind).  Off: a driver makes
+// its calls itself, one after another, on its own context.
+struct Driver;
+struct Svc {
+	int kind = 0;
+	bt2g_ctx* ctx = nullptr;
+	const bt2g_scoring* bsc = nullptr;
+	uint64_t stamp = 0;
+	// service thread: drivers with requests of this kind
+	std::mutex mu;
+	std::condition_variable cv;
+	std::vector<Driver*> pending;
+	void loop();
+	void run(std::vector<Rq>& v, std::vector<std::pair<Slot*, DpRes*>>& dp);
+	// the calls
+	void call_exact(std::vector<Rq>& v);
+	void call_1mm(std::vector<Rq>& v);
+	void call_seeds(std::vector<Rq>& v);
+	void call_ext(std::vector<Rq>& v);
+	void call_off(std::vector<Rq>& v);
+	void call_ug(std::vector<Rq>& v);
+	void call_dp(std::vector<std::pair<Slot*, DpRes*>>& v);
+	void run_dp(const std::vector<std::pair<Slot*, DpRes*>>& v, uint32_t cap, uint32_t maxaln);
+	uint32_t row_of(Pack& pk, Slot& s, int m);
+};
+
+bool services_on() {
+	static const bool on = [] { const char* e = getenv("BT2G_SERVICES"); return !(e && *e == '0'); }();
+	return on;
+}
+
 // ---- one driver thread --------------------------------------------------------
 struct Driver {
 	explicit Driver(int tid_) : tid(tid_), swcpu(nullptr), oswcpu(nullptr) {}
@@ -676,8 +716,14 @@ struct Driver {
 	// requests of this round
 	std::vector<Rq> rq[K_N];
 	std::vector<std::pair<Slot*, DpRes*>> rq_dp;
-	uint64_t stamp = 0;
 	size_t spec_k = 16;
+	// the engine calls: the device's services, or (services off) the driver's own
+	Svc* svc[K_N] = {};
+	Svc own;
+	std::mutex out_mu;
+	std::condition_variable out_cv;
+	int outstanding = 0;                 // kinds handed to services, not returned yet
+	void svc_done();
 
 	void feeder();
 	void run_loop();
@@ -687,17 +733,6 @@ struct Driver {
 	void setup_read(Slot& s);
 	void gpu_phase();
 	void prefetch_seeds(Slot& s, int mate);
-	uint32_t row_of(Pack& pk, Slot& s, int m);
-
-	// engine calls of a round
-	void call_exact();
-	void call_1mm();
-	void call_seeds();
-	void call_ext();
-	void call_off();
-	void call_ug();
-	void call_dp();
-	void run_dp(const std::vector<std::pair<Slot*, DpRes*>>& v, uint32_t cap, uint32_t maxaln);
 	void cpu_dp(Slot& s, DpRes& r, SwAligner& sw);
 
 	// helpers
@@ -710,7 +745,7 @@ struct Driver {
 	int ext(Slot& s) { return s.sd.paired ? s.sd.ext_step_paired(*this, s) : s.sd.ext_step(*this, s); }
 };
 
-uint32_t Driver::row_of(Pack& pk, Slot& s, int m) {
+uint32_t Svc::row_of(Pack& pk, Slot& s, int m) {
 	MateRes& x = s.mr[m];
 	if(x.row_stamp != stamp) {
 		x.row_stamp = stamp;
@@ -721,8 +756,7 @@ uint32_t Driver::row_of(Pack& pk, Slot& s, int m) {
 
 // ---- the engine calls of one round ---------------------------------------------
 // (grouped by each call's batch-wide arguments)
-void Driver::call_exact() {
-	std::vector<Rq>& v = rq[K_EXACT];
+void Svc::call_exact(std::vector<Rq>& v) {
 	if(v.empty()) return;
 	thread_local Pack pk;
 	thread_local std::vector<uint32_t> out;
@@ -750,8 +784,7 @@ void Driver::call_exact() {
 	g_req[K_EXACT] += v.size();
 }
 
-void Driver::call_1mm() {
-	std::vector<Rq>& v = rq[K_1MM];
+void Svc::call_1mm(std::vector<Rq>& v) {
 	if(v.empty()) return;
 	thread_local Pack pk;
 	thread_local std::vector<int32_t> ms, cnt;
@@ -781,7 +814,7 @@ void Driver::call_1mm() {
 			}
 			const uint64_t t0 = now_us();
 			int rc = bt2g_one_mm(ctx, pk.codes.data(), pk.quals.data(), pk.stride, pk.lens.data(), (uint32_t)n, ms.data(),
-			                     &bsc, nf, nr, cap, h.data(), cnt.data(), ops.data(), nullptr);
+			                     bsc, nf, nr, cap, h.data(), cnt.data(), ops.data(), nullptr);
 			g_call_us[K_1MM] += now_us() - t0;
 			g_calls[K_1MM]++;
 			if(rc && rc != BT2G_ERR_OVERFLOW) die("bt2g_one_mm", rc);
@@ -806,8 +839,7 @@ void Driver::call_1mm() {
 	g_req[K_1MM] += v.size();
 }
 
-void Driver::call_seeds() {
-	std::vector<Rq>& v = rq[K_SEEDS];
+void Svc::call_seeds(std::vector<Rq>& v) {
 	if(v.empty()) return;
 	thread_local Pack pk;
 	thread_local std::vector<uint32_t> out, ops;
@@ -852,8 +884,7 @@ void Driver::call_seeds() {
 	g_req[K_SEEDS] += v.size();
 }
 
-void Driver::call_ext() {
-	std::vector<Rq>& v = rq[K_EXT];
+void Svc::call_ext(std::vector<Rq>& v) {
 	if(v.empty()) return;
 	thread_local Pack pk;
 	thread_local std::vector<bt2g_ext_in> in;
@@ -884,8 +915,7 @@ void Driver::call_ext() {
 	g_req[K_EXT] += v.size();
 }
 
-void Driver::call_off() {
-	std::vector<Rq>& v = rq[K_OFF];
+void Svc::call_off(std::vector<Rq>& v) {
 	if(v.empty()) return;
 	thread_local std::vector<uint32_t> rows, offs;
 	rows.clear();
@@ -910,8 +940,7 @@ void Driver::call_off() {
 	g_req[K_OFF] += v.size();
 }
 
-void Driver::call_ug() {
-	std::vector<Rq>& v = rq[K_UG];
+void Svc::call_ug(std::vector<Rq>& v) {
 	if(v.empty()) return;
 	thread_local Pack pk;
 	thread_local std::vector<bt2g_ug_problem> P;
@@ -930,7 +959,7 @@ void Driver::call_ug() {
 	E.resize(v.size() * (size_t)maxedit);
 	const uint64_t t0 = now_us();
 	int rc = bt2g_ungapped(ctx, pk.codes.data(), pk.quals.data(), pk.stride, pk.lens.data(), P.data(), (uint32_t)v.size(),
-	                       &bsc, gReportOverhangs ? 1 : 0, maxedit, R.data(), E.data());
+	                       bsc, gReportOverhangs ? 1 : 0, maxedit, R.data(), E.data());
 	g_call_us[K_UG] += now_us() - t0;
 	g_calls[K_UG]++;
 	if(rc) die("bt2g_ungapped", rc);
@@ -946,7 +975,7 @@ void Driver::call_ug() {
 // (bt2g_sw_align_bt_packed).  A DP whose candidate list outgrew `cap`, or that
 // may have more than `maxaln` alignments, runs again alone with room for all;
 // one with more candidates than the engine takes goes to the CPU when used.
-void Driver::run_dp(const std::vector<std::pair<Slot*, DpRes*>>& v, uint32_t cap, uint32_t maxaln) {
+void Svc::run_dp(const std::vector<std::pair<Slot*, DpRes*>>& v, uint32_t cap, uint32_t maxaln) {
 	struct B {
 		Pack pk;
 		std::vector<bt2g_sw_problem> P;
@@ -991,7 +1020,7 @@ void Driver::run_dp(const std::vector<std::pair<Slot*, DpRes*>>& v, uint32_t cap
 	uint64_t tot[3] = {0, 0, 0};
 	const uint64_t t0 = now_us();
 	int rc = bt2g_sw_align_bt_packed(ctx, b.pk.codes.data(), b.pk.quals.data(), b.pk.stride, b.pk.lens.data(), b.P.data(),
-	                                 (uint32_t)n, nullptr, 0, b.RC.data(), &bsc, R_enable8 ? 1 : 0, cap, b.R.data(),
+	                                 (uint32_t)n, nullptr, 0, b.RC.data(), bsc, R_enable8 ? 1 : 0, cap, b.R.data(),
 	                                 maxaln, maxedit, b.NA.data(), b.A.data(), b.C.data(), b.F.data(), b.E.data(), tot);
 	g_call_us[K_DP] += now_us() - t0;
 	g_calls[K_DP]++;
@@ -1039,12 +1068,12 @@ void Driver::run_dp(const std::vector<std::pair<Slot*, DpRes*>>& v, uint32_t cap
 	if(!again.empty()) run_dp(again, cap2, maxaln2);
 }
 
-void Driver::call_dp() {
-	if(rq_dp.empty()) return;
-	g_req[K_DP] += rq_dp.size();
+void Svc::call_dp(std::vector<std::pair<Slot*, DpRes*>>& v) {
+	if(v.empty()) return;
+	g_req[K_DP] += v.size();
 	// long reads (> 1024 bases) batch apart: a batch is padded to its longest read
 	std::vector<std::pair<Slot*, DpRes*>> sh, lg;
-	for(auto& q : rq_dp) (q.first->rdlens[q.second->mate] > 1024 ? lg : sh).push_back(q);
+	for(auto& q : v) (q.first->rdlens[q.second->mate] > 1024 ? lg : sh).push_back(q);
 	const uint32_t cap = R_localAlign ? 2048 : 512;
 	if(!sh.empty()) run_dp(sh, cap, 8);
 	if(!lg.empty()) run_dp(lg, cap, 8);
@@ -2762,15 +2791,83 @@ void Driver::step_read(Slot& s) {
 	s.pc = P_FINISH;
 }
 
+void Svc::run(std::vector<Rq>& v, std::vector<std::pair<Slot*, DpRes*>>& dp) {
+	switch(kind) {
+	case K_EXACT: call_exact(v); break;
+	case K_1MM: call_1mm(v); break;
+	case K_SEEDS: call_seeds(v); break;
+	case K_EXT: call_ext(v); break;
+	case K_OFF: call_off(v); break;
+	case K_UG: call_ug(v); break;
+	case K_DP: call_dp(dp); break;
+	}
+}
+
+// A service thread: every driver's pending requests of its kind in one call.
+void Svc::loop() {
+	char nm[16];
+	snprintf(nm, sizeof(nm), "bt2g-svc%d", kind);
+	pthread_setname_np(pthread_self(), nm);
+	bt2g_prof_thread(4 + kind);
+	std::vector<Driver*> got;
+	std::vector<Rq> v;
+	std::vector<std::pair<Slot*, DpRes*>> dp;
+	for(;;) {
+		{
+			std::unique_lock<std::mutex> lk(mu);
+			cv.wait(lk, [this] { return !pending.empty(); });
+			got.swap(pending);
+		}
+		v.clear();
+		dp.clear();
+		for(Driver* d : got) {
+			if(kind == K_DP) dp.insert(dp.end(), d->rq_dp.begin(), d->rq_dp.end());
+			else v.insert(v.end(), d->rq[kind].begin(), d->rq[kind].end());
+		}
+		run(v, dp);
+		for(Driver* d : got) d->svc_done();
+		got.clear();
+	}
+}
+
+void Driver::svc_done() {
+	std::lock_guard<std::mutex> lk(out_mu);
+	if(--outstanding == 0) out_cv.notify_one();
+}
+
+// The device's services, started by its first driver.
+std::mutex g_svc_mu;
+std::vector<std::array<Svc*, K_N>> g_svcs;
+
 void Driver::gpu_phase() {
-	++stamp;
-	call_exact();
-	call_seeds();
-	call_1mm();
-	call_ext();
-	call_off();
-	call_ug();
-	call_dp();
+	std::vector<std::pair<Slot*, DpRes*>> none;
+	if(!services_on()) {
+		static const int order[K_N] = {K_EXACT, K_SEEDS, K_1MM, K_EXT, K_OFF, K_UG, K_DP};
+		for(int k : order) {
+			own.kind = k;
+			own.run(rq[k], rq_dp);
+		}
+	} else {
+		int n = 0;
+		for(int k = 0; k < K_N; k++) n += (k == K_DP ? !rq_dp.empty() : !rq[k].empty()) ? 1 : 0;
+		if(n) {
+			{
+				std::lock_guard<std::mutex> lk(out_mu);
+				outstanding = n;
+			}
+			for(int k = 0; k < K_N; k++) {
+				if(k == K_DP ? rq_dp.empty() : rq[k].empty()) continue;
+				Svc* v = svc[k];
+				{
+					std::lock_guard<std::mutex> lk(v->mu);
+					v->pending.push_back(this);
+				}
+				v->cv.notify_one();
+			}
+			std::unique_lock<std::mutex> lk(out_mu);
+			out_cv.wait(lk, [this] { return outstanding == 0; });
+		}
+	}
 	for(int k = 0; k < K_N; k++) rq[k].clear();
 	rq_dp.clear();
 }
@@ -2890,6 +2987,27 @@ void Driver::run_loop() {
 	ebwtBw = R_ebwtBw;
 	ref = R_refs;
 	bsc_ok = to_scoring(*sc, bsc);
+	own.ctx = ctx;
+	own.bsc = &bsc;
+	if(services_on()) {
+		const size_t dev = (size_t)tid % ndev;
+		std::lock_guard<std::mutex> lk(g_svc_mu);
+		if(g_svcs.size() < ndev) g_svcs.resize(ndev, std::array<Svc*, K_N>{});
+		if(!g_svcs[dev][0]) {
+			static bt2g_scoring s_bsc;              // (the same scoring for every driver)
+			s_bsc = bsc;
+			for(int k = 0; k < K_N; k++) {
+				Svc* v = new Svc();                 // lives as long as the server
+				v->kind = k;
+				v->bsc = &s_bsc;
+				int rc2 = bt2g_open_shared(g_bases[dev], &v->ctx);
+				if(rc2) die("bt2g_open_shared", rc2);
+				g_svcs[dev][k] = v;
+				std::thread(&Svc::loop, v).detach();
+			}
+		}
+		for(int k = 0; k < K_N; k++) svc[k] = g_svcs[dev][k];
+	}
 	rp.reset(new ReportingParams(R_allHits ? std::numeric_limits<THitInt>::max() : R_khits, R_mhits, 0, R_msample,
 	                             gReportDiscordant, gReportMixed));
 	mapq.reset(new_mapq(R_mapqv, R_scoreMin, *sc));

@@ -146,6 +146,14 @@ def test_batch_no_speculation_cpu(indexes, tmp_path):
     assert st["dp"][0] == 0
 
 
+def test_batch_no_services_cpu(indexes, tmp_path):
+    """BT2G_SERVICES=0: every driver makes its own engine calls, one kind after another."""
+    _need(rs.SERVER, rs.CLIENT, SRV_BATCH_STUB)
+    base, idx = indexes["synth"]
+    chunks = _reads(idx, 800, 13, str(tmp_path))
+    compare(SRV_BATCH_STUB, base, chunks, [], str(tmp_path), threads=3, env_extra={"BT2G_SERVICES": "0"})
+
+
 def test_batch_cpu_fallback_cpu(indexes, tmp_path):
     """-N 1 seeds (the engine's seed search is exact-only) and --ignore-quals (a
     mismatch model the engines do not implement): the driver runs the
