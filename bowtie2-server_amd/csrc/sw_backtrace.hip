@@ -43,6 +43,7 @@
 // stack, and tests/test_gpu_bt.py).
 #include <hip/hip_runtime.h>
 #include <stdint.h>
+#include <stdlib.h>
 #include "bt2g_kernels.h"
 
 namespace {
@@ -118,11 +119,19 @@ __device__ unsigned long long g_bt_wave_t0[1u << 16], g_bt_wave_t1[1u << 16];   
 #define BT2G_BT_EE_STEPS 0xffffffffu   // end-to-end: a whole walk per iteration (4, 8, 16: same 32 ms)
 #endif
 // LOCAL: the alignment mode, compile-time (each mode's kernel keeps only its
-// own filters and moves); FLAT: the loop shape, flat for local (see below)
-template <int KIND, bool LOCAL, bool FLAT = LOCAL>
+// own filters and moves); FLAT: the loop shape, flat for local (see below).
+// LDSRES (kind 2 only): a workgroup per problem -- its 64 lanes copy the
+// problem's decision plane into LDS and clear its reportedThrough tiles there,
+// then lane 0 walks with every plane and mark access in LDS.  A batch of a few
+// thousand DPs (the batch driver's rounds) is bound by the longest walk chain,
+// one dependent HBM load after another in the lane-per-problem kernel
+// (~3 ms per 400-DP call, r04d): LDS latency is an order of magnitude lower.
+// For big batches the lane-per-problem kernel keeps the throughput.
+template <int KIND, bool LOCAL, bool FLAT = LOCAL, bool LDSRES = false>
 __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(BT2G_BT_WAVES)))
 k_sw_bt(BtArgs A) {
-	const uint32_t p = blockIdx.x * 64u + threadIdx.x;
+	static_assert(!LDSRES || (KIND == 2 && !LOCAL), "LDS-resident walks: kind-2 planes only");
+	const uint32_t p = LDSRES ? blockIdx.x : blockIdx.x * 64u + threadIdx.x;
 	if(p >= A.nprob) return;
 #ifdef BT2G_BT_PROF
 	uint32_t pc[13] = {0};
@@ -138,8 +147,9 @@ k_sw_bt(BtArgs A) {
 	} flush_{pc};
 #endif
 	const bt2g_sw_result R = A.res[p];
-	if(!R.aligned || R.ncand <= 0) { A.naln[p] = 0; return; }
-	if((uint32_t)R.ncand > A.cap) { A.naln[p] = -5; return; }   // truncated list: not the reference's
+	const bool writer = !LDSRES || threadIdx.x == 0;
+	if(!R.aligned || R.ncand <= 0) { if(writer) A.naln[p] = 0; return; }
+	if((uint32_t)R.ncand > A.cap) { if(writer) A.naln[p] = -5; return; }   // truncated list: not the reference's
 	const bt2g_sw_problem P = A.probs[p];
 	const uint32_t nrow = A.lens[P.read], ncol = P.ncol;
 	constexpr bool local = LOCAL;
@@ -152,7 +162,7 @@ k_sw_bt(BtArgs A) {
 	uint32_t pad = 0;
 	const uint8_t* slot = nullptr;
 	{
-		if(KIND == 0 && variant != 0) { A.naln[p] = -4; return; }   // i16 fill, u8-only plane
+		if(KIND == 0 && variant != 0) { if(writer) A.naln[p] = -4; return; }   // i16 fill, u8-only plane
 		const size_t es = KIND == 1 ? 2 : 1;   // kind 2: the u8 plane's layout, 8 B per block column
 		// systolic end-to-end: last row at the stack bottom; one-problem-per-lane
 		// fills: top-aligned; systolic local: padded rows (round16) at the bottom
@@ -239,6 +249,20 @@ k_sw_bt(BtArgs A) {
 	// (Valid bits in LDS instead: measured slower.)
 	uint32_t* marks = A.marks + (size_t)p * A.mslot;
 	const uint32_t tcols = A.rwords, trows = A.rrows, vw = (tcols + 31u) / 32u;
+	if constexpr(LDSRES) {
+		// the plane's 16-row blocks (8 B per block column) and the marks, in LDS
+		extern __shared__ uint4 s_res[];
+		const uint32_t n16 = (A.cstride >> 4) * A.pcols * 8u / 16u;
+		const uint4* src = (const uint4*)slot;
+		for(uint32_t i = threadIdx.x; i < n16; i += 64u) s_res[i] = src[i];
+		uint32_t* lm = (uint32_t*)(s_res + n16);
+		for(uint32_t i = threadIdx.x; i < trows * vw; i += 64u) lm[(size_t)trows * tcols * 2u + i] = 0u;
+		__syncthreads();
+		if(threadIdx.x != 0) return;
+		slot = (const uint8_t*)s_res;
+		pl.base = slot;
+		marks = lm;
+	}
 	uint32_t* valid = marks + (size_t)trows * tcols * 2u;
 	for(uint32_t i = 0; i < trows * vw; i++) valid[i] = 0u;
 	uint32_t ttr = 0xffffffffu, ttc = 0;
@@ -848,8 +872,32 @@ extern "C" int bt2g_bt_prof_read(unsigned long long* out) {
 }
 #endif
 
+// LDS bytes of an LDS-resident walk (k_sw_bt<2, false, false, true>): the
+// plane's blocks and the reportedThrough tiles with their valid words
+static uint32_t bt_lds_bytes(const BtArgs& a) {
+	const uint64_t plane = (uint64_t)(a.cstride >> 4) * a.pcols * 8u;
+	const uint64_t marks = ((uint64_t)a.rrows * a.rwords * 2u + (uint64_t)a.rrows * ((a.rwords + 31u) / 32u)) * 4u;
+	const uint64_t n = plane + marks;
+	return n > 0xffffffffull ? 0xffffffffu : (uint32_t)n;
+}
+
+// batches up to $BT2G_BT_LDS_MAX problems (default 8192; 0: never) walk
+// LDS-resident when a problem's plane and marks fit in 64 KB
+// (read at every launch: the parity tests run one batch both ways)
+static uint32_t bt_lds_max() {
+	const char* e = getenv("BT2G_BT_LDS_MAX");
+	return e ? (uint32_t)atol(e) : 8192u;
+}
+
 void launch_sw_bt(int kind, const BtArgs& a, hipStream_t st) {
 	if(a.nprob == 0) return;
+	if(kind == 2 && !a.local && !a.queue && a.nprob <= bt_lds_max()) {
+		const uint32_t lds = bt_lds_bytes(a);
+		if(lds <= 65536u) {
+			hipLaunchKernelGGL((k_sw_bt<2, false, false, true>), dim3(a.nprob), dim3(64), lds, st, a);
+			return;
+		}
+	}
 	const dim3 grid((a.nprob + 63u) / 64u), block(64);
 	if(a.local) {
 		// local fills leave a u16 plane

@@ -193,6 +193,10 @@ const char* const K_NAMES[K_N] = {"exact_sweep", "one_mm", "seed_search", "exten
 std::atomic<uint64_t> g_req[K_N], g_calls[K_N], g_call_us[K_N], g_cpu[K_N];
 std::atomic<uint64_t> g_reads{0}, g_rounds{0}, g_round_us{0}, g_cpu_us{0}, g_gpu_us{0};
 std::atomic<uint64_t> g_dp_spec{0}, g_dp_used{0}, g_dp_reuse{0}, g_dp_miss{0};
+// rounds per read: total and a histogram (bin b: [2^b, 2^(b+1)))
+std::atomic<uint64_t> g_steps{0}, g_steps_hist[16];
+// reads in flight summed over rounds; drivers' time with no read in flight
+std::atomic<uint64_t> g_inflight{0}, g_idle_us{0};
 char g_stats_path[4096];
 
 void write_stats() {
@@ -208,7 +212,12 @@ void write_stats() {
 		n += snprintf(buf + n, sizeof(buf) - n, ", \"%s\": [%llu, %llu, %llu, %.1f]", K_NAMES[k],
 		              (unsigned long long)g_req[k].load(), (unsigned long long)g_cpu[k].load(),
 		              (unsigned long long)g_calls[k].load(), g_call_us[k].load() / 1000.0);
-	n += snprintf(buf + n, sizeof(buf) - n, "}\n");
+	n += snprintf(buf + n, sizeof(buf) - n, ", \"inflight_sum\": %llu, \"idle_ms\": %.1f",
+	              (unsigned long long)g_inflight.load(), g_idle_us.load() / 1000.0);
+	n += snprintf(buf + n, sizeof(buf) - n, ", \"steps\": %llu, \"steps_hist\": [", (unsigned long long)g_steps.load());
+	for(int b = 0; b < 16; b++)
+		n += snprintf(buf + n, sizeof(buf) - n, "%s%llu", b ? ", " : "", (unsigned long long)g_steps_hist[b].load());
+	n += snprintf(buf + n, sizeof(buf) - n, "]}\n");
 	FILE* f = fopen(g_stats_path, "w");
 	if(f) {
 		fwrite(buf, 1, (size_t)n, f);
@@ -575,6 +584,7 @@ struct Slot {
 
 	// multiseedSearchWorker's per-read locals (bt2_search.cpp:3283-3451, 3814-3823)
 	int pc = P_START;
+	uint32_t nsteps = 0;         // rounds this read was stepped in
 	size_t rdlens[2] = {0, 0};
 	TAlScore minsc[2] = {0, 0};
 	bool nfilt[2] = {true, true}, scfilt[2] = {true, true}, lenfilt[2] = {true, true}, qcfilt[2] = {true, true};
@@ -2878,7 +2888,10 @@ void Driver::feeder() {
 	for(;;) {
 		{
 			std::unique_lock<std::mutex> lk(in_mu);
-			room_cv.wait(lk, [this] { return inbox.size() < 4 && active_a.load() < max_slots; });
+			// (buffers hold <= 16 reads, pat.cpp:2023): the slots fill up to max_slots --
+			// not a few buffers per round, which held a driver's intake to ~64 reads a
+			// round (r04c: ~250 reads in flight per driver against 2048 slots)
+			room_cv.wait(lk, [this] { return active_a.load() + 16 * inbox.size() < max_slots; });
 		}
 		ReadElement re = R_factory->nextReadPair();      // blocks until a connection has reads
 		Elem* e = new Elem(re);
@@ -2942,6 +2955,7 @@ void Driver::admit(Elem* e) {
 		s->msink = &ps->msink();
 		s->conn = e->conn;
 		s->pc = P_START;
+		s->nsteps = 0;
 		n++;
 		active++;
 		run.push_back(s);
@@ -2969,12 +2983,17 @@ void Driver::admit(Elem* e) {
 }
 
 void Driver::release(Slot* s) {
+	g_steps += s->nsteps;
+	{
+		int b = 0;
+		while(b < 15 && (2u << b) <= s->nsteps) b++;
+		g_steps_hist[b]++;
+	}
 	active--;
 	freel.push_back(s);
 	if(((++g_reads) & 0xffff) == 0) write_stats();
 	conn_done(s->conn, 1);
 	s->conn = nullptr;
-	if(active_a.exchange(active) >= max_slots && active < max_slots) room_cv.notify_one();
 }
 
 void Driver::run_loop() {
@@ -3036,20 +3055,28 @@ void Driver::run_loop() {
 		std::deque<Elem*> got;
 		{
 			std::unique_lock<std::mutex> lk(in_mu);
-			if(active == 0) in_cv.wait(lk, [this] { return !inbox.empty(); });
+			if(active == 0 && inbox.empty()) {
+				const uint64_t ti = now_us();
+				in_cv.wait(lk, [this] { return !inbox.empty(); });
+				g_idle_us += now_us() - ti;
+			}
 			got.swap(inbox);
 		}
 		for(Elem* e : got) admit(e);
 		if(!got.empty()) room_cv.notify_one();
 		const uint64_t t0 = now_us();
+		g_inflight += run.size();
 		bt2g_prof_role(3);
 		for(size_t k = 0; k < run.size(); k++) {
 			Slot* s = run[k];
+			s->nsteps++;
 			step_read(*s);
 			if(s->pc == P_FINISH) release(s);
 			else next.push_back(s);
 		}
 		run.clear();
+		active_a.store(active);
+		room_cv.notify_one();
 		const uint64_t t1 = now_us();
 		bt2g_prof_role(1);
 		gpu_phase();

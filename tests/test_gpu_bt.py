@@ -225,3 +225,23 @@ def test_bt_long_reads_vs_oracle(eng, local):
         ea, ee, ef = _oracle_expect(orc, gen, codes, quals, probs, rects, local)
         check_against(naln, alns, edits, fates, res, None, ea, ee, ef, f"long{L}")
         assert (naln > 0).sum() > 8
+
+
+def test_bt_lds_resident_equals_lane_kernel(eng, monkeypatch):
+    """Batches up to BT2G_BT_LDS_MAX problems walk LDS-resident (a workgroup per
+    problem, sw_backtrace.hip LDSRES); BT2G_BT_LDS_MAX=0 forces the lane-per-problem
+    kernel.  Both give the same alignments, edits and fates on the same batch."""
+    gen = get_index("lambda").ref_codes[0]
+    codes, quals, lens, probs, rects = _synth_problems(gen, 900, 53)
+    outs = []
+    for lim in ("8192", "0"):
+        monkeypatch.setenv("BT2G_BT_LDS_MAX", lim)
+        outs.append(eng.sw_align_bt(codes, quals, lens, probs, rects=rects, cap=1024, maxaln=64, maxedit=512))
+    a, b = outs
+    for x, y in zip(a, b):
+        if x.dtype.names:
+            for f in x.dtype.names:
+                assert np.array_equal(x[f], y[f]), f
+        else:
+            assert np.array_equal(x, y)
+    assert (a[2] > 0).sum() > 600
