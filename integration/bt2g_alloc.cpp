@@ -32,6 +32,7 @@
 #include <stdint.h>
 #include <stdlib.h>
 #include <string.h>
+#include <sched.h>
 #include <sys/mman.h>
 
 #include <atomic>
@@ -91,7 +92,12 @@ bool enabled() {
 struct Spin {
 	std::atomic_flag f = ATOMIC_FLAG_INIT;
 	void lock() {
-		while(f.test_and_set(std::memory_order_acquire)) __builtin_ia32_pause();
+		// (yields after a while: with more threads than cores the holder may be
+		// descheduled -- r04f: 16 drivers + 7 engine services on a 16-CPU quota)
+		for(int k = 0; f.test_and_set(std::memory_order_acquire); k++) {
+			if(k < 64) __builtin_ia32_pause();
+			else sched_yield();
+		}
 	}
 	void unlock() { f.clear(std::memory_order_release); }
 };
@@ -156,30 +162,54 @@ const size_t SLAB = (size_t)1 << 20;
 // tens of thousands of slots would pass the kernel's limit on mappings
 // (vm.max_map_count, 65 530).  $BT2G_ARENA_GB sizes the range (default
 // 8192); when it cannot be reserved, or is used up, malloc as before.
-char* arena_take(size_t bytes) {
-	static const size_t cap = [] {
-		const char* e = getenv("BT2G_ARENA_GB");
-		const long gb = e ? atol(e) : 8192;
-		return gb > 0 ? (size_t)gb << 30 : (size_t)0;
-	}();
-	static char* const base = [] {
-		if(!cap) return (char*)nullptr;
+// The small classes' 1 MiB slabs come from a second such range, with
+// transparent huge pages asked for (MADV_HUGEPAGE: a slab's blocks are all
+// initialised at once, 256 page faults a slab otherwise -- and a slab from
+// malloc was an mmap of its own: r04f, 45 k mappings and half the drivers'
+// CPU in the allocator while their slots were first filled).  The big blocks'
+// range keeps small pages: the 20 MB pools are mostly never touched.
+struct Range {
+	char* base = nullptr;
+	size_t cap = 0;
+	std::atomic<size_t> used{0};
+	Range(size_t gb, bool huge) {
+		cap = gb << 30;
+		if(!cap) return;
 		void* m = mmap(nullptr, cap, PROT_READ | PROT_WRITE, MAP_PRIVATE | MAP_ANONYMOUS | MAP_NORESERVE, -1, 0);
-		return m == MAP_FAILED ? (char*)nullptr : (char*)m;
-	}();
-	static std::atomic<size_t> used{0};
-	if(!base) return nullptr;
-	bytes = (bytes + 4095) & ~(size_t)4095;
-	const size_t o = used.fetch_add(bytes, std::memory_order_relaxed);
-	if(o + bytes > cap) return nullptr;
-	return base + o;
+		if(m == MAP_FAILED) return;
+		base = (char*)m;
+		if(huge) (void)madvise(base, cap, MADV_HUGEPAGE);
+	}
+	char* take(size_t bytes) {
+		if(!base) return nullptr;
+		bytes = (bytes + 4095) & ~(size_t)4095;
+		const size_t o = used.fetch_add(bytes, std::memory_order_relaxed);
+		if(o + bytes > cap) return nullptr;
+		return base + o;
+	}
+};
+
+size_t arena_gb() {
+	const char* e = getenv("BT2G_ARENA_GB");
+	const long gb = e ? atol(e) : 8192;
+	return gb > 0 ? (size_t)gb : 0;
+}
+
+char* arena_take(size_t bytes) {
+	static Range* r = new (malloc(sizeof(Range))) Range(arena_gb(), false);
+	return r->take(bytes);
+}
+
+char* slab_take(size_t bytes) {
+	static Range* r = new (malloc(sizeof(Range))) Range(arena_gb() ? 1024 : 0, true);
+	return r->take(bytes);
 }
 
 void* fresh(int c) {
 	if(stats_on()) g_fresh[c].fetch_add(1, std::memory_order_relaxed);
 	const size_t bsz = HDR + size_of(c);
 	const size_t nb = size_of(c) < ((size_t)64 << 10) && !t_dead ? SLAB / bsz : 1;
-	char* p = size_of(c) >= ((size_t)1 << 20) ? arena_take(bsz) : nullptr;
+	char* p = size_of(c) >= ((size_t)1 << 20) ? arena_take(bsz) : nb > 1 ? slab_take(bsz * nb) : nullptr;
 	if(!p) p = (char*)malloc(bsz * nb);
 	if(!p) return nullptr;
 	for(size_t i = 0; i < nb; i++) {

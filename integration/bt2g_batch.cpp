@@ -196,7 +196,7 @@ std::atomic<uint64_t> g_dp_spec{0}, g_dp_used{0}, g_dp_reuse{0}, g_dp_miss{0};
 // rounds per read: total and a histogram (bin b: [2^b, 2^(b+1)))
 std::atomic<uint64_t> g_steps{0}, g_steps_hist[16];
 // reads in flight summed over rounds; drivers' time with no read in flight
-std::atomic<uint64_t> g_inflight{0}, g_idle_us{0};
+std::atomic<uint64_t> g_inflight{0}, g_idle_us{0}, g_slots{0};
 char g_stats_path[4096];
 
 void write_stats() {
@@ -212,8 +212,8 @@ void write_stats() {
 		n += snprintf(buf + n, sizeof(buf) - n, ", \"%s\": [%llu, %llu, %llu, %.1f]", K_NAMES[k],
 		              (unsigned long long)g_req[k].load(), (unsigned long long)g_cpu[k].load(),
 		              (unsigned long long)g_calls[k].load(), g_call_us[k].load() / 1000.0);
-	n += snprintf(buf + n, sizeof(buf) - n, ", \"inflight_sum\": %llu, \"idle_ms\": %.1f",
-	              (unsigned long long)g_inflight.load(), g_idle_us.load() / 1000.0);
+	n += snprintf(buf + n, sizeof(buf) - n, ", \"inflight_sum\": %llu, \"idle_ms\": %.1f, \"slots\": %llu",
+	              (unsigned long long)g_inflight.load(), g_idle_us.load() / 1000.0, (unsigned long long)g_slots.load());
 	n += snprintf(buf + n, sizeof(buf) - n, ", \"steps\": %llu, \"steps_hist\": [", (unsigned long long)g_steps.load());
 	for(int b = 0; b < 16; b++)
 		n += snprintf(buf + n, sizeof(buf) - n, "%s%llu", b ? ", " : "", (unsigned long long)g_steps_hist[b].load());
@@ -2943,6 +2943,7 @@ void Driver::admit(Elem* e) {
 		Slot* s;
 		if(freel.empty()) {
 			all.emplace_back(new Slot(*rp, *mapq, (size_t)tid));
+			g_slots++;
 			s = all.back().get();
 		} else {
 			s = freel.back();
