@@ -199,9 +199,11 @@ std::atomic<uint64_t> g_steps{0}, g_steps_hist[16];
 std::atomic<uint64_t> g_inflight{0}, g_idle_us{0}, g_slots{0};
 char g_stats_path[4096];
 
+int svc_stats(char* buf, size_t cap);   // the services' kernel times and work (below)
+
 void write_stats() {
 	if(!g_stats_path[0]) return;
-	char buf[4096];
+	char buf[8192];
 	int n = snprintf(buf, sizeof(buf), "{\"driver\": \"batch\", \"reads\": %llu, \"rounds\": %llu, \"round_ms\": %.1f, "
 	                 "\"cpu_ms\": %.1f, \"gpu_ms\": %.1f, \"dp\": [%llu, %llu, %llu, %llu]",
 	                 (unsigned long long)g_reads.load(), (unsigned long long)g_rounds.load(),
@@ -217,7 +219,9 @@ void write_stats() {
 	n += snprintf(buf + n, sizeof(buf) - n, ", \"steps\": %llu, \"steps_hist\": [", (unsigned long long)g_steps.load());
 	for(int b = 0; b < 16; b++)
 		n += snprintf(buf + n, sizeof(buf) - n, "%s%llu", b ? ", " : "", (unsigned long long)g_steps_hist[b].load());
-	n += snprintf(buf + n, sizeof(buf) - n, "]}\n");
+	n += snprintf(buf + n, sizeof(buf) - n, "]");
+	n += svc_stats(buf + n, sizeof(buf) - n);
+	n += snprintf(buf + n, sizeof(buf) - n, "}\n");
 	FILE* f = fopen(g_stats_path, "w");
 	if(f) {
 		fwrite(buf, 1, (size_t)n, f);
@@ -669,10 +673,22 @@ struct Svc {
 	bt2g_ctx* ctx = nullptr;
 	const bt2g_scoring* bsc = nullptr;
 	uint64_t stamp = 0;
-	// service thread: drivers with requests of this kind
+	// the kind's queue (its first worker's): drivers with requests of this kind;
+	// the kind's workers ($BT2G_SVC_WORKERS, DP $BT2G_DP_WORKERS) each take what is
+	// pending when they are free, on contexts of their own
+	Svc* q = this;
+	std::vector<Svc*> workers;
 	std::mutex mu;
 	std::condition_variable cv;
 	std::vector<Driver*> pending;
+	// $BT2G_KPROF=1: the engine's per-launch kernel times (HIP events on the
+	// context's stream, bt2g_set_profiling) by kernel id, cumulative; and the
+	// algorithmic work of the calls -- FM kinds: bytes (64 B per occurrence-table
+	// side gathered + the read bytes walked, bench.py's figures), DP: cells
+	std::mutex st_mu;
+	uint64_t k_launch[8] = {};
+	double k_ms[8] = {};
+	std::atomic<uint64_t> work{0}, items{0};
 	void loop();
 	void run(std::vector<Rq>& v, std::vector<std::pair<Slot*, DpRes*>>& dp);
 	// the calls
@@ -686,6 +702,13 @@ struct Svc {
 	void run_dp(const std::vector<std::pair<Slot*, DpRes*>>& v, uint32_t cap, uint32_t maxaln);
 	uint32_t row_of(Pack& pk, Slot& s, int m);
 };
+
+std::atomic<uint64_t> g_stamp{0};
+
+bool kprof_on() {
+	static const bool on = [] { const char* e = getenv("BT2G_KPROF"); return e && *e == '1'; }();
+	return on;
+}
 
 bool services_on() {
 	static const bool on = [] { const char* e = getenv("BT2G_SERVICES"); return !(e && *e == '0'); }();
@@ -789,7 +812,13 @@ void Svc::call_exact(std::vector<Rq>& v) {
 		g_call_us[K_EXACT] += now_us() - t0;
 		g_calls[K_EXACT]++;
 		if(rc) die("bt2g_exact_sweep", rc);
-		for(size_t i = 0; i < sub.size(); i++) memcpy(sub[i].s->mr[sub[i].m].sweep, &out[8 * i], 8 * sizeof(uint32_t));
+		uint64_t w = 0;
+		for(size_t i = 0; i < sub.size(); i++) {
+			memcpy(sub[i].s->mr[sub[i].m].sweep, &out[8 * i], 8 * sizeof(uint32_t));
+			w += 64ull * out[8 * i + 7] + 2ull * pk.lens[i];
+		}
+		work += w;
+		items += sub.size();
 	}
 	g_req[K_EXACT] += v.size();
 }
@@ -800,6 +829,7 @@ void Svc::call_1mm(std::vector<Rq>& v) {
 	thread_local std::vector<int32_t> ms, cnt;
 	thread_local std::vector<uint32_t> ops;
 	thread_local std::vector<bt2g_mm1> h;
+	thread_local std::vector<uint32_t> ld;
 	for(int g = 0; g < 4; g++) {
 		const int nf = (g >> 1) & 1, nr = g & 1;
 		std::vector<Rq> sub;
@@ -823,8 +853,15 @@ void Svc::call_1mm(std::vector<Rq>& v) {
 				ms[i] = sub[i].s->mr[sub[i].m].mm_minsc;
 			}
 			const uint64_t t0 = now_us();
+			ld.resize(n);
 			int rc = bt2g_one_mm(ctx, pk.codes.data(), pk.quals.data(), pk.stride, pk.lens.data(), (uint32_t)n, ms.data(),
-			                     bsc, nf, nr, cap, h.data(), cnt.data(), ops.data(), nullptr);
+			                     bsc, nf, nr, cap, h.data(), cnt.data(), ops.data(), kprof_on() ? ld.data() : nullptr);
+			if(kprof_on()) {
+				uint64_t w = 0;
+				for(size_t i = 0; i < n; i++) w += 64ull * ld[i] + 4ull * pk.lens[i];
+				work += w;
+				items += n;
+			}
 			g_call_us[K_1MM] += now_us() - t0;
 			g_calls[K_1MM]++;
 			if(rc && rc != BT2G_ERR_OVERFLOW) die("bt2g_one_mm", rc);
@@ -852,7 +889,7 @@ void Svc::call_1mm(std::vector<Rq>& v) {
 void Svc::call_seeds(std::vector<Rq>& v) {
 	if(v.empty()) return;
 	thread_local Pack pk;
-	thread_local std::vector<uint32_t> out, ops;
+	thread_local std::vector<uint32_t> out, ops, ld;
 	thread_local std::vector<int32_t> ns;
 	std::vector<bool> taken(v.size(), false);
 	for(size_t a = 0; a < v.size(); a++) {
@@ -875,8 +912,15 @@ void Svc::call_seeds(std::vector<Rq>& v) {
 		ops.resize(n);
 		ns.resize(n);
 		const uint64_t t0 = now_us();
+		ld.resize(n);
 		int rc = bt2g_seed_search(ctx, pk.codes.data(), pk.stride, pk.lens.data(), (uint32_t)n, x0.sd_L, x0.sd_per,
-		                          x0.sd_off, maxs, out.data(), ns.data(), ops.data(), nullptr);
+		                          x0.sd_off, maxs, out.data(), ns.data(), ops.data(), kprof_on() ? ld.data() : nullptr);
+		if(kprof_on()) {
+			uint64_t w = 0;
+			for(size_t i = 0; i < n; i++) w += 64ull * ld[i] + (uint64_t)std::max(ns[i], 0) * 2u * (x0.sd_L + 12u);
+			work += w;
+			items += n;
+		}
 		g_call_us[K_SEEDS] += now_us() - t0;
 		g_calls[K_SEEDS]++;
 		if(rc) die("bt2g_seed_search", rc);
@@ -927,12 +971,19 @@ void Svc::call_ext(std::vector<Rq>& v) {
 
 void Svc::call_off(std::vector<Rq>& v) {
 	if(v.empty()) return;
-	thread_local std::vector<uint32_t> rows, offs;
+	thread_local std::vector<uint32_t> rows, offs, ld;
 	rows.clear();
 	for(const Rq& q : v) rows.insert(rows.end(), q.s->off_rows.begin(), q.s->off_rows.end());
 	offs.resize(rows.size());
 	const uint64_t t0 = now_us();
-	int rc = bt2g_get_offset(ctx, rows.data(), (uint32_t)rows.size(), offs.data(), nullptr);
+	ld.resize(rows.size());
+	int rc = bt2g_get_offset(ctx, rows.data(), (uint32_t)rows.size(), offs.data(), kprof_on() ? ld.data() : nullptr);
+	if(kprof_on()) {
+		uint64_t w = 0;
+		for(uint32_t x : ld) w += 64ull * x + 12u;
+		work += w;
+		items += rows.size();
+	}
 	g_call_us[K_OFF] += now_us() - t0;
 	g_calls[K_OFF]++;
 	if(rc) die("bt2g_get_offset", rc);
@@ -1001,7 +1052,7 @@ void Svc::run_dp(const std::vector<std::pair<Slot*, DpRes*>>& v, uint32_t cap, u
 	uint32_t stride = 1;
 	for(auto& q : v) stride = std::max<uint32_t>(stride, (uint32_t)q.first->rdlens[q.second->mate]);
 	b.pk.reset(stride);
-	++stamp;
+	stamp = g_stamp.fetch_add(1) + 1;   // (unique over the kind's workers: a slot's rows are per call)
 	const size_t n = v.size();
 	b.P.resize(n);
 	b.RC.resize(n);
@@ -1017,6 +1068,12 @@ void Svc::run_dp(const std::vector<std::pair<Slot*, DpRes*>>& v, uint32_t cap, u
 		p.ncol = r.ncol;
 		p.minsc = r.minsc;
 		b.RC[i] = r.rect;
+	}
+	if(kprof_on()) {
+		uint64_t cells = 0;
+		for(size_t i = 0; i < n; i++) cells += (uint64_t)b.pk.lens[b.P[i].read] * b.P[i].ncol;
+		work += cells;
+		items += n;
 	}
 	const uint32_t maxedit = 2 * stride + 8;
 	b.R.resize(n);
@@ -2824,9 +2881,9 @@ void Svc::loop() {
 	std::vector<std::pair<Slot*, DpRes*>> dp;
 	for(;;) {
 		{
-			std::unique_lock<std::mutex> lk(mu);
-			cv.wait(lk, [this] { return !pending.empty(); });
-			got.swap(pending);
+			std::unique_lock<std::mutex> lk(q->mu);
+			q->cv.wait(lk, [this] { return !q->pending.empty(); });
+			got.swap(q->pending);
 		}
 		v.clear();
 		dp.clear();
@@ -2835,6 +2892,10 @@ void Svc::loop() {
 			else v.insert(v.end(), d->rq[kind].begin(), d->rq[kind].end());
 		}
 		run(v, dp);
+		if(kprof_on()) {
+			std::lock_guard<std::mutex> lk(st_mu);
+			for(int k = 0; k < 8; k++) (void)bt2g_kernel_stats(ctx, k, &k_launch[k], &k_ms[k]);
+		}
 		for(Driver* d : got) d->svc_done();
 		got.clear();
 	}
@@ -2848,6 +2909,33 @@ void Driver::svc_done() {
 // The device's services, started by its first driver.
 std::mutex g_svc_mu;
 std::vector<std::array<Svc*, K_N>> g_svcs;
+
+// "kernels": {kind: [[launches, ms] of kernel ids 0..7], work, items} summed over devices
+int svc_stats(char* buf, size_t cap) {
+	if(!kprof_on()) return 0;
+	std::lock_guard<std::mutex> lk(g_svc_mu);
+	int n = snprintf(buf, cap, ", \"kernels\": {");
+	for(int k = 0; k < K_N; k++) {
+		uint64_t L[8] = {}, W = 0, I = 0;
+		double M[8] = {};
+		for(auto& dv : g_svcs) {
+			if(!dv[k]) continue;
+			for(Svc* v : dv[k]->workers) {
+				std::lock_guard<std::mutex> l2(v->st_mu);
+				for(int i = 0; i < 8; i++) { L[i] += v->k_launch[i]; M[i] += v->k_ms[i]; }
+				W += v->work.load();
+				I += v->items.load();
+			}
+		}
+		n += snprintf(buf + n, cap - n, "%s\"%s\": {\"work\": %llu, \"items\": %llu, \"ids\": [", k ? ", " : "",
+		              K_NAMES[k], (unsigned long long)W, (unsigned long long)I);
+		for(int i = 0; i < 8; i++)
+			n += snprintf(buf + n, cap - n, "%s[%llu, %.3f]", i ? ", " : "", (unsigned long long)L[i], M[i]);
+		n += snprintf(buf + n, cap - n, "]}");
+	}
+	n += snprintf(buf + n, cap - n, "}");
+	return n;
+}
 
 void Driver::gpu_phase() {
 	std::vector<std::pair<Slot*, DpRes*>> none;
@@ -3016,14 +3104,23 @@ void Driver::run_loop() {
 		if(!g_svcs[dev][0]) {
 			static bt2g_scoring s_bsc;              // (the same scoring for every driver)
 			s_bsc = bsc;
+			const int nw = std::max(1, (int)env_or("BT2G_SVC_WORKERS", 2));
+			const int nd = std::max(1, (int)env_or("BT2G_DP_WORKERS", 3));
 			for(int k = 0; k < K_N; k++) {
-				Svc* v = new Svc();                 // lives as long as the server
-				v->kind = k;
-				v->bsc = &s_bsc;
-				int rc2 = bt2g_open_shared(g_bases[dev], &v->ctx);
-				if(rc2) die("bt2g_open_shared", rc2);
-				g_svcs[dev][k] = v;
-				std::thread(&Svc::loop, v).detach();
+				Svc* owner = nullptr;
+				for(int w = 0; w < (k == K_DP ? nd : nw); w++) {
+					Svc* v = new Svc();             // lives as long as the server
+					v->kind = k;
+					v->bsc = &s_bsc;
+					int rc2 = bt2g_open_shared(g_bases[dev], &v->ctx);
+					if(rc2) die("bt2g_open_shared", rc2);
+					if(kprof_on()) (void)bt2g_set_profiling(v->ctx, 1);
+					if(!owner) owner = v;
+					v->q = owner;
+					owner->workers.push_back(v);
+				}
+				g_svcs[dev][k] = owner;
+				for(Svc* v : owner->workers) std::thread(&Svc::loop, v).detach();
 			}
 		}
 		for(int k = 0; k < K_N; k++) svc[k] = g_svcs[dev][k];
