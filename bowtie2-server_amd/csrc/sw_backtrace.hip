@@ -251,7 +251,7 @@ k_sw_bt(BtArgs A) {
 	const uint32_t tcols = A.rwords, trows = A.rrows, vw = (tcols + 31u) / 32u;
 	if constexpr(LDSRES) {
 		// the plane's 16-row blocks (8 B per block column) and the marks, in LDS
-		extern __shared__ uint4 s_res[];
+		HIP_DYNAMIC_SHARED(uint4, s_res)
 		const uint32_t n16 = (A.cstride >> 4) * A.pcols * 8u / 16u;
 		const uint4* src = (const uint4*)slot;
 		for(uint32_t i = threadIdx.x; i < n16; i += 64u) s_res[i] = src[i];
@@ -892,6 +892,16 @@ static uint32_t bt_lds_max() {
 void launch_sw_bt(int kind, const BtArgs& a, hipStream_t st) {
 	if(a.nprob == 0) return;
 	if(kind == 2 && !a.local && !a.queue && a.nprob <= bt_lds_max()) {
+		// $BT2G_BT_WG=0: the LDS-resident one-walker kernel instead of the
+		// parallel-candidate one (sw_backtrace_wg.hip)
+		const char* e = getenv("BT2G_BT_WG");
+		if(!(e && *e == '0')) {
+			const uint32_t lw = sw_bt_wg_lds(a);
+			if(lw <= 65536u) {
+				launch_sw_bt_wg(a, lw, st);
+				return;
+			}
+		}
 		const uint32_t lds = bt_lds_bytes(a);
 		if(lds <= 65536u) {
 			hipLaunchKernelGGL((k_sw_bt<2, false, false, true>), dim3(a.nprob), dim3(64), lds, st, a);

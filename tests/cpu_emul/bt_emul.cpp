@@ -8,6 +8,9 @@
 #include <stdlib.h>
 
 thread_local uint3v threadIdx, blockIdx;
+// the workgroup kernel (sw_backtrace_wg.hip) runs in tests/cpu_emul/wg_emul.cpp
+uint32_t sw_bt_wg_lds(const BtArgs&) { return 0xffffffffu; }
+void launch_sw_bt_wg(const BtArgs&, uint32_t, hipStream_t) { abort(); }
 #ifdef BT2G_BT_COUNT
 unsigned long long bt_counts[16];
 extern "C" unsigned long long* bt_emul_counts() { return bt_counts; }
@@ -37,6 +40,7 @@ extern "C" int bt_emul_run(int kind, const bt2g_sw_problem* probs, uint32_t npro
 	uint32_t queue = 0;
 	const char* st = getenv("BT_EMUL_STATIC");
 	a.queue = st && *st == '1' ? nullptr : &queue;
+	setenv("BT2G_BT_LDS_MAX", "0", 1);          // lane-per-problem kernels only (one lane at a time here)
 	launch_sw_bt(kind, a, nullptr);
 	return 0;
 }

@@ -42,3 +42,7 @@ inline int __ffsll(unsigned long long x) { return __builtin_ffsll((long long)x);
 inline int __popcll(unsigned long long x) { return __builtin_popcountll(x); }
 inline int __shfl(int v, int) { return v; }
 inline uint32_t atomicAdd(uint32_t* a, uint32_t v) { const uint32_t o = *a; *a += v; return o; }
+// (the LDS-resident variants need a whole workgroup: never launched here,
+// bt_emul.cpp sets BT2G_BT_LDS_MAX=0; they only have to compile)
+inline void __syncthreads() {}
+#define HIP_DYNAMIC_SHARED(type, var) static type var[1];

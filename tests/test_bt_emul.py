@@ -84,9 +84,54 @@ def decision_nibbles(h, e, f, rd, q33, rf, sc):
                                       ("log_loc", 1), ("rand_loc", 2), ("log_loc", 2), ("rand_ee", 3),
                                       ("log_ee", 3)])
 def test_bt_kernel_source_on_cpu(lib, src, kind):
+    x = _inputs(src, kind)
+    lib.bt_emul_run(C.c_int({0: 0, 1: 1, 2: 1, 3: 2}[kind]), _p(x["probs"]), C.c_uint32(x["n"]), _p(x["reads"]),
+                    _p(x["quals"]), C.c_uint32(x["stride"]), _p(x["lens"]), _p(x["rf"]), _p(x["rects"]),
+                    _p(x["res"]), _p(x["cands"]), C.c_uint32(x["cap"]), _p(x["plane"]), C.c_uint64(x["slot"]),
+                    C.c_uint32(x["S16"]), C.c_int(x["plane_top"]), C.c_uint32(x["maxrow"]), C.c_uint32(x["maxcol"]),
+                    C.byref(swconst(x["local"])), C.c_int(int(x["local"])), C.c_double(0.0), C.c_double(0.15),
+                    C.c_uint32(x["maxaln"]), C.c_uint32(x["maxedit"]), _p(x["naln"]), _p(x["alns"]), _p(x["edits"]),
+                    _p(x["fates"]))
+    _check(x, src, kind)
+
+
+WG_SRC = [os.path.join(EMUL, "wg_emul.cpp"), os.path.join(ROOT, "bowtie2-server_amd", "csrc", "sw_backtrace_wg.hip"),
+          os.path.join(ROOT, "bowtie2-server_amd", "csrc", "bt2g_kernels.h"),
+          os.path.join(EMUL, "stub_wg", "hip", "hip_runtime.h")]
+WG_LIB = os.path.join(EMUL, "libwg_emul.so")
+
+
+@pytest.fixture(scope="module")
+def wglib():
+    if not os.path.exists(CLANG):
+        pytest.skip("clang++ missing")
+    if not os.path.exists(WG_LIB) or os.path.getmtime(WG_LIB) < max(os.path.getmtime(s) for s in WG_SRC):
+        subprocess.check_call([CLANG, "-O1", "-g", "-std=c++17", "-fPIC", "-shared", "-Wno-unknown-attributes",
+                               "-pthread", "-I", os.path.join(EMUL, "stub_wg"), "-I", os.path.join(ROOT, "include"),
+                               WG_SRC[0], "-o", WG_LIB])
+    return C.CDLL(WG_LIB)
+
+
+@pytest.mark.parametrize("src,maxaln", [("rand_ee", 256), ("log_ee", 256), ("log_ee", 2)])
+def test_bt_wg_kernel_source_on_cpu(wglib, src, maxaln):
+    """sw_backtrace_wg.hip (a workgroup per DP, candidates walked in parallel, the
+    reportedThrough resolution by the wave) run as 64 host threads per workgroup:
+    every alignment, edit and candidate fate equals the reference's (maxaln 2:
+    the loop's stop after the second alignment)."""
+    x = _inputs(src, 3, maxaln=maxaln)
+    x["n"] = min(x["n"], 120)           # (64 host threads per workgroup: a subset keeps the CPU suite short)
+    wglib.wg_emul_run(_p(x["probs"]), C.c_uint32(x["n"]), _p(x["reads"]), _p(x["quals"]), C.c_uint32(x["stride"]),
+                      _p(x["lens"]), _p(x["rf"]), _p(x["rects"]), _p(x["res"]), _p(x["cands"]), C.c_uint32(x["cap"]),
+                      _p(x["plane"]), C.c_uint64(x["slot"]), C.c_uint32(x["S16"]), C.c_uint32(x["maxcol"]),
+                      C.byref(swconst(False)), C.c_double(0.0), C.c_double(0.15), C.c_uint32(x["maxaln"]),
+                      C.c_uint32(x["maxedit"]), _p(x["naln"]), _p(x["alns"]), _p(x["edits"]), _p(x["fates"]))
+    _check(x, src, 3, maxaln=maxaln)
+
+
+def _inputs(src, kind, maxaln=None):
     import bt2g
     from oracle.oracle import Oracle
-    from test_oracle_golden import bt_expected, sw_problems
+    from test_oracle_golden import sw_problems
     orc = Oracle()
     g, b = load_golden("sw_" + src), load_golden("sw_bt_" + src)
     local = bool(g["local"])
@@ -181,23 +226,33 @@ def test_bt_kernel_source_on_cpu(lib, src, kind):
                     masks.astype(np.uint16).view(np.uint8)
     rects = np.zeros(n, bt2g.SWRECT_DTYPE)
     rects["triml"], rects["corel"], rects["corer"] = b["triml"], b["corel"], b["corer"]
-    maxaln, maxedit = 4096 if local else 256, 512
+    if maxaln is None:
+        maxaln = 4096 if local else 256
+    maxedit = 512
     naln = np.zeros(n, np.int32)
     alns = np.zeros((n, maxaln), bt2g.SWALN_DTYPE)
     edits = np.zeros((n, maxaln, maxedit), bt2g.EDIT_DTYPE)
     fates = np.zeros((n, cap), np.int8)
     lens = np.ascontiguousarray(g["lens"], np.uint32)
-    lib.bt_emul_run(C.c_int({0: 0, 1: 1, 2: 1, 3: 2}[kind]), _p(probs), C.c_uint32(n), _p(g["reads"]), _p(g["quals"]), C.c_uint32(stride),
-                    _p(lens), _p(g["rf"]), _p(rects), _p(res), _p(cands), C.c_uint32(cap), _p(plane),
-                    C.c_uint64(slot), C.c_uint32(S16), C.c_int(plane_top), C.c_uint32(maxrow), C.c_uint32(maxcol),
-                    C.byref(swconst(local)), C.c_int(int(local)), C.c_double(0.0), C.c_double(0.15),
-                    C.c_uint32(maxaln), C.c_uint32(maxedit), _p(naln), _p(alns), _p(edits), _p(fates))
+    return dict(probs=probs, n=n, reads=g["reads"], quals=g["quals"], stride=stride, lens=lens, rf=g["rf"],
+                rects=rects, res=res, cands=cands, cap=cap, plane=plane, slot=slot, S16=S16, plane_top=plane_top,
+                maxrow=maxrow, maxcol=maxcol, local=local, maxaln=maxaln, maxedit=maxedit, naln=naln, alns=alns,
+                edits=edits, fates=fates, keep=keep, b=b)
+
+
+def _check(x, src, kind, maxaln=None):
+    from test_oracle_golden import bt_expected
+    n, keep, naln, alns, edits, fates, b = (x[k] for k in ("n", "keep", "naln", "alns", "edits", "fates", "b"))
     nal = 0
     for p in range(n):
         if not keep[p]:
             assert naln[p] == -4
             continue
         ea, eeds, efates = bt_expected(b, p)
+        if maxaln is not None and len(ea) > maxaln:
+            # the loop stops at maxaln: the first maxaln alignments, the fates up to the last of them
+            last = int(ea[maxaln - 1, 0])
+            ea, eeds, efates = ea[:maxaln], eeds[:maxaln], efates[:last + 1]
         assert naln[p] == len(ea), (src, kind, p)
         for k in range(len(ea)):
             got = alns[p, k]
@@ -208,4 +263,4 @@ def test_bt_kernel_source_on_cpu(lib, src, kind):
         if len(efates):
             assert np.array_equal(fates[p, :len(efates)], efates), (src, kind, p)
         nal += len(ea)
-    assert nal > 40
+    assert nal > (8 if maxaln is not None else 40)
