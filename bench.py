@@ -504,17 +504,166 @@ def pmc_traffic(fetch_csv, write_csv, kernel):
     return total
 
 
-def real_schedule(cpu):
-    """The north-star rate: the reference server bound to the
-    engines (integration/, the drop-in) on the reference's own schedule, through
-    its own client, SAM compared with the stock server's on the same reads."""
-    if not cpu or "dropin_server" not in cpu or "reference_server" not in cpu \
-            or "value" not in cpu.get("reference_server", {}):
-        return None
-    d, r = cpu["dropin_server"], cpu["reference_server"]
-    return {"dropin_value": d["value"], "stock_value": r["value"], "unit": d["unit"],
-            "vs_stock": d["value"] / r["value"], "sam_identical": d.get("sam_identical_to_reference"),
-            "stock_cores": r.get("cores"), "sample": r.get("sample")}
+BATCH_SERVER = os.path.join(ROOT, "oracle", "_ref", "bowtie2-align-server-batch")
+# the engine services' kernel ids (bt2g_api.cpp ProfScope) by call kind, and the
+# kernels' names in the line
+SERVER_KERNELS = [("exact_sweep", 0, "k_exact_sweep", "hbm"), ("seed_search", 1, "k_seed_search", "hbm"),
+                  ("one_mm", 2, "k_one_mm (items/q/near/far/branch/compact)", "hbm"),
+                  ("get_offset", 3, "k_get_offset", "hbm"), ("extend", 3, "k_extend", None),
+                  ("ungapped", 6, "k_ungapped", None), ("sw_dp", 4, "k_sw_sys (fill + candidate gather)", "valu"),
+                  ("sw_dp", 5, "k_sw_bt_wg / k_sw_bt (nextAlignment loop)", None)]
+
+
+def policy_args(mode, preset):
+    """Server options of a bench mode (BASELINE.json configs)."""
+    a = ["--local"] if mode == "local" else []
+    if preset == "very-sensitive":
+        a.append("--very-sensitive-local" if mode == "local" else "--very-sensitive")
+    return a
+
+
+def count_aligned(sam_texts, paired):
+    """Reads (pairs) with an alignment in SAM text: primary records (no 0x100 /
+    0x800) without 0x4; a pair counts when either mate aligned (its first
+    mate's record: 0x4 or 0x8 clear)."""
+    n = 0
+    for t in sam_texts:
+        for ln in t.split(b"\n"):
+            if not ln or ln[:1] == b"@":
+                continue
+            a = ln.index(b"\t")
+            flag = int(ln[a + 1:ln.index(b"\t", a + 1)])
+            if flag & 0x900:
+                continue
+            if paired:
+                if flag & 0x40 and (flag & 0xC) != 0xC:
+                    n += 1
+            elif not flag & 0x4:
+                n += 1
+    return n
+
+
+def server_kernels(st):
+    """Kernel times and algorithmic work of a batch-server run (its BT2G_KPROF
+    stats: per engine service, the HIP-event time of every launch and the work
+    of its calls).  FM kernels: bytes = 64 B per occurrence-table side gathered
+    + the read bytes walked (SURVEY.md 8(d), the figures of the chain below);
+    the SW fill: SW_OPS_PER_CELL integer ops per DP cell."""
+    out = {}
+    ks = (st or {}).get("kernels") or {}
+    for kind, kid, name, bound in SERVER_KERNELS:
+        k = ks.get(kind)
+        if not k:
+            continue
+        launches, ms = k["ids"][kid]
+        if not launches:
+            continue
+        e = {"kernel": name, "launches": launches, "ms_total": ms, "ms_per_launch": ms / launches,
+             "items": k["items"]}
+        if bound == "hbm" and k["work"]:
+            e.update(bound="hbm", bytes_total=k["work"], achieved=k["work"] / (ms / 1e3) / 1e9, unit="GB/s",
+                     peak=HBM_PEAK_GBS)
+        elif bound == "valu" and k["work"]:
+            e.update(bound="valu", cells_total=k["work"], achieved=k["work"] * SW_OPS_PER_CELL / (ms / 1e3) / 1e12,
+                     unit="T int-ops/s", peak=VALU_PEAK_TOPS, ops_per_cell=SW_OPS_PER_CELL)
+        if "achieved" in e:
+            e["frac"] = e["achieved"] / e["peak"]
+        out[f"{kind}:{kid}"] = e
+    return out
+
+
+def schedule_run(args, rank, world, local, base, reads_np, quals_np, workdir, binary=None):
+    """The north-star number: the reference's real schedule -- its server,
+    client, per-read logic and SAM -- with the batch-first driver
+    (integration/bt2g_batch.cpp) on this rank's GPU.  The reads go out in
+    <= 10 000-read client connections, args.clients at a time (BASELINE.md
+    section 3; the same k as the stock server below).  Warmup: the first
+    args.warmup_chunks chunks, args.warmup times (the server's slots and
+    caches reach their working size); then args.steps timed passes over every
+    chunk, bracketed by barriers across ranks.  Returns the timing, the
+    aligned count (from the SAM), the last pass's SAM texts and the server's
+    engine statistics."""
+    import torch
+    import torch.distributed as dist
+    from oracle import ref_server as rs
+    binary = binary or BATCH_SERVER
+    if not os.path.exists(binary):
+        raise RuntimeError(f"{binary} is not built (python -c 'import __graft_entry__ as g; g.build()')")
+    gpu = torch.cuda.is_available()
+    paired = args.mode == "paired"
+    n = args.reads
+    if paired:
+        chunks = rs.write_fastq_chunks(workdir, reads_np[:n], quals_np[:n], codes2=reads_np[n:], quals2=quals_np[n:])
+    else:
+        chunks = rs.write_fastq_chunks(workdir, reads_np, quals_np)
+    stats = os.path.join(workdir, "stats.json")
+    env = rs.dropin_env(base, stats, device=local)
+    env["BT2G_KPROF"] = "1"
+    multi = world > 1 and dist.is_initialized()
+    with rs.Server(base, threads=args.drivers, args=policy_args(args.mode, args.preset), binary=binary,
+                   env=env, log_path=os.path.join(workdir, "server.log")) as srv:
+        log(f"[rank {rank}] batch server ready in {srv.load_s:.1f}s (-p {args.drivers})")
+        for _ in range(args.warmup):
+            srv.run(chunks[:max(1, args.warmup_chunks)], k=args.clients)
+        if multi:
+            dist.barrier()
+        if gpu:
+            torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        aligned, outs, cpu_s = 0, None, 0.0
+        for _ in range(args.steps):
+            _, outs = srv.run(chunks, k=args.clients)
+            cpu_s += srv.last_cpu_s
+            aligned += count_aligned(outs, paired)
+        if gpu:
+            torch.cuda.synchronize()
+        if multi:
+            dist.barrier()
+        elapsed = time.perf_counter() - t0
+        threads_cpu = srv.last_threads
+        rss = srv.last_rss_gb
+    st = None
+    for _ in range(50):                         # written by the server at SIGTERM
+        if os.path.exists(stats):
+            try:
+                st = json.load(open(stats))
+                break
+            except ValueError:
+                pass
+        time.sleep(0.1)
+    return {"elapsed": elapsed, "aligned": aligned, "outs": outs, "chunks": chunks, "stats": st,
+            "server_cpu_s": cpu_s, "server_threads_cpu": threads_cpu, "server_rss_gb": rss}
+
+
+def stock_baseline(args, base, chunks, batch_outs, workdir):
+    """cpu_baseline: the stock reference server (oracle/_ref/bowtie2-align-server-s,
+    built from /root/reference by oracle/ref/Makefile, -p <usable cores>) on
+    the first args.stock_sample reads of the same chunks, same k and warmup;
+    its sorted SAM against the batch server's for those chunks."""
+    from oracle import ref_server as rs
+    host = rs.host_cpus()
+    threads = args.cpu_threads or host["usable"]
+    m = max(1, min(len(chunks), (args.stock_sample + rs.CHUNK - 1) // rs.CHUNK))
+    sample = chunks[:m]
+    paired = args.mode == "paired"
+    with rs.Server(base, threads=threads, args=policy_args(args.mode, args.preset), binary=rs.SERVER,
+                   log_path=os.path.join(workdir, "server_stock.log")) as srv:
+        for _ in range(args.warmup):
+            srv.run(sample[:max(1, min(args.warmup_chunks, m))], k=args.clients)
+        dt, outs = srv.run(sample, k=args.clients)
+        cpu_s = srv.last_cpu_s
+    a, b = rs.sorted_records(outs), rs.sorted_records(batch_outs[:m])
+    differ = sum(1 for x, y in zip(a, b) if x != y) + abs(len(a) - len(b))
+    nreads = min(args.reads, m * rs.CHUNK)
+    unit = "read pairs/s" if paired else "reads/s"
+    return {"value": count_aligned(outs, paired) / dt, "unit": "aligned " + unit, "cores": threads,
+            "kind": "reference", "host": host, "reads_per_s": nreads / dt, "seconds": dt, "server_cpu_s": cpu_s,
+            "sample": f"the stock reference server (bowtie2-align-server-s built from the reference's sources, "
+                      f"-p {threads} = the usable cores of this host, {host['model']}) on the first {nreads} "
+                      f"{'pairs' if paired else 'reads'} of the batch, <= 10 000 per client connection, "
+                      f"{args.clients} connections at a time, after {args.warmup} warmup pass(es) over "
+                      f"{min(args.warmup_chunks, m)} chunk(s)"}, \
+        {"sample_reads": nreads, "records": len(a), "records_differing": differ, "identical": differ == 0}
 
 
 def combine_ranks(elapsed, n_aligned, dev, eng=None):
@@ -653,49 +802,6 @@ def cpu_baseline(idx, reads, quals, pipe, sample, threads, base=None):
     chain.close()
     ref["index_base"] = base
     return dt, ref, mate, secs
-
-
-def server_baseline(base, reads, quals, pol, sample, threads, workers, args_srv, log_dir, dropin_binary=None,
-                    dropin_args=()):
-    """The north-star comparison on the reference's real schedule (BASELINE.md
-    section 3): the stock reference server (oracle/_ref/bowtie2-align-server-s,
-    -p <usable cores>) and the same server with its seams bound to the engines
-    (integration/bt2g_seams.cpp -> oracle/_ref/bowtie2-align-server-gpu, -p
-    <workers>) on the same `sample` reads (pairs) and index, driven by the
-    reference's own client in <= 10 000-read connections, 8 at a time; sorted
-    SAM compared record by record.  `dropin_args`: server options of the
-    drop-in only that change no alignment (--reads-per-batch: a worker aligns
-    its batch's reads one after another)."""
-    from oracle import ref_server as rs
-    n = sample
-    if pol.paired:
-        P = len(reads) // 2
-        chunks = rs.write_fastq_chunks(log_dir, reads[:n], quals[:n], codes2=reads[P:P + n], quals2=quals[P:P + n])
-    else:
-        chunks = rs.write_fastq_chunks(log_dir, reads[:n], quals[:n])
-    out, sams = {}, {}
-    for tag, binary, th in (("stock", rs.SERVER, threads),
-                            ("dropin", dropin_binary or os.path.join(rs.REF_DIR, "bowtie2-align-server-gpu"),
-                             workers)):
-        stats = os.path.join(log_dir, f"stats_{tag}.json")
-        env = rs.dropin_env(base, stats)
-        with rs.Server(base, threads=th, args=list(args_srv) + (list(dropin_args) if tag == "dropin" else []),
-                       binary=binary, env=env,
-                       log_path=os.path.join(log_dir, f"server_{tag}.log")) as srv:
-            dt, outs = srv.run(chunks, k=8, warmup=chunks[:4])   # (the drop-in sizes its caches and staging first)
-        sams[tag] = rs.sorted_records(outs)
-        out[tag] = {"rate": n / dt, "seconds": dt, "threads": th, "records": len(sams[tag]),
-                    "server_args": list(args_srv) + (list(dropin_args) if tag == "dropin" else []),
-                    "server_cpu_s": srv.last_cpu_s, "server_cores_busy": srv.last_cpu_s / dt}
-        time.sleep(0.5)
-        if os.path.exists(stats):
-            import json as _j
-            out[tag]["engine_calls"] = _j.load(open(stats))
-    a, b = sams["stock"], sams["dropin"]
-    out["sam_identical"] = a == b
-    out["sam_records_differing"] = sum(1 for x, y in zip(a, b) if x != y) + abs(len(a) - len(b))
-    out["dropin_vs_stock"] = out["dropin"]["rate"] / out["stock"]["rate"]
-    return out
 
 
 def gpu_chain(pipe, ids):
@@ -868,9 +974,18 @@ def workload(args):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=3)
-    ap.add_argument("--warmup", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=1, help="timed passes of the batch server over every read")
+    ap.add_argument("--warmup", type=int, default=1, help="untimed passes over the first --warmup-chunks chunks")
     ap.add_argument("--reads", type=int, default=1_000_000, help="reads (paired: read pairs) per GPU per step")
+    ap.add_argument("--drivers", type=int, default=16, help="batch server driver threads (-p)")
+    ap.add_argument("--clients", type=int, default=32, help="concurrent client connections (both servers)")
+    ap.add_argument("--warmup-chunks", type=int, default=8)
+    ap.add_argument("--stock-sample", type=int, default=200_000,
+                    help="reads (pairs) timed through the stock server for cpu_baseline and SAM parity (0: skip)")
+    ap.add_argument("--chain-steps", type=int, default=2, help="timed steps of the kernel chain (0: skip it)")
+    ap.add_argument("--chain-warmup", type=int, default=1)
+    ap.add_argument("--chain-cpu-baseline", action="store_true",
+                    help="also time the reference's own chain on the host (oracle/ref_chain.py) for the kernel chain")
     ap.add_argument("--read-len", type=int, default=150)
     ap.add_argument("--mode", choices=("ee", "local", "paired"), default="ee",
                     help="ee: BASELINE configs[1] (--end-to-end --sensitive); local: configs[3] (--local); "
@@ -881,15 +996,10 @@ def main():
     ap.add_argument("--genome-mb", type=float, default=3100.0,
                     help="synthetic genome size (default: hg38's 3.1 Gbp; the index is built on the GPU, ~160 s)")
     ap.add_argument("--genome-model", choices=("hg38like", "simple"), default="hg38like")
-    ap.add_argument("--cpu-sample", type=int, default=1_000_000)
+    ap.add_argument("--cpu-sample", type=int, default=200_000, help="reads of the chain's CPU baseline")
     ap.add_argument("--cpu-threads", type=int, default=0, help="0: the usable cores of the host (cgroup quota / "
                                                                    "affinity)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--server-sample", type=int, default=200_000,
-                    help="reads (pairs) timed through the stock reference server and the drop-in server (0: skip)")
-    ap.add_argument("--server-workers", type=int, default=4096, help="drop-in server workers (-p; fibers)")
-    ap.add_argument("--server-dropin-args", default="--reads-per-batch 4",
-                    help="drop-in server options that change no alignment (one string)")
     ap.add_argument("--index-cache", default="auto",
                     help="reuse/write the built index at this base path ('auto': under $TMPDIR keyed by the "
                          "genome model and size; '': always build)")
@@ -920,12 +1030,19 @@ def main():
         import tempfile
         cache = os.path.join(tempfile.gettempdir(), "bt2g_bench_index",
                              f"{args.genome_model}_{args.genome_mb:g}mb", "g")
-    if cache and os.path.exists(cache + ".rev.2.bt2"):
+    if not cache:
+        import tempfile
+        cache = os.path.join(tempfile.mkdtemp(prefix="bt2g_bench_index_"), "g")   # (the servers read it from disk)
+    if world > 1 and not os.path.exists(cache + ".rev.2.bt2"):
+        # rank 0 builds and writes the index; the others read it
+        if rank != 0:
+            dist.barrier()
+    if os.path.exists(cache + ".rev.2.bt2"):
         idx = bi.read_index(cache)                  # same seed -> same genome -> same index
         log(f"[rank {rank}] index read from {cache}")
     else:
         idx = bi.build_index_device(parts, names=names, device=str(dev))
-        if cache and rank == 0:
+        if rank == 0:
             # written beside, then renamed into place: a reader never sees half an index
             import shutil
             d = os.path.dirname(cache)
@@ -936,25 +1053,123 @@ def main():
                 shutil.rmtree(d, ignore_errors=True)
             os.makedirs(os.path.dirname(d), exist_ok=True)
             os.rename(tmpd, d)
+        if world > 1:
+            dist.barrier()
     torch.cuda.synchronize()
     log(f"[rank {rank}] index built on GPU in {time.time()-t1:.1f}s")
     torch.cuda.empty_cache()
-    eng = bt2g.Engine(index=idx, device=local)
-    if world > 1:
-        comm_setup(eng, rank, world)
-    info = eng.info()
     t2 = time.time()
     if args.mode == "paired":
         reads_np, quals_np = make_pairs(parts, args.reads, args.read_len, seed=shard_seed(rank))
     else:
         reads_np, quals_np = make_reads(parts, args.reads, args.read_len, seed=shard_seed(rank))
-    log(f"[rank {rank}] {args.reads} reads in {time.time()-t2:.1f}s; index resident: {info[12]/1e9:.2f} GB")
+    log(f"[rank {rank}] {args.reads} reads in {time.time()-t2:.1f}s")
+
+    # ---- the north-star number: the reference's real schedule on the batch server ----
+    import tempfile
+    wd = tempfile.mkdtemp(prefix=f"bt2g_sched_r{rank}_")
+    sched = schedule_run(args, rank, world, local, cache, reads_np, quals_np, wd)
+    elapsed, n_aligned = combine_ranks(sched["elapsed"], sched["aligned"], dev)
+    value = n_aligned / elapsed
+    total_reads = args.reads * args.steps * world
+    log(f"[rank {rank}] real schedule: {sched['aligned']} aligned of {args.reads * args.steps} in "
+        f"{sched['elapsed']:.2f}s; whole job {value:.0f} aligned/s")
+    kern = server_kernels(sched["stats"])
+    dom_k = max((k for k in kern if "achieved" in kern[k]), key=lambda k: kern[k]["ms_total"], default=None)
+    cpu, sam = None, None
+    if rank == 0 and world == 1 and args.stock_sample and not args.no_cpu_baseline:
+        try:
+            cpu, sam = stock_baseline(args, cache, sched["chunks"], sched["outs"], wd)
+            log(f"[rank 0] stock server {cpu['value']:.0f} {cpu['unit']} on {cpu['cores']} cores; SAM {sam}")
+        except Exception as e:        # a checker: its failure must not hide the measurement
+            import traceback
+            traceback.print_exc()
+            cpu = {"error": repr(e)[:500]}
+    sched["outs"] = None
+    chain = None
+    if args.chain_steps > 0:
+        chain = run_chain(args, rank, world, local, dev, idx, cache, reads_np, quals_np)
+    if rank == 0:
+        unit = "read pairs/s" if args.mode == "paired" else "reads/s"
+        st = sched["stats"] or {}
+        rl = None
+        if dom_k:
+            d = kern[dom_k]
+            rl = {"bound": d["bound"], "kernel": d["kernel"], "achieved": d["achieved"], "peak": d["peak"],
+                  "unit": d["unit"], "frac": d["frac"], "traffic": None,
+                  "ms_per_launch": d["ms_per_launch"], "launches": d["launches"],
+                  "per_launch_work": (d.get("bytes_total") or d.get("cells_total")) / d["launches"],
+                  "work_unit": "bytes" if d["bound"] == "hbm" else "DP cells",
+                  "note": "kernel times: HIP events around every launch of the batch server's engine services "
+                          "over warmup + timed passes (BT2G_KPROF); per-launch work: the algorithmic figure of "
+                          "SURVEY.md 8(d) for the requests of each call.  Latency-bound here: the batch "
+                          "server's calls carry a round's requests (hundreds to a few thousand items); the "
+                          "throughput regime of the same kernels is kernel_chain.roofline"}
+        out = {
+            "metric": "reads aligned/sec (whole node), 150 bp vs hg38, at 1/2/4/8 MI355X",
+            "value": value, "unit": "aligned " + unit, "n_gpus": world,
+            "steps": args.steps, "warmup": args.warmup,
+            "ms_per_step": elapsed / args.steps * 1e3, "higher_is_better": True, "scaling": "weak",
+            "vs_baseline": None, "dtype": "u8/i16 DP, u32 FM", "data": "synthetic",
+            "config": {"workload": schedule_workload(args), "global_batch": args.reads * world,
+                       "seq_len": args.read_len, "parallelism": f"dp{world} (a batch server per GPU)",
+                       "aligned_frac": n_aligned / total_reads, "drivers": args.drivers,
+                       "client_connections": args.clients, "reads_per_connection": 10_000,
+                       "warmup_chunks": args.warmup_chunks},
+            "roofline": rl,
+            "reads_per_s": total_reads / elapsed,
+            "server_kernels": kern,
+            "server": {k: st.get(k) for k in ("reads", "rounds", "slots", "steps", "idle_ms")} |
+                      {"server_cpu_s": sched["server_cpu_s"], "server_rss_gb": sched["server_rss_gb"],
+                       "cpu_us_per_read": sched["server_cpu_s"] / max(1, args.reads * args.steps) * 1e6,
+                       "calls": {k: st.get(k) for k in ("exact_sweep", "one_mm", "seed_search", "extend",
+                                                        "get_offset", "ungapped", "sw_dp")},
+                       "threads_cpu": sched["server_threads_cpu"]},
+            "cpu_baseline": cpu,
+            "sam_parity": sam,
+            "vs_cpu_baseline": value / cpu["value"] if cpu and cpu.get("value") else None,
+            "kernel_chain": chain,
+        }
+        print(json.dumps(out), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+def schedule_workload(args):
+    vs = args.preset == "very-sensitive"
+    if args.mode == "paired":
+        cfg = "configs[4] policy, --end-to-end --very-sensitive" if vs else "configs[2], --end-to-end --sensitive"
+        what = f"{args.reads} synthetic 2 x {args.read_len} bp read pairs per GPU per step ({cfg})"
+    else:
+        mode = "--local (configs[3])" if args.mode == "local" else "--end-to-end --sensitive (configs[1])"
+        if vs:
+            mode = "--local --very-sensitive-local" if args.mode == "local" else "--end-to-end --very-sensitive"
+        what = f"{args.reads} synthetic {args.read_len} bp unpaired reads per GPU per step, {mode}"
+    size = "hg38-size " if args.genome_mb >= 3000 else ""
+    return (f"{what}, vs a {args.genome_mb:.0f} Mbp {size}synthetic genome ({args.genome_model}; hg38 is "
+            f"unavailable offline), through the reference's own server, client and per-read logic with the "
+            f"batch-first driver on the engines (oracle/_ref/bowtie2-align-server-batch), SAM output; "
+            f"<= 10 000 reads per client connection, {args.clients} connections at a time")
+
+
+def run_chain(args, rank, world, local, dev, idx, cache, reads_np, quals_np):
+    """The kernel chain (the module docstring's fixed policy, reads resident in
+    HBM): the engines in their throughput regime, with the roofline of its
+    dominant kernel.  Returns the kernel_chain block of the bench line."""
+    import torch
+    import torch.distributed as dist
+    import bt2g
+    eng = bt2g.Engine(index=idx, device=local)
+    if world > 1:
+        comm_setup(eng, rank, world)
+    info = eng.info()
+    log(f"[rank {rank}] chain engine: index resident {info[12]/1e9:.2f} GB")
     reads = torch.from_numpy(reads_np).to(dev)
     quals = torch.from_numpy(quals_np).to(dev)
     pipe = Pipeline(eng, idx, reads, quals, args.read_len, args.mode, args.preset)
 
     engs = [eng] + ([pipe.eng2] if args.mode == "paired" else [])
-    for _ in range(args.warmup):
+    for _ in range(args.chain_warmup):
         pipe.step()
     torch.cuda.synchronize()
     for e in engs:
@@ -965,8 +1180,8 @@ def main():
     torch.cuda.synchronize()
     ts = time.perf_counter()
     n_aligned = 0
-    for k in range(args.steps):
-        aligned = pipe.step(keep=(k == args.steps - 1))
+    for k in range(args.chain_steps):
+        aligned = pipe.step(keep=(k == args.chain_steps - 1))
         n_aligned += int(aligned.sum())
     torch.cuda.synchronize()
     if world > 1:
@@ -977,7 +1192,7 @@ def main():
     stats = {k: eng.kernel_stats(k) for k in range(6)}
     mstats = {k: pipe.eng2.kernel_stats(k) for k in (4, 5, 7)} if args.mode == "paired" else {}
     elapsed, n_aligned = combine_ranks(elapsed, n_aligned, dev, eng if world > 1 else None)
-    total_reads = args.reads * args.steps * world
+    total_reads = args.reads * args.chain_steps * world
     value = total_reads / elapsed
 
     # ---- roofline of the dominant kernel (per launch, rank 0's view) --------
@@ -1006,7 +1221,7 @@ def main():
     # in integer ops, SW_OPS_PER_CELL per DP cell (VALU-bound)
     work_k = dict(bytes_k)
     work_k[4] = sw_cells * SW_OPS_PER_CELL if 4 in per_launch else None
-    step_ms = {k: stats[k][1] / args.steps for k in per_launch}
+    step_ms = {k: stats[k][1] / args.chain_steps for k in per_launch}
     dom = max((k for k in per_launch if work_k.get(k)), key=lambda k: step_ms[k])
     achieved = work_k[dom] / (per_launch[dom] / 1e3) / (1e12 if dom == 4 else 1e9)
     for k in per_launch:
@@ -1049,15 +1264,15 @@ def main():
                 "dps_at_maxaln": int((naln_np >= pipe.maxaln).sum()), "maxaln": pipe.maxaln,
                 "dps_cand_overflow": int((naln_np == -5).sum()),
                 "cand_overflow_reruns_total": int(pipe.stats.get("cand_overflow_reruns", 0))}
-    log(f"[rank {rank}] SW: {last['npb']} DPs/step, {sw_gcups:.0f} GCUPS; aligned {n_aligned/(args.steps*world*args.reads):.4f}; backtrace {bt_stats}")
+    log(f"[rank {rank}] SW: {last['npb']} DPs/step, {sw_gcups:.0f} GCUPS; aligned {n_aligned/(args.chain_steps*world*args.reads):.4f}; backtrace {bt_stats}")
     mate_stats = None
     if args.mode == "paired":
-        mk = {k: v[1] / args.steps for k, v in mstats.items()}          # ms per step
+        mk = {k: v[1] / args.chain_steps for k, v in mstats.items()}          # ms per step
         mcells = last["m_dps"] * args.read_len * pipe.mate_cols
         mate_stats = {"anchors": last["m_anchors"], "mate_dps": last["m_dps"], "pairs_mate_found": last["m_found"],
                       "frame_ms_per_step": mk[7], "fill_ms_per_step": mk[4], "backtrace_ms_per_step": mk[5],
                       "fill_gcups": mcells / (mk[4] / 1e3) / 1e9 if mk[4] else None,
-                      "launches_per_step": mstats[4][0] / args.steps}
+                      "launches_per_step": mstats[4][0] / args.chain_steps}
         log(f"[rank {rank}] mate search: {mate_stats}")
 
     # ---- the repeat landscape the last step saw (rank 0's batch) -------------
@@ -1086,12 +1301,11 @@ def main():
                                             "p90": q[1], "p99": q[2], "p999": q[3], "max": float(mmo.max())}
     log(f"[rank {rank}] landscape {landscape}")
 
-    # ---- CPU baseline: the reference on the host cores, rank 0, N=1 ---------
+    # ---- optional: the reference's own chain on the host cores, rank 0, N=1 ---
     cpu = None
     parity = None
-    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+    if rank == 0 and world == 1 and args.chain_cpu_baseline:
         from oracle import ref_server as rs
-        from oracle.ref_chain import compare
         host = rs.host_cpus()
         threads = args.cpu_threads or host["usable"]
         sample = min(args.cpu_sample, pipe.npairs if args.mode == "paired" else pipe.n)
@@ -1099,96 +1313,52 @@ def main():
             dt, ref, mate, secs = cpu_baseline(idx, reads_np, quals_np, pipe, sample, threads, base=cache or None)
             paired = args.mode == "paired"
             cpu = {"value": sample / dt, "unit": "read pairs/s" if paired else "reads/s", "cores": threads,
-                   "kind": "reference", "host": host, "stage_seconds": secs,
+                   "kind": "reference", "stage_seconds": secs,
                    "sample": f"first {sample} {'pairs (both mates)' if paired else 'reads'} of the batch through "
-                             f"the reference's own chain: exactSweep, gated oneMmSearch, searchAllSeeds, getOffset "
-                             f"of its own hit rows, joinedToTextOff, frameSeedExtensionRect of the bench's two "
-                             f"diagonals per read, SwAligner::align and the nextAlignment loop "
-                             f"({len(ref['sw'])} DPs)"
-                             + (f", then otherMate + frameFindMateRect + the mate DPs of the GPU's anchors "
-                                f"({len(mate['out_ref'])})" if paired else "")
-                             + f"; {threads} threads = the usable cores of this host ({host['model']})"}
+                             f"the reference's own chain (oracle/ref_chain.py) on {threads} threads"}
             parity = chain_parity(pipe, ref, mate)
-            log(f"[rank 0] cpu baseline {sample/dt:.0f} {cpu['unit']} on {threads} threads ({dt:.1f}s); parity {parity}")
-            if args.server_sample:
-              try:
-                import tempfile
-                srv_args = ["--local"] if args.mode == "local" else []
-                if args.preset == "very-sensitive":
-                    srv_args.append("--very-sensitive-local" if args.mode == "local" else "--very-sensitive")
-                srv = server_baseline(ref["index_base"], reads_np, quals_np, pipe.pol,
-                                      min(args.server_sample, sample), threads, args.server_workers, srv_args,
-                                      tempfile.mkdtemp(prefix="bt2srv_"), dropin_args=args.server_dropin_args.split())
-                cpu["reference_server"] = {"value": srv["stock"]["rate"], "unit": cpu["unit"], "cores": threads,
-                                           "sample": f"first {min(args.server_sample, sample)} of the batch, "
-                                                     f"<= 10 000 per client connection, 8 connections at a time",
-                                           **{k: v for k, v in srv["stock"].items() if k != "rate"}}
-                cpu["dropin_server"] = {"value": srv["dropin"]["rate"], "unit": cpu["unit"],
-                                        "sam_identical_to_reference": srv["sam_identical"],
-                                        "sam_records_differing": srv["sam_records_differing"],
-                                        "vs_reference_server": srv["dropin_vs_stock"],
-                                        **{k: v for k, v in srv["dropin"].items() if k != "rate"}}
-                log(f"[rank 0] reference server {srv['stock']['rate']:.0f}, drop-in {srv['dropin']['rate']:.0f} "
-                    f"{cpu['unit']}; SAM identical {srv['sam_identical']}")
-              except Exception as e:       # the servers are checkers: their failure must not hide the rest
-                import traceback
-                traceback.print_exc()
-                cpu["reference_server"] = {"error": repr(e)[:500]}
+            log(f"[rank 0] chain cpu baseline {sample/dt:.0f} {cpu['unit']} ({dt:.1f}s); parity {parity}")
         except Exception as e:  # the reference build is optional on the box
             import traceback
             traceback.print_exc()
-            log(f"[rank 0] cpu baseline unavailable: {e!r}")
-
-    if rank == 0:
-        out = {
-            "metric": "reads aligned/sec (whole node), 150 bp vs hg38, at 1/2/4/8 MI355X",
-            "value": value, "unit": "read pairs/s" if args.mode == "paired" else "reads/s", "n_gpus": world,
-            "steps": args.steps, "warmup": args.warmup,
-            "ms_per_step": elapsed / args.steps * 1e3, "higher_is_better": True, "scaling": "weak",
-            "vs_baseline": None, "dtype": "u8/i16 DP, u32 FM", "data": "synthetic",
-            "config": {"workload": workload(args),
-                       "global_batch": args.reads * world, "seq_len": args.read_len, "parallelism": f"dp{world}",
-                       "aligned_frac": n_aligned / total_reads},
-            "roofline": dict({"bound": "hbm", "kernel": names_k[dom], "achieved": achieved, "peak": HBM_PEAK_GBS,
-                              "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS, "bytes_per_launch": bytes_k[dom]}
-                             if dom != 4 else
-                             {"bound": "valu", "kernel": "sw_align (systolic fill + decision plane, candidate sort)",
-                              "achieved": achieved, "peak": VALU_PEAK_TOPS, "unit": "T int-ops/s",
-                              "frac": achieved / VALU_PEAK_TOPS, "ops_per_cell": SW_OPS_PER_CELL,
-                              "cells_per_launch": sw_cells, "gcups": sw_gcups,
-                              "issued_valu_lane_ops_per_cell": VALU_OPS_PER_CELL},
-                             ms_per_launch=per_launch[dom], ms_per_step=step_ms[dom],
-                             traffic=pmc_traffic(args.pmc_fetch, args.pmc_write, PMC_KERNEL[dom])),
-            "aligned_per_s": n_aligned / elapsed,
-            "schedule": "bench chain: exact sweep, gated 1-mm search, round-0 exact seeds, getOffset of each hit "
-                        "range's top row, <= 2 seed-extension DPs per read (fixed policy), fill + nextAlignment "
-                        "loop; the reference's real schedule (RNG-driven prioritisation, streaks, re-seeding, "
-                        "SAM) is timed by real_schedule",
-            "real_schedule": real_schedule(cpu),
-            "kernels_ms": {names_k[k]: per_launch[k] for k in per_launch},
-            "kernels_gbs": {names_k[k]: bytes_k[k] / (per_launch[k] / 1e3) / 1e9 for k in per_launch
-                            if bytes_k.get(k)},
-            "side_loads_per_step": {names_k[k]: (bytes_k[k] // 64) for k in (0, 1, 2, 3) if bytes_k.get(k)},
-            "sw_gcups": sw_gcups,
-            # the SW fill against its VALU ceiling (north_star: VALU utilisation of the SW kernel)
-            # issued (not algorithmic) VALU work of the fill: its instruction mix, from
-            # the PMC pass scripts/pmc_fill.sh (a constant measured on another run)
-            "sw_issue": {"issued_valu_lane_ops_per_cell": VALU_OPS_PER_CELL,
-                         "issued_T_lane_ops_per_s": sw_gcups * VALU_OPS_PER_CELL / 1e3,
-                         "of_valu_peak": sw_gcups * VALU_OPS_PER_CELL / 1e3 / VALU_PEAK_TOPS,
-                         "of_packed_issue_ceiling": sw_gcups * VALU_OPS_PER_CELL / 1e3 / VALU_PACKED_TOPS}
-            if args.mode == "ee" else None,
-            "backtrace": bt_stats,
-            "landscape": landscape,
-            "mate_search": mate_stats,
-            "cpu_baseline": cpu,
-            "parity_sample": parity,
-        }
-        print(json.dumps(out), flush=True)
+            log(f"[rank 0] chain cpu baseline unavailable: {e!r}")
     for e in engs[::-1]:
         e.close()
-    if world > 1:
-        dist.destroy_process_group()
+    torch.cuda.synchronize()
+    torch.cuda.empty_cache()
+    return {
+        "value": value, "unit": "read pairs/s" if args.mode == "paired" else "reads/s",
+        "steps": args.chain_steps, "warmup": args.chain_warmup, "ms_per_step": elapsed / args.chain_steps * 1e3,
+        "aligned_frac": n_aligned / total_reads, "aligned_per_s": n_aligned / elapsed,
+        "workload": workload(args),
+        "schedule": "fixed policy: exact sweep, gated 1-mm search, round-0 exact seeds, getOffset of each hit "
+                    "range's top row, <= 2 seed-extension DPs per read, fill + nextAlignment loop; every read's "
+                    "batch resident in HBM",
+        "roofline": dict({"bound": "hbm", "kernel": names_k[dom], "achieved": achieved, "peak": HBM_PEAK_GBS,
+                          "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS, "bytes_per_launch": bytes_k[dom]}
+                         if dom != 4 else
+                         {"bound": "valu", "kernel": "sw_align (systolic fill + decision plane, candidate sort)",
+                          "achieved": achieved, "peak": VALU_PEAK_TOPS, "unit": "T int-ops/s",
+                          "frac": achieved / VALU_PEAK_TOPS, "ops_per_cell": SW_OPS_PER_CELL,
+                          "cells_per_launch": sw_cells, "gcups": sw_gcups,
+                          "issued_valu_lane_ops_per_cell": VALU_OPS_PER_CELL},
+                         ms_per_launch=per_launch[dom], ms_per_step=step_ms[dom],
+                         traffic=pmc_traffic(args.pmc_fetch, args.pmc_write, PMC_KERNEL[dom])),
+        "kernels_ms": {names_k[k]: per_launch[k] for k in per_launch},
+        "kernels_gbs": {names_k[k]: bytes_k[k] / (per_launch[k] / 1e3) / 1e9 for k in per_launch if bytes_k.get(k)},
+        "side_loads_per_step": {names_k[k]: (bytes_k[k] // 64) for k in (0, 1, 2, 3) if bytes_k.get(k)},
+        "sw_gcups": sw_gcups,
+        "sw_issue": {"issued_valu_lane_ops_per_cell": VALU_OPS_PER_CELL,
+                     "issued_T_lane_ops_per_s": sw_gcups * VALU_OPS_PER_CELL / 1e3,
+                     "of_valu_peak": sw_gcups * VALU_OPS_PER_CELL / 1e3 / VALU_PEAK_TOPS,
+                     "of_packed_issue_ceiling": sw_gcups * VALU_OPS_PER_CELL / 1e3 / VALU_PACKED_TOPS}
+        if args.mode == "ee" else None,
+        "backtrace": bt_stats,
+        "landscape": landscape,
+        "mate_search": mate_stats,
+        "cpu_baseline": cpu,
+        "parity_sample": parity,
+    }
 
 
 if __name__ == "__main__":

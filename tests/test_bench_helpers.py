@@ -112,18 +112,22 @@ def test_ref_chain_compare_cpu():
     assert c["offset_mismatch"] == 1 and c["frame_mismatch"] == 1 and c["exact_sweep_mismatch"] == 1, c
 
 
-def test_server_baseline_cpu():
-    """bench.server_baseline end to end on CPU: the stock reference server and the
-    drop-in binding over the CPU stand-in (bowtie2-align-server-stub) on 300
-    reads of a small synthetic index; identical sorted SAM, both rates set."""
+def test_schedule_and_stock_baseline_cpu():
+    """bench.schedule_run + bench.stock_baseline end to end on CPU: the batch
+    server over the CPU stand-in of the engines (bowtie2-align-server-batch-stub)
+    and the stock reference server on 2 500 reads of a small synthetic index
+    (one chunk, k = 2):
+    identical sorted SAM, the aligned count taken from the SAM, the server's
+    engine statistics read back."""
     import os
     import tempfile
+    import types
     import pytest
     import bench
     import bt2_index as bi
     import synth
     from oracle import ref_server as rs
-    stub = os.path.join(rs.REF_DIR, "bowtie2-align-server-stub")
+    stub = os.path.join(rs.REF_DIR, "bowtie2-align-server-batch-stub")
     if not (os.path.exists(rs.SERVER) and os.path.exists(stub)):
         pytest.skip("oracle/_ref servers not built")
     g = synth.genome(7, 100_000, n_repeats=10, rep_len=1500, n_copies=3, n_runs=2)
@@ -131,8 +135,19 @@ def test_server_baseline_cpu():
     d = tempfile.mkdtemp()
     base = os.path.join(d, "g")
     bi.write_index(base, idx)
-    r, q = bench.make_reads(idx.ref_codes, 300, 150, 5)
-    out = bench.server_baseline(base, r, q, bench.Policy("ee", 150), 300, 2, 8, [], d, dropin_binary=stub)
-    assert out["sam_identical"] and out["sam_records_differing"] == 0
-    assert out["stock"]["records"] == 300 and out["dropin"]["rate"] > 0
-    assert out["dropin"]["engine_calls"]["exact_sweep"][0] > 0
+    r, q = bench.make_reads(idx.ref_codes, 2500, 150, 5)
+    args = types.SimpleNamespace(mode="ee", preset="sensitive", reads=2500, drivers=2, clients=2, warmup=1,
+                                 warmup_chunks=1, steps=1, stock_sample=2500, cpu_threads=2)
+    sc = bench.schedule_run(args, 0, 1, 0, base, r, q, d, binary=stub)
+    assert sc["aligned"] == bench.count_aligned(sc["outs"], False) and 2000 < sc["aligned"] <= 2500
+    assert sc["stats"]["driver"] == "batch" and sc["stats"]["reads"] >= 2500
+    cpu, sam = bench.stock_baseline(args, base, sc["chunks"], sc["outs"], d)
+    assert sam["identical"] and sam["records"] == 2500
+    assert cpu["value"] > 0 and cpu["kind"] == "reference"
+
+
+def test_count_aligned_flags():
+    sam = [b"r1\t0\tc\t1\n@CO x\nr2\t4\t*\t0\nr3\t256\tc\t5\nr4\t16\tc\t9\n",
+           b"p1\t77\t*\t0\np1\t141\t*\t0\np2\t73\tc\t1\np2\t133\t*\t0\np3\t99\tc\t1\np3\t147\tc\t9\n"]
+    assert bench.count_aligned(sam[:1], False) == 2
+    assert bench.count_aligned(sam[1:], True) == 2
