@@ -65,7 +65,7 @@ __host__ __device__ inline WgLayout wg_layout(uint32_t cstride, uint32_t pcols) 
 	L.marks = L.plane + (cstride >> 4) * pcols * 8u;
 	L.moves = L.marks + r16(L.mkw * 4u);
 	L.info = L.moves + r16(64u * L.mw * 4u);
-	L.rd = L.info + 64u * 16u;
+	L.rd = L.info + 64u * 32u;
 	L.qu = L.rd + r16(cstride);
 	L.rf = L.qu + r16(cstride);
 	L.total = L.rf + r16(pcols + 4u);
@@ -108,7 +108,7 @@ __global__ void __launch_bounds__(64) k_sw_bt_wg(BtArgs A) {
 	const uint32_t* const dec = (const uint32_t*)(lds + L.plane);
 	uint32_t* const marks = (uint32_t*)(lds + L.marks);
 	uint32_t* const moves = (uint32_t*)(lds + L.moves);
-	uint32_t* const info = (uint32_t*)(lds + L.info);      // per lane: moves, ok, row0, col0
+	uint32_t* const info = (uint32_t*)(lds + L.info);      // per lane: moves, ok, row0, col0, score
 	uint8_t* const srd = lds + L.rd;
 	uint8_t* const squ = lds + L.qu;
 	uint8_t* const srf = lds + L.rf;
@@ -197,10 +197,12 @@ __global__ void __launch_bounds__(64) k_sw_bt_wg(BtArgs A) {
 		{
 			const uint32_t ci = c0 + lane;
 			uint32_t T = 0, ok = 0, r0 = 0, q0 = 0;
+			int32_t sc0 = 0;
 			if(ci < ncand) {
 				const bt2g_sw_cand cd = cl[ci];
 				r0 = (uint32_t)cd.row;
 				q0 = (uint32_t)cd.col;
+				sc0 = cd.score;
 				if(cd.score >= P.minsc) {
 					uint32_t row = r0, col = q0;
 					int st = WST_H;
@@ -231,10 +233,13 @@ __global__ void __launch_bounds__(64) k_sw_bt_wg(BtArgs A) {
 					ok = core && ns <= nceil ? 1u : 0u;
 				}
 			}
-			info[lane * 4u] = T;
-			info[lane * 4u + 1u] = ok;
-			info[lane * 4u + 2u] = r0;
-			info[lane * 4u + 3u] = q0;
+			// (phase B reads the candidates from here, not from global memory: a
+			// dependent global load per candidate would be most of the loop)
+			info[lane * 8u] = T;
+			info[lane * 8u + 1u] = ok;
+			info[lane * 8u + 2u] = r0;
+			info[lane * 8u + 3u] = q0;
+			info[lane * 8u + 4u] = (uint32_t)sc0;
 		}
 		__syncthreads();
 		// ---- B: the candidates in the reference's order -----------------------------
@@ -244,15 +249,14 @@ __global__ void __launch_bounds__(64) k_sw_bt_wg(BtArgs A) {
 		for(uint32_t ci = c0; ci < cend; ci++) {
 			if(nal >= (int32_t)A.maxaln) { stop = true; break; }
 			const uint32_t j = ci - c0;
-			const bt2g_sw_cand cd = cl[ci];
 			int8_t fate;
-			const uint32_t r0 = info[j * 4u + 2u], q0 = info[j * 4u + 3u];
-			if(cd.score < P.minsc) {
+			const uint32_t r0 = info[j * 8u + 2u], q0 = info[j * 8u + 3u];
+			if((int32_t)info[j * 8u + 4u] < P.minsc) {
 				fate = 5;                               // BT_CAND_FATE_FILT_SCORE
 			} else if(!bottom(r0) && ((marks[mark_bit(r0, q0) >> 5] >> (mark_bit(r0, q0) & 31u)) & 1u)) {
 				fate = 3;                               // BT_CAND_FATE_FILT_START
 			} else {
-				const uint32_t T = info[j * 4u], ncell = T + 1u;
+				const uint32_t T = info[j * 8u], ncell = T + 1u;
 				const uint32_t* mv = moves + (size_t)j * L.mw;
 				const uint32_t ch = (ncell + 63u) / 64u;
 				const uint32_t lo = lane * ch < ncell ? lane * ch : ncell, hi = lo + ch < ncell ? lo + ch : ncell;
@@ -294,7 +298,7 @@ __global__ void __launch_bounds__(64) k_sw_bt_wg(BtArgs A) {
 					}
 				}
 				__syncthreads();
-				if(tstar == 0xffffffffu && info[j * 4u + 1u]) {
+				if(tstar == 0xffffffffu && info[j * 8u + 1u]) {
 					fate = 1;                           // BT_CAND_FATE_SUCCEEDED
 					if(lane == nsucc) succ = ci;
 					nsucc++;

@@ -59,13 +59,8 @@ struct Node {
 };
 
 inline int cls_of(size_t n) {
-	size_t s = 16;
-	int c = 0;
-	while(s < n) {
-		s <<= 1;
-		c++;
-	}
-	return c;
+	// the smallest c with 16 << c >= n
+	return n <= 16 ? 0 : 60 - __builtin_clzll((unsigned long long)(n - 1));
 }
 inline size_t size_of(int c) { return (size_t)16 << c; }
 // blocks a thread keeps per class before half go to the depot (~4 MiB per class
