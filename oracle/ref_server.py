@@ -49,6 +49,23 @@ def dropin_env(index_base, stats_path=None, device=0):
     return env
 
 
+def host_cpu_seconds():
+    """CPU seconds (user + system) this container has spent -- the cgroup's
+    cpu.stat (the GPU box's CPU quota is shared by the server, its clients and
+    the harness), else the host's /proc/stat."""
+    try:
+        for ln in open("/sys/fs/cgroup/cpu.stat"):
+            if ln.startswith("usage_usec"):
+                return int(ln.split()[1]) / 1e6
+    except (OSError, ValueError, IndexError):
+        pass
+    try:
+        f = open("/proc/stat").readline().split()
+        return (int(f[1]) + int(f[2]) + int(f[3]) + int(f[6]) + int(f[7])) / os.sysconf("SC_CLK_TCK")
+    except (OSError, ValueError, IndexError):
+        return float("nan")
+
+
 def free_port():
     s = socket.socket()
     s.bind(("127.0.0.1", 0))
@@ -138,6 +155,7 @@ class Server:
                 outs[i] = r.stdout
 
         c0 = self.cpu_seconds()
+        h0 = host_cpu_seconds()
         t0 = time.perf_counter()
         ths = [threading.Thread(target=worker) for _ in range(max(1, min(k, len(chunk_args))))]
         for t in ths:
@@ -146,6 +164,7 @@ class Server:
             t.join()
         dt = time.perf_counter() - t0
         self.last_cpu_s = self.cpu_seconds() - c0        # server CPU time (all threads) over the run
+        self.last_host_cpu_s = host_cpu_seconds() - h0   # every process of the host (clients included)
         self.last_rss_gb = self.rss_gb()
         self.last_threads = self.thread_cpu()
         if errs:
