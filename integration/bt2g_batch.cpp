@@ -3088,8 +3088,12 @@ void Driver::release(Slot* s) {
 void Driver::run_loop() {
 	open_bases();
 	const size_t ndev = g_bases.size();
-	int rc = bt2g_open_shared(g_bases[(size_t)tid % ndev], &ctx);
-	if(rc) die("bt2g_open_shared", rc);
+	if(!services_on()) {
+		// (with the services a driver makes no engine call: no context, so that its
+		// stream takes none of the device's hardware queues)
+		int rc = bt2g_open_shared(g_bases[(size_t)tid % ndev], &ctx);
+		if(rc) die("bt2g_open_shared", rc);
+	}
 	sc = R_sc;
 	ebwtFw = R_ebwtFw;
 	ebwtBw = R_ebwtBw;
