@@ -26,6 +26,7 @@
 // allocation (r03p at 3.1 Gbp: mprotect 14 % of the carriers' CPU, all of it
 // under this allocator's malloc calls).  Larger blocks go to malloc / free
 // directly.  $BT2G_ALLOC=0 keeps glibc's allocator.
+#include <dlfcn.h>
 #include <errno.h>
 #include <execinfo.h>
 #include <stdio.h>
@@ -269,8 +270,12 @@ void* alloc(size_t n) {
 	return fresh(c);
 }
 
+bool xtrace_on();
+void xcheck(void* p);
+
 void release(void* p) {
 	if(!p) return;
+	if(xtrace_on()) xcheck(p);
 	Hdr* h = (Hdr*)((char*)p - HDR);
 	if(h->magic == MAGIC_MALLOC) {
 		free(h);
@@ -309,6 +314,46 @@ void release(void* p) {
 
 }  // namespace
 
+// $BT2G_ALLOC_XTRACE=1 (diagnostics): every block remembers its allocating
+// thread and call site (the header's spare word); a block freed by another
+// thread counts its call site -- which code feeds the cross-thread flows that
+// make the depot traffic.  Dumped with the stats (call sites as module + offset).
+namespace {
+bool xtrace_on() {
+	static const bool on = getenv("BT2G_ALLOC_XTRACE") != nullptr;
+	return on;
+}
+std::atomic<uint32_t> g_tid_next{1};
+thread_local uint32_t t_tid = 0;
+inline uint64_t my_tid() {
+	if(!t_tid) t_tid = g_tid_next.fetch_add(1) & 0xffffu;
+	return t_tid;
+}
+const size_t XSLOT = 1u << 14;
+std::atomic<uint64_t> g_xpc[XSLOT];
+std::atomic<uint64_t> g_xcnt[XSLOT];
+inline void xtag(void* p, void* ra) {
+	if(!p) return;
+	Hdr* h = (Hdr*)((char*)p - HDR);
+	h->pad = (my_tid() << 48) | ((uint64_t)(uintptr_t)ra & 0xffffffffffffull);
+}
+inline void xcheck(void* p) {
+	Hdr* h = (Hdr*)((char*)p - HDR);
+	const uint64_t t = h->pad >> 48;
+	if(!t || t == my_tid()) return;
+	const uint64_t pc = h->pad & 0xffffffffffffull;
+	size_t k = (size_t)((pc * 0x9E3779B97F4A7C15ull) >> 50) & (XSLOT - 1);
+	for(int probe = 0; probe < 64; probe++, k = (k + 1) & (XSLOT - 1)) {
+		uint64_t cur = g_xpc[k].load(std::memory_order_relaxed);
+		if(cur == pc) { g_xcnt[k].fetch_add(1, std::memory_order_relaxed); return; }
+		if(cur == 0) {
+			uint64_t z = 0;
+			if(g_xpc[k].compare_exchange_strong(z, pc) || z == pc) { g_xcnt[k].fetch_add(1, std::memory_order_relaxed); return; }
+		}
+	}
+}
+}  // namespace
+
 extern "C" void bt2g_alloc_stats_dump() {
 	const char* path = getenv("BT2G_ALLOC_STATS");
 	if(!path) return;
@@ -320,17 +365,28 @@ extern "C" void bt2g_alloc_stats_dump() {
 		        c < NCLASS ? (unsigned long long)g_topot[c].load() : 0ull, c < NCLASS ? (unsigned long long)depot().n[c] : 0ull);
 	for(int b = 0; b < 48; b++)
 		if(g_big[b].load()) fprintf(f, "big<=2^%d %llu\n", b, (unsigned long long)g_big[b].load());
+	if(xtrace_on())
+		for(size_t k = 0; k < XSLOT; k++) {
+			const uint64_t pc = g_xpc[k].load();
+			if(!pc) continue;
+			Dl_info di;
+			if(dladdr((void*)(uintptr_t)pc, &di) && di.dli_fname)
+				fprintf(f, "xfree %s %lx %llu\n", di.dli_fname, (unsigned long)(pc - (uint64_t)(uintptr_t)di.dli_fbase),
+				        (unsigned long long)g_xcnt[k].load());
+		}
 	fclose(f);
 }
 
 void* operator new(size_t n) {
 	void* p = alloc(n);
 	if(!p) throw std::bad_alloc();
+	if(xtrace_on()) xtag(p, __builtin_return_address(0));
 	return p;
 }
 void* operator new[](size_t n) {
 	void* p = alloc(n);
 	if(!p) throw std::bad_alloc();
+	if(xtrace_on()) xtag(p, __builtin_return_address(0));
 	return p;
 }
 void* operator new(size_t n, const std::nothrow_t&) noexcept { return alloc(n); }

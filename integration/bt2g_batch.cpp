@@ -391,6 +391,12 @@ thread_local std::atomic<uint64_t>* t_cpu_ext = nullptr;
 // One engine DP: SwAligner::initRead + initRef + align and every
 // nextAlignment walk of it (bt2g_sw_align_bt), keyed by the problem.
 struct DpRes {
+	DpRes() {
+		cands.reserve(128);
+		fates.reserve(128);
+		alns.reserve(8);
+		edits.reserve(256);
+	}
 	int mate = 0;          // the read of the DP (its row in the slot)
 	int32_t fw = 0;
 	uint32_t refidx = 0;
@@ -525,6 +531,30 @@ struct Conn {
 	long live = 0;
 	Elem* last = nullptr;
 };
+
+// Buffer elements are made by a driver's feeder and freed by whichever driver
+// returns the buffer: recycled through one pool rather than the allocator (a
+// block freed on another thread than it was made on travels through the
+// allocator's shared depot).
+std::mutex g_elem_mu;
+std::vector<Elem*> g_elem_pool;
+Elem* elem_new(const ReadElement& re) {
+	Elem* e = nullptr;
+	{
+		std::lock_guard<std::mutex> lk(g_elem_mu);
+		if(!g_elem_pool.empty()) {
+			e = g_elem_pool.back();
+			g_elem_pool.pop_back();
+		}
+	}
+	if(!e) return new Elem(re);
+	e->~Elem();                               // (ReadElement holds a reference: rebuilt in place)
+	return new (e) Elem(re);
+}
+void elem_free(Elem* e) {
+	std::lock_guard<std::mutex> lk(g_elem_mu);
+	g_elem_pool.push_back(e);
+}
 std::mutex g_conn_mu;
 std::unordered_map<const void*, Conn> g_conns;
 
@@ -535,6 +565,13 @@ enum {
 
 // Engine results of one mate.
 struct MateRes {
+	// (result vectors sized up front: the services' workers fill them, and a
+	// vector grown on one worker and regrown on another moves its blocks between
+	// threads through the allocator's shared depot)
+	MateRes() {
+		mm.reserve(64);
+		sd_out.reserve(256);
+	}
 	uint32_t sweep[8] = {0};
 	bool sweep_asked = false;
 	int32_t mm_minsc = 0;
@@ -565,7 +602,15 @@ struct Slot {
 		: scCurrent((uint64_t)R_seedCacheCurrentMB * 1024 * 1024, false),
 		  ca(&scCurrent, NULL, NULL),
 		  sd((size_t)R_exactCacheCurrentMB * 1024 * 1024),
-		  msinkwrap(rp, mapq, tid) {}
+		  msinkwrap(rp, mapq, tid) {
+		ext_in.reserve(64);
+		ext_out.reserve(64);
+		off_rows.reserve(1024);
+		off_vals.reserve(1024);
+		off_where.reserve(1024);
+		ug_ed.reserve(64);
+		dps.reserve(64);
+	}
 	AlignmentCache scCurrent;
 	AlignmentCacheIface ca;
 	SwDriverB sd;
@@ -743,7 +788,7 @@ struct Driver {
 	// reads in: a feeder thread pops the factory's ready queue for this driver
 	std::mutex in_mu;
 	std::condition_variable in_cv, room_cv;
-	std::deque<Elem*> inbox;
+	std::vector<Elem*> inbox, got;   // (swapped each round: no allocation once grown)
 	size_t max_slots = 2048;         // reads in flight per driver ($BT2G_BATCH_SLOTS)
 	std::atomic<size_t> active_a{0}; // `active` for the feeder
 	// requests of this round
@@ -2982,7 +3027,7 @@ void Driver::feeder() {
 			room_cv.wait(lk, [this] { return active_a.load() + 16 * inbox.size() < max_slots; });
 		}
 		ReadElement re = R_factory->nextReadPair();      // blocks until a connection has reads
-		Elem* e = new Elem(re);
+		Elem* e = elem_new(re);
 		e->conn = &re.ps->msink();
 		{
 			std::lock_guard<std::mutex> lk(g_conn_mu);
@@ -3011,7 +3056,7 @@ void conn_done(const void* c, long n) {
 	}
 	if(ret) {
 		R_factory->returnUnready(ret->re);
-		delete ret;
+		elem_free(ret);
 	}
 }
 
@@ -3063,7 +3108,7 @@ void Driver::admit(Elem* e) {
 	}
 	if(prev) {
 		R_factory->returnUnready(prev->re);
-		delete prev;
+		elem_free(prev);
 		conn_done(conn, 1);
 	} else {
 		conn_done(conn, 0);                   // (returned now if none of its reads is in flight)
@@ -3154,7 +3199,7 @@ void Driver::run_loop() {
 	}
 	std::thread(&Driver::feeder, this).detach();
 	for(;;) {
-		std::deque<Elem*> got;
+		got.clear();
 		{
 			std::unique_lock<std::mutex> lk(in_mu);
 			if(active == 0 && inbox.empty()) {
