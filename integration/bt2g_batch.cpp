@@ -191,6 +191,8 @@ bool g_stub = false;
 enum { K_EXACT, K_1MM, K_SEEDS, K_EXT, K_OFF, K_UG, K_DP, K_N };
 const char* const K_NAMES[K_N] = {"exact_sweep", "one_mm", "seed_search", "extend", "get_offset", "ungapped", "sw_dp"};
 std::atomic<uint64_t> g_req[K_N], g_calls[K_N], g_call_us[K_N], g_cpu[K_N];
+// service workers' busy time per kind (a call's packing and unpacking included)
+std::atomic<uint64_t> g_svc_us[K_N];
 std::atomic<uint64_t> g_reads{0}, g_rounds{0}, g_round_us{0}, g_cpu_us{0}, g_gpu_us{0};
 std::atomic<uint64_t> g_dp_spec{0}, g_dp_used{0}, g_dp_reuse{0}, g_dp_miss{0};
 // rounds per read: total and a histogram (bin b: [2^b, 2^(b+1)))
@@ -214,6 +216,10 @@ void write_stats() {
 		n += snprintf(buf + n, sizeof(buf) - n, ", \"%s\": [%llu, %llu, %llu, %.1f]", K_NAMES[k],
 		              (unsigned long long)g_req[k].load(), (unsigned long long)g_cpu[k].load(),
 		              (unsigned long long)g_calls[k].load(), g_call_us[k].load() / 1000.0);
+	n += snprintf(buf + n, sizeof(buf) - n, ", \"svc_busy_ms\": [");
+	for(int k = 0; k < K_N; k++)
+		n += snprintf(buf + n, sizeof(buf) - n, "%s%.1f", k ? ", " : "", g_svc_us[k].load() / 1000.0);
+	n += snprintf(buf + n, sizeof(buf) - n, "]");
 	n += snprintf(buf + n, sizeof(buf) - n, ", \"inflight_sum\": %llu, \"idle_ms\": %.1f, \"slots\": %llu",
 	              (unsigned long long)g_inflight.load(), g_idle_us.load() / 1000.0, (unsigned long long)g_slots.load());
 	n += snprintf(buf + n, sizeof(buf) - n, ", \"steps\": %llu, \"steps_hist\": [", (unsigned long long)g_steps.load());
@@ -2932,11 +2938,13 @@ void Svc::loop() {
 		}
 		v.clear();
 		dp.clear();
+		const uint64_t t0 = now_us();
 		for(Driver* d : got) {
 			if(kind == K_DP) dp.insert(dp.end(), d->rq_dp.begin(), d->rq_dp.end());
 			else v.insert(v.end(), d->rq[kind].begin(), d->rq[kind].end());
 		}
 		run(v, dp);
+		g_svc_us[kind] += now_us() - t0;
 		if(kprof_on()) {
 			std::lock_guard<std::mutex> lk(st_mu);
 			for(int k = 0; k < 8; k++) (void)bt2g_kernel_stats(ctx, k, &k_launch[k], &k_ms[k]);
