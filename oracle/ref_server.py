@@ -49,6 +49,18 @@ def dropin_env(index_base, stats_path=None, device=0):
     return env
 
 
+def cgroup_throttled_seconds():
+    """Time this container's threads spent throttled by its CPU quota (cgroup
+    cpu.stat throttled_usec; nan without a cgroup v2 quota)."""
+    try:
+        for ln in open("/sys/fs/cgroup/cpu.stat"):
+            if ln.startswith("throttled_usec"):
+                return int(ln.split()[1]) / 1e6
+    except (OSError, ValueError, IndexError):
+        pass
+    return float("nan")
+
+
 def host_cpu_seconds():
     """CPU seconds (user + system) this container has spent -- the cgroup's
     cpu.stat (the GPU box's CPU quota is shared by the server, its clients and
@@ -156,6 +168,7 @@ class Server:
 
         c0 = self.cpu_seconds()
         h0 = host_cpu_seconds()
+        th0 = cgroup_throttled_seconds()
         t0 = time.perf_counter()
         ths = [threading.Thread(target=worker) for _ in range(max(1, min(k, len(chunk_args))))]
         for t in ths:
@@ -165,6 +178,7 @@ class Server:
         dt = time.perf_counter() - t0
         self.last_cpu_s = self.cpu_seconds() - c0        # server CPU time (all threads) over the run
         self.last_host_cpu_s = host_cpu_seconds() - h0   # every process of the host (clients included)
+        self.last_throttled_s = cgroup_throttled_seconds() - th0
         self.last_rss_gb = self.rss_gb()
         self.last_threads = self.thread_cpu()
         if errs:

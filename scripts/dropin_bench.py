@@ -97,7 +97,7 @@ def main():
         unit = "pairs/s" if a.mode == "paired" else "reads/s"
         out[tag] = {"seconds": dt, "rate": a.reads / dt, "unit": unit, "threads": th, "records": len(sams[tag]),
                     "server_cpu_s": s.last_cpu_s, "server_cores_busy": s.last_cpu_s / dt, "server_rss_gb": s.last_rss_gb,
-                    "host_cpu_s": s.last_host_cpu_s,
+                    "host_cpu_s": s.last_host_cpu_s, "throttled_s": s.last_throttled_s,
                     "server_threads_cpu": s.last_threads}
         time.sleep(0.5)
         if os.path.exists(stats):
