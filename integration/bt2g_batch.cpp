@@ -59,6 +59,7 @@
 #include <string.h>
 #include <sys/time.h>
 #include <pthread.h>
+#include <sched.h>
 #include <signal.h>
 #include <execinfo.h>
 #include <unistd.h>
@@ -275,10 +276,43 @@ void on_fault(int sig) {
 	raise(sig);
 }
 
+// $BT2G_PIN_CPUS: run the server's threads on that many CPUs of its affinity
+// mask ("auto": as many as the cgroup's CPU quota, cpu.max, when the mask is
+// larger -- the GPU box gives a 16-CPU quota over a 256-CPU mask, and threads
+// spread over 256 CPUs burn the quota in bursts and are then throttled
+// together for the rest of the period).  Off by default.
+void pin_cpus() {
+	const char* e = getenv("BT2G_PIN_CPUS");
+	if(!e || !*e || !strcmp(e, "0")) return;
+	long n = atol(e);
+	if(!strcmp(e, "auto")) {
+		n = 0;
+		if(FILE* f = fopen("/sys/fs/cgroup/cpu.max", "r")) {
+			char q[64] = {0};
+			unsigned long period = 0;
+			if(fscanf(f, "%63s %lu", q, &period) == 2 && strcmp(q, "max") != 0 && period > 0)
+				n = (long)((strtoul(q, nullptr, 10) + period - 1) / period);
+			fclose(f);
+		}
+	}
+	cpu_set_t set;
+	if(n <= 0 || sched_getaffinity(0, sizeof(set), &set) != 0 || CPU_COUNT(&set) <= n) return;
+	cpu_set_t pin;
+	CPU_ZERO(&pin);
+	long k = 0;
+	for(int c = 0; c < CPU_SETSIZE && k < n; c++)
+		if(CPU_ISSET(c, &set)) {
+			CPU_SET(c, &pin);
+			k++;
+		}
+	if(sched_setaffinity(0, sizeof(pin), &pin) == 0) fprintf(stderr, "bt2g batch: threads pinned to %ld CPUs\n", k);
+}
+
 // Environment of the engines, set before any thread starts (static
 // initialiser): the runtime reads it at its first HIP call.
 struct EnvInit {
 	EnvInit() {
+		pin_cpus();
 		setenv("BT2G_SYNC", "poll", 0);
 		const char* hq = getenv("BT2G_HW_QUEUES");
 		long q = hq ? atol(hq) : 16;
