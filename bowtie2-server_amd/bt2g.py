@@ -112,6 +112,8 @@ def lib():
                                       vp, vp, vp, vp]
         L.bt2g_one_mm_gated_dev.argtypes = [vp, vp, vp, u32, vp, u32, vp, C.POINTER(Scoring), vp, u32, vp, vp, vp,
                                             vp, vp]
+        L.bt2g_exact_sweep_1mm.argtypes = [vp, vp, vp, u32, vp, u32, u32, C.c_int, C.c_int, C.c_int, vp,
+                                           C.POINTER(Scoring), u32, vp, vp, vp, vp]
         L.bt2g_reserve_sw.argtypes = [vp, u32, u32]
         L.bt2g_bench_collect_rows_dev.argtypes = [u32, vp, vp, vp, vp, u32, vp, vp, u32, u32, u32, vp, vp, vp, vp, vp,
                                                   u32, vp]
@@ -274,6 +276,21 @@ class Engine:
                                C.byref(sc), int(nofw), int(norc), cap, _ptr(hits), _ptr(cnt), _ptr(ops), _ptr(loads))
         _chk(rc)
         return hits, cnt, ops, loads
+
+    def exact_sweep_1mm(self, reads, quals, lens, minsc, local, nofw=False, norc=False, skip_exact=False, cap=64):
+        """bt2g_exact_sweep_1mm: the sweep and the sweep-gated 1-mm search in one call."""
+        reads, quals, lens = _c(reads, np.uint8), _c(quals, np.uint8), _c(lens, np.uint32)
+        ms = _c(minsc, np.int32)
+        n = len(lens)
+        sweep = np.zeros((n, 8), np.uint32)
+        hits = np.zeros((n, cap), MM1_DTYPE)
+        cnt = np.zeros(n, np.int32)
+        ops = np.zeros(n, np.uint32)
+        sc = scoring(local)
+        _chk(lib().bt2g_exact_sweep_1mm(self.h, _ptr(reads), _ptr(quals), reads.shape[1], _ptr(lens), n, 2, int(nofw),
+                                        int(norc), int(skip_exact), _ptr(ms), C.byref(sc), cap, _ptr(sweep),
+                                        _ptr(hits), _ptr(cnt), _ptr(ops)))
+        return sweep, hits, cnt, ops
 
     def extend(self, reads, lens, ranges):
         """SwDriver::extend per seed-hit range; ranges n x 8 = (read, fw, off, len,

@@ -41,6 +41,9 @@ struct MmBranch {
 // near_state / near_dep / fb_items / fb_st4 / fb_sdep / slot_flag: n*4 each;
 // brq: brq_cap branch records (items meeting a full queue are redone whole by
 // the in-place state machine k_one_mm_q)
+// launch_one_mm's nofw with this bit and a gate: the reference's rule alone
+// (bt2_search.cpp:3649-3650), no skip of reads with an exact end-to-end hit
+const int MM_GATE_KEEP_EXACT = 2;
 void launch_one_mm_q(const DevEbwt& F, const DevEbwt& B, const uint8_t* reads, const uint8_t* quals, uint32_t stride,
                      const uint32_t* lens, uint32_t n, const int32_t* minsc, const bt2g_scoring& sc, int nofw,
                      int norc, const uint32_t* gate, uint32_t cap, uint32_t* items, uint32_t* counters,

@@ -102,14 +102,16 @@ k_one_mm_items(const uint8_t* __restrict__ reads, uint32_t stride, const uint32_
 	uint32_t runmask = 0, ns = 0;
 	if(r < n) {
 		ns = ncount[lane];
-		bool nofw_r = nofw, norc_r = norc, gated_off = false;
+		const bool nofw1 = (nofw & 1) != 0, keep_exact = (nofw & MM_GATE_KEEP_EXACT) != 0;
+		bool nofw_r = nofw1, norc_r = norc, gated_off = false;
 		if(gate) {
 			// bt2_search.cpp:3476-3506, 3640-3667: skipped when an exact end-to-end hit
-			// exists (bestmin == 0); otherwise nofw = !(mineFw <= 1), norc = !(mineRc <= 1)
+			// exists (bestmin == 0; not with MM_GATE_KEEP_EXACT); otherwise nofw =
+			// !(mineFw <= 1), norc = !(mineRc <= 1)
 			const uint32_t mfw = gate[(size_t)r * 8 + 0], mrc = gate[(size_t)r * 8 + 1];
 			const uint32_t bestmin = mfw < mrc ? mfw : mrc;
-			const bool yfw = mfw <= 1 && !nofw, yrc = mrc <= 1 && !norc;
-			gated_off = bestmin == 0 || !(yfw || yrc);
+			const bool yfw = mfw <= 1 && !nofw1, yrc = mrc <= 1 && !norc;
+			gated_off = (bestmin == 0 && !keep_exact) || !(yfw || yrc);
 			nofw_r = !yfw;
 			norc_r = !yrc;
 		}

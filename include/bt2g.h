@@ -172,6 +172,19 @@ int bt2g_one_mm_gated_dev(bt2g_ctx* ctx, const uint8_t* reads, const uint8_t* qu
                           const uint32_t* sweep, uint32_t cap, bt2g_mm1* hits, int32_t* counts, uint32_t* bwops,
                           uint32_t* loads, void* stream);
 
+/* bt2g_exact_sweep and, in the same call, bt2g_one_mm gated per read by the
+ * sweep's result (nofw / norc: the reads' strand options, as for both calls):
+ * one round trip for a read's two up-front searches (bt2_search.cpp:3453-3667).
+ * With yfw = sweep[i*8] <= 1 && !nofw, yrc = sweep[i*8+1] <= 1 && !norc
+ * (bt2_search.cpp:3649-3650), the 1-mm search of read i ran iff yfw || yrc --
+ * and, with skip_exact, min(sweep[i*8], sweep[i*8+1]) != 0 (the rule of
+ * bt2g_one_mm_gated_dev) -- as bt2g_one_mm on that read with nofw = !yfw,
+ * norc = !yrc; counts[i] may exceed cap (no error: the caller asks again). */
+int bt2g_exact_sweep_1mm(bt2g_ctx* ctx, const uint8_t* reads, const uint8_t* quals, uint32_t stride,
+                         const uint32_t* lens, uint32_t n, uint32_t mine_max, int nofw, int norc, int skip_exact,
+                         const int32_t* minsc, const bt2g_scoring* sc, uint32_t cap, uint32_t* sweep,
+                         bt2g_mm1* hits, int32_t* counts, uint32_t* bwops);
+
 /* Ebwt::getOffset (bt2_idx.cpp:150-171): joined-text offset of each SA row.
  * loads (optional): 64-B sides gathered per row. */
 int bt2g_get_offset(bt2g_ctx* ctx, const uint32_t* rows, uint32_t n, uint32_t* offs, uint32_t* loads);

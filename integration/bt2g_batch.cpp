@@ -196,6 +196,7 @@ std::atomic<uint64_t> g_req[K_N], g_calls[K_N], g_call_us[K_N], g_cpu[K_N];
 std::atomic<uint64_t> g_svc_us[K_N];
 std::atomic<uint64_t> g_reads{0}, g_rounds{0}, g_round_us{0}, g_cpu_us{0}, g_gpu_us{0};
 std::atomic<uint64_t> g_dp_spec{0}, g_dp_used{0}, g_dp_reuse{0}, g_dp_miss{0};
+std::atomic<uint64_t> g_mm_pf{0}, g_mm_pf_used{0};   // 1-mm searches prefetched with the sweep / taken
 // rounds per read: total and a histogram (bin b: [2^b, 2^(b+1)))
 std::atomic<uint64_t> g_steps{0}, g_steps_hist[16];
 // reads in flight summed over rounds; drivers' time with no read in flight
@@ -217,6 +218,8 @@ void write_stats() {
 		n += snprintf(buf + n, sizeof(buf) - n, ", \"%s\": [%llu, %llu, %llu, %.1f]", K_NAMES[k],
 		              (unsigned long long)g_req[k].load(), (unsigned long long)g_cpu[k].load(),
 		              (unsigned long long)g_calls[k].load(), g_call_us[k].load() / 1000.0);
+	n += snprintf(buf + n, sizeof(buf) - n, ", \"one_mm_prefetch\": [%llu, %llu]", (unsigned long long)g_mm_pf.load(),
+	              (unsigned long long)g_mm_pf_used.load());
 	n += snprintf(buf + n, sizeof(buf) - n, ", \"svc_busy_ms\": [");
 	for(int k = 0; k < K_N; k++)
 		n += snprintf(buf + n, sizeof(buf) - n, "%s%.1f", k ? ", " : "", g_svc_us[k].load() / 1000.0);
@@ -617,6 +620,12 @@ struct MateRes {
 	int32_t mm_minsc = 0;
 	int mm_nofw = 0, mm_norc = 0;
 	bool mm_asked = false;
+	// the 1-mm search prefetched with the exact sweep (bt2g_exact_sweep_1mm):
+	// pf_want set when the sweep is asked, pf_ok when it ran within the cap;
+	// taken only for the identical request (flags and minsc)
+	bool pf_want = false, pf_ok = false;
+	int pf_nofw = 0, pf_norc = 0;
+	int32_t pf_minsc = 0;
 	std::vector<bt2g_mm1> mm;
 	int32_t mm_cnt = 0;
 	uint32_t mm_ops = 0;
@@ -790,6 +799,12 @@ struct Svc {
 
 std::atomic<uint64_t> g_stamp{0};
 
+// $BT2G_MM_PREFETCH=0: no 1-mm search with the exact sweep
+bool mm_prefetch_on() {
+	static const bool on = [] { const char* e = getenv("BT2G_MM_PREFETCH"); return !(e && *e == '0'); }();
+	return on;
+}
+
 bool kprof_on() {
 	static const bool on = [] { const char* e = getenv("BT2G_KPROF"); return e && *e == '1'; }();
 	return on;
@@ -878,12 +893,18 @@ void Svc::call_exact(std::vector<Rq>& v) {
 	if(v.empty()) return;
 	thread_local Pack pk;
 	thread_local std::vector<uint32_t> out;
-	for(int g = 0; g < 4; g++) {
-		const bool nf = (g & 2) != 0, nr = (g & 1) != 0;
+	thread_local std::vector<int32_t> ms, cnt;
+	thread_local std::vector<uint32_t> ops;
+	thread_local std::vector<bt2g_mm1> h;
+	const uint32_t cap = 16;
+	for(int g = 0; g < 8; g++) {
+		// (reads grouped by their strand options, and by whether their 1-mm search
+		// rides along: bt2g_exact_sweep_1mm)
+		const bool nf = (g & 2) != 0, nr = (g & 1) != 0, pf = (g & 4) != 0;
 		std::vector<Rq> sub;
 		uint32_t stride = 1;
 		for(const Rq& q : v)
-			if(q.s->nofw[q.m] == nf && q.s->norc[q.m] == nr) {
+			if(q.s->nofw[q.m] == nf && q.s->norc[q.m] == nr && q.s->mr[q.m].pf_want == pf) {
 				sub.push_back(q);
 				stride = std::max<uint32_t>(stride, (uint32_t)q.s->rdlens[q.m]);
 			}
@@ -892,8 +913,36 @@ void Svc::call_exact(std::vector<Rq>& v) {
 		for(const Rq& q : sub) pk.add(*q.s->rds[q.m]);
 		out.resize(8 * sub.size());
 		const uint64_t t0 = now_us();
-		int rc = bt2g_exact_sweep(ctx, pk.codes.data(), pk.stride, pk.lens.data(), pk.n(), 2, nf ? 1 : 0, nr ? 1 : 0,
-		                          out.data());
+		int rc;
+		if(pf) {
+			const size_t n = sub.size();
+			ms.resize(n);
+			cnt.resize(n);
+			ops.resize(n);
+			h.resize(n * (size_t)cap);
+			for(size_t i = 0; i < n; i++) ms[i] = sub[i].s->mr[sub[i].m].pf_minsc;
+			rc = bt2g_exact_sweep_1mm(ctx, pk.codes.data(), pk.quals.data(), pk.stride, pk.lens.data(), (uint32_t)n, 2,
+			                          nf ? 1 : 0, nr ? 1 : 0, 0, ms.data(), bsc, cap, out.data(), h.data(), cnt.data(),
+			                          ops.data());
+			for(size_t i = 0; i < n && !rc; i++) {
+				MateRes& x = sub[i].s->mr[sub[i].m];
+				// the gate bt2g_exact_sweep_1mm applied (include/bt2g.h)
+				const uint32_t mfw = out[8 * i], mrc = out[8 * i + 1];
+				const bool yfw = mfw <= 1 && !nf, yrc = mrc <= 1 && !nr;
+				const bool ran = yfw || yrc;
+				x.pf_ok = ran && cnt[i] <= (int32_t)cap;
+				if(!x.pf_ok) continue;
+				g_mm_pf++;
+				x.pf_nofw = yfw ? 0 : 1;
+				x.pf_norc = yrc ? 0 : 1;
+				x.mm_cnt = cnt[i];
+				x.mm_ops = ops[i];
+				x.mm.assign(&h[i * cap], &h[i * cap] + cnt[i]);
+			}
+		} else {
+			rc = bt2g_exact_sweep(ctx, pk.codes.data(), pk.stride, pk.lens.data(), pk.n(), 2, nf ? 1 : 0, nr ? 1 : 0,
+			                      out.data());
+		}
 		g_call_us[K_EXACT] += now_us() - t0;
 		g_calls[K_EXACT]++;
 		if(rc) die("bt2g_exact_sweep", rc);
@@ -2632,6 +2681,16 @@ void Driver::step_read(Slot& s) {
 				if(engine_read(s, (int)m)) {
 					rq[K_EXACT].push_back(Rq{&s, (int)m});
 					s.mr[m].sweep_asked = true;
+					{
+						// the 1-mm search rides with the sweep when the engine takes it
+						// (its gate is the sweep's result, bt2_search.cpp:3649-3650)
+						MateRes& x = s.mr[m];
+						x.pf_ok = false;
+						x.pf_want = R_do1mmUpFront && !R_seedSumm && bsc_ok && s.minsc[m] >= std::numeric_limits<int32_t>::min() &&
+						            s.minsc[m] <= std::numeric_limits<int32_t>::max() && R_localAlign == !sc->monotone &&
+						            mm_prefetch_on();
+						x.pf_minsc = (int32_t)s.minsc[m];
+					}
 					s.round_off[m] = 0;
 					prefetch_seeds(s, (int)m);
 					asked = true;
@@ -2726,8 +2785,13 @@ void Driver::step_read(Slot& s) {
 						x.mm_norc = s.yrc[m] ? 0 : 1;
 						x.mm_minsc = (int32_t)s.minsc[m];
 						x.mm_asked = true;
-						rq[K_1MM].push_back(Rq{&s, (int)m});
-						asked = true;
+						if(x.pf_ok && x.pf_nofw == x.mm_nofw && x.pf_norc == x.mm_norc && x.pf_minsc == x.mm_minsc) {
+							x.pf_ok = false;               // (its hits are in x.mm already)
+							g_mm_pf_used++;
+						} else {
+							rq[K_1MM].push_back(Rq{&s, (int)m});
+							asked = true;
+						}
 					} else {
 						al.oneMmSearch(ebwtFw, ebwtBw, *s.rds[m], *sc, s.minsc[m], !s.yfw[m], !s.yrc[m], R_localAlign, false,
 						               true, s.shs[m], sdm);

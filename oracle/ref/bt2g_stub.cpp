@@ -142,6 +142,26 @@ int bt2g_one_mm(bt2g_ctx* c, const uint8_t* reads, const uint8_t* quals, uint32_
 	return rc;
 }
 
+int bt2g_exact_sweep_1mm(bt2g_ctx* c, const uint8_t* reads, const uint8_t* quals, uint32_t stride,
+                         const uint32_t* lens, uint32_t n, uint32_t mine_max, int nofw, int norc, int skip_exact,
+                         const int32_t* minsc, const bt2g_scoring* sc, uint32_t cap, uint32_t* sweep,
+                         bt2g_mm1* hits, int32_t* counts, uint32_t* bwops) {
+	int rc = bt2g_exact_sweep(c, reads, stride, lens, n, mine_max, nofw, norc, sweep);
+	if(rc) return rc;
+	for(uint32_t i = 0; i < n; i++) {
+		// the gate of bt2g_one_mm_gated_dev (fm_one_mm.hip k_one_mm_items)
+		const uint32_t mfw = sweep[8 * (size_t)i], mrc = sweep[8 * (size_t)i + 1];
+		const bool yfw = mfw <= 1 && !nofw, yrc = mrc <= 1 && !norc;
+		counts[i] = 0;
+		bwops[i] = 0;
+		if(((mfw < mrc ? mfw : mrc) == 0 && skip_exact) || !(yfw || yrc)) continue;
+		rc = bt2g_one_mm(c, reads + (size_t)i * stride, quals + (size_t)i * stride, stride, lens + i, 1, minsc + i, sc,
+		                 !yfw, !yrc, cap, hits + (size_t)i * cap, counts + i, bwops + i, nullptr);
+		if(rc && rc != BT2G_ERR_OVERFLOW) return rc;
+	}
+	return BT2G_OK;
+}
+
 int bt2g_seed_search(bt2g_ctx* c, const uint8_t* reads, uint32_t stride, const uint32_t* lens, uint32_t n,
                      uint32_t seedlen, uint32_t interval, uint32_t offset, uint32_t maxseeds, uint32_t* out,
                      int32_t* nseeds, uint32_t* bwops, uint32_t*) {

@@ -148,3 +148,30 @@ def test_open_from_files_and_edge_cases(tmp_path):
         assert (a[:, 0] == 0).all() and (a[:, 2] == 0).all()
         b = e.exact_sweep(g["reads"], g["lens"])
         assert np.array_equal(a[:, [1, 4, 5]], b[:, [1, 4, 5]])
+
+
+@pytest.mark.parametrize("skip_exact", [False, True])
+@pytest.mark.parametrize("strand", ["both", "norc"])
+def test_exact_sweep_1mm_fused(engines, skip_exact, strand):
+    """bt2g_exact_sweep_1mm (the batch driver's up-front searches in one call)
+    equals bt2g_exact_sweep, then bt2g_one_mm on each read the gate lets through
+    with nofw = !(mineFw <= 1), norc = !(mineRc <= 1) (bt2_search.cpp:3649-3667):
+    sweep, hit lists in discovery order, counts and bwops."""
+    g = load_golden("fm_synth")
+    e = engines["synth"]
+    norc = strand == "norc"
+    reads, quals, lens, ms = g["reads"], g["quals"], g["lens"], g["mmminsc_ee"]
+    sw, hits, cnt, ops = e.exact_sweep_1mm(reads, quals, lens, ms, False, norc=norc, skip_exact=skip_exact)
+    assert np.array_equal(sw, e.exact_sweep(reads, lens, norc=norc))
+    ran = 0
+    for i in range(len(lens)):
+        yfw, yrc = sw[i, 0] <= 1, sw[i, 1] <= 1 and not norc
+        if (skip_exact and min(sw[i, 0], sw[i, 1]) == 0) or not (yfw or yrc):
+            assert cnt[i] == 0, i
+            continue
+        h1, c1, o1, _ = e.one_mm(reads[i:i + 1], quals[i:i + 1], lens[i:i + 1], ms[i:i + 1], False,
+                                 nofw=not yfw, norc=not yrc)
+        assert cnt[i] == c1[0] and ops[i] == o1[0], i
+        assert np.array_equal(hits[i, :cnt[i]], h1[0, :c1[0]]), i
+        ran += 1
+    assert ran > 20
