@@ -113,7 +113,7 @@ def lib():
         L.bt2g_one_mm_gated_dev.argtypes = [vp, vp, vp, u32, vp, u32, vp, C.POINTER(Scoring), vp, u32, vp, vp, vp,
                                             vp, vp]
         L.bt2g_exact_sweep_1mm.argtypes = [vp, vp, vp, u32, vp, u32, u32, C.c_int, C.c_int, C.c_int, vp,
-                                           C.POINTER(Scoring), u32, vp, vp, vp, vp]
+                                           C.POINTER(Scoring), u32, vp, vp, vp, vp, u32, vp]
         L.bt2g_reserve_sw.argtypes = [vp, u32, u32]
         L.bt2g_bench_collect_rows_dev.argtypes = [u32, vp, vp, vp, vp, u32, vp, vp, u32, u32, u32, vp, vp, vp, vp, vp,
                                                   u32, vp]
@@ -277,8 +277,10 @@ class Engine:
         _chk(rc)
         return hits, cnt, ops, loads
 
-    def exact_sweep_1mm(self, reads, quals, lens, minsc, local, nofw=False, norc=False, skip_exact=False, cap=64):
-        """bt2g_exact_sweep_1mm: the sweep and the sweep-gated 1-mm search in one call."""
+    def exact_sweep_1mm(self, reads, quals, lens, minsc, local, nofw=False, norc=False, skip_exact=False, cap=64,
+                        off_cap=0):
+        """bt2g_exact_sweep_1mm: the sweep and the sweep-gated 1-mm search in one call
+        (off_cap > 0: also the offsets of the small ranges' rows, returned fifth)."""
         reads, quals, lens = _c(reads, np.uint8), _c(quals, np.uint8), _c(lens, np.uint32)
         ms = _c(minsc, np.int32)
         n = len(lens)
@@ -287,10 +289,11 @@ class Engine:
         cnt = np.zeros(n, np.int32)
         ops = np.zeros(n, np.uint32)
         sc = scoring(local)
+        offs = np.zeros((n, 2 + cap, off_cap), np.uint32) if off_cap else None
         _chk(lib().bt2g_exact_sweep_1mm(self.h, _ptr(reads), _ptr(quals), reads.shape[1], _ptr(lens), n, 2, int(nofw),
                                         int(norc), int(skip_exact), _ptr(ms), C.byref(sc), cap, _ptr(sweep),
-                                        _ptr(hits), _ptr(cnt), _ptr(ops)))
-        return sweep, hits, cnt, ops
+                                        _ptr(hits), _ptr(cnt), _ptr(ops), off_cap, _ptr(offs) if off_cap else None))
+        return (sweep, hits, cnt, ops, offs) if off_cap else (sweep, hits, cnt, ops)
 
     def extend(self, reads, lens, ranges):
         """SwDriver::extend per seed-hit range; ranges n x 8 = (read, fw, off, len,

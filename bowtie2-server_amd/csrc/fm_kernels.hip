@@ -316,6 +316,59 @@ void launch_get_offset(const DevEbwt& e, const uint32_t* rows, uint32_t n, uint3
 	hipLaunchKernelGGL(k_get_offset, dim3((n + 255) / 256), dim3(256), 0, st, e, rows, n, offs, loads);
 }
 
+// The offsets of the rows of every small SA range an up-front search reported
+// (bt2g_exact_sweep_1mm): the exact end-to-end ranges of each strand (sweep
+// n x 8: mine, range) and the 1-mm hits (hits n x cap, counts); one lane per
+// (read, range, row), ranges of more than off_cap rows skipped.  offs: n x
+// (2 + cap) x off_cap, BT2G_OFF_MASK where no row.  The same walk as
+// k_get_offset (Ebwt::getOffset, bt2_idx.cpp:150-171).
+__global__ void __launch_bounds__(256)
+k_range_offsets(DevEbwt e, const uint32_t* __restrict__ sweep, const bt2g_mm1* __restrict__ hits,
+                const int32_t* __restrict__ counts, uint32_t n, uint32_t cap, uint32_t off_cap,
+                uint32_t* __restrict__ offs) {
+	const uint64_t gid = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+	const uint64_t per = (uint64_t)(2u + cap) * off_cap;
+	if(gid >= (uint64_t)n * per) return;
+	const uint32_t i = (uint32_t)(gid / per), slot = (uint32_t)((gid % per) / off_cap), j = (uint32_t)(gid % off_cap);
+	uint32_t top = 0, bot = 0;
+	if(slot < 2) {
+		const uint32_t* w = sweep + (size_t)i * 8;
+		if(w[slot] == 0) { top = w[2 + 2 * slot]; bot = w[3 + 2 * slot]; }
+	} else if(hits && (int32_t)(slot - 2) < (counts[i] < (int32_t)cap ? counts[i] : (int32_t)cap)) {
+		const bt2g_mm1 h = hits[(size_t)i * cap + (slot - 2)];
+		top = h.top;
+		bot = h.bot;
+	}
+	uint32_t res = BT2G_OFF_MASK;
+	if(bot > top && bot - top <= off_cap && j < bot - top) {
+		uint32_t row = top + j;
+		const uint32_t mask = BT2G_OFF_MASK << e.off_rate;
+		uint32_t jumps = 0;
+		if(row == e.zoff) res = 0;
+		else if((row & mask) == row) res = e.offs[row >> e.off_rate];
+		else {
+			for(;;) {
+				SideData sd;
+				load_side(e, row / 192u, sd);
+				const int c = side_rowL(sd, row % 192u);
+				row = occ1(e, sd, row, c);
+				jumps++;
+				if(row == e.zoff) { res = jumps; break; }
+				if((row & mask) == row) { res = jumps + e.offs[row >> e.off_rate]; break; }
+			}
+		}
+	}
+	offs[gid] = res;
+}
+
+void launch_range_offsets(const DevEbwt& e, const uint32_t* sweep, const bt2g_mm1* hits, const int32_t* counts,
+                          uint32_t n, uint32_t cap, uint32_t off_cap, uint32_t* offs, hipStream_t st) {
+	const uint64_t tot = (uint64_t)n * (2u + cap) * off_cap;
+	if(!tot) return;
+	hipLaunchKernelGGL(k_range_offsets, dim3((uint32_t)((tot + 255) / 256)), dim3(256), 0, st, e, sweep, hits, counts,
+	                   n, cap, off_cap, offs);
+}
+
 // --------------------------------------------------------------------------
 // SwDriver::extend (aligner_sw_driver.cpp:299-483): one lane = one seed-hit
 // range.  Left: the range walks leftward in the forward index while it keeps

@@ -179,11 +179,16 @@ int bt2g_one_mm_gated_dev(bt2g_ctx* ctx, const uint8_t* reads, const uint8_t* qu
  * (bt2_search.cpp:3649-3650), the 1-mm search of read i ran iff yfw || yrc --
  * and, with skip_exact, min(sweep[i*8], sweep[i*8+1]) != 0 (the rule of
  * bt2g_one_mm_gated_dev) -- as bt2g_one_mm on that read with nofw = !yfw,
- * norc = !yrc; counts[i] may exceed cap (no error: the caller asks again). */
+ * norc = !yrc; counts[i] may exceed cap (no error: the caller asks again).
+ * offs (optional, n x (2 + cap) x off_cap): Ebwt::getOffset of every row of
+ * the exact ranges (slots 0, 1: fw, rc, when their mine is 0) and of the
+ * stored 1-mm hits' ranges (slots 2..), for ranges of at most off_cap rows;
+ * BT2G_OFF_MASK elsewhere -- the rows the extension of those hits resolves
+ * first (GroupWalk2S, group_walk.h:862-1216), without a round trip. */
 int bt2g_exact_sweep_1mm(bt2g_ctx* ctx, const uint8_t* reads, const uint8_t* quals, uint32_t stride,
                          const uint32_t* lens, uint32_t n, uint32_t mine_max, int nofw, int norc, int skip_exact,
                          const int32_t* minsc, const bt2g_scoring* sc, uint32_t cap, uint32_t* sweep,
-                         bt2g_mm1* hits, int32_t* counts, uint32_t* bwops);
+                         bt2g_mm1* hits, int32_t* counts, uint32_t* bwops, uint32_t off_cap, uint32_t* offs);
 
 /* Ebwt::getOffset (bt2_idx.cpp:150-171): joined-text offset of each SA row.
  * loads (optional): 64-B sides gathered per row. */

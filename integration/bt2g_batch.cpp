@@ -197,6 +197,7 @@ std::atomic<uint64_t> g_svc_us[K_N];
 std::atomic<uint64_t> g_reads{0}, g_rounds{0}, g_round_us{0}, g_cpu_us{0}, g_gpu_us{0};
 std::atomic<uint64_t> g_dp_spec{0}, g_dp_used{0}, g_dp_reuse{0}, g_dp_miss{0};
 std::atomic<uint64_t> g_mm_pf{0}, g_mm_pf_used{0};   // 1-mm searches prefetched with the sweep / taken
+std::atomic<uint64_t> g_rows_pf{0};                   // SA rows resolved with the sweep
 // rounds per read: total and a histogram (bin b: [2^b, 2^(b+1)))
 std::atomic<uint64_t> g_steps{0}, g_steps_hist[16];
 // reads in flight summed over rounds; drivers' time with no read in flight
@@ -218,8 +219,9 @@ void write_stats() {
 		n += snprintf(buf + n, sizeof(buf) - n, ", \"%s\": [%llu, %llu, %llu, %.1f]", K_NAMES[k],
 		              (unsigned long long)g_req[k].load(), (unsigned long long)g_cpu[k].load(),
 		              (unsigned long long)g_calls[k].load(), g_call_us[k].load() / 1000.0);
-	n += snprintf(buf + n, sizeof(buf) - n, ", \"one_mm_prefetch\": [%llu, %llu]", (unsigned long long)g_mm_pf.load(),
-	              (unsigned long long)g_mm_pf_used.load());
+	n += snprintf(buf + n, sizeof(buf) - n, ", \"one_mm_prefetch\": [%llu, %llu], \"rows_prefetched\": %llu",
+	              (unsigned long long)g_mm_pf.load(), (unsigned long long)g_mm_pf_used.load(),
+	              (unsigned long long)g_rows_pf.load());
 	n += snprintf(buf + n, sizeof(buf) - n, ", \"svc_busy_ms\": [");
 	for(int k = 0; k < K_N; k++)
 		n += snprintf(buf + n, sizeof(buf) - n, "%s%.1f", k ? ", " : "", g_svc_us[k].load() / 1000.0);
@@ -614,6 +616,7 @@ struct MateRes {
 	MateRes() {
 		mm.reserve(64);
 		sd_out.reserve(256);
+		pf_rows.reserve(160);
 	}
 	uint32_t sweep[8] = {0};
 	bool sweep_asked = false;
@@ -626,6 +629,9 @@ struct MateRes {
 	bool pf_want = false, pf_ok = false;
 	int pf_nofw = 0, pf_norc = 0;
 	int32_t pf_minsc = 0;
+	// (row, offset) of the rows of the small exact / 1-mm ranges, resolved in the
+	// same call, sorted by row: resolve_rows_request takes them from here
+	std::vector<std::pair<uint32_t, uint32_t>> pf_rows;
 	std::vector<bt2g_mm1> mm;
 	int32_t mm_cnt = 0;
 	uint32_t mm_ops = 0;
@@ -894,9 +900,9 @@ void Svc::call_exact(std::vector<Rq>& v) {
 	thread_local Pack pk;
 	thread_local std::vector<uint32_t> out;
 	thread_local std::vector<int32_t> ms, cnt;
-	thread_local std::vector<uint32_t> ops;
+	thread_local std::vector<uint32_t> ops, offs;
 	thread_local std::vector<bt2g_mm1> h;
-	const uint32_t cap = 16;
+	const uint32_t cap = 16, off_cap = 8;
 	for(int g = 0; g < 8; g++) {
 		// (reads grouped by their strand options, and by whether their 1-mm search
 		// rides along: bt2g_exact_sweep_1mm)
@@ -920,12 +926,31 @@ void Svc::call_exact(std::vector<Rq>& v) {
 			cnt.resize(n);
 			ops.resize(n);
 			h.resize(n * (size_t)cap);
+			const size_t per = (size_t)(2 + cap) * off_cap;
+			offs.resize(n * per);
 			for(size_t i = 0; i < n; i++) ms[i] = sub[i].s->mr[sub[i].m].pf_minsc;
 			rc = bt2g_exact_sweep_1mm(ctx, pk.codes.data(), pk.quals.data(), pk.stride, pk.lens.data(), (uint32_t)n, 2,
 			                          nf ? 1 : 0, nr ? 1 : 0, 0, ms.data(), bsc, cap, out.data(), h.data(), cnt.data(),
-			                          ops.data());
+			                          ops.data(), off_cap, offs.data());
 			for(size_t i = 0; i < n && !rc; i++) {
 				MateRes& x = sub[i].s->mr[sub[i].m];
+				// the resolved rows of the small ranges (slots: fw, rc exact ranges, 1-mm hits)
+				x.pf_rows.clear();
+				for(uint32_t slot = 0; slot < 2 + cap; slot++) {
+					uint32_t top = 0, bot = 0;
+					if(slot < 2) {
+						if(out[8 * i + slot] == 0) { top = out[8 * i + 2 + 2 * slot]; bot = out[8 * i + 3 + 2 * slot]; }
+					} else if((int32_t)(slot - 2) < std::min<int32_t>(cnt[i], (int32_t)cap)) {
+						top = h[i * cap + slot - 2].top;
+						bot = h[i * cap + slot - 2].bot;
+					}
+					if(bot <= top || bot - top > off_cap) continue;
+					for(uint32_t j = 0; j < bot - top; j++) {
+						const uint32_t o = offs[i * per + (size_t)slot * off_cap + j];
+						if(o != OFF_MASK) x.pf_rows.emplace_back(top + j, o);
+					}
+				}
+				std::sort(x.pf_rows.begin(), x.pf_rows.end());
 				// the gate bt2g_exact_sweep_1mm applied (include/bt2g.h)
 				const uint32_t mfw = out[8 * i], mrc = out[8 * i + 1];
 				const bool yfw = mfw <= 1 && !nf, yrc = mrc <= 1 && !nr;
@@ -1500,11 +1525,27 @@ void Driver::resolve_rows_request(Slot& s) {
 	const size_t MAX_ROWS = 8192;          // per read (the rest: Ebwt::getOffset in advanceElement)
 	s.off_rows.clear();
 	s.off_where.clear();
+	const auto& p0 = s.mr[0].pf_rows;
+	const auto& p1 = s.mr[1].pf_rows;
+	auto known = [](const std::vector<std::pair<uint32_t, uint32_t>>& p, uint32_t row, uint32_t& off) {
+		auto it = std::lower_bound(p.begin(), p.end(), std::make_pair(row, 0u));
+		if(it == p.end() || it->first != row) return false;
+		off = it->second;
+		return true;
+	};
 	for(size_t r = 0; r < s.tab.gw.size(); r++) {
 		GwRange& x = s.tab.gw[r];
 		for(size_t j = 0; j < x.size && s.off_rows.size() < MAX_ROWS; j++)
 			if(x.offs[j] == OFF_MASK) {
-				s.off_rows.push_back((uint32_t)(x.topf + j));
+				const uint32_t row = (uint32_t)(x.topf + j);
+				uint32_t off;
+				// a row the exact sweep / 1-mm call already resolved (its small ranges)
+				if((!p0.empty() && known(p0, row, off)) || (!p1.empty() && known(p1, row, off))) {
+					x.offs[j] = off;
+					g_rows_pf++;
+					continue;
+				}
+				s.off_rows.push_back(row);
 				s.off_where.emplace_back(r, j);
 			}
 	}

@@ -145,7 +145,7 @@ int bt2g_one_mm(bt2g_ctx* c, const uint8_t* reads, const uint8_t* quals, uint32_
 int bt2g_exact_sweep_1mm(bt2g_ctx* c, const uint8_t* reads, const uint8_t* quals, uint32_t stride,
                          const uint32_t* lens, uint32_t n, uint32_t mine_max, int nofw, int norc, int skip_exact,
                          const int32_t* minsc, const bt2g_scoring* sc, uint32_t cap, uint32_t* sweep,
-                         bt2g_mm1* hits, int32_t* counts, uint32_t* bwops) {
+                         bt2g_mm1* hits, int32_t* counts, uint32_t* bwops, uint32_t off_cap, uint32_t* offs) {
 	int rc = bt2g_exact_sweep(c, reads, stride, lens, n, mine_max, nofw, norc, sweep);
 	if(rc) return rc;
 	for(uint32_t i = 0; i < n; i++) {
@@ -158,6 +158,26 @@ int bt2g_exact_sweep_1mm(bt2g_ctx* c, const uint8_t* reads, const uint8_t* quals
 		rc = bt2g_one_mm(c, reads + (size_t)i * stride, quals + (size_t)i * stride, stride, lens + i, 1, minsc + i, sc,
 		                 !yfw, !yrc, cap, hits + (size_t)i * cap, counts + i, bwops + i, nullptr);
 		if(rc && rc != BT2G_ERR_OVERFLOW) return rc;
+	}
+	if(offs) {
+		// the small ranges' rows (include/bt2g.h), by the reference's getOffset
+		const size_t per = (size_t)(2 + cap) * off_cap;
+		for(uint32_t i = 0; i < n; i++) {
+			for(size_t k = 0; k < per; k++) offs[i * per + k] = 0xffffffffu;
+			for(uint32_t slot = 0; slot < 2 + cap; slot++) {
+				uint32_t top = 0, bot = 0;
+				if(slot < 2) {
+					if(sweep[8 * (size_t)i + slot] == 0) { top = sweep[8 * (size_t)i + 2 + 2 * slot]; bot = sweep[8 * (size_t)i + 3 + 2 * slot]; }
+				} else if((int32_t)(slot - 2) < std::min<int32_t>(counts[i], (int32_t)cap)) {
+					top = hits[(size_t)i * cap + slot - 2].top;
+					bot = hits[(size_t)i * cap + slot - 2].bot;
+				}
+				if(bot <= top || bot - top > off_cap) continue;
+				std::vector<uint32_t> rows(bot - top);
+				for(uint32_t j = 0; j < bot - top; j++) rows[j] = top + j;
+				bt2g_get_offset(c, rows.data(), (uint32_t)rows.size(), offs + i * per + (size_t)slot * off_cap, nullptr);
+			}
+		}
 	}
 	return BT2G_OK;
 }
