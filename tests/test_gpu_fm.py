@@ -161,8 +161,24 @@ def test_exact_sweep_1mm_fused(engines, skip_exact, strand):
     e = engines["synth"]
     norc = strand == "norc"
     reads, quals, lens, ms = g["reads"], g["quals"], g["lens"], g["mmminsc_ee"]
-    sw, hits, cnt, ops = e.exact_sweep_1mm(reads, quals, lens, ms, False, norc=norc, skip_exact=skip_exact)
+    sw, hits, cnt, ops, offs = e.exact_sweep_1mm(reads, quals, lens, ms, False, norc=norc, skip_exact=skip_exact,
+                                                 cap=16, off_cap=8)
     assert np.array_equal(sw, e.exact_sweep(reads, lens, norc=norc))
+    # the small ranges' rows: Ebwt::getOffset of each (bt2g_get_offset), BT2G_OFF_MASK elsewhere
+    want = np.full(offs.shape, 0xFFFFFFFF, np.uint32)
+    rows, where = [], []
+    for i in range(len(lens)):
+        rg = [(sw[i, 2], sw[i, 3]) if sw[i, 0] == 0 else (0, 0), (sw[i, 4], sw[i, 5]) if sw[i, 1] == 0 else (0, 0)]
+        rg += [(int(hits[i, k]["top"]), int(hits[i, k]["bot"])) for k in range(min(cnt[i], 16))]
+        for slot, (t, b) in enumerate(rg):
+            if 0 < int(b) - int(t) <= 8:
+                for j in range(int(b) - int(t)):
+                    rows.append(int(t) + j)
+                    where.append((i, slot, j))
+    got_offs, _ = e.get_offset(np.array(rows, np.uint32))
+    for (i, slot, j), o in zip(where, got_offs):
+        want[i, slot, j] = o
+    assert np.array_equal(offs, want) and len(rows) > 50
     ran = 0
     for i in range(len(lens)):
         yfw, yrc = sw[i, 0] <= 1, sw[i, 1] <= 1 and not norc
@@ -170,8 +186,9 @@ def test_exact_sweep_1mm_fused(engines, skip_exact, strand):
             assert cnt[i] == 0, i
             continue
         h1, c1, o1, _ = e.one_mm(reads[i:i + 1], quals[i:i + 1], lens[i:i + 1], ms[i:i + 1], False,
-                                 nofw=not yfw, norc=not yrc)
+                                 nofw=not yfw, norc=not yrc, cap=16)
         assert cnt[i] == c1[0] and ops[i] == o1[0], i
         assert np.array_equal(hits[i, :cnt[i]], h1[0, :c1[0]]), i
         ran += 1
-    assert ran > 20
+    # (the bench rule with --norc: the skipped strand's mine is 0, so every read is skipped)
+    assert ran > 20 or (norc and skip_exact)
