@@ -105,6 +105,7 @@ def lib():
         L.bt2g_exact_sweep.argtypes = [vp, vp, u32, vp, u32, u32, C.c_int, C.c_int, vp]
         L.bt2g_exact_sweep_dev.argtypes = [vp, vp, u32, vp, u32, u32, C.c_int, C.c_int, vp, vp]
         L.bt2g_seed_search.argtypes = [vp, vp, u32, vp, u32, u32, u32, u32, u32, vp, vp, vp, vp]
+        L.bt2g_seed_search_ext.argtypes = [vp, vp, u32, vp, u32, u32, u32, u32, u32, vp, vp, vp, vp, vp, u32, vp]
         L.bt2g_seed_search_dev.argtypes = [vp, vp, u32, vp, u32, u32, u32, u32, u32, vp, vp, vp, vp, vp]
         L.bt2g_one_mm.argtypes = [vp, vp, vp, u32, vp, u32, vp, C.POINTER(Scoring), C.c_int, C.c_int, u32, vp, vp,
                                   vp, vp]
@@ -262,6 +263,22 @@ class Engine:
         _chk(lib().bt2g_seed_search(self.h, _ptr(reads), reads.shape[1], _ptr(lens), n, seedlen, interval, offset,
                                     maxseeds, _ptr(out), _ptr(ns), _ptr(ops), _ptr(loads)))
         return out, ns, ops, loads
+
+    def seed_search_ext(self, reads, lens, seedlen, interval, offset, maxseeds=64, off_cap=8):
+        """bt2g_seed_search_ext: seed_search plus, per seed range, SwDriver::extend
+        (ext n x 2 x maxseeds x 4) and the offsets of its rows when it has at most
+        off_cap of them (offs n x 2 x maxseeds x off_cap)."""
+        reads, lens = _c(reads, np.uint8), _c(lens, np.uint32)
+        n = len(lens)
+        out = np.zeros((n, 2, maxseeds, 4), np.uint32)
+        ns = np.zeros(n, np.int32)
+        ops = np.zeros(n, np.uint32)
+        ext = np.zeros((n, 2, maxseeds, 4), np.uint32)
+        offs = np.zeros((n, 2, maxseeds, max(off_cap, 1)), np.uint32)
+        _chk(lib().bt2g_seed_search_ext(self.h, _ptr(reads), reads.shape[1], _ptr(lens), n, seedlen, interval, offset,
+                                        maxseeds, _ptr(out), _ptr(ns), _ptr(ops), None, _ptr(ext), off_cap,
+                                        _ptr(offs) if off_cap else None))
+        return out, ns, ops, ext, offs
 
     def one_mm(self, reads, quals, lens, minsc, local, nofw=False, norc=False, cap=64):
         reads, quals, lens = _c(reads, np.uint8), _c(quals, np.uint8), _c(lens, np.uint32)

@@ -1335,6 +1335,41 @@ int bt2g_seed_search(bt2g_ctx* c, const uint8_t* reads, uint32_t stride, const u
 	return t.finish();
 }
 
+int bt2g_seed_search_ext(bt2g_ctx* c, const uint8_t* reads, uint32_t stride, const uint32_t* lens, uint32_t n,
+                         uint32_t seedlen, uint32_t interval, uint32_t offset, uint32_t maxseeds, uint32_t* out,
+                         int32_t* nseeds, uint32_t* bwops, uint32_t* loads, bt2g_ext_out* ext, uint32_t off_cap,
+                         uint32_t* offs) {
+	if(!c) return fail(BT2G_ERR_ARG, "null ctx");
+	if(offs && (!c->fw.offs || off_cap == 0)) return fail(BT2G_ERR_ARG, "offsets need the SA sample and off_cap > 0");
+	HIPCHK(hipSetDevice(c->device));
+	Tmp t(c);
+	uint8_t* dr;
+	uint32_t *dl, *dout, *dops, *dld = nullptr, *doffs = nullptr;
+	bt2g_ext_out* dext = nullptr;
+	int32_t* dns;
+	int rc;
+	const size_t nr = (size_t)n * 2 * maxseeds;
+	if((rc = t.up(&dr, reads, (size_t)n * stride)) || (rc = t.up(&dl, lens, n)) || (rc = t.out(&dout, out, nr * 4)) ||
+	   (rc = t.out(&dns, nseeds, n)) || (rc = t.out(&dops, bwops, n)))
+		return rc;
+	if(loads && (rc = t.out(&dld, loads, n))) return rc;
+	if(ext && (rc = t.out(&dext, ext, nr))) return rc;
+	if(offs && (rc = t.out(&doffs, offs, nr * off_cap))) return rc;
+	if((rc = t.send())) return rc;
+	if((rc = bt2g_seed_search_dev(c, dr, stride, dl, n, seedlen, interval, offset, maxseeds, dout, dns, dops, dld,
+	                              c->stream)))
+		return rc;
+	if(n && (dext || doffs)) {
+		ProfScope ps(c, 3, c->stream);
+		if(dext)
+			launch_seed_extend(c->fw, c->bw, c->bw.sides != nullptr, dr, stride, dl, n, seedlen, interval, offset,
+			                   maxseeds, dout, dext, c->stream);
+		if(doffs) launch_seed_offsets(c->fw, dout, nr, off_cap, doffs, c->stream);
+		HIPCHK(hipGetLastError());
+	}
+	return t.finish();
+}
+
 int bt2g_one_mm(bt2g_ctx* c, const uint8_t* reads, const uint8_t* quals, uint32_t stride, const uint32_t* lens,
                 uint32_t n, const int32_t* minsc, const bt2g_scoring* sc, int nofw, int norc, uint32_t cap,
                 bt2g_mm1* hits, int32_t* counts, uint32_t* bwops, uint32_t* loads) {

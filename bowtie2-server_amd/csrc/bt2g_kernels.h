@@ -66,6 +66,11 @@ void launch_extend(const DevEbwt& F, const DevEbwt& B, int has_bw, const uint8_t
 void launch_get_offset(const DevEbwt& e, const uint32_t* rows, uint32_t n, uint32_t* offs, uint32_t* loads,
                        hipStream_t st);
 // offsets of the rows of the small ranges of an exact sweep + 1-mm search (bt2g_exact_sweep_1mm)
+void launch_seed_offsets(const DevEbwt& e, const uint32_t* out, uint64_t nrange, uint32_t off_cap, uint32_t* offs,
+                         hipStream_t st);
+void launch_seed_extend(const DevEbwt& F, const DevEbwt& B, int has_bw, const uint8_t* reads, uint32_t stride,
+                        const uint32_t* lens, uint32_t n, uint32_t seedlen, uint32_t interval, uint32_t offset,
+                        uint32_t maxseeds, const uint32_t* out, bt2g_ext_out* ext, hipStream_t st);
 void launch_range_offsets(const DevEbwt& e, const uint32_t* sweep, const bt2g_mm1* hits, const int32_t* counts,
                           uint32_t n, uint32_t cap, uint32_t off_cap, uint32_t* offs, hipStream_t st);
 void launch_sw_partition(const bt2g_sw_problem* probs, uint32_t nprob, int local, int enable8, uint32_t* list8,

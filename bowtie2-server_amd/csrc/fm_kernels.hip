@@ -322,6 +322,20 @@ void launch_get_offset(const DevEbwt& e, const uint32_t* rows, uint32_t n, uint3
 // (read, range, row), ranges of more than off_cap rows skipped.  offs: n x
 // (2 + cap) x off_cap, BT2G_OFF_MASK where no row.  The same walk as
 // k_get_offset (Ebwt::getOffset, bt2_idx.cpp:150-171).
+__device__ __forceinline__ uint32_t row_offset(const DevEbwt& e, uint32_t row) {
+	const uint32_t mask = BT2G_OFF_MASK << e.off_rate;
+	if(row == e.zoff) return 0;
+	if((row & mask) == row) return e.offs[row >> e.off_rate];
+	for(uint32_t jumps = 1;; jumps++) {
+		SideData sd;
+		load_side(e, row / 192u, sd);
+		const int c = side_rowL(sd, row % 192u);
+		row = occ1(e, sd, row, c);
+		if(row == e.zoff) return jumps;
+		if((row & mask) == row) return jumps + e.offs[row >> e.off_rate];
+	}
+}
+
 __global__ void __launch_bounds__(256)
 k_range_offsets(DevEbwt e, const uint32_t* __restrict__ sweep, const bt2g_mm1* __restrict__ hits,
                 const int32_t* __restrict__ counts, uint32_t n, uint32_t cap, uint32_t off_cap,
@@ -339,26 +353,27 @@ k_range_offsets(DevEbwt e, const uint32_t* __restrict__ sweep, const bt2g_mm1* _
 		top = h.top;
 		bot = h.bot;
 	}
-	uint32_t res = BT2G_OFF_MASK;
-	if(bot > top && bot - top <= off_cap && j < bot - top) {
-		uint32_t row = top + j;
-		const uint32_t mask = BT2G_OFF_MASK << e.off_rate;
-		uint32_t jumps = 0;
-		if(row == e.zoff) res = 0;
-		else if((row & mask) == row) res = e.offs[row >> e.off_rate];
-		else {
-			for(;;) {
-				SideData sd;
-				load_side(e, row / 192u, sd);
-				const int c = side_rowL(sd, row % 192u);
-				row = occ1(e, sd, row, c);
-				jumps++;
-				if(row == e.zoff) { res = jumps; break; }
-				if((row & mask) == row) { res = jumps + e.offs[row >> e.off_rate]; break; }
-			}
-		}
-	}
-	offs[gid] = res;
+	offs[gid] = (bot > top && bot - top <= off_cap && j < bot - top) ? row_offset(e, top + j) : BT2G_OFF_MASK;
+}
+
+// The same for the seed ranges of one seed round (bt2g_seed_search_ext): out
+// n x 2 x maxseeds x 4 as k_seed_search wrote it, offs n x 2 x maxseeds x off_cap.
+__global__ void __launch_bounds__(256)
+k_seed_offsets(DevEbwt e, const uint32_t* __restrict__ out, uint64_t nrange, uint32_t off_cap,
+               uint32_t* __restrict__ offs) {
+	const uint64_t gid = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+	if(gid >= nrange * off_cap) return;
+	const uint64_t k = gid / off_cap;
+	const uint32_t j = (uint32_t)(gid % off_cap), top = out[k * 4], bot = out[k * 4 + 1];
+	offs[gid] = (bot > top && bot - top <= off_cap && j < bot - top) ? row_offset(e, top + j) : BT2G_OFF_MASK;
+}
+
+void launch_seed_offsets(const DevEbwt& e, const uint32_t* out, uint64_t nrange, uint32_t off_cap, uint32_t* offs,
+                         hipStream_t st) {
+	const uint64_t tot = nrange * off_cap;
+	if(!tot) return;
+	hipLaunchKernelGGL(k_seed_offsets, dim3((uint32_t)((tot + 255) / 256)), dim3(256), 0, st, e, out, nrange, off_cap,
+	                   offs);
 }
 
 void launch_range_offsets(const DevEbwt& e, const uint32_t* sweep, const bt2g_mm1* hits, const int32_t* counts,
@@ -417,14 +432,8 @@ __device__ __forceinline__ uint32_t ext_walk(const DevEbwt& e, uint32_t top, uin
 	return n;
 }
 
-__global__ void __launch_bounds__(256)
-k_extend(DevEbwt F, DevEbwt B, int has_bw, const uint8_t* __restrict__ reads, uint32_t stride,
-         const uint32_t* __restrict__ lens, const bt2g_ext_in* __restrict__ in, uint32_t n, bt2g_ext_out* __restrict__ out) {
-	const uint32_t k = blockIdx.x * blockDim.x + threadIdx.x;
-	if(k >= n) return;
-	const bt2g_ext_in q = in[k];
-	const uint32_t rdlen = lens[q.read];
-	const uint8_t* row = reads + (size_t)q.read * stride;
+__device__ __forceinline__ bt2g_ext_out ext_one(const DevEbwt& F, const DevEbwt& B, int has_bw, const uint8_t* row,
+                                                uint32_t rdlen, const bt2g_ext_in& q) {
 	const bool fw = q.fw != 0;
 	uint32_t fmops = 0, nlex = 0, nrex = 0;
 	// left, forward index (aligner_sw_driver.cpp:335-408)
@@ -433,11 +442,59 @@ k_extend(DevEbwt F, DevEbwt B, int has_bw, const uint8_t* __restrict__ reads, ui
 	// right, mirror index (aligner_sw_driver.cpp:411-475)
 	lim = fw ? rdlen - q.len - q.off : q.off;
 	if(lim > 0 && has_bw) nrex = ext_walk(B, q.topb, q.botb, row, rdlen, fw, lim, fw ? q.len + q.off : rdlen - q.off, 1, fmops);
-	out[k] = bt2g_ext_out{nlex, nrex, fmops, 0u};
+	return bt2g_ext_out{nlex, nrex, fmops, 0u};
+}
+
+__global__ void __launch_bounds__(256)
+k_extend(DevEbwt F, DevEbwt B, int has_bw, const uint8_t* __restrict__ reads, uint32_t stride,
+         const uint32_t* __restrict__ lens, const bt2g_ext_in* __restrict__ in, uint32_t n, bt2g_ext_out* __restrict__ out) {
+	const uint32_t k = blockIdx.x * blockDim.x + threadIdx.x;
+	if(k >= n) return;
+	const bt2g_ext_in q = in[k];
+	out[k] = ext_one(F, B, has_bw, reads + (size_t)q.read * stride, lens[q.read], q);
 }
 
 void launch_extend(const DevEbwt& F, const DevEbwt& B, int has_bw, const uint8_t* reads, uint32_t stride,
                    const uint32_t* lens, const bt2g_ext_in* in, uint32_t n, bt2g_ext_out* out, hipStream_t st) {
 	if(n == 0) return;
 	hipLaunchKernelGGL(k_extend, dim3((n + 255) / 256), dim3(256), 0, st, F, B, has_bw, reads, stride, lens, in, n, out);
+}
+
+// SwDriver::extend for every range of one seed round, as prioritizeSATups would
+// ask it (bt2g_seed_search_ext): one lane = one (read, strand, seed); the seed
+// at depth s * interval + offset, min(seedlen, len) long (k_seed_search).
+// ext[k] = {0, 0, 0, 0} where the seed has no range.
+__global__ void __launch_bounds__(256)
+k_seed_extend(DevEbwt F, DevEbwt B, int has_bw, const uint8_t* __restrict__ reads, uint32_t stride,
+              const uint32_t* __restrict__ lens, uint32_t n, uint32_t seedlen, uint32_t interval, uint32_t offset,
+              uint32_t maxseeds, const uint32_t* __restrict__ out, bt2g_ext_out* __restrict__ ext) {
+	const uint64_t gid = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+	if(gid >= (uint64_t)n * 2 * maxseeds) return;
+	const uint32_t r = (uint32_t)(gid / (2u * maxseeds)), rem = (uint32_t)(gid % (2u * maxseeds));
+	const uint32_t strand = rem / maxseeds, s = rem % maxseeds;
+	const uint32_t* o = out + gid * 4;
+	const uint32_t len = lens[r], L = seedlen < len ? seedlen : len, depth = s * interval + offset;
+	bt2g_ext_out res{0u, 0u, 0u, 0u};
+	if(o[1] > o[0] && depth + L <= len) {
+		bt2g_ext_in q;
+		q.read = r;
+		q.fw = strand == 0 ? 1 : 0;
+		q.off = depth;
+		q.len = L;
+		q.topf = o[0];
+		q.botf = o[1];
+		q.topb = o[2];
+		q.botb = o[3];
+		res = ext_one(F, B, has_bw, reads + (size_t)r * stride, len, q);
+	}
+	ext[gid] = res;
+}
+
+void launch_seed_extend(const DevEbwt& F, const DevEbwt& B, int has_bw, const uint8_t* reads, uint32_t stride,
+                        const uint32_t* lens, uint32_t n, uint32_t seedlen, uint32_t interval, uint32_t offset,
+                        uint32_t maxseeds, const uint32_t* out, bt2g_ext_out* ext, hipStream_t st) {
+	const uint64_t tot = (uint64_t)n * 2 * maxseeds;
+	if(!tot) return;
+	hipLaunchKernelGGL(k_seed_extend, dim3((uint32_t)((tot + 255) / 256)), dim3(256), 0, st, F, B, has_bw, reads, stride,
+	                   lens, n, seedlen, interval, offset, maxseeds, out, ext);
 }

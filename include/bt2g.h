@@ -222,6 +222,21 @@ int bt2g_extend(bt2g_ctx* ctx, const uint8_t* reads, uint32_t stride, const uint
 int bt2g_extend_dev(bt2g_ctx* ctx, const uint8_t* reads, uint32_t stride, const uint32_t* lens,
                     const bt2g_ext_in* in, uint32_t n, bt2g_ext_out* out, void* stream);
 
+/* bt2g_seed_search, and in the same call what the seed-extension stage asks of
+ * the round's ranges (bt2g_exact_sweep_1mm does the same for the up-front
+ * searches): ext (n x 2 x maxseeds, may be NULL) = SwDriver::extend of each
+ * seed's range (as bt2g_extend with fw = strand 0, off = the seed's depth
+ * s * interval + offset, len = min(seedlen, read length); prioritizeSATups,
+ * aligner_sw_driver.cpp:574-589 asks it of every range it keeps), zeros where
+ * the seed has no range; offs (n x 2 x maxseeds x off_cap, may be NULL) = the
+ * offsets (Ebwt::getOffset) of rows topf .. botf-1 of every range of at most
+ * off_cap rows, BT2G_OFF_MASK elsewhere (the rows GroupWalk2S::init resolves
+ * for the ranges it takes, aligner_sw_driver.cpp:610-620 and 706-722). */
+int bt2g_seed_search_ext(bt2g_ctx* ctx, const uint8_t* reads, uint32_t stride, const uint32_t* lens, uint32_t n,
+                         uint32_t seedlen, uint32_t interval, uint32_t offset, uint32_t maxseeds, uint32_t* out,
+                         int32_t* nseeds, uint32_t* bwops, uint32_t* loads, bt2g_ext_out* ext, uint32_t off_cap,
+                         uint32_t* offs);
+
 /* ---- SW engine ----------------------------------------------------------- */
 
 /* One dynamic-programming problem (SwAligner::initRead + initRef,

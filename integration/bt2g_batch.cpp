@@ -197,7 +197,8 @@ std::atomic<uint64_t> g_svc_us[K_N];
 std::atomic<uint64_t> g_reads{0}, g_rounds{0}, g_round_us{0}, g_cpu_us{0}, g_gpu_us{0};
 std::atomic<uint64_t> g_dp_spec{0}, g_dp_used{0}, g_dp_reuse{0}, g_dp_miss{0};
 std::atomic<uint64_t> g_mm_pf{0}, g_mm_pf_used{0};   // 1-mm searches prefetched with the sweep / taken
-std::atomic<uint64_t> g_rows_pf{0};                   // SA rows resolved with the sweep
+std::atomic<uint64_t> g_rows_pf{0};                   // SA rows resolved with the sweep or the seeds
+std::atomic<uint64_t> g_ext_pf{0};                    // extend requests answered by the seed call
 // rounds per read: total and a histogram (bin b: [2^b, 2^(b+1)))
 std::atomic<uint64_t> g_steps{0}, g_steps_hist[16];
 // reads in flight summed over rounds; drivers' time with no read in flight
@@ -219,9 +220,9 @@ void write_stats() {
 		n += snprintf(buf + n, sizeof(buf) - n, ", \"%s\": [%llu, %llu, %llu, %.1f]", K_NAMES[k],
 		              (unsigned long long)g_req[k].load(), (unsigned long long)g_cpu[k].load(),
 		              (unsigned long long)g_calls[k].load(), g_call_us[k].load() / 1000.0);
-	n += snprintf(buf + n, sizeof(buf) - n, ", \"one_mm_prefetch\": [%llu, %llu], \"rows_prefetched\": %llu",
+	n += snprintf(buf + n, sizeof(buf) - n, ", \"one_mm_prefetch\": [%llu, %llu], \"rows_prefetched\": %llu, \"ext_prefetched\": %llu",
 	              (unsigned long long)g_mm_pf.load(), (unsigned long long)g_mm_pf_used.load(),
-	              (unsigned long long)g_rows_pf.load());
+	              (unsigned long long)g_rows_pf.load(), (unsigned long long)g_ext_pf.load());
 	n += snprintf(buf + n, sizeof(buf) - n, ", \"svc_busy_ms\": [");
 	for(int k = 0; k < K_N; k++)
 		n += snprintf(buf + n, sizeof(buf) - n, "%s%.1f", k ? ", " : "", g_svc_us[k].load() / 1000.0);
@@ -616,7 +617,9 @@ struct MateRes {
 	MateRes() {
 		mm.reserve(64);
 		sd_out.reserve(256);
+		sd_ext.reserve(64);
 		pf_rows.reserve(160);
+		sd_rows.reserve(160);
 	}
 	uint32_t sweep[8] = {0};
 	bool sweep_asked = false;
@@ -640,6 +643,11 @@ struct MateRes {
 	bool sd_ready = false;
 	uint32_t sd_L = 0, sd_per = 0, sd_off = 0, sd_nof = 0;
 	std::vector<uint32_t> sd_out;      // [strand][offset][topf, botf, topb, botb]
+	// with the seed search (bt2g_seed_search_ext): SwDriver::extend of each seed's
+	// range ([strand][offset]; empty when not asked) and the (row, offset) of the
+	// small ranges' rows, sorted by row (the seed-extension stage's two requests)
+	std::vector<bt2g_ext_out> sd_ext;
+	std::vector<std::pair<uint32_t, uint32_t>> sd_rows;
 	int32_t sd_ns = 0;
 	uint32_t sd_ops = 0;
 	// row in this round's engine call
@@ -808,6 +816,12 @@ std::atomic<uint64_t> g_stamp{0};
 // $BT2G_MM_PREFETCH=0: no 1-mm search with the exact sweep
 bool mm_prefetch_on() {
 	static const bool on = [] { const char* e = getenv("BT2G_MM_PREFETCH"); return !(e && *e == '0'); }();
+	return on;
+}
+
+// $BT2G_SEED_PREFETCH=0: the seed search without its ranges' extension and rows
+bool seed_prefetch_on() {
+	static const bool on = [] { const char* e = getenv("BT2G_SEED_PREFETCH"); return !(e && *e == '0'); }();
 	return on;
 }
 
@@ -1048,8 +1062,11 @@ void Svc::call_1mm(std::vector<Rq>& v) {
 void Svc::call_seeds(std::vector<Rq>& v) {
 	if(v.empty()) return;
 	thread_local Pack pk;
-	thread_local std::vector<uint32_t> out, ops, ld;
+	thread_local std::vector<uint32_t> out, ops, ld, offs;
+	thread_local std::vector<bt2g_ext_out> ext;
 	thread_local std::vector<int32_t> ns;
+	const bool pf = seed_prefetch_on();
+	const uint32_t OFF_CAP = 8;
 	std::vector<bool> taken(v.size(), false);
 	for(size_t a = 0; a < v.size(); a++) {
 		if(taken[a]) continue;
@@ -1072,8 +1089,13 @@ void Svc::call_seeds(std::vector<Rq>& v) {
 		ns.resize(n);
 		const uint64_t t0 = now_us();
 		ld.resize(n);
-		int rc = bt2g_seed_search(ctx, pk.codes.data(), pk.stride, pk.lens.data(), (uint32_t)n, x0.sd_L, x0.sd_per,
-		                          x0.sd_off, maxs, out.data(), ns.data(), ops.data(), kprof_on() ? ld.data() : nullptr);
+		if(pf) {
+			ext.resize(n * 2 * maxs);
+			offs.resize(n * 2 * maxs * OFF_CAP);
+		}
+		int rc = bt2g_seed_search_ext(ctx, pk.codes.data(), pk.stride, pk.lens.data(), (uint32_t)n, x0.sd_L, x0.sd_per,
+		                              x0.sd_off, maxs, out.data(), ns.data(), ops.data(), kprof_on() ? ld.data() : nullptr,
+		                              pf ? ext.data() : nullptr, OFF_CAP, pf ? offs.data() : nullptr);
 		if(kprof_on()) {
 			uint64_t w = 0;
 			for(size_t i = 0; i < n; i++) w += 64ull * ld[i] + (uint64_t)std::max(ns[i], 0) * 2u * (x0.sd_L + 12u);
@@ -1091,6 +1113,21 @@ void Svc::call_seeds(std::vector<Rq>& v) {
 			for(int f = 0; f < 2; f++)
 				for(uint32_t k = 0; k < x.sd_nof && k < maxs; k++)
 					memcpy(&x.sd_out[((size_t)f * x.sd_nof + k) * 4], &out[((i * 2 + f) * maxs + k) * 4], 16);
+			x.sd_ext.clear();
+			x.sd_rows.clear();
+			if(pf) {
+				x.sd_ext.assign(2 * (size_t)x.sd_nof, bt2g_ext_out{0, 0, 0, 0});
+				for(int f = 0; f < 2; f++)
+					for(uint32_t k = 0; k < x.sd_nof && k < maxs; k++) {
+						const size_t g = (i * 2 + f) * maxs + k;
+						x.sd_ext[(size_t)f * x.sd_nof + k] = ext[g];
+						const uint32_t top = out[g * 4], bot = out[g * 4 + 1];
+						if(bot > top && bot - top <= OFF_CAP)
+							for(uint32_t j = 0; j < bot - top; j++)
+								if(offs[g * OFF_CAP + j] != OFF_MASK) x.sd_rows.emplace_back(top + j, offs[g * OFF_CAP + j]);
+					}
+				std::sort(x.sd_rows.begin(), x.sd_rows.end());
+			}
 			x.sd_ready = true;
 		}
 	}
@@ -1527,6 +1564,8 @@ void Driver::resolve_rows_request(Slot& s) {
 	s.off_where.clear();
 	const auto& p0 = s.mr[0].pf_rows;
 	const auto& p1 = s.mr[1].pf_rows;
+	const auto& q0 = s.mr[0].sd_rows;
+	const auto& q1 = s.mr[1].sd_rows;
 	auto known = [](const std::vector<std::pair<uint32_t, uint32_t>>& p, uint32_t row, uint32_t& off) {
 		auto it = std::lower_bound(p.begin(), p.end(), std::make_pair(row, 0u));
 		if(it == p.end() || it->first != row) return false;
@@ -1539,8 +1578,10 @@ void Driver::resolve_rows_request(Slot& s) {
 			if(x.offs[j] == OFF_MASK) {
 				const uint32_t row = (uint32_t)(x.topf + j);
 				uint32_t off;
-				// a row the exact sweep / 1-mm call already resolved (its small ranges)
-				if((!p0.empty() && known(p0, row, off)) || (!p1.empty() && known(p1, row, off))) {
+				// a row the exact sweep / 1-mm call or the seed search already
+				// resolved (their small ranges)
+				if((!p0.empty() && known(p0, row, off)) || (!p1.empty() && known(p1, row, off)) ||
+				   (!q0.empty() && known(q0, row, off)) || (!q1.empty() && known(q1, row, off))) {
 					x.offs[j] = off;
 					g_rows_pf++;
 					continue;
@@ -1604,8 +1645,30 @@ static void ext_request(Driver& d, Slot& s, SwDriverB& x) {
 	}
 }
 
+// The extend requests of ext_request answered from the seed call's results
+// (MateRes::sd_ext) when every one of them is a seed of the round's search with
+// the same range; else false and the engine is asked.
+static bool ext_from_seeds(Slot& s, size_t mate) {
+	const MateRes& x = s.mr[mate];
+	if(x.sd_ext.size() != 2 * (size_t)x.sd_nof || x.sd_per == 0) return false;
+	const uint32_t L = std::min<uint32_t>(x.sd_L, (uint32_t)s.rdlens[mate]);
+	s.ext_out.resize(s.ext_in.size());
+	for(size_t i = 0; i < s.ext_in.size(); i++) {
+		const bt2g_ext_in& q = s.ext_in[i];
+		if(q.off < x.sd_off || (q.off - x.sd_off) % x.sd_per != 0 || q.len != L) return false;
+		const size_t k = (q.off - x.sd_off) / x.sd_per, f = q.fw ? 0 : 1;
+		if(k >= x.sd_nof) return false;
+		const uint32_t* o = &x.sd_out[(f * x.sd_nof + k) * 4];
+		if(o[0] != q.topf || o[1] != q.botf || o[2] != q.topb || o[3] != q.botb) return false;
+		s.ext_out[i] = x.sd_ext[f * x.sd_nof + k];
+	}
+	g_ext_pf += s.ext_in.size();
+	return true;
+}
+
 #define BT2GB_PRIO_SETUP(LABEL_EXT, LABEL_ROWS)                                                        \
 	ext_request(d, s, *this);                                                                          \
+	if(!s.ext_in.empty() && ext_from_seeds(s, mate)) goto LABEL_EXT;                                   \
 	if(!s.ext_in.empty()) {                                                                            \
 		d.rq[K_EXT].push_back(Rq{&s, mate});                                                           \
 		pc = X_AFTER_EXT;                                                                              \

@@ -197,6 +197,39 @@ int bt2g_seed_search(bt2g_ctx* c, const uint8_t* reads, uint32_t stride, const u
 	return BT2G_OK;
 }
 
+// bt2g_seed_search + bt2g_extend of each seed's range + the small ranges' rows
+// (include/bt2g.h), each by the reference's own code
+int bt2g_seed_search_ext(bt2g_ctx* c, const uint8_t* reads, uint32_t stride, const uint32_t* lens, uint32_t n,
+                         uint32_t seedlen, uint32_t interval, uint32_t offset, uint32_t maxseeds, uint32_t* out,
+                         int32_t* nseeds, uint32_t* bwops, uint32_t* loads, bt2g_ext_out* ext, uint32_t off_cap,
+                         uint32_t* offs) {
+	int rc = bt2g_seed_search(c, reads, stride, lens, n, seedlen, interval, offset, maxseeds, out, nseeds, bwops, loads);
+	if(rc) return rc;
+	for(uint32_t i = 0; i < n; i++)
+		for(uint32_t f = 0; f < 2; f++)
+			for(uint32_t s = 0; s < maxseeds; s++) {
+				const size_t k = ((size_t)i * 2 + f) * maxseeds + s;
+				const uint32_t* o = out + k * 4;
+				const uint32_t L = std::min(seedlen, lens[i]), depth = s * interval + offset;
+				if(ext) {
+					ext[k] = bt2g_ext_out{0, 0, 0, 0};
+					if(o[1] > o[0] && depth + L <= lens[i]) {
+						const bt2g_ext_in q{i, f == 0 ? 1 : 0, depth, L, o[0], o[1], o[2], o[3]};
+						if((rc = bt2g_extend(c, reads, stride, lens, n, &q, 1, &ext[k]))) return rc;
+					}
+				}
+				if(offs) {
+					for(uint32_t j = 0; j < off_cap; j++) offs[k * off_cap + j] = 0xffffffffu;
+					if(o[1] > o[0] && o[1] - o[0] <= off_cap) {
+						std::vector<uint32_t> rows(o[1] - o[0]);
+						for(uint32_t j = 0; j < rows.size(); j++) rows[j] = o[0] + j;
+						bt2g_get_offset(c, rows.data(), (uint32_t)rows.size(), offs + k * off_cap, nullptr);
+					}
+				}
+			}
+	return BT2G_OK;
+}
+
 int bt2g_ungapped(bt2g_ctx* c, const uint8_t* reads, const uint8_t* quals, uint32_t stride, const uint32_t* lens,
                   const bt2g_ug_problem* probs, uint32_t n, const bt2g_scoring* sc, int ohang, uint32_t maxedit,
                   bt2g_ug_result* res, bt2g_edit* edits) {

@@ -192,3 +192,50 @@ def test_exact_sweep_1mm_fused(engines, skip_exact, strand):
         ran += 1
     # (the bench rule with --norc: the skipped strand's mine is 0, so every read is skipped)
     assert ran > 20 or (norc and skip_exact)
+
+
+@pytest.mark.parametrize("pol", ["s22", "s10"])
+def test_seed_search_ext_fused(engines, pol):
+    """bt2g_seed_search_ext (the batch driver's seed call) equals bt2g_seed_search,
+    then bt2g_extend of every seed range as prioritizeSATups asks it (fw = strand
+    0, off = the seed's depth, len = the seed length; aligner_sw_driver.cpp:574-589)
+    and bt2g_get_offset of the rows of every range of at most off_cap rows."""
+    import synth
+    g = load_golden("fm_synth")
+    L, iv, off = (int(x) for x in g["seedpol_" + pol])
+    idx = get_index("synth")
+    codes, _, _, _ = synth.reads(99, np.concatenate(idx.ref_codes), 600, 150, sub=0.01, nrate=0.002)
+    lens = np.full(len(codes), 150, np.uint32)
+    lens[::7] = 60
+    for i in range(0, len(codes), 7):
+        codes[i, 60:] = 4
+    reads = np.concatenate([g["reads"], codes])            # (the golden reads are 150 wide)
+    lens = np.concatenate([g["lens"].astype(np.uint32), lens])
+    e = engines["synth"]
+    maxs = 16
+    out, ns, ops, ext, offs = e.seed_search_ext(reads, lens, L, iv, off, maxs, off_cap=8)
+    o0, ns0, ops0, _ = e.seed_search(reads, lens, L, iv, off, maxs)
+    assert np.array_equal(out, o0) and np.array_equal(ns, ns0) and np.array_equal(ops, ops0)
+    rg, where, rows, rwhere = [], [], [], []
+    for i in range(len(lens)):
+        for f in range(2):
+            for s in range(maxs):
+                t, b, tb, bb = (int(v) for v in out[i, f, s])
+                depth, sl = s * iv + off, min(L, int(lens[i]))
+                if b > t and depth + sl <= lens[i]:
+                    rg.append((i, 1 - f, depth, sl, t, b, tb, bb))
+                    where.append((i, f, s))
+                if 0 < b - t <= 8:
+                    for j in range(b - t):
+                        rows.append(t + j)
+                        rwhere.append((i, f, s, j))
+    want = np.zeros_like(ext)
+    got = e.extend(reads, lens, np.array(rg, np.uint32))
+    for (i, f, s), x in zip(where, got):
+        want[i, f, s] = x
+    assert np.array_equal(ext, want) and len(rg) > 500
+    wo = np.full(offs.shape, 0xFFFFFFFF, np.uint32)
+    ov, _ = e.get_offset(np.array(rows, np.uint32))
+    for (i, f, s, j), o in zip(rwhere, ov):
+        wo[i, f, s, j] = o
+    assert np.array_equal(offs, wo) and len(rows) > 500
