@@ -599,9 +599,16 @@ def schedule_run(args, rank, world, local, base, reads_np, quals_np, workdir, bi
     stats = os.path.join(workdir, "stats.json")
     env = rs.dropin_env(base, stats, device=local)
     env["BT2G_KPROF"] = "1"
+    # $BT2G_BENCH_SERVER_PREFIX: a profiler in front of the batch server's command line
+    # (e.g. "rocprofv3 --kernel-trace --stats -d DIR -o run --"); the server then exits
+    # through exit() at SIGTERM so that the profile is written
+    import shlex
+    prefix = tuple(shlex.split(os.environ.get("BT2G_BENCH_SERVER_PREFIX", "")))
+    if prefix:
+        env["BT2G_EXIT_CLEAN"] = "1"
     multi = world > 1 and dist.is_initialized()
     with rs.Server(base, threads=args.drivers, args=policy_args(args.mode, args.preset), binary=binary,
-                   env=env, log_path=os.path.join(workdir, "server.log")) as srv:
+                   env=env, log_path=os.path.join(workdir, "server.log"), prefix=prefix) as srv:
         log(f"[rank {rank}] batch server ready in {srv.load_s:.1f}s (-p {args.drivers})")
         for _ in range(args.warmup):
             srv.run(chunks[:max(1, args.warmup_chunks)], k=args.clients)

@@ -40,6 +40,16 @@ ktrace)
   cp /tmp/db/server_dropin.log $O/server_ktrace.log
   python3 scripts/gap_trace.py $O/ktrace 10 > $O/ktrace_gap.txt 2>&1; head -60 $O/ktrace_gap.txt
   find $O/ktrace -name "*.csv" -size +40M -delete ;;
+bench)
+  # the driver's round-end command, as it runs it
+  timeout -k 10 1100 python3 -u bench.py > $O/bench.json 2> $O/bench.log || { tail -30 $O/bench.log; exit 1; }
+  cat $O/bench.json | cut -c1-1500 ;;
+benchprof)
+  # the same command with rocprofv3 --kernel-trace --stats in front of its batch server
+  BT2G_BENCH_SERVER_PREFIX="rocprofv3 --kernel-trace --stats --output-format csv -d $PWD/$O/bprof -o run --" \
+    timeout -k 10 1100 python3 -u bench.py --chain-steps 0 $BENCH_ARGS > $O/bench_prof.json 2> $O/bench_prof.log || { tail -30 $O/bench_prof.log; exit 1; }
+  find $O/bprof -name "*kernel_stats.csv"
+  find $O/bprof -name "*.csv" -size +40M -delete ;;
 tests)
   timeout -k 10 1000 python -u -m pytest tests -m gpu -x -v --timeout 600 --timeout-method thread > $O/gpu_tests.log 2>&1 || { tail -20 $O/gpu_tests.log; exit 1; }
   tail -2 $O/gpu_tests.log
