@@ -1624,14 +1624,18 @@ int bt2g_sw_align_bt_packed(bt2g_ctx* c, const uint8_t* reads, const uint8_t* qu
 		   (fates && (rc = t.up(&dpf, (const int8_t*)nullptr, (size_t)nprob * cap))))
 			return rc;
 	}
-	if((rc = t.send())) return rc;
 	const SwHint hint = sw_hint(probs, nprob, lens, enable8);
-	if((rc = sw_align_bt_impl(c, dr, dq, stride, dl, dp, nprob, dw, drc, sc, enable8, cap, dres, dc, maxaln, maxedit,
-	                          dna, dal, ded, dft, c->stream, &hint)))
-		return rc;
-	launch_sw_pack(dres, dna, dal, dc, dft, ded, nprob, cap, maxaln, maxedit, dcnt, doff, dpc, dpf, dpe, c->stream);
-	HIPCHK(hipGetLastError());
-	if((rc = t.down(tot, doff + 3 * (size_t)nprob, 3))) return rc;
+	{
+		// (kernel-stats id 7: the call's whole span on the stream, copies included)
+		ProfScope ps(c, 7, c->stream);
+		if((rc = t.send())) return rc;
+		if((rc = sw_align_bt_impl(c, dr, dq, stride, dl, dp, nprob, dw, drc, sc, enable8, cap, dres, dc, maxaln, maxedit,
+		                          dna, dal, ded, dft, c->stream, &hint)))
+			return rc;
+		launch_sw_pack(dres, dna, dal, dc, dft, ded, nprob, cap, maxaln, maxedit, dcnt, doff, dpc, dpf, dpe, c->stream);
+		HIPCHK(hipGetLastError());
+		if((rc = t.down(tot, doff + 3 * (size_t)nprob, 3))) return rc;
+	}
 	if((rc = t.finish())) return rc;
 	if(direct) {
 		memcpy(cands, hpc, sizeof(bt2g_sw_cand) * tot[0]);

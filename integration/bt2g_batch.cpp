@@ -198,7 +198,8 @@ std::atomic<uint64_t> g_reads{0}, g_rounds{0}, g_round_us{0}, g_cpu_us{0}, g_gpu
 std::atomic<uint64_t> g_dp_spec{0}, g_dp_used{0}, g_dp_reuse{0}, g_dp_miss{0};
 std::atomic<uint64_t> g_mm_pf{0}, g_mm_pf_used{0};   // 1-mm searches prefetched with the sweep / taken
 std::atomic<uint64_t> g_rows_pf{0};                   // SA rows resolved with the sweep or the seeds
-std::atomic<uint64_t> g_ext_pf{0};                    // extend requests answered by the seed call
+std::atomic<uint64_t> g_ext_pf{0};
+std::atomic<uint64_t> g_dp_pre_us{0}, g_dp_post_us{0};   // the DP service's host work around its calls                    // extend requests answered by the seed call
 // rounds per read: total and a histogram (bin b: [2^b, 2^(b+1)))
 std::atomic<uint64_t> g_steps{0}, g_steps_hist[16];
 // reads in flight summed over rounds; drivers' time with no read in flight
@@ -220,9 +221,11 @@ void write_stats() {
 		n += snprintf(buf + n, sizeof(buf) - n, ", \"%s\": [%llu, %llu, %llu, %.1f]", K_NAMES[k],
 		              (unsigned long long)g_req[k].load(), (unsigned long long)g_cpu[k].load(),
 		              (unsigned long long)g_calls[k].load(), g_call_us[k].load() / 1000.0);
-	n += snprintf(buf + n, sizeof(buf) - n, ", \"one_mm_prefetch\": [%llu, %llu], \"rows_prefetched\": %llu, \"ext_prefetched\": %llu",
+	n += snprintf(buf + n, sizeof(buf) - n, ", \"one_mm_prefetch\": [%llu, %llu], \"rows_prefetched\": %llu, \"ext_prefetched\": %llu"
+	              ", \"dp_host_ms\": [%.1f, %.1f]",
 	              (unsigned long long)g_mm_pf.load(), (unsigned long long)g_mm_pf_used.load(),
-	              (unsigned long long)g_rows_pf.load(), (unsigned long long)g_ext_pf.load());
+	              (unsigned long long)g_rows_pf.load(), (unsigned long long)g_ext_pf.load(), g_dp_pre_us.load() / 1000.0,
+	              g_dp_post_us.load() / 1000.0);
 	n += snprintf(buf + n, sizeof(buf) - n, ", \"svc_busy_ms\": [");
 	for(int k = 0; k < K_N; k++)
 		n += snprintf(buf + n, sizeof(buf) - n, "%s%.1f", k ? ", " : "", g_svc_us[k].load() / 1000.0);
@@ -1245,6 +1248,7 @@ void Svc::run_dp(const std::vector<std::pair<Slot*, DpRes*>>& v, uint32_t cap, u
 		std::vector<bt2g_edit> E;
 	};
 	thread_local B b;
+	const uint64_t tpre = now_us();
 	uint32_t stride = 1;
 	for(auto& q : v) stride = std::max<uint32_t>(stride, (uint32_t)q.first->rdlens[q.second->mate]);
 	b.pk.reset(stride);
@@ -1282,10 +1286,12 @@ void Svc::run_dp(const std::vector<std::pair<Slot*, DpRes*>>& v, uint32_t cap, u
 	if(b.E.size() < n * (size_t)maxaln * maxedit) b.E.resize(n * (size_t)maxaln * maxedit);
 	uint64_t tot[3] = {0, 0, 0};
 	const uint64_t t0 = now_us();
+	g_dp_pre_us += t0 - tpre;
 	int rc = bt2g_sw_align_bt_packed(ctx, b.pk.codes.data(), b.pk.quals.data(), b.pk.stride, b.pk.lens.data(), b.P.data(),
 	                                 (uint32_t)n, nullptr, 0, b.RC.data(), bsc, R_enable8 ? 1 : 0, cap, b.R.data(),
 	                                 maxaln, maxedit, b.NA.data(), b.A.data(), b.C.data(), b.F.data(), b.E.data(), tot);
-	g_call_us[K_DP] += now_us() - t0;
+	const uint64_t t1 = now_us();
+	g_call_us[K_DP] += t1 - t0;
 	g_calls[K_DP]++;
 	if(rc && rc != BT2G_ERR_OVERFLOW) die("bt2g_sw_align_bt_packed", rc);
 	std::vector<std::pair<Slot*, DpRes*>> again;
@@ -1323,6 +1329,7 @@ void Svc::run_dp(const std::vector<std::pair<Slot*, DpRes*>>& v, uint32_t cap, u
 		r.edits.assign(b.E.begin() + e0, b.E.begin() + e0 + ne);
 		r.ready = true;
 	}
+	g_dp_post_us += now_us() - t1;
 	if(oc != tot[0] || oe != tot[2]) {
 		fprintf(stderr, "bt2g batch: packed DP outputs %llu/%llu, expected %zu/%zu\n", (unsigned long long)tot[0],
 		        (unsigned long long)tot[2], oc, oe);
