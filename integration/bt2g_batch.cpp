@@ -324,7 +324,10 @@ struct EnvInit {
 		pin_cpus();
 		setenv("BT2G_SYNC", "poll", 0);
 		const char* hq = getenv("BT2G_HW_QUEUES");
-		long q = hq ? atol(hq) : 16;
+		// (32: a hardware queue per stream -- six DP workers and two per other kind,
+		// each with its own context and stream, plus the 1-mm search's second stream;
+		// r04r: 190 k reads/s with 16, 214 k with 32)
+		long q = hq ? atol(hq) : 32;
 		if(q < 1) q = 1;
 		if(q > 32) q = 32;                      // the runtime refuses more
 		char b[16];
@@ -3371,7 +3374,10 @@ void Driver::run_loop() {
 			static bt2g_scoring s_bsc;              // (the same scoring for every driver)
 			s_bsc = bsc;
 			const int nw = std::max(1, (int)env_or("BT2G_SVC_WORKERS", 2));
-			const int nd = std::max(1, (int)env_or("BT2G_DP_WORKERS", 3));
+			// (DP calls are the longest, ~3-6 ms: with three workers the DP service was
+			// saturated and the drivers queued for it -- r04q 112-129 k reads/s, r04r
+			// 190-214 k with six)
+			const int nd = std::max(1, (int)env_or("BT2G_DP_WORKERS", 6));
 			for(int k = 0; k < K_N; k++) {
 				Svc* owner = nullptr;
 				for(int w = 0; w < (k == K_DP ? nd : nw); w++) {

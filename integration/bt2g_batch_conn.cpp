@@ -9,7 +9,8 @@
 // (bt2g_batch.cpp), so a few buffers keep a connection's reads flowing, and
 // the rest were only allocation churn on the connection's thread (each
 // connection made and freed ~65 x 16 x 2 Reads at -p 16).  $BT2G_READAHEAD
-// sets the depth (default 16); never more than the reference's.
+// sets a smaller depth; by default the reference's (r04q: 16 buffers starved
+// the drivers -- ~400 reads in flight per driver against ~640 with 65).
 #include <pthread.h>
 #include <stdlib.h>
 #include <unistd.h>
@@ -52,7 +53,7 @@ bool PatternSourceServiceFactory::align(int fd, long data_size) {
 	// (the member is const in pat.h and read through `this` at every connection)
 	static std::once_flag once;
 	std::call_once(once, [this] {
-		unsigned int depth = 16;
+		unsigned int depth = n_readahead_;
 		if(const char* e = getenv("BT2G_READAHEAD"))
 			if(atol(e) > 0) depth = (unsigned int)atol(e);
 		if(depth < n_readahead_) const_cast<unsigned int&>(n_readahead_) = depth;
