@@ -13,7 +13,12 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
 def local(path):
-    """A GPU box's path of a repository file, mapped into this checkout."""
+    """A GPU box's path of a repository file, mapped into this checkout
+    ($BT2G_SYM_BIN=<file>: use that file for the batch server's samples -- the
+    binary of the run, when the checkout has been rebuilt since)."""
+    alt = os.environ.get("BT2G_SYM_BIN")
+    if alt and path.endswith("/bowtie2-align-server-batch"):
+        return alt
     if os.path.exists(path) or "/repo/" not in path:
         return path
     return os.path.join(ROOT, path.split("/repo/", 1)[1])
