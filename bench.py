@@ -507,11 +507,16 @@ def pmc_traffic(fetch_csv, write_csv, kernel):
 BATCH_SERVER = os.path.join(ROOT, "oracle", "_ref", "bowtie2-align-server-batch")
 # the engine services' kernel ids (bt2g_api.cpp ProfScope) by call kind, and the
 # kernels' names in the line
-SERVER_KERNELS = [("exact_sweep", 0, "k_exact_sweep", "hbm"), ("seed_search", 1, "k_seed_search", "hbm"),
+SERVER_KERNELS = [("exact_sweep", 0, "k_exact_sweep", "hbm"),
+                  ("exact_sweep", 2, "k_one_mm in the sweep's call (bt2g_exact_sweep_1mm)", None),
+                  ("exact_sweep", 3, "k_range_offsets (the sweep's small ranges' rows)", None),
+                  ("seed_search", 1, "k_seed_search", "hbm"),
+                  ("seed_search", 3, "k_seed_extend + k_seed_offsets (bt2g_seed_search_ext)", None),
                   ("one_mm", 2, "k_one_mm (items/q/near/far/branch/compact)", "hbm"),
                   ("get_offset", 3, "k_get_offset", "hbm"), ("extend", 3, "k_extend", None),
                   ("ungapped", 6, "k_ungapped", None), ("sw_dp", 4, "k_sw_sys (fill + candidate gather)", "valu"),
-                  ("sw_dp", 5, "k_sw_bt_wg / k_sw_bt (nextAlignment loop)", None)]
+                  ("sw_dp", 5, "k_sw_bt_wg / k_sw_bt (nextAlignment loop)", None),
+                  ("sw_dp", 7, "the DP call's whole stream span (copies, fill, walk, pack)", None)]
 
 
 def policy_args(mode, preset):
@@ -611,7 +616,7 @@ def schedule_run(args, rank, world, local, base, reads_np, quals_np, workdir, bi
                    env=env, log_path=os.path.join(workdir, "server.log"), prefix=prefix) as srv:
         log(f"[rank {rank}] batch server ready in {srv.load_s:.1f}s (-p {args.drivers})")
         for _ in range(args.warmup):
-            srv.run(chunks[:max(1, args.warmup_chunks)], k=args.clients)
+            srv.run(chunks[:args.warmup_chunks] if args.warmup_chunks > 0 else chunks, k=args.clients)
         if multi:
             dist.barrier()
         if gpu:
@@ -656,7 +661,7 @@ def stock_baseline(args, base, chunks, batch_outs, workdir):
     with rs.Server(base, threads=threads, args=policy_args(args.mode, args.preset), binary=rs.SERVER,
                    log_path=os.path.join(workdir, "server_stock.log")) as srv:
         for _ in range(args.warmup):
-            srv.run(sample[:max(1, min(args.warmup_chunks, m))], k=args.clients)
+            srv.run(sample[:min(args.warmup_chunks, m)] if args.warmup_chunks > 0 else sample, k=args.clients)
         dt, outs = srv.run(sample, k=args.clients)
         cpu_s = srv.last_cpu_s
     a, b = rs.sorted_records(outs), rs.sorted_records(batch_outs[:m])
@@ -669,7 +674,7 @@ def stock_baseline(args, base, chunks, batch_outs, workdir):
                       f"-p {threads} = the usable cores of this host, {host['model']}) on the first {nreads} "
                       f"{'pairs' if paired else 'reads'} of the batch, <= 10 000 per client connection, "
                       f"{args.clients} connections at a time, after {args.warmup} warmup pass(es) over "
-                      f"{min(args.warmup_chunks, m)} chunk(s)"}, \
+                      f"{min(args.warmup_chunks, m) if args.warmup_chunks > 0 else m} chunk(s)"}, \
         {"sample_reads": nreads, "records": len(a), "records_differing": differ, "identical": differ == 0}
 
 
@@ -986,7 +991,8 @@ def main():
     ap.add_argument("--reads", type=int, default=1_000_000, help="reads (paired: read pairs) per GPU per step")
     ap.add_argument("--drivers", type=int, default=16, help="batch server driver threads (-p)")
     ap.add_argument("--clients", type=int, default=32, help="concurrent client connections (both servers)")
-    ap.add_argument("--warmup-chunks", type=int, default=8)
+    ap.add_argument("--warmup-chunks", type=int, default=0,
+                    help="chunks of a warmup pass (0: all of them -- a warmup step is a whole pass)")
     ap.add_argument("--stock-sample", type=int, default=200_000,
                     help="reads (pairs) timed through the stock server for cpu_baseline and SAM parity (0: skip)")
     ap.add_argument("--chain-steps", type=int, default=2, help="timed steps of the kernel chain (0: skip it)")
