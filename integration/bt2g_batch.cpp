@@ -782,6 +782,16 @@ struct Rq {
 // stream per kind instead of one per driver and kind).  Off: a driver makes
 // its calls itself, one after another, on its own context.
 struct Driver;
+// A driver's reads are split in lanes ($BT2G_LANES, 2): while one lane's
+// requests are with the services, the driver steps the other lane's reads, so
+// a round costs max(stepping, waiting) instead of their sum.
+struct Lane {
+	std::vector<Rq> rq[K_N];                        // this lane's requests of its round, by kind
+	std::vector<std::pair<Slot*, DpRes*>> rq_dp;
+	std::vector<Slot*> run, next;                   // its reads to step, and those stepped
+	int outstanding = 0;                            // kinds handed to services (Driver::out_mu)
+	Driver* d = nullptr;
+};
 struct Svc {
 	int kind = 0;
 	bt2g_ctx* ctx = nullptr;
@@ -794,7 +804,7 @@ struct Svc {
 	std::vector<Svc*> workers;
 	std::mutex mu;
 	std::condition_variable cv;
-	std::vector<Driver*> pending;
+	std::vector<Lane*> pending;
 	// $BT2G_KPROF=1: the engine's per-launch kernel times (HIP events on the
 	// context's stream, bt2g_set_profiling) by kernel id, cumulative; and the
 	// algorithmic work of the calls -- FM kinds: bytes (64 B per occurrence-table
@@ -864,7 +874,9 @@ struct Driver {
 	ReportingMetrics rpm;
 	// slots
 	std::vector<std::unique_ptr<Slot>> all;
-	std::vector<Slot*> freel, run, next;
+	std::vector<Slot*> freel;
+	Lane lanes[2];
+	Lane* cur = &lanes[0];               // the lane being stepped (admitted reads join it)
 	size_t active = 0;
 	// reads in: a feeder thread pops the factory's ready queue for this driver
 	std::mutex in_mu;
@@ -872,17 +884,16 @@ struct Driver {
 	std::vector<Elem*> inbox, got;   // (swapped each round: no allocation once grown)
 	size_t max_slots = 2048;         // reads in flight per driver ($BT2G_BATCH_SLOTS)
 	std::atomic<size_t> active_a{0}; // `active` for the feeder
-	// requests of this round
-	std::vector<Rq> rq[K_N];
-	std::vector<std::pair<Slot*, DpRes*>> rq_dp;
+	// requests of this round: the stepping lane's lists
+	std::vector<Rq>* rq = lanes[0].rq;
+	std::vector<std::pair<Slot*, DpRes*>>* rq_dp = &lanes[0].rq_dp;
 	size_t spec_k = 16;
 	// the engine calls: the device's services, or (services off) the driver's own
 	Svc* svc[K_N] = {};
 	Svc own;
 	std::mutex out_mu;
 	std::condition_variable out_cv;
-	int outstanding = 0;                 // kinds handed to services, not returned yet
-	void svc_done();
+	void svc_done(Lane* l);
 
 	void feeder();
 	void run_loop();
@@ -890,7 +901,8 @@ struct Driver {
 	void release(Slot* s);
 	void step_read(Slot& s);
 	void setup_read(Slot& s);
-	void gpu_phase();
+	void submit(Lane& l);
+	void wait(Lane& l);
 	void prefetch_seeds(Slot& s, int mate);
 	void cpu_dp(Slot& s, DpRes& r, SwAligner& sw);
 
@@ -1416,11 +1428,11 @@ bool SwDriverB::need_dp(Driver& d, Slot& s, int m, bool f, TIndexOffU ti, TRefOf
 		rp.start(x);
 		return true;
 	}
-	d.rq_dp.emplace_back(&s, x);
+	d.rq_dp->emplace_back(&s, x);
 	if(spec && d.spec_k > 1) {
 		std::vector<DpRes*> more;
 		speculate(d, s, more, d.spec_k - 1);
-		for(DpRes* q : more) d.rq_dp.emplace_back(&s, q);
+		for(DpRes* q : more) d.rq_dp->emplace_back(&s, q);
 		g_dp_spec += more.size();
 	}
 	rp.dp = x;
@@ -3139,7 +3151,7 @@ void Svc::loop() {
 	snprintf(nm, sizeof(nm), "bt2g-svc%d", kind);
 	pthread_setname_np(pthread_self(), nm);
 	bt2g_prof_thread(4 + kind);
-	std::vector<Driver*> got;
+	std::vector<Lane*> got;
 	std::vector<Rq> v;
 	std::vector<std::pair<Slot*, DpRes*>> dp;
 	for(;;) {
@@ -3151,9 +3163,9 @@ void Svc::loop() {
 		v.clear();
 		dp.clear();
 		const uint64_t t0 = now_us();
-		for(Driver* d : got) {
-			if(kind == K_DP) dp.insert(dp.end(), d->rq_dp.begin(), d->rq_dp.end());
-			else v.insert(v.end(), d->rq[kind].begin(), d->rq[kind].end());
+		for(Lane* l : got) {
+			if(kind == K_DP) dp.insert(dp.end(), l->rq_dp.begin(), l->rq_dp.end());
+			else v.insert(v.end(), l->rq[kind].begin(), l->rq[kind].end());
 		}
 		run(v, dp);
 		g_svc_us[kind] += now_us() - t0;
@@ -3161,14 +3173,14 @@ void Svc::loop() {
 			std::lock_guard<std::mutex> lk(st_mu);
 			for(int k = 0; k < 8; k++) (void)bt2g_kernel_stats(ctx, k, &k_launch[k], &k_ms[k]);
 		}
-		for(Driver* d : got) d->svc_done();
+		for(Lane* l : got) l->d->svc_done(l);
 		got.clear();
 	}
 }
 
-void Driver::svc_done() {
+void Driver::svc_done(Lane* l) {
 	std::lock_guard<std::mutex> lk(out_mu);
-	if(--outstanding == 0) out_cv.notify_one();
+	if(--l->outstanding == 0) out_cv.notify_one();
 }
 
 // The device's services, started by its first driver.
@@ -3202,37 +3214,43 @@ int svc_stats(char* buf, size_t cap) {
 	return n;
 }
 
-void Driver::gpu_phase() {
-	std::vector<std::pair<Slot*, DpRes*>> none;
+// Hand lane l's requests to the services (services off: make the calls here,
+// one kind after another, on the driver's own context).
+void Driver::submit(Lane& l) {
 	if(!services_on()) {
 		static const int order[K_N] = {K_EXACT, K_SEEDS, K_1MM, K_EXT, K_OFF, K_UG, K_DP};
 		for(int k : order) {
 			own.kind = k;
-			own.run(rq[k], rq_dp);
+			own.run(l.rq[k], l.rq_dp);
 		}
-	} else {
-		int n = 0;
-		for(int k = 0; k < K_N; k++) n += (k == K_DP ? !rq_dp.empty() : !rq[k].empty()) ? 1 : 0;
-		if(n) {
-			{
-				std::lock_guard<std::mutex> lk(out_mu);
-				outstanding = n;
-			}
-			for(int k = 0; k < K_N; k++) {
-				if(k == K_DP ? rq_dp.empty() : rq[k].empty()) continue;
-				Svc* v = svc[k];
-				{
-					std::lock_guard<std::mutex> lk(v->mu);
-					v->pending.push_back(this);
-				}
-				v->cv.notify_one();
-			}
-			std::unique_lock<std::mutex> lk(out_mu);
-			out_cv.wait(lk, [this] { return outstanding == 0; });
-		}
+		return;
 	}
-	for(int k = 0; k < K_N; k++) rq[k].clear();
-	rq_dp.clear();
+	int n = 0;
+	for(int k = 0; k < K_N; k++) n += (k == K_DP ? !l.rq_dp.empty() : !l.rq[k].empty()) ? 1 : 0;
+	if(!n) return;
+	{
+		std::lock_guard<std::mutex> lk(out_mu);
+		l.outstanding = n;
+	}
+	for(int k = 0; k < K_N; k++) {
+		if(k == K_DP ? l.rq_dp.empty() : l.rq[k].empty()) continue;
+		Svc* v = svc[k];
+		{
+			std::lock_guard<std::mutex> lk(v->mu);
+			v->pending.push_back(&l);
+		}
+		v->cv.notify_one();
+	}
+}
+
+// Wait until the services have answered lane l's requests.
+void Driver::wait(Lane& l) {
+	{
+		std::unique_lock<std::mutex> lk(out_mu);
+		out_cv.wait(lk, [&l] { return l.outstanding == 0; });
+	}
+	for(int k = 0; k < K_N; k++) l.rq[k].clear();
+	l.rq_dp.clear();
 }
 
 void Driver::feeder() {
@@ -3312,7 +3330,7 @@ void Driver::admit(Elem* e) {
 		s->nsteps = 0;
 		n++;
 		active++;
-		run.push_back(s);
+		cur->run.push_back(s);
 	} while(ps->nextReadPairReady());
 	// this buffer is held; the one held before goes back (a connection cannot end
 	// while one of its buffers is held, whether or not the input has ended --
@@ -3421,7 +3439,13 @@ void Driver::run_loop() {
 		std::call_once(once, [] { std::thread(term_watch).detach(); });
 	}
 	std::thread(&Driver::feeder, this).detach();
-	for(;;) {
+	const int nlanes = (int)std::min<long>(2, std::max<long>(1, env_or("BT2G_LANES", 2)));
+	for(Lane& l : lanes) l.d = this;
+	for(int li = 0;;) {
+		Lane& L = lanes[li];
+		cur = &L;
+		rq = L.rq;
+		rq_dp = &L.rq_dp;
 		got.clear();
 		{
 			std::unique_lock<std::mutex> lk(in_mu);
@@ -3435,23 +3459,28 @@ void Driver::run_loop() {
 		for(Elem* e : got) admit(e);
 		if(!got.empty()) room_cv.notify_one();
 		const uint64_t t0 = now_us();
-		g_inflight += run.size();
+		g_inflight += L.run.size();
 		bt2g_prof_role(3);
-		for(size_t k = 0; k < run.size(); k++) {
-			Slot* s = run[k];
+		for(size_t k = 0; k < L.run.size(); k++) {
+			Slot* s = L.run[k];
 			s->nsteps++;
 			step_read(*s);
 			if(s->pc == P_FINISH) release(s);
-			else next.push_back(s);
+			else L.next.push_back(s);
 		}
-		run.clear();
+		L.run.clear();
 		active_a.store(active);
 		room_cv.notify_one();
 		const uint64_t t1 = now_us();
 		bt2g_prof_role(1);
-		gpu_phase();
+		submit(L);
+		// the other lane's requests went out a step ago: their answers are what this
+		// driver waits for while L's are served (one lane: L's own)
+		li = (li + 1) % nlanes;
+		Lane& M = lanes[li];
+		wait(M);
+		M.run.swap(M.next);
 		const uint64_t t2 = now_us();
-		run.swap(next);
 		g_rounds++;
 		g_cpu_us += t1 - t0;
 		g_gpu_us += t2 - t1;
