@@ -1,4 +1,7 @@
-# round-4 GPU step: bench.py as the driver runs it, then with rocprofv3 in front of its batch server
+# round-4 GPU step: two lanes vs one, then bench.py as the driver runs it
 set -o pipefail
-bash scripts/gpu_r04.sh bench r04t || exit 1
-bash scripts/gpu_r04.sh benchprof r04t
+export K=32 WARM=8 READS=400000 BT2G_KPROF=1
+bash scripts/gpu_r04.sh batch r04u_l2 "16" || exit 1
+SKIP=--skip-stock BT2G_LANES=1 bash scripts/gpu_r04.sh batch r04u_l1 "16" || exit 1
+unset K WARM READS BT2G_KPROF
+bash scripts/gpu_r04.sh bench r04u
