@@ -354,7 +354,35 @@ inline void xcheck(void* p) {
 		}
 	}
 }
+// $BT2G_ALLOC_SITES=1 (diagnostics): bytes allocated inside a scope the caller
+// marks (bt2g_alloc_site_scope: the batch driver's slot construction), by call
+// site -- what makes a slot's footprint.  Dumped with the stats.
+std::atomic<uint64_t> g_spc[XSLOT], g_scnt[XSLOT], g_sbytes[XSLOT];
+thread_local int t_site_scope = 0;
+bool sites_on() {
+	static const bool on = getenv("BT2G_ALLOC_SITES") != nullptr;
+	return on;
+}
+inline void site_count(void* ra, size_t n) {
+	const uint64_t pc = (uint64_t)(uintptr_t)ra;
+	size_t k = (size_t)((pc * 0x9E3779B97F4A7C15ull) >> 50) & (XSLOT - 1);
+	for(int probe = 0; probe < 64; probe++, k = (k + 1) & (XSLOT - 1)) {
+		uint64_t cur = g_spc[k].load(std::memory_order_relaxed);
+		if(cur == 0) {
+			uint64_t z = 0;
+			if(!g_spc[k].compare_exchange_strong(z, pc) && z != pc) continue;
+			cur = pc;
+		}
+		if(cur == pc) {
+			g_scnt[k].fetch_add(1, std::memory_order_relaxed);
+			g_sbytes[k].fetch_add(n, std::memory_order_relaxed);
+			return;
+		}
+	}
+}
 }  // namespace
+
+extern "C" void bt2g_alloc_site_scope(int on) { t_site_scope += on ? 1 : -1; }
 
 extern "C" void bt2g_alloc_stats_dump() {
 	const char* path = getenv("BT2G_ALLOC_STATS");
@@ -376,6 +404,15 @@ extern "C" void bt2g_alloc_stats_dump() {
 				fprintf(f, "xfree %s %lx %llu\n", di.dli_fname, (unsigned long)(pc - (uint64_t)(uintptr_t)di.dli_fbase),
 				        (unsigned long long)g_xcnt[k].load());
 		}
+	if(sites_on())
+		for(size_t k = 0; k < XSLOT; k++) {
+			const uint64_t pc = g_spc[k].load();
+			if(!pc) continue;
+			Dl_info di;
+			if(dladdr((void*)(uintptr_t)pc, &di) && di.dli_fname)
+				fprintf(f, "site %s %lx %llu %llu\n", di.dli_fname, (unsigned long)(pc - (uint64_t)(uintptr_t)di.dli_fbase),
+				        (unsigned long long)g_scnt[k].load(), (unsigned long long)g_sbytes[k].load());
+		}
 	fclose(f);
 }
 
@@ -383,12 +420,14 @@ void* operator new(size_t n) {
 	void* p = alloc(n);
 	if(!p) throw std::bad_alloc();
 	if(xtrace_on()) xtag(p, __builtin_return_address(0));
+	if(t_site_scope && sites_on()) site_count(__builtin_return_address(0), n);
 	return p;
 }
 void* operator new[](size_t n) {
 	void* p = alloc(n);
 	if(!p) throw std::bad_alloc();
 	if(xtrace_on()) xtag(p, __builtin_return_address(0));
+	if(t_site_scope && sites_on()) site_count(__builtin_return_address(0), n);
 	return p;
 }
 void* operator new(size_t n, const std::nothrow_t&) noexcept { return alloc(n); }

@@ -245,7 +245,8 @@ void write_stats() {
 	}
 }
 
-extern "C" void bt2g_alloc_stats_dump();   // bt2g_alloc.cpp ($BT2G_ALLOC_STATS)
+extern "C" void bt2g_alloc_stats_dump();
+extern "C" void bt2g_alloc_site_scope(int on);   // bt2g_alloc.cpp ($BT2G_ALLOC_SITES)   // bt2g_alloc.cpp ($BT2G_ALLOC_STATS)
 
 // $BT2G_EXIT_CLEAN=1: SIGTERM ends the process through exit() (atexit handlers
 // run: a profiler preloaded into the server writes its trace), from a thread
@@ -3313,7 +3314,9 @@ void Driver::admit(Elem* e) {
 		if(ra.rdid < R_skipReads || ra.rdid >= R_qUpto) continue;
 		Slot* s;
 		if(freel.empty()) {
+			bt2g_alloc_site_scope(1);
 			all.emplace_back(new Slot(*rp, *mapq, (size_t)tid));
+			bt2g_alloc_site_scope(0);
 			g_slots++;
 			s = all.back().get();
 		} else {
