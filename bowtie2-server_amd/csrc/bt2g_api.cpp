@@ -20,6 +20,7 @@
 #include <mutex>
 #include <string>
 #include <unordered_map>
+#include <chrono>
 #include <vector>
 
 #include "bt2g_kernels.h"
@@ -70,8 +71,8 @@ struct bt2g_ctx {
 	struct Pending { int kid; hipEvent_t a, b; };
 	std::vector<Pending> pending;
 	std::vector<hipEvent_t> evpool;
-	uint64_t launches[8] = {0};
-	double total_ms[8] = {0};
+	uint64_t launches[16] = {0};      // 0-7: kernels (HIP events); 8-15: host phases of a call
+	double total_ms[16] = {0};
 	// persistent SW scratch (bt2g_reserve_sw): no allocation / sync per call
 	uint32_t sw_max_prob = 0, sw_max_cols = 0;
 	uint32_t* sw_lists = nullptr;
@@ -628,7 +629,7 @@ int bt2g_set_profiling(bt2g_ctx* c, int on) {
 }
 
 int bt2g_kernel_stats(bt2g_ctx* c, int k, uint64_t* launches, double* total_ms) {
-	if(!c || k < 0 || k >= 8) return fail(BT2G_ERR_ARG, "bad kernel id");
+	if(!c || k < 0 || k >= 16) return fail(BT2G_ERR_ARG, "bad kernel id");
 	drain_prof(c);
 	if(launches) *launches = c->launches[k];
 	if(total_ms) *total_ms = c->total_ms[k];
@@ -1580,6 +1581,13 @@ int bt2g_sw_align_bt_packed(bt2g_ctx* c, const uint8_t* reads, const uint8_t* qu
 	HIPCHK(hipSetDevice(c->device));
 	totals[0] = totals[1] = totals[2] = 0;
 	if(nprob == 0) return BT2G_OK;
+	// (profiling: host phases as ids 8 staging, 9 enqueueing, 10 waiting + copying out)
+	auto hnow = [] { return std::chrono::steady_clock::now(); };
+	auto hadd = [c](int k, std::chrono::steady_clock::time_point a, std::chrono::steady_clock::time_point b) {
+		c->launches[k]++;
+		c->total_ms[k] += std::chrono::duration<double, std::milli>(b - a).count();
+	};
+	const auto h0 = hnow();
 	uint32_t nreads = 0;
 	for(uint32_t i = 0; i < nprob; i++) nreads = probs[i].read + 1 > nreads ? probs[i].read + 1 : nreads;
 	Tmp t(c);
@@ -1625,6 +1633,7 @@ int bt2g_sw_align_bt_packed(bt2g_ctx* c, const uint8_t* reads, const uint8_t* qu
 			return rc;
 	}
 	const SwHint hint = sw_hint(probs, nprob, lens, enable8);
+	const auto h1 = hnow();
 	{
 		// (kernel-stats id 7: the call's whole span on the stream, copies included)
 		ProfScope ps(c, 7, c->stream);
@@ -1636,6 +1645,7 @@ int bt2g_sw_align_bt_packed(bt2g_ctx* c, const uint8_t* reads, const uint8_t* qu
 		HIPCHK(hipGetLastError());
 		if((rc = t.down(tot, doff + 3 * (size_t)nprob, 3))) return rc;
 	}
+	const auto h2 = hnow();
 	if((rc = t.finish())) return rc;
 	if(direct) {
 		memcpy(cands, hpc, sizeof(bt2g_sw_cand) * tot[0]);
@@ -1650,6 +1660,12 @@ int bt2g_sw_align_bt_packed(bt2g_ctx* c, const uint8_t* reads, const uint8_t* qu
 	totals[0] = tot[0];
 	totals[1] = tot[1];
 	totals[2] = tot[2];
+	if(c->prof) {
+		const auto h3 = hnow();
+		hadd(8, h0, h1);
+		hadd(9, h1, h2);
+		hadd(10, h2, h3);
+	}
 	for(uint32_t i = 0; i < nprob; i++)
 		if(res[i].ncand > (int32_t)cap) return fail(BT2G_ERR_OVERFLOW, "problem %u: %d candidates > cap %u", i,
 		                                             res[i].ncand, cap);

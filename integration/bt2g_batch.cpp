@@ -783,7 +783,7 @@ struct Rq {
 // stream per kind instead of one per driver and kind).  Off: a driver makes
 // its calls itself, one after another, on its own context.
 struct Driver;
-// A driver's reads are split in lanes ($BT2G_LANES, 2): while one lane's
+// A driver's reads can be split in lanes ($BT2G_LANES=2; default 1): while one lane's
 // requests are with the services, the driver steps the other lane's reads, so
 // a round costs max(stepping, waiting) instead of their sum.
 struct Lane {
@@ -811,8 +811,8 @@ struct Svc {
 	// algorithmic work of the calls -- FM kinds: bytes (64 B per occurrence-table
 	// side gathered + the read bytes walked, bench.py's figures), DP: cells
 	std::mutex st_mu;
-	uint64_t k_launch[8] = {};
-	double k_ms[8] = {};
+	uint64_t k_launch[16] = {};     // bt2g_kernel_stats ids 0-15
+	double k_ms[16] = {};
 	std::atomic<uint64_t> work{0}, items{0};
 	void loop();
 	void run(std::vector<Rq>& v, std::vector<std::pair<Slot*, DpRes*>>& dp);
@@ -3172,7 +3172,7 @@ void Svc::loop() {
 		g_svc_us[kind] += now_us() - t0;
 		if(kprof_on()) {
 			std::lock_guard<std::mutex> lk(st_mu);
-			for(int k = 0; k < 8; k++) (void)bt2g_kernel_stats(ctx, k, &k_launch[k], &k_ms[k]);
+			for(int k = 0; k < 16; k++) (void)bt2g_kernel_stats(ctx, k, &k_launch[k], &k_ms[k]);
 		}
 		for(Lane* l : got) l->d->svc_done(l);
 		got.clear();
@@ -3188,26 +3188,26 @@ void Driver::svc_done(Lane* l) {
 std::mutex g_svc_mu;
 std::vector<std::array<Svc*, K_N>> g_svcs;
 
-// "kernels": {kind: [[launches, ms] of kernel ids 0..7], work, items} summed over devices
+// "kernels": {kind: [[launches, ms] of ids 0..15 (kernels, then host phases)], work, items} summed over devices
 int svc_stats(char* buf, size_t cap) {
 	if(!kprof_on()) return 0;
 	std::lock_guard<std::mutex> lk(g_svc_mu);
 	int n = snprintf(buf, cap, ", \"kernels\": {");
 	for(int k = 0; k < K_N; k++) {
-		uint64_t L[8] = {}, W = 0, I = 0;
-		double M[8] = {};
+		uint64_t L[16] = {}, W = 0, I = 0;
+		double M[16] = {};
 		for(auto& dv : g_svcs) {
 			if(!dv[k]) continue;
 			for(Svc* v : dv[k]->workers) {
 				std::lock_guard<std::mutex> l2(v->st_mu);
-				for(int i = 0; i < 8; i++) { L[i] += v->k_launch[i]; M[i] += v->k_ms[i]; }
+				for(int i = 0; i < 16; i++) { L[i] += v->k_launch[i]; M[i] += v->k_ms[i]; }
 				W += v->work.load();
 				I += v->items.load();
 			}
 		}
 		n += snprintf(buf + n, cap - n, "%s\"%s\": {\"work\": %llu, \"items\": %llu, \"ids\": [", k ? ", " : "",
 		              K_NAMES[k], (unsigned long long)W, (unsigned long long)I);
-		for(int i = 0; i < 8; i++)
+		for(int i = 0; i < 16; i++)
 			n += snprintf(buf + n, cap - n, "%s[%llu, %.3f]", i ? ", " : "", (unsigned long long)L[i], M[i]);
 		n += snprintf(buf + n, cap - n, "]}");
 	}
@@ -3442,7 +3442,10 @@ void Driver::run_loop() {
 		std::call_once(once, [] { std::thread(term_watch).detach(); });
 	}
 	std::thread(&Driver::feeder, this).detach();
-	const int nlanes = (int)std::min<long>(2, std::max<long>(1, env_or("BT2G_LANES", 2)));
+	// (r04u: two lanes 144 k reads/s against 217 k with one -- half-size lanes
+	// double the services' calls, and their per-call cost, not the stepping, is
+	// what the other lane's wait hides)
+	const int nlanes = (int)std::min<long>(2, std::max<long>(1, env_or("BT2G_LANES", 1)));
 	for(Lane& l : lanes) l.d = this;
 	for(int li = 0;;) {
 		Lane& L = lanes[li];
