@@ -242,7 +242,9 @@ struct Arena {
 			// nothing of an earlier call is in flight: it synchronised before returning
 			if(c->arena) (void)hipFree(c->arena);
 			c->arena = nullptr;
-			size_t cap = std::max<size_t>(c->arena_need + c->arena_need / 4, (size_t)64 << 20);
+			// (doubling: a regrowth frees and re-allocates -- hipFree waits for the device --
+		// so a context that meets bigger and bigger calls regrows a few times, not at each)
+		size_t cap = std::max<size_t>(c->arena_need * 2, (size_t)64 << 20);
 			if(hipMalloc((void**)&c->arena, cap) == hipSuccess) {
 				c->arena_cap = cap;
 			} else {
@@ -256,7 +258,7 @@ struct Arena {
 			if(c->pin_dev) (void)hipFree(c->pin_dev);
 			c->pin = nullptr;
 			c->pin_dev = nullptr;
-			size_t cap = std::max<size_t>(c->pin_need + c->pin_need / 4, (size_t)16 << 20);
+			size_t cap = std::max<size_t>(c->pin_need * 2, (size_t)16 << 20);
 			if(hipHostMalloc((void**)&c->pin, cap, hipHostMallocDefault) == hipSuccess &&
 			   hipMalloc((void**)&c->pin_dev, cap) == hipSuccess &&
 			   hipHostGetDevicePointer((void**)&c->pin_dview, c->pin, 0) == hipSuccess) {

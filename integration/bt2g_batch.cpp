@@ -199,7 +199,8 @@ std::atomic<uint64_t> g_dp_spec{0}, g_dp_used{0}, g_dp_reuse{0}, g_dp_miss{0};
 std::atomic<uint64_t> g_mm_pf{0}, g_mm_pf_used{0};   // 1-mm searches prefetched with the sweep / taken
 std::atomic<uint64_t> g_rows_pf{0};                   // SA rows resolved with the sweep or the seeds
 std::atomic<uint64_t> g_ext_pf{0};
-std::atomic<uint64_t> g_dp_pre_us{0}, g_dp_post_us{0};   // the DP service's host work around its calls                    // extend requests answered by the seed call
+std::atomic<uint64_t> g_dp_pre_us{0}, g_dp_post_us{0};   // the DP service's host work around its calls
+std::atomic<uint64_t> g_dp_again{0};                   // DPs run again (candidates, alignments or edits over the room)                    // extend requests answered by the seed call
 // rounds per read: total and a histogram (bin b: [2^b, 2^(b+1)))
 std::atomic<uint64_t> g_steps{0}, g_steps_hist[16];
 // reads in flight summed over rounds; drivers' time with no read in flight
@@ -222,10 +223,10 @@ void write_stats() {
 		              (unsigned long long)g_req[k].load(), (unsigned long long)g_cpu[k].load(),
 		              (unsigned long long)g_calls[k].load(), g_call_us[k].load() / 1000.0);
 	n += snprintf(buf + n, sizeof(buf) - n, ", \"one_mm_prefetch\": [%llu, %llu], \"rows_prefetched\": %llu, \"ext_prefetched\": %llu"
-	              ", \"dp_host_ms\": [%.1f, %.1f]",
+	              ", \"dp_host_ms\": [%.1f, %.1f], \"dp_again\": %llu",
 	              (unsigned long long)g_mm_pf.load(), (unsigned long long)g_mm_pf_used.load(),
 	              (unsigned long long)g_rows_pf.load(), (unsigned long long)g_ext_pf.load(), g_dp_pre_us.load() / 1000.0,
-	              g_dp_post_us.load() / 1000.0);
+	              g_dp_post_us.load() / 1000.0, (unsigned long long)g_dp_again.load());
 	n += snprintf(buf + n, sizeof(buf) - n, ", \"svc_busy_ms\": [");
 	for(int k = 0; k < K_N; k++)
 		n += snprintf(buf + n, sizeof(buf) - n, "%s%.1f", k ? ", " : "", g_svc_us[k].load() / 1000.0);
@@ -824,7 +825,7 @@ struct Svc {
 	void call_off(std::vector<Rq>& v);
 	void call_ug(std::vector<Rq>& v);
 	void call_dp(std::vector<std::pair<Slot*, DpRes*>>& v);
-	void run_dp(const std::vector<std::pair<Slot*, DpRes*>>& v, uint32_t cap, uint32_t maxaln);
+	void run_dp(const std::vector<std::pair<Slot*, DpRes*>>& v, uint32_t cap, uint32_t maxaln, uint32_t me);
 	uint32_t row_of(Pack& pk, Slot& s, int m);
 };
 
@@ -1251,7 +1252,7 @@ void Svc::call_ug(std::vector<Rq>& v) {
 // (bt2g_sw_align_bt_packed).  A DP whose candidate list outgrew `cap`, or that
 // may have more than `maxaln` alignments, runs again alone with room for all;
 // one with more candidates than the engine takes goes to the CPU when used.
-void Svc::run_dp(const std::vector<std::pair<Slot*, DpRes*>>& v, uint32_t cap, uint32_t maxaln) {
+void Svc::run_dp(const std::vector<std::pair<Slot*, DpRes*>>& v, uint32_t cap, uint32_t maxaln, uint32_t me) {
 	struct B {
 		Pack pk;
 		std::vector<bt2g_sw_problem> P;
@@ -1291,7 +1292,12 @@ void Svc::run_dp(const std::vector<std::pair<Slot*, DpRes*>>& v, uint32_t cap, u
 		work += cells;
 		items += n;
 	}
-	const uint32_t maxedit = 2 * stride + 8;
+	// edits stored per alignment: `me` (0: all an alignment can have, 2 x stride + 8);
+	// an alignment with more runs again with room for all (the engine reports
+	// the true count).  The output blocks are sized nprob x maxaln x maxedit:
+	// the full bound made ~20 KB of pinned staging per DP
+	const uint32_t full = 2 * stride + 8;
+	const uint32_t maxedit = me && me < full ? me : full;
 	b.R.resize(n);
 	b.NA.resize(n);
 	b.A.resize(n * (size_t)maxaln);
@@ -1311,7 +1317,7 @@ void Svc::run_dp(const std::vector<std::pair<Slot*, DpRes*>>& v, uint32_t cap, u
 	g_calls[K_DP]++;
 	if(rc && rc != BT2G_ERR_OVERFLOW) die("bt2g_sw_align_bt_packed", rc);
 	std::vector<std::pair<Slot*, DpRes*>> again;
-	uint32_t cap2 = cap, maxaln2 = maxaln;
+	uint32_t cap2 = cap, maxaln2 = maxaln, me2 = me;
 	size_t oc = 0, oe = 0;
 	for(size_t i = 0; i < n; i++) {
 		DpRes& r = *v[i].second;
@@ -1329,10 +1335,14 @@ void Svc::run_dp(const std::vector<std::pair<Slot*, DpRes*>>& v, uint32_t cap, u
 			r.ready = true;
 			continue;
 		}
-		if(o.ncand > (int32_t)cap || (b.NA[i] == (int32_t)maxaln && o.ncand > (int32_t)maxaln)) {
+		bool trunc = false;
+		for(uint32_t k = 0; k < na; k++) trunc = trunc || b.A[i * maxaln + k].nedit > (int32_t)maxedit;
+		if(o.ncand > (int32_t)cap || (b.NA[i] == (int32_t)maxaln && o.ncand > (int32_t)maxaln) || trunc) {
 			again.push_back(v[i]);
-			cap2 = std::max<uint32_t>(cap2, (uint32_t)o.ncand);
-			maxaln2 = std::max<uint32_t>(maxaln2, (uint32_t)o.ncand);
+			if(o.ncand > (int32_t)cap) cap2 = std::max<uint32_t>(cap2, (uint32_t)o.ncand);
+			if(b.NA[i] == (int32_t)maxaln && o.ncand > (int32_t)maxaln)
+				maxaln2 = std::max<uint32_t>(maxaln2, (uint32_t)o.ncand);
+			if(trunc) me2 = 0;
 			continue;
 		}
 		if(b.NA[i] < 0) die("bt2g_sw_align_bt_packed (status)", b.NA[i]);
@@ -1351,7 +1361,10 @@ void Svc::run_dp(const std::vector<std::pair<Slot*, DpRes*>>& v, uint32_t cap, u
 		        (unsigned long long)tot[2], oc, oe);
 		abort();
 	}
-	if(!again.empty()) run_dp(again, cap2, maxaln2);
+	if(!again.empty()) {
+		g_dp_again += again.size();
+		run_dp(again, cap2, maxaln2, me2);
+	}
 }
 
 void Svc::call_dp(std::vector<std::pair<Slot*, DpRes*>>& v) {
@@ -1361,8 +1374,9 @@ void Svc::call_dp(std::vector<std::pair<Slot*, DpRes*>>& v) {
 	std::vector<std::pair<Slot*, DpRes*>> sh, lg;
 	for(auto& q : v) (q.first->rdlens[q.second->mate] > 1024 ? lg : sh).push_back(q);
 	const uint32_t cap = R_localAlign ? 2048 : 512;
-	if(!sh.empty()) run_dp(sh, cap, 8);
-	if(!lg.empty()) run_dp(lg, cap, 8);
+	static const uint32_t me = (uint32_t)env_or("BT2G_DP_MAXEDIT", 48);
+	if(!sh.empty()) run_dp(sh, cap, 8, me);
+	if(!lg.empty()) run_dp(lg, cap, 8, me);
 }
 
 // A DP the engine does not take (reads at or above --cp-min, longer than

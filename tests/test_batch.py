@@ -146,6 +146,18 @@ def test_batch_no_speculation_cpu(indexes, tmp_path):
     assert st["dp"][0] == 0
 
 
+def test_batch_dp_reruns_cpu(indexes, tmp_path):
+    """Tiny first-pass room (BT2G_DP_MAXEDIT=2 edits per alignment; two lanes per
+    driver): DPs whose alignments have more edits run again with room for all,
+    and the SAM is the same."""
+    _need(rs.SERVER, rs.CLIENT, SRV_BATCH_STUB)
+    base, idx = indexes["synth"]
+    chunks = _reads(idx, 800, 19, str(tmp_path))
+    _, _, _, st = compare(SRV_BATCH_STUB, base, chunks, [], str(tmp_path),
+                          env_extra={"BT2G_DP_MAXEDIT": "2", "BT2G_LANES": "2"})
+    assert st["dp_again"] > 0
+
+
 def test_batch_no_services_cpu(indexes, tmp_path):
     """BT2G_SERVICES=0: every driver makes its own engine calls, one kind after another."""
     _need(rs.SERVER, rs.CLIENT, SRV_BATCH_STUB)
