@@ -505,6 +505,32 @@ def pmc_traffic(fetch_csv, write_csv, kernel):
 
 
 BATCH_SERVER = os.path.join(ROOT, "oracle", "_ref", "bowtie2-align-server-batch")
+# HBM traffic per launch of the batch server's kernels: the summary of separate
+# rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes over this same bench command
+# (scripts/gpu_r04.sh benchpmc -> scripts/pmc_summary.py), committed under profiles/
+SERVER_PMC = os.path.join(ROOT, "profiles", "r04", "server_pmc.json")
+
+
+def server_traffic(path, kernel):
+    """(bytes per launch, note) of `kernel` (name prefix) from a pmc_summary.py
+    file: FETCH_SIZE doubled (gfx950 counts 64 B per 128-B request) + WRITE_SIZE,
+    summed over the kernel's instantiations weighted by their dispatches."""
+    try:
+        d = json.load(open(path))
+    except (OSError, ValueError):
+        return None, None
+    tot, n = 0.0, 0
+    for name, v in d.get("kernels", {}).items():
+        if not (name == kernel or name.startswith(kernel + "<") or name.startswith(kernel + "_")):
+            continue
+        if v.get("fetch_bytes_x2") is None or v.get("write_bytes") is None:
+            continue
+        tot += (v["fetch_bytes_x2"] + v["write_bytes"]) * v["dispatches"]
+        n += v["dispatches"]
+    if not n:
+        return None, None
+    return tot / n, (f"{os.path.relpath(path, ROOT)}: FETCH_SIZE x 2 + WRITE_SIZE per dispatch of {kernel}* "
+                     f"({n} dispatches of separate --pmc passes of bench.py with rocprofv3 in front of the server)")
 # the engine services' kernel ids (bt2g_api.cpp ProfScope) by call kind, and the
 # kernels' names in the line
 SERVER_KERNELS = [("exact_sweep", 0, "k_exact_sweep", "hbm"),
@@ -1018,6 +1044,8 @@ def main():
                          "genome model and size; '': always build)")
     ap.add_argument("--pmc-fetch", default="", help="rocprofv3 --pmc FETCH_SIZE counter_collection.csv of this "
                                                     "command: fills roofline.traffic")
+    ap.add_argument("--server-pmc", default=SERVER_PMC, help="pmc_summary.py file for the batch server's kernels "
+                    "(roofline.traffic)")
     ap.add_argument("--pmc-write", default="", help="same for WRITE_SIZE")
     args = ap.parse_args()
 
@@ -1108,8 +1136,9 @@ def main():
         rl = None
         if dom_k:
             d = kern[dom_k]
+            traffic, tnote = server_traffic(args.server_pmc, PMC_KERNEL.get(int(dom_k.split(":")[1]), "?"))
             rl = {"bound": d["bound"], "kernel": d["kernel"], "achieved": d["achieved"], "peak": d["peak"],
-                  "unit": d["unit"], "frac": d["frac"], "traffic": None,
+                  "unit": d["unit"], "frac": d["frac"], "traffic": traffic, "traffic_source": tnote,
                   "ms_per_launch": d["ms_per_launch"], "launches": d["launches"],
                   "per_launch_work": (d.get("bytes_total") or d.get("cells_total")) / d["launches"],
                   "work_unit": "bytes" if d["bound"] == "hbm" else "DP cells",

@@ -50,6 +50,14 @@ benchprof)
     timeout -k 10 1100 python3 -u bench.py --chain-steps 0 $BENCH_ARGS > $O/bench_prof.json 2> $O/bench_prof.log || { tail -30 $O/bench_prof.log; exit 1; }
   find $O/bprof -name "*kernel_stats.csv"
   find $O/bprof -name "*.csv" -size +40M -delete ;;
+benchpmc)
+  # separate FETCH_SIZE / WRITE_SIZE passes over the batch server's kernels (bench.py, 200 k reads)
+  for c in FETCH_SIZE WRITE_SIZE; do
+    BT2G_BENCH_SERVER_PREFIX="rocprofv3 --pmc $c --output-format csv -d $PWD/$O/pmc_$c -o run --" \
+      timeout -k 10 900 python3 -u bench.py --chain-steps 0 --no-cpu-baseline --reads 200000 > $O/bench_pmc_$c.json 2> $O/bench_pmc_$c.log || { tail -30 $O/bench_pmc_$c.log; exit 1; }
+  done
+  python3 scripts/pmc_summary.py $O/pmc_FETCH_SIZE $O/pmc_WRITE_SIZE $O/server_pmc.json
+  find $O -name "*.csv" -size +40M -delete ;;
 tests)
   timeout -k 10 1000 python -u -m pytest tests -m gpu -x -v --timeout 600 --timeout-method thread > $O/gpu_tests.log 2>&1 || { tail -20 $O/gpu_tests.log; exit 1; }
   tail -2 $O/gpu_tests.log

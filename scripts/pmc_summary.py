@@ -1,0 +1,50 @@
+#!/usr/bin/env python3
+"""Per-kernel HBM traffic from rocprofv3 --pmc passes (one pass per counter):
+
+  python scripts/pmc_summary.py FETCH_DIR WRITE_DIR OUT.json
+
+Every *counter_collection.csv under each directory (one per profiled process)
+is read; per kernel name (template arguments kept), the mean FETCH_SIZE and
+WRITE_SIZE per dispatch in KiB and bytes.  FETCH_SIZE is also given doubled:
+on gfx950 it counts 64 B per 128-B request for wide coalesced reads
+(/opt/skills/guides/MI355X_MICROARCH.md, HBM section), uncalibrated for 64-B
+gathers -- both figures are kept."""
+import collections
+import csv
+import glob
+import json
+import os
+import sys
+
+
+def per_kernel(d, counter):
+    vals = collections.defaultdict(list)
+    for path in glob.glob(os.path.join(d, "**", "*counter_collection.csv"), recursive=True):
+        for r in csv.DictReader(open(path)):
+            if r.get("Counter_Name", counter) != counter:
+                continue
+            name = r["Kernel_Name"].split("(")[0].replace("void ", "").strip()
+            vals[name].append(float(r["Counter_Value"]))
+    return vals
+
+
+def main():
+    fd, wd, out = sys.argv[1:4]
+    f = per_kernel(fd, "FETCH_SIZE")
+    w = per_kernel(wd, "WRITE_SIZE")
+    res = {}
+    for k in sorted(set(f) | set(w)):
+        fk = sum(f[k]) / len(f[k]) if f.get(k) else None
+        wk = sum(w[k]) / len(w[k]) if w.get(k) else None
+        res[k] = {"dispatches": max(len(f.get(k, [])), len(w.get(k, []))),
+                  "fetch_kib": fk, "write_kib": wk,
+                  "fetch_bytes": fk * 1024 if fk is not None else None,
+                  "fetch_bytes_x2": fk * 2048 if fk is not None else None,
+                  "write_bytes": wk * 1024 if wk is not None else None}
+    json.dump({"source": {"fetch": fd, "write": wd}, "kernels": res}, open(out, "w"), indent=1)
+    for k, v in sorted(res.items(), key=lambda kv: -(kv[1]["dispatches"] or 0))[:20]:
+        print(k[:80], v["dispatches"], v["fetch_kib"], v["write_kib"])
+
+
+if __name__ == "__main__":
+    main()
