@@ -1,7 +1,4 @@
-# round-4 GPU step: DP staging fix (first-pass edit room, doubling arenas), local kernels, bench
+# round-4 GPU step: PMC passes of the batch server's kernels, then the kernel-trace profile of the bench command
 set -o pipefail
-export K=32 WARM=8 READS=400000 BT2G_KPROF=1
-bash scripts/gpu_r04.sh batch r04w "16" || exit 1
-SKIP=--skip-stock SARGS=--local READS=200000 bash scripts/gpu_r04.sh batch r04w_local "16" || exit 1
-unset K WARM READS BT2G_KPROF
-bash scripts/gpu_r04.sh bench r04w
+bash scripts/gpu_r04.sh benchpmc r04x || exit 1
+BENCH_ARGS="--no-cpu-baseline" bash scripts/gpu_r04.sh benchprof r04x
