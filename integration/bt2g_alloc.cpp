@@ -197,12 +197,19 @@ char* arena_take(size_t bytes) {
 }
 
 char* slab_take(size_t bytes) {
-	static Range* r = new (malloc(sizeof(Range))) Range(arena_gb() ? 1024 : 0, true);
+	// (small pages unless $BT2G_SLAB_HUGE=1: with THP defrag "madvise" a huge-page
+	// fault may compact memory first -- the CPU stand-in's drivers spent 29 % of their
+	// samples in the slab's first touch with huge pages, 15 % without)
+	static const bool huge = [] { const char* e = getenv("BT2G_SLAB_HUGE"); return e && *e == '1'; }();
+	static Range* r = new (malloc(sizeof(Range))) Range(arena_gb() ? 1024 : 0, huge);
 	return r->take(bytes);
 }
 
+thread_local size_t t_fresh = 0;        // bytes of the slab the last allocation took ($BT2G_ALLOC_SITES=fresh)
+
 void* fresh(int c) {
 	if(stats_on()) g_fresh[c].fetch_add(1, std::memory_order_relaxed);
+	t_fresh = size_of(c) < ((size_t)64 << 10) ? SLAB : HDR + size_of(c);
 	const size_t bsz = HDR + size_of(c);
 	const size_t nb = size_of(c) < ((size_t)64 << 10) && !t_dead ? SLAB / bsz : 1;
 	// (64 KiB - 1 MiB blocks one at a time from the slab range too: from malloc they
@@ -363,6 +370,20 @@ bool sites_on() {
 	static const bool on = getenv("BT2G_ALLOC_SITES") != nullptr;
 	return on;
 }
+// $BT2G_ALLOC_SITES=fresh: only the allocations that took new memory (a slab,
+// or a block of its own), counted with the bytes taken
+bool sites_fresh() {
+	static const bool on = [] { const char* e = getenv("BT2G_ALLOC_SITES"); return e && !strcmp(e, "fresh"); }();
+	return on;
+}
+// $BT2G_ALLOC_SITES_CLASS=<bytes>: also every allocation of that size class, anywhere
+int sites_cls() {
+	static const int c = [] {
+		const char* e = getenv("BT2G_ALLOC_SITES_CLASS");
+		return e && atol(e) > 0 ? cls_of((size_t)atol(e)) : -1;
+	}();
+	return c;
+}
 inline void site_count(void* ra, size_t n) {
 	const uint64_t pc = (uint64_t)(uintptr_t)ra;
 	size_t k = (size_t)((pc * 0x9E3779B97F4A7C15ull) >> 50) & (XSLOT - 1);
@@ -420,14 +441,28 @@ void* operator new(size_t n) {
 	void* p = alloc(n);
 	if(!p) throw std::bad_alloc();
 	if(xtrace_on()) xtag(p, __builtin_return_address(0));
-	if(t_site_scope && sites_on()) site_count(__builtin_return_address(0), n);
+	if(sites_on()) {
+		if(sites_fresh()) {
+			if(t_fresh) site_count(__builtin_return_address(0), t_fresh);
+		} else if(t_site_scope || (n <= MAXSZ && cls_of(n) == sites_cls())) {
+			site_count(__builtin_return_address(0), n);
+		}
+		t_fresh = 0;
+	}
 	return p;
 }
 void* operator new[](size_t n) {
 	void* p = alloc(n);
 	if(!p) throw std::bad_alloc();
 	if(xtrace_on()) xtag(p, __builtin_return_address(0));
-	if(t_site_scope && sites_on()) site_count(__builtin_return_address(0), n);
+	if(sites_on()) {
+		if(sites_fresh()) {
+			if(t_fresh) site_count(__builtin_return_address(0), t_fresh);
+		} else if(t_site_scope || (n <= MAXSZ && cls_of(n) == sites_cls())) {
+			site_count(__builtin_return_address(0), n);
+		}
+		t_fresh = 0;
+	}
 	return p;
 }
 void* operator new(size_t n, const std::nothrow_t&) noexcept { return alloc(n); }
