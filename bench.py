@@ -540,7 +540,8 @@ SERVER_KERNELS = [("exact_sweep", 0, "k_exact_sweep", "hbm"),
                   ("seed_search", 3, "k_seed_extend + k_seed_offsets (bt2g_seed_search_ext)", None),
                   ("one_mm", 2, "k_one_mm (items/q/near/far/branch/compact)", "hbm"),
                   ("get_offset", 3, "k_get_offset", "hbm"), ("extend", 3, "k_extend", None),
-                  ("ungapped", 6, "k_ungapped", None), ("sw_dp", 4, "k_sw_sys (fill + candidate gather)", "valu"),
+                  ("ungapped", 6, "k_ungapped", None), ("sw_dp", 4, "k_sw_sys (fill, with the candidate gather)", "valu"),
+                  ("sw_dp", 11, "k_sort_small / k_sort_big (candidate sort)", None),
                   ("sw_dp", 5, "k_sw_bt_wg / k_sw_bt (nextAlignment loop)", None),
                   ("sw_dp", 7, "the DP call's whole stream span (copies, fill, walk, pack)", None)]
 

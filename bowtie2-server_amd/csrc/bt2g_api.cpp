@@ -897,6 +897,9 @@ static int sw_align_impl(bt2g_ctx* c, const uint8_t* reads, const uint8_t* quals
 			               c->ref_starts, C, cap, bnd, maxcol, res, cands, mat, mat_off, satl, counts + 3, po, st);
 		}
 		}
+	}
+	{
+		ProfScope ps(c, 11, st);            // (kernel-stats id 11: the candidate sort)
 		launch_sort_cands(res, cands, nprob, cap, list8, counts + 4, st);   // list8 is free again
 	}
 	HIPCHK(hipGetLastError());

@@ -886,7 +886,9 @@ static uint32_t bt_lds_bytes(const BtArgs& a) {
 // (read at every launch: the parity tests run one batch both ways)
 static uint32_t bt_lds_max() {
 	const char* e = getenv("BT2G_BT_LDS_MAX");
-	return e ? (uint32_t)atol(e) : 8192u;
+	// (the workgroup walk at any batch-server size: r04x, 76 DP calls over 8 192
+	// problems took the lane-per-DP walk at ~11 ms each against ~0.3 ms)
+	return e ? (uint32_t)atol(e) : 65536u;
 }
 
 void launch_sw_bt(int kind, const BtArgs& a, hipStream_t st) {

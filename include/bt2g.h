@@ -504,7 +504,7 @@ int bt2g_set_profiling(bt2g_ctx* ctx, int on);
 /* kernel ids: 0 exact_sweep, 1 seed_search, 2 one_mm, 3 get_offset / extend / range offsets, 4 sw_align,
  * 5 sw_backtrace, 6 ungapped, 7 frame / the whole stream span of a bt2g_sw_align_bt_packed call;
  * host phases of a bt2g_sw_align_bt_packed call (wall time): 8 staging, 9 enqueueing, 10 waiting and
- * copying out */
+ * copying out; 11 the SW candidate sort (kernels, HIP events) */
 int bt2g_kernel_stats(bt2g_ctx* ctx, int kernel, uint64_t* launches, double* total_ms);
 int bt2g_reset_stats(bt2g_ctx* ctx);
 
