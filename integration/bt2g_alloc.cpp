@@ -197,10 +197,11 @@ char* arena_take(size_t bytes) {
 }
 
 char* slab_take(size_t bytes) {
-	// (small pages unless $BT2G_SLAB_HUGE=1: with THP defrag "madvise" a huge-page
-	// fault may compact memory first -- the CPU stand-in's drivers spent 29 % of their
-	// samples in the slab's first touch with huge pages, 15 % without)
-	static const bool huge = [] { const char* e = getenv("BT2G_SLAB_HUGE"); return e && *e == '1'; }();
+	// ($BT2G_SLAB_HUGE=0: small pages.  On the CPU stand-in the drivers spent 29 %
+	// of their samples in a slab's first touch with huge pages and 15 % without, but
+	// on the GPU box the drivers' CPU rose from 29.8 s to 45.7 s without them, r04w
+	// vs r04y: huge pages by default)
+	static const bool huge = [] { const char* e = getenv("BT2G_SLAB_HUGE"); return !(e && *e == '0'); }();
 	static Range* r = new (malloc(sizeof(Range))) Range(arena_gb() ? 1024 : 0, huge);
 	return r->take(bytes);
 }
