@@ -1,7 +1,7 @@
-# round-4 GPU step: slab pages A/B on one box, then bench
+# round-4 GPU step: speculative DPs per ask and slots per driver, on one box
 set -o pipefail
-export K=32 WARM=8 READS=400000 BT2G_KPROF=1
-bash scripts/gpu_r04.sh batch r04z "16" || exit 1
-SKIP=--skip-stock BT2G_SLAB_HUGE=0 bash scripts/gpu_r04.sh batch r04z_small "16" || exit 1
-unset K WARM READS BT2G_KPROF
-bash scripts/gpu_r04.sh bench r04z
+export K=32 WARM=8 READS=400000 SKIP=--skip-stock
+bash scripts/gpu_r04.sh batch r04aa "16" || exit 1
+BT2G_SPEC_DPS=8 bash scripts/gpu_r04.sh batch r04aa_spec8 "16" || exit 1
+BT2G_SPEC_DPS=4 bash scripts/gpu_r04.sh batch r04aa_spec4 "16" || exit 1
+BT2G_BATCH_SLOTS=1024 bash scripts/gpu_r04.sh batch r04aa_sl1k "16"
