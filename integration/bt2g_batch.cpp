@@ -1370,12 +1370,20 @@ void Svc::run_dp(const std::vector<std::pair<Slot*, DpRes*>>& v, uint32_t cap, u
 void Svc::call_dp(std::vector<std::pair<Slot*, DpRes*>>& v) {
 	if(v.empty()) return;
 	g_req[K_DP] += v.size();
-	// long reads (> 1024 bases) batch apart: a batch is padded to its longest read
-	std::vector<std::pair<Slot*, DpRes*>> sh, lg;
-	for(auto& q : v) (q.first->rdlens[q.second->mate] > 1024 ? lg : sh).push_back(q);
+	// long reads (> 1024 bases) batch apart: a batch is padded to its longest read;
+	// and DPs wider than twice their read (mate searches, ~150 x 700) apart from the
+	// rest: the engine picks the walk for a whole call by its widest DP, and one
+	// wide DP would send a call's seed extensions to the H-plane walk (r04v
+	// paired: 14.5 ms DP calls) instead of the decision plane + workgroup walk
+	std::vector<std::pair<Slot*, DpRes*>> sh, wide, lg;
+	for(auto& q : v) {
+		const size_t len = q.first->rdlens[q.second->mate];
+		(len > 1024 ? lg : (size_t)q.second->ncol > 2 * len ? wide : sh).push_back(q);
+	}
 	const uint32_t cap = R_localAlign ? 2048 : 512;
 	static const uint32_t me = (uint32_t)env_or("BT2G_DP_MAXEDIT", 48);
 	if(!sh.empty()) run_dp(sh, cap, 8, me);
+	if(!wide.empty()) run_dp(wide, cap, 8, me);
 	if(!lg.empty()) run_dp(lg, cap, 8, me);
 }
 
