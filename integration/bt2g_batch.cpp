@@ -889,7 +889,7 @@ struct Driver {
 	// requests of this round: the stepping lane's lists
 	std::vector<Rq>* rq = lanes[0].rq;
 	std::vector<std::pair<Slot*, DpRes*>>* rq_dp = &lanes[0].rq_dp;
-	size_t spec_k = 16;
+	size_t spec_k = 8;
 	// the engine calls: the device's services, or (services off) the driver's own
 	Svc* svc[K_N] = {};
 	Svc own;
@@ -3452,7 +3452,10 @@ void Driver::run_loop() {
 	pepol.reset(new PairedEndPolicy(pepolFlag, gMaxInsert, gMinInsert, R_localAlign, gFlippedMatesOK, gDovetailMatesOK,
 	                                gContainMatesOK, gOlapMatesOK, gExpandToFrag));
 	max_slots = env_or("BT2G_BATCH_SLOTS", 2048);
-	spec_k = env_or("BT2G_SPEC_DPS", 16);
+	// (r04aa, one box: 16 -> 200 k reads/s, 8 -> 228 k, 4 -> 219 k: past 8 the
+	// speculative DPs cost the drivers and the DP service more than the rounds
+	// they save)
+	spec_k = env_or("BT2G_SPEC_DPS", 8);
 	{
 		char nm[16];
 		snprintf(nm, sizeof(nm), "bt2g-drv%d", tid);
