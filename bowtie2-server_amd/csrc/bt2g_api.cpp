@@ -950,6 +950,17 @@ static SwHint sw_hint(const bt2g_sw_problem* probs, uint32_t nprob, const uint32
 	return h;
 }
 
+// The widest DP (columns / rows) whose fill writes the walk's decision plane
+// ($BT2G_DEC_RATIO, default 2: wider ones -- mate searches -- keep the H plane:
+// the decision bits cost fill work on every cell, and a walk touches few)
+static uint32_t dec_ratio() {
+	static const uint32_t r = [] {
+		const char* e = getenv("BT2G_DEC_RATIO");
+		return e && atol(e) > 0 ? (uint32_t)atol(e) : 2u;
+	}();
+	return r;
+}
+
 static bool bt_hplane() {
 	static const bool on = [] { const char* e = getenv("BT2G_BT_HPLANE"); return e && *e == '1'; }();
 	return on;
@@ -1021,7 +1032,7 @@ static int sw_align_bt_impl(bt2g_ctx* c, const uint8_t* reads, const uint8_t* qu
 		hb = packed && all8 && !sc->local ? 1 : 2;
 		// end-to-end systolic fills, u8 and i16 alike (long reads: minsc < -254), write
 		// the walk's decisions (kind 2, the u8 plane's layout)
-		if(packed && !sc->local && !bt_hplane() && maxcol <= 2u * maxrow) hb = 1;
+		if(packed && !sc->local && !bt_hplane() && maxcol <= dec_ratio() * maxrow) hb = 1;
 		if((rc = talloc((void**)&plane, (size_t)sw_plane_slot(stride, maxcol, hb) * nprob))) return rc;
 	}
 	// systolic fill: bottom-aligned rows, u8 (hb 1) or u16 plane with block masks;
@@ -1030,7 +1041,7 @@ static int sw_align_bt_impl(bt2g_ctx* c, const uint8_t* reads, const uint8_t* qu
 	// 2, 4 bits); BT2G_BT_HPLANE=1 keeps the H score plane (kind 0) for A/B runs
 	// (wide DPs -- mate searches, 150 x 705 -- keep the H plane: the decision bits
 	// cost fill work per cell, and their walks touch a small share of the cells)
-	const bool dec = packed && !sc->local && !bt_hplane() && maxcol <= 2u * maxrow && (!reserved || hb == 1);
+	const bool dec = packed && !sc->local && !bt_hplane() && maxcol <= dec_ratio() * maxrow && (!reserved || hb == 1);
 	const int kind = dec ? 2 : hb == 1 ? 0 : 1;
 	a.plane = plane;
 	a.slot = sw_plane_slot(stride, maxcol, hb);

@@ -899,7 +899,7 @@ void launch_sw_bt(int kind, const BtArgs& a, hipStream_t st) {
 		const char* e = getenv("BT2G_BT_WG");
 		if(!(e && *e == '0')) {
 			const uint32_t lw = sw_bt_wg_lds(a);
-			if(lw <= 65536u) {
+			if(lw <= sw_bt_wg_lds_limit()) {
 				launch_sw_bt_wg(a, lw, st);
 				return;
 			}

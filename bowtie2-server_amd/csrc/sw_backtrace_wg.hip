@@ -397,6 +397,26 @@ uint32_t sw_bt_wg_lds(const BtArgs& a) {
 	return L.total;
 }
 
+// The dynamic LDS a workgroup of k_sw_bt_wg may take: 64 KiB, or (BT2G_BT_WG_LDS=1)
+// what the device lets a block opt in to (up to the CU's 160 KiB), set once on
+// the kernel -- wide planes (mate searches) then fit.
+uint32_t sw_bt_wg_lds_limit() {
+	static const uint32_t lim = [] {
+		const char* e = getenv("BT2G_BT_WG_LDS");
+		if(!(e && *e == '1')) return 65536u;
+		int dev = 0, v = 0;
+		if(hipGetDevice(&dev) != hipSuccess ||
+		   hipDeviceGetAttribute(&v, hipDeviceAttributeSharedMemPerBlockOptin, dev) != hipSuccess || v <= 65536)
+			return 65536u;
+		if(hipFuncSetAttribute((const void*)k_sw_bt_wg, hipFuncAttributeMaxDynamicSharedMemorySize, v) != hipSuccess) {
+			(void)hipGetLastError();
+			return 65536u;
+		}
+		return (uint32_t)v;
+	}();
+	return lim;
+}
+
 void launch_sw_bt_wg(const BtArgs& a, uint32_t lds, hipStream_t st) {
 	hipLaunchKernelGGL(k_sw_bt_wg, dim3(a.nprob), dim3(64), lds, st, a);
 }

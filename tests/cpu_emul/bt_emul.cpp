@@ -10,6 +10,7 @@
 thread_local uint3v threadIdx, blockIdx;
 // the workgroup kernel (sw_backtrace_wg.hip) runs in tests/cpu_emul/wg_emul.cpp
 uint32_t sw_bt_wg_lds(const BtArgs&) { return 0xffffffffu; }
+uint32_t sw_bt_wg_lds_limit() { return 65536u; }
 void launch_sw_bt_wg(const BtArgs&, uint32_t, hipStream_t) { abort(); }
 #ifdef BT2G_BT_COUNT
 unsigned long long bt_counts[16];

@@ -24,6 +24,15 @@ inline uint4 make_uint4(uint32_t a, uint32_t b, uint32_t c, uint32_t d) { return
 extern thread_local uint3v threadIdx, blockIdx;
 typedef void* hipStream_t;
 typedef void* hipEvent_t;
+// (sw_bt_wg_lds_limit: the emulation keeps the 64 KiB default)
+typedef int hipError_t;
+enum { hipSuccess = 0 };
+enum { hipDeviceAttributeSharedMemPerBlockOptin = 0 };
+enum { hipFuncAttributeMaxDynamicSharedMemorySize = 0 };
+inline hipError_t hipGetDevice(int* d) { *d = 0; return hipSuccess; }
+inline hipError_t hipDeviceGetAttribute(int* v, int, int) { *v = 65536; return hipSuccess; }
+inline hipError_t hipFuncSetAttribute(const void*, int, int) { return hipSuccess; }
+inline hipError_t hipGetLastError() { return hipSuccess; }
 struct int2 { int32_t x, y; };
 struct uint2 { uint32_t x, y; };
 
