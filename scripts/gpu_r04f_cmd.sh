@@ -1,3 +1,5 @@
-# round-4 GPU step: the whole GPU test suite and smoke(), as the driver runs them
+# round-4 GPU step: paired with the decision plane + workgroup walk for mate searches (SAM vs stock), and without
 set -o pipefail
-bash scripts/gpu_r04.sh tests r04ac
+export K=32 WARM=8 MODE=paired READS=200000
+BT2G_DEC_RATIO=6 BT2G_BT_WG_LDS=1 bash scripts/gpu_r04.sh batch r04ad_wide "16" || exit 1
+SKIP=--skip-stock bash scripts/gpu_r04.sh batch r04ad "16"
