@@ -397,13 +397,13 @@ uint32_t sw_bt_wg_lds(const BtArgs& a) {
 	return L.total;
 }
 
-// The dynamic LDS a workgroup of k_sw_bt_wg may take: 64 KiB, or (BT2G_BT_WG_LDS=1)
-// what the device lets a block opt in to (up to the CU's 160 KiB), set once on
-// the kernel -- wide planes (mate searches) then fit.
+// The dynamic LDS a workgroup of k_sw_bt_wg may take: what the device lets a
+// block opt in to (up to the CU's 160 KiB), set once on the kernel -- wide
+// planes (mate searches, ~90 KB) then fit; 64 KiB with $BT2G_BT_WG_LDS=0.
 uint32_t sw_bt_wg_lds_limit() {
 	static const uint32_t lim = [] {
 		const char* e = getenv("BT2G_BT_WG_LDS");
-		if(!(e && *e == '1')) return 65536u;
+		if(e && *e == '0') return 65536u;
 		int dev = 0, v = 0;
 		if(hipGetDevice(&dev) != hipSuccess ||
 		   hipDeviceGetAttribute(&v, hipDeviceAttributeSharedMemPerBlockOptin, dev) != hipSuccess || v <= 65536)

@@ -1,5 +1,4 @@
-# round-4 GPU step: paired with the decision plane + workgroup walk for mate searches (SAM vs stock), and without
+# round-4 GPU step: GPU test suite + smoke with the wide decision plane defaults, then bench.py
 set -o pipefail
-export K=32 WARM=8 MODE=paired READS=200000
-BT2G_DEC_RATIO=6 BT2G_BT_WG_LDS=1 bash scripts/gpu_r04.sh batch r04ad_wide "16" || exit 1
-SKIP=--skip-stock bash scripts/gpu_r04.sh batch r04ad "16"
+bash scripts/gpu_r04.sh tests r04ae || exit 1
+bash scripts/gpu_r04.sh bench r04ae
