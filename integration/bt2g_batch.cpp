@@ -326,10 +326,11 @@ struct EnvInit {
 		pin_cpus();
 		setenv("BT2G_SYNC", "poll", 0);
 		const char* hq = getenv("BT2G_HW_QUEUES");
-		// (32: a hardware queue per stream -- six DP workers and two per other kind,
-		// each with its own context and stream, plus the 1-mm search's second stream;
-		// r04r: 190 k reads/s with 16, 214 k with 32)
-		long q = hq ? atol(hq) : 32;
+		// (16 for ~20 streams -- six DP workers and two per other kind, each with its
+		// own context and stream: r04r measured 190 k reads/s with 16 and 214 k with
+		// 32 on different runs, but r04ae with 32 ran every service kernel slower,
+		// the 1-mm work queue 6x, and the server at 123 k against r04ab's 205 k)
+		long q = hq ? atol(hq) : 16;
 		if(q < 1) q = 1;
 		if(q > 32) q = 32;                      // the runtime refuses more
 		char b[16];

@@ -40,9 +40,10 @@ def dropin_env(index_base, stats_path=None, device=0):
     """Environment of the drop-in server (integration/): the index its engines
     open and where the binding writes its call counts.  (The servers set their
     HIP hardware queues themselves before their first HIP call -- the GPU box
-    exports 4; BT2G_HW_QUEUES overrides, default here 32: the batch server's
-    services run ~20 streams -- and the server is started with it too.)"""
-    hq = os.environ.get("BT2G_HW_QUEUES", "32")
+    exports 4; BT2G_HW_QUEUES overrides, default 16: with 32 every kernel of
+    the batch server's services ran slower, the 1-mm work queue 6x (r04ae) --
+    and the server is started with it too.)"""
+    hq = os.environ.get("BT2G_HW_QUEUES", "16")
     env = {"BT2G_INDEX": index_base, "BT2G_DEVICE": str(device), "BT2G_HW_QUEUES": hq, "GPU_MAX_HW_QUEUES": hq}
     if stats_path:
         env["BT2G_ADAPTER_STATS"] = stats_path

@@ -1,4 +1,4 @@
-# round-4 GPU step: GPU test suite + smoke with the wide decision plane defaults, then bench.py
+# round-4 GPU step: bench.py with 16 hardware queues again, then paired through the batch server
 set -o pipefail
-bash scripts/gpu_r04.sh tests r04ae || exit 1
-bash scripts/gpu_r04.sh bench r04ae
+bash scripts/gpu_r04.sh bench r04af || exit 1
+K=32 WARM=8 MODE=paired READS=200000 SKIP=--skip-stock bash scripts/gpu_r04.sh batch r04af_paired "16"
