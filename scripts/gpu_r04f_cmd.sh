@@ -1,4 +1,4 @@
-# round-4 GPU step: bench.py with 16 hardware queues again, then paired through the batch server
+# round-4 GPU step: kernel-trace profile of the final bench command, then local through the batch server vs stock
 set -o pipefail
-bash scripts/gpu_r04.sh bench r04af || exit 1
-K=32 WARM=8 MODE=paired READS=200000 SKIP=--skip-stock bash scripts/gpu_r04.sh batch r04af_paired "16"
+BENCH_ARGS="--no-cpu-baseline" bash scripts/gpu_r04.sh benchprof r04ag || exit 1
+K=32 WARM=8 SARGS=--local READS=200000 bash scripts/gpu_r04.sh batch r04ag_local "16"
