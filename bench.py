@@ -648,19 +648,24 @@ def schedule_run(args, rank, world, local, base, reads_np, quals_np, workdir, bi
             dist.barrier()
         if gpu:
             torch.cuda.synchronize()
+        rss = [srv.last_rss_gb]                 # after the warmup, then after every timed pass
         t0 = time.perf_counter()
         aligned, outs, cpu_s = 0, None, 0.0
-        for _ in range(args.steps):
+        for i in range(args.steps):
             _, outs = srv.run(chunks, k=args.clients)
             cpu_s += srv.last_cpu_s
+            rss.append(srv.last_rss_gb)
             aligned += count_aligned(outs, paired)
+            if i + 1 < args.steps:
+                outs = None                     # (only the last pass's SAM is kept)
+            log(f"[rank {rank}] pass {i + 1}/{args.steps}: server RSS {rss[-1]:.1f} GB")
         if gpu:
             torch.cuda.synchronize()
         if multi:
             dist.barrier()
         elapsed = time.perf_counter() - t0
         threads_cpu = srv.last_threads
-        rss = srv.last_rss_gb
+        smaps = srv.smaps_top()
     st = None
     for _ in range(50):                         # written by the server at SIGTERM
         if os.path.exists(stats):
@@ -671,7 +676,19 @@ def schedule_run(args, rank, world, local, base, reads_np, quals_np, workdir, bi
                 pass
         time.sleep(0.1)
     return {"elapsed": elapsed, "aligned": aligned, "outs": outs, "chunks": chunks, "stats": st,
-            "server_cpu_s": cpu_s, "server_threads_cpu": threads_cpu, "server_rss_gb": rss}
+            "server_cpu_s": cpu_s, "server_threads_cpu": threads_cpu, "server_rss_gb": rss[-1],
+            "server_rss_gb_per_pass": rss, "binary": binary_id(binary), "smaps_top": smaps}
+
+
+def binary_id(path):
+    """Which server binary ran: its path, size and sha256 (the box runs the
+    prebuilt file the snapshot carried)."""
+    import hashlib
+    h = hashlib.sha256()
+    with open(path, "rb") as f:
+        for b in iter(lambda: f.read(1 << 20), b""):
+            h.update(b)
+    return {"path": os.path.relpath(path, ROOT), "bytes": os.path.getsize(path), "sha256": h.hexdigest()}
 
 
 def stock_baseline(args, base, chunks, batch_outs, workdir):
@@ -1162,8 +1179,11 @@ def main():
             "roofline": rl,
             "reads_per_s": total_reads / elapsed,
             "server_kernels": kern,
-            "server": {k: st.get(k) for k in ("reads", "rounds", "slots", "steps", "idle_ms")} |
-                      {"server_cpu_s": sched["server_cpu_s"], "server_rss_gb": sched["server_rss_gb"],
+            "server": {k: st.get(k) for k in ("reads", "rounds", "slots", "slots_live", "slots_rebuilt",
+                                              "slot_kib_hist", "steps", "idle_ms")} |
+                      {"binary": sched["binary"], "server_cpu_s": sched["server_cpu_s"],
+                       "server_rss_gb": sched["server_rss_gb"], "server_rss_gb_per_pass": sched["server_rss_gb_per_pass"],
+                       "smaps_top": sched["smaps_top"],
                        "cpu_us_per_read": sched["server_cpu_s"] / max(1, args.reads * args.steps) * 1e6,
                        "calls": {k: st.get(k) for k in ("exact_sweep", "one_mm", "seed_search", "extend",
                                                         "get_offset", "ungapped", "sw_dp")},

@@ -35,6 +35,7 @@
 #include <string.h>
 #include <sched.h>
 #include <sys/mman.h>
+#include <malloc.h>
 
 #include <atomic>
 #include <new>
@@ -174,7 +175,10 @@ struct Range {
 		void* m = mmap(nullptr, cap, PROT_READ | PROT_WRITE, MAP_PRIVATE | MAP_ANONYMOUS | MAP_NORESERVE, -1, 0);
 		if(m == MAP_FAILED) return;
 		base = (char*)m;
-		if(huge) (void)madvise(base, cap, MADV_HUGEPAGE);
+		// (the big blocks' range asks for small pages outright: with transparent huge
+		// pages "always" a slot's 20 MB pool, of which a read touches a few 16 KB
+		// pages, would be backed 2 MB at a time)
+		(void)madvise(base, cap, huge ? MADV_HUGEPAGE : MADV_NOHUGEPAGE);
 	}
 	char* take(size_t bytes) {
 		if(!base) return nullptr;
@@ -207,6 +211,10 @@ char* slab_take(size_t bytes) {
 }
 
 thread_local size_t t_fresh = 0;        // bytes of the slab the last allocation took ($BT2G_ALLOC_SITES=fresh)
+// bytes this thread allocated minus bytes it freed (block sizes incl. headers):
+// the batch driver charges a read slot with the difference across its steps, and
+// rebuilds slots whose reference objects grew big (bt2g_alloc_thread_net)
+thread_local long long t_net = 0;
 
 void* fresh(int c) {
 	if(stats_on()) g_fresh[c].fetch_add(1, std::memory_order_relaxed);
@@ -251,9 +259,11 @@ void* alloc(size_t n) {
 		void* p = malloc(HDR + n);
 		if(!p) return nullptr;
 		((Hdr*)p)->magic = MAGIC_MALLOC;
+		t_net += (long long)(HDR + n);
 		return (char*)p + HDR;
 	}
 	const int c = cls_of(n);
+	t_net += (long long)(HDR + size_of(c));
 	if(!t_dead) {
 		Cache& tc = t_cache;
 		if(!tc.head[c]) {
@@ -288,11 +298,13 @@ void release(void* p) {
 	if(xtrace_on()) xcheck(p);
 	Hdr* h = (Hdr*)((char*)p - HDR);
 	if(h->magic == MAGIC_MALLOC) {
+		t_net -= (long long)malloc_usable_size(h);
 		free(h);
 		return;
 	}
 	if(h->magic != MAGIC_CACHED || h->cls >= (uint32_t)NCLASS) abort();   // not ours: a heap corruption
 	const int c = (int)h->cls;
+	t_net -= (long long)(HDR + size_of(c));
 	Node* b = (Node*)p;
 	if(t_dead) {
 		Depot& d = depot();
@@ -405,6 +417,9 @@ inline void site_count(void* ra, size_t n) {
 }  // namespace
 
 extern "C" void bt2g_alloc_site_scope(int on) { t_site_scope += on ? 1 : -1; }
+
+// Bytes the calling thread allocated minus those it freed (0 with $BT2G_ALLOC=0).
+extern "C" long long bt2g_alloc_thread_net() { return enabled() ? t_net : 0; }
 
 extern "C" void bt2g_alloc_stats_dump() {
 	const char* path = getenv("BT2G_ALLOC_STATS");

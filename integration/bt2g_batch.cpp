@@ -63,6 +63,7 @@
 #include <signal.h>
 #include <execinfo.h>
 #include <unistd.h>
+#include <sys/mman.h>
 
 #include <algorithm>
 #include <array>
@@ -205,6 +206,9 @@ std::atomic<uint64_t> g_dp_again{0};                   // DPs run again (candida
 std::atomic<uint64_t> g_steps{0}, g_steps_hist[16];
 // reads in flight summed over rounds; drivers' time with no read in flight
 std::atomic<uint64_t> g_inflight{0}, g_idle_us{0}, g_slots{0};
+// slot footprints at release (bin b: [2^b, 2^(b+1)) KiB) and slots rebuilt for size
+std::atomic<uint64_t> g_slot_mem_hist[16], g_slots_rebuilt{0}, g_slots_live{0};
+std::atomic<uint64_t> g_pool_trims{0}, g_pool_trim_pages{0};   // pool_trim calls and pages handed back
 char g_stats_path[4096];
 
 int svc_stats(char* buf, size_t cap);   // the services' kernel times and work (below)
@@ -233,6 +237,13 @@ void write_stats() {
 	n += snprintf(buf + n, sizeof(buf) - n, "]");
 	n += snprintf(buf + n, sizeof(buf) - n, ", \"inflight_sum\": %llu, \"idle_ms\": %.1f, \"slots\": %llu",
 	              (unsigned long long)g_inflight.load(), g_idle_us.load() / 1000.0, (unsigned long long)g_slots.load());
+	n += snprintf(buf + n, sizeof(buf) - n, ", \"pool_trims\": [%llu, %llu]", (unsigned long long)g_pool_trims.load(),
+	              (unsigned long long)g_pool_trim_pages.load());
+	n += snprintf(buf + n, sizeof(buf) - n, ", \"slots_live\": %llu, \"slots_rebuilt\": %llu, \"slot_kib_hist\": [",
+	              (unsigned long long)g_slots_live.load(), (unsigned long long)g_slots_rebuilt.load());
+	for(int b = 0; b < 16; b++)
+		n += snprintf(buf + n, sizeof(buf) - n, "%s%llu", b ? ", " : "", (unsigned long long)g_slot_mem_hist[b].load());
+	n += snprintf(buf + n, sizeof(buf) - n, "]");
 	n += snprintf(buf + n, sizeof(buf) - n, ", \"steps\": %llu, \"steps_hist\": [", (unsigned long long)g_steps.load());
 	for(int b = 0; b < 16; b++)
 		n += snprintf(buf + n, sizeof(buf) - n, "%s%llu", b ? ", " : "", (unsigned long long)g_steps_hist[b].load());
@@ -247,6 +258,7 @@ void write_stats() {
 }
 
 extern "C" void bt2g_alloc_stats_dump();
+extern "C" long long bt2g_alloc_thread_net();    // bt2g_alloc.cpp: this thread's allocated - freed bytes
 extern "C" void bt2g_alloc_site_scope(int on);   // bt2g_alloc.cpp ($BT2G_ALLOC_SITES)   // bt2g_alloc.cpp ($BT2G_ALLOC_STATS)
 
 // $BT2G_EXIT_CLEAN=1: SIGTERM ends the process through exit() (atexit handlers
@@ -500,6 +512,45 @@ struct Replay {
 struct Driver;
 struct Slot;
 
+// ---- a slot's 20 MB cache pools ---------------------------------------------------
+// Each slot owns the two ds.h Pools a worker thread owns (AlignmentCache's for the
+// current read's seed hits, aligner_cache.h:474, and SwDriver's for end-to-end hit
+// offsets, aligner_sw_driver.h:308).  Their pages are committed as a read first
+// writes them -- AlignmentCache::addOnTheFlyImpl writes an OFF_MASK entry for every
+// element of a seed's SA range (aligner_cache.cpp:85-91), up to the whole 20 MB for
+// a read in a high-copy repeat -- and a pool keeps them: a worker thread of the
+// stock server holds two such pools, but ~14 k slots would each keep the
+// high-water mark of every read they served (r05a: +10 GB of host memory per pass
+// of 1 M reads, 79 GB in these pools after 7).  So when a read has used more than
+// POOL_KEEP pages of a pool, the pages past that are handed back to the kernel
+// (MADV_DONTNEED: zero pages on the next touch; a pool's pages are always
+// written before they are read).  The cost is a page fault per 16 KB the next heavy
+// read writes, against the ~4 k entries it writes there.
+// Pool's own fields (ds.h:3145-3149) are private: read through the rule that an
+// explicit instantiation may name any member.
+template<typename Tag, typename Tag::type M> struct PoolPeek {
+	friend typename Tag::type peek(Tag) { return M; }
+};
+struct PoolSuper { typedef uint8_t* Pool::*type; friend type peek(PoolSuper); };
+struct PoolCur { typedef size_t Pool::*type; friend type peek(PoolCur); };
+template struct PoolPeek<PoolSuper, &Pool::super_pages>;
+template struct PoolPeek<PoolCur, &Pool::cur_>;
+
+const size_t POOL_KEEP = 64;                   // pages (16 KB each, CACHE_PAGE_SZ) a pool keeps
+
+// After a read: the pages the pool handed out beyond POOL_KEEP go back.
+void pool_trim(Pool& p) {
+	const size_t used = p.*peek(PoolCur());
+	if(used <= POOL_KEEP) return;
+	uint8_t* base = p.*peek(PoolSuper());
+	const uintptr_t lo = ((uintptr_t)base + POOL_KEEP * CACHE_PAGE_SZ + 4095) & ~(uintptr_t)4095;
+	const uintptr_t hi = ((uintptr_t)base + used * CACHE_PAGE_SZ) & ~(uintptr_t)4095;
+	if(hi <= lo) return;
+	(void)madvise((void*)lo, hi - lo, MADV_DONTNEED);
+	g_pool_trims++;
+	g_pool_trim_pages += used - POOL_KEEP;
+}
+
 // ---- SwDriver::extendSeeds / extendSeedsPaired as resumable state machines ----
 // (aligner_sw_driver.cpp:756-1297 and 1385-2402).  Members of the reference's
 // SwDriver (satpos_, gws_, rands_, eehits_, seenDiags*_, red*_, res*_,
@@ -512,6 +563,7 @@ enum { X_START = 0, X_AFTER_EE_ROWS, X_AFTER_EXT, X_AFTER_PRIO_ROWS, X_AFTER_UG,
 
 struct SwDriverB : public SwDriver {
 	explicit SwDriverB(size_t bytes) : SwDriver(bytes) {}
+	Pool& ee_pool() { return pool_; }
 
 	// extendSeeds / extendSeedsPaired arguments (bt2_search.cpp:3505-3593 and twins)
 	int mate = 0;                  // the anchor mate (0: mate 1)
@@ -731,6 +783,13 @@ struct Slot {
 	bt2g_ug_problem ug_p{};
 	bt2g_ug_result ug_r{};
 	std::vector<bt2g_edit> ug_ed;
+	// bytes this slot's objects grew by since it was built (allocations minus frees
+	// on the driver thread while it was stepped; the construction's ~150 KB and
+	// two 20 MB pools, ds.h Pool, mostly untouched, not counted): past $BT2G_SLOT_MAX_KB the slot is
+	// rebuilt when its read finishes, so a slot does not keep the high-water
+	// mark of every read it ever served (ELists keep their capacity)
+	long long mem = 0;
+	size_t idx = 0;                  // position in Driver::all
 	// the read's DP table (asked and speculative DPs)
 	std::vector<std::unique_ptr<DpRes>> dps;
 	size_t ndps = 0;
@@ -886,6 +945,7 @@ struct Driver {
 	std::condition_variable in_cv, room_cv;
 	std::vector<Elem*> inbox, got;   // (swapped each round: no allocation once grown)
 	size_t max_slots = 2048;         // reads in flight per driver ($BT2G_BATCH_SLOTS)
+	long long slot_max = 1 << 20;     // a slot's bytes past which it is rebuilt ($BT2G_SLOT_MAX_KB)
 	std::atomic<size_t> active_a{0}; // `active` for the feeder
 	// requests of this round: the stepping lane's lists
 	std::vector<Rq>* rq = lanes[0].rq;
@@ -3341,13 +3401,17 @@ void Driver::admit(Elem* e) {
 			all.emplace_back(new Slot(*rp, *mapq, (size_t)tid));
 			bt2g_alloc_site_scope(0);
 			g_slots++;
+			g_slots_live++;
 			s = all.back().get();
+			s->idx = all.size() - 1;
 		} else {
 			s = freel.back();
 			freel.pop_back();
 		}
+		const long long m1 = bt2g_alloc_thread_net();
 		s->rdbuf[0] = ra;
 		s->rdbuf[1] = ps->read_b();
+		s->mem += bt2g_alloc_thread_net() - m1;
 		s->paired = !ps->read_b().empty();
 		s->rdid = ra.rdid;
 		s->msink = &ps->msink();
@@ -3377,7 +3441,6 @@ void Driver::admit(Elem* e) {
 	} else {
 		conn_done(conn, 0);                   // (returned now if none of its reads is in flight)
 	}
-	active_a.store(active);
 }
 
 void Driver::release(Slot* s) {
@@ -3388,10 +3451,32 @@ void Driver::release(Slot* s) {
 		g_steps_hist[b]++;
 	}
 	active--;
-	freel.push_back(s);
-	if(((++g_reads) & 0xffff) == 0) write_stats();
-	conn_done(s->conn, 1);
+	{
+		const long long kib = s->mem >> 10;
+		int b = 0;
+		while(b < 15 && (2ll << b) <= kib) b++;
+		g_slot_mem_hist[b]++;
+	}
+	const void* conn = s->conn;
 	s->conn = nullptr;
+	pool_trim(s->scCurrent.pool());
+	pool_trim(s->sd.ee_pool());
+	if(s->mem > slot_max) {
+		// rebuilt: its memory goes back to this thread's allocator cache, where the
+		// next slot (or the next heavy read) takes it
+		const size_t i = s->idx;
+		if(i + 1 != all.size()) {
+			all[i].swap(all.back());
+			all[i]->idx = i;
+		}
+		all.pop_back();
+		g_slots_rebuilt++;
+		g_slots_live--;
+	} else {
+		freel.push_back(s);
+	}
+	if(((++g_reads) & 0xffff) == 0) write_stats();
+	conn_done(conn, 1);
 }
 
 void Driver::run_loop() {
@@ -3453,6 +3538,9 @@ void Driver::run_loop() {
 	pepol.reset(new PairedEndPolicy(pepolFlag, gMaxInsert, gMinInsert, R_localAlign, gFlippedMatesOK, gDovetailMatesOK,
 	                                gContainMatesOK, gOlapMatesOK, gExpandToFrag));
 	max_slots = env_or("BT2G_BATCH_SLOTS", 2048);
+	// (r05a: at 1 MB, 18 % of the reads had their slot rebuilt -- a slot's objects
+	// grow to ~0.5-2 MB on hg38-like reads -- and the drivers' CPU per read doubled)
+	slot_max = (long long)env_or("BT2G_SLOT_MAX_KB", 16384) << 10;
 	// (r04aa, one box: 16 -> 200 k reads/s, 8 -> 228 k, 4 -> 219 k: past 8 the
 	// speculative DPs cost the drivers and the DP service more than the rounds
 	// they save)
@@ -3487,8 +3575,13 @@ void Driver::run_loop() {
 				g_idle_us += now_us() - ti;
 			}
 			got.swap(inbox);
+			// (the feeder counts the taken buffers' reads as in flight until they are
+			// admitted: it had seen an empty inbox and a stale count meanwhile, and
+			// the slots overshot max_slots -- r04af: 45 727 slots for 16 x 2 048)
+			active_a.store(active + 16 * got.size());
 		}
 		for(Elem* e : got) admit(e);
+		active_a.store(active);
 		if(!got.empty()) room_cv.notify_one();
 		const uint64_t t0 = now_us();
 		g_inflight += L.run.size();
@@ -3496,7 +3589,9 @@ void Driver::run_loop() {
 		for(size_t k = 0; k < L.run.size(); k++) {
 			Slot* s = L.run[k];
 			s->nsteps++;
+			const long long m0 = bt2g_alloc_thread_net();
 			step_read(*s);
+			s->mem += bt2g_alloc_thread_net() - m0;
 			if(s->pc == P_FINISH) release(s);
 			else L.next.push_back(s);
 		}

@@ -211,6 +211,27 @@ class Server:
             e[2] = max(e[2], cs)
         return out
 
+    def smaps_top(self, k=6):
+        """The server's largest mappings by resident size (MB, with the part in
+        transparent huge pages): where its memory is."""
+        rows, cur = [], None
+        try:
+            for ln in open(f"/proc/{self.proc.pid}/smaps"):
+                f = ln.split()
+                if not f:
+                    continue
+                if "-" in f[0] and not f[0].endswith(":"):
+                    cur = {"range": f[0], "name": f[5] if len(f) > 5 else "", "rss_mb": 0.0, "thp_mb": 0.0}
+                    rows.append(cur)
+                elif f[0] == "Rss:" and cur is not None:
+                    cur["rss_mb"] = int(f[1]) / 1024
+                elif f[0] == "AnonHugePages:" and cur is not None:
+                    cur["thp_mb"] = int(f[1]) / 1024
+        except (OSError, ValueError):
+            return []
+        rows.sort(key=lambda r: -r["rss_mb"])
+        return rows[:k]
+
     def rss_gb(self):
         """Resident memory of the server (GB)."""
         try:

@@ -1,0 +1,30 @@
+#!/bin/bash
+# Round-5 GPU steps, one gpurun call each:
+#   bash scripts/gpu_r05.sh mem TAG [STEPS]   bench.py's batch server over STEPS passes: RSS per pass, THP mode
+#   bash scripts/gpu_r05.sh bench TAG         the driver's round-end command, as it runs it
+#   bash scripts/gpu_r05.sh tests TAG         the GPU test suite and smoke()
+set -o pipefail
+cd /tmp && export TMPDIR=/tmp
+cd "$GRAFT_REPO_ROOT" || exit 1
+O=gpurun_out/${2:-r05}
+mkdir -p $O
+( while sleep 50; do date +%T >> $O/heartbeat; done ) &
+HB=$!
+trap "kill $HB 2>/dev/null" EXIT
+case "$1" in
+mem)
+  cat /sys/kernel/mm/transparent_hugepage/enabled /sys/kernel/mm/transparent_hugepage/defrag > $O/thp.txt 2>&1
+  free -g >> $O/thp.txt 2>&1; cat $O/thp.txt
+  timeout -k 10 800 python3 -u bench.py --steps ${3:-6} --warmup 1 --chain-steps 0 --stock-sample 0 $BENCH_ARGS \
+    > $O/bench.json 2> $O/bench.log || { tail -30 $O/bench.log; exit 1; }
+  grep "RSS\|real schedule" $O/bench.log
+  python3 -c "import json; d=json.load(open('$O/bench.json')); print(d['value'], json.dumps(d['server'])[:3000])" ;;
+bench)
+  /usr/bin/time -v timeout -k 10 1100 python3 -u bench.py --gpus 1 --steps 20 --warmup 5 > $O/bench.json 2> $O/bench.log || { tail -30 $O/bench.log; exit 1; }
+  tail -25 $O/bench.log | grep -v "^\s*$"; cut -c1-1500 $O/bench.json ;;
+tests)
+  timeout -k 10 1000 python -u -m pytest tests -m gpu -x -v --timeout 600 --timeout-method thread > $O/gpu_tests.log 2>&1 || { tail -20 $O/gpu_tests.log; exit 1; }
+  tail -2 $O/gpu_tests.log
+  timeout -k 10 300 python -u -c "import __graft_entry__ as g; g.smoke()" > $O/smoke.log 2>&1 || { tail $O/smoke.log; exit 1; }
+  echo smoke ok ;;
+esac
