@@ -154,7 +154,8 @@ void launch_sw_bt(int kind, const BtArgs& a, hipStream_t st);
 // sw_backtrace_wg.hip: one end-to-end kind-2 DP per workgroup, candidates walked
 // in parallel; LDS bytes it needs for this launch's geometry
 uint32_t sw_bt_wg_lds(const BtArgs& a);
-uint32_t sw_bt_wg_lds_limit();
+void sw_bt_wg_lds_init(int dev);          // once per device, from bt2g_open
+uint32_t sw_bt_wg_lds_limit(int dev);
 void launch_sw_bt_wg(const BtArgs& a, uint32_t lds, hipStream_t st);
 
 // backtrace mark scratch per problem of <= rows x cols (sw_backtrace.hip):

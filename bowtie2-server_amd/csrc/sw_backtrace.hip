@@ -881,8 +881,9 @@ static uint32_t bt_lds_bytes(const BtArgs& a) {
 	return n > 0xffffffffull ? 0xffffffffu : (uint32_t)n;
 }
 
-// batches up to $BT2G_BT_LDS_MAX problems (default 8192; 0: never) walk
-// LDS-resident when a problem's plane and marks fit in 64 KB
+// batches up to $BT2G_BT_LDS_MAX problems (default 65536; 0: never) walk
+// LDS-resident (the workgroup walk, else the one-walker kernel when a problem's
+// plane and marks fit in 64 KB)
 // (read at every launch: the parity tests run one batch both ways)
 static uint32_t bt_lds_max() {
 	const char* e = getenv("BT2G_BT_LDS_MAX");
@@ -899,7 +900,9 @@ void launch_sw_bt(int kind, const BtArgs& a, hipStream_t st) {
 		const char* e = getenv("BT2G_BT_WG");
 		if(!(e && *e == '0')) {
 			const uint32_t lw = sw_bt_wg_lds(a);
-			if(lw <= sw_bt_wg_lds_limit()) {
+			int dev = 0;
+			(void)hipGetDevice(&dev);              // (the caller's context device)
+			if(lw <= sw_bt_wg_lds_limit(dev)) {
 				launch_sw_bt_wg(a, lw, st);
 				return;
 			}

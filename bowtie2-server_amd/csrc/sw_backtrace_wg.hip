@@ -26,6 +26,8 @@
 // The end-to-end rules the kernel relies on: every cell of the bottom
 // gap-barrier rows is left unmarked (sw_backtrace.hip: such walks stay on
 // their diagonals); a cell in a gap-barrier row moves diagonally only.
+#include <atomic>
+#include <mutex>
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 #include <stdlib.h>
@@ -397,24 +399,38 @@ uint32_t sw_bt_wg_lds(const BtArgs& a) {
 	return L.total;
 }
 
-// The dynamic LDS a workgroup of k_sw_bt_wg may take: what the device lets a
-// block opt in to (up to the CU's 160 KiB), set once on the kernel -- wide
-// planes (mate searches, ~90 KB) then fit; 64 KiB with $BT2G_BT_WG_LDS=0.
-uint32_t sw_bt_wg_lds_limit() {
-	static const uint32_t lim = [] {
-		const char* e = getenv("BT2G_BT_WG_LDS");
-		if(e && *e == '0') return 65536u;
-		int dev = 0, v = 0;
-		if(hipGetDevice(&dev) != hipSuccess ||
-		   hipDeviceGetAttribute(&v, hipDeviceAttributeSharedMemPerBlockOptin, dev) != hipSuccess || v <= 65536)
-			return 65536u;
-		if(hipFuncSetAttribute((const void*)k_sw_bt_wg, hipFuncAttributeMaxDynamicSharedMemorySize, v) != hipSuccess) {
+// The dynamic LDS a workgroup of k_sw_bt_wg may take on a device: what the
+// device lets a block opt in to (up to the CU's 160 KiB; the kernel declares no
+// static LDS, so dynamic is all of it) -- wide planes (mate searches, ~90 KB)
+// then fit; 64 KiB with $BT2G_BT_WG_LDS=0 or before sw_bt_wg_lds_init.
+// HIP keeps function attributes per device, so the opt-in is made for every
+// device a context is opened on, from bt2g_open, before that context has a
+// stream or any worker thread launches on it (it had been made lazily, once per
+// process, on whichever device was current at the first walk).
+static std::atomic<uint32_t> g_wg_lds_lim[64];
+static std::mutex g_wg_lds_mu;
+
+void sw_bt_wg_lds_init(int dev) {
+	if(dev < 0 || dev >= 64) return;
+	std::lock_guard<std::mutex> lk(g_wg_lds_mu);
+	if(g_wg_lds_lim[dev].load()) return;
+	uint32_t lim = 65536u;
+	const char* e = getenv("BT2G_BT_WG_LDS");
+	int v = 0;
+	if(!(e && *e == '0') &&
+	   hipDeviceGetAttribute(&v, hipDeviceAttributeSharedMemPerBlockOptin, dev) == hipSuccess && v > 65536) {
+		// (the caller made `dev` current: bt2g_open_mem)
+		if(hipFuncSetAttribute((const void*)k_sw_bt_wg, hipFuncAttributeMaxDynamicSharedMemorySize, v) == hipSuccess)
+			lim = (uint32_t)v;
+		else
 			(void)hipGetLastError();
-			return 65536u;
-		}
-		return (uint32_t)v;
-	}();
-	return lim;
+	}
+	g_wg_lds_lim[dev].store(lim);
+}
+
+uint32_t sw_bt_wg_lds_limit(int dev) {
+	const uint32_t v = dev >= 0 && dev < 64 ? g_wg_lds_lim[dev].load() : 0u;
+	return v ? v : 65536u;
 }
 
 void launch_sw_bt_wg(const BtArgs& a, uint32_t lds, hipStream_t st) {

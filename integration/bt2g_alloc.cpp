@@ -292,10 +292,15 @@ void* alloc(size_t n) {
 
 bool xtrace_on();
 void xcheck(void* p);
+bool live_on();
+}  // namespace
+void live_untag(void* p);
+namespace {
 
 void release(void* p) {
 	if(!p) return;
 	if(xtrace_on()) xcheck(p);
+	if(live_on()) live_untag(p);
 	Hdr* h = (Hdr*)((char*)p - HDR);
 	if(h->magic == MAGIC_MALLOC) {
 		t_net -= (long long)malloc_usable_size(h);
@@ -416,6 +421,47 @@ inline void site_count(void* ra, size_t n) {
 }
 }  // namespace
 
+// $BT2G_ALLOC_LIVE=1 (diagnostics): bytes live by allocation site -- a block
+// remembers its call site in the header's spare word and gives its bytes back to
+// that site when freed; dumped with the stats ("live <module> <offset> <bytes>").
+namespace {
+bool live_on() {
+	static const bool on = getenv("BT2G_ALLOC_LIVE") != nullptr;
+	return on;
+}
+std::atomic<uint64_t> g_lpc[XSLOT];
+std::atomic<long long> g_lbytes[XSLOT];
+inline size_t live_slot(uint64_t pc) {
+	size_t k = (size_t)((pc * 0x9E3779B97F4A7C15ull) >> 50) & (XSLOT - 1);
+	for(int probe = 0; probe < 256; probe++, k = (k + 1) & (XSLOT - 1)) {
+		uint64_t cur = g_lpc[k].load(std::memory_order_relaxed);
+		if(cur == pc) return k;
+		if(cur == 0) {
+			uint64_t z = 0;
+			if(g_lpc[k].compare_exchange_strong(z, pc) || z == pc) return k;
+		}
+	}
+	return XSLOT;
+}
+inline void live_tag(void* p, void* ra) {
+	if(!p) return;
+	Hdr* h = (Hdr*)((char*)p - HDR);
+	const size_t k = live_slot((uint64_t)(uintptr_t)ra);
+	h->pad = k;
+	if(k < XSLOT) {
+		const long long n = h->magic == MAGIC_MALLOC ? (long long)malloc_usable_size(h) : (long long)(HDR + size_of((int)h->cls));
+		g_lbytes[k].fetch_add(n, std::memory_order_relaxed);
+	}
+}
+}  // namespace
+void live_untag(void* p) {
+	Hdr* h = (Hdr*)((char*)p - HDR);
+	const size_t k = (size_t)h->pad;
+	if(k >= XSLOT) return;
+	const long long n = h->magic == MAGIC_MALLOC ? (long long)malloc_usable_size(h) : (long long)(HDR + size_of((int)h->cls));
+	g_lbytes[k].fetch_sub(n, std::memory_order_relaxed);
+}
+
 extern "C" void bt2g_alloc_site_scope(int on) { t_site_scope += on ? 1 : -1; }
 
 // Bytes the calling thread allocated minus those it freed (0 with $BT2G_ALLOC=0).
@@ -441,6 +487,15 @@ extern "C" void bt2g_alloc_stats_dump() {
 				fprintf(f, "xfree %s %lx %llu\n", di.dli_fname, (unsigned long)(pc - (uint64_t)(uintptr_t)di.dli_fbase),
 				        (unsigned long long)g_xcnt[k].load());
 		}
+	if(live_on())
+		for(size_t k = 0; k < XSLOT; k++) {
+			const uint64_t pc = g_lpc[k].load();
+			if(!pc) continue;
+			Dl_info di;
+			if(dladdr((void*)(uintptr_t)pc, &di) && di.dli_fname)
+				fprintf(f, "live %s %lx %lld\n", di.dli_fname, (unsigned long)(pc - (uint64_t)(uintptr_t)di.dli_fbase),
+				        (long long)g_lbytes[k].load());
+		}
 	if(sites_on())
 		for(size_t k = 0; k < XSLOT; k++) {
 			const uint64_t pc = g_spc[k].load();
@@ -457,6 +512,7 @@ void* operator new(size_t n) {
 	void* p = alloc(n);
 	if(!p) throw std::bad_alloc();
 	if(xtrace_on()) xtag(p, __builtin_return_address(0));
+	if(live_on()) live_tag(p, __builtin_return_address(0));
 	if(sites_on()) {
 		if(sites_fresh()) {
 			if(t_fresh) site_count(__builtin_return_address(0), t_fresh);
@@ -471,6 +527,7 @@ void* operator new[](size_t n) {
 	void* p = alloc(n);
 	if(!p) throw std::bad_alloc();
 	if(xtrace_on()) xtag(p, __builtin_return_address(0));
+	if(live_on()) live_tag(p, __builtin_return_address(0));
 	if(sites_on()) {
 		if(sites_fresh()) {
 			if(t_fresh) site_count(__builtin_return_address(0), t_fresh);
@@ -481,8 +538,16 @@ void* operator new[](size_t n) {
 	}
 	return p;
 }
-void* operator new(size_t n, const std::nothrow_t&) noexcept { return alloc(n); }
-void* operator new[](size_t n, const std::nothrow_t&) noexcept { return alloc(n); }
+void* operator new(size_t n, const std::nothrow_t&) noexcept {
+	void* p = alloc(n);
+	if(live_on()) live_tag(p, __builtin_return_address(0));
+	return p;
+}
+void* operator new[](size_t n, const std::nothrow_t&) noexcept {
+	void* p = alloc(n);
+	if(live_on()) live_tag(p, __builtin_return_address(0));
+	return p;
+}
 void operator delete(void* p) noexcept { release(p); }
 void operator delete[](void* p) noexcept { release(p); }
 void operator delete(void* p, size_t) noexcept { release(p); }

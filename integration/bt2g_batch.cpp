@@ -536,7 +536,7 @@ struct PoolCur { typedef size_t Pool::*type; friend type peek(PoolCur); };
 template struct PoolPeek<PoolSuper, &Pool::super_pages>;
 template struct PoolPeek<PoolCur, &Pool::cur_>;
 
-const size_t POOL_KEEP = 64;                   // pages (16 KB each, CACHE_PAGE_SZ) a pool keeps
+const size_t POOL_KEEP = 16;                   // pages (16 KB each, CACHE_PAGE_SZ) a pool keeps
 
 // After a read: the pages the pool handed out beyond POOL_KEEP go back.
 void pool_trim(Pool& p) {
@@ -944,7 +944,7 @@ struct Driver {
 	std::mutex in_mu;
 	std::condition_variable in_cv, room_cv;
 	std::vector<Elem*> inbox, got;   // (swapped each round: no allocation once grown)
-	size_t max_slots = 2048;         // reads in flight per driver ($BT2G_BATCH_SLOTS)
+	size_t max_slots = 1024;         // reads in flight per driver ($BT2G_BATCH_SLOTS)
 	long long slot_max = 1 << 20;     // a slot's bytes past which it is rebuilt ($BT2G_SLOT_MAX_KB)
 	std::atomic<size_t> active_a{0}; // `active` for the feeder
 	// requests of this round: the stepping lane's lists
@@ -1436,15 +1436,20 @@ void Svc::call_dp(std::vector<std::pair<Slot*, DpRes*>>& v) {
 	// rest: the engine picks the walk for a whole call by its widest DP, and one
 	// wide DP would send a call's seed extensions to the H-plane walk (r04v
 	// paired: 14.5 ms DP calls) instead of the decision plane + workgroup walk
-	std::vector<std::pair<Slot*, DpRes*>> sh, wide, lg;
+	// DPs wider than the engine's decision-plane ratio ($BT2G_DEC_RATIO, default 6,
+	// the same variable and default as bt2g_api.cpp dec_ratio) go in calls of their
+	// own too: one of them would send a whole call of mate searches to the H plane
+	std::vector<std::pair<Slot*, DpRes*>> sh, wide, wider, lg;
+	static const size_t ratio = env_or("BT2G_DEC_RATIO", 6);
 	for(auto& q : v) {
-		const size_t len = q.first->rdlens[q.second->mate];
-		(len > 1024 ? lg : (size_t)q.second->ncol > 2 * len ? wide : sh).push_back(q);
+		const size_t len = q.first->rdlens[q.second->mate], nc = q.second->ncol;
+		(len > 1024 ? lg : nc > ratio * len ? wider : nc > 2 * len ? wide : sh).push_back(q);
 	}
 	const uint32_t cap = R_localAlign ? 2048 : 512;
 	static const uint32_t me = (uint32_t)env_or("BT2G_DP_MAXEDIT", 48);
 	if(!sh.empty()) run_dp(sh, cap, 8, me);
 	if(!wide.empty()) run_dp(wide, cap, 8, me);
+	if(!wider.empty()) run_dp(wider, cap, 8, me);
 	if(!lg.empty()) run_dp(lg, cap, 8, me);
 }
 
@@ -3537,10 +3542,13 @@ void Driver::run_loop() {
 	else pepolFlag = PE_POLICY_RR;
 	pepol.reset(new PairedEndPolicy(pepolFlag, gMaxInsert, gMinInsert, R_localAlign, gFlippedMatesOK, gDovetailMatesOK,
 	                                gContainMatesOK, gOlapMatesOK, gExpandToFrag));
-	max_slots = env_or("BT2G_BATCH_SLOTS", 2048);
+	// (r05c, hg38-like genome, 16 drivers: 2 048 slots per driver 203 k reads/s at
+	// 98 GB of host memory after 7 passes, 1 024 192 k at 57 GB after 4, 640 171 k
+	// at 43 GB: a slot holds ~1-2 MB of the reference's per-read objects)
+	max_slots = env_or("BT2G_BATCH_SLOTS", 1024);
 	// (r05a: at 1 MB, 18 % of the reads had their slot rebuilt -- a slot's objects
 	// grow to ~0.5-2 MB on hg38-like reads -- and the drivers' CPU per read doubled)
-	slot_max = (long long)env_or("BT2G_SLOT_MAX_KB", 16384) << 10;
+	slot_max = (long long)env_or("BT2G_SLOT_MAX_KB", 4096) << 10;
 	// (r04aa, one box: 16 -> 200 k reads/s, 8 -> 228 k, 4 -> 219 k: past 8 the
 	// speculative DPs cost the drivers and the DP service more than the rounds
 	// they save)

@@ -19,8 +19,15 @@ mem)
     > $O/bench.json 2> $O/bench.log || { tail -30 $O/bench.log; exit 1; }
   grep "RSS\|real schedule" $O/bench.log
   python3 -c "import json; d=json.load(open('$O/bench.json')); print(d['value'], json.dumps(d['server'])[:3000])" ;;
+slots)
+  # the batch server at several slot caps (reads in flight per driver): rate, RSS, CPU per read
+  for S in ${SLOTS:-1024 768}; do
+    BT2G_BATCH_SLOTS=$S timeout -k 10 500 python3 -u bench.py --steps ${3:-3} --warmup 1 --chain-steps 0 --stock-sample 0 $BENCH_ARGS \
+      > $O/bench_s$S.json 2> $O/bench_s$S.log || { tail -30 $O/bench_s$S.log; exit 1; }
+    python3 -c "import json; d=json.load(open('$O/bench_s$S.json')); s=d['server']; print($S, round(d['value']), s['slots'], s['server_rss_gb_per_pass'], round(s['cpu_us_per_read'],1))"
+  done ;;
 bench)
-  /usr/bin/time -v timeout -k 10 1100 python3 -u bench.py --gpus 1 --steps 20 --warmup 5 > $O/bench.json 2> $O/bench.log || { tail -30 $O/bench.log; exit 1; }
+  T0=$(date +%s); timeout -k 10 1100 python3 -u bench.py --gpus 1 --steps 20 --warmup 5 > $O/bench.json 2> $O/bench.log || { tail -30 $O/bench.log; exit 1; }; echo "wall $(( $(date +%s) - T0 )) s"
   tail -25 $O/bench.log | grep -v "^\s*$"; cut -c1-1500 $O/bench.json ;;
 tests)
   timeout -k 10 1000 python -u -m pytest tests -m gpu -x -v --timeout 600 --timeout-method thread > $O/gpu_tests.log 2>&1 || { tail -20 $O/gpu_tests.log; exit 1; }
