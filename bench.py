@@ -58,7 +58,8 @@ VALU_PEAK_TOPS = 78.6
 # E = max(E - ext, H - open), F likewise, with the gap-barrier vetoes
 SW_OPS_PER_CELL = 10
 # the kernel whose PMC counters make roofline.traffic (per bench kernel id)
-PMC_KERNEL = {0: "k_exact_sweep", 1: "k_seed_search", 2: "k_one_mm", 3: "k_get_offset", 4: "k_sw_sys"}
+PMC_KERNEL = {0: "k_exact_sweep", 1: "k_seed_search", 2: "k_one_mm", 3: "k_get_offset", 4: "k_sw_sys",
+              12: "k_seed_extend"}
 VALU_PACKED_TOPS = 37.0
 SEEDLEN, INTERVAL = 22, 15     # --sensitive, 150 bp: -L 22, -i S,1,1.15 -> 1+1.15*sqrt(150) = 15
 
@@ -531,19 +532,24 @@ def server_traffic(path, kernel):
         return None, None
     return tot / n, (f"{os.path.relpath(path, ROOT)}: FETCH_SIZE x 2 + WRITE_SIZE per dispatch of {kernel}* "
                      f"({n} dispatches of separate --pmc passes of bench.py with rocprofv3 in front of the server)")
-# the engine services' kernel ids (bt2g_api.cpp ProfScope) by call kind, and the
-# kernels' names in the line
+# the engine services' kernel ids (bt2g_api.cpp ProfScope) by call kind, the
+# kernels' names in the line, and their bound (None: no roofline, e.g. the DP
+# call's whole stream span); the algorithmic work of each comes from the server
+# per kernel id (FM kernels: bytes; the fill: DP cells)
 SERVER_KERNELS = [("exact_sweep", 0, "k_exact_sweep", "hbm"),
-                  ("exact_sweep", 2, "k_one_mm in the sweep's call (bt2g_exact_sweep_1mm)", None),
+                  ("exact_sweep", 2, "k_one_mm (items/q/near/far/branch/compact) in the sweep's call "
+                                     "(bt2g_exact_sweep_1mm)", "hbm"),
                   ("exact_sweep", 3, "k_range_offsets (the sweep's small ranges' rows)", None),
                   ("seed_search", 1, "k_seed_search", "hbm"),
-                  ("seed_search", 3, "k_seed_extend + k_seed_offsets (bt2g_seed_search_ext)", None),
+                  ("seed_search", 12, "k_seed_extend (SwDriver::extend of every seed range, bt2g_seed_search_ext)",
+                   "hbm"),
+                  ("seed_search", 3, "k_seed_offsets (the seed ranges' small rows)", None),
                   ("one_mm", 2, "k_one_mm (items/q/near/far/branch/compact)", "hbm"),
-                  ("get_offset", 3, "k_get_offset", "hbm"), ("extend", 3, "k_extend", None),
+                  ("get_offset", 3, "k_get_offset", "hbm"), ("extend", 12, "k_extend", "hbm"),
                   ("ungapped", 6, "k_ungapped", None), ("sw_dp", 4, "k_sw_sys (fill, with the candidate gather)", "valu"),
                   ("sw_dp", 11, "k_sort_small / k_sort_big (candidate sort)", None),
                   ("sw_dp", 5, "k_sw_bt_wg / k_sw_bt (nextAlignment loop)", None),
-                  ("sw_dp", 7, "the DP call's whole stream span (copies, fill, walk, pack)", None)]
+                  ("sw_dp", 7, "the DP call's whole stream span (copies, fill, walk, pack)", "span")]
 
 
 def policy_args(mode, preset):
@@ -577,31 +583,44 @@ def count_aligned(sam_texts, paired):
 
 def server_kernels(st):
     """Kernel times and algorithmic work of a batch-server run (its BT2G_KPROF
-    stats: per engine service, the HIP-event time of every launch and the work
-    of its calls).  FM kernels: bytes = 64 B per occurrence-table side gathered
-    + the read bytes walked (SURVEY.md 8(d), the figures of the chain below);
-    the SW fill: SW_OPS_PER_CELL integer ops per DP cell."""
+    stats: per engine service and kernel id, the HIP-event time of every launch
+    and the algorithmic work of the requests it carried).  FM kernels: bytes =
+    64 B per occurrence-table side gathered + the read bytes walked (SURVEY.md
+    8(d), the figures of the chain below); the SW fill: SW_OPS_PER_CELL integer
+    ops per DP cell."""
     out = {}
     ks = (st or {}).get("kernels") or {}
     for kind, kid, name, bound in SERVER_KERNELS:
         k = ks.get(kind)
         if not k:
             continue
-        launches, ms = k["ids"][kid]
+        row = k["ids"][kid]
+        launches, ms = row[0], row[1]
+        work, items = (row[2], row[3]) if len(row) > 3 else (0, 0)
         if not launches:
             continue
         e = {"kernel": name, "launches": launches, "ms_total": ms, "ms_per_launch": ms / launches,
-             "items": k["items"]}
-        if bound == "hbm" and k["work"]:
-            e.update(bound="hbm", bytes_total=k["work"], achieved=k["work"] / (ms / 1e3) / 1e9, unit="GB/s",
-                     peak=HBM_PEAK_GBS)
-        elif bound == "valu" and k["work"]:
-            e.update(bound="valu", cells_total=k["work"], achieved=k["work"] * SW_OPS_PER_CELL / (ms / 1e3) / 1e12,
-                     unit="T int-ops/s", peak=VALU_PEAK_TOPS, ops_per_cell=SW_OPS_PER_CELL)
+             "items": items}
+        if bound == "span":
+            e["span"] = True
+        if bound == "hbm" and work:
+            e.update(bound="hbm", bytes_total=work, bytes_per_launch=work / launches,
+                     achieved=work / (ms / 1e3) / 1e9, unit="GB/s", peak=HBM_PEAK_GBS)
+        elif bound == "valu" and work:
+            e.update(bound="valu", cells_total=work, cells_per_launch=work / launches,
+                     achieved=work * SW_OPS_PER_CELL / (ms / 1e3) / 1e12, unit="T int-ops/s", peak=VALU_PEAK_TOPS,
+                     ops_per_cell=SW_OPS_PER_CELL)
         if "achieved" in e:
             e["frac"] = e["achieved"] / e["peak"]
         out[f"{kind}:{kid}"] = e
     return out
+
+
+def dominant_kernel(kern):
+    """The kernel with the largest total time over the run (the DP call's stream
+    span is not a kernel)."""
+    ks = [k for k in kern if not kern[k].get("span")]
+    return max(ks, key=lambda k: kern[k]["ms_total"], default=None)
 
 
 def schedule_run(args, rank, world, local, base, reads_np, quals_np, workdir, binary=None):
@@ -1134,7 +1153,7 @@ def main():
     log(f"[rank {rank}] real schedule: {sched['aligned']} aligned of {args.reads * args.steps} in "
         f"{sched['elapsed']:.2f}s; whole job {value:.0f} aligned/s")
     kern = server_kernels(sched["stats"])
-    dom_k = max((k for k in kern if "achieved" in kern[k]), key=lambda k: kern[k]["ms_total"], default=None)
+    dom_k = dominant_kernel(kern)
     cpu, sam = None, None
     if rank == 0 and world == 1 and args.stock_sample and not args.no_cpu_baseline:
         try:
@@ -1152,12 +1171,14 @@ def main():
         unit = "read pairs/s" if args.mode == "paired" else "reads/s"
         st = sched["stats"] or {}
         rl = None
-        if dom_k:
+        if dom_k and "achieved" in kern[dom_k]:
             d = kern[dom_k]
             traffic, tnote = server_traffic(args.server_pmc, PMC_KERNEL.get(int(dom_k.split(":")[1]), "?"))
             rl = {"bound": d["bound"], "kernel": d["kernel"], "achieved": d["achieved"], "peak": d["peak"],
                   "unit": d["unit"], "frac": d["frac"], "traffic": traffic, "traffic_source": tnote,
-                  "ms_per_launch": d["ms_per_launch"], "launches": d["launches"],
+                  "ms_per_launch": d["ms_per_launch"], "launches": d["launches"], "ms_total": d["ms_total"],
+                  "share_of_kernel_time": d["ms_total"] / sum(v["ms_total"] for v in kern.values()
+                                                              if not v.get("span")),
                   "per_launch_work": (d.get("bytes_total") or d.get("cells_total")) / d["launches"],
                   "work_unit": "bytes" if d["bound"] == "hbm" else "DP cells",
                   "note": "kernel times: HIP events around every launch of the batch server's engine services "
@@ -1180,7 +1201,9 @@ def main():
             "reads_per_s": total_reads / elapsed,
             "server_kernels": kern,
             "server": {k: st.get(k) for k in ("reads", "rounds", "slots", "slots_live", "slots_rebuilt",
-                                              "slot_kib_hist", "steps", "idle_ms")} |
+                                              "slot_kib_hist", "pool_trims", "steps", "idle_ms", "phases_ms",
+                                              "ext_speculative", "ext_prefetched")
+                       if k in st} |
                       {"binary": sched["binary"], "server_cpu_s": sched["server_cpu_s"],
                        "server_rss_gb": sched["server_rss_gb"], "server_rss_gb_per_pass": sched["server_rss_gb_per_pass"],
                        "smaps_top": sched["smaps_top"],

@@ -114,7 +114,7 @@ def lib():
         L.bt2g_one_mm_gated_dev.argtypes = [vp, vp, vp, u32, vp, u32, vp, C.POINTER(Scoring), vp, u32, vp, vp, vp,
                                             vp, vp]
         L.bt2g_exact_sweep_1mm.argtypes = [vp, vp, vp, u32, vp, u32, u32, C.c_int, C.c_int, C.c_int, vp,
-                                           C.POINTER(Scoring), u32, vp, vp, vp, vp, u32, vp]
+                                           C.POINTER(Scoring), u32, vp, vp, vp, vp, vp, u32, vp]
         L.bt2g_reserve_sw.argtypes = [vp, u32, u32]
         L.bt2g_bench_collect_rows_dev.argtypes = [u32, vp, vp, vp, vp, u32, vp, vp, u32, u32, u32, vp, vp, vp, vp, vp,
                                                   u32, vp]
@@ -307,14 +307,16 @@ class Engine:
         ops = np.zeros(n, np.uint32)
         sc = scoring(local)
         offs = np.zeros((n, 2 + cap, off_cap), np.uint32) if off_cap else None
+        self.last_mm_loads = np.zeros(n, np.uint32)
         _chk(lib().bt2g_exact_sweep_1mm(self.h, _ptr(reads), _ptr(quals), reads.shape[1], _ptr(lens), n, 2, int(nofw),
                                         int(norc), int(skip_exact), _ptr(ms), C.byref(sc), cap, _ptr(sweep),
-                                        _ptr(hits), _ptr(cnt), _ptr(ops), off_cap, _ptr(offs) if off_cap else None))
+                                        _ptr(hits), _ptr(cnt), _ptr(ops), _ptr(self.last_mm_loads), off_cap,
+                                        _ptr(offs) if off_cap else None))
         return (sweep, hits, cnt, ops, offs) if off_cap else (sweep, hits, cnt, ops)
 
     def extend(self, reads, lens, ranges):
         """SwDriver::extend per seed-hit range; ranges n x 8 = (read, fw, off, len,
-        topf, botf, topb, botb).  Returns n x 4 (nlex, nrex, LF steps, 0)."""
+        topf, botf, topb, botb).  Returns n x 4 (nlex, nrex, LF steps, 64-B sides gathered)."""
         reads, lens = _c(reads, np.uint8), _c(lens, np.uint32)
         rg = _c(ranges, np.uint32)
         out = np.zeros((len(rg), 4), np.uint32)

@@ -811,7 +811,7 @@ int bt2g_extend_dev(bt2g_ctx* c, const uint8_t* reads, uint32_t stride, const ui
 	if(n == 0) return BT2G_OK;
 	hipStream_t st = pick(c, stream);
 	{
-		ProfScope ps(c, 3, st);
+		ProfScope ps(c, 12, st);
 		launch_extend(c->fw, c->bw, c->bw.sides != nullptr, reads, stride, lens, in, n, out, st);
 	}
 	HIPCHK(hipGetLastError());
@@ -1380,12 +1380,16 @@ int bt2g_seed_search_ext(bt2g_ctx* c, const uint8_t* reads, uint32_t stride, con
 	if((rc = bt2g_seed_search_dev(c, dr, stride, dl, n, seedlen, interval, offset, maxseeds, dout, dns, dops, dld,
 	                              c->stream)))
 		return rc;
-	if(n && (dext || doffs)) {
+	// (kernel-stats ids: 12 the seed ranges' extension, 3 their rows' offsets)
+	if(n && dext) {
+		ProfScope ps(c, 12, c->stream);
+		launch_seed_extend(c->fw, c->bw, c->bw.sides != nullptr, dr, stride, dl, n, seedlen, interval, offset, maxseeds,
+		                   dout, dext, c->stream);
+		HIPCHK(hipGetLastError());
+	}
+	if(n && doffs) {
 		ProfScope ps(c, 3, c->stream);
-		if(dext)
-			launch_seed_extend(c->fw, c->bw, c->bw.sides != nullptr, dr, stride, dl, n, seedlen, interval, offset,
-			                   maxseeds, dout, dext, c->stream);
-		if(doffs) launch_seed_offsets(c->fw, dout, nr, off_cap, doffs, c->stream);
+		launch_seed_offsets(c->fw, dout, nr, off_cap, doffs, c->stream);
 		HIPCHK(hipGetLastError());
 	}
 	return t.finish();
@@ -1421,7 +1425,8 @@ int bt2g_one_mm(bt2g_ctx* c, const uint8_t* reads, const uint8_t* quals, uint32_
 int bt2g_exact_sweep_1mm(bt2g_ctx* c, const uint8_t* reads, const uint8_t* quals, uint32_t stride,
                          const uint32_t* lens, uint32_t n, uint32_t mine_max, int nofw, int norc, int skip_exact,
                          const int32_t* minsc, const bt2g_scoring* sc, uint32_t cap, uint32_t* sweep,
-                         bt2g_mm1* hits, int32_t* counts, uint32_t* bwops, uint32_t off_cap, uint32_t* offs) {
+                         bt2g_mm1* hits, int32_t* counts, uint32_t* bwops, uint32_t* mm_loads, uint32_t off_cap,
+                         uint32_t* offs) {
 	if(!c || !sc) return fail(BT2G_ERR_ARG, "null argument");
 	if(offs && (!c->fw.offs || off_cap == 0)) return fail(BT2G_ERR_ARG, "offsets need the SA sample and off_cap > 0");
 	HIPCHK(hipSetDevice(c->device));
@@ -1436,14 +1441,15 @@ int bt2g_exact_sweep_1mm(bt2g_ctx* c, const uint8_t* reads, const uint8_t* quals
 	   (rc = t.up(&dl, lens, n)) || (rc = t.up(&dms, minsc, n)) || (rc = t.out(&dsw, sweep, (size_t)n * 8)) ||
 	   (rc = t.out(&dh, hits, (size_t)n * cap)) || (rc = t.out(&dcnt, counts, n)) || (rc = t.out(&dops, bwops, n)))
 		return rc;
-	uint32_t* doffs = nullptr;
+	uint32_t *doffs = nullptr, *dld = nullptr;
 	if(offs && (rc = t.out(&doffs, offs, (size_t)n * (2u + cap) * off_cap))) return rc;
+	if(mm_loads && (rc = t.out(&dld, mm_loads, n))) return rc;
 	if((rc = t.send())) return rc;
 	if((rc = bt2g_exact_sweep_dev(c, dr, stride, dl, n, mine_max, nofw, norc, dsw, c->stream))) return rc;
 	// the gate reads the sweep on the device: no round trip between the two searches
 	// (the items kernel reads the gate rule from bit 1 of nofw: MM_GATE_KEEP_EXACT)
 	if((rc = one_mm_impl(c, dr, dq, stride, dl, n, dms, sc, (nofw ? 1 : 0) | (skip_exact ? 0 : MM_GATE_KEEP_EXACT),
-	                     norc ? 1 : 0, dsw, cap, dh, dcnt, dops, nullptr, c->stream, false)))
+	                     norc ? 1 : 0, dsw, cap, dh, dcnt, dops, dld, c->stream, false)))
 		return rc;
 	if(doffs) {
 		{

@@ -155,7 +155,7 @@ void launch_sw_bt(int kind, const BtArgs& a, hipStream_t st);
 // in parallel; LDS bytes it needs for this launch's geometry
 uint32_t sw_bt_wg_lds(const BtArgs& a);
 void sw_bt_wg_lds_init(int dev);          // once per device, from bt2g_open
-uint32_t sw_bt_wg_lds_limit(int dev);
+uint32_t sw_bt_wg_lds_limit();             // on the current device
 void launch_sw_bt_wg(const BtArgs& a, uint32_t lds, hipStream_t st);
 
 // backtrace mark scratch per problem of <= rows x cols (sw_backtrace.hip):

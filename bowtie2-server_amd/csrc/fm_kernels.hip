@@ -394,7 +394,7 @@ void launch_range_offsets(const DevEbwt& e, const uint32_t* sweep, const bt2g_mm
 // --------------------------------------------------------------------------
 __device__ __forceinline__ uint32_t ext_walk(const DevEbwt& e, uint32_t top, uint32_t bot, const uint8_t* row,
                                              uint32_t rdlen, bool fw, uint32_t lim, uint32_t i0, int dir,
-                                             uint32_t& fmops) {
+                                             uint32_t& fmops, uint32_t& loads) {
 	uint32_t n = 0;
 	for(uint32_t ii = 0; ii < lim; ii++) {
 		const uint32_t i = (uint32_t)((int64_t)i0 + (int64_t)dir * ii);
@@ -403,7 +403,7 @@ __device__ __forceinline__ uint32_t ext_walk(const DevEbwt& e, uint32_t top, uin
 		fmops++;
 		if(bot - top > 1) {
 			uint32_t t[4], b[4];
-			bi_step_tb(e, top, bot, t, b);
+			loads += (uint32_t)bi_step_tb(e, top, bot, t, b);
 			int nonz = -1;
 			bool abort = false;
 			const uint32_t orig = bot - top;
@@ -420,6 +420,7 @@ __device__ __forceinline__ uint32_t ext_walk(const DevEbwt& e, uint32_t top, uin
 			int c = -1;
 			if(top != e.zoff) {
 				SideData s;
+				loads++;
 				load_side(e, top / 192u, s);
 				c = side_rowL(s, top % 192u);
 				top = occ1(e, s, top, c);
@@ -435,14 +436,16 @@ __device__ __forceinline__ uint32_t ext_walk(const DevEbwt& e, uint32_t top, uin
 __device__ __forceinline__ bt2g_ext_out ext_one(const DevEbwt& F, const DevEbwt& B, int has_bw, const uint8_t* row,
                                                 uint32_t rdlen, const bt2g_ext_in& q) {
 	const bool fw = q.fw != 0;
-	uint32_t fmops = 0, nlex = 0, nrex = 0;
+	uint32_t fmops = 0, nlex = 0, nrex = 0, loads = 0;
 	// left, forward index (aligner_sw_driver.cpp:335-408)
 	uint32_t lim = fw ? q.off : rdlen - q.len - q.off;
-	if(lim > 0) nlex = ext_walk(F, q.topf, q.botf, row, rdlen, fw, lim, fw ? q.off - 1 : rdlen - q.off - q.len - 1, -1, fmops);
+	if(lim > 0)
+		nlex = ext_walk(F, q.topf, q.botf, row, rdlen, fw, lim, fw ? q.off - 1 : rdlen - q.off - q.len - 1, -1, fmops, loads);
 	// right, mirror index (aligner_sw_driver.cpp:411-475)
 	lim = fw ? rdlen - q.len - q.off : q.off;
-	if(lim > 0 && has_bw) nrex = ext_walk(B, q.topb, q.botb, row, rdlen, fw, lim, fw ? q.len + q.off : rdlen - q.off, 1, fmops);
-	return bt2g_ext_out{nlex, nrex, fmops, 0u};
+	if(lim > 0 && has_bw)
+		nrex = ext_walk(B, q.topb, q.botb, row, rdlen, fw, lim, fw ? q.len + q.off : rdlen - q.off, 1, fmops, loads);
+	return bt2g_ext_out{nlex, nrex, fmops, loads};
 }
 
 __global__ void __launch_bounds__(256)

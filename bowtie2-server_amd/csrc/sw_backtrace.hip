@@ -900,9 +900,7 @@ void launch_sw_bt(int kind, const BtArgs& a, hipStream_t st) {
 		const char* e = getenv("BT2G_BT_WG");
 		if(!(e && *e == '0')) {
 			const uint32_t lw = sw_bt_wg_lds(a);
-			int dev = 0;
-			(void)hipGetDevice(&dev);              // (the caller's context device)
-			if(lw <= sw_bt_wg_lds_limit(dev)) {
+			if(lw <= sw_bt_wg_lds_limit()) {
 				launch_sw_bt_wg(a, lw, st);
 				return;
 			}

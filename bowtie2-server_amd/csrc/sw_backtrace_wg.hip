@@ -428,7 +428,10 @@ void sw_bt_wg_lds_init(int dev) {
 	g_wg_lds_lim[dev].store(lim);
 }
 
-uint32_t sw_bt_wg_lds_limit(int dev) {
+// (on the calling thread's current device: the caller's context device)
+uint32_t sw_bt_wg_lds_limit() {
+	int dev = 0;
+	if(hipGetDevice(&dev) != hipSuccess) return 65536u;
 	const uint32_t v = dev >= 0 && dev < 64 ? g_wg_lds_lim[dev].load() : 0u;
 	return v ? v : 65536u;
 }

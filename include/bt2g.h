@@ -184,11 +184,14 @@ int bt2g_one_mm_gated_dev(bt2g_ctx* ctx, const uint8_t* reads, const uint8_t* qu
  * the exact ranges (slots 0, 1: fw, rc, when their mine is 0) and of the
  * stored 1-mm hits' ranges (slots 2..), for ranges of at most off_cap rows;
  * BT2G_OFF_MASK elsewhere -- the rows the extension of those hits resolves
- * first (GroupWalk2S, group_walk.h:862-1216), without a round trip. */
+ * first (GroupWalk2S, group_walk.h:862-1216), without a round trip.
+ * mm_loads (optional, n): 64-B sides the 1-mm search gathered per read (0 where
+ * it did not run; the sweep's own are sweep[i*8+7]). */
 int bt2g_exact_sweep_1mm(bt2g_ctx* ctx, const uint8_t* reads, const uint8_t* quals, uint32_t stride,
                          const uint32_t* lens, uint32_t n, uint32_t mine_max, int nofw, int norc, int skip_exact,
                          const int32_t* minsc, const bt2g_scoring* sc, uint32_t cap, uint32_t* sweep,
-                         bt2g_mm1* hits, int32_t* counts, uint32_t* bwops, uint32_t off_cap, uint32_t* offs);
+                         bt2g_mm1* hits, int32_t* counts, uint32_t* bwops, uint32_t* mm_loads, uint32_t off_cap,
+                         uint32_t* offs);
 
 /* Ebwt::getOffset (bt2_idx.cpp:150-171): joined-text offset of each SA row.
  * loads (optional): 64-B sides gathered per row. */
@@ -210,7 +213,7 @@ typedef struct {
 typedef struct {
 	uint32_t nlex, nrex; /* positions the hit extends to the left / right without an edit */
 	uint32_t fmops;      /* LF steps taken (PerReadMetrics::nSdFmops increments) */
-	uint32_t pad;
+	uint32_t loads;      /* 64-B occurrence-table sides gathered (roofline bytes; not a reference output) */
 } bt2g_ext_out;
 
 /* SwDriver::extend (aligner_sw_driver.cpp:299-483), called by
@@ -501,10 +504,10 @@ int bt2g_allreduce_counts(bt2g_ctx* ctx, uint64_t* counts, uint32_t k);
 /* ---- measurement --------------------------------------------------------- */
 /* Kernel timing with HIP events on the launch stream (off by default). */
 int bt2g_set_profiling(bt2g_ctx* ctx, int on);
-/* kernel ids: 0 exact_sweep, 1 seed_search, 2 one_mm, 3 get_offset / extend / range offsets, 4 sw_align,
+/* kernel ids: 0 exact_sweep, 1 seed_search, 2 one_mm, 3 get_offset / range offsets, 4 sw_align,
  * 5 sw_backtrace, 6 ungapped, 7 frame / the whole stream span of a bt2g_sw_align_bt_packed call;
  * host phases of a bt2g_sw_align_bt_packed call (wall time): 8 staging, 9 enqueueing, 10 waiting and
- * copying out; 11 the SW candidate sort (kernels, HIP events) */
+ * copying out; 11 the SW candidate sort (kernels, HIP events); 12 extend (k_extend, k_seed_extend) */
 int bt2g_kernel_stats(bt2g_ctx* ctx, int kernel, uint64_t* launches, double* total_ms);
 int bt2g_reset_stats(bt2g_ctx* ctx);
 

@@ -200,6 +200,7 @@ std::atomic<uint64_t> g_dp_spec{0}, g_dp_used{0}, g_dp_reuse{0}, g_dp_miss{0};
 std::atomic<uint64_t> g_mm_pf{0}, g_mm_pf_used{0};   // 1-mm searches prefetched with the sweep / taken
 std::atomic<uint64_t> g_rows_pf{0};                   // SA rows resolved with the sweep or the seeds
 std::atomic<uint64_t> g_ext_pf{0};
+std::atomic<uint64_t> g_ext_spec{0};                   // seed ranges extended in the seed call (bt2g_seed_search_ext)
 std::atomic<uint64_t> g_dp_pre_us{0}, g_dp_post_us{0};   // the DP service's host work around its calls
 std::atomic<uint64_t> g_dp_again{0};                   // DPs run again (candidates, alignments or edits over the room)                    // extend requests answered by the seed call
 // rounds per read: total and a histogram (bin b: [2^b, 2^(b+1)))
@@ -209,13 +210,49 @@ std::atomic<uint64_t> g_inflight{0}, g_idle_us{0}, g_slots{0};
 // slot footprints at release (bin b: [2^b, 2^(b+1)) KiB) and slots rebuilt for size
 std::atomic<uint64_t> g_slot_mem_hist[16], g_slots_rebuilt{0}, g_slots_live{0};
 std::atomic<uint64_t> g_pool_trims{0}, g_pool_trim_pages{0};   // pool_trim calls and pages handed back
+// $BT2G_PHASES=1 (diagnostics): the drivers' CPU by phase of the per-read logic,
+// inclusive TSC cycles and calls, summed into the stats once per round
+enum { PH_STEP, PH_SETUP, PH_ADMIT, PH_RELEASE, PH_INST, PH_AFTER_SEEDS, PH_RANK, PH_EESAT, PH_PRIO, PH_ROWS,
+       PH_NEXTELT, PH_NEEDDP, PH_DPFOUND, PH_REPLAY, PH_REDUND, PH_REPORT, PH_FINISH, PH_SUBMIT, PH_N };
+const char* const PH_NAMES[PH_N] = {"step", "setup_read", "admit", "release", "instantiate", "after_seeds",
+                                    "rankSeedHits", "eeSaTups", "prioritizeSATups", "rows_request", "next_element",
+                                    "need_dp", "dp_found", "replay_next", "redundant", "report", "finishRead",
+                                    "submit_wait"};
+bool phases_on() {
+	static const bool on = [] { const char* e = getenv("BT2G_PHASES"); return e && *e == '1'; }();
+	return on;
+}
+thread_local uint64_t t_ph[PH_N], t_phn[PH_N];
+std::atomic<uint64_t> g_ph[PH_N], g_phn[PH_N];
+std::atomic<uint64_t> g_tsc0{0}, g_us0{0};
+struct Ph {
+	int id;
+	uint64_t t0;
+	explicit Ph(int i) : id(i), t0(phases_on() ? __builtin_ia32_rdtsc() : 0) {}
+	~Ph() {
+		if(t0) {
+			t_ph[id] += __builtin_ia32_rdtsc() - t0;
+			t_phn[id]++;
+		}
+	}
+};
+void ph_flush() {
+	if(!phases_on()) return;
+	for(int k = 0; k < PH_N; k++) {
+		if(t_phn[k]) {
+			g_ph[k] += t_ph[k];
+			g_phn[k] += t_phn[k];
+			t_ph[k] = t_phn[k] = 0;
+		}
+	}
+}
 char g_stats_path[4096];
 
 int svc_stats(char* buf, size_t cap);   // the services' kernel times and work (below)
 
 void write_stats() {
 	if(!g_stats_path[0]) return;
-	char buf[8192];
+	char buf[16384];
 	int n = snprintf(buf, sizeof(buf), "{\"driver\": \"batch\", \"reads\": %llu, \"rounds\": %llu, \"round_ms\": %.1f, "
 	                 "\"cpu_ms\": %.1f, \"gpu_ms\": %.1f, \"dp\": [%llu, %llu, %llu, %llu]",
 	                 (unsigned long long)g_reads.load(), (unsigned long long)g_rounds.load(),
@@ -226,6 +263,7 @@ void write_stats() {
 		n += snprintf(buf + n, sizeof(buf) - n, ", \"%s\": [%llu, %llu, %llu, %.1f]", K_NAMES[k],
 		              (unsigned long long)g_req[k].load(), (unsigned long long)g_cpu[k].load(),
 		              (unsigned long long)g_calls[k].load(), g_call_us[k].load() / 1000.0);
+	n += snprintf(buf + n, sizeof(buf) - n, ", \"ext_speculative\": %llu", (unsigned long long)g_ext_spec.load());
 	n += snprintf(buf + n, sizeof(buf) - n, ", \"one_mm_prefetch\": [%llu, %llu], \"rows_prefetched\": %llu, \"ext_prefetched\": %llu"
 	              ", \"dp_host_ms\": [%.1f, %.1f], \"dp_again\": %llu",
 	              (unsigned long long)g_mm_pf.load(), (unsigned long long)g_mm_pf_used.load(),
@@ -237,6 +275,15 @@ void write_stats() {
 	n += snprintf(buf + n, sizeof(buf) - n, "]");
 	n += snprintf(buf + n, sizeof(buf) - n, ", \"inflight_sum\": %llu, \"idle_ms\": %.1f, \"slots\": %llu",
 	              (unsigned long long)g_inflight.load(), g_idle_us.load() / 1000.0, (unsigned long long)g_slots.load());
+	if(phases_on() && g_tsc0.load()) {
+		// TSC cycles -> ns from the TSC and the steady clock since the first round
+		const double ns_per_cyc = (now_us() - g_us0.load()) * 1e3 / (double)(__builtin_ia32_rdtsc() - g_tsc0.load());
+		n += snprintf(buf + n, sizeof(buf) - n, ", \"phases_ms\": {");
+		for(int k = 0; k < PH_N; k++)
+			n += snprintf(buf + n, sizeof(buf) - n, "%s\"%s\": [%.1f, %llu]", k ? ", " : "", PH_NAMES[k],
+			              g_ph[k].load() * ns_per_cyc / 1e6, (unsigned long long)g_phn[k].load());
+		n += snprintf(buf + n, sizeof(buf) - n, "}");
+	}
 	n += snprintf(buf + n, sizeof(buf) - n, ", \"pool_trims\": [%llu, %llu]", (unsigned long long)g_pool_trims.load(),
 	              (unsigned long long)g_pool_trim_pages.load());
 	n += snprintf(buf + n, sizeof(buf) - n, ", \"slots_live\": %llu, \"slots_rebuilt\": %llu, \"slot_kib_hist\": [",
@@ -875,6 +922,10 @@ struct Svc {
 	uint64_t k_launch[16] = {};     // bt2g_kernel_stats ids 0-15
 	double k_ms[16] = {};
 	std::atomic<uint64_t> work{0}, items{0};
+	// algorithmic work by kernel id (same figures, per kernel of a fused call: the
+	// sweep's call also runs the 1-mm search (id 2), the seed call the ranges'
+	// extension (id 12)); and the seed ranges extended ahead vs. taken
+	std::atomic<uint64_t> kwork[16] = {}, kitems[16] = {};
 	void loop();
 	void run(std::vector<Rq>& v, std::vector<std::pair<Slot*, DpRes*>>& dp);
 	// the calls
@@ -995,7 +1046,7 @@ void Svc::call_exact(std::vector<Rq>& v) {
 	thread_local Pack pk;
 	thread_local std::vector<uint32_t> out;
 	thread_local std::vector<int32_t> ms, cnt;
-	thread_local std::vector<uint32_t> ops, offs;
+	thread_local std::vector<uint32_t> ops, offs, mld;
 	thread_local std::vector<bt2g_mm1> h;
 	const uint32_t cap = 16, off_cap = 8;
 	for(int g = 0; g < 8; g++) {
@@ -1024,9 +1075,22 @@ void Svc::call_exact(std::vector<Rq>& v) {
 			const size_t per = (size_t)(2 + cap) * off_cap;
 			offs.resize(n * per);
 			for(size_t i = 0; i < n; i++) ms[i] = sub[i].s->mr[sub[i].m].pf_minsc;
+			mld.resize(n);
 			rc = bt2g_exact_sweep_1mm(ctx, pk.codes.data(), pk.quals.data(), pk.stride, pk.lens.data(), (uint32_t)n, 2,
 			                          nf ? 1 : 0, nr ? 1 : 0, 0, ms.data(), bsc, cap, out.data(), h.data(), cnt.data(),
-			                          ops.data(), off_cap, offs.data());
+			                          ops.data(), kprof_on() ? mld.data() : nullptr, off_cap, offs.data());
+			if(kprof_on() && !rc) {
+				// the 1-mm search's bytes: 64 B per side + the read and its qualities walked
+				// per strand (as call_1mm counts them); the reads it ran on
+				uint64_t w = 0, k = 0;
+				for(size_t i = 0; i < n; i++)
+					if(mld[i]) {
+						w += 64ull * mld[i] + 4ull * pk.lens[i];
+						k++;
+					}
+				kwork[2] += w;
+				kitems[2] += k;
+			}
 			for(size_t i = 0; i < n && !rc; i++) {
 				MateRes& x = sub[i].s->mr[sub[i].m];
 				// the resolved rows of the small ranges (slots: fw, rc exact ranges, 1-mm hits)
@@ -1073,6 +1137,8 @@ void Svc::call_exact(std::vector<Rq>& v) {
 		}
 		work += w;
 		items += sub.size();
+		kwork[0] += w;
+		kitems[0] += sub.size();
 	}
 	g_req[K_EXACT] += v.size();
 }
@@ -1115,6 +1181,8 @@ void Svc::call_1mm(std::vector<Rq>& v) {
 				for(size_t i = 0; i < n; i++) w += 64ull * ld[i] + 4ull * pk.lens[i];
 				work += w;
 				items += n;
+				kwork[2] += w;
+				kitems[2] += n;
 			}
 			g_call_us[K_1MM] += now_us() - t0;
 			g_calls[K_1MM]++;
@@ -1182,6 +1250,23 @@ void Svc::call_seeds(std::vector<Rq>& v) {
 			for(size_t i = 0; i < n; i++) w += 64ull * ld[i] + (uint64_t)std::max(ns[i], 0) * 2u * (x0.sd_L + 12u);
 			work += w;
 			items += n;
+			kwork[1] += w;
+			kitems[1] += n;
+		}
+		if(pf && !rc) {
+			// the ranges' extension (k_seed_extend): 64 B per side gathered + one read
+			// byte per LF step; every range with a hit, asked or not
+			uint64_t w = 0, k = 0;
+			for(size_t g = 0; g < n * 2 * maxs; g++)
+				if(ext[g].fmops) {
+					w += 64ull * ext[g].loads + ext[g].fmops;
+					k++;
+				}
+			g_ext_spec += k;
+			if(kprof_on()) {
+				kwork[12] += w;
+				kitems[12] += k;
+			}
 		}
 		g_call_us[K_SEEDS] += now_us() - t0;
 		g_calls[K_SEEDS]++;
@@ -1238,6 +1323,12 @@ void Svc::call_ext(std::vector<Rq>& v) {
 	g_call_us[K_EXT] += now_us() - t0;
 	g_calls[K_EXT]++;
 	if(rc) die("bt2g_extend", rc);
+	if(kprof_on()) {
+		uint64_t w = 0;
+		for(const bt2g_ext_out& o : out) w += 64ull * o.loads + o.fmops;
+		kwork[12] += w;
+		kitems[12] += out.size();
+	}
 	size_t k = 0;
 	for(const Rq& q : v) {
 		q.s->ext_out.assign(out.begin() + k, out.begin() + k + q.s->ext_in.size());
@@ -1260,6 +1351,8 @@ void Svc::call_off(std::vector<Rq>& v) {
 		for(uint32_t x : ld) w += 64ull * x + 12u;
 		work += w;
 		items += rows.size();
+		kwork[3] += w;
+		kitems[3] += rows.size();
 	}
 	g_call_us[K_OFF] += now_us() - t0;
 	g_calls[K_OFF]++;
@@ -1352,6 +1445,8 @@ void Svc::run_dp(const std::vector<std::pair<Slot*, DpRes*>>& v, uint32_t cap, u
 		for(size_t i = 0; i < n; i++) cells += (uint64_t)b.pk.lens[b.P[i].read] * b.P[i].ncol;
 		work += cells;
 		items += n;
+		kwork[4] += cells;
+		kitems[4] += n;
 	}
 	// edits stored per alignment: `me` (0: all an alignment can have, 2 x stride + 8);
 	// an alignment with more runs again with room for all (the engine reports
@@ -1716,10 +1811,16 @@ void Driver::resolve_rows_request(Slot& s) {
 	s.tab.gw.clear();                                                                                  \
 	s.tab.gw_on = true;                                                                                \
 	t_tab = &s.tab;                                                                                    \
-	eeMode = eeSaTups(rd, s.shs[mate], ebwtFw, ref, s.rnd, d.wlm, d.swmSeed, nelt, maxIters, all);     \
+	{                                                                                                  \
+		Ph ph_(PH_EESAT);                                                                              \
+		eeMode = eeSaTups(rd, s.shs[mate], ebwtFw, ref, s.rnd, d.wlm, d.swmSeed, nelt, maxIters, all); \
+	}                                                                                                  \
 	s.tab.gw_on = false;                                                                               \
 	t_tab = nullptr;                                                                                   \
-	d.resolve_rows_request(s);                                                                         \
+	{                                                                                                  \
+		Ph ph_(PH_ROWS);                                                                               \
+		d.resolve_rows_request(s);                                                                     \
+	}                                                                                                  \
 	if(!s.off_rows.empty()) {                                                                          \
 		pc = X_AFTER_EE_ROWS;                                                                          \
 		return EXTEND_BLOCKED;                                                                         \
@@ -1795,12 +1896,18 @@ static bool ext_from_seeds(Slot& s, size_t mate) {
 	s.tab.gw_on = true;                                                                                \
 	t_tab = &s.tab;                                                                                    \
 	t_cpu_ext = &g_cpu[K_EXT];                                                                         \
-	prioritizeSATups(rd, s.shs[mate], ebwtFw, d.ebwtBw, ref, seedmms, maxIters, R_doExtend, true, true, 5, \
-	                 s.ca, s.rnd, d.wlm, s.prm, nelt, all);                                            \
+	{                                                                                                  \
+		Ph ph_(PH_PRIO);                                                                               \
+		prioritizeSATups(rd, s.shs[mate], ebwtFw, d.ebwtBw, ref, seedmms, maxIters, R_doExtend, true, true, 5, \
+		                 s.ca, s.rnd, d.wlm, s.prm, nelt, all);                                        \
+	}                                                                                                  \
 	s.tab.ext_on = false;                                                                              \
 	s.tab.gw_on = false;                                                                               \
 	t_tab = nullptr;                                                                                   \
-	d.resolve_rows_request(s);                                                                         \
+	{                                                                                                  \
+		Ph ph_(PH_ROWS);                                                                               \
+		d.resolve_rows_request(s);                                                                     \
+	}                                                                                                  \
 	if(!s.off_rows.empty()) {                                                                          \
 		pc = X_AFTER_PRIO_ROWS;                                                                        \
 		return EXTEND_BLOCKED;                                                                         \
@@ -1811,6 +1918,7 @@ static bool ext_from_seeds(Slot& s, size_t mate) {
 // (aligner_sw_driver.cpp:924-952, 1626-1651).
 #define BT2GB_NEXT_ELEMENT()                                                                           \
 	{                                                                                                  \
+		Ph ph_(PH_NEXTELT);                                                                            \
 		WalkResult wr;                                                                                 \
 		const size_t elt = rands_[i].next(s.rnd);                                                      \
 		SARangeWithOffs<TSlice> sa;                                                                    \
@@ -2038,15 +2146,21 @@ int SwDriverB::ext_step(Driver& d, Slot& s) {
 						rect.initIval(refival);
 						seenDiags1_.add(refival);
 					}
-					if(!need_dp(d, s, mate, fw, tidx, tlen, rect, *minsc, true, true, false, a)) {
-						pc = X_AFTER_DP;
-						return EXTEND_BLOCKED;
+					{
+						Ph ph(PH_NEEDDP);
+						if(!need_dp(d, s, mate, fw, tidx, tlen, rect, *minsc, true, true, false, a)) {
+							pc = X_AFTER_DP;
+							return EXTEND_BLOCKED;
+						}
 					}
 				after_dp:
 					a.start(a.dp);
 					{
 						TAlScore bestCell = std::numeric_limits<TAlScore>::min();
-						found = dp_found(d, s, a, false, *minsc, bestCell);
+						{
+							Ph ph(PH_DPFOUND);
+							found = dp_found(d, s, a, false, *minsc, bestCell);
+						}
 						d.swmSeed.tallyGappedDp(readGaps, refGaps);
 						s.prm.nExDps++;
 						if(!found) {
@@ -2076,7 +2190,10 @@ int SwDriverB::ext_step(Driver& d, Slot& s) {
 					} else {
 						resGap_.reset();
 						if(replay_done(d, a, false)) break;
-						replay_next(d, s, a, false, *minsc, resGap_);
+						{
+							Ph ph(PH_REPLAY);
+							replay_next(d, s, a, false, *minsc, resGap_);
+						}
 						found = !resGap_.empty();
 						if(!found) break;
 						res = &resGap_;
@@ -2088,11 +2205,17 @@ int SwDriverB::ext_step(Driver& d, Slot& s) {
 						if(res->alres.refExtent() == 0) continue;
 					}
 					if(!refival.overlapsIgnoreOrient(res->alres.refival())) continue;
-					if(redAnchor_.overlap(res->alres)) continue;
-					redAnchor_.add(res->alres);
+					{
+						Ph ph(PH_REDUND);
+						if(redAnchor_.overlap(res->alres)) continue;
+						redAnchor_.add(res->alres);
+					}
 					res->alres.setParams(seedmms, seedlen, seedival, *minsc);
-					if(msink->report(0, anchor1 ? &res->alres : NULL, anchor1 ? NULL : &res->alres))
-						return EXTEND_POLICY_FULFILLED;
+					{
+						Ph ph(PH_REPORT);
+						if(msink->report(0, anchor1 ? &res->alres : NULL, anchor1 ? NULL : &res->alres))
+							return EXTEND_POLICY_FULFILLED;
+					}
 					tighten_unp(*this, msink);
 				}
 			}
@@ -2265,15 +2388,21 @@ int SwDriverB::ext_step_paired(Driver& d, Slot& s) {
 						rect.initIval(refival);
 						seenDiags().add(refival);
 					}
-					if(!need_dp(d, s, mate, fw, tidx, tlen, rect, *minsc, true, true, false, a)) {
-						pc = X_AFTER_DP;
-						return EXTEND_BLOCKED;
+					{
+						Ph ph(PH_NEEDDP);
+						if(!need_dp(d, s, mate, fw, tidx, tlen, rect, *minsc, true, true, false, a)) {
+							pc = X_AFTER_DP;
+							return EXTEND_BLOCKED;
+						}
 					}
 				after_dp:
 					a.start(a.dp);
 					{
 						TAlScore bestCell = std::numeric_limits<TAlScore>::min();
-						found = dp_found(d, s, a, false, *minsc, bestCell);
+						{
+							Ph ph(PH_DPFOUND);
+							found = dp_found(d, s, a, false, *minsc, bestCell);
+						}
 						d.swmSeed.tallyGappedDp(readGaps, refGaps);
 						s.prm.nExDps++;
 						s.prm.nDpFail++;        // failed until proven successful
@@ -2298,7 +2427,10 @@ int SwDriverB::ext_step_paired(Driver& d, Slot& s) {
 					} else {
 						resGap_.reset();
 						if(replay_done(d, a, false)) break;
-						replay_next(d, s, a, false, *minsc, resGap_);
+						{
+							Ph ph(PH_REPLAY);
+							replay_next(d, s, a, false, *minsc, resGap_);
+						}
 						found = !resGap_.empty();
 						if(!found) break;
 						res_kind = FOUND_NONE_;
@@ -2884,7 +3016,10 @@ void Driver::step_read(Slot& s) {
 	case P_EXT_SEEDS: mate = s.matemap[s.matei]; goto ext_seeds;
 	default: abort();
 	}
-	setup_read(s);
+	{
+		Ph ph(PH_SETUP);
+		setup_read(s);
+	}
 	// exact end-to-end alignments (bt2_search.cpp:3453-3631)
 	if(R_doExactUpFront) {
 		{
@@ -3115,7 +3250,11 @@ void Driver::step_read(Slot& s) {
 				al.searchAllSeeds(s.seeds[mate], ebwtFw, ebwtBw, rd, *sc, s.ca, s.shs[mate], sdm, s.prm);
 				g_cpu[K_SEEDS]++;
 			} else {
-				const int inst = instantiate(s, (int)mate, s.round_off[mate]);
+				int inst;
+				{
+					Ph ph(PH_INST);
+					inst = instantiate(s, (int)mate, s.round_off[mate]);
+				}
 				if(inst == 0) {
 					s.done[mate] = true;
 					break;
@@ -3127,7 +3266,10 @@ void Driver::step_read(Slot& s) {
 					fprintf(stderr, "bt2g batch: seed search of the round not asked\n");
 					abort();
 				}
-				after_seeds(s, (int)mate);
+				{
+					Ph ph(PH_AFTER_SEEDS);
+					after_seeds(s, (int)mate);
+				}
 			}
 			if(s.shs[mate].empty()) {
 				s.done[mate] = true;
@@ -3170,7 +3312,10 @@ void Driver::step_read(Slot& s) {
 			}
 			if(R_seedSumm) continue;
 			if(s.shs[mate].empty()) continue;
-			s.shs[mate].rankSeedHits(s.rnd, s.msinkwrap.allHits());
+			{
+				Ph ph(PH_RANK);
+				s.shs[mate].rankSeedHits(s.rnd, s.msinkwrap.allHits());
+			}
 			start_ext(s, (int)mate, R_multiseedMms, s.seedlens[mate], s.interval[mate]);
 		ext_seeds:
 			ret = ext(s);
@@ -3216,9 +3361,12 @@ void Driver::step_read(Slot& s) {
 		s.prm.seedsPerNuc = totnucs > 0 ? ((float)s.seedsTried / totnucs) : -1;
 		for(int k = 0; k < 4; k++) s.prm.seedsPerNucMS[k] = totnucs > 0 ? ((float)s.seedsTriedMS[k] / totnucs) : -1;
 	}
-	s.msinkwrap.finishRead(&s.shs[0], &s.shs[1], s.exhaustive[0], s.exhaustive[1], s.nfilt[0], s.nfilt[1], s.scfilt[0],
-	                       s.scfilt[1], s.lenfilt[0], s.lenfilt[1], s.qcfilt[0], s.qcfilt[1], s.rnd, rpm, s.prm, *sc,
-	                       !R_seedSumm, R_seedSumm, R_scUnMapped, R_xeq);
+	{
+		Ph ph(PH_FINISH);
+		s.msinkwrap.finishRead(&s.shs[0], &s.shs[1], s.exhaustive[0], s.exhaustive[1], s.nfilt[0], s.nfilt[1], s.scfilt[0],
+		                       s.scfilt[1], s.lenfilt[0], s.lenfilt[1], s.qcfilt[0], s.qcfilt[1], s.rnd, rpm, s.prm, *sc,
+		                       !R_seedSumm, R_seedSumm, R_scUnMapped, R_xeq);
+	}
 	s.pc = P_FINISH;
 }
 
@@ -3282,21 +3430,28 @@ int svc_stats(char* buf, size_t cap) {
 	std::lock_guard<std::mutex> lk(g_svc_mu);
 	int n = snprintf(buf, cap, ", \"kernels\": {");
 	for(int k = 0; k < K_N; k++) {
-		uint64_t L[16] = {}, W = 0, I = 0;
+		uint64_t L[16] = {}, W = 0, I = 0, KW[16] = {}, KI[16] = {};
 		double M[16] = {};
 		for(auto& dv : g_svcs) {
 			if(!dv[k]) continue;
 			for(Svc* v : dv[k]->workers) {
 				std::lock_guard<std::mutex> l2(v->st_mu);
-				for(int i = 0; i < 16; i++) { L[i] += v->k_launch[i]; M[i] += v->k_ms[i]; }
+				for(int i = 0; i < 16; i++) {
+					L[i] += v->k_launch[i];
+					M[i] += v->k_ms[i];
+					KW[i] += v->kwork[i].load();
+					KI[i] += v->kitems[i].load();
+				}
 				W += v->work.load();
 				I += v->items.load();
 			}
 		}
 		n += snprintf(buf + n, cap - n, "%s\"%s\": {\"work\": %llu, \"items\": %llu, \"ids\": [", k ? ", " : "",
 		              K_NAMES[k], (unsigned long long)W, (unsigned long long)I);
+		// [launches, ms, algorithmic work, items] per kernel id
 		for(int i = 0; i < 16; i++)
-			n += snprintf(buf + n, cap - n, "%s[%llu, %.3f]", i ? ", " : "", (unsigned long long)L[i], M[i]);
+			n += snprintf(buf + n, cap - n, "%s[%llu, %.3f, %llu, %llu]", i ? ", " : "", (unsigned long long)L[i], M[i],
+			              (unsigned long long)KW[i], (unsigned long long)KI[i]);
 		n += snprintf(buf + n, cap - n, "]}");
 	}
 	n += snprintf(buf + n, cap - n, "}");
@@ -3588,7 +3743,14 @@ void Driver::run_loop() {
 			// the slots overshot max_slots -- r04af: 45 727 slots for 16 x 2 048)
 			active_a.store(active + 16 * got.size());
 		}
-		for(Elem* e : got) admit(e);
+		{
+			Ph ph(PH_ADMIT);
+			for(Elem* e : got) admit(e);
+		}
+		if(phases_on() && !g_tsc0.load()) {
+			uint64_t z = 0;
+			if(g_tsc0.compare_exchange_strong(z, __builtin_ia32_rdtsc())) g_us0 = now_us();
+		}
 		active_a.store(active);
 		if(!got.empty()) room_cv.notify_one();
 		const uint64_t t0 = now_us();
@@ -3598,16 +3760,24 @@ void Driver::run_loop() {
 			Slot* s = L.run[k];
 			s->nsteps++;
 			const long long m0 = bt2g_alloc_thread_net();
-			step_read(*s);
+			{
+				Ph ph(PH_STEP);
+				step_read(*s);
+			}
 			s->mem += bt2g_alloc_thread_net() - m0;
-			if(s->pc == P_FINISH) release(s);
-			else L.next.push_back(s);
+			if(s->pc == P_FINISH) {
+				Ph ph(PH_RELEASE);
+				release(s);
+			} else {
+				L.next.push_back(s);
+			}
 		}
 		L.run.clear();
 		active_a.store(active);
 		room_cv.notify_one();
 		const uint64_t t1 = now_us();
 		bt2g_prof_role(1);
+		ph_flush();
 		submit(L);
 		// the other lane's requests went out a step ago: their answers are what this
 		// driver waits for while L's are served (one lane: L's own)

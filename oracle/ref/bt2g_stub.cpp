@@ -145,7 +145,9 @@ int bt2g_one_mm(bt2g_ctx* c, const uint8_t* reads, const uint8_t* quals, uint32_
 int bt2g_exact_sweep_1mm(bt2g_ctx* c, const uint8_t* reads, const uint8_t* quals, uint32_t stride,
                          const uint32_t* lens, uint32_t n, uint32_t mine_max, int nofw, int norc, int skip_exact,
                          const int32_t* minsc, const bt2g_scoring* sc, uint32_t cap, uint32_t* sweep,
-                         bt2g_mm1* hits, int32_t* counts, uint32_t* bwops, uint32_t off_cap, uint32_t* offs) {
+                         bt2g_mm1* hits, int32_t* counts, uint32_t* bwops, uint32_t* mm_loads, uint32_t off_cap,
+                         uint32_t* offs) {
+	if(mm_loads) memset(mm_loads, 0, sizeof(uint32_t) * n);     // (the stand-in gathers no sides)
 	int rc = bt2g_exact_sweep(c, reads, stride, lens, n, mine_max, nofw, norc, sweep);
 	if(rc) return rc;
 	for(uint32_t i = 0; i < n; i++) {
@@ -337,7 +339,7 @@ int bt2g_extend(bt2g_ctx* c, const uint8_t* reads, uint32_t stride, const uint32
 		const char* qp = qq.c_str();
 		uint32_t tb[4] = {q.topf, q.botf, q.topb, q.botb}, o[3];
 		bt2ref_extend(c->ref, 1, &sp, &qp, &q.fw, &q.off, &q.len, tb, o);
-		out[i].nlex = o[0]; out[i].nrex = o[1]; out[i].fmops = o[2]; out[i].pad = 0;
+		out[i].nlex = o[0]; out[i].nrex = o[1]; out[i].fmops = o[2]; out[i].loads = 0;
 	}
 	return BT2G_OK;
 }

@@ -26,6 +26,20 @@ slots)
       > $O/bench_s$S.json 2> $O/bench_s$S.log || { tail -30 $O/bench_s$S.log; exit 1; }
     python3 -c "import json; d=json.load(open('$O/bench_s$S.json')); s=d['server']; print($S, round(d['value']), s['slots'], s['server_rss_gb_per_pass'], round(s['cpu_us_per_read'],1))"
   done ;;
+phases)
+  # the batch server's per-read logic by phase ($BT2G_PHASES) and a flat CPU profile ($BT2G_SAMPLE)
+  BT2G_PHASES=1 BT2G_SAMPLE=$PWD/$O/samples.txt timeout -k 10 600 python3 -u bench.py --steps ${3:-2} --warmup 1 --chain-steps 0 \
+    --stock-sample 0 $BENCH_ARGS > $O/bench.json 2> $O/bench.log || { tail -30 $O/bench.log; exit 1; }
+  cp oracle/_ref/bowtie2-align-server-batch $O/server.bin
+  python3 -c "import json; d=json.load(open('$O/bench.json')); print(d['value'], d['server']['cpu_us_per_read'])" ;;
+drivers)
+  # driver threads x slots per driver: "D:S D:S ..." ($DS)
+  for ds in ${DS:-24:683 20:820}; do
+    D=${ds%%:*}; S=${ds##*:}
+    BT2G_BATCH_SLOTS=$S timeout -k 10 500 python3 -u bench.py --drivers $D --steps ${3:-3} --warmup 1 --chain-steps 0 --stock-sample 0 $BENCH_ARGS \
+      > $O/bench_d$D.json 2> $O/bench_d$D.log || { tail -30 $O/bench_d$D.log; exit 1; }
+    python3 -c "import json; d=json.load(open('$O/bench_d$D.json')); s=d['server']; print($D, $S, round(d['value']), s['slots'], s['server_rss_gb_per_pass'][-1], round(s['cpu_us_per_read'],1), s['idle_ms'])"
+  done ;;
 bench)
   T0=$(date +%s); timeout -k 10 1100 python3 -u bench.py --gpus 1 --steps 20 --warmup 5 > $O/bench.json 2> $O/bench.log || { tail -30 $O/bench.log; exit 1; }; echo "wall $(( $(date +%s) - T0 )) s"
   tail -25 $O/bench.log | grep -v "^\s*$"; cut -c1-1500 $O/bench.json ;;
