@@ -243,3 +243,58 @@ def test_seed_search_ext_fused(engines, pol):
     for (i, f, s, j), o in zip(rwhere, ov):
         wo[i, f, s, j] = o
     assert np.array_equal(offs, wo) and len(rows) > 500
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("name", ["lambda", "synth"])
+@pytest.mark.parametrize("skip", [0, 1])
+def test_exact_sweep_1mm_reference(engines, name, skip):
+    """bt2g_exact_sweep_1mm against the REFERENCE's composition of the same calls
+    (tests/golden/fused.npz, make_golden_fused.py: exactSweep, the gate of
+    bt2_search.cpp:3649-3650, oneMmSearch, getOffset of the small ranges' rows)."""
+    f = load_golden("fused")
+    g = load_golden("fm_" + name)
+    e = engines[name]
+    cap = 16
+    sw, hits, cnt, ops, offs = e.exact_sweep_1mm(g["reads"], g["quals"], g["lens"], g["mmminsc_ee"], False,
+                                                 skip_exact=bool(skip), cap=cap, off_cap=8)
+    assert np.array_equal(sw[:, :7], _gold_exact_to_gpu_layout(f[f"sweep_{name}"]))
+    rc = f[f"mmn_{name}_{skip}"]
+    assert np.array_equal(cnt, rc.clip(0))
+    assert np.array_equal(ops, f[f"mmops_{name}_{skip}"].astype(np.uint32))
+    ref, roffs = f[f"mm_{name}_{skip}"], f[f"offs_{name}_{skip}"]
+    assert np.array_equal(offs[:, :2], roffs[:, :2])           # the exact ranges' rows
+    whole = 0
+    for i in range(len(rc)):
+        if rc[i] > cap:
+            continue                                          # (over the cap: the caller asks again)
+        whole += 1
+        for k in range(rc[i]):
+            x, h = ref[i, k], hits[i, k]
+            assert (h["top"], h["bot"], h["fw"], h["score"], h["pos"]) == tuple(int(v) for v in x[:5]), (i, k)
+            assert (x[5] & 0xff) == ord("ACGTN"[h["chr"]]) and (x[5] >> 8) == ord("ACGTN"[h["qchr"]])
+        assert np.array_equal(offs[i], roffs[i]), i
+    assert whole > 100 and (rc > 0).sum() > 50
+    assert (e.last_mm_loads[rc <= 0] == 0).all() and (e.last_mm_loads[rc > 0] > 0).all()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("name", ["lambda", "synth"])
+@pytest.mark.parametrize("pol", ["s22", "s10"])
+def test_seed_search_ext_reference(engines, name, pol):
+    """bt2g_seed_search_ext against the REFERENCE: its seed round, SwDriver::extend
+    of every range as prioritizeSATups asks it (aligner_sw_driver.cpp:574-589)
+    and getOffset of the small ranges' rows (tests/golden/fused.npz)."""
+    f = load_golden("fused")
+    g = load_golden("fm_" + name)
+    L, iv, off = (int(x) for x in f[f"seedpol_{name}_{pol}"])
+    sx, so = f[f"sx_{name}_{pol}"], f[f"so_{name}_{pol}"]
+    out, ns, ops, ext, offs = engines[name].seed_search_ext(g["reads"], g["lens"], L, iv, off, sx.shape[2],
+                                                            off_cap=so.shape[3])
+    assert np.array_equal(out, f[f"seed_{name}_{pol}"]) and np.array_equal(ns, f[f"seedn_{name}_{pol}"])
+    assert np.array_equal(ops, f[f"seedops_{name}_{pol}"].astype(np.uint32))
+    assert np.array_equal(ext[..., :3], sx)
+    # side loads: one or two 64-B sides per LF step (the roofline's bytes)
+    steps, loads = ext[..., 2].astype(np.int64), ext[..., 3].astype(np.int64)
+    assert (loads <= 2 * steps).all() and loads.sum() >= 0.9 * steps.sum() > 0
+    assert np.array_equal(offs, so)

@@ -183,3 +183,79 @@ def test_frame(orc):
             assert got == exp, (name, i, x[i].tolist(), got, exp)
             nframed += got[0]
     assert nframed > 30000
+
+
+# ---- the fused calls' reference fixtures (tests/golden/fused.npz, make_golden_fused.py) ----
+def oracle_sweep_1mm(orc, fe, be, g, name, skip, off_cap=8, mm_cap=16):
+    """The oracle composed as bt2g_exact_sweep_1mm composes the reference's calls
+    (bt2_search.cpp:3453-3667): sweep, the gate, the gated 1-mm search, the small
+    ranges' row offsets.  Returns (sweep, hits, counts (-1: gated off), bwops, offs)."""
+    reads, quals, lens = g["reads"], g["quals"], g["lens"]
+    ms = g["mmminsc_ee"]
+    sw = orc.exact_sweep(fe, reads, lens)
+    n = len(lens)
+    hits = np.zeros((n, 64, 7), np.int64)
+    cnt = np.full(n, -1, np.int32)
+    ops = np.zeros(n, np.uint64)
+    offs = np.full((n, 2 + mm_cap, off_cap), 0xFFFFFFFF, np.uint32)
+    for i in range(n):
+        mfw, mrc = int(sw[i, 0]), int(sw[i, 1])
+        yfw, yrc = mfw <= 1, mrc <= 1
+        rg = [(int(sw[i, 3]), int(sw[i, 4])) if mfw == 0 else (0, 0),
+              (int(sw[i, 5]), int(sw[i, 6])) if mrc == 0 else (0, 0)]
+        if not ((skip and min(mfw, mrc) == 0) or not (yfw or yrc)):
+            h, c, bw = orc.one_mm(fe, be, reads[i:i + 1], quals[i:i + 1], lens[i:i + 1], ms[i:i + 1], False,
+                                  nofw=not yfw, norc=not yrc)
+            hits[i], cnt[i], ops[i] = h[0], c[0], bw[0]
+            rg += [(int(h[0, k, 0]), int(h[0, k, 1])) for k in range(min(int(c[0]), mm_cap))]
+        for slot, (t, b) in enumerate(rg):
+            if 0 < b - t <= off_cap:
+                for j in range(b - t):
+                    offs[i, slot, j] = orc.get_offset(fe, t + j)
+    return sw, hits, cnt, ops, offs
+
+
+@pytest.mark.parametrize("name", ["lambda", "synth"])
+@pytest.mark.parametrize("skip", [0, 1])
+def test_fused_sweep_1mm(orc, name, skip):
+    """The oracle, composed as bt2g_exact_sweep_1mm, against the reference's own
+    composition (sweep, gated oneMmSearch, getOffset of the small ranges)."""
+    f = load_golden("fused")
+    g = load_golden("fm_" + name)
+    fe, be = _ebwts(orc, name)
+    sw, hits, cnt, ops, offs = oracle_sweep_1mm(orc, fe, be, g, name, skip)
+    assert np.array_equal(sw, f[f"sweep_{name}"].astype(np.uint64))
+    rc = f[f"mmn_{name}_{skip}"]
+    assert np.array_equal(cnt, rc)
+    _mm_eq(f[f"mm_{name}_{skip}"], rc.clip(0), hits, cnt.clip(0))
+    assert np.array_equal(ops, f[f"mmops_{name}_{skip}"])
+    assert np.array_equal(offs, f[f"offs_{name}_{skip}"])
+
+
+@pytest.mark.parametrize("name", ["lambda", "synth"])
+@pytest.mark.parametrize("pol", ["s22", "s10"])
+def test_fused_seed_ext(orc, name, pol):
+    """The oracle's seed round + SwDriver::extend of every range + row offsets
+    against the reference's (bt2g_seed_search_ext's definition)."""
+    f = load_golden("fused")
+    g = load_golden("fm_" + name)
+    fe, be = _ebwts(orc, name)
+    L, iv, off0 = (int(x) for x in f[f"seedpol_{name}_{pol}"])
+    maxs = f[f"sx_{name}_{pol}"].shape[2]
+    out, ns, ops = orc.seed_search(fe, be, g["reads"], g["lens"], L, iv, off0, maxs)
+    assert np.array_equal(out, f[f"seed_{name}_{pol}"]) and np.array_equal(ns, f[f"seedn_{name}_{pol}"])
+    sx = np.zeros_like(f[f"sx_{name}_{pol}"])
+    so = np.full_like(f[f"so_{name}_{pol}"], 0xFFFFFFFF)
+    for i in range(len(ns)):
+        ln = int(g["lens"][i])
+        for s_ in range(2):
+            for k in range(maxs):
+                t, b, tb, bb = (int(x) for x in out[i, s_, k])
+                depth, sl = off0 + k * iv, min(L, ln)
+                if b > t and depth + sl <= ln:
+                    sx[i, s_, k] = orc.extend(fe, be, g["reads"][i, :ln], 1 - s_, depth, sl, t, b, tb, bb)
+                if 0 < b - t <= so.shape[3]:
+                    for j in range(b - t):
+                        so[i, s_, k, j] = orc.get_offset(fe, t + j)
+    assert np.array_equal(sx, f[f"sx_{name}_{pol}"])
+    assert np.array_equal(so, f[f"so_{name}_{pol}"])
