@@ -227,21 +227,53 @@ def test_bt_long_reads_vs_oracle(eng, local):
         assert (naln > 0).sum() > 8
 
 
-def test_bt_lds_resident_equals_lane_kernel(eng, monkeypatch):
-    """Batches up to BT2G_BT_LDS_MAX problems walk LDS-resident (a workgroup per
-    problem, sw_backtrace.hip LDSRES); BT2G_BT_LDS_MAX=0 forces the lane-per-problem
-    kernel.  Both give the same alignments, edits and fates on the same batch."""
+@pytest.mark.parametrize("shape", ["seedext", "mate"])
+@pytest.mark.parametrize("variant", ["wg", "one_walker", "wg_lds64k"])
+def test_bt_lds_resident_equals_lane_kernel(eng, monkeypatch, shape, variant):
+    """Batches up to BT2G_BT_LDS_MAX problems walk LDS-resident: by default the
+    workgroup walk (sw_backtrace_wg.hip; wide planes with the >64 KiB LDS opt-in),
+    with BT2G_BT_WG=0 the one-walker LDS-resident kernel, with BT2G_BT_WG_LDS=0 the
+    workgroup walk only where its layout fits 64 KiB (else the one-walker or the
+    lane kernel).  BT2G_BT_LDS_MAX=0 forces the lane-per-problem kernel.  All give
+    the same alignments, edits and fates on the same batch -- seed-extension
+    shapes (150 x 210) and mate-search shapes (150 x ~700: the decision plane up to
+    $BT2G_DEC_RATIO and the opt-in launch), the latter also against the oracle."""
     gen = get_index("lambda").ref_codes[0]
-    codes, quals, lens, probs, rects = _synth_problems(gen, 900, 53)
+    maxgap, n = (15, 900) if shape == "seedext" else (137, 300)
+    codes, quals, lens, probs, rects = _synth_problems(gen, n, 53, maxgap=maxgap)
+    env = {"wg": {}, "one_walker": {"BT2G_BT_WG": "0"}, "wg_lds64k": {"BT2G_BT_WG_LDS": "0"}}[variant]
     outs = []
-    for lim in ("8192", "0"):
+    for lim in ("65536", "0"):
         monkeypatch.setenv("BT2G_BT_LDS_MAX", lim)
+        for k, v in env.items():
+            monkeypatch.setenv(k, v)
         outs.append(eng.sw_align_bt(codes, quals, lens, probs, rects=rects, cap=1024, maxaln=64, maxedit=512))
+        for k in env:
+            monkeypatch.delenv(k)
     a, b = outs
-    for x, y in zip(a, b):
+    # results, candidate lists, counts: whole; alignments, edits and fates: the
+    # valid parts (slots past them are not written)
+    for x, y in zip(a[:3], b[:3]):
         if x.dtype.names:
             for f in x.dtype.names:
                 assert np.array_equal(x[f], y[f]), f
         else:
             assert np.array_equal(x, y)
-    assert (a[2] > 0).sum() > 600
+    naln = a[2]
+    for p in range(n):
+        k = max(int(naln[p]), 0)
+        for f in a[3].dtype.names:
+            assert np.array_equal(a[3][f][p, :k], b[3][f][p, :k]), (p, f)
+        for j in range(k):
+            ne = min(int(a[3]["nedit"][p, j]), a[4].shape[2])
+            for f in ("pos", "type", "chr", "qchr"):
+                assert np.array_equal(a[4][f][p, j, :ne], b[4][f][p, j, :ne]), (p, j, f)
+        nc = min(int(a[0]["ncand"][p]), a[5].shape[1])
+        assert np.array_equal(a[5][p, :nc], b[5][p, :nc]), p
+    assert (a[2] > 0).sum() > 0.6 * n
+    if shape == "mate" and variant == "wg":
+        from oracle.oracle import Oracle
+        res, cands, naln, alns, edits, fates = a
+        k = 64
+        ea, ee, ef = _oracle_expect(Oracle(), gen, codes[:k], quals[:k], probs[:k], rects[:k], False)
+        check_against(naln[:k], alns[:k], edits[:k], fates[:k], res[:k], None, ea, ee, ef, "mate")

@@ -275,7 +275,7 @@ def test_exact_sweep_1mm_reference(engines, name, skip):
             assert (x[5] & 0xff) == ord("ACGTN"[h["chr"]]) and (x[5] >> 8) == ord("ACGTN"[h["qchr"]])
         assert np.array_equal(offs[i], roffs[i]), i
     assert whole > 100 and (rc > 0).sum() > 50
-    assert (e.last_mm_loads[rc <= 0] == 0).all() and (e.last_mm_loads[rc > 0] > 0).all()
+    assert (e.last_mm_loads[rc < 0] == 0).all() and (e.last_mm_loads[rc > 0] > 0).all()
 
 
 @pytest.mark.gpu
