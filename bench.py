@@ -509,7 +509,7 @@ BATCH_SERVER = os.path.join(ROOT, "oracle", "_ref", "bowtie2-align-server-batch"
 # HBM traffic per launch of the batch server's kernels: the summary of separate
 # rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes over this same bench command
 # (scripts/gpu_r04.sh benchpmc -> scripts/pmc_summary.py), committed under profiles/
-SERVER_PMC = os.path.join(ROOT, "profiles", "r04", "server_pmc.json")
+SERVER_PMC = os.path.join(ROOT, "profiles", "r05", "server_pmc.json")
 
 
 def server_traffic(path, kernel):
@@ -530,8 +530,15 @@ def server_traffic(path, kernel):
         n += v["dispatches"]
     if not n:
         return None, None
-    return tot / n, (f"{os.path.relpath(path, ROOT)}: FETCH_SIZE x 2 + WRITE_SIZE per dispatch of {kernel}* "
-                     f"({n} dispatches of separate --pmc passes of bench.py with rocprofv3 in front of the server)")
+    note = (f"{os.path.relpath(path, ROOT)}: FETCH_SIZE x 2 + WRITE_SIZE per dispatch of {kernel}* "
+            f"({n} dispatches of separate --pmc passes of bench.py with rocprofv3 in front of the server)")
+    lib = os.path.join(PKG, "libbt2g.so")
+    want = (d.get("build_sha256") or {}).get("bowtie2-server_amd/libbt2g.so")
+    if want is None:
+        note += "; STALE? the summary records no build"
+    elif os.path.exists(lib) and binary_id(lib)["sha256"] != want:
+        note += "; STALE: taken on another build of libbt2g.so than the one benchmarked"
+    return tot / n, note
 # the engine services' kernel ids (bt2g_api.cpp ProfScope) by call kind, the
 # kernels' names in the line, and their bound (None: no roofline, e.g. the DP
 # call's whole stream span); the algorithmic work of each comes from the server
@@ -603,6 +610,8 @@ def server_kernels(st):
              "items": items}
         if bound == "span":
             e["span"] = True
+        if (kind, kid) in FAMILY_IDS:
+            e["family"] = True
         if bound == "hbm" and work:
             e.update(bound="hbm", bytes_total=work, bytes_per_launch=work / launches,
                      achieved=work / (ms / 1e3) / 1e9, unit="GB/s", peak=HBM_PEAK_GBS)
@@ -616,10 +625,17 @@ def server_kernels(st):
     return out
 
 
+# ids whose time spans several kernels (the 1-mm search's items / near / far /
+# branch / compact launches): a family, not one kernel
+FAMILY_IDS = {("exact_sweep", 2), ("one_mm", 2)}
+
+
 def dominant_kernel(kern):
-    """The kernel with the largest total time over the run (the DP call's stream
-    span is not a kernel)."""
-    ks = [k for k in kern if not kern[k].get("span")]
+    """The single kernel with the largest total time over the run (the DP call's
+    stream span and multi-kernel families are not one kernel; their shares are
+    in server_kernels) -- the kernel rocprofv3's summary of the same command
+    ranks first, whose average duration the line's ms_per_launch must match."""
+    ks = [k for k in kern if not kern[k].get("span") and not kern[k].get("family")]
     return max(ks, key=lambda k: kern[k]["ms_total"], default=None)
 
 
@@ -657,6 +673,11 @@ def schedule_run(args, rank, world, local, base, reads_np, quals_np, workdir, bi
     prefix = tuple(shlex.split(os.environ.get("BT2G_BENCH_SERVER_PREFIX", "")))
     if prefix:
         env["BT2G_EXIT_CLEAN"] = "1"
+        # the profiler times the kernels itself; the engines' own HIP-event timing
+        # under rocprofv3 faulted inside librocprofiler-sdk (r04ag, r05h: SIGSEGV under
+        # hipEventRecord of ProfScope::~ProfScope, DP service threads) -- off unless
+        # $BT2G_BENCH_KPROF=1
+        env["BT2G_KPROF"] = os.environ.get("BT2G_BENCH_KPROF", "0")
     multi = world > 1 and dist.is_initialized()
     with rs.Server(base, threads=args.drivers, args=policy_args(args.mode, args.preset), binary=binary,
                    env=env, log_path=os.path.join(workdir, "server.log"), prefix=prefix) as srv:

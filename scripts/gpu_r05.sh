@@ -40,6 +40,20 @@ drivers)
       > $O/bench_d$D.json 2> $O/bench_d$D.log || { tail -30 $O/bench_d$D.log; exit 1; }
     python3 -c "import json; d=json.load(open('$O/bench_d$D.json')); s=d['server']; print($D, $S, round(d['value']), s['slots'], s['server_rss_gb_per_pass'][-1], round(s['cpu_us_per_read'],1), s['idle_ms'])"
   done ;;
+prof)
+  # rocprofv3 kernel trace of the bench command's batch server (default path: the workgroup
+  # walk with its LDS opt-in), then the FETCH_SIZE / WRITE_SIZE passes (separate runs)
+  BT2G_BENCH_SERVER_PREFIX="rocprofv3 --kernel-trace --stats --output-format csv -d $PWD/$O/bprof -o run --" \
+    timeout -k 10 600 python3 -u bench.py --steps 1 --warmup 1 --chain-steps 0 --stock-sample 0 > $O/bench_prof.json 2> $O/bench_prof.log || { tail -30 $O/bench_prof.log; exit 1; }
+  find $O/bprof -name "*kernel_stats.csv" -exec cp {} $O/run_kernel_stats.csv \;
+  find $O/bprof -name "*.csv" -size +40M -delete
+  for c in FETCH_SIZE WRITE_SIZE; do
+    BT2G_BENCH_SERVER_PREFIX="rocprofv3 --pmc $c --output-format csv -d $PWD/$O/pmc_$c -o run --" \
+      timeout -k 10 500 python3 -u bench.py --steps 1 --warmup 1 --chain-steps 0 --stock-sample 0 --reads 200000 > $O/bench_pmc_$c.json 2> $O/bench_pmc_$c.log || { tail -30 $O/bench_pmc_$c.log; exit 1; }
+  done
+  python3 scripts/pmc_summary.py $O/pmc_FETCH_SIZE $O/pmc_WRITE_SIZE $O/server_pmc.json
+  find $O -name "*.csv" -size +40M -delete
+  head -25 $O/run_kernel_stats.csv | cut -d, -f1-6 ;;
 bench)
   T0=$(date +%s); timeout -k 10 1100 python3 -u bench.py --gpus 1 --steps 20 --warmup 5 > $O/bench.json 2> $O/bench.log || { tail -30 $O/bench.log; exit 1; }; echo "wall $(( $(date +%s) - T0 )) s"
   tail -25 $O/bench.log | grep -v "^\s*$"; cut -c1-1500 $O/bench.json ;;

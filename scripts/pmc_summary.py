@@ -41,7 +41,18 @@ def main():
                   "fetch_bytes": fk * 1024 if fk is not None else None,
                   "fetch_bytes_x2": fk * 2048 if fk is not None else None,
                   "write_bytes": wk * 1024 if wk is not None else None}
-    json.dump({"source": {"fetch": fd, "write": wd}, "kernels": res}, open(out, "w"), indent=1)
+    # the build the counters were taken on: bench.py flags a summary whose engine
+    # library differs from the one it benchmarks (traffic_stale)
+    import hashlib
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    build = {}
+    for rel in ("bowtie2-server_amd/libbt2g.so", "oracle/_ref/bowtie2-align-server-batch"):
+        try:
+            build[rel] = hashlib.sha256(open(os.path.join(root, rel), "rb").read()).hexdigest()
+        except OSError:
+            pass
+    json.dump({"source": {"fetch": fd, "write": wd}, "build_sha256": build, "kernels": res}, open(out, "w"),
+              indent=1)
     for k, v in sorted(res.items(), key=lambda kv: -(kv[1]["dispatches"] or 0))[:20]:
         print(k[:80], v["dispatches"], v["fetch_kib"], v["write_kib"])
 
