@@ -505,7 +505,7 @@ def pmc_traffic(fetch_csv, write_csv, kernel):
     return total
 
 
-BATCH_SERVER = os.path.join(ROOT, "oracle", "_ref", "bowtie2-align-server-batch")
+BATCH_SERVER = os.path.join(ROOT, "integration", "bin", "bowtie2-align-server-batch")
 # HBM traffic per launch of the batch server's kernels: the summary of separate
 # rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes over this same bench command
 # (scripts/gpu_r04.sh benchpmc -> scripts/pmc_summary.py), committed under profiles/
@@ -639,6 +639,25 @@ def dominant_kernel(kern):
     return max(ks, key=lambda k: kern[k]["ms_total"], default=None)
 
 
+# host memory of one batch server (r05d, 16 drivers, hg38-like genome): ~12 GB
+# without slots (the reference's index on the host, the engines' pinned staging,
+# the HIP runtime) + ~2.8 MB per read slot (the reference's per-read objects and
+# the slot's cache pools after pool_trim), plus ~10 GB for the bench process
+SERVER_BASE_GB, SLOT_MB, BENCH_PROC_GB = 12.0, 2.8, 10.0
+
+
+def slots_per_driver(world, drivers, rank_mem_gb=0.0):
+    """Reads in flight per driver thread ($BT2G_BATCH_SLOTS) within a per-rank
+    host-memory budget: one GPU keeps the server's default (1 024); with several
+    ranks per node every rank's server and bench process must fit
+    rank_mem_gb (default 56 GB: 8 ranks in ~450 GB of the node's host memory)."""
+    if world <= 1 and not rank_mem_gb:
+        return 1024
+    budget = rank_mem_gb or 56.0
+    per = int((budget - BENCH_PROC_GB - SERVER_BASE_GB) * 1024 / (drivers * SLOT_MB))
+    return max(128, min(1024, per // 64 * 64))
+
+
 def schedule_run(args, rank, world, local, base, reads_np, quals_np, workdir, binary=None):
     """The north-star number: the reference's real schedule -- its server,
     client, per-read logic and SAM -- with the batch-first driver
@@ -666,6 +685,9 @@ def schedule_run(args, rank, world, local, base, reads_np, quals_np, workdir, bi
     stats = os.path.join(workdir, "stats.json")
     env = rs.dropin_env(base, stats, device=local)
     env["BT2G_KPROF"] = "1"
+    slots = int(os.environ.get("BT2G_BATCH_SLOTS") or
+                slots_per_driver(world, args.drivers, getattr(args, "rank_mem_gb", 0.0)))
+    env["BT2G_BATCH_SLOTS"] = str(slots)
     # $BT2G_BENCH_SERVER_PREFIX: a profiler in front of the batch server's command line
     # (e.g. "rocprofv3 --kernel-trace --stats -d DIR -o run --"); the server then exits
     # through exit() at SIGTERM so that the profile is written
@@ -715,7 +737,7 @@ def schedule_run(args, rank, world, local, base, reads_np, quals_np, workdir, bi
             except ValueError:
                 pass
         time.sleep(0.1)
-    return {"elapsed": elapsed, "aligned": aligned, "outs": outs, "chunks": chunks, "stats": st,
+    return {"elapsed": elapsed, "aligned": aligned, "outs": outs, "chunks": chunks, "stats": st, "slots_per_driver": slots,
             "server_cpu_s": cpu_s, "server_threads_cpu": threads_cpu, "server_rss_gb": rss[-1],
             "server_rss_gb_per_pass": rss, "binary": binary_id(binary), "smaps_top": smaps}
 
@@ -1075,6 +1097,9 @@ def main():
     ap.add_argument("--reads", type=int, default=1_000_000, help="reads (paired: read pairs) per GPU per step")
     ap.add_argument("--drivers", type=int, default=16, help="batch server driver threads (-p)")
     ap.add_argument("--clients", type=int, default=32, help="concurrent client connections (both servers)")
+    ap.add_argument("--rank-mem-gb", type=float, default=0.0,
+                    help="host-memory budget per rank (batch server + this process) that sizes the server's "
+                         "read slots (0: 1 024 slots per driver on one GPU, 56 GB per rank with several)")
     ap.add_argument("--warmup-chunks", type=int, default=0,
                     help="chunks of a warmup pass (0: all of them -- a warmup step is a whole pass)")
     ap.add_argument("--stock-sample", type=int, default=200_000,
@@ -1162,6 +1187,7 @@ def main():
         reads_np, quals_np = make_pairs(parts, args.reads, args.read_len, seed=shard_seed(rank))
     else:
         reads_np, quals_np = make_reads(parts, args.reads, args.read_len, seed=shard_seed(rank))
+    del parts                                   # (3.1 GB: the reads are made, the index holds the rest)
     log(f"[rank {rank}] {args.reads} reads in {time.time()-t2:.1f}s")
 
     # ---- the north-star number: the reference's real schedule on the batch server ----
@@ -1216,6 +1242,7 @@ def main():
             "config": {"workload": schedule_workload(args), "global_batch": args.reads * world,
                        "seq_len": args.read_len, "parallelism": f"dp{world} (a batch server per GPU)",
                        "aligned_frac": n_aligned / total_reads, "drivers": args.drivers,
+                       "slots_per_driver": sched["slots_per_driver"],
                        "client_connections": args.clients, "reads_per_connection": 10_000,
                        "warmup_chunks": args.warmup_chunks},
             "roofline": rl,
@@ -1255,7 +1282,7 @@ def schedule_workload(args):
     size = "hg38-size " if args.genome_mb >= 3000 else ""
     return (f"{what}, vs a {args.genome_mb:.0f} Mbp {size}synthetic genome ({args.genome_model}; hg38 is "
             f"unavailable offline), through the reference's own server, client and per-read logic with the "
-            f"batch-first driver on the engines (oracle/_ref/bowtie2-align-server-batch), SAM output; "
+            f"batch-first driver on the engines (integration/bin/bowtie2-align-server-batch), SAM output; "
             f"<= 10 000 reads per client connection, {args.clients} connections at a time")
 
 

@@ -604,6 +604,82 @@ void pool_trim(Pool& p) {
 // mateStreaks_) are used as the reference uses them; the loops' locals live
 // here so that a loop can stop where it needs an engine result and resume
 // there.
+// RedundantAlns (aligner_result.h:1657-1692, aligner_result.cpp:929-1010)
+// restated flat: the reference keeps one sorted set of (ref, strand, ref offset,
+// read row) cells per read row and inserts ~150 of them per reported alignment;
+// here an alignment is its [left, right) reference interval per read row, kept
+// in one array per read, and overlap() compares a candidate's intervals row by
+// row with those of the same reference and strand.  Same cells, same answers:
+// the intervals are computed by the reference's own walk over the edits
+// (including its invertEdits round trip for reverse-strand alignments).
+struct RedFlat {
+	struct Aln {
+		TRefId ref;
+		bool fw;
+		size_t row0;                      // first read row
+		size_t nrow;
+		size_t at;                        // its intervals in iv
+	};
+	std::vector<Aln> alns;
+	std::vector<std::pair<TRefOff, TRefOff>> iv, tmp;
+	void reset() {
+		alns.clear();
+		iv.clear();
+	}
+	// the cells of res: per row, [left, right) (aligner_result.cpp:930-969)
+	static size_t cells(const AlnRes& res, std::vector<std::pair<TRefOff, TRefOff>>& out) {
+		TRefOff left = res.refoff(), right;
+		const size_t len = res.readExtentRows();
+		const size_t start = res.trimmedLeft(true);
+		if(!res.fw()) const_cast<AlnRes&>(res).invertEdits();
+		const EList<Edit>& ned = res.ned();
+		size_t nedidx = 0;
+		for(size_t i = start; i < start + len; i++) {
+			size_t diff = 1;
+			right = left + 1;
+			while(nedidx < ned.size() && ned[nedidx].pos == i) {
+				if(ned[nedidx].isRefGap()) diff = 0;
+				nedidx++;
+			}
+			if(i < start + len - 1) {
+				size_t nx = nedidx;
+				while(nx < ned.size() && ned[nx].pos == i + 1) {
+					if(ned[nx].isReadGap()) right++;
+					nx++;
+				}
+			}
+			out.emplace_back(left, right);
+			left = right + diff - 1;
+		}
+		if(!res.fw()) const_cast<AlnRes&>(res).invertEdits();
+		return start;
+	}
+	bool overlap(const AlnRes& res) {
+		tmp.clear();
+		const size_t row0 = cells(res, tmp);
+		const size_t row1 = row0 + tmp.size();
+		for(const Aln& a : alns) {
+			if(a.ref != res.refid() || a.fw != res.fw()) continue;
+			const size_t lo = std::max(row0, a.row0), hi = std::min(row1, a.row0 + a.nrow);
+			for(size_t r = lo; r < hi; r++) {
+				const std::pair<TRefOff, TRefOff>& x = tmp[r - row0];
+				const std::pair<TRefOff, TRefOff>& y = iv[a.at + (r - a.row0)];
+				if(std::max(x.first, y.first) < std::min(x.second, y.second)) return true;
+			}
+		}
+		return false;
+	}
+	void add(const AlnRes& res) {
+		Aln a;
+		a.ref = res.refid();
+		a.fw = res.fw();
+		a.at = iv.size();
+		a.row0 = cells(res, iv);
+		a.nrow = iv.size() - a.at;
+		alns.push_back(a);
+	}
+};
+
 enum { EXTEND_BLOCKED = 0 };
 enum { FOUND_NONE_ = 0, FOUND_EE_, FOUND_UNGAPPED_ };
 enum { X_START = 0, X_AFTER_EE_ROWS, X_AFTER_EXT, X_AFTER_PRIO_ROWS, X_AFTER_UG, X_AFTER_DP, X_AFTER_MDP };
@@ -611,6 +687,19 @@ enum { X_START = 0, X_AFTER_EE_ROWS, X_AFTER_EXT, X_AFTER_PRIO_ROWS, X_AFTER_UG,
 struct SwDriverB : public SwDriver {
 	explicit SwDriverB(size_t bytes) : SwDriver(bytes) {}
 	Pool& ee_pool() { return pool_; }
+	RedFlat redA, redM1, redM2;            // redAnchor_, redMate1_, redMate2_ (RedFlat above)
+	// SwDriver::nextRead (aligner_sw_driver.h:422-441) with the flat redundancy sets
+	void next_read() {
+		redA.reset();
+		seenDiags1_.reset();
+		seenDiags2_.reset();
+		seedExRangeFw_[0].clear();
+		seedExRangeFw_[1].clear();
+		seedExRangeRc_[0].clear();
+		seedExRangeRc_[1].clear();
+		redM1.reset();
+		redM2.reset();
+	}
 
 	// extendSeeds / extendSeedsPaired arguments (bt2_search.cpp:3505-3593 and twins)
 	int mate = 0;                  // the anchor mate (0: mate 1)
@@ -1635,7 +1724,13 @@ void SwDriverB::speculate(Driver& d, Slot& s, std::vector<DpRes*>& out, size_t k
 	DynProgFramer dpframe(!gReportOverhangs);
 	struct Diag { uint32_t t; int64_t o; bool f; };
 	std::vector<Diag> seen;
-	for(size_t ii = 0; ii < gws_.size() && out.size() < k; ii++) {
+	// (speculation never changes a result -- a speculative DP serves only the same
+	// problem asked later -- so where it looks is a matter of cost only)
+	// (from the loop's current range i: the loop has left the ranges before it,
+	// aligner_sw_driver.cpp:883-1030; r05i: resuming instead at a cursor past every
+	// element examined so far asked 41 % more DPs for the same reads -- it skips
+	// the elements whose rows the loop resolves as it goes, the ones it asks next)
+	for(size_t ii = i; ii < gws_.size() && out.size() < k; ii++) {
 		const SATupleAndPos& p = satpos_[ii];
 		const bool f = p.pos.fw;
 		uint32_t ro = p.pos.rdoff;
@@ -2207,8 +2302,8 @@ int SwDriverB::ext_step(Driver& d, Slot& s) {
 					if(!refival.overlapsIgnoreOrient(res->alres.refival())) continue;
 					{
 						Ph ph(PH_REDUND);
-						if(redAnchor_.overlap(res->alres)) continue;
-						redAnchor_.add(res->alres);
+						if(redA.overlap(res->alres)) continue;
+						redA.add(res->alres);
 					}
 					res->alres.setParams(seedmms, seedlen, seedival, *minsc);
 					{
@@ -2444,8 +2539,8 @@ int SwDriverB::ext_step_paired(Driver& d, Slot& s) {
 							if(res->alres.refExtent() == 0) continue;
 						}
 						if(!refival.overlapsIgnoreOrient(res->alres.refival())) continue;
-						if(redAnchor_.overlap(res->alres)) continue;
-						redAnchor_.add(res->alres);
+						if(redA.overlap(res->alres)) continue;
+						redA.add(res->alres);
 						res->alres.setParams(seedmms, seedlen, seedival, *minsc);
 						foundMate = false;
 						off = res->alres.refoff();
@@ -2509,7 +2604,7 @@ int SwDriverB::ext_step_paired(Driver& d, Slot& s) {
 							SwResult* res = res_ptr();
 							Interval refival(tidx, 0, fw, tlen);
 							if(foundMate) {
-								if(!redAnchor_.overlap(oresGap_.alres)) redAnchor_.add(oresGap_.alres);
+								if(!redA.overlap(oresGap_.alres)) redA.add(oresGap_.alres);
 								oresGap_.alres.setParams(seedmms, seedlen, seedival, *ominsc);
 								if(gReportOverhangs && !refival.containsIgnoreOrient(oresGap_.alres.refival())) {
 									oresGap_.alres.clipOutside(true, 0, tlen);
@@ -2535,16 +2630,16 @@ int SwDriverB::ext_step_paired(Driver& d, Slot& s) {
 								if(!anchor1 || !didAnchor) {
 									if(anchor1) didAnchor = true;
 									const AlnRes& r1 = anchor1 ? res->alres : oresGap_.alres;
-									if(!redMate1_.overlap(r1)) {
-										redMate1_.add(r1);
+									if(!redM1.overlap(r1)) {
+										redM1.add(r1);
 										if(msink->report(0, &r1, NULL)) doneUnpaired = true;
 									}
 								}
 								if(anchor1 || !didAnchor) {
 									if(!anchor1) didAnchor = true;
 									const AlnRes& r2 = anchor1 ? oresGap_.alres : res->alres;
-									if(!redMate2_.overlap(r2)) {
-										redMate2_.add(r2);
+									if(!redM2.overlap(r2)) {
+										redM2.add(r2);
 										if(msink->report(0, NULL, &r2)) doneUnpaired = true;
 									}
 								}
@@ -2571,7 +2666,7 @@ int SwDriverB::ext_step_paired(Driver& d, Slot& s) {
 								didAnchor = true;
 								if(!msink->state().doneUnpaired(anchor1)) {
 									const AlnRes& r = res->alres;
-									RedundantAlns& red = anchor1 ? redMate1_ : redMate2_;
+									RedFlat& red = anchor1 ? redM1 : redM2;
 									const AlnRes* r1 = anchor1 ? &res->alres : NULL;
 									const AlnRes* r2 = anchor1 ? NULL : &res->alres;
 									if(!red.overlap(r)) {
@@ -2588,7 +2683,7 @@ int SwDriverB::ext_step_paired(Driver& d, Slot& s) {
 							SwResult* res = res_ptr();
 							if(!msink->state().doneUnpaired(anchor1)) {
 								const AlnRes& r = res->alres;
-								RedundantAlns& red = anchor1 ? redMate1_ : redMate2_;
+								RedFlat& red = anchor1 ? redM1 : redM2;
 								const AlnRes* r1 = anchor1 ? &res->alres : NULL;
 								const AlnRes* r2 = anchor1 ? NULL : &res->alres;
 								if(!red.overlap(r)) {
@@ -2766,7 +2861,7 @@ void Driver::setup_read(Slot& s) {
 	}
 	for(int m = 0; m < 2; m++) s.filt[m] = s.nfilt[m] && s.scfilt[m] && s.lenfilt[m] && s.qcfilt[m];
 	s.prm.nFilt += (s.filt[0] ? 0 : 1) + (s.filt[1] ? 0 : 1);
-	s.sd.nextRead(paired, s.rdlens[0], s.rdlens[1]);
+	s.sd.next_read();
 	s.minedfw[0] = s.minedfw[1] = s.minedrc[0] = s.minedrc[1] = 0;
 	s.nofw[0] = paired ? (gMate1fw ? gNofw : gNorc) : gNofw;
 	s.norc[0] = paired ? (gMate1fw ? gNorc : gNofw) : gNorc;
@@ -3545,6 +3640,22 @@ void conn_done(const void* c, long n) {
 // The reads of one buffer, in the order the reference's worker takes them
 // (bt2_search.cpp:3201-3211, 4174: the buffer is read to its end), copied into
 // slots.
+// $BT2G_READ_SWAP=0: copy the buffer's reads into the slot (Read::operator=)
+bool read_swap_on() {
+	static const bool on = [] { const char* e = getenv("BT2G_READ_SWAP"); return !(e && *e == '0'); }();
+	return on;
+}
+
+// Exchange two Reads' members: every member of a Read (read.h:246-267) is a value
+// or owns its heap buffer through a pointer (SStringExpandable), none points into
+// the object itself, so exchanging the bytes exchanges the reads.
+void swap_read(Read& a, Read& b) {
+	alignas(Read) unsigned char t[sizeof(Read)];
+	memcpy(t, (void*)&a, sizeof(Read));
+	memcpy((void*)&a, (void*)&b, sizeof(Read));
+	memcpy((void*)&b, t, sizeof(Read));
+}
+
 void Driver::admit(Elem* e) {
 	PatternSourcePerThread* ps = e->re.ps;
 	long n = 0;
@@ -3568,12 +3679,21 @@ void Driver::admit(Elem* e) {
 			s = freel.back();
 			freel.pop_back();
 		}
-		const long long m1 = bt2g_alloc_thread_net();
-		s->rdbuf[0] = ra;
-		s->rdbuf[1] = ps->read_b();
-		s->mem += bt2g_alloc_thread_net() - m1;
 		s->paired = !ps->read_b().empty();
 		s->rdid = ra.rdid;
+		if(read_swap_on()) {
+			// the buffer's reads move into the slot and the slot's previous ones into
+			// the buffer, which the connection's parser resets and refills
+			// (PerThreadReadBuf::reset, pat.h) -- no copy of the ~8 strings a Read holds
+			swap_read(s->rdbuf[0], ra);
+			if(s->paired) swap_read(s->rdbuf[1], ps->read_b());
+			else s->rdbuf[1].reset();
+		} else {
+			const long long m1 = bt2g_alloc_thread_net();
+			s->rdbuf[0] = ra;
+			s->rdbuf[1] = ps->read_b();
+			s->mem += bt2g_alloc_thread_net() - m1;
+		}
 		s->msink = &ps->msink();
 		s->conn = e->conn;
 		s->pc = P_START;

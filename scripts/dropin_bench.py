@@ -3,7 +3,7 @@
 
 The stock reference server (oracle/_ref/bowtie2-align-server-s, CPU, -p <usable
 cores>) and the same server with its seams bound to the MI355X engines
-(oracle/_ref/bowtie2-align-server-gpu, integration/bt2g_seams.cpp, -p <many>
+(integration/bin/bowtie2-align-server-gpu, integration/bt2g_seams.cpp, -p <many>
 workers feeding the batching dispatcher) align the same reads against the same
 index, each driven by k concurrent reference clients with <= 10 000 reads per
 connection.  Prints one JSON line: both rates, the SAM comparison, the engine
@@ -45,7 +45,7 @@ def main():
     ap.add_argument("--dropin-args", default="",
                     help="extra server options for the drop-in only, one string (throughput knobs that do not "
                          "change alignments, e.g. --dropin-args='--reads-per-batch 4')")
-    ap.add_argument("--dropin-binary", default="", help="default oracle/_ref/bowtie2-align-server-gpu "
+    ap.add_argument("--dropin-binary", default="", help="default integration/bin/bowtie2-align-server-gpu "
                                                        "(-stub: the binding over the CPU stand-in)")
     ap.add_argument("--dropin-prefix", default="", help="a launcher before the drop-in's command line, one string "
                     "(e.g. 'rocprofv3 --kernel-trace --stats -d DIR --'; the server gets BT2G_EXIT_CLEAN=1)")
@@ -82,7 +82,7 @@ def main():
            "k": a.k, "host": cpus}
     sams = {}
     runs = [] if a.skip_stock else [("stock", rs.SERVER, threads)]
-    runs.append(("dropin", a.dropin_binary or os.path.join(rs.REF_DIR, "bowtie2-align-server-gpu"), a.gpu_workers))
+    runs.append(("dropin", a.dropin_binary or os.path.join(os.path.dirname(rs.HERE), "integration", "bin", "bowtie2-align-server-gpu"), a.gpu_workers))
     for tag, binary, th in runs:
         stats = os.path.join(a.workdir, f"stats_{tag}.json")
         env = rs.dropin_env(base, stats)

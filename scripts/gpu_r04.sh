@@ -23,7 +23,7 @@ batch)
   # 3.1 Gbp hg38-like genome, 200 k reads, <= 10 k per connection, 8 connections
   for p in ${3:-32}; do
     BT2G_SAMPLE=$PWD/$O/samples_p$p.txt timeout -k 10 900 python3 -u scripts/dropin_bench.py --genome-mb 3100 --workdir /tmp/db \
-      --dropin-binary oracle/_ref/bowtie2-align-server-batch --gpu-workers $p --k ${K:-8} --warmup-chunks ${WARM:-1} --reads ${READS:-200000} --mode ${MODE:-unpaired} ${SARGS:+--args=$SARGS} $SKIP > $O/batch_p$p.json 2> $O/batch_p$p.log \
+      --dropin-binary integration/bin/bowtie2-align-server-batch --gpu-workers $p --k ${K:-8} --warmup-chunks ${WARM:-1} --reads ${READS:-200000} --mode ${MODE:-unpaired} ${SARGS:+--args=$SARGS} $SKIP > $O/batch_p$p.json 2> $O/batch_p$p.log \
       || { tail -30 $O/batch_p$p.log; tail -30 /tmp/db/server_dropin.log; exit 1; }
     cp /tmp/db/server_dropin.log $O/server_p$p.log
     SKIP=--skip-stock
@@ -34,7 +34,7 @@ ktrace)
   # exits through exit() at SIGTERM so that the trace is written)
   p=${3:-16}
   timeout -k 10 900 python3 -u scripts/dropin_bench.py --genome-mb 3100 --reads ${4:-100000} --workdir /tmp/db \
-    --dropin-binary oracle/_ref/bowtie2-align-server-batch --gpu-workers $p --skip-stock \
+    --dropin-binary integration/bin/bowtie2-align-server-batch --gpu-workers $p --skip-stock \
     --dropin-prefix "rocprofv3 --kernel-trace --stats --output-format csv -d $PWD/$O/ktrace -o run --" \
     > $O/ktrace_p$p.json 2> $O/ktrace_p$p.log || { tail -30 $O/ktrace_p$p.log; tail -30 /tmp/db/server_dropin.log; exit 1; }
   cp /tmp/db/server_dropin.log $O/server_ktrace.log

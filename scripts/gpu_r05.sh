@@ -30,7 +30,7 @@ phases)
   # the batch server's per-read logic by phase ($BT2G_PHASES) and a flat CPU profile ($BT2G_SAMPLE)
   BT2G_PHASES=1 BT2G_SAMPLE=$PWD/$O/samples.txt timeout -k 10 600 python3 -u bench.py --steps ${3:-2} --warmup 1 --chain-steps 0 \
     --stock-sample 0 $BENCH_ARGS > $O/bench.json 2> $O/bench.log || { tail -30 $O/bench.log; exit 1; }
-  cp oracle/_ref/bowtie2-align-server-batch $O/server.bin
+  cp integration/bin/bowtie2-align-server-batch $O/server.bin
   python3 -c "import json; d=json.load(open('$O/bench.json')); print(d['value'], d['server']['cpu_us_per_read'])" ;;
 drivers)
   # driver threads x slots per driver: "D:S D:S ..." ($DS)

@@ -28,7 +28,7 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--workers", type=int, default=512, help="drop-in server -p (fibers)")
     ap.add_argument("--cpu-threads", type=int, default=0, help="stock server -p (0: usable host cores)")
-    ap.add_argument("--dropin-binary", default=os.path.join(rs.REF_DIR, "bowtie2-align-server-gpu"))
+    ap.add_argument("--dropin-binary", default=os.path.join(ROOT, "integration", "bin", "bowtie2-align-server-gpu"))
     ap.add_argument("--repeat", type=int, default=1, help="connections of the whole file, one at a time")
     ap.add_argument("--workdir", default="", help="index, server logs (default: a fresh temporary directory)")
     a = ap.parse_args()

@@ -46,7 +46,7 @@ def main():
     import hashlib
     root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
     build = {}
-    for rel in ("bowtie2-server_amd/libbt2g.so", "oracle/_ref/bowtie2-align-server-batch"):
+    for rel in ("bowtie2-server_amd/libbt2g.so", "integration/bin/bowtie2-align-server-batch"):
         try:
             build[rel] = hashlib.sha256(open(os.path.join(root, rel), "rb").read()).hexdigest()
         except OSError:

@@ -11,7 +11,7 @@ connection):
     over the CPU stand-in of the ABI (the reference answers every engine call),
     which checks the driver's own logic -- the restated control flow, RNG
     order, DP table reuse across minimum scores, CPU fallbacks;
-  * GPU: oracle/_ref/bowtie2-align-server-batch on libbt2g.so.
+  * GPU: integration/bin/bowtie2-align-server-batch on libbt2g.so.
 """
 import json
 import os
@@ -29,7 +29,7 @@ import bt2_index as bi  # noqa: E402
 import synth  # noqa: E402
 from oracle import ref_server as rs  # noqa: E402
 
-SRV_BATCH = os.path.join(rs.REF_DIR, "bowtie2-align-server-batch")
+SRV_BATCH = os.path.join(ROOT, "integration", "bin", "bowtie2-align-server-batch")
 SRV_BATCH_STUB = os.path.join(rs.REF_DIR, "bowtie2-align-server-batch-stub")
 LONGREADS = os.path.join(ROOT, "tests", "golden", "longreads.fq.gz")     # example/reads/longreads.fq
 LAMBDA_PE = [os.path.join(ROOT, "tests", "golden", f"reads_{m}.fq.gz") for m in (1, 2)]  # example/reads/reads_{1,2}.fq

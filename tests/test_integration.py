@@ -5,7 +5,7 @@ times with its unchanged host code (multiseedSearchWorker, SeedResults /
 AlignmentCache, SwDriver with its RNG, AlnSinkWrap, MAPQ, SAM writer):
 
   * stock:     oracle/_ref/bowtie2-align-server-s (the reference, CPU);
-  * drop-in:   oracle/_ref/bowtie2-align-server-gpu, the same objects linked
+  * drop-in:   integration/bin/bowtie2-align-server-gpu, the same objects linked
                with integration/bt2g_seams.cpp so that exactSweep,
                oneMmSearch, searchAllSeeds, ungappedAlign, SwAligner::align and
                nextAlignment are served by libbt2g.so on the GPU (-m gpu), or
@@ -36,7 +36,7 @@ import bt2_index as bi  # noqa: E402
 import synth  # noqa: E402
 from oracle import ref_server as rs  # noqa: E402
 
-SRV_GPU = os.path.join(rs.REF_DIR, "bowtie2-align-server-gpu")
+SRV_GPU = os.path.join(ROOT, "integration", "bin", "bowtie2-align-server-gpu")
 SRV_STUB = os.path.join(rs.REF_DIR, "bowtie2-align-server-stub")
 LONGREADS = os.path.join(ROOT, "tests", "golden", "longreads.fq.gz")     # example/reads/longreads.fq
 LAMBDA_PE = [os.path.join(ROOT, "tests", "golden", f"reads_{m}.fq.gz") for m in (1, 2)]  # example/reads/reads_{1,2}.fq
