@@ -522,6 +522,7 @@ int bt2g_open_mem(const bt2g_index_mem* m, int device, bt2g_ctx** out) {
 	// the workgroup walk's LDS opt-in on this device, before the context has a
 	// stream (sw_backtrace_wg.hip)
 	sw_bt_wg_lds_init(device);
+	sw_bt_lds_init(device);
 	bt2g_ctx* c = new bt2g_ctx();
 	c->device = device;
 	int rc;

@@ -148,6 +148,7 @@ struct BtArgs {
 	bt2g_edit* edits;
 	int8_t* fates;                    // may be null
 	uint32_t* queue;                  // null: one DP per lane; else a zeroed counter: lanes take DPs from it
+	int lds_marks_only;               // LDS-resident local walk: marks in LDS, the plane read in place
 };
 // kind: 0 u8 score plane, 1 u16 score plane, 2 decision nibbles (end-to-end u8 fills)
 void launch_sw_bt(int kind, const BtArgs& a, hipStream_t st);
@@ -155,8 +156,20 @@ void launch_sw_bt(int kind, const BtArgs& a, hipStream_t st);
 // in parallel; LDS bytes it needs for this launch's geometry
 uint32_t sw_bt_wg_lds(const BtArgs& a);
 void sw_bt_wg_lds_init(int dev);          // once per device, from bt2g_open
+void sw_bt_lds_init(int dev);             // the LDS-resident local walk's opt-in, likewise
 uint32_t sw_bt_wg_lds_limit();             // on the current device
 void launch_sw_bt_wg(const BtArgs& a, uint32_t lds, hipStream_t st);
+
+// uint4s of a problem's plane an LDS-resident walk copies (sw_backtrace.hip):
+// kind 2 (decision planes) 8 B per 16-row block column; kind 1 (local u16
+// planes) 32 B per block column, then the block masks (2 B per column) that the
+// fill stores right after the plane
+__host__ __device__ inline uint32_t sw_bt_lds_plane16(const BtArgs& a, int kind) {
+	if(kind == 2) return (a.cstride >> 4) * a.pcols * 8u / 16u;
+	if(a.lds_marks_only) return 0u;
+	const uint64_t b = (uint64_t)(a.cstride >> 4) * a.pcols * 32u + (a.use_mask ? (uint64_t)a.pcols * 2u : 0u);
+	return (uint32_t)((b + 15u) / 16u);
+}
 
 // backtrace mark scratch per problem of <= rows x cols (sw_backtrace.hip):
 // reportedThrough in 8x8-cell bit tiles (2 words each) + one valid bit per

@@ -44,6 +44,9 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 #include <stdlib.h>
+#include <string.h>
+#include <atomic>
+#include <mutex>
 #include "bt2g_kernels.h"
 
 namespace {
@@ -120,17 +123,21 @@ __device__ unsigned long long g_bt_wave_t0[1u << 16], g_bt_wave_t1[1u << 16];   
 #endif
 // LOCAL: the alignment mode, compile-time (each mode's kernel keeps only its
 // own filters and moves); FLAT: the loop shape, flat for local (see below).
-// LDSRES (kind 2 only): a workgroup per problem -- its 64 lanes copy the
-// problem's decision plane into LDS and clear its reportedThrough tiles there,
-// then lane 0 walks with every plane and mark access in LDS.  A batch of a few
-// thousand DPs (the batch driver's rounds) is bound by the longest walk chain,
-// one dependent HBM load after another in the lane-per-problem kernel
-// (~3 ms per 400-DP call, r04d): LDS latency is an order of magnitude lower.
-// For big batches the lane-per-problem kernel keeps the throughput.
+// LDSRES (kind-2 end-to-end decision planes, kind-1 local u16 planes): a
+// workgroup per problem -- its 64 lanes copy the problem's plane (local: with
+// its block masks) into LDS and its mark tiles (reportedThrough; local also the
+// FILT_DOMINATED squares) live there too, then lane 0 walks with every plane and
+// mark access in LDS.  A batch of a few thousand DPs (the batch driver's rounds)
+// is bound by the longest walk chain, one dependent HBM load after another in
+// the lane-per-problem kernel (~3 ms per 400-DP call, r04d; local: ~55 walks and
+// ~1 200 candidates per DP one after another): LDS latency is an order of
+// magnitude lower.  For big batches the lane-per-problem kernel keeps the
+// throughput.
 template <int KIND, bool LOCAL, bool FLAT = LOCAL, bool LDSRES = false>
 __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(BT2G_BT_WAVES)))
 k_sw_bt(BtArgs A) {
-	static_assert(!LDSRES || (KIND == 2 && !LOCAL), "LDS-resident walks: kind-2 planes only");
+	static_assert(!LDSRES || (KIND == 2 && !LOCAL) || (KIND == 1 && LOCAL),
+	              "LDS-resident walks: kind-2 end-to-end or kind-1 local planes");
 	const uint32_t p = LDSRES ? blockIdx.x : blockIdx.x * 64u + threadIdx.x;
 	if(p >= A.nprob) return;
 #ifdef BT2G_BT_PROF
@@ -249,18 +256,33 @@ k_sw_bt(BtArgs A) {
 	// (Valid bits in LDS instead: measured slower.)
 	uint32_t* marks = A.marks + (size_t)p * A.mslot;
 	const uint32_t tcols = A.rwords, trows = A.rrows, vw = (tcols + 31u) / 32u;
+	const bt2g_sw_cand* lcl = nullptr;      // (LDSRES local: the candidate list's copy in LDS)
 	if constexpr(LDSRES) {
-		// the plane's 16-row blocks (8 B per block column) and the marks, in LDS
+		// the plane's 16-row blocks (kind 2: 8 B per block column; kind 1: 32 B, then
+		// the columns' block masks) and the marks, in LDS (layout: sw_bt_lds_bytes)
 		HIP_DYNAMIC_SHARED(uint4, s_res)
-		const uint32_t n16 = (A.cstride >> 4) * A.pcols * 8u / 16u;
+		const uint32_t n16 = sw_bt_lds_plane16(A, KIND);
 		const uint4* src = (const uint4*)slot;
 		for(uint32_t i = threadIdx.x; i < n16; i += 64u) s_res[i] = src[i];
 		uint32_t* lm = (uint32_t*)(s_res + n16);
 		for(uint32_t i = threadIdx.x; i < trows * vw; i += 64u) lm[(size_t)trows * tcols * 2u + i] = 0u;
+		if(KIND == 1) {
+			// local: the sorted candidate list too (~1 200 per DP, most of them only
+			// tested against the marks: streamed from HBM one at a time by the walker,
+			// each a dependent round trip), after the whole mark slot
+			const uint32_t nc = (uint32_t)R.ncand < A.cap ? (uint32_t)R.ncand : A.cap;
+			uint32_t* lc = lm + A.mslot;
+			const uint32_t* gc = (const uint32_t*)(A.cands + (size_t)p * A.cap);
+			for(uint32_t i = threadIdx.x; i < 3u * nc; i += 64u) lc[i] = gc[i];
+			lcl = (const bt2g_sw_cand*)lc;
+		}
 		__syncthreads();
 		if(threadIdx.x != 0) return;
-		slot = (const uint8_t*)s_res;
-		pl.base = slot;
+		if(n16) {
+			slot = (const uint8_t*)s_res;
+			pl.base = slot;
+			if(KIND == 1 && A.use_mask) pl.mask = (const uint16_t*)(slot + (size_t)A.cstride * A.pcols * 2u);
+		}
 		marks = lm;
 	}
 	uint32_t* valid = marks + (size_t)trows * tcols * 2u;
@@ -403,7 +425,7 @@ k_sw_bt(BtArgs A) {
 	constexpr uint32_t BT_DCH = 2u * BT_CHUNK;
 	uint32_t db = 0xffffffffu, dc0 = 0;
 	const uint32_t ncand = (uint32_t)R.ncand < A.cap ? (uint32_t)R.ncand : A.cap;
-	const bt2g_sw_cand* cl = A.cands + (size_t)p * A.cap;
+	const bt2g_sw_cand* cl = lcl ? lcl : A.cands + (size_t)p * A.cap;
 	// local mode, FILT_DOMINATED (aligner_sw.cpp nextAlignment): a candidate
 	// within SQ rows and SQ columns of one already walked is skipped.  Each
 	// walked candidate sets its (2SQ+1)^2 square in a second set of 8x8 bit
@@ -872,13 +894,48 @@ extern "C" int bt2g_bt_prof_read(unsigned long long* out) {
 }
 #endif
 
-// LDS bytes of an LDS-resident walk (k_sw_bt<2, false, false, true>): the
-// plane's blocks and the reportedThrough tiles with their valid words
-static uint32_t bt_lds_bytes(const BtArgs& a) {
-	const uint64_t plane = (uint64_t)(a.cstride >> 4) * a.pcols * 8u;
-	const uint64_t marks = ((uint64_t)a.rrows * a.rwords * 2u + (uint64_t)a.rrows * ((a.rwords + 31u) / 32u)) * 4u;
-	const uint64_t n = plane + marks;
+// LDS bytes of an LDS-resident walk (k_sw_bt<., ., ., true>): the plane's
+// blocks (sw_bt_lds_plane16: local with the block masks) and the problem's
+// whole mark slot (reportedThrough tiles with their valid words; local also the
+// FILT_DOMINATED tiles, A.mdom words in)
+static uint32_t bt_lds_bytes(const BtArgs& a, int kind) {
+	const uint64_t plane = (uint64_t)sw_bt_lds_plane16(a, kind) * 16u;
+	const uint64_t marks = (kind == 1 ? a.mslot
+	                                  : (uint64_t)a.rrows * a.rwords * 2u + (uint64_t)a.rrows * ((a.rwords + 31u) / 32u)) * 4u;
+	const uint64_t cands = kind == 1 ? (uint64_t)a.cap * sizeof(bt2g_sw_cand) : 0u;   // (local: the candidate list)
+	const uint64_t n = plane + marks + cands;
 	return n > 0xffffffffull ? 0xffffffffu : (uint32_t)n;
+}
+
+// The dynamic LDS the LDS-resident local walk may take on a device: its opt-in
+// (up to the CU's 160 KiB less the kernel's static LDS, the lanes' window cache),
+// made per device at context open (bt2g_open_mem), as for the workgroup walk.
+static std::atomic<uint32_t> g_loc_lds_lim[64];
+static std::mutex g_loc_lds_mu;
+static constexpr uint32_t BT_STATIC_LDS = 64u * BT_LDSW * 4u;
+
+void sw_bt_lds_init(int dev) {
+	if(dev < 0 || dev >= 64) return;
+	std::lock_guard<std::mutex> lk(g_loc_lds_mu);
+	if(g_loc_lds_lim[dev].load()) return;
+	uint32_t lim = 65536u - BT_STATIC_LDS;
+	int v = 0;
+	if(hipDeviceGetAttribute(&v, hipDeviceAttributeSharedMemPerBlockOptin, dev) == hipSuccess && v > 65536 &&
+	   hipFuncSetAttribute((const void*)k_sw_bt<1, true, true, true>, hipFuncAttributeMaxDynamicSharedMemorySize,
+	                       v - (int)BT_STATIC_LDS) == hipSuccess)
+		lim = (uint32_t)v - BT_STATIC_LDS;
+	else
+		(void)hipGetLastError();
+	g_loc_lds_lim[dev].store(lim);
+}
+
+static uint32_t bt_loc_lds_limit() {
+	const char* e = getenv("BT2G_BT_WG_LDS");           // (0: no opt-in, as for the workgroup walk)
+	if(e && *e == '0') return 65536u - BT_STATIC_LDS;
+	int dev = 0;
+	if(hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return 65536u - BT_STATIC_LDS;
+	const uint32_t v = g_loc_lds_lim[dev].load();
+	return v ? v : 65536u - BT_STATIC_LDS;
 }
 
 // batches up to $BT2G_BT_LDS_MAX problems (default 65536; 0: never) walk
@@ -905,10 +962,26 @@ void launch_sw_bt(int kind, const BtArgs& a, hipStream_t st) {
 				return;
 			}
 		}
-		const uint32_t lds = bt_lds_bytes(a);
-		if(lds <= 65536u) {
+		const uint32_t lds = bt_lds_bytes(a, 2);
+		if(lds <= 65536u - BT_STATIC_LDS) {
 			hipLaunchKernelGGL((k_sw_bt<2, false, false, true>), dim3(a.nprob), dim3(64), lds, st, a);
 			return;
+		}
+	}
+	if(kind == 1 && a.local && !a.queue && a.nprob <= bt_lds_max()) {
+		// $BT2G_BT_LOC_LDS: 0 local walks stay lane-per-problem; "plane" the u16 plane
+		// in LDS too (one workgroup per CU at ~80 KB); default: the marks only, the
+		// plane read in place (just written by the fill: mostly cache hits), so a CU
+		// holds many walkers
+		const char* e = getenv("BT2G_BT_LOC_LDS");
+		if(!(e && *e == '0')) {
+			BtArgs b = a;
+			b.lds_marks_only = !(e && !strcmp(e, "plane"));
+			const uint32_t lds = bt_lds_bytes(b, 1);
+			if(lds <= bt_loc_lds_limit()) {
+				hipLaunchKernelGGL((k_sw_bt<1, true, true, true>), dim3(b.nprob), dim3(64), lds, st, b);
+				return;
+			}
 		}
 	}
 	const dim3 grid((a.nprob + 63u) / 64u), block(64);

@@ -54,6 +54,23 @@ prof)
   python3 scripts/pmc_summary.py $O/pmc_FETCH_SIZE $O/pmc_WRITE_SIZE $O/server_pmc.json
   find $O -name "*.csv" -size +40M -delete
   head -25 $O/run_kernel_stats.csv | cut -d, -f1-6 ;;
+mode)
+  # one bench line of another mode ($MODE: local | paired; $PRESET) with the stock server on 200 k
+  timeout -k 10 900 python3 -u bench.py --mode ${MODE:-local} --preset ${PRESET:-sensitive} --steps ${3:-1} --warmup 1 \
+    --chain-steps 0 --stock-sample 200000 $BENCH_ARGS > $O/bench_${MODE:-local}.json 2> $O/bench_${MODE:-local}.log || { tail -30 $O/bench_${MODE:-local}.log; exit 1; }
+  python3 -c "
+import json; d=json.load(open('$O/bench_${MODE:-local}.json')); s=d['server']
+print(round(d['value']), d['vs_cpu_baseline'], d['sam_parity'], s['cpu_us_per_read'], s['server_rss_gb_per_pass'])
+for k, v in d['server_kernels'].items(): print(k, v['kernel'][:40], v['launches'], round(v['ms_per_launch'], 3), v.get('frac'))" ;;
+localab)
+  # the local walk variants through the batch server ($BT2G_BT_LOC_LDS: marks | plane | 0)
+  timeout -k 10 300 python -u -m pytest tests/test_gpu_bt.py -x -q --timeout 200 --timeout-method thread > $O/bt_tests.log 2>&1 || { tail -30 $O/bt_tests.log; exit 1; }
+  tail -1 $O/bt_tests.log
+  for v in ${VARS:-marks plane}; do
+    BT2G_BT_LOC_LDS=$v timeout -k 10 500 python3 -u bench.py --mode local --steps 1 --warmup 1 --chain-steps 0 --stock-sample 0 $BENCH_ARGS \
+      > $O/bench_$v.json 2> $O/bench_$v.log || { tail -30 $O/bench_$v.log; exit 1; }
+    python3 -c "import json; d=json.load(open('$O/bench_$v.json')); k=d['server_kernels']; print('$v', round(d['value']), round(k['sw_dp:5']['ms_per_launch'],2), round(k['sw_dp:7']['ms_per_launch'],2), round(k['exact_sweep:2']['ms_per_launch'],2))"
+  done ;;
 bench)
   T0=$(date +%s); timeout -k 10 1100 python3 -u bench.py --gpus 1 --steps 20 --warmup 5 > $O/bench.json 2> $O/bench.log || { tail -30 $O/bench.log; exit 1; }; echo "wall $(( $(date +%s) - T0 )) s"
   tail -25 $O/bench.log | grep -v "^\s*$"; cut -c1-1500 $O/bench.json ;;

@@ -277,3 +277,51 @@ def test_bt_lds_resident_equals_lane_kernel(eng, monkeypatch, shape, variant):
         k = 64
         ea, ee, ef = _oracle_expect(Oracle(), gen, codes[:k], quals[:k], probs[:k], rects[:k], False)
         check_against(naln[:k], alns[:k], edits[:k], fates[:k], res[:k], None, ea, ee, ef, "mate")
+
+
+@pytest.mark.parametrize("lds", ["marks", "plane", "plane64k"])
+def test_bt_local_lds_resident_equals_lane_kernel(eng, monkeypatch, lds):
+    """Local mode: batches up to BT2G_BT_LDS_MAX walk LDS-resident, one walker per
+    workgroup: both mark tile sets in LDS and the u16 plane read in place (default),
+    or the plane and its block masks in LDS too (BT2G_BT_LOC_LDS=plane, past 64 KiB
+    with the device's opt-in, else the lane kernel) -- the same alignments, edits and
+    candidate fates as the lane-per-problem walk (BT2G_BT_LDS_MAX=0), and as the
+    oracle on a sample."""
+    from oracle.oracle import Oracle
+    gen = get_index("lambda").ref_codes[0]
+    n = 400
+    codes, quals, lens, probs, rects = _synth_problems(gen, n, 61, minsc=60, sub=0.01)
+    outs = []
+    for lim in ("65536", "0"):
+        monkeypatch.setenv("BT2G_BT_LDS_MAX", lim)
+        if lds.startswith("plane"):
+            monkeypatch.setenv("BT2G_BT_LOC_LDS", "plane")     # (default: the marks only)
+        if lds == "plane64k":
+            monkeypatch.setenv("BT2G_BT_WG_LDS", "0")
+        outs.append(eng.sw_align_bt(codes, quals, lens, probs, rects=rects, local=True, cap=4096, maxaln=64,
+                                    maxedit=512))
+        monkeypatch.delenv("BT2G_BT_WG_LDS", raising=False)
+        monkeypatch.delenv("BT2G_BT_LOC_LDS", raising=False)
+    a, b = outs
+    for x, y in zip(a[:3], b[:3]):
+        if x.dtype.names:
+            for f in x.dtype.names:
+                assert np.array_equal(x[f], y[f]), f
+        else:
+            assert np.array_equal(x, y)
+    naln = a[2]
+    for p in range(n):
+        k = max(int(naln[p]), 0)
+        for f in a[3].dtype.names:
+            assert np.array_equal(a[3][f][p, :k], b[3][f][p, :k]), (p, f)
+        for j in range(k):
+            ne = min(int(a[3]["nedit"][p, j]), a[4].shape[2])
+            for f in ("pos", "type", "chr", "qchr"):
+                assert np.array_equal(a[4][f][p, j, :ne], b[4][f][p, j, :ne]), (p, j, f)
+        nc = min(int(a[0]["ncand"][p]), a[5].shape[1])
+        assert np.array_equal(a[5][p, :nc], b[5][p, :nc]), p
+    assert (naln > 0).sum() > 0.6 * n
+    res, cands, naln, alns, edits, fates = a
+    k = 48
+    ea, ee, ef = _oracle_expect(Oracle(), gen, codes[:k], quals[:k], probs[:k], rects[:k], True)
+    check_against(naln[:k], alns[:k], edits[:k], fates[:k], res[:k], None, ea, ee, ef, "local_lds")
