@@ -646,13 +646,16 @@ def dominant_kernel(kern):
 SERVER_BASE_GB, SLOT_MB, BENCH_PROC_GB = 12.0, 2.8, 10.0
 
 
-def slots_per_driver(world, drivers, rank_mem_gb=0.0):
+def slots_per_driver(world, drivers, rank_mem_gb=0.0, mode="ee"):
     """Reads in flight per driver thread ($BT2G_BATCH_SLOTS) within a per-rank
-    host-memory budget: one GPU keeps the server's default (1 024); with several
-    ranks per node every rank's server and bench process must fit
-    rank_mem_gb (default 56 GB: 8 ranks in ~450 GB of the node's host memory)."""
+    host-memory budget: one GPU keeps the server's default (1 024; --local 2 048:
+    its rounds wait on ~12 ms DP calls -- the local walks, one per workgroup -- with
+    the drivers' CPU mostly idle, so reads in flight are its throughput: r05n 45 k
+    -> 65 k aligned reads/s at 64 -> 108 GB of host memory); with several ranks
+    per node every rank's server and bench process must fit rank_mem_gb (default
+    56 GB: 8 ranks in ~450 GB of the node's host memory)."""
     if world <= 1 and not rank_mem_gb:
-        return 1024
+        return 2048 if mode == "local" else 1024
     budget = rank_mem_gb or 56.0
     per = int((budget - BENCH_PROC_GB - SERVER_BASE_GB) * 1024 / (drivers * SLOT_MB))
     return max(128, min(1024, per // 64 * 64))
@@ -686,7 +689,7 @@ def schedule_run(args, rank, world, local, base, reads_np, quals_np, workdir, bi
     env = rs.dropin_env(base, stats, device=local)
     env["BT2G_KPROF"] = "1"
     slots = int(os.environ.get("BT2G_BATCH_SLOTS") or
-                slots_per_driver(world, args.drivers, getattr(args, "rank_mem_gb", 0.0)))
+                slots_per_driver(world, args.drivers, getattr(args, "rank_mem_gb", 0.0), args.mode))
     env["BT2G_BATCH_SLOTS"] = str(slots)
     # $BT2G_BENCH_SERVER_PREFIX: a profiler in front of the batch server's command line
     # (e.g. "rocprofv3 --kernel-trace --stats -d DIR -o run --"); the server then exits
@@ -712,10 +715,11 @@ def schedule_run(args, rank, world, local, base, reads_np, quals_np, workdir, bi
             torch.cuda.synchronize()
         rss = [srv.last_rss_gb]                 # after the warmup, then after every timed pass
         t0 = time.perf_counter()
-        aligned, outs, cpu_s = 0, None, 0.0
+        aligned, outs, cpu_s, client_s = 0, None, 0.0, 0.0
         for i in range(args.steps):
             _, outs = srv.run(chunks, k=args.clients)
             cpu_s += srv.last_cpu_s
+            client_s += srv.last_client_cpu_s
             rss.append(srv.last_rss_gb)
             aligned += count_aligned(outs, paired)
             if i + 1 < args.steps:
@@ -738,7 +742,7 @@ def schedule_run(args, rank, world, local, base, reads_np, quals_np, workdir, bi
                 pass
         time.sleep(0.1)
     return {"elapsed": elapsed, "aligned": aligned, "outs": outs, "chunks": chunks, "stats": st, "slots_per_driver": slots,
-            "server_cpu_s": cpu_s, "server_threads_cpu": threads_cpu, "server_rss_gb": rss[-1],
+            "server_cpu_s": cpu_s, "client_cpu_s": client_s, "server_threads_cpu": threads_cpu, "server_rss_gb": rss[-1],
             "server_rss_gb_per_pass": rss, "binary": binary_id(binary), "smaps_top": smaps}
 
 
@@ -770,12 +774,14 @@ def stock_baseline(args, base, chunks, batch_outs, workdir):
             srv.run(sample[:min(args.warmup_chunks, m)] if args.warmup_chunks > 0 else sample, k=args.clients)
         dt, outs = srv.run(sample, k=args.clients)
         cpu_s = srv.last_cpu_s
+        client_s = srv.last_client_cpu_s
     a, b = rs.sorted_records(outs), rs.sorted_records(batch_outs[:m])
     differ = sum(1 for x, y in zip(a, b) if x != y) + abs(len(a) - len(b))
     nreads = min(args.reads, m * rs.CHUNK)
     unit = "read pairs/s" if paired else "reads/s"
     return {"value": count_aligned(outs, paired) / dt, "unit": "aligned " + unit, "cores": threads,
             "kind": "reference", "host": host, "reads_per_s": nreads / dt, "seconds": dt, "server_cpu_s": cpu_s,
+            "client_cpu_s": client_s,
             "sample": f"the stock reference server (bowtie2-align-server-s built from the reference's sources, "
                       f"-p {threads} = the usable cores of this host, {host['model']}) on the first {nreads} "
                       f"{'pairs' if paired else 'reads'} of the batch, <= 10 000 per client connection, "
@@ -1256,6 +1262,10 @@ def main():
                        "server_rss_gb": sched["server_rss_gb"], "server_rss_gb_per_pass": sched["server_rss_gb_per_pass"],
                        "smaps_top": sched["smaps_top"],
                        "cpu_us_per_read": sched["server_cpu_s"] / max(1, args.reads * args.steps) * 1e6,
+                       # the reference's client processes (32 at a time, single-threaded each:
+                       # read parsing, the wire, SAM receipt) on the same CPU quota
+                       "client_cpu_s": sched["client_cpu_s"],
+                       "client_cpu_us_per_read": sched["client_cpu_s"] / max(1, args.reads * args.steps) * 1e6,
                        "calls": {k: st.get(k) for k in ("exact_sweep", "one_mm", "seed_search", "extend",
                                                         "get_offset", "ungapped", "sw_dp")},
                        "threads_cpu": sched["server_threads_cpu"]},

@@ -922,6 +922,8 @@ void sw_bt_lds_init(int dev) {
 	int v = 0;
 	if(hipDeviceGetAttribute(&v, hipDeviceAttributeSharedMemPerBlockOptin, dev) == hipSuccess && v > 65536 &&
 	   hipFuncSetAttribute((const void*)k_sw_bt<1, true, true, true>, hipFuncAttributeMaxDynamicSharedMemorySize,
+	                       v - (int)BT_STATIC_LDS) == hipSuccess &&
+	   hipFuncSetAttribute((const void*)k_sw_bt<1, true, false, true>, hipFuncAttributeMaxDynamicSharedMemorySize,
 	                       v - (int)BT_STATIC_LDS) == hipSuccess)
 		lim = (uint32_t)v - BT_STATIC_LDS;
 	else
@@ -979,7 +981,12 @@ void launch_sw_bt(int kind, const BtArgs& a, hipStream_t st) {
 			b.lds_marks_only = !(e && !strcmp(e, "plane"));
 			const uint32_t lds = bt_lds_bytes(b, 1);
 			if(lds <= bt_loc_lds_limit()) {
-				hipLaunchKernelGGL((k_sw_bt<1, true, true, true>), dim3(b.nprob), dim3(64), lds, st, b);
+				// (one walker per workgroup: no lanes to diverge, so a walk runs to its
+				// end in the inner loop -- the flat loop's one body per step is the
+				// union of the filter and the walk; $BT2G_BT_LOC_FLAT=1 keeps it)
+				const char* fl = getenv("BT2G_BT_LOC_FLAT");
+				if(fl && *fl == '1') hipLaunchKernelGGL((k_sw_bt<1, true, true, true>), dim3(b.nprob), dim3(64), lds, st, b);
+				else hipLaunchKernelGGL((k_sw_bt<1, true, false, true>), dim3(b.nprob), dim3(64), lds, st, b);
 				return;
 			}
 		}

@@ -42,6 +42,36 @@ __global__ void __launch_bounds__(256) k_chain(const u32x4* __restrict__ t, uint
 	}
 	out[gid] = acc;
 }
+// The same chain with the wave's 64 sides of a step loaded cooperatively and
+// staged in LDS ("coalesced occ-table gathers with LDS-staged rank blocks"):
+// in round k (0..3) lane i loads quarter i&3 of the side of lane 16k + i/4, so
+// one dwordx4 instruction covers 16 whole 64-B lines (the per-lane form: 64
+// lines, a quarter each, 4 instructions per side); the lanes then read their
+// own side back from LDS.
+__global__ void __launch_bounds__(256) k_chain_lds(const u32x4* __restrict__ t, uint32_t nside, uint32_t iters,
+                                                   uint32_t* out) {
+	__shared__ u32x4 st[4][64][4];                // [wave of the block][lane][quarter]
+	const uint32_t gid = blockIdx.x * blockDim.x + threadIdx.x, lane = threadIdx.x & 63u, wv = threadIdx.x >> 6;
+	uint32_t s = hash(gid) % nside, acc = 0;
+	for(uint32_t it = 0; it < iters; it++) {
+		u32x4 q[4];
+#pragma unroll
+		for(int k = 0; k < 4; k++) {
+			const uint32_t owner = 16u * k + (lane >> 2);
+			const uint32_t so = __shfl(s, owner);
+			q[k] = t[(size_t)so * 4 + (lane & 3u)];
+		}
+#pragma unroll
+		for(int k = 0; k < 4; k++) st[wv][16u * k + (lane >> 2)][lane & 3u] = q[k];
+		__builtin_amdgcn_wave_barrier();
+		__builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+		const u32x4 a = st[wv][lane][0], b = st[wv][lane][1], c = st[wv][lane][2], d = st[wv][lane][3];
+		acc += a.x ^ b.y ^ c.z ^ d.w;
+		__builtin_amdgcn_wave_barrier();
+		s = hash(acc ^ (gid * 0x9e3779b9u) ^ it) % nside;
+	}
+	out[gid] = acc;
+}
 __global__ void k_fill(uint32_t* t, size_t n) {
 	for(size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < n; i += (size_t)gridDim.x * blockDim.x)
 		t[i] = hash((uint32_t)i * 2654435761u + 12345u);
@@ -81,6 +111,8 @@ int main() {
 		run(nm, [&] { hipLaunchKernelGGL(k_indep<4>, dim3(blocks), dim3(256), 0, 0, t, nside, iters, o); }, g * 4);
 		snprintf(nm, sizeof nm, "chain     %2d blk/CU", blocksPerCU);
 		run(nm, [&] { hipLaunchKernelGGL(k_chain, dim3(blocks), dim3(256), 0, 0, t, nside, iters, o); }, g);
+		snprintf(nm, sizeof nm, "chain LDS-staged %2d blk/CU", blocksPerCU);
+		run(nm, [&] { hipLaunchKernelGGL(k_chain_lds, dim3(blocks), dim3(256), 0, 0, t, nside, iters, o); }, g);
 	}
 	return 0;
 }

@@ -279,7 +279,7 @@ def test_bt_lds_resident_equals_lane_kernel(eng, monkeypatch, shape, variant):
         check_against(naln[:k], alns[:k], edits[:k], fates[:k], res[:k], None, ea, ee, ef, "mate")
 
 
-@pytest.mark.parametrize("lds", ["marks", "plane", "plane64k"])
+@pytest.mark.parametrize("lds", ["marks", "marks_flat", "plane", "plane64k"])
 def test_bt_local_lds_resident_equals_lane_kernel(eng, monkeypatch, lds):
     """Local mode: batches up to BT2G_BT_LDS_MAX walk LDS-resident, one walker per
     workgroup: both mark tile sets in LDS and the u16 plane read in place (default),
@@ -298,10 +298,13 @@ def test_bt_local_lds_resident_equals_lane_kernel(eng, monkeypatch, lds):
             monkeypatch.setenv("BT2G_BT_LOC_LDS", "plane")     # (default: the marks only)
         if lds == "plane64k":
             monkeypatch.setenv("BT2G_BT_WG_LDS", "0")
+        if lds == "marks_flat":
+            monkeypatch.setenv("BT2G_BT_LOC_FLAT", "1")
         outs.append(eng.sw_align_bt(codes, quals, lens, probs, rects=rects, local=True, cap=4096, maxaln=64,
                                     maxedit=512))
         monkeypatch.delenv("BT2G_BT_WG_LDS", raising=False)
         monkeypatch.delenv("BT2G_BT_LOC_LDS", raising=False)
+        monkeypatch.delenv("BT2G_BT_LOC_FLAT", raising=False)
     a, b = outs
     for x, y in zip(a[:3], b[:3]):
         if x.dtype.names:
