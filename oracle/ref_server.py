@@ -167,6 +167,8 @@ class Server:
                     errs.append((i, r.returncode, r.stderr[-2000:]))
                 outs[i] = r.stdout
 
+        import resource
+        ru0 = resource.getrusage(resource.RUSAGE_CHILDREN)
         c0 = self.cpu_seconds()
         h0 = host_cpu_seconds()
         th0 = cgroup_throttled_seconds()
@@ -178,6 +180,9 @@ class Server:
             t.join()
         dt = time.perf_counter() - t0
         self.last_cpu_s = self.cpu_seconds() - c0        # server CPU time (all threads) over the run
+        ru1 = resource.getrusage(resource.RUSAGE_CHILDREN)
+        # the clients' CPU time (the reference's client processes of this run, reaped)
+        self.last_client_cpu_s = (ru1.ru_utime + ru1.ru_stime) - (ru0.ru_utime + ru0.ru_stime)
         self.last_host_cpu_s = host_cpu_seconds() - h0   # every process of the host (clients included)
         self.last_throttled_s = cgroup_throttled_seconds() - th0
         self.last_rss_gb = self.rss_gb()

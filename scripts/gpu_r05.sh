@@ -71,6 +71,16 @@ localab)
       > $O/bench_$v.json 2> $O/bench_$v.log || { tail -30 $O/bench_$v.log; exit 1; }
     python3 -c "import json; d=json.load(open('$O/bench_$v.json')); k=d['server_kernels']; print('$v', round(d['value']), round(k['sw_dp:5']['ms_per_launch'],2), round(k['sw_dp:7']['ms_per_launch'],2), round(k['exact_sweep:2']['ms_per_launch'],2))"
   done ;;
+envab)
+  # bench.py --mode $MODE under several server environments: ENVS="A=1 B=2;A=3" (';' between settings)
+  IFS=';' read -ra SETS <<< "${ENVS:-BT2G_DP_WORKERS=6}"
+  i=0
+  for set in "${SETS[@]}"; do
+    i=$((i+1))
+    env $set timeout -k 10 500 python3 -u bench.py --mode ${MODE:-local} --steps ${3:-1} --warmup 1 --chain-steps 0 --stock-sample 0 $BENCH_ARGS \
+      > $O/bench_$i.json 2> $O/bench_$i.log || { tail -30 $O/bench_$i.log; exit 1; }
+    python3 -c "import json; d=json.load(open('$O/bench_$i.json')); s=d['server']; k=d['server_kernels']; print('$set', round(d['value']), round(s['cpu_us_per_read'],1), s['server_rss_gb_per_pass'][-1], round(k['sw_dp:7']['ms_per_launch'],2), k['sw_dp:7']['launches'])"
+  done ;;
 bench)
   T0=$(date +%s); timeout -k 10 1100 python3 -u bench.py --gpus 1 --steps 20 --warmup 5 > $O/bench.json 2> $O/bench.log || { tail -30 $O/bench.log; exit 1; }; echo "wall $(( $(date +%s) - T0 )) s"
   tail -25 $O/bench.log | grep -v "^\s*$"; cut -c1-1500 $O/bench.json ;;
