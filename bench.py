@@ -674,8 +674,9 @@ def schedule_run(args, rank, world, local, base, reads_np, quals_np, workdir, bi
     engine statistics."""
     import torch
     import torch.distributed as dist
-    from oracle import ref_server as rs
+    import serve as rs
     binary = binary or BATCH_SERVER
+    client = client_binary(args)
     if not os.path.exists(binary):
         raise RuntimeError(f"{binary} is not built (python -c 'import __graft_entry__ as g; g.build()')")
     gpu = torch.cuda.is_available()
@@ -708,7 +709,7 @@ def schedule_run(args, rank, world, local, base, reads_np, quals_np, workdir, bi
                    env=env, log_path=os.path.join(workdir, "server.log"), prefix=prefix) as srv:
         log(f"[rank {rank}] batch server ready in {srv.load_s:.1f}s (-p {args.drivers})")
         for _ in range(args.warmup):
-            srv.run(chunks[:args.warmup_chunks] if args.warmup_chunks > 0 else chunks, k=args.clients)
+            srv.run(chunks[:args.warmup_chunks] if args.warmup_chunks > 0 else chunks, k=args.clients, client=client)
         if multi:
             dist.barrier()
         if gpu:
@@ -717,7 +718,7 @@ def schedule_run(args, rank, world, local, base, reads_np, quals_np, workdir, bi
         t0 = time.perf_counter()
         aligned, outs, cpu_s, client_s = 0, None, 0.0, 0.0
         for i in range(args.steps):
-            _, outs = srv.run(chunks, k=args.clients)
+            _, outs = srv.run(chunks, k=args.clients, client=client)
             cpu_s += srv.last_cpu_s
             client_s += srv.last_client_cpu_s
             rss.append(srv.last_rss_gb)
@@ -743,7 +744,22 @@ def schedule_run(args, rank, world, local, base, reads_np, quals_np, workdir, bi
         time.sleep(0.1)
     return {"elapsed": elapsed, "aligned": aligned, "outs": outs, "chunks": chunks, "stats": st, "slots_per_driver": slots,
             "server_cpu_s": cpu_s, "client_cpu_s": client_s, "server_threads_cpu": threads_cpu, "server_rss_gb": rss[-1],
-            "server_rss_gb_per_pass": rss, "binary": binary_id(binary), "smaps_top": smaps}
+            "server_rss_gb_per_pass": rss, "binary": binary_id(binary), "client": binary_id(client),
+            "smaps_top": smaps}
+
+
+def client_binary(args):
+    """The client that sends the reads: this repository's multi-connection client
+    (integration/bin/bt2g-client, row (f)-4: one process, args.clients
+    connections, SAM identical to the reference client's, tests/test_client.py)
+    or, with --client reference, one reference client process per chunk
+    (oracle/_ref/bowtie2-align-l, A/B runs)."""
+    if getattr(args, "client", "native") == "reference":
+        return os.path.join(ROOT, "oracle", "_ref", "bowtie2-align-l")
+    import serve
+    if not os.path.exists(serve.NATIVE_CLIENT):
+        raise RuntimeError(f"{serve.NATIVE_CLIENT} is not built (make -C integration client)")
+    return serve.NATIVE_CLIENT
 
 
 def binary_id(path):
@@ -1103,6 +1119,9 @@ def main():
     ap.add_argument("--reads", type=int, default=1_000_000, help="reads (paired: read pairs) per GPU per step")
     ap.add_argument("--drivers", type=int, default=16, help="batch server driver threads (-p)")
     ap.add_argument("--clients", type=int, default=32, help="concurrent client connections (both servers)")
+    ap.add_argument("--client", choices=("native", "reference"), default="native",
+                    help="client of the timed passes: native = integration/bin/bt2g-client (row (f)-4, SAM "
+                         "identical to the reference client's); reference = one bowtie2-align-l per chunk")
     ap.add_argument("--rank-mem-gb", type=float, default=0.0,
                     help="host-memory budget per rank (batch server + this process) that sizes the server's "
                          "read slots (0: 1 024 slots per driver on one GPU, 56 GB per rank with several)")
@@ -1262,8 +1281,9 @@ def main():
                        "server_rss_gb": sched["server_rss_gb"], "server_rss_gb_per_pass": sched["server_rss_gb_per_pass"],
                        "smaps_top": sched["smaps_top"],
                        "cpu_us_per_read": sched["server_cpu_s"] / max(1, args.reads * args.steps) * 1e6,
-                       # the reference's client processes (32 at a time, single-threaded each:
-                       # read parsing, the wire, SAM receipt) on the same CPU quota
+                       # the client side (read parsing, the wire, SAM receipt) on the same CPU
+                       # quota: bt2g-client, or the reference's client processes (--client reference)
+                       "client": sched["client"],
                        "client_cpu_s": sched["client_cpu_s"],
                        "client_cpu_us_per_read": sched["client_cpu_s"] / max(1, args.reads * args.steps) * 1e6,
                        "calls": {k: st.get(k) for k in ("exact_sweep", "one_mm", "seed_search", "extend",
@@ -1290,10 +1310,12 @@ def schedule_workload(args):
             mode = "--local --very-sensitive-local" if args.mode == "local" else "--end-to-end --very-sensitive"
         what = f"{args.reads} synthetic {args.read_len} bp unpaired reads per GPU per step, {mode}"
     size = "hg38-size " if args.genome_mb >= 3000 else ""
+    clt = ("the reference's own client, one process per connection" if getattr(args, "client", "native") == "reference"
+           else "read by this repository's multi-connection client (integration/bin/bt2g-client, one process)")
     return (f"{what}, vs a {args.genome_mb:.0f} Mbp {size}synthetic genome ({args.genome_model}; hg38 is "
-            f"unavailable offline), through the reference's own server, client and per-read logic with the "
-            f"batch-first driver on the engines (integration/bin/bowtie2-align-server-batch), SAM output; "
-            f"<= 10 000 reads per client connection, {args.clients} connections at a time")
+            f"unavailable offline), through the reference's own server and per-read logic with the "
+            f"batch-first driver on the engines (integration/bin/bowtie2-align-server-batch), SAM output, "
+            f"{clt}; <= 10 000 reads per client connection, {args.clients} connections at a time")
 
 
 def run_chain(args, rank, world, local, dev, idx, cache, reads_np, quals_np):
