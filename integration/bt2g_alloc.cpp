@@ -394,6 +394,11 @@ bool sites_fresh() {
 	static const bool on = [] { const char* e = getenv("BT2G_ALLOC_SITES"); return e && !strcmp(e, "fresh"); }();
 	return on;
 }
+// $BT2G_ALLOC_SITES=all: every allocation, anywhere (which call sites allocate per read)
+bool sites_all() {
+	static const bool on = [] { const char* e = getenv("BT2G_ALLOC_SITES"); return e && !strcmp(e, "all"); }();
+	return on;
+}
 // $BT2G_ALLOC_SITES_CLASS=<bytes>: also every allocation of that size class, anywhere
 int sites_cls() {
 	static const int c = [] {
@@ -516,7 +521,7 @@ void* operator new(size_t n) {
 	if(sites_on()) {
 		if(sites_fresh()) {
 			if(t_fresh) site_count(__builtin_return_address(0), t_fresh);
-		} else if(t_site_scope || (n <= MAXSZ && cls_of(n) == sites_cls())) {
+		} else if(sites_all() || t_site_scope || (n <= MAXSZ && cls_of(n) == sites_cls())) {
 			site_count(__builtin_return_address(0), n);
 		}
 		t_fresh = 0;
@@ -531,7 +536,7 @@ void* operator new[](size_t n) {
 	if(sites_on()) {
 		if(sites_fresh()) {
 			if(t_fresh) site_count(__builtin_return_address(0), t_fresh);
-		} else if(t_site_scope || (n <= MAXSZ && cls_of(n) == sites_cls())) {
+		} else if(sites_all() || t_site_scope || (n <= MAXSZ && cls_of(n) == sites_cls())) {
 			site_count(__builtin_return_address(0), n);
 		}
 		t_fresh = 0;

@@ -201,6 +201,7 @@ std::atomic<uint64_t> g_mm_pf{0}, g_mm_pf_used{0};   // 1-mm searches prefetched
 std::atomic<uint64_t> g_rows_pf{0};                   // SA rows resolved with the sweep or the seeds
 std::atomic<uint64_t> g_ext_pf{0};
 std::atomic<uint64_t> g_ext_spec{0};                   // seed ranges extended in the seed call (bt2g_seed_search_ext)
+std::atomic<uint64_t> g_gw_inits{0}, g_gw_elts{0}, g_gw_adv{0};   // (diagnostic) GroupWalk2S inits, their elements, advanceElement calls
 std::atomic<uint64_t> g_dp_pre_us{0}, g_dp_post_us{0};   // the DP service's host work around its calls
 std::atomic<uint64_t> g_dp_again{0};                   // DPs run again (candidates, alignments or edits over the room)                    // extend requests answered by the seed call
 // rounds per read: total and a histogram (bin b: [2^b, 2^(b+1)))
@@ -264,6 +265,8 @@ void write_stats() {
 		              (unsigned long long)g_req[k].load(), (unsigned long long)g_cpu[k].load(),
 		              (unsigned long long)g_calls[k].load(), g_call_us[k].load() / 1000.0);
 	n += snprintf(buf + n, sizeof(buf) - n, ", \"ext_speculative\": %llu", (unsigned long long)g_ext_spec.load());
+	n += snprintf(buf + n, sizeof(buf) - n, ", \"gw\": [%llu, %llu, %llu]", (unsigned long long)g_gw_inits.load(),
+	              (unsigned long long)g_gw_elts.load(), (unsigned long long)g_gw_adv.load());
 	n += snprintf(buf + n, sizeof(buf) - n, ", \"one_mm_prefetch\": [%llu, %llu], \"rows_prefetched\": %llu, \"ext_prefetched\": %llu"
 	              ", \"dp_host_ms\": [%.1f, %.1f], \"dp_again\": %llu",
 	              (unsigned long long)g_mm_pf.load(), (unsigned long long)g_mm_pf_used.load(),
@@ -490,6 +493,7 @@ struct GwRange {
 	TIndexOffU topf;
 	size_t size;
 	TSlice offs;
+	bool fresh;          // every row asked (or taken from a call that resolved it), none read first
 };
 struct RefTables {
 	bool ext_on = false;
@@ -745,6 +749,70 @@ struct SwDriverB : public SwDriver {
 	SwResult* res_ptr() { return res_kind == FOUND_EE_ ? &resEe_ : res_kind == FOUND_UNGAPPED_ ? &resUngap_ : &resGap_; }
 	EIvalMergeListBinned& seenDiags() { return anchor1 ? seenDiags1_ : seenDiags2_; }
 
+	// SwDriver::prioritizeSATups restated flat (prio_flat, below): the picks as
+	// (range in satpos2_, element) pairs, materialised only as the loop reaches them
+	struct PrioEnt {
+		uint32_t src, elt;     // satpos2_ index; element, or WHOLE (a small range, all of it)
+		int32_t rnd;           // WHOLE: its Random1toN in rands_ (-1 until the loop gets there)
+		uint8_t done;          // one element: given out
+	};
+	static constexpr uint32_t WHOLE = 0xFFFFFFFFu;
+	std::vector<PrioEnt> pe_;
+	bool lazy_ = false;        // the loop's ranges are pe_ (else satpos_/rands_/gws_, eeSaTups)
+	void prio_flat(const Read& read, SeedResults& sh, const Ebwt& ebwtFw, const Ebwt* ebwtBw, int seedmms,
+	               size_t maxelt, bool doExtend, AlignmentCacheIface& ca, RandomSource& rnd, PerReadMetrics& prm,
+	               size_t& nelt_out, bool all, RefTables& tab);
+	size_t n_ent() const { return lazy_ ? pe_.size() : gws_.size(); }
+	size_t ent_size(size_t k) const {
+		if(!lazy_) return satpos_[k].sat.size();
+		return pe_[k].elt == WHOLE ? satpos2_[pe_[k].src].sat.size() : 1;
+	}
+	const SeedPos& ent_pos(size_t k) const { return lazy_ ? satpos2_[pe_[k].src].pos : satpos_[k].pos; }
+	TIndexOffU ent_topf(size_t k) const {
+		if(!lazy_) return satpos_[k].sat.topf;
+		return satpos2_[pe_[k].src].sat.topf + (pe_[k].elt == WHOLE ? 0 : pe_[k].elt);
+	}
+	uint32_t ent_len(size_t k) const { return lazy_ ? satpos2_[pe_[k].src].sat.key.len : satpos_[k].sat.key.len; }
+	TSlice ent_offs(size_t k) const {
+		if(!lazy_) return satpos_[k].sat.offs;
+		const SATupleAndPos& p = satpos2_[pe_[k].src];
+		if(pe_[k].elt == WHOLE) return p.sat.offs;
+		TSlice o;
+		o.init(p.sat.offs, pe_[k].elt, pe_[k].elt + 1);
+		return o;
+	}
+	TIndexOffU ent_off(size_t k, size_t e) const {
+		if(!lazy_) return satpos_[k].sat.offs[e];
+		const SATupleAndPos& p = satpos2_[pe_[k].src];
+		return p.sat.offs[(pe_[k].elt == WHOLE ? 0 : pe_[k].elt) + e];
+	}
+	Random1toN& ent_rand(size_t k, bool all_) {
+		PrioEnt& e = pe_[k];
+		if(e.rnd < 0) {           // a small range's Random1toN, made when first needed (init draws nothing)
+			rands_.expand();
+			rands_.back().init(satpos2_[e.src].sat.size(), all_);
+			e.rnd = (int32_t)rands_.size() - 1;
+		}
+		return rands_[e.rnd];
+	}
+	bool ent_done(size_t k) {
+		if(!lazy_) return rands_[k].done();
+		if(pe_[k].elt != WHOLE) return pe_[k].done != 0;
+		return ent_rand(k, all).done();
+	}
+	size_t ent_next(size_t k, RandomSource& rnd) {
+		if(!lazy_) return rands_[k].next(rnd);
+		if(pe_[k].elt != WHOLE) {   // Random1toN of one: 0, no draw (random_util.h:88-94)
+			pe_[k].done = 1;
+			return 0;
+		}
+		return ent_rand(k, all).next(rnd);
+	}
+	void ent_set_done(size_t k) {
+		if(!lazy_) rands_[k].setDone();
+		else if(pe_[k].elt != WHOLE) pe_[k].done = 1;
+		else ent_rand(k, all).setDone();
+	}
 	int ext_step(Driver& d, Slot& s);          // extendSeeds
 	int ext_step_paired(Driver& d, Slot& s);   // extendSeedsPaired
 	bool need_dp(Driver& d, Slot& s, int m, bool f, TIndexOffU ti, TRefOff tl, const DPRect& r, TAlScore ms,
@@ -1730,17 +1798,18 @@ void SwDriverB::speculate(Driver& d, Slot& s, std::vector<DpRes*>& out, size_t k
 	// aligner_sw_driver.cpp:883-1030; r05i: resuming instead at a cursor past every
 	// element examined so far asked 41 % more DPs for the same reads -- it skips
 	// the elements whose rows the loop resolves as it goes, the ones it asks next)
-	for(size_t ii = i; ii < gws_.size() && out.size() < k; ii++) {
-		const SATupleAndPos& p = satpos_[ii];
-		const bool f = p.pos.fw;
-		uint32_t ro = p.pos.rdoff;
-		if(!f) ro = (uint32_t)(rdlen - ro - p.pos.seedlen);
-		for(size_t e = 0; e < p.sat.size() && out.size() < k; e++) {
-			const TIndexOffU so = p.sat.offs[e];
+	for(size_t ii = i; ii < n_ent() && out.size() < k; ii++) {
+		const SeedPos& pos = ent_pos(ii);
+		const bool f = pos.fw;
+		uint32_t ro = pos.rdoff;
+		if(!f) ro = (uint32_t)(rdlen - ro - pos.seedlen);
+		const size_t esz = ent_size(ii);
+		for(size_t e = 0; e < esz && out.size() < k; e++) {
+			const TIndexOffU so = ent_off(ii, e);
 			if(so == OFF_MASK) continue;
 			TIndexOffU ti = 0, to = 0, tl = 0;
 			bool straddled = false;
-			d.ebwtFw->joinedToTextOff(p.sat.key.len, so, ti, to, tl, false, straddled);
+			d.ebwtFw->joinedToTextOff(ent_len(ii), so, ti, to, tl, false, straddled);
 			if(ti == OFF_MASK) continue;
 			const int64_t ro64 = (int64_t)to - ro;
 			Coord c(ti, ro64, f);
@@ -1875,6 +1944,26 @@ void Driver::resolve_rows_request(Slot& s) {
 	};
 	for(size_t r = 0; r < s.tab.gw.size(); r++) {
 		GwRange& x = s.tab.gw[r];
+		if(x.fresh) {
+			// (prio_flat's picks: nothing was written for them -- every row is
+			// asked, or taken from a call that resolved it; past MAX_ROWS marked
+			// unresolved, for advanceElement's CPU path)
+			for(size_t j = 0; j < x.size; j++) {
+				const uint32_t row = (uint32_t)(x.topf + j);
+				uint32_t off;
+				if((!p0.empty() && known(p0, row, off)) || (!p1.empty() && known(p1, row, off)) ||
+				   (!q0.empty() && known(q0, row, off)) || (!q1.empty() && known(q1, row, off))) {
+					x.offs[j] = off;
+					g_rows_pf++;
+				} else if(s.off_rows.size() < MAX_ROWS) {
+					s.off_rows.push_back(row);
+					s.off_where.emplace_back(r, j);
+				} else {
+					x.offs[j] = OFF_MASK;
+				}
+			}
+			continue;
+		}
 		for(size_t j = 0; j < x.size && s.off_rows.size() < MAX_ROWS; j++)
 			if(x.offs[j] == OFF_MASK) {
 				const uint32_t row = (uint32_t)(x.topf + j);
@@ -1903,6 +1992,7 @@ void Driver::resolve_rows_request(Slot& s) {
 // they hand GroupWalk2S resolved.  Expanded into each loop (below) so that
 // their resume points stay in one function each.
 #define BT2GB_EE_SETUP(LABEL_ROWS)                                                                     \
+	lazy_ = false;                                                                                     \
 	s.tab.gw.clear();                                                                                  \
 	s.tab.gw_on = true;                                                                                \
 	t_tab = &s.tab;                                                                                    \
@@ -1973,6 +2063,122 @@ static bool ext_from_seeds(Slot& s, size_t mate) {
 	return true;
 }
 
+// $BT2G_PRIO_REF=1: the reference's prioritizeSATups and GroupWalk2S objects
+// instead of prio_flat (A/B; the SAM is the same either way)
+static bool prio_ref() {
+	static const bool on = [] { const char* e = getenv("BT2G_PRIO_REF"); return e && *e == '1'; }();
+	return on;
+}
+
+// SwDriver::prioritizeSATups (aligner_sw_driver.cpp:490-738), restated for the
+// batch driver.  Kept exactly: the seed-hit ranges and their order (hitsByRank,
+// queryQval), the ranges an earlier extension covers (seedmms 0), the
+// extensions (SwDriver::extend, served from the seed call's table), the sort,
+// then the picks -- the first nsmall ranges whole (nsm 5), then single
+// elements of the rest drawn by RowSampler (lengths and sizes squared) and
+// each range's Random1toN, with the same draws from rnd in the same order, up
+// to maxelt elements.  Changed: a pick is recorded as (range, element) in pe_;
+// the SATuple, Random1toN and GroupWalk2S the reference builds for every pick
+// are not built (the loop examines ~6 of a read's ~45 picks, r05r: 3.19 M
+// GroupWalk2S::init for 0.43 M advanceElement over 70 k reads), and the picks'
+// rows go to the rows request straight from pe_ (GwRange::fresh).  Random1toN::
+// init draws nothing, so a small range's chooser is made when the loop gets to it.
+void SwDriverB::prio_flat(const Read& read, SeedResults& sh, const Ebwt& ebwtFw, const Ebwt* ebwtBw, int seedmms,
+                          size_t maxelt, bool doExtend, AlignmentCacheIface& ca, RandomSource& rnd,
+                          PerReadMetrics& prm, size_t& nelt_out, bool all_, RefTables& tab) {
+	const size_t nsm = 5;
+	const int matei = read.mate <= 1 ? 0 : 1;
+	satups_.clear();
+	gws_.clear();
+	rands_.clear();
+	rands2_.clear();
+	satpos_.clear();
+	satpos2_.clear();
+	pe_.clear();
+	lazy_ = true;
+	size_t nrange = 0, nelt = 0, nsmall = 0;
+	const size_t nz = sh.nonzeroOffsets();
+	for(size_t h = 0; h < nz; h++) {
+		bool hfw = true;
+		uint32_t offidx = 0, hoff = 0, hlen = 0;
+		QVal qv = sh.hitsByRank(h, offidx, hoff, hfw, hlen);
+		ca.queryQval(qv, satups_, nrange, nelt);
+		EList<ExtendRange>& exr = hfw ? seedExRangeFw_[matei] : seedExRangeRc_[matei];
+		for(size_t j = 0; j < satups_.size(); j++) {
+			const size_t sz = satups_[j].size();
+			if(seedmms == 0) {
+				// inside an extension already made, from a range no bigger: skipped
+				bool covered = false;
+				for(size_t k = 0; k < exr.size() && !covered; k++)
+					covered = exr[k].off <= hoff && exr[k].off + exr[k].len >= (size_t)hoff + hlen && sz <= exr[k].sz;
+				if(covered) {
+					nrange--;
+					nelt -= sz;
+					continue;
+				}
+			}
+			satpos2_.expand();
+			SATupleAndPos& p = satpos2_.back();
+			p.sat = satups_[j];
+			p.origSz = sz;
+			p.pos.init(hfw, offidx, hoff, hlen);
+			if(sz <= nsm) nsmall++;
+			size_t nlex = 0, nrex = 0;
+			if(doExtend)
+				extend(read, ebwtFw, ebwtBw, p.sat.topf, (TIndexOffU)(p.sat.topf + sz), p.sat.topb,
+				       (TIndexOffU)(p.sat.topb + sz), hfw, hoff, hlen, prm, nlex, nrex);
+			p.nlex = nlex;
+			p.nrex = nrex;
+			if(seedmms == 0 && (nlex > 0 || nrex > 0)) {
+				exr.expand();
+				exr.back().off = hoff - (hfw ? nlex : nrex);
+				exr.back().len = hlen + nlex + nrex;
+				exr.back().sz = sz;
+			}
+		}
+		satups_.clear();
+	}
+	nelt_out = nelt;
+	satpos2_.sort();
+	size_t added = 0;
+	for(size_t j = 0; j < nsmall && added < maxelt; j++) {
+		pe_.push_back(PrioEnt{(uint32_t)j, WHOLE, -1, 0});
+		added += satpos2_[j].sat.size();
+	}
+	if(added < maxelt && nsmall != satpos2_.size()) {
+		rowsamp_.init(satpos2_, nsmall, satpos2_.size(), true, true);
+		rands2_.resize(satpos2_.size());
+		for(size_t j = 0; j < satpos2_.size(); j++) rands2_[j].reset();
+		while(added < maxelt && added < nelt) {
+			const size_t ri = rowsamp_.next(rnd) + nsmall;
+			Random1toN& rr = rands2_[ri];
+			if(!rr.inited()) rr.init(satpos2_[ri].sat.size(), all_);
+			const size_t r = rr.next(rnd);
+			if(rr.done()) rowsamp_.finishedRange(ri - nsmall);
+			pe_.push_back(PrioEnt{(uint32_t)ri, (uint32_t)r, -1, 0});
+			added++;
+		}
+	}
+	nelt_out = added;
+	// the picks' rows, for the rows request (resolve_rows_request)
+	tab.gw.clear();
+	for(size_t k = 0; k < pe_.size(); k++)
+		tab.gw.push_back(GwRange{ent_topf(k), ent_size(k), ent_offs(k), true});
+}
+
+// GroupWalk2S::advanceElement as the drop-in serves it (the specialisation
+// below) for a prio_flat pick: the row's offset from the rows request, or
+// Ebwt::getOffset on the CPU for a row past the request's cap.
+static inline void adv_flat(TIndexOffU elt, const Ebwt& ebwtFw, SARangeWithOffs<TSlice>& sa, WalkResult& res,
+                            WalkMetrics& met) {
+	if(sa.offs[elt] == OFF_MASK) {
+		sa.offs[elt] = ebwtFw.getOffset(sa.topf + elt);
+		g_cpu[K_OFF]++;
+	}
+	met.reports++;
+	res.init(0, false, 0, elt, sa.topf + elt, (TIndexOffU)sa.len, sa.offs[elt]);
+}
+
 #define BT2GB_PRIO_SETUP(LABEL_EXT, LABEL_ROWS)                                                        \
 	ext_request(d, s, *this);                                                                          \
 	if(!s.ext_in.empty() && ext_from_seeds(s, mate)) goto LABEL_EXT;                                   \
@@ -1993,8 +2199,14 @@ static bool ext_from_seeds(Slot& s, size_t mate) {
 	t_cpu_ext = &g_cpu[K_EXT];                                                                         \
 	{                                                                                                  \
 		Ph ph_(PH_PRIO);                                                                               \
-		prioritizeSATups(rd, s.shs[mate], ebwtFw, d.ebwtBw, ref, seedmms, maxIters, R_doExtend, true, true, 5, \
-		                 s.ca, s.rnd, d.wlm, s.prm, nelt, all);                                        \
+		if(prio_ref()) {                                                                               \
+			lazy_ = false;                                                                             \
+			prioritizeSATups(rd, s.shs[mate], ebwtFw, d.ebwtBw, ref, seedmms, maxIters, R_doExtend, true, \
+			                 true, 5, s.ca, s.rnd, d.wlm, s.prm, nelt, all);                           \
+		} else {                                                                                       \
+			prio_flat(rd, s.shs[mate], ebwtFw, d.ebwtBw, seedmms, maxIters, R_doExtend, s.ca, s.rnd,   \
+			          s.prm, nelt, all, s.tab);                                                        \
+		}                                                                                              \
 	}                                                                                                  \
 	s.tab.ext_on = false;                                                                              \
 	s.tab.gw_on = false;                                                                               \
@@ -2015,12 +2227,13 @@ static bool ext_from_seeds(Slot& s, size_t mate) {
 	{                                                                                                  \
 		Ph ph_(PH_NEXTELT);                                                                            \
 		WalkResult wr;                                                                                 \
-		const size_t elt = rands_[i].next(s.rnd);                                                      \
+		const size_t elt = ent_next(i, s.rnd);                                                         \
 		SARangeWithOffs<TSlice> sa;                                                                    \
-		sa.topf = satpos_[i].sat.topf;                                                                 \
-		sa.len = satpos_[i].sat.key.len;                                                               \
-		sa.offs = satpos_[i].sat.offs;                                                                 \
-		gws_[i].advanceElement((TIndexOffU)elt, ebwtFw, ref, sa, gwstate_, wr, d.wlm, s.prm);          \
+		sa.topf = ent_topf(i);                                                                         \
+		sa.len = ent_len(i);                                                                           \
+		sa.offs = ent_offs(i);                                                                         \
+		if(lazy_) adv_flat((TIndexOffU)elt, ebwtFw, sa, wr, d.wlm);                                    \
+		else gws_[i].advanceElement((TIndexOffU)elt, ebwtFw, ref, sa, gwstate_, wr, d.wlm, s.prm);     \
 		eltsDone++;                                                                                    \
 		BT2GB_NELT_DEC;                                                                                \
 		tidx = 0;                                                                                      \
@@ -2154,15 +2367,15 @@ int SwDriverB::ext_step(Driver& d, Slot& s) {
 			}
 			if(neltLeft == 0) break;    // finished examining gapped candidates
 		}
-		for(i = 0; i < gws_.size(); i++) {
+		for(i = 0; i < n_ent(); i++) {
 			if(eeMode && eehits_[i].score < *minsc) return EXTEND_PERFECT_SCORE;
-			is_small = satpos_[i].sat.size() < 5;
-			fw = satpos_[i].pos.fw;
-			rdoff = satpos_[i].pos.rdoff;
-			seedhitlen = satpos_[i].pos.seedlen;
+			is_small = ent_size(i) < 5;
+			fw = ent_pos(i).fw;
+			rdoff = ent_pos(i).rdoff;
+			seedhitlen = ent_pos(i).seedlen;
 			if(!fw) rdoff = (uint32_t)(rdlen - rdoff - seedhitlen);
 			first = true;
-			while(!rands_[i].done() && (first || is_small || eeMode)) {
+			while(!ent_done(i) && (first || is_small || eeMode)) {
 				if(*minsc == perfectScore) {
 					if(!eeMode || eehits_[i].score < perfectScore) return EXTEND_PERFECT_SCORE;
 				} else if(eeMode && eehits_[i].score < *minsc) {
@@ -2375,7 +2588,7 @@ int SwDriverB::ext_step_paired(Driver& d, Slot& s) {
 				firstEe = false;
 				BT2GB_EE_SETUP(after_ee_rows)
 				neltLeft = nelt;
-				mateStreaks_.resize(gws_.size());
+				mateStreaks_.resize(n_ent());
 				mateStreaks_.fill(0);
 			} else {
 				eeMode = false;
@@ -2389,20 +2602,20 @@ int SwDriverB::ext_step_paired(Driver& d, Slot& s) {
 				BT2GB_PRIO_SETUP(after_ext, after_prio_rows)
 				neltLeft = nelt;
 				firstExtend = false;
-				mateStreaks_.resize(gws_.size());
+				mateStreaks_.resize(n_ent());
 				mateStreaks_.fill(0);
 			}
 			if(neltLeft == 0) break;
 		}
-		for(i = 0; i < gws_.size(); i++) {
+		for(i = 0; i < n_ent(); i++) {
 			if(eeMode && eehits_[i].score < *minsc) return EXTEND_PERFECT_SCORE;
-			is_small = satpos_[i].sat.size() < 5;
-			fw = satpos_[i].pos.fw;
-			rdoff = satpos_[i].pos.rdoff;
-			seedhitlen = satpos_[i].pos.seedlen;
+			is_small = ent_size(i) < 5;
+			fw = ent_pos(i).fw;
+			rdoff = ent_pos(i).rdoff;
+			seedhitlen = ent_pos(i).seedlen;
 			if(!fw) rdoff = (uint32_t)(rdlen - rdoff - seedhitlen);
 			first = true;
-			while(!rands_[i].done() && (first || is_small || eeMode)) {
+			while(!ent_done(i) && (first || is_small || eeMode)) {
 				if(*minsc == perfectScore) {
 					if(!eeMode || eehits_[i].score < perfectScore) return EXTEND_PERFECT_SCORE;
 				} else if(eeMode && eehits_[i].score < *minsc) {
@@ -2415,7 +2628,7 @@ int SwDriverB::ext_step_paired(Driver& d, Slot& s) {
 				if(!eeMode && s.prm.nDpFail >= maxDpStreak) return EXTEND_EXCEEDED_SOFT_LIMIT;
 				if(!eeMode && s.prm.nUgFail >= maxUgStreak) return EXTEND_EXCEEDED_SOFT_LIMIT;
 				if(mateStreaks_[i] >= maxMateStreak) {
-					rands_[i].setDone();       // don't try this seed range anymore
+					ent_set_done(i);           // don't try this seed range anymore
 					break;
 				}
 				s.prm.nExIters++;
@@ -2776,10 +2989,12 @@ void GroupWalk2S<TSlice, 16>::init(const Ebwt& ebwtFw, const BitPairReference& r
 	(void)ebwtFw; (void)ref; (void)rnd; (void)met;
 	reset();
 	elt_ += sa.size();
+	g_gw_inits.fetch_add(1, std::memory_order_relaxed);
+	g_gw_elts.fetch_add(sa.size(), std::memory_order_relaxed);
 	// the range's offset slots as the cache would hold them before any walk
 	// (AlignmentCache::addOnTheFlyImpl only reserves them, bt2g_refspec.h)
 	static_cast<bt2gref::TSliceAcc&>(sa.offs).fill(OFF_MASK);
-	if(t_tab && t_tab->gw_on) t_tab->gw.push_back(GwRange{sa.topf, sa.size(), sa.offs});
+	if(t_tab && t_tab->gw_on) t_tab->gw.push_back(GwRange{sa.topf, sa.size(), sa.offs, false});
 }
 
 template <>
@@ -2787,6 +3002,7 @@ bool GroupWalk2S<TSlice, 16>::advanceElement(TIndexOffU elt, const Ebwt& ebwtFw,
                                              SARangeWithOffs<TSlice>& sa, GroupWalkState& gws, WalkResult& res,
                                              WalkMetrics& met, PerReadMetrics& prm) {
 	(void)ref; (void)gws; (void)prm;
+	g_gw_adv.fetch_add(1, std::memory_order_relaxed);
 	if(sa.offs[elt] == OFF_MASK) {       // not batched: the reference's getOffset on the CPU
 		sa.offs[elt] = ebwtFw.getOffset(sa.topf + elt);
 		g_cpu[K_OFF]++;
@@ -2990,19 +3206,22 @@ void Driver::after_seeds(Slot& s, int mate) {
 			possearches++;
 			seedsearches++;
 			const BTDnaString& seq = sr.seqs(fw)[i];
-			SeedSearchCache srcache(seq, sr.quals(fw)[i]);
 			const uint32_t* q = &x.sd_out[((size_t)fwi * nof + i) * 4];
-			if(q[1] > q[0]) srcache.addOnTheFly(seq, q[0], q[1], q[2], q[3]);
-			if(srcache.beginAlign(s.ca) == -1) {
+			// SeedSearchCache's protocol (aligner_seed.h:1461-1580) without its
+			// per-seed vector: beginAlign; the range, if any, added while the
+			// cache aligns (addAllCached: false when it does not); finishAlign
+			QVal qv;
+			const int ret = s.ca.beginAlign(seq, sr.quals(fw)[i], qv);
+			if(ret == -1 || !s.ca.aligning()) {
 				ooms++;
 				continue;
 			}
-			if(!srcache.addAllCached()) {
+			if(q[1] > q[0] && !s.ca.addOnTheFly(seq, q[0], q[1], q[2], q[3])) {
 				ooms++;
 				continue;
 			}
-			srcache.finishAlign();
-			if(srcache.qvValid()) sr.add(srcache.getQv(), s.ca.current(), (uint32_t)i, fw);
+			qv = s.ca.finishAlign();
+			if(qv.valid()) sr.add(qv, s.ca.current(), (uint32_t)i, fw);
 		}
 	}
 	s.prm.nSeedRanges = sr.numRanges();

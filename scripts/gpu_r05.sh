@@ -81,6 +81,13 @@ envab)
       > $O/bench_$i.json 2> $O/bench_$i.log || { tail -30 $O/bench_$i.log; exit 1; }
     python3 -c "import json; d=json.load(open('$O/bench_$i.json')); s=d['server']; k=d['server_kernels']; print('$set', round(d['value']), round(s['cpu_us_per_read'],1), s['server_rss_gb_per_pass'][-1], round(k['sw_dp:7']['ms_per_launch'],2), k['sw_dp:7']['launches'])"
   done ;;
+clientab)
+  # the timed passes with the multi-connection client and with the reference client
+  for c in ${CLIENTS:-native reference}; do
+    timeout -k 10 500 python3 -u bench.py --client $c --steps ${3:-3} --warmup 1 --chain-steps 0 --stock-sample 0 $BENCH_ARGS \
+      > $O/bench_$c.json 2> $O/bench_$c.log || { tail -30 $O/bench_$c.log; exit 1; }
+    python3 -c "import json; d=json.load(open('$O/bench_$c.json')); s=d['server']; print('$c', round(d['value']), round(s['cpu_us_per_read'],1), round(s['client_cpu_us_per_read'],2), s['server_rss_gb_per_pass'][-1])"
+  done ;;
 bench)
   T0=$(date +%s); timeout -k 10 1100 python3 -u bench.py --gpus 1 --steps 20 --warmup 5 > $O/bench.json 2> $O/bench.log || { tail -30 $O/bench.log; exit 1; }; echo "wall $(( $(date +%s) - T0 )) s"
   tail -25 $O/bench.log | grep -v "^\s*$"; cut -c1-1500 $O/bench.json ;;
