@@ -716,11 +716,14 @@ def schedule_run(args, rank, world, local, base, reads_np, quals_np, workdir, bi
             torch.cuda.synchronize()
         rss = [srv.last_rss_gb]                 # after the warmup, then after every timed pass
         t0 = time.perf_counter()
-        aligned, outs, cpu_s, client_s = 0, None, 0.0, 0.0
+        aligned, outs, cpu_s, client_s, host_s, thr_s, run_s = 0, None, 0.0, 0.0, 0.0, 0.0, 0.0
         for i in range(args.steps):
-            _, outs = srv.run(chunks, k=args.clients, client=client)
+            dt_i, outs = srv.run(chunks, k=args.clients, client=client)
             cpu_s += srv.last_cpu_s
             client_s += srv.last_client_cpu_s
+            host_s += srv.last_host_cpu_s
+            thr_s += srv.last_throttled_s
+            run_s += dt_i
             rss.append(srv.last_rss_gb)
             aligned += count_aligned(outs, paired)
             if i + 1 < args.steps:
@@ -743,7 +746,8 @@ def schedule_run(args, rank, world, local, base, reads_np, quals_np, workdir, bi
                 pass
         time.sleep(0.1)
     return {"elapsed": elapsed, "aligned": aligned, "outs": outs, "chunks": chunks, "stats": st, "slots_per_driver": slots,
-            "server_cpu_s": cpu_s, "client_cpu_s": client_s, "server_threads_cpu": threads_cpu, "server_rss_gb": rss[-1],
+            "server_cpu_s": cpu_s, "client_cpu_s": client_s, "host_cpu_s": host_s, "throttled_s": thr_s,
+            "passes_s": run_s, "server_threads_cpu": threads_cpu, "server_rss_gb": rss[-1],
             "server_rss_gb_per_pass": rss, "binary": binary_id(binary), "client": binary_id(client),
             "smaps_top": smaps}
 
@@ -1284,6 +1288,10 @@ def main():
                        # the client side (read parsing, the wire, SAM receipt) on the same CPU
                        # quota: bt2g-client, or the reference's client processes (--client reference)
                        "client": sched["client"],
+                       # the whole CPU share's use over the timed passes (cgroup cpu.stat: every
+                       # process of the job) and the time its quota throttled it
+                       "host_cores_busy": sched["host_cpu_s"] / max(1e-9, sched["passes_s"]),
+                       "throttled_s": sched["throttled_s"],
                        "client_cpu_s": sched["client_cpu_s"],
                        "client_cpu_us_per_read": sched["client_cpu_s"] / max(1, args.reads * args.steps) * 1e6,
                        "calls": {k: st.get(k) for k in ("exact_sweep", "one_mm", "seed_search", "extend",

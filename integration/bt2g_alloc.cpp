@@ -284,6 +284,10 @@ void* alloc(size_t n) {
 		if(Node* b = tc.head[c]) {
 			tc.head[c] = b->next;
 			tc.n[c]--;
+			// the next block of the class, whose link the next allocation reads: a
+			// cold line otherwise (a block freed long ago; r05s: the link load was
+			// ~60 % of the allocator's samples)
+			if(tc.head[c]) __builtin_prefetch(tc.head[c], 1, 3);
 			return b;
 		}
 	}

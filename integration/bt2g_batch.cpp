@@ -586,6 +586,9 @@ struct PoolSuper { typedef uint8_t* Pool::*type; friend type peek(PoolSuper); };
 struct PoolCur { typedef size_t Pool::*type; friend type peek(PoolCur); };
 template struct PoolPeek<PoolSuper, &Pool::super_pages>;
 template struct PoolPeek<PoolCur, &Pool::cur_>;
+// EIvalMergeListBinned's bins (ival_list.h:296), for clearing only the bins a read used
+struct DiagBins { typedef EList<EIvalMergeList> EIvalMergeListBinned::*type; friend type peek(DiagBins); };
+template struct PoolPeek<DiagBins, &EIvalMergeListBinned::bins_>;
 
 const size_t POOL_KEEP = 16;                   // pages (16 KB each, CACHE_PAGE_SZ) a pool keeps
 
@@ -629,6 +632,7 @@ struct RedFlat {
 	void reset() {
 		alns.clear();
 		iv.clear();
+		last = nullptr;
 	}
 	// the cells of res: per row, [left, right) (aligner_result.cpp:930-969)
 	static size_t cells(const AlnRes& res, std::vector<std::pair<TRefOff, TRefOff>>& out) {
@@ -658,9 +662,13 @@ struct RedFlat {
 		if(!res.fw()) const_cast<AlnRes&>(res).invertEdits();
 		return start;
 	}
+	const AlnRes* last = nullptr;         // the alignment whose cells tmp holds (overlap, then add)
+	size_t last_row0 = 0;
 	bool overlap(const AlnRes& res) {
 		tmp.clear();
 		const size_t row0 = cells(res, tmp);
+		last = &res;
+		last_row0 = row0;
 		const size_t row1 = row0 + tmp.size();
 		for(const Aln& a : alns) {
 			if(a.ref != res.refid() || a.fw != res.fw()) continue;
@@ -673,12 +681,20 @@ struct RedFlat {
 		}
 		return false;
 	}
+	// (every call follows overlap() on the same, unchanged alignment: its cells
+	// are taken from tmp instead of walked again)
 	void add(const AlnRes& res) {
 		Aln a;
 		a.ref = res.refid();
 		a.fw = res.fw();
 		a.at = iv.size();
-		a.row0 = cells(res, iv);
+		if(last == &res) {
+			iv.insert(iv.end(), tmp.begin(), tmp.end());
+			a.row0 = last_row0;
+		} else {
+			a.row0 = cells(res, iv);
+		}
+		last = nullptr;
 		a.nrow = iv.size() - a.at;
 		alns.push_back(a);
 	}
@@ -693,10 +709,28 @@ struct SwDriverB : public SwDriver {
 	Pool& ee_pool() { return pool_; }
 	RedFlat redA, redM1, redM2;            // redAnchor_, redMate1_, redMate2_ (RedFlat above)
 	// SwDriver::nextRead (aligner_sw_driver.h:422-441) with the flat redundancy sets
+	// seenDiags1_ / seenDiags2_ with the bins each read added to (bin = the
+	// reference id's low 7 bits, ival_list.h:232-236): the next read clears
+	// those bins only, the same state as EIvalMergeListBinned::reset's clear of
+	// all 128 (r05s: the two resets were ~5 % of the drivers' samples; a read
+	// touches a few bins)
+	uint64_t sd_used[2][2] = {{0, 0}, {0, 0}};
+	void sd_add(int which, const Interval& iv) {
+		const size_t bin = iv.ref() & ~(0xffffffff << EIvalMergeListBinned::NBIN);
+		sd_used[which][bin >> 6] |= 1ull << (bin & 63);
+		(which ? seenDiags2_ : seenDiags1_).add(iv);
+	}
+	void sd_clear(int which) {
+		EList<EIvalMergeList>& bins = (which ? seenDiags2_ : seenDiags1_).*peek(DiagBins());
+		for(int w = 0; w < 2; w++) {
+			for(uint64_t m = sd_used[which][w]; m; m &= m - 1) bins[w * 64 + __builtin_ctzll(m)].clear();
+			sd_used[which][w] = 0;
+		}
+	}
 	void next_read() {
 		redA.reset();
-		seenDiags1_.reset();
-		seenDiags2_.reset();
+		sd_clear(0);
+		sd_clear(1);
 		seedExRangeFw_[0].clear();
 		seedExRangeFw_[1].clear();
 		seedExRangeRc_[0].clear();
@@ -2162,6 +2196,7 @@ void SwDriverB::prio_flat(const Read& read, SeedResults& sh, const Ebwt& ebwtFw,
 	nelt_out = added;
 	// the picks' rows, for the rows request (resolve_rows_request)
 	tab.gw.clear();
+	tab.gw.reserve(pe_.size());
 	for(size_t k = 0; k < pe_.size(); k++)
 		tab.gw.push_back(GwRange{ent_topf(k), ent_size(k), ent_offs(k), true});
 }
@@ -2415,10 +2450,10 @@ int SwDriverB::ext_step(Driver& d, Slot& s) {
 					if(h.mms() > 0) resEe_.alres.ned().push_back(h.e1);
 					state = FOUND_EE_;
 					found = true;
-					seenDiags1_.add(Interval(refcoord, 1));
+					sd_add(0, Interval(refcoord, 1));
 				} else if(R_doUngapped && ungapped) {
 					BT2GB_UNGAPPED(after_ug)
-					seenDiags1_.add(Interval(refcoord, 1));
+					sd_add(0, Interval(refcoord, 1));
 					s.prm.nExUgs++;
 					if(ug_ret == 0) {
 						s.prm.nExUgFails++;
@@ -2445,14 +2480,14 @@ int SwDriverB::ext_step(Driver& d, Slot& s) {
 					DynProgFramer dpframe(!gReportOverhangs);
 					found = dpframe.frameSeedExtensionRect(refoff, rows, tlen, readGaps, refGaps, (size_t)nceil, R_maxhalf,
 					                                       rect);
-					seenDiags1_.add(Interval(refcoord, 1));
+					sd_add(0, Interval(refcoord, 1));
 					if(!found) continue;
 				}
 				if(state == FOUND_NONE_) {
 					{
 						Interval refival(tidx, 0, fw, 0);
 						rect.initIval(refival);
-						seenDiags1_.add(refival);
+						sd_add(0, refival);
 					}
 					{
 						Ph ph(PH_NEEDDP);
@@ -2662,13 +2697,13 @@ int SwDriverB::ext_step_paired(Driver& d, Slot& s) {
 					if(h.mms() > 0) resEe_.alres.ned().push_back(h.e1);
 					state = FOUND_EE_;
 					found = true;
-					seenDiags().add(Interval(refcoord, 1));
+					sd_add(anchor1 ? 0 : 1, Interval(refcoord, 1));
 					s.prm.nExEes++;
 					s.prm.nEeFail++;        // failed until proven successful
 					s.prm.nExEeFails++;
 				} else if(R_doUngapped && ungapped) {
 					BT2GB_UNGAPPED(after_ug)
-					seenDiags().add(Interval(refcoord, 1));
+					sd_add(anchor1 ? 0 : 1, Interval(refcoord, 1));
 					s.prm.nExUgs++;
 					s.prm.nUgFail++;        // failed until proven successful
 					s.prm.nExUgFails++;
@@ -2687,14 +2722,14 @@ int SwDriverB::ext_step_paired(Driver& d, Slot& s) {
 					DynProgFramer dpframe(!gReportOverhangs);
 					found = dpframe.frameSeedExtensionRect(refoff, rows, tlen, readGaps, refGaps, (size_t)nceil, R_maxhalf,
 					                                       rect);
-					seenDiags().add(Interval(refcoord, 1));
+					sd_add(anchor1 ? 0 : 1, Interval(refcoord, 1));
 					if(!found) continue;
 				}
 				if(state == FOUND_NONE_) {
 					{
 						Interval refival(tidx, 0, fw, 0);
 						rect.initIval(refival);
-						seenDiags().add(refival);
+						sd_add(anchor1 ? 0 : 1, refival);
 					}
 					{
 						Ph ph(PH_NEEDDP);
@@ -3168,10 +3203,31 @@ int Driver::instantiate(Slot& s, int mate, size_t offset) {
 		for(int i = 0; i < nseeds; i++) {
 			const int depth = i * per + (int)offset;
 			const int sl = std::min<int>(len, (int)rd.length());
-			al.instantiateSeq(rd, sr.seqs(fw)[i], sr.quals(fw)[i], sl, depth, fw);
+			// SeedAligner::instantiateSeq (aligner_seed.cpp:471-491): the seed's
+			// bases as they align to the Watson strand (rc: complemented, reversed)
+			// and its qualities, with the N test of the instantiation
+			BTDnaString& sq = sr.seqs(fw)[i];
+			BTString& sqq = sr.quals(fw)[i];
+			sq.resize(sl);
+			sqq.resize(sl);
+			const char* pf = rd.patFw.buf();
+			const char* qf = rd.qual.buf();
 			bool ok = true;
-			const BTDnaString& q = sr.seqs(fw)[i];
-			for(int k = 0; k < sl && ok; k++) ok = (int)q[k] < 4;
+			if(fw) {
+				for(int k = 0; k < sl; k++) {
+					const int c = pf[depth + k];
+					sq.set(c, k);
+					sqq.set(qf[depth + k], k);
+					ok = ok && c < 4;
+				}
+			} else {
+				for(int k = 0; k < sl; k++) {
+					const int c = pf[depth + sl - k - 1];
+					sq.set(c < 4 ? 3 - c : 4, k);
+					sqq.set(qf[depth + sl - k - 1], k);
+					ok = ok && c < 4;
+				}
+			}
 			if(ok) {
 				set_valid(x, fw, (size_t)i);
 				ninst++;
