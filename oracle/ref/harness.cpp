@@ -310,7 +310,11 @@ void bt2ref_seed_search(void* vh, int n, const char** seqs, const char** quals,
 	// (aligner_cache.cpp:82-96) -- giant ranges of e.g. poly-A 22-mers at hg38
 	// scale; that resource limit is reproduced by the drop-in server, which runs
 	// the reference's own cache code (integration/bt2g_seams.cpp), not here.
-	AlignmentCache scCurrent((size_t)1 << 30, false);
+	// (one per thread, kept across calls -- ca.nextRead() clears it for every
+	// read: the CPU stand-in server calls this once per read, and a 1 GB block
+	// made and freed per call was an mmap / munmap pair per read whose TLB
+	// shootdowns slowed every thread of that server)
+	static thread_local AlignmentCache scCurrent((size_t)1 << 30, false);
 	AlignmentCacheIface ca(&scCurrent, NULL, NULL);
 	EList<Seed> seeds;
 	Constraint gc = Constraint::penaltyFuncBased(sc.scoreMin);
