@@ -663,7 +663,6 @@ int bt2g_exact_sweep_dev(bt2g_ctx* c, const uint8_t* reads, uint32_t stride, con
 	if(int rc = check_reads(stride, n)) return rc;
 	if(n == 0) return BT2G_OK;
 	hipStream_t st = pick(c, stream);
-	HIPCHK(hipMemsetAsync(out, 0, sizeof(uint32_t) * 8 * (size_t)n, st));   // bwops / loads accumulate
 	{
 		ProfScope ps(c, 0, st);
 		launch_exact_sweep(c->fw, reads, stride, lens, n, mine_max, nofw, norc, out, st);
@@ -746,8 +745,7 @@ static int one_mm_impl(bt2g_ctx* c, const uint8_t* reads, const uint8_t* quals, 
 	HIPCHK(amalloc(c, (void**)&s.fb_sdep, sizeof(uint32_t) * (size_t)n * 4, st));
 	HIPCHK(amalloc(c, (void**)&s.slot_flag, sizeof(uint32_t) * (size_t)n * 4, st));
 	HIPCHK(hipMemsetAsync(s.ovf, 0, sizeof(int32_t) * 16, st));
-	HIPCHK(hipMemsetAsync(bwops, 0, sizeof(uint32_t) * n, st));
-	if(loads) HIPCHK(hipMemsetAsync(loads, 0, sizeof(uint32_t) * n, st));
+	// (bwops, loads and the slot flags are zeroed by k_one_mm_items, the first kernel)
 	{
 		ProfScope ps(c, 2, st);
 		launch_one_mm(c->fw, c->bw, reads, quals, stride, lens, n, minsc, *sc, nofw, norc, gate, cap, s.items,

@@ -120,6 +120,21 @@ __device__ __forceinline__ int side_rowL(const SideData& s, uint32_t charOff) {
 }
 
 
+// Issue priority of the latency-bound walkers ($BT2G_WALK_PRIO at build time,
+// 0 = none): a walker wave issues a few instructions between dependent HBM
+// gathers, and on a SIMD shared with VALU-heavy waves of another service's
+// kernel (the SW fill) it loses issue arbitration to older waves (priority,
+// then age: MI355X_MICROARCH.md, "Two waves per SIMD", item 2) -- s_setprio at
+// entry puts its few instructions first.
+#ifndef BT2G_WALK_PRIO
+#define BT2G_WALK_PRIO 0
+#endif
+__device__ __forceinline__ void walk_prio() {
+#if BT2G_WALK_PRIO > 0
+	__builtin_amdgcn_s_setprio(BT2G_WALK_PRIO);
+#endif
+}
+
 // fchr[c] without a data-dependent index into the (kernel-argument) array
 __device__ __forceinline__ uint32_t fchr_at(const DevEbwt& e, int c) {
 	return c == 0 ? e.fchr[0] : c == 1 ? e.fchr[1] : c == 2 ? e.fchr[2] : c == 3 ? e.fchr[3] : e.fchr[4];

@@ -21,6 +21,7 @@
 __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(BT2G_SWEEP_WAVES)))
 k_exact_sweep(DevEbwt e, const uint8_t* __restrict__ reads, uint32_t stride, const uint32_t* __restrict__ lens,
               uint32_t n, uint32_t mine_max, int nofw, int norc, uint32_t* __restrict__ out) {
+	walk_prio();
 	// lanes 2r, 2r+1: the two strands of read r (strand-homogeneous waves
 	// measured slower: half the reads of any wave come from either strand)
 	const uint32_t gid = blockIdx.x * blockDim.x + threadIdx.x;
@@ -116,13 +117,16 @@ k_exact_sweep(DevEbwt e, const uint8_t* __restrict__ reads, uint32_t stride, con
 		mine = nedit;
 		if(nedit == 0 && bot > top) { otop = top; obot = bot; }
 	}
+	// bwops / side loads of the read = sum of both strands: the pair's lanes are
+	// neighbours in one wave (2r, 2r+1), so the sum is a lane swap and the read's
+	// words are plain stores (no memset of the output before the launch)
+	const uint32_t bw2 = bwops + (uint32_t)__shfl_xor((int)bwops, 1);
+	const uint32_t ld2 = loads + (uint32_t)__shfl_xor((int)loads, 1);
 	if(!valid) return;
 	out[(size_t)r * 8 + strand] = mine;
 	out[(size_t)r * 8 + 2 + 2 * strand] = otop;
 	out[(size_t)r * 8 + 3 + 2 * strand] = obot;
-	// bwops / side loads of the read = sum of both strands (words zeroed by the caller)
-	if(bwops) atomicAdd(&out[(size_t)r * 8 + 6], bwops);
-	if(loads) atomicAdd(&out[(size_t)r * 8 + 7], loads);
+	out[(size_t)r * 8 + 6 + strand] = strand == 0 ? bw2 : ld2;
 }
 
 // --------------------------------------------------------------------------
@@ -135,6 +139,7 @@ k_seed_search(DevEbwt F, DevEbwt B, const uint8_t* __restrict__ reads, uint32_t 
               const uint32_t* __restrict__ lens, uint32_t n, uint32_t seedlen, uint32_t interval,
               uint32_t offset, uint32_t maxseeds, uint32_t* __restrict__ out, int32_t* __restrict__ nseeds,
               uint32_t* __restrict__ bwops, uint32_t* __restrict__ loads_out) {
+	walk_prio();
 	uint32_t gid = blockIdx.x * blockDim.x + threadIdx.x;
 	uint32_t per = 2 * maxseeds;
 	uint32_t r = gid / per, rem = gid % per, strand = rem / maxseeds, s = rem % maxseeds;
@@ -255,6 +260,7 @@ __global__ void k_one_mm_compact(bt2g_mm1* __restrict__ slots, const int32_t* __
 __global__ void __launch_bounds__(256)
 k_get_offset(DevEbwt e, const uint32_t* __restrict__ rows, uint32_t n, uint32_t* __restrict__ offs,
              uint32_t* __restrict__ loads_out) {
+	walk_prio();
 	uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
 	if(i >= n) return;
 	uint32_t row = rows[i];
@@ -340,6 +346,7 @@ __global__ void __launch_bounds__(256)
 k_range_offsets(DevEbwt e, const uint32_t* __restrict__ sweep, const bt2g_mm1* __restrict__ hits,
                 const int32_t* __restrict__ counts, uint32_t n, uint32_t cap, uint32_t off_cap,
                 uint32_t* __restrict__ offs) {
+	walk_prio();
 	const uint64_t gid = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
 	const uint64_t per = (uint64_t)(2u + cap) * off_cap;
 	if(gid >= (uint64_t)n * per) return;
@@ -361,6 +368,7 @@ k_range_offsets(DevEbwt e, const uint32_t* __restrict__ sweep, const bt2g_mm1* _
 __global__ void __launch_bounds__(256)
 k_seed_offsets(DevEbwt e, const uint32_t* __restrict__ out, uint64_t nrange, uint32_t off_cap,
                uint32_t* __restrict__ offs) {
+	walk_prio();
 	const uint64_t gid = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
 	if(gid >= nrange * off_cap) return;
 	const uint64_t k = gid / off_cap;
@@ -451,6 +459,7 @@ __device__ __forceinline__ bt2g_ext_out ext_one(const DevEbwt& F, const DevEbwt&
 __global__ void __launch_bounds__(256)
 k_extend(DevEbwt F, DevEbwt B, int has_bw, const uint8_t* __restrict__ reads, uint32_t stride,
          const uint32_t* __restrict__ lens, const bt2g_ext_in* __restrict__ in, uint32_t n, bt2g_ext_out* __restrict__ out) {
+	walk_prio();
 	const uint32_t k = blockIdx.x * blockDim.x + threadIdx.x;
 	if(k >= n) return;
 	const bt2g_ext_in q = in[k];
@@ -471,6 +480,7 @@ __global__ void __launch_bounds__(256)
 k_seed_extend(DevEbwt F, DevEbwt B, int has_bw, const uint8_t* __restrict__ reads, uint32_t stride,
               const uint32_t* __restrict__ lens, uint32_t n, uint32_t seedlen, uint32_t interval, uint32_t offset,
               uint32_t maxseeds, const uint32_t* __restrict__ out, bt2g_ext_out* __restrict__ ext) {
+	walk_prio();
 	const uint64_t gid = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
 	if(gid >= (uint64_t)n * 2 * maxseeds) return;
 	const uint32_t r = (uint32_t)(gid / (2u * maxseeds)), rem = (uint32_t)(gid % (2u * maxseeds));

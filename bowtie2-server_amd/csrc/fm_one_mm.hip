@@ -60,7 +60,8 @@ __device__ __forceinline__ void set4(uint32_t a[4], int i, uint32_t v) {
 __global__ void __launch_bounds__(256)
 k_one_mm_items(const uint8_t* __restrict__ reads, uint32_t stride, const uint32_t* __restrict__ lens, uint32_t n,
                const uint32_t* __restrict__ gate, int nofw, int norc, uint32_t* __restrict__ items,
-               uint32_t* __restrict__ nitems, int32_t* __restrict__ slot_counts) {
+               uint32_t* __restrict__ nitems, int32_t* __restrict__ slot_counts, uint32_t* __restrict__ ops,
+               uint32_t* __restrict__ loads, uint32_t* __restrict__ slot_flag) {
 	// one wave of 64 reads: their rows are contiguous, so the Ns are counted
 	// from coalesced dword loads (N = code 4: bit 2 of a byte) into per-read
 	// LDS counters
@@ -119,7 +120,12 @@ k_one_mm_items(const uint8_t* __restrict__ reads, uint32_t stride, const uint32_
 			const bool fw = (d >> 1) == 0;
 			if(!gated_off && ns <= 1 && !((fw && nofw_r) || (!fw && norc_r))) runmask |= 1u << d;
 			slot_counts[(size_t)r * 4 + d] = 0;
+			slot_flag[(size_t)r * 4 + d] = 0;
 		}
+		// the read's FM-op and side-load counters, accumulated by the walks after
+		// this kernel (were three memsets of the call's stream)
+		ops[r] = 0;
+		if(loads) loads[r] = 0;
 	}
 	// two lists by index direction (BWT: d even, BWT': d odd) so that each
 	// search launch reads one index with wave-uniform parameters
@@ -141,6 +147,7 @@ k_one_mm_near(DevEbwt F, DevEbwt B, const uint8_t* __restrict__ reads, uint32_t 
               const uint32_t* __restrict__ lens, const uint32_t* __restrict__ items,
               const uint32_t* __restrict__ nitems_p, uint4* __restrict__ st4, uint32_t* __restrict__ sdep,
               uint32_t* __restrict__ ops_out, uint32_t* __restrict__ loads_out) {
+	walk_prio();
 	const uint32_t qi = blockIdx.x * blockDim.x + threadIdx.x;
 	if(qi >= *nitems_p) return;
 	const DevEbwt& E = EBWTFW ? F : B;
@@ -216,6 +223,7 @@ k_one_mm_q(DevEbwt F, DevEbwt B, const uint8_t* __restrict__ reads, const uint8_
            const uint32_t* __restrict__ sdep, uint32_t cap, bt2g_mm1* __restrict__ slots, int32_t* __restrict__ slot_counts, uint32_t* __restrict__ ops_out,
            uint32_t* __restrict__ loads_out, MmBranch* __restrict__ brq, uint32_t* __restrict__ brq_n,
            uint32_t brq_cap) {
+	walk_prio();
 	const uint32_t nitems = *nitems_p;
 	const int64_t matchsc = (int64_t)((float)P.match + 0.5f);
 
@@ -477,6 +485,7 @@ k_one_mm_far(DevEbwt F, DevEbwt B, const uint8_t* __restrict__ reads, const uint
              uint32_t* __restrict__ brq_n, uint32_t brq_cap, uint32_t* __restrict__ fb_items,
              uint4* __restrict__ fb_st4, uint32_t* __restrict__ fb_sdep, uint32_t* __restrict__ fb_n,
              uint32_t* __restrict__ slot_flag) {
+	walk_prio();
 	const uint32_t qi = blockIdx.x * blockDim.x + threadIdx.x;
 	// Far-half branches are staged in LDS per wave and go to the global queue in
 	// one allocation and a coalesced copy when the wave is done: a global atomic
@@ -681,6 +690,7 @@ k_one_mm_branch(DevEbwt F, DevEbwt B, const uint8_t* __restrict__ reads, uint32_
                 const uint32_t* __restrict__ brq_n, uint32_t brq_cap, uint32_t cap, bt2g_mm1* __restrict__ slots,
                 int32_t* __restrict__ slot_counts, uint32_t* __restrict__ ops_out, uint32_t* __restrict__ loads_out,
                 const uint32_t* __restrict__ slot_flag) {
+	walk_prio();
 	const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
 	const uint32_t nq = *brq_n < brq_cap ? *brq_n : brq_cap;
 	if(i >= nq) return;
@@ -744,10 +754,9 @@ void launch_one_mm_q(const DevEbwt& F, const DevEbwt& B, const uint8_t* reads, c
 	hipStream_t s2 = two ? st2 : st;
 	// counters[0]/[2] = item counts of the BWT / BWT' lists (zeroed by the caller)
 	hipLaunchKernelGGL(k_one_mm_items, dim3((n + 255) / 256), dim3(256), 0, st, reads, stride, lens, n, gate, nofw,
-	                   norc, items, counters, slot_counts);
+	                   norc, items, counters, slot_counts, ops, loads, slot_flag);
 	const uint32_t grid = (2 * n + 255) / 256;   // list capacity; lanes past the count exit
 	const size_t half = 2 * (size_t)n;
-	(void)hipMemsetAsync(slot_flag, 0, sizeof(uint32_t) * (size_t)n * 4, st);
 	if(two) {
 		(void)hipEventRecord(ev[0], st);
 		(void)hipStreamWaitEvent(s2, ev[0], 0);

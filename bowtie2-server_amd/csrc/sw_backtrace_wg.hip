@@ -96,6 +96,7 @@ __device__ __forceinline__ uint32_t wave_sum_excl(uint32_t v, uint32_t lane) {
 }  // namespace
 
 __global__ void __launch_bounds__(64) k_sw_bt_wg(BtArgs A) {
+	walk_prio();
 	HIP_DYNAMIC_SHARED(uint4, s_wg)
 	const uint32_t p = blockIdx.x, lane = threadIdx.x;
 	if(p >= A.nprob) return;
