@@ -85,6 +85,7 @@ struct bt2g_ctx {
 	uint32_t* bt_marks = nullptr;
 	// the 1-mm search's second stream (the BWT' direction) and its fork/join events
 	hipStream_t aux = nullptr;
+	int prio = 0;                       // stream priority (bt2g_set_priority); 0 = default
 	hipEvent_t mm_ev[4] = {nullptr, nullptr, nullptr, nullptr};
 	// host-wrapper scratch (Arena): one device block reused call after call
 	uint8_t* arena = nullptr;
@@ -541,6 +542,32 @@ int bt2g_open_mem(const bt2g_index_mem* m, int device, bt2g_ctx** out) {
 	return BT2G_OK;
 }
 
+int bt2g_set_priority(bt2g_ctx* c, int high) {
+	if(!c) return fail(BT2G_ERR_ARG, "null ctx");
+	HIPCHK(hipSetDevice(c->device));
+	int least = 0, greatest = 0;
+	HIPCHK(hipDeviceGetStreamPriorityRange(&least, &greatest));
+	const int p = high ? greatest : 0;
+	if(p == c->prio) return BT2G_OK;
+	hipStream_t s = nullptr;
+	HIPCHK(hipStreamCreateWithPriority(&s, hipStreamNonBlocking, p));
+	if(c->stream) {
+		(void)hipStreamSynchronize(c->stream);
+		drain_prof(c);
+		(void)hipStreamDestroy(c->stream);
+	}
+	c->stream = s;
+	if(c->aux) {                        // made again, at the new priority, when next needed
+		(void)hipStreamSynchronize(c->aux);
+		(void)hipStreamDestroy(c->aux);
+		c->aux = nullptr;
+		for(hipEvent_t& e : c->mm_ev)
+			if(e) { (void)hipEventDestroy(e); e = nullptr; }
+	}
+	c->prio = p;
+	return BT2G_OK;
+}
+
 int bt2g_open_shared(bt2g_ctx* base, bt2g_ctx** out) {
 	if(!base || !out) return fail(BT2G_ERR_ARG, "null argument");
 	HIPCHK(hipSetDevice(base->device));
@@ -717,7 +744,7 @@ static int one_mm_impl(bt2g_ctx* c, const uint8_t* reads, const uint8_t* quals, 
 	hipStream_t st = pick(c, stream);
 	if(!c->aux) {
 		// the second direction's stream (created once; without it the directions run in turn)
-		bool ok = hipStreamCreateWithFlags(&c->aux, hipStreamNonBlocking) == hipSuccess;
+		bool ok = hipStreamCreateWithPriority(&c->aux, hipStreamNonBlocking, c->prio) == hipSuccess;
 		for(int i = 0; ok && i < 4; i++) ok = hipEventCreateWithFlags(&c->mm_ev[i], hipEventDisableTiming) == hipSuccess;
 		if(!ok) {
 			for(hipEvent_t& e : c->mm_ev)

@@ -101,6 +101,12 @@ int bt2g_open_mem(const bt2g_index_mem* m, int device, bt2g_ctx** out);
  * Contexts are not thread-safe; one thread drives each (the drop-in binding
  * gives every dispatcher thread its own, integration/bt2g_seams.cpp). */
 int bt2g_open_shared(bt2g_ctx* base, bt2g_ctx** out);
+/* Scheduling priority of the context's streams: high != 0 -> the device's
+ * highest stream priority (hipDeviceGetStreamPriorityRange), 0 -> the default.
+ * For a caller that runs latency-bound searches beside throughput-bound
+ * alignment on one device (the batch server's services; no reference
+ * counterpart -- the reference has no device).  Call between calls, not during. */
+int bt2g_set_priority(bt2g_ctx* ctx, int high);
 /* Release a context (a shared one first, then the index owner). */
 int bt2g_close(bt2g_ctx* ctx);
 /* out: [len, zoff_fw, zoff_bw, fchr0..4, ftab_chars, off_rate, num_sides,

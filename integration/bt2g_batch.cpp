@@ -4071,6 +4071,13 @@ void Driver::run_loop() {
 					int rc2 = bt2g_open_shared(g_bases[dev], &v->ctx);
 					if(rc2) die("bt2g_open_shared", rc2);
 					if(kprof_on()) (void)bt2g_set_profiling(v->ctx, 1);
+					// $BT2G_SVC_PRIO=1: the FM services' streams (exact sweep, seeds,
+					// offsets, ungapped: latency-bound dependent gathers) at the
+					// device's highest priority, the DP service's at the default
+					if(k != K_DP && env_or("BT2G_SVC_PRIO", 0) == 1) {
+						int rc3 = bt2g_set_priority(v->ctx, 1);
+						if(rc3) die("bt2g_set_priority", rc3);
+					}
 					if(!owner) owner = v;
 					v->q = owner;
 					owner->workers.push_back(v);

@@ -88,6 +88,11 @@ int bt2g_open(const char* base, int, bt2g_ctx** out) {
 	return BT2G_OK;
 }
 
+int bt2g_set_priority(bt2g_ctx* c, int high) {
+	(void)high;
+	return c ? BT2G_OK : fail(BT2G_ERR_ARG, "null ctx");
+}
+
 int bt2g_open_shared(bt2g_ctx* base, bt2g_ctx** out) {
 	if(!base || !out) return fail(BT2G_ERR_ARG, "null argument");
 	bt2g_ctx* c = new bt2g_ctx();
