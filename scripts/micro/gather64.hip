@@ -101,6 +101,23 @@ int main() {
 		printf("%-34s %8.3f ms  %7.2f G gathers/s  %7.1f GB/s (64 B each)\n", name, best, gathers / best / 1e6,
 		       gathers * 64 / best / 1e6);
 	};
+	// the latency of one dependent 64-B gather: few waves (one per workgroup), a
+	// long chain -- what an LF walk over a small batch sees step by step
+	for(uint32_t waves : {16u, 256u, 1024u}) {
+		const uint32_t iters = 2000;
+		float best = 1e9f;
+		for(int rep = 0; rep < 3; rep++) {
+			(void)hipEventRecord(e0);
+			hipLaunchKernelGGL(k_chain, dim3(waves), dim3(64), 0, 0, t, nside, iters, o);
+			(void)hipEventRecord(e1);
+			(void)hipEventSynchronize(e1);
+			float ms;
+			(void)hipEventElapsedTime(&ms, e0, e1);
+			if(rep && ms < best) best = ms;
+		}
+		printf("chain latency %5u waves x 64 lanes  %8.3f ms  %6.3f us per dependent step\n", waves, best,
+		       best * 1e3 / iters);
+	}
 	for(int blocksPerCU : {4, 8, 16}) {
 		const uint32_t blocks = 256 * blocksPerCU, iters = 64;
 		const double g = (double)blocks * 256 * iters;
