@@ -33,14 +33,22 @@ k_exact_sweep(DevEbwt e, const uint8_t* __restrict__ reads, uint32_t stride, con
 	// the LF loop's base at depth dep: fw row[len-dep-1], rc comp(row[dep]), via a register window
 	ReadWin rw{reads, reads + (size_t)n * stride};
 	const uint8_t* row = seq.p;
-	auto base_at = [&](uint32_t d) -> int {
-		const int c = rw.at(row + (strand == 1 ? d : len - d - 1));
+	// seq[k] through the window: fw row[k], rc comp(row[len-1-k])
+	auto seq_at = [&](uint32_t k) -> int {
+		const int c = rw.at(row + (strand == 1 ? len - 1 - k : k));
 		return strand == 1 ? (c > 3 ? 4 : 3 - c) : c;
 	};
+	auto base_at = [&](uint32_t d) -> int { return seq_at(len - d - 1); };
 	const uint32_t flen = e.ftab_chars;
 	uint32_t dep = 0, nedit = 0, top = 0, bot = 0, mine = 0;
 	uint32_t bwops = 0, loads = 0;
 	bool doinit = true, done = !active;
+	// (r05v: on an idle GPU a launch of 256-540 reads took 0.385 ms, 2.6 us per
+	// step against 0.61 us for one dependent 64-B gather: the ftab characters were
+	// byte loads one after another, the two ftab words and their eftab entries
+	// were waited for in turn, and the single-row and range steps had a side-load
+	// site each -- a wave whose lanes took both paid two latencies a step.  Now
+	// every load of a step is issued before any of them is waited for.)
 	while(dep < len && !done) {
 		if(doinit) {
 			top = bot = 0;
@@ -50,17 +58,22 @@ k_exact_sweep(DevEbwt e, const uint8_t* __restrict__ reads, uint32_t stride, con
 			if(doftab) {
 				// ftabSeqToInt(seq, left-flen, rev=false) on the forward index
 				for(uint32_t i = 0; i < flen; i++) {
-					int c = seq[left - flen + i];
+					int c = seq_at(left - flen + i);
 					if(c > 3) { doftab = false; break; }
 					fi = (fi << 2) | (uint32_t)c;
 				}
 			}
 			if(doftab) {
-				top = ftab_hi(e, fi);
-				bot = ftab_lo(e, fi + 1);
+				// ftab_hi(fi), ftab_lo(fi + 1): both words, then both eftab entries
+				const uint32_t v0 = e.ftab[fi], v1 = e.ftab[fi + 1];
+				const bool x0 = v0 > e.len, x1 = v1 > e.len;
+				const uint32_t et = x0 ? e.eftab[(v0 ^ BT2G_OFF_MASK) * 2 + 1] : v0;
+				const uint32_t eb = x1 ? e.eftab[(v1 ^ BT2G_OFF_MASK) * 2] : v1;
+				top = et;
+				bot = eb;
 				dep += flen;
 			} else {
-				int c = seq[len - dep - 1];
+				int c = seq_at(len - dep - 1);
 				if(c < 4) { top = fchr_at(e, c); bot = fchr_at(e, c + 1); }
 				dep++;
 			}
@@ -73,34 +86,29 @@ k_exact_sweep(DevEbwt e, const uint8_t* __restrict__ reads, uint32_t stride, con
 		}
 		if(dep < len) {
 			const int c = base_at(dep);
+			const bool rng = bot - top > 1;
+			const uint32_t st = top / 192u, sb = rng ? bot / 192u : st;
+			// the step's sides, issued together (the second is the first again
+			// for a single row or a range inside one side: a hit on the same
+			// line); both paths read both, so neither load sinks into one path
+			SideData s1, s2;
+			load_side(e, st, s1);
+			load_side(e, sb, s2);
 			if(c > 3) {
 				top = bot = 0;
-			} else if(bot - top > 1) {
+			} else if(rng) {
 				bwops += 2;
-				uint32_t st = top / 192u, sb = bot / 192u;
-				SideData s1;
-				load_side(e, st, s1);
-				loads++;
-				uint32_t nt = occ1(e, s1, top, c), nb;
-				if(sb == st) {
-					nb = occ1(e, s1, bot, c);
-				} else {
-					SideData s2;
-					load_side(e, sb, s2);
-					loads++;
-					nb = occ1(e, s2, bot, c);
-				}
+				loads += sb == st ? 1u : 2u;
+				const uint32_t nt = occ1(e, s1, top, c), nb = occ1(e, s2, bot, c);
 				top = nt; bot = nb;
 			} else {
 				bwops += 1;
-				SideData s1;
-				load_side(e, top / 192u, s1);
 				loads++;
 				uint32_t co = top % 192u;
 				if(side_rowL(s1, co) != c || top == e.zoff) {
 					top = bot = 0;
 				} else {
-					top = occ1(e, s1, top, c);
+					top = occ1(e, s2, top, c);     // (s2 holds side st here)
 					bot = top + 1;
 				}
 			}

@@ -26,9 +26,17 @@ def main():
     import bench
     import bt2_index as bi
     import bt2g
+    import tempfile
     t0 = time.time()
     parts, names = bench.make_genome(a.mb)
-    idx = bi.build_index_device(parts, names=names, device="cuda:0")
+    # (bench.py's index cache: a bench run after this one in the same call reads it)
+    cache = os.path.join(tempfile.gettempdir(), "bt2g_bench_index", f"hg38like_{a.mb:g}mb", "g")
+    if os.path.exists(cache + ".rev.2.bt2"):
+        idx = bi.read_index(cache)
+    else:
+        idx = bi.build_index_device(parts, names=names, device="cuda:0")
+        os.makedirs(os.path.dirname(cache), exist_ok=True)
+        bi.write_index(cache, idx)
     print(f"index {a.mb:.0f} Mbp in {time.time() - t0:.0f} s", flush=True)
     reads, quals = bench.make_reads(parts, 65536, 150, 3)
     lens = np.full(len(reads), 150, np.uint32)
