@@ -191,24 +191,33 @@ struct BiRange {
 __device__ __forceinline__ int bi_step(const DevEbwt& e, uint32_t top, uint32_t bot, uint32_t topp,
                                        uint32_t t[4], uint32_t b[4], uint32_t tp[4], uint32_t bp[4]) {
 	uint32_t st = top / 192u, sb = bot / 192u;
+	int loads = sb == st ? 1 : 2;
+#ifndef BT2G_LEAN_BISTEP
+	// both sides issued before either is consumed: one memory latency per step
+	// (the second is the first again when both rows share a side: a hit on the
+	// line in flight).  r05w: the split form paid two latencies whenever a
+	// wave's lanes had both cases.
+	SideData s1, s2;
+	load_side(e, st, s1);
+	load_side(e, sb, s2);
+	occ4(e, s1, top, t);
+	occ4(e, s2, bot, b);
+#else
 	SideData s1;
 	load_side(e, st, s1);
 	occ4(e, s1, top, t);
-	int loads = 1;
 	if(sb == st) {
 		occ4(e, s1, bot, b);
 	} else {
-#ifdef BT2G_LEAN_BISTEP
 		// second side only after the first is consumed: one SideData live
 		uint32_t z;
 		asm volatile("v_mov_b32 %0, 0" : "=v"(z) : "v"(t[0]), "v"(t[3]));
 		sb += z;
-#endif
 		SideData s2;
 		load_side(e, sb, s2);
 		occ4(e, s2, bot, b);
-		loads = 2;
 	}
+#endif
 	bp[0] = tp[0] + (b[0] - t[0]);
 	tp[1] = bp[0];
 	bp[1] = tp[1] + (b[1] - t[1]);
@@ -223,17 +232,12 @@ __device__ __forceinline__ int bi_step(const DevEbwt& e, uint32_t top, uint32_t 
 // them: mirror top of character j = topp + sum of the range sizes below j)
 __device__ __forceinline__ int bi_step_tb(const DevEbwt& e, uint32_t top, uint32_t bot, uint32_t t[4], uint32_t b[4]) {
 	const uint32_t st = top / 192u, sb = bot / 192u;
-	SideData s1;
+	SideData s1, s2;
 	load_side(e, st, s1);
+	load_side(e, sb, s2);     // (as bi_step: both issued, then both consumed)
 	occ4(e, s1, top, t);
-	if(sb == st) {
-		occ4(e, s1, bot, b);
-		return 1;
-	}
-	SideData s2;
-	load_side(e, sb, s2);
 	occ4(e, s2, bot, b);
-	return 2;
+	return sb == st ? 1 : 2;
 }
 
 // A read (or its reverse complement / reversal) as the reference's BTDnaString
