@@ -568,6 +568,34 @@ int bt2g_set_priority(bt2g_ctx* c, int high) {
 	return BT2G_OK;
 }
 
+int bt2g_set_cu_share(bt2g_ctx* c, uint32_t num, uint32_t den) {
+	if(!c) return fail(BT2G_ERR_ARG, "null ctx");
+	HIPCHK(hipSetDevice(c->device));
+	int ncu = 0;
+	HIPCHK(hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, c->device));
+	hipStream_t s = nullptr;
+	if(den == 0 || num >= den) {
+		HIPCHK(hipStreamCreateWithPriority(&s, hipStreamNonBlocking, c->prio));
+	} else {
+		std::vector<uint32_t> mask((size_t)(ncu + 31) / 32, 0u);
+		int kept = 0;
+		for(int i = 0; i < ncu; i++)
+			if((uint32_t)i % den < num) {
+				mask[(size_t)i / 32] |= 1u << (i % 32);
+				kept++;
+			}
+		if(kept == 0) return fail(BT2G_ERR_ARG, "CU share %u/%u keeps no CU", num, den);
+		HIPCHK(hipExtStreamCreateWithCUMask(&s, (uint32_t)mask.size(), mask.data()));
+	}
+	if(c->stream) {
+		(void)hipStreamSynchronize(c->stream);
+		drain_prof(c);
+		(void)hipStreamDestroy(c->stream);
+	}
+	c->stream = s;
+	return BT2G_OK;
+}
+
 int bt2g_open_shared(bt2g_ctx* base, bt2g_ctx** out) {
 	if(!base || !out) return fail(BT2G_ERR_ARG, "null argument");
 	HIPCHK(hipSetDevice(base->device));

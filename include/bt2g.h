@@ -107,6 +107,11 @@ int bt2g_open_shared(bt2g_ctx* base, bt2g_ctx** out);
  * alignment on one device (the batch server's services; no reference
  * counterpart -- the reference has no device).  Call between calls, not during. */
 int bt2g_set_priority(bt2g_ctx* ctx, int high);
+/* Confine the context's stream to `num` of every `den` compute units (CU i is
+ * used iff i % den < num; num >= den or den == 0: every CU, the default), so
+ * that long launches on it leave CUs to other contexts' short ones (the batch
+ * server's DP service beside its FM services).  Call between calls. */
+int bt2g_set_cu_share(bt2g_ctx* ctx, uint32_t num, uint32_t den);
 /* Release a context (a shared one first, then the index owner). */
 int bt2g_close(bt2g_ctx* ctx);
 /* out: [len, zoff_fw, zoff_bw, fchr0..4, ftab_chars, off_rate, num_sides,

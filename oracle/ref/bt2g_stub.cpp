@@ -93,6 +93,12 @@ int bt2g_set_priority(bt2g_ctx* c, int high) {
 	return c ? BT2G_OK : fail(BT2G_ERR_ARG, "null ctx");
 }
 
+int bt2g_set_cu_share(bt2g_ctx* c, uint32_t num, uint32_t den) {
+	(void)num;
+	(void)den;
+	return c ? BT2G_OK : fail(BT2G_ERR_ARG, "null ctx");
+}
+
 int bt2g_open_shared(bt2g_ctx* base, bt2g_ctx** out) {
 	if(!base || !out) return fail(BT2G_ERR_ARG, "null argument");
 	bt2g_ctx* c = new bt2g_ctx();
