@@ -4078,16 +4078,17 @@ void Driver::run_loop() {
 						int rc3 = bt2g_set_priority(v->ctx, 1);
 						if(rc3) die("bt2g_set_priority", rc3);
 					}
-					// $BT2G_DP_CU="num/den" (default 7/8; "0/0": every CU): the DP
-					// service's streams on num of every den CUs, the rest left to the FM
-					// services' short launches.  r05ae, --local: its one-walker backtrace
-					// launches (~10 ms) had filled the device and the one-mm family waited
-					// for CUs, 5.2 ms per launch -> 1.7 ms, 71.4 k -> 88.2 k aligned
-					// reads/s (3/4: 85.4 k); r05af, end-to-end: 202.2 k -> 205.3 k (3/4:
-					// 199.6 k), within the box's spread
+					// $BT2G_DP_CU="num/den" (default 7/8 with --local, else every CU;
+					// "0/0": every CU): the DP service's streams on num of every den CUs,
+					// the rest left to the FM services' short launches.  r05ae, --local:
+					// its one-walker backtrace launches (~10 ms) had filled the device and
+					// the one-mm family waited for CUs, 5.2 ms per launch -> 1.7 ms, 71.4 k
+					// -> 88.2 k aligned reads/s (3/4: 85.4 k); r05af, end-to-end: 202.2 k
+					// -> 205.3 k (3/4: 199.6 k), within the box's spread; r05ag, paired:
+					// 107.9 k -> 65.0 k pairs/s (the DP call's span 2.0 -> 4.3 ms)
 					if(k == K_DP) {
 						static const std::pair<unsigned, unsigned> share = [] {
-							unsigned a = 7, b = 8;
+							unsigned a = R_localAlign ? 7 : 0, b = R_localAlign ? 8 : 0;
 							if(const char* e = getenv("BT2G_DP_CU"))
 								if(sscanf(e, "%u/%u", &a, &b) != 2) a = b = 0;
 							return std::make_pair(a, b);
