@@ -375,7 +375,7 @@ class Pipeline:
         self.inv[sel] = torch.arange(m, dtype=torch.int32, device=self.dev)
         self.counters.zero_()
         P = self._p
-        chk(L.bt2g_bench_collect_rows_dev(n, P(self.lens), P(self.sweep), P(self.mm_hits), P(self.mm_cnt),
+        chk(self.bt2g.bench_lib().bt2g_bench_collect_rows_dev(n, P(self.lens), P(self.sweep), P(self.mm_hits), P(self.mm_cnt),
                                           self.mm_cap, P(self.seeds), P(self.inv), self.maxseeds, pol.seedlen,
                                           pol.interval,
                                           P(self.rows), P(self.meta), P(self.read_base), P(self.read_cnt),
@@ -387,7 +387,7 @@ class Pipeline:
         self._mark("offsets")
         # 6. joinedToTextOff + straddle filter, <= 2 diagonals per read (device), framed by
         #    frameSeedExtensionRect (bt2g_frame_dev kind 0)
-        chk(L.bt2g_bench_frame_dev(n, P(self.lens), P(self.offs), P(self.meta), P(self.read_base),
+        chk(self.bt2g.bench_lib().bt2g_bench_frame_dev(n, P(self.lens), P(self.offs), P(self.meta), P(self.read_base),
                                    P(self.read_cnt), P(self.fr[0]), P(self.fr[1]), P(self.fr[2]), P(self.fr[3]),
                                    self.nfrag, pol.minsc, P(self.fin0),
                                    P(self.counters[1:]), self.max_probs, S))
@@ -508,8 +508,8 @@ def pmc_traffic(fetch_csv, write_csv, kernel):
 BATCH_SERVER = os.path.join(ROOT, "integration", "bin", "bowtie2-align-server-batch")
 # HBM traffic per launch of the batch server's kernels: the summary of separate
 # rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes over this same bench command
-# (scripts/gpu_r04.sh benchpmc -> scripts/pmc_summary.py), committed under profiles/
-SERVER_PMC = os.path.join(ROOT, "profiles", "r05", "server_pmc.json")
+# (scripts/gpu_r06.sh prof -> scripts/pmc_summary.py), committed under profiles/
+SERVER_PMC = os.path.join(ROOT, "profiles", "r06", "server_pmc.json")
 
 
 def server_traffic(path, kernel):
@@ -556,6 +556,9 @@ SERVER_KERNELS = [("exact_sweep", 0, "k_exact_sweep", "hbm"),
                   ("ungapped", 6, "k_ungapped", None), ("sw_dp", 4, "k_sw_sys (fill, with the candidate gather)", "valu"),
                   ("sw_dp", 11, "k_sort_small / k_sort_big (candidate sort)", None),
                   ("sw_dp", 5, "k_sw_bt_wg / k_sw_bt (nextAlignment loop)", None),
+                  ("sw_dp", 8, "host: the DP call's staging (packing into pinned memory)", "span"),
+                  ("sw_dp", 9, "host: the DP call's enqueueing (copies and launches)", "span"),
+                  ("sw_dp", 10, "host: the DP call's wait and copy out", "span"),
                   ("sw_dp", 7, "the DP call's whole stream span (copies, fill, walk, pack)", "span")]
 
 
@@ -629,14 +632,99 @@ def server_kernels(st):
 # branch / compact launches): a family, not one kernel
 FAMILY_IDS = {("exact_sweep", 2), ("one_mm", 2)}
 
+# kernel-name prefixes of each id in a rocprofv3 --pmc summary (the 1-mm family's
+# kernels serve both the sweep's fused call and the rare standalone 1-mm call)
+PMC_NAMES = {"exact_sweep:0": ("k_exact_sweep",), "exact_sweep:2": ("k_one_mm_",), "one_mm:2": ("k_one_mm_",),
+             "exact_sweep:3": ("k_range_offsets",), "seed_search:1": ("k_seed_search",),
+             "seed_search:12": ("k_seed_extend",), "seed_search:3": ("k_seed_offsets",),
+             "get_offset:3": ("k_get_offset",), "extend:12": ("k_extend",), "ungapped:6": ("k_ungapped",),
+             "sw_dp:4": ("k_sw_sys",), "sw_dp:5": ("k_sw_bt",), "sw_dp:11": ("k_sort_",)}
+
 
 def dominant_kernel(kern):
-    """The single kernel with the largest total time over the run (the DP call's
-    stream span and multi-kernel families are not one kernel; their shares are
-    in server_kernels) -- the kernel rocprofv3's summary of the same command
-    ranks first, whose average duration the line's ms_per_launch must match."""
-    ks = [k for k in kern if not kern[k].get("span") and not kern[k].get("family")]
+    """The kernel -- or multi-kernel family, such as the 1-mm search's five
+    launches per call -- with the largest total time over the run (the DP call's
+    whole stream span is not one kernel).  round 6: families are candidates
+    (the 1-mm family was the largest GPU consumer, ~28 % of kernel
+    time, and the line named k_sw_sys)."""
+    ks = [k for k in kern if not kern[k].get("span")]
     return max(ks, key=lambda k: kern[k]["ms_total"], default=None)
+
+
+def work_by_kernel(st):
+    """{kind:id: [algorithmic work total, items]} of a run's server statistics
+    (bytes for the FM kernels, DP cells for the fill): with a --pmc pass of the
+    same command, the PMC-to-algorithmic traffic ratio of every kernel."""
+    out = {}
+    for kind, kid, _name, _bound in SERVER_KERNELS:
+        row = (((st or {}).get("kernels") or {}).get(kind) or {}).get("ids")
+        if row and len(row[kid]) > 3 and row[kid][2]:
+            out[f"{kind}:{kid}"] = [row[kid][2], row[kid][3]]
+    return out
+
+
+def pmc_ratio(path, key):
+    """(HBM bytes per algorithmic byte, note) of kernel id `key` from a
+    pmc_summary.py file that carries the algorithmic work of its own passes:
+    FETCH_SIZE x 2 over every dispatch of the id's kernels in the FETCH pass,
+    over the algorithmic bytes the server counted in that pass, plus the same
+    for WRITE_SIZE in the WRITE pass (each --pmc pass is its own run of the
+    same bench command)."""
+    try:
+        d = json.load(open(path))
+    except (OSError, ValueError):
+        return None, None
+    works = d.get("work_by_kernel") or {}
+    names = PMC_NAMES.get(key)
+    if not names or not all(key in (works.get(c) or {}) for c in ("fetch", "write")):
+        return None, None
+
+    def alg(c):                     # the id's work, with the ids sharing its kernels
+        w = works[c]
+        return sum(w[k][0] for k in w if k == key or PMC_NAMES.get(k) == names)
+
+    fx2, wr, nd = 0.0, 0.0, 0
+    for name, v in d.get("kernels", {}).items():
+        if not any(name.startswith(p) for p in names):
+            continue
+        if v.get("fetch_bytes_x2") is None or v.get("write_bytes") is None:
+            continue
+        fx2 += v["fetch_bytes_x2"] * v["dispatches"]
+        wr += v["write_bytes"] * v["dispatches"]
+        nd += v["dispatches"]
+    if not nd or not alg("fetch") or not alg("write"):
+        return None, None
+    ratio = fx2 / alg("fetch") + wr / alg("write")
+    note = (f"{os.path.relpath(path, ROOT)}: FETCH_SIZE x 2 + WRITE_SIZE over {nd} dispatches of "
+            f"{'/'.join(names)}* in separate rocprofv3 --pmc passes of bench.py, each over the algorithmic bytes the "
+            f"server counted in the same pass (ratio {ratio:.2f}; traffic = ratio x this run's bytes per launch)")
+    lib = os.path.join(PKG, "libbt2g.so")
+    want = (d.get("build_sha256") or {}).get("bowtie2-server_amd/libbt2g.so")
+    if want is None:
+        note += "; STALE? the summary records no build"
+    elif os.path.exists(lib) and binary_id(lib)["sha256"] != want:
+        note += "; STALE: taken on another build of libbt2g.so than the one benchmarked"
+    return ratio, note
+
+
+def roofline_entry(kern, key, server_pmc):
+    """The line's roofline object for kernel id `key` of server_kernels."""
+    d = kern[key]
+    ratio, tnote = pmc_ratio(server_pmc, key)
+    per = (d.get("bytes_total") or d.get("cells_total")) / d["launches"]
+    if ratio is not None and d["bound"] == "hbm":
+        traffic = ratio * per
+    elif d.get("family"):
+        ratio, traffic, tnote = None, None, "no PMC summary with this run's algorithmic work (work_by_kernel)"
+    else:
+        ratio = None
+        traffic, tnote = server_traffic(server_pmc, PMC_KERNEL.get(int(key.split(":")[1]), "?"))
+    return {"bound": d["bound"], "kernel": d["kernel"], "family": bool(d.get("family")), "achieved": d["achieved"],
+            "peak": d["peak"], "unit": d["unit"], "frac": d["frac"], "traffic": traffic, "traffic_ratio": ratio,
+            "traffic_source": tnote, "ms_per_launch": d["ms_per_launch"], "launches": d["launches"],
+            "ms_total": d["ms_total"],
+            "share_of_kernel_time": d["ms_total"] / sum(v["ms_total"] for v in kern.values() if not v.get("span")),
+            "per_launch_work": per, "work_unit": "bytes" if d["bound"] == "hbm" else "DP cells"}
 
 
 # host memory of one batch server (r05d, 16 drivers, hg38-like genome): ~12 GB
@@ -704,6 +792,9 @@ def schedule_run(args, rank, world, local, base, reads_np, quals_np, workdir, bi
         # hipEventRecord of ProfScope::~ProfScope, DP service threads) -- off unless
         # $BT2G_BENCH_KPROF=1
         env["BT2G_KPROF"] = os.environ.get("BT2G_BENCH_KPROF", "0")
+        # (the algorithmic work by kernel id is still counted: a --pmc pass sets its
+        # counters against the work of the same dispatches, bench.pmc_ratio)
+        env["BT2G_KWORK"] = "1"
     multi = world > 1 and dist.is_initialized()
     with rs.Server(base, threads=args.drivers, args=policy_args(args.mode, args.preset), binary=binary,
                    env=env, log_path=os.path.join(workdir, "server.log"), prefix=prefix) as srv:
@@ -715,25 +806,40 @@ def schedule_run(args, rank, world, local, base, reads_np, quals_np, workdir, bi
         if gpu:
             torch.cuda.synchronize()
         rss = [srv.last_rss_gb]                 # after the warmup, then after every timed pass
+        native = os.path.basename(client) == os.path.basename(rs.NATIVE_CLIENT)
         t0 = time.perf_counter()
         aligned, outs, cpu_s, client_s, host_s, thr_s, run_s = 0, None, 0.0, 0.0, 0.0, 0.0, 0.0
+        pass_s, client_aligned = [], []
         for i in range(args.steps):
-            dt_i, outs = srv.run(chunks, k=args.clients, client=client)
+            last = i + 1 == args.steps
+            # (the aligned reads of a pass are counted by the native client as the SAM
+            # arrives; only the last pass's SAM is kept, for sam_parity, and counted
+            # again here after the timed region -- counting 1 M records in Python took
+            # ~1 s per pass, inside the timed region, with the server idle)
+            dt_i, outs = srv.run(chunks, k=args.clients, client=client, keep=last or not native)
             cpu_s += srv.last_cpu_s
             client_s += srv.last_client_cpu_s
             host_s += srv.last_host_cpu_s
             thr_s += srv.last_throttled_s
             run_s += dt_i
+            pass_s.append(dt_i)
             rss.append(srv.last_rss_gb)
-            aligned += count_aligned(outs, paired)
-            if i + 1 < args.steps:
-                outs = None                     # (only the last pass's SAM is kept)
-            log(f"[rank {rank}] pass {i + 1}/{args.steps}: server RSS {rss[-1]:.1f} GB")
+            if native:
+                client_aligned.append(srv.last_aligned)
+                aligned += srv.last_aligned
+            else:
+                aligned += count_aligned(outs, paired)
+            log(f"[rank {rank}] pass {i + 1}/{args.steps}: {dt_i:.3f} s, server RSS {rss[-1]:.1f} GB")
         if gpu:
             torch.cuda.synchronize()
         if multi:
             dist.barrier()
         elapsed = time.perf_counter() - t0
+        if native and outs is not None:
+            # the client's count of the last pass against the SAM it returned
+            py = count_aligned(outs, paired)
+            if py != client_aligned[-1]:
+                raise RuntimeError(f"aligned count: client {client_aligned[-1]} vs SAM {py}")
         threads_cpu = srv.last_threads
         smaps = srv.smaps_top()
     st = None
@@ -747,7 +853,7 @@ def schedule_run(args, rank, world, local, base, reads_np, quals_np, workdir, bi
         time.sleep(0.1)
     return {"elapsed": elapsed, "aligned": aligned, "outs": outs, "chunks": chunks, "stats": st, "slots_per_driver": slots,
             "server_cpu_s": cpu_s, "client_cpu_s": client_s, "host_cpu_s": host_s, "throttled_s": thr_s,
-            "passes_s": run_s, "server_threads_cpu": threads_cpu, "server_rss_gb": rss[-1],
+            "passes_s": run_s, "pass_s": pass_s, "server_threads_cpu": threads_cpu, "server_rss_gb": rss[-1],
             "server_rss_gb_per_pass": rss, "binary": binary_id(binary), "client": binary_id(client),
             "smaps_top": smaps}
 
@@ -780,34 +886,46 @@ def binary_id(path):
 def stock_baseline(args, base, chunks, batch_outs, workdir):
     """cpu_baseline: the stock reference server (oracle/_ref/bowtie2-align-server-s,
     built from /root/reference by oracle/ref/Makefile, -p <usable cores>) on
-    the first args.stock_sample reads of the same chunks, same k and warmup;
-    its sorted SAM against the batch server's for those chunks."""
+    the first args.stock_sample reads of the same chunks, same k and warmup,
+    through the reference's own client (bowtie2-align-l, one process per
+    connection); args.stock_runs timed runs, the median reported (BASELINE.md
+    section 3).  Its sorted SAM against the batch server's for those chunks
+    (which bt2g-client received): the engines and the client are checked
+    against the reference server and client together."""
     from oracle import ref_server as rs
     host = rs.host_cpus()
     threads = args.cpu_threads or host["usable"]
     m = max(1, min(len(chunks), (args.stock_sample + rs.CHUNK - 1) // rs.CHUNK))
     sample = chunks[:m]
     paired = args.mode == "paired"
+    runs = []
     with rs.Server(base, threads=threads, args=policy_args(args.mode, args.preset), binary=rs.SERVER,
                    log_path=os.path.join(workdir, "server_stock.log")) as srv:
         for _ in range(args.warmup):
             srv.run(sample[:min(args.warmup_chunks, m)] if args.warmup_chunks > 0 else sample, k=args.clients)
-        dt, outs = srv.run(sample, k=args.clients)
-        cpu_s = srv.last_cpu_s
-        client_s = srv.last_client_cpu_s
+        for _ in range(max(1, getattr(args, "stock_runs", 3))):
+            dt, outs = srv.run(sample, k=args.clients)
+            runs.append({"seconds": dt, "aligned": count_aligned(outs, paired), "server_cpu_s": srv.last_cpu_s,
+                         "client_cpu_s": srv.last_client_cpu_s})
     a, b = rs.sorted_records(outs), rs.sorted_records(batch_outs[:m])
     differ = sum(1 for x, y in zip(a, b) if x != y) + abs(len(a) - len(b))
     nreads = min(args.reads, m * rs.CHUNK)
     unit = "read pairs/s" if paired else "reads/s"
-    return {"value": count_aligned(outs, paired) / dt, "unit": "aligned " + unit, "cores": threads,
-            "kind": "reference", "host": host, "reads_per_s": nreads / dt, "seconds": dt, "server_cpu_s": cpu_s,
-            "client_cpu_s": client_s,
+    med = sorted(runs, key=lambda r: r["seconds"])[len(runs) // 2]
+    dt = med["seconds"]
+    return {"value": med["aligned"] / dt, "unit": "aligned " + unit, "cores": threads,
+            "kind": "reference", "host": host, "reads_per_s": nreads / dt, "seconds": dt,
+            "server_cpu_s": med["server_cpu_s"], "client_cpu_s": med["client_cpu_s"],
+            "runs": [{"value": r["aligned"] / r["seconds"], "seconds": r["seconds"]} for r in runs],
             "sample": f"the stock reference server (bowtie2-align-server-s built from the reference's sources, "
                       f"-p {threads} = the usable cores of this host, {host['model']}) on the first {nreads} "
-                      f"{'pairs' if paired else 'reads'} of the batch, <= 10 000 per client connection, "
-                      f"{args.clients} connections at a time, after {args.warmup} warmup pass(es) over "
-                      f"{min(args.warmup_chunks, m) if args.warmup_chunks > 0 else m} chunk(s)"}, \
-        {"sample_reads": nreads, "records": len(a), "records_differing": differ, "identical": differ == 0}
+                      f"{'pairs' if paired else 'reads'} of the batch through the reference client "
+                      f"(bowtie2-align-l), <= 10 000 per client connection, {args.clients} connections at a time, "
+                      f"after {args.warmup} warmup pass(es) over "
+                      f"{min(args.warmup_chunks, m) if args.warmup_chunks > 0 else m} chunk(s); median of "
+                      f"{len(runs)} timed runs"}, \
+        {"sample_reads": nreads, "records": len(a), "records_differing": differ, "identical": differ == 0,
+         "batch_client": "integration/bin/bt2g-client", "stock_client": "oracle/_ref/bowtie2-align-l"}
 
 
 def combine_ranks(elapsed, n_aligned, dev, eng=None):
@@ -1159,6 +1277,9 @@ def main():
     ap.add_argument("--server-pmc", default=SERVER_PMC, help="pmc_summary.py file for the batch server's kernels "
                     "(roofline.traffic)")
     ap.add_argument("--pmc-write", default="", help="same for WRITE_SIZE")
+    ap.add_argument("--allow-fallbacks", action="store_true",
+                    help="do not fail the run when the server's reference-CPU fallbacks served requests")
+    ap.add_argument("--stock-runs", type=int, default=3, help="timed runs of the stock server's sample (median)")
     args = ap.parse_args()
 
     import torch
@@ -1246,22 +1367,29 @@ def main():
     if rank == 0:
         unit = "read pairs/s" if args.mode == "paired" else "reads/s"
         st = sched["stats"] or {}
-        rl = None
+        rl, rls = None, []
         if dom_k and "achieved" in kern[dom_k]:
-            d = kern[dom_k]
-            traffic, tnote = server_traffic(args.server_pmc, PMC_KERNEL.get(int(dom_k.split(":")[1]), "?"))
-            rl = {"bound": d["bound"], "kernel": d["kernel"], "achieved": d["achieved"], "peak": d["peak"],
-                  "unit": d["unit"], "frac": d["frac"], "traffic": traffic, "traffic_source": tnote,
-                  "ms_per_launch": d["ms_per_launch"], "launches": d["launches"], "ms_total": d["ms_total"],
-                  "share_of_kernel_time": d["ms_total"] / sum(v["ms_total"] for v in kern.values()
-                                                              if not v.get("span")),
-                  "per_launch_work": (d.get("bytes_total") or d.get("cells_total")) / d["launches"],
-                  "work_unit": "bytes" if d["bound"] == "hbm" else "DP cells",
-                  "note": "kernel times: HIP events around every launch of the batch server's engine services "
-                          "over warmup + timed passes (BT2G_KPROF); per-launch work: the algorithmic figure of "
-                          "SURVEY.md 8(d) for the requests of each call.  Latency-bound here: the batch "
+            rl = roofline_entry(kern, dom_k, args.server_pmc)
+            rl["note"] = ("kernel times: HIP events around every launch of the batch server's engine services "
+                          "over warmup + timed passes (BT2G_KPROF); a family's time is its call's launches from "
+                          "the first kernel's start to the last one's end; per-launch work: the algorithmic figure "
+                          "of SURVEY.md 8(d) for the requests of each call.  Latency-bound here: the batch "
                           "server's calls carry a round's requests (hundreds to a few thousand items); the "
-                          "throughput regime of the same kernels is kernel_chain.roofline"}
+                          "throughput regime of the same kernels is kernel_chain.roofline")
+        # every kernel (family) with a bound, largest total time first
+        for k in sorted(kern, key=lambda k: -kern[k]["ms_total"]):
+            if "achieved" in kern[k]:
+                e = roofline_entry(kern, k, args.server_pmc)
+                rls.append({"id": k, **{x: e[x] for x in ("kernel", "bound", "frac", "achieved", "unit",
+                                                          "ms_per_launch", "share_of_kernel_time", "traffic",
+                                                          "traffic_ratio", "per_launch_work")}})
+        calls = {k: st.get(k) for k in ("exact_sweep", "one_mm", "seed_search", "extend", "get_offset", "ungapped",
+                                        "sw_dp")}
+        # the reference's CPU code inside the product server (bt2g_batch.cpp's live
+        # fallbacks: exactSweep, oneMmSearch, ungappedAlign, SwAligner::align,
+        # Ebwt::getOffset) must not have served any request of the run
+        fallbacks = {k: v[1] for k, v in calls.items() if v and v[1]}
+        dp = st.get("dp") or [0, 0, 0, 0]
         out = {
             "metric": "reads aligned/sec (whole node), 150 bp vs hg38, at 1/2/4/8 MI355X",
             "value": value, "unit": "aligned " + unit, "n_gpus": world,
@@ -1275,6 +1403,7 @@ def main():
                        "client_connections": args.clients, "reads_per_connection": 10_000,
                        "warmup_chunks": args.warmup_chunks},
             "roofline": rl,
+            "rooflines": rls,
             "reads_per_s": total_reads / elapsed,
             "server_kernels": kern,
             "server": {k: st.get(k) for k in ("reads", "rounds", "slots", "slots_live", "slots_rebuilt",
@@ -1294,8 +1423,15 @@ def main():
                        "throttled_s": sched["throttled_s"],
                        "client_cpu_s": sched["client_cpu_s"],
                        "client_cpu_us_per_read": sched["client_cpu_s"] / max(1, args.reads * args.steps) * 1e6,
-                       "calls": {k: st.get(k) for k in ("exact_sweep", "one_mm", "seed_search", "extend",
-                                                        "get_offset", "ungapped", "sw_dp")},
+                       "calls": calls,
+                       "cpu_fallbacks": fallbacks,
+                       # speculative DPs (bt2g_batch.cpp: the first DP an extension loop needs
+                       # goes out with up to 7 of its others): filled, taken by the loops, taken
+                       # at a tightened minimum score, and DPs asked for that were not ready
+                       "dp_speculation": {"speculated": dp[0], "used": dp[1], "reused": dp[2], "missed": dp[3],
+                                          "consumed_frac": dp[1] / dp[0] if dp[0] else None},
+                       "pass_s": sched["pass_s"], "passes_s": sched["passes_s"],
+                       "work_by_kernel": work_by_kernel(st),
                        "threads_cpu": sched["server_threads_cpu"]},
             "cpu_baseline": cpu,
             "sam_parity": sam,
@@ -1303,6 +1439,10 @@ def main():
             "kernel_chain": chain,
         }
         print(json.dumps(out), flush=True)
+        if fallbacks and not args.allow_fallbacks:
+            # (after the line, so that what ran is on record; the exit status fails the run)
+            log(f"[rank 0] FAIL: the reference's CPU code served requests in the product server: {fallbacks}")
+            sys.exit(3)
     if world > 1:
         dist.destroy_process_group()
 

@@ -80,12 +80,31 @@ class IndexMem(C.Structure):
 
 def build(force=False):
     """Compile libbt2g.so for gfx950 (make -C bowtie2-server_amd)."""
-    if force or not os.path.exists(LIB_PATH):
+    if force or not os.path.exists(LIB_PATH) or not os.path.exists(BENCH_LIB_PATH):
         subprocess.check_call(["make", "-C", HERE, "-j8"], stdout=subprocess.DEVNULL)
     return LIB_PATH
 
 
 _lib = None
+_bench_lib = None
+BENCH_LIB_PATH = os.path.join(HERE, "libbt2g_bench.so")
+
+
+def bench_lib():
+    """libbt2g_bench.so (include/bt2g_bench.h): bench.py's kernel-chain glue,
+    kept out of the product library."""
+    global _bench_lib
+    if _bench_lib is None:
+        if not os.path.exists(BENCH_LIB_PATH):
+            raise RuntimeError(f"{BENCH_LIB_PATH} is missing: build it with `make -C bowtie2-server_amd`")
+        L = C.CDLL(BENCH_LIB_PATH)
+        vp, u32 = C.c_void_p, C.c_uint32
+        L.bt2g_bench_collect_rows_dev.argtypes = [u32, vp, vp, vp, vp, u32, vp, vp, u32, u32, u32, vp, vp, vp, vp, vp,
+                                                  u32, vp]
+        L.bt2g_bench_frame_dev.argtypes = [u32, vp, vp, vp, vp, vp, vp, vp, vp, vp, u32, C.c_int32, vp, vp,
+                                           u32, vp]
+        _bench_lib = L
+    return _bench_lib
 
 
 def lib():
@@ -116,10 +135,6 @@ def lib():
         L.bt2g_exact_sweep_1mm.argtypes = [vp, vp, vp, u32, vp, u32, u32, C.c_int, C.c_int, C.c_int, vp,
                                            C.POINTER(Scoring), u32, vp, vp, vp, vp, vp, u32, vp]
         L.bt2g_reserve_sw.argtypes = [vp, u32, u32]
-        L.bt2g_bench_collect_rows_dev.argtypes = [u32, vp, vp, vp, vp, u32, vp, vp, u32, u32, u32, vp, vp, vp, vp, vp,
-                                                  u32, vp]
-        L.bt2g_bench_frame_dev.argtypes = [u32, vp, vp, vp, vp, vp, vp, vp, vp, vp, u32, C.c_int32, vp, vp,
-                                           u32, vp]
         L.bt2g_get_offset.argtypes = [vp, vp, u32, vp, vp]
         L.bt2g_extend.argtypes = [vp, vp, u32, vp, u32, vp, u32, vp]
         L.bt2g_extend_dev.argtypes = [vp, vp, u32, vp, vp, u32, vp, vp]

@@ -14,6 +14,7 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 #include "bt2g_kernels.h"
+#include "bt2g_bench.h"
 #include "dev_util.h"
 
 namespace {

@@ -7,6 +7,7 @@
 #include <atomic>
 #include <dlfcn.h>
 #include <hip/hip_runtime.h>
+#include <sys/prctl.h>
 #include <stdint.h>
 #include <stdio.h>
 #include <string.h>
@@ -86,6 +87,7 @@ struct bt2g_ctx {
 	// the 1-mm search's second stream (the BWT' direction) and its fork/join events
 	hipStream_t aux = nullptr;
 	int prio = 0;                       // stream priority (bt2g_set_priority); 0 = default
+	bool cu_masked = false;             // the stream is CU-masked (bt2g_set_cu_share)
 	hipEvent_t mm_ev[4] = {nullptr, nullptr, nullptr, nullptr};
 	// host-wrapper scratch (Arena): one device block reused call after call
 	uint8_t* arena = nullptr;
@@ -129,6 +131,10 @@ hipError_t stream_wait(bt2g_ctx* c, hipStream_t st) {
 		const char* e = getenv("BT2G_POLL_US");
 		return e && atol(e) > 0 ? atol(e) : 20L;
 	}();
+	// (the thread's timer slack, 50 us by default, would stretch every 20-us sleep
+	// to ~70 us: 1 us for a thread that waits here)
+	static thread_local bool slack = (prctl(PR_SET_TIMERSLACK, 1000UL, 0, 0, 0), true);
+	(void)slack;
 	hipError_t e;
 	if(!c->poll_ev && (e = hipEventCreateWithFlags(&c->poll_ev, hipEventDisableTiming)) != hipSuccess) return e;
 	if((e = hipEventRecord(c->poll_ev, st)) != hipSuccess) return e;
@@ -369,6 +375,27 @@ void drain_prof(bt2g_ctx* c) {
 	c->pending.clear();
 }
 
+// The context's second stream (the 1-mm search's BWT' direction) with its
+// fork/join events, and the event the poll wait records: made when the context
+// is opened (or its stream remade), on the opening thread -- round 6: they had
+// been made lazily by whichever service thread first needed them, after a
+// profiler's tool init; the r04ag/r05aa/r05h SIGSEGVs inside the profiler's HSA
+// intercept came from such threads' first launches.  Without the aux stream
+// (creation failed) the directions run in turn.
+void make_aux(bt2g_ctx* c) {
+	if(!c->aux) {
+		bool ok = hipStreamCreateWithPriority(&c->aux, hipStreamNonBlocking, c->prio) == hipSuccess;
+		for(int i = 0; ok && i < 4; i++) ok = hipEventCreateWithFlags(&c->mm_ev[i], hipEventDisableTiming) == hipSuccess;
+		if(!ok) {
+			for(hipEvent_t& e : c->mm_ev)
+				if(e) { (void)hipEventDestroy(e); e = nullptr; }
+			if(c->aux) (void)hipStreamDestroy(c->aux);
+			c->aux = nullptr;
+		}
+	}
+	if(!c->poll_ev) (void)hipEventCreateWithFlags(&c->poll_ev, hipEventDisableTiming);
+}
+
 // NULL is the null (legacy default) stream, as everywhere in HIP; the host
 // wrappers below pass the context stream explicitly.
 hipStream_t pick(bt2g_ctx*, void* s) { return (hipStream_t)s; }
@@ -538,6 +565,7 @@ int bt2g_open_mem(const bt2g_index_mem* m, int device, bt2g_ctx** out) {
 		return rc;
 	}
 	c->nref = m->nref;
+	make_aux(c);
 	*out = c;
 	return BT2G_OK;
 }
@@ -549,6 +577,7 @@ int bt2g_set_priority(bt2g_ctx* c, int high) {
 	HIPCHK(hipDeviceGetStreamPriorityRange(&least, &greatest));
 	const int p = high ? greatest : 0;
 	if(p == c->prio) return BT2G_OK;
+	if(c->cu_masked) return fail(BT2G_ERR_ARG, "bt2g_set_priority on a context with a CU share (bt2g_set_cu_share)");
 	hipStream_t s = nullptr;
 	HIPCHK(hipStreamCreateWithPriority(&s, hipStreamNonBlocking, p));
 	if(c->stream) {
@@ -557,7 +586,7 @@ int bt2g_set_priority(bt2g_ctx* c, int high) {
 		(void)hipStreamDestroy(c->stream);
 	}
 	c->stream = s;
-	if(c->aux) {                        // made again, at the new priority, when next needed
+	if(c->aux) {                        // made again, at the new priority
 		(void)hipStreamSynchronize(c->aux);
 		(void)hipStreamDestroy(c->aux);
 		c->aux = nullptr;
@@ -565,6 +594,7 @@ int bt2g_set_priority(bt2g_ctx* c, int high) {
 			if(e) { (void)hipEventDestroy(e); e = nullptr; }
 	}
 	c->prio = p;
+	make_aux(c);
 	return BT2G_OK;
 }
 
@@ -577,6 +607,7 @@ int bt2g_set_cu_share(bt2g_ctx* c, uint32_t num, uint32_t den) {
 	if(den == 0 || num >= den) {
 		HIPCHK(hipStreamCreateWithPriority(&s, hipStreamNonBlocking, c->prio));
 	} else {
+		if(c->prio) return fail(BT2G_ERR_ARG, "bt2g_set_cu_share on a context with a priority (bt2g_set_priority)");
 		std::vector<uint32_t> mask((size_t)(ncu + 31) / 32, 0u);
 		int kept = 0;
 		for(int i = 0; i < ncu; i++)
@@ -593,6 +624,7 @@ int bt2g_set_cu_share(bt2g_ctx* c, uint32_t num, uint32_t den) {
 		(void)hipStreamDestroy(c->stream);
 	}
 	c->stream = s;
+	c->cu_masked = den != 0 && num < den;
 	return BT2G_OK;
 }
 
@@ -615,6 +647,7 @@ int bt2g_open_shared(bt2g_ctx* base, bt2g_ctx** out) {
 	c->hbm_bytes = base->hbm_bytes;
 	c->base = base;
 	base->shares++;
+	make_aux(c);
 	*out = c;
 	return BT2G_OK;
 }
@@ -686,6 +719,14 @@ int bt2g_info(bt2g_ctx* c, uint64_t* out, int n) {
 int bt2g_set_profiling(bt2g_ctx* c, int on) {
 	if(!c) return fail(BT2G_ERR_ARG, "null ctx");
 	c->prof = on != 0;
+	// the events of the first calls made here, on the calling thread (a service
+	// thread then only takes them from the pool: see make_aux)
+	HIPCHK(hipSetDevice(c->device));
+	while(on && c->evpool.size() < 64) {
+		hipEvent_t e;
+		if(hipEventCreate(&e) != hipSuccess) break;
+		c->evpool.push_back(e);
+	}
 	return BT2G_OK;
 }
 
@@ -770,17 +811,6 @@ static int one_mm_impl(bt2g_ctx* c, const uint8_t* reads, const uint8_t* quals, 
 	if(cap == 0) return fail(BT2G_ERR_ARG, "cap must be > 0");
 	if(n == 0) return BT2G_OK;
 	hipStream_t st = pick(c, stream);
-	if(!c->aux) {
-		// the second direction's stream (created once; without it the directions run in turn)
-		bool ok = hipStreamCreateWithPriority(&c->aux, hipStreamNonBlocking, c->prio) == hipSuccess;
-		for(int i = 0; ok && i < 4; i++) ok = hipEventCreateWithFlags(&c->mm_ev[i], hipEventDisableTiming) == hipSuccess;
-		if(!ok) {
-			for(hipEvent_t& e : c->mm_ev)
-				if(e) { (void)hipEventDestroy(e); e = nullptr; }
-			if(c->aux) (void)hipStreamDestroy(c->aux);
-			c->aux = nullptr;
-		}
-	}
 	OneMmScratch s;
 	HIPCHK(amalloc(c, (void**)&s.slots, sizeof(bt2g_mm1) * (size_t)n * 4 * cap, st));
 	HIPCHK(amalloc(c, (void**)&s.slot_counts, sizeof(int32_t) * (size_t)n * 4, st));

@@ -467,34 +467,6 @@ int bt2g_frame_dev(bt2g_ctx* ctx, const bt2g_frame_in* in, uint32_t n, const uin
                    const bt2g_scoring* sc, const bt2g_pe_policy* pe, int32_t maxhalf, int trim_to_ref,
                    bt2g_sw_problem* probs, bt2g_sw_rect* rects, int32_t* ok, void* stream);
 
-/* ---- bench batch glue (NOT reference seams) -------------------------------
- * Device-side glue used by bench.py between the seed-phase calls and
- * bt2g_sw_align_dev.  The reference's SwDriver::extendSeeds chooses hits with
- * RNG-driven prioritisation (aligner_sw_driver.cpp:756-1297); the bench's
- * fixed policy is documented in DESIGN.md section 5. */
-
-/* Top SA rows of each read's exact end-to-end hit (sweep, as returned by
- * bt2g_exact_sweep_dev), 1-mm hits (mm, mm_cnt; cap mm_cap per read) and exact
- * seed hits (seeds of bt2g_seed_search_dev over the reads with inv[r] >= 0 at
- * compacted index inv[r]); contiguous per read at rows[read_base[r] ..
- * + read_cnt[r]), meta = fw << 31 | seed depth << 16 | hit length.  *total
- * (zeroed by the caller) receives the row count; beyond cap rows are dropped. */
-int bt2g_bench_collect_rows_dev(uint32_t n, const uint32_t* lens, const uint32_t* sweep, const bt2g_mm1* mm,
-                                const int32_t* mm_cnt, uint32_t mm_cap, const uint32_t* seeds, const int32_t* inv,
-                                uint32_t maxseeds, uint32_t seedlen, uint32_t interval, uint32_t* rows,
-                                uint32_t* meta, uint32_t* read_base, uint32_t* read_cnt, uint32_t* total,
-                                uint32_t cap, void* stream);
-/* Rows' joined offsets (bt2g_get_offset_dev) -> seed-extension frame inputs
- * (kind 0, off = the read's start on the reference) for bt2g_frame_dev: one
- * per distinct (strand, reference, diagonal), the two smallest per read;
- * fragments as in the .1.bt2 rstarts (joined offset, text id, text offset) plus
- * each fragment's joined end.  *nprob (zeroed by the caller) receives the
- * count. */
-int bt2g_bench_frame_dev(uint32_t n, const uint32_t* lens, const uint32_t* offs, const uint32_t* meta,
-                         const uint32_t* read_base, const uint32_t* read_cnt, const uint32_t* fr_joff,
-                         const uint32_t* fr_tid, const uint32_t* fr_toff, const uint32_t* fr_end, uint32_t nfrag,
-                         int32_t minsc, bt2g_frame_in* fin, uint32_t* nprob, uint32_t cap, void* stream);
-
 /* ---- multi-GPU ----------------------------------------------------------- */
 /* The only collective of the path: reads shard across ranks
  * (one process per GPU, a full index replica each) and the ranks sum a few

@@ -259,7 +259,8 @@ void* alloc(size_t n) {
 		void* p = malloc(HDR + n);
 		if(!p) return nullptr;
 		((Hdr*)p)->magic = MAGIC_MALLOC;
-		t_net += (long long)(HDR + n);
+		// (the bytes release() will count back: malloc's usable size, not HDR + n)
+		t_net += (long long)malloc_usable_size(p);
 		return (char*)p + HDR;
 	}
 	const int c = cls_of(n);
@@ -435,7 +436,16 @@ inline void site_count(void* ra, size_t n) {
 // that site when freed; dumped with the stats ("live <module> <offset> <bytes>").
 namespace {
 bool live_on() {
-	static const bool on = getenv("BT2G_ALLOC_LIVE") != nullptr;
+	// (the live tag and $BT2G_ALLOC_XTRACE's tag share the header's spare word:
+	// with both set, the live tag is off)
+	static const bool on = [] {
+		if(!getenv("BT2G_ALLOC_LIVE")) return false;
+		if(xtrace_on()) {
+			fprintf(stderr, "bt2g alloc: BT2G_ALLOC_LIVE ignored with BT2G_ALLOC_XTRACE (one header word)\n");
+			return false;
+		}
+		return true;
+	}();
 	return on;
 }
 std::atomic<uint64_t> g_lpc[XSLOT];

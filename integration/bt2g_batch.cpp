@@ -1150,6 +1150,15 @@ bool kprof_on() {
 	return on;
 }
 
+// The calls' algorithmic work by kernel id (bytes, DP cells): with $BT2G_KPROF,
+// or alone with $BT2G_KWORK=1 -- a rocprofv3 --pmc pass of the same command
+// then sets the counters' HBM bytes against the work of the same dispatches
+// (bench.py pmc_ratio) without the engines' own HIP events under the profiler.
+bool kwork_on() {
+	static const bool on = [] { const char* e = getenv("BT2G_KWORK"); return kprof_on() || (e && *e == '1'); }();
+	return on;
+}
+
 bool services_on() {
 	static const bool on = [] { const char* e = getenv("BT2G_SERVICES"); return !(e && *e == '0'); }();
 	return on;
@@ -1269,8 +1278,8 @@ void Svc::call_exact(std::vector<Rq>& v) {
 			mld.resize(n);
 			rc = bt2g_exact_sweep_1mm(ctx, pk.codes.data(), pk.quals.data(), pk.stride, pk.lens.data(), (uint32_t)n, 2,
 			                          nf ? 1 : 0, nr ? 1 : 0, 0, ms.data(), bsc, cap, out.data(), h.data(), cnt.data(),
-			                          ops.data(), kprof_on() ? mld.data() : nullptr, off_cap, offs.data());
-			if(kprof_on() && !rc) {
+			                          ops.data(), kwork_on() ? mld.data() : nullptr, off_cap, offs.data());
+			if(kwork_on() && !rc) {
 				// the 1-mm search's bytes: 64 B per side + the read and its qualities walked
 				// per strand (as call_1mm counts them); the reads it ran on
 				uint64_t w = 0, k = 0;
@@ -1366,8 +1375,8 @@ void Svc::call_1mm(std::vector<Rq>& v) {
 			const uint64_t t0 = now_us();
 			ld.resize(n);
 			int rc = bt2g_one_mm(ctx, pk.codes.data(), pk.quals.data(), pk.stride, pk.lens.data(), (uint32_t)n, ms.data(),
-			                     bsc, nf, nr, cap, h.data(), cnt.data(), ops.data(), kprof_on() ? ld.data() : nullptr);
-			if(kprof_on()) {
+			                     bsc, nf, nr, cap, h.data(), cnt.data(), ops.data(), kwork_on() ? ld.data() : nullptr);
+			if(kwork_on()) {
 				uint64_t w = 0;
 				for(size_t i = 0; i < n; i++) w += 64ull * ld[i] + 4ull * pk.lens[i];
 				work += w;
@@ -1434,9 +1443,9 @@ void Svc::call_seeds(std::vector<Rq>& v) {
 			offs.resize(n * 2 * maxs * OFF_CAP);
 		}
 		int rc = bt2g_seed_search_ext(ctx, pk.codes.data(), pk.stride, pk.lens.data(), (uint32_t)n, x0.sd_L, x0.sd_per,
-		                              x0.sd_off, maxs, out.data(), ns.data(), ops.data(), kprof_on() ? ld.data() : nullptr,
+		                              x0.sd_off, maxs, out.data(), ns.data(), ops.data(), kwork_on() ? ld.data() : nullptr,
 		                              pf ? ext.data() : nullptr, OFF_CAP, pf ? offs.data() : nullptr);
-		if(kprof_on()) {
+		if(kwork_on()) {
 			uint64_t w = 0;
 			for(size_t i = 0; i < n; i++) w += 64ull * ld[i] + (uint64_t)std::max(ns[i], 0) * 2u * (x0.sd_L + 12u);
 			work += w;
@@ -1454,7 +1463,7 @@ void Svc::call_seeds(std::vector<Rq>& v) {
 					k++;
 				}
 			g_ext_spec += k;
-			if(kprof_on()) {
+			if(kwork_on()) {
 				kwork[12] += w;
 				kitems[12] += k;
 			}
@@ -1514,7 +1523,7 @@ void Svc::call_ext(std::vector<Rq>& v) {
 	g_call_us[K_EXT] += now_us() - t0;
 	g_calls[K_EXT]++;
 	if(rc) die("bt2g_extend", rc);
-	if(kprof_on()) {
+	if(kwork_on()) {
 		uint64_t w = 0;
 		for(const bt2g_ext_out& o : out) w += 64ull * o.loads + o.fmops;
 		kwork[12] += w;
@@ -1536,8 +1545,8 @@ void Svc::call_off(std::vector<Rq>& v) {
 	offs.resize(rows.size());
 	const uint64_t t0 = now_us();
 	ld.resize(rows.size());
-	int rc = bt2g_get_offset(ctx, rows.data(), (uint32_t)rows.size(), offs.data(), kprof_on() ? ld.data() : nullptr);
-	if(kprof_on()) {
+	int rc = bt2g_get_offset(ctx, rows.data(), (uint32_t)rows.size(), offs.data(), kwork_on() ? ld.data() : nullptr);
+	if(kwork_on()) {
 		uint64_t w = 0;
 		for(uint32_t x : ld) w += 64ull * x + 12u;
 		work += w;
@@ -1631,7 +1640,7 @@ void Svc::run_dp(const std::vector<std::pair<Slot*, DpRes*>>& v, uint32_t cap, u
 		p.minsc = r.minsc;
 		b.RC[i] = r.rect;
 	}
-	if(kprof_on()) {
+	if(kwork_on()) {
 		uint64_t cells = 0;
 		for(size_t i = 0; i < n; i++) cells += (uint64_t)b.pk.lens[b.P[i].read] * b.P[i].ncol;
 		work += cells;
@@ -3796,7 +3805,7 @@ std::vector<std::array<Svc*, K_N>> g_svcs;
 
 // "kernels": {kind: [[launches, ms] of ids 0..15 (kernels, then host phases)], work, items} summed over devices
 int svc_stats(char* buf, size_t cap) {
-	if(!kprof_on()) return 0;
+	if(!kwork_on()) return 0;
 	std::lock_guard<std::mutex> lk(g_svc_mu);
 	int n = snprintf(buf, cap, ", \"kernels\": {");
 	for(int k = 0; k < K_N; k++) {

@@ -86,7 +86,7 @@ struct Opts {
     int port = 0, conns = 1, threads = 0, trim5 = 0, trim3 = 0;
     long long per_conn = 0;                 // 0: every read over one connection
     long long skip = 0, upto = -1;          // -s / -u: reads [skip, upto) of the input (rdid)
-    bool phred64 = false, xr = false, stats = false, mark = false;
+    bool phred64 = false, xr = false, stats = false, mark = false, count = false;
     std::vector<std::string> U, m1, m2;
 };
 
@@ -418,6 +418,11 @@ struct Conn {
     std::string in_buf;                      // received, not yet processed
     std::string sam;
     long long warned_lines = 0;
+    // --count-aligned: reads (pairs) with an alignment among the records received,
+    // counted as bench.py's count_aligned does (primary records without 0x4; a
+    // pair by its first mate's record, 0x4 and 0x8 not both set)
+    bool count = false;
+    long long aligned = 0;
 };
 
 // LockedOrigBufMap::take_ownership (pat.h:2519-2538); -1 when both maps are full
@@ -534,6 +539,13 @@ void read_line(Conn& c, const char* line, size_t n, bool xr) {
     const Rec& a = in.a[r];
     c.sam.append(in.arena.data() + a.name, a.name_len);
     c.sam.append(line + 4, n - 4);
+    if (c.count) {
+        const unsigned long f = strtoul(tab + 1, nullptr, 10);
+        if (!(f & 0x900)) {
+            if (in.paired()) c.aligned += (f & 0x40) && (f & 0xC) != 0xC;
+            else c.aligned += !(f & 0x4);
+        }
+    }
     if (xr) {
         unsigned long flags = strtoul(tab + 1, nullptr, 10);
         bool mate2 = (flags & 0x1) && (flags & 0x80);
@@ -712,7 +724,7 @@ struct Shared {
     Sink& sink;
     std::atomic<size_t> next_job{0};
     std::atomic<int> failed{0};
-    std::atomic<long long> reads{0}, bad_names{0}, bytes_out{0}, bytes_in{0};
+    std::atomic<long long> reads{0}, bad_names{0}, bytes_out{0}, bytes_in{0}, aligned{0};
 };
 
 void worker(Shared& S, int cap) {
@@ -738,6 +750,7 @@ void worker(Shared& S, int cap) {
             if (in->bad_names) S.bad_names += in->bad_names;
         }
         c->next = c->lo;
+        c->count = o.count;
         for (int m = 0; m < 2; m++) {
             c->slot[m].assign(BUF_CAPACITY, NO_READ);
             c->present[m].assign(BUF_CAPACITY, 0);
@@ -815,6 +828,7 @@ void worker(Shared& S, int cap) {
                     epoll_ctl(ep, EPOLL_CTL_DEL, c.fd, nullptr);
                     close(c.fd);
                     S.reads += (long long)(c.hi - c.lo);
+                    S.aligned += c.aligned;
                     if (c.used_cnt[0] || c.used_cnt[1]) {
                         fprintf(stderr, "ERROR: Did not process all the input file\n");
                         S.failed = 1;
@@ -858,7 +872,7 @@ void usage() {
             "                   [-S out.sam] [--server-host H] [--server-port P] [--passthrough] [-3 n] [-5 n]\n"
             "                   [--phred33|--phred64] [-s skip] [-u upto] [--no-hd] [-q] [--stats]\n"
             "       bt2g-client -x <index> --chunks LIST [-k conns] [-p threads] [--out-dir D | -S out.sam]\n"
-            "                   [--mark-chunks]\n");
+            "                   [--mark-chunks] [--count-aligned]\n");
 }
 
 }  // namespace
@@ -898,6 +912,7 @@ int main(int argc, char** argv) {
         else if (a == "--passthrough" || a == "--xr") o.xr = true;
         else if (a == "--stats") o.stats = true;
         else if (a == "--mark-chunks") o.mark = true;
+        else if (a == "--count-aligned") o.count = true;
         else if (a == "-q" || a == "--no-hd" || a == "--quiet" || a == "-t") {
         } else if (a == "-h" || a == "--help") {
             usage();
@@ -983,6 +998,8 @@ int main(int argc, char** argv) {
                     (long long)S.reads, jobs.size(), conns, nt,
                     (t1.tv_sec - t0.tv_sec) + 1e-9 * (t1.tv_nsec - t0.tv_nsec), S.bytes_out / 1e6,
                     S.bytes_in / 1e6);
+        if (o.count)
+            fprintf(stderr, "bt2g-client: aligned %lld of %lld\n", (long long)S.aligned, (long long)S.reads);
         ret = S.failed ? 1 : 0;
     } catch (const std::exception& ex) {
         fprintf(stderr, "%s\n", ex.what());

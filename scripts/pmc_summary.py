@@ -1,7 +1,13 @@
 #!/usr/bin/env python3
 """Per-kernel HBM traffic from rocprofv3 --pmc passes (one pass per counter):
 
-  python scripts/pmc_summary.py FETCH_DIR WRITE_DIR OUT.json
+  python scripts/pmc_summary.py FETCH_DIR WRITE_DIR OUT.json [FETCH_BENCH.json WRITE_BENCH.json]
+
+With the two passes' bench.py lines (run with BT2G_KWORK=1 in the server:
+server.work_by_kernel, the algorithmic bytes the server counted per kernel
+id), the summary also carries each pass's algorithmic work, so that bench.py
+sets the counters' bytes against the work of the same dispatches
+(bench.pmc_ratio).
 
 Every *counter_collection.csv under each directory (one per profiled process)
 is read; per kernel name (template arguments kept), the mean FETCH_SIZE and
@@ -30,6 +36,12 @@ def per_kernel(d, counter):
 
 def main():
     fd, wd, out = sys.argv[1:4]
+    works = {}
+    for key, path in zip(("fetch", "write"), sys.argv[4:6]):
+        try:
+            works[key] = json.load(open(path))["server"]["work_by_kernel"]
+        except (OSError, ValueError, KeyError, TypeError):
+            print(f"no work_by_kernel in {path}")
     f = per_kernel(fd, "FETCH_SIZE")
     w = per_kernel(wd, "WRITE_SIZE")
     res = {}
@@ -51,8 +63,8 @@ def main():
             build[rel] = hashlib.sha256(open(os.path.join(root, rel), "rb").read()).hexdigest()
         except OSError:
             pass
-    json.dump({"source": {"fetch": fd, "write": wd}, "build_sha256": build, "kernels": res}, open(out, "w"),
-              indent=1)
+    json.dump({"source": {"fetch": fd, "write": wd}, "build_sha256": build, "kernels": res,
+               "work_by_kernel": works}, open(out, "w"), indent=1)
     for k, v in sorted(res.items(), key=lambda kv: -(kv[1]["dispatches"] or 0))[:20]:
         print(k[:80], v["dispatches"], v["fetch_kib"], v["write_kib"])
 

@@ -6,8 +6,8 @@ import re
 from conftest import PKG, ROOT
 
 
-def declared_symbols():
-    src = open(os.path.join(ROOT, "include", "bt2g.h")).read()
+def declared_symbols(header="bt2g.h"):
+    src = open(os.path.join(ROOT, "include", header)).read()
     return sorted(set(re.findall(r"\b(bt2g_[a-z0-9_]+)\s*\(", src)))
 
 
@@ -19,6 +19,17 @@ def test_library_exports_all_symbols():
     assert len(syms) >= 18
     missing = [s for s in syms if not hasattr(lib, s)]
     assert not missing, missing
+    # bench.py's glue lives in a library of its own (include/bt2g_bench.h), not the product's
+    assert not any(hasattr(lib, s) for s in declared_symbols("bt2g_bench.h"))
+
+
+def test_bench_library_exports_its_symbols():
+    import bt2g
+    bt2g.build()
+    lib = ctypes.CDLL(bt2g.BENCH_LIB_PATH)
+    syms = declared_symbols("bt2g_bench.h")
+    assert syms == ["bt2g_bench_collect_rows_dev", "bt2g_bench_frame_dev"]
+    assert all(hasattr(lib, s) for s in syms)
 
 
 def test_library_is_gfx950_only():

@@ -137,13 +137,15 @@ def test_schedule_and_stock_baseline_cpu():
     bi.write_index(base, idx)
     r, q = bench.make_reads(idx.ref_codes, 2500, 150, 5)
     args = types.SimpleNamespace(mode="ee", preset="sensitive", reads=2500, drivers=2, clients=2, warmup=1,
-                                 warmup_chunks=1, steps=1, stock_sample=2500, cpu_threads=2)
+                                 warmup_chunks=1, steps=2, stock_sample=2500, cpu_threads=2, stock_runs=2)
     sc = bench.schedule_run(args, 0, 1, 0, base, r, q, d, binary=stub)
-    assert sc["aligned"] == bench.count_aligned(sc["outs"], False) and 2000 < sc["aligned"] <= 2500
+    # two timed passes: the first counted by the client alone, the last also from its SAM
+    assert len(sc["pass_s"]) == 2
+    assert sc["aligned"] == 2 * bench.count_aligned(sc["outs"], False) and 4000 < sc["aligned"] <= 5000
     assert sc["stats"]["driver"] == "batch" and sc["stats"]["reads"] >= 2500
     cpu, sam = bench.stock_baseline(args, base, sc["chunks"], sc["outs"], d)
     assert sam["identical"] and sam["records"] == 2500
-    assert cpu["value"] > 0 and cpu["kind"] == "reference"
+    assert cpu["value"] > 0 and cpu["kind"] == "reference" and len(cpu["runs"]) == 2
 
 
 def test_count_aligned_flags():
