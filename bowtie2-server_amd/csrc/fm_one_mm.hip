@@ -142,13 +142,12 @@ k_one_mm_items(const uint8_t* __restrict__ reads, uint32_t stride, const uint32_
 // per item, lean state (it is most of the LF work and runs at high occupancy);
 // the surviving range (+ mirror) and depth go to the far-half kernel.
 template <bool EBWTFW>
-__global__ void __launch_bounds__(256)
-k_one_mm_near(DevEbwt F, DevEbwt B, const uint8_t* __restrict__ reads, uint32_t stride,
+__device__ __forceinline__ void one_mm_near_body(const uint32_t blk_, DevEbwt F, DevEbwt B, const uint8_t* __restrict__ reads, uint32_t stride,
               const uint32_t* __restrict__ lens, const uint32_t* __restrict__ items,
               const uint32_t* __restrict__ nitems_p, uint4* __restrict__ st4, uint32_t* __restrict__ sdep,
               uint32_t* __restrict__ ops_out, uint32_t* __restrict__ loads_out) {
 	walk_prio();
-	const uint32_t qi = blockIdx.x * blockDim.x + threadIdx.x;
+	const uint32_t qi = blk_ * blockDim.x + threadIdx.x;
 	if(qi >= *nitems_p) return;
 	const DevEbwt& E = EBWTFW ? F : B;
 	const DevEbwt& Ep = EBWTFW ? B : F;
@@ -211,12 +210,20 @@ k_one_mm_near(DevEbwt F, DevEbwt B, const uint8_t* __restrict__ reads, uint32_t 
 	if(ops && loads_out) atomicAdd(&loads_out[r], loads);
 }
 
+template <bool EBWTFW>
+__global__ void __launch_bounds__(256)
+k_one_mm_near(DevEbwt F, DevEbwt B, const uint8_t* __restrict__ reads, uint32_t stride,
+              const uint32_t* __restrict__ lens, const uint32_t* __restrict__ items,
+              const uint32_t* __restrict__ nitems_p, uint4* __restrict__ st4, uint32_t* __restrict__ sdep,
+              uint32_t* __restrict__ ops_out, uint32_t* __restrict__ loads_out) {
+	one_mm_near_body<EBWTFW>(blockIdx.x, F, B, reads, stride, lens, items, nitems_p, st4, sdep, ops_out, loads_out);
+}
+
 #ifndef BT2G_MM_WAVES
 #define BT2G_MM_WAVES 3
 #endif
 template <bool EBWTFW>
-__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(BT2G_MM_WAVES)))
-k_one_mm_q(DevEbwt F, DevEbwt B, const uint8_t* __restrict__ reads, const uint8_t* __restrict__ quals,
+__device__ __forceinline__ void one_mm_q_body(const uint32_t blk_, uint32_t (*alt_s)[256], DevEbwt F, DevEbwt B, const uint8_t* __restrict__ reads, const uint8_t* __restrict__ quals,
            uint32_t stride, const uint32_t* __restrict__ lens, const int32_t* __restrict__ minscs, MmParams P,
            double ncl_const, double ncl_lin, const uint32_t* __restrict__ items,
            const uint32_t* __restrict__ nitems_p, const uint4* __restrict__ st4,
@@ -242,7 +249,6 @@ k_one_mm_q(DevEbwt F, DevEbwt B, const uint8_t* __restrict__ reads, const uint8_
 	uint32_t top = 0, bot = 0, topp = 0, botp = 0;            // main range (+ mirror)
 	// the far step's four ranges (+ mirrors) live in LDS: read only when
 	// alternatives are enumerated, they would otherwise pin 16 registers
-	__shared__ uint32_t alt_s[16][256];
 	const uint32_t tid = threadIdx.x;
 #define T_(i) alt_s[(i)][tid]
 #define B_(i) alt_s[4 + (i)][tid]
@@ -328,7 +334,7 @@ k_one_mm_q(DevEbwt F, DevEbwt B, const uint8_t* __restrict__ reads, const uint8_
 			// items there is no tail to fill, and the queue costs registers)
 			if(exhausted) break;
 			exhausted = true;
-			const uint32_t qi = blockIdx.x * blockDim.x + threadIdx.x;
+			const uint32_t qi = blk_ * blockDim.x + threadIdx.x;
 			if(qi >= nitems) continue;
 			// ---- item initialisation (aligner_seed.cpp:1003-1100)
 			const uint32_t item = items[qi];
@@ -443,6 +449,19 @@ k_one_mm_q(DevEbwt F, DevEbwt B, const uint8_t* __restrict__ reads, const uint8_
 	}
 }
 
+template <bool EBWTFW>
+__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(BT2G_MM_WAVES)))
+k_one_mm_q(DevEbwt F, DevEbwt B, const uint8_t* __restrict__ reads, const uint8_t* __restrict__ quals,
+           uint32_t stride, const uint32_t* __restrict__ lens, const int32_t* __restrict__ minscs, MmParams P,
+           double ncl_const, double ncl_lin, const uint32_t* __restrict__ items,
+           const uint32_t* __restrict__ nitems_p, const uint4* __restrict__ st4,
+           const uint32_t* __restrict__ sdep, uint32_t cap, bt2g_mm1* __restrict__ slots, int32_t* __restrict__ slot_counts, uint32_t* __restrict__ ops_out,
+           uint32_t* __restrict__ loads_out, MmBranch* __restrict__ brq, uint32_t* __restrict__ brq_n,
+           uint32_t brq_cap) {
+	__shared__ uint32_t alt_s[16][256];
+	one_mm_q_body<EBWTFW>(blockIdx.x, alt_s, F, B, reads, quals, stride, lens, minscs, P, ncl_const, ncl_lin, items, nitems_p, st4, sdep, cap, slots, slot_counts, ops_out, loads_out, brq, brq_n, brq_cap);
+}
+
 // Far half, lean form (aligner_seed.cpp:1110-1315): the main path's LF steps
 // with the read's base at every far depth, and for each non-empty alternative
 // base the hit it would make -- queued for k_one_mm_branch when the walk has
@@ -475,8 +494,7 @@ extern "C" int bt2g_mm_prof_waves(unsigned long long* t0, unsigned long long* t1
 #define BT2G_MM_FAR_WAVES 3      // 4 and 5 spill (84 / 152 B per lane)
 #endif
 template <bool EBWTFW>
-__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(BT2G_MM_FAR_WAVES)))
-k_one_mm_far(DevEbwt F, DevEbwt B, const uint8_t* __restrict__ reads, const uint8_t* __restrict__ quals,
+__device__ __forceinline__ void one_mm_far_body(const uint32_t blk_, MmBranch (*s_br)[MM_BRBUF], uint32_t* s_brn, DevEbwt F, DevEbwt B, const uint8_t* __restrict__ reads, const uint8_t* __restrict__ quals,
              uint32_t stride, const uint32_t* __restrict__ lens, const int32_t* __restrict__ minscs, MmParams P,
              double ncl_const, double ncl_lin, const uint32_t* __restrict__ items,
              const uint32_t* __restrict__ nitems_p, const uint4* __restrict__ st4, const uint32_t* __restrict__ sdep,
@@ -486,14 +504,12 @@ k_one_mm_far(DevEbwt F, DevEbwt B, const uint8_t* __restrict__ reads, const uint
              uint4* __restrict__ fb_st4, uint32_t* __restrict__ fb_sdep, uint32_t* __restrict__ fb_n,
              uint32_t* __restrict__ slot_flag) {
 	walk_prio();
-	const uint32_t qi = blockIdx.x * blockDim.x + threadIdx.x;
+	const uint32_t qi = blk_ * blockDim.x + threadIdx.x;
 	// Far-half branches are staged in LDS per wave and go to the global queue in
 	// one allocation and a coalesced copy when the wave is done: a global atomic
 	// (whose return the store waits for) and a store inside the LF loop made
 	// every later side load of the wave wait behind them (vmcnt is in order) --
 	// ~13 us per LF step with most waves pushing at some step.
-	__shared__ MmBranch s_br[4][MM_BRBUF];
-	__shared__ uint32_t s_brn[4];
 	const uint32_t wv = threadIdx.x >> 6;
 	if((threadIdx.x & 63u) == 0) s_brn[wv] = 0;
 	if(qi >= *nitems_p) return;
@@ -678,20 +694,35 @@ k_one_mm_far(DevEbwt F, DevEbwt B, const uint8_t* __restrict__ reads, const uint
 	if(ops && loads_out) atomicAdd(&loads_out[r], loads);
 }
 
+template <bool EBWTFW>
+__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(BT2G_MM_FAR_WAVES)))
+k_one_mm_far(DevEbwt F, DevEbwt B, const uint8_t* __restrict__ reads, const uint8_t* __restrict__ quals,
+             uint32_t stride, const uint32_t* __restrict__ lens, const int32_t* __restrict__ minscs, MmParams P,
+             double ncl_const, double ncl_lin, const uint32_t* __restrict__ items,
+             const uint32_t* __restrict__ nitems_p, const uint4* __restrict__ st4, const uint32_t* __restrict__ sdep,
+             uint32_t cap, bt2g_mm1* __restrict__ slots, int32_t* __restrict__ slot_counts,
+             uint32_t* __restrict__ ops_out, uint32_t* __restrict__ loads_out, MmBranch* __restrict__ brq,
+             uint32_t* __restrict__ brq_n, uint32_t brq_cap, uint32_t* __restrict__ fb_items,
+             uint4* __restrict__ fb_st4, uint32_t* __restrict__ fb_sdep, uint32_t* __restrict__ fb_n,
+             uint32_t* __restrict__ slot_flag) {
+	__shared__ MmBranch s_br[4][MM_BRBUF];
+	__shared__ uint32_t s_brn[4];
+	one_mm_far_body<EBWTFW>(blockIdx.x, s_br, s_brn, F, B, reads, quals, stride, lens, minscs, P, ncl_const, ncl_lin, items, nitems_p, st4, sdep, cap, slots, slot_counts, ops_out, loads_out, brq, brq_n, brq_cap, fb_items, fb_st4, fb_sdep, fb_n, slot_flag);
+}
+
 // Walk every queued far-half branch to the read's end (or its death), one
 // lane per branch: exact steps on the read's remaining bases with the same LF
 // operations and op counting as the in-place walk (ST_BR above).  A completed
 // valid branch appends its hit to its slot (after the far kernel's own hits,
 // slot_counts[] is the slot's running count).
 template <bool EBWTFW>
-__global__ void __launch_bounds__(256)
-k_one_mm_branch(DevEbwt F, DevEbwt B, const uint8_t* __restrict__ reads, uint32_t stride,
+__device__ __forceinline__ void one_mm_branch_body(const uint32_t blk_, DevEbwt F, DevEbwt B, const uint8_t* __restrict__ reads, uint32_t stride,
                 const uint32_t* __restrict__ lens, const MmBranch* __restrict__ brq,
                 const uint32_t* __restrict__ brq_n, uint32_t brq_cap, uint32_t cap, bt2g_mm1* __restrict__ slots,
                 int32_t* __restrict__ slot_counts, uint32_t* __restrict__ ops_out, uint32_t* __restrict__ loads_out,
                 const uint32_t* __restrict__ slot_flag) {
 	walk_prio();
-	const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+	const uint32_t i = blk_ * blockDim.x + threadIdx.x;
 	const uint32_t nq = *brq_n < brq_cap ? *brq_n : brq_cap;
 	if(i >= nq) return;
 	const MmBranch b = brq[i];
@@ -742,6 +773,67 @@ k_one_mm_branch(DevEbwt F, DevEbwt B, const uint8_t* __restrict__ reads, uint32_
 	if(ops && loads_out) atomicAdd(&loads_out[r], loads);
 }
 
+template <bool EBWTFW>
+__global__ void __launch_bounds__(256)
+k_one_mm_branch(DevEbwt F, DevEbwt B, const uint8_t* __restrict__ reads, uint32_t stride,
+                const uint32_t* __restrict__ lens, const MmBranch* __restrict__ brq,
+                const uint32_t* __restrict__ brq_n, uint32_t brq_cap, uint32_t cap, bt2g_mm1* __restrict__ slots,
+                int32_t* __restrict__ slot_counts, uint32_t* __restrict__ ops_out, uint32_t* __restrict__ loads_out,
+                const uint32_t* __restrict__ slot_flag) {
+	one_mm_branch_body<EBWTFW>(blockIdx.x, F, B, reads, stride, lens, brq, brq_n, brq_cap, cap, slots, slot_counts, ops_out, loads_out, slot_flag);
+}
+
+
+// Both index directions in one launch (round 6): blocks [0, g_) walk the BWT's
+// items, [g_, 2 g_) the mirror index's (their lists at +half_, their item
+// count at +2, their fallback lists at +half_ and count +1).  Two launches on a
+// second stream had joined through events: ~0.1-0.3 ms of cross-queue waits
+// per call in the batch server's trace (r06a), a near-half launch's worth.
+__global__ void __launch_bounds__(256)
+k_one_mm_near2(const uint32_t g_, const size_t half_, DevEbwt F, DevEbwt B, const uint8_t* __restrict__ reads, uint32_t stride,
+              const uint32_t* __restrict__ lens, const uint32_t* __restrict__ items,
+              const uint32_t* __restrict__ nitems_p, uint4* __restrict__ st4, uint32_t* __restrict__ sdep,
+              uint32_t* __restrict__ ops_out, uint32_t* __restrict__ loads_out) {
+	if(blockIdx.x < g_) one_mm_near_body<true>(blockIdx.x, F, B, reads, stride, lens, items, nitems_p, st4, sdep, ops_out, loads_out);
+	else one_mm_near_body<false>(blockIdx.x - g_, F, B, reads, stride, lens, items + half_, nitems_p + 2, st4 + half_, sdep + half_, ops_out, loads_out);
+}
+__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(BT2G_MM_FAR_WAVES)))
+k_one_mm_far2(const uint32_t g_, const size_t half_, DevEbwt F, DevEbwt B, const uint8_t* __restrict__ reads, const uint8_t* __restrict__ quals,
+             uint32_t stride, const uint32_t* __restrict__ lens, const int32_t* __restrict__ minscs, MmParams P,
+             double ncl_const, double ncl_lin, const uint32_t* __restrict__ items,
+             const uint32_t* __restrict__ nitems_p, const uint4* __restrict__ st4, const uint32_t* __restrict__ sdep,
+             uint32_t cap, bt2g_mm1* __restrict__ slots, int32_t* __restrict__ slot_counts,
+             uint32_t* __restrict__ ops_out, uint32_t* __restrict__ loads_out, MmBranch* __restrict__ brq,
+             uint32_t* __restrict__ brq_n, uint32_t brq_cap, uint32_t* __restrict__ fb_items,
+             uint4* __restrict__ fb_st4, uint32_t* __restrict__ fb_sdep, uint32_t* __restrict__ fb_n,
+             uint32_t* __restrict__ slot_flag) {
+	__shared__ MmBranch s_br[4][MM_BRBUF];
+	__shared__ uint32_t s_brn[4];
+	if(blockIdx.x < g_) one_mm_far_body<true>(blockIdx.x, s_br, s_brn, F, B, reads, quals, stride, lens, minscs, P, ncl_const, ncl_lin, items, nitems_p, st4, sdep, cap, slots, slot_counts, ops_out, loads_out, brq, brq_n, brq_cap, fb_items, fb_st4, fb_sdep, fb_n, slot_flag);
+	else one_mm_far_body<false>(blockIdx.x - g_, s_br, s_brn, F, B, reads, quals, stride, lens, minscs, P, ncl_const, ncl_lin, items + half_, nitems_p + 2, st4 + half_, sdep + half_, cap, slots, slot_counts, ops_out, loads_out, brq, brq_n, brq_cap, fb_items + half_, fb_st4 + half_, fb_sdep + half_, fb_n + 1, slot_flag);
+}
+__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(BT2G_MM_WAVES)))
+k_one_mm_q2(const uint32_t g_, const size_t half_, DevEbwt F, DevEbwt B, const uint8_t* __restrict__ reads, const uint8_t* __restrict__ quals,
+           uint32_t stride, const uint32_t* __restrict__ lens, const int32_t* __restrict__ minscs, MmParams P,
+           double ncl_const, double ncl_lin, const uint32_t* __restrict__ items,
+           const uint32_t* __restrict__ nitems_p, const uint4* __restrict__ st4,
+           const uint32_t* __restrict__ sdep, uint32_t cap, bt2g_mm1* __restrict__ slots, int32_t* __restrict__ slot_counts, uint32_t* __restrict__ ops_out,
+           uint32_t* __restrict__ loads_out, MmBranch* __restrict__ brq, uint32_t* __restrict__ brq_n,
+           uint32_t brq_cap) {
+	__shared__ uint32_t alt_s[16][256];
+	if(blockIdx.x < g_) one_mm_q_body<true>(blockIdx.x, alt_s, F, B, reads, quals, stride, lens, minscs, P, ncl_const, ncl_lin, items, nitems_p, st4, sdep, cap, slots, slot_counts, ops_out, loads_out, brq, brq_n, brq_cap);
+	else one_mm_q_body<false>(blockIdx.x - g_, alt_s, F, B, reads, quals, stride, lens, minscs, P, ncl_const, ncl_lin, items + half_, nitems_p + 1, st4 + half_, sdep + half_, cap, slots, slot_counts, ops_out, loads_out, brq, brq_n, brq_cap);
+}
+__global__ void __launch_bounds__(256)
+k_one_mm_branch2(const uint32_t g_, const size_t half_, DevEbwt F, DevEbwt B, const uint8_t* __restrict__ reads, uint32_t stride,
+                const uint32_t* __restrict__ lens, const MmBranch* __restrict__ brq,
+                const uint32_t* __restrict__ brq_n, uint32_t brq_cap, uint32_t cap, bt2g_mm1* __restrict__ slots,
+                int32_t* __restrict__ slot_counts, uint32_t* __restrict__ ops_out, uint32_t* __restrict__ loads_out,
+                const uint32_t* __restrict__ slot_flag) {
+	if(blockIdx.x < g_) one_mm_branch_body<true>(blockIdx.x, F, B, reads, stride, lens, brq, brq_n, brq_cap, cap, slots, slot_counts, ops_out, loads_out, slot_flag);
+	else one_mm_branch_body<false>(blockIdx.x - g_, F, B, reads, stride, lens, brq, brq_n, brq_cap, cap, slots, slot_counts, ops_out, loads_out, slot_flag);
+}
+
 void launch_one_mm_q(const DevEbwt& F, const DevEbwt& B, const uint8_t* reads, const uint8_t* quals, uint32_t stride,
                      const uint32_t* lens, uint32_t n, const int32_t* minsc, const bt2g_scoring& sc, int nofw,
                      int norc, const uint32_t* gate, uint32_t cap, uint32_t* items, uint32_t* counters,
@@ -749,6 +841,27 @@ void launch_one_mm_q(const DevEbwt& F, const DevEbwt& B, const uint8_t* reads, c
                      uint32_t* loads, MmBranch* brq, uint32_t brq_cap, uint32_t* fb_items, uint4* fb_st4,
                      uint32_t* fb_sdep, uint32_t* slot_flag, hipStream_t st, hipStream_t st2, hipEvent_t* ev) {
 	MmParams P{sc.match, sc.mmp_max, sc.mmp_min, sc.npen, sc.local, 0, 0};
+	// $BT2G_MM_MERGED=0: the two index directions as separate launches on two
+	// streams (forked and joined by events), as before round 6; default: one
+	// launch per stage for both (k_one_mm_*2)
+	static const bool merged = [] { const char* e = getenv("BT2G_MM_MERGED"); return !(e && *e == '0'); }();
+	if(merged) {
+		hipLaunchKernelGGL(k_one_mm_items, dim3((n + 255) / 256), dim3(256), 0, st, reads, stride, lens, n, gate, nofw,
+		                   norc, items, counters, slot_counts, ops, loads, slot_flag);
+		const uint32_t g = (2 * n + 255) / 256, gb = (brq_cap + 255) / 256;
+		const size_t half = 2 * (size_t)n;
+		hipLaunchKernelGGL(k_one_mm_near2, dim3(2 * g), dim3(256), 0, st, g, half, F, B, reads, stride, lens, items,
+		                   counters, near_state, near_dep, ops, loads);
+		hipLaunchKernelGGL(k_one_mm_far2, dim3(2 * g), dim3(256), 0, st, g, half, F, B, reads, quals, stride, lens, minsc,
+		                   P, sc.ncl_const, sc.ncl_lin, items, counters, near_state, near_dep, cap, slots, slot_counts,
+		                   ops, loads, brq, counters + 4, brq_cap, fb_items, fb_st4, fb_sdep, counters + 5, slot_flag);
+		hipLaunchKernelGGL(k_one_mm_q2, dim3(2 * g), dim3(256), 0, st, g, half, F, B, reads, quals, stride, lens, minsc,
+		                   P, sc.ncl_const, sc.ncl_lin, fb_items, counters + 5, fb_st4, fb_sdep, cap, slots, slot_counts,
+		                   ops, loads, brq, counters + 7, 0u);
+		hipLaunchKernelGGL(k_one_mm_branch2, dim3(2 * gb), dim3(256), 0, st, gb, half, F, B, reads, stride, lens, brq,
+		                   counters + 4, brq_cap, cap, slots, slot_counts, ops, loads, slot_flag);
+		return;
+	}
 	// the BWT' direction's kernels on s2 (st2, forked from st and joined back), or after the BWT ones on st
 	const bool two = st2 != nullptr && ev != nullptr;
 	hipStream_t s2 = two ? st2 : st;

@@ -180,6 +180,22 @@ class Server:
                 outs[i] = r.stdout
 
         def native():
+            if any(not (len(a) == 2 and a[0] == "-U") and not (len(a) == 4 and a[0] == "-1" and a[2] == "-2")
+                   for a in chunk_args):
+                # other inputs (-f, --tab6, ...): one client process per chunk, in turn
+                tot = 0
+                for i, a in enumerate(chunk_args):
+                    r = subprocess.run([client, "-x", self.index_base, "--no-hd", "--count-aligned"] + list(a),
+                                       env=env, stdout=subprocess.PIPE, stderr=subprocess.PIPE, timeout=timeout)
+                    if r.returncode != 0:
+                        errs.append((i, r.returncode, r.stderr[-2000:]))
+                        return
+                    for ln in r.stderr.splitlines():
+                        if ln.startswith(b"bt2g-client: aligned "):
+                            tot += int(ln.split()[2])
+                    outs[i] = r.stdout
+                self.last_aligned = tot
+                return
             lst = tempfile.mktemp(prefix="bt2g_chunks_", suffix=".txt")
             with open(lst, "w") as f:
                 for a in chunk_args:

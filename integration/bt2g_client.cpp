@@ -33,6 +33,24 @@
 //     the read's original FASTQ record, %-escaped (copyOptFieldNewlineEscaped,
 //     pat.cpp:2258-2284).
 //
+// Other inputs (round 6), as the reference client's PatternSource family
+// (pat.h:878-1232) parses them before readPair2Tab6:
+//
+//   * -f FASTA: FastaPatternSource (pat.cpp:790-912): a record is '>' and every
+//     byte up to the next '>', the name its first line, the sequence every
+//     letter ('.' as N) after it except the record's last byte, qualities 'I';
+//   * --tab5 / --12 / --tab6 (files of one read or pair per line):
+//     TabbedPatternSource (pat.cpp:1524-1661, tabbed_parse): NAME\tSEQ\tQUAL,
+//     then \tSEQ\tQUAL (tab5, the mate named as the first) or \tNAME\tSEQ\tQUAL
+//     (tab6) for a pair -- unpaired and paired lines may mix in one file;
+//   * -r raw (RawPatternSource, pat.cpp:1743-1817): one sequence a line, named
+//     by its read number, qualities 'I';
+//   * -c: the -U / -1 / -2 arguments are the reads themselves, SEQ[:QUALS]
+//     comma-separated (VectorPatternSource, pat.cpp:614-700: named by their
+//     index, parsed as tab5 lines).
+// A read that does not parse is skipped, its read number spent (the client
+// loop of bt2_search.cpp:4578-4586).
+//
 // Per connection the SAM bytes are those of the reference client given the
 // same reads (tests/test_client.py diffs the two on the same server).  What
 // differs is packaging: the reference prints "Read name does not end in /1!"
@@ -87,6 +105,7 @@ struct Opts {
     long long per_conn = 0;                 // 0: every read over one connection
     long long skip = 0, upto = -1;          // -s / -u: reads [skip, upto) of the input (rdid)
     bool phred64 = false, xr = false, stats = false, mark = false, count = false;
+    enum Fmt { FASTQ, FASTA, TAB5, TAB6, RAW, CMDLINE } fmt = FASTQ;
     std::vector<std::string> U, m1, m2;
 };
 
@@ -116,9 +135,10 @@ struct Rec {                 // one mate, offsets into Input::arena
 struct Input {
     std::string arena;        // names and TAB6 fields; the first `used` bytes are taken
     size_t used = 0;
-    std::vector<Rec> a, b;    // b empty: unpaired
+    std::vector<Rec> a, b;    // b empty: unpaired; else b[i].tab_len == 0 for an unpaired read i (tabbed input)
     long long bad_names = 0;  // names of mate 1 without "/1" (pat.cpp:2289-2291)
     bool paired() const { return !b.empty(); }
+    bool pair(size_t i) const { return !b.empty() && b[i].tab_len != 0; }
 };
 
 std::string slurp(const std::string& path) {
@@ -348,8 +368,288 @@ void parse_rec(const char* r, size_t len, long long rdid, const Opts& o, Input& 
     if (w > 0xF0000000u) throw Fail("Error: input of one connection over 3.7 GB");
 }
 
+// A parsed read into in.arena: its name (mate 1: without a final "/1",
+// saveOrigBufs), "\tSEQ\tQUAL" and the %-escaped original bytes (--passthrough).
+void emit(Input& in, const Opts& o, Rec& rec, const char* name, size_t name_len, const std::string& seq,
+          const std::string& qual, const char* orig, size_t orig_len, bool mate1) {
+    size_t need = in.used + name_len + seq.size() + qual.size() + 3 * orig_len + 16;
+    if (need > in.arena.size()) in.arena.resize(std::max(need, in.arena.size() * 2));
+    char* A = &in.arena[0];
+    size_t w = in.used;
+    size_t keep = name_len;
+    if (mate1) {
+        if (name_len < 3 || memcmp(name + name_len - 2, "/1", 2) != 0) in.bad_names++;
+        else keep -= 2;
+    }
+    memcpy(A + w, name, keep);
+    rec.name = (uint32_t)w;
+    rec.name_len = (uint32_t)keep;
+    w += keep;
+    rec.tab = (uint32_t)w;
+    A[w++] = '\t';
+    memcpy(A + w, seq.data(), seq.size());
+    w += seq.size();
+    A[w++] = '\t';
+    memcpy(A + w, qual.data(), qual.size());
+    w += qual.size();
+    rec.tab_len = (uint32_t)(w - rec.tab);
+    rec.orig = (uint32_t)w;
+    if (o.xr) {
+        static const char hex[] = "0123456789ABCDEF";
+        for (size_t k = 0; k < orig_len; k++) {
+            unsigned char c = (unsigned char)orig[k];
+            if (c == 10 || c == 13 || c == '%') {
+                A[w++] = '%';
+                A[w++] = hex[c >> 4];
+                A[w++] = hex[c & 15];
+            } else {
+                A[w++] = (char)c;
+            }
+        }
+    }
+    rec.orig_len = (uint32_t)(w - rec.orig);
+    in.used = w;
+    if (w > 0xF0000000u) throw Fail("Error: input of one connection over 3.7 GB");
+}
+
+// --trim5 / --trim3 of a parsed sequence and its qualities (Read::patFw /
+// qual trimEnd; the 5' letters were dropped while parsing)
+void trim3(std::string& seq, std::string& qual, int t3) {
+    const size_t k = std::min(seq.size(), (size_t)std::max(0, t3));
+    seq.resize(seq.size() - k);
+    qual.resize(qual.size() - std::min(qual.size(), (size_t)std::max(0, t3)));
+}
+
+// Phred+33 of a quality character (charToPhred33, qual.h:105-146; FASTQ's rules)
+int qual33(int ch, const Opts& o) {
+    if (ch == ' ')
+        throw Fail("Saw a space but expected an ASCII-encoded quality value.\n"
+                   "Are quality values formatted as integers?  If so, try --integer-quals.");
+    if (o.phred64) {
+        if (ch < 64)
+            throw Fail("Saw ASCII character " + std::to_string(ch) + " but expected 64-based Phred qual.\n"
+                       "Try not specifying --solexa1.3-quals/--phred64-quals.");
+        return ch - (64 - 33);
+    }
+    if (ch < 33) throw Fail("Saw ASCII character " + std::to_string(ch) + " but expected 33-based Phred qual.");
+    return ch;
+}
+
+// FastaPatternSource::nextBatchFromFile + parse (pat.cpp:790-912) over a file
+// in memory: every record of `s` into dst (rdid counts every record, parsed
+// or not).
+void load_fasta(const std::string& s, const Opts& o, Input& in, std::vector<Rec>& dst, long long& rdid, bool mate1) {
+    const char* p = s.data();
+    const size_t n = s.size();
+    size_t i = 0;
+    while (i < n && (p[i] == '\r' || p[i] == '\n')) i++;
+    if (i >= n) return;
+    if (p[i] != '>') throw Fail("Error: reads file does not look like a FASTA file");
+    std::string seq, qual;
+    while (i < n) {
+        // the record: '>' and every byte up to the next '>'
+        const size_t start = i;
+        const char* nx = (const char*)memchr(p + i + 1, '>', n - i - 1);
+        const size_t end = nx ? (size_t)(nx - p) : n;
+        i = end;
+        const char* r = p + start;
+        const size_t len = end - start;
+        const long long id = rdid++;
+        if (len == 1 && !nx) break;                 // a lone '>' at EOF: no record (pat.cpp:836-838)
+        size_t cur = 1;
+        int c = -1;
+        size_t name_end = 1;
+        bool ended = false;
+        while (cur < len) {                          // the name: the first line
+            c = (unsigned char)r[cur++];
+            if (c == '\n' || c == '\r') {
+                name_end = cur - 1;
+                do {
+                    c = cur < len ? (unsigned char)r[cur] : 0;
+                    cur++;
+                } while ((c == '\n' || c == '\r') && cur < len);
+                ended = true;
+                break;
+            }
+        }
+        if (!ended) name_end = cur;
+        if (cur >= len) continue;                    // "FASTA ended prematurely": not parsed
+        seq.clear();
+        int nchar = 0;
+        while (cur < len) {                          // the record's last byte is never a base
+            if (c == '.') c = 'N';
+            if (isalpha(c) && nchar++ >= o.trim5) seq.push_back(dna_char((unsigned char)c));
+            c = (unsigned char)r[cur++];
+            if ((c == '\n' || c == '\r') && cur < len && r[cur] != '>') c = (unsigned char)r[cur++];
+        }
+        qual.assign(seq.size(), 'I');
+        trim3(seq, qual, o.trim3);
+        std::string dflt;
+        const char* name = r + 1;
+        size_t name_len = name_end - 1;
+        if (name_len == 0) {
+            dflt = std::to_string(id);
+            name = dflt.data();
+            name_len = dflt.size();
+        }
+        Rec rec;
+        emit(in, o, rec, name, name_len, seq, qual, r, len, mate1);
+        dst.push_back(rec);
+    }
+}
+
+// tabbed_parse (pat.cpp:1550-1654) of one line: false when it does not parse;
+// pb true when it held a pair.
+bool tab_line(const char* r, size_t len, bool tab6, const Opts& o, std::string nm[2], std::string sq[2],
+              std::string ql[2], bool& pb) {
+    int c = '\t';
+    size_t cur = 0;
+    pb = false;
+    auto at = [&](size_t k) -> int { return k < len ? (unsigned char)r[k] : 0; };
+    for (int e = 0; e < 2 && c == '\t'; e++) {
+        nm[e].clear();
+        sq[e].clear();
+        ql[e].clear();
+        if (e == 0 || tab6) {
+            c = at(cur++);
+            while (c != '\t' && cur < len) {
+                nm[e].push_back((char)c);
+                c = at(cur++);
+            }
+            if (c != '\t' || cur >= len) return false;
+        } else {
+            nm[1] = nm[0];
+        }
+        c = at(cur++);
+        int nchar = 0;
+        while (c != '\t' && cur < len) {
+            if (isalpha(c) && nchar++ >= o.trim5) sq[e].push_back(dna_char((unsigned char)c));
+            c = at(cur++);
+        }
+        if (c != '\t' || cur >= len) return false;
+        c = at(cur++);
+        int nqual = 0;
+        while (c != '\t' && c != '\n' && c != '\r') {
+            if (c == ' ')                            // wrongQualityFormat (pat.cpp:2199-2205)
+                throw Fail("Error: Encountered one or more spaces while parsing the quality string for read " + nm[e] +
+                           ".  If this is a FASTQ file with integer (non-ASCII-encoded) qualities, try re-running "
+                           "with the --integer-quals option.");
+            const int q = qual33(c, o);
+            if (++nqual > o.trim5) ql[e].push_back((char)q);
+            if (cur >= len) break;
+            c = at(cur++);
+        }
+        if (nchar > nqual)
+            throw Fail("Error: Read " + nm[e] + " has more read characters than quality values.");
+        if (nqual > nchar)
+            throw Fail("Error: Read " + nm[e] + " has more quality values than read characters.");
+        trim3(sq[e], ql[e], o.trim3);
+        if (e == 1) pb = true;
+    }
+    return true;
+}
+
+// Lines of a tabbed (or raw) file in memory, as their light parsers split
+// them: blank lines skipped.
+void lines_of(const std::string& s, std::vector<RecSpan>& out) {
+    const char* p = s.data();
+    const size_t n = s.size();
+    size_t i = 0;
+    while (i < n) {
+        while (i < n && (p[i] == '\n' || p[i] == '\r')) i++;
+        if (i >= n) break;
+        const size_t st = i;
+        while (i < n && p[i] != '\n' && p[i] != '\r') i++;
+        out.push_back({st, i - st});
+    }
+}
+
+// --tab5 / --tab6 / --12 (and -c, as tab5 lines): pairs and unpaired reads
+// may mix; a[i], b[i] (b[i].tab_len == 0: read i unpaired)
+void load_tabbed(const std::vector<std::string>& lines_src, bool from_files, bool tab6, const Opts& o, Input& in) {
+    std::vector<Rec> a, b;
+    bool any_pair = false;
+    long long rdid = 0;
+    std::string nm[2], sq[2], ql[2];
+    auto one = [&](const char* r, size_t len) {
+        bool pb = false;
+        rdid++;
+        if (!tab_line(r, len, tab6, o, nm, sq, ql, pb)) return;
+        Rec ra, rb{};
+        emit(in, o, ra, nm[0].data(), nm[0].size(), sq[0], ql[0], r, len, true);
+        if (pb) {
+            emit(in, o, rb, nm[1].data(), nm[1].size(), sq[1], ql[1], r, 0, false);
+            any_pair = true;
+        }
+        a.push_back(ra);
+        b.push_back(rb);
+    };
+    if (from_files) {
+        for (const auto& f : lines_src) {
+            std::string s = slurp(f);
+            std::vector<RecSpan> ls;
+            lines_of(s, ls);
+            for (const auto& l : ls) one(s.data() + l.off, l.len);
+        }
+    } else {
+        for (const auto& l : lines_src) one(l.data(), l.size());
+    }
+    in.a.swap(a);
+    if (any_pair) in.b.swap(b);
+}
+
+// -r: RawPatternSource (pat.cpp:1743-1817)
+void load_raw(const std::string& s, const Opts& o, Input& in, std::vector<Rec>& dst, long long& rdid, bool mate1) {
+    std::vector<RecSpan> ls;
+    lines_of(s, ls);
+    std::string seq, qual;
+    for (const auto& l : ls) {
+        const char* r = s.data() + l.off;
+        const long long id = rdid++;
+        seq.clear();
+        int nchar = 0;
+        for (size_t k = 0; k < l.len; k++)
+            if (isalpha((unsigned char)r[k]) && nchar++ >= o.trim5) seq.push_back(dna_char((unsigned char)r[k]));
+        qual.assign(seq.size(), 'I');
+        trim3(seq, qual, o.trim3);
+        const std::string name = std::to_string(id);
+        Rec rec;
+        emit(in, o, rec, name.data(), name.size(), seq, qual, r, l.len, mate1);
+        dst.push_back(rec);
+    }
+}
+
 void load_mate(const std::vector<std::string>& files, const Opts& o, Input& in, std::vector<Rec>& dst, bool mate1) {
     long long rdid = 0;
+    if (o.fmt == Opts::FASTA || o.fmt == Opts::RAW) {
+        for (const auto& f : files) {
+            std::string s = slurp(f);
+            if (o.fmt == Opts::FASTA) load_fasta(s, o, in, dst, rdid, mate1);
+            else load_raw(s, o, in, dst, rdid, mate1);
+        }
+        return;
+    }
+    if (o.fmt == Opts::CMDLINE) {
+        // VectorPatternSource: "i\tSEQ\tQUALS" (QUALS 'I' when not given)
+        Input tmp;
+        std::vector<std::string> lines;
+        for (size_t i = 0; i < files.size(); i++) {
+            const std::string& t = files[i];
+            const size_t k = t.find(':');
+            const std::string sq = t.substr(0, k);
+            lines.push_back(std::to_string(i) + "\t" + sq + "\t" +
+                            (k == std::string::npos ? std::string(sq.size(), 'I') : t.substr(k + 1)));
+        }
+        tmp.arena.swap(in.arena);
+        tmp.used = in.used;
+        tmp.bad_names = in.bad_names;
+        load_tabbed(lines, false, false, o, tmp);
+        in.arena.swap(tmp.arena);
+        in.used = tmp.used;
+        in.bad_names = tmp.bad_names;
+        for (const Rec& r : tmp.a) dst.push_back(r);
+        return;
+    }
     for (const auto& f : files) {
         std::string s = slurp(f);
         std::string scratch;
@@ -369,7 +669,10 @@ void load_mate(const std::vector<std::string>& files, const Opts& o, Input& in, 
 std::unique_ptr<Input> load_input(const std::vector<std::string>& U, const std::vector<std::string>& m1,
                                    const std::vector<std::string>& m2, const Opts& o) {
     std::unique_ptr<Input> in(new Input);
-    if (!m1.empty() || !m2.empty()) {
+    if (o.fmt == Opts::TAB5 || o.fmt == Opts::TAB6) {
+        // (the files of --tab5 / --tab6 / --12 come in U: one read or pair a line)
+        load_tabbed(U, true, o.fmt == Opts::TAB6, o, *in);
+    } else if (!m1.empty() || !m2.empty()) {
         load_mate(m1, o, *in, in->a, true);
         load_mate(m2, o, *in, in->b, false);
         if (in->a.size() < in->b.size())
@@ -432,7 +735,7 @@ inline int take_slot(Conn& c, uint32_t read) {
             int id = c.used_idx[m]++;
             c.used_cnt[m]++;
             c.slot[m][id] = read;
-            c.present[m][id] = c.in->paired() ? 3 : 1;
+            c.present[m][id] = c.in->pair(read) ? 3 : 1;
             return id + m * BUF_CAPACITY;
         }
     }
@@ -487,7 +790,7 @@ bool fill_out(Conn& c) {
             hex4(nm, id);
             c.out.append(nm, 6);
             c.out.append(A + a.tab, a.tab_len);
-            if (in.paired()) {
+            if (in.pair(c.next)) {
                 const Rec& b = in.b[c.next];
                 nm[5] = '2';
                 c.out.push_back('\t');
@@ -542,7 +845,7 @@ void read_line(Conn& c, const char* line, size_t n, bool xr) {
     if (c.count) {
         const unsigned long f = strtoul(tab + 1, nullptr, 10);
         if (!(f & 0x900)) {
-            if (in.paired()) c.aligned += (f & 0x40) && (f & 0xC) != 0xC;
+            if (f & 0x1) c.aligned += (f & 0x40) && (f & 0xC) != 0xC;
             else c.aligned += !(f & 0x4);
         }
     }
@@ -550,7 +853,7 @@ void read_line(Conn& c, const char* line, size_t n, bool xr) {
         unsigned long flags = strtoul(tab + 1, nullptr, 10);
         bool mate2 = (flags & 0x1) && (flags & 0x80);
         if (!mate2) c.sam.append(in.arena.data() + a.orig, a.orig_len);
-        else if (in.paired()) c.sam.append(in.arena.data() + in.b[r].orig, in.b[r].orig_len);
+        else if (in.pair(r)) c.sam.append(in.arena.data() + in.b[r].orig, in.b[r].orig_len);
         c.sam.push_back('\n');
     }
 }
@@ -870,7 +1173,8 @@ void usage() {
     fprintf(stderr,
             "Usage: bt2g-client -x <index> (-U f[,f..] | -1 f1 -2 f2) [-k conns] [-R reads/conn] [-p threads]\n"
             "                   [-S out.sam] [--server-host H] [--server-port P] [--passthrough] [-3 n] [-5 n]\n"
-            "                   [--phred33|--phred64] [-s skip] [-u upto] [--no-hd] [-q] [--stats]\n"
+            "                   [--phred33|--phred64] [-s skip] [-u upto] [--no-hd] [--stats]\n"
+            "                   [-q | -f | -r | -c | --tab5 f | --12 f | --tab6 f]\n"
             "       bt2g-client -x <index> --chunks LIST [-k conns] [-p threads] [--out-dir D | -S out.sam]\n"
             "                   [--mark-chunks] [--count-aligned]\n");
 }
@@ -913,7 +1217,13 @@ int main(int argc, char** argv) {
         else if (a == "--stats") o.stats = true;
         else if (a == "--mark-chunks") o.mark = true;
         else if (a == "--count-aligned") o.count = true;
-        else if (a == "-q" || a == "--no-hd" || a == "--quiet" || a == "-t") {
+        else if (a == "-f" || a == "--fasta") o.fmt = Opts::FASTA;
+        else if (a == "-q" || a == "--fastq") o.fmt = Opts::FASTQ;
+        else if (a == "-r" || a == "--raw") o.fmt = Opts::RAW;
+        else if (a == "-c") o.fmt = Opts::CMDLINE;
+        else if (a == "--tab5" || a == "--12") { o.fmt = Opts::TAB5; split_commas(val(), o.U); }
+        else if (a == "--tab6") { o.fmt = Opts::TAB6; split_commas(val(), o.U); }
+        else if (a == "--no-hd" || a == "--quiet" || a == "-t") {
         } else if (a == "-h" || a == "--help") {
             usage();
             return 0;

@@ -67,6 +67,9 @@ trace)
   find $O/tprof -name "*memory_copy_stats.csv" -exec cp {} $O/trace_copy_stats.csv \;
   python3 scripts/trace_gaps.py $O/tprof > $O/trace_gaps.txt 2>&1; tail -40 $O/trace_gaps.txt
   find $O/tprof -name "*.csv" -size +60M -delete ;;
+fmtests)
+  timeout -k 10 600 python -u -m pytest tests/test_gpu_fm.py tests/test_batch.py -m gpu -x -v --timeout 300 --timeout-method thread > $O/fm_tests.log 2>&1 || { tail -20 $O/fm_tests.log; exit 1; }
+  tail -2 $O/fm_tests.log ;;
 diag)
   bash $0 tests $2 && bash $0 quick $2 && bash $0 trace $2 ;;
 quick)

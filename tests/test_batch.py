@@ -62,12 +62,12 @@ def _reads(idx, n, seed, dirpath, read_len=150, paired=False):
     return rs.write_fastq_chunks(dirpath, r, q)
 
 
-def _run(binary, base, chunks, args, dirpath, tag, threads=2, env_extra=None):
+def _run(binary, base, chunks, args, dirpath, tag, threads=2, env_extra=None, client=None):
     stats = os.path.join(dirpath, f"stats_{tag}.json")
     env = dict(rs.dropin_env(base, stats), **(env_extra or {}))
     with rs.Server(base, threads=threads, args=args, binary=binary, env=env,
                    log_path=os.path.join(dirpath, f"server_{tag}.log")) as s:
-        dt, outs = s.run(chunks, k=2)
+        dt, outs = s.run(chunks, k=2, client=client or rs.CLIENT)
     st = None
     for _ in range(50):                      # written by the driver's SIGTERM handler
         if os.path.exists(stats):
@@ -77,9 +77,12 @@ def _run(binary, base, chunks, args, dirpath, tag, threads=2, env_extra=None):
     return dt, rs.sorted_records(outs), st
 
 
-def compare(binary, base, chunks, args, dirpath, threads=2, env_extra=None, cpu_ok=()):
+def compare(binary, base, chunks, args, dirpath, threads=2, env_extra=None, cpu_ok=(), client=None):
+    """The stock server through the reference client against `binary` through
+    `client` (default: the reference client too; rs.NATIVE_CLIENT: bt2g-client,
+    as bench.py sends its reads): sorted SAM identical, no CPU fallback."""
     t_ref, a, _ = _run(rs.SERVER, base, chunks, args, dirpath, "ref")
-    t_new, b, st = _run(binary, base, chunks, args, dirpath, "batch", threads, env_extra)
+    t_new, b, st = _run(binary, base, chunks, args, dirpath, "batch", threads, env_extra, client)
     assert len(a) == len(b) and len(a) > 0
     bad = [(x, y) for x, y in zip(a, b) if x != y]
     assert not bad, f"{len(bad)} SAM records differ, first:\nref   {bad[0][0][:400]}\nbatch {bad[0][1][:400]}"
@@ -223,3 +226,44 @@ def test_batch_longreads_gpu(indexes, tmp_path):
     t_ref, t_new, nrec, st = compare(SRV_BATCH, indexes["lambda"], [["-U", LONGREADS]], [], str(tmp_path),
                                      cpu_ok=("exact_sweep", "seed_search", "extend", "sw_dp"))
     print(f"\n[longreads] {nrec} records identical; stock {t_ref:.2f}s, batch {t_new:.2f}s; {st}")
+
+
+def _client_inputs(idx, dirpath):
+    """Reads for the client checks: FASTQ chunks, and the same reads as FASTA and tab6."""
+    import bench
+    r, q = bench.make_pairs(idx.ref_codes, 3000, 150, 31)
+    n = 3000
+    acgt = b"ACGTN"
+    fa = os.path.join(dirpath, "r.fa")
+    t6 = os.path.join(dirpath, "r.tab6")
+    with open(fa, "wb") as f:
+        f.write(b"".join(b">f%d\n%s\n" % (i, bytes(acgt[c] for c in r[i])) for i in range(n)))
+    with open(t6, "wb") as f:
+        f.write(b"".join(b"t%d/1\t%s\t%s\tt%d/2\t%s\t%s\n" % (i, bytes(acgt[c] for c in r[i]), bytes(q[i]), i,
+                                                               bytes(acgt[c] for c in r[n + i]), bytes(q[n + i]))
+                         for i in range(n)))
+    return [["-f", "-U", fa], ["--tab6", t6]]
+
+
+@pytest.mark.parametrize("fmt", [0, 1], ids=["fasta", "tab6"])
+def test_batch_native_client_cpu(indexes, tmp_path, fmt):
+    """Row (f)-4 on the stand-in: bt2g-client into the batch server, the reference
+    client into the stock server -- same SAM (FASTA and paired/unpaired-mixed
+    tab6 inputs; FASTQ in the GPU case and bench.py's sam_parity)."""
+    _need(rs.SERVER, rs.CLIENT, SRV_BATCH_STUB, rs.NATIVE_CLIENT)
+    base, idx = indexes["synth"]
+    compare(SRV_BATCH_STUB, base, [_client_inputs(idx, str(tmp_path))[fmt]], [], str(tmp_path),
+            client=rs.NATIVE_CLIENT)
+
+
+@pytest.mark.gpu
+def test_batch_native_client_gpu(indexes, tmp_path):
+    """Row (f)-4 on the GPU box: the batch server on the engines fed by bt2g-client
+    (FASTQ chunks of unpaired reads and pairs, FASTA, tab6) against the stock
+    server fed by the reference client (bowtie2-align-l)."""
+    _need(rs.SERVER, rs.CLIENT, SRV_BATCH, rs.NATIVE_CLIENT)
+    base, idx = indexes["synth"]
+    chunks = _reads(idx, 12000, 37, str(tmp_path)) + _reads(idx, 3000, 41, str(tmp_path), paired=True)
+    compare(SRV_BATCH, base, chunks, [], str(tmp_path), threads=8, client=rs.NATIVE_CLIENT)
+    for inp in _client_inputs(idx, str(tmp_path)):
+        compare(SRV_BATCH, base, [inp], [], str(tmp_path), threads=8, client=rs.NATIVE_CLIENT)

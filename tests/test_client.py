@@ -216,3 +216,85 @@ def test_errors_like_reference(server, tmp_path):
     assert r.returncode != 0 and b"does not look like a FASTQ file" in r.stderr
     r = subprocess.run([CLIENT, "-x", base, "-U", str(bad), "--server-port", "1"], capture_output=True, timeout=60)
     assert r.returncode != 0
+
+
+def _seqs(idx, n, seed):
+    import bench
+    r, q = bench.make_reads(idx.ref_codes, n, 150, seed)
+    acgt = b"ACGTN"
+    return [bytes(acgt[c] for c in r[i]) for i in range(n)], [bytes(q[i]) for i in range(n)]
+
+
+def test_fasta_same_sam(server, tmp_path):
+    """-f: FastaPatternSource (pat.cpp:790-912) -- multi-line records, lower case,
+    '.' and IUPAC letters, CRLF, an empty name (its read number), blank lines,
+    no newline after the last record (whose last base the reference drops);
+    unpaired, trimmed, and -1/-2 pairs."""
+    s, base, idx = server["synth"]
+    seqs, _ = _seqs(idx, 60, 21)
+    recs = []
+    for i, sq in enumerate(seqs):
+        name = [b"f%d/1" % i, b"f%d desc" % i, b"", b"f%d" % i][i % 4]
+        if i % 5 == 2:
+            sq = sq[:40].lower() + sq[40:]
+        if i % 7 == 3:
+            sq = sq[:50] + b"R.Y" + sq[53:]
+        nl = b"\r\n" if i % 3 == 0 else b"\n"
+        body = nl.join(sq[k:k + 60] for k in range(0, len(sq), 60))
+        recs.append(b">" + name + nl + body + nl + (b"\n" if i % 6 == 5 else b""))
+    f = tmp_path / "r.fa"
+    f.write_bytes(b"\n" + b"".join(recs).rstrip(b"\n"))
+    for extra in ([], ["-5", "3", "-3", "6"]):
+        a = ["-f", "-U", str(f)] + extra
+        _same(_ref(s, base, a), _ours(s, base, a))
+    r, q, r2, q2 = _reads(idx, 300, 22, paired=True)
+    acgt = b"ACGTN"
+    f1, f2 = tmp_path / "p1.fa", tmp_path / "p2.fa"
+    f1.write_bytes(b"".join(b">p%d/1\n%s\n" % (i, bytes(acgt[c] for c in r[i])) for i in range(len(r))))
+    f2.write_bytes(b"".join(b">p%d/2\n%s\n" % (i, bytes(acgt[c] for c in r2[i])) for i in range(len(r2))))
+    a = ["-f", "-1", str(f1), "-2", str(f2)]
+    _same(_ref(s, base, a), _ours(s, base, a))
+    a += ["--passthrough"]
+    _same(_ref(s, base, a), _ours(s, base, a))
+
+
+def test_tabbed_same_sam(server, tmp_path):
+    """--tab5 / --12 / --tab6: TabbedPatternSource (pat.cpp:1524-1661) -- unpaired
+    and paired lines mixed in one file, blank lines, CRLF; --passthrough."""
+    s, base, idx = server["synth"]
+    r, q, r2, q2 = _reads(idx, 200, 23, paired=True)
+    acgt = b"ACGTN"
+    l5, l6 = [], []
+    for i in range(len(r)):
+        s1, q1 = bytes(acgt[c] for c in r[i]), bytes(q[i])
+        s2, qq2 = bytes(acgt[c] for c in r2[i]), bytes(q2[i])
+        nl = b"\r\n" if i % 4 == 0 else b"\n"
+        if i % 3 == 0:
+            l5.append(b"u%d\t%s\t%s%s" % (i, s1, q1, nl))
+            l6.append(b"u%d\t%s\t%s%s" % (i, s1, q1, nl))
+        else:
+            l5.append(b"t%d\t%s\t%s\t%s\t%s%s" % (i, s1, q1, s2, qq2, nl))
+            l6.append(b"t%d/1\t%s\t%s\tt%d/2\t%s\t%s%s" % (i, s1, q1, i, s2, qq2, nl))
+        if i % 17 == 5:
+            l5.append(b"\n")
+    f5, f6 = tmp_path / "r.tab5", tmp_path / "r.tab6"
+    f5.write_bytes(b"".join(l5))
+    f6.write_bytes(b"".join(l6))
+    for a in (["--tab5", str(f5)], ["--12", str(f5)], ["--tab6", str(f6)], ["--tab6", str(f6), "--passthrough"],
+              ["--tab5", str(f5), "-3", "5"]):
+        _same(_ref(s, base, a), _ours(s, base, a))
+
+
+def test_raw_and_cmdline_same_sam(server, tmp_path):
+    """-r (RawPatternSource, pat.cpp:1743-1817) and -c (VectorPatternSource,
+    pat.cpp:614-700: SEQ[:QUALS] arguments)."""
+    s, base, idx = server["synth"]
+    seqs, quals = _seqs(idx, 80, 24)
+    f = tmp_path / "r.raw"
+    f.write_bytes(b"".join(sq + (b"\r\n" if i % 5 == 0 else b"\n") + (b"\n" if i % 9 == 2 else b"")
+                           for i, sq in enumerate(seqs)))
+    _same(_ref(s, base, ["-r", "-U", str(f)]), _ours(s, base, ["-r", "-U", str(f)]))
+    # (qualities without ',' or ':', the argument's separators)
+    qs = [bytes(65 + c % 9 for c in qv).decode() for qv in quals]
+    cl = ",".join(sq.decode() + (":" + qs[i] if i % 2 else "") for i, sq in enumerate(seqs[:12]))
+    _same(_ref(s, base, ["-c", "-U", cl]), _ours(s, base, ["-c", "-U", cl]))
