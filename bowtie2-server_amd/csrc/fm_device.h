@@ -240,6 +240,94 @@ __device__ __forceinline__ int bi_step_tb(const DevEbwt& e, uint32_t top, uint32
 	return sb == st ? 1 : 2;
 }
 
+// ---- the cooperative step: a quad of lanes per walk ------------------------
+// north_star: LF mapping "via coalesced occ-table gathers with LDS-staged rank
+// blocks".  In the batch server the FM calls carry a round's few hundred reads:
+// one lane per walk leaves ~15 waves on 1 024 SIMDs, each issuing ~200 VALU
+// instructions of side counting per dependent step (round 5: ~2.2 us per step
+// against ~0.6 us for the gather).  Here a side is counted by the four lanes of
+// a quad (countBt2Side, bt2_idx.h:1758-1919): lane q loads 16 B of the 64-B
+// side -- q = 0..2 the BWT words 4q..4q+3 (rows 64q..64q+63), q = 3 the four
+// occurrence counts -- in ONE coalesced 64-B request per quad, counts its four
+// words, and the quad sums by DPP (quad_perm) in registers; lane 3's counts
+// reach the others the same way.  Every lane of a quad runs the walk's control
+// flow on identical values, so the quad never diverges.
+struct QuadSide {
+	uint32_t w[4];
+};
+
+__device__ __forceinline__ void load_quad(const DevEbwt& e, uint32_t side, uint32_t q, QuadSide& s) {
+	typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+	typedef const __attribute__((address_space(1))) u32x4 gu32x4;
+	const gu32x4* p = (const gu32x4*)(e.sides + (size_t)side * 64u) + q;
+	const u32x4 a = *p;
+	s.w[0] = a.x; s.w[1] = a.y; s.w[2] = a.z; s.w[3] = a.w;
+}
+
+// sum over the lane's quad (quad_perm [1,0,3,2] then [2,3,0,1])
+__device__ __forceinline__ uint32_t quad_sum(uint32_t x) {
+	x += (uint32_t)__builtin_amdgcn_mov_dpp((int)x, 0xB1, 0xF, 0xF, false);
+	x += (uint32_t)__builtin_amdgcn_mov_dpp((int)x, 0x4E, 0xF, 0xF, false);
+	return x;
+}
+// lane 3's value in every lane of the quad (quad_perm [3,3,3,3])
+__device__ __forceinline__ uint32_t quad_lane3(uint32_t x) {
+	return (uint32_t)__builtin_amdgcn_mov_dpp((int)x, 0xFF, 0xF, 0xF, false);
+}
+
+// w[i] of a quad side without a data-dependent register index
+__device__ __forceinline__ uint32_t quad_word(const QuadSide& s, uint32_t i) {
+	uint32_t x0 = s.w[0], x1 = s.w[1], x2 = s.w[2], x3 = s.w[3];
+	asm volatile("" : "+v"(x0), "+v"(x1), "+v"(x2), "+v"(x3));
+	return i == 0 ? x0 : i == 1 ? x1 : i == 2 ? x2 : x3;
+}
+
+// this lane's share of the count of `ch` among the side's first charOff rows
+// (lane 3, the occurrence counts: 0)
+__device__ __forceinline__ uint32_t quad_part1(const QuadSide& s, uint32_t q, uint32_t charOff, int ch) {
+	const uint32_t x = (uint32_t)(3 - ch) * 0x55555555u;
+	const int rem = q < 3u ? (int)charOff - 64 * (int)q : 0;
+	uint32_t n = 0;
+#pragma unroll
+	for(int k = 0; k < 4; k++) {
+		int nk = rem - 16 * k;
+		nk = nk < 0 ? 0 : (nk > 16 ? 16 : nk);
+		const uint32_t m = nk >= 16 ? 0x55555555u : ((1u << (2 * nk)) - 1u) & 0x55555555u;
+		const uint32_t y = s.w[k] ^ x;
+		n += __builtin_popcount(y & (y >> 1) & m);
+	}
+	return n;
+}
+
+// countBt2Side for one character, the side in the quad (occ1's quad form)
+__device__ __forceinline__ uint32_t quad_occ1(const DevEbwt& e, const QuadSide& s, uint32_t q, uint32_t row, int ch) {
+	const uint32_t side = row / 192u, co = row % 192u;
+	uint32_t n = quad_sum(quad_part1(s, q, co, ch));
+	if(ch == 0 && dollar_before(e, side, co)) n--;
+	return n + quad_lane3(quad_word(s, (uint32_t)ch)) + fchr_at(e, ch);
+}
+
+// top's count in side s1 and bot's in side s2 for one character: one packed
+// quad sum (each share is <= 64)
+__device__ __forceinline__ void quad_occ2(const DevEbwt& e, const QuadSide& s1, const QuadSide& s2, uint32_t q,
+                                          uint32_t top, uint32_t bot, int ch, uint32_t& nt, uint32_t& nb) {
+	const uint32_t st = top / 192u, ct = top % 192u, sb = bot / 192u, cb = bot % 192u;
+	const uint32_t p = quad_sum(quad_part1(s1, q, ct, ch) | (quad_part1(s2, q, cb, ch) << 16));
+	uint32_t a = p & 0xffffu, b = p >> 16;
+	if(ch == 0 && dollar_before(e, st, ct)) a--;
+	if(ch == 0 && dollar_before(e, sb, cb)) b--;
+	const uint32_t f = fchr_at(e, ch);
+	nt = a + quad_lane3(quad_word(s1, (uint32_t)ch)) + f;
+	nb = b + quad_lane3(quad_word(s2, (uint32_t)ch)) + f;
+}
+
+// character of row charOff of the quad's side (side_rowL's quad form)
+__device__ __forceinline__ int quad_rowL(const QuadSide& s, uint32_t q, uint32_t charOff) {
+	const uint32_t k = charOff >> 4;                 // the word: lane k >> 2, its word k & 3
+	const uint32_t v = ((k >> 2) == q) ? ((quad_word(s, k & 3u) >> (2 * (charOff & 15))) & 3u) + 1u : 0u;
+	return (int)quad_sum(v) - 1;
+}
+
 // A read (or its reverse complement / reversal) as the reference's BTDnaString
 // views: patFw (rev=0,cmp=0), patRc (1,1), patFwRev (1,0), patRcRev (0,1).
 struct SeqView {

@@ -137,6 +137,111 @@ k_exact_sweep(DevEbwt e, const uint8_t* __restrict__ reads, uint32_t stride, con
 	out[(size_t)r * 8 + 6 + strand] = strand == 0 ? bw2 : ld2;
 }
 
+// The exact sweep with a quad of lanes per (read, strand) (fm_device.h, the
+// cooperative step): lanes 8r..8r+3 strand 0 of read r, 8r+4..8r+7 strand 1.
+// Same control flow and outputs as k_exact_sweep, lane for quad.
+__global__ void __launch_bounds__(256)
+k_exact_sweep_quad(DevEbwt e, const uint8_t* __restrict__ reads, uint32_t stride, const uint32_t* __restrict__ lens,
+                   uint32_t n, uint32_t mine_max, int nofw, int norc, uint32_t* __restrict__ out) {
+	walk_prio();
+	const uint32_t gid = blockIdx.x * blockDim.x + threadIdx.x;
+	const uint32_t q = gid & 3u, chain = gid >> 2;
+	const uint32_t r = chain >> 1, strand = chain & 1u;
+	const bool valid = r < n;
+	const bool active = valid && !((strand == 0 && nofw) || (strand == 1 && norc));
+	const uint32_t len = active ? lens[r] : 0;
+	ReadWin rw{reads, reads + (size_t)n * stride};
+	const uint8_t* row = reads + (size_t)(active ? r : 0) * stride;
+	auto seq_at = [&](uint32_t k) -> int {
+		const int c = rw.at(row + (strand == 1 ? len - 1 - k : k));
+		return strand == 1 ? (c > 3 ? 4 : 3 - c) : c;
+	};
+	auto base_at = [&](uint32_t d) -> int { return seq_at(len - d - 1); };
+	const uint32_t flen = e.ftab_chars;
+	uint32_t dep = 0, nedit = 0, top = 0, bot = 0, mine = 0;
+	uint32_t bwops = 0, loads = 0;
+	bool doinit = true, done = !active;
+	while(dep < len && !done) {
+		if(doinit) {
+			top = bot = 0;
+			uint32_t left = len - dep;
+			bool doftab = flen > 1 && left >= flen;
+			uint32_t fi = 0;
+			if(doftab) {
+				for(uint32_t i = 0; i < flen; i++) {
+					int c = seq_at(left - flen + i);
+					if(c > 3) { doftab = false; break; }
+					fi = (fi << 2) | (uint32_t)c;
+				}
+			}
+			if(doftab) {
+				const uint32_t v0 = e.ftab[fi], v1 = e.ftab[fi + 1];
+				const bool x0 = v0 > e.len, x1 = v1 > e.len;
+				const uint32_t et = x0 ? e.eftab[(v0 ^ BT2G_OFF_MASK) * 2 + 1] : v0;
+				const uint32_t eb = x1 ? e.eftab[(v1 ^ BT2G_OFF_MASK) * 2] : v1;
+				top = et;
+				bot = eb;
+				dep += flen;
+			} else {
+				int c = seq_at(len - dep - 1);
+				if(c < 4) { top = fchr_at(e, c); bot = fchr_at(e, c + 1); }
+				dep++;
+			}
+			if(bot <= top) {
+				nedit++;
+				if(nedit >= mine_max) { mine = nedit; done = true; }
+				continue;
+			}
+			doinit = false;
+		}
+		if(dep < len) {
+			const int c = base_at(dep);
+			const bool rng = bot - top > 1;
+			const uint32_t st = top / 192u, sb = rng ? bot / 192u : st;
+			QuadSide s1, s2;
+			load_quad(e, st, q, s1);
+			load_quad(e, sb, q, s2);
+			if(c > 3) {
+				top = bot = 0;
+			} else if(rng) {
+				bwops += 2;
+				loads += sb == st ? 1u : 2u;
+				uint32_t nt, nb;
+				quad_occ2(e, s1, s2, q, top, bot, c, nt, nb);
+				top = nt; bot = nb;
+			} else {
+				bwops += 1;
+				loads++;
+				if(quad_rowL(s1, q, top % 192u) != c || top == e.zoff) {
+					top = bot = 0;
+				} else {
+					top = quad_occ1(e, s1, q, top, c);
+					bot = top + 1;
+				}
+			}
+			if(bot <= top) {
+				nedit++;
+				if(nedit >= mine_max) { mine = nedit; done = true; }
+				doinit = true;
+			}
+			dep++;
+		}
+	}
+	uint32_t otop = 0, obot = 0;
+	if(active && !done && dep >= len) {
+		mine = nedit;
+		if(nedit == 0 && bot > top) { otop = top; obot = bot; }
+	}
+	// both strands' bwops / side loads: the other strand's quad is 4 lanes away
+	const uint32_t bw2 = bwops + (uint32_t)__shfl_xor((int)bwops, 4);
+	const uint32_t ld2 = loads + (uint32_t)__shfl_xor((int)loads, 4);
+	if(!valid || q != 0) return;
+	out[(size_t)r * 8 + strand] = mine;
+	out[(size_t)r * 8 + 2 + 2 * strand] = otop;
+	out[(size_t)r * 8 + 3 + 2 * strand] = obot;
+	out[(size_t)r * 8 + 6 + strand] = strand == 0 ? bw2 : ld2;
+}
+
 // --------------------------------------------------------------------------
 // Exact seeds: instantiateSeeds (aligner_seed.cpp:498-587, Seed::instantiate
 // 214-358) + searchSeedBi for SEED_TYPE_EXACT (80-122, 1633-1714, 1854-2033).
@@ -297,6 +402,15 @@ k_get_offset(DevEbwt e, const uint32_t* __restrict__ rows, uint32_t n, uint32_t*
 // --------------------------------------------------------------------------
 void launch_exact_sweep(const DevEbwt& e, const uint8_t* reads, uint32_t stride, const uint32_t* lens, uint32_t n,
                         uint32_t mine_max, int nofw, int norc, uint32_t* out, hipStream_t st) {
+	// $BT2G_FM_QUAD=0: one lane per (read, strand); default (round 6): a quad of
+	// lanes per walk (k_exact_sweep_quad) -- read at every launch (A/B in one process)
+	const char* qe = getenv("BT2G_FM_QUAD");
+	if(!(qe && *qe == '0')) {
+		const uint64_t threads = (uint64_t)n * 8;
+		hipLaunchKernelGGL(k_exact_sweep_quad, dim3((uint32_t)((threads + 255) / 256)), dim3(256), 0, st, e, reads,
+		                   stride, lens, n, mine_max, nofw, norc, out);
+		return;
+	}
 	const uint32_t threads = n * 2;
 	hipLaunchKernelGGL(k_exact_sweep, dim3((threads + 255) / 256), dim3(256), 0, st, e, reads, stride, lens, n,
 	                   mine_max, nofw, norc, out);

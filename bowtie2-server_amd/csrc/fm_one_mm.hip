@@ -844,7 +844,8 @@ void launch_one_mm_q(const DevEbwt& F, const DevEbwt& B, const uint8_t* reads, c
 	// $BT2G_MM_MERGED=0: the two index directions as separate launches on two
 	// streams (forked and joined by events), as before round 6; default: one
 	// launch per stage for both (k_one_mm_*2)
-	static const bool merged = [] { const char* e = getenv("BT2G_MM_MERGED"); return !(e && *e == '0'); }();
+	const char* me = getenv("BT2G_MM_MERGED");            // (read per call: A/B in one process)
+	const bool merged = !(me && *me == '0');
 	if(merged) {
 		hipLaunchKernelGGL(k_one_mm_items, dim3((n + 255) / 256), dim3(256), 0, st, reads, stride, lens, n, gate, nofw,
 		                   norc, items, counters, slot_counts, ops, loads, slot_flag);

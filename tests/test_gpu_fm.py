@@ -114,6 +114,56 @@ def test_large_batch_vs_oracle(engines, orc):
                 tuple(int(v) for v in h_cpu[i, k])
 
 
+def _reads_with_errors(n, seed):
+    import synth
+    idx = get_index("synth")
+    gen = np.concatenate(idx.ref_codes)
+    codes, quals, _, _ = synth.reads(seed, gen, n, 150, sub=0.01, nrate=0.002)
+    lens = np.full(n, 150, np.uint32)
+    rng = np.random.default_rng(seed)
+    short = rng.random(n) < 0.1
+    lens[short] = rng.integers(1, 150, short.sum())
+    for i in np.nonzero(short)[0]:
+        codes[i, lens[i]:] = 4
+    return codes, quals, lens
+
+
+@pytest.mark.parametrize("n", [1, 7, 450, 20000])
+def test_exact_sweep_quad_equals_lane(engines, n, monkeypatch):
+    """The quad-cooperative exact sweep (k_exact_sweep_quad, fm_device.h: a side
+    counted by four lanes, summed by DPP) against the one-lane kernel on the same
+    reads, every output word (ranges, mine, bwops, side loads), nofw / norc too;
+    and against the reference's golden sweep."""
+    codes, _, lens = _reads_with_errors(max(n, 2), 77 + n)
+    codes, lens = codes[:n], lens[:n]
+    e = engines["synth"]
+    for nofw, norc in ((0, 0), (1, 0), (0, 1)):
+        monkeypatch.setenv("BT2G_FM_QUAD", "0")
+        a = e.exact_sweep(codes, lens, nofw=nofw, norc=norc)
+        monkeypatch.setenv("BT2G_FM_QUAD", "1")
+        b = e.exact_sweep(codes, lens, nofw=nofw, norc=norc)
+        assert np.array_equal(a, b), (nofw, norc, np.nonzero((a != b).any(1))[0][:5])
+    for name in ("lambda", "synth"):
+        g = load_golden("fm_" + name)
+        out = engines[name].exact_sweep(g["reads"], g["lens"])
+        assert np.array_equal(out[:, :7], _gold_exact_to_gpu_layout(g["exact"]))
+
+
+def test_one_mm_merged_equals_split(engines, monkeypatch):
+    """The 1-mm search with both index directions in one launch per stage
+    (k_one_mm_*2, the default) against the two-stream form: hits, counts, bwops."""
+    codes, quals, lens = _reads_with_errors(3000, 91)
+    ms = np.array([int(-0.6 - 0.6 * L) for L in lens], np.int64)
+    e = engines["synth"]
+    monkeypatch.setenv("BT2G_MM_MERGED", "0")
+    h0, c0, o0, l0 = e.one_mm(codes, quals, lens, ms, False)
+    monkeypatch.setenv("BT2G_MM_MERGED", "1")
+    h1, c1, o1, l1 = e.one_mm(codes, quals, lens, ms, False)
+    assert np.array_equal(c0, c1) and np.array_equal(o0, o1)
+    for i in np.nonzero(c0)[0]:
+        assert np.array_equal(h0[i, :c0[i]], h1[i, :c0[i]]), i
+
+
 @pytest.mark.parametrize("brq_cap", [1, 7, 64])
 def test_one_mm_branch_queue_overflow(engines, brq_cap, monkeypatch):
     """A branch queue far too small for the batch ($BT2G_MM_BRQ_CAP): items whose
