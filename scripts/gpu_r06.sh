@@ -67,6 +67,12 @@ trace)
   find $O/tprof -name "*memory_copy_stats.csv" -exec cp {} $O/trace_copy_stats.csv \;
   python3 scripts/trace_gaps.py $O/tprof > $O/trace_gaps.txt 2>&1; tail -40 $O/trace_gaps.txt
   find $O/tprof -name "*.csv" -size +60M -delete ;;
+cpuprof)
+  # the batch server's per-read logic by phase ($BT2G_PHASES) and a flat CPU profile of its threads ($BT2G_SAMPLE)
+  BT2G_PHASES=1 BT2G_SAMPLE=$PWD/$O/samples.txt timeout -k 10 600 python3 -u bench.py --steps ${3:-3} --warmup 1 --chain-steps 0 \
+    --stock-sample 0 $BENCH_ARGS > $O/bench_phases.json 2> $O/bench_phases.log || { tail -30 $O/bench_phases.log; exit 1; }
+  cp integration/bin/bowtie2-align-server-batch $O/server.bin
+  summ $O/bench_phases.json phases ;;
 fmtests)
   timeout -k 10 600 python -u -m pytest tests/test_gpu_fm.py tests/test_batch.py -m gpu -x -v --timeout 300 --timeout-method thread > $O/fm_tests.log 2>&1 || { tail -20 $O/fm_tests.log; exit 1; }
   tail -2 $O/fm_tests.log ;;
