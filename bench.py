@@ -505,7 +505,9 @@ def pmc_traffic(fetch_csv, write_csv, kernel):
     return total
 
 
-BATCH_SERVER = os.path.join(ROOT, "integration", "bin", "bowtie2-align-server-batch")
+# ($BT2G_BENCH_SERVER_BIN: another build of it, for A/B runs on one lease)
+BATCH_SERVER = os.environ.get("BT2G_BENCH_SERVER_BIN") or os.path.join(ROOT, "integration", "bin",
+                                                                     "bowtie2-align-server-batch")
 # HBM traffic per launch of the batch server's kernels: the summary of separate
 # rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes over this same bench command
 # (scripts/gpu_r06.sh prof -> scripts/pmc_summary.py), committed under profiles/

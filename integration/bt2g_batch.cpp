@@ -64,6 +64,8 @@
 #include <execinfo.h>
 #include <unistd.h>
 #include <sys/mman.h>
+#include <sys/resource.h>
+#include <sys/syscall.h>
 
 #include <algorithm>
 #include <array>
@@ -590,11 +592,16 @@ template struct PoolPeek<PoolCur, &Pool::cur_>;
 struct DiagBins { typedef EList<EIvalMergeList> EIvalMergeListBinned::*type; friend type peek(DiagBins); };
 template struct PoolPeek<DiagBins, &EIvalMergeListBinned::bins_>;
 
-const size_t POOL_KEEP = 16;                   // pages (16 KB each, CACHE_PAGE_SZ) a pool keeps
+// pages (16 KB each, CACHE_PAGE_SZ) a pool keeps ($BT2G_POOL_KEEP_PAGES, default 16)
+size_t pool_keep() {
+	static const size_t k = env_or("BT2G_POOL_KEEP_PAGES", 16);
+	return k;
+}
 
-// After a read: the pages the pool handed out beyond POOL_KEEP go back.
+// After a read: the pages the pool handed out beyond pool_keep() go back.
 void pool_trim(Pool& p) {
 	const size_t used = p.*peek(PoolCur());
+	const size_t POOL_KEEP = pool_keep();
 	if(used <= POOL_KEEP) return;
 	uint8_t* base = p.*peek(PoolSuper());
 	const uintptr_t lo = ((uintptr_t)base + POOL_KEEP * CACHE_PAGE_SZ + 4095) & ~(uintptr_t)4095;
@@ -604,6 +611,95 @@ void pool_trim(Pool& p) {
 	g_pool_trims++;
 	g_pool_trim_pages += used - POOL_KEEP;
 }
+
+// Random1toN (random_util.h:32-215, random_util.cpp: swap list below 128
+// elements or without replacement, else a seen list converted to a swap list
+// past max(16, 0.1 n) draws) with the same draws and the same answers, but its
+// swap list kept sparse: the list is the identity except where a draw swapped,
+// so only those (position, value) pairs are stored.  The reference fills the
+// whole list (up to 127 entries, and an EList growth) at a range's first draw
+// -- 6 % of the drivers' CPU in r06c's profile, for ~1-2 draws per range.
+struct R1N {
+	size_t n = 0, cur = 0, thresh = 0;
+	bool swaplist = false, converted = false;
+	std::vector<std::pair<size_t, size_t>> sw;    // swap-list entries that are not the identity
+	std::vector<size_t> seen, list;               // seen list; the materialised list after a conversion
+	void init(size_t n_, bool withoutReplacement) {
+		n = n_;
+		converted = false;
+		swaplist = n_ < 128 || withoutReplacement;
+		cur = 0;
+		sw.clear();
+		seen.clear();
+		list.clear();
+		thresh = std::max<size_t>(16, (size_t)(0.10f * n_));
+	}
+	void reset() {
+		n = cur = thresh = 0;
+		swaplist = converted = false;
+		sw.clear();
+		seen.clear();
+		list.clear();
+	}
+	bool inited() const { return n > 0; }
+	void setDone() { cur = n; }
+	bool done() const { return inited() && cur >= n; }
+	size_t get(size_t i) const {
+		if(converted) return list[i];
+		for(const auto& p : sw)
+			if(p.first == i) return p.second;
+		return i;
+	}
+	void set(size_t i, size_t v) {
+		if(converted) {
+			list[i] = v;
+			return;
+		}
+		for(auto& p : sw)
+			if(p.first == i) {
+				p.second = v;
+				return;
+			}
+		sw.emplace_back(i, v);
+	}
+	size_t next(RandomSource& rnd) {
+		if(cur == 0 && !converted && n == 1) {
+			cur = 1;
+			return 0;
+		}
+		if(swaplist) {
+			const size_t r = cur + (rnd.nextU32() % (n - cur));
+			const size_t vr = get(r);
+			if(r != cur) set(r, get(cur));       // (position cur is never read again)
+			cur++;
+			return vr;
+		}
+		size_t rn = 0;
+		for(bool again = true; again;) {
+			rn = rnd.nextU32() % n;
+			again = std::find(seen.begin(), seen.end(), rn) != seen.end();
+		}
+		seen.push_back(rn);
+		cur++;
+		if(seen.size() >= thresh && cur < n) {
+			std::sort(seen.begin(), seen.end());
+			list.clear();
+			list.reserve(n - cur);
+			size_t prev = 0;
+			for(size_t x : seen) {
+				for(size_t j = prev; j < x; j++) list.push_back(j);
+				prev = x + 1;
+			}
+			for(size_t j = prev; j < n; j++) list.push_back(j);
+			seen.clear();
+			cur = 0;
+			n = list.size();
+			converted = true;
+			swaplist = true;
+		}
+		return rn;
+	}
+};
 
 // ---- SwDriver::extendSeeds / extendSeedsPaired as resumable state machines ----
 // (aligner_sw_driver.cpp:756-1297 and 1385-2402).  Members of the reference's
@@ -820,14 +916,16 @@ struct SwDriverB : public SwDriver {
 		const SATupleAndPos& p = satpos2_[pe_[k].src];
 		return p.sat.offs[(pe_[k].elt == WHOLE ? 0 : pe_[k].elt) + e];
 	}
-	Random1toN& ent_rand(size_t k, bool all_) {
+	std::vector<R1N> lr_, lr2_;   // the lazy path's Random1toNs: picks' small ranges; prio_flat's (rands2_)
+	size_t nlr_ = 0;              // lr_ entries in use
+	R1N& ent_rand(size_t k, bool all_) {
 		PrioEnt& e = pe_[k];
 		if(e.rnd < 0) {           // a small range's Random1toN, made when first needed (init draws nothing)
-			rands_.expand();
-			rands_.back().init(satpos2_[e.src].sat.size(), all_);
-			e.rnd = (int32_t)rands_.size() - 1;
+			if(nlr_ == lr_.size()) lr_.emplace_back();
+			lr_[nlr_].init(satpos2_[e.src].sat.size(), all_);
+			e.rnd = (int32_t)nlr_++;
 		}
-		return rands_[e.rnd];
+		return lr_[e.rnd];
 	}
 	bool ent_done(size_t k) {
 		if(!lazy_) return rands_[k].done();
@@ -1224,6 +1322,7 @@ struct Driver {
 	bool seeds_valid(const MateRes& m, bool fw, size_t i) const;
 	void set_valid(MateRes& m, bool fw, size_t i);
 	void resolve_rows_request(Slot& s);
+	void take_offsets(Slot& s);
 	void after_seeds(Slot& s, int mate);
 	int instantiate(Slot& s, int mate, size_t offset);
 	bool engine_read(const Slot& s, int m) const { return s.rdlens[m] > 0 && s.rdlens[m] <= BT2G_MAX_READ_LEN; }
@@ -1557,16 +1656,17 @@ void Svc::call_off(std::vector<Rq>& v) {
 	g_call_us[K_OFF] += now_us() - t0;
 	g_calls[K_OFF]++;
 	if(rc) die("bt2g_get_offset", rc);
+	// each read's offsets as one contiguous copy: its driver puts them where the
+	// reference's walks leave them when it resumes the read (take_offsets).
+	// (round 6: the scatter into the slots' cache pages had run here, ~1 ms per
+	// call of ~50 k rows, between the kernel and the answer every driver of the
+	// call was waiting for -- 87 % of this service's CPU in r06c's profile)
 	size_t k = 0;
 	for(const Rq& q : v) {
 		Slot* s = q.s;
-		// into the ranges' offset slots in the cache, where the reference's walks leave them
-		for(size_t j = 0; j < s->off_rows.size(); j++) {
-			const std::pair<size_t, size_t>& w = s->off_where[j];
-			s->tab.gw[w.first].offs[w.second] = offs[k + j];
-		}
-		k += s->off_rows.size();
-		s->tab.gw.clear();
+		const size_t m = s->off_rows.size();
+		s->off_vals.assign(offs.begin() + (std::ptrdiff_t)k, offs.begin() + (std::ptrdiff_t)(k + m));
+		k += m;
 	}
 	g_req[K_OFF] += v.size();
 }
@@ -1972,34 +2072,20 @@ bool SwDriverB::replay_next(Driver& d, Slot& s, Replay& rp, bool opp, TAlScore m
 // The rows handed to GroupWalk2S::init by the call that just returned, as one
 // engine request (bt2g_get_offset == Ebwt::getOffset, bt2_idx.cpp:150-171).
 void Driver::resolve_rows_request(Slot& s) {
-	const size_t MAX_ROWS = 8192;          // per read (the rest: Ebwt::getOffset in advanceElement)
+	const size_t MAX_ROWS = 16384;         // per read (the rest: Ebwt::getOffset in advanceElement)
 	s.off_rows.clear();
 	s.off_where.clear();
-	const auto& p0 = s.mr[0].pf_rows;
-	const auto& p1 = s.mr[1].pf_rows;
-	const auto& q0 = s.mr[0].sd_rows;
-	const auto& q1 = s.mr[1].sd_rows;
-	auto known = [](const std::vector<std::pair<uint32_t, uint32_t>>& p, uint32_t row, uint32_t& off) {
-		auto it = std::lower_bound(p.begin(), p.end(), std::make_pair(row, 0u));
-		if(it == p.end() || it->first != row) return false;
-		off = it->second;
-		return true;
-	};
+	// (round 6: every row goes to the engine, also a row the sweep or the seed call
+	// resolved already -- the offsets are the same either way, and looking each row
+	// up in those calls' lists was ~6 % of the drivers' CPU, for a few rows of ~100)
 	for(size_t r = 0; r < s.tab.gw.size(); r++) {
 		GwRange& x = s.tab.gw[r];
 		if(x.fresh) {
-			// (prio_flat's picks: nothing was written for them -- every row is
-			// asked, or taken from a call that resolved it; past MAX_ROWS marked
-			// unresolved, for advanceElement's CPU path)
+			// (prio_flat's picks: nothing was written for them -- every row is asked;
+			// past MAX_ROWS marked unresolved, for advanceElement's CPU path)
 			for(size_t j = 0; j < x.size; j++) {
-				const uint32_t row = (uint32_t)(x.topf + j);
-				uint32_t off;
-				if((!p0.empty() && known(p0, row, off)) || (!p1.empty() && known(p1, row, off)) ||
-				   (!q0.empty() && known(q0, row, off)) || (!q1.empty() && known(q1, row, off))) {
-					x.offs[j] = off;
-					g_rows_pf++;
-				} else if(s.off_rows.size() < MAX_ROWS) {
-					s.off_rows.push_back(row);
+				if(s.off_rows.size() < MAX_ROWS) {
+					s.off_rows.push_back((uint32_t)(x.topf + j));
 					s.off_where.emplace_back(r, j);
 				} else {
 					x.offs[j] = OFF_MASK;
@@ -2009,17 +2095,7 @@ void Driver::resolve_rows_request(Slot& s) {
 		}
 		for(size_t j = 0; j < x.size && s.off_rows.size() < MAX_ROWS; j++)
 			if(x.offs[j] == OFF_MASK) {
-				const uint32_t row = (uint32_t)(x.topf + j);
-				uint32_t off;
-				// a row the exact sweep / 1-mm call or the seed search already
-				// resolved (their small ranges)
-				if((!p0.empty() && known(p0, row, off)) || (!p1.empty() && known(p1, row, off)) ||
-				   (!q0.empty() && known(q0, row, off)) || (!q1.empty() && known(q1, row, off))) {
-					x.offs[j] = off;
-					g_rows_pf++;
-					continue;
-				}
-				s.off_rows.push_back(row);
+				s.off_rows.push_back((uint32_t)(x.topf + j));
 				s.off_where.emplace_back(r, j);
 			}
 	}
@@ -2135,6 +2211,7 @@ void SwDriverB::prio_flat(const Read& read, SeedResults& sh, const Ebwt& ebwtFw,
 	gws_.clear();
 	rands_.clear();
 	rands2_.clear();
+	nlr_ = 0;
 	satpos_.clear();
 	satpos2_.clear();
 	pe_.clear();
@@ -2190,11 +2267,11 @@ void SwDriverB::prio_flat(const Read& read, SeedResults& sh, const Ebwt& ebwtFw,
 	}
 	if(added < maxelt && nsmall != satpos2_.size()) {
 		rowsamp_.init(satpos2_, nsmall, satpos2_.size(), true, true);
-		rands2_.resize(satpos2_.size());
-		for(size_t j = 0; j < satpos2_.size(); j++) rands2_[j].reset();
+		if(lr2_.size() < satpos2_.size()) lr2_.resize(satpos2_.size());
+		for(size_t j = 0; j < satpos2_.size(); j++) lr2_[j].reset();
 		while(added < maxelt && added < nelt) {
 			const size_t ri = rowsamp_.next(rnd) + nsmall;
-			Random1toN& rr = rands2_[ri];
+			R1N& rr = lr2_[ri];
 			if(!rr.inited()) rr.init(satpos2_[ri].sat.size(), all_);
 			const size_t r = rr.next(rnd);
 			if(rr.done()) rowsamp_.finishedRange(ri - nsmall);
@@ -3379,7 +3456,19 @@ void after_ext(Driver& d, Slot& s, int mate, int ret, bool perfect_check) {
 	}
 }
 
+// The offsets a rows request brought back (Svc::call_off), into the ranges'
+// offset slots in the read's cache, where the reference's walks leave them.
+void Driver::take_offsets(Slot& s) {
+	for(size_t j = 0; j < s.off_vals.size(); j++) {
+		const std::pair<size_t, size_t>& w = s.off_where[j];
+		s.tab.gw[w.first].offs[w.second] = s.off_vals[j];
+	}
+	s.off_vals.clear();
+	s.tab.gw.clear();
+}
+
 void Driver::step_read(Slot& s) {
+	if(!s.off_vals.empty()) take_offsets(s);
 	const bool paired = s.paired;
 	const size_t nmates = paired ? 2 : 1;
 	const size_t eePeEeltLimit = std::numeric_limits<size_t>::max();
@@ -4145,6 +4234,11 @@ void Driver::run_loop() {
 		pthread_setname_np(pthread_self(), nm);
 		bt2g_prof_thread(1);
 	}
+	// $BT2G_DRV_NICE=n: the driver threads at nice n (the engine services and the
+	// connections' threads keep 0): a service thread that wakes for a call's
+	// result then preempts a stepping driver instead of queueing behind it on
+	// the job's CPU quota
+	if(const size_t nv = env_or("BT2G_DRV_NICE", 0)) (void)setpriority(PRIO_PROCESS, (id_t)syscall(SYS_gettid), (int)nv);
 	if(exit_clean()) {
 		static std::once_flag once;
 		std::call_once(once, [] { std::thread(term_watch).detach(); });
