@@ -382,8 +382,15 @@ void drain_prof(bt2g_ctx* c) {
 // profiler's tool init; the r04ag/r05aa/r05h SIGSEGVs inside the profiler's HSA
 // intercept came from such threads' first launches.  Without the aux stream
 // (creation failed) the directions run in turn.
-void make_aux(bt2g_ctx* c) {
-	if(!c->aux) {
+bool mm_merged() {
+	const char* e = getenv("BT2G_MM_MERGED");
+	return !(e && *e == '0');
+}
+
+void make_aux(bt2g_ctx* c, bool need) {
+	// (only for the two-stream 1-mm search, $BT2G_MM_MERGED=0: a stream made is a
+	// stream the runtime maps onto one of its few hardware queues, used or not)
+	if(!c->aux && need) {
 		bool ok = hipStreamCreateWithPriority(&c->aux, hipStreamNonBlocking, c->prio) == hipSuccess;
 		for(int i = 0; ok && i < 4; i++) ok = hipEventCreateWithFlags(&c->mm_ev[i], hipEventDisableTiming) == hipSuccess;
 		if(!ok) {
@@ -565,7 +572,7 @@ int bt2g_open_mem(const bt2g_index_mem* m, int device, bt2g_ctx** out) {
 		return rc;
 	}
 	c->nref = m->nref;
-	make_aux(c);
+	make_aux(c, !mm_merged());
 	*out = c;
 	return BT2G_OK;
 }
@@ -594,7 +601,7 @@ int bt2g_set_priority(bt2g_ctx* c, int high) {
 			if(e) { (void)hipEventDestroy(e); e = nullptr; }
 	}
 	c->prio = p;
-	make_aux(c);
+	make_aux(c, !mm_merged());
 	return BT2G_OK;
 }
 
@@ -647,7 +654,7 @@ int bt2g_open_shared(bt2g_ctx* base, bt2g_ctx** out) {
 	c->hbm_bytes = base->hbm_bytes;
 	c->base = base;
 	base->shares++;
-	make_aux(c);
+	make_aux(c, !mm_merged());
 	*out = c;
 	return BT2G_OK;
 }
@@ -811,6 +818,7 @@ static int one_mm_impl(bt2g_ctx* c, const uint8_t* reads, const uint8_t* quals, 
 	if(cap == 0) return fail(BT2G_ERR_ARG, "cap must be > 0");
 	if(n == 0) return BT2G_OK;
 	hipStream_t st = pick(c, stream);
+	if(!c->aux && !mm_merged()) make_aux(c, true);     // (the variable changed after the context opened)
 	OneMmScratch s;
 	HIPCHK(amalloc(c, (void**)&s.slots, sizeof(bt2g_mm1) * (size_t)n * 4 * cap, st));
 	HIPCHK(amalloc(c, (void**)&s.slot_counts, sizeof(int32_t) * (size_t)n * 4, st));

@@ -4162,7 +4162,11 @@ void Driver::run_loop() {
 			const int nd = std::max(1, (int)env_or("BT2G_DP_WORKERS", 6));
 			for(int k = 0; k < K_N; k++) {
 				Svc* owner = nullptr;
-				for(int w = 0; w < (k == K_DP ? nd : nw); w++) {
+				// (the standalone 1-mm and extend kinds are nearly never asked -- the sweep's
+				// and the seed call carry them -- so one worker each: every context is a
+				// stream the runtime maps onto one of its GPU_MAX_HW_QUEUES)
+				const int nk = k == K_DP ? nd : (k == K_1MM || k == K_EXT) ? 1 : nw;
+				for(int w = 0; w < nk; w++) {
 					Svc* v = new Svc();             // lives as long as the server
 					v->kind = k;
 					v->bsc = &s_bsc;
