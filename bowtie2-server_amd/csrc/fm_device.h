@@ -328,6 +328,75 @@ __device__ __forceinline__ int quad_rowL(const QuadSide& s, uint32_t q, uint32_t
 	return (int)quad_sum(v) - 1;
 }
 
+// this lane's share of the A, C, G counts among the side's first charOff rows
+// (side_counts' quad form; T follows from charOff)
+__device__ __forceinline__ void quad_part3(const QuadSide& s, uint32_t q, uint32_t charOff, uint32_t& a, uint32_t& c,
+                                           uint32_t& g) {
+	const int rem = q < 3u ? (int)charOff - 64 * (int)q : 0;
+	a = c = g = 0;
+#pragma unroll
+	for(int k = 0; k < 4; k++) {
+		int nk = rem - 16 * k;
+		nk = nk < 0 ? 0 : (nk > 16 ? 16 : nk);
+		const uint32_t m = nk >= 16 ? 0x55555555u : ((1u << (2 * nk)) - 1u) & 0x55555555u;
+		const uint32_t lo = s.w[k] & 0x55555555u, hi = (s.w[k] >> 1) & 0x55555555u;
+		a += __builtin_popcount(~(lo | hi) & m);
+		c += __builtin_popcount(lo & ~hi & m);
+		g += __builtin_popcount(hi & ~lo & m);
+	}
+}
+
+// countBt2SideEx of top (its side in s1) and bot (in s2), all four characters
+// (bi_step_tb's counting, quad form): the six shares (<= 64 each, sums <= 192)
+// packed into two quad sums, the occurrence counts from lane 3
+__device__ __forceinline__ void quad_occ4x2(const DevEbwt& e, const QuadSide& s1, const QuadSide& s2, uint32_t q,
+                                            uint32_t top, uint32_t bot, uint32_t t[4], uint32_t b[4]) {
+	const uint32_t st = top / 192u, ct = top % 192u, sb = bot / 192u, cb = bot % 192u;
+	uint32_t a1, c1, g1, a2, c2, g2;
+	quad_part3(s1, q, ct, a1, c1, g1);
+	quad_part3(s2, q, cb, a2, c2, g2);
+	const uint32_t p1 = quad_sum(a1 | (c1 << 8) | (g1 << 16) | (a2 << 24));
+	const uint32_t p2 = quad_sum(c2 | (g2 << 8));
+	uint32_t A1 = p1 & 0xffu, C1 = (p1 >> 8) & 0xffu, G1 = (p1 >> 16) & 0xffu, A2 = p1 >> 24;
+	uint32_t C2 = p2 & 0xffu, G2 = (p2 >> 8) & 0xffu;
+	const uint32_t T1 = ct - A1 - C1 - G1, T2 = cb - A2 - C2 - G2;
+	if(dollar_before(e, st, ct)) A1--;
+	if(dollar_before(e, sb, cb)) A2--;
+	t[0] = A1 + quad_lane3(s1.w[0]) + e.fchr[0];
+	t[1] = C1 + quad_lane3(s1.w[1]) + e.fchr[1];
+	t[2] = G1 + quad_lane3(s1.w[2]) + e.fchr[2];
+	t[3] = T1 + quad_lane3(s1.w[3]) + e.fchr[3];
+	b[0] = A2 + quad_lane3(s2.w[0]) + e.fchr[0];
+	b[1] = C2 + quad_lane3(s2.w[1]) + e.fchr[1];
+	b[2] = G2 + quad_lane3(s2.w[2]) + e.fchr[2];
+	b[3] = T2 + quad_lane3(s2.w[3]) + e.fchr[3];
+}
+
+// bi_step_tb / bi_step in quad form: both sides issued together (lane q's
+// 16 B of each), then counted; the mirror ranges as bi_step derives them
+__device__ __forceinline__ int quad_bi_step_tb(const DevEbwt& e, uint32_t q, uint32_t top, uint32_t bot, uint32_t t[4],
+                                               uint32_t b[4]) {
+	const uint32_t st = top / 192u, sb = bot / 192u;
+	QuadSide s1, s2;
+	load_quad(e, st, q, s1);
+	load_quad(e, sb, q, s2);
+	quad_occ4x2(e, s1, s2, q, top, bot, t, b);
+	return sb == st ? 1 : 2;
+}
+__device__ __forceinline__ int quad_bi_step(const DevEbwt& e, uint32_t q, uint32_t top, uint32_t bot, uint32_t topp,
+                                            uint32_t t[4], uint32_t b[4], uint32_t tp[4], uint32_t bp[4]) {
+	const int loads = quad_bi_step_tb(e, q, top, bot, t, b);
+	tp[0] = topp;
+	bp[0] = tp[0] + (b[0] - t[0]);
+	tp[1] = bp[0];
+	bp[1] = tp[1] + (b[1] - t[1]);
+	tp[2] = bp[1];
+	bp[2] = tp[2] + (b[2] - t[2]);
+	tp[3] = bp[2];
+	bp[3] = tp[3] + (b[3] - t[3]);
+	return loads;
+}
+
 // A read (or its reverse complement / reversal) as the reference's BTDnaString
 // views: patFw (rev=0,cmp=0), patRc (1,1), patFwRev (1,0), patRcRev (0,1).
 struct SeqView {

@@ -625,11 +625,109 @@ k_seed_extend(DevEbwt F, DevEbwt B, int has_bw, const uint8_t* __restrict__ read
 	ext[gid] = res;
 }
 
+// ext_walk / ext_one with a quad of lanes per range (fm_device.h)
+__device__ __forceinline__ uint32_t ext_walk_quad(const DevEbwt& e, uint32_t q, uint32_t top, uint32_t bot,
+                                                  const uint8_t* row, uint32_t rdlen, bool fw, uint32_t lim, uint32_t i0,
+                                                  int dir, uint32_t& fmops, uint32_t& loads) {
+	uint32_t n = 0;
+	for(uint32_t ii = 0; ii < lim; ii++) {
+		const uint32_t i = (uint32_t)((int64_t)i0 + (int64_t)dir * ii);
+		int rdc = fw ? row[i] : row[rdlen - 1 - i];
+		if(!fw) rdc = rdc > 3 ? 4 : 3 - rdc;
+		fmops++;
+		if(bot - top > 1) {
+			uint32_t t[4], b[4];
+			loads += (uint32_t)quad_bi_step_tb(e, q, top, bot, t, b);
+			int nonz = -1;
+			bool abort = false;
+			const uint32_t orig = bot - top;
+			for(int j = 0; j < 4; j++) {
+				if(b[j] > t[j]) {
+					if(nonz >= 0) { abort = true; break; }
+					nonz = j;
+					top = t[j];
+					bot = b[j];
+				}
+			}
+			if(abort || (nonz != rdc && rdc <= 3) || bot - top < orig) break;
+		} else {
+			int c = -1;
+			if(top != e.zoff) {
+				QuadSide s;
+				loads++;
+				load_quad(e, top / 192u, q, s);
+				c = quad_rowL(s, q, top % 192u);
+				top = quad_occ1(e, s, q, top, c);
+			}
+			if(c != rdc && rdc <= 3) break;
+			bot = top + 1;
+		}
+		if(++n == 255u) break;
+	}
+	return n;
+}
+
+__device__ __forceinline__ bt2g_ext_out ext_one_quad(const DevEbwt& F, const DevEbwt& B, int has_bw, uint32_t q,
+                                                     const uint8_t* row, uint32_t rdlen, const bt2g_ext_in& x) {
+	const bool fw = x.fw != 0;
+	uint32_t fmops = 0, nlex = 0, nrex = 0, loads = 0;
+	uint32_t lim = fw ? x.off : rdlen - x.len - x.off;
+	if(lim > 0)
+		nlex = ext_walk_quad(F, q, x.topf, x.botf, row, rdlen, fw, lim, fw ? x.off - 1 : rdlen - x.off - x.len - 1, -1,
+		                     fmops, loads);
+	lim = fw ? rdlen - x.len - x.off : x.off;
+	if(lim > 0 && has_bw)
+		nrex = ext_walk_quad(B, q, x.topb, x.botb, row, rdlen, fw, lim, fw ? x.len + x.off : rdlen - x.off, 1, fmops,
+		                     loads);
+	return bt2g_ext_out{nlex, nrex, fmops, loads};
+}
+
+// k_seed_extend with a quad per (read, strand, seed): lanes 4k..4k+3 for range k
+__global__ void __launch_bounds__(256)
+k_seed_extend_quad(DevEbwt F, DevEbwt B, int has_bw, const uint8_t* __restrict__ reads, uint32_t stride,
+                   const uint32_t* __restrict__ lens, uint32_t n, uint32_t seedlen, uint32_t interval, uint32_t offset,
+                   uint32_t maxseeds, const uint32_t* __restrict__ out, bt2g_ext_out* __restrict__ ext) {
+	walk_prio();
+	const uint64_t lane = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+	const uint64_t gid = lane >> 2;
+	const uint32_t q = (uint32_t)(lane & 3u);
+	if(gid >= (uint64_t)n * 2 * maxseeds) return;
+	const uint32_t r = (uint32_t)(gid / (2u * maxseeds)), rem = (uint32_t)(gid % (2u * maxseeds));
+	const uint32_t strand = rem / maxseeds, s = rem % maxseeds;
+	const uint32_t* o = out + gid * 4;
+	const uint32_t len = lens[r], L = seedlen < len ? seedlen : len, depth = s * interval + offset;
+	bt2g_ext_out res{0u, 0u, 0u, 0u};
+	if(o[1] > o[0] && depth + L <= len) {
+		bt2g_ext_in x;
+		x.read = r;
+		x.fw = strand == 0 ? 1 : 0;
+		x.off = depth;
+		x.len = L;
+		x.topf = o[0];
+		x.botf = o[1];
+		x.topb = o[2];
+		x.botb = o[3];
+		res = ext_one_quad(F, B, has_bw, q, reads + (size_t)r * stride, len, x);
+	}
+	if(q == 0) ext[gid] = res;
+}
+
+// $BT2G_FM_QUAD=0: the one-lane FM kernels (read at every launch)
+static bool fm_quad() {
+	const char* e = getenv("BT2G_FM_QUAD");
+	return !(e && *e == '0');
+}
+
 void launch_seed_extend(const DevEbwt& F, const DevEbwt& B, int has_bw, const uint8_t* reads, uint32_t stride,
                         const uint32_t* lens, uint32_t n, uint32_t seedlen, uint32_t interval, uint32_t offset,
                         uint32_t maxseeds, const uint32_t* out, bt2g_ext_out* ext, hipStream_t st) {
 	const uint64_t tot = (uint64_t)n * 2 * maxseeds;
 	if(!tot) return;
+	if(fm_quad()) {
+		hipLaunchKernelGGL(k_seed_extend_quad, dim3((uint32_t)((4 * tot + 255) / 256)), dim3(256), 0, st, F, B, has_bw,
+		                   reads, stride, lens, n, seedlen, interval, offset, maxseeds, out, ext);
+		return;
+	}
 	hipLaunchKernelGGL(k_seed_extend, dim3((uint32_t)((tot + 255) / 256)), dim3(256), 0, st, F, B, has_bw, reads, stride,
 	                   lens, n, seedlen, interval, offset, maxseeds, out, ext);
 }

@@ -784,6 +784,140 @@ k_one_mm_branch(DevEbwt F, DevEbwt B, const uint8_t* __restrict__ reads, uint32_
 }
 
 
+
+// The near half and the branch walks with a quad of lanes per item / branch
+// (fm_device.h, the cooperative step; $BT2G_FM_QUAD=0: one lane each).
+template <bool EBWTFW>
+__device__ __forceinline__ void one_mm_near_quad_body(const uint32_t blk_, DevEbwt F, DevEbwt B, const uint8_t* __restrict__ reads, uint32_t stride,
+              const uint32_t* __restrict__ lens, const uint32_t* __restrict__ items,
+              const uint32_t* __restrict__ nitems_p, uint4* __restrict__ st4, uint32_t* __restrict__ sdep,
+              uint32_t* __restrict__ ops_out, uint32_t* __restrict__ loads_out) {
+	walk_prio();
+	const uint32_t lane_ = blk_ * blockDim.x + threadIdx.x;
+	const uint32_t qi = lane_ >> 2, q = lane_ & 3u;   // a quad of lanes per item
+	if(qi >= *nitems_p) return;
+	const DevEbwt& E = EBWTFW ? F : B;
+	const DevEbwt& Ep = EBWTFW ? B : F;
+	const uint32_t item = items[qi];
+	const uint32_t r = item >> 3;
+	const bool fw = ((item >> 2) & 1u) == 0;
+	const uint32_t len = lens[r];
+	// seq = fw ? (ebwtfw ? patFw : patFwRev) : (ebwtfw ? patRc : patRcRev)
+	const SeqView seq{reads + (size_t)r * stride, len, fw ? !EBWTFW : EBWTFW, !fw};
+	const uint32_t nea = EBWTFW ? (len >> 1) : (len >> 1) + (len & 1);
+	const uint32_t flen = E.ftab_chars;
+	uint32_t top = 0, bot = 0, topp = 0, botp = 0, dep = 0, ops = 0, loads = 0;
+	bool alive = len != 0;
+	if(item & 1u)                               // the read has an N: none may be in the near half
+		for(uint32_t d = 0; alive && d < nea; d++)
+			if(seq[len - d - 1] > 3) alive = false;
+	if(alive) {
+		if(flen > 1 && flen <= nea) {
+			// ftabSeqToInt(seq, len-flen, rev=!ebwtfw) (bt2_idx.h:1383-1390)
+			uint32_t fi = 0, fip = 0;
+			for(uint32_t i = 0; i < flen; i++) {
+				fi = (fi << 2) | (uint32_t)seq[len - flen + i];
+				fip = (fip << 2) | (uint32_t)seq[len - 1 - i];
+			}
+			top = ftab_hi(E, fi); bot = ftab_lo(E, fi + 1);
+			topp = ftab_hi(Ep, fip); botp = ftab_lo(Ep, fip + 1);
+			dep = flen;
+		} else {
+			const int c = seq[len - 1];
+			top = topp = fchr_at(E, c);
+			bot = botp = fchr_at(E, c + 1);
+			dep = 1;
+		}
+		alive = bot != top;
+	}
+	SeqWin sw{seq, ReadWin{seq.p, seq.p + stride}};
+	while(alive && dep < nea) {
+		const int c = sw[len - dep - 1];
+		ops++;
+		if(bot - top > 1) {
+			uint32_t t[4] = {0, 0, 0, 0}, b[4] = {0, 0, 0, 0}, tp[4], bp[4];
+			tp[0] = topp;
+			loads += quad_bi_step(E, q, top, bot, topp, t, b, tp, bp);
+			const uint32_t nt = at4(t, c), nb = at4(b, c);
+			if(nb <= nt) { alive = false; break; }
+			top = nt; bot = nb; topp = at4(tp, c); botp = at4(bp, c);
+		} else {
+			QuadSide s1;
+			load_quad(E, top / 192u, q, s1);
+			loads++;
+			if(quad_rowL(s1, q, top % 192u) != c || top == E.zoff) { alive = false; break; }
+			top = quad_occ1(E, s1, q, top, c);
+			bot = top + 1;
+		}
+		dep++;
+	}
+	if(q != 0) return;
+	st4[qi] = alive ? make_uint4(top, bot, topp, botp) : make_uint4(0, 0, 0, 0);
+	sdep[qi] = dep | (alive ? 0x80000000u : 0u);
+	if(ops) atomicAdd(&ops_out[r], ops);
+	if(ops && loads_out) atomicAdd(&loads_out[r], loads);
+}
+
+template <bool EBWTFW>
+__device__ __forceinline__ void one_mm_branch_quad_body(const uint32_t blk_, DevEbwt F, DevEbwt B, const uint8_t* __restrict__ reads, uint32_t stride,
+                const uint32_t* __restrict__ lens, const MmBranch* __restrict__ brq,
+                const uint32_t* __restrict__ brq_n, uint32_t brq_cap, uint32_t cap, bt2g_mm1* __restrict__ slots,
+                int32_t* __restrict__ slot_counts, uint32_t* __restrict__ ops_out, uint32_t* __restrict__ loads_out,
+                const uint32_t* __restrict__ slot_flag) {
+	walk_prio();
+	const uint32_t lane_ = blk_ * blockDim.x + threadIdx.x;
+	const uint32_t i = lane_ >> 2, q = lane_ & 3u;   // a quad of lanes per branch
+	const uint32_t nq = *brq_n < brq_cap ? *brq_n : brq_cap;
+	if(i >= nq) return;
+	const MmBranch b = brq[i];
+	// one launch per index direction: the index a lane walks is then uniform (a
+	// per-lane choice between the two DevEbwt arguments put both on the stack)
+	const bool ebwtfw = (b.meta >> 25) & 1u;
+	if(ebwtfw != EBWTFW) return;
+	if(slot_flag[b.slot]) return;                 // its item was redone whole by the state machine
+	const DevEbwt& E = EBWTFW ? F : B;
+	const uint32_t r = b.slot >> 2;
+	const bool fw = ((b.slot >> 1) & 1u) == 0;
+	const uint32_t len = lens[r];
+	const SeqView sv{reads + (size_t)r * stride, len, fw ? !ebwtfw : ebwtfw, !fw};
+	SeqWin seq{sv, ReadWin{sv.p, sv.p + stride}};
+	uint32_t topm = b.rng.x, botm = b.rng.y, topmp = b.rng.z, botmp = b.rng.w;
+	uint32_t depm = b.meta & 0xffffu;
+	uint32_t ops = 0, loads = 0;
+	bool done = false;
+	while(depm < len) {
+		const int c = seq[len - depm - 1];
+		ops++;
+		bool dead;
+		if(botm - topm > 1) {
+			uint32_t ot[4] = {0, 0, 0, 0}, ob[4] = {0, 0, 0, 0}, otp[4], obp[4];
+			otp[0] = topmp;
+			loads += quad_bi_step(E, q, topm, botm, topmp, ot, ob, otp, obp);
+			topm = at4(ot, c); botm = at4(ob, c); topmp = at4(otp, c); botmp = at4(obp, c);
+			dead = botm <= topm;
+		} else {
+			QuadSide s1;
+			load_quad(E, topm / 192u, q, s1);
+			loads++;
+			const int rowl = quad_rowL(s1, q, topm % 192u);
+			dead = rowl != c || topm == E.zoff;
+			if(!dead) { topm = quad_occ1(E, s1, q, topm, rowl); botm = topm + 1; }
+		}
+		if(dead) break;
+		if(++depm == len) done = true;
+	}
+	if(q != 0) return;
+	if(done && ((b.meta >> 24) & 1u)) {
+		const int32_t p = atomicAdd(&slot_counts[b.slot], 1);
+		if((uint32_t)p < cap)
+			slots[(size_t)b.slot * cap + p] = bt2g_mm1{ebwtfw ? topm : topmp, ebwtfw ? botm : botmp, fw ? 1 : 0,
+			                                           b.score, b.off5p, (int32_t)((b.meta >> 16) & 0xfu),
+			                                           (int32_t)((b.meta >> 20) & 0xfu), (int32_t)b.seq};
+	}
+	if(ops) atomicAdd(&ops_out[r], ops);
+	if(ops && loads_out) atomicAdd(&loads_out[r], loads);
+}
+
 // Both index directions in one launch (round 6): blocks [0, g_) walk the BWT's
 // items, [g_, 2 g_) the mirror index's (their lists at +half_, their item
 // count at +2, their fallback lists at +half_ and count +1).  Two launches on a
@@ -834,6 +968,32 @@ k_one_mm_branch2(const uint32_t g_, const size_t half_, DevEbwt F, DevEbwt B, co
 	else one_mm_branch_body<false>(blockIdx.x - g_, F, B, reads, stride, lens, brq, brq_n, brq_cap, cap, slots, slot_counts, ops_out, loads_out, slot_flag);
 }
 
+__global__ void __launch_bounds__(256)
+k_one_mm_near2q(const uint32_t g_, const size_t half_, DevEbwt F, DevEbwt B, const uint8_t* __restrict__ reads,
+                uint32_t stride, const uint32_t* __restrict__ lens, const uint32_t* __restrict__ items,
+                const uint32_t* __restrict__ nitems_p, uint4* __restrict__ st4, uint32_t* __restrict__ sdep,
+                uint32_t* __restrict__ ops_out, uint32_t* __restrict__ loads_out) {
+	if(blockIdx.x < g_)
+		one_mm_near_quad_body<true>(blockIdx.x, F, B, reads, stride, lens, items, nitems_p, st4, sdep, ops_out, loads_out);
+	else
+		one_mm_near_quad_body<false>(blockIdx.x - g_, F, B, reads, stride, lens, items + half_, nitems_p + 2, st4 + half_,
+		                             sdep + half_, ops_out, loads_out);
+}
+__global__ void __launch_bounds__(256)
+k_one_mm_branch2q(const uint32_t g_, const size_t half_, DevEbwt F, DevEbwt B, const uint8_t* __restrict__ reads,
+                  uint32_t stride, const uint32_t* __restrict__ lens, const MmBranch* __restrict__ brq,
+                  const uint32_t* __restrict__ brq_n, uint32_t brq_cap, uint32_t cap, bt2g_mm1* __restrict__ slots,
+                  int32_t* __restrict__ slot_counts, uint32_t* __restrict__ ops_out, uint32_t* __restrict__ loads_out,
+                  const uint32_t* __restrict__ slot_flag) {
+	(void)half_;
+	if(blockIdx.x < g_)
+		one_mm_branch_quad_body<true>(blockIdx.x, F, B, reads, stride, lens, brq, brq_n, brq_cap, cap, slots, slot_counts,
+		                              ops_out, loads_out, slot_flag);
+	else
+		one_mm_branch_quad_body<false>(blockIdx.x - g_, F, B, reads, stride, lens, brq, brq_n, brq_cap, cap, slots,
+		                               slot_counts, ops_out, loads_out, slot_flag);
+}
+
 void launch_one_mm_q(const DevEbwt& F, const DevEbwt& B, const uint8_t* reads, const uint8_t* quals, uint32_t stride,
                      const uint32_t* lens, uint32_t n, const int32_t* minsc, const bt2g_scoring& sc, int nofw,
                      int norc, const uint32_t* gate, uint32_t cap, uint32_t* items, uint32_t* counters,
@@ -851,16 +1011,27 @@ void launch_one_mm_q(const DevEbwt& F, const DevEbwt& B, const uint8_t* reads, c
 		                   norc, items, counters, slot_counts, ops, loads, slot_flag);
 		const uint32_t g = (2 * n + 255) / 256, gb = (brq_cap + 255) / 256;
 		const size_t half = 2 * (size_t)n;
-		hipLaunchKernelGGL(k_one_mm_near2, dim3(2 * g), dim3(256), 0, st, g, half, F, B, reads, stride, lens, items,
-		                   counters, near_state, near_dep, ops, loads);
+		// ($BT2G_FM_QUAD=0: one lane per item and branch, else a quad: fm_device.h)
+		const char* qe = getenv("BT2G_FM_QUAD");
+		const bool quad = !(qe && *qe == '0');
+		if(quad)
+			hipLaunchKernelGGL(k_one_mm_near2q, dim3(8 * g), dim3(256), 0, st, 4 * g, half, F, B, reads, stride, lens,
+			                   items, counters, near_state, near_dep, ops, loads);
+		else
+			hipLaunchKernelGGL(k_one_mm_near2, dim3(2 * g), dim3(256), 0, st, g, half, F, B, reads, stride, lens, items,
+			                   counters, near_state, near_dep, ops, loads);
 		hipLaunchKernelGGL(k_one_mm_far2, dim3(2 * g), dim3(256), 0, st, g, half, F, B, reads, quals, stride, lens, minsc,
 		                   P, sc.ncl_const, sc.ncl_lin, items, counters, near_state, near_dep, cap, slots, slot_counts,
 		                   ops, loads, brq, counters + 4, brq_cap, fb_items, fb_st4, fb_sdep, counters + 5, slot_flag);
 		hipLaunchKernelGGL(k_one_mm_q2, dim3(2 * g), dim3(256), 0, st, g, half, F, B, reads, quals, stride, lens, minsc,
 		                   P, sc.ncl_const, sc.ncl_lin, fb_items, counters + 5, fb_st4, fb_sdep, cap, slots, slot_counts,
 		                   ops, loads, brq, counters + 7, 0u);
-		hipLaunchKernelGGL(k_one_mm_branch2, dim3(2 * gb), dim3(256), 0, st, gb, half, F, B, reads, stride, lens, brq,
-		                   counters + 4, brq_cap, cap, slots, slot_counts, ops, loads, slot_flag);
+		if(quad)
+			hipLaunchKernelGGL(k_one_mm_branch2q, dim3(8 * gb), dim3(256), 0, st, 4 * gb, half, F, B, reads, stride, lens,
+			                   brq, counters + 4, brq_cap, cap, slots, slot_counts, ops, loads, slot_flag);
+		else
+			hipLaunchKernelGGL(k_one_mm_branch2, dim3(2 * gb), dim3(256), 0, st, gb, half, F, B, reads, stride, lens, brq,
+			                   counters + 4, brq_cap, cap, slots, slot_counts, ops, loads, slot_flag);
 		return;
 	}
 	// the BWT' direction's kernels on s2 (st2, forked from st and joined back), or after the BWT ones on st

@@ -164,6 +164,28 @@ def test_one_mm_merged_equals_split(engines, monkeypatch):
         assert np.array_equal(h0[i, :c0[i]], h1[i, :c0[i]]), i
 
 
+@pytest.mark.parametrize("n", [3, 450, 3000])
+def test_fm_quad_equals_lane(engines, n, monkeypatch):
+    """Every kernel with a quad form (BT2G_FM_QUAD, default on: the 1-mm near half
+    and branch walks, the seed ranges' extension) against its one-lane form on the
+    same reads: 1-mm hits / counts / bwops, seed ranges, extensions, offsets."""
+    codes, quals, lens = _reads_with_errors(max(n, 2), 500 + n)
+    codes, quals, lens = codes[:n], quals[:n], lens[:n]
+    ms = np.array([int(-0.6 - 0.6 * L) for L in lens], np.int64)
+    e = engines["synth"]
+    res = {}
+    for v in ("0", "1"):
+        monkeypatch.setenv("BT2G_FM_QUAD", v)
+        res[v] = (e.one_mm(codes, quals, lens, ms, False), e.seed_search_ext(codes, lens, 20, 10, 0, 16, off_cap=8))
+    (h0, c0, o0, _), x0 = res["0"]
+    (h1, c1, o1, _), x1 = res["1"]
+    assert np.array_equal(c0, c1) and np.array_equal(o0, o1)
+    for i in np.nonzero(c0)[0]:
+        assert np.array_equal(h0[i, :c0[i]], h1[i, :c0[i]]), i
+    for a, b in zip(x0, x1):
+        assert np.array_equal(a, b)
+
+
 @pytest.mark.parametrize("brq_cap", [1, 7, 64])
 def test_one_mm_branch_queue_overflow(engines, brq_cap, monkeypatch):
     """A branch queue far too small for the batch ($BT2G_MM_BRQ_CAP): items whose
