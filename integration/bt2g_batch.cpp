@@ -2072,19 +2072,38 @@ bool SwDriverB::replay_next(Driver& d, Slot& s, Replay& rp, bool opp, TAlScore m
 // The rows handed to GroupWalk2S::init by the call that just returned, as one
 // engine request (bt2g_get_offset == Ebwt::getOffset, bt2_idx.cpp:150-171).
 void Driver::resolve_rows_request(Slot& s) {
-	const size_t MAX_ROWS = 16384;         // per read (the rest: Ebwt::getOffset in advanceElement)
+	const size_t MAX_ROWS = 8192;          // per read (the rest: Ebwt::getOffset in advanceElement)
 	s.off_rows.clear();
 	s.off_where.clear();
-	// (round 6: every row goes to the engine, also a row the sweep or the seed call
-	// resolved already -- the offsets are the same either way, and looking each row
-	// up in those calls' lists was ~6 % of the drivers' CPU, for a few rows of ~100)
+	const std::vector<std::pair<uint32_t, uint32_t>>* known[4] = {&s.mr[0].pf_rows, &s.mr[1].pf_rows, &s.mr[0].sd_rows,
+	                                                               &s.mr[1].sd_rows};
+	// the offsets of range x's rows that the sweep's or the seed call's small ranges
+	// already brought (sorted (row, offset) lists), matched by a merge over the
+	// range's rows: a read whose rows are all known makes no rows request -- no
+	// round.  (round 6: was a binary search in each list per row, ~6 % of the
+	// drivers' CPU; asking every row instead made 24 % more rounds, r06d)
+	thread_local std::vector<uint32_t> kv;
+	auto match = [&](TIndexOffU topf, size_t size) {
+		kv.assign(size, OFF_MASK);
+		for(const auto* L : known) {
+			if(L->empty() || L->back().first < topf || L->front().first >= topf + size) continue;
+			for(auto it = std::lower_bound(L->begin(), L->end(), std::make_pair((uint32_t)topf, 0u));
+			    it != L->end() && it->first < topf + size; ++it)
+				kv[it->first - topf] = it->second;
+		}
+	};
 	for(size_t r = 0; r < s.tab.gw.size(); r++) {
 		GwRange& x = s.tab.gw[r];
 		if(x.fresh) {
-			// (prio_flat's picks: nothing was written for them -- every row is asked;
-			// past MAX_ROWS marked unresolved, for advanceElement's CPU path)
+			// (prio_flat's picks: nothing was written for them -- every row is
+			// asked, or taken from a call that resolved it; past MAX_ROWS marked
+			// unresolved, for advanceElement's CPU path)
+			match(x.topf, x.size);
 			for(size_t j = 0; j < x.size; j++) {
-				if(s.off_rows.size() < MAX_ROWS) {
+				if(kv[j] != OFF_MASK) {
+					x.offs[j] = kv[j];
+					g_rows_pf++;
+				} else if(s.off_rows.size() < MAX_ROWS) {
 					s.off_rows.push_back((uint32_t)(x.topf + j));
 					s.off_where.emplace_back(r, j);
 				} else {
@@ -2093,8 +2112,18 @@ void Driver::resolve_rows_request(Slot& s) {
 			}
 			continue;
 		}
+		bool matched = false;
 		for(size_t j = 0; j < x.size && s.off_rows.size() < MAX_ROWS; j++)
 			if(x.offs[j] == OFF_MASK) {
+				if(!matched) {
+					match(x.topf, x.size);
+					matched = true;
+				}
+				if(kv[j] != OFF_MASK) {
+					x.offs[j] = kv[j];
+					g_rows_pf++;
+					continue;
+				}
 				s.off_rows.push_back((uint32_t)(x.topf + j));
 				s.off_where.emplace_back(r, j);
 			}
