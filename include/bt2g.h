@@ -110,7 +110,11 @@ int bt2g_set_priority(bt2g_ctx* ctx, int high);
 /* Confine the context's stream to `num` of every `den` compute units (CU i is
  * used iff i % den < num; num >= den or den == 0: every CU, the default), so
  * that long launches on it leave CUs to other contexts' short ones (the batch
- * server's DP service beside its FM services).  Call between calls. */
+ * server's DP service beside its FM services).  Call between calls.  The
+ * masked stream (hipExtStreamCreateWithCUMask) is a blocking stream (it
+ * synchronises with the null stream) and gets an HSA queue of its own outside
+ * the GPU_MAX_HW_QUEUES pool; it has no priority: combining this call with
+ * bt2g_set_priority on one context fails with BT2G_ERR_ARG either way round. */
 int bt2g_set_cu_share(bt2g_ctx* ctx, uint32_t num, uint32_t den);
 /* Release a context (a shared one first, then the index owner). */
 int bt2g_close(bt2g_ctx* ctx);

@@ -1197,6 +1197,7 @@ struct Lane {
 struct Svc {
 	int kind = 0;
 	bt2g_ctx* ctx = nullptr;
+	bool cu_masked = false;     // the DP worker's stream is on a CU share by default (--local)
 	const bt2g_scoring* bsc = nullptr;
 	uint64_t stamp = 0;
 	// the kind's queue (its first worker's): drivers with requests of this kind;
@@ -1234,6 +1235,7 @@ struct Svc {
 };
 
 std::atomic<uint64_t> g_stamp{0};
+std::atomic<bool> g_paired_seen{false};   // a read pair was admitted (Driver::admit)
 
 // $BT2G_MM_PREFETCH=0: no 1-mm search with the exact sweep
 bool mm_prefetch_on() {
@@ -3900,6 +3902,15 @@ void Svc::loop() {
 		}
 		v.clear();
 		dp.clear();
+		if(cu_masked && g_paired_seen.load(std::memory_order_relaxed)) {
+			// (the DP service's CU share is a --local gain for unpaired
+			// reads; with pairs -- mate searches -- it lost, r05ag: 107.9 -> 65.0 k
+			// pairs/s.  At the first pair the server has seen, the worker's stream
+			// goes back to every CU, unless $BT2G_DP_CU asked for the share)
+			int rc = bt2g_set_cu_share(ctx, 0, 0);
+			if(rc) die("bt2g_set_cu_share", rc);
+			cu_masked = false;
+		}
 		const uint64_t t0 = now_us();
 		for(Lane* l : got) {
 			if(kind == K_DP) dp.insert(dp.end(), l->rq_dp.begin(), l->rq_dp.end());
@@ -4086,6 +4097,7 @@ void Driver::admit(Elem* e) {
 			freel.pop_back();
 		}
 		s->paired = !ps->read_b().empty();
+		if(s->paired && !g_paired_seen.load(std::memory_order_relaxed)) g_paired_seen.store(true);
 		s->rdid = ra.rdid;
 		if(read_swap_on()) {
 			// the buffer's reads move into the slot and the slot's previous ones into
@@ -4231,6 +4243,7 @@ void Driver::run_loop() {
 						if(share.second) {
 							int rc3 = bt2g_set_cu_share(v->ctx, share.first, share.second);
 							if(rc3) die("bt2g_set_cu_share", rc3);
+							v->cu_masked = share.first < share.second && !getenv("BT2G_DP_CU");
 						}
 					}
 					if(!owner) owner = v;
