@@ -901,8 +901,9 @@ def stock_baseline(args, base, chunks, batch_outs, workdir):
     sample = chunks[:m]
     paired = args.mode == "paired"
     runs = []
+    cpus = rs.serve.pinned_cpus()     # (the CPUs the batch server pinned itself to, if it did)
     with rs.Server(base, threads=threads, args=policy_args(args.mode, args.preset), binary=rs.SERVER,
-                   log_path=os.path.join(workdir, "server_stock.log")) as srv:
+                   log_path=os.path.join(workdir, "server_stock.log"), cpus=cpus) as srv:
         for _ in range(args.warmup):
             srv.run(sample[:min(args.warmup_chunks, m)] if args.warmup_chunks > 0 else sample, k=args.clients)
         for _ in range(max(1, getattr(args, "stock_runs", 3))):
@@ -925,7 +926,9 @@ def stock_baseline(args, base, chunks, batch_outs, workdir):
                       f"(bowtie2-align-l), <= 10 000 per client connection, {args.clients} connections at a time, "
                       f"after {args.warmup} warmup pass(es) over "
                       f"{min(args.warmup_chunks, m) if args.warmup_chunks > 0 else m} chunk(s); median of "
-                      f"{len(runs)} timed runs"}, \
+                      f"{len(runs)} timed runs" + (f"; server pinned to the {len(cpus)} CPUs the batch server uses"
+                                                   if cpus else ""),
+            "cpus": cpus}, \
         {"sample_reads": nreads, "records": len(a), "records_differing": differ, "identical": differ == 0,
          "batch_client": "integration/bin/bt2g-client", "stock_client": "oracle/_ref/bowtie2-align-l"}
 

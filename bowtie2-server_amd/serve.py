@@ -114,20 +114,46 @@ def write_fastq_chunks(dirpath, codes, quals, names=None, chunk=CHUNK, codes2=No
     return out
 
 
+def pinned_cpus():
+    """The CPUs the batch server pins itself to ($BT2G_PIN_CPUS, default "auto":
+    the first ceil(cgroup quota) CPUs of the affinity mask when the mask is
+    larger; integration/bt2g_batch.cpp pin_cpus), or None (no pinning) -- so that
+    the stock server can run on the same CPUs."""
+    e = os.environ.get("BT2G_PIN_CPUS", "auto")
+    if not e or e == "0":
+        return None
+    n = 0
+    if e == "auto":
+        try:
+            q, period = open("/sys/fs/cgroup/cpu.max").read().split()[:2]
+            if q != "max" and int(period) > 0:
+                n = -(-int(q) // int(period))
+        except (OSError, ValueError):
+            n = 0
+    else:
+        n = int(e)
+    mask = sorted(os.sched_getaffinity(0))
+    if n <= 0 or len(mask) <= n:
+        return None
+    return mask[:n]
+
+
 class Server:
     """One alignment server process on a free port (context manager)."""
 
     def __init__(self, index_base, threads=1, args=(), binary=BATCH_SERVER, env=None, ready_timeout=600,
-                 log_path=None, prefix=()):
+                 log_path=None, prefix=(), cpus=None):
         """`prefix`: a launcher put before the server's command line that runs the
-        server in its own process (rocprofv3 ... --)."""
+        server in its own process (rocprofv3 ... --).  `cpus`: the server process's
+        CPU affinity (the stock server on the CPUs the batch server pins itself to)."""
         self.index_base = index_base
         self.port = free_port()
         cmd = list(prefix) + [binary, "-x", index_base, "-p", str(threads), "--server-port", str(self.port)] + list(args)
         self.log_path = log_path or tempfile.mktemp(prefix="bt2srv_", suffix=".log")
         self._log = open(self.log_path, "wb")
         self.proc = subprocess.Popen(cmd, stdout=self._log, stderr=subprocess.STDOUT,
-                                     env=dict(os.environ, **(env or {})))
+                                     env=dict(os.environ, **(env or {})),
+                                     preexec_fn=(lambda: os.sched_setaffinity(0, cpus)) if cpus else None)
         t0 = time.time()
         while True:
             txt = open(self.log_path, "rb").read()
