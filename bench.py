@@ -1244,7 +1244,8 @@ def main():
     ap.add_argument("--steps", type=int, default=1, help="timed passes of the batch server over every read")
     ap.add_argument("--warmup", type=int, default=1, help="untimed passes over the first --warmup-chunks chunks")
     ap.add_argument("--reads", type=int, default=1_000_000, help="reads (paired: read pairs) per GPU per step")
-    ap.add_argument("--drivers", type=int, default=16, help="batch server driver threads (-p)")
+    ap.add_argument("--drivers", type=int, default=int(os.environ.get("BT2G_BENCH_DRIVERS") or 16),
+                    help="batch server driver threads (-p; $BT2G_BENCH_DRIVERS for A/B runs)")
     ap.add_argument("--clients", type=int, default=32, help="concurrent client connections (both servers)")
     ap.add_argument("--client", choices=("native", "reference"), default="native",
                     help="client of the timed passes: native = integration/bin/bt2g-client (row (f)-4, SAM "
