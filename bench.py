@@ -653,6 +653,43 @@ def dominant_kernel(kern):
     return max(ks, key=lambda k: kern[k]["ms_total"], default=None)
 
 
+def line_rooflines(kern, server_pmc):
+    """(roofline, rooflines) of a line: the largest consumer's roofline object and
+    every kernel (family) with a bound, largest total time first.  When the
+    largest consumer has no bound (--local: the one-walker backtrace, a chain of
+    dependent LDS accesses whose per-step work the host does not see), the
+    roofline is the largest kernel WITH one and names that consumer in
+    `largest_consumer`."""
+    dom_k = dominant_kernel(kern)
+    rl, rls, largest = None, [], None
+    if dom_k and "achieved" not in kern[dom_k]:
+        largest = {"id": dom_k, "kernel": kern[dom_k]["kernel"], "ms_per_launch": kern[dom_k]["ms_per_launch"],
+                   "share_of_kernel_time": kern[dom_k]["ms_total"] / max(1e-9, sum(
+                       v["ms_total"] for v in kern.values() if not v.get("span"))),
+                   "why_no_roofline": "a chain of dependent LDS accesses per DP (one walker per workgroup; local: "
+                                      "~55 walks and ~1 200 candidates per DP): latency-bound, no algorithmic "
+                                      "byte or op count the host sees"}
+        bounded = [k for k in kern if "achieved" in kern[k] and not kern[k].get("span")]
+        dom_k = max(bounded, key=lambda k: kern[k]["ms_total"], default=None)
+    if dom_k:
+        rl = roofline_entry(kern, dom_k, server_pmc)
+        if largest:
+            rl["largest_consumer"] = largest
+        rl["note"] = ("kernel times: HIP events around every launch of the batch server's engine services "
+                      "over warmup + timed passes (BT2G_KPROF); a family's time is its call's launches from "
+                      "the first kernel's start to the last one's end; per-launch work: the algorithmic figure "
+                      "of SURVEY.md 8(d) for the requests of each call.  Latency-bound here: the batch "
+                      "server's calls carry a round's requests (hundreds to a few thousand items); the "
+                      "throughput regime of the same kernels is kernel_chain.roofline")
+    for k in sorted(kern, key=lambda k: -kern[k]["ms_total"]):
+        if "achieved" in kern[k]:
+            e = roofline_entry(kern, k, server_pmc)
+            rls.append({"id": k, **{x: e[x] for x in ("kernel", "bound", "frac", "achieved", "unit",
+                                                      "ms_per_launch", "share_of_kernel_time", "traffic",
+                                                      "traffic_ratio", "per_launch_work")}})
+    return rl, rls
+
+
 def work_by_kernel(st):
     """{kind:id: [algorithmic work total, items]} of a run's server statistics
     (bytes for the FM kernels, DP cells for the fill): with a --pmc pass of the
@@ -1356,7 +1393,6 @@ def main():
     log(f"[rank {rank}] real schedule: {sched['aligned']} aligned of {args.reads * args.steps} in "
         f"{sched['elapsed']:.2f}s; whole job {value:.0f} aligned/s")
     kern = server_kernels(sched["stats"])
-    dom_k = dominant_kernel(kern)
     cpu, sam = None, None
     if rank == 0 and world == 1 and args.stock_sample and not args.no_cpu_baseline:
         try:
@@ -1373,22 +1409,7 @@ def main():
     if rank == 0:
         unit = "read pairs/s" if args.mode == "paired" else "reads/s"
         st = sched["stats"] or {}
-        rl, rls = None, []
-        if dom_k and "achieved" in kern[dom_k]:
-            rl = roofline_entry(kern, dom_k, args.server_pmc)
-            rl["note"] = ("kernel times: HIP events around every launch of the batch server's engine services "
-                          "over warmup + timed passes (BT2G_KPROF); a family's time is its call's launches from "
-                          "the first kernel's start to the last one's end; per-launch work: the algorithmic figure "
-                          "of SURVEY.md 8(d) for the requests of each call.  Latency-bound here: the batch "
-                          "server's calls carry a round's requests (hundreds to a few thousand items); the "
-                          "throughput regime of the same kernels is kernel_chain.roofline")
-        # every kernel (family) with a bound, largest total time first
-        for k in sorted(kern, key=lambda k: -kern[k]["ms_total"]):
-            if "achieved" in kern[k]:
-                e = roofline_entry(kern, k, args.server_pmc)
-                rls.append({"id": k, **{x: e[x] for x in ("kernel", "bound", "frac", "achieved", "unit",
-                                                          "ms_per_launch", "share_of_kernel_time", "traffic",
-                                                          "traffic_ratio", "per_launch_work")}})
+        rl, rls = line_rooflines(kern, args.server_pmc)
         calls = {k: st.get(k) for k in ("exact_sweep", "one_mm", "seed_search", "extend", "get_offset", "ungapped",
                                         "sw_dp")}
         # the reference's CPU code inside the product server (bt2g_batch.cpp's live

@@ -133,11 +133,22 @@ __device__ unsigned long long g_bt_wave_t0[1u << 16], g_bt_wave_t1[1u << 16];   
 // ~1 200 candidates per DP one after another): LDS latency is an order of
 // magnitude lower.  For big batches the lane-per-problem kernel keeps the
 // throughput.
-template <int KIND, bool LOCAL, bool FLAT = LOCAL, bool LDSRES = false>
+// WPF (LDS-resident local only): the wave-parallel candidate filter.  Between
+// two walks nothing a filter reads changes (the marks and the dominated squares
+// are written by walks alone), so the wave's 64 lanes test the next 64
+// candidates at once -- score, FILT_DOMINATED, FILT_START, in the reference's
+// order (aligner_sw.cpp nextAlignment; aligner_swsse_loc_i16.cpp:1420-1500) --
+// and a ballot finds the first that survives; one lane testing ~1 200
+// candidates per DP, one after another, is what it replaces.  The walks
+// themselves are then run by all 64 lanes on identical values (the same
+// loads, the same stores to the same addresses): no lane leaves the loop, so
+// the wave stays converged for the next filter's ballot.
+template <int KIND, bool LOCAL, bool FLAT = LOCAL, bool LDSRES = false, bool WPF = false>
 __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(BT2G_BT_WAVES)))
 k_sw_bt(BtArgs A) {
 	static_assert(!LDSRES || (KIND == 2 && !LOCAL) || (KIND == 1 && LOCAL),
 	              "LDS-resident walks: kind-2 end-to-end or kind-1 local planes");
+	static_assert(!WPF || (LDSRES && LOCAL && !FLAT), "the wave-parallel filter: LDS-resident local walks");
 	const uint32_t p = LDSRES ? blockIdx.x : blockIdx.x * 64u + threadIdx.x;
 	if(p >= A.nprob) return;
 #ifdef BT2G_BT_PROF
@@ -277,7 +288,7 @@ k_sw_bt(BtArgs A) {
 			lcl = (const bt2g_sw_cand*)lc;
 		}
 		__syncthreads();
-		if(threadIdx.x != 0) return;
+		if(!WPF && threadIdx.x != 0) return;
 		if(n16) {
 			slot = (const uint8_t*)s_res;
 			pl.base = slot;
@@ -506,7 +517,45 @@ k_sw_bt(BtArgs A) {
 	bt2g_sw_cand nxt_cd = ncand ? cl[0] : bt2g_sw_cand{0, 0, 0};
 	int32_t cscore = 0;
 	while(true) {
-		if(!walking) {
+		if(WPF && !walking) {
+			if(ci >= ncand || nal >= (int32_t)A.maxaln) break;
+			// the cached reportedThrough tile and valid word back to LDS, where the
+			// other lanes read them
+			if(tdirty) {
+				*(uint64_t*)(marks + ((size_t)ttr * tcols + ttc) * 2u) = tbits;
+				vword(ttr * vw + (ttc >> 5)) |= 1u << (ttc & 31u);
+				vdirty = true;
+				tdirty = false;
+			}
+			if(vdirty) { valid[vidx] = vval; vdirty = false; }
+			__syncthreads();
+			for(;;) {
+				const uint32_t j = ci + threadIdx.x;
+				int8_t fj = 0;
+				if(j < ncand) {
+					const bt2g_sw_cand c = cl[j];
+					const uint32_t r = (uint32_t)c.row, cc = (uint32_t)c.col;
+					const uint32_t tr = r >> 3, tc = cc >> 3;
+					const bool mk = ((valid[tr * vw + (tc >> 5)] >> (tc & 31u)) & 1u) &&
+					                (*(const uint64_t*)(marks + ((size_t)tr * tcols + tc) * 2u) & rbit(r, cc));
+					if(c.score < P.minsc) fj = 5;                      // BT_CAND_FATE_FILT_SCORE
+					else if(!A.fates && dom_test(r, cc)) fj = 4;        // BT_CAND_FATE_FILT_DOMINATED
+					else if(mk) fj = 3;                                 // BT_CAND_FATE_FILT_START
+					else if(A.fates && dom_test(r, cc)) fj = 4;
+				}
+				const uint64_t stop = __ballot(j >= ncand || fj == 0);
+				const uint32_t f = stop ? (uint32_t)__builtin_ctzll(stop) : 64u;
+				if(A.fates && threadIdx.x < f) A.fates[(size_t)p * A.cap + j] = fj;
+				ci += f;
+				if(stop) break;
+			}
+			if(ci >= ncand) break;
+			const bt2g_sw_cand cd = cl[ci];
+			ed = A.edits + ((size_t)p * A.maxaln + (size_t)nal) * A.maxedit;
+			row0 = (uint32_t)cd.row; col0 = (uint32_t)cd.col; cur = cd.score; cscore = cd.score;
+			replay = false;
+			start_walk(true, first);
+		} else if(!walking) {
 			if(ci >= ncand || nal >= (int32_t)A.maxaln) break;
 			const bt2g_sw_cand cd = nxt_cd;
 			nxt_cd = cl[ci + 1u < ncand ? ci + 1u : ci];
@@ -924,7 +973,9 @@ void sw_bt_lds_init(int dev) {
 	   hipFuncSetAttribute((const void*)k_sw_bt<1, true, true, true>, hipFuncAttributeMaxDynamicSharedMemorySize,
 	                       v - (int)BT_STATIC_LDS) == hipSuccess &&
 	   hipFuncSetAttribute((const void*)k_sw_bt<1, true, false, true>, hipFuncAttributeMaxDynamicSharedMemorySize,
-	                       v - (int)BT_STATIC_LDS) == hipSuccess)
+	                       v - (int)BT_STATIC_LDS) == hipSuccess &&
+	   hipFuncSetAttribute((const void*)k_sw_bt<1, true, false, true, true>,
+	                       hipFuncAttributeMaxDynamicSharedMemorySize, v - (int)BT_STATIC_LDS) == hipSuccess)
 		lim = (uint32_t)v - BT_STATIC_LDS;
 	else
 		(void)hipGetLastError();
@@ -984,9 +1035,13 @@ void launch_sw_bt(int kind, const BtArgs& a, hipStream_t st) {
 				// (one walker per workgroup: no lanes to diverge, so a walk runs to its
 				// end in the inner loop -- the flat loop's one body per step is the
 				// union of the filter and the walk; $BT2G_BT_LOC_FLAT=1 keeps it)
+				// $BT2G_BT_LOC_WPF=0: the candidates filtered by the walker alone, one at a
+				// time (round 5), not by the wave (read at every launch: A/B in one process)
 				const char* fl = getenv("BT2G_BT_LOC_FLAT");
+				const char* wp = getenv("BT2G_BT_LOC_WPF");
 				if(fl && *fl == '1') hipLaunchKernelGGL((k_sw_bt<1, true, true, true>), dim3(b.nprob), dim3(64), lds, st, b);
-				else hipLaunchKernelGGL((k_sw_bt<1, true, false, true>), dim3(b.nprob), dim3(64), lds, st, b);
+				else if(wp && *wp == '0') hipLaunchKernelGGL((k_sw_bt<1, true, false, true>), dim3(b.nprob), dim3(64), lds, st, b);
+				else hipLaunchKernelGGL((k_sw_bt<1, true, false, true, true>), dim3(b.nprob), dim3(64), lds, st, b);
 				return;
 			}
 		}

@@ -4,6 +4,7 @@
 #   bash scripts/gpu_r06.sh tests TAG          the GPU test suite and smoke()
 #   bash scripts/gpu_r06.sh vs TAG             configs[4]'s per-GPU shard (paired --very-sensitive, 1.25 M pairs)
 #   bash scripts/gpu_r06.sh prof TAG           rocprofv3 kernel trace of the bench command + FETCH/WRITE passes
+#   bash scripts/gpu_r06.sh kprof TAG [STEPS]  the same kernel trace with the engines' HIP-event timing on (BT2G_KPROF)
 #   bash scripts/gpu_r06.sh envab TAG [STEPS]  the bench under several server environments (ENVS="A=1;B=2"), REPS each
 #   bash scripts/gpu_r06.sh mode TAG [STEPS]   another mode's line ($MODE local | paired, $PRESET) with a stock sample
 set -o pipefail
@@ -58,6 +59,15 @@ prof)
   python3 scripts/pmc_summary.py $O/pmc_FETCH_SIZE $O/pmc_WRITE_SIZE $O/server_pmc.json $O/bench_pmc_FETCH_SIZE.json $O/bench_pmc_WRITE_SIZE.json
   find $O -name "*.csv" -size +40M -delete
   head -25 $O/run_kernel_stats.csv | cut -d, -f1-6 ;;
+kprof)
+  # rocprofv3 kernel trace of the bench command with the engines' own HIP-event timing on too
+  # (BT2G_KPROF: the r04ag / r05h SIGSEGV under the profiler; events now made at context open)
+  BT2G_BENCH_KPROF=1 BT2G_BENCH_SERVER_PREFIX="rocprofv3 --kernel-trace --stats --output-format csv -d $PWD/$O/kprof -o run --" \
+    timeout -k 10 600 python3 -u bench.py --steps ${3:-2} --warmup 1 --chain-steps 0 --stock-sample 0 \
+    > $O/bench_kprof.json 2> $O/bench_kprof.log || { tail -30 $O/bench_kprof.log; exit 1; }
+  find $O/kprof -name "*kernel_stats.csv" -exec cp {} $O/kprof_kernel_stats.csv \;
+  find $O/kprof -name "*.csv" -size +40M -delete
+  summ $O/bench_kprof.json kprof; head -12 $O/kprof_kernel_stats.csv | cut -d, -f1-6 ;;
 trace)
   # kernel + memory-copy trace of one pass (timeline of the calls: gaps between a stream's kernels and copies)
   BT2G_BENCH_SERVER_PREFIX="rocprofv3 --kernel-trace --memory-copy-trace --stats --output-format csv -d $PWD/$O/tprof -o run --" \

@@ -53,3 +53,5 @@ inline uint32_t atomicAdd(uint32_t* a, uint32_t v) { const uint32_t o = *a; *a +
 // bt_emul.cpp sets BT2G_BT_LDS_MAX=0; they only have to compile)
 inline void __syncthreads() {}
 #define HIP_DYNAMIC_SHARED(type, var) static type var[1];
+// (fm_device.h's quad FM step, never called here: a lane is its own quad)
+#define __builtin_amdgcn_mov_dpp(x, ctrl, rm, bm, bc) (x)

@@ -92,3 +92,5 @@ void emul_launch(K k, dim3 g, dim3 b, size_t sh, A... a) {
 	}
 }
 #define hipLaunchKernelGGL(k, g, b, sh, st, ...) emul_launch(k, g, b, sh, __VA_ARGS__)
+// (fm_device.h's quad FM step, never called here: a lane is its own quad)
+#define __builtin_amdgcn_mov_dpp(x, ctrl, rm, bm, bc) (x)

@@ -153,3 +153,25 @@ def test_count_aligned_flags():
            b"p1\t77\t*\t0\np1\t141\t*\t0\np2\t73\tc\t1\np2\t133\t*\t0\np3\t99\tc\t1\np3\t147\tc\t9\n"]
     assert bench.count_aligned(sam[:1], False) == 2
     assert bench.count_aligned(sam[1:], True) == 2
+
+
+def test_line_roofline_names_largest_consumer():
+    """The line's roofline is the largest consumer's; when that one has no bound
+    (--local: the one-walker backtrace) it is the largest bounded kernel's, and the
+    consumer is named in it."""
+    def ids(**rows):
+        v = [[0, 0.0, 0, 0] for _ in range(16)]
+        for k, r in rows.items():
+            v[int(k[1:])] = r
+        return {"ids": v}
+    st = {"kernels": {"exact_sweep": ids(i0=[100, 40.0, 10 ** 9, 4000], i2=[100, 90.0, 2 * 10 ** 9, 3000]),
+                      "sw_dp": ids(i4=[100, 70.0, 10 ** 10, 5000], i5=[100, 500.0, 0, 0], i7=[100, 900.0, 0, 0])}}
+    kern = bench.server_kernels(st)
+    rl, rls = bench.line_rooflines(kern, "/nonexistent.json")
+    assert rl["kernel"].startswith("k_one_mm") and rl["family"]
+    assert rl["largest_consumer"]["id"] == "sw_dp:5"
+    assert abs(rl["largest_consumer"]["share_of_kernel_time"] - 500 / 700) < 1e-9
+    assert [e["id"] for e in rls] == ["exact_sweep:2", "sw_dp:4", "exact_sweep:0"]
+    st["kernels"]["sw_dp"]["ids"][5] = [100, 5.0, 0, 0]
+    rl, _ = bench.line_rooflines(bench.server_kernels(st), "/nonexistent.json")
+    assert rl["kernel"].startswith("k_one_mm") and "largest_consumer" not in rl
