@@ -1188,7 +1188,7 @@ struct Rq {
 // stream per kind instead of one per driver and kind).  Off: a driver makes
 // its calls itself, one after another, on its own context.
 struct Driver;
-// A driver's reads can be split in lanes ($BT2G_LANES=2; default 1): while one lane's
+// A driver's reads are split in two lanes ($BT2G_LANES; default 2, --local 1): while one lane's
 // requests are with the services, the driver steps the other lane's reads, so
 // a round costs max(stepping, waiting) instead of their sum.
 struct Lane {
@@ -4299,9 +4299,14 @@ void Driver::run_loop() {
 	}
 	std::thread(&Driver::feeder, this).detach();
 	// (r04u: two lanes 144 k reads/s against 217 k with one -- half-size lanes
-	// double the services' calls, and their per-call cost, not the stepping, is
-	// what the other lane's wait hides)
-	const int nlanes = (int)std::min<long>(2, std::max<long>(1, env_or("BT2G_LANES", 1)));
+	// doubled the services' calls when each driver made its own.  Round 6, the
+	// services merging every driver's requests into one call per kind: two
+	// lanes 272.6 / 289.0 / 287.4 k against 259.5 / 261.2 / 251.1 k, one lease,
+	// r06j; r06h 280.3 / 272.9 k against 240.4 / 256.1 k -- the default.  --local,
+	// whose rounds wait on a ~13 ms DP call: 102.8 / 102.2 k against 104.9 /
+	// 105.7 k with one lane, r06l -- one lane there)
+	const int nlanes =
+	    (int)std::min<long>(2, std::max<long>(1, env_or("BT2G_LANES", R_localAlign ? 1 : 2)));
 	for(Lane& l : lanes) l.d = this;
 	for(int li = 0;;) {
 		Lane& L = lanes[li];
