@@ -277,7 +277,7 @@ k_sw_bt(BtArgs A) {
 		for(uint32_t i = threadIdx.x; i < n16; i += 64u) s_res[i] = src[i];
 		uint32_t* lm = (uint32_t*)(s_res + n16);
 		for(uint32_t i = threadIdx.x; i < trows * vw; i += 64u) lm[(size_t)trows * tcols * 2u + i] = 0u;
-		if(KIND == 1) {
+		if(KIND == 1 && A.cands_lds) {
 			// local: the sorted candidate list too (~1 200 per DP, most of them only
 			// tested against the marks: streamed from HBM one at a time by the walker,
 			// each a dependent round trip), after the whole mark slot
@@ -951,7 +951,9 @@ static uint32_t bt_lds_bytes(const BtArgs& a, int kind) {
 	const uint64_t plane = (uint64_t)sw_bt_lds_plane16(a, kind) * 16u;
 	const uint64_t marks = (kind == 1 ? a.mslot
 	                                  : (uint64_t)a.rrows * a.rwords * 2u + (uint64_t)a.rrows * ((a.rwords + 31u) / 32u)) * 4u;
-	const uint64_t cands = kind == 1 ? (uint64_t)a.cap * sizeof(bt2g_sw_cand) : 0u;   // (local: the candidate list)
+	// (local: the candidate list, but for the wave-parallel filter, which reads it
+	// from HBM 64 candidates at a time: ~24 KB less per workgroup at cap 2 048)
+	const uint64_t cands = kind == 1 && a.cands_lds ? (uint64_t)a.cap * sizeof(bt2g_sw_cand) : 0u;
 	const uint64_t n = plane + marks + cands;
 	return n > 0xffffffffull ? 0xffffffffu : (uint32_t)n;
 }
@@ -1030,17 +1032,22 @@ void launch_sw_bt(int kind, const BtArgs& a, hipStream_t st) {
 		if(!(e && *e == '0')) {
 			BtArgs b = a;
 			b.lds_marks_only = !(e && !strcmp(e, "plane"));
+			// (one walker per workgroup: no lanes to diverge, so a walk runs to its
+			// end in the inner loop -- the flat loop's one body per step is the
+			// union of the filter and the walk; $BT2G_BT_LOC_FLAT=1 keeps it)
+			// $BT2G_BT_LOC_WPF=0: the candidates filtered by the walker alone, one at a
+			// time (round 5), not by the wave (read at every launch: A/B in one process)
+			const char* fl = getenv("BT2G_BT_LOC_FLAT");
+			const char* wp = getenv("BT2G_BT_LOC_WPF");
+			const int form = (fl && *fl == '1') ? 0 : (wp && *wp == '0') ? 1 : 2;
+			// $BT2G_BT_LOC_CANDS=lds: the wave-parallel filter's candidates copied to LDS
+			// as the serial filter's are (one dependent load per candidate there)
+			const char* cl = getenv("BT2G_BT_LOC_CANDS");
+			b.cands_lds = form != 2 || (cl && !strcmp(cl, "lds"));
 			const uint32_t lds = bt_lds_bytes(b, 1);
 			if(lds <= bt_loc_lds_limit()) {
-				// (one walker per workgroup: no lanes to diverge, so a walk runs to its
-				// end in the inner loop -- the flat loop's one body per step is the
-				// union of the filter and the walk; $BT2G_BT_LOC_FLAT=1 keeps it)
-				// $BT2G_BT_LOC_WPF=0: the candidates filtered by the walker alone, one at a
-				// time (round 5), not by the wave (read at every launch: A/B in one process)
-				const char* fl = getenv("BT2G_BT_LOC_FLAT");
-				const char* wp = getenv("BT2G_BT_LOC_WPF");
-				if(fl && *fl == '1') hipLaunchKernelGGL((k_sw_bt<1, true, true, true>), dim3(b.nprob), dim3(64), lds, st, b);
-				else if(wp && *wp == '0') hipLaunchKernelGGL((k_sw_bt<1, true, false, true>), dim3(b.nprob), dim3(64), lds, st, b);
+				if(form == 0) hipLaunchKernelGGL((k_sw_bt<1, true, true, true>), dim3(b.nprob), dim3(64), lds, st, b);
+				else if(form == 1) hipLaunchKernelGGL((k_sw_bt<1, true, false, true>), dim3(b.nprob), dim3(64), lds, st, b);
 				else hipLaunchKernelGGL((k_sw_bt<1, true, false, true, true>), dim3(b.nprob), dim3(64), lds, st, b);
 				return;
 			}

@@ -279,11 +279,12 @@ def test_bt_lds_resident_equals_lane_kernel(eng, monkeypatch, shape, variant):
         check_against(naln[:k], alns[:k], edits[:k], fates[:k], res[:k], None, ea, ee, ef, "mate")
 
 
-@pytest.mark.parametrize("lds", ["marks", "marks_serial", "marks_flat", "plane", "plane64k"])
+@pytest.mark.parametrize("lds", ["marks", "marks_cands", "marks_serial", "marks_flat", "plane", "plane64k"])
 def test_bt_local_lds_resident_equals_lane_kernel(eng, monkeypatch, lds):
     """Local mode: batches up to BT2G_BT_LDS_MAX walk LDS-resident, one walker per
     workgroup, its candidates filtered by the wave 64 at a time (default) or by the
-    walker one at a time (BT2G_BT_LOC_WPF=0, "marks_serial"):
+    walker one at a time (BT2G_BT_LOC_WPF=0, "marks_serial"), the wave reading the
+    candidates from HBM (default) or from an LDS copy (BT2G_BT_LOC_CANDS=lds):
     both mark tile sets in LDS and the u16 plane read in place (default),
     or the plane and its block masks in LDS too (BT2G_BT_LOC_LDS=plane, past 64 KiB
     with the device's opt-in, else the lane kernel) -- the same alignments, edits and
@@ -304,9 +305,12 @@ def test_bt_local_lds_resident_equals_lane_kernel(eng, monkeypatch, lds):
             monkeypatch.setenv("BT2G_BT_LOC_FLAT", "1")
         if lds == "marks_serial":
             monkeypatch.setenv("BT2G_BT_LOC_WPF", "0")
+        if lds == "marks_cands":
+            monkeypatch.setenv("BT2G_BT_LOC_CANDS", "lds")
         outs.append(eng.sw_align_bt(codes, quals, lens, probs, rects=rects, local=True, cap=4096, maxaln=64,
                                     maxedit=512))
         monkeypatch.delenv("BT2G_BT_LOC_WPF", raising=False)
+        monkeypatch.delenv("BT2G_BT_LOC_CANDS", raising=False)
         monkeypatch.delenv("BT2G_BT_WG_LDS", raising=False)
         monkeypatch.delenv("BT2G_BT_LOC_LDS", raising=False)
         monkeypatch.delenv("BT2G_BT_LOC_FLAT", raising=False)
