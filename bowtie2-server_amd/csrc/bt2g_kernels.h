@@ -150,6 +150,7 @@ struct BtArgs {
 	uint32_t* queue;                  // null: one DP per lane; else a zeroed counter: lanes take DPs from it
 	int lds_marks_only;               // LDS-resident local walk: marks in LDS, the plane read in place
 	int cands_lds;                    // LDS-resident local walk: the candidate list copied to LDS too
+	int wpf;                          // LDS-resident local walk: 2 the walks in parallel (64 paths in LDS)
 };
 // kind: 0 u8 score plane, 1 u16 score plane, 2 decision nibbles (end-to-end u8 fills)
 void launch_sw_bt(int kind, const BtArgs& a, hipStream_t st);

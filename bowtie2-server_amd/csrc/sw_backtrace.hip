@@ -143,12 +143,30 @@ __device__ unsigned long long g_bt_wave_t0[1u << 16], g_bt_wave_t1[1u << 16];   
 // themselves are then run by all 64 lanes on identical values (the same
 // loads, the same stores to the same addresses): no lane leaves the loop, so
 // the wave stays converged for the next filter's ballot.
-template <int KIND, bool LOCAL, bool FLAT = LOCAL, bool LDSRES = false, bool WPF = false>
+// WPF 2 (the default): the walks themselves in parallel too, as the end-to-end
+// workgroup walk does (sw_backtrace_wg.hip).  A walk's path does not depend on
+// the marks -- only where it stops does -- and the filters only ever grow (a
+// candidate filtered now stays filtered), so:
+//   scan: the lanes test the next candidates 64 at a time against the current
+//     marks and squares and collect up to 64 survivors, in order;
+//   A: lane s walks survivor s without marks, recording its moves (2 bits each)
+//     and whether the path itself succeeds (a core diagonal touched, Ns within
+//     the ceiling) -- the plane reads and move decisions, in parallel;
+//   B: the wave resolves the batch in the reference's order: the candidates
+//     between two survivors get their fates at that point (in parallel, as the
+//     scan), a survivor is tested again (an earlier walk of the batch may have
+//     filtered it) and, if it still stands, its recorded path is replayed
+//     against the marks, marking each cell, failing at the first marked one,
+//     then its dominance square is set -- what the serial walk does, minus the
+//     plane reads;
+//   C: the lanes whose walks succeeded walk again writing their edits and
+//     alignment records (as a later success is replayed in the serial walk).
+template <int KIND, bool LOCAL, bool FLAT = LOCAL, bool LDSRES = false, int WPF = 0>
 __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(BT2G_BT_WAVES)))
 k_sw_bt(BtArgs A) {
 	static_assert(!LDSRES || (KIND == 2 && !LOCAL) || (KIND == 1 && LOCAL),
 	              "LDS-resident walks: kind-2 end-to-end or kind-1 local planes");
-	static_assert(!WPF || (LDSRES && LOCAL && !FLAT), "the wave-parallel filter: LDS-resident local walks");
+	static_assert(WPF == 0 || (LDSRES && LOCAL && !FLAT), "the wave-parallel filter: LDS-resident local walks");
 	const uint32_t p = LDSRES ? blockIdx.x : blockIdx.x * 64u + threadIdx.x;
 	if(p >= A.nprob) return;
 #ifdef BT2G_BT_PROF
@@ -268,6 +286,7 @@ k_sw_bt(BtArgs A) {
 	uint32_t* marks = A.marks + (size_t)p * A.mslot;
 	const uint32_t tcols = A.rwords, trows = A.rrows, vw = (tcols + 31u) / 32u;
 	const bt2g_sw_cand* lcl = nullptr;      // (LDSRES local: the candidate list's copy in LDS)
+	uint32_t* lpath = nullptr;              // (WPF 2: 64 recorded paths, then the survivors' indices and infos)
 	if constexpr(LDSRES) {
 		// the plane's 16-row blocks (kind 2: 8 B per block column; kind 1: 32 B, then
 		// the columns' block masks) and the marks, in LDS (layout: sw_bt_lds_bytes)
@@ -287,8 +306,9 @@ k_sw_bt(BtArgs A) {
 			for(uint32_t i = threadIdx.x; i < 3u * nc; i += 64u) lc[i] = gc[i];
 			lcl = (const bt2g_sw_cand*)lc;
 		}
+		if(WPF == 2) lpath = lm + A.mslot + (A.cands_lds ? 3u * A.cap : 0u);
 		__syncthreads();
-		if(!WPF && threadIdx.x != 0) return;
+		if(WPF == 0 && threadIdx.x != 0) return;
 		if(n16) {
 			slot = (const uint8_t*)s_res;
 			pl.base = slot;
@@ -508,6 +528,34 @@ k_sw_bt(BtArgs A) {
 		walking = true;
 		BTC(0);
 	};
+	// the alignment record of a walk that succeeded (its edits at ed): candidate
+	// `cand`, alignment k of the problem
+	auto record_aln = [&](uint32_t cand, uint32_t k) {
+		const uint32_t trimBeg = w.row, trimEnd = nrow - row0 - 1;
+		// res.reverse(), AlnRes::setShape trim shift, invertEdits for !fw
+		// (aligner_result.cpp:101-117, 822-828; edit.cpp:50-78)
+		const uint32_t ned = w.ned, nst = ned < A.maxedit ? ned : A.maxedit;
+		if(fw) {
+			for(uint32_t i = 0; i < nst / 2; i++) {
+				const bt2g_edit t = ed[i];
+				ed[i] = ed[nst - 1 - i];
+				ed[nst - 1 - i] = t;
+			}
+			for(uint32_t i = 0; i < nst; i++) ed[i].pos -= trimBeg;
+		} else {
+			const uint32_t sz = nrow - trimBeg - trimEnd;
+			for(uint32_t i = 0; i < nst; i++)
+				ed[i].pos = sz - (ed[i].pos - trimBeg) - (ed[i].type == 1 ? 0u : 1u);
+		}
+		int32_t refns = 0;
+		for(uint32_t c = w.col; c <= col0; c++) refns += rf_at(c) > 15;
+		bt2g_sw_aln a;
+		a.cand = (int32_t)cand; a.score = w.score; a.off = (int32_t)w.col; a.ns = w.ns; a.gaps = w.gaps;
+		a.refns = refns; a.nedit = (int32_t)ned;
+		a.trim5p = (int32_t)(fw ? trimBeg : trimEnd); a.trim3p = (int32_t)(fw ? trimEnd : trimBeg);
+		a.pad = 0;
+		A.alns[(size_t)p * A.maxaln + (size_t)k] = a;
+	};
 	uint32_t ndone = 0, wq0 = 0, wq1 = 0, wq2 = 0, wq3 = 0;   // walked candidates: row << 16 | col
 #ifdef BT2G_BT_WQ8
 	uint32_t wq4 = 0, wq5 = 0, wq6 = 0, wq7 = 0;
@@ -516,8 +564,140 @@ k_sw_bt(BtArgs A) {
 	// the next candidate is loaded one ahead (its load overlaps the current walk)
 	bt2g_sw_cand nxt_cd = ncand ? cl[0] : bt2g_sw_cand{0, 0, 0};
 	int32_t cscore = 0;
+	// WPF 2: the batch (survivor s's candidate index sidx[s], its path's moves and
+	// success winfo[s]), this lane's path words, its survivor and alignment index
+	const uint32_t PW = ((A.rrows * 8u + A.pcols) >> 4) + 1u;      // >= (rows + cols) / 16 + 1
+	uint32_t* const sidx = lpath + 64u * PW;
+	uint32_t* const winfo = sidx + 64u;
+	uint32_t* const mypath = lpath + threadIdx.x * PW;
+	int wphase = 0;                          // 0 between batches, 1 speculative walks (A), 2 emitting walks (C)
+	bool wdone = false, wrec = false, my_succ = false;
+	uint32_t nsurv = 0, bend = 0, my_cj = 0, my_kk = 0, nmv = 0, pacc = 0;
+	// the walker's cached reportedThrough tile and valid word back to LDS, where
+	// the other lanes read them
+	auto flush_tile = [&]() {
+		if(tdirty) {
+			*(uint64_t*)(marks + ((size_t)ttr * tcols + ttc) * 2u) = tbits;
+			vword(ttr * vw + (ttc >> 5)) |= 1u << (ttc & 31u);
+			vdirty = true;
+			tdirty = false;
+		}
+		if(vdirty) { valid[vidx] = vval; vdirty = false; }
+		__syncthreads();
+	};
+	// a candidate's filter at this point, from LDS (after flush_tile): 5 score,
+	// 4 dominated, 3 start marked, 0 none -- in the reference's order
+	auto filt_lds = [&](const bt2g_sw_cand& c) -> int8_t {
+		const uint32_t r = (uint32_t)c.row, cc = (uint32_t)c.col;
+		const uint32_t tr = r >> 3, tc = cc >> 3;
+		const bool mk = ((valid[tr * vw + (tc >> 5)] >> (tc & 31u)) & 1u) &&
+		                (*(const uint64_t*)(marks + ((size_t)tr * tcols + tc) * 2u) & rbit(r, cc));
+		if(c.score < P.minsc) return 5;                      // BT_CAND_FATE_FILT_SCORE
+		if(!A.fates && dom_test(r, cc)) return 4;            // BT_CAND_FATE_FILT_DOMINATED
+		if(mk) return 3;                                     // BT_CAND_FATE_FILT_START
+		if(A.fates && dom_test(r, cc)) return 4;
+		return 0;
+	};
 	while(true) {
-		if(WPF && !walking) {
+		if constexpr(WPF == 2) {
+			if(__ballot(walking) == 0ull) {
+				if(wphase == 1) {
+					// ---- B: the batch in the reference's order -------------------------
+					__syncthreads();                     // (the lanes' paths and infos)
+					uint32_t pos = ci;
+					my_succ = false;
+					for(uint32_t sv = 0; sv <= nsurv; sv++) {
+						if(nal >= (int32_t)A.maxaln) { wdone = true; break; }
+						const uint32_t cj = sv < nsurv ? sidx[sv] : bend;
+						// the candidates up to the survivor: filtered at the scan, so filtered
+						// now; their fates as of this point
+						flush_tile();
+						if(A.fates)
+							for(uint32_t x = pos; x < cj; x += 64u) {
+								const uint32_t j = x + threadIdx.x;
+								if(j < cj) A.fates[(size_t)p * A.cap + j] = filt_lds(cl[j]);
+							}
+						pos = cj;
+						if(sv == nsurv) break;
+						const bt2g_sw_cand c = cl[cj];
+						int8_t fate = filt_lds(c);
+						if(!fate) {
+							// its walk: the recorded path against the marks
+							const uint32_t info = winfo[sv], nm = info >> 1;
+							const uint32_t* pp = lpath + sv * PW;
+							uint32_t r = (uint32_t)c.row, cc = (uint32_t)c.col;
+							bool ok = true;
+							for(uint32_t i = 0;; i++) {
+								tile_get(r, cc);
+								const uint64_t bt = rbit(r, cc);
+								if(tbits & bt) { ok = false; break; }
+								tbits |= bt;
+								tdirty = true;
+								if(i == nm) break;
+								const uint32_t code = (pp[i >> 4] >> (2u * (i & 15u))) & 3u;
+								// (a walk never moves past row or column 0: a guard, not a case)
+								if((code != 2u && r == 0u) || (code != 1u && cc == 0u)) { ok = false; break; }
+								if(code != 2u) r--;          // diagonal or up
+								if(code != 1u) cc--;         // diagonal or left
+							}
+							dom_add((uint32_t)c.row, (uint32_t)c.col);
+							if(ok && (info & 1u)) {
+								if(threadIdx.x == sv) { my_succ = true; my_kk = (uint32_t)nal; }
+								nal++;
+								fate = 1;                        // BT_CAND_FATE_SUCCEEDED
+							} else {
+								fate = 2;                        // BT_CAND_FATE_FAILED
+							}
+						}
+						if(A.fates && threadIdx.x == 0) A.fates[(size_t)p * A.cap + cj] = fate;
+						pos = cj + 1u;
+					}
+					ci = pos;
+					// ---- C: the successes walked again, writing their edits ------------
+					if(my_succ) {
+						const bt2g_sw_cand c = cl[my_cj];
+						ed = A.edits + ((size_t)p * A.maxaln + (size_t)my_kk) * A.maxedit;
+						row0 = (uint32_t)c.row; col0 = (uint32_t)c.col; cur = c.score;
+						wrec = false;
+						start_walk(false, true);
+					}
+					wphase = 2;
+				} else {
+					// ---- the next batch: up to 64 survivors of the filters as they stand --
+					if(wdone || ci >= ncand || nal >= (int32_t)A.maxaln) break;
+					flush_tile();
+					nsurv = 0;
+					bool full = false;
+					uint32_t wpos = ci;
+					while(nsurv < 64u && wpos < ncand) {
+						const uint32_t j = wpos + threadIdx.x;
+						const bool sv = j < ncand && filt_lds(cl[j]) == 0;
+						const uint64_t m = __ballot(sv);
+						const uint32_t nm = (uint32_t)__popcll(m), take = nm < 64u - nsurv ? nm : 64u - nsurv;
+						const uint32_t rk = (uint32_t)__popcll(m & ((1ull << threadIdx.x) - 1ull));
+						if(sv && rk < take) sidx[nsurv + rk] = j;
+						nsurv += take;
+						wpos += 64u;
+						if(take < nm) { full = true; break; }
+					}
+					__syncthreads();
+					// (a full batch ends at its last survivor; else at the scanned end)
+					bend = full ? sidx[63] + 1u : (wpos < ncand ? wpos : ncand);
+					if(threadIdx.x < nsurv) {
+						my_cj = sidx[threadIdx.x];
+						const bt2g_sw_cand c = cl[my_cj];
+						row0 = (uint32_t)c.row; col0 = (uint32_t)c.col; cur = c.score;
+						wrec = true;
+						nmv = 0;
+						pacc = 0;
+						start_walk(false, false);
+					}
+					wphase = 1;
+				}
+			}
+			if(!walking) continue;
+		}
+		if(WPF == 1 && !walking) {
 			if(ci >= ncand || nal >= (int32_t)A.maxaln) break;
 			// the cached reportedThrough tile and valid word back to LDS, where the
 			// other lanes read them
@@ -832,6 +1012,11 @@ k_sw_bt(BtArgs A) {
 					col--; w.gaps++;
 				}
 				cur = nxt;
+				if(WPF == 2 && wrec) {
+					// the move, for the replay against the marks: 0 diagonal, 1 up, 2 left
+					pacc |= (uint32_t)(mv == 0 ? 0 : mv <= 2 ? 1 : 2) << (2u * (nmv & 15u));
+					if((++nmv & 15u) == 0u) { mypath[(nmv >> 4) - 1u] = pacc; pacc = 0u; }
+				}
 			}
 		}
 		} while(!ended && ++ks < (FLAT ? 1u : (uint32_t)BT2G_BT_EE_STEPS));
@@ -851,6 +1036,17 @@ k_sw_bt(BtArgs A) {
 			}
 			if(mt == -1) w.ns++;
 			if(w.ns > nceil) w.ok = false;
+		}
+		if constexpr(WPF == 2) {
+			walking = false;
+			if(wphase == 1) {
+				// A: the path and whether it succeeds where no mark stops it
+				if(nmv & 15u) mypath[nmv >> 4] = pacc;
+				winfo[threadIdx.x] = (nmv << 1) | (w.ok ? 1u : 0u);
+			} else if(w.ok) {
+				record_aln(my_cj, my_kk);           // C (the same path: it succeeds)
+			}
+			continue;
 		}
 		if(w.ok && !first && !replay) {
 			// a later walk that succeeded: walk it again, unmarked, writing its edits
@@ -877,30 +1073,7 @@ k_sw_bt(BtArgs A) {
 			ndone++;
 		}
 		if(w.ok) {
-			const uint32_t trimBeg = w.row, trimEnd = nrow - row0 - 1;
-			// res.reverse(), AlnRes::setShape trim shift, invertEdits for !fw
-			// (aligner_result.cpp:101-117, 822-828; edit.cpp:50-78)
-			const uint32_t ned = w.ned, nst = ned < A.maxedit ? ned : A.maxedit;
-			if(fw) {
-				for(uint32_t i = 0; i < nst / 2; i++) {
-					const bt2g_edit t = ed[i];
-					ed[i] = ed[nst - 1 - i];
-					ed[nst - 1 - i] = t;
-				}
-				for(uint32_t i = 0; i < nst; i++) ed[i].pos -= trimBeg;
-			} else {
-				const uint32_t sz = nrow - trimBeg - trimEnd;
-				for(uint32_t i = 0; i < nst; i++)
-					ed[i].pos = sz - (ed[i].pos - trimBeg) - (ed[i].type == 1 ? 0u : 1u);
-			}
-			int32_t refns = 0;
-			for(uint32_t c = w.col; c <= col0; c++) refns += rf_at(c) > 15;
-			bt2g_sw_aln a;
-			a.cand = (int32_t)ci; a.score = w.score; a.off = (int32_t)w.col; a.ns = w.ns; a.gaps = w.gaps;
-			a.refns = refns; a.nedit = (int32_t)ned;
-			a.trim5p = (int32_t)(fw ? trimBeg : trimEnd); a.trim3p = (int32_t)(fw ? trimEnd : trimBeg);
-			a.pad = 0;
-			A.alns[(size_t)p * A.maxaln + (size_t)nal] = a;
+			record_aln(ci, (uint32_t)nal);
 			nal++;
 			fate = 1;                                       // BT_CAND_FATE_SUCCEEDED
 		} else {
@@ -954,7 +1127,10 @@ static uint32_t bt_lds_bytes(const BtArgs& a, int kind) {
 	// (local: the candidate list, but for the wave-parallel filter, which reads it
 	// from HBM 64 candidates at a time: ~24 KB less per workgroup at cap 2 048)
 	const uint64_t cands = kind == 1 && a.cands_lds ? (uint64_t)a.cap * sizeof(bt2g_sw_cand) : 0u;
-	const uint64_t n = plane + marks + cands;
+	// (the parallel walks: 64 recorded paths of (rows + cols) / 16 + 1 words, the
+	// survivors' indices and infos)
+	const uint64_t paths = kind == 1 && a.wpf == 2 ? (64ull * (((a.rrows * 8u + a.pcols) >> 4) + 1u) + 128u) * 4u : 0u;
+	const uint64_t n = plane + marks + cands + paths;
 	return n > 0xffffffffull ? 0xffffffffu : (uint32_t)n;
 }
 
@@ -976,7 +1152,9 @@ void sw_bt_lds_init(int dev) {
 	                       v - (int)BT_STATIC_LDS) == hipSuccess &&
 	   hipFuncSetAttribute((const void*)k_sw_bt<1, true, false, true>, hipFuncAttributeMaxDynamicSharedMemorySize,
 	                       v - (int)BT_STATIC_LDS) == hipSuccess &&
-	   hipFuncSetAttribute((const void*)k_sw_bt<1, true, false, true, true>,
+	   hipFuncSetAttribute((const void*)k_sw_bt<1, true, false, true, 1>,
+	                       hipFuncAttributeMaxDynamicSharedMemorySize, v - (int)BT_STATIC_LDS) == hipSuccess &&
+	   hipFuncSetAttribute((const void*)k_sw_bt<1, true, false, true, 2>,
 	                       hipFuncAttributeMaxDynamicSharedMemorySize, v - (int)BT_STATIC_LDS) == hipSuccess)
 		lim = (uint32_t)v - BT_STATIC_LDS;
 	else
@@ -1035,20 +1213,28 @@ void launch_sw_bt(int kind, const BtArgs& a, hipStream_t st) {
 			// (one walker per workgroup: no lanes to diverge, so a walk runs to its
 			// end in the inner loop -- the flat loop's one body per step is the
 			// union of the filter and the walk; $BT2G_BT_LOC_FLAT=1 keeps it)
-			// $BT2G_BT_LOC_WPF=0: the candidates filtered by the walker alone, one at a
-			// time (round 5), not by the wave (read at every launch: A/B in one process)
+			// $BT2G_BT_LOC_WPF (read at every launch: A/B in one process): 0 the
+			// candidates filtered and walked by the walker alone, one at a time (round
+			// 5); 1 filtered by the wave, walked one at a time; default: filtered and
+			// walked by the wave (the recorded paths take LDS: a batch whose paths do
+			// not fit takes form 1)
 			const char* fl = getenv("BT2G_BT_LOC_FLAT");
 			const char* wp = getenv("BT2G_BT_LOC_WPF");
-			const int form = (fl && *fl == '1') ? 0 : (wp && *wp == '0') ? 1 : 2;
-			// $BT2G_BT_LOC_CANDS=lds: the wave-parallel filter's candidates copied to LDS
+			// $BT2G_BT_LOC_CANDS=lds: the wave-parallel forms' candidates copied to LDS
 			// as the serial filter's are (one dependent load per candidate there)
 			const char* cl = getenv("BT2G_BT_LOC_CANDS");
-			b.cands_lds = form != 2 || (cl && !strcmp(cl, "lds"));
-			const uint32_t lds = bt_lds_bytes(b, 1);
-			if(lds <= bt_loc_lds_limit()) {
+			for(int form = (fl && *fl == '1') ? 0 : (wp && *wp == '0') ? 1 : (wp && *wp == '1') ? 2 : 3; form >= 0;) {
+				b.wpf = form == 3 ? 2 : form == 2 ? 1 : 0;
+				b.cands_lds = form < 2 || (cl && !strcmp(cl, "lds"));
+				const uint32_t lds = bt_lds_bytes(b, 1);
+				if(lds > bt_loc_lds_limit()) {
+					if(form == 3) { form = 2; continue; }
+					break;
+				}
 				if(form == 0) hipLaunchKernelGGL((k_sw_bt<1, true, true, true>), dim3(b.nprob), dim3(64), lds, st, b);
 				else if(form == 1) hipLaunchKernelGGL((k_sw_bt<1, true, false, true>), dim3(b.nprob), dim3(64), lds, st, b);
-				else hipLaunchKernelGGL((k_sw_bt<1, true, false, true, true>), dim3(b.nprob), dim3(64), lds, st, b);
+				else if(form == 2) hipLaunchKernelGGL((k_sw_bt<1, true, false, true, 1>), dim3(b.nprob), dim3(64), lds, st, b);
+				else hipLaunchKernelGGL((k_sw_bt<1, true, false, true, 2>), dim3(b.nprob), dim3(64), lds, st, b);
 				return;
 			}
 		}

@@ -279,11 +279,14 @@ def test_bt_lds_resident_equals_lane_kernel(eng, monkeypatch, shape, variant):
         check_against(naln[:k], alns[:k], edits[:k], fates[:k], res[:k], None, ea, ee, ef, "mate")
 
 
-@pytest.mark.parametrize("lds", ["marks", "marks_cands", "marks_serial", "marks_flat", "plane", "plane64k"])
+@pytest.mark.parametrize("lds", ["marks", "marks_wpf1", "marks_cands", "marks_serial", "marks_flat", "plane",
+                                 "plane64k"])
 def test_bt_local_lds_resident_equals_lane_kernel(eng, monkeypatch, lds):
     """Local mode: batches up to BT2G_BT_LDS_MAX walk LDS-resident, one walker per
-    workgroup, its candidates filtered by the wave 64 at a time (default) or by the
-    walker one at a time (BT2G_BT_LOC_WPF=0, "marks_serial"), the wave reading the
+    workgroup, its candidates filtered and walked by the wave, up to 64 walks at a
+    time resolved in the reference's order (default), filtered by the wave and
+    walked one at a time (BT2G_BT_LOC_WPF=1), or filtered and walked by the walker
+    one at a time (BT2G_BT_LOC_WPF=0, "marks_serial"), the wave reading the
     candidates from HBM (default) or from an LDS copy (BT2G_BT_LOC_CANDS=lds):
     both mark tile sets in LDS and the u16 plane read in place (default),
     or the plane and its block masks in LDS too (BT2G_BT_LOC_LDS=plane, past 64 KiB
@@ -305,6 +308,8 @@ def test_bt_local_lds_resident_equals_lane_kernel(eng, monkeypatch, lds):
             monkeypatch.setenv("BT2G_BT_LOC_FLAT", "1")
         if lds == "marks_serial":
             monkeypatch.setenv("BT2G_BT_LOC_WPF", "0")
+        if lds == "marks_wpf1":
+            monkeypatch.setenv("BT2G_BT_LOC_WPF", "1")
         if lds == "marks_cands":
             monkeypatch.setenv("BT2G_BT_LOC_CANDS", "lds")
         outs.append(eng.sw_align_bt(codes, quals, lens, probs, rects=rects, local=True, cap=4096, maxaln=64,
