@@ -656,8 +656,8 @@ def dominant_kernel(kern):
 def line_rooflines(kern, server_pmc):
     """(roofline, rooflines) of a line: the largest consumer's roofline object and
     every kernel (family) with a bound, largest total time first.  When the
-    largest consumer has no bound (--local: the one-walker backtrace, a chain of
-    dependent LDS accesses whose per-step work the host does not see), the
+    largest consumer has no bound (--local: the backtrace, dependent plane reads
+    and LDS mark tests whose per-step work the host does not see), the
     roofline is the largest kernel WITH one and names that consumer in
     `largest_consumer`."""
     dom_k = dominant_kernel(kern)
@@ -666,9 +666,10 @@ def line_rooflines(kern, server_pmc):
         largest = {"id": dom_k, "kernel": kern[dom_k]["kernel"], "ms_per_launch": kern[dom_k]["ms_per_launch"],
                    "share_of_kernel_time": kern[dom_k]["ms_total"] / max(1e-9, sum(
                        v["ms_total"] for v in kern.values() if not v.get("span"))),
-                   "why_no_roofline": "a chain of dependent LDS accesses per DP (one walker per workgroup; local: "
-                                      "~55 walks and ~1 200 candidates per DP): latency-bound, no algorithmic "
-                                      "byte or op count the host sees"}
+                   "why_no_roofline": "dependent plane reads and LDS mark tests per DP (one workgroup per DP; "
+                                      "local: ~55 walks over ~1 200 candidates, up to 64 walked at once, then "
+                                      "resolved in the reference's order): latency-bound, and the host sees no "
+                                      "per-step byte or op count"}
         bounded = [k for k in kern if "achieved" in kern[k] and not kern[k].get("span")]
         dom_k = max(bounded, key=lambda k: kern[k]["ms_total"], default=None)
     if dom_k:
