@@ -92,6 +92,20 @@ def _synth_problems(gen, n, seed, length=150, maxgap=15, minsc=-90, sub=0.02, in
     return codes, quals, np.full(n, length, np.uint32), probs, rects
 
 
+def _same_results_and_lists(a, b):
+    """Two sw_align_bt outputs: the same results and alignment counts, and the same
+    candidate lists up to each problem's ncand (the slots past it are never
+    written: whatever the output buffer held, which differs between a call whose
+    outputs fit the context's pinned block and one whose outputs did not)."""
+    for f in a[0].dtype.names:
+        assert np.array_equal(a[0][f], b[0][f]), f
+    assert np.array_equal(a[2], b[2])
+    nc = np.minimum(np.maximum(a[0]["ncand"], 0), a[1].shape[1])
+    for p in range(len(nc)):
+        for f in a[1].dtype.names:
+            assert np.array_equal(a[1][f][p, :nc[p]], b[1][f][p, :nc[p]]), (p, f)
+
+
 def _oracle_expect(orc, gen, codes, quals, probs, rects, local, sc=None, enable8=True):
     ea, ee, ef = [], [], []
     for p in range(len(probs)):
@@ -251,14 +265,9 @@ def test_bt_lds_resident_equals_lane_kernel(eng, monkeypatch, shape, variant):
         for k in env:
             monkeypatch.delenv(k)
     a, b = outs
-    # results, candidate lists, counts: whole; alignments, edits and fates: the
+    # results and counts: whole; candidate lists, alignments, edits and fates: the
     # valid parts (slots past them are not written)
-    for x, y in zip(a[:3], b[:3]):
-        if x.dtype.names:
-            for f in x.dtype.names:
-                assert np.array_equal(x[f], y[f]), f
-        else:
-            assert np.array_equal(x, y)
+    _same_results_and_lists(a, b)
     naln = a[2]
     for p in range(n):
         k = max(int(naln[p]), 0)
@@ -320,12 +329,7 @@ def test_bt_local_lds_resident_equals_lane_kernel(eng, monkeypatch, lds):
         monkeypatch.delenv("BT2G_BT_LOC_LDS", raising=False)
         monkeypatch.delenv("BT2G_BT_LOC_FLAT", raising=False)
     a, b = outs
-    for x, y in zip(a[:3], b[:3]):
-        if x.dtype.names:
-            for f in x.dtype.names:
-                assert np.array_equal(x[f], y[f]), f
-        else:
-            assert np.array_equal(x, y)
+    _same_results_and_lists(a, b)
     naln = a[2]
     for p in range(n):
         k = max(int(naln[p]), 0)
@@ -342,3 +346,57 @@ def test_bt_local_lds_resident_equals_lane_kernel(eng, monkeypatch, lds):
     k = 48
     ea, ee, ef = _oracle_expect(Oracle(), gen, codes[:k], quals[:k], probs[:k], rects[:k], True)
     check_against(naln[:k], alns[:k], edits[:k], fates[:k], res[:k], None, ea, ee, ef, "local_lds")
+
+
+@pytest.mark.parametrize("maxaln", [1, 2, 64])
+def test_bt_local_maxaln_lds_equals_lane_kernel(eng, monkeypatch, maxaln):
+    """Local DPs with several alignments each (windows holding three mutated
+    copies of the read) and a maxaln that binds: the wave-parallel walk (the
+    default LDS-resident form) stops where the serial walk does -- its in-order
+    resolution of a batch of speculative walks ends at the maxaln-th success -- so
+    the alignments, edits and candidate fates equal the lane-per-problem kernel's
+    (BT2G_BT_LDS_MAX=0)."""
+    gen = get_index("lambda").ref_codes[0]
+    n = 200
+    codes, quals, lens, probs, rects = _synth_problems(gen, n, 77, minsc=60, sub=0.01)
+    rng = np.random.default_rng(78)
+    wins, offs = [], []
+    for p in range(n):
+        parts = []
+        for k in range(3):
+            seg = codes[p].astype(np.int32).copy()
+            flip = rng.random(seg.size) < 0.03
+            seg[flip] = (seg[flip] + rng.integers(1, 4, int(flip.sum()))) % 4
+            parts += [seg, rng.integers(0, 4, 20)]
+        w = np.concatenate(parts)
+        offs.append(sum(len(x) for x in wins))
+        wins.append(np.where(w > 3, 16, 1 << np.minimum(w, 3)).astype(np.uint8))
+    probs = probs.copy()
+    probs["fw"] = 1
+    probs["win_off"] = offs
+    probs["ncol"] = [len(x) - 1 for x in wins]
+    rects = rects.copy()
+    rects["corel"], rects["corer"] = -200, 1000
+    windows = np.concatenate(wins)
+    outs = []
+    for lim in ("65536", "0"):
+        monkeypatch.setenv("BT2G_BT_LDS_MAX", lim)
+        outs.append(eng.sw_align_bt(codes, quals, lens, probs, windows=windows, rects=rects, local=True, cap=4096,
+                                    maxaln=maxaln, maxedit=512))
+    monkeypatch.delenv("BT2G_BT_LDS_MAX", raising=False)
+    a, b = outs
+    _same_results_and_lists(a, b)
+    for p in range(n):
+        k = max(int(a[2][p]), 0)
+        for f in a[3].dtype.names:
+            assert np.array_equal(a[3][f][p, :k], b[3][f][p, :k]), (p, f)
+        for j in range(k):
+            ne = min(int(a[3]["nedit"][p, j]), a[4].shape[2])
+            for f in ("pos", "type", "chr", "qchr"):
+                assert np.array_equal(a[4][f][p, j, :ne], b[4][f][p, j, :ne]), (p, j, f)
+        nc = min(int(a[0]["ncand"][p]), a[5].shape[1])
+        assert np.array_equal(a[5][p, :nc], b[5][p, :nc]), p
+    if maxaln < 64:
+        assert (a[2] == maxaln).sum() > 0.5 * n          # the bound binds
+    else:
+        assert (a[2] >= 3).sum() > 0.5 * n               # three copies, three alignments
